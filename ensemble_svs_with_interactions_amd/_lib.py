@@ -1,0 +1,82 @@
+"""ctypes binding of libensvs.so (the gfx950 C ABI declared in include/ensvs.h).
+
+The product path has no fallback: if the shared library is missing or cannot
+be loaded, importing anything that launches a kernel raises immediately.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libensvs.so")
+
+c_int = ctypes.c_int
+c_ll = ctypes.c_longlong
+c_float = ctypes.c_float
+c_vp = ctypes.c_void_p
+
+STATUS = {0: "OK", 1: "E_SHAPE", 2: "E_DTYPE", 3: "E_HIP", 4: "E_ARG"}
+
+PAD_ZERO, PAD_REFLECT, PAD_REPLICATE = 0, 1, 2
+DT_F32, DT_BF16 = 0, 1
+EPI_PLAIN, EPI_GATE, EPI_RESSKIP, EPI_GATE_BWD, EPI_ADDSCALE = 0, 1, 2, 3, 4
+
+
+class ConvSeg(ctypes.Structure):
+    _fields_ = [
+        ("x", c_vp), ("radd", c_vp), ("wofs", c_ll),
+        ("ld", c_int), ("K", c_int), ("taps", c_int), ("dil", c_int), ("shift0", c_int),
+        ("pad", c_int), ("radd_ld", c_int), ("Tin", c_int), ("Kp", c_int),
+    ]
+
+
+class PackDesc(ctypes.Structure):
+    _fields_ = [
+        ("src", c_vp), ("src2", c_vp), ("dst", c_vp),
+        ("sn", c_ll), ("sk", c_ll), ("sj", c_ll),
+        ("N", c_int), ("K", c_int), ("taps", c_int), ("Npad", c_int), ("Kp", c_int),
+        ("perm_c", c_int), ("flip", c_int), ("transpose", c_int), ("dtype", c_int),
+        ("scale", c_float),
+    ]
+
+
+# name -> argtypes (every entry point returns int status)
+SIGNATURES = {
+    "ensvs_conv_gemm": [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int,
+                        c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_float, c_int, c_vp],
+    "ensvs_conv_wgrad": [c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                         c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_ll, c_ll, c_int,
+                         c_int, c_vp],
+    "ensvs_pack_weights": [c_vp, c_int, c_int, c_vp],
+    "ensvs_colsum": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_vp, c_int,
+                     c_vp],
+}
+
+_lib = None
+
+
+def load():
+    """Load libensvs.so once; raise (never fall back) when it is unavailable."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"ensvs: {LIB_PATH} not found — build it with `make` (or __graft_entry__.build()); "
+                "there is no CPU fallback on the product path")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = c_int
+        _lib = lib
+    return _lib
+
+
+def call(name, *args):
+    status = getattr(load(), name)(*args)
+    if status != 0:
+        raise RuntimeError(f"{name} failed with {STATUS.get(status, status)}")
+
+
+def ptr(t):
+    """Raw device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()

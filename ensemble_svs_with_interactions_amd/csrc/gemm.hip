@@ -1,0 +1,633 @@
+// Implicit-GEMM engine for every dense contraction on the multi-track SVS
+// path: Linear layers, Conv1d (any taps / dilation / zero-reflect-replicate
+// padding), LSTM input projections, the DiffNet residual-block convolutions
+// and their backward passes (dgrad = same kernel over transposed packed
+// weights; wgrad = the frame-reduction kernel below).
+//
+//   fwd:   Y[m, n] = sum_seg sum_tap sum_k  X_seg[src(m, tap), k] * Wp[seg][tap][n][k]
+//   wgrad: P[s, tap, n, k] = sum_{m in split s} dY[m, n] * X[src(m, tap), k]
+//
+// m = b*Tout + t is a frame row, src(m, tap) = b*Tin + pad(t + shift0 + tap*dil).
+// Tiles are 128x128x32 on 4 waves (2x2, 64x64 per wave = 4x4 MFMA 16x16 tiles).
+// MFMA type is a template parameter: __bf16 (v_mfma_f32_16x16x32_bf16) for
+// the production path, float (v_mfma_f32_16x16x4_f32, exact fp32) for parity.
+// Activations stay fp32 in HBM and are rounded to the MFMA type while staged
+// into LDS, so one kernel serves both precisions.
+#include "common.h"
+#include "ensvs.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 32, NTHR = 256;
+
+template <typename T> struct Lds;
+template <> struct Lds<__bf16> { static constexpr int K = 40; };  // 80 B rows
+template <> struct Lds<float> { static constexpr int K = 36; };   // 144 B rows
+
+enum {
+  EPI_PLAIN = 0,     // Y = (accum ? Y : 0) + acc + bias, optional relu
+  EPI_GATE = 1,      // DiffNet: gate/filter interleaved by 16 -> GF save + z = sig(g)*tanh(f)
+  EPI_RESSKIP = 2,   // DiffNet: res/skip interleaved by 16 -> x' = (x + r)/sqrt2, skip (+)= s
+  EPI_GATE_BWD = 3,  // DiffNet backward: dz -> d(gate), d(filter) pre-activation grads
+  EPI_ADDSCALE = 4,  // Y = alpha * aux1 + acc + bias
+};
+
+struct SegDesc {
+  const float* x;     // frame rows of this K-segment (already offset to its first channel)
+  const float* radd;  // optional per-sequence vector added to in-range values (y = x + d[b])
+  long long wofs;     // element offset of this segment's packed weights [taps][Npad][Kp]
+  int ld, K, taps, dil, shift0, pad, radd_ld, Tin, Kp, vec;
+};
+
+struct GemmArgs {
+  SegDesc seg[3];
+  int nseg;
+  int Tout, M, N, Npad;
+  const void* W;
+  const float* bias;
+  float* Y;
+  int ldy;
+  int epi, relu, accum;
+  float* aux0;
+  const float* aux1;
+  int ld0, ld1;
+  float alpha;
+  int C;
+};
+
+template <typename T>
+__device__ __forceinline__ void store4(T* dst, float a, float b, float c, float d);
+template <>
+__device__ __forceinline__ void store4<float>(float* dst, float a, float b, float c, float d) {
+  *(f32x4*)dst = f32x4{a, b, c, d};
+}
+template <>
+__device__ __forceinline__ void store4<__bf16>(__bf16* dst, float a, float b, float c, float d) {
+  *(bf16x4*)dst = bf16x4{(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+}
+
+// acc[mt][nt] += A_s[rows of wave][k] * B_s[cols of wave][k] over one BK tile.
+template <typename T>
+__device__ __forceinline__ void mma_tile(const T* As, const T* Bs, int wr, int wc, int lane,
+                                         f32x4 (&acc)[4][4]) {
+  constexpr int LK = Lds<T>::K;
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i] = *(const bf16x8*)(As + (wr * 64 + i * 16 + (lane & 15)) * LK + 8 * (lane >> 4));
+      b[i] = *(const bf16x8*)(Bs + (wc * 64 + i * 16 + (lane & 15)) * LK + 8 * (lane >> 4));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f32x4 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i] = *(const f32x4*)(As + (wr * 64 + i * 16 + (lane & 15)) * LK + 16 * h + 4 * (lane >> 4));
+        b[i] = *(const f32x4*)(Bs + (wc * 64 + i * 16 + (lane & 15)) * LK + 16 * h + 4 * (lane >> 4));
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ forward
+template <typename T>
+__global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
+  constexpr int LK = Lds<T>::K;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* As = (T*)smem;
+  T* Bs = As + 2 * BM * LK;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+
+  // A staging: 4 float4 chunks per thread; rows (tid>>3) + 32 i, chunk column tid&7.
+  int rb[4], rt[4];
+  bool rok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int m = m0 + (tid >> 3) + 32 * i;
+    rok[i] = m < a.M;
+    int b = rok[i] ? m / a.Tout : 0;
+    rb[i] = b;
+    rt[i] = rok[i] ? m - b * a.Tout : 0;
+  }
+  const int ac4 = tid & 7;
+
+  int nk[3];
+  int nit = 0;
+  for (int s = 0; s < a.nseg; ++s) {
+    nk[s] = (a.seg[s].K + BK - 1) / BK;
+    nit += nk[s] * a.seg[s].taps;
+  }
+
+  f32x4 ra[4];
+  constexpr int BCH = sizeof(T) == 2 ? 2 : 4;  // 16-B B chunks per thread
+  uint4 rbw[BCH];
+
+  auto decode = [&](int it, int& s, int& j, int& kc) {
+    s = 0;
+    while (it >= nk[s] * a.seg[s].taps) { it -= nk[s] * a.seg[s].taps; ++s; }
+    j = it / nk[s];
+    kc = it - j * nk[s];
+  };
+
+  auto load = [&](int it) {
+    int s, j, kc;
+    decode(it, s, j, kc);
+    const SegDesc& g = a.seg[s];
+    const int k = kc * BK + ac4 * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (rok[i] && k < g.K) {
+        int src = pad_src(rt[i] + g.shift0 + j * g.dil, g.Tin, g.pad);
+        if (src >= 0) {
+          const float* p = g.x + (long long)(rb[i] * g.Tin + src) * g.ld + k;
+          if (g.vec) {
+            v = *(const f32x4*)p;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (k + e < g.K) ? p[e] : 0.f;
+          }
+          if (k + 4 > g.K) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) if (k + e >= g.K) v[e] = 0.f;
+          }
+          if (g.radd) {
+            const float* q = g.radd + (long long)rb[i] * g.radd_ld + k;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) if (k + e < g.K) v[e] += q[e];
+          }
+        }
+      }
+      ra[i] = v;
+    }
+    const char* wbase = (const char*)a.W +
+        ((g.wofs + ((long long)j * a.Npad + n0) * g.Kp + kc * BK) * (long long)sizeof(T));
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      int q = tid + NTHR * i;
+      int row = sizeof(T) == 2 ? (q >> 2) : (q >> 3);
+      int c = sizeof(T) == 2 ? (q & 3) : (q & 7);
+      rbw[i] = *(const uint4*)(wbase + (long long)row * g.Kp * sizeof(T) + c * 16);
+    }
+  };
+
+  auto store = [&](int buf) {
+    T* A = As + buf * BM * LK;
+    T* B = Bs + buf * BN * LK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      store4<T>(A + ((tid >> 3) + 32 * i) * LK + ac4 * 4, ra[i][0], ra[i][1], ra[i][2], ra[i][3]);
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      int q = tid + NTHR * i;
+      int row = sizeof(T) == 2 ? (q >> 2) : (q >> 3);
+      int c = sizeof(T) == 2 ? (q & 3) : (q & 7);
+      *(uint4*)((char*)(B + row * LK) + c * 16) = rbw[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nit > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < nit; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < nit) load(it + 1);
+    mma_tile<T>(As + buf * BM * LK, Bs + buf * BN * LK, wr, wc, lane, acc);
+    if (it + 1 < nit) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const int rbase = m0 + wr * 64 + (lane >> 4) * 4;
+  if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int pc = n0 + wc * 64 + p * 32 + (lane & 15);
+      const int c = (n0 + wc * 64) / 2 + p * 16 + (lane & 15);
+      if (c >= a.C) continue;
+      const float b0 = a.bias ? a.bias[pc] : 0.f;
+      const float b1 = a.bias ? a.bias[pc + 16] : 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rbase + mt * 16 + r;
+          if (row >= a.M) continue;
+          const float v0 = acc[mt][2 * p][r] + b0;
+          const float v1 = acc[mt][2 * p + 1][r] + b1;
+          if (a.epi == EPI_GATE) {
+            a.aux0[(long long)row * a.ld0 + c] = v0;
+            a.aux0[(long long)row * a.ld0 + a.C + c] = v1;
+            a.Y[(long long)row * a.ldy + c] = sigmoidf_(v0) * tanhf(v1);
+          } else {
+            const float xr = a.aux1[(long long)row * a.ld1 + c];
+            a.Y[(long long)row * a.ldy + c] = (xr + v0) * 0.70710678118654752f;
+            float* sk = a.aux0 + (long long)row * a.ld0 + c;
+            *sk = a.accum ? (*sk + v1) : v1;
+          }
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int col = n0 + wc * 64 + nt * 16 + (lane & 15);
+    if (col >= a.N) continue;
+    const float bv = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbase + mt * 16 + r;
+        if (row >= a.M) continue;
+        float v = acc[mt][nt][r] + bv;
+        float* y = a.Y + (long long)row * a.ldy + col;
+        if (a.epi == EPI_PLAIN) {
+          if (a.accum) v += *y;
+          if (a.relu) v = fmaxf(v, 0.f);
+          *y = v;
+        } else if (a.epi == EPI_ADDSCALE) {
+          *y = a.alpha * a.aux1[(long long)row * a.ld1 + col] + v;
+        } else if (a.epi == EPI_GATE_BWD) {
+          const float g = a.aux1[(long long)row * a.ld1 + col];
+          const float f = a.aux1[(long long)row * a.ld1 + a.C + col];
+          const float sg = sigmoidf_(g), th = tanhf(f);
+          a.Y[(long long)row * a.ldy + col] = v * th * sg * (1.f - sg);
+          a.Y[(long long)row * a.ldy + a.C + col] = v * sg * (1.f - th * th);
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------ weight grads
+struct WgradArgs {
+  const float* dy;
+  const float* x;
+  const float* radd;
+  float* part;  // [splits][taps][N][K]
+  int ldy, ldx, K, taps, dil, shift0, pad, Tin, radd_ld;
+  int Tout, M, N, splits, rows_per_split, vecy, vecx;
+};
+
+template <typename T>
+__global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
+  constexpr int LK = Lds<T>::K;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* As = (T*)smem;
+  T* Bs = As + 2 * BM * LK;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int n0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
+  const int j = blockIdx.z % a.taps, s = blockIdx.z / a.taps;
+  const int mbeg = s * a.rows_per_split;
+  const int mend = min(a.M, mbeg + a.rows_per_split);
+  const int nch = mbeg < mend ? (mend - mbeg + BK - 1) / BK : 0;
+
+  // Staging map: lanes walk frames (f = q & 31) so the transposed LDS writes
+  // are contiguous; channel quad c4 = q >> 5.
+  f32x4 ra[4], rx[4];
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = tid + NTHR * i;
+      const int f = q & 31, c4 = q >> 5;
+      const int m = mbeg + ch * BK + f;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
+      if (m < mend) {
+        const int n = n0 + c4 * 4;
+        if (n < a.N) {
+          const float* p = a.dy + (long long)m * a.ldy + n;
+          if (a.vecy && n + 4 <= a.N) v = *(const f32x4*)p;
+          else
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (n + e < a.N) ? p[e] : 0.f;
+        }
+        const int k = k0 + c4 * 4;
+        if (k < a.K) {
+          const int b = m / a.Tout, t = m - b * a.Tout;
+          const int src = pad_src(t + a.shift0 + j * a.dil, a.Tin, a.pad);
+          if (src >= 0) {
+            const float* p = a.x + (long long)(b * a.Tin + src) * a.ldx + k;
+            if (a.vecx && k + 4 <= a.K) w = *(const f32x4*)p;
+            else
+#pragma unroll
+              for (int e = 0; e < 4; ++e) w[e] = (k + e < a.K) ? p[e] : 0.f;
+            if (a.radd) {
+              const float* r = a.radd + (long long)b * a.radd_ld + k;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) if (k + e < a.K) w[e] += r[e];
+            }
+          }
+        }
+      }
+      ra[i] = v;
+      rx[i] = w;
+    }
+  };
+  auto store = [&](int buf) {
+    T* A = As + buf * BM * LK;
+    T* B = Bs + buf * BN * LK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = tid + NTHR * i;
+      const int f = q & 31, c4 = q >> 5;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        A[(c4 * 4 + e) * LK + f] = (T)ra[i][e];
+        B[(c4 * 4 + e) * LK + f] = (T)rx[i][e];
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nch > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const int buf = ch & 1;
+    if (ch + 1 < nch) load(ch + 1);
+    mma_tile<T>(As + buf * BM * LK, Bs + buf * BN * LK, wr, wc, lane, acc);
+    if (ch + 1 < nch) store(buf ^ 1);
+    __syncthreads();
+  }
+  float* out = a.part + ((long long)(s * a.taps + j) * a.N) * a.K;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int k = k0 + wc * 64 + nt * 16 + (lane & 15);
+    if (k >= a.K) continue;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wr * 64 + mt * 16 + (lane >> 4) * 4 + r;
+        if (n < a.N) out[(long long)n * a.K + k] = acc[mt][nt][r];
+      }
+  }
+}
+
+// dst[n*sn + k*sk + j*sj] (+)= sum_s part[s][j][n][k]   (fixed summation order)
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dst,
+                                    int splits, int taps, int N, int K, long long sn,
+                                    long long sk, long long sj, int accum) {
+  const long long total = (long long)taps * N * K;
+  const long long stride = (long long)N * K * taps;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % K);
+    const int n = (int)((i / K) % N);
+    const int j = (int)(i / ((long long)K * N));
+    float v = 0.f;
+    for (int s = 0; s < splits; ++s) v += part[s * stride + i];
+    float* d = dst + n * sn + k * sk + j * sj;
+    *d = accum ? (*d + v) : v;
+  }
+}
+
+// ---------------------------------------------------------- weight packing
+struct PackDesc {
+  const float* src;
+  const float* src2;  // optional second source added element-wise (fused biases)
+  void* dst;
+  long long sn, sk, sj;
+  int N, K, taps, Npad, Kp, perm_c, flip, transpose, dtype;
+  float scale;
+};
+
+__global__ void pack_kernel(const PackDesc* __restrict__ descs) {
+  const PackDesc d = descs[blockIdx.y];
+  const long long total = (long long)d.taps * d.Npad * d.Kp;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % d.Kp);
+    const int n = (int)((i / d.Kp) % d.Npad);
+    const int j = (int)(i / ((long long)d.Kp * d.Npad));
+    // logical (packed) n -> source output row
+    int nn = n;
+    if (d.perm_c > 0) {  // 16-interleave of two halves of width perm_c
+      const int q = n >> 5, w = n & 31;
+      nn = (w < 16) ? q * 16 + w : d.perm_c + q * 16 + (w - 16);
+    }
+    const int jj = d.flip ? (d.taps - 1 - j) : j;
+    const int nlim = d.transpose ? d.K : d.N;
+    const int klim = d.transpose ? d.N : d.K;
+    float v = 0.f;
+    if (nn < nlim && k < klim && n < (d.perm_c > 0 ? 2 * d.perm_c : nlim)) {
+      long long off = d.transpose ? (k * d.sn + (long long)nn * d.sk + jj * d.sj)
+                                  : ((long long)nn * d.sn + k * d.sk + jj * d.sj);
+      v = d.src[off];
+      if (d.src2) v += d.src2[off];
+      v *= d.scale;
+    }
+    if (d.dtype == DT_BF16) ((__bf16*)d.dst)[i] = (__bf16)v;
+    else ((float*)d.dst)[i] = v;
+  }
+}
+
+// --------------------------------------------------------- column reductions
+// part[s][n] = sum over rows [s*rps, (s+1)*rps) of f(Y[row, n]); mode 0: y, 1: (y-mean)^2
+__global__ void colsum_partial_kernel(const float* __restrict__ y, int ld, int M, int N, int rps,
+                                      const float* __restrict__ mean, float* __restrict__ part) {
+  // grid.z = row group (rows [z*M, (z+1)*M)); part layout [group][split][N]
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  const int s = blockIdx.y;
+  y += (long long)blockIdx.z * M * ld;
+  part += (long long)blockIdx.z * gridDim.y * N;
+  const int r0 = s * rps, r1 = min(M, r0 + rps);
+  float acc = 0.f;
+  if (col < N) {
+    const float mu = mean ? mean[col] : 0.f;
+    for (int r = r0 + g; r < r1; r += 4) {
+      float v = y[(long long)r * ld + col];
+      if (mean) { v -= mu; v *= v; }
+      acc += v;
+    }
+  }
+  red[g][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (g == 0 && col < N)
+    part[(long long)s * N + col] = (red[0][threadIdx.x] + red[1][threadIdx.x]) +
+                                   (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ part, int S, int N, float scale,
+                                    float* __restrict__ out, int accum) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= N) return;
+  part += (long long)blockIdx.y * S * N;
+  out += (long long)blockIdx.y * N;
+  double acc = 0.0;
+  for (int s = 0; s < S; ++s) acc += part[(long long)s * N + col];
+  float v = (float)(acc * scale);
+  out[col] = accum ? out[col] + v : v;
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+
+
+ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N,
+                              int Npad, const void* W, int wdtype, const float* bias, float* Y,
+                              int ldy, int epi, int relu, int accum, float* aux0, int ld0,
+                              const float* aux1, int ld1, float alpha, int C, void* stream) {
+  if (nseg < 1 || nseg > 3 || B <= 0 || Tout <= 0 || N <= 0 || Npad % BN != 0 || Npad < N)
+    return ENSVS_E_SHAPE;
+  GemmArgs a{};
+  for (int s = 0; s < nseg; ++s) {
+    const ensvs_conv_seg& g = segs[s];
+    if (g.Kp % BK != 0 || g.Kp < g.K || g.taps < 1) return ENSVS_E_SHAPE;
+    a.seg[s].x = g.x;
+    a.seg[s].radd = g.radd;
+    a.seg[s].wofs = g.wofs;
+    a.seg[s].ld = g.ld;
+    a.seg[s].K = g.K;
+    a.seg[s].taps = g.taps;
+    a.seg[s].dil = g.dil;
+    a.seg[s].shift0 = g.shift0;
+    a.seg[s].pad = g.pad;
+    a.seg[s].radd_ld = g.radd_ld;
+    a.seg[s].Tin = g.Tin;
+    a.seg[s].Kp = g.Kp;
+    a.seg[s].vec = (g.ld % 4 == 0) && (((uintptr_t)g.x & 15) == 0);
+  }
+  a.nseg = nseg;
+  a.Tout = Tout;
+  a.M = B * Tout;
+  a.N = N;
+  a.Npad = Npad;
+  a.W = W;
+  a.bias = bias;
+  a.Y = Y;
+  a.ldy = ldy;
+  a.epi = epi;
+  a.relu = relu;
+  a.accum = accum;
+  a.aux0 = aux0;
+  a.aux1 = aux1;
+  a.ld0 = ld0;
+  a.ld1 = ld1;
+  a.alpha = alpha;
+  a.C = C;
+  dim3 grid(cdiv(a.M, BM), Npad / BN);
+  hipStream_t st = (hipStream_t)stream;
+  if (wdtype == DT_BF16) {
+    size_t lds = 2 * (BM + BN) * Lds<__bf16>::K * sizeof(__bf16);
+    hipLaunchKernelGGL(conv_gemm_kernel<__bf16>, grid, dim3(NTHR), lds, st, a);
+  } else if (wdtype == DT_F32) {
+    size_t lds = 2 * (BM + BN) * Lds<float>::K * sizeof(float);
+    hipLaunchKernelGGL(conv_gemm_kernel<float>, grid, dim3(NTHR), lds, st, a);
+  } else {
+    return ENSVS_E_DTYPE;
+  }
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+// Weight gradient of a conv/linear: dst[n*sn + k*sk + j*sj] (+)= sum_m dY[m,n] X[src(m,j),k].
+// `part` must hold splits*taps*N*K floats.
+ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx, const float* radd,
+                               int radd_ld, int B, int Tout, int Tin, int N, int K, int taps, int dil,
+                               int shift0, int pad, int splits, float* part, float* dst,
+                               long long sn, long long sk, long long sj, int accum, int dtype,
+                               void* stream) {
+  if (B <= 0 || Tout <= 0 || N <= 0 || K <= 0 || taps <= 0 || splits <= 0) return ENSVS_E_SHAPE;
+  WgradArgs a{};
+  a.dy = dy;
+  a.x = x;
+  a.radd = radd;
+  a.part = part;
+  a.ldy = ldy;
+  a.ldx = ldx;
+  a.K = K;
+  a.taps = taps;
+  a.dil = dil;
+  a.shift0 = shift0;
+  a.pad = pad;
+  a.Tin = Tin;
+  a.radd_ld = radd_ld;
+  a.Tout = Tout;
+  a.M = B * Tout;
+  a.N = N;
+  a.splits = splits;
+  a.rows_per_split = (cdiv(a.M, splits) + BK - 1) / BK * BK;
+  a.vecy = (ldy % 4 == 0) && (((uintptr_t)dy & 15) == 0);
+  a.vecx = (ldx % 4 == 0) && (((uintptr_t)x & 15) == 0);
+  dim3 grid(cdiv(N, BM), cdiv(K, BN), taps * splits);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DT_BF16) {
+    size_t lds = 2 * (BM + BN) * Lds<__bf16>::K * sizeof(__bf16);
+    hipLaunchKernelGGL(wgrad_kernel<__bf16>, grid, dim3(NTHR), lds, st, a);
+  } else {
+    size_t lds = 2 * (BM + BN) * Lds<float>::K * sizeof(float);
+    hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(NTHR), lds, st, a);
+  }
+  ENSVS_CHECK_LAUNCH();
+  long long total = (long long)taps * N * K;
+  int blocks = (int)std::min<long long>(4096, (total + 255) / 256);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, part, dst, splits, taps,
+                     N, K, sn, sk, sj, accum);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+
+// Batched weight repack: `descs` is a DEVICE array of `n` descriptors.
+ENSVS_API int ensvs_pack_weights(const ensvs_pack_desc* descs, int n, int max_elems, void* stream) {
+  static_assert(sizeof(ensvs_pack_desc) == sizeof(PackDesc), "desc layout");
+  if (n <= 0) return ENSVS_OK;
+  int bx = std::min(1024, std::max(1, (max_elems + 255) / 256));
+  hipLaunchKernelGGL(pack_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream,
+                     (const PackDesc*)descs);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+// out[g][n] (+)= scale * sum_{m < M} f(Y[g*M + m, n]) for g < groups;
+// f = identity, or (y - mean[n])^2 when mean != null.  `part` holds groups*max_splits*N floats.
+ENSVS_API int ensvs_colsum(const float* y, int ld, int M, int groups, int N, const float* mean,
+                           float scale, float* part, int max_splits, float* out, int accum,
+                           void* stream) {
+  if (M <= 0 || N <= 0 || groups <= 0) return ENSVS_E_SHAPE;
+  int S = std::max(1, std::min(max_splits, M / 64));
+  int rps = cdiv(M, S);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(cdiv(N, 64), S, groups), dim3(256), 0, st, y, ld, M,
+                     N, rps, mean, part);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(N, 256), groups), dim3(256), 0, st, part, S, N,
+                     scale, out, accum);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}

@@ -1,0 +1,156 @@
+"""Thin launch layer over libensvs.so: packed-weight management and GEMM calls.
+
+Everything here only moves pointers and sizes; all arithmetic happens in the
+HIP kernels of ``csrc/``.  Tensors are fp32, channels-last frame rows.
+"""
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+
+from . import _lib
+from ._lib import ConvSeg, PackDesc, call, ptr
+
+BM = 128
+BK = 32
+
+
+def _roundup(x, m):
+    return (x + m - 1) // m * m
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+@dataclass
+class PackedRef:
+    """Where one packed GEMM operand lives inside a PackedBuffer."""
+    offset: int  # elements
+    N: int
+    K: int
+    taps: int
+    Npad: int
+    Kp: int
+
+
+class PackedBuffer:
+    """A set of weights repacked to the GEMM layout [tap][Npad][Kp] by ONE launch.
+
+    Sources are views into the model's flat fp32 parameter buffer; the packed
+    copy is refreshed with :meth:`repack` after every optimizer step.
+    """
+
+    def __init__(self, dtype: int):
+        self.dtype = dtype
+        self.specs = []
+        self.size = 0
+        self.buf = None
+        self._dev_descs = None
+        self._max = 0
+
+    def add(self, src: torch.Tensor, N: int, K: int, taps: int, sn: int, sk: int, sj: int,
+            perm_c: int = 0, flip: bool = False, transpose: bool = False, scale: float = 1.0,
+            src2: Optional[torch.Tensor] = None, npad_to: int = BM, kpad_to: int = BK) -> PackedRef:
+        gn, gk = (K, N) if transpose else (N, K)  # GEMM (rows of packed, reduction)
+        Npad = _roundup(gn, npad_to)
+        Kp = _roundup(gk, kpad_to)
+        ref = PackedRef(self.size, gn, gk, taps, Npad, Kp)
+        self.specs.append(dict(src=src, src2=src2, sn=sn, sk=sk, sj=sj, N=N, K=K, taps=taps,
+                               Npad=Npad, Kp=Kp, perm_c=perm_c, flip=int(flip),
+                               transpose=int(transpose), scale=float(scale), ref=ref))
+        n = taps * Npad * Kp
+        self.size += _roundup(n, 64)
+        self._max = max(self._max, n)
+        return ref
+
+    def finalize(self, device):
+        tdtype = torch.bfloat16 if self.dtype == _lib.DT_BF16 else torch.float32
+        self.buf = torch.zeros(max(self.size, 64), dtype=tdtype, device=device)
+        n = len(self.specs)
+        arr = (PackDesc * max(n, 1))()
+        esz = self.buf.element_size()
+        for i, s in enumerate(self.specs):
+            d = arr[i]
+            d.src = s["src"].data_ptr()
+            d.src2 = None if s["src2"] is None else s["src2"].data_ptr()
+            d.dst = self.buf.data_ptr() + s["ref"].offset * esz
+            d.sn, d.sk, d.sj = s["sn"], s["sk"], s["sj"]
+            d.N, d.K, d.taps, d.Npad, d.Kp = s["N"], s["K"], s["taps"], s["Npad"], s["Kp"]
+            d.perm_c, d.flip, d.transpose = s["perm_c"], s["flip"], s["transpose"]
+            d.dtype, d.scale = self.dtype, s["scale"]
+        raw = bytes(arr)
+        host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+        self._dev_descs = host.to(device)
+        self._n = n
+
+    def repack(self):
+        if self._n:
+            call("ensvs_pack_weights", self._dev_descs.data_ptr(), self._n, self._max, stream())
+
+
+@dataclass
+class Seg:
+    """One K-segment of a GEMM's activation operand."""
+    x: torch.Tensor         # any tensor whose data_ptr is the segment's first channel of frame 0
+    ld: int                 # row stride (floats)
+    K: int                  # channels
+    ref: PackedRef          # packed weights of this segment
+    Tin: int
+    taps: int = 1
+    dil: int = 1
+    shift0: int = 0
+    pad: int = _lib.PAD_ZERO
+    radd: Optional[torch.Tensor] = None
+    radd_ld: int = 0
+    xoff: int = 0           # element offset added to x.data_ptr()
+
+
+def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: int,
+         bias=None, epi=_lib.EPI_PLAIN, relu=False, accum=False, aux0=None, ld0=0, aux1=None,
+         ld1=0, alpha=0.0, C=0, yoff=0, bias_off=0):
+    arr = (ConvSeg * len(segs))()
+    Npad = segs[0].ref.Npad
+    for i, s in enumerate(segs):
+        assert s.ref.Npad == Npad and s.ref.taps == s.taps and s.ref.Kp >= s.K
+        d = arr[i]
+        d.x = s.x.data_ptr() + 4 * s.xoff
+        d.radd = None if s.radd is None else s.radd.data_ptr()
+        d.wofs = s.ref.offset
+        d.ld, d.K, d.taps, d.dil, d.shift0 = s.ld, s.K, s.taps, s.dil, s.shift0
+        d.pad, d.radd_ld, d.Tin, d.Kp = s.pad, s.radd_ld, s.Tin, s.ref.Kp
+    bptr = None if bias is None else bias.data_ptr() + 4 * bias_off
+    call("ensvs_conv_gemm", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,
+         W.buf.data_ptr(), W.dtype, bptr, Y.data_ptr() + 4 * yoff, ldy, epi, int(relu),
+         int(accum), ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, stream())
+
+
+_part_cache = {}
+
+
+def scratch(nfloats, device, key="part"):
+    t = _part_cache.get((key, device))
+    if t is None or t.numel() < nfloats:
+        t = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
+        _part_cache[(key, device)] = t
+    return t
+
+
+def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, sk, sj,
+          accum=False, dtype=_lib.DT_BF16, radd=None, radd_ld=0, dyoff=0, xoff=0, splits=None):
+    M = B * Tout
+    if splits is None:
+        tiles = -(-N // 128) * -(-K // 128) * taps
+        splits = max(1, min(64, 512 // max(tiles, 1), -(-M // 256)))
+    part = scratch(splits * taps * N * K, dy.device)
+    call("ensvs_conv_wgrad", dy.data_ptr() + 4 * dyoff, ldy, x.data_ptr() + 4 * xoff, ldx,
+         ptr(radd), radd_ld, B, Tout, Tin, N, K, taps, dil, shift0, pad, splits,
+         part.data_ptr(), dst.data_ptr(), sn, sk, sj, int(accum), dtype, stream())
+
+
+def colsum(y, ld, M, N, out, groups=1, mean=None, scale=1.0, accum=False, yoff=0):
+    max_splits = 64
+    part = scratch(groups * max_splits * N, y.device, key="colsum")
+    call("ensvs_colsum", y.data_ptr() + 4 * yoff, ld, M, groups, N, ptr(mean), float(scale),
+         part.data_ptr(), max_splits, out.data_ptr(), int(accum), stream())

@@ -1,0 +1,156 @@
+"""Numerics of the MFMA implicit-GEMM engine against plain PyTorch fp32 ops."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from ensemble_svs_with_interactions_amd import kernels as K
+from ensemble_svs_with_interactions_amd import _lib as L
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+def pack(dtype, w, transpose=False, flip=False, perm_c=0, scale=1.0, src2=None):
+    """w: Conv1d weight (N, K, taps)."""
+    pb = K.PackedBuffer(dtype)
+    N, Kc, taps = w.shape
+    ref = pb.add(w, N, Kc, taps, Kc * taps, taps, 1, perm_c=perm_c, flip=flip,
+                 transpose=transpose, scale=scale, src2=src2)
+    pb.finalize(w.device)
+    pb.repack()
+    return pb, ref
+
+
+@pytest.mark.parametrize("dt,tol", [(L.DT_F32, 2e-5), (L.DT_BF16, 2e-2)])
+@pytest.mark.parametrize("taps,dil,pad", [(1, 1, L.PAD_ZERO), (7, 1, L.PAD_REFLECT),
+                                          (3, 2, L.PAD_ZERO), (3, 4, L.PAD_REPLICATE)])
+def test_conv_fwd(dt, tol, taps, dil, pad):
+    torch.manual_seed(0)
+    B, T, Cin, Cout = 3, 57, 70, 133
+    x = torch.randn(B, T, Cin, device=DEV)
+    w = torch.randn(Cout, Cin, taps, device=DEV) / (Cin * taps) ** 0.5
+    b = torch.randn(Cout, device=DEV)
+    half = (taps - 1) // 2 * dil
+    mode = {L.PAD_ZERO: "constant", L.PAD_REFLECT: "reflect", L.PAD_REPLICATE: "replicate"}[pad]
+    xp = F.pad(x.transpose(1, 2), (half, half), mode=mode)
+    ref = F.conv1d(xp, w, b, dilation=dil).transpose(1, 2)
+    pb, r = pack(dt, w)
+    y = torch.empty(B, T, Cout, device=DEV)
+    K.gemm([K.Seg(x, Cin, Cin, r, T, taps=taps, dil=dil, shift0=-half, pad=pad)], B, T, Cout,
+           pb, y, Cout, bias=b)
+    torch.cuda.synchronize()
+    assert rel(y, ref) < tol
+
+
+@pytest.mark.parametrize("dt,tol", [(L.DT_F32, 2e-5), (L.DT_BF16, 2e-2)])
+def test_diffnet_gate_and_resskip(dt, tol):
+    torch.manual_seed(1)
+    B, T, C, E, dil = 2, 45, 64, 48, 2
+    x = torch.randn(B, T, C, device=DEV)
+    cond = torch.randn(B, T, E, device=DEV)
+    d = torch.randn(B, C, device=DEV)
+    wd = torch.randn(2 * C, C, 3, device=DEV) / (3 * C) ** 0.5
+    bd = torch.randn(2 * C, device=DEV)
+    wc = torch.randn(2 * C, E, 1, device=DEV) / E ** 0.5
+    bc = torch.randn(2 * C, device=DEV)
+    wo = torch.randn(2 * C, C, 1, device=DEV) / C ** 0.5
+    bo = torch.randn(2 * C, device=DEV)
+    # reference (denoiser.py ResidualBlock with pre-projected diffusion step d)
+    y = x.transpose(1, 2) + d[:, :, None]
+    yy = F.conv1d(y, wd, bd, padding=dil, dilation=dil) + F.conv1d(cond.transpose(1, 2), wc, bc)
+    gate, filt = yy.chunk(2, dim=1)
+    z = torch.sigmoid(gate) * torch.tanh(filt)
+    o = F.conv1d(z, wo, bo)
+    res, skip = o.chunk(2, dim=1)
+    xn_ref = ((x.transpose(1, 2) + res) / 2 ** 0.5).transpose(1, 2)
+
+    pb = K.PackedBuffer(dt)
+    rd = pb.add(wd, 2 * C, C, 3, 3 * C, 3, 1, perm_c=C)
+    rc = pb.add(wc, 2 * C, E, 1, E, 1, 1, perm_c=C)
+    ro = pb.add(wo, 2 * C, C, 1, C, 1, 1, perm_c=C)
+    pb.finalize(DEV)
+    pb.repack()
+    bb = K.PackedBuffer(L.DT_F32)
+    rbg = bb.add(bd.view(-1, 1, 1), 2 * C, 1, 1, 1, 1, 1, perm_c=C, src2=bc.view(-1, 1, 1), kpad_to=1)
+    rbo = bb.add(bo.view(-1, 1, 1), 2 * C, 1, 1, 1, 1, 1, perm_c=C, kpad_to=1)
+    bb.finalize(DEV)
+    bb.repack()
+
+    Z = torch.empty(B, T, C, device=DEV)
+    GF = torch.empty(B, T, 2 * C, device=DEV)
+    K.gemm([K.Seg(x, C, C, rd, T, taps=3, dil=dil, shift0=-dil, radd=d, radd_ld=C),
+            K.Seg(cond, E, E, rc, T)], B, T, 2 * C, pb, Z, C, bias=bb.buf, bias_off=rbg.offset,
+           epi=L.EPI_GATE, aux0=GF, ld0=2 * C, C=C)
+    skip_acc = torch.full((B, T, C), 0.5, device=DEV)
+    xn = torch.empty(B, T, C, device=DEV)
+    K.gemm([K.Seg(Z, C, C, ro, T)], B, T, 2 * C, pb, xn, C, bias=bb.buf, bias_off=rbo.offset,
+           epi=L.EPI_RESSKIP, aux0=skip_acc, ld0=C, aux1=x, ld1=C, accum=True, C=C)
+    torch.cuda.synchronize()
+    assert rel(Z, z.transpose(1, 2)) < tol
+    assert rel(GF[..., :C], gate.transpose(1, 2)) < tol
+    assert rel(GF[..., C:], filt.transpose(1, 2)) < tol
+    assert rel(xn, xn_ref) < tol
+    assert rel(skip_acc, skip.transpose(1, 2) + 0.5) < tol
+
+
+@pytest.mark.parametrize("dt,tol", [(L.DT_F32, 2e-5), (L.DT_BF16, 2e-2)])
+def test_conv_dgrad_wgrad(dt, tol):
+    torch.manual_seed(2)
+    B, T, Cin, Cout, taps, dil = 2, 70, 36, 150, 3, 2
+    x = torch.randn(B, T, Cin, device=DEV, requires_grad=True)
+    w = (torch.randn(Cout, Cin, taps, device=DEV) / (Cin * taps) ** 0.5).requires_grad_()
+    y = F.conv1d(x.transpose(1, 2), w, padding=dil, dilation=dil).transpose(1, 2)
+    g = torch.randn(y.shape, device=DEV)
+    y.backward(g)
+    # dgrad: conv over g with flipped, transposed weights
+    pb, r = pack(dt, w.detach(), transpose=True, flip=True)
+    dx = torch.empty(B, T, Cin, device=DEV)
+    K.gemm([K.Seg(g, Cout, Cout, r, T, taps=taps, dil=dil, shift0=-dil)], B, T, Cin, pb, dx, Cin)
+    dw = torch.empty(Cout, Cin, taps, device=DEV)
+    K.wgrad(g, Cout, x.detach(), Cin, B, T, T, Cout, Cin, taps, dil, -dil, L.PAD_ZERO, dw,
+            Cin * taps, taps, 1, dtype=dt)
+    torch.cuda.synchronize()
+    assert rel(dx, x.grad) < tol
+    assert rel(dw, w.grad) < tol
+
+
+@pytest.mark.parametrize("dt,tol", [(L.DT_F32, 2e-5), (L.DT_BF16, 2e-2)])
+def test_reflect_wgrad_and_full_dgrad(dt, tol):
+    torch.manual_seed(3)
+    B, T, Cin, Cout = 2, 40, 20, 24
+    x = torch.randn(B, T, Cin, device=DEV, requires_grad=True)
+    w = (torch.randn(Cout, Cin, 7, device=DEV) / (Cin * 7) ** 0.5).requires_grad_()
+    y = F.conv1d(F.pad(x.transpose(1, 2), (3, 3), mode="reflect"), w).transpose(1, 2)
+    g = torch.randn(y.shape, device=DEV)
+    y.backward(g)
+    dw = torch.empty(Cout, Cin, 7, device=DEV)
+    K.wgrad(g, Cout, x.detach(), Cin, B, T, T, Cout, Cin, 7, 1, -3, L.PAD_REFLECT, dw,
+            Cin * 7, 7, 1, dtype=dt)
+    # full conv -> gradient of the padded input, then fold the reflection
+    pb, r = pack(dt, w.detach(), transpose=True, flip=True)
+    dxp = torch.empty(B, T + 6, Cin, device=DEV)
+    K.gemm([K.Seg(g, Cout, Cout, r, T, taps=7, dil=1, shift0=-6)], B, T + 6, Cin, pb, dxp, Cin)
+    torch.cuda.synchronize()
+    ref_p = torch.zeros(B, T + 6, Cin, device=DEV)
+    xp = F.pad(x.detach().transpose(1, 2), (3, 3), mode="reflect").requires_grad_()
+    F.conv1d(xp, w.detach()).transpose(1, 2).backward(g)
+    assert rel(dxp, xp.grad.transpose(1, 2)) < tol
+    assert rel(dw, w.grad) < tol
+
+
+def test_colsum_grouped():
+    torch.manual_seed(4)
+    y = torch.randn(3, 333, 70, device=DEV)
+    out = torch.empty(3, 70, device=DEV)
+    K.colsum(y, 70, 333, 70, out, groups=3)
+    mean = y.reshape(-1, 70).mean(0)
+    var = torch.empty(70, device=DEV)
+    K.colsum(y, 70, 999, 70, var, mean=mean, scale=1.0 / 999)
+    torch.cuda.synchronize()
+    assert rel(out, y.sum(1)) < 1e-5
+    assert rel(var, y.reshape(-1, 70).var(0, unbiased=False)) < 1e-5

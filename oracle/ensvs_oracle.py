@@ -88,6 +88,8 @@ def conv_stack(P, prefix, x, training, bn_updates=None, momentum=0.1, eps=1e-5):
         rv = P[bn + ".running_var"].clone()
         h = F.batch_norm(h, rm, rv, P[bn + ".weight"], P[bn + ".bias"], training, momentum, eps)
         if bn_updates is not None and training:
+            # running statistics are module state: later calls see this update
+            P[bn + ".running_mean"], P[bn + ".running_var"] = rm, rv
             bn_updates.setdefault(bn, []).append((rm, rv))
         h = F.relu(h)
     return h.transpose(1, 2)

@@ -1,0 +1,486 @@
+"""Generate the golden fixtures in tests/golden/ FROM THE REFERENCE ITSELF.
+
+Runs only in the build container (the reference lives at /root/reference and
+never travels):   python tests/golden/gen_goldens.py
+
+The reference package is imported with a stub loader for absent,
+non-arithmetic dependencies (pyworld, librosa, hydra, ...).
+Parameters come from oracle/weights.py (seeded by key), random draws
+(AR-decoder dropout masks, diffusion t / noise) are injected so that the
+oracle and the HIP path can replay them.  Fixtures store inputs, draws and
+outputs only; weights are regenerated from the seed.
+
+Deviation recorded for capture: nn.LSTM's internal inter-layer dropout of
+the V/UV model (p=0.1) draws from torch's C++ RNG and cannot be replayed, so
+training-mode goldens run it with dropout=0.
+"""
+import importlib.abc
+import importlib.machinery
+import json
+import logging
+import os
+import sys
+import tempfile
+import types
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, "/root/reference")
+sys.dont_write_bytecode = True
+
+STUB_ROOTS = {"pyworld", "pysptk", "librosa", "pyloudnorm", "nnmnkwii", "mlflow", "h5py",
+              "torchaudio", "tkinter", "hydra", "omegaconf", "tensorboard", "pysinsy", "soundfile"}
+
+
+class _AnyObj:
+    def __call__(self, *a, **k):
+        return _AnyObj()
+
+    def __getattr__(self, n):
+        return _AnyObj()
+
+    def __mro_entries__(self, bases):
+        return (object,)
+
+
+class _Any(types.ModuleType):
+    def __getattr__(self, n):
+        if n.startswith("__"):
+            raise AttributeError(n)
+        return _AnyObj()
+
+
+class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
+    def find_spec(self, name, path, target=None):
+        if name.split(".")[0] in STUB_ROOTS:
+            return importlib.machinery.ModuleSpec(name, self, is_package=True)
+
+    def create_module(self, spec):
+        return _Any(spec.name)
+
+    def exec_module(self, m):
+        m.__path__ = []
+
+
+sys.meta_path.insert(0, _Finder())
+_tb = types.ModuleType("torch.utils.tensorboard")
+_tb.SummaryWriter = object
+sys.modules["torch.utils.tensorboard"] = _tb
+import matplotlib  # noqa: E402
+
+matplotlib.use("Agg")
+import matplotlib.pyplot as plt  # noqa: E402
+
+plt.style.use = lambda *a, **k: None
+
+import torch  # noqa: E402
+import torch.nn.functional as TF  # noqa: E402
+
+import nnsvs.acoustic_models.tacotron_f0 as ref_tacotron_f0  # noqa: E402
+import nnsvs.diffsinger.diffusion as ref_diffusion  # noqa: E402
+from nnsvs.acoustic_models.util import pad_inference_multitrack  # noqa: E402
+from nnsvs.bin.train_acoustic_multitrack import train_step as ref_train_step  # noqa: E402
+from nnsvs import train_util as ref_train_util  # noqa: E402
+from nnsvs.util import make_non_pad_mask as ref_make_non_pad_mask  # noqa: E402
+
+from ensemble_svs_with_interactions_amd import configs, data  # noqa: E402
+from oracle.weights import seeded_state_dict  # noqa: E402
+
+SEED = 20250321
+torch.set_num_threads(8)
+
+
+# ------------------------------------------------------------ injection
+
+class _DropoutF:
+    """Proxy for tacotron_f0.F whose dropout() replays queued keep masks."""
+
+    def __init__(self):
+        self.queue = []
+        self.log = []
+
+    def __getattr__(self, n):
+        return getattr(TF, n)
+
+    def dropout(self, x, p=0.5, training=True, inplace=False):
+        m = self.queue.pop(0)
+        self.log.append(m)
+        return x * m
+
+
+DROP = _DropoutF()
+ref_tacotron_f0.F = DROP
+
+
+class inject_diffusion:
+    """Replace torch.randint / torch.randn_like / torch.randn with queued draws."""
+
+    def __init__(self, ints=(), normals=()):
+        self.ints = list(ints)
+        self.normals = list(normals)
+
+    def __enter__(self):
+        self.saved = (torch.randint, torch.randn_like, torch.randn)
+        torch.randint = lambda *a, **k: self.ints.pop(0)
+        torch.randn_like = lambda x, **k: self.normals.pop(0)
+        torch.randn = lambda *a, **k: self.normals.pop(0)
+        # p_sample binds noise_fn=torch.randn at definition time (diffusion.py:194)
+        self.saved_defaults = ref_diffusion.GaussianDiffusion.p_sample.__wrapped__.__defaults__
+        ref_diffusion.GaussianDiffusion.p_sample.__wrapped__.__defaults__ = (torch.randn,) + \
+            self.saved_defaults[1:]
+        return self
+
+    def __exit__(self, *exc):
+        torch.randint, torch.randn_like, torch.randn = self.saved
+        ref_diffusion.GaussianDiffusion.p_sample.__wrapped__.__defaults__ = self.saved_defaults
+        assert not self.ints and not self.normals, "unconsumed draws"
+
+
+def build_ref(cfg_mine, seed=SEED):
+    cfg = configs.to_reference_targets(cfg_mine)
+    torch.manual_seed(0)
+    model = configs.instantiate(cfg)
+    shapes = {k: tuple(v.shape) for k, v in model.state_dict().items()}
+    sd = seeded_state_dict(shapes, seed)
+    missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()},
+                                                strict=False)
+    assert not unexpected
+    return model, shapes
+
+
+def rng_for(name):
+    return np.random.default_rng([SEED, zlib.crc32(name.encode())])
+
+
+def grad_summary(module, prefix=""):
+    """{key: [sum, abs-sum, l2]} of every parameter gradient (float64)."""
+    out = {}
+    for k, p in module.named_parameters():
+        g = p.grad
+        if g is None:
+            out[prefix + k] = [0.0, 0.0, 0.0]
+        else:
+            g = g.double()
+            out[prefix + k] = [g.sum().item(), g.abs().sum().item(), g.norm().item()]
+    return out
+
+
+def save(name, arrays, meta):
+    path = os.path.join(HERE, name + ".npz")
+    arrays = {k: np.asarray(v) for k, v in arrays.items()}
+    arrays["meta_json"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez_compressed(path, **arrays)
+    print(f"{name}: {os.path.getsize(path) / 1e6:.2f} MB")
+
+
+def T_(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def ar_masks(name, B, Tr):
+    r = rng_for(name)
+    return (r.random((B, Tr, 1)) < 0.5).astype(np.float32) * 2.0
+
+
+# ---------------------------------------------------------------- cases
+
+def case_diffnet(model, which, B, T, full_grads):
+    gd = getattr(model, which + "_model")
+    net = gd.denoise_fn
+    M = net.in_dim
+    E = net.residual_layers[0].conditioner_projection.in_channels
+    r = rng_for("diffnet_" + which)
+    spec = r.standard_normal((B, 1, M, T)).astype(np.float32) * 0.5
+    t = r.integers(0, 100, size=B).astype(np.int64)
+    cond = r.standard_normal((B, E, T)).astype(np.float32)
+    R = r.standard_normal((B, 1, M, T)).astype(np.float32)
+    spec_t = T_(spec).requires_grad_()
+    cond_t = T_(cond).requires_grad_()
+    net.zero_grad()
+    out = net(spec_t, T_(t), cond_t)
+    (out * T_(R)).sum().backward()
+    arrays = dict(spec=spec, t=t, cond=cond, R=R, out=out.detach().numpy(),
+                  d_spec=spec_t.grad.numpy(), d_cond=cond_t.grad.numpy())
+    for k in full_grads:
+        arrays["grad::" + k] = dict(net.named_parameters())[k].grad.numpy()
+    meta = dict(prefix=f"{which}_model.denoise_fn.", grad_summary=grad_summary(net))
+    save(f"diffnet_{which}", arrays, meta)
+
+
+def case_ffconvlstm(model, which, B, T, lengths):
+    enc = {"mgc": model.mgc_model.encoder, "bap": model.bap_model.encoder,
+           "vuv": model.vuv_model}[which]
+    prefix = {"mgc": "mgc_model.encoder.", "bap": "bap_model.encoder.", "vuv": "vuv_model."}[which]
+    enc.train()
+    if which == "vuv":
+        enc.lstm.dropout = 0.0
+    batch = data.synthetic_batch(B, T, SEED + 7, lengths=lengths)
+    if which == "vuv":
+        x = np.concatenate([batch["x_main"], batch["y_main"][:, :, :60],
+                            batch["y_main"][:, :, 60:61]], -1)
+    else:
+        x = np.concatenate([batch["x_main"], batch["y_main"][:, :, 60:61]], -1)
+    r = rng_for("ffconvlstm_" + which)
+    spk = (0.3 * r.standard_normal((B, 1, enc.emb.embedding_dim))).astype(np.float32)
+    spk_t = T_(spk).requires_grad_()
+    enc.zero_grad()
+    out = enc(T_(x), T_(batch["lengths"]), spk_embs=spk_t.expand(B, T, -1))
+    R = r.standard_normal(tuple(out.shape)).astype(np.float32)
+    (out * T_(R)).sum().backward()
+    bn = {k: v.numpy().copy() for k, v in enc.state_dict().items() if "running" in k}
+    arrays = dict(x=x, lengths=batch["lengths"], spk=spk, R=R, out=out.detach().numpy(),
+                  d_spk=spk_t.grad.numpy(), **{"bn::" + k: v for k, v in bn.items()})
+    meta = dict(prefix=prefix, grad_summary=grad_summary(enc))
+    save(f"ffconvlstm_{which}", arrays, meta)
+
+
+def case_lf0(model, B, T, lengths):
+    lm = model.lf0_model
+    lm.train()
+    model._set_lf0_params()
+    batch = data.synthetic_batch(B, T, SEED + 11, lengths=lengths)
+    r = rng_for("lf0")
+    E = model.speaker_embedding.emb.embedding_dim
+    s0 = (0.3 * r.standard_normal((B, 1, E))).astype(np.float32)
+    s1 = (0.3 * r.standard_normal((B, 1, E))).astype(np.float32)
+    s0_t, s1_t = T_(s0).requires_grad_(), T_(s1).requires_grad_()
+    masks = ar_masks("lf0_masks", B, T // 4)
+    DROP.queue = [T_(masks[:, t]) for t in range(T // 4)]
+    lm.zero_grad()
+    lf0, res = lm(T_(batch["x_main"]), T_(batch["x_sub"]), s0_t.expand(B, T, -1),
+                  s1_t.expand(B, T, -1), T_(batch["lengths"]))
+    assert not DROP.queue
+    R1 = r.standard_normal(tuple(lf0.shape)).astype(np.float32)
+    R2 = r.standard_normal(tuple(res.shape)).astype(np.float32)
+    ((lf0 * T_(R1)).sum() + (res * T_(R2)).sum()).backward()
+    bn = {k: v.numpy().copy() for k, v in lm.state_dict().items() if "running" in k}
+    arrays = dict(x_main=batch["x_main"], x_sub=batch["x_sub"], lengths=batch["lengths"],
+                  spk_main=s0, spk_sub=s1, masks=masks, R1=R1, R2=R2,
+                  lf0=lf0.detach().numpy(), res=res.detach().numpy(),
+                  d_spk_main=s0_t.grad.numpy(), d_spk_sub=s1_t.grad.numpy(),
+                  **{"bn::" + k: v for k, v in bn.items()})
+    meta = dict(prefix="lf0_model.", grad_summary=grad_summary(lm),
+                lf0_stats={k: getattr(model, k) for k in configs.LF0_STATS})
+    save("lf0_model", arrays, meta)
+
+
+def model_draws(name, P, T, cfg):
+    r = rng_for(name)
+    d = dict(lf0_main=ar_masks(name + "_lm", P, T // 4), lf0_sub=ar_masks(name + "_ls", P, T // 4),
+             mgc_t=r.integers(0, 100, size=P).astype(np.int64),
+             mgc_noise=r.standard_normal((P, 1, 60, T)).astype(np.float32),
+             bap_t=r.integers(0, 100, size=P).astype(np.int64),
+             bap_noise=r.standard_normal((P, 1, 5, T)).astype(np.float32))
+    return d
+
+
+def queue_draws(d, T):
+    DROP.queue = [T_(d["lf0_main"][:, t]) for t in range(T // 4)] + \
+                 [T_(d["lf0_sub"][:, t]) for t in range(T // 4)]
+    return inject_diffusion(ints=[T_(d["mgc_t"]), T_(d["bap_t"])],
+                            normals=[T_(d["mgc_noise"]), T_(d["bap_noise"])])
+
+
+def case_model_forward_full():
+    cfg = configs.multitrack_diffusion(num_speakers=4)
+    model, shapes = build_ref(cfg)
+    model.train()
+    model.vuv_model.lstm.dropout = 0.0
+    P, T = 2, 32
+    batch = data.synthetic_batch(P, T, SEED + 13, lengths=[32, 28])
+    d = model_draws("fwd_full", P, T, cfg)
+    with queue_draws(d, T):
+        ((mgc, lf0, vuv, bap), res), sub = model(
+            T_(batch["x_main"]), T_(batch["x_sub"]),
+            (T_(batch["spk_main"]).int(), T_(batch["spk_sub"]).int()),
+            lengths=T_(batch["lengths"]), ys=[T_(batch["y_main"]), T_(batch["y_sub"])])
+    assert sub == (None, None) and not DROP.queue
+    arrays = dict(**{k: v for k, v in batch.items()}, **{"draw::" + k: v for k, v in d.items()},
+                  mgc_noise_out=mgc[0].detach().numpy(), mgc_recon=mgc[1].detach().numpy(),
+                  lf0=lf0.detach().numpy(), vuv=vuv.detach().numpy(),
+                  bap_noise_out=bap[0].detach().numpy(), bap_recon=bap[1].detach().numpy(),
+                  res=res.detach().numpy())
+    save("model_forward_full", arrays, dict(shapes={k: list(v) for k, v in shapes.items()}))
+    return model, shapes
+
+
+def case_train_step_tiny(steps=2, lr=1e-3):
+    cfg = configs.multitrack_diffusion(num_speakers=4, tiny=True)
+    model, shapes = build_ref(cfg)
+    model.vuv_model.lstm.dropout = 0.0
+    P, T = 3, 48
+    batch = data.synthetic_batch(P, T, SEED + 17, lengths=[48, 40, 32])
+    opt = torch.optim.Adam(model.parameters(), lr=lr, betas=(0.9, 0.999), weight_decay=0.0)
+    model_config = types.SimpleNamespace(stream_sizes=[60, 1, 1, 5])
+    optim_config = types.SimpleNamespace(clip_norm=1.0)
+    logger = logging.getLogger("golden")
+    before = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    arrays = dict(**{k: v for k, v in batch.items()})
+    meta = dict(shapes={k: list(v) for k, v in shapes.items()}, lr=lr, steps=steps)
+    losses, norms = [], []
+    for s in range(steps):
+        d = model_draws(f"tiny_step{s}", P, T, cfg)
+        for k, v in d.items():
+            arrays[f"draw{s}::{k}"] = v
+        # record the grad norm that clip_grad_norm_ returns
+        norm_box = {}
+        orig = torch.nn.utils.clip_grad_norm_
+
+        def clip(params, max_norm, *a, **k):
+            n = orig(params, max_norm, *a, **k)
+            norm_box["n"] = float(n)
+            return n
+        torch.nn.utils.clip_grad_norm_ = clip
+        try:
+            with queue_draws(d, T):
+                loss, metrics = ref_train_step(
+                    logger, model, model_config, optim_config, opt, None, True,
+                    (T_(batch["x_main"]), T_(batch["x_sub"])),
+                    [T_(batch["y_main"]), T_(batch["y_sub"])],
+                    (T_(batch["spk_main"]).int(), T_(batch["spk_sub"]).int()),
+                    (T_(batch["lengths"]), T_(batch["lengths"])),
+                    None, None, feats_criterion="l1", pitch_reg_weight=0.0,
+                    logf0_diff_weight=0.0, mgc_diff_weight=0.0)
+        finally:
+            torch.nn.utils.clip_grad_norm_ = orig
+        losses.append(float(loss))
+        norms.append(norm_box["n"])
+        after = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        if s == 0:
+            for k in after:
+                if after[k].dtype == torch.float32:
+                    arrays[f"delta0::{k}"] = (after[k] - before[k]).numpy()
+    for k, v in model.state_dict().items():
+        if v.dtype == torch.float32:
+            arrays[f"final::{k}"] = v.numpy()
+    meta.update(losses=losses, grad_norms=norms)
+    save("train_step_tiny", arrays, meta)
+
+
+def case_inference_bap(model):
+    gd = model.bap_model
+    gd.eval()
+    B, T = 1, 32
+    batch = data.synthetic_batch(B, T, SEED + 19)
+    cond_in = np.concatenate([batch["x_main"], batch["y_main"][:, :, 60:61]], -1)
+    r = rng_for("inference_bap")
+    spk = (0.3 * r.standard_normal((B, 1, 256))).astype(np.float32)
+    noises = r.standard_normal((101, B, 1, 5, T)).astype(np.float32)
+    with torch.no_grad(), inject_diffusion(normals=[T_(n) for n in noises]):
+        out = gd.inference(T_(cond_in), T_(batch["lengths"]), spk_embs=T_(spk).expand(B, T, -1))
+    save("inference_bap", dict(cond_in=cond_in, lengths=batch["lengths"], spk=spk, noises=noises,
+                               out=out.numpy()), {})
+
+
+def case_model_inference_tiny():
+    cfg = configs.multitrack_diffusion(num_speakers=4, tiny=True)
+    model, shapes = build_ref(cfg)
+    model.eval()
+    arrays, meta = {}, {}
+    for T in (28, 29, 30, 31):
+        batch = data.synthetic_batch(1, T, SEED + 23 + T)
+        pad = 4 - T % 4
+        Tp = T + pad
+        r = rng_for(f"inf_tiny_{T}")
+        masks = ar_masks(f"inf_tiny_masks_{T}", 2, Tp // 4)
+        nm = r.standard_normal((101, 1, 1, 60, Tp)).astype(np.float32)
+        nb = r.standard_normal((101, 1, 1, 5, Tp)).astype(np.float32)
+        DROP.queue = [T_(masks[0:1, t]) for t in range(Tp // 4)] + \
+                     [T_(masks[1:2, t]) for t in range(Tp // 4)]
+        with torch.no_grad(), inject_diffusion(normals=[T_(n) for n in nm] + [T_(n) for n in nb]):
+            out = model.inference(T_(batch["x_main"]), T_(batch["x_sub"]),
+                                  spks=(T_(batch["spk_main"]).int(), T_(batch["spk_sub"]).int()),
+                                  lengths=T_(batch["lengths"]))
+        assert not DROP.queue
+        for k in ("x_main", "x_sub", "spk_main", "spk_sub", "lengths"):
+            arrays[f"T{T}::{k}"] = batch[k]
+        arrays[f"T{T}::masks"] = masks
+        arrays[f"T{T}::noise_mgc"] = nm
+        arrays[f"T{T}::noise_bap"] = nb
+        arrays[f"T{T}::out"] = out.numpy()
+        meta[f"T{T}"] = dict(pad=pad, out_shape=list(out.shape))
+    meta["shapes"] = {k: list(v) for k, v in shapes.items()}
+    save("model_inference_tiny", arrays, meta)
+
+
+def case_data_path():
+    """Integer/byte fixtures: pairing, collation, masks (bit-exact)."""
+    r = rng_for("data_path")
+    arrays, meta = {}, {}
+    with tempfile.TemporaryDirectory() as d:
+        names = []
+        for spk in ("Vo1", "S1", "ritsu", "A2"):
+            for seg in ("seg01", "seg02", "songB_003"):
+                if spk == "A2" and seg == "seg02":
+                    continue
+                n = int(r.integers(20, 60))
+                np.save(os.path.join(d, f"{spk}_{seg}-feats.npy"), np.zeros((n, 3), np.float32))
+                names.append(f"{spk}_{seg}")
+        pairs, plens = ref_train_util.get_filtered_files_multitrack(d, None)
+        meta["pairs"] = [[os.path.basename(a), os.path.basename(b)] for a, b in pairs]
+        meta["pair_lengths"] = [[int(a), int(b)] for a, b in plens]
+        files = sorted(os.path.join(d, f) for f in os.listdir(d))
+        meta["files"] = [os.path.basename(f) for f in files]
+        meta["file_lengths"] = [int(len(np.load(f))) for f in files]
+    batch = []
+    for i in range(5):
+        n0, n1 = int(r.integers(17, 40)), int(r.integers(17, 40))
+        x0 = r.standard_normal((n0, 6)).astype(np.float32)
+        y0 = r.standard_normal((n0, 4)).astype(np.float32)
+        x1 = r.standard_normal((n1, 6)).astype(np.float32)
+        y1 = r.standard_normal((n1, 4)).astype(np.float32)
+        batch.append((x0, y0, int(r.integers(0, 3)), np.zeros(3), x1, y1, int(r.integers(0, 3)),
+                      np.zeros(3)))
+        for k, v in dict(x0=x0, y0=y0, x1=x1, y1=y1).items():
+            arrays[f"in{i}::{k}"] = v
+        arrays[f"in{i}::spk"] = np.array([batch[-1][2], batch[-1][6]])
+    out = ref_train_util.collate_fn_syncmultitrack_acoustic(batch, reduction_factor=4)
+    for i, o in enumerate(out):
+        arrays[f"collate{i}"] = o.numpy()
+    lengths = r.integers(1, 50, size=7)
+    arrays["mask_lengths"] = lengths
+    arrays["non_pad_mask"] = ref_make_non_pad_mask(torch.from_numpy(lengths)).numpy()
+    # pad_inference_multitrack frame arithmetic (util.py:157-158)
+    meta["pad_inference"] = {str(T): int(4 - T % 4) for T in range(24, 33)}
+    save("data_path", arrays, meta)
+
+
+def main():
+    which = sys.argv[1:] or ["all"]
+    run = lambda n: "all" in which or n in which  # noqa: E731
+    full = lambda: build_ref(configs.multitrack_diffusion(num_speakers=4))[0]  # noqa: E731
+    # every case starts from freshly seeded parameters (BatchNorm running stats!)
+    if run("model"):
+        case_model_forward_full()
+    if run("diffnet"):
+        case_diffnet(full(), "mgc", 2, 64, ["input_projection.weight",
+                                            "residual_layers.19.output_projection.weight",
+                                            "residual_layers.3.conditioner_projection.weight"])
+        case_diffnet(full(), "bap", 2, 257, ["residual_layers.0.dilated_conv.weight",
+                                             "skip_projection.weight", "mlp.0.weight"])
+    if run("ffconvlstm"):
+        for w in ("mgc", "bap", "vuv"):
+            case_ffconvlstm(full(), w, 3, 64, [64, 52, 40])
+    if run("lf0"):
+        case_lf0(full(), 2, 64, [64, 56])
+    if run("inference"):
+        case_inference_bap(full())
+    if run("tiny"):
+        case_train_step_tiny()
+    if run("inference_tiny"):
+        case_model_inference_tiny()
+    if run("data"):
+        case_data_path()
+    with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
+        json.dump(dict(seed=SEED, torch=torch.__version__, numpy=np.__version__,
+                       reference="sarulab-speech/ensemble_svs_with_interactions @ 2025-03-21",
+                       files=sorted(x for x in os.listdir(HERE) if x.endswith(".npz"))),
+                  f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,86 @@
+"""Loading helpers for the reference-generated fixtures in tests/golden/."""
+import json
+import os
+
+import numpy as np
+import torch
+
+from oracle import ensvs_oracle as O
+from oracle.weights import seeded_state_dict
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+SEED = 20250321
+
+
+def load_case(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    arrays = {k: z[k] for k in z.files if k != "meta_json"}
+    meta = json.loads(bytes(z["meta_json"]).decode())
+    return arrays, meta
+
+
+def full_shapes():
+    return load_case("model_forward_full")[1]["shapes"]
+
+
+def tiny_shapes():
+    return load_case("train_step_tiny")[1]["shapes"]
+
+
+def params_from_shapes(shapes, seed=SEED, requires_grad=False):
+    """Seeded parameters + diffusion schedule buffers, as torch tensors."""
+    sd = seeded_state_dict(shapes, seed)
+    P = {k: torch.from_numpy(v.copy()) for k, v in sd.items()}
+    for prefix in ("mgc_model.", "bap_model."):
+        for k, v in O.diffusion_schedule().items():
+            if prefix + k in shapes:
+                P[prefix + k] = v
+    if requires_grad:
+        for k, v in P.items():
+            if "running" not in k and v.dtype == torch.float32 and not _is_buffer(k):
+                v.requires_grad_()
+    return P
+
+
+def _is_buffer(k):
+    from oracle.weights import SCHEDULE_BUFFERS
+    return k.rsplit(".", 1)[-1] in SCHEDULE_BUFFERS
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).double()
+    b = torch.as_tensor(b).double()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()
+
+
+def check_grad_summary(grads, summary, prefix, rtol=1e-4, atol=1e-7):
+    """grads: {full_key: tensor}; summary: {module_key: [sum, abs, l2]} from the golden."""
+    bad = []
+    for k, (s, a, l2) in summary.items():
+        if _pre_bn_bias(k):
+            # Conv bias feeding a training-mode BatchNorm: analytically zero
+            # gradient, the stored values are float cancellation noise.
+            g = grads.get(prefix + k)
+            w = summary[k.replace(".bias", ".weight")][2]
+            if g is not None and g.double().norm().item() > 1e-5 * w + 1e-6:
+                bad.append((k, "pre-BN bias grad not ~0"))
+            continue
+        g = grads.get(prefix + k)
+        if g is None:
+            gs = [0.0, 0.0, 0.0]
+        else:
+            g = g.double()
+            gs = [g.sum().item(), g.abs().sum().item(), g.norm().item()]
+        ref = [s, a, l2]
+        scale = max(abs(a), atol)
+        for x, y in zip(gs, ref):
+            if abs(x - y) > rtol * scale + atol:
+                bad.append((k, gs, ref))
+                break
+    return bad
+
+
+def _pre_bn_bias(k):
+    parts = k.split(".")
+    return len(parts) >= 3 and parts[-3] == "conv" and parts[-1] == "bias" and \
+        parts[-2] in ("1", "5", "9")

@@ -18,7 +18,7 @@ STATUS = {0: "OK", 1: "E_SHAPE", 2: "E_DTYPE", 3: "E_HIP", 4: "E_ARG"}
 
 PAD_ZERO, PAD_REFLECT, PAD_REPLICATE = 0, 1, 2
 DT_F32, DT_BF16 = 0, 1
-EPI_PLAIN, EPI_GATE, EPI_RESSKIP, EPI_GATE_BWD, EPI_ADDSCALE = 0, 1, 2, 3, 4
+EPI_PLAIN, EPI_GATE, EPI_RESSKIP, EPI_GATE_BWD, EPI_ADDSCALE, EPI_RELU_MASK = 0, 1, 2, 3, 4, 5
 
 
 class ConvSeg(ctypes.Structure):
@@ -35,7 +35,7 @@ class PackDesc(ctypes.Structure):
         ("sn", c_ll), ("sk", c_ll), ("sj", c_ll),
         ("N", c_int), ("K", c_int), ("taps", c_int), ("Npad", c_int), ("Kp", c_int),
         ("perm_c", c_int), ("flip", c_int), ("transpose", c_int), ("dtype", c_int),
-        ("scale", c_float),
+        ("scale", c_float), ("ldk", c_int), ("pad_", c_int),
     ]
 
 
@@ -45,10 +45,56 @@ SIGNATURES = {
                         c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_float, c_int, c_vp],
     "ensvs_conv_wgrad": [c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_ll, c_ll, c_int,
-                         c_int, c_vp],
+                         c_float, c_int, c_vp],
     "ensvs_pack_weights": [c_vp, c_int, c_int, c_vp],
     "ensvs_colsum": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_vp, c_int,
-                     c_vp],
+                     c_int, c_vp],
+    "ensvs_lstm_fwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp,
+                       c_vp],
+    "ensvs_lstm_bwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int,
+                       c_vp],
+    "ensvs_ardec_pack": [c_vp, c_int, c_vp, c_vp, c_vp],
+    "ensvs_ardec_fwd": [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
+                        c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp, c_vp, c_vp,
+                        c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ensvs_ardec_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_float,
+                        c_float, c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ensvs_downsample_fwd": [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp,
+                             c_vp, c_int, c_int, c_vp, c_int, c_vp],
+    "ensvs_downsample_bwd": [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_int,
+                             c_int, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
+    "ensvs_phoneme_ids": [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp],
+    "ensvs_embed_add": [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
+    "ensvs_embed_bwd": [c_vp, c_int, c_ll, c_int, c_vp, c_vp, c_vp],
+    "ensvs_spk_scatter": [c_vp, c_int, c_int, c_vp, c_vp, c_vp],
+    "ensvs_gather_rows": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
+    "ensvs_bn_finalize": [c_vp, c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_vp, c_float, c_int,
+                          c_vp],
+    "ensvs_bn_apply_relu": [c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                            c_vp],
+    "ensvs_bn_bwd": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp,
+                     c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
+    "ensvs_sinusoidal": [c_vp, c_int, c_int, c_vp, c_vp],
+    "ensvs_mish_fwd": [c_vp, c_vp, c_ll, c_vp],
+    "ensvs_mish_bwd": [c_vp, c_vp, c_vp, c_ll, c_vp],
+    "ensvs_q_sample": [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_float,
+                       c_vp, c_int, c_vp],
+    "ensvs_p_sample": [c_vp, c_vp, c_vp, c_ll, c_float, c_float, c_float, c_float, c_float, c_vp],
+    "ensvs_masked_l1": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int,
+                        c_float, c_vp, c_vp, c_vp],
+    "ensvs_l2norm": [c_vp, c_ll, c_vp, c_vp, c_vp],
+    "ensvs_adam": [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_float, c_float, c_float, c_float, c_float,
+                   c_float, c_float, c_vp],
+    "ensvs_copy_cols": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_vp],
+    "ensvs_axpy": [c_vp, c_vp, c_float, c_ll, c_vp],
+    "ensvs_axpby": [c_vp, c_float, c_vp, c_float, c_ll, c_vp],
+    "ensvs_mul": [c_vp, c_vp, c_ll, c_vp],
+    "ensvs_mul_out": [c_vp, c_vp, c_vp, c_ll, c_vp],
+    "ensvs_relu_mask": [c_vp, c_vp, c_vp, c_ll, c_vp],
+    "ensvs_reflect_fold": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "ensvs_randn": [c_vp, c_ll, ctypes.c_ulonglong, c_vp],
+    "ensvs_dropout_mask": [c_vp, c_ll, c_float, ctypes.c_ulonglong, c_vp],
+    "ensvs_randint": [c_vp, c_ll, c_ll, ctypes.c_ulonglong, c_vp],
 }
 
 _lib = None

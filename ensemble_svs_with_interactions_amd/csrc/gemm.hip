@@ -30,6 +30,7 @@ enum {
   EPI_RESSKIP = 2,   // DiffNet: res/skip interleaved by 16 -> x' = (x + r)/sqrt2, skip (+)= s
   EPI_GATE_BWD = 3,  // DiffNet backward: dz -> d(gate), d(filter) pre-activation grads
   EPI_ADDSCALE = 4,  // Y = alpha * aux1 + acc + bias
+  EPI_RELU_MASK = 5, // Y = (accum ? Y : 0) + (aux1 > 0 ? acc + bias : 0)   (ReLU backward)
 };
 
 struct SegDesc {
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
             const float xr = a.aux1[(long long)row * a.ld1 + c];
             a.Y[(long long)row * a.ldy + c] = (xr + v0) * 0.70710678118654752f;
             float* sk = a.aux0 + (long long)row * a.ld0 + c;
-            *sk = a.accum ? (*sk + v1) : v1;
+            *sk = a.accum ? fmaf(a.alpha, v1, *sk) : a.alpha * v1;
           }
         }
     }
@@ -272,6 +273,9 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
           *y = v;
         } else if (a.epi == EPI_ADDSCALE) {
           *y = a.alpha * a.aux1[(long long)row * a.ld1 + col] + v;
+        } else if (a.epi == EPI_RELU_MASK) {
+          v = a.aux1[(long long)row * a.ld1 + col] > 0.f ? v : 0.f;
+          *y = a.accum ? *y + v : v;
         } else if (a.epi == EPI_GATE_BWD) {
           const float g = a.aux1[(long long)row * a.ld1 + col];
           const float f = a.aux1[(long long)row * a.ld1 + a.C + col];
@@ -398,7 +402,7 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
 // dst[n*sn + k*sk + j*sj] (+)= sum_s part[s][j][n][k]   (fixed summation order)
 __global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dst,
                                     int splits, int taps, int N, int K, long long sn,
-                                    long long sk, long long sj, int accum) {
+                                    long long sk, long long sj, int accum, float scale) {
   const long long total = (long long)taps * N * K;
   const long long stride = (long long)N * K * taps;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -408,6 +412,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __res
     const int j = (int)(i / ((long long)K * N));
     float v = 0.f;
     for (int s = 0; s < splits; ++s) v += part[s * stride + i];
+    v *= scale;
     float* d = dst + n * sn + k * sk + j * sj;
     *d = accum ? (*d + v) : v;
   }
@@ -421,6 +426,7 @@ struct PackDesc {
   long long sn, sk, sj;
   int N, K, taps, Npad, Kp, perm_c, flip, transpose, dtype;
   float scale;
+  int ldk, pad_;  // dst row stride (elements); 0 -> Kp
 };
 
 __global__ void pack_kernel(const PackDesc* __restrict__ descs) {
@@ -448,8 +454,9 @@ __global__ void pack_kernel(const PackDesc* __restrict__ descs) {
       if (d.src2) v += d.src2[off];
       v *= d.scale;
     }
-    if (d.dtype == DT_BF16) ((__bf16*)d.dst)[i] = (__bf16)v;
-    else ((float*)d.dst)[i] = v;
+    const long long o = d.ldk > 0 ? ((long long)j * d.Npad + n) * d.ldk + k : i;
+    if (d.dtype == DT_BF16) ((__bf16*)d.dst)[o] = (__bf16)v;
+    else ((float*)d.dst)[o] = v;
   }
 }
 
@@ -467,7 +474,7 @@ __global__ void colsum_partial_kernel(const float* __restrict__ y, int ld, int M
   const int r0 = s * rps, r1 = min(M, r0 + rps);
   float acc = 0.f;
   if (col < N) {
-    const float mu = mean ? mean[col] : 0.f;
+    const float mu = mean ? mean[(long long)blockIdx.z * N + col] : 0.f;
     for (int r = r0 + g; r < r1; r += 4) {
       float v = y[(long long)r * ld + col];
       if (mean) { v -= mu; v *= v; }
@@ -482,11 +489,11 @@ __global__ void colsum_partial_kernel(const float* __restrict__ y, int ld, int M
 }
 
 __global__ void colsum_final_kernel(const float* __restrict__ part, int S, int N, float scale,
-                                    float* __restrict__ out, int accum) {
+                                    float* __restrict__ out, int ldo, int accum) {
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   if (col >= N) return;
   part += (long long)blockIdx.y * S * N;
-  out += (long long)blockIdx.y * N;
+  out += (long long)blockIdx.y * ldo;
   double acc = 0.0;
   for (int s = 0; s < S; ++s) acc += part[(long long)s * N + col];
   float v = (float)(acc * scale);
@@ -560,8 +567,8 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
 ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx, const float* radd,
                                int radd_ld, int B, int Tout, int Tin, int N, int K, int taps, int dil,
                                int shift0, int pad, int splits, float* part, float* dst,
-                               long long sn, long long sk, long long sj, int accum, int dtype,
-                               void* stream) {
+                               long long sn, long long sk, long long sj, int accum, float scale,
+                               int dtype, void* stream) {
   if (B <= 0 || Tout <= 0 || N <= 0 || K <= 0 || taps <= 0 || splits <= 0) return ENSVS_E_SHAPE;
   WgradArgs a{};
   a.dy = dy;
@@ -597,7 +604,7 @@ ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx
   long long total = (long long)taps * N * K;
   int blocks = (int)std::min<long long>(4096, (total + 255) / 256);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, part, dst, splits, taps,
-                     N, K, sn, sk, sj, accum);
+                     N, K, sn, sk, sj, accum, scale);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
@@ -615,9 +622,9 @@ ENSVS_API int ensvs_pack_weights(const ensvs_pack_desc* descs, int n, int max_el
 }
 
 // out[g][n] (+)= scale * sum_{m < M} f(Y[g*M + m, n]) for g < groups;
-// f = identity, or (y - mean[n])^2 when mean != null.  `part` holds groups*max_splits*N floats.
+// f = identity, or (y - mean[g][n])^2 when mean != null.  `part` holds groups*max_splits*N floats.
 ENSVS_API int ensvs_colsum(const float* y, int ld, int M, int groups, int N, const float* mean,
-                           float scale, float* part, int max_splits, float* out, int accum,
+                           float scale, float* part, int max_splits, float* out, int ldo, int accum,
                            void* stream) {
   if (M <= 0 || N <= 0 || groups <= 0) return ENSVS_E_SHAPE;
   int S = std::max(1, std::min(max_splits, M / 64));
@@ -627,7 +634,7 @@ ENSVS_API int ensvs_colsum(const float* y, int ld, int M, int groups, int N, con
                      N, rps, mean, part);
   ENSVS_CHECK_LAUNCH();
   hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(N, 256), groups), dim3(256), 0, st, part, S, N,
-                     scale, out, accum);
+                     scale, out, ldo > 0 ? ldo : N, accum);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }

@@ -1,0 +1,660 @@
+// Memory-bound kernels around the GEMMs and recurrences: phoneme argmax +
+// embedding, BatchNorm1d (training statistics, apply+ReLU, backward), DiffNet
+// step embedding / Mish, diffusion q_sample / p_sample, the masked L1 loss with
+// its fused gradient, and the clip-by-global-norm + Adam update over the flat
+// parameter buffer.  All are HBM-bound: grid-stride loops, one pass each.
+#include "common.h"
+#include "ensvs.h"
+
+namespace {
+
+#define GRID_LOOP(i, n) \
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (n); \
+       i += (long long)gridDim.x * blockDim.x)
+
+inline int grid_for(long long n) { return (int)std::min<long long>(8192, (n + 255) / 256); }
+
+// ------------------------------------------------------------- embeddings
+// ids[m] = argmax over x[m][ph0 .. ph0+nv) (first maximum; all-zero row -> 0),
+// nnsvs/model.py:905 / tacotron_f0.py:939 torch.argmax semantics.
+__global__ void phoneme_ids_kernel(const float* __restrict__ x, int ld, long long M, int ph0,
+                                   int nv, int* __restrict__ ids) {
+  GRID_LOOP(m, M) {
+    const float* r = x + m * ld + ph0;
+    float best = r[0];
+    int bi = 0;
+    for (int v = 1; v < nv; ++v) {
+      const float z = r[v];
+      if (z > best) { best = z; bi = v; }
+    }
+    ids[m] = bi;
+  }
+}
+
+// Y[m][c] += sum_k emb[ids_k[m]][c] + spk_k[m / T][c]   (k over 1 or 2 tracks)
+__global__ void embed_add_kernel(float* __restrict__ y, int ldy, long long M, int C, int T,
+                                 const float* __restrict__ emb, const int* __restrict__ ids0,
+                                 const int* __restrict__ ids1, const float* __restrict__ spk0,
+                                 const float* __restrict__ spk1, int ldspk) {
+  GRID_LOOP(i, M * C) {
+    const long long m = i / C;
+    const int c = (int)(i % C);
+    const long long b = m / T;
+    float v = y[m * ldy + c];
+    if (ids0) v += emb[(long long)ids0[m] * C + c];
+    if (ids1) v += emb[(long long)ids1[m] * C + c];
+    if (spk0) v += spk0[b * ldspk + c];
+    if (spk1) v += spk1[b * ldspk + c];
+    y[m * ldy + c] = v;
+  }
+}
+
+// demb[ids[m]][c] += dy[m][c]  (scatter-add, float atomics)
+__global__ void embed_bwd_kernel(const float* __restrict__ dy, int ldy, long long M, int C,
+                                 const int* __restrict__ ids, float* __restrict__ demb) {
+  GRID_LOOP(i, M * C) {
+    const long long m = i / C;
+    const int c = (int)(i % C);
+    atomicAdd(demb + (long long)ids[m] * C + c, dy[m * ldy + c]);
+  }
+}
+
+// dtable[spk[b]][c] += dseq[b][c]
+__global__ void spk_scatter_kernel(const float* __restrict__ dseq, int B, int C,
+                                   const long long* __restrict__ spk, float* __restrict__ dtab) {
+  GRID_LOOP(i, (long long)B * C) {
+    const int b = (int)(i / C), c = (int)(i % C);
+    atomicAdd(dtab + spk[b] * C + c, dseq[i]);
+  }
+}
+
+// out[b][c] = table[spk[b]][c]
+__global__ void gather_rows_kernel(const float* __restrict__ table, const long long* __restrict__ idx,
+                                   int B, int C, float* __restrict__ out) {
+  GRID_LOOP(i, (long long)B * C) {
+    const int b = (int)(i / C), c = (int)(i % C);
+    out[i] = table[idx[b] * C + c];
+  }
+}
+
+// ------------------------------------------------------------- BatchNorm1d
+// stats[g][0][c] = mean, stats[g][1][c] = rstd from (sum, sumsq-about-mean) already in
+// mean/var buffers: var_biased = var_sum / M.
+__global__ void bn_finalize_kernel(float* __restrict__ mean, float* __restrict__ var, int G, int C,
+                                   long long Mg, float eps, float* __restrict__ rstd,
+                                   float* __restrict__ rmean, float* __restrict__ rvar,
+                                   float momentum, int update) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float rm = update ? rmean[c] : 0.f, rv = update ? rvar[c] : 0.f;
+  for (int g = 0; g < G; ++g) {
+    const float mu = mean[g * C + c];
+    const float vb = var[g * C + c];  // biased variance
+    rstd[g * C + c] = 1.f / sqrtf(vb + eps);
+    if (update) {
+      const float vu = Mg > 1 ? vb * (float)Mg / (float)(Mg - 1) : vb;
+      rm = (1.f - momentum) * rm + momentum * mu;
+      rv = (1.f - momentum) * rv + momentum * vu;
+    }
+  }
+  if (update) {
+    rmean[c] = rm;
+    rvar[c] = rv;
+  }
+}
+
+// out = relu((y - mean_g) * rstd_g * gamma + beta); group g = m / Mg
+__global__ void bn_apply_relu_kernel(const float* __restrict__ y, int ldy, long long M, int C,
+                                     long long Mg, const float* __restrict__ mean,
+                                     const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                     const float* __restrict__ beta, float* __restrict__ out,
+                                     int ldo) {
+  GRID_LOOP(i, M * C) {
+    const long long m = i / C;
+    const int c = (int)(i % C);
+    const int g = (int)(m / Mg);
+    const float v = (y[m * ldy + c] - mean[g * C + c]) * rstd[g * C + c] * gamma[c] + beta[c];
+    out[m * ldo + c] = fmaxf(v, 0.f);
+  }
+}
+
+// Per-group column partials of dz and dz*xhat, dz = dout * (z > 0).
+__global__ void bn_bwd_reduce_kernel(const float* __restrict__ dout, int ldd,
+                                     const float* __restrict__ y, int ldy, long long Mg, int C,
+                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                     int rps, float* __restrict__ part) {
+  // grid: (ceil(C/64), S, G); part[g][s][2][C]
+  __shared__ float red[2][4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;
+  const int s = blockIdx.y, g = blockIdx.z, S = gridDim.y;
+  const long long r0 = (long long)g * Mg + (long long)s * rps;
+  const long long r1 = min((long long)g * Mg + Mg, r0 + rps);
+  float a = 0.f, bsum = 0.f;
+  if (col < C) {
+    const float mu = mean[g * C + col], rs = rstd[g * C + col], ga = gamma[col], be = beta[col];
+    for (long long r = r0 + w; r < r1; r += 4) {
+      const float xh = (y[r * ldy + col] - mu) * rs;
+      const float z = xh * ga + be;
+      const float dz = z > 0.f ? dout[r * ldd + col] : 0.f;
+      a += dz;
+      bsum += dz * xh;
+    }
+  }
+  red[0][w][threadIdx.x & 63] = a;
+  red[1][w][threadIdx.x & 63] = bsum;
+  __syncthreads();
+  if (w == 0 && col < C) {
+    float* p = part + (((long long)g * S + s) * 2) * C;
+    p[col] = (red[0][0][threadIdx.x] + red[0][1][threadIdx.x]) +
+             (red[0][2][threadIdx.x] + red[0][3][threadIdx.x]);
+    p[C + col] = (red[1][0][threadIdx.x] + red[1][1][threadIdx.x]) +
+                 (red[1][2][threadIdx.x] + red[1][3][threadIdx.x]);
+  }
+}
+
+// sums[g][0|1][c] = sum_s part; dgamma[c] += sum_g sums1, dbeta[c] += sum_g sums0
+__global__ void bn_bwd_final_kernel(const float* __restrict__ part, int S, int G, int C,
+                                    float* __restrict__ sums, float* __restrict__ dgamma,
+                                    float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double tg = 0.0, tb = 0.0;
+  for (int g = 0; g < G; ++g) {
+    double a = 0.0, b = 0.0;
+    for (int s = 0; s < S; ++s) {
+      a += part[(((long long)g * S + s) * 2) * C + c];
+      b += part[(((long long)g * S + s) * 2 + 1) * C + c];
+    }
+    sums[(g * 2) * C + c] = (float)a;
+    sums[(g * 2 + 1) * C + c] = (float)b;
+    tb += a;
+    tg += b;
+  }
+  dgamma[c] += (float)tg;
+  dbeta[c] += (float)tb;
+}
+
+// dy = gamma * rstd / Mg * (Mg * dz - sum dz - xhat * sum dz*xhat)
+__global__ void bn_bwd_apply_kernel(const float* __restrict__ dout, int ldd,
+                                    const float* __restrict__ y, int ldy, long long M, int C,
+                                    long long Mg, const float* __restrict__ mean,
+                                    const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                    const float* __restrict__ beta, const float* __restrict__ sums,
+                                    float* __restrict__ dy, int lddy) {
+  GRID_LOOP(i, M * C) {
+    const long long m = i / C;
+    const int c = (int)(i % C);
+    const int g = (int)(m / Mg);
+    const float rs = rstd[g * C + c];
+    const float xh = (y[m * ldy + c] - mean[g * C + c]) * rs;
+    const float z = xh * gamma[c] + beta[c];
+    const float dz = z > 0.f ? dout[m * ldd + c] : 0.f;
+    const float s0 = sums[(g * 2) * C + c], s1 = sums[(g * 2 + 1) * C + c];
+    dy[m * lddy + c] = gamma[c] * rs * (dz - (s0 + xh * s1) / (float)Mg);
+  }
+}
+
+// ------------------------------------------------------------- DiffNet head
+// out[b][j] = sin(t_b * e_j) (j < C/2), cos(...) (j >= C/2); e_j = exp(-j ln(1e4)/(C/2-1))
+__global__ void sinusoidal_kernel(const long long* __restrict__ t, int B, int C,
+                                  float* __restrict__ out) {
+  GRID_LOOP(i, (long long)B * C) {
+    const int b = (int)(i / C), j = (int)(i % C);
+    const int half = C / 2;
+    const int jj = j < half ? j : j - half;
+    const float scale = logf(10000.f) / (float)(half - 1);
+    const float e = expf((float)jj * -scale);
+    const float a = (float)t[b] * e;
+    out[i] = j < half ? sinf(a) : cosf(a);
+  }
+}
+
+__device__ __forceinline__ float softplus_(float x) {
+  return x > 20.f ? x : log1pf(expf(x));  // torch softplus, beta 1, threshold 20
+}
+
+// y = x * tanh(softplus(x))  (denoiser.py:9-11)
+__global__ void mish_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, long long n) {
+  GRID_LOOP(i, n) {
+    const float v = x[i];
+    y[i] = v * tanhf(softplus_(v));
+  }
+}
+
+__global__ void mish_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                float* __restrict__ dx, long long n) {
+  GRID_LOOP(i, n) {
+    const float v = x[i];
+    const float sp = softplus_(v);
+    const float tsp = tanhf(sp);
+    const float sig = v > 20.f ? 1.f : 1.f / (1.f + expf(-v));
+    dx[i] = dy[i] * (tsp + v * (1.f - tsp * tsp) * sig);
+  }
+}
+
+// ------------------------------------------------------------- diffusion
+// xn[m][j] = sa[t_b] * y[m][j] / ns + s1ma[t_b] * noise[m][j]   (diffusion.py:261-267, 289-295)
+__global__ void q_sample_kernel(const float* __restrict__ y, int ldy, const float* __restrict__ noise,
+                                int ldn, const long long* __restrict__ t,
+                                const float* __restrict__ sa, const float* __restrict__ s1ma,
+                                long long M, int Mc, int T, float inv_ns, float* __restrict__ xn,
+                                int ldx) {
+  GRID_LOOP(i, M * Mc) {
+    const long long m = i / Mc;
+    const int j = (int)(i % Mc);
+    const long long tb = t[m / T];
+    xn[m * ldx + j] = sa[tb] * (y[m * ldy + j] * inv_ns) + s1ma[tb] * noise[m * ldn + j];
+  }
+}
+
+// One reverse step (diffusion.py:170-204) at scalar step i:
+// x_recon = clamp(sra*x - srm1*eps, -1, 1); x = c1*x_recon + c2*x + nz*exp(.5 logvar)*noise
+__global__ void p_sample_kernel(float* __restrict__ x, const float* __restrict__ eps,
+                                const float* __restrict__ noise, long long n, float sra,
+                                float srm1, float c1, float c2, float sigma) {
+  GRID_LOOP(i, n) {
+    const float xv = x[i];
+    float xr = sra * xv - srm1 * eps[i];
+    xr = fminf(fmaxf(xr, -1.f), 1.f);
+    x[i] = (c1 * xr + c2 * xv) + sigma * noise[i];
+  }
+}
+
+// ------------------------------------------------------------- loss
+struct LossStream {
+  const float* a;  // prediction (or x_recon)
+  const float* b;  // target (or noise)
+  float* ga;       // gradient w.r.t. a (written)
+  int lda, ldb, ldg, n;
+};
+struct LossArgs {
+  LossStream s[4];
+  int ns, T, B;
+  float invN;
+};
+
+// loss partial sums of |a - b| over non-padded frames; ga = sign(a - b) / N (0 on padding).
+__global__ void masked_l1_kernel(LossArgs a, const long long* __restrict__ lengths,
+                                 float* __restrict__ part) {
+  __shared__ float red[256];
+  float acc = 0.f;
+  const long long M = (long long)a.B * a.T;
+  for (int k = 0; k < a.ns; ++k) {
+    const LossStream& s = a.s[k];
+    GRID_LOOP(i, M * s.n) {
+      const long long m = i / s.n;
+      const int j = (int)(i % s.n);
+      const int t = (int)(m % a.T);
+      const long long b = m / a.T;
+      float g = 0.f;
+      if (t < lengths[b]) {
+        const float d = s.a[m * s.lda + j] - s.b[m * s.ldb + j];
+        acc += fabsf(d);
+        g = d > 0.f ? a.invN : (d < 0.f ? -a.invN : 0.f);
+      }
+      if (s.ga) s.ga[m * s.ldg + j] = g;
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void sum_partials_kernel(const float* __restrict__ part, int n, float scale,
+                                    float* __restrict__ out) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (float)(red[0] * scale);
+}
+
+// ------------------------------------------------------------- optimizer
+__global__ void sumsq_kernel(const float* __restrict__ x, long long n, float* __restrict__ part) {
+  __shared__ float red[256];
+  float acc = 0.f;
+  GRID_LOOP(i, n) {
+    const float v = x[i];
+    acc = fmaf(v, v, acc);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void norm_final_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (float)sqrt(red[0]);
+}
+
+// clip_grad_norm_(max_norm) then torch.optim.Adam (weight_decay 0, amsgrad off);
+// skipped entirely when the norm is not finite (train_acoustic_multitrack.py:369-380).
+__global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, long long n, const float* __restrict__ norm,
+                            float max_norm, float lr, float b1, float b2, float eps, float bc1,
+                            float sqrt_bc2) {
+  const float nv = norm[0];
+  if (!isfinite(nv)) return;
+  const float coef = fminf(max_norm / (nv + 1e-6f), 1.f);
+  const float step = lr / bc1;
+  GRID_LOOP(i, n) {
+    const float gi = g[i] * coef;
+    g[i] = gi;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / sqrt_bc2 + eps;
+    p[i] = p[i] - step * (mi / denom);
+  }
+}
+
+__global__ void copy_cols_kernel(const float* __restrict__ src, int lds, float* __restrict__ dst,
+                                 int ldd, long long M, int n) {
+  GRID_LOOP(i, M * n) {
+    const long long m = i / n;
+    const int j = (int)(i % n);
+    dst[m * ldd + j] = src[m * lds + j];
+  }
+}
+
+__global__ void axpy_kernel(float* __restrict__ y, const float* __restrict__ x, float a,
+                            long long n) {
+  GRID_LOOP(i, n) y[i] += a * x[i];
+}
+
+__global__ void axpby_kernel(float* __restrict__ y, float a, const float* __restrict__ x, float b,
+                             long long n) {
+  GRID_LOOP(i, n) y[i] = a * y[i] + b * x[i];
+}
+
+__global__ void mul_kernel(float* __restrict__ y, const float* __restrict__ x, long long n) {
+  GRID_LOOP(i, n) y[i] *= x[i];
+}
+
+__global__ void relu_mask_kernel(float* __restrict__ out, const float* __restrict__ dy,
+                                 const float* __restrict__ act, long long n) {
+  GRID_LOOP(i, n) out[i] = act[i] > 0.f ? dy[i] : 0.f;
+}
+
+__global__ void mul_out_kernel(float* __restrict__ out, const float* __restrict__ a,
+                               const float* __restrict__ b, long long n) {
+  GRID_LOOP(i, n) out[i] = a[i] * b[i];
+}
+
+__global__ void reflect_fold_kernel(const float* __restrict__ dxp, int B, int T, int pad, int C,
+                                    float* __restrict__ dx) {
+  const int Tp = T + 2 * pad;
+  GRID_LOOP(i, (long long)B * T * C) {
+    const int c = (int)(i % C);
+    const long long bt = i / C;
+    const int t = (int)(bt % T);
+    const long long b = bt / T;
+    const float* src = dxp + b * Tp * C + c;
+    float v = src[(long long)(t + pad) * C];
+    if (t >= 1 && t <= pad) v += src[(long long)(pad - t) * C];
+    if (t >= T - 1 - pad && t <= T - 2) v += src[(long long)(2 * (T - 1) - t + pad) * C];
+    dx[i] = v;
+  }
+}
+
+// ---- counter-based RNG: a 64-bit mix of (seed, index) (splitmix64 finaliser) ----
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float u01(unsigned long long r) {  // (0, 1]
+  return ((float)(r >> 40) + 1.f) * (1.f / 16777216.f);
+}
+
+__global__ void randn_kernel(float* __restrict__ out, long long n, unsigned long long seed) {
+  GRID_LOOP(i, n) {
+    const unsigned long long r = mix64(seed ^ mix64((unsigned long long)i));
+    const float u1 = u01(r), u2 = u01(r << 24 | r >> 40);
+    out[i] = sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+  }
+}
+
+__global__ void dropout_mask_kernel(float* __restrict__ out, long long n, float p,
+                                    unsigned long long seed) {
+  const float keep = 1.f / (1.f - p);
+  GRID_LOOP(i, n) {
+    const unsigned long long r = mix64(seed ^ mix64((unsigned long long)i));
+    out[i] = u01(r) > p ? keep : 0.f;
+  }
+}
+
+__global__ void randint_kernel(long long* __restrict__ out, long long n, long long hi,
+                               unsigned long long seed) {
+  GRID_LOOP(i, n) {
+    const unsigned long long r = mix64(seed ^ mix64((unsigned long long)i));
+    out[i] = (long long)((r >> 11) % (unsigned long long)hi);
+  }
+}
+
+}  // namespace
+
+#define LAUNCH(kernel, n, ...)                                                                  \
+  do {                                                                                          \
+    hipLaunchKernelGGL(kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, __VA_ARGS__); \
+    ENSVS_CHECK_LAUNCH();                                                                       \
+  } while (0)
+
+ENSVS_API int ensvs_phoneme_ids(const float* x, int ld, long long M, int ph0, int nv, int* ids,
+                                void* stream) {
+  LAUNCH(phoneme_ids_kernel, M, x, ld, M, ph0, nv, ids);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_embed_add(float* y, int ldy, long long M, int C, int T, const float* emb,
+                              const int* ids0, const int* ids1, const float* spk0,
+                              const float* spk1, int ldspk, void* stream) {
+  LAUNCH(embed_add_kernel, M * C, y, ldy, M, C, T, emb, ids0, ids1, spk0, spk1, ldspk);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_embed_bwd(const float* dy, int ldy, long long M, int C, const int* ids,
+                              float* demb, void* stream) {
+  LAUNCH(embed_bwd_kernel, M * C, dy, ldy, M, C, ids, demb);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_spk_scatter(const float* dseq, int B, int C, const long long* spk, float* dtab,
+                                void* stream) {
+  LAUNCH(spk_scatter_kernel, (long long)B * C, dseq, B, C, spk, dtab);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_gather_rows(const float* table, const long long* idx, int B, int C, float* out,
+                                void* stream) {
+  LAUNCH(gather_rows_kernel, (long long)B * C, table, idx, B, C, out);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_bn_finalize(float* mean, float* var, int G, int C, long long Mg, float eps,
+                                float* rstd, float* rmean, float* rvar, float momentum, int update,
+                                void* stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream,
+                     mean, var, G, C, Mg, eps, rstd, rmean, rvar, momentum, update);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_bn_apply_relu(const float* y, int ldy, long long M, int C, long long Mg,
+                                  const float* mean, const float* rstd, const float* gamma,
+                                  const float* beta, float* out, int ldo, void* stream) {
+  LAUNCH(bn_apply_relu_kernel, M * C, y, ldy, M, C, Mg, mean, rstd, gamma, beta, out, ldo);
+  return ENSVS_OK;
+}
+
+// part: G*S*2*C floats (S <= max_splits), sums: G*2*C floats
+ENSVS_API int ensvs_bn_bwd(const float* dout, int ldd, const float* y, int ldy, long long M, int C,
+                           long long Mg, const float* mean, const float* rstd, const float* gamma,
+                           const float* beta, float* part, int max_splits, float* sums,
+                           float* dgamma, float* dbeta, float* dy, int lddy, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int G = (int)(M / Mg);
+  int S = (int)std::max<long long>(1, std::min<long long>(max_splits, Mg / 64));
+  int rps = (int)((Mg + S - 1) / S);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(cdiv(C, 64), S, G), dim3(256), 0, st, dout, ldd, y,
+                     ldy, Mg, C, mean, rstd, gamma, beta, rps, part);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, part, S, G, C, sums,
+                     dgamma, dbeta);
+  ENSVS_CHECK_LAUNCH();
+  LAUNCH(bn_bwd_apply_kernel, M * C, dout, ldd, y, ldy, M, C, Mg, mean, rstd, gamma, beta, sums, dy,
+         lddy);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_sinusoidal(const long long* t, int B, int C, float* out, void* stream) {
+  LAUNCH(sinusoidal_kernel, (long long)B * C, t, B, C, out);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_mish_fwd(const float* x, float* y, long long n, void* stream) {
+  LAUNCH(mish_fwd_kernel, n, x, y, n);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_mish_bwd(const float* x, const float* dy, float* dx, long long n, void* stream) {
+  LAUNCH(mish_bwd_kernel, n, x, dy, dx, n);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_q_sample(const float* y, int ldy, const float* noise, int ldn,
+                             const long long* t, const float* sa, const float* s1ma, long long M,
+                             int Mc, int T, float inv_ns, float* xn, int ldx, void* stream) {
+  LAUNCH(q_sample_kernel, M * Mc, y, ldy, noise, ldn, t, sa, s1ma, M, Mc, T, inv_ns, xn, ldx);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_p_sample(float* x, const float* eps, const float* noise, long long n, float sra,
+                             float srm1, float c1, float c2, float sigma, void* stream) {
+  LAUNCH(p_sample_kernel, n, x, eps, noise, n, sra, srm1, c1, c2, sigma);
+  return ENSVS_OK;
+}
+
+// streams: arrays of 4 (a, b, ga, lda, ldb, ldg, n); part >= 1024 floats; loss_out: 1 float
+ENSVS_API int ensvs_masked_l1(const float* const* a, const float* const* b, float* const* ga,
+                              const int* lda, const int* ldb, const int* ldg, const int* n, int ns,
+                              const long long* lengths, int B, int T, float invN, float* part,
+                              float* loss_out, void* stream) {
+  if (ns < 1 || ns > 4) return ENSVS_E_ARG;
+  LossArgs args{};
+  long long maxn = 0;
+  for (int k = 0; k < ns; ++k) {
+    args.s[k] = {a[k], b[k], ga[k], lda[k], ldb[k], ldg[k], n[k]};
+    maxn = std::max<long long>(maxn, (long long)B * T * n[k]);
+  }
+  args.ns = ns;
+  args.T = T;
+  args.B = B;
+  args.invN = invN;
+  int blocks = std::min(1024, grid_for(maxn));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(masked_l1_kernel, dim3(blocks), dim3(256), 0, st, args, lengths, part);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, st, part, blocks, invN, loss_out);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+// norm_out[0] = ||x||_2 over n floats (part >= 1024 floats)
+ENSVS_API int ensvs_l2norm(const float* x, long long n, float* part, float* norm_out, void* stream) {
+  int blocks = std::min(1024, grid_for(n));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(blocks), dim3(256), 0, st, x, n, part);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(256), 0, st, part, blocks, norm_out);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_adam(float* p, float* g, float* m, float* v, long long n, const float* norm,
+                         float max_norm, float lr, float b1, float b2, float eps, float bc1,
+                         float sqrt_bc2, void* stream) {
+  LAUNCH(adam_kernel, n, p, g, m, v, n, norm, max_norm, lr, b1, b2, eps, bc1, sqrt_bc2);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_copy_cols(const float* src, int lds, float* dst, int ldd, long long M, int n,
+                              void* stream) {
+  LAUNCH(copy_cols_kernel, M * n, src, lds, dst, ldd, M, n);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_axpy(float* y, const float* x, float a, long long n, void* stream) {
+  LAUNCH(axpy_kernel, n, y, x, a, n);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_axpby(float* y, float a, const float* x, float b, long long n, void* stream) {
+  LAUNCH(axpby_kernel, n, y, a, x, b, n);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_mul(float* y, const float* x, long long n, void* stream) {
+  LAUNCH(mul_kernel, n, y, x, n);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_reflect_fold(const float* dxp, int B, int T, int pad, int C, float* dx,
+                                 void* stream) {
+  if (pad >= T) return ENSVS_E_SHAPE;
+  LAUNCH(reflect_fold_kernel, (long long)B * T * C, dxp, B, T, pad, C, dx);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_randn(float* out, long long n, unsigned long long seed, void* stream) {
+  LAUNCH(randn_kernel, n, out, n, seed);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_dropout_mask(float* out, long long n, float p, unsigned long long seed,
+                                 void* stream) {
+  LAUNCH(dropout_mask_kernel, n, out, n, p, seed);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_randint(long long* out, long long n, long long hi, unsigned long long seed,
+                            void* stream) {
+  LAUNCH(randint_kernel, n, out, n, hi, seed);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_relu_mask(float* out, const float* dy, const float* act, long long n,
+                              void* stream) {
+  LAUNCH(relu_mask_kernel, n, out, dy, act, n);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_mul_out(float* out, const float* a, const float* b, long long n, void* stream) {
+  LAUNCH(mul_out_kernel, n, out, a, b, n);
+  return ENSVS_OK;
+}

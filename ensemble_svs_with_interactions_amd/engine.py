@@ -1,0 +1,182 @@
+"""Execution plumbing shared by every module of the path.
+
+* GEMM precision (``bf16`` MFMA operands with fp32 accumulation for production,
+  exact ``fp32`` MFMA for parity runs).
+* Flat parameter / gradient buffers: every parameter is a view into one fp32
+  buffer and its ``.grad`` a view into another, so clipping, Adam and the
+  RCCL all-reduce each touch one contiguous buffer (one launch / one
+  collective).  Backward kernels always ACCUMULATE into ``.grad`` (autograd
+  semantics); ``zero_grad`` zeroes the flat buffer.
+* ``ModulePacks``: per-module packed GEMM operands, rebuilt when parameters
+  move and repacked (one launch) when they change.
+"""
+import torch
+
+from . import _lib
+from .kernels import PackedBuffer
+
+_STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None}
+
+
+def next_seed() -> int:
+    """64-bit seed for the counter-based RNG kernels, derived from torch's global seed so
+    torch.manual_seed() makes runs reproducible."""
+    import random
+    if _STATE["rng"] is None or _STATE["rng"][0] != torch.initial_seed():
+        _STATE["rng"] = (torch.initial_seed(), random.Random(torch.initial_seed()))
+    return _STATE["rng"][1].getrandbits(64)
+
+
+def set_gemm_precision(p: str):
+    """'bf16' (default; MFMA bf16 operands, fp32 accumulate) or 'fp32' (exact fp32 MFMA)."""
+    _STATE["gemm_dtype"] = {"bf16": _lib.DT_BF16, "fp32": _lib.DT_F32}[p]
+
+
+def gemm_precision():
+    return "bf16" if _STATE["gemm_dtype"] == _lib.DT_BF16 else "fp32"
+
+
+def gemm_dtype():
+    return _STATE["gemm_dtype"]
+
+
+def weights_updated():
+    """Call after parameters were modified through raw pointers (fused optimizer)."""
+    _STATE["epoch"] += 1
+
+
+def grad_of(p: torch.Tensor) -> torch.Tensor:
+    """The tensor backward kernels accumulate into for parameter ``p``."""
+    if p.grad is None:
+        g = getattr(p, "_ensvs_gview", None)
+        if g is None:
+            g = torch.zeros_like(p)
+        else:
+            g.zero_()
+        p.grad = g
+    return p.grad
+
+
+def flatten_parameters(module: torch.nn.Module, align: int = 64):
+    """Re-home every parameter of ``module`` into one flat fp32 buffer (and grads
+    into another).  Returns (flat_params, flat_grads)."""
+    params = [p for p in module.parameters()]
+    sizes = [(p.numel() + align - 1) // align * align for p in params]
+    dev = params[0].device
+    flat = torch.zeros(sum(sizes), dtype=torch.float32, device=dev)
+    gflat = torch.zeros_like(flat)
+    o = 0
+    for p, n in zip(params, sizes):
+        v = flat[o:o + p.numel()].view_as(p)
+        v.copy_(p.data)
+        p.data = v
+        g = gflat[o:o + p.numel()].view_as(p)
+        p._ensvs_gview = g
+        p.grad = g
+        o += n
+    module._ensvs_flat = (flat, gflat)
+    weights_updated()
+    return flat, gflat
+
+
+def _sig(params):
+    return (_STATE["epoch"], _STATE["gemm_dtype"],
+            tuple((p.data_ptr(), p._version) for p in params))
+
+
+class ModulePacks:
+    """Packed GEMM operands of one module.
+
+    ``build(fn)`` calls ``fn(packs)`` to register weights (fwd / bwd / bias
+    buffers) whenever parameter storage or precision changed; ``refresh``
+    repacks when values changed.
+    """
+
+    def __init__(self):
+        self.sig = None
+        self.layout_sig = None
+
+    def ensure(self, module, register):
+        params = list(module.parameters())
+        sig = _sig(params)
+        if sig == self.sig:
+            return self
+        layout = (sig[1], tuple(p.data_ptr() for p in params))
+        if layout != self.layout_sig:
+            self.fwd = PackedBuffer(gemm_dtype())
+            self.bwd = PackedBuffer(gemm_dtype())
+            self.bias = PackedBuffer(_lib.DT_F32)
+            self.refs = {}
+            register(self)
+            dev = params[0].device
+            for pb in (self.fwd, self.bwd, self.bias):
+                pb.finalize(dev)
+            self.layout_sig = layout
+        for pb in (self.fwd, self.bwd, self.bias):
+            pb.repack()
+        self.sig = sig
+        return self
+
+    # ---- registration helpers ------------------------------------------------
+    def linear(self, name, w, cols=None, bwd=True, scale=1.0, perm_c=0):
+        """Linear weight (N, K) or a column range of it."""
+        N, K = w.shape
+        c0, c1 = (0, K) if cols is None else cols
+        src = w[:, c0:c1]
+        self.refs[name] = self.fwd.add(src, N, c1 - c0, 1, K, 1, 1, perm_c=perm_c, scale=scale)
+        if bwd:
+            self.refs[name + "^T"] = self.bwd.add(src, N, c1 - c0, 1, K, 1, 1, transpose=True,
+                                                   scale=scale)
+
+    def linear_rows(self, name, w, rows, bwd=True, scale=1.0):
+        """Row range [r0, r1) of a Linear weight as its own GEMM operand."""
+        N, K = w.shape
+        r0, r1 = rows
+        src = w[r0:r1]
+        self.refs[name] = self.fwd.add(src, r1 - r0, K, 1, K, 1, 1, scale=scale)
+        if bwd:
+            self.refs[name + "^T"] = self.bwd.add(src, r1 - r0, K, 1, K, 1, 1, transpose=True,
+                                                   scale=scale)
+
+    def conv(self, name, w, cols=None, bwd=True, perm_c=0, scale=1.0, bwd_rows=None,
+             bwd_scale=None):
+        """Conv1d weight (N, K, taps) (or input-channel range).  The backward operand is
+        transposed and tap-flipped (the dgrad convolution); ``bwd_rows`` restricts it to
+        output rows [r0, r1)."""
+        N, K, taps = w.shape
+        c0, c1 = (0, K) if cols is None else cols
+        src = w[:, c0:c1]
+        self.refs[name] = self.fwd.add(src, N, c1 - c0, taps, K * taps, taps, 1, perm_c=perm_c,
+                                       scale=scale)
+        if bwd:
+            r0, r1 = (0, N) if bwd_rows is None else bwd_rows
+            self.refs[name + "^T"] = self.bwd.add(
+                w[r0:r1, c0:c1], r1 - r0, c1 - c0, taps, K * taps, taps, 1, transpose=True,
+                flip=True, scale=scale if bwd_scale is None else bwd_scale)
+
+    def bias_vec(self, name, b, perm_c=0, b2=None):
+        N = b.shape[0]
+        self.refs[name] = self.bias.add(b.view(N, 1, 1), N, 1, 1, 1, 1, 1, perm_c=perm_c,
+                                        src2=None if b2 is None else b2.view(N, 1, 1), kpad_to=1)
+
+    def __getitem__(self, name):
+        return self.refs[name]
+
+    def bias_ptr_args(self, name):
+        return dict(bias=self.bias.buf, bias_off=self.refs[name].offset)
+
+
+def empty(*shape, device, dtype=torch.float32):
+    return torch.empty(*shape, dtype=dtype, device=device)
+
+
+def lengths_pair(lengths, B, T, device):
+    """Host list + device int64 tensor of sequence lengths (None -> all T)."""
+    if lengths is None:
+        host = [T] * B
+    elif isinstance(lengths, torch.Tensor):
+        host = [int(v) for v in lengths.detach().cpu().tolist()]
+    else:
+        host = [int(v) for v in lengths]
+    dev = torch.tensor(host, dtype=torch.int64, device=device)
+    return host, dev

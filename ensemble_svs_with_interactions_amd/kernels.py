@@ -65,6 +65,34 @@ class PackedBuffer:
         self._max = max(self._max, n)
         return ref
 
+    def add_rowcat(self, srcs, N, K, transpose_blocks=False, scale=1.0):
+        """One GEMM operand made of several Linear weights.
+
+        transpose_blocks=False: rows concatenated  -> packed (len*N) x K   (stacked outputs)
+        transpose_blocks=True:  W_l^T side by side  -> packed K x (len*N)  (summed inputs)
+        """
+        L = len(srcs)
+        if not transpose_blocks:
+            Npad, Kp = _roundup(L * N, BM), _roundup(K, BK)
+            ref = PackedRef(self.size, L * N, K, 1, Npad, Kp)
+            for l, w in enumerate(srcs):
+                sub = PackedRef(self.size + l * N * Kp, N, K, 1, N, Kp)
+                self.specs.append(dict(src=w, src2=None, sn=K, sk=1, sj=1, N=N, K=K, taps=1,
+                                       Npad=N, Kp=Kp, perm_c=0, flip=0, transpose=0,
+                                       scale=float(scale), ref=sub, ldk=0))
+        else:
+            Npad, Kp = _roundup(K, BM), _roundup(L * N, BK)
+            ref = PackedRef(self.size, K, L * N, 1, Npad, Kp)
+            for l, w in enumerate(srcs):
+                sub = PackedRef(self.size + l * N, K, N, 1, Npad, N)
+                self.specs.append(dict(src=w, src2=None, sn=K, sk=1, sj=1, N=N, K=K, taps=1,
+                                       Npad=Npad, Kp=N, perm_c=0, flip=0, transpose=1,
+                                       scale=float(scale), ref=sub, ldk=Kp))
+        n = Npad * Kp
+        self.size += _roundup(n, 64)
+        self._max = max(self._max, n)
+        return ref
+
     def finalize(self, device):
         tdtype = torch.bfloat16 if self.dtype == _lib.DT_BF16 else torch.float32
         self.buf = torch.zeros(max(self.size, 64), dtype=tdtype, device=device)
@@ -80,6 +108,7 @@ class PackedBuffer:
             d.N, d.K, d.taps, d.Npad, d.Kp = s["N"], s["K"], s["taps"], s["Npad"], s["Kp"]
             d.perm_c, d.flip, d.transpose = s["perm_c"], s["flip"], s["transpose"]
             d.dtype, d.scale = self.dtype, s["scale"]
+            d.ldk = s.get("ldk", 0)
         raw = bytes(arr)
         host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
         self._dev_descs = host.to(device)
@@ -138,7 +167,8 @@ def scratch(nfloats, device, key="part"):
 
 
 def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, sk, sj,
-          accum=False, dtype=_lib.DT_BF16, radd=None, radd_ld=0, dyoff=0, xoff=0, splits=None):
+          accum=False, dtype=_lib.DT_BF16, radd=None, radd_ld=0, dyoff=0, xoff=0, splits=None,
+          scale=1.0, dstoff=0):
     M = B * Tout
     if splits is None:
         tiles = -(-N // 128) * -(-K // 128) * taps
@@ -146,11 +176,14 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
     part = scratch(splits * taps * N * K, dy.device)
     call("ensvs_conv_wgrad", dy.data_ptr() + 4 * dyoff, ldy, x.data_ptr() + 4 * xoff, ldx,
          ptr(radd), radd_ld, B, Tout, Tin, N, K, taps, dil, shift0, pad, splits,
-         part.data_ptr(), dst.data_ptr(), sn, sk, sj, int(accum), dtype, stream())
+         part.data_ptr(), dst.data_ptr() + 4 * dstoff, sn, sk, sj, int(accum), float(scale),
+         dtype, stream())
 
 
-def colsum(y, ld, M, N, out, groups=1, mean=None, scale=1.0, accum=False, yoff=0):
+def colsum(y, ld, M, N, out, groups=1, mean=None, scale=1.0, accum=False, yoff=0, ldo=0,
+           outoff=0):
+    """out[g*ldo + n] (+)= scale * sum over the M rows of group g (ldo 0 -> N)."""
     max_splits = 64
     part = scratch(groups * max_splits * N, y.device, key="colsum")
     call("ensvs_colsum", y.data_ptr() + 4 * yoff, ld, M, groups, N, ptr(mean), float(scale),
-         part.data_ptr(), max_splits, out.data_ptr(), int(accum), stream())
+         part.data_ptr(), max_splits, out.data_ptr() + 4 * outoff, ldo, int(accum), stream())

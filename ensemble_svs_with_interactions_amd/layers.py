@@ -1,0 +1,372 @@
+"""Forward/backward building blocks shared by the encoders of the path.
+
+Each block runs entirely in libensvs.so kernels (MFMA GEMMs, persistent
+recurrences, memory-bound kernels); tensors here are only allocations and
+views.  All activations are channels-last frame rows (B*T, C) fp32.
+
+Blocks mirror the reference layer stacks:
+  * phoneme embedding input   nnsvs/model.py:895-910, tacotron_f0.py:929-965
+  * FF stack 3x(Linear+ReLU)  nnsvs/model.py:837-844, tacotron_f0.py:852-859
+  * conv stack 3x(ReflectionPad1d(3)+Conv1d k7+BatchNorm1d+ReLU)
+                              nnsvs/model.py:846-859, tacotron_f0.py:861-874
+  * packed bi-LSTM            nnsvs/model.py:862-869,914-916
+"""
+import torch
+
+from . import _lib
+from . import kernels as K
+from ._lib import call, ptr
+from .engine import empty, gemm_dtype, grad_of, next_seed
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+DEBUG = None  # set to a dict to capture intermediates (tests / tools only)
+
+
+def _dbg(name, t):
+    if DEBUG is not None:
+        DEBUG[name] = t.detach().clone()
+
+
+def dropout_mask(n, p, device):
+    """Scaled keep mask of F.dropout(p, training=True) from the counter-based RNG kernel."""
+    m = empty(n, device=device)
+    call("ensvs_dropout_mask", m.data_ptr(), n, float(p), next_seed(), stream())
+    return m
+
+
+def randn(n, device):
+    z = empty(n, device=device)
+    call("ensvs_randn", z.data_ptr(), n, next_seed(), stream())
+    return z
+
+
+def colsum_into(dy, ld, M, N, param, groups=1, scale=1.0, off=0, yoff=0):
+    """param.grad[off:off+N] += scale * column sums of dy."""
+    g = grad_of(param)
+    if off == 0 and groups == 1:
+        K.colsum(dy, ld, M, N, g, scale=scale, accum=True, yoff=yoff)
+    else:
+        tmp = empty(groups * N, device=dy.device)
+        K.colsum(dy, ld, M // groups, N, tmp, groups=groups, scale=scale, yoff=yoff)
+        call("ensvs_axpy", g.data_ptr() + 4 * off, tmp.data_ptr(), 1.0, N, stream())
+
+
+def wgrad_into(param, dy, ldy, x, ldx, B, Tout, Tin, N, Kc, taps=1, dil=1, shift0=0,
+               pad=_lib.PAD_ZERO, col0=0, scale=1.0, radd=None, radd_ld=0, dyoff=0, xoff=0,
+               row0=0):
+    """param.grad (+)= dy^T x for a Linear (N, K) or Conv1d (N, K, taps) weight, optionally
+    into an input-column range starting at col0 / output rows from row0."""
+    g = grad_of(param)
+    if g.dim() == 2:
+        sn, sk, sj = g.shape[1], 1, 1
+    else:
+        sn, sk, sj = g.shape[1] * g.shape[2], g.shape[2], 1
+    K.wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, Kc, taps, dil, shift0, pad, g, sn, sk, sj,
+            accum=True, dtype=gemm_dtype(), radd=radd, radd_ld=radd_ld, dyoff=dyoff, xoff=xoff,
+            scale=scale, dstoff=row0 * sn + col0 * sk)
+
+
+# ----------------------------------------------------------------- input
+
+def phoneme_input_register(pk, emb_mod, fc_in):
+    pk.linear("fc_in", fc_in.weight, bwd=False)
+    pk.bias_vec("fc_in.b", fc_in.bias)
+
+
+def gather_input(sources, ph0, ph1, M, device):
+    """Split logical input columns into (phoneme one-hot source, contiguous non-phoneme
+    copy).  sources: list of (tensor, ld, col_offset, ncols) covering columns in order."""
+    Kin = sum(s[3] for s in sources) - (ph1 - ph0)
+    ldx = (Kin + 3) // 4 * 4
+    X = empty(M, ldx, device=device)  # columns >= Kin are masked by the GEMM loaders
+    ph_src = None
+    col = 0  # logical column of the current source start
+    out = 0
+    for (t, ld, off, n) in sources:
+        lo, hi = col, col + n
+        pieces = []
+        if hi <= ph0 or lo >= ph1:
+            pieces.append((lo, hi))
+        else:
+            if lo < ph0:
+                pieces.append((lo, ph0))
+            if hi > ph1:
+                pieces.append((ph1, hi))
+            assert lo <= ph0 and hi >= ph1, "phoneme columns must lie in one source"
+            ph_src = (t, ld, off + (ph0 - lo))
+        for a, b in pieces:
+            call("ensvs_copy_cols", t.data_ptr() + 4 * (off + a - lo), ld,
+                 X.data_ptr() + 4 * out, ldx, M, b - a, stream())
+            out += b - a
+        col = hi
+    return ph_src, X, Kin, ldx
+
+
+def embed_fwd(pk, emb_weight, sources, ph0, ph1, B, T, spk_seq=None, spk_ld=0, device=None):
+    """x = emb(argmax onehot) + fc_in(other cols) [+ spk]  -> (M, E); returns saved dict."""
+    M = B * T
+    ph_src, X, Kin, ldx = gather_input(sources, ph0, ph1, M, device)
+    ids = torch.empty(M, dtype=torch.int32, device=device)
+    t, ld, off = ph_src
+    call("ensvs_phoneme_ids", t.data_ptr() + 4 * off, ld, M, 0, ph1 - ph0, ids.data_ptr(), stream())
+    E = emb_weight.shape[1]
+    Y = empty(M, E, device=device)
+    K.gemm([K.Seg(X, ldx, Kin, pk["fc_in"], T)], B, T, E, pk.fwd, Y, E,
+           **pk.bias_ptr_args("fc_in.b"))
+    call("ensvs_embed_add", Y.data_ptr(), E, M, E, T, emb_weight.data_ptr(), ids.data_ptr(), None,
+         ptr(spk_seq), None, spk_ld, stream())
+    return Y, dict(ids=ids, X=X, Kin=Kin, ldx=ldx)
+
+
+def embed_bwd(emb_mod, fc_in, sv, dY, B, T, dspk_seq=None):
+    """Grads of emb / fc_in (and per-sequence speaker vectors, summed over frames)."""
+    M = B * T
+    E = dY.shape[1]
+    call("ensvs_embed_bwd", dY.data_ptr(), E, M, E, sv["ids"].data_ptr(),
+         grad_of(emb_mod.weight).data_ptr(), stream())
+    wgrad_into(fc_in.weight, dY, E, sv["X"], sv["ldx"], B, T, T, E, sv["Kin"])
+    colsum_into(dY, E, M, E, fc_in.bias)
+    if dspk_seq is not None:
+        K.colsum(dY, E, T, E, dspk_seq, groups=B, accum=True)
+
+
+# ----------------------------------------------------------------- FF stack
+
+def ff_register(pk, ff):
+    for i in (0, 2, 4):
+        pk.linear(f"ff{i}", ff[i].weight)
+        pk.bias_vec(f"ff{i}.b", ff[i].bias)
+
+
+def ff_fwd(pk, ff, X, B, T, device):
+    M = B * T
+    hs = []
+    h, ldh = X, X.shape[1]
+    for i in (0, 2, 4):
+        N = ff[i].weight.shape[0]
+        Kc = ff[i].weight.shape[1]
+        out = empty(M, N, device=device)
+        K.gemm([K.Seg(h, ldh, Kc, pk[f"ff{i}"], T)], B, T, N, pk.fwd, out, N, relu=True,
+               **pk.bias_ptr_args(f"ff{i}.b"))
+        hs.append(out)
+        h, ldh = out, N
+    return hs
+
+
+def ff_bwd(pk, ff, X, hs, dH3, B, T, device, need_dx=True):
+    """dH3: grad of the last ReLU output.  Returns grad w.r.t. X."""
+    M = B * T
+    ins = [X, hs[0], hs[1]]
+    d = empty(M, dH3.shape[1], device=device)
+    call("ensvs_relu_mask", d.data_ptr(), dH3.data_ptr(), hs[2].data_ptr(), d.numel(), stream())
+    dx = None
+    for li, i in enumerate((4, 2, 0)):
+        lay = ff[i]
+        N, Kc = lay.weight.shape
+        xin = ins[2 - li]
+        wgrad_into(lay.weight, d, N, xin, xin.shape[1], B, T, T, N, Kc)
+        colsum_into(d, N, M, N, lay.bias)
+        if i == 0 and not need_dx:
+            break
+        nd = empty(M, Kc, device=device)
+        if i > 0:
+            K.gemm([K.Seg(d, N, N, pk[f"ff{i}^T"], T)], B, T, Kc, pk.bwd, nd, Kc,
+                   epi=_lib.EPI_RELU_MASK, aux1=hs[2 - li - 1], ld1=Kc)
+        else:
+            K.gemm([K.Seg(d, N, N, pk[f"ff{i}^T"], T)], B, T, Kc, pk.bwd, nd, Kc)
+            dx = nd
+        d = nd
+    return dx
+
+
+# ----------------------------------------------------------------- conv stack
+
+CONV_IDX = ((1, 2), (5, 6), (9, 10))
+
+
+def conv_register(pk, conv, first_cols=None, first_bwd_cols=None):
+    """first_cols: list of (name, (c0, c1)) input-column ranges of conv.1 (segments)."""
+    for li, (ci, bi) in enumerate(CONV_IDX):
+        w = conv[ci].weight
+        if li == 0 and first_cols is not None:
+            for name, cols in first_cols:
+                pk.conv(f"conv{ci}@{name}", w, cols=cols,
+                        bwd=first_bwd_cols is not None and name in first_bwd_cols)
+        else:
+            pk.conv(f"conv{ci}", w)
+        pk.bias_vec(f"conv{ci}.b", conv[ci].bias)
+
+
+def conv_fwd(pk, conv, first_segs, B, T, device, training, groups=1, save=True,
+             update_running=True):
+    """first_segs: list of (name, tensor, ld, K, xoff) for conv.1.  Returns (out, saved)."""
+    M = B * T
+    Mg = M // groups
+    sv = []
+    segs = [K.Seg(t, ld, Kc, pk[f"conv1@{name}"] if name else pk["conv1"], T, taps=7, dil=1,
+                  shift0=-3, pad=_lib.PAD_REFLECT, xoff=xoff)
+            for (name, t, ld, Kc, xoff) in first_segs]
+    a = None
+    for li, (ci, bi) in enumerate(CONV_IDX):
+        C = conv[ci].weight.shape[0]
+        if li > 0:
+            segs = [K.Seg(a, C_prev, C_prev, pk[f"conv{ci}"], T, taps=7, dil=1, shift0=-3,
+                          pad=_lib.PAD_REFLECT)]
+        y = empty(M, C, device=device)
+        K.gemm(segs, B, T, C, pk.fwd, y, C, **pk.bias_ptr_args(f"conv{ci}.b"))
+        bn = conv[bi]
+        mean = empty(groups, C, device=device)
+        rstd = empty(groups, C, device=device)
+        if training:
+            var = empty(groups, C, device=device)
+            K.colsum(y, C, Mg, C, mean, groups=groups, scale=1.0 / Mg)
+            K.colsum(y, C, Mg, C, var, groups=groups, mean=mean, scale=1.0 / Mg)
+            upd = int(update_running and bn.track_running_stats)
+            call("ensvs_bn_finalize", mean.data_ptr(), var.data_ptr(), groups, C, Mg,
+                 float(bn.eps), rstd.data_ptr(), bn.running_mean.data_ptr(),
+                 bn.running_var.data_ptr(), float(bn.momentum), upd, stream())
+            if upd:
+                bn.num_batches_tracked.add_(groups)
+            Mg_apply = Mg
+        else:
+            # eval: running statistics, one group
+            mean = bn.running_mean
+            call("ensvs_bn_finalize", mean.data_ptr(), bn.running_var.data_ptr(), 1, C, M,
+                 float(bn.eps), rstd.data_ptr(), None, None, 0.0, 0, stream())
+            Mg_apply = M
+        out = empty(M, C, device=device)
+        call("ensvs_bn_apply_relu", y.data_ptr(), C, M, C, Mg_apply, mean.data_ptr(),
+             rstd.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(), out.data_ptr(), C,
+             stream())
+        if save:
+            sv.append(dict(y=y, mean=mean, rstd=rstd, out=out, segs=segs))
+        a, C_prev = out, C
+    return a, sv
+
+
+def conv_bwd(pk, conv, sv, dout, B, T, device, groups=1, first_dx=None):
+    """dout: grad of the stack output.  first_dx: list of (name, K) of conv.1 segments whose
+    input gradient is wanted (returned in order as a list)."""
+    M = B * T
+    Mg = M // groups
+    d = dout
+    res = []
+    for li in (2, 1, 0):
+        ci, bi = CONV_IDX[li]
+        s = sv[li]
+        C = conv[ci].weight.shape[0]
+        bn = conv[bi]
+        dy = empty(M, C, device=device)
+        part = K.scratch(groups * 64 * 2 * C, device, key="bn")
+        sums = empty(groups * 2 * C, device=device)
+        call("ensvs_bn_bwd", d.data_ptr(), C, s["y"].data_ptr(), C, M, C, Mg, s["mean"].data_ptr(),
+             s["rstd"].data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(), part.data_ptr(), 64,
+             sums.data_ptr(), grad_of(bn.weight).data_ptr(), grad_of(bn.bias).data_ptr(),
+             dy.data_ptr(), C, stream())
+        _dbg(f"conv{li}.dout", d)
+        _dbg(f"conv{li}.dy", dy)
+        colsum_into(dy, C, M, C, conv[ci].bias)
+        w = conv[ci].weight
+        col = 0
+        for seg in s["segs"]:
+            wgrad_into(w, dy, C, seg.x, seg.ld, B, T, T, C, seg.K, taps=7, dil=1, shift0=-3,
+                       pad=_lib.PAD_REFLECT, col0=col, xoff=seg.xoff)
+            col += seg.K
+        if li > 0:
+            Cin = w.shape[1]
+            dxp = empty(B * (T + 6), Cin, device=device)
+            K.gemm([K.Seg(dy, C, C, pk[f"conv{ci}^T"], T, taps=7, dil=1, shift0=-6)], B, T + 6,
+                   Cin, pk.bwd, dxp, Cin)
+            dprev = empty(M, Cin, device=device)
+            call("ensvs_reflect_fold", dxp.data_ptr(), B, T, 3, Cin, dprev.data_ptr(), stream())
+            d = dprev
+        else:
+            for (name, Kc) in (first_dx or []):
+                ref = pk[f"conv{ci}@{name}^T"] if name else pk[f"conv{ci}^T"]
+                dxp = empty(B * (T + 6), Kc, device=device)
+                K.gemm([K.Seg(dy, C, C, ref, T, taps=7, dil=1, shift0=-6)], B, T + 6, Kc, pk.bwd,
+                       dxp, Kc)
+                dx = empty(M, Kc, device=device)
+                call("ensvs_reflect_fold", dxp.data_ptr(), B, T, 3, Kc, dx.data_ptr(), stream())
+                res.append(dx)
+    return res
+
+
+# ----------------------------------------------------------------- bi-LSTM
+
+def lstm_register(pk, lstm):
+    for l in range(lstm.num_layers):
+        for sfx in ("", "_reverse"):
+            pk.linear(f"ih{l}{sfx}", getattr(lstm, f"weight_ih_l{l}{sfx}"))
+            pk.bias_vec(f"b{l}{sfx}", getattr(lstm, f"bias_ih_l{l}{sfx}"),
+                        b2=getattr(lstm, f"bias_hh_l{l}{sfx}"))
+
+
+def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=True):
+    """Packed bidirectional multi-layer LSTM.  Returns (Y (M, 2H), saved list)."""
+    M = B * T
+    H = lstm.hidden_size
+    sv = []
+    h, ldh = X, ldx
+    for l in range(lstm.num_layers):
+        Kc = getattr(lstm, f"weight_ih_l{l}").shape[1]
+        gx = empty(M, 8 * H, device=device)
+        for d, sfx in enumerate(("", "_reverse")):
+            K.gemm([K.Seg(h, ldh, Kc, pk[f"ih{l}{sfx}"], T)], B, T, 4 * H, pk.fwd, gx, 8 * H,
+                   yoff=d * 4 * H, **pk.bias_ptr_args(f"b{l}{sfx}"))
+        y = empty(M, 2 * H, device=device)
+        saved = empty(M * 2 * 5 * H, device=device)
+        call("ensvs_lstm_fwd", gx.data_ptr(), 8 * H, getattr(lstm, f"weight_hh_l{l}").data_ptr(),
+             getattr(lstm, f"weight_hh_l{l}_reverse").data_ptr(), lens_dev.data_ptr(), B, T, H,
+             y.data_ptr(), 2 * H, saved.data_ptr(), stream())
+        del gx
+        yin = y
+        mask = None
+        if dropout_masks is not None and l < lstm.num_layers - 1:
+            mask = dropout_masks[l]
+            yin = empty(M, 2 * H, device=device)
+            call("ensvs_mul_out", yin.data_ptr(), y.data_ptr(), mask.data_ptr(), yin.numel(),
+                 stream())
+        if save:
+            sv.append(dict(x=h, ldx=ldh, y=y, saved=saved, mask=mask, yin=yin))
+        h, ldh = yin, 2 * H
+    return h, sv
+
+
+def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
+    M = B * T
+    H = lstm.hidden_size
+    d = dY
+    dx = None
+    for l in reversed(range(lstm.num_layers)):
+        s = sv[l]
+        Kc = getattr(lstm, f"weight_ih_l{l}").shape[1]
+        dg = empty(M, 8 * H, device=device)
+        call("ensvs_lstm_bwd", d.data_ptr(), 2 * H, getattr(lstm, f"weight_hh_l{l}").data_ptr(),
+             getattr(lstm, f"weight_hh_l{l}_reverse").data_ptr(), lens_dev.data_ptr(), B, T, H,
+             s["saved"].data_ptr(), dg.data_ptr(), 8 * H, stream())
+        for di, sfx in enumerate(("", "_reverse")):
+            wgrad_into(getattr(lstm, f"weight_ih_l{l}{sfx}"), dg, 8 * H, s["x"], s["ldx"], B, T, T,
+                       4 * H, Kc, dyoff=di * 4 * H)
+            # h_{t-1} in processing order: t-1 forward, t+1 reverse (zero outside [0, L))
+            wgrad_into(getattr(lstm, f"weight_hh_l{l}{sfx}"), dg, 8 * H, s["y"], 2 * H, B, T, T,
+                       4 * H, H, shift0=(-1 if di == 0 else 1), dyoff=di * 4 * H, xoff=di * H)
+            colsum_into(dg, 8 * H, M, 4 * H, getattr(lstm, f"bias_ih_l{l}{sfx}"), yoff=di * 4 * H)
+            colsum_into(dg, 8 * H, M, 4 * H, getattr(lstm, f"bias_hh_l{l}{sfx}"), yoff=di * 4 * H)
+        if l == 0 and not need_dx:
+            break
+        nd = empty(M, Kc, device=device)
+        K.gemm([K.Seg(dg, 8 * H, 4 * H, pk[f"ih{l}^T"], T),
+                K.Seg(dg, 8 * H, 4 * H, pk[f"ih{l}_reverse^T"], T, xoff=4 * H)],
+               B, T, Kc, pk.bwd, nd, Kc)
+        if l > 0:
+            prev_mask = sv[l - 1].get("mask")
+            if prev_mask is not None:
+                call("ensvs_mul", nd.data_ptr(), prev_mask.data_ptr(), nd.numel(), stream())
+        d = nd
+        dx = nd
+    return dx

@@ -1,0 +1,240 @@
+"""Encoders of the multi-track path: ``FFConvLSTM`` and ``SpeakerEmbedding``.
+
+Drop-in for nnsvs.model.FFConvLSTM (nnsvs/model.py:779-927) and
+nnsvs.model.SpeakerEmbedding (nnsvs/model.py:35-53): same constructor
+arguments, ``forward``/``inference`` signatures and ``state_dict`` keys.  The
+nn.Linear / nn.Conv1d / nn.BatchNorm1d / nn.LSTM members are parameter
+containers only; their forward methods are never called — every op runs in
+libensvs.so.
+"""
+import torch
+from torch import nn
+
+from . import layers as Ly
+from .base import BaseModel, PredictionType
+from .engine import ModulePacks, empty, lengths_pair
+
+
+def init_weights(net, init_type="normal", init_gain=0.02):
+    """nnsvs/util.py:31-67 (initialisation only; plumbing)."""
+    if init_type == "none" or init_type is None:
+        return
+
+    def init_func(m):
+        classname = m.__class__.__name__
+        if hasattr(m, "weight") and (classname.find("Conv") != -1 or classname.find("Linear") != -1):
+            if init_type == "normal":
+                nn.init.normal_(m.weight.data, 0.0, init_gain)
+            elif init_type == "xavier_normal":
+                nn.init.xavier_normal_(m.weight.data, gain=init_gain)
+            elif init_type == "kaiming_normal":
+                nn.init.kaiming_normal_(m.weight.data, a=0, mode="fan_in")
+            elif init_type == "orthogonal":
+                nn.init.orthogonal_(m.weight.data, gain=init_gain)
+            else:
+                raise NotImplementedError(init_type)
+            if hasattr(m, "bias") and m.bias is not None:
+                nn.init.constant_(m.bias.data, 0.0)
+        elif classname.find("BatchNorm2d") != -1:
+            nn.init.normal_(m.weight.data, 1.0, init_gain)
+            nn.init.constant_(m.bias.data, 0.0)
+
+    net.apply(init_func)
+
+
+class SpeakerEmbedding(BaseModel):
+    """nnsvs/model.py:35-53."""
+
+    def __init__(self, num_embeddings, embedding_dim, padding_idx, std=0.01):
+        super().__init__()
+        self.emb = nn.Embedding(num_embeddings, embedding_dim, padding_idx=padding_idx)
+        self.std = std
+
+    def forward(self, x, lengths=None, y=None):
+        return _GatherFn.apply(self.emb.weight, x)
+
+    def embedding_dim(self):
+        return self.emb.embedding_dim
+
+
+class _GatherFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, table, idx):
+        from ._lib import call
+        shp = idx.shape
+        flat = idx.reshape(-1).to(torch.int64).contiguous()
+        out = empty(flat.numel(), table.shape[1], device=table.device)
+        call("ensvs_gather_rows", table.data_ptr(), flat.data_ptr(), flat.numel(), table.shape[1],
+             out.data_ptr(), Ly.stream())
+        ctx.save_for_backward(flat)
+        ctx.shape = (table.shape, shp)
+        return out.view(*shp, table.shape[1])
+
+    @staticmethod
+    def backward(ctx, g):
+        from ._lib import call
+        (flat,) = ctx.saved_tensors
+        tshape, _ = ctx.shape
+        dt = torch.zeros(tshape, dtype=torch.float32, device=g.device)
+        g = g.reshape(-1, tshape[1]).contiguous()
+        call("ensvs_spk_scatter", g.data_ptr(), flat.numel(), tshape[1], flat.data_ptr(),
+             dt.data_ptr(), Ly.stream())
+        return dt, None
+
+
+class FFConvLSTM(BaseModel):
+    """FFN + Conv1d + LSTM (nnsvs/model.py:779-927), MI355X kernels."""
+
+    def __init__(self, in_dim, ff_hidden_dim=2048, conv_hidden_dim=1024, lstm_hidden_dim=256,
+                 out_dim=67, dropout=0.0, num_lstm_layers=2, bidirectional=True, init_type="none",
+                 use_mdn=False, dim_wise=True, num_gaussians=4, in_ph_start_idx: int = 1,
+                 in_ph_end_idx: int = 50, embed_dim=None):
+        super().__init__()
+        if use_mdn:
+            raise NotImplementedError("FFConvLSTM(use_mdn=True) is not on the multi-track path")
+        self.in_dim = in_dim
+        self.out_dim = out_dim
+        self.in_ph_start_idx = in_ph_start_idx
+        self.in_ph_end_idx = in_ph_end_idx
+        self.num_vocab = in_ph_end_idx - in_ph_start_idx
+        self.embed_dim = embed_dim
+        self.use_mdn = use_mdn
+        if embed_dim is None:
+            raise NotImplementedError("FFConvLSTM without phoneme embedding is not on the path")
+        assert in_dim > self.num_vocab
+        self.emb = nn.Embedding(self.num_vocab, embed_dim)
+        self.fc_in = nn.Linear(in_dim - self.num_vocab, embed_dim)
+        self.ff = nn.Sequential(
+            nn.Linear(embed_dim, ff_hidden_dim), nn.ReLU(),
+            nn.Linear(ff_hidden_dim, ff_hidden_dim), nn.ReLU(),
+            nn.Linear(ff_hidden_dim, ff_hidden_dim), nn.ReLU(),
+        )
+        self.conv = nn.Sequential(
+            nn.ReflectionPad1d(3), nn.Conv1d(ff_hidden_dim, conv_hidden_dim, 7, padding=0),
+            nn.BatchNorm1d(conv_hidden_dim), nn.ReLU(),
+            nn.ReflectionPad1d(3), nn.Conv1d(conv_hidden_dim, conv_hidden_dim, 7, padding=0),
+            nn.BatchNorm1d(conv_hidden_dim), nn.ReLU(),
+            nn.ReflectionPad1d(3), nn.Conv1d(conv_hidden_dim, conv_hidden_dim, 7, padding=0),
+            nn.BatchNorm1d(conv_hidden_dim), nn.ReLU(),
+        )
+        num_direction = 2 if bidirectional else 1
+        # like the reference (model.py:862-869) the LSTM is always bidirectional
+        self.lstm = nn.LSTM(conv_hidden_dim, lstm_hidden_dim, num_lstm_layers, bidirectional=True,
+                            batch_first=True, dropout=dropout)
+        self.fc = nn.Linear(num_direction * lstm_hidden_dim, out_dim)
+        init_weights(self, init_type)
+        self._packs = ModulePacks()
+
+    def prediction_type(self):
+        return PredictionType.DETERMINISTIC
+
+    # ---- kernels -----------------------------------------------------------------
+    def _register(self, pk):
+        Ly.phoneme_input_register(pk, self.emb, self.fc_in)
+        Ly.ff_register(pk, self.ff)
+        Ly.conv_register(pk, self.conv)
+        Ly.lstm_register(pk, self.lstm)
+        pk.linear("fc", self.fc.weight)
+        pk.bias_vec("fc.b", self.fc.bias)
+
+    def _fwd(self, sources, B, T, lens_dev, spk_seq=None, spk_ld=0, training=None,
+             lstm_masks=None, save=True):
+        """sources: [(tensor, ld, col_offset, ncols)] of the logical input columns.
+        Returns (out (B*T, out_dim), saved state)."""
+        training = self.training if training is None else training
+        pk = self._packs.ensure(self, self._register)
+        dev = self.fc.weight.device
+        X0, esv = Ly.embed_fwd(pk, self.emb.weight, sources, self.in_ph_start_idx,
+                               self.in_ph_end_idx, B, T, spk_seq, spk_ld, dev)
+        hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
+        F = hs[2].shape[1]
+        a, csv = Ly.conv_fwd(pk, self.conv, [("", hs[2], F, F, 0)], B, T, dev, training,
+                             save=save)
+        if training and self.lstm.dropout > 0 and lstm_masks is None:
+            lstm_masks = [Ly.dropout_mask(B * T * 2 * self.lstm.hidden_size, self.lstm.dropout,
+                                          dev)
+                          for _ in range(self.lstm.num_layers - 1)]
+        C = a.shape[1]
+        y, lsv = Ly.lstm_fwd(pk, self.lstm, a, C, B, T, lens_dev, dev,
+                             lstm_masks if training else None, save=save)
+        out = empty(B * T, self.out_dim, device=dev)
+        H2 = 2 * self.lstm.hidden_size
+        Ly.K.gemm([Ly.K.Seg(y, H2, H2, pk["fc"], T)], B, T, self.out_dim, pk.fwd, out,
+                  self.out_dim, **pk.bias_ptr_args("fc.b"))
+        st = dict(X0=X0, esv=esv, hs=hs, csv=csv, lsv=lsv, y=y, B=B, T=T, lens=lens_dev) \
+            if save else None
+        return out, st
+
+    def _bwd(self, st, dout, want_spk=False):
+        """dout (B*T, out_dim).  Accumulates parameter grads; returns (dX0 per-frame input
+        grad (B*T, E), dspk per-sequence (B, E) or None)."""
+        pk = self._packs
+        dev = dout.device
+        B, T = st["B"], st["T"]
+        M = B * T
+        H2 = 2 * self.lstm.hidden_size
+        Ly.wgrad_into(self.fc.weight, dout, self.out_dim, st["y"], H2, B, T, T, self.out_dim, H2)
+        Ly.colsum_into(dout, self.out_dim, M, self.out_dim, self.fc.bias)
+        dy = empty(M, H2, device=dev)
+        Ly.K.gemm([Ly.K.Seg(dout, self.out_dim, self.out_dim, pk["fc^T"], T)], B, T, H2, pk.bwd,
+                  dy, H2)
+        da = Ly.lstm_bwd(pk, self.lstm, st["lsv"], dy, B, T, st["lens"], dev)
+        F = st["hs"][2].shape[1]
+        (dh3,) = Ly.conv_bwd(pk, self.conv, st["csv"], da, B, T, dev, first_dx=[("", F)])
+        dX0 = Ly.ff_bwd(pk, self.ff, st["X0"], st["hs"], dh3, B, T, dev)
+        dspk = None
+        if want_spk:
+            dspk = torch.zeros(B, self.embed_dim, device=dev)
+        Ly.embed_bwd(self.emb, self.fc_in, st["esv"], dX0, B, T, dspk)
+        return dX0, dspk
+
+    # ---- reference API -----------------------------------------------------------
+    def forward(self, x, lengths=None, y=None, spk_embs=None):
+        B, T, _ = x.shape
+        x = x.contiguous().float()
+        return _FFConvLSTMFn.apply(self, x, spk_embs, lengths, self.fc.weight)
+
+    def inference(self, x, lengths=None, spk_embs=None):
+        return self(x, lengths, spk_embs=spk_embs)
+
+
+def _spk_args(spk_embs, B, T):
+    """Per-sequence pointer view of an (expanded) (B, T, E) speaker-embedding tensor."""
+    if spk_embs is None:
+        return None, 0, None
+    if spk_embs.dim() == 3 and spk_embs.stride(1) == 0 and spk_embs.stride(2) == 1:
+        return spk_embs, spk_embs.stride(0), None
+    full = spk_embs.reshape(B * T, -1).contiguous()
+    return full, full.shape[1], full
+
+
+class _FFConvLSTMFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mod, x, spk_embs, lengths, anchor):
+        B, T, D = x.shape
+        dev = x.device
+        lens_host, lens_dev = lengths_pair(lengths, B, T, dev)
+        spk, spk_ld, full = _spk_args(spk_embs, B, T)
+        if full is not None:
+            raise NotImplementedError("per-frame speaker embeddings are not on the path")
+        out, st = mod._fwd([(x, D, 0, D)], B, T, lens_dev, spk, spk_ld,
+                           save=torch.is_grad_enabled() or True)
+        ctx.mod, ctx.st = mod, st
+        ctx.spk_needs = spk_embs is not None and spk_embs.requires_grad
+        Tm = max(lens_host)
+        out = out.view(B, T, -1)
+        return out[:, :Tm] if Tm < T else out
+
+    @staticmethod
+    def backward(ctx, g):
+        st = ctx.st
+        B, T = st["B"], st["T"]
+        g = g.contiguous()
+        if g.shape[1] < T:
+            gg = torch.zeros(B, T, g.shape[2], device=g.device)
+            gg[:, :g.shape[1]] = g
+            g = gg
+        dX0, _ = ctx.mod._bwd(st, g.view(B * T, -1), want_spk=False)
+        dspk = dX0.view(B, T, -1) if ctx.spk_needs else None
+        ctx.st = None
+        return None, None, dspk, None, None

@@ -22,7 +22,7 @@ enum { ENSVS_STATUS_OK = 0, ENSVS_STATUS_E_SHAPE = 1, ENSVS_STATUS_E_DTYPE = 2,
 enum { ENSVS_PAD_ZERO = 0, ENSVS_PAD_REFLECT = 1, ENSVS_PAD_REPLICATE = 2 };
 enum { ENSVS_DT_F32 = 0, ENSVS_DT_BF16 = 1 };
 enum { ENSVS_EPI_PLAIN = 0, ENSVS_EPI_GATE = 1, ENSVS_EPI_RESSKIP = 2, ENSVS_EPI_GATE_BWD = 3,
-       ENSVS_EPI_ADDSCALE = 4 };
+       ENSVS_EPI_ADDSCALE = 4, ENSVS_EPI_RELU_MASK = 5 };
 
 /* One K-segment of the implicit-GEMM activation operand. */
 typedef struct ensvs_conv_seg {
@@ -40,6 +40,7 @@ typedef struct ensvs_pack_desc {
   long long sn, sk, sj;
   int N, K, taps, Npad, Kp, perm_c, flip, transpose, dtype;
   float scale;
+  int ldk, pad_;  /* destination row stride in elements (0: Kp) */
 } ensvs_pack_desc;
 
 /* Conv1d / Linear forward and input-gradient as an MFMA implicit GEMM.
@@ -55,14 +56,120 @@ int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N
 int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx, const float* radd,
                      int radd_ld, int B, int Tout, int Tin, int N, int K, int taps, int dil,
                      int shift0, int pad, int splits, float* part, float* dst, long long sn,
-                     long long sk, long long sj, int accum, int dtype, void* stream);
+                     long long sk, long long sj, int accum, float scale, int dtype, void* stream);
 
 /* Batched weight repack (descs is a DEVICE array). */
 int ensvs_pack_weights(const ensvs_pack_desc* descs, int n, int max_elems, void* stream);
 
 /* Grouped column sums (bias grads, BatchNorm statistics). */
 int ensvs_colsum(const float* y, int ld, int M, int groups, int N, const float* mean, float scale,
-                 float* part, int max_splits, float* out, int accum, void* stream);
+                 float* part, int max_splits, float* out, int ldo, int accum, void* stream);
+
+
+/* ---- recurrences ------------------------------------------------------ */
+
+/* Packed bidirectional LSTM recurrence, one layer (input projections precomputed
+ * by ensvs_conv_gemm into gx [B*T][ldg], dir d gates at cols d*4H + {i,f,g,o}*H).
+ * Replaces the time loop of nn.LSTM(bidirectional=True) over pack_padded_sequence:
+ * nnsvs/model.py:862-869,914-916 and acoustic_models/tacotron_f0.py:876-883,981-983.
+ * H in {8,16,32,64,128}; saved holds [B*T][2][5H]. */
+int ensvs_lstm_fwd(const float* gx, int ldg, const float* whh_f, const float* whh_r,
+                   const long long* lengths, int B, int T, int H, float* y, int ldy, float* saved,
+                   void* stream);
+/* Backward through time: pre-activation gate gradients dg [B*T][lddg] (zero past L_b). */
+int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* whh_r,
+                   const long long* lengths, int B, int T, int H, const float* saved, float* dg,
+                   int lddg, void* stream);
+
+/* Free-running residual-F0 AR decoder (acoustic_models/tacotron_f0.py:126-237 with
+ * ZoneOutCell(LSTMCell), tacotron/decoder.py:20-48).  H in {16,...,256}, T % 4 == 0. */
+int ensvs_ardec_pack(const float* whh, int H, float* wpf, float* wpb, void* stream);
+int ensvs_ardec_fwd(const float* gx, int ldgx, const float* ofx, int ldo, const float* wpf,
+                    const float* wih_p, const float* wfo, int ldwfo, const float* score, int lds,
+                    const float* mask, int B, int T, int H, float in_min, float in_max, float mean,
+                    float scale, float* lf0, float* res, float* sg, float* sc, float* sh,
+                    float* so, float* sp, void* stream);
+int ensvs_ardec_bwd(const float* glf0, const float* gres, const float* wpb, const float* wih_p,
+                    const float* wfo, int ldwfo, const float* mask, int B, int T, int H,
+                    float in_min, float in_max, float mean, float scale, const float* sg,
+                    const float* sc, const float* so, float* dg, float* do4, void* stream);
+/* Depthwise Conv1d(k=4, s=4, groups=C) down-sampling (tacotron_f0.py:104-111,161-164). */
+int ensvs_downsample_fwd(const float* p0, int ld0, int n0, const float* p1, int ld1, int n1,
+                         const float* p2, int ld2, int n2, const float* w, const float* bias, int B,
+                         int T, float* e, int lde, void* stream);
+int ensvs_downsample_bwd(const float* de, int lde, const float* p0, int ld0, int n0,
+                         const float* p1, int ld1, int n1, const float* p2, int ld2, int n2,
+                         const float* w, int B, int T, float* dx, int lddx, float* dw, float* db,
+                         void* stream);
+
+/* ---- memory-bound kernels --------------------------------------------- */
+
+/* torch.argmax over the phoneme one-hot columns (model.py:905, tacotron_f0.py:939). */
+int ensvs_phoneme_ids(const float* x, int ld, long long M, int ph0, int nv, int* ids,
+                      void* stream);
+/* y += emb[ids0] (+ emb[ids1]) + spk0[b] (+ spk1[b])  (nn.Embedding + speaker add,
+ * model.py:906-910, tacotron_f0.py:941-965). */
+int ensvs_embed_add(float* y, int ldy, long long M, int C, int T, const float* emb,
+                    const int* ids0, const int* ids1, const float* spk0, const float* spk1,
+                    int ldspk, void* stream);
+int ensvs_embed_bwd(const float* dy, int ldy, long long M, int C, const int* ids, float* demb,
+                    void* stream);
+/* SpeakerEmbedding (model.py:35-53): gather / scatter-add of table rows. */
+int ensvs_spk_scatter(const float* dseq, int B, int C, const long long* spk, float* dtab,
+                      void* stream);
+int ensvs_gather_rows(const float* table, const long long* idx, int B, int C, float* out,
+                      void* stream);
+/* BatchNorm1d training mode (model.py:846-859): finalize stats + running update,
+ * apply+ReLU, and backward (+ReLU).  Groups of Mg rows keep separate statistics. */
+int ensvs_bn_finalize(float* mean, float* var, int G, int C, long long Mg, float eps, float* rstd,
+                      float* rmean, float* rvar, float momentum, int update, void* stream);
+int ensvs_bn_apply_relu(const float* y, int ldy, long long M, int C, long long Mg,
+                        const float* mean, const float* rstd, const float* gamma,
+                        const float* beta, float* out, int ldo, void* stream);
+int ensvs_bn_bwd(const float* dout, int ldd, const float* y, int ldy, long long M, int C,
+                 long long Mg, const float* mean, const float* rstd, const float* gamma,
+                 const float* beta, float* part, int max_splits, float* sums, float* dgamma,
+                 float* dbeta, float* dy, int lddy, void* stream);
+/* DiffNet step embedding (denoiser.py:9-26). */
+int ensvs_sinusoidal(const long long* t, int B, int C, float* out, void* stream);
+int ensvs_mish_fwd(const float* x, float* y, long long n, void* stream);
+int ensvs_mish_bwd(const float* x, const float* dy, float* dx, long long n, void* stream);
+/* GaussianDiffusion q_sample (diffusion.py:261-267,289-295) and one p_sample step
+ * (diffusion.py:170-204). */
+int ensvs_q_sample(const float* y, int ldy, const float* noise, int ldn, const long long* t,
+                   const float* sa, const float* s1ma, long long M, int Mc, int T, float inv_ns,
+                   float* xn, int ldx, void* stream);
+int ensvs_p_sample(float* x, const float* eps, const float* noise, long long n, float sra,
+                   float srm1, float c1, float c2, float sigma, void* stream);
+/* Masked L1 loss summed over streams / N with its gradient fused
+ * (bin/train_acoustic_multitrack.py:115-173). */
+int ensvs_masked_l1(const float* const* a, const float* const* b, float* const* ga,
+                    const int* lda, const int* ldb, const int* ldg, const int* n, int ns,
+                    const long long* lengths, int B, int T, float invN, float* part,
+                    float* loss_out, void* stream);
+/* clip_grad_norm_ + torch.optim.Adam over the flat parameter buffer
+ * (bin/train_acoustic_multitrack.py:369-380). */
+int ensvs_l2norm(const float* x, long long n, float* part, float* norm_out, void* stream);
+int ensvs_adam(float* p, float* g, float* m, float* v, long long n, const float* norm,
+               float max_norm, float lr, float b1, float b2, float eps, float bc1,
+               float sqrt_bc2, void* stream);
+int ensvs_copy_cols(const float* src, int lds, float* dst, int ldd, long long M, int n,
+                    void* stream);
+int ensvs_axpy(float* y, const float* x, float a, long long n, void* stream);
+/* y = a*y + b*x ; y *= x (dropout masks) */
+int ensvs_axpby(float* y, float a, const float* x, float b, long long n, void* stream);
+int ensvs_mul(float* y, const float* x, long long n, void* stream);
+int ensvs_mul_out(float* out, const float* a, const float* b, long long n, void* stream);
+/* out = act > 0 ? dy : 0 (ReLU backward; out may alias dy) */
+int ensvs_relu_mask(float* out, const float* dy, const float* act, long long n, void* stream);
+/* Gradient of ReflectionPad1d(pad) (model.py:846-859): dx[b][t] from dxp[b][T+2pad]. */
+int ensvs_reflect_fold(const float* dxp, int B, int T, int pad, int C, float* dx, void* stream);
+/* Counter-based RNG (stateless hash of (seed, index)): N(0,1), keep-masks scaled by
+ * 1/(1-p) (F.dropout), and uniform integers in [0, hi) (torch.randint). */
+int ensvs_randn(float* out, long long n, unsigned long long seed, void* stream);
+int ensvs_dropout_mask(float* out, long long n, float p, unsigned long long seed, void* stream);
+int ensvs_randint(long long* out, long long n, long long hi, unsigned long long seed,
+                  void* stream);
 
 #ifdef __cplusplus
 }

@@ -66,14 +66,23 @@ def phoneme_embed(P, prefix, x, ph_start, ph_end):
                                                                torch.cat([first, last], -1))
 
 
-def ff_stack(P, prefix, x):
+def _relu(x, masks, key):
+    """ReLU, or multiplication by a given 0/1 mask (mask-matched gradient checks: the
+    checker reuses the device's ReLU decisions so fp32 rounding at the kink cannot flip
+    an element between the two implementations)."""
+    if masks is not None and key in masks:
+        return x * masks[key]
+    return F.relu(x)
+
+
+def ff_stack(P, prefix, x, masks=None):
     """3 x (Linear + ReLU): nnsvs/model.py:837-844, tacotron_f0.py:852-859."""
     for i in (0, 2, 4):
-        x = F.relu(linear(P, f"{prefix}ff.{i}", x))
+        x = _relu(linear(P, f"{prefix}ff.{i}", x), masks, f"ff{i}")
     return x
 
 
-def conv_stack(P, prefix, x, training, bn_updates=None, momentum=0.1, eps=1e-5):
+def conv_stack(P, prefix, x, training, bn_updates=None, momentum=0.1, eps=1e-5, masks=None):
     """3 x (ReflectionPad1d(3) -> Conv1d k7 -> BatchNorm1d -> ReLU) on (B, T, C).
 
     nnsvs/model.py:846-859, tacotron_f0.py:861-874.  BatchNorm training
@@ -91,7 +100,8 @@ def conv_stack(P, prefix, x, training, bn_updates=None, momentum=0.1, eps=1e-5):
             # running statistics are module state: later calls see this update
             P[bn + ".running_mean"], P[bn + ".running_var"] = rm, rv
             bn_updates.setdefault(bn, []).append((rm, rv))
-        h = F.relu(h)
+        h = _relu(h, None if masks is None else
+                  {k: v.transpose(1, 2) for k, v in masks.items()}, f"bn{bi}")
     return h.transpose(1, 2)
 
 
@@ -174,14 +184,14 @@ def bilstm(P, prefix, x, lengths, num_layers, layer_dropout_masks=None, fast=Fal
 # ------------------------------------------------------------- encoders
 
 def ffconvlstm(P, prefix, cfg, x, lengths, spk_embs=None, training=True, bn_updates=None,
-               lstm_dropout_masks=None, fast=False):
+               lstm_dropout_masks=None, fast=False, relu_masks=None):
     """FFConvLSTM.forward: nnsvs/model.py:891-918."""
     if cfg.get("embed_dim") is not None:
         x = phoneme_embed(P, prefix, x, cfg["in_ph_start_idx"], cfg["in_ph_end_idx"])
     if spk_embs is not None:
         x = x + spk_embs
-    out = ff_stack(P, prefix, x)
-    out = conv_stack(P, prefix, out, training, bn_updates)
+    out = ff_stack(P, prefix, x, relu_masks)
+    out = conv_stack(P, prefix, out, training, bn_updates, masks=relu_masks)
     out = bilstm(P, prefix, out, lengths, cfg["num_lstm_layers"], lstm_dropout_masks, fast)
     return linear(P, prefix + "fc", out)
 

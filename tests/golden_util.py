@@ -84,3 +84,10 @@ def _pre_bn_bias(k):
     parts = k.split(".")
     return len(parts) >= 3 and parts[-3] == "conv" and parts[-1] == "bias" and \
         parts[-2] in ("1", "5", "9")
+
+
+def grad_close(g, ref, rtol):
+    """Relative L2 error of a gradient tensor (robust to isolated ReLU-kink flips)."""
+    g = torch.as_tensor(g).double()
+    ref = torch.as_tensor(ref).double()
+    return ((g - ref).norm() / (ref.norm() + 1e-30)).item() <= rtol

@@ -89,7 +89,7 @@ def test_diffnet_gate_and_resskip(dt, tol):
     skip_acc = torch.full((B, T, C), 0.5, device=DEV)
     xn = torch.empty(B, T, C, device=DEV)
     K.gemm([K.Seg(Z, C, C, ro, T)], B, T, 2 * C, pb, xn, C, bias=bb.buf, bias_off=rbo.offset,
-           epi=L.EPI_RESSKIP, aux0=skip_acc, ld0=C, aux1=x, ld1=C, accum=True, C=C)
+           epi=L.EPI_RESSKIP, aux0=skip_acc, ld0=C, aux1=x, ld1=C, accum=True, C=C, alpha=1.0)
     torch.cuda.synchronize()
     assert rel(Z, z.transpose(1, 2)) < tol
     assert rel(GF[..., :C], gate.transpose(1, 2)) < tol

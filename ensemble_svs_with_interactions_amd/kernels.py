@@ -65,7 +65,7 @@ class PackedBuffer:
         self._max = max(self._max, n)
         return ref
 
-    def add_rowcat(self, srcs, N, K, transpose_blocks=False, scale=1.0):
+    def add_rowcat(self, srcs, N, K, transpose_blocks=False, scale=1.0, kpad_to=BK):
         """One GEMM operand made of several Linear weights.
 
         transpose_blocks=False: rows concatenated  -> packed (len*N) x K   (stacked outputs)
@@ -73,7 +73,7 @@ class PackedBuffer:
         """
         L = len(srcs)
         if not transpose_blocks:
-            Npad, Kp = _roundup(L * N, BM), _roundup(K, BK)
+            Npad, Kp = _roundup(L * N, BM), _roundup(K, kpad_to)
             ref = PackedRef(self.size, L * N, K, 1, Npad, Kp)
             for l, w in enumerate(srcs):
                 sub = PackedRef(self.size + l * N * Kp, N, K, 1, N, Kp)

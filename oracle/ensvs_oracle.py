@@ -271,15 +271,16 @@ def mish(x):
     return x * torch.tanh(F.softplus(x))
 
 
-def diffnet(P, prefix, cfg, spec, t, cond):
+def diffnet(P, prefix, cfg, spec, t, cond, relu_masks=None):
     """DiffNet.forward: spec (B,1,M,T), t (B,), cond (B,E,T) -> (B,1,M,T).
 
     nnsvs/diffsinger/denoiser.py:101-124 with ResidualBlock :54-66.
+    relu_masks: optional {"in", "skip"} (B, C, T) 0/1 masks (mask-matched checks).
     """
     L = cfg["residual_layers"]
     C = cfg["residual_channels"]
-    x = F.relu(F.conv1d(spec[:, 0], P[prefix + "input_projection.weight"],
-                        P[prefix + "input_projection.bias"]))
+    x = _relu(F.conv1d(spec[:, 0], P[prefix + "input_projection.weight"],
+                       P[prefix + "input_projection.bias"]), relu_masks, "in")
     d = sinusoidal_pos_emb(t, C)
     d = F.linear(mish(F.linear(d, P[prefix + "mlp.0.weight"], P[prefix + "mlp.0.bias"])),
                  P[prefix + "mlp.2.weight"], P[prefix + "mlp.2.bias"])
@@ -301,7 +302,8 @@ def diffnet(P, prefix, cfg, spec, t, cond):
         x = (x + res) / math.sqrt(2.0)
         skips.append(skip)
     x = torch.sum(torch.stack(skips), dim=0) / math.sqrt(L)
-    x = F.relu(F.conv1d(x, P[prefix + "skip_projection.weight"], P[prefix + "skip_projection.bias"]))
+    x = _relu(F.conv1d(x, P[prefix + "skip_projection.weight"], P[prefix + "skip_projection.bias"]),
+              relu_masks, "skip")
     x = F.conv1d(x, P[prefix + "output_projection.weight"], P[prefix + "output_projection.bias"])
     return x[:, None]
 

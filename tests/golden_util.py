@@ -86,8 +86,12 @@ def _pre_bn_bias(k):
         parts[-2] in ("1", "5", "9")
 
 
-def grad_close(g, ref, rtol):
-    """Relative L2 error of a gradient tensor (robust to isolated ReLU-kink flips)."""
+def rel_l2(g, ref):
     g = torch.as_tensor(g).double()
     ref = torch.as_tensor(ref).double()
-    return ((g - ref).norm() / (ref.norm() + 1e-30)).item() <= rtol
+    return ((g - ref).norm() / (ref.norm() + 1e-30)).item()
+
+
+def grad_close(g, ref, rtol):
+    """Relative L2 error of a gradient tensor (robust to isolated ReLU-kink flips)."""
+    return rel_l2(g, ref) <= rtol

@@ -1,0 +1,599 @@
+"""Multi-track acoustic models on MI355X kernels.
+
+* ``ResF0NonAttentiveDecoder`` / ``MultiTrackBiLSTMResF0NonAttentiveDecoder``:
+  the cross-singer log-F0 model (nnsvs/acoustic_models/tacotron_f0.py:19-243,
+  757-991): main+sub feature fusion, FF + Conv/BN + bi-LSTM encoder and the
+  free-running autoregressive residual-F0 decoder (persistent ardec kernels).
+* ``MultiTrackNPSSMDNMultistreamParametricModel``: the pairwise ensemble
+  diffusion model (nnsvs/acoustic_models/multistream.py:1482-1778).
+
+Same constructor arguments, forward/inference signatures, prediction types
+and state_dict keys as the reference; ``_target_`` strings are the only change
+a recipe needs (configs.py).
+"""
+import torch
+from torch import nn
+
+from . import _lib
+from . import kernels as K
+from . import layers as Ly
+from ._lib import call, ptr
+from .base import BaseModel, PredictionType
+from .engine import ModulePacks, _sig, empty, grad_of, lengths_pair
+from .model import init_weights
+
+
+class ZoneOutCell(nn.Module):
+    """nnsvs/tacotron/decoder.py:20-48 (container).  The recipe uses zoneout 0, for which
+    the cell output is exactly the LSTMCell output in train and eval modes."""
+
+    def __init__(self, cell, zoneout=0.1):
+        super().__init__()
+        self.cell = cell
+        self.hidden_size = cell.hidden_size
+        self.zoneout = zoneout
+
+
+class ResF0NonAttentiveDecoder(BaseModel):
+    """tacotron_f0.py:19-243 (parameter container; run by the ardec kernels)."""
+
+    def __init__(self, in_dim=512, out_dim=1, layers=2, hidden_dim=1024, prenet_layers=2,
+                 prenet_hidden_dim=256, prenet_dropout=0.5, zoneout=0.1, reduction_factor=1,
+                 downsample_by_conv=False, scaled_tanh=True, in_lf0_idx=300, in_lf0_min=5.3936276,
+                 in_lf0_max=6.491111, out_lf0_idx=180, out_lf0_mean=5.953093881972361,
+                 out_lf0_scale=0.23435173188961034, init_type="none", eval_dropout=True):
+        super().__init__()
+        if prenet_layers != 0 or layers != 1 or out_dim != 1 or zoneout != 0.0 \
+                or reduction_factor != 4 or not downsample_by_conv or not scaled_tanh:
+            raise NotImplementedError(
+                "the MI355X AR decoder implements the multi-track recipe configuration "
+                "(prenet_layers 0, 1 LSTM layer, out_dim 1, zoneout 0, r 4, conv downsample, "
+                "scaled tanh)")
+        self.out_dim = out_dim
+        self.reduction_factor = reduction_factor
+        self.prenet_dropout = prenet_dropout
+        self.scaled_tanh = scaled_tanh
+        self.in_lf0_idx = in_lf0_idx
+        self.in_lf0_min = in_lf0_min
+        self.in_lf0_max = in_lf0_max
+        self.out_lf0_idx = out_lf0_idx
+        self.out_lf0_mean = out_lf0_mean
+        self.out_lf0_scale = out_lf0_scale
+        self.prenet = None
+        lstm_in_dim = in_dim + out_dim
+        self.lstm = nn.ModuleList([ZoneOutCell(nn.LSTMCell(lstm_in_dim, hidden_dim), zoneout)])
+        self.feat_out = nn.Linear(in_dim + hidden_dim, out_dim * reduction_factor, bias=False)
+        self.conv_downsample = nn.Conv1d(in_dim, in_dim, kernel_size=reduction_factor,
+                                         stride=reduction_factor, groups=in_dim)
+        init_weights(self, init_type)
+
+    def is_autoregressive(self):
+        return True
+
+    def has_residual_lf0_prediction(self):
+        return True
+
+
+class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
+    """tacotron_f0.py:757-991: cross-singer log-F0 model (additive main+sub fusion)."""
+
+    def __init__(self, in_dim=512, ff_hidden_dim=2048, conv_hidden_dim=1024, lstm_hidden_dim=256,
+                 num_lstm_layers=2, dropout=0.0, out_dim=80, num_speaker=15, decoder_layers=2,
+                 decoder_hidden_dim=1024, prenet_layers=2, prenet_hidden_dim=256,
+                 prenet_dropout=0.5, zoneout=0.1, reduction_factor=1, downsample_by_conv=False,
+                 scaled_tanh=True, in_lf0_idx=300, in_lf0_min=5.3936276, in_lf0_max=6.491111,
+                 out_lf0_idx=180, out_lf0_mean=5.953093881972361,
+                 out_lf0_scale=0.23435173188961034, use_mdn=False, num_gaussians=4,
+                 sampling_mode="mean", in_ph_start_idx: int = 1, in_ph_end_idx: int = 50,
+                 embed_dim=None, init_type="none"):
+        super().__init__()
+        if use_mdn or embed_dim is None:
+            raise NotImplementedError("use_mdn / no phoneme embedding are not on the path")
+        self.reduction_factor = reduction_factor
+        self.in_lf0_idx = in_lf0_idx
+        self.in_lf0_min = in_lf0_min
+        self.in_lf0_max = in_lf0_max
+        self.out_lf0_idx = out_lf0_idx
+        self.out_lf0_mean = out_lf0_mean
+        self.out_lf0_scale = out_lf0_scale
+        self.use_mdn = use_mdn
+        self.in_dim = in_dim
+        self.in_ph_start_idx = in_ph_start_idx
+        self.in_ph_end_idx = in_ph_end_idx
+        self.num_vocab = in_ph_end_idx - in_ph_start_idx
+        self.embed_dim = embed_dim
+        self.emb = nn.Embedding(self.num_vocab, embed_dim)
+        self.fc_in = nn.Linear(in_dim - self.num_vocab, embed_dim)
+        self.ff = nn.Sequential(
+            nn.Linear(embed_dim, ff_hidden_dim), nn.ReLU(),
+            nn.Linear(ff_hidden_dim, ff_hidden_dim), nn.ReLU(),
+            nn.Linear(ff_hidden_dim, ff_hidden_dim), nn.ReLU())
+        self.conv = nn.Sequential(
+            nn.ReflectionPad1d(3), nn.Conv1d(ff_hidden_dim + 2, conv_hidden_dim, 7, padding=0),
+            nn.BatchNorm1d(conv_hidden_dim), nn.ReLU(),
+            nn.ReflectionPad1d(3), nn.Conv1d(conv_hidden_dim, conv_hidden_dim, 7, padding=0),
+            nn.BatchNorm1d(conv_hidden_dim), nn.ReLU(),
+            nn.ReflectionPad1d(3), nn.Conv1d(conv_hidden_dim, conv_hidden_dim, 7, padding=0),
+            nn.BatchNorm1d(conv_hidden_dim), nn.ReLU())
+        self.lstm = nn.LSTM(conv_hidden_dim, lstm_hidden_dim, num_lstm_layers, bidirectional=True,
+                            batch_first=True, dropout=dropout)
+        decoder_in_dim = 2 * lstm_hidden_dim + 2
+        self.decoder = ResF0NonAttentiveDecoder(
+            in_dim=decoder_in_dim, out_dim=out_dim, layers=decoder_layers,
+            hidden_dim=decoder_hidden_dim, prenet_layers=prenet_layers,
+            prenet_hidden_dim=prenet_hidden_dim, prenet_dropout=prenet_dropout, zoneout=zoneout,
+            reduction_factor=reduction_factor, downsample_by_conv=downsample_by_conv,
+            scaled_tanh=scaled_tanh, in_lf0_idx=-2, in_lf0_min=in_lf0_min, in_lf0_max=in_lf0_max,
+            out_lf0_idx=out_lf0_idx, out_lf0_mean=out_lf0_mean, out_lf0_scale=out_lf0_scale)
+        init_weights(self, init_type)
+        self._packs = ModulePacks()
+        self._ar = None
+
+    def is_autoregressive(self):
+        return True
+
+    def has_residual_lf0_prediction(self):
+        return True
+
+    def _set_lf0_params(self):
+        self.decoder.in_lf0_min = self.in_lf0_min
+        self.decoder.in_lf0_max = self.in_lf0_max
+        self.decoder.out_lf0_mean = self.out_lf0_mean
+        self.decoder.out_lf0_scale = self.out_lf0_scale
+
+    # ------------------------------------------------------------------ packs
+    def _register(self, pk):
+        Ly.phoneme_input_register(pk, self.emb, self.fc_in)
+        Ly.ff_register(pk, self.ff)
+        F = self.ff[4].weight.shape[0]
+        Ly.conv_register(pk, self.conv, first_cols=[("ff", (0, F)), ("s0", (F, F + 1)),
+                                                    ("s1", (F + 1, F + 2))],
+                         first_bwd_cols=["ff"])
+        Ly.lstm_register(pk, self.lstm)
+        cell = self.decoder.lstm[0].cell
+        Ce = self.decoder.conv_downsample.weight.shape[0]
+        H = cell.hidden_size
+        pk.linear("dec_ih_e", cell.weight_ih, cols=(0, Ce))
+        pk.bias_vec("dec_b", cell.bias_ih, b2=cell.bias_hh)
+        pk.linear("dec_fo_e", self.decoder.feat_out.weight, cols=(H, H + Ce))
+
+    def _ar_prepare(self):
+        """Packed W_hh layouts and the contiguous prenet column of W_ih for the ardec kernels."""
+        cell = self.decoder.lstm[0].cell
+        params = [cell.weight_hh, cell.weight_ih]
+        sig = _sig(params)
+        if self._ar is not None and self._ar[0] == sig:
+            return self._ar[1]
+        H = cell.hidden_size
+        dev = cell.weight_hh.device
+        wpf = empty(4 * H * H, device=dev)
+        wpb = empty(4 * H * H, device=dev)
+        call("ensvs_ardec_pack", cell.weight_hh.data_ptr(), H, wpf.data_ptr(), wpb.data_ptr(),
+             Ly.stream())
+        Ce1 = cell.weight_ih.shape[1]
+        wih_p = empty(4 * H, device=dev)
+        call("ensvs_copy_cols", cell.weight_ih.data_ptr() + 4 * (Ce1 - 1), Ce1, wih_p.data_ptr(), 1,
+             4 * H, 1, Ly.stream())
+        self._ar = (sig, (wpf, wpb, wih_p))
+        return self._ar[1]
+
+    # ------------------------------------------------------------------ kernels
+    def _embed(self, pk, x0, x1, ld, B, T, s0, s1, spk_ld, dev):
+        """x = (emb + fc_in + spk)(track 0) + (same)(track 1)   (tacotron_f0.py:929-965)."""
+        M = B * T
+        ph0, ph1 = self.in_ph_start_idx, self.in_ph_end_idx
+        E = self.embed_dim
+        Y = empty(M, E, device=dev)
+        saved = []
+        ids = []
+        for k, x in enumerate((x0, x1)):
+            ph_src, X, Kin, ldx = Ly.gather_input([(x, ld, 0, ld)], ph0, ph1, M, dev)
+            idv = torch.empty(M, dtype=torch.int32, device=dev)
+            t, lds, off = ph_src
+            call("ensvs_phoneme_ids", t.data_ptr() + 4 * off, lds, M, 0, ph1 - ph0, idv.data_ptr(),
+                 Ly.stream())
+            K.gemm([K.Seg(X, ldx, Kin, pk["fc_in"], T)], B, T, E, pk.fwd, Y, E, accum=k > 0,
+                   **pk.bias_ptr_args("fc_in.b"))
+            saved.append(dict(ids=idv, X=X, Kin=Kin, ldx=ldx))
+            ids.append(idv)
+        call("ensvs_embed_add", Y.data_ptr(), E, M, E, T, self.emb.weight.data_ptr(),
+             ids[0].data_ptr(), ids[1].data_ptr(), ptr(s0), ptr(s1), spk_ld, Ly.stream())
+        return Y, saved
+
+    def _fwd(self, x_main, x_sub, ld, B, T, lens_dev, s_main, s_sub, spk_ld, masks=None,
+             training=None, save=True):
+        """Main-track call of the lf0 model.  Returns (lf0 (B*T,), res (B*T,), state)."""
+        self._set_lf0_params()
+        training = self.training if training is None else training
+        pk = self._packs.ensure(self, self._register)
+        dev = self.fc_in.weight.device
+        M = B * T
+        li = self.in_lf0_idx
+        X0, esv = self._embed(pk, x_main, x_sub, ld, B, T, s_main, s_sub, spk_ld, dev)
+        hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
+        F = hs[2].shape[1]
+        a, csv = Ly.conv_fwd(pk, self.conv, [("ff", hs[2], F, F, 0), ("s0", x_main, ld, 1, li),
+                                             ("s1", x_sub, ld, 1, li)], B, T, dev, training,
+                             save=save)
+        C = a.shape[1]
+        y, lsv = Ly.lstm_fwd(pk, self.lstm, a, C, B, T, lens_dev, dev, None, save=save)
+        dec = self.decoder
+        cell = dec.lstm[0].cell
+        H = cell.hidden_size
+        Hl2 = y.shape[1]
+        Ce = Hl2 + 2
+        Tr = T // 4
+        e = empty(B * Tr, Ce, device=dev)
+        call("ensvs_downsample_fwd", y.data_ptr(), Hl2, Hl2, x_main.data_ptr() + 4 * li, ld, 1,
+             x_sub.data_ptr() + 4 * li, ld, 1, dec.conv_downsample.weight.data_ptr(),
+             dec.conv_downsample.bias.data_ptr(), B, T, e.data_ptr(), Ce, Ly.stream())
+        gx = empty(B * Tr, 4 * H, device=dev)
+        K.gemm([K.Seg(e, Ce, Ce, pk["dec_ih_e"], Tr)], B, Tr, 4 * H, pk.fwd, gx, 4 * H,
+               **pk.bias_ptr_args("dec_b"))
+        ofx = empty(B * Tr, 4, device=dev)
+        K.gemm([K.Seg(e, Ce, Ce, pk["dec_fo_e"], Tr)], B, Tr, 4, pk.fwd, ofx, 4)
+        wpf, wpb, wih_p = self._ar_prepare()
+        if masks is None:
+            masks = Ly.dropout_mask(B * Tr, dec.prenet_dropout, dev)
+        lf0 = empty(M, device=dev)
+        res = empty(M, device=dev)
+        sg = empty(B * Tr, 4 * H, device=dev)
+        sc = empty(B * Tr, H, device=dev)
+        sh = empty(B * Tr, H, device=dev)
+        so = empty(B * Tr, 4, device=dev)
+        sp = empty(B * Tr, device=dev)
+        call("ensvs_ardec_fwd", gx.data_ptr(), 4 * H, ofx.data_ptr(), 4, wpf.data_ptr(),
+             wih_p.data_ptr(), dec.feat_out.weight.data_ptr(), dec.feat_out.weight.shape[1],
+             x_main.data_ptr() + 4 * li, ld, masks.data_ptr(), B, T, H, float(dec.in_lf0_min),
+             float(dec.in_lf0_max), float(dec.out_lf0_mean), float(dec.out_lf0_scale),
+             lf0.data_ptr(), res.data_ptr(), sg.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+             so.data_ptr(), sp.data_ptr(), Ly.stream())
+        st = None
+        if save:
+            st = dict(X0=X0, esv=esv, hs=hs, csv=csv, lsv=lsv, y=y, e=e, masks=masks, sg=sg,
+                      sc=sc, sh=sh, so=so, sp=sp, B=B, T=T, lens=lens_dev, x_main=x_main,
+                      x_sub=x_sub, ld=ld)
+        return lf0, res, st
+
+    def _bn_only(self, x_main, x_sub, ld, B, T, s_main, s_sub, spk_ld):
+        """Forward of a call whose outputs are unused in training (the sub-track call with
+        output_subtrack=False, multistream.py:1649-1651): only its BatchNorm running-statistic
+        updates are observable, so only embed + FF + the conv/BN stack run."""
+        pk = self._packs.ensure(self, self._register)
+        dev = self.fc_in.weight.device
+        li = self.in_lf0_idx
+        X0, _ = self._embed(pk, x_main, x_sub, ld, B, T, s_main, s_sub, spk_ld, dev)
+        hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
+        F = hs[2].shape[1]
+        Ly.conv_fwd(pk, self.conv, [("ff", hs[2], F, F, 0), ("s0", x_main, ld, 1, li),
+                                    ("s1", x_sub, ld, 1, li)], B, T, dev, True, save=False)
+
+    def _bwd(self, st, dlf0, dres=None, want_spk=True):
+        """dlf0 / dres: (B*T,) grads of the lf0 / residual outputs.  Returns per-sequence
+        grads of the main / sub speaker vectors (B, E) each."""
+        pk = self._packs
+        dev = dlf0.device
+        B, T = st["B"], st["T"]
+        M, Tr = B * T, T // 4
+        dec = self.decoder
+        cell = dec.lstm[0].cell
+        H = cell.hidden_size
+        Ce = st["e"].shape[1]
+        wpf, wpb, wih_p = self._ar_prepare()
+        dg = empty(B * Tr, 4 * H, device=dev)
+        do4 = empty(B * Tr, 4, device=dev)
+        call("ensvs_ardec_bwd", dlf0.data_ptr(), ptr(dres), wpb.data_ptr(), wih_p.data_ptr(),
+             dec.feat_out.weight.data_ptr(), dec.feat_out.weight.shape[1], st["masks"].data_ptr(),
+             B, T, H, float(dec.in_lf0_min), float(dec.in_lf0_max), float(dec.out_lf0_mean),
+             float(dec.out_lf0_scale), st["sg"].data_ptr(), st["sc"].data_ptr(),
+             st["so"].data_ptr(), dg.data_ptr(), do4.data_ptr(), Ly.stream())
+        wg = Ly.wgrad_into
+        # decoder weights
+        wg(cell.weight_hh, dg, 4 * H, st["sh"], H, B, Tr, Tr, 4 * H, H, shift0=-1)
+        wg(cell.weight_ih, dg, 4 * H, st["e"], Ce, B, Tr, Tr, 4 * H, Ce, col0=0)
+        wg(cell.weight_ih, dg, 4 * H, st["sp"], 1, B, Tr, Tr, 4 * H, 1, col0=Ce)
+        Ly.colsum_into(dg, 4 * H, B * Tr, 4 * H, cell.bias_ih)
+        Ly.colsum_into(dg, 4 * H, B * Tr, 4 * H, cell.bias_hh)
+        wg(dec.feat_out.weight, do4, 4, st["sh"], H, B, Tr, Tr, 4, H, col0=0)
+        wg(dec.feat_out.weight, do4, 4, st["e"], Ce, B, Tr, Tr, 4, Ce, col0=H)
+        de = empty(B * Tr, Ce, device=dev)
+        K.gemm([K.Seg(dg, 4 * H, 4 * H, pk["dec_ih_e^T"], Tr),
+                K.Seg(do4, 4, 4, pk["dec_fo_e^T"], Tr)], B, Tr, Ce, pk.bwd, de, Ce)
+        Hl2 = st["y"].shape[1]
+        dy = empty(M, Hl2, device=dev)
+        li = self.in_lf0_idx
+        call("ensvs_downsample_bwd", de.data_ptr(), Ce, st["y"].data_ptr(), Hl2, Hl2,
+             st["x_main"].data_ptr() + 4 * li, st["ld"], 1, st["x_sub"].data_ptr() + 4 * li,
+             st["ld"], 1, dec.conv_downsample.weight.data_ptr(), B, T, dy.data_ptr(), Hl2,
+             grad_of(dec.conv_downsample.weight).data_ptr(),
+             grad_of(dec.conv_downsample.bias).data_ptr(), Ly.stream())
+        # encoder
+        da = Ly.lstm_bwd(pk, self.lstm, st["lsv"], dy, B, T, st["lens"], dev)
+        F = st["hs"][2].shape[1]
+        (dh3,) = Ly.conv_bwd(pk, self.conv, st["csv"], da, B, T, dev, first_dx=[("ff", F)])
+        dX0 = Ly.ff_bwd(pk, self.ff, st["X0"], st["hs"], dh3, B, T, dev)
+        E = self.embed_dim
+        dspk = torch.zeros(B, E, device=dev) if want_spk else None
+        for k, sv in enumerate(st["esv"]):
+            Ly.embed_bwd(self.emb, self.fc_in, sv, dX0, B, T, dspk if k == 0 else None)
+        # both tracks' speaker vectors receive the same per-sequence sum
+        return dspk, dspk, dX0
+
+    # ---------------------------------------------------------------- reference API
+    def forward(self, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths=None, y=None):
+        if y is not None:
+            raise NotImplementedError("teacher-forced lf0 decoding is not used by the "
+                                      "multi-track diffusion model (multistream.py:1646-1651)")
+        return _Lf0Fn.apply(self, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths,
+                            self.fc_in.weight)
+
+
+class _Lf0Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mod, x_main, x_sub, s0, s1, lengths, anchor):
+        from .model import _spk_args
+        B, T, D = x_main.shape
+        x_main = x_main.contiguous().float()
+        x_sub = x_sub.contiguous().float()
+        _, lens_dev = lengths_pair(lengths, B, T, x_main.device)
+        p0, ld0, f0 = _spk_args(s0, B, T)
+        p1, ld1, f1 = _spk_args(s1, B, T)
+        if f0 is not None or f1 is not None or ld0 != ld1:
+            raise NotImplementedError("per-frame speaker embeddings are not on the path")
+        lf0, res, st = mod._fwd(x_main, x_sub, D, B, T, lens_dev, p0, p1, ld0)
+        ctx.mod, ctx.st = mod, st
+        ctx.needs = (s0 is not None and s0.requires_grad, s1 is not None and s1.requires_grad)
+        return lf0.view(B, T, 1), res.view(B, T, 1)
+
+    @staticmethod
+    def backward(ctx, glf0, gres):
+        st = ctx.st
+        B, T = st["B"], st["T"]
+        dev = st["y"].device
+        glf0 = glf0.contiguous().view(-1) if glf0 is not None else torch.zeros(B * T, device=dev)
+        gres = gres.contiguous().view(-1) if gres is not None else None
+        _, _, dX0 = ctx.mod._bwd(st, glf0, gres, want_spk=False)
+        ctx.st = None
+        # per-frame grad of each (expanded) speaker embedding = grad of the fused input
+        d = dX0.view(B, T, -1)
+        return (None, None, None, d if ctx.needs[0] else None, d if ctx.needs[1] else None,
+                None, None)
+
+
+class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
+    """multistream.py:1482-1778: pairwise (main, sub) ensemble diffusion model."""
+
+    def __init__(self, in_dim: int, out_dim: int, stream_sizes: list, reduction_factor: int,
+                 lf0_model: nn.Module, mgc_model: nn.Module, bap_model: nn.Module,
+                 vuv_model: nn.Module, speaker_embedding: nn.Module, in_rest_idx=0, in_lf0_idx=51,
+                 in_lf0_min=5.3936276, in_lf0_max=6.491111, out_lf0_idx=60,
+                 out_lf0_mean=5.953093881972361, out_lf0_scale=0.23435173188961034,
+                 vuv_model_bap_conditioning=True, vuv_model_bap0_conditioning=False,
+                 vuv_model_lf0_conditioning=True, vuv_model_mgc_conditioning=False,
+                 output_subtrack=False):
+        super().__init__()
+        self.in_dim = in_dim
+        self.out_dim = out_dim
+        self.stream_sizes = stream_sizes
+        self.reduction_factor = reduction_factor
+        self.vuv_model_bap_conditioning = vuv_model_bap_conditioning
+        self.vuv_model_bap0_conditioning = vuv_model_bap0_conditioning
+        self.vuv_model_lf0_conditioning = vuv_model_lf0_conditioning
+        self.vuv_model_mgc_conditioning = vuv_model_mgc_conditioning
+        self.output_subtrack = output_subtrack
+        assert len(stream_sizes) in [4]
+        self.lf0_model = lf0_model
+        self.mgc_model = mgc_model
+        self.bap_model = bap_model
+        self.vuv_model = vuv_model
+        self.speaker_embedding = speaker_embedding
+        self.in_rest_idx = in_rest_idx
+        self.in_lf0_idx = in_lf0_idx
+        self.in_lf0_min = in_lf0_min
+        self.in_lf0_max = in_lf0_max
+        self.out_lf0_idx = out_lf0_idx
+        self.out_lf0_mean = out_lf0_mean
+        self.out_lf0_scale = out_lf0_scale
+
+    def _set_lf0_params(self):
+        if hasattr(self.lf0_model, "out_lf0_mean"):
+            self.lf0_model.in_lf0_min = self.in_lf0_min
+            self.lf0_model.in_lf0_max = self.in_lf0_max
+            self.lf0_model.out_lf0_mean = self.out_lf0_mean
+            self.lf0_model.out_lf0_scale = self.out_lf0_scale
+
+    def prediction_type(self):
+        return PredictionType.MULTISTREAM_HYBRID
+
+    def is_autoregressive(self):
+        return True  # the lf0 model is autoregressive
+
+    def has_residual_lf0_prediction(self):
+        return True
+
+    # ------------------------------------------------------------------ helpers
+    def _stream_cols(self):
+        s = self.stream_sizes
+        o = [0]
+        for n in s:
+            o.append(o[-1] + n)
+        return o  # mgc [o0,o1) lf0 [o1,o2) vuv [o2,o3) bap [o3,o4)
+
+    def _vuv_sources(self, x, ldx, y, ldy):
+        o = self._stream_cols()
+        src = [(x, ldx, 0, ldx)]
+        if self.vuv_model_mgc_conditioning:
+            src.append((y, ldy, o[0], o[1] - o[0]))
+        if self.vuv_model_lf0_conditioning:
+            src.append((y, ldy, o[1], o[2] - o[1]))
+        if self.vuv_model_bap_conditioning:
+            n = 1 if self.vuv_model_bap0_conditioning else o[4] - o[3]
+            src.append((y, ldy, o[3], n))
+        # merge adjacent column ranges of the same tensor
+        merged = [src[0]]
+        for s in src[1:]:
+            p = merged[-1]
+            if s[0] is p[0] and p[2] + p[3] == s[2]:
+                merged[-1] = (p[0], p[1], p[2], p[3] + s[3])
+            else:
+                merged.append(s)
+        return merged
+
+    def _spk_vectors(self, spk0, spk1, B):
+        table = self.speaker_embedding.emb.weight
+        E = table.shape[1]
+        out = []
+        for s in (spk0, spk1):
+            idx = s.reshape(-1).to(device=table.device, dtype=torch.int64).contiguous()
+            v = empty(B, E, device=table.device)
+            call("ensvs_gather_rows", table.data_ptr(), idx.data_ptr(), B, E, v.data_ptr(),
+                 Ly.stream())
+            out.append((v, idx))
+        return out
+
+    # ------------------------------------------------------------------ training
+    def _train_fwd(self, x_main, x_sub, y_main, spk0, spk1, lengths, draws=None):
+        """One training forward.  x_* (B, T, in_dim), y_main (B, T, out_dim) contiguous fp32
+        device tensors.  Returns (outputs dict of (B*T, .) tensors, state)."""
+        self._set_lf0_params()
+        draws = draws or {}
+        B, T, D = x_main.shape
+        Dy = y_main.shape[2]
+        dev = x_main.device
+        lens_host, lens_dev = lengths_pair(lengths, B, T, dev)
+        (s0, i0), (s1, i1) = self._spk_vectors(spk0, spk1, B)
+        E = s0.shape[1]
+        lf0, res, st_lf0 = self.lf0_model._fwd(x_main, x_sub, D, B, T, lens_dev, s0, s1, E,
+                                               masks=draws.get("lf0_main"))
+        if self.training:
+            # sub-track call (outputs unused without output_subtrack): BN statistics only
+            self.lf0_model._bn_only(x_sub, x_main, D, B, T, s1, s0, E)
+        o = self._stream_cols()
+        enc_src = [(x_main, D, 0, D), (y_main, Dy, o[1], o[2] - o[1])]
+        nm, rm, st_mgc = self.mgc_model._fwd(enc_src, B, T, lens_dev, (y_main, Dy, o[0]), s0, E,
+                                             t=draws.get("mgc_t"), noise=draws.get("mgc_noise"))
+        nb, rb, st_bap = self.bap_model._fwd(enc_src, B, T, lens_dev, (y_main, Dy, o[3]), s0, E,
+                                             t=draws.get("bap_t"), noise=draws.get("bap_noise"))
+        vuv, st_vuv = self.vuv_model._fwd(self._vuv_sources(x_main, D, y_main, Dy), B, T,
+                                          lens_dev, s0, E, lstm_masks=draws.get("vuv_lstm"))
+        outs = dict(mgc_noise=nm, mgc_recon=rm, lf0=lf0, vuv=vuv, bap_noise=nb, bap_recon=rb,
+                    lf0_residual=res)
+        st = dict(lf0=st_lf0, mgc=st_mgc, bap=st_bap, vuv=st_vuv, i0=i0, i1=i1, B=B, T=T, E=E,
+                  lens_host=lens_host, lens_dev=lens_dev)
+        return outs, st
+
+    def _train_bwd(self, st, g):
+        """g: dict of grads (B*T, .) for mgc_recon, lf0, vuv, bap_recon [, lf0_residual]."""
+        B, E = st["B"], st["E"]
+        dev = st["lens_dev"].device
+        ds0 = torch.zeros(B, E, device=dev)
+        dsp = self.mgc_model._bwd(st["mgc"], g["mgc_recon"])
+        call("ensvs_axpy", ds0.data_ptr(), dsp.data_ptr(), 1.0, B * E, Ly.stream())
+        dsp = self.bap_model._bwd(st["bap"], g["bap_recon"])
+        call("ensvs_axpy", ds0.data_ptr(), dsp.data_ptr(), 1.0, B * E, Ly.stream())
+        _, dsp = self.vuv_model._bwd(st["vuv"], g["vuv"], want_spk=True)
+        call("ensvs_axpy", ds0.data_ptr(), dsp.data_ptr(), 1.0, B * E, Ly.stream())
+        dmain, dsub, _ = self.lf0_model._bwd(st["lf0"], g["lf0"], g.get("lf0_residual"))
+        call("ensvs_axpy", ds0.data_ptr(), dmain.data_ptr(), 1.0, B * E, Ly.stream())
+        table = grad_of(self.speaker_embedding.emb.weight)
+        call("ensvs_spk_scatter", ds0.data_ptr(), B, E, st["i0"].data_ptr(), table.data_ptr(),
+             Ly.stream())
+        call("ensvs_spk_scatter", dsub.data_ptr(), B, E, st["i1"].data_ptr(), table.data_ptr(),
+             Ly.stream())
+
+    # ------------------------------------------------------------------ inference
+    def _infer(self, x_main, x_sub, spk0, spk1, lengths, noises=None, masks=None):
+        self._set_lf0_params()
+        B, T, D = x_main.shape
+        dev = x_main.device
+        _, lens_dev = lengths_pair(lengths, B, T, dev)
+        (s0, _), (s1, _) = self._spk_vectors(spk0, spk1, B)
+        E = s0.shape[1]
+        lf0, _, _ = self.lf0_model._fwd(x_main, x_sub, D, B, T, lens_dev, s0, s1, E,
+                                        masks=masks, training=False, save=False)
+        o = self._stream_cols()
+        Dy = self.out_dim
+        out = empty(B * T, Dy, device=dev)
+        call("ensvs_copy_cols", lf0.data_ptr(), 1, out.data_ptr() + 4 * o[1], Dy, B * T, 1,
+             Ly.stream())
+        enc_src = [(x_main, D, 0, D), (out, Dy, o[1], 1)]
+        nz = noises or {}
+        mgc = self.mgc_model._inference(enc_src, B, T, lens_dev, s0, E, nz.get("mgc"))
+        bap = self.bap_model._inference(enc_src, B, T, lens_dev, s0, E, nz.get("bap"))
+        call("ensvs_copy_cols", mgc.data_ptr(), o[1] - o[0], out.data_ptr() + 4 * o[0], Dy, B * T,
+             o[1] - o[0], Ly.stream())
+        call("ensvs_copy_cols", bap.data_ptr(), o[4] - o[3], out.data_ptr() + 4 * o[3], Dy, B * T,
+             o[4] - o[3], Ly.stream())
+        vuv, _ = self.vuv_model._fwd(self._vuv_sources(x_main, D, out, Dy), B, T, lens_dev, s0, E,
+                                     training=False, save=False)
+        call("ensvs_copy_cols", vuv.data_ptr(), 1, out.data_ptr() + 4 * o[2], Dy, B * T, 1,
+             Ly.stream())
+        return out.view(B, T, Dy)
+
+    # ---------------------------------------------------------------- reference API
+    def forward(self, x_main, x_sub, spks_list, lengths=None, ys=None):
+        assert x_main.shape[-1] == self.in_dim
+        if ys is None:
+            out = self._infer(x_main.contiguous().float(), x_sub.contiguous().float(),
+                              spks_list[0], spks_list[1], lengths)
+            return out, out
+        if self.output_subtrack:
+            raise NotImplementedError("output_subtrack=True (interaction-loss variant) is the "
+                                      "next step of the build")
+        outs = _MultiTrackFn.apply(self, x_main, x_sub, ys[0], spks_list[0], spks_list[1],
+                                   lengths, self.speaker_embedding.emb.weight)
+        nm, rm, lf0, vuv, nb, rb, res = outs
+        return ((nm, rm), lf0, vuv, (nb, rb)), res
+
+    def inference(self, x_main, x_sub, spks=None, lengths=None):
+        """pad_inference_multitrack (acoustic_models/util.py:154-188): replicate-pad to a
+        multiple of r (r frames when already divisible), run, trim."""
+        r = self.reduction_factor
+        B, T, D = x_main.shape
+        lens = [int(v) for v in (lengths if lengths is not None else [T] * B)]
+        pad = r - max(lens) % r
+        dev = x_main.device
+        xs = []
+        for x in (x_main, x_sub):
+            x = x.contiguous().float()
+            xp = empty(B, T + pad, D, device=dev)
+            call("ensvs_copy_cols", x.data_ptr(), T * D, xp.data_ptr(), (T + pad) * D, B, T * D,
+                 Ly.stream())
+            for k in range(pad):  # replicate the last frame
+                call("ensvs_copy_cols", x.data_ptr() + 4 * (T - 1) * D, T * D,
+                     xp.data_ptr() + 4 * (T + k) * D, (T + pad) * D, B, D, Ly.stream())
+            xs.append(xp)
+        out = self._infer(xs[0], xs[1], spks[0], spks[1], [v + pad for v in lens])
+        return out[:, :-pad]
+
+
+class _MultiTrackFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mod, x_main, x_sub, y_main, spk0, spk1, lengths, anchor):
+        B, T, _ = x_main.shape
+        outs, st = mod._train_fwd(x_main.contiguous().float(), x_sub.contiguous().float(),
+                                  y_main.contiguous().float(), spk0, spk1, lengths)
+        ctx.mod, ctx.st = mod, st
+        ctx.mark_non_differentiable(outs["mgc_noise"], outs["bap_noise"])
+        v = lambda t: t.view(B, T, -1)  # noqa: E731
+        return (v(outs["mgc_noise"]), v(outs["mgc_recon"]), v(outs["lf0"]), v(outs["vuv"]),
+                v(outs["bap_noise"]), v(outs["bap_recon"]), v(outs["lf0_residual"]))
+
+    @staticmethod
+    def backward(ctx, g_nm, g_rm, g_lf0, g_vuv, g_nb, g_rb, g_res):
+        st = ctx.st
+        B, T = st["B"], st["T"]
+        dev = st["lens_dev"].device
+
+        def flat(g, n):
+            if g is None:
+                return torch.zeros(B * T, n, device=dev)
+            return g.contiguous().view(B * T, n)
+        g = dict(mgc_recon=flat(g_rm, g_rm.shape[-1] if g_rm is not None else 60),
+                 lf0=flat(g_lf0, 1).view(-1), vuv=flat(g_vuv, 1),
+                 bap_recon=flat(g_rb, g_rb.shape[-1] if g_rb is not None else 5))
+        if g_res is not None:
+            g["lf0_residual"] = g_res.contiguous().view(-1)
+        ctx.mod._train_bwd(st, g)
+        ctx.st = None
+        return (None,) * 8

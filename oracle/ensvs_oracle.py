@@ -238,7 +238,7 @@ def resf0_decoder(P, prefix, cfg, enc, dropout_masks):
 
 
 def lf0_model(P, prefix, cfg, x_main, x_sub, spk_main, spk_sub, lengths, dropout_masks,
-              training=True, bn_updates=None, fast=False):
+              training=True, bn_updates=None, fast=False, relu_masks=None):
     """MultiTrackBiLSTMResF0NonAttentiveDecoder.forward (tacotron_f0.py:924-991)."""
     li = cfg["in_lf0_idx"]
     s_main = x_main[:, :, li].unsqueeze(-1)
@@ -246,9 +246,9 @@ def lf0_model(P, prefix, cfg, x_main, x_sub, spk_main, spk_sub, lengths, dropout
     a = phoneme_embed(P, prefix, x_main, cfg["in_ph_start_idx"], cfg["in_ph_end_idx"]) + spk_main
     b = phoneme_embed(P, prefix, x_sub, cfg["in_ph_start_idx"], cfg["in_ph_end_idx"]) + spk_sub
     x = a + b
-    out = ff_stack(P, prefix, x)
+    out = ff_stack(P, prefix, x, relu_masks)
     out = torch.cat([out, s_main, s_sub], -1)
-    out = conv_stack(P, prefix, out, training, bn_updates)
+    out = conv_stack(P, prefix, out, training, bn_updates, masks=relu_masks)
     out = bilstm(P, prefix, out, lengths, cfg["num_lstm_layers"], None, fast)
     out = torch.cat([out, s_main[:, :out.shape[1]], s_sub[:, :out.shape[1]]], -1)
     dcfg = dict(cfg)

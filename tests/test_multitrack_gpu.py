@@ -1,0 +1,131 @@
+"""Multi-track lf0 model, full pairwise model and the fused train step on MI355X."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ensvs_oracle as O
+from ensemble_svs_with_interactions_amd import configs, engine
+from ensemble_svs_with_interactions_amd.train import FusedAdam, train_step
+from golden_util import load_case, full_shapes, rel, grad_close, rel_l2, _pre_bn_bias
+from gpu_util import build
+
+pytestmark = pytest.mark.gpu
+CFG = configs.multitrack_diffusion(num_speakers=4)
+
+
+def _masks(st, B, T):
+    m = {}
+    for n, i in enumerate((0, 2, 4)):
+        m[f"ff{i}"] = (st["hs"][n] > 0).float().cpu().view(B, T, -1)
+    for li, bi in enumerate((2, 6, 10)):
+        m[f"bn{bi}"] = (st["csv"][li]["out"] > 0).float().cpu().view(B, T, -1)
+    return m
+
+
+def test_lf0_model_matches_reference():
+    engine.set_gemm_precision("fp32")
+    a, meta = load_case("lf0_model")
+    cfg = dict(CFG["lf0_model"])
+    mod = build(cfg, full_shapes(), "lf0_model.")
+    for k, v in meta["lf0_stats"].items():
+        setattr(mod, k, v)
+    mod.train()
+    P0 = {k: v.detach().cpu().clone() for k, v in mod.state_dict().items()}
+    B, T, D = a["x_main"].shape
+    xm = torch.from_numpy(a["x_main"]).cuda()
+    xs = torch.from_numpy(a["x_sub"]).cuda()
+    s0 = torch.from_numpy(a["spk_main"]).cuda().view(B, -1).contiguous()
+    s1 = torch.from_numpy(a["spk_sub"]).cuda().view(B, -1).contiguous()
+    lens = torch.tensor(a["lengths"].tolist(), device="cuda")
+    masks = torch.from_numpy(a["masks"]).cuda().view(-1).contiguous()
+    lf0, res, st = mod._fwd(xm, xs, D, B, T, lens, s0, s1, s0.shape[1], masks=masks)
+    R1 = torch.from_numpy(a["R1"]).cuda().view(-1).contiguous()
+    R2 = torch.from_numpy(a["R2"]).cuda().view(-1).contiguous()
+    d0, d1, _ = mod._bwd(st, R1, R2)
+    torch.cuda.synchronize()
+    assert rel(lf0.cpu().view(B, T, 1), a["lf0"]) < 1e-4
+    assert rel(res.cpu().view(B, T, 1), a["res"]) < 1e-4
+    # mask-matched oracle backward
+    ocfg = dict(cfg)
+    ocfg.update(meta["lf0_stats"])
+    Pg = {k: (v.clone() if "running" in k else v.clone().requires_grad_())
+          for k, v in P0.items() if v.dtype == torch.float32}
+    sm = torch.from_numpy(a["spk_main"]).requires_grad_()
+    ss = torch.from_numpy(a["spk_sub"]).requires_grad_()
+    ol, orr = O.lf0_model(Pg, "", ocfg, torch.from_numpy(a["x_main"]), torch.from_numpy(a["x_sub"]),
+                          sm.expand(B, T, -1), ss.expand(B, T, -1), a["lengths"],
+                          torch.from_numpy(a["masks"]), relu_masks=_masks(st, B, T))
+    ((ol * torch.from_numpy(a["R1"])).sum() + (orr * torch.from_numpy(a["R2"])).sum()).backward()
+    assert rel(d0.cpu(), sm.grad.view(B, -1)) < 2e-4
+    for k, p in mod.named_parameters():
+        if _pre_bn_bias(k):
+            continue
+        assert rel(p.grad.cpu(), Pg[k].grad) < 5e-4, k
+    assert grad_close(d0.cpu(), torch.from_numpy(a["d_spk_main"]).view(B, -1), 5e-2)
+
+
+def _draws(a, pfx, B, T):
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(a[pfx + k])).cuda()  # noqa: E731
+    return dict(
+        lf0_main=t("lf0_main").view(-1).contiguous(),
+        mgc_t=t("mgc_t"), bap_t=t("bap_t"),
+        mgc_noise=t("mgc_noise")[:, 0].transpose(1, 2).contiguous().view(B * T, -1),
+        bap_noise=t("bap_noise")[:, 0].transpose(1, 2).contiguous().view(B * T, -1))
+
+
+def _batch(a):
+    g = lambda k: torch.from_numpy(a[k]).cuda().contiguous()  # noqa: E731
+    return g("x_main"), g("x_sub"), g("y_main"), g("spk_main"), g("spk_sub"), a["lengths"].tolist()
+
+
+def test_model_forward_full():
+    engine.set_gemm_precision("fp32")
+    a, meta = load_case("model_forward_full")
+    model = build(configs.multitrack_diffusion(num_speakers=4), meta["shapes"])
+    model.train()
+    model.vuv_model.lstm.dropout = 0.0
+    xm, xs, ym, s0, s1, lens = _batch(a)
+    B, T = xm.shape[:2]
+    outs, st = model._train_fwd(xm, xs, ym, s0, s1, lens, _draws(a, "draw::", B, T))
+    torch.cuda.synchronize()
+    v = lambda k: outs[k].cpu().view(B, T, -1)  # noqa: E731
+    assert rel(v("mgc_recon"), a["mgc_recon"]) < 1e-4
+    assert rel(v("bap_recon"), a["bap_recon"]) < 1e-4
+    assert rel(v("lf0"), a["lf0"]) < 1e-4
+    assert rel(v("lf0_residual"), a["res"]) < 1e-4
+    assert rel(v("vuv"), a["vuv"]) < 1e-4
+
+
+def test_train_step_tiny_matches_reference():
+    engine.set_gemm_precision("fp32")
+    a, meta = load_case("train_step_tiny")
+    model = build(configs.multitrack_diffusion(num_speakers=4, tiny=True), meta["shapes"])
+    model.vuv_model.lstm.dropout = 0.0
+    opt = FusedAdam(model, lr=meta["lr"])
+    xm, xs, ym, s0, s1, lens = _batch(a)
+    B, T = xm.shape[:2]
+    p0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    for s in range(meta["steps"]):
+        loss, norm = train_step(model, opt, xm, xs, ym, s0, s1, lens,
+                                draws=_draws(a, f"draw{s}::", B, T))
+        torch.cuda.synchronize()
+        print(f"step {s}: loss {loss.item():.7f} ref {meta['losses'][s]:.7f} | "
+              f"norm {norm.item():.6f} ref {meta['grad_norms'][s]:.6f}")
+        assert abs(loss.item() - meta["losses"][s]) < 1e-5 * abs(meta["losses"][s])
+        assert abs(norm.item() - meta["grad_norms"][s]) < 2e-2 * meta["grad_norms"][s]
+        if s == 0:
+            bad = []
+            for k, v in model.state_dict().items():
+                if v.dtype != torch.float32 or "delta0::" + k not in a or _pre_bn_bias(k):
+                    continue
+                d = (v - p0[k]).cpu()
+                ref = torch.from_numpy(a["delta0::" + k])
+                # Adam's first step is ~lr*sign(g): count elements off by > lr/10
+                frac = ((d - ref).abs() > 0.1 * meta["lr"]).float().mean().item()
+                if frac > 0.02:
+                    bad.append((k, frac))
+            assert not bad, bad[:5]
+    sd = model.state_dict()
+    for k in sd:
+        if "running" in k and "final::" + k in a:
+            assert rel(sd[k].cpu(), a["final::" + k]) < 1e-4, k

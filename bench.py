@@ -1,0 +1,222 @@
+"""Throughput bench of the MI355X multi-track SVS training step.
+
+Metric (BASELINE.json): acoustic-model train frames/sec (4-track ensemble), i.e.
+main-track frames of (main, sub) pairs through forward + backward + clip + Adam
+of MultiTrackNPSSMDNMultistreamParametricModel (recipe diffusion config,
+23.5 M parameters, 4 speakers).  Workload per GPU: 3 SATB segments x 10 (i <= j)
+pairs = 30 pairs x 1024 frames of synthetic features.
+GEMMs run on bf16 MFMA with fp32 accumulation; everything else fp32.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+Multi-GPU: one process per GPU via torch.distributed.run, RCCL gradient
+all-reduce, pairs sharded per rank (weak scaling).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from ensemble_svs_with_interactions_amd import configs, data, engine  # noqa: E402
+from ensemble_svs_with_interactions_amd.train import FusedAdam, train_step  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+TRAIN_FLOP_PER_FRAME = 127.5e6  # SURVEY.md §6 (torch.utils.flop_counter on the oracle)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pairs", type=int, default=30)
+    ap.add_argument("--frames", type=int, default=1024)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def gate_gemm_timing(model, P, T, dev, iters=20):
+    """Average duration of the dominant kernel (mgc DiffNet block gate GEMM:
+    M = P*T frames, N = 2C = 512, K = 3C + E = 1024) with HIP events on its stream."""
+    net = model.mgc_model.denoise_fn
+    C, E, L = net.C, net.E, len(net.residual_layers)
+    M = P * T
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(M, C, device=dev, generator=g)
+    cond = torch.randn(M, E, device=dev, generator=g)
+    ds = torch.randn(P, L * C, device=dev, generator=g)
+    z = torch.empty(M, C, device=dev)
+    gf = torch.empty(M, 2 * C, device=dev)
+    net._packs.ensure(net, net._register)
+    for _ in range(3):
+        net._gate_gemm(0, x, cond, E, ds, P, T, z, gf)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        net._gate_gemm(0, x, cond, E, ds, P, T, z, gf)
+    e.record()
+    torch.cuda.synchronize()
+    sec = s.elapsed_time(e) / 1e3 / iters
+    flops = 2.0 * M * (2 * C) * (3 * C + E)
+    return sec, flops
+
+
+def cpu_baseline(args, budget_s):
+    """The oracle (CPU PyTorch restatement of the reference, fused CPU LSTM) on host
+    cores: full-size model, bounded sample of the same workload."""
+    from oracle import ensvs_oracle as O
+    from oracle.weights import seeded_state_dict
+    cores = os.cpu_count() or 1
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    torch.set_num_threads(cores)
+    cfg = configs.multitrack_diffusion(num_speakers=4)
+    model = configs.instantiate(cfg)
+    shapes = {k: tuple(v.shape) for k, v in model.state_dict().items()}
+    del model
+    P = {k: torch.from_numpy(v) for k, v in seeded_state_dict(shapes, 1).items()}
+    for pre in ("mgc_model.", "bap_model."):
+        for k, v in O.diffusion_schedule().items():
+            P[pre + k] = v
+    trainable = [k for k in P if "running" not in k and k.rsplit(".", 1)[-1] not in
+                 O.diffusion_schedule()]
+    Pp, T = 6, 1024
+    b = data.synthetic_batch(Pp, T, 7)
+    x = (torch.from_numpy(b["x_main"]), torch.from_numpy(b["x_sub"]))
+    y = (torch.from_numpy(b["y_main"]), torch.from_numpy(b["y_sub"]))
+    spk = (torch.from_numpy(b["spk_main"]), torch.from_numpy(b["spk_sub"]))
+    rng = torch.Generator().manual_seed(3)
+    state, times = {}, []
+    t_start = time.time()
+    step = 0
+    while True:
+        for k in trainable:
+            P[k] = P[k].detach().requires_grad_()
+        draws = dict(
+            lf0_main=(torch.rand(Pp, T // 4, 1, generator=rng) < 0.5).float() * 2,
+            lf0_sub=(torch.rand(Pp, T // 4, 1, generator=rng) < 0.5).float() * 2,
+            mgc_t=torch.randint(0, 100, (Pp,), generator=rng),
+            mgc_noise=torch.randn(Pp, 1, 60, T, generator=rng),
+            bap_t=torch.randint(0, 100, (Pp,), generator=rng),
+            bap_noise=torch.randn(Pp, 1, 5, T, generator=rng),
+            vuv_lstm=[(torch.rand(Pp, T, 128, generator=rng) > 0.1).float() / 0.9])
+        t0 = time.time()
+        preds, _ = O.model_forward(P, cfg, x[0], x[1], spk, b["lengths"], y, draws,
+                                   bn_updates={}, fast=True)
+        loss = O.masked_l1_loss(preds, y[0], b["lengths"], cfg["stream_sizes"])
+        loss.backward()
+        grads = {k: P[k].grad for k in trainable}
+        params = {k: P[k].detach() for k in trainable}
+        O.clip_and_adam(params, grads, state, step=step + 1)
+        P.update(params)
+        times.append(time.time() - t0)
+        step += 1
+        if time.time() - t_start > budget_s and step >= 3:
+            break
+    sec = float(np.median(times[1:]))
+    return dict(value=Pp * T / sec, unit="main-track frames/s", cores=cores, kind="port",
+                sample=f"oracle (CPU PyTorch restatement, fused CPU LSTM) full-size model, "
+                       f"{Pp} pairs x {T} frames fp32, median of {len(times) - 1} steps "
+                       f"after 1 warm-up ({sum(times):.1f} s of CPU work)")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    engine.set_gemm_precision(args.precision)
+    torch.manual_seed(20250321)
+    model = configs.instantiate(configs.multitrack_diffusion(num_speakers=4)).to(dev)
+    opt = FusedAdam(model, lr=1e-4, clip_norm=1.0)
+    P, T = args.pairs, args.frames
+    b = data.synthetic_batch(P, T, 1000 + rank)
+    g = lambda k: torch.from_numpy(b[k]).to(dev).contiguous()  # noqa: E731
+    xm, xs, ym = g("x_main"), g("x_sub"), g("y_main")
+    s0, s1 = g("spk_main"), g("spk_sub")
+    lens = b["lengths"].tolist()
+    for _ in range(args.warmup):
+        loss, norm = train_step(model, opt, xm, xs, ym, s0, s1, lens)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+    barrier()
+    t0 = time.time()
+    for _ in range(args.steps):
+        loss, norm = train_step(model, opt, xm, xs, ym, s0, s1, lens)
+    barrier()
+    elapsed = time.time() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    frames = P * T * world * args.steps
+    value = frames / elapsed
+    loss_v, norm_v = loss.item(), norm.item()
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    sec, flops = gate_gemm_timing(model, P, T, dev)
+    achieved = flops / sec / 1e12
+    out = {
+        "metric": "acoustic-model train frames/sec/GPU (4-track ensemble); synth RTF",
+        "value": value, "unit": "main-track frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": args.precision, "data": "synthetic (SURVEY.md §8(d) feature layout), random-init "
+                                          "weights of the recipe architecture",
+        "config": {"workload": "4-track SATB ensemble, MultiTrackNPSSMDNMultistreamParametric"
+                               "Model (multitrack_acoustic_nnsvs_world_multi_ar_f0_diff_mgcbap)",
+                   "pairs_per_gpu": P, "frames_per_pair": T, "global_batch_pairs": P * world,
+                   "parallelism": f"dp{world}"},
+        "train_loss": loss_v, "grad_norm": norm_v,
+        "model_tflops_per_s": value * TRAIN_FLOP_PER_FRAME / 1e12,
+        "roofline": {"kernel": "conv_gemm_kernel<bf16> (mgc DiffNet block gate GEMM, "
+                               f"M={P * T} N=512 K=1024)" if args.precision == "bf16" else
+                     "conv_gemm_kernel<float>",
+                     "bound": "mfma", "achieved": achieved,
+                     "peak": PEAK_BF16_TFLOPS if args.precision == "bf16" else 157.3,
+                     "unit": "TFLOP/s",
+                     "frac": achieved / (PEAK_BF16_TFLOPS if args.precision == "bf16" else 157.3),
+                     "launch_us": sec * 1e6, "traffic": _traffic()},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+
+
+def _traffic():
+    """HBM bytes per launch of the gate GEMM from the committed rocprofv3 PMC pass, if any."""
+    p = os.path.join(ROOT, "profiles", "gate_gemm_pmc.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    return None
+
+
+if __name__ == "__main__":
+    main()

@@ -152,15 +152,10 @@ class DiffNet(nn.Module):
         X, Z, GF = [x], [], []
         z = gf = None
         for l, blk in enumerate(self.residual_layers):
-            dl = blk.dilation
             if save or z is None:
                 z = empty(M, C, device=dev)
                 gf = empty(M, 2 * C, device=dev)
-            K.gemm([K.Seg(x, C, C, pk[f"dil{l}"], T, taps=3, dil=dl, shift0=-dl,
-                          radd=ds[:, l * C:], radd_ld=L * C),
-                    K.Seg(cond, ldc, E, pk[f"cond{l}"], T)],
-                   B, T, 2 * C, pk.fwd, z, C, epi=_lib.EPI_GATE, aux0=gf, ld0=2 * C, C=C,
-                   **pk.bias_ptr_args(f"g{l}.b"))
+            self._gate_gemm(l, x, cond, ldc, ds, B, T, z, gf)
             xn = empty(M, C, device=dev) if save else x
             K.gemm([K.Seg(z, C, C, pk[f"out{l}"], T)], B, T, 2 * C, pk.fwd, xn, C,
                    epi=_lib.EPI_RESSKIP, aux0=S, ld0=C, aux1=x, ld1=C, accum=l > 0,
@@ -182,6 +177,17 @@ class DiffNet(nn.Module):
             st = dict(xin=xin, ldx=ldx, X=X, Z=Z, GF=GF, S=S, p1=p1, demb=demb, m1=m1, mi=mi, d=d,
                       ds=ds, cond=cond, ldc=ldc, B=B, T=T)
         return out, st
+
+    def _gate_gemm(self, l, x, cond, ldc, ds, B, T, z, gf):
+        """Block l's fused gate GEMM (dilated conv + conditioner + sigmoid*tanh)."""
+        pk = self._packs
+        C, L, E = self.C, len(self.residual_layers), self.E
+        dl = self.residual_layers[l].dilation
+        K.gemm([K.Seg(x, C, C, pk[f"dil{l}"], T, taps=3, dil=dl, shift0=-dl,
+                      radd=ds[:, l * C:], radd_ld=L * C),
+                K.Seg(cond, ldc, E, pk[f"cond{l}"], T)],
+               B, T, 2 * C, pk.fwd, z, C, epi=_lib.EPI_GATE, aux0=gf, ld0=2 * C, C=C,
+               **pk.bias_ptr_args(f"g{l}.b"))
 
     def _bwd(self, st, dout):
         """dout (B*T, in_dim) -> dcond (B*T, E); parameter grads accumulated."""

@@ -105,101 +105,122 @@ __device__ __forceinline__ void mma_tile(const T* As, const T* Bs, int wr, int w
 }
 
 // ------------------------------------------------------------------ forward
+struct SegSel {  // the K-segment of one iteration, held in (wave-uniform) scalars
+  const float* x;
+  const float* radd;
+  long long wofs;
+  int ld, K, dil, shift0, pad, radd_ld, Tin, Kp, vec, j, kc;
+};
+
+__device__ __forceinline__ f32x4 load_a_row(const SegSel& g, int k, bool ok, int b, int t) {
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (!ok || k >= g.K) return v;
+  const int src = pad_src(t + g.shift0 + g.j * g.dil, g.Tin, g.pad);
+  if (src < 0) return v;
+  const float* p = g.x + (long long)(b * g.Tin + src) * g.ld + k;
+  if (g.vec) {
+    v = *(const f32x4*)p;
+    if (k + 4 > g.K) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) if (k + e >= g.K) v[e] = 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (k + e < g.K) ? p[e] : 0.f;
+  }
+  if (g.radd) {
+    const float* q = g.radd + (long long)b * g.radd_ld + k;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) if (k + e < g.K) v[e] += q[e];
+  }
+  return v;
+}
+
 template <typename T>
 __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
   constexpr int LK = Lds<T>::K;
+  constexpr int BCH = sizeof(T) == 2 ? 2 : 4;  // 16-B B chunks per thread
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* As = (T*)smem;
   T* Bs = As + 2 * BM * LK;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int M = a.M, Tout = a.Tout, Npad = a.Npad;
+  const char* const W = (const char*)a.W;
 
-  // A staging: 4 float4 chunks per thread; rows (tid>>3) + 32 i, chunk column tid&7.
-  int rb[4], rt[4];
-  bool rok[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int m = m0 + (tid >> 3) + 32 * i;
-    rok[i] = m < a.M;
-    int b = rok[i] ? m / a.Tout : 0;
-    rb[i] = b;
-    rt[i] = rok[i] ? m - b * a.Tout : 0;
+  // A staging: rows r_i = (tid>>3) + 32 i, 4 floats at column (tid&7)*4 of the k-chunk.
+  const int ac4 = tid & 7, arow = tid >> 3;
+  int b0, t0, b1, t1, b2, t2, b3, t3;
+  bool ok0, ok1, ok2, ok3;
+#define ROWINIT(i)                                     \
+  {                                                    \
+    const int m = m0 + arow + 32 * i;                  \
+    ok##i = m < M;                                     \
+    b##i = ok##i ? m / Tout : 0;                       \
+    t##i = ok##i ? m - b##i * Tout : 0;                \
   }
-  const int ac4 = tid & 7;
+  ROWINIT(0) ROWINIT(1) ROWINIT(2) ROWINIT(3)
+#undef ROWINIT
 
-  int nk[3];
-  int nit = 0;
-  for (int s = 0; s < a.nseg; ++s) {
-    nk[s] = (a.seg[s].K + BK - 1) / BK;
-    nit += nk[s] * a.seg[s].taps;
-  }
+  // Flattened K iteration space (segment, tap, k-chunk); segment fields are picked with
+  // wave-uniform selects on static indices.
+  const int nseg = a.nseg;
+  const int nk0 = __builtin_amdgcn_readfirstlane((a.seg[0].K + BK - 1) / BK);
+  const int nk1 = __builtin_amdgcn_readfirstlane(nseg > 1 ? (a.seg[1].K + BK - 1) / BK : 0);
+  const int nk2 = __builtin_amdgcn_readfirstlane(nseg > 2 ? (a.seg[2].K + BK - 1) / BK : 0);
+  const int cum1 = nk0 * a.seg[0].taps;
+  const int cum2 = cum1 + (nseg > 1 ? nk1 * a.seg[1].taps : 0);
+  const int nit = cum2 + (nseg > 2 ? nk2 * a.seg[2].taps : 0);
 
-  f32x4 ra[4];
-  constexpr int BCH = sizeof(T) == 2 ? 2 : 4;  // 16-B B chunks per thread
-  uint4 rbw[BCH];
-
-  auto decode = [&](int it, int& s, int& j, int& kc) {
-    s = 0;
-    while (it >= nk[s] * a.seg[s].taps) { it -= nk[s] * a.seg[s].taps; ++s; }
-    j = it / nk[s];
-    kc = it - j * nk[s];
+  auto select = [&](int it) __attribute__((always_inline)) {
+    const int s = __builtin_amdgcn_readfirstlane((it >= cum1) + (it >= cum2));
+    const SegDesc& d = a.seg[s];  // uniform index into the kernarg segment: scalar loads
+    SegSel g;
+    const int base = s == 0 ? 0 : (s == 1 ? cum1 : cum2);
+    const int nks = s == 0 ? nk0 : (s == 1 ? nk1 : nk2);
+    g.j = __builtin_amdgcn_readfirstlane((it - base) / nks);
+    g.kc = (it - base) - g.j * nks;
+    g.x = d.x; g.radd = d.radd; g.wofs = d.wofs;
+    g.ld = d.ld; g.K = d.K; g.dil = d.dil; g.shift0 = d.shift0;
+    g.pad = d.pad; g.radd_ld = d.radd_ld; g.Tin = d.Tin; g.Kp = d.Kp;
+    g.vec = d.vec;
+    return g;
   };
 
-  auto load = [&](int it) {
-    int s, j, kc;
-    decode(it, s, j, kc);
-    const SegDesc& g = a.seg[s];
-    const int k = kc * BK + ac4 * 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (rok[i] && k < g.K) {
-        int src = pad_src(rt[i] + g.shift0 + j * g.dil, g.Tin, g.pad);
-        if (src >= 0) {
-          const float* p = g.x + (long long)(rb[i] * g.Tin + src) * g.ld + k;
-          if (g.vec) {
-            v = *(const f32x4*)p;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = (k + e < g.K) ? p[e] : 0.f;
-          }
-          if (k + 4 > g.K) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) if (k + e >= g.K) v[e] = 0.f;
-          }
-          if (g.radd) {
-            const float* q = g.radd + (long long)rb[i] * g.radd_ld + k;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) if (k + e < g.K) v[e] += q[e];
-          }
-        }
-      }
-      ra[i] = v;
-    }
-    const char* wbase = (const char*)a.W +
-        ((g.wofs + ((long long)j * a.Npad + n0) * g.Kp + kc * BK) * (long long)sizeof(T));
+  f32x4 ra0, ra1, ra2, ra3;
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  u32x4_t rw[BCH];
+  auto load = [&](int it) __attribute__((always_inline)) {
+    const SegSel g = select(it);
+    const int k = g.kc * BK + ac4 * 4;
+    ra0 = load_a_row(g, k, ok0, b0, t0);
+    ra1 = load_a_row(g, k, ok1, b1, t1);
+    ra2 = load_a_row(g, k, ok2, b2, t2);
+    ra3 = load_a_row(g, k, ok3, b3, t3);
+    const char* wbase = W + ((g.wofs + ((long long)g.j * Npad + n0) * g.Kp + g.kc * BK) *
+                             (long long)sizeof(T));
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
-      int q = tid + NTHR * i;
-      int row = sizeof(T) == 2 ? (q >> 2) : (q >> 3);
-      int c = sizeof(T) == 2 ? (q & 3) : (q & 7);
-      rbw[i] = *(const uint4*)(wbase + (long long)row * g.Kp * sizeof(T) + c * 16);
+      const int q = tid + NTHR * i;
+      const int row = sizeof(T) == 2 ? (q >> 2) : (q >> 3);
+      const int c = sizeof(T) == 2 ? (q & 3) : (q & 7);
+      rw[i] = *(const u32x4_t*)(wbase + (long long)row * g.Kp * sizeof(T) + c * 16);
     }
   };
-
-  auto store = [&](int buf) {
-    T* A = As + buf * BM * LK;
+  auto store = [&](int buf) __attribute__((always_inline)) {
+    T* A = As + buf * BM * LK + arow * LK + ac4 * 4;
+    store4<T>(A, ra0[0], ra0[1], ra0[2], ra0[3]);
+    store4<T>(A + 32 * LK, ra1[0], ra1[1], ra1[2], ra1[3]);
+    store4<T>(A + 64 * LK, ra2[0], ra2[1], ra2[2], ra2[3]);
+    store4<T>(A + 96 * LK, ra3[0], ra3[1], ra3[2], ra3[3]);
     T* B = Bs + buf * BN * LK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      store4<T>(A + ((tid >> 3) + 32 * i) * LK + ac4 * 4, ra[i][0], ra[i][1], ra[i][2], ra[i][3]);
-#pragma unroll
     for (int i = 0; i < BCH; ++i) {
-      int q = tid + NTHR * i;
-      int row = sizeof(T) == 2 ? (q >> 2) : (q >> 3);
-      int c = sizeof(T) == 2 ? (q & 3) : (q & 7);
-      *(uint4*)((char*)(B + row * LK) + c * 16) = rbw[i];
+      const int q = tid + NTHR * i;
+      const int row = sizeof(T) == 2 ? (q >> 2) : (q >> 3);
+      const int c = sizeof(T) == 2 ? (q & 3) : (q & 7);
+      *(u32x4_t*)((char*)(B + row * LK) + c * 16) = rw[i];
     }
   };
 

@@ -272,10 +272,10 @@ struct LossStream {
 struct LossArgs {
   LossStream s[4];
   int ns, T, B;
-  float invN;
+  float invN, gscale;
 };
 
-// loss partial sums of |a - b| over non-padded frames; ga = sign(a - b) / N (0 on padding).
+// loss partial sums of |a - b| over non-padded frames; ga = gscale * sign(a - b) (0 on padding).
 __global__ void masked_l1_kernel(LossArgs a, const long long* __restrict__ lengths,
                                  float* __restrict__ part) {
   __shared__ float red[256];
@@ -292,7 +292,7 @@ __global__ void masked_l1_kernel(LossArgs a, const long long* __restrict__ lengt
       if (t < lengths[b]) {
         const float d = s.a[m * s.lda + j] - s.b[m * s.ldb + j];
         acc += fabsf(d);
-        g = d > 0.f ? a.invN : (d < 0.f ? -a.invN : 0.f);
+        g = d > 0.f ? a.gscale : (d < 0.f ? -a.gscale : 0.f);
       }
       if (s.ga) s.ga[m * s.ldg + j] = g;
     }
@@ -563,8 +563,8 @@ ENSVS_API int ensvs_p_sample(float* x, const float* eps, const float* noise, lon
 // streams: arrays of 4 (a, b, ga, lda, ldb, ldg, n); part >= 1024 floats; loss_out: 1 float
 ENSVS_API int ensvs_masked_l1(const float* const* a, const float* const* b, float* const* ga,
                               const int* lda, const int* ldb, const int* ldg, const int* n, int ns,
-                              const long long* lengths, int B, int T, float invN, float* part,
-                              float* loss_out, void* stream) {
+                              const long long* lengths, int B, int T, float invN, float gscale,
+                              float* part, float* loss_out, void* stream) {
   if (ns < 1 || ns > 4) return ENSVS_E_ARG;
   LossArgs args{};
   long long maxn = 0;
@@ -576,6 +576,7 @@ ENSVS_API int ensvs_masked_l1(const float* const* a, const float* const* b, floa
   args.T = T;
   args.B = B;
   args.invN = invN;
+  args.gscale = invN * gscale;
   int blocks = std::min(1024, grid_for(maxn));
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(masked_l1_kernel, dim3(blocks), dim3(256), 0, st, args, lengths, part);

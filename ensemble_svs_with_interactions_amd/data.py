@@ -131,3 +131,12 @@ def sort_pair_batch(len0, len1):
     l0 = np.asarray(len0)[i0]
     l1 = np.asarray(len1)[i1]
     return i0, i1, np.maximum(l0, l1)
+
+
+def shard_pairs(batches, rank, world):
+    """Per-rank mini-batches for data parallelism over pairs (train_util.py:1176-1182):
+    each index batch is split as ``x[rank::world]`` and batches whose size is not a
+    multiple of ``world`` are dropped, as the reference does."""
+    if world == 1:
+        return [list(x) for x in batches]
+    return [list(x[rank::world]) for x in batches if len(x) % world == 0]

@@ -64,11 +64,12 @@ class FusedAdam:
         weights_updated()
 
 
-def masked_l1(preds, targets, lengths_dev, n_valid_frames, B, T):
+def masked_l1(preds, targets, lengths_dev, n_valid_frames, B, T, grad_scale=1.0):
     """Masked L1 summed over streams / element count, with its gradient.
 
     preds/targets: lists of (tensor, ld, col) with stream widths.  Returns
-    (loss (1,) device tensor, list of grad tensors (B*T, n)).
+    (loss (1,) device tensor, list of grad tensors (B*T, n)).  The gradients are
+    additionally multiplied by ``grad_scale`` (1/world under data parallelism).
     """
     ns = len(preds)
     dev = preds[0][0].device
@@ -94,19 +95,27 @@ def masked_l1(preds, targets, lengths_dev, n_valid_frames, B, T):
     loss = empty(1, device=dev)
     call("ensvs_masked_l1", ctypes.addressof(pa), ctypes.addressof(pb), ctypes.addressof(pg),
          ctypes.addressof(la), ctypes.addressof(lb), ctypes.addressof(lg), ctypes.addressof(nn_),
-         ns, lengths_dev.data_ptr(), B, T, 1.0 / N, part.data_ptr(), loss.data_ptr(), Ly.stream())
+         ns, lengths_dev.data_ptr(), B, T, 1.0 / N, float(grad_scale), part.data_ptr(), loss.data_ptr(), Ly.stream())
     return loss, grads
 
 
-def allreduce_grads(optimizer, group=None):
-    """Data-parallel gradient average over RCCL (one collective on the flat buffer)."""
+def world_size(group=None):
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size(group)
+
+
+def allreduce_grads(gflat, group=None):
+    """Data-parallel gradient exchange: ONE sum all-reduce (RCCL over xGMI on the GPU
+    box) of the flat gradient buffer.  The 1/world average is already folded into the
+    loss gradient (``masked_l1(grad_scale=1/world)``), so no extra pass over the buffer.
+    The reference's DDP (train_util.py:1176-1182 batch split + DistributedDataParallel)
+    averages the same per-rank gradients."""
+    import torch.distributed as dist
+    if world_size(group) == 1:
         return
-    w = dist.get_world_size()
-    dist.all_reduce(optimizer.gflat, group=group)
-    call("ensvs_axpby", optimizer.gflat.data_ptr(), 1.0 / w, optimizer.gflat.data_ptr(), 0.0,
-         optimizer.gflat.numel(), Ly.stream())
+    dist.all_reduce(gflat, op=dist.ReduceOp.SUM, group=group)
 
 
 def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws=None,
@@ -126,10 +135,11 @@ def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengt
              (outs["bap_recon"], nb, 0, nb)]
     targets = [(outs["mgc_noise"], nm, 0), (y_main, Dy, o[1]), (y_main, Dy, o[2]),
                (outs["bap_noise"], nb, 0)]
+    W = world_size() if ddp else 1
     loss, (g_m, g_l, g_v, g_b) = masked_l1(preds, targets, st["lens_dev"], sum(st["lens_host"]),
-                                           B, T)
+                                           B, T, grad_scale=1.0 / W)
     model._train_bwd(st, dict(mgc_recon=g_m, lf0=g_l.view(-1), vuv=g_v, bap_recon=g_b))
-    if ddp:
-        allreduce_grads(optimizer)
+    if W > 1:
+        allreduce_grads(optimizer.gflat)
     optimizer.step()
     return loss, optimizer.norm

@@ -142,11 +142,14 @@ int ensvs_q_sample(const float* y, int ldy, const float* noise, int ldn, const l
 int ensvs_p_sample(float* x, const float* eps, const float* noise, long long n, float sra,
                    float srm1, float c1, float c2, float sigma, void* stream);
 /* Masked L1 loss summed over streams / N with its gradient fused
- * (bin/train_acoustic_multitrack.py:115-173). */
+ * (bin/train_acoustic_multitrack.py:115-173).  loss = invN * sum|a-b| over valid
+ * frames; ga = gscale * invN * sign(a-b) (0 on padding).  gscale = 1/world folds the
+ * data-parallel gradient average into the loss gradient, so the RCCL all-reduce is a
+ * plain sum. */
 int ensvs_masked_l1(const float* const* a, const float* const* b, float* const* ga,
                     const int* lda, const int* ldb, const int* ldg, const int* n, int ns,
-                    const long long* lengths, int B, int T, float invN, float* part,
-                    float* loss_out, void* stream);
+                    const long long* lengths, int B, int T, float invN, float gscale,
+                    float* part, float* loss_out, void* stream);
 /* clip_grad_norm_ + torch.optim.Adam over the flat parameter buffer
  * (bin/train_acoustic_multitrack.py:369-380). */
 int ensvs_l2norm(const float* x, long long n, float* part, float* norm_out, void* stream);

@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--frames", type=int, default=1024)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--serial", action="store_true",
+                    help="run the lf0/mgc/bap/vuv branches serially (no side streams)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
 
@@ -143,6 +145,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     engine.set_gemm_precision(args.precision)
+    engine.set_concurrency(not args.serial)
     torch.manual_seed(20250321)
     model = configs.instantiate(configs.multitrack_diffusion(num_speakers=4)).to(dev)
     opt = FusedAdam(model, lr=1e-4, clip_norm=1.0)

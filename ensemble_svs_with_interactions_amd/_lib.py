@@ -65,7 +65,8 @@ SIGNATURES = {
                              c_int, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
     "ensvs_phoneme_ids": [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp],
     "ensvs_embed_add": [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
-    "ensvs_embed_bwd": [c_vp, c_int, c_ll, c_int, c_vp, c_vp, c_vp],
+    "ensvs_embed_bwd": [c_vp, c_int, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
+    "ensvs_embed_bwd_workspace": [c_ll, c_int, c_int],
     "ensvs_spk_scatter": [c_vp, c_int, c_int, c_vp, c_vp, c_vp],
     "ensvs_gather_rows": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
     "ensvs_bn_finalize": [c_vp, c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_vp, c_float, c_int,
@@ -97,6 +98,9 @@ SIGNATURES = {
     "ensvs_randint": [c_vp, c_ll, c_ll, ctypes.c_ulonglong, c_vp],
 }
 
+# entry points returning a value instead of a status code
+RESTYPES = {"ensvs_embed_bwd_workspace": c_ll}
+
 _lib = None
 
 
@@ -112,7 +116,7 @@ def load():
         for name, argtypes in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.argtypes = argtypes
-            fn.restype = c_int
+            fn.restype = RESTYPES.get(name, c_int)
         _lib = lib
     return _lib
 
@@ -121,6 +125,11 @@ def call(name, *args):
     status = getattr(load(), name)(*args)
     if status != 0:
         raise RuntimeError(f"{name} failed with {STATUS.get(status, status)}")
+
+
+def query(name, *args):
+    """Call a size-query entry point (RESTYPES) and return its value."""
+    return getattr(load(), name)(*args)
 
 
 def ptr(t):

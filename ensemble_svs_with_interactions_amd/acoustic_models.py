@@ -19,7 +19,7 @@ from . import kernels as K
 from . import layers as Ly
 from ._lib import call, ptr
 from .base import BaseModel, PredictionType
-from .engine import ModulePacks, _sig, empty, grad_of, lengths_pair
+from .engine import Branches, ModulePacks, _sig, empty, grad_of, lengths_pair
 from .model import init_weights
 
 
@@ -463,19 +463,29 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
         lens_host, lens_dev = lengths_pair(lengths, B, T, dev)
         (s0, i0), (s1, i1) = self._spk_vectors(spk0, spk1, B)
         E = s0.shape[1]
-        lf0, res, st_lf0 = self.lf0_model._fwd(x_main, x_sub, D, B, T, lens_dev, s0, s1, E,
-                                               masks=draws.get("lf0_main"))
-        if self.training:
-            # sub-track call (outputs unused without output_subtrack): BN statistics only
-            self.lf0_model._bn_only(x_sub, x_main, D, B, T, s1, s0, E)
         o = self._stream_cols()
         enc_src = [(x_main, D, 0, D), (y_main, Dy, o[1], o[2] - o[1])]
-        nm, rm, st_mgc = self.mgc_model._fwd(enc_src, B, T, lens_dev, (y_main, Dy, o[0]), s0, E,
-                                             t=draws.get("mgc_t"), noise=draws.get("mgc_noise"))
-        nb, rb, st_bap = self.bap_model._fwd(enc_src, B, T, lens_dev, (y_main, Dy, o[3]), s0, E,
-                                             t=draws.get("bap_t"), noise=draws.get("bap_noise"))
-        vuv, st_vuv = self.vuv_model._fwd(self._vuv_sources(x_main, D, y_main, Dy), B, T,
-                                          lens_dev, s0, E, lstm_masks=draws.get("vuv_lstm"))
+        # The four branches are independent until the loss: concurrent HIP streams
+        # (the recurrences alone occupy only 2*B workgroups each).
+        with Branches(dev) as br:
+            with br.on(0):
+                lf0, res, st_lf0 = self.lf0_model._fwd(x_main, x_sub, D, B, T, lens_dev, s0, s1,
+                                                       E, masks=draws.get("lf0_main"))
+                if self.training:
+                    # sub-track call (outputs unused without output_subtrack): BN statistics
+                    self.lf0_model._bn_only(x_sub, x_main, D, B, T, s1, s0, E)
+            with br.on(1):
+                nm, rm, st_mgc = self.mgc_model._fwd(enc_src, B, T, lens_dev, (y_main, Dy, o[0]),
+                                                     s0, E, t=draws.get("mgc_t"),
+                                                     noise=draws.get("mgc_noise"))
+            with br.on(2):
+                nb, rb, st_bap = self.bap_model._fwd(enc_src, B, T, lens_dev, (y_main, Dy, o[3]),
+                                                     s0, E, t=draws.get("bap_t"),
+                                                     noise=draws.get("bap_noise"))
+            with br.on(3):
+                vuv, st_vuv = self.vuv_model._fwd(self._vuv_sources(x_main, D, y_main, Dy), B, T,
+                                                  lens_dev, s0, E,
+                                                  lstm_masks=draws.get("vuv_lstm"))
         outs = dict(mgc_noise=nm, mgc_recon=rm, lf0=lf0, vuv=vuv, bap_noise=nb, bap_recon=rb,
                     lf0_residual=res)
         st = dict(lf0=st_lf0, mgc=st_mgc, bap=st_bap, vuv=st_vuv, i0=i0, i1=i1, B=B, T=T, E=E,
@@ -486,15 +496,19 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
         """g: dict of grads (B*T, .) for mgc_recon, lf0, vuv, bap_recon [, lf0_residual]."""
         B, E = st["B"], st["E"]
         dev = st["lens_dev"].device
+        with Branches(dev) as br:  # same branch -> stream assignment as _train_fwd
+            with br.on(0):
+                dmain, dsub, _ = self.lf0_model._bwd(st["lf0"], g["lf0"], g.get("lf0_residual"))
+            with br.on(1):
+                dsp_m = self.mgc_model._bwd(st["mgc"], g["mgc_recon"])
+            with br.on(2):
+                dsp_b = self.bap_model._bwd(st["bap"], g["bap_recon"])
+            with br.on(3):
+                _, dsp_v = self.vuv_model._bwd(st["vuv"], g["vuv"], want_spk=True)
+        # speaker-embedding gradient: the four branch contributions, summed after the join
         ds0 = torch.zeros(B, E, device=dev)
-        dsp = self.mgc_model._bwd(st["mgc"], g["mgc_recon"])
-        call("ensvs_axpy", ds0.data_ptr(), dsp.data_ptr(), 1.0, B * E, Ly.stream())
-        dsp = self.bap_model._bwd(st["bap"], g["bap_recon"])
-        call("ensvs_axpy", ds0.data_ptr(), dsp.data_ptr(), 1.0, B * E, Ly.stream())
-        _, dsp = self.vuv_model._bwd(st["vuv"], g["vuv"], want_spk=True)
-        call("ensvs_axpy", ds0.data_ptr(), dsp.data_ptr(), 1.0, B * E, Ly.stream())
-        dmain, dsub, _ = self.lf0_model._bwd(st["lf0"], g["lf0"], g.get("lf0_residual"))
-        call("ensvs_axpy", ds0.data_ptr(), dmain.data_ptr(), 1.0, B * E, Ly.stream())
+        for dsp in (dsp_m, dsp_b, dsp_v, dmain):
+            call("ensvs_axpy", ds0.data_ptr(), dsp.data_ptr(), 1.0, B * E, Ly.stream())
         table = grad_of(self.speaker_embedding.emb.weight)
         call("ensvs_spk_scatter", ds0.data_ptr(), B, E, st["i0"].data_ptr(), table.data_ptr(),
              Ly.stream())

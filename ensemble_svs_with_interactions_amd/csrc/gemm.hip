@@ -130,8 +130,12 @@ __device__ __forceinline__ f32x4 load_a_row(const SegSel& g, int k, bool ok, int
   }
   if (g.radd) {
     const float* q = g.radd + (long long)b * g.radd_ld + k;
+    if (g.vec && k + 4 <= g.K) {
+      v += *(const f32x4*)q;
+    } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) if (k + e < g.K) v[e] += q[e];
+      for (int e = 0; e < 4; ++e) if (k + e < g.K) v[e] += q[e];
+    }
   }
   return v;
 }
@@ -314,16 +318,39 @@ struct WgradArgs {
   const float* x;
   const float* radd;
   float* part;  // [splits][taps][N][K]
+  float* dst;   // splits == 1: written directly, dst[n*sn + k*sk + j*sj]
+  long long sn, sk, sj;
+  float scale;
+  int accum;
   int ldy, ldx, K, taps, dil, shift0, pad, Tin, radd_ld;
   int Tout, M, N, splits, rows_per_split, vecy, vecx;
 };
+
+// bf16 staging image of one operand: [BK frames][128 channels], 256-B rows whose 16-B
+// chunks are XOR-swizzled so the transposed MFMA-operand reads (ds_read_b64_tr_b16)
+// and the row writes are bank-conflict free (cdna_hip_programming.md T10, image (b)).
+__device__ __forceinline__ int wg_off(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+// Operand fragment for rows [c0, c0+16) of the image's channel axis: lane l gets
+// channel c0 + (l&15), frames 8(l>>4) .. +7 (the 16x16x32 A/B lane map).
+__device__ __forceinline__ bf16x8 wg_frag(const char* img, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int ch = (c0 >> 3) + (p >> 1);
+  const int o0 = wg_off(8 * g + q, ch) + 8 * (p & 1);
+  const int o1 = wg_off(8 * g + 4 + q, ch) + 8 * (p & 1);
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + o0));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + o1));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
 
 template <typename T>
 __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
   constexpr int LK = Lds<T>::K;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* As = (T*)smem;
-  T* Bs = As + 2 * BM * LK;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int n0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
@@ -332,14 +359,15 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
   const int mend = min(a.M, mbeg + a.rows_per_split);
   const int nch = mbeg < mend ? (mend - mbeg + BK - 1) / BK : 0;
 
-  // Staging map: lanes walk frames (f = q & 31) so the transposed LDS writes
-  // are contiguous; channel quad c4 = q >> 5.
+  // bf16: lanes walk channels (coalesced rows), images kept [frame][channel].
+  // fp32 (parity mode): lanes walk frames, images transposed [channel][frame].
   f32x4 ra[4], rx[4];
-  auto load = [&](int ch) {
+  auto load = [&](int ch) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int q = tid + NTHR * i;
-      const int f = q & 31, c4 = q >> 5;
+      const int f = sizeof(T) == 2 ? (q >> 5) : (q & 31);
+      const int c4 = sizeof(T) == 2 ? (q & 31) : (q >> 5);
       const int m = mbeg + ch * BK + f;
       f32x4 v = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
       if (m < mend) {
@@ -357,14 +385,17 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
           const int src = pad_src(t + a.shift0 + j * a.dil, a.Tin, a.pad);
           if (src >= 0) {
             const float* p = a.x + (long long)(b * a.Tin + src) * a.ldx + k;
-            if (a.vecx && k + 4 <= a.K) w = *(const f32x4*)p;
+            const bool full = a.vecx && k + 4 <= a.K;
+            if (full) w = *(const f32x4*)p;
             else
 #pragma unroll
               for (int e = 0; e < 4; ++e) w[e] = (k + e < a.K) ? p[e] : 0.f;
             if (a.radd) {
               const float* r = a.radd + (long long)b * a.radd_ld + k;
+              if (full) w += *(const f32x4*)r;
+              else
 #pragma unroll
-              for (int e = 0; e < 4; ++e) if (k + e < a.K) w[e] += r[e];
+                for (int e = 0; e < 4; ++e) if (k + e < a.K) w[e] += r[e];
             }
           }
         }
@@ -373,26 +404,54 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
       rx[i] = w;
     }
   };
-  auto store = [&](int buf) {
-    T* A = As + buf * BM * LK;
-    T* B = Bs + buf * BN * LK;
+  constexpr int IMG = sizeof(T) == 2 ? BK * 256 : BM * LK * (int)sizeof(T);  // bytes / image
+  auto store = [&](int buf) __attribute__((always_inline)) {
+    char* A = smem + buf * 2 * IMG;
+    char* B = A + IMG;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int q = tid + NTHR * i;
-      const int f = q & 31, c4 = q >> 5;
+      if constexpr (sizeof(T) == 2) {
+        const int f = q >> 5, c4 = q & 31;
+        const int o = wg_off(f, c4 >> 1) + 8 * (c4 & 1);
+        *(bf16x4*)(A + o) = bf16x4{(__bf16)ra[i][0], (__bf16)ra[i][1], (__bf16)ra[i][2],
+                                   (__bf16)ra[i][3]};
+        *(bf16x4*)(B + o) = bf16x4{(__bf16)rx[i][0], (__bf16)rx[i][1], (__bf16)rx[i][2],
+                                   (__bf16)rx[i][3]};
+      } else {
+        const int f = q & 31, c4 = q >> 5;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        A[(c4 * 4 + e) * LK + f] = (T)ra[i][e];
-        B[(c4 * 4 + e) * LK + f] = (T)rx[i][e];
+        for (int e = 0; e < 4; ++e) {
+          ((T*)A)[(c4 * 4 + e) * LK + f] = (T)ra[i][e];
+          ((T*)B)[(c4 * 4 + e) * LK + f] = (T)rx[i][e];
+        }
       }
     }
   };
-
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const char* A = smem + buf * 2 * IMG;
+    const char* B = A + IMG;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[i] = wg_frag(A, wr * 64 + i * 16, lane);
+        fb[i] = wg_frag(B, wc * 64 + i * 16, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
+    } else {
+      mma_tile<T>((const T*)A, (const T*)B, wr, wc, lane, acc);
+    }
+  };
   if (nch > 0) {
     load(0);
     store(0);
@@ -401,9 +460,28 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
   for (int ch = 0; ch < nch; ++ch) {
     const int buf = ch & 1;
     if (ch + 1 < nch) load(ch + 1);
-    mma_tile<T>(As + buf * BM * LK, Bs + buf * BN * LK, wr, wc, lane, acc);
+    compute(buf);
     if (ch + 1 < nch) store(buf ^ 1);
     __syncthreads();
+  }
+  if (a.splits == 1) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int k = k0 + wc * 64 + nt * 16 + (lane & 15);
+      if (k >= a.K) continue;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + wr * 64 + mt * 16 + (lane >> 4) * 4 + r;
+          if (n < a.N) {
+            float* d = a.dst + n * a.sn + k * a.sk + j * a.sj;
+            const float v = acc[mt][nt][r] * a.scale;
+            *d = a.accum ? *d + v : v;
+          }
+        }
+    }
+    return;
   }
   float* out = a.part + ((long long)(s * a.taps + j) * a.N) * a.K;
 #pragma unroll
@@ -420,23 +498,33 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
   }
 }
 
-// dst[n*sn + k*sk + j*sj] (+)= sum_s part[s][j][n][k]   (fixed summation order)
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dst,
-                                    int splits, int taps, int N, int K, long long sn,
-                                    long long sk, long long sj, int accum, float scale) {
-  const long long total = (long long)taps * N * K;
+// dst[n*sn + k*sk + j*sj] (+)= scale * sum_s part[s][j][n][k]   (fixed summation order)
+// grid (cdiv(K, 256), N * taps): one (tap, n) row of K per block row, coalesced over k.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
+                                                           float* __restrict__ dst, int splits,
+                                                           int taps, int N, int K, long long sn,
+                                                           long long sk, long long sj, int accum,
+                                                           float scale) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  const int row = blockIdx.y;  // j * N + n
+  const int j = row / N, n = row - j * N;
   const long long stride = (long long)N * K * taps;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int k = (int)(i % K);
-    const int n = (int)((i / K) % N);
-    const int j = (int)(i / ((long long)K * N));
-    float v = 0.f;
-    for (int s = 0; s < splits; ++s) v += part[s * stride + i];
-    v *= scale;
-    float* d = dst + n * sn + k * sk + j * sj;
-    *d = accum ? (*d + v) : v;
+  const float* p = part + (long long)row * K + k;
+  float v = 0.f;
+  int sp = 0;
+  for (; sp + 4 <= splits; sp += 4) {
+    const float a0 = p[sp * stride], a1 = p[(sp + 1) * stride];
+    const float a2 = p[(sp + 2) * stride], a3 = p[(sp + 3) * stride];
+    v += a0;
+    v += a1;
+    v += a2;
+    v += a3;
   }
+  for (; sp < splits; ++sp) v += p[sp * stride];
+  v *= scale;
+  float* d = dst + n * sn + k * sk + j * sj;
+  *d = accum ? (*d + v) : v;
 }
 
 // ---------------------------------------------------------- weight packing
@@ -483,42 +571,96 @@ __global__ void pack_kernel(const PackDesc* __restrict__ descs) {
 
 // --------------------------------------------------------- column reductions
 // part[s][n] = sum over rows [s*rps, (s+1)*rps) of f(Y[row, n]); mode 0: y, 1: (y-mean)^2
-__global__ void colsum_partial_kernel(const float* __restrict__ y, int ld, int M, int N, int rps,
-                                      const float* __restrict__ mean, float* __restrict__ part) {
-  // grid.z = row group (rows [z*M, (z+1)*M)); part layout [group][split][N]
-  __shared__ float red[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int g = threadIdx.x >> 6;
+// Column sums over frame rows (bias gradients, BatchNorm statistics, per-sequence
+// sums).  Memory-bound: 64 columns x 16 row lanes per block, float4 loads with 4
+// rows in flight per lane; partials [group][split][N] are reduced by colsum_final
+// in a fixed order (deterministic).
+template <bool VEC>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ y, int ld,
+                                                             int M, int N, int rps,
+                                                             const float* __restrict__ mean,
+                                                             float* __restrict__ part) {
+  __shared__ f32x4 red[16][17];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col = blockIdx.x * 64 + cq * 4;
   const int s = blockIdx.y;
   y += (long long)blockIdx.z * M * ld;
   part += (long long)blockIdx.z * gridDim.y * N;
   const int r0 = s * rps, r1 = min(M, r0 + rps);
-  float acc = 0.f;
-  if (col < N) {
-    const float mu = mean ? mean[(long long)blockIdx.z * N + col] : 0.f;
-    for (int r = r0 + g; r < r1; r += 4) {
-      float v = y[(long long)r * ld + col];
-      if (mean) { v -= mu; v *= v; }
-      acc += v;
-    }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 mu = {0.f, 0.f, 0.f, 0.f};
+  if (mean) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (col + e < N) mu[e] = mean[(long long)blockIdx.z * N + col + e];
   }
-  red[g][threadIdx.x & 63] = acc;
+  auto ld4 = [&](int r) -> f32x4 {
+    const float* q = y + (long long)r * ld + col;
+    f32x4 v;
+    if (VEC && col + 3 < N) {
+      v = *(const f32x4*)q;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = col + e < N ? q[e] : 0.f;
+    }
+    if (mean) {
+      v -= mu;
+      v *= v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) if (col + e >= N) v[e] = 0.f;
+    }
+    return v;
+  };
+  if (col < N) {
+    int r = r0 + rl;
+    for (; r + 48 < r1; r += 64) {
+      const f32x4 v0 = ld4(r), v1 = ld4(r + 16), v2 = ld4(r + 32), v3 = ld4(r + 48);
+      acc += (v0 + v1) + (v2 + v3);
+    }
+    for (; r < r1; r += 16) acc += ld4(r);
+  }
+  red[rl][cq] = acc;
   __syncthreads();
-  if (g == 0 && col < N)
-    part[(long long)s * N + col] = (red[0][threadIdx.x] + red[1][threadIdx.x]) +
-                                   (red[2][threadIdx.x] + red[3][threadIdx.x]);
+  if (threadIdx.x < 64) {
+    const int c = threadIdx.x;  // column within the block
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][c >> 2][c & 3];
+    const int gc = blockIdx.x * 64 + c;
+    if (gc < N) part[(long long)s * N + gc] = t;
+  }
 }
 
-__global__ void colsum_final_kernel(const float* __restrict__ part, int S, int N, float scale,
-                                    float* __restrict__ out, int ldo, int accum) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= N) return;
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int S,
+                                                           int N, float scale,
+                                                           float* __restrict__ out, int ldo,
+                                                           int accum) {
+  // 16 columns x 16 split lanes per block, 4 partial loads in flight per lane.
+  __shared__ double red[16][17];
+  const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + c;
   part += (long long)blockIdx.y * S * N;
   out += (long long)blockIdx.y * ldo;
-  double acc = 0.0;
-  for (int s = 0; s < S; ++s) acc += part[(long long)s * N + col];
-  float v = (float)(acc * scale);
-  out[col] = accum ? out[col] + v : v;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (col < N) {
+    int s = sl;
+    for (; s + 48 < S; s += 64) {
+      a0 += part[(long long)s * N + col];
+      a1 += part[(long long)(s + 16) * N + col];
+      a2 += part[(long long)(s + 32) * N + col];
+      a3 += part[(long long)(s + 48) * N + col];
+    }
+    for (; s < S; s += 16) a0 += part[(long long)s * N + col];
+  }
+  red[sl][c] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (sl == 0 && col < N) {
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][c];
+    const float v = (float)(t * scale);
+    out[col] = accum ? out[col] + v : v;
+  }
 }
 
 }  // namespace
@@ -548,7 +690,8 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
     a.seg[s].radd_ld = g.radd_ld;
     a.seg[s].Tin = g.Tin;
     a.seg[s].Kp = g.Kp;
-    a.seg[s].vec = (g.ld % 4 == 0) && (((uintptr_t)g.x & 15) == 0);
+    a.seg[s].vec = (g.ld % 4 == 0) && (((uintptr_t)g.x & 15) == 0) &&
+                   (!g.radd || ((g.radd_ld % 4 == 0) && (((uintptr_t)g.radd & 15) == 0)));
   }
   a.nseg = nseg;
   a.Tout = Tout;
@@ -611,22 +754,30 @@ ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx
   a.splits = splits;
   a.rows_per_split = (cdiv(a.M, splits) + BK - 1) / BK * BK;
   a.vecy = (ldy % 4 == 0) && (((uintptr_t)dy & 15) == 0);
-  a.vecx = (ldx % 4 == 0) && (((uintptr_t)x & 15) == 0);
+  a.vecx = (ldx % 4 == 0) && (((uintptr_t)x & 15) == 0) &&
+           (!radd || ((radd_ld % 4 == 0) && (((uintptr_t)radd & 15) == 0)));
+  a.dst = dst;
+  a.sn = sn;
+  a.sk = sk;
+  a.sj = sj;
+  a.scale = scale;
+  a.accum = accum;
   dim3 grid(cdiv(N, BM), cdiv(K, BN), taps * splits);
+  if (N * taps > 65535) return ENSVS_E_SHAPE;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DT_BF16) {
-    size_t lds = 2 * (BM + BN) * Lds<__bf16>::K * sizeof(__bf16);
+    size_t lds = 2 * 2 * BK * 256;
     hipLaunchKernelGGL(wgrad_kernel<__bf16>, grid, dim3(NTHR), lds, st, a);
   } else {
     size_t lds = 2 * (BM + BN) * Lds<float>::K * sizeof(float);
     hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(NTHR), lds, st, a);
   }
   ENSVS_CHECK_LAUNCH();
-  long long total = (long long)taps * N * K;
-  int blocks = (int)std::min<long long>(4096, (total + 255) / 256);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, part, dst, splits, taps,
-                     N, K, sn, sk, sj, accum, scale);
-  ENSVS_CHECK_LAUNCH();
+  if (splits > 1) {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(K, 256), N * taps), dim3(256), 0, st, part,
+                       dst, splits, taps, N, K, sn, sk, sj, accum, scale);
+    ENSVS_CHECK_LAUNCH();
+  }
   return ENSVS_OK;
 }
 
@@ -648,13 +799,20 @@ ENSVS_API int ensvs_colsum(const float* y, int ld, int M, int groups, int N, con
                            float scale, float* part, int max_splits, float* out, int ldo, int accum,
                            void* stream) {
   if (M <= 0 || N <= 0 || groups <= 0) return ENSVS_E_SHAPE;
-  int S = std::max(1, std::min(max_splits, M / 64));
+  // aim for >= ~2048 blocks (8 XCDs x 32 CUs x several waves), >= 128 rows per split
+  const int cb = cdiv(N, 64);
+  int S = std::max(1, std::min({max_splits, M / 128, cdiv(2048, cb * groups)}));
   int rps = cdiv(M, S);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3(cdiv(N, 64), S, groups), dim3(256), 0, st, y, ld, M,
-                     N, rps, mean, part);
+  const bool vec = (ld % 4 == 0) && (((uintptr_t)y & 15) == 0);
+  if (vec)
+    hipLaunchKernelGGL(colsum_partial_kernel<true>, dim3(cb, S, groups), dim3(256), 0, st, y, ld,
+                       M, N, rps, mean, part);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<false>, dim3(cb, S, groups), dim3(256), 0, st, y, ld,
+                       M, N, rps, mean, part);
   ENSVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(N, 256), groups), dim3(256), 0, st, part, S, N,
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(N, 16), groups), dim3(256), 0, st, part, S, N,
                      scale, out, ldo > 0 ? ldo : N, accum);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;

@@ -49,22 +49,59 @@ __global__ void embed_add_kernel(float* __restrict__ y, int ldy, long long M, in
   }
 }
 
-// demb[ids[m]][c] += dy[m][c]  (scatter-add, float atomics)
-__global__ void embed_bwd_kernel(const float* __restrict__ dy, int ldy, long long M, int C,
-                                 const int* __restrict__ ids, float* __restrict__ demb) {
-  GRID_LOOP(i, M * C) {
-    const long long m = i / C;
-    const int c = (int)(i % C);
-    atomicAdd(demb + (long long)ids[m] * C + c, dy[m * ldy + c]);
+// Embedding backward, deterministic.  Block (column block of 64, chunk of
+// EMB_CHUNK frames): 4 sub-chunks x 64 columns; each thread walks its frames in
+// order adding dy into an LDS table acc[sub][v][c]; the 4 sub-tables are summed in
+// order into part[chunk][v][c]; embed_reduce sums the chunks in order into demb.
+constexpr int EMB_CHUNK = 256;
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict__ dy, int ldy,
+                                                        long long M, int C,
+                                                        const int* __restrict__ ids, int V,
+                                                        float* __restrict__ part) {
+  extern __shared__ float acc[];  // [4][V][64]
+  const int c = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + c;
+  for (int i = threadIdx.x; i < 4 * V * 64; i += 256) acc[i] = 0.f;
+  __syncthreads();
+  const long long m0 = (long long)blockIdx.y * EMB_CHUNK + sub * (EMB_CHUNK / 4);
+  const long long m1 = min(M, m0 + EMB_CHUNK / 4);
+  float* a = acc + sub * V * 64 + c;
+  if (col < C)
+    for (long long m = m0; m < m1; ++m) a[ids[m] * 64] += dy[m * ldy + col];
+  __syncthreads();
+  float* out = part + (long long)blockIdx.y * V * C;
+  for (int i = threadIdx.x; i < V * 64; i += 256) {
+    const int v = i >> 6, cc = i & 63;
+    const int gc = blockIdx.x * 64 + cc;
+    if (gc < C)
+      out[(long long)v * C + gc] =
+          (acc[i] + acc[V * 64 + i]) + (acc[2 * V * 64 + i] + acc[3 * V * 64 + i]);
   }
 }
 
-// dtable[spk[b]][c] += dseq[b][c]
+__global__ void embed_reduce_kernel(const float* __restrict__ part, int nchunk, long long VC,
+                                    float* __restrict__ demb) {
+  GRID_LOOP(i, VC) {
+    float s = 0.f;
+    for (int k = 0; k < nchunk; ++k) s += part[k * VC + i];
+    demb[i] += s;
+  }
+}
+
+// dtable[spk[b]][c] += sum over b' with spk[b'] == spk[b] of dseq[b'][c], written by the
+// first such b (fixed summation order, no atomics).
 __global__ void spk_scatter_kernel(const float* __restrict__ dseq, int B, int C,
                                    const long long* __restrict__ spk, float* __restrict__ dtab) {
   GRID_LOOP(i, (long long)B * C) {
     const int b = (int)(i / C), c = (int)(i % C);
-    atomicAdd(dtab + spk[b] * C + c, dseq[i]);
+    const long long r = spk[b];
+    bool first = true;
+    for (int q = 0; q < b; ++q) first &= spk[q] != r;
+    if (!first) continue;
+    float s = 0.f;
+    for (int q = b; q < B; ++q)
+      if (spk[q] == r) s += dseq[(long long)q * C + c];
+    dtab[r * C + c] += s;
   }
 }
 
@@ -478,9 +515,21 @@ ENSVS_API int ensvs_embed_add(float* y, int ldy, long long M, int C, int T, cons
   return ENSVS_OK;
 }
 
-ENSVS_API int ensvs_embed_bwd(const float* dy, int ldy, long long M, int C, const int* ids,
-                              float* demb, void* stream) {
-  LAUNCH(embed_bwd_kernel, M * C, dy, ldy, M, C, ids, demb);
+ENSVS_API long long ensvs_embed_bwd_workspace(long long M, int C, int V) {
+  return (M + EMB_CHUNK - 1) / EMB_CHUNK * (long long)V * C;
+}
+
+ENSVS_API int ensvs_embed_bwd(const float* dy, int ldy, long long M, int C, const int* ids, int V,
+                              float* part, float* demb, void* stream) {
+  if (V <= 0 || V > 128 || M <= 0 || C <= 0) return ENSVS_E_SHAPE;
+  const int nchunk = (int)((M + EMB_CHUNK - 1) / EMB_CHUNK);
+  if (nchunk > 65535) return ENSVS_E_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(cdiv(C, 64), nchunk), dim3(256),
+                     4 * V * 64 * sizeof(float), st, dy, ldy, M, C, ids, V, part);
+  ENSVS_CHECK_LAUNCH();
+  const long long VC = (long long)V * C;
+  LAUNCH(embed_reduce_kernel, VC, part, nchunk, VC, demb);
   return ENSVS_OK;
 }
 

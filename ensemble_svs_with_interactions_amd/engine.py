@@ -15,7 +15,58 @@ import torch
 from . import _lib
 from .kernels import PackedBuffer
 
-_STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None}
+_STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None, "concurrent": True}
+_SIDE_STREAMS = {}
+
+
+def set_concurrency(on: bool):
+    """Run the independent branches of the step (lf0 / mgc / bap / vuv) on their own HIP
+    streams (default) or serially on the current stream."""
+    _STATE["concurrent"] = bool(on)
+
+
+class Branches:
+    """Fork/join of independent branches of one step onto concurrent HIP streams.
+
+    Branch ``i < n_side`` runs on side stream i, anything else on the current (main)
+    stream, so n_side + 1 branches use n_side + 1 hardware queues (GPU_MAX_HW_QUEUES
+    defaults to 4).  Side streams wait for the main stream at entry; the main stream
+    waits for every side stream at exit.  A branch's saved state must be consumed on
+    the same branch index in backward (stream-ordered reuse of freed memory).
+    """
+
+    def __init__(self, device, n_side=3):
+        self.device = device
+        self.on_side = _STATE["concurrent"] and torch.cuda.is_available()
+        if self.on_side:
+            key = (str(device), n_side)
+            if key not in _SIDE_STREAMS:
+                # branch 0 (the lf0 model with the AR decoder) is the critical path
+                _SIDE_STREAMS[key] = [torch.cuda.Stream(device, priority=-1 if i == 0 else 0)
+                                      for i in range(n_side)]
+            self.side = _SIDE_STREAMS[key]
+        else:
+            self.side = []
+
+    def __enter__(self):
+        if self.on_side:
+            self.main = torch.cuda.current_stream(self.device)
+            ev = self.main.record_event()
+            for s in self.side:
+                s.wait_event(ev)
+        return self
+
+    def on(self, i):
+        import contextlib
+        if self.on_side and i < len(self.side):
+            return torch.cuda.stream(self.side[i])
+        return contextlib.nullcontext()
+
+    def __exit__(self, *exc):
+        if self.on_side:
+            for s in self.side:
+                self.main.wait_stream(s)
+        return False
 
 
 def next_seed() -> int:

@@ -159,10 +159,13 @@ _part_cache = {}
 
 
 def scratch(nfloats, device, key="part"):
-    t = _part_cache.get((key, device))
+    """Reusable split-reduction workspace, one per (key, device, stream): launches on
+    one stream are ordered, launches on concurrent branch streams get their own."""
+    ck = (key, device, torch.cuda.current_stream(device).cuda_stream)
+    t = _part_cache.get(ck)
     if t is None or t.numel() < nfloats:
         t = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
-        _part_cache[(key, device)] = t
+        _part_cache[ck] = t
     return t
 
 
@@ -183,7 +186,8 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
 def colsum(y, ld, M, N, out, groups=1, mean=None, scale=1.0, accum=False, yoff=0, ldo=0,
            outoff=0):
     """out[g*ldo + n] (+)= scale * sum over the M rows of group g (ldo 0 -> N)."""
-    max_splits = 64
+    # row splits: what ensvs_colsum picks (>= 2048 blocks, >= 128 rows per split)
+    max_splits = max(1, min(256, M // 128, -(-2048 // (-(-N // 64) * groups))))
     part = scratch(groups * max_splits * N, y.device, key="colsum")
     call("ensvs_colsum", y.data_ptr() + 4 * yoff, ld, M, groups, N, ptr(mean), float(scale),
          part.data_ptr(), max_splits, out.data_ptr() + 4 * outoff, ldo, int(accum), stream())

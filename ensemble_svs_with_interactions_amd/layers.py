@@ -126,7 +126,9 @@ def embed_bwd(emb_mod, fc_in, sv, dY, B, T, dspk_seq=None):
     """Grads of emb / fc_in (and per-sequence speaker vectors, summed over frames)."""
     M = B * T
     E = dY.shape[1]
-    call("ensvs_embed_bwd", dY.data_ptr(), E, M, E, sv["ids"].data_ptr(),
+    V = emb_mod.weight.shape[0]
+    part = K.scratch(_lib.query("ensvs_embed_bwd_workspace", M, E, V), dY.device, key="emb")
+    call("ensvs_embed_bwd", dY.data_ptr(), E, M, E, sv["ids"].data_ptr(), V, part.data_ptr(),
          grad_of(emb_mod.weight).data_ptr(), stream())
     wgrad_into(fc_in.weight, dY, E, sv["X"], sv["ldx"], B, T, T, E, sv["Kin"])
     colsum_into(dY, E, M, E, fc_in.bias)

@@ -112,8 +112,12 @@ int ensvs_phoneme_ids(const float* x, int ld, long long M, int ph0, int nv, int*
 int ensvs_embed_add(float* y, int ldy, long long M, int C, int T, const float* emb,
                     const int* ids0, const int* ids1, const float* spk0, const float* spk1,
                     int ldspk, void* stream);
-int ensvs_embed_bwd(const float* dy, int ldy, long long M, int C, const int* ids, float* demb,
-                    void* stream);
+/* demb[ids[m]] += dy[m] over frames (nn.Embedding backward), deterministic: frame
+ * chunks accumulate in LDS, partials (>= ensvs_embed_bwd_workspace floats) are summed
+ * in a fixed order.  V = vocabulary rows (<= 128). */
+int ensvs_embed_bwd(const float* dy, int ldy, long long M, int C, const int* ids, int V,
+                    float* part, float* demb, void* stream);
+long long ensvs_embed_bwd_workspace(long long M, int C, int V);
 /* SpeakerEmbedding (model.py:35-53): gather / scatter-add of table rows. */
 int ensvs_spk_scatter(const float* dseq, int B, int C, const long long* spk, float* dtab,
                       void* stream);

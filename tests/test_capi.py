@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared():
     src = open(os.path.join(ROOT, "include", "ensvs.h")).read()
-    return sorted(set(re.findall(r"^int (ensvs_\w+)\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|long long) (ensvs_\w+)\(", src, flags=re.M)))
 
 
 def test_header_symbols_exported():
@@ -54,3 +54,8 @@ def test_library_newer_than_sources():
     lib_t = os.path.getmtime(_lib.LIB_PATH)
     for s in glob.glob(os.path.join(ROOT, "ensemble_svs_with_interactions_amd", "csrc", "*")):
         assert os.path.getmtime(s) <= lib_t, f"stale libensvs.so: {s} is newer (run make)"
+
+
+def test_workspace_query():
+    # 1000 frames -> 4 chunks of 256 frames, each a V x C partial table
+    assert _lib.query("ensvs_embed_bwd_workspace", 1000, 256, 47) == 4 * 47 * 256

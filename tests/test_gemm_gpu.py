@@ -154,3 +154,69 @@ def test_colsum_grouped():
     torch.cuda.synchronize()
     assert rel(out, y.sum(1)) < 1e-5
     assert rel(var, y.reshape(-1, 70).var(0, unbiased=False)) < 1e-5
+
+
+@pytest.mark.parametrize("dt,tol", [(L.DT_F32, 2e-5), (L.DT_BF16, 2e-2)])
+@pytest.mark.parametrize("splits", [1, 7])
+def test_wgrad_radd_tiles_splits(dt, tol, splits):
+    """Multi-tile wgrad (N, K not multiples of 128) of x + radd[b] with accumulate and
+    scale, direct (splits=1) and split-reduced."""
+    torch.manual_seed(5)
+    B, T, Cin, Cout, taps, dil = 3, 96, 260, 300, 3, 4
+    x = torch.randn(B, T, Cin, device=DEV)
+    radd = torch.randn(B, Cin, device=DEV)
+    xe = (x + radd[:, None, :]).requires_grad_()
+    w = (torch.randn(Cout, Cin, taps, device=DEV) / (Cin * taps) ** 0.5).requires_grad_()
+    y = F.conv1d(xe.transpose(1, 2), w, padding=dil, dilation=dil).transpose(1, 2)
+    g = torch.randn(y.shape, device=DEV)
+    y.backward(g)
+    dw0 = torch.randn(Cout, Cin, taps, device=DEV)
+    dw = dw0.clone()
+    K.wgrad(g, Cout, x, Cin, B, T, T, Cout, Cin, taps, dil, -dil, L.PAD_ZERO, dw,
+            Cin * taps, taps, 1, dtype=dt, radd=radd, radd_ld=Cin, accum=True, scale=0.5,
+            splits=splits)
+    torch.cuda.synchronize()
+    assert rel(dw - dw0, 0.5 * w.grad) < tol
+
+
+def test_colsum_vectorized_tail():
+    torch.manual_seed(6)
+    y = torch.randn(5000, 128, device=DEV)
+    out = torch.full((102,), 1.0, device=DEV)
+    K.colsum(y, 128, 5000, 102, out, accum=True, scale=2.0)
+    mean = y[:, :102].mean(0)
+    var = torch.empty(102, device=DEV)
+    K.colsum(y, 128, 5000, 102, var, mean=mean, scale=1.0 / 5000)
+    grp = torch.empty(4, 102, device=DEV)
+    K.colsum(y, 128, 1250, 102, grp, groups=4)
+    torch.cuda.synchronize()
+    assert rel(out, 1.0 + 2.0 * y[:, :102].sum(0)) < 1e-5
+    assert rel(var, y[:, :102].var(0, unbiased=False)) < 1e-5
+    assert rel(grp, y[:, :102].reshape(4, 1250, 102).sum(1)) < 1e-5
+
+
+def test_embedding_and_speaker_backward_deterministic():
+    from ensemble_svs_with_interactions_amd._lib import call, query
+    torch.manual_seed(7)
+    M, C, V, ld = 3000, 200, 47, 208
+    dy = torch.randn(M, ld, device=DEV)
+    ids = torch.randint(0, V, (M,), device=DEV, dtype=torch.int32)
+    outs = []
+    for _ in range(2):
+        demb = torch.ones(V, C, device=DEV)
+        part = torch.empty(query("ensvs_embed_bwd_workspace", M, C, V), device=DEV)
+        call("ensvs_embed_bwd", dy.data_ptr(), ld, M, C, ids.data_ptr(), V, part.data_ptr(),
+             demb.data_ptr(), K.stream())
+        outs.append(demb)
+    ref = torch.ones(V, C, device=DEV).index_add_(0, ids.long(), dy[:, :C])
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert rel(outs[0], ref) < 1e-5
+    B, R = 37, 5
+    dseq = torch.randn(B, C, device=DEV)
+    spk = torch.randint(0, R, (B,), device=DEV)
+    tab = torch.full((R, C), 0.5, device=DEV)
+    call("ensvs_spk_scatter", dseq.data_ptr(), B, C, spk.data_ptr(), tab.data_ptr(), K.stream())
+    ref = torch.full((R, C), 0.5, device=DEV).index_add_(0, spk, dseq)
+    torch.cuda.synchronize()
+    assert rel(tab, ref) < 1e-6

@@ -129,3 +129,31 @@ def test_train_step_tiny_matches_reference():
     for k in sd:
         if "running" in k and "final::" + k in a:
             assert rel(sd[k].cpu(), a["final::" + k]) < 1e-4, k
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_concurrent_branches_bitwise_equal_serial(prec):
+    """The lf0 / mgc / bap / vuv branches on concurrent HIP streams give bit-identical
+    loss, gradients and BN statistics to the serial schedule."""
+    engine.set_gemm_precision(prec)
+    a, meta = load_case("train_step_tiny")
+    xm, xs, ym, s0, s1, lens = _batch(a)
+    B, T = xm.shape[:2]
+    res = []
+    try:
+        for conc in (False, True):
+            engine.set_concurrency(conc)
+            model = build(configs.multitrack_diffusion(num_speakers=4, tiny=True), meta["shapes"])
+            model.vuv_model.lstm.dropout = 0.0
+            opt = FusedAdam(model, lr=meta["lr"])
+            loss, norm = train_step(model, opt, xm, xs, ym, s0, s1, lens,
+                                    draws=_draws(a, "draw0::", B, T))
+            torch.cuda.synchronize()
+            res.append((loss.item(), opt.gflat.clone(),
+                        {k: v.clone() for k, v in model.state_dict().items()}))
+    finally:
+        engine.set_concurrency(True)
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
+    for k in res[0][2]:
+        assert torch.equal(res[0][2][k], res[1][2][k]), k

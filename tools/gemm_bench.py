@@ -66,6 +66,30 @@ def case(name, M, N, segs_spec, dtype, iters, epi=_lib.EPI_PLAIN, T=1024):
                 torch_bf16_tflops=round(flops / ref_sec / 1e12, 1))
 
 
+def wcase(name, M, N, Kc, taps, dil, dtype, iters, T=1024):
+    """Weight gradient dW[n, k, tap] = sum_m dY[m, n] X[src(m, tap), k]."""
+    dev = torch.device("cuda")
+    B = M // T
+    dy = torch.randn(M, N, device=dev)
+    x = torch.randn(M, Kc, device=dev)
+    dw = torch.empty(N, Kc, taps, device=dev)
+    fn = lambda: K.wgrad(dy, N, x, Kc, B, T, T, N, Kc, taps, dil, -(taps // 2) * dil,  # noqa
+                         _lib.PAD_ZERO, dw, Kc * taps, taps, 1, dtype=dtype)
+    sec = timeit(fn, iters)
+    flops = 2.0 * M * N * Kc * taps
+    return dict(case="wgrad " + name, dtype="bf16" if dtype == _lib.DT_BF16 else "f32", M=M, N=N,
+                K=Kc * taps, us=round(sec * 1e6, 1), tflops=round(flops / sec / 1e12, 1))
+
+
+def ccase(M, N, iters):
+    dev = torch.device("cuda")
+    y = torch.randn(M, N, device=dev)
+    out = torch.empty(N, device=dev)
+    sec = timeit(lambda: K.colsum(y, N, M, N, out), iters)
+    return dict(case="colsum", M=M, N=N, us=round(sec * 1e6, 1),
+                gbps=round(M * N * 4 / sec / 1e9, 1))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
@@ -80,6 +104,14 @@ def main():
         case("linear 2048->2048", M, 2048, [(2048, 1, 1)], _lib.DT_BF16, args.iters),
         case("conv7 2048->1024", M, 1024, [(2048, 7, 1)], _lib.DT_BF16, args.iters),
         case("linear 1024->1024 f32", M, 1024, [(1024, 1, 1)], _lib.DT_F32, args.iters),
+    ]
+    rows += [
+        wcase("gate conv3 256->512", M, 512, 256, 3, 2, _lib.DT_BF16, args.iters),
+        wcase("linear 256->256", M, 256, 256, 1, 1, _lib.DT_BF16, args.iters),
+        wcase("linear 1024->1024", M, 1024, 1024, 1, 1, _lib.DT_BF16, args.iters),
+        wcase("conv7 2048->1024", M, 1024, 2048, 7, 1, _lib.DT_BF16, args.iters),
+        ccase(M, 512, args.iters),
+        ccase(M, 256, args.iters),
     ]
     for r in rows:
         print(json.dumps(r), flush=True)

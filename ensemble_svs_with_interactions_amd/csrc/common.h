@@ -34,18 +34,18 @@ enum { DT_F32 = 0, DT_BF16 = 1 };
 
 // PyTorch ReflectionPad1d index map (valid for |pad| < n).
 __device__ __forceinline__ int reflect_idx(int i, int n) {
-  if (i < 0) i = -i;
-  if (i >= n) i = 2 * (n - 1) - i;
-  return i;
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * (n - 1) - i : i;
 }
 
 // Map a source frame index under the given padding mode; returns -1 when the
-// frame reads as zero.
+// frame reads as zero.  Branch-free (selects): lanes of a wave hold different
+// frames, and a divergent branch here sits between the staging loads.
 __device__ __forceinline__ int pad_src(int s, int n, int mode) {
-  if (s >= 0 && s < n) return s;
-  if (mode == PAD_ZERO) return -1;
-  if (mode == PAD_REFLECT) return reflect_idx(s, n);
-  return s < 0 ? 0 : n - 1;  // replicate
+  const int refl = reflect_idx(s, n);
+  const int repl = s < 0 ? 0 : n - 1;
+  const int outside = mode == PAD_ZERO ? -1 : (mode == PAD_REFLECT ? refl : repl);
+  return (s >= 0 && s < n) ? s : outside;
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }

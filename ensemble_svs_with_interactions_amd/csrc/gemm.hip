@@ -112,35 +112,38 @@ struct SegSel {  // the K-segment of one iteration, held in (wave-uniform) scala
   int ld, K, dil, shift0, pad, radd_ld, Tin, Kp, vec, j, kc;
 };
 
-__device__ __forceinline__ f32x4 load_a_row(const SegSel& g, int k, bool ok, int b, int t) {
-  f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  if (!ok || k >= g.K) return v;
+// All staging loads are unconditional: an out-of-range row (padding, m >= M) or
+// column quad points at g_zero, so no load is branched around or masked after it
+// lands (a mask/add right after a load makes hipcc wait vmcnt(0) per row).  The
+// per-sequence vector radd is loaded the same way (g_zero when absent) and added in
+// the store phase, after the MFMAs.  VEC: every segment of the launch has K % 4 == 0,
+// ld % 4 == 0 and 16-B aligned rows (one dwordx4 per quad); otherwise 4 scalar loads.
+constexpr int ZERO_FLOATS = 64;
+__device__ __attribute__((aligned(16))) float g_zero[ZERO_FLOATS];
+
+template <bool VEC>
+__device__ __forceinline__ void load_a_raw(const SegSel& g, int k, bool ok, int b, int t,
+                                           f32x4& v, f32x4& r) {
   const int src = pad_src(t + g.shift0 + g.j * g.dil, g.Tin, g.pad);
-  if (src < 0) return v;
-  const float* p = g.x + (long long)(b * g.Tin + src) * g.ld + k;
-  if (g.vec) {
-    v = *(const f32x4*)p;
-    if (k + 4 > g.K) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) if (k + e >= g.K) v[e] = 0.f;
-    }
+  const bool row_ok = ok && src >= 0;
+  const float* xrow = g.x + (long long)(b * g.Tin + src) * g.ld;
+  const float* rrow = g.radd + (long long)b * g.radd_ld;
+  const bool has_r = g.radd != nullptr;
+  if constexpr (VEC) {
+    const bool q = row_ok && k < g.K;
+    v = *(const f32x4*)(q ? xrow + k : g_zero);
+    r = *(const f32x4*)((q && has_r) ? rrow + k : g_zero);
   } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (k + e < g.K) ? p[e] : 0.f;
-  }
-  if (g.radd) {
-    const float* q = g.radd + (long long)b * g.radd_ld + k;
-    if (g.vec && k + 4 <= g.K) {
-      v += *(const f32x4*)q;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) if (k + e < g.K) v[e] += q[e];
+    for (int e = 0; e < 4; ++e) {
+      const bool q = row_ok && k + e < g.K;
+      v[e] = *(q ? xrow + k + e : g_zero);
+      r[e] = *((q && has_r) ? rrow + k + e : g_zero);
     }
   }
-  return v;
 }
 
-template <typename T>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
   constexpr int LK = Lds<T>::K;
   constexpr int BCH = sizeof(T) == 2 ? 2 : 4;  // 16-B B chunks per thread
@@ -192,16 +195,16 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
     return g;
   };
 
-  f32x4 ra0, ra1, ra2, ra3;
+  f32x4 ra0, ra1, ra2, ra3, rr0, rr1, rr2, rr3;
   typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
   u32x4_t rw[BCH];
   auto load = [&](int it) __attribute__((always_inline)) {
     const SegSel g = select(it);
     const int k = g.kc * BK + ac4 * 4;
-    ra0 = load_a_row(g, k, ok0, b0, t0);
-    ra1 = load_a_row(g, k, ok1, b1, t1);
-    ra2 = load_a_row(g, k, ok2, b2, t2);
-    ra3 = load_a_row(g, k, ok3, b3, t3);
+    load_a_raw<VEC>(g, k, ok0, b0, t0, ra0, rr0);
+    load_a_raw<VEC>(g, k, ok1, b1, t1, ra1, rr1);
+    load_a_raw<VEC>(g, k, ok2, b2, t2, ra2, rr2);
+    load_a_raw<VEC>(g, k, ok3, b3, t3, ra3, rr3);
     const char* wbase = W + ((g.wofs + ((long long)g.j * Npad + n0) * g.Kp + g.kc * BK) *
                              (long long)sizeof(T));
 #pragma unroll
@@ -214,6 +217,10 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
   };
   auto store = [&](int buf) __attribute__((always_inline)) {
     T* A = As + buf * BM * LK + arow * LK + ac4 * 4;
+    ra0 += rr0;
+    ra1 += rr1;
+    ra2 += rr2;
+    ra3 += rr3;
     store4<T>(A, ra0[0], ra0[1], ra0[2], ra0[3]);
     store4<T>(A + 32 * LK, ra1[0], ra1[1], ra1[2], ra1[3]);
     store4<T>(A + 64 * LK, ra2[0], ra2[1], ra2[2], ra2[3]);
@@ -347,7 +354,7 @@ __device__ __forceinline__ bf16x8 wg_frag(const char* img, int c0, int lane) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <typename T>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
   constexpr int LK = Lds<T>::K;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -361,7 +368,19 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
 
   // bf16: lanes walk channels (coalesced rows), images kept [frame][channel].
   // fp32 (parity mode): lanes walk frames, images transposed [channel][frame].
-  f32x4 ra[4], rx[4];
+  // Loads are unconditional (g_zero for rows/quads out of range, and for radd when
+  // absent); radd is added in the store phase.  Each thread tracks the (b, t) of
+  // its 4 frame rows incrementally (no per-chunk division).
+  int fb[4], ft[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = tid + NTHR * i;
+    const int f = sizeof(T) == 2 ? (q >> 5) : (q & 31);
+    const int m = mbeg + f;
+    fb[i] = m / a.Tout;
+    ft[i] = m - fb[i] * a.Tout;
+  }
+  f32x4 ra[4], rx[4], rr[4];
   auto load = [&](int ch) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -369,39 +388,37 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
       const int f = sizeof(T) == 2 ? (q >> 5) : (q & 31);
       const int c4 = sizeof(T) == 2 ? (q & 31) : (q >> 5);
       const int m = mbeg + ch * BK + f;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
-      if (m < mend) {
-        const int n = n0 + c4 * 4;
-        if (n < a.N) {
-          const float* p = a.dy + (long long)m * a.ldy + n;
-          if (a.vecy && n + 4 <= a.N) v = *(const f32x4*)p;
-          else
+      const bool mv = m < mend;
+      const int b = fb[i], t = ft[i];
+      const int n = n0 + c4 * 4, k = k0 + c4 * 4;
+      const float* dyrow = a.dy + (long long)m * a.ldy;
+      const int src = pad_src(t + a.shift0 + j * a.dil, a.Tin, a.pad);
+      const bool xrow_ok = mv && src >= 0;
+      const float* xrow = a.x + (long long)(b * a.Tin + src) * a.ldx;
+      const float* rrow = a.radd + (long long)b * a.radd_ld;
+      const bool has_r = a.radd != nullptr;
+      if constexpr (VEC) {
+        ra[i] = *(const f32x4*)((mv && n < a.N) ? dyrow + n : g_zero);
+        const bool kq = xrow_ok && k < a.K;
+        rx[i] = *(const f32x4*)(kq ? xrow + k : g_zero);
+        rr[i] = *(const f32x4*)((kq && has_r) ? rrow + k : g_zero);
+      } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = (n + e < a.N) ? p[e] : 0.f;
-        }
-        const int k = k0 + c4 * 4;
-        if (k < a.K) {
-          const int b = m / a.Tout, t = m - b * a.Tout;
-          const int src = pad_src(t + a.shift0 + j * a.dil, a.Tin, a.pad);
-          if (src >= 0) {
-            const float* p = a.x + (long long)(b * a.Tin + src) * a.ldx + k;
-            const bool full = a.vecx && k + 4 <= a.K;
-            if (full) w = *(const f32x4*)p;
-            else
-#pragma unroll
-              for (int e = 0; e < 4; ++e) w[e] = (k + e < a.K) ? p[e] : 0.f;
-            if (a.radd) {
-              const float* r = a.radd + (long long)b * a.radd_ld + k;
-              if (full) w += *(const f32x4*)r;
-              else
-#pragma unroll
-                for (int e = 0; e < 4; ++e) if (k + e < a.K) w[e] += r[e];
-            }
-          }
+        for (int e = 0; e < 4; ++e) {
+          ra[i][e] = *((mv && n + e < a.N) ? dyrow + n + e : g_zero);
+          const bool kq = xrow_ok && k + e < a.K;
+          rx[i][e] = *(kq ? xrow + k + e : g_zero);
+          rr[i][e] = *((kq && has_r) ? rrow + k + e : g_zero);
         }
       }
-      ra[i] = v;
-      rx[i] = w;
+      // advance this row slot to the next chunk's frame
+      int nt = t + BK, nb = b;
+      while (nt >= a.Tout) {
+        nt -= a.Tout;
+        ++nb;
+      }
+      fb[i] = nb;
+      ft[i] = nt;
     }
   };
   constexpr int IMG = sizeof(T) == 2 ? BK * 256 : BM * LK * (int)sizeof(T);  // bytes / image
@@ -411,6 +428,7 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int q = tid + NTHR * i;
+      rx[i] += rr[i];
       if constexpr (sizeof(T) == 2) {
         const int f = q >> 5, c4 = q & 31;
         const int o = wg_off(f, c4 >> 1) + 8 * (c4 & 1);
@@ -690,9 +708,11 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
     a.seg[s].radd_ld = g.radd_ld;
     a.seg[s].Tin = g.Tin;
     a.seg[s].Kp = g.Kp;
-    a.seg[s].vec = (g.ld % 4 == 0) && (((uintptr_t)g.x & 15) == 0) &&
+    a.seg[s].vec = (g.K % 4 == 0) && (g.ld % 4 == 0) && (((uintptr_t)g.x & 15) == 0) &&
                    (!g.radd || ((g.radd_ld % 4 == 0) && (((uintptr_t)g.radd & 15) == 0)));
   }
+  bool vec = true;
+  for (int s = 0; s < nseg; ++s) vec = vec && a.seg[s].vec;
   a.nseg = nseg;
   a.Tout = Tout;
   a.M = B * Tout;
@@ -715,10 +735,16 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
   hipStream_t st = (hipStream_t)stream;
   if (wdtype == DT_BF16) {
     size_t lds = 2 * (BM + BN) * Lds<__bf16>::K * sizeof(__bf16);
-    hipLaunchKernelGGL(conv_gemm_kernel<__bf16>, grid, dim3(NTHR), lds, st, a);
+    if (vec)
+      hipLaunchKernelGGL((conv_gemm_kernel<__bf16, true>), grid, dim3(NTHR), lds, st, a);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<__bf16, false>), grid, dim3(NTHR), lds, st, a);
   } else if (wdtype == DT_F32) {
     size_t lds = 2 * (BM + BN) * Lds<float>::K * sizeof(float);
-    hipLaunchKernelGGL(conv_gemm_kernel<float>, grid, dim3(NTHR), lds, st, a);
+    if (vec)
+      hipLaunchKernelGGL((conv_gemm_kernel<float, true>), grid, dim3(NTHR), lds, st, a);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<float, false>), grid, dim3(NTHR), lds, st, a);
   } else {
     return ENSVS_E_DTYPE;
   }
@@ -753,9 +779,10 @@ ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx
   a.N = N;
   a.splits = splits;
   a.rows_per_split = (cdiv(a.M, splits) + BK - 1) / BK * BK;
-  a.vecy = (ldy % 4 == 0) && (((uintptr_t)dy & 15) == 0);
-  a.vecx = (ldx % 4 == 0) && (((uintptr_t)x & 15) == 0) &&
+  a.vecy = (N % 4 == 0) && (ldy % 4 == 0) && (((uintptr_t)dy & 15) == 0);
+  a.vecx = (K % 4 == 0) && (ldx % 4 == 0) && (((uintptr_t)x & 15) == 0) &&
            (!radd || ((radd_ld % 4 == 0) && (((uintptr_t)radd & 15) == 0)));
+  const bool vec = a.vecy && a.vecx;
   a.dst = dst;
   a.sn = sn;
   a.sk = sk;
@@ -767,10 +794,16 @@ ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DT_BF16) {
     size_t lds = 2 * 2 * BK * 256;
-    hipLaunchKernelGGL(wgrad_kernel<__bf16>, grid, dim3(NTHR), lds, st, a);
+    if (vec)
+      hipLaunchKernelGGL((wgrad_kernel<__bf16, true>), grid, dim3(NTHR), lds, st, a);
+    else
+      hipLaunchKernelGGL((wgrad_kernel<__bf16, false>), grid, dim3(NTHR), lds, st, a);
   } else {
     size_t lds = 2 * (BM + BN) * Lds<float>::K * sizeof(float);
-    hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(NTHR), lds, st, a);
+    if (vec)
+      hipLaunchKernelGGL((wgrad_kernel<float, true>), grid, dim3(NTHR), lds, st, a);
+    else
+      hipLaunchKernelGGL((wgrad_kernel<float, false>), grid, dim3(NTHR), lds, st, a);
   }
   ENSVS_CHECK_LAUNCH();
   if (splits > 1) {

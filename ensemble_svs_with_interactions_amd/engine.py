@@ -17,6 +17,26 @@ from .kernels import PackedBuffer
 
 _STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None, "concurrent": True}
 _SIDE_STREAMS = {}
+# Dev instrumentation: set to a list to collect (branch, start_event, end_event) per
+# branch region (tools/branch_times.py); None = off.
+BRANCH_TIMES = None
+
+
+class _timed:
+    def __init__(self, ctx, i):
+        self.ctx, self.i = ctx, i
+
+    def __enter__(self):
+        self.ctx.__enter__()
+        self.s = torch.cuda.Event(enable_timing=True)
+        self.s.record()
+        return self
+
+    def __exit__(self, *exc):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        BRANCH_TIMES.append((self.i, self.s, e))
+        return self.ctx.__exit__(*exc)
 
 
 def set_concurrency(on: bool):
@@ -59,8 +79,12 @@ class Branches:
     def on(self, i):
         import contextlib
         if self.on_side and i < len(self.side):
-            return torch.cuda.stream(self.side[i])
-        return contextlib.nullcontext()
+            ctx = torch.cuda.stream(self.side[i])
+        else:
+            ctx = contextlib.nullcontext()
+        if BRANCH_TIMES is None:
+            return ctx
+        return _timed(ctx, i)
 
     def __exit__(self, *exc):
         if self.on_side:

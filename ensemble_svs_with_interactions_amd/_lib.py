@@ -12,6 +12,7 @@ LIB_PATH = os.path.join(_HERE, "libensvs.so")
 c_int = ctypes.c_int
 c_ll = ctypes.c_longlong
 c_float = ctypes.c_float
+c_double = ctypes.c_double
 c_vp = ctypes.c_void_p
 
 STATUS = {0: "OK", 1: "E_SHAPE", 2: "E_DTYPE", 3: "E_HIP", 4: "E_ARG"}
@@ -19,13 +20,15 @@ STATUS = {0: "OK", 1: "E_SHAPE", 2: "E_DTYPE", 3: "E_HIP", 4: "E_ARG"}
 PAD_ZERO, PAD_REFLECT, PAD_REPLICATE = 0, 1, 2
 DT_F32, DT_BF16 = 0, 1
 EPI_PLAIN, EPI_GATE, EPI_RESSKIP, EPI_GATE_BWD, EPI_ADDSCALE, EPI_RELU_MASK = 0, 1, 2, 3, 4, 5
+EPI_GATE_TS = 6
+ACT_RELU, ACT_SIGMOID = 1, 2
 
 
 class ConvSeg(ctypes.Structure):
     _fields_ = [
-        ("x", c_vp), ("radd", c_vp), ("wofs", c_ll),
+        ("x", c_vp), ("radd", c_vp), ("pd", c_vp), ("wofs", c_ll),
         ("ld", c_int), ("K", c_int), ("taps", c_int), ("dil", c_int), ("shift0", c_int),
-        ("pad", c_int), ("radd_ld", c_int), ("Tin", c_int), ("Kp", c_int),
+        ("pad", c_int), ("radd_ld", c_int), ("Tin", c_int), ("Kp", c_int), ("pd_dil", c_int),
     ]
 
 
@@ -96,10 +99,17 @@ SIGNATURES = {
     "ensvs_randn": [c_vp, c_ll, ctypes.c_ulonglong, c_vp],
     "ensvs_dropout_mask": [c_vp, c_ll, c_float, ctypes.c_ulonglong, c_vp],
     "ensvs_randint": [c_vp, c_ll, c_ll, ctypes.c_ulonglong, c_vp],
+    "ensvs_weight_norm": [c_vp, c_vp, c_int, c_int, c_vp, c_ll, c_ll, c_vp],
+    "ensvs_usf_upsample": [c_vp, c_int, c_int, c_int, c_int, c_int, c_float, c_vp, c_vp, c_vp],
+    "ensvs_usf_dfactor": [c_vp, c_int, c_int, c_int, c_double, c_double, c_vp, c_vp],
+    "ensvs_usf_source_workspace": [c_int, c_int, c_int],
+    "ensvs_usf_source": [c_vp, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp,
+                         c_vp, c_vp, c_vp, c_int, c_vp],
+    "ensvs_usf_mix": [c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_vp],
 }
 
 # entry points returning a value instead of a status code
-RESTYPES = {"ensvs_embed_bwd_workspace": c_ll}
+RESTYPES = {"ensvs_embed_bwd_workspace": c_ll, "ensvs_usf_source_workspace": c_ll}
 
 _lib = None
 

@@ -22,6 +22,10 @@ REFERENCE_TARGETS = {
     f"{PKG}.diffsinger.DiffNet": "nnsvs.diffsinger.DiffNet",
     f"{PKG}.model.FFConvLSTM": "nnsvs.model.FFConvLSTM",
     f"{PKG}.model.SpeakerEmbedding": "nnsvs.model.SpeakerEmbedding",
+    # the recipe's vocoder config names the external package (usfgan.models.*); the
+    # reference vendors the same class under nnsvs.usfgan (generator.py:359)
+    f"{PKG}.usfgan.ParallelHnUSFGANGenerator":
+        "nnsvs.usfgan.models.generator.ParallelHnUSFGANGenerator",
 }
 
 # Scaler-derived constants that check_resf0_config (nnsvs/train_util.py:1668-1770)
@@ -98,6 +102,31 @@ def multitrack_diffusion(num_speakers=4, tiny=False, vuv_dropout=0.1):
     }
     cfg.update(LF0_STATS)
     return cfg
+
+
+def usfgan_generator():
+    """recipes/_common/conf/jp_dev_48k_nodyn/train_usfgan/generator/
+    nnsvs_world_parallel_hn_usfgan_sr48k.yaml (aux = 60 mcep + 5 codeap, hop 240 @ 48 kHz)."""
+    return {
+        "_target_": f"{PKG}.usfgan.ParallelHnUSFGANGenerator",
+        "harmonic_network_params": {"blockA": 20, "cycleA": 4, "blockF": 0, "cycleF": 0,
+                                    "cascade_mode": 0},
+        "noise_network_params": {"blockA": 0, "cycleA": 0, "blockF": 5, "cycleF": 5,
+                                 "cascade_mode": 0},
+        "filter_network_params": {"blockA": 0, "cycleA": 0, "blockF": 30, "cycleF": 3,
+                                  "cascade_mode": 0},
+        "periodicity_estimator_params": {"conv_layers": 3, "kernel_size": 5, "dilation": 1,
+                                         "padding_mode": "replicate"},
+        "in_channels": 1, "out_channels": 1, "residual_channels": 64, "gate_channels": 128,
+        "skip_channels": 64, "aux_channels": 65, "aux_context_window": 2,
+        "use_weight_norm": True, "upsample_params": {"upsample_scales": [5, 4, 4, 3]},
+    }
+
+
+# recipes/_common/conf/jp_dev_48k_nodyn/train_usfgan/data/nnsvs_world_sr48k.yaml:12-18
+USFGAN_DATA = {"sample_rate": 48000, "hop_size": 240, "dense_factor": 4, "sine_amp": 0.1,
+               "noise_amp": 0.003, "signal_types": ["sine", "noise"],
+               "sine_f0_type": "contf0", "df_f0_type": "contf0"}
 
 
 def to_reference_targets(cfg):

@@ -31,13 +31,16 @@ enum {
   EPI_GATE_BWD = 3,  // DiffNet backward: dz -> d(gate), d(filter) pre-activation grads
   EPI_ADDSCALE = 4,  // Y = alpha * aux1 + acc + bias
   EPI_RELU_MASK = 5, // Y = (accum ? Y : 0) + (aux1 > 0 ? acc + bias : 0)   (ReLU backward)
+  EPI_GATE_TS = 6,   // uSFGAN: xa/xb interleaved by 16 -> z = tanh(xa)*sigmoid(xb)
 };
+// `relu` of EPI_PLAIN / EPI_ADDSCALE selects the output activation: 1 ReLU, 2 sigmoid.
 
 struct SegDesc {
   const float* x;     // frame rows of this K-segment (already offset to its first channel)
   const float* radd;  // optional per-sequence vector added to in-range values (y = x + d[b])
+  const float* pd;    // segment 0 only: per-row pitch-dependent dilation factor (uSFGAN)
   long long wofs;     // element offset of this segment's packed weights [taps][Npad][Kp]
-  int ld, K, taps, dil, shift0, pad, radd_ld, Tin, Kp, vec;
+  int ld, K, taps, dil, shift0, pad, radd_ld, Tin, Kp, vec, pd_dil;
 };
 
 struct GemmArgs {
@@ -109,7 +112,7 @@ struct SegSel {  // the K-segment of one iteration, held in (wave-uniform) scala
   const float* x;
   const float* radd;
   long long wofs;
-  int ld, K, dil, shift0, pad, radd_ld, Tin, Kp, vec, j, kc;
+  int ld, K, dil, shift0, pad, radd_ld, Tin, Kp, vec, j, kc, s;
 };
 
 // All staging loads are unconditional: an out-of-range row (padding, m >= M) or
@@ -121,10 +124,20 @@ struct SegSel {  // the K-segment of one iteration, held in (wave-uniform) scala
 constexpr int ZERO_FLOATS = 64;
 __device__ __attribute__((aligned(16))) float g_zero[ZERO_FLOATS];
 
+// Pitch-dependent tap of an uSFGAN adaptive block (usfgan/utils/index.py:27-54), in the
+// reference's float32 arithmetic: past = rint((t - L) - d*dil) + L, future = rint(t + d*dil)
+// (round half to even); taps 0/1/2 = past/current/future, -1 = the zero padding.
+__device__ __forceinline__ int pd_src(float d, float dil, int t, int L, int j) {
+  const float dd = __fmul_rn(d, dil);
+  const int past = (int)rintf(__fadd_rn(-dd, (float)(t - L))) + L;
+  const int fut = (int)rintf(__fadd_rn(dd, (float)t));
+  const int s = j == 0 ? past : (j == 1 ? t : fut);
+  return (s >= 0 && s < L) ? s : -1;
+}
+
 template <bool VEC>
-__device__ __forceinline__ void load_a_raw(const SegSel& g, int k, bool ok, int b, int t,
+__device__ __forceinline__ void load_a_src(const SegSel& g, int k, int src, bool ok, int b,
                                            f32x4& v, f32x4& r) {
-  const int src = pad_src(t + g.shift0 + g.j * g.dil, g.Tin, g.pad);
   const bool row_ok = ok && src >= 0;
   const float* xrow = g.x + (long long)(b * g.Tin + src) * g.ld;
   const float* rrow = g.radd + (long long)b * g.radd_ld;
@@ -143,7 +156,7 @@ __device__ __forceinline__ void load_a_raw(const SegSel& g, int k, bool ok, int 
   }
 }
 
-template <typename T, bool VEC>
+template <typename T, bool VEC, bool PD>
 __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
   constexpr int LK = Lds<T>::K;
   constexpr int BCH = sizeof(T) == 2 ? 2 : 4;  // 16-B B chunks per thread
@@ -169,6 +182,16 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
   }
   ROWINIT(0) ROWINIT(1) ROWINIT(2) ROWINIT(3)
 #undef ROWINIT
+  // PD: the dilation factor of each staged row (segment 0 is the pitch-dependent one)
+  float pd0 = 0.f, pd1 = 0.f, pd2 = 0.f, pd3 = 0.f;
+  if constexpr (PD) {
+    const float* pdp = a.seg[0].pd;
+    pd0 = ok0 ? pdp[m0 + arow] : 0.f;
+    pd1 = ok1 ? pdp[m0 + arow + 32] : 0.f;
+    pd2 = ok2 ? pdp[m0 + arow + 64] : 0.f;
+    pd3 = ok3 ? pdp[m0 + arow + 96] : 0.f;
+  }
+  const float pdil = PD ? (float)a.seg[0].pd_dil : 0.f;
 
   // Flattened K iteration space (segment, tap, k-chunk); segment fields are picked with
   // wave-uniform selects on static indices.
@@ -192,6 +215,7 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
     g.ld = d.ld; g.K = d.K; g.dil = d.dil; g.shift0 = d.shift0;
     g.pad = d.pad; g.radd_ld = d.radd_ld; g.Tin = d.Tin; g.Kp = d.Kp;
     g.vec = d.vec;
+    g.s = s;
     return g;
   };
 
@@ -201,10 +225,23 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
   auto load = [&](int it) __attribute__((always_inline)) {
     const SegSel g = select(it);
     const int k = g.kc * BK + ac4 * 4;
-    load_a_raw<VEC>(g, k, ok0, b0, t0, ra0, rr0);
-    load_a_raw<VEC>(g, k, ok1, b1, t1, ra1, rr1);
-    load_a_raw<VEC>(g, k, ok2, b2, t2, ra2, rr2);
-    load_a_raw<VEC>(g, k, ok3, b3, t3, ra3, rr3);
+    int s0, s1, s2, s3;
+    if (PD && g.s == 0) {
+      s0 = pd_src(pd0, pdil, t0, g.Tin, g.j);
+      s1 = pd_src(pd1, pdil, t1, g.Tin, g.j);
+      s2 = pd_src(pd2, pdil, t2, g.Tin, g.j);
+      s3 = pd_src(pd3, pdil, t3, g.Tin, g.j);
+    } else {
+      const int sh = g.shift0 + g.j * g.dil;
+      s0 = pad_src(t0 + sh, g.Tin, g.pad);
+      s1 = pad_src(t1 + sh, g.Tin, g.pad);
+      s2 = pad_src(t2 + sh, g.Tin, g.pad);
+      s3 = pad_src(t3 + sh, g.Tin, g.pad);
+    }
+    load_a_src<VEC>(g, k, s0, ok0, b0, ra0, rr0);
+    load_a_src<VEC>(g, k, s1, ok1, b1, ra1, rr1);
+    load_a_src<VEC>(g, k, s2, ok2, b2, ra2, rr2);
+    load_a_src<VEC>(g, k, s3, ok3, b3, ra3, rr3);
     const char* wbase = W + ((g.wofs + ((long long)g.j * Npad + n0) * g.Kp + g.kc * BK) *
                              (long long)sizeof(T));
 #pragma unroll
@@ -256,7 +293,7 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
 
   // ---------------------------------------------------------------- epilogue
   const int rbase = m0 + wr * 64 + (lane >> 4) * 4;
-  if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP) {
+  if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const int pc = n0 + wc * 64 + p * 32 + (lane & 15);
@@ -276,6 +313,8 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
             a.aux0[(long long)row * a.ld0 + c] = v0;
             a.aux0[(long long)row * a.ld0 + a.C + c] = v1;
             a.Y[(long long)row * a.ldy + c] = sigmoidf_(v0) * tanhf(v1);
+          } else if (a.epi == EPI_GATE_TS) {
+            a.Y[(long long)row * a.ldy + c] = tanhf(v0) * sigmoidf_(v1);
           } else {
             const float xr = a.aux1[(long long)row * a.ld1 + c];
             a.Y[(long long)row * a.ldy + c] = (xr + v0) * 0.70710678118654752f;
@@ -301,10 +340,12 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
         float* y = a.Y + (long long)row * a.ldy + col;
         if (a.epi == EPI_PLAIN) {
           if (a.accum) v += *y;
-          if (a.relu) v = fmaxf(v, 0.f);
+          if (a.relu == 1) v = fmaxf(v, 0.f);
+          else if (a.relu == 2) v = sigmoidf_(v);
           *y = v;
         } else if (a.epi == EPI_ADDSCALE) {
-          *y = a.alpha * a.aux1[(long long)row * a.ld1 + col] + v;
+          v += a.alpha * a.aux1[(long long)row * a.ld1 + col];
+          *y = a.relu == 1 ? fmaxf(v, 0.f) : v;
         } else if (a.epi == EPI_RELU_MASK) {
           v = a.aux1[(long long)row * a.ld1 + col] > 0.f ? v : 0.f;
           *y = a.accum ? *y + v : v;
@@ -698,6 +739,10 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
     if (g.Kp % BK != 0 || g.Kp < g.K || g.taps < 1) return ENSVS_E_SHAPE;
     a.seg[s].x = g.x;
     a.seg[s].radd = g.radd;
+    a.seg[s].pd = g.pd;
+    a.seg[s].pd_dil = g.pd_dil;
+    // a pitch-dependent segment: the first one, 3 taps (past/current/future), Tin == Tout
+    if (g.pd && (s != 0 || g.taps != 3 || g.Tin != Tout)) return ENSVS_E_SHAPE;
     a.seg[s].wofs = g.wofs;
     a.seg[s].ld = g.ld;
     a.seg[s].K = g.K;
@@ -733,21 +778,26 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
   a.C = C;
   dim3 grid(cdiv(a.M, BM), Npad / BN);
   hipStream_t st = (hipStream_t)stream;
+  const bool pd = a.seg[0].pd != nullptr;
+#define LAUNCH_GEMM(T, V, P)                                                            \
+  hipLaunchKernelGGL((conv_gemm_kernel<T, V, P>), grid, dim3(NTHR),                    \
+                     2 * (BM + BN) * Lds<T>::K * sizeof(T), st, a)
   if (wdtype == DT_BF16) {
-    size_t lds = 2 * (BM + BN) * Lds<__bf16>::K * sizeof(__bf16);
-    if (vec)
-      hipLaunchKernelGGL((conv_gemm_kernel<__bf16, true>), grid, dim3(NTHR), lds, st, a);
-    else
-      hipLaunchKernelGGL((conv_gemm_kernel<__bf16, false>), grid, dim3(NTHR), lds, st, a);
+    if (pd) {
+      if (vec) LAUNCH_GEMM(__bf16, true, true); else LAUNCH_GEMM(__bf16, false, true);
+    } else {
+      if (vec) LAUNCH_GEMM(__bf16, true, false); else LAUNCH_GEMM(__bf16, false, false);
+    }
   } else if (wdtype == DT_F32) {
-    size_t lds = 2 * (BM + BN) * Lds<float>::K * sizeof(float);
-    if (vec)
-      hipLaunchKernelGGL((conv_gemm_kernel<float, true>), grid, dim3(NTHR), lds, st, a);
-    else
-      hipLaunchKernelGGL((conv_gemm_kernel<float, false>), grid, dim3(NTHR), lds, st, a);
+    if (pd) {
+      if (vec) LAUNCH_GEMM(float, true, true); else LAUNCH_GEMM(float, false, true);
+    } else {
+      if (vec) LAUNCH_GEMM(float, true, false); else LAUNCH_GEMM(float, false, false);
+    }
   } else {
     return ENSVS_E_DTYPE;
   }
+#undef LAUNCH_GEMM
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }

@@ -134,6 +134,8 @@ class Seg:
     radd: Optional[torch.Tensor] = None
     radd_ld: int = 0
     xoff: int = 0           # element offset added to x.data_ptr()
+    pd: Optional[torch.Tensor] = None  # per-row pitch-dependent dilation factor (uSFGAN)
+    pd_dil: int = 0
 
 
 def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: int,
@@ -146,6 +148,8 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
         d = arr[i]
         d.x = s.x.data_ptr() + 4 * s.xoff
         d.radd = None if s.radd is None else s.radd.data_ptr()
+        d.pd = None if s.pd is None else s.pd.data_ptr()
+        d.pd_dil = s.pd_dil
         d.wofs = s.ref.offset
         d.ld, d.K, d.taps, d.dil, d.shift0 = s.ld, s.K, s.taps, s.dil, s.shift0
         d.pad, d.radd_ld, d.Tin, d.Kp = s.pad, s.radd_ld, s.Tin, s.ref.Kp

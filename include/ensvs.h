@@ -22,14 +22,18 @@ enum { ENSVS_STATUS_OK = 0, ENSVS_STATUS_E_SHAPE = 1, ENSVS_STATUS_E_DTYPE = 2,
 enum { ENSVS_PAD_ZERO = 0, ENSVS_PAD_REFLECT = 1, ENSVS_PAD_REPLICATE = 2 };
 enum { ENSVS_DT_F32 = 0, ENSVS_DT_BF16 = 1 };
 enum { ENSVS_EPI_PLAIN = 0, ENSVS_EPI_GATE = 1, ENSVS_EPI_RESSKIP = 2, ENSVS_EPI_GATE_BWD = 3,
-       ENSVS_EPI_ADDSCALE = 4, ENSVS_EPI_RELU_MASK = 5 };
+       ENSVS_EPI_ADDSCALE = 4, ENSVS_EPI_RELU_MASK = 5, ENSVS_EPI_GATE_TS = 6 };
 
 /* One K-segment of the implicit-GEMM activation operand. */
 typedef struct ensvs_conv_seg {
   const float* x;     /* frame rows (offset to the segment's first channel) */
   const float* radd;  /* optional per-sequence vector added to in-range values */
+  const float* pd;    /* optional (first segment, taps 3): per-row pitch-dependent dilation
+                         factor; taps become past / current / future samples gathered with
+                         the uSFGAN index arithmetic (usfgan/utils/index.py:12-54) */
   long long wofs;     /* element offset of packed weights [taps][Npad][Kp] */
   int ld, K, taps, dil, shift0, pad, radd_ld, Tin, Kp;
+  int pd_dil;         /* dilation multiplying pd */
 } ensvs_conv_seg;
 
 /* Weight repack descriptor (reference layout -> GEMM layout [tap][Npad][Kp]). */
@@ -46,7 +50,10 @@ typedef struct ensvs_pack_desc {
 /* Conv1d / Linear forward and input-gradient as an MFMA implicit GEMM.
  * Replaces nn.Conv1d / nn.Linear / nn.ReflectionPad1d call sites in
  * nnsvs/model.py:837-859 (FFConvLSTM.ff/.conv), nnsvs/acoustic_models/tacotron_f0.py:852-874,
- * and the DiffNet convolutions nnsvs/diffsinger/denoiser.py:40-66,101-124. */
+ * the DiffNet convolutions nnsvs/diffsinger/denoiser.py:40-66,101-124 and every uSFGAN
+ * generator convolution (usfgan/layers/residual_block.py:123-234,389-399, upsample.py:166-168,
+ * usfgan/models/generator.py:427-466).  `relu`: output activation of EPI_PLAIN / EPI_ADDSCALE
+ * (1 ReLU, 2 sigmoid). */
 int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N, int Npad,
                     const void* W, int wdtype, const float* bias, float* Y, int ldy, int epi,
                     int relu, int accum, float* aux0, int ld0, const float* aux1, int ld1,
@@ -176,6 +183,34 @@ int ensvs_reflect_fold(const float* dxp, int B, int T, int pad, int C, float* dx
 int ensvs_randn(float* out, long long n, unsigned long long seed, void* stream);
 int ensvs_dropout_mask(float* out, long long n, float p, unsigned long long seed, void* stream);
 int ensvs_randint(long long* out, long long n, long long hi, unsigned long long seed,
+                  void* stream);
+
+/* ---- uSFGAN vocoder (synthesis) ----------------------------------------- */
+
+/* nn.utils.weight_norm folding (usfgan/models/generator.py:524-544, util.py:414):
+ * w[n*sn + k*sk] = v[n][k] * (g[n] / ||v[n][:]||) over rows of K contiguous elements;
+ * g == NULL copies v (plain weights into the same strided destination). */
+int ensvs_weight_norm(const float* g, const float* v, int N, int K, float* w, long long sn,
+                      long long sk, void* stream);
+/* One stage of UpsampleNetwork (usfgan/layers/upsample.py:86-128): nearest x s along time
+ * (F.interpolate scale_factor, inv_s = float(1/s)) then Conv2d(1,1,(1,2s+1), padding (0,s))
+ * with taps w.  x (B*Tin, ld) -> y (B*Tin*s, ld); channels C..ld-1 of y are zeroed. */
+int ensvs_usf_upsample(const float* x, int ld, int B, int Tin, int C, int s, float inv_s,
+                       const float* w, float* y, void* stream);
+/* dilated_factor + repeat(hop) (usfgan/utils/features.py:56-75, usfgan/__init__.py:50-58):
+ * d[b*T*hop + i] = float((fs / f0') / dense), f0' = f0[b][i/hop] (0 -> fs/dense). */
+int ensvs_usf_dfactor(const float* f0, int B, int T, int hop, double fs, double dense, float* d,
+                      void* stream);
+/* SignalGenerator(["sine", "noise"]) (usfgan/utils/features.py:112-164): out (B*T*hop, ldo)
+ * columns [sine + amp*sine_noise, noise]; scale = float(T)/float(T*hop) (nearest upsample of
+ * f0); the phase cumsum is scanned in fp64.  ws: ensvs_usf_source_workspace() doubles. */
+long long ensvs_usf_source_workspace(int B, int T, int hop);
+int ensvs_usf_source(const float* f0, int B, int T, int hop, float scale, float fs,
+                     float sine_amp, float noise_amp, const float* sine_noise, const float* noise,
+                     double* ws, float* out, int ldo, void* stream);
+/* Harmonic/noise mix (usfgan/models/generator.py:505-508): s = a*h + (1-a)*n; keep != 0 also
+ * stores h = a*h and n = (1-a)*n (the forward's debug outputs). */
+int ensvs_usf_mix(const float* a, float* h, float* n, float* s, long long total, int keep,
                   void* stream);
 
 #ifdef __cplusplus

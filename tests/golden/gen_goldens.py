@@ -449,6 +449,86 @@ def case_data_path():
     save("data_path", arrays, meta)
 
 
+class _AttrDict(dict):
+    """Stand-in for the OmegaConf vocoder config: attribute access + `in`."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError:
+            raise AttributeError(k)
+
+
+def case_usfgan():
+    """uSFGAN generator forward and USFGANWrapper.inference (usfgan/__init__.py:13-65) at
+    40 frames (9 600 samples: > the 512 dilation of the filter network), weight norm on."""
+    from nnsvs.usfgan import USFGANWrapper as RefWrapper
+    cfg = configs.to_reference_targets(configs.usfgan_generator())
+    torch.manual_seed(0)
+    gen = configs.instantiate(cfg)
+    shapes = {k: tuple(v.shape) for k, v in gen.state_dict().items()}
+    sd = seeded_state_dict(shapes, SEED)
+    gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    gen.eval()
+    r = rng_for("usfgan")
+    T = 40
+    f0 = np.repeat(r.uniform(110.0, 880.0, size=T // 5), 5).astype(np.float32)
+    f0[12:17] = 0.0  # unvoiced frames: d = 1, vuv = 0
+    f0 = f0.reshape(T, 1)
+    aux = r.standard_normal((T, 65)).astype(np.float32)
+    L = T * configs.USFGAN_DATA["hop_size"]
+    sine_noise = r.standard_normal((1, 1, L)).astype(np.float32)
+    noise = r.standard_normal((1, 1, L)).astype(np.float32)
+    cap = {}
+    orig = gen.forward
+
+    def capture(x, c, d):
+        out = orig(x, c, d)
+        cap.update(x=x, c=c, d=d, out=out)
+        return out
+    gen.forward = capture
+    wcfg = _AttrDict(data=_AttrDict(configs.USFGAN_DATA),
+                     generator=_AttrDict(aux_context_window=2))
+    wrapper = RefWrapper(wcfg, gen)
+    with torch.no_grad(), inject_diffusion(normals=[T_(sine_noise), T_(noise)]):
+        y = wrapper.inference(f0.copy(), T_(aux))
+    x_out, s, h, n, a = cap["out"]
+    assert torch.equal(y, x_out)
+    # the reference loads vocoders with remove_weight_norm() (nnsvs/util.py:412-414)
+    gen.forward = orig
+    gen.remove_weight_norm()
+    with torch.no_grad():
+        y_rwn = gen(cap["x"], cap["c"], cap["d"])[0]
+    save("usfgan", dict(f0=f0, aux=aux, sine_noise=sine_noise, noise=noise,
+                        x=cap["x"].numpy(), c=cap["c"].numpy(), d=cap["d"].numpy(),
+                        y=y.numpy(), s=s.numpy(), h=h.numpy(), n=n.numpy(),
+                        a4=a[:, :4].numpy(), y_rwn=y_rwn.numpy()),
+         dict(shapes={k: list(v) for k, v in shapes.items()}))
+
+
+def case_pd_index():
+    """Bit-exact pitch-dependent indexing (usfgan/utils/index.py:12-54) and dilated factors
+    (features.py:56-75) over 10 s at 48 kHz: source sample per (dilation, sample)."""
+    from nnsvs.usfgan.utils import dilated_factor as ref_df, index_initial, pd_indexing
+    r = rng_for("pd_index")
+    T, hop = 2000, configs.USFGAN_DATA["hop_size"]
+    L = T * hop
+    f0 = r.uniform(70.0, 1100.0, size=T).astype(np.float32)
+    f0[r.random(T) < 0.2] = 0.0
+    df = ref_df(f0.copy(), 48000, 4).repeat(hop, axis=0)
+    d = torch.FloatTensor(df).view(1, 1, -1)
+    x = torch.arange(1, L + 1, dtype=torch.float32).view(1, 1, L)  # value = sample + 1
+    bi, ci = index_initial(1, 1)
+    arrays = dict(f0=f0, d=d.numpy().reshape(-1))
+    n1 = np.arange(1, L + 1, dtype=np.int64)
+    for dil in (1, 2, 4, 8, 16):
+        xP, xF = pd_indexing(x, d, dil, bi, ci)
+        # stored as offsets from the sample itself (runs of equal values compress)
+        arrays[f"offP{dil}"] = (n1 - xP.numpy().reshape(-1).astype(np.int64)).astype(np.int32)
+        arrays[f"offF{dil}"] = (xF.numpy().reshape(-1).astype(np.int64) - n1).astype(np.int32)
+    save("usfgan_pd_index", arrays, dict(T=T, hop=hop))
+
+
 def main():
     which = sys.argv[1:] or ["all"]
     run = lambda n: "all" in which or n in which  # noqa: E731
@@ -475,6 +555,10 @@ def main():
         case_model_inference_tiny()
     if run("data"):
         case_data_path()
+    if run("usfgan"):
+        case_usfgan()
+    if run("pd_index"):
+        case_pd_index()
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(dict(seed=SEED, torch=torch.__version__, numpy=np.__version__,
                        reference="sarulab-speech/ensemble_svs_with_interactions @ 2025-03-21",

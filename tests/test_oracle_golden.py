@@ -143,3 +143,40 @@ def test_inference_bap():
                                              a["lengths"], T_(a["spk"]).expand(B, T, -1),
                                              T_(a["noises"]))
     assert rel(out, a["out"]) < 1e-4
+
+
+# ------------------------------------------------------------------ uSFGAN (a13)
+
+def _usfgan_params():
+    a, meta = load_case("usfgan")
+    return a, params_from_shapes(meta["shapes"])
+
+
+def test_usfgan_generator_and_inference():
+    from oracle import usfgan_oracle as U
+    a, P = _usfgan_params()
+    with torch.no_grad():
+        x, c, d = U.generator_inputs(a["f0"], T_(a["aux"]), T_(a["sine_noise"]), T_(a["noise"]))
+        # input pipeline: dilated factors bit-exact, sine source to fp32 rounding
+        assert torch.equal(d, T_(a["d"]))
+        assert torch.equal(c, T_(a["c"]))
+        assert (x - T_(a["x"])).abs().max().item() < 1e-6
+        y, s, h, n, av = U.generator_forward(P, T_(a["x"]), T_(a["c"]), T_(a["d"]))
+    for k, v in dict(y=y, s=s, h=h, n=n).items():
+        assert rel(v, a[k]) < 1e-4, k
+    assert rel(av[:, :4], a["a4"]) < 1e-5
+    assert rel(a["y_rwn"], a["y"]) < 1e-4  # remove_weight_norm leaves the output unchanged
+
+
+def test_usfgan_pd_indexing_bitexact():
+    from oracle import usfgan_oracle as U
+    a, meta = load_case("usfgan_pd_index")
+    L = meta["T"] * meta["hop"]
+    d = U.dilated_factor(a["f0"], 48000, 4).repeat(meta["hop"], axis=0)
+    assert np.array_equal(d.astype(np.float32), a["d"])
+    x = torch.arange(1, L + 1, dtype=torch.float32).view(1, 1, L)
+    n1 = np.arange(1, L + 1, dtype=np.int64)
+    for dil in (1, 2, 4, 8, 16):
+        xP, xF = U.pd_indexing(x, T_(a["d"]).view(1, 1, -1), dil)
+        assert np.array_equal(n1 - xP.numpy().reshape(-1).astype(np.int64), a[f"offP{dil}"])
+        assert np.array_equal(xF.numpy().reshape(-1).astype(np.int64) - n1, a[f"offF{dil}"])

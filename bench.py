@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--frames", type=int, default=1024)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-synth", action="store_true", help="skip the synthesis RTF leg")
     ap.add_argument("--serial", action="store_true",
                     help="run the lf0/mgc/bap/vuv branches serially (no side streams)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -70,6 +71,61 @@ def gate_gemm_timing(model, P, T, dev, iters=20):
     sec = s.elapsed_time(e) / 1e3 / iters
     flops = 2.0 * M * (2 * C) * (3 * C + E)
     return sec, flops
+
+
+def _median_time(fn, reps):
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.time()
+        out = fn()
+        torch.cuda.synchronize()
+        ts.append(time.time() - t0)
+    return float(np.median(ts)), out
+
+
+def synth_rtf(model, dev, T=2000, parts=6, reps=3):
+    """Synthesis real-time factor (BASELINE metric part 2): elapsed /
+    audio seconds (svs.py:449-452, 581-582) of acoustic inference (pad_inference_multitrack,
+    free-running AR log-F0, 100-step reverse diffusion for mgc and bap, V/UV) + the uSFGAN
+    generator on its output, for one (main, sub) pair of T frames (5 ms) and for a
+    `parts`-part ensemble (every part paired with its neighbour) batched in one pass.
+    Host glue of the reference (scalers, pyworld aperiodicity codec, gen.py:1637-1694) is
+    replaced by identity scalers on synthetic data."""
+    from ensemble_svs_with_interactions_amd import usfgan
+    torch.manual_seed(7)
+    voc = configs.instantiate(configs.usfgan_generator()).to(dev)
+    voc.remove_weight_norm()  # as load_vocoder does (nnsvs/util.py:412-414)
+    wrapper = usfgan.USFGANWrapper({"data": dict(configs.USFGAN_DATA),
+                                    "generator": {"aux_context_window": 2}}, voc)
+    model.eval()
+    sc, mu = configs.LF0_STATS["out_lf0_scale"], configs.LF0_STATS["out_lf0_mean"]
+    out = {}
+    for name, B in (("pair", 1), (f"ensemble_{parts}part", parts)):
+        b = data.synthetic_batch(B, T, 4242 + B)
+        g = lambda k: torch.from_numpy(b[k]).to(dev).contiguous()  # noqa: E731
+        xm, xs, s0, s1 = g("x_main"), g("x_sub"), g("spk_main"), g("spk_sub")
+
+        def acoustic():
+            return model.inference(xm, xs, spks=(s0, s1), lengths=[T] * B)
+
+        def vocoder(feats):
+            f0 = torch.exp(feats[:, :, 60] * sc + mu)  # de-normalised continuous log-F0
+            aux = torch.cat([feats[:, :, :60], feats[:, :, 62:67]], -1)
+            return wrapper.inference_batch(f0, aux)
+
+        feats = acoustic()  # warm-up (weight packing)
+        vocoder(feats)
+        ta, feats = _median_time(acoustic, reps)
+        tv, wav = _median_time(lambda: vocoder(feats), reps)
+        assert torch.isfinite(wav).all()
+        sec = T * 0.005
+        out[name] = dict(rtf=(ta + tv) / sec, acoustic_ms=ta * 1e3, vocoder_ms=tv * 1e3,
+                         tracks=B, samples_per_track=int(wav.shape[-1]))
+    model.train()
+    return dict(metric="synth RTF (acoustic inference + uSFGAN) / audio seconds",
+                frames=T, audio_s=T * 0.005, diffusion_steps=100, higher_is_better=False,
+                dtype=engine.gemm_precision(), **out)
 
 
 def cpu_baseline(args, budget_s):
@@ -207,6 +263,8 @@ def main():
                      "frac": achieved / (PEAK_BF16_TFLOPS if args.precision == "bf16" else 157.3),
                      "launch_us": sec * 1e6, "traffic": _traffic()},
     }
+    if not args.no_synth:
+        out["synth"] = synth_rtf(model, dev)
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     print(json.dumps(out), flush=True)

@@ -516,7 +516,9 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
              Ly.stream())
 
     # ------------------------------------------------------------------ inference
-    def _infer(self, x_main, x_sub, spk0, spk1, lengths, noises=None, masks=None):
+    def _infer(self, x_main, x_sub, spk0, spk1, lengths, noises=None, masks=None, graph=None):
+        """noises: {"mgc"/"bap": (K+1, B*T, M) replayed draws}; masks: (B*T/4,) AR-decoder
+        dropout keep-masks of the main-track call; graph: captured reverse diffusion."""
         self._set_lf0_params()
         B, T, D = x_main.shape
         dev = x_main.device
@@ -532,8 +534,18 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
              Ly.stream())
         enc_src = [(x_main, D, 0, D), (out, Dy, o[1], 1)]
         nz = noises or {}
-        mgc = self.mgc_model._inference(enc_src, B, T, lens_dev, s0, E, nz.get("mgc"))
-        bap = self.bap_model._inference(enc_src, B, T, lens_dev, s0, E, nz.get("bap"))
+        # the two reverse diffusions are independent: concurrent HIP streams
+        with Branches(dev) as br:
+            with br.on(1):
+                mgc = self.mgc_model._inference(enc_src, B, T, lens_dev, s0, E, nz.get("mgc"),
+                                                graph=graph)
+            with br.on(2):
+                bap = self.bap_model._inference(enc_src, B, T, lens_dev, s0, E, nz.get("bap"),
+                                                graph=graph)
+        if br.on_side:  # consumed on the main stream: keep the blocks alive for it
+            main = torch.cuda.current_stream(dev)
+            mgc.record_stream(main)
+            bap.record_stream(main)
         call("ensvs_copy_cols", mgc.data_ptr(), o[1] - o[0], out.data_ptr() + 4 * o[0], Dy, B * T,
              o[1] - o[0], Ly.stream())
         call("ensvs_copy_cols", bap.data_ptr(), o[4] - o[3], out.data_ptr() + 4 * o[3], Dy, B * T,
@@ -559,9 +571,10 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
         nm, rm, lf0, vuv, nb, rb, res = outs
         return ((nm, rm), lf0, vuv, (nb, rb)), res
 
-    def inference(self, x_main, x_sub, spks=None, lengths=None):
+    def inference(self, x_main, x_sub, spks=None, lengths=None, draws=None):
         """pad_inference_multitrack (acoustic_models/util.py:154-188): replicate-pad to a
-        multiple of r (r frames when already divisible), run, trim."""
+        multiple of r (r frames when already divisible), run, trim.  ``draws`` (tests only)
+        replays random draws: dict(noises=..., masks=..., graph=...) of ``_infer``."""
         r = self.reduction_factor
         B, T, D = x_main.shape
         lens = [int(v) for v in (lengths if lengths is not None else [T] * B)]
@@ -577,7 +590,7 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
                 call("ensvs_copy_cols", x.data_ptr() + 4 * (T - 1) * D, T * D,
                      xp.data_ptr() + 4 * (T + k) * D, (T + pad) * D, B, D, Ly.stream())
             xs.append(xp)
-        out = self._infer(xs[0], xs[1], spks[0], spks[1], [v + pad for v in lens])
+        out = self._infer(xs[0], xs[1], spks[0], spks[1], [v + pad for v in lens], **(draws or {}))
         return out[:, :-pad]
 
 

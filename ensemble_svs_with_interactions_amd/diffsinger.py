@@ -27,8 +27,12 @@ from . import layers as Ly
 from ._lib import call
 from .base import BaseModel, PredictionType
 from .engine import ModulePacks, empty, grad_of, lengths_pair, next_seed
+from .engine import gemm_dtype as engine_gemm_dtype
 
 SQRT1_2 = 1.0 / math.sqrt(2.0)
+# Reverse diffusion as a captured HIP graph when no noise is injected (set "on" False to
+# launch eagerly).
+USE_GRAPHS = {"on": True}
 
 
 def Conv1d(*args, **kwargs):
@@ -403,32 +407,103 @@ class GaussianDiffusion(BaseModel):
         _, dspk = self.encoder._bwd(st["est"], dcond, want_spk=True)
         return dspk
 
-    def _inference(self, sources, B, T, lens_dev, spk=None, spk_ld=0, noises=None):
+    def _schedule_host(self):
+        """Per-step p_sample constants (host floats; read once per schedule version)."""
+        key = (self.betas.data_ptr(), self.betas._version)
+        if getattr(self, "_sched_key", None) != key:
+            f = lambda b: b.detach().cpu().tolist()  # noqa: E731
+            self._sched = (f(self.sqrt_recip_alphas_cumprod),
+                           f(self.sqrt_recipm1_alphas_cumprod), f(self.posterior_mean_coef1),
+                           f(self.posterior_mean_coef2), f(self.posterior_log_variance_clipped))
+            self._sched_key = key
+        return self._sched
+
+    def _steps(self, B, dev):
+        """(K, B) int64 diffusion steps K-1 .. 0 (p_sample's t for every sequence)."""
+        K_ = self.K_step
+        return torch.arange(K_ - 1, -1, -1, device=dev, dtype=torch.int64) \
+            .repeat_interleave(B).view(K_, B)
+
+    def _reverse(self, x, cond, E, B, T, noise_at, steps=None):
+        """The K-step reverse process (diffusion.py:193-204, 302-336) on x in place:
+        DiffNet + p_sample per step, then x *= norm_scale.  noise_at(k) -> (M, Mc) draw."""
+        dev = x.device
+        M, Mc, K_ = B * T, self.out_dim, self.K_step
+        sra, srm1, c1, c2, lv = self._schedule_host()
+        if steps is None:
+            steps = self._steps(B, dev)
+        for k, i in enumerate(reversed(range(K_))):
+            eps, _ = self.denoise_fn._fwd(x, Mc, steps[k], cond, E, B, T, save=False)
+            sigma = 0.0 if i == 0 else math.exp(0.5 * lv[i])
+            call("ensvs_p_sample", x.data_ptr(), eps.data_ptr(), noise_at(k).data_ptr(), M * Mc,
+                 sra[i], srm1[i], c1[i], c2[i], sigma, Ly.stream())
+        call("ensvs_axpby", x.data_ptr(), float(self.norm_scale), x.data_ptr(), 0.0, M * Mc,
+             Ly.stream())
+
+    def _reverse_graph(self, cond, E, B, T, noises=None):
+        """The reverse process captured once per (B, T) as a HIP graph: ~46 launches x K
+        steps become one graph launch.  Inputs (cond, the K+1 noise draws) are copied into /
+        drawn in static buffers before each replay, so every call gets fresh noise."""
+        dev = cond.device
+        M, Mc, K_ = B * T, self.out_dim, self.K_step
+        sig = (B, T, E, str(dev), engine_gemm_dtype(),
+               tuple((p.data_ptr(), p._version) for p in self.denoise_fn.parameters()),
+               self.betas._version)
+        cache = getattr(self, "_graphs", None)
+        if cache is None:
+            cache = self._graphs = {}
+        ent = cache.get((B, T, E, str(dev)))
+        if ent is None or ent["sig"] != sig:
+            cache.pop((B, T, E, str(dev)), None)
+            st = dict(cond=empty(M, E, device=dev), noise=empty((K_ + 1) * M * Mc, device=dev),
+                      x=empty(M, Mc, device=dev), sig=sig, steps=self._steps(B, dev))
+            nz = st["noise"].view(K_ + 1, M, Mc)
+            # warm-up outside capture (packs the weights, reads the schedule to the host)
+            self.denoise_fn._packs.ensure(self.denoise_fn, self.denoise_fn._register)
+            self._schedule_host()
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(side), torch.cuda.graph(g, stream=side):
+                call("ensvs_copy_cols", nz[0].data_ptr(), Mc, st["x"].data_ptr(), Mc, M, Mc,
+                     Ly.stream())
+                self._reverse(st["x"], st["cond"], E, B, T, lambda k: nz[k + 1], st["steps"])
+            torch.cuda.current_stream(dev).wait_stream(side)
+            st["graph"] = g
+            cache[(B, T, E, str(dev))] = ent = st
+        call("ensvs_copy_cols", cond.data_ptr(), E, ent["cond"].data_ptr(), E, M, E, Ly.stream())
+        if noises is None:
+            call("ensvs_randn", ent["noise"].data_ptr(), ent["noise"].numel(), next_seed(),
+                 Ly.stream())
+        else:  # replayed draws (K+1, M, Mc)
+            nzs = noises.contiguous().float()
+            call("ensvs_copy_cols", nzs.data_ptr(), Mc, ent["noise"].data_ptr(), Mc,
+                 (K_ + 1) * M, Mc, Ly.stream())
+        ent["graph"].replay()
+        out = empty(M, Mc, device=dev)
+        call("ensvs_copy_cols", ent["x"].data_ptr(), Mc, out.data_ptr(), Mc, M, Mc, Ly.stream())
+        return out
+
+    def _inference(self, sources, B, T, lens_dev, spk=None, spk_ld=0, noises=None, graph=None):
+        """noises: optional (K+1, B*T, Mc) replayed draws (x_K, then one per step).
+        graph: run the captured reverse process (default: USE_GRAPHS unless draws are
+        replayed)."""
         dev = self.betas.device
         M, Mc = B * T, self.out_dim
         cond, _ = self.encoder._fwd(sources, B, T, lens_dev, spk, spk_ld, training=False,
                                     save=False)
         E = cond.shape[1]
-        K_ = self.K_step
-        x = noises[0].clone() if noises is not None else Ly.randn(M * Mc, dev).view(M, Mc)
-        sra = self.sqrt_recip_alphas_cumprod.cpu().tolist()
-        srm1 = self.sqrt_recipm1_alphas_cumprod.cpu().tolist()
-        c1 = self.posterior_mean_coef1.cpu().tolist()
-        c2 = self.posterior_mean_coef2.cpu().tolist()
-        lv = self.posterior_log_variance_clipped.cpu().tolist()
-        steps = torch.arange(K_ - 1, -1, -1, device=dev, dtype=torch.int64).repeat_interleave(B) \
-            .view(K_, B)
-        for k, i in enumerate(reversed(range(K_))):
-            eps, _ = self.denoise_fn._fwd(x, Mc, steps[k], cond, E, B, T, save=False)
-            if noises is not None:
-                z = noises[k + 1]
-            else:
-                z = Ly.randn(M * Mc, dev).view(M, Mc)
-            sigma = 0.0 if i == 0 else math.exp(0.5 * lv[i])
-            call("ensvs_p_sample", x.data_ptr(), eps.data_ptr(), z.data_ptr(), M * Mc, sra[i],
-                 srm1[i], c1[i], c2[i], sigma, Ly.stream())
-        call("ensvs_axpby", x.data_ptr(), float(self.norm_scale), x.data_ptr(), 0.0, M * Mc,
-             Ly.stream())
+        if graph is None:
+            graph = USE_GRAPHS["on"] and noises is None
+        if graph:
+            return self._reverse_graph(cond, E, B, T, noises)
+        if noises is not None:
+            x = noises[0].clone()
+            noise_at = lambda k: noises[k + 1]  # noqa: E731
+        else:
+            x = Ly.randn(M * Mc, dev).view(M, Mc)
+            noise_at = lambda k: Ly.randn(M * Mc, dev).view(M, Mc)  # noqa: E731
+        self._reverse(x, cond, E, B, T, noise_at)
         return x
 
     # ---------------------------------------------------------------- reference API

@@ -86,6 +86,8 @@ SIGNATURES = {
     "ensvs_p_sample": [c_vp, c_vp, c_vp, c_ll, c_float, c_float, c_float, c_float, c_float, c_vp],
     "ensvs_masked_l1": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int,
                         c_float, c_float, c_vp, c_vp, c_vp],
+    "ensvs_lf0_interaction": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_int,
+                              c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ensvs_l2norm": [c_vp, c_ll, c_vp, c_vp, c_vp],
     "ensvs_adam": [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_float, c_float, c_float, c_float, c_float,
                    c_float, c_float, c_vp],

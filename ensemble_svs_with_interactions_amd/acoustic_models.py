@@ -471,7 +471,14 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
             with br.on(0):
                 lf0, res, st_lf0 = self.lf0_model._fwd(x_main, x_sub, D, B, T, lens_dev, s0, s1,
                                                        E, masks=draws.get("lf0_main"))
-                if self.training:
+                if self.output_subtrack:
+                    # sub-track call with its outputs (multistream.py:1649-1651, 1759-1768):
+                    # the lf0 prediction the interaction loss compares with the main one.
+                    # Same stream as the main call: BatchNorm running statistics are
+                    # updated main-then-sub, as in the reference.
+                    lf0_s, res_s, st_lf0_s = self.lf0_model._fwd(
+                        x_sub, x_main, D, B, T, lens_dev, s1, s0, E, masks=draws.get("lf0_sub"))
+                elif self.training:
                     # sub-track call (outputs unused without output_subtrack): BN statistics
                     self.lf0_model._bn_only(x_sub, x_main, D, B, T, s1, s0, E)
             with br.on(1):
@@ -490,15 +497,26 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
                     lf0_residual=res)
         st = dict(lf0=st_lf0, mgc=st_mgc, bap=st_bap, vuv=st_vuv, i0=i0, i1=i1, B=B, T=T, E=E,
                   lens_host=lens_host, lens_dev=lens_dev)
+        if self.output_subtrack:
+            outs.update(lf0_sub=lf0_s, lf0_residual_sub=res_s)
+            st["lf0_sub"] = st_lf0_s
         return outs, st
 
     def _train_bwd(self, st, g):
-        """g: dict of grads (B*T, .) for mgc_recon, lf0, vuv, bap_recon [, lf0_residual]."""
+        """g: dict of grads (B*T, .) for mgc_recon, lf0, vuv, bap_recon [, lf0_residual]
+        [, lf0_sub, lf0_residual_sub (output_subtrack)]."""
         B, E = st["B"], st["E"]
         dev = st["lens_dev"].device
+        dsc = None
         with Branches(dev) as br:  # same branch -> stream assignment as _train_fwd
             with br.on(0):
                 dmain, dsub, _ = self.lf0_model._bwd(st["lf0"], g["lf0"], g.get("lf0_residual"))
+                if st.get("lf0_sub") is not None and (g.get("lf0_sub") is not None or
+                                                      g.get("lf0_residual_sub") is not None):
+                    gs = g.get("lf0_sub")
+                    if gs is None:
+                        gs = torch.zeros(B * st["T"], device=dev)
+                    dsc, _, _ = self.lf0_model._bwd(st["lf0_sub"], gs, g.get("lf0_residual_sub"))
             with br.on(1):
                 dsp_m = self.mgc_model._bwd(st["mgc"], g["mgc_recon"])
             with br.on(2):
@@ -507,8 +525,10 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
                 _, dsp_v = self.vuv_model._bwd(st["vuv"], g["vuv"], want_spk=True)
         # speaker-embedding gradient: the four branch contributions, summed after the join
         ds0 = torch.zeros(B, E, device=dev)
-        for dsp in (dsp_m, dsp_b, dsp_v, dmain):
+        for dsp in (dsp_m, dsp_b, dsp_v, dmain) + ((dsc,) if dsc is not None else ()):
             call("ensvs_axpy", ds0.data_ptr(), dsp.data_ptr(), 1.0, B * E, Ly.stream())
+        if dsc is not None:  # the sub call's fused input holds both speaker vectors too
+            call("ensvs_axpy", dsub.data_ptr(), dsc.data_ptr(), 1.0, B * E, Ly.stream())
         table = grad_of(self.speaker_embedding.emb.weight)
         call("ensvs_spk_scatter", ds0.data_ptr(), B, E, st["i0"].data_ptr(), table.data_ptr(),
              Ly.stream())
@@ -563,13 +583,17 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
             out = self._infer(x_main.contiguous().float(), x_sub.contiguous().float(),
                               spks_list[0], spks_list[1], lengths)
             return out, out
-        if self.output_subtrack:
-            raise NotImplementedError("output_subtrack=True (interaction-loss variant) is the "
-                                      "next step of the build")
         outs = _MultiTrackFn.apply(self, x_main, x_sub, ys[0], spks_list[0], spks_list[1],
                                    lengths, self.speaker_embedding.emb.weight)
-        nm, rm, lf0, vuv, nb, rb, res = outs
-        return ((nm, rm), lf0, vuv, (nb, rb)), res
+        nm, rm, lf0, vuv, nb, rb, res = outs[:7]
+        main = (((nm, rm), lf0, vuv, (nb, rb)), res)
+        if not self.output_subtrack:
+            return main, (None, None)
+        # sub track: ground truth except lf0 (multistream.py:1759-1764)
+        o = self._stream_cols()
+        y1 = ys[1]
+        sub = (y1[..., o[0]:o[1]], outs[7], y1[..., o[2]:o[3]], y1[..., o[3]:o[4]])
+        return main, (sub, outs[8])
 
     def inference(self, x_main, x_sub, spks=None, lengths=None, draws=None):
         """pad_inference_multitrack (acoustic_models/util.py:154-188): replicate-pad to a
@@ -598,16 +622,21 @@ class _MultiTrackFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, mod, x_main, x_sub, y_main, spk0, spk1, lengths, anchor):
         B, T, _ = x_main.shape
+        # _replay_draws (tests only): random draws to replay, as train_step(draws=...)
         outs, st = mod._train_fwd(x_main.contiguous().float(), x_sub.contiguous().float(),
-                                  y_main.contiguous().float(), spk0, spk1, lengths)
+                                  y_main.contiguous().float(), spk0, spk1, lengths,
+                                  getattr(mod, "_replay_draws", None))
         ctx.mod, ctx.st = mod, st
         ctx.mark_non_differentiable(outs["mgc_noise"], outs["bap_noise"])
         v = lambda t: t.view(B, T, -1)  # noqa: E731
-        return (v(outs["mgc_noise"]), v(outs["mgc_recon"]), v(outs["lf0"]), v(outs["vuv"]),
-                v(outs["bap_noise"]), v(outs["bap_recon"]), v(outs["lf0_residual"]))
+        ret = (v(outs["mgc_noise"]), v(outs["mgc_recon"]), v(outs["lf0"]), v(outs["vuv"]),
+               v(outs["bap_noise"]), v(outs["bap_recon"]), v(outs["lf0_residual"]))
+        if "lf0_sub" in outs:
+            ret = ret + (v(outs["lf0_sub"]), v(outs["lf0_residual_sub"]))
+        return ret
 
     @staticmethod
-    def backward(ctx, g_nm, g_rm, g_lf0, g_vuv, g_nb, g_rb, g_res):
+    def backward(ctx, g_nm, g_rm, g_lf0, g_vuv, g_nb, g_rb, g_res, *g_sub):
         st = ctx.st
         B, T = st["B"], st["T"]
         dev = st["lens_dev"].device
@@ -621,6 +650,10 @@ class _MultiTrackFn(torch.autograd.Function):
                  bap_recon=flat(g_rb, g_rb.shape[-1] if g_rb is not None else 5))
         if g_res is not None:
             g["lf0_residual"] = g_res.contiguous().view(-1)
+        if g_sub and g_sub[0] is not None:
+            g["lf0_sub"] = g_sub[0].contiguous().view(-1)
+        if g_sub and g_sub[1] is not None:
+            g["lf0_residual_sub"] = g_sub[1].contiguous().view(-1)
         ctx.mod._train_bwd(st, g)
         ctx.st = None
         return (None,) * 8

@@ -62,7 +62,9 @@ def _diffusion(out_dim, enc, C, L, norm_scale=None):
     return d
 
 
-def multitrack_diffusion(num_speakers=4, tiny=False, vuv_dropout=0.1):
+def multitrack_diffusion(num_speakers=4, tiny=False, vuv_dropout=0.1, output_subtrack=False):
+    """output_subtrack=True: the interaction-loss variant
+    (multitrack_acoustic_nnsvs_world_multi_ar_f0_diff_mgcbap_subtrack.yaml:61)."""
     if tiny:
         E, lf0 = 32, dict(ff=32, conv=16, lstm=8, dec=16)
         mgc_enc = _ffconvlstm(87, 32, 32, 16, 32, E)
@@ -82,6 +84,7 @@ def multitrack_diffusion(num_speakers=4, tiny=False, vuv_dropout=0.1):
         "in_rest_idx": 0, "in_lf0_idx": 51, "out_lf0_idx": 60,
         "vuv_model_bap_conditioning": False, "vuv_model_bap0_conditioning": False,
         "vuv_model_lf0_conditioning": True, "vuv_model_mgc_conditioning": True,
+        "output_subtrack": output_subtrack,
         "lf0_model": {
             "_target_": f"{PKG}.acoustic_models.MultiTrackBiLSTMResF0NonAttentiveDecoder",
             "in_dim": 86, "out_dim": 1, "in_ph_start_idx": 3, "in_ph_end_idx": 50,

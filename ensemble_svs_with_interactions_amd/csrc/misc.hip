@@ -708,3 +708,116 @@ ENSVS_API int ensvs_mul_out(float* out, const float* a, const float* b, long lon
   LAUNCH(mul_out_kernel, n, out, a, b, n);
   return ENSVS_OK;
 }
+
+// ------------------------------------------------- log-F0 interaction loss
+// bin/train_acoustic_multitrack.py:175-182 (logf0_diff_weight > 0, output_subtrack model):
+//   sel(b, t) = t < len_b and vuv_main > 0 and vuv_sub > 0
+//   L = mean_sel |(lf0_m - lf0_s) - (y_lf0_m - y_lf0_s)|,  loss_out += w * L
+//   dL/dlf0_m = gscale * w * sign(.) / N_sel  (accumulated), dL/dlf0_s = - the same (written)
+namespace {
+
+__global__ __launch_bounds__(256) void lf0_int_partial_kernel(
+    const float* __restrict__ pm, const float* __restrict__ ps, const float* __restrict__ ym,
+    const float* __restrict__ ys, int ldy, int lf0_col, int vuv_col,
+    const long long* __restrict__ lengths, int B, int T, float* __restrict__ part) {
+  __shared__ float rs[256], rc[256];
+  float s = 0.f, c = 0.f;
+  GRID_LOOP(m, (long long)B * T) {
+    const int t = (int)(m % T);
+    const long long b = m / T;
+    const float* a = ym + m * ldy;
+    const float* q = ys + m * ldy;
+    if (t < lengths[b] && a[vuv_col] > 0.f && q[vuv_col] > 0.f) {
+      s += fabsf((pm[m] - ps[m]) - (a[lf0_col] - q[lf0_col]));
+      c += 1.f;
+    }
+  }
+  rs[threadIdx.x] = s;
+  rc[threadIdx.x] = c;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) {
+      rs[threadIdx.x] += rs[threadIdx.x + st];
+      rc[threadIdx.x] += rc[threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = rs[0];
+    part[2 * blockIdx.x + 1] = rc[0];
+  }
+}
+
+// one block: loss_out[0] += w * sum / count; coef[0] = gscale * w / count (inf when empty,
+// as the reference's mean over an empty selection)
+__global__ __launch_bounds__(256) void lf0_int_final_kernel(const float* __restrict__ part,
+                                                            int n, float w, float gscale,
+                                                            float* __restrict__ loss_out,
+                                                            float* __restrict__ coef) {
+  __shared__ double rs[256], rc[256];
+  double s = 0.0, c = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    s += part[2 * i];
+    c += part[2 * i + 1];
+  }
+  rs[threadIdx.x] = s;
+  rc[threadIdx.x] = c;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) {
+      rs[threadIdx.x] += rs[threadIdx.x + st];
+      rc[threadIdx.x] += rc[threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float cnt = (float)rc[0];
+    loss_out[0] += w * ((float)rs[0] / cnt);
+    coef[0] = gscale * w / cnt;
+  }
+}
+
+__global__ void lf0_int_grad_kernel(const float* __restrict__ pm, const float* __restrict__ ps,
+                                    const float* __restrict__ ym, const float* __restrict__ ys,
+                                    int ldy, int lf0_col, int vuv_col,
+                                    const long long* __restrict__ lengths, int B, int T,
+                                    const float* __restrict__ coef, float* __restrict__ gm,
+                                    float* __restrict__ gs) {
+  const float k = coef[0];
+  GRID_LOOP(m, (long long)B * T) {
+    const int t = (int)(m % T);
+    const long long b = m / T;
+    const float* a = ym + m * ldy;
+    const float* q = ys + m * ldy;
+    float g = 0.f;
+    if (t < lengths[b] && a[vuv_col] > 0.f && q[vuv_col] > 0.f) {
+      const float d = (pm[m] - ps[m]) - (a[lf0_col] - q[lf0_col]);
+      g = d > 0.f ? k : (d < 0.f ? -k : 0.f);
+    }
+    gm[m] += g;
+    gs[m] = -g;
+  }
+}
+
+}  // namespace
+
+ENSVS_API int ensvs_lf0_interaction(const float* lf0_m, const float* lf0_s, const float* y_m,
+                                    const float* y_s, int ldy, int lf0_col, int vuv_col,
+                                    const long long* lengths, int B, int T, float weight,
+                                    float gscale, float* part, float* loss_out, float* g_m,
+                                    float* g_s, void* stream) {
+  if (B <= 0 || T <= 0 || lf0_col >= ldy || vuv_col >= ldy) return ENSVS_E_SHAPE;
+  const long long M = (long long)B * T;
+  const int blocks = std::min(511, grid_for(M));  // part: 2*blocks partials + 1 coefficient
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(lf0_int_partial_kernel, dim3(blocks), dim3(256), 0, st, lf0_m, lf0_s, y_m,
+                     y_s, ldy, lf0_col, vuv_col, lengths, B, T, part);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(lf0_int_final_kernel, dim3(1), dim3(256), 0, st, part, blocks, weight,
+                     gscale, loss_out, part + 1023);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(lf0_int_grad_kernel, dim3(grid_for(M)), dim3(256), 0, st, lf0_m, lf0_s, y_m,
+                     y_s, ldy, lf0_col, vuv_col, lengths, B, T, part + 1023, g_m, g_s);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}

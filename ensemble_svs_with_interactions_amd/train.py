@@ -2,7 +2,8 @@
 
 ``train_step`` is the reference step with the recipe settings
 (feats_criterion l1, stream_wise_loss False, pitch_reg_weight 0,
-logf0_diff_weight 0, clip_norm 1.0, Adam): forward of the pairwise model,
+logf0_diff_weight 0 -- or > 0 with the output_subtrack model, the interaction-loss
+recipe -- clip_norm 1.0, Adam): forward of the pairwise model,
 masked L1 over all streams divided by the element count, backward, optional
 RCCL gradient all-reduce (data parallel over pairs), global-norm clipping,
 non-finite skip and Adam — every arithmetic op in libensvs.so, no host sync.
@@ -119,10 +120,12 @@ def allreduce_grads(gflat, group=None):
 
 
 def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws=None,
-               ddp=True):
+               ddp=True, y_sub=None, logf0_diff_weight=0.0):
     """One training step on a (main, sub) pair batch.  Returns (loss, grad_norm) device tensors.
 
     lengths = max(L_main, L_sub) per pair (train_acoustic_multitrack.py:82).
+    logf0_diff_weight > 0 adds the log-F0 interaction loss between the main and sub tracks
+    (train_acoustic_multitrack.py:175-182, 296; needs the output_subtrack model and y_sub).
     """
     model.train()
     optimizer.zero_grad()
@@ -138,7 +141,19 @@ def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengt
     W = world_size() if ddp else 1
     loss, (g_m, g_l, g_v, g_b) = masked_l1(preds, targets, st["lens_dev"], sum(st["lens_host"]),
                                            B, T, grad_scale=1.0 / W)
-    model._train_bwd(st, dict(mgc_recon=g_m, lf0=g_l.view(-1), vuv=g_v, bap_recon=g_b))
+    g = dict(mgc_recon=g_m, lf0=g_l.view(-1), vuv=g_v, bap_recon=g_b)
+    if logf0_diff_weight > 0.0:
+        if not model.output_subtrack or y_sub is None:
+            raise ValueError("logf0_diff_weight > 0 needs output_subtrack=True and y_sub")
+        y_sub = y_sub.contiguous().float()
+        g_sub = empty(B * T, device=y_main.device)
+        part = empty(1024, device=y_main.device)
+        call("ensvs_lf0_interaction", outs["lf0"].data_ptr(), outs["lf0_sub"].data_ptr(),
+             y_main.data_ptr(), y_sub.data_ptr(), Dy, o[1], o[2], st["lens_dev"].data_ptr(), B, T,
+             float(logf0_diff_weight), 1.0 / W, part.data_ptr(), loss.data_ptr(),
+             g["lf0"].data_ptr(), g_sub.data_ptr(), Ly.stream())
+        g["lf0_sub"] = g_sub
+    model._train_bwd(st, g)
     if W > 1:
         allreduce_grads(optimizer.gflat)
     optimizer.step()

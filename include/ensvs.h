@@ -161,6 +161,16 @@ int ensvs_masked_l1(const float* const* a, const float* const* b, float* const* 
                     const int* lda, const int* ldb, const int* ldg, const int* n, int ns,
                     const long long* lengths, int B, int T, float invN, float gscale,
                     float* part, float* loss_out, void* stream);
+/* Log-F0 interaction loss between the main and sub tracks of a pair
+ * (bin/train_acoustic_multitrack.py:175-182; output_subtrack model, logf0_diff_weight > 0):
+ * loss_out += weight * mean over {t < len_b, vuv_main > 0, vuv_sub > 0} of
+ * |(lf0_m - lf0_s) - (y_m[lf0_col] - y_s[lf0_col])|; g_m += gscale*weight*sign/N (accumulated
+ * onto the masked-L1 gradient), g_s = -(same).  y_m / y_s: target rows (ldy); part >= 1024
+ * floats.  lf0_m / lf0_s / g_m / g_s: (B*T) contiguous. */
+int ensvs_lf0_interaction(const float* lf0_m, const float* lf0_s, const float* y_m,
+                          const float* y_s, int ldy, int lf0_col, int vuv_col,
+                          const long long* lengths, int B, int T, float weight, float gscale,
+                          float* part, float* loss_out, float* g_m, float* g_s, void* stream);
 /* clip_grad_norm_ + torch.optim.Adam over the flat parameter buffer
  * (bin/train_acoustic_multitrack.py:369-380). */
 int ensvs_l2norm(const float* x, long long n, float* part, float* norm_out, void* stream);

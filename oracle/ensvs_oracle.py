@@ -373,13 +373,15 @@ def gaussian_diffusion_inference(P, prefix, cfg, cond_in, lengths, spk_embs, noi
 # ------------------------------------------------------------- full model
 
 def model_forward(P, cfg, x_main, x_sub, spks, lengths, ys, draws, training=True,
-                  bn_updates=None, fast=False):
+                  bn_updates=None, fast=False, with_sub=False):
     """MultiTrackNPSSMDNMultistreamParametricModel.forward, training branch.
 
     nnsvs/acoustic_models/multistream.py:1594-1757 (output_subtrack=False).
     draws: dict with 'lf0_main'/'lf0_sub' AR dropout masks (B, T/r, 1),
     'mgc_t','mgc_noise','bap_t','bap_noise', 'vuv_lstm' (list of masks or None).
-    Returns ((mgc=(noise,x_recon), lf0, vuv, bap=(noise,x_recon)), lf0_residual).
+    Returns ((mgc=(noise,x_recon), lf0, vuv, bap=(noise,x_recon)), lf0_residual); with
+    ``with_sub`` also the sub-track lf0 prediction, the one output of the sub call that
+    output_subtrack=True returns (:1759-1768, used by the interaction loss).
     """
     lcfg = cfg["lf0_model"]
     for k in ("in_lf0_min", "in_lf0_max", "out_lf0_mean", "out_lf0_scale"):
@@ -394,8 +396,8 @@ def model_forward(P, cfg, x_main, x_sub, spks, lengths, ys, draws, training=True
                                        draws["lf0_main"], training, bn_updates, fast)
     # The sub-track call (:1649-1651) feeds only the (unreturned) sub outputs; it
     # still updates BatchNorm running statistics, so it is run for parity.
-    lf0_model(P, "lf0_model.", lcfg, x_sub, x_main, s1, s0, lengths, draws["lf0_sub"],
-              training, bn_updates, fast)
+    lf0_sub, _ = lf0_model(P, "lf0_model.", lcfg, x_sub, x_main, s1, s0, lengths,
+                           draws["lf0_sub"], training, bn_updates, fast)
     mgc = gaussian_diffusion_forward(P, "mgc_model.", cfg["mgc_model"],
                                      torch.cat([x_main, y_lf0], -1), lengths, y_mgc, s0,
                                      draws["mgc_t"], draws["mgc_noise"], training, bn_updates, fast)
@@ -411,7 +413,21 @@ def model_forward(P, cfg, x_main, x_sub, spks, lengths, ys, draws, training=True
         vuv_in.append(y_bap[:, :, 0:1] if cfg.get("vuv_model_bap0_conditioning") else y_bap)
     vuv = ffconvlstm(P, "vuv_model.", cfg["vuv_model"], torch.cat(vuv_in, -1), lengths, s0,
                      training, bn_updates, draws.get("vuv_lstm"), fast)
+    if with_sub:
+        return ((mgc, lf0_main, vuv, bap), lf0_res_main), lf0_sub
     return (mgc, lf0_main, vuv, bap), lf0_res_main
+
+
+def lf0_interaction_loss(lf0_main, lf0_sub, y_main, y_sub, lengths, stream_sizes):
+    """train_acoustic_multitrack.py:175-182 (criterion l1): mean over non-padded frames
+    voiced in both tracks of |(lf0_main - lf0_sub) - (y_lf0_main - y_lf0_sub)|."""
+    mask = make_non_pad_mask(lengths).unsqueeze(-1)
+    sm = split_streams(y_main, stream_sizes)
+    ss = split_streams(y_sub, stream_sizes)
+    sel = mask & (sm[2] > 0) & (ss[2] > 0)
+    pred = lf0_main - lf0_sub
+    tgt = sm[1] - ss[1]
+    return (pred.masked_select(sel) - tgt.masked_select(sel)).abs().mean()
 
 
 def masked_l1_loss(preds, ys, lengths, stream_sizes):

@@ -308,8 +308,11 @@ def case_model_forward_full():
     return model, shapes
 
 
-def case_train_step_tiny(steps=2, lr=1e-3):
-    cfg = configs.multitrack_diffusion(num_speakers=4, tiny=True)
+def case_train_step_tiny(steps=2, lr=1e-3, logf0_diff_weight=0.0, name="train_step_tiny"):
+    """logf0_diff_weight > 0: the interaction-loss recipe (output_subtrack model,
+    train_acoustic_multitrack.py:175-182, 296)."""
+    il = logf0_diff_weight > 0
+    cfg = configs.multitrack_diffusion(num_speakers=4, tiny=True, output_subtrack=il)
     model, shapes = build_ref(cfg)
     model.vuv_model.lstm.dropout = 0.0
     P, T = 3, 48
@@ -344,11 +347,14 @@ def case_train_step_tiny(steps=2, lr=1e-3):
                     (T_(batch["spk_main"]).int(), T_(batch["spk_sub"]).int()),
                     (T_(batch["lengths"]), T_(batch["lengths"])),
                     None, None, feats_criterion="l1", pitch_reg_weight=0.0,
-                    logf0_diff_weight=0.0, mgc_diff_weight=0.0)
+                    logf0_diff_weight=logf0_diff_weight, mgc_diff_weight=0.0)
         finally:
             torch.nn.utils.clip_grad_norm_ = orig
         losses.append(float(loss))
         norms.append(norm_box["n"])
+        if il:
+            meta.setdefault("interaction_losses", []).append(
+                float(metrics["Loss_LogF0_Interaction"]))
         after = {k: v.detach().clone() for k, v in model.state_dict().items()}
         if s == 0:
             for k in after:
@@ -357,8 +363,8 @@ def case_train_step_tiny(steps=2, lr=1e-3):
     for k, v in model.state_dict().items():
         if v.dtype == torch.float32:
             arrays[f"final::{k}"] = v.numpy()
-    meta.update(losses=losses, grad_norms=norms)
-    save("train_step_tiny", arrays, meta)
+    meta.update(losses=losses, grad_norms=norms, logf0_diff_weight=logf0_diff_weight)
+    save(name, arrays, meta)
 
 
 def case_inference_bap(model):
@@ -551,6 +557,8 @@ def main():
         case_inference_bap(full())
     if run("tiny"):
         case_train_step_tiny()
+    if run("tiny_il"):
+        case_train_step_tiny(logf0_diff_weight=0.5, name="train_step_tiny_il")
     if run("inference_tiny"):
         case_model_inference_tiny()
     if run("data"):

@@ -68,6 +68,7 @@ def _draws(a, pfx, B, T):
     t = lambda k: torch.from_numpy(np.ascontiguousarray(a[pfx + k])).cuda()  # noqa: E731
     return dict(
         lf0_main=t("lf0_main").view(-1).contiguous(),
+        lf0_sub=t("lf0_sub").view(-1).contiguous(),
         mgc_t=t("mgc_t"), bap_t=t("bap_t"),
         mgc_noise=t("mgc_noise")[:, 0].transpose(1, 2).contiguous().view(B * T, -1),
         bap_noise=t("bap_noise")[:, 0].transpose(1, 2).contiguous().view(B * T, -1))
@@ -96,18 +97,25 @@ def test_model_forward_full():
     assert rel(v("vuv"), a["vuv"]) < 1e-4
 
 
-def test_train_step_tiny_matches_reference():
+@pytest.mark.parametrize("case", ["train_step_tiny", "train_step_tiny_il"])
+def test_train_step_tiny_matches_reference(case):
+    """2 fused training steps vs the reference train_step; _il: the interaction-loss recipe
+    (output_subtrack model, logf0_diff_weight 0.5)."""
     engine.set_gemm_precision("fp32")
-    a, meta = load_case("train_step_tiny")
-    model = build(configs.multitrack_diffusion(num_speakers=4, tiny=True), meta["shapes"])
+    a, meta = load_case(case)
+    w_il = meta.get("logf0_diff_weight", 0.0)
+    model = build(configs.multitrack_diffusion(num_speakers=4, tiny=True,
+                                               output_subtrack=w_il > 0), meta["shapes"])
     model.vuv_model.lstm.dropout = 0.0
     opt = FusedAdam(model, lr=meta["lr"])
     xm, xs, ym, s0, s1, lens = _batch(a)
+    ysub = torch.from_numpy(a["y_sub"]).cuda().contiguous()
     B, T = xm.shape[:2]
     p0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
     for s in range(meta["steps"]):
         loss, norm = train_step(model, opt, xm, xs, ym, s0, s1, lens,
-                                draws=_draws(a, f"draw{s}::", B, T))
+                                draws=_draws(a, f"draw{s}::", B, T), y_sub=ysub,
+                                logf0_diff_weight=w_il)
         torch.cuda.synchronize()
         print(f"step {s}: loss {loss.item():.7f} ref {meta['losses'][s]:.7f} | "
               f"norm {norm.item():.6f} ref {meta['grad_norms'][s]:.6f}")
@@ -115,20 +123,31 @@ def test_train_step_tiny_matches_reference():
         assert abs(norm.item() - meta["grad_norms"][s]) < 2e-2 * meta["grad_norms"][s]
         if s == 0:
             bad = []
+            grads = {k: p.grad.detach().cpu() for k, p in model.named_parameters()}
             for k, v in model.state_dict().items():
                 if v.dtype != torch.float32 or "delta0::" + k not in a or _pre_bn_bias(k):
                     continue
                 d = (v - p0[k]).cpu()
                 ref = torch.from_numpy(a["delta0::" + k])
+                err = (d - ref).abs()
+                if k in grads:
+                    # gradient elements at the float noise floor (near-dead ReLU units) move
+                    # Adam by a rounding-sensitive fraction of lr: not compared
+                    g = grads[k].abs()
+                    err = err.masked_fill(g < 1e-7 * (1.0 + g.max()), 0.0)
                 # Adam's first step is ~lr*sign(g): count elements off by > lr/10
-                frac = ((d - ref).abs() > 0.1 * meta["lr"]).float().mean().item()
+                frac = (err > 0.1 * meta["lr"]).float().mean().item()
                 if frac > 0.02:
                     bad.append((k, frac))
             assert not bad, bad[:5]
     sd = model.state_dict()
     for k in sd:
         if "running" in k and "final::" + k in a:
-            assert rel(sd[k].cpu(), a["final::" + k]) < 1e-4, k
+            # running statistics carry the pre-BN conv biases, whose zero-gradient Adam
+            # updates are noise-driven (~lr): absolute tolerance lr/10
+            ref = torch.from_numpy(a["final::" + k])
+            err = (sd[k].cpu() - ref).abs().max().item()
+            assert err < 0.1 * meta["lr"] + 1e-5 * ref.abs().max().item(), k
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])

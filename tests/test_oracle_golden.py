@@ -96,12 +96,22 @@ def test_model_forward_full():
 
 
 def test_train_step_tiny():
-    a, meta = load_case("train_step_tiny")
-    cfg = configs.multitrack_diffusion(num_speakers=4, tiny=True)
+    _train_step_tiny("train_step_tiny")
+
+
+def test_train_step_tiny_interaction_loss():
+    """The interaction-loss recipe: output_subtrack model + logf0_diff_weight 0.5."""
+    _train_step_tiny("train_step_tiny_il")
+
+
+def _train_step_tiny(name):
+    a, meta = load_case(name)
+    w_il = meta.get("logf0_diff_weight", 0.0)
+    cfg = configs.multitrack_diffusion(num_speakers=4, tiny=True, output_subtrack=w_il > 0)
     P = params_from_shapes(meta["shapes"])
     trainable = [k for k in P if "running" not in k and k.rsplit(".", 1)[-1] not in
                  O.diffusion_schedule()]
-    state = {}
+    state, noise = {}, {}
     x = (T_(a["x_main"]), T_(a["x_sub"]))
     y = (T_(a["y_main"]), T_(a["y_sub"]))
     spk = (T_(a["spk_main"]), T_(a["spk_sub"]))
@@ -110,12 +120,23 @@ def test_train_step_tiny():
         for k in trainable:
             P[k] = P[k].detach().requires_grad_()
         upd = {}
-        preds, _ = O.model_forward(P, cfg, x[0], x[1], spk, a["lengths"], y,
-                                   _draws(a, f"draw{s}::"), bn_updates=upd)
+        (preds, _), lf0_sub = O.model_forward(P, cfg, x[0], x[1], spk, a["lengths"], y,
+                                              _draws(a, f"draw{s}::"), bn_updates=upd,
+                                              with_sub=True)
         loss = O.masked_l1_loss(preds, y[0], a["lengths"], cfg["stream_sizes"])
+        if w_il > 0:
+            il = O.lf0_interaction_loss(preds[1], lf0_sub, y[0], y[1], a["lengths"],
+                                        cfg["stream_sizes"])
+            assert abs(il.item() - meta["interaction_losses"][s]) < 1e-5 * abs(il.item())
+            loss = loss + w_il * il
         assert abs(loss.item() - meta["losses"][s]) < 1e-5 * abs(meta["losses"][s])
         loss.backward()
         grads = {k: P[k].grad for k in trainable}
+        # elements whose gradient is at the float noise floor (near-dead ReLU units): Adam
+        # moves them by a rounding-sensitive fraction of lr, so updates are not compared there
+        for k, g in grads.items():
+            nf = g.abs() < 1e-7 * (1.0 + g.abs().max())
+            noise[k] = nf if k not in noise else noise[k] | nf
         params = {k: P[k].detach() for k in trainable}
         norm, ok = O.clip_and_adam(params, grads, state, lr=meta["lr"], step=s + 1)
         assert ok and abs(norm.item() - meta["grad_norms"][s]) < 1e-4 * meta["grad_norms"][s]
@@ -127,11 +148,18 @@ def test_train_step_tiny():
                 d = (P[k] - p0[k]).detach()
                 ref = a["delta0::" + k]
                 # Adam's first step is ~lr*sign(g): compare updates at lr scale
-                assert (d - T_(ref)).abs().max().item() < 2e-2 * meta["lr"], k
+                err = (d - T_(ref)).abs().masked_fill(noise[k], 0.0)
+                assert err.max().item() < 2e-2 * meta["lr"], k
     for k in P:
         if "final::" + k in a and not _pre_bn_bias(k):
-            assert (P[k].detach() - T_(a["final::" + k])).abs().max().item() < 3e-2 * meta["lr"] \
-                + 1e-5 * T_(a["final::" + k]).abs().max().item(), k
+            ref = T_(a["final::" + k])
+            err = (P[k].detach() - ref).abs()
+            if k in noise:
+                err = err.masked_fill(noise[k], 0.0)
+            # running statistics also carry the pre-BN conv biases, whose zero-gradient
+            # updates are noise-driven (skipped above): tolerance lr/10 there
+            tol = (0.1 if "running" in k else 3e-2) * meta["lr"]
+            assert err.max().item() < tol + 1e-5 * ref.abs().max().item(), k
 
 
 def test_inference_bap():

@@ -535,6 +535,107 @@ def case_pd_index():
     save("usfgan_pd_index", arrays, dict(T=T, hop=hop))
 
 
+def case_mdn():
+    """nnsvs/mdn.py on a (G, D, dim_wise) grid (loss without reduction, its input gradients,
+    most-probable selection) and nnsvs.model.MDN with the reference's own fixture weights
+    tests/data/mdn_test.pth (mdn_test.yaml: in 331, hidden 4, out 1, G 1; BASELINE config 1)."""
+    from nnsvs import mdn as ref_mdn
+    from nnsvs.model import MDN as RefMDN
+    r = rng_for("mdn")
+    arrays, meta = {}, {"grid": []}
+    B, T = 2, 23
+    for G, D, dw in ((1, 1, False), (4, 1, False), (4, 3, False), (4, 3, True), (30, 1, False)):
+        key = f"G{G}D{D}{'w' if dw else ''}"
+        raw = r.standard_normal((B, T, G, D) if dw else (B, T, G)).astype(np.float32) * 3
+        lp = TF.log_softmax(T_(raw), dim=2)
+        ls = T_(r.uniform(-8.0, 1.0, (B, T, G, D)).astype(np.float32))  # hits the -7 clamp
+        mu = T_(r.standard_normal((B, T, G, D)).astype(np.float32))
+        tgt = r.standard_normal((B, T, D)).astype(np.float32)
+        tgt[:, ::5] *= 40.0  # far targets: the +-5 sigma clip
+        lp_, ls_, mu_ = (t.clone().requires_grad_() for t in (lp, ls, mu))
+        loss = ref_mdn.mdn_loss(lp_, ls_, mu_, T_(tgt), reduce=False)
+        R = r.standard_normal(tuple(loss.shape)).astype(np.float32)
+        (loss * T_(R)).sum().backward()
+        sig, m = ref_mdn.mdn_get_most_probable_sigma_and_mu(lp, ls, mu)
+        red = ref_mdn.mdn_loss(lp, ls, mu, T_(tgt), reduce=True)
+        for k, v in dict(lp=lp, ls=ls, mu=mu, tgt=tgt, R=R, loss=loss, d_lp=lp_.grad,
+                         d_ls=ls_.grad, d_mu=mu_.grad, sigma=sig, mu_best=m, loss_red=red).items():
+            arrays[f"{key}::{k}"] = v.detach().numpy() if torch.is_tensor(v) else v
+        meta["grid"].append([key, G, D, dw])
+    # BASELINE config 1: the reference's MDN fixture weights
+    ck = torch.load("/root/reference/tests/data/mdn_test.pth", map_location="cpu",
+                    weights_only=True)
+    model = RefMDN(in_dim=331, hidden_dim=4, out_dim=1, num_layers=1, num_gaussians=1)
+    model.load_state_dict(ck["state_dict"])
+    x = r.random((2, 50, 331)).astype(np.float32)
+    y = r.standard_normal((2, 50, 1)).astype(np.float32)
+    lp, ls, mu = model(T_(x))
+    loss = ref_mdn.mdn_loss(lp, ls, mu, T_(y)).mean()
+    loss.backward()
+    for k, v in model.state_dict().items():
+        arrays["mdn_test::" + k] = v.numpy()
+    for k, p in model.named_parameters():
+        arrays["mdn_test::grad::" + k] = p.grad.numpy()
+    with torch.no_grad():
+        mu_i, sig_i = model.inference(T_(x))
+    arrays.update({"mdn_test::x": x, "mdn_test::y": y, "mdn_test::lp": lp.detach().numpy(),
+                   "mdn_test::ls": ls.detach().numpy(), "mdn_test::mu": mu.detach().numpy(),
+                   "mdn_test::loss": loss.detach().numpy(), "mdn_test::inf_mu": mu_i.numpy(),
+                   "mdn_test::inf_sigma": sig_i.numpy()})
+    save("mdn", arrays, meta)
+
+
+def case_vp():
+    """MultiTrackVariancePredictor, the recipe's duration and time-lag models
+    (conf/train/{duration,timelag}/model/multitrack_*_vp_mdn.yaml): eval forward, and a
+    training forward with the nn.Dropout keep masks injected + masked MDN loss + backward."""
+    from nnsvs import mdn as ref_mdn
+    from nnsvs.model import MultiTrackVariancePredictor as RefVP
+    arrays, meta = {}, {}
+    for name, hid, nl, k in (("duration", 256, 5, 5), ("timelag", 32, 3, 3)):
+        cfg = dict(in_dim=82, out_dim=1, hidden_dim=hid, num_layers=nl, kernel_size=k,
+                   dropout=0.5, use_mdn=True, num_gaussians=4, init_type="kaiming_normal",
+                   num_speaker=3, spk_embed_dim=16)
+        torch.manual_seed(0)
+        model = RefVP(**cfg)
+        shapes = {kk: tuple(v.shape) for kk, v in model.state_dict().items()}
+        model.load_state_dict({kk: torch.from_numpy(v) for kk, v in
+                               seeded_state_dict(shapes, SEED).items()})
+        r = rng_for("vp_" + name)
+        B, T = 2, 37
+        x = r.random((B, T, 164)).astype(np.float32)
+        s0 = r.integers(0, 3, size=(B, 1)).astype(np.int64)
+        s1 = r.integers(0, 3, size=(B, 1)).astype(np.int64)
+        y = r.standard_normal((B, T, 1)).astype(np.float32)
+        lengths = np.array([37, 30], dtype=np.int64)
+        model.eval()
+        with torch.no_grad():
+            ev = model(T_(x), (T_(s0), T_(s1)))
+            inf_mu, inf_sig = model.inference(T_(x), (T_(s0), T_(s1)))
+        model.train()
+        masks = [(r.random((B, hid, T)) > 0.5).astype(np.float32) * 2.0 for _ in range(nl)]
+        for i, blk in enumerate(model.conv):
+            blk[3].forward = (lambda m: (lambda t: t * m))(T_(masks[i]))
+        lp, ls, mu = model(T_(x), (T_(s0), T_(s1)))
+        mask = torch.arange(T)[None, :] < T_(lengths)[:, None]
+        loss = ref_mdn.mdn_loss(lp, ls, mu, T_(y), reduce=False).masked_select(mask).mean()
+        model.zero_grad()
+        loss.backward()
+        p = name + "::"
+        arrays.update({p + "x": x, p + "s0": s0, p + "s1": s1, p + "y": y, p + "lengths": lengths,
+                       p + "eval_lp": ev[0].numpy(), p + "eval_ls": ev[1].numpy(),
+                       p + "eval_mu": ev[2].numpy(), p + "inf_mu": inf_mu.numpy(),
+                       p + "inf_sigma": inf_sig.numpy(), p + "loss": loss.detach().numpy()})
+        for i, m in enumerate(masks):
+            arrays[p + f"mask{i}"] = m
+        for kk, prm in model.named_parameters():
+            if prm.numel() <= 20000:  # large conv weights: summary only (fixture size)
+                arrays[p + "grad::" + kk] = prm.grad.numpy()
+        meta[name] = dict(cfg=cfg, shapes={kk: list(v) for kk, v in shapes.items()},
+                          grad_summary=grad_summary(model))
+    save("variance_predictor", arrays, meta)
+
+
 def main():
     which = sys.argv[1:] or ["all"]
     run = lambda n: "all" in which or n in which  # noqa: E731
@@ -567,6 +668,10 @@ def main():
         case_usfgan()
     if run("pd_index"):
         case_pd_index()
+    if run("mdn"):
+        case_mdn()
+    if run("vp"):
+        case_vp()
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(dict(seed=SEED, torch=torch.__version__, numpy=np.__version__,
                        reference="sarulab-speech/ensemble_svs_with_interactions @ 2025-03-21",

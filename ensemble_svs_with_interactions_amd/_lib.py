@@ -108,6 +108,15 @@ SIGNATURES = {
     "ensvs_usf_source": [c_vp, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp,
                          c_vp, c_vp, c_vp, c_int, c_vp],
     "ensvs_usf_mix": [c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_vp],
+    "ensvs_mdn_log_softmax": [c_vp, c_ll, c_int, c_int, c_int, c_vp],
+    "ensvs_mdn_log_softmax_bwd": [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_vp],
+    "ensvs_mdn_loss": [c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_int, c_int, c_int, c_float,
+                       c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ensvs_mdn_most_probable": [c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp],
+    "ensvs_layer_norm_fwd": [c_vp, c_int, c_ll, c_int, c_vp, c_vp, c_float, c_vp, c_int, c_vp,
+                             c_vp, c_vp],
+    "ensvs_layer_norm_bwd": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp,
+                             c_int, c_vp, c_vp],
 }
 
 # entry points returning a value instead of a status code

@@ -26,7 +26,19 @@ REFERENCE_TARGETS = {
     # reference vendors the same class under nnsvs.usfgan (generator.py:359)
     f"{PKG}.usfgan.ParallelHnUSFGANGenerator":
         "nnsvs.usfgan.models.generator.ParallelHnUSFGANGenerator",
+    f"{PKG}.timing.MultiTrackVariancePredictor": "nnsvs.model.MultiTrackVariancePredictor",
+    f"{PKG}.timing.MDN": "nnsvs.model.MDN",
 }
+
+
+def multitrack_timing(which="duration", num_speaker=3):
+    """recipes/jaCappella_ritsu/dev-48k-world-multitrack/conf/train/{duration,timelag}/model/
+    multitrack_{duration,timelag}_vp_mdn.yaml (netG)."""
+    hid, nl, k = (256, 5, 5) if which == "duration" else (32, 3, 3)
+    return {"_target_": f"{PKG}.timing.MultiTrackVariancePredictor", "in_dim": 82, "out_dim": 1,
+            "hidden_dim": hid, "num_layers": nl, "kernel_size": k, "dropout": 0.5,
+            "use_mdn": True, "num_gaussians": 4, "init_type": "kaiming_normal",
+            "num_speaker": num_speaker, "spk_embed_dim": 16}
 
 # Scaler-derived constants that check_resf0_config (nnsvs/train_util.py:1668-1770)
 # injects in a real run; fixed here for synthetic data.

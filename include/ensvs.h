@@ -223,6 +223,37 @@ int ensvs_usf_source(const float* f0, int B, int T, int hop, float scale, float 
 int ensvs_usf_mix(const float* a, float* h, float* n, float* s, long long total, int keep,
                   void* stream);
 
+/* ---- timing models (duration / time-lag) -------------------------------- */
+
+/* MDN head (nnsvs/mdn.py).  Per item = frame (or frame x output dim when dim_wise), the G
+ * mixture components live in one lane group of the wavefront (xor-shuffle reductions).
+ * Layouts: log_pi [M][G] (dim_wise: [M][G][D]), log_sigma / mu [M][G][D], target [M][ldt].
+ * G <= 64. */
+/* log_softmax over the mixture, in place (MDNLayer.forward, mdn.py:62-70) and its backward
+ * (g <- g - exp(y) * sum(g), in place). */
+int ensvs_mdn_log_softmax(float* lp, long long M, int G, int D, int dim_wise, void* stream);
+int ensvs_mdn_log_softmax_bwd(const float* y, float* g, long long M, int G, int D, int dim_wise,
+                              void* stream);
+/* mdn_loss(reduce=False) (mdn.py:78-154) -> loss [items]; with gloss != NULL also the
+ * gradients of sum(gloss * loss) w.r.t. log_pi, log_sigma, mu (written). */
+int ensvs_mdn_loss(const float* lp, const float* ls, const float* mu, const float* tgt, int ldt,
+                   long long M, int G, int D, int dim_wise, float lp_min, float ls_min,
+                   float* loss, const float* gloss, float* dlp, float* dls, float* dmu,
+                   void* stream);
+/* mdn_get_most_probable_sigma_and_mu (mdn.py:167-212): sigma, mu_out [M][D]. */
+int ensvs_mdn_most_probable(const float* lp, const float* ls, const float* mu, long long M,
+                            int G, int D, int dim_wise, float* sigma, float* mu_out,
+                            void* stream);
+/* Channel LayerNorm of the VariancePredictor conv stack (nnsvs/layers/layer_norm.py:10-35,
+ * model.py:1256; eps 1e-12), one wavefront per frame row; saves mean / rstd per row.  The
+ * backward writes dx and dy*xhat [M][C] (column sums: the gamma gradient). */
+int ensvs_layer_norm_fwd(const float* x, int ldx, long long M, int C, const float* gamma,
+                         const float* beta, float eps, float* y, int ldy, float* mean,
+                         float* rstd, void* stream);
+int ensvs_layer_norm_bwd(const float* dy, int lddy, const float* x, int ldx, long long M, int C,
+                         const float* gamma, const float* mean, const float* rstd, float* dx,
+                         int lddx, float* dyxhat, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

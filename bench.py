@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from ensemble_svs_with_interactions_amd import configs, data, engine  # noqa: E402
-from ensemble_svs_with_interactions_amd.train import FusedAdam, train_step  # noqa: E402
+from ensemble_svs_with_interactions_amd.train import FusedAdam, GraphedTrainStep, train_step  # noqa: E402,E501
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 TRAIN_FLOP_PER_FRAME = 127.5e6  # SURVEY.md §6 (torch.utils.flop_counter on the oracle)
@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--no-synth", action="store_true", help="skip the synthesis RTF leg")
     ap.add_argument("--serial", action="store_true",
                     help="run the lf0/mgc/bap/vuv branches serially (no side streams)")
+    ap.add_argument("--eager", action="store_true",
+                    help="issue every kernel from the host each step (no HIP graph replay)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
 
@@ -211,8 +213,17 @@ def main():
     xm, xs, ym = g("x_main"), g("x_sub"), g("y_main")
     s0, s1 = g("spk_main"), g("spk_sub")
     lens = b["lengths"].tolist()
-    for _ in range(args.warmup):
-        loss, norm = train_step(model, opt, xm, xs, ym, s0, s1, lens)
+    if args.eager:
+        def step():
+            return train_step(model, opt, xm, xs, ym, s0, s1, lens)
+        for _ in range(args.warmup):
+            step()
+    else:
+        # one eager warm-up step, capture, then replays: every step is a full training step
+        graphed = GraphedTrainStep(model, opt, xm, xs, ym, s0, s1, lens, warmup=1)
+        step = graphed.step
+        for _ in range(max(0, args.warmup - 1)):
+            step()
     torch.cuda.synchronize()
 
     def barrier():
@@ -223,7 +234,7 @@ def main():
     barrier()
     t0 = time.time()
     for _ in range(args.steps):
-        loss, norm = train_step(model, opt, xm, xs, ym, s0, s1, lens)
+        loss, norm = step()
     barrier()
     elapsed = time.time() - t0
     if world > 1:
@@ -251,7 +262,8 @@ def main():
         "config": {"workload": "4-track SATB ensemble, MultiTrackNPSSMDNMultistreamParametric"
                                "Model (multitrack_acoustic_nnsvs_world_multi_ar_f0_diff_mgcbap)",
                    "pairs_per_gpu": P, "frames_per_pair": T, "global_batch_pairs": P * world,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "execution": "eager" if args.eager else "hip-graph replay"},
         "train_loss": loss_v, "grad_norm": norm_v,
         "model_tflops_per_s": value * TRAIN_FLOP_PER_FRAME / 1e12,
         "roofline": {"kernel": "conv_gemm_kernel<bf16> (mgc DiffNet block gate GEMM, "

@@ -91,6 +91,9 @@ SIGNATURES = {
     "ensvs_l2norm": [c_vp, c_ll, c_vp, c_vp, c_vp],
     "ensvs_adam": [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_float, c_float, c_float, c_float, c_float,
                    c_float, c_float, c_vp],
+    "ensvs_adam_step": [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_float, c_double, c_double, c_float,
+                        c_vp, c_vp],
+    "ensvs_rng_advance": [c_vp],
     "ensvs_copy_cols": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_vp],
     "ensvs_axpy": [c_vp, c_vp, c_float, c_ll, c_vp],
     "ensvs_axpby": [c_vp, c_float, c_vp, c_float, c_ll, c_vp],

@@ -389,14 +389,17 @@ __global__ void norm_final_kernel(const float* __restrict__ part, int n, float* 
 
 // clip_grad_norm_(max_norm) then torch.optim.Adam (weight_decay 0, amsgrad off);
 // skipped entirely when the norm is not finite (train_acoustic_multitrack.py:369-380).
+// `st` (device-side optimizer state, see adam_prepare_kernel) replaces the host scalars
+// lr / bc1 and sqrt_bc2 when given, so the update can be replayed from a HIP graph.
 __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, long long n, const float* __restrict__ norm,
                             float max_norm, float lr, float b1, float b2, float eps, float bc1,
-                            float sqrt_bc2) {
+                            float sqrt_bc2, const double* __restrict__ st) {
   const float nv = norm[0];
   if (!isfinite(nv)) return;
   const float coef = fminf(max_norm / (nv + 1e-6f), 1.f);
-  const float step = lr / bc1;
+  const float step = st ? (float)st[1] : lr / bc1;
+  if (st) sqrt_bc2 = (float)st[2];
   GRID_LOOP(i, n) {
     const float gi = g[i] * coef;
     g[i] = gi;
@@ -407,6 +410,19 @@ __global__ void adam_kernel(float* __restrict__ p, float* __restrict__ g, float*
     const float denom = sqrtf(vi) / sqrt_bc2 + eps;
     p[i] = p[i] - step * (mi / denom);
   }
+}
+
+// Device-side Adam step counter: st = {step, lr / (1 - b1^step), sqrt(1 - b2^step), lr}.
+// The step only advances when the gradient norm is finite, like torch.optim.Adam whose
+// step() the reference skips on a non-finite norm (train_acoustic_multitrack.py:365-380);
+// the bias corrections are the reference's double-precision Python scalars.
+__global__ void adam_prepare_kernel(const float* __restrict__ norm, double* __restrict__ st,
+                                    double b1, double b2) {
+  if (threadIdx.x != 0 || !isfinite(norm[0])) return;
+  const double c = st[0] + 1.0;
+  st[0] = c;
+  st[1] = st[3] / (1.0 - pow(b1, c));
+  st[2] = sqrt(1.0 - pow(b2, c));
 }
 
 __global__ void copy_cols_kernel(const float* __restrict__ src, int lds, float* __restrict__ dst,
@@ -465,11 +481,23 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
+// Replay epoch of the RNG kernels: 0 (the eager default) leaves every seed as given; a
+// captured training step advances it once per replay so each replay draws fresh numbers.
+__device__ unsigned long long g_rng_epoch = 0ull;
+__device__ __forceinline__ unsigned long long epoch_seed(unsigned long long seed) {
+  const unsigned long long e = g_rng_epoch;
+  return e ? seed ^ mix64(e * 0xD1B54A32D192ED03ull) : seed;
+}
 __device__ __forceinline__ float u01(unsigned long long r) {  // (0, 1]
   return ((float)(r >> 40) + 1.f) * (1.f / 16777216.f);
 }
 
+__global__ void rng_advance_kernel() {
+  if (threadIdx.x == 0) g_rng_epoch += 1ull;
+}
+
 __global__ void randn_kernel(float* __restrict__ out, long long n, unsigned long long seed) {
+  seed = epoch_seed(seed);
   GRID_LOOP(i, n) {
     const unsigned long long r = mix64(seed ^ mix64((unsigned long long)i));
     const float u1 = u01(r), u2 = u01(r << 24 | r >> 40);
@@ -480,6 +508,7 @@ __global__ void randn_kernel(float* __restrict__ out, long long n, unsigned long
 __global__ void dropout_mask_kernel(float* __restrict__ out, long long n, float p,
                                     unsigned long long seed) {
   const float keep = 1.f / (1.f - p);
+  seed = epoch_seed(seed);
   GRID_LOOP(i, n) {
     const unsigned long long r = mix64(seed ^ mix64((unsigned long long)i));
     out[i] = u01(r) > p ? keep : 0.f;
@@ -488,6 +517,7 @@ __global__ void dropout_mask_kernel(float* __restrict__ out, long long n, float 
 
 __global__ void randint_kernel(long long* __restrict__ out, long long n, long long hi,
                                unsigned long long seed) {
+  seed = epoch_seed(seed);
   GRID_LOOP(i, n) {
     const unsigned long long r = mix64(seed ^ mix64((unsigned long long)i));
     out[i] = (long long)((r >> 11) % (unsigned long long)hi);
@@ -649,7 +679,26 @@ ENSVS_API int ensvs_l2norm(const float* x, long long n, float* part, float* norm
 ENSVS_API int ensvs_adam(float* p, float* g, float* m, float* v, long long n, const float* norm,
                          float max_norm, float lr, float b1, float b2, float eps, float bc1,
                          float sqrt_bc2, void* stream) {
-  LAUNCH(adam_kernel, n, p, g, m, v, n, norm, max_norm, lr, b1, b2, eps, bc1, sqrt_bc2);
+  LAUNCH(adam_kernel, n, p, g, m, v, n, norm, max_norm, lr, b1, b2, eps, bc1, sqrt_bc2,
+         (const double*)nullptr);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_adam_step(float* p, float* g, float* m, float* v, long long n,
+                              const float* norm, float max_norm, double b1, double b2, float eps,
+                              double* state, void* stream) {
+  if (!state) return ENSVS_E_ARG;
+  hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, norm, state,
+                     b1, b2);
+  ENSVS_CHECK_LAUNCH();
+  LAUNCH(adam_kernel, n, p, g, m, v, n, norm, max_norm, 0.f, (float)b1, (float)b2, eps, 1.f, 1.f,
+         (const double*)state);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_rng_advance(void* stream) {
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream);
+  ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
 

@@ -253,5 +253,14 @@ def lengths_pair(lengths, B, T, device):
         host = [int(v) for v in lengths.detach().cpu().tolist()]
     else:
         host = [int(v) for v in lengths]
-    dev = torch.tensor(host, dtype=torch.int64, device=device)
+    # cached: one upload per distinct lengths vector, none inside a captured step
+    key = (tuple(host), str(torch.device(device)))
+    dev = _LENGTHS.get(key)
+    if dev is None:
+        if len(_LENGTHS) >= 256:
+            _LENGTHS.clear()
+        dev = _LENGTHS[key] = torch.tensor(host, dtype=torch.int64, device=device)
     return host, dev
+
+
+_LENGTHS = {}

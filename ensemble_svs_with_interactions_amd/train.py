@@ -9,7 +9,6 @@ RCCL gradient all-reduce (data parallel over pairs), global-norm clipping,
 non-finite skip and Adam — every arithmetic op in libensvs.so, no host sync.
 """
 import ctypes
-import math
 
 import torch
 
@@ -23,7 +22,9 @@ class FusedAdam:
 
     Same update as torch.optim.Adam(weight_decay=0, amsgrad=False) after
     torch.nn.utils.clip_grad_norm_; the step is skipped when the norm is not
-    finite (train_acoustic_multitrack.py:369-380).
+    finite (train_acoustic_multitrack.py:369-380).  The step counter and the bias
+    corrections live on the device (ensvs_adam_step), so a skipped step does not
+    advance the counter and the update replays correctly from a HIP graph.
     """
 
     def __init__(self, model, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
@@ -36,10 +37,28 @@ class FusedAdam:
         self.flat, self.gflat = model._ensvs_flat
         self.m = torch.zeros_like(self.flat)
         self.v = torch.zeros_like(self.flat)
-        self.lr, self.betas, self.eps, self.clip_norm = lr, betas, eps, clip_norm
-        self.step_count = 0
+        self.betas, self.eps, self.clip_norm = betas, eps, clip_norm
+        self.step_count = 0  # host count of step() calls (skipped steps included)
+        # {device step, lr / bc1, sqrt(bc2), lr}
+        self.state = torch.zeros(4, dtype=torch.float64, device=self.flat.device)
+        self.lr = lr
         self.norm = torch.zeros(1, device=self.flat.device)
         self._part = torch.empty(1024, device=self.flat.device)
+
+    @property
+    def lr(self):
+        return self._lr
+
+    @lr.setter
+    def lr(self, value):
+        """Takes effect from the next step, eager or replayed."""
+        self._lr = float(value)
+        self.state[3].fill_(self._lr)
+
+    @property
+    def device_step(self):
+        """Number of applied (finite-norm) updates, read from the device."""
+        return int(self.state[0].item())
 
     def zero_grad(self):
         self.gflat.zero_()
@@ -56,12 +75,9 @@ class FusedAdam:
         self.step_count += 1
         b1, b2 = self.betas
         self.grad_norm()
-        bc1 = 1.0 - b1 ** self.step_count
-        bc2 = 1.0 - b2 ** self.step_count
-        call("ensvs_adam", self.flat.data_ptr(), self.gflat.data_ptr(), self.m.data_ptr(),
+        call("ensvs_adam_step", self.flat.data_ptr(), self.gflat.data_ptr(), self.m.data_ptr(),
              self.v.data_ptr(), self.flat.numel(), self.norm.data_ptr(), float(self.clip_norm),
-             float(self.lr), float(b1), float(b2), float(self.eps), float(bc1),
-             float(math.sqrt(bc2)), Ly.stream())
+             float(b1), float(b2), float(self.eps), self.state.data_ptr(), Ly.stream())
         weights_updated()
 
 
@@ -127,6 +143,17 @@ def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengt
     logf0_diff_weight > 0 adds the log-F0 interaction loss between the main and sub tracks
     (train_acoustic_multitrack.py:175-182, 296; needs the output_subtrack model and y_sub).
     """
+    loss = _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
+                           draws, ddp, y_sub, logf0_diff_weight)
+    if ddp and world_size() > 1:
+        allreduce_grads(optimizer.gflat)
+    optimizer.step()
+    return loss, optimizer.norm
+
+
+def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws,
+                    ddp, y_sub, logf0_diff_weight):
+    """zero_grad + forward + masked L1 (+ interaction loss) + backward into the flat grads."""
     model.train()
     optimizer.zero_grad()
     outs, st = model._train_fwd(x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws)
@@ -154,7 +181,81 @@ def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengt
              g["lf0"].data_ptr(), g_sub.data_ptr(), Ly.stream())
         g["lf0_sub"] = g_sub
     model._train_bwd(st, g)
-    if W > 1:
-        allreduce_grads(optimizer.gflat)
-    optimizer.step()
-    return loss, optimizer.norm
+    return loss
+
+
+class GraphedTrainStep:
+    """``train_step`` on fixed shapes, captured as HIP graphs and replayed.
+
+    Capture records every launch of one step: graph 1 = RNG epoch advance, zero_grad,
+    forward, loss, backward; graph 2 = grad-norm, clip and Adam.  Between them the RCCL
+    gradient all-reduce runs eagerly when the process group has more than one rank (one
+    collective on the flat gradient buffer), so data-parallel runs never depend on
+    collective capture.  Each replay draws fresh diffusion steps, noise and dropout masks
+    (ensvs_rng_advance) and takes the Adam step count and bias corrections from the
+    device (FusedAdam.state), so replay k is the k-th training step, not a repeat.
+
+    ``warmup`` eager steps (real optimizer steps) run first on the capture stream so
+    every lazily built cache (packed-weight descriptors, workspaces, lengths) exists
+    before capture.  Inputs are copied into static buffers: call ``step(**batch)`` with
+    new tensors of the captured shapes, or ``step()`` to retrain on the same batch.
+    """
+
+    def __init__(self, model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
+                 warmup=1, ddp=True, y_sub=None, logf0_diff_weight=0.0, draws=None):
+        self.model, self.opt, self.ddp = model, optimizer, ddp
+        # explicit draws (train_step's `draws`) become static buffers refilled per step
+        self.draws = None if draws is None else {k: v.clone() for k, v in draws.items()}
+        self.lengths = [int(v) for v in lengths]
+        self.kw = dict(y_sub=None if y_sub is None else y_sub.clone(),
+                       logf0_diff_weight=logf0_diff_weight)
+        self.inputs = dict(x_main=x_main.clone(), x_sub=x_sub.clone(), y_main=y_main.clone(),
+                           spk_main=spk_main.clone(), spk_sub=spk_sub.clone())
+        dev = x_main.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                loss = self._eager()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        self.warmup_result = (loss, optimizer.norm.clone())
+        self.g_grads, self.g_update = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_grads):
+            call("ensvs_rng_advance", Ly.stream())
+            self.loss = self._grads()
+        with torch.cuda.graph(self.g_update, pool=self.g_grads.pool()):
+            optimizer.step()
+        self.norm = optimizer.norm
+
+    def _grads(self):
+        i = self.inputs
+        return _loss_and_grads(self.model, self.opt, i["x_main"], i["x_sub"], i["y_main"],
+                               i["spk_main"], i["spk_sub"], self.lengths, self.draws, self.ddp,
+                               self.kw["y_sub"], self.kw["logf0_diff_weight"])
+
+    def _eager(self):
+        loss = self._grads()
+        if self.ddp and world_size() > 1:
+            allreduce_grads(self.opt.gflat)
+        self.opt.step()
+        return loss
+
+    def step(self, draws=None, **batch):
+        """One training step (replay).  Returns the static (loss, grad_norm) tensors."""
+        for k, v in (draws or {}).items():
+            if self.draws is None or self.draws[k].shape != v.shape:
+                raise ValueError(f"draws[{k}]: not captured with this shape")
+            self.draws[k].copy_(v, non_blocking=True)
+        for k, v in batch.items():
+            dst = self.kw["y_sub"] if k == "y_sub" else self.inputs[k]
+            if dst is None or dst.shape != v.shape:
+                raise ValueError(f"{k}: shape {tuple(v.shape)} differs from the captured one")
+            dst.copy_(v, non_blocking=True)
+        self.g_grads.replay()
+        if self.ddp and world_size() > 1:
+            allreduce_grads(self.opt.gflat)
+        self.g_update.replay()
+        self.opt.step_count += 1
+        weights_updated()
+        return self.loss, self.norm

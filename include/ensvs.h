@@ -177,6 +177,15 @@ int ensvs_l2norm(const float* x, long long n, float* part, float* norm_out, void
 int ensvs_adam(float* p, float* g, float* m, float* v, long long n, const float* norm,
                float max_norm, float lr, float b1, float b2, float eps, float bc1,
                float sqrt_bc2, void* stream);
+/* Graph-replayable clip + Adam: state = {step, lr / (1 - b1^step), sqrt(1 - b2^step), lr}
+   (4 doubles on the device; the host sets state[3] = lr).  The step advances on the
+   device only when *norm is finite (train_acoustic_multitrack.py:365-380 skips
+   optimizer.step()); replaces the torch.optim.Adam step of train_acoustic_multitrack.py:382. */
+int ensvs_adam_step(float* p, float* g, float* m, float* v, long long n, const float* norm,
+                    float max_norm, double b1, double b2, float eps, double* state, void* stream);
+/* Advance the RNG replay epoch (randn / randint / dropout masks): a captured step calls it
+   first so every replay draws fresh numbers; epoch 0 (eager) leaves seeds unchanged. */
+int ensvs_rng_advance(void* stream);
 int ensvs_copy_cols(const float* src, int lds, float* dst, int ldd, long long M, int n,
                     void* stream);
 int ensvs_axpy(float* y, const float* x, float a, long long n, void* stream);

@@ -7,13 +7,20 @@
 // MFMA GEMM beforehand (gemm.hip); only h_{t-1} W_hh^T stays in the loop.
 //
 // One workgroup per (sequence, direction) runs every step of its sequence
-// (persistent), holding its W_hh slice in VGPRs:
-//   thread (u, q), u = unit (16 per wave, lane & 15), q = lane >> 4 (K quarter)
-//   fwd: w[g][k] = W_hh[g*H + u][q*H/4 + k], g in {i,f,g,o}
-//   bwd: w[g][k] = W_hh[q*H + ?]... (transposed: column u of gate block q)
-// The four K-quarter partial sums are combined with cross-lane xor shuffles,
-// h (fwd) / dG (bwd) is exchanged through a double-buffered LDS vector: one
-// __syncthreads per time step.
+// (persistent), holding its W_hh slice in VGPRs.  KP lanes (4 or 8, adjacent lanes of
+// one quad / half-row) share a unit u and split its dot products:
+//   fwd: lane q holds w[g][k] = W_hh[g*H + u][q*H/KP + k] (the 4 gates, K-part q);
+//   bwd: lane q holds w[j]    = W_hh[q*4H/KP + j][u]     (column u, part q of 4H).
+// Partial sums are combined with DPP (row_half_mirror, quad_perm xor 1 / xor 2) in
+// registers, so every lane of the unit ends with the same bits.  In the forward step
+// lane q evaluates only gate q&3 (tanh(x) = 2 sigmoid(2x) - 1 for g) and the four
+// activations are exchanged by quad broadcasts.
+//
+// Global memory stays off the per-step critical path: inputs are staged through LDS in
+// chunks of CH steps (loaded to registers one chunk ahead), outputs are collected in
+// LDS and written back at the chunk boundary.  (vmcnt counts loads and stores in issue
+// order, so a per-step prefetch would wait on the previous step's stores.)  h (fwd) /
+// dG (bwd) is exchanged through a double-buffered LDS vector: one barrier per step.
 //
 // Packed semantics: sequence b has length L_b; the forward direction runs
 // t = 0..L_b-1, the reverse direction t = L_b-1..0 from a zero state, and
@@ -23,11 +30,64 @@
 
 namespace {
 
-// 16 units per wave (lane & 15), 4 K-parts (lane >> 4); H < 16 pads idle units.
+// Lanes per unit (KPF forward, KPB backward; measured on MI355X at 30 x 1024 frames):
+// the forward H=128 step is FMA-issue bound and prefers 512 threads, the backward one
+// is bound by its dependent dot-product chain and prefers 1024.
 template <int H> struct Geo {
-  static constexpr int WAVES = H >= 16 ? H / 16 : 1;
-  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int KPF = H == 64 ? 8 : 4, KPB = H >= 64 ? 8 : 4;
+  static constexpr int TF = H * KPF, TB = H * KPB;  // threads
+  static constexpr int Q = H / KPF;                 // fwd: h elements per lane
+  static constexpr int QB = 4 * H / KPB;            // bwd: dG elements per lane
+  // steps per staged chunk (bwd H=128: 8, keeping its prefetch within 128 VGPRs)
+  static constexpr int CHF = 16, CHB = H >= 128 ? 8 : 16;
+  // The exchanged vectors (h: KPF parts of Q, dG: KPB parts of QB) are stored with a
+  // 16-B pad after each part, so the distinct addresses one wave reads per
+  // ds_read_b128 fall in distinct banks.
+  static constexpr int HP = Q + 4, GP = QB + 4;
+  static constexpr int HBUF = KPF * HP, GBUF = KPB * GP;
+  // LDS bytes: fwd h[2] + in[CH][4H] + out[CH][6H]; bwd dG[2] + in[CH][7H] + out[CH][4H]
+  static constexpr int FWD_LDS = (2 * HBUF + CHF * 4 * H + CHF * 6 * H) * 4;
+  static constexpr int BWD_LDS = (2 * GBUF + CHB * 7 * H + CHB * 4 * H) * 4;
 };
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL,
+                                                            0xF, 0xF, false));
+}
+// sum over the KP lanes of a unit; identical bits in all of them
+template <int KP>
+__device__ __forceinline__ float unit_sum(float v) {
+  if constexpr (KP == 8) v += dpp<0x141>(v);  // row_half_mirror: lane i + lane 7-i
+  v += dpp<0xB1>(v);                          // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);                          // quad_perm [2,3,0,1]
+  return v;
+}
+
+// Recurrence nonlinearities on v_exp / v_rcp (absolute error ~1e-7; the IEEE division
+// and the branchy libm tanhf would sit on the per-step dependency chain).
+__device__ __forceinline__ float sigm(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
+__device__ __forceinline__ float tanh_fast(float x) {
+  return fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)), 1.f);
+}
+// one of four values by a lane index, with bit selects (no exec-mask branches)
+__device__ __forceinline__ float pick4(const float (&v)[4], int i) {
+  const unsigned m0 = i == 0 ? ~0u : 0u, m1 = i == 1 ? ~0u : 0u, m2 = i == 2 ? ~0u : 0u,
+                 m3 = i == 3 ? ~0u : 0u;
+  return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, v[0]) & m0) |
+                                       (__builtin_bit_cast(unsigned, v[1]) & m1) |
+                                       (__builtin_bit_cast(unsigned, v[2]) & m2) |
+                                       (__builtin_bit_cast(unsigned, v[3]) & m3));
+}
+// Make the waitcnt pass retire a register's load here (before the step loop) instead
+// of with a conservative vmcnt(0) inside it, which would also drain the chunk prefetch.
+template <int N>
+__device__ __forceinline__ void settle(const float (&v)[N]) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) asm volatile("" ::"v"(v[k]));
+}
 
 template <int N>
 __device__ __forceinline__ void load_row(float (&dst)[N], const float* src) {
@@ -44,147 +104,220 @@ __device__ __forceinline__ void load_row(float (&dst)[N], const float* src) {
 }
 
 template <int H>
-__global__ __launch_bounds__(Geo<H>::THREADS) void lstm_fwd_kernel(
+__global__ __launch_bounds__(Geo<H>::TF) void lstm_fwd_kernel(
     const float* __restrict__ gx, int ldg,        // [B*T][ldg], dir d gates at cols d*4H + g*H + u
     const float* __restrict__ whh0, const float* __restrict__ whh1,  // [4H][H] per direction
     const long long* __restrict__ lengths, int T,
     float* __restrict__ y, int ldy,               // [B*T][ldy], dir d at cols d*H + u
     float* __restrict__ sv) {                     // saved [B*T][2][5H]: i,f,g,o,c
-  constexpr int Q = H / 4;
-  __shared__ __attribute__((aligned(16))) float hbuf[2][H];
+  using G = Geo<H>;
+  constexpr int KP = G::KPF, Q = G::Q, NT = G::TF, GW = 4 * H, OW = 6 * H, CH = G::CHF;
+  constexpr int PF = CH * GW / 4 / NT;  // float4 of one input chunk per thread (= CH / KP)
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* hbuf = lds;              // [2][KP][Q + 4]
+  float* gin = hbuf + 2 * G::HBUF;  // [CH][4H] gate pre-activations x W_ih^T + b
+  float* out = gin + CH * GW;     // [CH][6H]: h, then i f g o c
   const int b = blockIdx.x, dir = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int u = wave * 16 + (lane & 15), q = lane >> 4;
-  const bool act = u < H;
+  const int tid = threadIdx.x, u = tid / KP, q = tid % KP, gq = q & 3;
   const int L = (int)lengths[b];
   const float* W = dir ? whh1 : whh0;
 
   float w[4][Q];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    if (act) load_row<Q>(w[g], W + (long long)(g * H + u) * H + q * Q);
-    else
+  for (int g = 0; g < 4; ++g) load_row<Q>(w[g], W + (long long)(g * H + u) * H + q * Q);
 #pragma unroll
-      for (int k = 0; k < Q; ++k) w[g][k] = 0.f;
-  }
-  if (tid < H) hbuf[0][tid] = 0.f;
+  for (int g = 0; g < 4; ++g) settle(w[g]);
+  for (int i = tid; i < G::HBUF; i += NT) hbuf[i] = 0.f;
+  const int hslot = (u / Q) * G::HP + u % Q;  // where unit u's h goes
   float c = 0.f;
-  __syncthreads();
 
   const long long rowb = (long long)b * T;
-  for (int i = tid; i < (T - L) * H; i += Geo<H>::THREADS)
+  for (int i = tid; i < (T - L) * H; i += NT)
     y[(rowb + L + i / H) * ldy + dir * H + (i % H)] = 0.f;
 
-  float gnext[4] = {0.f, 0.f, 0.f, 0.f};
-  if (L > 0 && act) {
-    const int t0 = dir ? L - 1 : 0;
-    const float* gp = gx + (rowb + t0) * ldg + dir * 4 * H + u;
+  const int nch = (L + CH - 1) / CH;
+  f32x4 rin[PF];
+  auto load_chunk = [&](int ch) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) gnext[g] = gp[g * H];
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + i * NT, st = e / (GW / 4), c4 = e % (GW / 4);
+      const int s = ch * CH + st;
+      const int row = dir ? L - 1 - s : s;
+      rin[i] = s < L ? *(const f32x4*)(gx + (rowb + row) * ldg + dir * GW + c4 * 4)
+                     : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_in = [&]() {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + i * NT;
+      *(f32x4*)(gin + (e / (GW / 4)) * GW + (e % (GW / 4)) * 4) = rin[i];
+    }
+  };
+  auto flush = [&](int ch) {
+    const int n = min(CH, L - ch * CH);
+    for (int e = tid; e < n * (OW / 4); e += NT) {
+      const int st = e / (OW / 4), c4 = e % (OW / 4);
+      const int s = ch * CH + st;
+      const long long row = rowb + (dir ? L - 1 - s : s);
+      const f32x4 v = *(const f32x4*)(out + st * OW + c4 * 4);
+      if (c4 < H / 4) *(f32x4*)(y + row * ldy + dir * H + c4 * 4) = v;
+      else *(f32x4*)(sv + (row * 2 + dir) * 5 * H + (c4 - H / 4) * 4) = v;
+    }
+  };
+
+  if (nch > 0) {
+    load_chunk(0);
+    store_in();
   }
-  for (int s = 0; s < L; ++s) {
-    const int t = dir ? L - 1 - s : s;
-    const float* hc = hbuf[s & 1] + q * Q;
-    float acc[4];
+  if (nch > 1) load_chunk(1);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const int n = min(CH, L - ch * CH);
+    for (int st = 0; st < n; ++st) {
+      const int s = ch * CH + st;
+      const float* hc = hbuf + (s & 1) * G::HBUF + q * G::HP;
+      float p[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int g = 0; g < 4; ++g) acc[g] = gnext[g];
-    if (s + 1 < L && act) {
-      const int tn = dir ? t - 1 : t + 1;
-      const float* gp = gx + (rowb + tn) * ldg + dir * 4 * H + u;
+      for (int k = 0; k < Q; ++k) {
+        const float hv = hc[k];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) gnext[g] = gp[g * H];
-    }
-    float p[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < Q; ++k) {
-      const float hv = hc[k];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) p[g] = fmaf(w[g][k], hv, p[g]);
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      p[g] += __shfl_xor(p[g], 16);
-      p[g] += __shfl_xor(p[g], 32);
-      acc[g] += p[g];
-    }
-    const float ig = sigmoidf_(acc[0]);
-    const float fg = sigmoidf_(acc[1]);
-    const float gg = tanhf(acc[2]);
-    const float og = sigmoidf_(acc[3]);
-    c = fg * c + ig * gg;
-    const float h = og * tanhf(c);
-    if (act) {
-      const long long row = rowb + t;
-      if (q == 0) {
-        hbuf[(s + 1) & 1][u] = h;
-        y[row * ldy + dir * H + u] = h;
+        for (int g = 0; g < 4; ++g) p[g] = fmaf(w[g][k], hv, p[g]);
       }
-      float* svp = sv + (row * 2 + dir) * 5 * H + u;
-      const float mine = q == 0 ? ig : q == 1 ? fg : q == 2 ? gg : og;
-      svp[q * H] = mine;
-      if (q == 0) svp[4 * H] = c;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) p[g] = unit_sum<KP>(p[g]);
+      const float x = gin[st * GW + gq * H + u] + pick4(p, gq);
+      const float sg = sigm(gq == 2 ? 2.f * x : x);
+      const float act = gq == 2 ? fmaf(2.f, sg, -1.f) : sg;
+      const float ig = dpp<0x00>(act), fg = dpp<0x55>(act), gg = dpp<0xAA>(act),
+                  og = dpp<0xFF>(act);
+      c = fg * c + ig * gg;
+      const float h = og * tanh_fast(c);
+      float* o = out + st * OW;
+      if (q == 0) {
+        hbuf[((s + 1) & 1) * G::HBUF + hslot] = h;
+        o[u] = h;
+        o[5 * H + u] = c;
+      }
+      if (q < 4) o[H + q * H + u] = act;
+      __syncthreads();
     }
+    if (ch + 1 < nch) store_in();
+    flush(ch);
+    if (ch + 2 < nch) load_chunk(ch + 2);
     __syncthreads();
   }
 }
 
 template <int H>
-__global__ __launch_bounds__(Geo<H>::THREADS) void lstm_bwd_kernel(
+__global__ __launch_bounds__(Geo<H>::TB) void lstm_bwd_kernel(
     const float* __restrict__ dy, int lddy,       // [B*T][lddy], grad of outputs
     const float* __restrict__ whh0, const float* __restrict__ whh1,  // [4H][H] per direction
     const long long* __restrict__ lengths, int T,
     const float* __restrict__ sv,                 // saved [B*T][2][5H]
     float* __restrict__ dg, int lddg) {           // [B*T][lddg], dir d pre-act grads at d*4H + g*H + u
-  __shared__ __attribute__((aligned(16))) float gbuf[2][4 * H];
+  using G = Geo<H>;
+  constexpr int KP = G::KPB, QB = G::QB, NT = G::TB, IW = 7 * H, GW = 4 * H, CH = G::CHB;
+  constexpr int NIN = CH * IW / 4;                 // float4 per input chunk
+  constexpr int PF = (NIN + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* gbuf = lds;              // [2][KP][QB + 4] dG exchange
+  float* gin = gbuf + 2 * G::GBUF;  // [CH][7H]: i f g o c (row t), dy (row t), c (previous step)
+  float* out = gin + CH * IW;     // [CH][4H]
   const int b = blockIdx.x, dir = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int u = wave * 16 + (lane & 15), q = lane >> 4;
-  const bool act = u < H;
+  const int tid = threadIdx.x, u = tid / KP, q = tid % KP, gq = q & 3;
   const int L = (int)lengths[b];
   const float* W = dir ? whh1 : whh0;
 
-  // column u of gate block q: w[j] = W_hh[q*H + j][u]
-  float w[H];
+  float w[QB];
 #pragma unroll
-  for (int j = 0; j < H; ++j) w[j] = act ? W[(long long)(q * H + j) * H + u] : 0.f;
+  for (int j = 0; j < QB; ++j) w[j] = W[(long long)(q * QB + j) * H + u];
+  settle(w);
+  const int f = gq * H + u;                      // this lane's gate gradient (q < 4)
+  const int gslot = (f / QB) * G::GP + f % QB;
 
   const long long rowb = (long long)b * T;
-  for (int i = tid; i < (T - L) * 4 * H; i += Geo<H>::THREADS)
-    dg[(rowb + L + i / (4 * H)) * lddg + dir * 4 * H + (i % (4 * H))] = 0.f;
+  for (int i = tid; i < (T - L) * GW; i += NT)
+    dg[(rowb + L + i / GW) * lddg + dir * GW + (i % GW)] = 0.f;
 
-  float dhr = 0.f, dc = 0.f;
-  for (int s = L - 1; s >= 0; --s) {
-    const int t = dir ? L - 1 - s : s;
-    const long long row = rowb + t;
-    float* gb = gbuf[s & 1];
-    if (act) {
-      const float* svp = sv + (row * 2 + dir) * 5 * H + u;
-      const float ig = svp[0], fg = svp[H], gg = svp[2 * H], og = svp[3 * H], ct = svp[4 * H];
-      float cp = 0.f;
-      if (s > 0) {
-        const int tp = dir ? t + 1 : t - 1;
-        cp = sv[((rowb + tp) * 2 + dir) * 5 * H + 4 * H + u];
+  // chunk ch holds processing steps s = L-1-ch*CH-st, st = 0..CH-1 (descending s)
+  const int nch = (L + CH - 1) / CH;
+  f32x4 rin[PF];
+  auto svrow = [&](int s) { return sv + ((rowb + (dir ? L - 1 - s : s)) * 2 + dir) * 5 * H; };
+  auto load_chunk = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + i * NT, st = e / (IW / 4), c4 = e % (IW / 4);
+      const int s = L - 1 - ch * CH - st;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (e < NIN && s >= 0) {
+        if (c4 < 5 * H / 4) v = *(const f32x4*)(svrow(s) + c4 * 4);
+        else if (c4 < 6 * H / 4)
+          v = *(const f32x4*)(dy + (rowb + (dir ? L - 1 - s : s)) * lddy + dir * H +
+                              (c4 - 5 * H / 4) * 4);
+        else if (s > 0) v = *(const f32x4*)(svrow(s - 1) + 4 * H + (c4 - 6 * H / 4) * 4);
       }
-      const float dh = dy[row * lddy + dir * H + u] + dhr;
-      const float tc = tanhf(ct);
+      rin[i] = v;
+    }
+  };
+  auto store_in = [&]() {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + i * NT;
+      if (e < NIN) *(f32x4*)(gin + (e / (IW / 4)) * IW + (e % (IW / 4)) * 4) = rin[i];
+    }
+  };
+  auto flush = [&](int ch) {
+    const int n = min(CH, L - ch * CH);
+    for (int e = tid; e < n * (GW / 4); e += NT) {
+      const int st = e / (GW / 4), c4 = e % (GW / 4);
+      const int s = L - 1 - ch * CH - st;
+      const long long row = rowb + (dir ? L - 1 - s : s);
+      *(f32x4*)(dg + row * lddg + dir * GW + c4 * 4) = *(const f32x4*)(out + st * GW + c4 * 4);
+    }
+  };
+
+  if (nch > 0) {
+    load_chunk(0);
+    store_in();
+  }
+  if (nch > 1) load_chunk(1);
+  __syncthreads();
+  float dhr = 0.f, dc = 0.f;
+  for (int ch = 0; ch < nch; ++ch) {
+    const int n = min(CH, L - ch * CH);
+    for (int st = 0; st < n; ++st) {
+      const int s = L - 1 - ch * CH - st;
+      const float* in = gin + st * IW;
+      const float ig = in[u], fg = in[H + u], gg = in[2 * H + u], og = in[3 * H + u];
+      const float ct = in[4 * H + u], dyv = in[5 * H + u], cp = in[6 * H + u];
+      const float dh = dyv + dhr;
+      const float tc = tanh_fast(ct);
       const float dcc = dc + dh * og * (1.f - tc * tc);
       const float d_i = dcc * gg * ig * (1.f - ig);
       const float d_f = dcc * cp * fg * (1.f - fg);
       const float d_g = dcc * ig * (1.f - gg * gg);
       const float d_o = dh * tc * og * (1.f - og);
       dc = dcc * fg;
-      const float mine = q == 0 ? d_i : q == 1 ? d_f : q == 2 ? d_g : d_o;
-      gb[q * H + u] = mine;
-      dg[row * lddg + dir * 4 * H + q * H + u] = mine;
+      const float dgs[4] = {d_i, d_f, d_g, d_o};
+      const float mine = pick4(dgs, gq);
+      float* gb = gbuf + (s & 1) * G::GBUF;
+      if (q < 4) {
+        gb[gslot] = mine;
+        out[st * GW + f] = mine;
+      }
+      __syncthreads();
+      const float* gp = gb + q * G::GP;
+      float p[4] = {0.f, 0.f, 0.f, 0.f};  // 4 chains: the FMA latency, not issue, bounds one
+#pragma unroll
+      for (int j = 0; j < QB; ++j) p[j & 3] = fmaf(w[j], gp[j], p[j & 3]);
+      dhr = unit_sum<KP>((p[0] + p[1]) + (p[2] + p[3]));
     }
     __syncthreads();
-    float p = 0.f;
-    const float* gq = gb + q * H;
-#pragma unroll
-    for (int j = 0; j < H; ++j) p = fmaf(w[j], gq[j], p);
-    p += __shfl_xor(p, 16);
-    p += __shfl_xor(p, 32);
-    dhr = p;
+    if (ch + 1 < nch) store_in();
+    flush(ch);
+    if (ch + 2 < nch) load_chunk(ch + 2);
+    __syncthreads();
   }
 }
 
@@ -192,8 +325,13 @@ template <int H>
 int launch_fwd(const float* gx, int ldg, const float* w0, const float* w1,
                const long long* lengths, int B, int T, float* y, int ldy, float* sv,
                hipStream_t st) {
-  hipLaunchKernelGGL(lstm_fwd_kernel<H>, dim3(B, 2), dim3(Geo<H>::THREADS), 0, st, gx, ldg, w0, w1,
-                     lengths, T, y, ldy, sv);
+  if (ldg % 4 || ldy % 4 || ((uintptr_t)gx | (uintptr_t)y | (uintptr_t)sv) % 16)
+    return ENSVS_E_ARG;
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)lstm_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, Geo<H>::FWD_LDS);
+  if (attr != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(lstm_fwd_kernel<H>, dim3(B, 2), dim3(Geo<H>::TF), Geo<H>::FWD_LDS, st,
+                     gx, ldg, w0, w1, lengths, T, y, ldy, sv);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
@@ -202,8 +340,13 @@ template <int H>
 int launch_bwd(const float* dy, int lddy, const float* w0, const float* w1,
                const long long* lengths, int B, int T, const float* sv, float* dg, int lddg,
                hipStream_t st) {
-  hipLaunchKernelGGL(lstm_bwd_kernel<H>, dim3(B, 2), dim3(Geo<H>::THREADS), 0, st, dy, lddy, w0, w1,
-                     lengths, T, sv, dg, lddg);
+  if (lddy % 4 || lddg % 4 || ((uintptr_t)dy | (uintptr_t)sv | (uintptr_t)dg) % 16)
+    return ENSVS_E_ARG;
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)lstm_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, Geo<H>::BWD_LDS);
+  if (attr != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(lstm_bwd_kernel<H>, dim3(B, 2), dim3(Geo<H>::TB), Geo<H>::BWD_LDS, st,
+                     dy, lddy, w0, w1, lengths, T, sv, dg, lddg);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }

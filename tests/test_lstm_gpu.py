@@ -1,0 +1,65 @@
+"""LSTM recurrence kernels (ensvs_lstm_fwd / ensvs_lstm_bwd, lstm.hip) against torch.nn.LSTM
+(fp32 CPU, packed bidirectional, as FFConvLSTM / the lf0 encoder use it: nnsvs/model.py:862-869,
+914-916), for every hidden size the C-ABI dispatches, with lengths that end inside, at and
+one past a staging chunk (16 steps; 8 for the H=128 backward) and a length-1 sequence.
+Tolerances (fp32): outputs rel 1e-5, gradients rel 1e-4."""
+import pytest
+import torch
+from torch.nn.utils.rnn import pack_padded_sequence, pad_packed_sequence
+
+from ensemble_svs_with_interactions_amd._lib import call
+from golden_util import rel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("H", [8, 16, 32, 64, 128])
+def test_lstm_recurrence_matches_torch(H):
+    torch.manual_seed(H)
+    B, T, I = 5, 37, 24
+    lengths = [37, 17, 16, 9, 1]
+    lstm = torch.nn.LSTM(I, H, batch_first=True, bidirectional=True)
+    x = torch.randn(B, T, I, requires_grad=True)
+    out, _ = lstm(pack_padded_sequence(x, lengths, batch_first=True, enforce_sorted=False))
+    y_ref, _ = pad_packed_sequence(out, batch_first=True, total_length=T)
+    gy = torch.randn(B, T, 2 * H)
+    (y_ref * gy).sum().backward()
+
+    P = dict(lstm.named_parameters())
+    with torch.no_grad():
+        gx = torch.cat([x @ P["weight_ih_l0" + s].T + P["bias_ih_l0" + s] + P["bias_hh_l0" + s]
+                        for s in ("", "_reverse")], dim=2).reshape(B * T, 8 * H)
+    dev = "cuda"
+    st = torch.cuda.current_stream().cuda_stream
+    gx_d = gx.contiguous().to(dev)
+    whh = [P["weight_hh_l0" + s].detach().contiguous().to(dev) for s in ("", "_reverse")]
+    lens = torch.tensor(lengths, dtype=torch.int64, device=dev)
+    y = torch.empty(B * T, 2 * H, device=dev)
+    saved = torch.empty(B * T * 2 * 5 * H, device=dev)
+    assert call("ensvs_lstm_fwd", gx_d.data_ptr(), 8 * H, whh[0].data_ptr(), whh[1].data_ptr(),
+                lens.data_ptr(), B, T, H, y.data_ptr(), 2 * H, saved.data_ptr(), st) in (0, None)
+    assert rel(y.cpu().view(B, T, 2 * H), y_ref.detach()) < 1e-5
+
+    dg = torch.empty(B * T, 8 * H, device=dev)
+    gy_d = gy.reshape(B * T, 2 * H).contiguous().to(dev)
+    call("ensvs_lstm_bwd", gy_d.data_ptr(), 2 * H, whh[0].data_ptr(), whh[1].data_ptr(),
+         lens.data_ptr(), B, T, H, saved.data_ptr(), dg.data_ptr(), 8 * H, st)
+    dg = dg.cpu().view(B, T, 8 * H)
+    hy = y.cpu().view(B, T, 2 * H)
+    for d, s in enumerate(("", "_reverse")):
+        g = dg[:, :, 4 * H * d:4 * H * (d + 1)]
+        assert torch.all(g[1, 17:] == 0)  # padded frames
+        # h_{t-1} in processing order (zero state at the sequence start)
+        h = hy[:, :, H * d:H * (d + 1)]
+        hp = torch.zeros_like(h)
+        for b, L in enumerate(lengths):
+            if d == 0:
+                hp[b, 1:L] = h[b, :L - 1]
+            else:
+                hp[b, :L - 1] = h[b, 1:L]
+        dwhh = torch.einsum("btg,bth->gh", g, hp)
+        assert rel(dwhh, P["weight_hh_l0" + s].grad) < 1e-4, s
+        assert rel(g.sum((0, 1)), P["bias_hh_l0" + s].grad) < 1e-4, s
+    dx = sum(dg[:, :, 4 * H * d:4 * H * (d + 1)] @ P["weight_ih_l0" + s].detach()
+             for d, s in enumerate(("", "_reverse")))
+    assert rel(dx, x.grad) < 1e-4

@@ -46,6 +46,10 @@ class PackDesc(ctypes.Structure):
 SIGNATURES = {
     "ensvs_conv_gemm": [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int,
                         c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_float, c_int, c_vp],
+    "ensvs_conv_gemm_bf16a": [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
+                              c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_float, c_int,
+                              c_int, c_vp],
+    "ensvs_cast_bf16": [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_int, c_vp, c_int, c_vp],
     "ensvs_conv_wgrad": [c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_ll, c_ll, c_int,
                          c_float, c_int, c_vp],
@@ -97,6 +101,7 @@ SIGNATURES = {
     "ensvs_copy_cols": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_vp],
     "ensvs_axpy": [c_vp, c_vp, c_float, c_ll, c_vp],
     "ensvs_axpby": [c_vp, c_float, c_vp, c_float, c_ll, c_vp],
+    "ensvs_axpby_to": [c_vp, c_vp, c_float, c_vp, c_float, c_ll, c_vp],
     "ensvs_mul": [c_vp, c_vp, c_ll, c_vp],
     "ensvs_mul_out": [c_vp, c_vp, c_vp, c_ll, c_vp],
     "ensvs_relu_mask": [c_vp, c_vp, c_vp, c_ll, c_vp],

@@ -107,6 +107,91 @@ __device__ __forceinline__ void mma_tile(const T* As, const T* Bs, int wr, int w
   }
 }
 
+// Output tile of this workgroup, XCD-aware (cdna_hip_programming.md T1): workgroups are
+// dispatched round-robin over the 8 XCDs in flattened-id order; remap so that each XCD
+// walks a contiguous range of tiles in N-fastest order -- the N tiles that re-read one
+// 128-row A panel then run together on one XCD and share its L2.  Bijective for any grid.
+__device__ __forceinline__ void xcd_tile(int& m0, int& n0) {
+  const int nM = gridDim.x, nN = gridDim.y, total = nM * nN;
+  const int orig = blockIdx.x + blockIdx.y * nM;
+  const int xcd = orig & 7, q = total >> 3, r = total & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  m0 = (wg / nN) * BM;
+  n0 = (wg % nN) * BN;
+}
+
+// ---------------------------------------------------------------- epilogue
+// Shared by both forward kernels: acc holds the wave's 64x64 sub-tile (4x4 MFMA tiles).
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], int m0,
+                                              int n0, int wr, int wc, int lane) {
+  const int rbase = m0 + wr * 64 + (lane >> 4) * 4;
+  if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int pc = n0 + wc * 64 + p * 32 + (lane & 15);
+      const int c = (n0 + wc * 64) / 2 + p * 16 + (lane & 15);
+      if (c >= a.C) continue;
+      const float b0 = a.bias ? a.bias[pc] : 0.f;
+      const float b1 = a.bias ? a.bias[pc + 16] : 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rbase + mt * 16 + r;
+          if (row >= a.M) continue;
+          const float v0 = acc[mt][2 * p][r] + b0;
+          const float v1 = acc[mt][2 * p + 1][r] + b1;
+          if (a.epi == EPI_GATE) {
+            a.aux0[(long long)row * a.ld0 + c] = v0;
+            a.aux0[(long long)row * a.ld0 + a.C + c] = v1;
+            a.Y[(long long)row * a.ldy + c] = sigmoidf_(v0) * tanhf(v1);
+          } else if (a.epi == EPI_GATE_TS) {
+            a.Y[(long long)row * a.ldy + c] = tanhf(v0) * sigmoidf_(v1);
+          } else {
+            const float xr = a.aux1[(long long)row * a.ld1 + c];
+            a.Y[(long long)row * a.ldy + c] = (xr + v0) * 0.70710678118654752f;
+            float* sk = a.aux0 + (long long)row * a.ld0 + c;
+            *sk = a.accum ? fmaf(a.alpha, v1, *sk) : a.alpha * v1;
+          }
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int col = n0 + wc * 64 + nt * 16 + (lane & 15);
+    if (col >= a.N) continue;
+    const float bv = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbase + mt * 16 + r;
+        if (row >= a.M) continue;
+        float v = acc[mt][nt][r] + bv;
+        float* y = a.Y + (long long)row * a.ldy + col;
+        if (a.epi == EPI_PLAIN) {
+          if (a.accum) v += *y;
+          if (a.relu == 1) v = fmaxf(v, 0.f);
+          else if (a.relu == 2) v = sigmoidf_(v);
+          *y = v;
+        } else if (a.epi == EPI_ADDSCALE) {
+          v += a.alpha * a.aux1[(long long)row * a.ld1 + col];
+          *y = a.relu == 1 ? fmaxf(v, 0.f) : v;
+        } else if (a.epi == EPI_RELU_MASK) {
+          v = a.aux1[(long long)row * a.ld1 + col] > 0.f ? v : 0.f;
+          *y = a.accum ? *y + v : v;
+        } else if (a.epi == EPI_GATE_BWD) {
+          const float g = a.aux1[(long long)row * a.ld1 + col];
+          const float f = a.aux1[(long long)row * a.ld1 + a.C + col];
+          const float sg = sigmoidf_(g), th = tanhf(f);
+          a.Y[(long long)row * a.ldy + col] = v * th * sg * (1.f - sg);
+          a.Y[(long long)row * a.ldy + a.C + col] = v * sg * (1.f - th * th);
+        }
+      }
+  }
+}
+
 // ------------------------------------------------------------------ forward
 struct SegSel {  // the K-segment of one iteration, held in (wave-uniform) scalars
   const float* x;
@@ -165,7 +250,8 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
   T* Bs = As + 2 * BM * LK;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int m0, n0;
+  xcd_tile(m0, n0);
   const int M = a.M, Tout = a.Tout, Npad = a.Npad;
   const char* const W = (const char*)a.W;
 
@@ -291,72 +377,247 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_kernel(const GemmArgs a) {
     __syncthreads();
   }
 
-  // ---------------------------------------------------------------- epilogue
-  const int rbase = m0 + wr * 64 + (lane >> 4) * 4;
-  if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
+  gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
+}
+
+// ------------------------------------------------- forward, bf16 activations
+// Same contraction with every A segment already rounded to bf16 in HBM (ensvs_cast_bf16
+// applies the rounding -- and the per-sequence radd -- that conv_gemm_kernel applies
+// while staging; the MFMAs run over the same 32-deep k chunks in the same order, so both
+// kernels return identical bits).  Both operands go HBM/L2 -> LDS by
+// global_load_lds_dwordx4 (no staging VGPRs, no conversion VALU), K-steps of 64, STAGES
+// deep with a counted vmcnt so younger tiles stay in flight across the raw s_barrier.
+// LDS image per operand and stage: [128 rows][64 k] bf16, 128-B rows whose 16-B chunks
+// are XOR-swizzled by (row >> 1) & 7, so a ds_read_b128 of 16 rows at one k-chunk hits 16
+// distinct bank groups; glds writes lane-linearly (wave-instruction = 8 rows x 128 B), so
+// the swizzle is applied to the source address (cdna_hip_programming.md §5.4 rule 21).
+// The (segment, tap, k-step) cursor advances incrementally in scalars.
+constexpr int BK2 = 64;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+__device__ __forceinline__ int swz(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ void glds16(const void* g, char* l) {
+  __builtin_amdgcn_global_load_lds((glb_void*)g, (lds_void*)l, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+}
+
+struct B16Cursor {  // wave-uniform position of the next tile to stage
+  int s, j, kc;
+};
+
+// One segment's fields, wave-uniform.  Read once per kernel into SGPRs (readfirstlane),
+// not re-loaded from the kernarg segment inside the K loop.
+struct SegU {
+  const __bf16* x;
+  const char* w;  // packed weights of this segment (bytes)
+  int ld, K, Tin, pad, Kp, shift0, dil, taps, nk;
+};
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+template <typename P>
+__device__ __forceinline__ P* unip(P* p) {
+  const unsigned long long u = (unsigned long long)p;
+  const unsigned lo = (unsigned)uni((int)(unsigned)u), hi = (unsigned)uni((int)(unsigned)(u >> 32));
+  return (P*)(((unsigned long long)hi << 32) | lo);
+}
+
+__device__ __forceinline__ SegU seg_u(const SegDesc& d, const void* W) {
+  SegU u;
+  u.x = unip((const __bf16*)d.x);
+  u.w = unip((const char*)W + d.wofs * 2);
+  u.ld = uni(d.ld);
+  u.K = uni(d.K);
+  u.Tin = uni(d.Tin);
+  u.pad = uni(d.pad);
+  u.Kp = uni(d.Kp);
+  u.shift0 = uni(d.shift0);
+  u.dil = uni(d.dil);
+  u.taps = uni(d.taps);
+  u.nk = uni((d.K + BK2 - 1) / BK2);
+  return u;
+}
+
+// Stage one 64-deep K-step of both operand images (A at As, B at As + TILE).
+// rb[i] = (b_i * Tin + t_i) * ld: this lane's A row i at tap shift 0 (segment-specific).
+// Per-lane staging pointers of the current (segment, tap): A row i at k = 0 of this
+// lane's chunk (or invalid: zero padding / rows past M), B row i likewise.  Rebuilt when
+// the staging cursor enters a new tap; a K-step then only adds kb and checks the chunk
+// against K (A) / Kp (B).  Passed by value (a reference or a capturing lambda would put
+// these arrays in scratch).
+struct TapPtrs {
+  const char* pa[4];
+  const char* pb[4];
+  unsigned va;  // bit i: A row i reads data (else zeros)
+  int K, Kp;    // wave-uniform
+};
+
+__device__ __forceinline__ TapPtrs tap_ptrs(const SegU S, int j, int Npad, int n0, int rl,
+                                            int cq8a, int cq8b, const int b0, const int b1,
+                                            const int b2, const int b3, const int t0,
+                                            const int t1, const int t2, const int t3,
+                                            unsigned okm) {
+  TapPtrs P;
+  const int bt[4] = {b0, b1, b2, b3}, tt[4] = {t0, t1, t2, t3};
+  const int shj = S.shift0 + j * S.dil;
+  P.va = 0;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int pc = n0 + wc * 64 + p * 32 + (lane & 15);
-      const int c = (n0 + wc * 64) / 2 + p * 16 + (lane & 15);
-      if (c >= a.C) continue;
-      const float b0 = a.bias ? a.bias[pc] : 0.f;
-      const float b1 = a.bias ? a.bias[pc + 16] : 0.f;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rbase + mt * 16 + r;
-          if (row >= a.M) continue;
-          const float v0 = acc[mt][2 * p][r] + b0;
-          const float v1 = acc[mt][2 * p + 1][r] + b1;
-          if (a.epi == EPI_GATE) {
-            a.aux0[(long long)row * a.ld0 + c] = v0;
-            a.aux0[(long long)row * a.ld0 + a.C + c] = v1;
-            a.Y[(long long)row * a.ldy + c] = sigmoidf_(v0) * tanhf(v1);
-          } else if (a.epi == EPI_GATE_TS) {
-            a.Y[(long long)row * a.ldy + c] = tanhf(v0) * sigmoidf_(v1);
-          } else {
-            const float xr = a.aux1[(long long)row * a.ld1 + c];
-            a.Y[(long long)row * a.ldy + c] = (xr + v0) * 0.70710678118654752f;
-            float* sk = a.aux0 + (long long)row * a.ld0 + c;
-            *sk = a.accum ? fmaf(a.alpha, v1, *sk) : a.alpha * v1;
-          }
-        }
-    }
-    return;
+  for (int i = 0; i < 4; ++i) {
+    const int c8 = (i & 1) ? cq8b : cq8a;
+    const int ts = tt[i] + shj;
+    const int src = S.pad == PAD_ZERO ? ((unsigned)ts < (unsigned)S.Tin ? ts : -1)
+                                      : pad_src(ts, S.Tin, S.pad);
+    const bool ok = ((okm >> i) & 1) && src >= 0;
+    P.va |= ok ? (1u << i) : 0u;
+    P.pa[i] = (const char*)(S.x + (unsigned)((bt[i] * S.Tin + (ok ? src : 0)) * S.ld + c8));
+    P.pb[i] = S.w + ((unsigned)((j * Npad + n0 + rl + 8 * i) * S.Kp + c8)) * 2;
   }
+  P.K = S.K;
+  P.Kp = S.Kp;
+  return P;
+}
+
+template <int STAGES>
+__global__ __launch_bounds__(NTHR) void conv_gemm_b16_kernel(const GemmArgs a) {
+  static_assert(STAGES >= 2 && STAGES <= 3, "stages");
+  constexpr int TILE = BM * BK2 * 2;  // bytes of one operand image (16 KB)
+  constexpr int GL = 8;               // glds per thread per tile (4 A rows + 4 B rows)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  int m0, n0;
+  xcd_tile(m0, n0);
+  const int M = a.M, Tout = a.Tout, Npad = a.Npad;
+  const int nseg = a.nseg;
+  const SegU S0 = seg_u(a.seg[0], a.W);
+  const SegU S1 = nseg > 1 ? seg_u(a.seg[1], a.W) : S0;
+  const SegU S2 = nseg > 2 ? seg_u(a.seg[2], a.W) : S0;
+  const int nit = S0.nk * S0.taps + (nseg > 1 ? S1.nk * S1.taps : 0) +
+                  (nseg > 2 ? S2.nk * S2.taps : 0);
+
+  // Rows this lane stages (glds i of its wave: row wid*32 + 8i + lane/8) and the logical
+  // 16-B chunk it fetches into its lane-linear slot: swz(rl + 8i, slot) = cq ^ 4(i & 1).
+  const int rl = wid * 32 + (lane >> 3), slot = lane & 7;
+  const int cq = swz(rl, slot), cq8a = cq * 8, cq8b = (cq ^ 4) * 8;
+  int bt[4], tt[4];
+  unsigned okm = 0;
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    const int col = n0 + wc * 64 + nt * 16 + (lane & 15);
-    if (col >= a.N) continue;
-    const float bv = a.bias ? a.bias[col] : 0.f;
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + rl + 8 * i;
+    const bool ok = m < M;
+    bt[i] = ok ? m / Tout : 0;
+    tt[i] = ok ? m - bt[i] * Tout : 0;
+    okm |= ok ? (1u << i) : 0u;
+  }
+  // g_zero's address, opaque to the compiler: it would otherwise re-load it from the GOT
+  // (s_load + lgkmcnt wait) at every use inside the K loop
+  unsigned long long zpu = (unsigned long long)(const void*)g_zero;
+  asm volatile("" : "+s"(zpu));
+  const char* zp = (const char*)zpu;
+  const int c8[4] = {cq8a, cq8b, cq8a, cq8b};
+
+  int qs = 0, qj = 0, qkc = 0;  // staging cursor (segment, tap, k-step)
+#define TAP_PTRS(S) \
+  tap_ptrs(S, qj, Npad, n0, rl, cq8a, cq8b, bt[0], bt[1], bt[2], bt[3], tt[0], tt[1], tt[2], tt[3], okm)
+  TapPtrs P = TAP_PTRS(S0);
+#define ISSUE(it)                                                                        \
+  do {                                                                                   \
+    char* As_ = smem + ((it) % STAGES) * 2 * TILE + wid * 32 * 128;                      \
+    const int kb_ = qkc * BK2;                                                           \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                      \
+      const bool oa = ((P.va >> i) & 1) && kb_ + c8[i] < P.K;                            \
+      glds16(oa ? (const void*)(P.pa[i] + kb_ * 2) : (const void*)zp, As_ + i * 1024);   \
+    }                                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                      \
+      const bool ob = kb_ + c8[i] < P.Kp;                                                \
+      glds16(ob ? (const void*)(P.pb[i] + kb_ * 2) : (const void*)zp,                    \
+             As_ + TILE + i * 1024);                                                     \
+    }                                                                                    \
+    const int nks_ = qs == 0 ? S0.nk : (qs == 1 ? S1.nk : S2.nk);                        \
+    const int taps_ = qs == 0 ? S0.taps : (qs == 1 ? S1.taps : S2.taps);                 \
+    if (++qkc == nks_) {                                                                 \
+      qkc = 0;                                                                           \
+      if (++qj == taps_) {                                                               \
+        qj = 0;                                                                          \
+        ++qs;                                                                            \
+      }                                                                                  \
+      if (qs < nseg) P = qs == 0 ? TAP_PTRS(S0) : (qs == 1 ? TAP_PTRS(S1) : TAP_PTRS(S2)); \
+    }                                                                                    \
+  } while (0)
+
+  f32x4 acc[4][4];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rbase + mt * 16 + r;
-        if (row >= a.M) continue;
-        float v = acc[mt][nt][r] + bv;
-        float* y = a.Y + (long long)row * a.ldy + col;
-        if (a.epi == EPI_PLAIN) {
-          if (a.accum) v += *y;
-          if (a.relu == 1) v = fmaxf(v, 0.f);
-          else if (a.relu == 2) v = sigmoidf_(v);
-          *y = v;
-        } else if (a.epi == EPI_ADDSCALE) {
-          v += a.alpha * a.aux1[(long long)row * a.ld1 + col];
-          *y = a.relu == 1 ? fmaxf(v, 0.f) : v;
-        } else if (a.epi == EPI_RELU_MASK) {
-          v = a.aux1[(long long)row * a.ld1 + col] > 0.f ? v : 0.f;
-          *y = a.accum ? *y + v : v;
-        } else if (a.epi == EPI_GATE_BWD) {
-          const float g = a.aux1[(long long)row * a.ld1 + col];
-          const float f = a.aux1[(long long)row * a.ld1 + a.C + col];
-          const float sg = sigmoidf_(g), th = tanhf(f);
-          a.Y[(long long)row * a.ldy + col] = v * th * sg * (1.f - sg);
-          a.Y[(long long)row * a.ldy + a.C + col] = v * sg * (1.f - th * th);
-        }
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int p = 0; p < STAGES - 1; ++p)
+    if (p < nit) ISSUE(p);
+  const int arow = lane & 15, kq = lane >> 4;
+  // fragment read offsets: rows ra + 16i share swz(ra, .), so i only adds 2048 B
+  const int ra = wr * 64 + arow, rbr = wc * 64 + arow;
+  const int oa0 = ra * 128 + swz(ra, kq) * 16, oa1 = ra * 128 + swz(ra, kq + 4) * 16;
+  const int ob0 = TILE + rbr * 128 + swz(rbr, kq) * 16, ob1 = TILE + rbr * 128 + swz(rbr, kq + 4) * 16;
+  for (int it = 0; it < nit; ++it) {
+    if constexpr (STAGES == 3) {
+      if (it + 1 < nit) wait_vm<GL>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();  // tile `it` visible; every wave is done with tile it-1
+    if (it + STAGES - 1 < nit) ISSUE(it + STAGES - 1);
+    // (both 32-halves always: a zero half adds exact zeros, and a data-dependent skip
+    // makes hipcc move the accumulators out of AGPRs every iteration)
+    const char* St = smem + (it % STAGES) * 2 * TILE;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[i] = *(const bf16x8*)(St + (h ? oa1 : oa0) + i * 2048);
+        fb[i] = *(const bf16x8*)(St + (h ? ob1 : ob0) + i * 2048);
       }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#undef ISSUE
+#undef TAP_PTRS
+  gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
+}
+
+// y[m][k] = bf16(x[m][k] + radd[m / T][k]) for the bf16-activation GEMM (8 elements per thread).
+__global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ x, int ldx,
+                                                        const float* __restrict__ radd,
+                                                        int radd_ld, int T, long long M, int K,
+                                                        __bf16* __restrict__ y, int ldy) {
+  const int K8 = K / 8;
+  const long long n = M * K8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / K8;
+    const int k = (int)(i - m * K8) * 8;
+    f32x4 v0 = *(const f32x4*)(x + m * ldx + k), v1 = *(const f32x4*)(x + m * ldx + k + 4);
+    if (radd) {
+      const float* r = radd + (m / T) * radd_ld + k;
+      v0 += *(const f32x4*)r;
+      v1 += *(const f32x4*)(r + 4);
+    }
+    *(bf16x8*)(y + m * ldy + k) = bf16x8{(__bf16)v0[0], (__bf16)v0[1], (__bf16)v0[2],
+                                         (__bf16)v0[3], (__bf16)v1[0], (__bf16)v1[1],
+                                         (__bf16)v1[2], (__bf16)v1[3]};
   }
 }
 
@@ -727,13 +988,12 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
 // =================================================================== C ABI
 
 
-ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N,
-                              int Npad, const void* W, int wdtype, const float* bias, float* Y,
-                              int ldy, int epi, int relu, int accum, float* aux0, int ld0,
-                              const float* aux1, int ld1, float alpha, int C, void* stream) {
+static int fill_gemm_args(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, int Tout,
+                          int N, int Npad, const void* W, const float* bias, float* Y, int ldy,
+                          int epi, int relu, int accum, float* aux0, int ld0, const float* aux1,
+                          int ld1, float alpha, int C) {
   if (nseg < 1 || nseg > 3 || B <= 0 || Tout <= 0 || N <= 0 || Npad % BN != 0 || Npad < N)
     return ENSVS_E_SHAPE;
-  GemmArgs a{};
   for (int s = 0; s < nseg; ++s) {
     const ensvs_conv_seg& g = segs[s];
     if (g.Kp % BK != 0 || g.Kp < g.K || g.taps < 1) return ENSVS_E_SHAPE;
@@ -756,8 +1016,6 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
     a.seg[s].vec = (g.K % 4 == 0) && (g.ld % 4 == 0) && (((uintptr_t)g.x & 15) == 0) &&
                    (!g.radd || ((g.radd_ld % 4 == 0) && (((uintptr_t)g.radd & 15) == 0)));
   }
-  bool vec = true;
-  for (int s = 0; s < nseg; ++s) vec = vec && a.seg[s].vec;
   a.nseg = nseg;
   a.Tout = Tout;
   a.M = B * Tout;
@@ -776,6 +1034,19 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
   a.ld1 = ld1;
   a.alpha = alpha;
   a.C = C;
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N,
+                              int Npad, const void* W, int wdtype, const float* bias, float* Y,
+                              int ldy, int epi, int relu, int accum, float* aux0, int ld0,
+                              const float* aux1, int ld1, float alpha, int C, void* stream) {
+  GemmArgs a{};
+  const int rc = fill_gemm_args(a, segs, nseg, B, Tout, N, Npad, W, bias, Y, ldy, epi, relu,
+                                accum, aux0, ld0, aux1, ld1, alpha, C);
+  if (rc != ENSVS_OK) return rc;
+  bool vec = true;
+  for (int s = 0; s < nseg; ++s) vec = vec && a.seg[s].vec;
   dim3 grid(cdiv(a.M, BM), Npad / BN);
   hipStream_t st = (hipStream_t)stream;
   const bool pd = a.seg[0].pd != nullptr;
@@ -798,6 +1069,62 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
     return ENSVS_E_DTYPE;
   }
 #undef LAUNCH_GEMM
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N,
+                                    int Npad, const void* W, const float* bias, float* Y, int ldy,
+                                    int epi, int relu, int accum, float* aux0, int ld0,
+                                    const float* aux1, int ld1, float alpha, int C, int stages,
+                                    void* stream) {
+  GemmArgs a{};
+  const int rc = fill_gemm_args(a, segs, nseg, B, Tout, N, Npad, W, bias, Y, ldy, epi, relu,
+                                accum, aux0, ld0, aux1, ld1, alpha, C);
+  if (rc != ENSVS_OK) return rc;
+  for (int s = 0; s < nseg; ++s) {
+    const ensvs_conv_seg& g = segs[s];
+    if (g.radd || g.pd || g.K % 8 || g.ld % 8 || ((uintptr_t)g.x & 15)) return ENSVS_E_ARG;
+  }
+  if (((uintptr_t)W & 15)) return ENSVS_E_ARG;
+  dim3 grid(cdiv(a.M, BM), Npad / BN);
+  hipStream_t st = (hipStream_t)stream;
+  for (int s = 0; s < nseg; ++s) {  // 32-bit element offsets inside the kernel
+    const ensvs_conv_seg& g = segs[s];
+    if ((long long)B * g.Tin * g.ld >= (1ll << 31) ||
+        (long long)g.taps * Npad * g.Kp >= (1ll << 30))
+      return ENSVS_E_SHAPE;
+  }
+  const size_t lds = (size_t)2 * BM * BK2 * 2;  // one stage (A + B images)
+  if (stages == 2) {
+    static const hipError_t e2 = hipFuncSetAttribute((const void*)conv_gemm_b16_kernel<2>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(2 * lds));
+    if (e2 != hipSuccess) return ENSVS_E_HIP;
+    hipLaunchKernelGGL(conv_gemm_b16_kernel<2>, grid, dim3(NTHR), 2 * lds, st, a);
+  } else if (stages == 3) {
+    static const hipError_t e3 = hipFuncSetAttribute((const void*)conv_gemm_b16_kernel<3>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(3 * lds));
+    if (e3 != hipSuccess) return ENSVS_E_HIP;
+    hipLaunchKernelGGL(conv_gemm_b16_kernel<3>, grid, dim3(NTHR), 3 * lds, st, a);
+  } else {
+    return ENSVS_E_ARG;
+  }
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_cast_bf16(const float* x, int ldx, const float* radd, int radd_ld, int T,
+                              long long M, int K, void* y, int ldy, void* stream) {
+  if (M <= 0 || K <= 0) return ENSVS_OK;
+  if (K % 8 || ldx % 4 || ldy % 8 || (radd && (radd_ld % 4 || T <= 0)) ||
+      (((uintptr_t)x | (uintptr_t)y | (uintptr_t)radd) & 15))
+    return ENSVS_E_ARG;
+  const long long n = M * (K / 8);
+  const int blocks = (int)std::min<long long>(8192, (n + 255) / 256);
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, ldx,
+                     radd, radd_ld, T, M, K, (__bf16*)y, ldy);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }

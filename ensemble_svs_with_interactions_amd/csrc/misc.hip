@@ -444,6 +444,12 @@ __global__ void axpby_kernel(float* __restrict__ y, float a, const float* __rest
   GRID_LOOP(i, n) y[i] = a * y[i] + b * x[i];
 }
 
+// out = a * y + b * x (the same expression as axpby_kernel, out of place)
+__global__ void axpby_to_kernel(float* __restrict__ out, const float* __restrict__ y, float a,
+                                const float* __restrict__ x, float b, long long n) {
+  GRID_LOOP(i, n) out[i] = a * y[i] + b * x[i];
+}
+
 __global__ void mul_kernel(float* __restrict__ y, const float* __restrict__ x, long long n) {
   GRID_LOOP(i, n) y[i] *= x[i];
 }
@@ -715,6 +721,12 @@ ENSVS_API int ensvs_axpy(float* y, const float* x, float a, long long n, void* s
 
 ENSVS_API int ensvs_axpby(float* y, float a, const float* x, float b, long long n, void* stream) {
   LAUNCH(axpby_kernel, n, y, a, x, b, n);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_axpby_to(float* out, const float* y, float a, const float* x, float b,
+                             long long n, void* stream) {
+  LAUNCH(axpby_to_kernel, n, out, y, a, x, b, n);
   return ENSVS_OK;
 }
 

@@ -26,7 +26,7 @@ from . import kernels as K
 from . import layers as Ly
 from ._lib import call
 from .base import BaseModel, PredictionType
-from .engine import ModulePacks, empty, grad_of, lengths_pair, next_seed
+from .engine import AuxStream, ModulePacks, empty, grad_of, lengths_pair, next_seed
 from .engine import gemm_dtype as engine_gemm_dtype
 
 SQRT1_2 = 1.0 / math.sqrt(2.0)
@@ -216,8 +216,9 @@ class DiffNet(nn.Module):
         dx = None
         dpre_all = empty(M, L * 2 * C, device=dev)
         dd_all = empty(B, L * C, device=dev)
-        dy = empty(M, C, device=dev)
-        tmpb = empty(2 * C, device=dev)
+        # The dgrad chain (gate_bwd GEMM -> dilated-conv^T GEMM -> next block) stays on this
+        # stream; each block's weight / bias gradients go to a trailing auxiliary stream.
+        aux = AuxStream(dev)
         for l in reversed(range(L)):
             blk = self.residual_layers[l]
             dl = blk.dilation
@@ -226,36 +227,41 @@ class DiffNet(nn.Module):
                 segs.insert(0, K.Seg(dx, C, C, pk[f"out{l}^Tres"], T))
             K.gemm(segs, B, T, C, pk.bwd, dpre_all, L * 2 * C, yoff=l * 2 * C,
                    epi=_lib.EPI_GATE_BWD, aux1=st["GF"][l], ld1=2 * C, C=C)
-            w_o = blk.output_projection
-            if dx is not None:
-                wg(w_o.weight, dx, C, st["Z"][l], C, B, T, T, C, C, scale=SQRT1_2, row0=0)
-                _colsum_off(dx, C, M, C, w_o.bias, 0, SQRT1_2)
-            wg(w_o.weight, dss, C, st["Z"][l], C, B, T, T, C, C, row0=C)
-            _colsum_off(dss, C, M, C, w_o.bias, C, 1.0)
             # dilated conv input grad (transposed, flipped taps)
+            dy = empty(M, C, device=dev)
             K.gemm([K.Seg(dpre_all, L * 2 * C, 2 * C, pk[f"dil{l}^T"], T, taps=3, dil=dl,
                           shift0=-dl, xoff=l * 2 * C)], B, T, C, pk.bwd, dy, C)
             K.colsum(dy, C, T, C, dd_all, groups=B, ldo=L * C, outoff=l * C)
+            with aux.run(*([dss, dpre_all, dd_all] + ([dx] if dx is not None else []))):
+                w_o = blk.output_projection
+                if dx is not None:
+                    wg(w_o.weight, dx, C, st["Z"][l], C, B, T, T, C, C, scale=SQRT1_2, row0=0)
+                    _colsum_off(dx, C, M, C, w_o.bias, 0, SQRT1_2)
+                wg(w_o.weight, dss, C, st["Z"][l], C, B, T, T, C, C, row0=C)
+                _colsum_off(dss, C, M, C, w_o.bias, C, 1.0)
+                # weight grads of the gate GEMM
+                wg(blk.dilated_conv.weight, dpre_all, L * 2 * C, st["X"][l], C, B, T, T, 2 * C,
+                   C, taps=3, dil=dl, shift0=-dl, radd=st["ds"][:, l * C:], radd_ld=L * C,
+                   dyoff=l * 2 * C)
+                wg(blk.conditioner_projection.weight, dpre_all, L * 2 * C, st["cond"], st["ldc"],
+                   B, T, T, 2 * C, E, dyoff=l * 2 * C)
+                tmpb = empty(2 * C, device=dev)
+                K.colsum(dpre_all, L * 2 * C, M, 2 * C, tmpb, yoff=l * 2 * C)
+                call("ensvs_axpy", grad_of(blk.dilated_conv.bias).data_ptr(), tmpb.data_ptr(),
+                     1.0, 2 * C, Ly.stream())
+                call("ensvs_axpy", grad_of(blk.conditioner_projection.bias).data_ptr(),
+                     tmpb.data_ptr(), 1.0, 2 * C, Ly.stream())
+                # diffusion projection (per-sequence rows)
+                dpj = blk.diffusion_projection
+                wg(dpj.weight, dd_all, L * C, st["d"], C, 1, B, B, C, C, dyoff=l * C)
+                cs(dd_all, L * C, B, C, dpj.bias, yoff=l * C)
             if dx is None:
                 dx = dy
-                dy = empty(M, C, device=dev)
             else:
-                call("ensvs_axpby", dx.data_ptr(), SQRT1_2, dy.data_ptr(), 1.0, M * C, Ly.stream())
-            # weight grads of the gate GEMM
-            wg(blk.dilated_conv.weight, dpre_all, L * 2 * C, st["X"][l], C, B, T, T, 2 * C, C,
-               taps=3, dil=dl, shift0=-dl, radd=st["ds"][:, l * C:], radd_ld=L * C,
-               dyoff=l * 2 * C)
-            wg(blk.conditioner_projection.weight, dpre_all, L * 2 * C, st["cond"], st["ldc"], B, T,
-               T, 2 * C, E, dyoff=l * 2 * C)
-            K.colsum(dpre_all, L * 2 * C, M, 2 * C, tmpb, yoff=l * 2 * C)
-            call("ensvs_axpy", grad_of(blk.dilated_conv.bias).data_ptr(), tmpb.data_ptr(), 1.0,
-                 2 * C, Ly.stream())
-            call("ensvs_axpy", grad_of(blk.conditioner_projection.bias).data_ptr(),
-                 tmpb.data_ptr(), 1.0, 2 * C, Ly.stream())
-            # diffusion projection (per-sequence rows)
-            dpj = blk.diffusion_projection
-            wg(dpj.weight, dd_all, L * C, st["d"], C, 1, B, B, C, C, dyoff=l * C)
-            cs(dd_all, L * C, B, C, dpj.bias, yoff=l * C)
+                dxn = empty(M, C, device=dev)  # out of place: the aux stream still reads dx
+                call("ensvs_axpby_to", dxn.data_ptr(), dx.data_ptr(), SQRT1_2, dy.data_ptr(), 1.0,
+                     M * C, Ly.stream())
+                dx = dxn
         # conditioner input grad of all blocks at once
         dcond = empty(M, E, device=dev)
         K.gemm([K.Seg(dpre_all, L * 2 * C, L * 2 * C, pk["condT"], T)], B, T, E, pk.bwd, dcond, E)
@@ -279,6 +285,7 @@ class DiffNet(nn.Module):
         ip = self.input_projection
         wg(ip.weight, dpre0, C, st["xin"], st["ldx"], B, T, T, C, Mc)
         cs(dpre0, C, M, C, ip.bias)
+        aux.join()
         return dcond
 
     # ---------------------------------------------------------------- reference API

@@ -10,12 +10,15 @@
 * ``ModulePacks``: per-module packed GEMM operands, rebuilt when parameters
   move and repacked (one launch) when they change.
 """
+import os
+
 import torch
 
 from . import _lib
 from .kernels import PackedBuffer
 
-_STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None, "concurrent": True}
+_STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None, "concurrent": True,
+          "aux": os.environ.get("ENSVS_AUX", "0") == "1", "aux_pending": []}
 _SIDE_STREAMS = {}
 # Dev instrumentation: set to a list to collect (branch, start_event, end_event) per
 # branch region (tools/branch_times.py); None = off.
@@ -61,7 +64,9 @@ class Branches:
         if self.on_side:
             key = (str(device), n_side)
             if key not in _SIDE_STREAMS:
-                # branch 0 (the lf0 model with the AR decoder) is the critical path
+                # branch 0 (the lf0 model with its AR decoder) gets the high priority: its
+                # serial recurrences only need a few CUs and then finish early; giving it to
+                # the mgc branch instead measured slower (tools/branch_times.py)
                 _SIDE_STREAMS[key] = [torch.cuda.Stream(device, priority=-1 if i == 0 else 0)
                                       for i in range(n_side)]
             self.side = _SIDE_STREAMS[key]
@@ -74,6 +79,7 @@ class Branches:
             ev = self.main.record_event()
             for s in self.side:
                 s.wait_event(ev)
+            _STATE["aux_pending"].append([])
         return self
 
     def on(self, i):
@@ -90,7 +96,58 @@ class Branches:
         if self.on_side:
             for s in self.side:
                 self.main.wait_stream(s)
+            # auxiliary streams forked inside the branches join here, into the stream the
+            # branches forked from (joining them into a branch stream instead crashes HIP
+            # graph capture on ROCm 7: tools/debug_graph_nested.py)
+            for aux in _STATE["aux_pending"].pop():
+                self.main.wait_stream(aux.stream)
+                aux.keep = []
         return False
+
+
+_AUX_STREAMS = {}
+
+
+class AuxStream:
+    """(Off by default -- ENSVS_AUX=1 enables it: with 4 hardware queues the extra streams
+    share queues with the other branches, and HIP graph replay of the resulting topology
+    measured slower, 55-61 ms vs 32 ms per step.)
+
+    Off-critical-path work (weight gradients) on an auxiliary HIP stream that trails the
+    current stream: each ``with aux.run(*tensors):`` block starts after everything issued so
+    far on the current stream and overlaps what the current stream issues next.  Tensors
+    named there are referenced until ``join()`` (which makes the current stream wait for the
+    auxiliary one), so their memory is not reused under the auxiliary stream -- no
+    record_stream, which is also safe inside graph capture.  Serial schedule: in place."""
+
+    def __init__(self, device):
+        self.on = _STATE["concurrent"] and _STATE["aux"] and torch.cuda.is_available()
+        self.keep = []
+        if self.on:
+            self.main = torch.cuda.current_stream(device)
+            key = (str(device), self.main.cuda_stream)
+            if key not in _AUX_STREAMS:
+                _AUX_STREAMS[key] = torch.cuda.Stream(device)
+            self.stream = _AUX_STREAMS[key]
+
+    def run(self, *tensors):
+        import contextlib
+        if not self.on:
+            return contextlib.nullcontext()
+        self.keep.extend(tensors)
+        self.stream.wait_event(self.main.record_event())
+        return torch.cuda.stream(self.stream)
+
+    def join(self):
+        """Inside Branches: deferred to the branches' join; otherwise the current stream
+        waits for the auxiliary one now."""
+        if not self.on:
+            return
+        if _STATE["aux_pending"]:
+            _STATE["aux_pending"][-1].append(self)
+        else:
+            self.main.wait_stream(self.stream)
+            self.keep = []
 
 
 def next_seed() -> int:

@@ -138,25 +138,69 @@ class Seg:
     pd_dil: int = 0
 
 
+# bf16-operand GEMMs: activations rounded to bf16 in HBM by one cast pass (radd fused),
+# then both operands staged by global_load_lds (ensvs_conv_gemm_bf16a).  Same bits as the
+# register-staged kernel; pays where the A tile is re-read (several N tiles or taps).
+BF16_ACT = {"on": True, "stages": 2, "min_reuse": 2, "min_rows": 8192}
+
+
+def _bf16_act_ok(segs, W, Npad, M):
+    if any(s.x.dtype == torch.bfloat16 for s in segs):  # operands already rounded
+        assert W.dtype == _lib.DT_BF16 and all(s.radd is None and s.pd is None for s in segs)
+        return True
+    if not BF16_ACT["on"] or W.dtype != _lib.DT_BF16 or M < BF16_ACT["min_rows"]:
+        return False
+    if any(s.pd is not None or s.K % 8 for s in segs):
+        return False
+    return max(s.taps for s in segs) * (Npad // 128) >= BF16_ACT["min_reuse"]
+
+
+def gemm_dtype_is_bf16(W):
+    return W.dtype == _lib.DT_BF16
+
+
+def cast_bf16(x, ld, K, rows, xoff=0, radd=None, radd_ld=0, T=1):
+    """bf16 copy [rows, K] of x (row stride ld floats, + radd[row // T] when given)."""
+    y = torch.empty(rows, K, dtype=torch.bfloat16, device=x.device)
+    call("ensvs_cast_bf16", x.data_ptr() + 4 * xoff, ld, ptr(radd), radd_ld, T, rows, K,
+         y.data_ptr(), K, stream())
+    return y
+
+
 def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: int,
          bias=None, epi=_lib.EPI_PLAIN, relu=False, accum=False, aux0=None, ld0=0, aux1=None,
          ld1=0, alpha=0.0, C=0, yoff=0, bias_off=0):
     arr = (ConvSeg * len(segs))()
     Npad = segs[0].ref.Npad
+    a16 = _bf16_act_ok(segs, W, Npad, B * Tout)
+    keep = []
     for i, s in enumerate(segs):
         assert s.ref.Npad == Npad and s.ref.taps == s.taps and s.ref.Kp >= s.K
         d = arr[i]
-        d.x = s.x.data_ptr() + 4 * s.xoff
-        d.radd = None if s.radd is None else s.radd.data_ptr()
+        if a16 and s.x.dtype == torch.bfloat16:
+            d.x, d.ld, d.radd, d.radd_ld = s.x.data_ptr() + 2 * s.xoff, s.ld, None, 0
+        elif a16:
+            xb = cast_bf16(s.x, s.ld, s.K, B * s.Tin, s.xoff, s.radd, s.radd_ld, s.Tin)
+            keep.append(xb)
+            d.x, d.ld, d.radd, d.radd_ld = xb.data_ptr(), s.K, None, 0
+        else:
+            d.x = s.x.data_ptr() + 4 * s.xoff
+            d.radd = None if s.radd is None else s.radd.data_ptr()
+            d.ld, d.radd_ld = s.ld, s.radd_ld
         d.pd = None if s.pd is None else s.pd.data_ptr()
         d.pd_dil = s.pd_dil
         d.wofs = s.ref.offset
-        d.ld, d.K, d.taps, d.dil, d.shift0 = s.ld, s.K, s.taps, s.dil, s.shift0
-        d.pad, d.radd_ld, d.Tin, d.Kp = s.pad, s.radd_ld, s.Tin, s.ref.Kp
+        d.K, d.taps, d.dil, d.shift0 = s.K, s.taps, s.dil, s.shift0
+        d.pad, d.Tin, d.Kp = s.pad, s.Tin, s.ref.Kp
     bptr = None if bias is None else bias.data_ptr() + 4 * bias_off
-    call("ensvs_conv_gemm", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,
-         W.buf.data_ptr(), W.dtype, bptr, Y.data_ptr() + 4 * yoff, ldy, epi, int(relu),
-         int(accum), ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, stream())
+    if a16:
+        call("ensvs_conv_gemm_bf16a", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,
+             W.buf.data_ptr(), bptr, Y.data_ptr() + 4 * yoff, ldy, epi, int(relu), int(accum),
+             ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, BF16_ACT["stages"], stream())
+    else:
+        call("ensvs_conv_gemm", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,
+             W.buf.data_ptr(), W.dtype, bptr, Y.data_ptr() + 4 * yoff, ldy, epi, int(relu),
+             int(accum), ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, stream())
 
 
 _part_cache = {}

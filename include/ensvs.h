@@ -59,6 +59,18 @@ int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N
                     int relu, int accum, float* aux0, int ld0, const float* aux1, int ld1,
                     float alpha, int C, void* stream);
 
+/* The same contraction with bf16 activations: every segment's x is a const __bf16* (ld and
+ * K multiples of 8, 16-B aligned, radd and pd NULL) -- ensvs_cast_bf16 output, which
+ * holds the rounding ensvs_conv_gemm applies while staging, so both give identical bits.
+ * Operands are staged by global_load_lds, `stages` (2 or 3) 64-deep K tiles.  wdtype is bf16. */
+int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N, int Npad,
+                          const void* W, const float* bias, float* Y, int ldy, int epi, int relu,
+                          int accum, float* aux0, int ld0, const float* aux1, int ld1, float alpha,
+                          int C, int stages, void* stream);
+/* y[m][k] = bf16(x[m][k] + radd[m / T][k]) (radd optional), K % 8 == 0. */
+int ensvs_cast_bf16(const float* x, int ldx, const float* radd, int radd_ld, int T, long long M,
+                    int K, void* y, int ldy, void* stream);
+
 /* Weight gradient of the same contraction (autograd of nn.Conv1d/nn.Linear weights). */
 int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx, const float* radd,
                      int radd_ld, int B, int Tout, int Tin, int N, int K, int taps, int dil,
@@ -191,6 +203,9 @@ int ensvs_copy_cols(const float* src, int lds, float* dst, int ldd, long long M,
 int ensvs_axpy(float* y, const float* x, float a, long long n, void* stream);
 /* y = a*y + b*x ; y *= x (dropout masks) */
 int ensvs_axpby(float* y, float a, const float* x, float b, long long n, void* stream);
+/* out = a*y + b*x, bitwise the same as ensvs_axpby but out of place. */
+int ensvs_axpby_to(float* out, const float* y, float a, const float* x, float b, long long n,
+                   void* stream);
 int ensvs_mul(float* y, const float* x, long long n, void* stream);
 int ensvs_mul_out(float* out, const float* a, const float* b, long long n, void* stream);
 /* out = act > 0 ? dy : 0 (ReLU backward; out may alias dy) */

@@ -1,0 +1,103 @@
+"""bf16-activation GEMM path (ensvs_cast_bf16 + ensvs_conv_gemm_bf16a: global_load_lds
+staging, swizzled LDS, counted vmcnt) against the register-staged bf16 kernel: identical
+bits for every epilogue, padding mode, tap/dilation, multi-segment K and ragged M/N/K."""
+import pytest
+import torch
+
+from ensemble_svs_with_interactions_amd import kernels as K
+from ensemble_svs_with_interactions_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _pack(ws):
+    pb = K.PackedBuffer(L.DT_BF16)
+    refs = [pb.add(w, w.shape[0], w.shape[1], w.shape[2], w.shape[1] * w.shape[2], w.shape[2], 1)
+            for w in ws]
+    pb.finalize(DEV)
+    pb.repack()
+    return pb, refs
+
+
+def _both(run):
+    """run() with the bf16-activation path forced off, then forced on."""
+    saved = dict(K.BF16_ACT)
+    outs = []
+    try:
+        for on in (False, True):
+            K.BF16_ACT.update(on=on, min_reuse=1, min_rows=0)
+            outs.append(run())
+            torch.cuda.synchronize()
+    finally:
+        K.BF16_ACT.clear()
+        K.BF16_ACT.update(saved)
+    return outs
+
+
+@pytest.mark.parametrize("stages", [2, 3])
+@pytest.mark.parametrize("B,T,specs,N", [
+    (3, 100, [(64, 3, 2, L.PAD_ZERO, True), (32, 1, 1, L.PAD_ZERO, False)], 256),
+    (2, 77, [(40, 5, 1, L.PAD_REFLECT, False)], 200),
+    (4, 33, [(24, 3, 4, L.PAD_REPLICATE, True), (16, 1, 1, L.PAD_ZERO, False),
+             (8, 2, 1, L.PAD_ZERO, False)], 130),
+    (30, 1024, [(256, 3, 8, L.PAD_ZERO, True), (256, 1, 1, L.PAD_ZERO, False)], 512),
+])
+def test_bf16a_plain_bitwise(stages, B, T, specs, N):
+    torch.manual_seed(stages + B)
+    segs_in = []
+    for (Kc, taps, dil, pad, radd) in specs:
+        x = torch.randn(B * T, Kc + 8, device=DEV)  # ld > K
+        w = torch.randn(N, Kc, taps, device=DEV) / (Kc * taps) ** 0.5
+        r = torch.randn(B, Kc, device=DEV) if radd else None
+        segs_in.append((x, w, Kc, taps, dil, pad, r))
+    pb, refs = _pack([s[1] for s in segs_in])
+    segs = [K.Seg(x, Kc + 8, Kc, ref, T, taps=taps, dil=dil, shift0=-(taps // 2) * dil, pad=pad,
+                  radd=r, radd_ld=0 if r is None else Kc)
+            for (x, w, Kc, taps, dil, pad, r), ref in zip(segs_in, refs)]
+    bias = torch.randn(N, device=DEV)
+
+    def run():
+        y = torch.randn(B * T, N, device=DEV, generator=torch.Generator(DEV).manual_seed(5))
+        K.BF16_ACT["stages"] = stages
+        K.gemm(segs, B, T, N, pb, y, N, bias=bias, relu=True, accum=True)
+        return y
+    a, b = _both(run)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("epi", [L.EPI_GATE, L.EPI_RESSKIP, L.EPI_GATE_BWD, L.EPI_ADDSCALE,
+                                 L.EPI_RELU_MASK, L.EPI_GATE_TS, "sigmoid"])
+def test_bf16a_epilogues_bitwise(epi):
+    torch.manual_seed(7)
+    B, T, C, E = 2, 150, 64, 48
+    x = torch.randn(B * T, C, device=DEV)
+    cond = torch.randn(B * T, E, device=DEV)
+    d = torch.randn(B, C, device=DEV)
+    N = 2 * C
+    wd = torch.randn(N, C, 3, device=DEV) / (3 * C) ** 0.5
+    wc = torch.randn(N, E, 1, device=DEV) / E ** 0.5
+    pb, (rd, rc) = _pack([wd, wc])
+    segs = [K.Seg(x, C, C, rd, T, taps=3, dil=2, shift0=-2, radd=d, radd_ld=C),
+            K.Seg(cond, E, E, rc, T)]
+    bias = torch.randn(N, device=DEV)
+    aux1 = torch.randn(B * T, N, device=DEV)
+
+    def run():
+        g = torch.Generator(DEV).manual_seed(3)
+        y = torch.randn(B * T, N, device=DEV, generator=g)
+        aux0 = torch.randn(B * T, N, device=DEV, generator=g)
+        kw = dict(bias=bias)
+        if epi == "sigmoid":
+            kw.update(relu=2)
+        elif epi in (L.EPI_GATE, L.EPI_RESSKIP, L.EPI_GATE_TS):
+            kw.update(epi=epi, aux0=aux0, ld0=N, aux1=aux1, ld1=N, C=C, alpha=0.5, accum=True)
+        elif epi == L.EPI_GATE_BWD:
+            kw.update(epi=epi, aux1=aux1, ld1=N, C=C)
+        else:
+            kw.update(epi=epi, aux1=aux1, ld1=N, alpha=0.25, accum=True)
+        Nn = C if epi == L.EPI_GATE_BWD else N
+        K.gemm(segs, B, T, Nn, pb, y, N, **kw)
+        return y, aux0
+    (y0, a0), (y1, a1) = _both(run)
+    assert torch.equal(y0, y1) and torch.equal(a0, a1)

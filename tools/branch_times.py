@@ -42,9 +42,11 @@ def run(conc, P, T, steps=3):
     n = len(rec) // steps
     last = rec[-n:]  # last step: 4 fwd regions then 4 bwd regions
     out = {}
+    t_ref = last[0][1]
     for k, (i, s, e) in enumerate(last):
         phase = "fwd" if k < 4 else "bwd"
-        out[f"{NAMES[i]}.{phase}"] = round(s.elapsed_time(e), 2)
+        out[f"{NAMES[i]}.{phase}"] = (f"{s.elapsed_time(e):.2f}"
+                                      f"[{t_ref.elapsed_time(s):.1f}-{t_ref.elapsed_time(e):.1f}]")
     return step_ms, out
 
 

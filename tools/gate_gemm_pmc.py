@@ -17,5 +17,5 @@ engine.set_gemm_precision("bf16")
 dev = torch.device("cuda", 0)
 torch.manual_seed(20250321)
 model = configs.instantiate(configs.multitrack_diffusion(num_speakers=4)).to(dev)
-sec, flops = bench.gate_gemm_timing(model, 30, 1024, dev, iters=20)
+sec, _, flops = bench.gate_gemm_timing(model, 30, 1024, dev, iters=20)
 print(f"gate GEMM {sec * 1e6:.1f} us/launch, {flops / sec / 1e12:.1f} TFLOP/s", flush=True)

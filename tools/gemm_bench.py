@@ -96,15 +96,24 @@ def main():
     args = ap.parse_args()
     _lib.load()
     M = 30 * 1024
-    rows = [
-        case("gate_gemm(conv3+cond)", M, 512, [(256, 3, 2), (256, 1, 1)], _lib.DT_BF16, args.iters,
-             epi=_lib.EPI_GATE),
-        case("linear 256->512", M, 512, [(256, 1, 1)], _lib.DT_BF16, args.iters),
-        case("linear 1024->1024", M, 1024, [(1024, 1, 1)], _lib.DT_BF16, args.iters),
-        case("linear 2048->2048", M, 2048, [(2048, 1, 1)], _lib.DT_BF16, args.iters),
-        case("conv7 2048->1024", M, 1024, [(2048, 7, 1)], _lib.DT_BF16, args.iters),
-        case("linear 1024->1024 f32", M, 1024, [(1024, 1, 1)], _lib.DT_F32, args.iters),
-    ]
+    rows = []
+    for mode in ("reg", "glds2", "glds3"):
+        K.BF16_ACT.update(on=mode != "reg", stages=int(mode[-1]) if mode != "reg" else 3,
+                          min_reuse=1)
+        for r in (case("gate_gemm(conv3+cond)", M, 512, [(256, 3, 2), (256, 1, 1)],
+                       _lib.DT_BF16, args.iters, epi=_lib.EPI_GATE),
+                  case("linear 256->512", M, 512, [(256, 1, 1)], _lib.DT_BF16, args.iters),
+                  case("linear 512->256", M, 256, [(512, 1, 1)], _lib.DT_BF16, args.iters),
+                  case("linear 1024->1024", M, 1024, [(1024, 1, 1)], _lib.DT_BF16, args.iters)):
+            r["path"] = mode
+            rows.append(r)
+            print(json.dumps(r), flush=True)
+    K.BF16_ACT.update(on=True, stages=3, min_reuse=2)
+    x = torch.randn(M, 256, device="cuda")
+    sec = timeit(lambda: K.cast_bf16(x, 256, 256, M), args.iters)
+    print(json.dumps(dict(case="cast_bf16 30720x256", us=round(sec * 1e6, 1),
+                          gbps=round(M * 256 * 6 / sec / 1e9, 1))), flush=True)
+    rows = []
     rows += [
         wcase("gate conv3 256->512", M, 512, 256, 3, 2, _lib.DT_BF16, args.iters),
         wcase("linear 256->256", M, 256, 256, 1, 1, _lib.DT_BF16, args.iters),

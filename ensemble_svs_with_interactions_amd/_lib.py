@@ -102,6 +102,7 @@ SIGNATURES = {
     "ensvs_axpy": [c_vp, c_vp, c_float, c_ll, c_vp],
     "ensvs_axpby": [c_vp, c_float, c_vp, c_float, c_ll, c_vp],
     "ensvs_axpby_to": [c_vp, c_vp, c_float, c_vp, c_float, c_ll, c_vp],
+    "ensvs_axpby_to_bf16": [c_vp, c_vp, c_vp, c_float, c_vp, c_float, c_ll, c_vp],
     "ensvs_mul": [c_vp, c_vp, c_ll, c_vp],
     "ensvs_mul_out": [c_vp, c_vp, c_vp, c_ll, c_vp],
     "ensvs_relu_mask": [c_vp, c_vp, c_vp, c_ll, c_vp],

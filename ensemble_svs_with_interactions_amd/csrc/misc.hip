@@ -444,10 +444,16 @@ __global__ void axpby_kernel(float* __restrict__ y, float a, const float* __rest
   GRID_LOOP(i, n) y[i] = a * y[i] + b * x[i];
 }
 
-// out = a * y + b * x (the same expression as axpby_kernel, out of place)
-__global__ void axpby_to_kernel(float* __restrict__ out, const float* __restrict__ y, float a,
-                                const float* __restrict__ x, float b, long long n) {
-  GRID_LOOP(i, n) out[i] = a * y[i] + b * x[i];
+// out = a * y + b * x (the same expression as axpby_kernel, out of place), and an
+// optional bf16 shadow of out for the GEMM that reads it next
+__global__ void axpby_to_kernel(float* __restrict__ out, __bf16* __restrict__ outb,
+                                const float* __restrict__ y, float a, const float* __restrict__ x,
+                                float b, long long n) {
+  GRID_LOOP(i, n) {
+    const float v = a * y[i] + b * x[i];
+    out[i] = v;
+    if (outb) outb[i] = (__bf16)v;
+  }
 }
 
 __global__ void mul_kernel(float* __restrict__ y, const float* __restrict__ x, long long n) {
@@ -726,7 +732,13 @@ ENSVS_API int ensvs_axpby(float* y, float a, const float* x, float b, long long 
 
 ENSVS_API int ensvs_axpby_to(float* out, const float* y, float a, const float* x, float b,
                              long long n, void* stream) {
-  LAUNCH(axpby_to_kernel, n, out, y, a, x, b, n);
+  LAUNCH(axpby_to_kernel, n, out, (__bf16*)nullptr, y, a, x, b, n);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_axpby_to_bf16(float* out, void* outb, const float* y, float a, const float* x,
+                                  float b, long long n, void* stream) {
+  LAUNCH(axpby_to_kernel, n, out, (__bf16*)outb, y, a, x, b, n);
   return ENSVS_OK;
 }
 

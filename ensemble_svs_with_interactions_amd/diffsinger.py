@@ -136,9 +136,6 @@ class DiffNet(nn.Module):
         dev = xin.device
         C, L, E, Mc = self.C, len(self.residual_layers), self.E, self.in_dim
         M = B * T
-        x = empty(M, C, device=dev)
-        K.gemm([K.Seg(xin, ldx, Mc, pk["in"], T)], B, T, C, pk.fwd, x, C, relu=True,
-               **pk.bias_ptr_args("in.b"))
         demb = empty(B, C, device=dev)
         call("ensvs_sinusoidal", t.data_ptr(), B, C, demb.data_ptr(), Ly.stream())
         m1 = empty(B, 4 * C, device=dev)
@@ -152,6 +149,12 @@ class DiffNet(nn.Module):
         ds = empty(B, L * C, device=dev)
         K.gemm([K.Seg(d, C, C, pk["dp"], B)], 1, B, L * C, pk.fwd, ds, L * C,
                **pk.bias_ptr_args("dp.b"))
+        # bf16 operands: cond feeds all L gate GEMMs, so it is rounded once here (the
+        # per-block operands x + d_l and z are rounded by the GEMM's own cast pass)
+        condb = K.cast_bf16(cond, ldc, E, M) if K.bf16_operands(pk.fwd, M) else None
+        x = empty(M, C, device=dev)
+        K.gemm([K.Seg(xin, ldx, Mc, pk["in"], T)], B, T, C, pk.fwd, x, C, relu=True,
+               **pk.bias_ptr_args("in.b"))
         S = empty(M, C, device=dev)
         X, Z, GF = [x], [], []
         z = gf = None
@@ -159,7 +162,7 @@ class DiffNet(nn.Module):
             if save or z is None:
                 z = empty(M, C, device=dev)
                 gf = empty(M, 2 * C, device=dev)
-            self._gate_gemm(l, x, cond, ldc, ds, B, T, z, gf)
+            self._gate_gemm(l, x, cond, ldc, ds, B, T, z, gf, condb=condb)
             xn = empty(M, C, device=dev) if save else x
             K.gemm([K.Seg(z, C, C, pk[f"out{l}"], T)], B, T, 2 * C, pk.fwd, xn, C,
                    epi=_lib.EPI_RESSKIP, aux0=S, ld0=C, aux1=x, ld1=C, accum=l > 0,
@@ -182,15 +185,17 @@ class DiffNet(nn.Module):
                       ds=ds, cond=cond, ldc=ldc, B=B, T=T)
         return out, st
 
-    def _gate_gemm(self, l, x, cond, ldc, ds, B, T, z, gf):
-        """Block l's fused gate GEMM (dilated conv + conditioner + sigmoid*tanh)."""
+    def _gate_gemm(self, l, x, cond, ldc, ds, B, T, z, gf, condb=None):
+        """Block l's fused gate GEMM (dilated conv + conditioner + sigmoid*tanh); condb:
+        cond already rounded to bf16 (shared by every block)."""
         pk = self._packs
         C, L, E = self.C, len(self.residual_layers), self.E
         dl = self.residual_layers[l].dilation
-        K.gemm([K.Seg(x, C, C, pk[f"dil{l}"], T, taps=3, dil=dl, shift0=-dl,
+        segs = [K.Seg(x, C, C, pk[f"dil{l}"], T, taps=3, dil=dl, shift0=-dl,
                       radd=ds[:, l * C:], radd_ld=L * C),
-                K.Seg(cond, ldc, E, pk[f"cond{l}"], T)],
-               B, T, 2 * C, pk.fwd, z, C, epi=_lib.EPI_GATE, aux0=gf, ld0=2 * C, C=C,
+                K.Seg(cond, ldc, E, pk[f"cond{l}"], T) if condb is None else
+                K.Seg(condb, E, E, pk[f"cond{l}"], T)]
+        K.gemm(segs, B, T, 2 * C, pk.fwd, z, C, epi=_lib.EPI_GATE, aux0=gf, ld0=2 * C, C=C,
                **pk.bias_ptr_args(f"g{l}.b"))
 
     def _bwd(self, st, dout):
@@ -211,10 +216,17 @@ class DiffNet(nn.Module):
                epi=_lib.EPI_RELU_MASK, aux1=st["p1"], ld1=C)
         wg(sp.weight, dp1, C, st["S"], C, B, T, T, C, C)
         cs(dp1, C, M, C, sp.bias)
+        # bf16 operands: each is rounded once where it is produced (dss feeds all L blocks,
+        # dx comes out of the axpby, dpre is rounded per block into one buffer that the
+        # dilated-conv dgrad and the final conditioner GEMM both read)
+        b16 = K.bf16_operands(pk.bwd, M)
+        bf = lambda *shape: empty(*shape, device=dev, dtype=torch.bfloat16)  # noqa: E731
         dss = empty(M, C, device=dev)  # d(skip_l) = dS / sqrt(L)  (same for every block)
         K.gemm([K.Seg(dp1, C, C, pk["skip^T"], T)], B, T, C, pk.bwd, dss, C)
-        dx = None
+        dssb = K.cast_bf16(dss, C, C, M) if b16 else None
+        dx = dxb = None
         dpre_all = empty(M, L * 2 * C, device=dev)
+        dpre_b = bf(M, L * 2 * C) if b16 else None
         dd_all = empty(B, L * C, device=dev)
         # The dgrad chain (gate_bwd GEMM -> dilated-conv^T GEMM -> next block) stays on this
         # stream; each block's weight / bias gradients go to a trailing auxiliary stream.
@@ -222,15 +234,19 @@ class DiffNet(nn.Module):
         for l in reversed(range(L)):
             blk = self.residual_layers[l]
             dl = blk.dilation
-            segs = [K.Seg(dss, C, C, pk[f"out{l}^Tskip"], T)]
+            segs = [K.Seg(dssb if b16 else dss, C, C, pk[f"out{l}^Tskip"], T)]
             if dx is not None:
-                segs.insert(0, K.Seg(dx, C, C, pk[f"out{l}^Tres"], T))
+                segs.insert(0, K.Seg(dxb if b16 else dx, C, C, pk[f"out{l}^Tres"], T))
             K.gemm(segs, B, T, C, pk.bwd, dpre_all, L * 2 * C, yoff=l * 2 * C,
                    epi=_lib.EPI_GATE_BWD, aux1=st["GF"][l], ld1=2 * C, C=C)
+            if b16:
+                K.cast_bf16(dpre_all, L * 2 * C, 2 * C, M, xoff=l * 2 * C, out=dpre_b,
+                            out_ld=L * 2 * C, out_off=l * 2 * C)
             # dilated conv input grad (transposed, flipped taps)
             dy = empty(M, C, device=dev)
-            K.gemm([K.Seg(dpre_all, L * 2 * C, 2 * C, pk[f"dil{l}^T"], T, taps=3, dil=dl,
-                          shift0=-dl, xoff=l * 2 * C)], B, T, C, pk.bwd, dy, C)
+            K.gemm([K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, 2 * C, pk[f"dil{l}^T"], T,
+                          taps=3, dil=dl, shift0=-dl, xoff=l * 2 * C)], B, T, C, pk.bwd, dy, C)
+            dyb = K.cast_bf16(dy, C, C, M) if (dx is None and b16) else None
             K.colsum(dy, C, T, C, dd_all, groups=B, ldo=L * C, outoff=l * C)
             with aux.run(*([dss, dpre_all, dd_all] + ([dx] if dx is not None else []))):
                 w_o = blk.output_projection
@@ -256,15 +272,21 @@ class DiffNet(nn.Module):
                 wg(dpj.weight, dd_all, L * C, st["d"], C, 1, B, B, C, C, dyoff=l * C)
                 cs(dd_all, L * C, B, C, dpj.bias, yoff=l * C)
             if dx is None:
-                dx = dy
+                dx, dxb = dy, dyb
             else:
                 dxn = empty(M, C, device=dev)  # out of place: the aux stream still reads dx
-                call("ensvs_axpby_to", dxn.data_ptr(), dx.data_ptr(), SQRT1_2, dy.data_ptr(), 1.0,
-                     M * C, Ly.stream())
+                if b16:
+                    dxb = bf(M, C)
+                    call("ensvs_axpby_to_bf16", dxn.data_ptr(), dxb.data_ptr(), dx.data_ptr(),
+                         SQRT1_2, dy.data_ptr(), 1.0, M * C, Ly.stream())
+                else:
+                    call("ensvs_axpby_to", dxn.data_ptr(), dx.data_ptr(), SQRT1_2, dy.data_ptr(),
+                         1.0, M * C, Ly.stream())
                 dx = dxn
         # conditioner input grad of all blocks at once
         dcond = empty(M, E, device=dev)
-        K.gemm([K.Seg(dpre_all, L * 2 * C, L * 2 * C, pk["condT"], T)], B, T, E, pk.bwd, dcond, E)
+        K.gemm([K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, L * 2 * C, pk["condT"], T)],
+               B, T, E, pk.bwd, dcond, E)
         # step-embedding MLP
         ddv = empty(B, C, device=dev)
         K.gemm([K.Seg(dd_all, L * C, L * C, pk["dpT"], B)], 1, B, C, pk.bwd, ddv, C)

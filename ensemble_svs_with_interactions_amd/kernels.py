@@ -146,7 +146,8 @@ BF16_ACT = {"on": True, "stages": 2, "min_reuse": 2, "min_rows": 8192}
 
 def _bf16_act_ok(segs, W, Npad, M):
     if any(s.x.dtype == torch.bfloat16 for s in segs):  # operands already rounded
-        assert W.dtype == _lib.DT_BF16 and all(s.radd is None and s.pd is None for s in segs)
+        assert W.dtype == _lib.DT_BF16 and all(s.pd is None and s.K % 8 == 0 for s in segs)
+        assert all(s.radd is None for s in segs if s.x.dtype == torch.bfloat16)
         return True
     if not BF16_ACT["on"] or W.dtype != _lib.DT_BF16 or M < BF16_ACT["min_rows"]:
         return False
@@ -159,17 +160,21 @@ def gemm_dtype_is_bf16(W):
     return W.dtype == _lib.DT_BF16
 
 
-def cast_bf16(x, ld, K, rows, xoff=0, radd=None, radd_ld=0, T=1):
-    """bf16 copy [rows, K] of x (row stride ld floats, + radd[row // T] when given)."""
-    y = torch.empty(rows, K, dtype=torch.bfloat16, device=x.device)
+def cast_bf16(x, ld, K, rows, xoff=0, radd=None, radd_ld=0, T=1, out=None, out_ld=0, out_off=0):
+    """bf16 copy [rows, K] of x (row stride ld floats, + radd[row // T] when given); into
+    `out` (row stride out_ld, element offset out_off) when given."""
+    if out is None:
+        out, out_ld, out_off = torch.empty(rows, K, dtype=torch.bfloat16, device=x.device), K, 0
     call("ensvs_cast_bf16", x.data_ptr() + 4 * xoff, ld, ptr(radd), radd_ld, T, rows, K,
-         y.data_ptr(), K, stream())
-    return y
+         out.data_ptr() + 2 * out_off, out_ld, stream())
+    return out
 
 
 def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: int,
          bias=None, epi=_lib.EPI_PLAIN, relu=False, accum=False, aux0=None, ld0=0, aux1=None,
          ld1=0, alpha=0.0, C=0, yoff=0, bias_off=0):
+    """One implicit-GEMM launch (bf16-operand kernel when the A panels are bf16 or worth a
+    cast pass, register-staged kernel otherwise)."""
     arr = (ConvSeg * len(segs))()
     Npad = segs[0].ref.Npad
     a16 = _bf16_act_ok(segs, W, Npad, B * Tout)
@@ -201,6 +206,12 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
         call("ensvs_conv_gemm", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,
              W.buf.data_ptr(), W.dtype, bptr, Y.data_ptr() + 4 * yoff, ldy, epi, int(relu),
              int(accum), ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, stream())
+
+
+def bf16_operands(W, M):
+    """Whether GEMMs on these packed weights with M rows take pre-rounded bf16 operands
+    (callers then round an operand shared by several GEMMs once, instead of per GEMM)."""
+    return BF16_ACT["on"] and W.dtype == _lib.DT_BF16 and M >= BF16_ACT["min_rows"]
 
 
 _part_cache = {}

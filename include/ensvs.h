@@ -206,6 +206,9 @@ int ensvs_axpby(float* y, float a, const float* x, float b, long long n, void* s
 /* out = a*y + b*x, bitwise the same as ensvs_axpby but out of place. */
 int ensvs_axpby_to(float* out, const float* y, float a, const float* x, float b, long long n,
                    void* stream);
+/* ensvs_axpby_to plus outb[i] = bf16(out[i]) (the next GEMM's pre-rounded operand). */
+int ensvs_axpby_to_bf16(float* out, void* outb, const float* y, float a, const float* x, float b,
+                        long long n, void* stream);
 int ensvs_mul(float* y, const float* x, long long n, void* stream);
 int ensvs_mul_out(float* out, const float* a, const float* b, long long n, void* stream);
 /* out = act > 0 ? dy : 0 (ReLU backward; out may alias dy) */

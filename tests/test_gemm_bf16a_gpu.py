@@ -101,3 +101,33 @@ def test_bf16a_epilogues_bitwise(epi):
         return y, aux0
     (y0, a0), (y1, a1) = _both(run)
     assert torch.equal(y0, y1) and torch.equal(a0, a1)
+
+
+@pytest.mark.parametrize("which", ["mgc", "bap"])
+def test_diffnet_bf16_operands_bitwise(which):
+    """DiffNet forward + backward on the bf16-operand path (cond, dss and dpre rounded once,
+    dx rounded by its axpby, the rest by per-GEMM casts) equals the register-staged path
+    bit for bit."""
+    from ensemble_svs_with_interactions_amd import configs, engine
+    from golden_util import full_shapes, load_case
+    from gpu_util import build
+    engine.set_gemm_precision("bf16")
+    a, meta = load_case(f"diffnet_{which}")
+    cfg = configs.multitrack_diffusion(num_speakers=4)[f"{which}_model"]["denoise_fn"]
+    B, _, Mc, T = a["spec"].shape
+    E = a["cond"].shape[1]
+    xin = torch.from_numpy(a["spec"])[:, 0].transpose(1, 2).contiguous().view(B * T, Mc).cuda()
+    cnd = torch.from_numpy(a["cond"]).transpose(1, 2).contiguous().view(B * T, E).cuda()
+    t = torch.from_numpy(a["t"]).cuda()
+    R = torch.from_numpy(a["R"])[:, 0].transpose(1, 2).contiguous().view(B * T, Mc).cuda()
+
+    def run():
+        mod = build(cfg, full_shapes(), meta["prefix"])
+        out, st = mod._fwd(xin, Mc, t, cnd, E, B, T)
+        dcond = mod._bwd(st, R)
+        torch.cuda.synchronize()
+        return out.clone(), dcond.clone(), {k: p.grad.clone() for k, p in mod.named_parameters()}
+    (o0, d0, g0), (o1, d1, g1) = _both(run)
+    assert torch.equal(o0, o1) and torch.equal(d0, d1)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k

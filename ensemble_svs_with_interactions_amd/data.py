@@ -112,6 +112,85 @@ def collate_syncmultitrack_acoustic(batch, reduction_factor=1):
     return tuple(data)
 
 
+def onset_merge_indices(a, b):
+    """Row alignment of two tracks by note onset: the two-pointer merge of
+    gen.py:321-356 (time-lag), gen.py:637-676 (duration) and train_util.py:811-852
+    (collate_fn_syncmultitrack).  a, b: sorted onset times of tracks 0 / 1; the
+    reference appends the sentinel inf = a[-1] + b[-1] to both and merges while either
+    track has notes left, advancing the earlier one (both on a tie).  Returns int64
+    arrays (i0, i1): the source note of each track per merged row, -1 where that track
+    has no note there (a zero row, mask False)."""
+    a = np.asarray(a)
+    b = np.asarray(b)
+    inf = a[-1] + b[-1]
+    a = np.append(a, inf)
+    b = np.append(b, inf)
+    i0, i1 = [], []
+    aid = bid = 0
+    while aid < len(a) - 1 or bid < len(b) - 1:
+        if a[aid] < b[bid]:
+            i0.append(aid)
+            i1.append(-1)
+            aid += 1
+        elif a[aid] > b[bid]:
+            i0.append(-1)
+            i1.append(bid)
+            bid += 1
+        else:
+            i0.append(aid)
+            i1.append(bid)
+            aid += 1
+            bid += 1
+    return np.asarray(i0, dtype=np.int64), np.asarray(i1, dtype=np.int64)
+
+
+def _take_rows(x, idx, like):
+    """Rows idx of x (float32), zero rows where idx < 0 (the reference's zeros_like of
+    the OTHER track's row: same width)."""
+    out = np.zeros((len(idx), like.shape[1]), dtype=np.float32)
+    ok = idx >= 0
+    out[ok] = x[idx[ok]]
+    return out
+
+
+def merge_tracks_by_onset(x0, x1, a, b):
+    """gen.py:637-676: (new_x0, new_x1, mask0, mask1), both tracks on the merged rows."""
+    i0, i1 = onset_merge_indices(a, b)
+    return _take_rows(x0, i0, x0), _take_rows(x1, i1, x0), i0 >= 0, i1 >= 0
+
+
+def collate_syncmultitrack(batch, reduction_factor=1):
+    """collate_fn_syncmultitrack (train_util.py:776-934, stream selection off) on numpy:
+    the timing models' collate.  batch: 8-tuples (x0, y0, spk0, times0, x1, y1, spk1,
+    times1); both tracks of a sample are first aligned by onset (onset_merge_indices).
+    Returns (x0, y0, spk0, len0, mask0, x1, y1, spk1, len1, mask1); lengths are the
+    reference's: measured BEFORE the merge (train_util.py:806-809)."""
+    lengths_list = [[len(ensure_divisible_by(x[idx], reduction_factor)) for x in batch]
+                    for idx in (0, 4)]
+    merged = []
+    for x in batch:
+        i0, i1 = onset_merge_indices(x[3], x[7])
+        nx0, nx1 = _take_rows(x[0], i0, x[0]), _take_rows(x[4], i1, x[0])
+        ny0, ny1 = _take_rows(x[1], i0, x[1]), _take_rows(x[5], i1, x[1])
+        merged.append((nx0, ny0, x[2], i0 >= 0, nx1, ny1, x[6], i1 >= 0))
+    max_len = max(len(ensure_divisible_by(m[idx], reduction_factor))
+                  for m in merged for idx in (0, 4))
+    data = []
+    for t, idx in enumerate((0, 4)):
+        data.append(np.stack([pad_2d(ensure_divisible_by(m[idx], reduction_factor), max_len)
+                              for m in merged]))
+        data.append(np.stack([pad_2d(ensure_divisible_by(m[idx + 1], reduction_factor),
+                                     max_len) for m in merged]))
+        data.append(np.array([[float(m[idx + 2])] for m in merged], dtype=np.float32))
+        data.append(np.asarray(lengths_list[t], dtype=np.int64))
+        masks = []
+        for m in merged:
+            mk = ensure_divisible_by(m[idx + 3], reduction_factor)
+            masks.append(np.concatenate([mk, np.zeros(max_len - len(mk), dtype=bool)]))
+        data.append(np.stack(masks))
+    return tuple(data)
+
+
 def make_pad_mask(lengths, maxlen=None):
     lengths = np.asarray(lengths, dtype=np.int64)
     maxlen = int(lengths.max()) if maxlen is None else int(maxlen)

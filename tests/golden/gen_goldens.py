@@ -636,6 +636,37 @@ def case_vp():
     save("variance_predictor", arrays, meta)
 
 
+def case_onset_merge():
+    """Timing-path onset merge (collate_fn_syncmultitrack, train_util.py:776-934): two
+    tracks' note rows aligned by onset time, with ties, empty overlaps and ragged ends
+    (bit-exact)."""
+    r = rng_for("onset_merge")
+    arrays, meta = {}, {"cases": []}
+    for rf in (1, 4):
+        batch = []
+        for i in range(4):
+            n0, n1 = int(r.integers(5, 30)), int(r.integers(5, 30))
+            # onsets on a coarse grid so that ties are frequent; sorted, distinct per track
+            a = np.sort(r.choice(np.arange(0, 80), size=n0, replace=False)) * 50000
+            b = np.sort(r.choice(np.arange(0, 80), size=n1, replace=False)) * 50000
+            x0 = r.standard_normal((n0, 7)).astype(np.float32)
+            y0 = r.standard_normal((n0, 2)).astype(np.float32)
+            x1 = r.standard_normal((n1, 7)).astype(np.float32)
+            y1 = r.standard_normal((n1, 2)).astype(np.float32)
+            s0, s1 = int(r.integers(0, 3)), int(r.integers(0, 3))
+            batch.append((x0, y0, s0, a, x1, y1, s1, b))
+            key = f"rf{rf}_in{i}"
+            for k, v in dict(x0=x0, y0=y0, a=a, x1=x1, y1=y1, b=b).items():
+                arrays[f"{key}::{k}"] = v
+            arrays[f"{key}::spk"] = np.array([s0, s1])
+        out = ref_train_util.collate_fn_syncmultitrack(
+            [tuple(x) for x in batch], reduction_factor=rf)
+        for j, o in enumerate(out):
+            arrays[f"rf{rf}::out{j}"] = o.numpy()
+        meta["cases"].append(rf)
+    save("onset_merge", arrays, meta)
+
+
 def main():
     which = sys.argv[1:] or ["all"]
     run = lambda n: "all" in which or n in which  # noqa: E731
@@ -672,6 +703,8 @@ def main():
         case_mdn()
     if run("vp"):
         case_vp()
+    if run("onset"):
+        case_onset_merge()
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(dict(seed=SEED, torch=torch.__version__, numpy=np.__version__,
                        reference="sarulab-speech/ensemble_svs_with_interactions @ 2025-03-21",

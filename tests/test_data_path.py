@@ -50,3 +50,36 @@ def test_independent_track_sort_quirk():
     # train_acoustic_multitrack.py:472-483 sorts the two tracks independently
     i0, i1, lens = data.sort_pair_batch([10, 30, 20], [30, 10, 20])
     assert list(i0) == [1, 2, 0] and list(i1) == [0, 2, 1] and list(lens) == [30, 20, 10]
+
+
+def test_onset_merge_collate_bit_exact():
+    """Timing-path collate (collate_fn_syncmultitrack, train_util.py:776-934): rows of the
+    two tracks aligned by note onset (ties merged), padded, masks and pre-merge lengths."""
+    a, meta = load_case("onset_merge")
+    for rf in meta["cases"]:
+        batch, i = [], 0
+        while f"rf{rf}_in{i}::x0" in a:
+            g = lambda k: a[f"rf{rf}_in{i}::{k}"]  # noqa: E731
+            s = g("spk")
+            batch.append((g("x0"), g("y0"), int(s[0]), g("a"), g("x1"), g("y1"), int(s[1]),
+                          g("b")))
+            i += 1
+        out = data.collate_syncmultitrack(batch, reduction_factor=rf)
+        assert len(out) == 10
+        for j, o in enumerate(out):
+            ref = a[f"rf{rf}::out{j}"]
+            assert o.shape == ref.shape, (rf, j)
+            assert np.array_equal(o, ref), (rf, j)
+
+
+def test_onset_merge_indices_edge_cases():
+    # tie at the first note, one track exhausted first, identical tracks
+    i0, i1 = data.onset_merge_indices([0, 5, 10], [0, 3, 10, 12])
+    assert i0.tolist() == [0, -1, 1, 2, -1] and i1.tolist() == [0, 1, -1, 2, 3]
+    i0, i1 = data.onset_merge_indices([2, 4], [2, 4])
+    assert i0.tolist() == [0, 1] and i1.tolist() == [0, 1]
+    x0 = np.arange(6, dtype=np.float32).reshape(3, 2)
+    x1 = -np.arange(4, dtype=np.float32).reshape(2, 2) - 1
+    n0, n1, m0, m1 = data.merge_tracks_by_onset(x0, x1, [0, 1, 2], [1, 3])
+    assert m0.tolist() == [True, True, True, False] and m1.tolist() == [False, True, False, True]
+    assert np.array_equal(n1[1], x1[0]) and np.array_equal(n0[3], np.zeros(2, np.float32))

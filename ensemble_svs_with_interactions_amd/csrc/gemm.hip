@@ -57,6 +57,7 @@ struct GemmArgs {
   int ld0, ld1;
   float alpha;
   int C;
+  int vec_out;  // Y / aux0 / aux1 rows 16-B aligned with ld % 4 == 0: 16-B epilogue stores
 };
 
 template <typename T>
@@ -189,6 +190,156 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4]
           a.Y[(long long)row * a.ldy + a.C + col] = v * sg * (1.f - th * th);
         }
       }
+  }
+}
+
+// ---------------------------------------------------------- LDS-staged epilogue
+// The fp32 output tile goes through LDS (row stride 132 floats: the fragment writes of a
+// wave hit 64 distinct banks), then every thread handles 4 consecutive output columns of
+// a row: one 16-B load / store per operand instead of four 4-B accesses (the per-element
+// epilogue above is store-issue bound).  Same arithmetic per element as gemm_epilogue.
+constexpr int EP = 132;
+constexpr int EPI_LDS = BM * EP * 4;
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *(f32x4*)p = v; }
+
+__device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[4][4], int m0,
+                                                  int n0, int wr, int wc, int lane, int tid,
+                                                  char* smem) {
+  float* T = (float*)smem;
+  __syncthreads();  // every wave is done with the K-loop images
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        T[(wr * 64 + mt * 16 + (lane >> 4) * 4 + r) * EP + wc * 64 + nt * 16 + (lane & 15)] =
+            acc[mt][nt][r];
+  __syncthreads();
+  const int M = a.M;
+  if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
+    // this tile holds 64 output channels (gate/filter interleaved by 16 in the packed columns)
+    for (int it = tid; it < BM * 16; it += NTHR) {
+      const int row = it >> 4, q4 = it & 15;
+      const int m = m0 + row;
+      const int q = q4 >> 2, j = (q4 & 3) * 4;
+      const int c = n0 / 2 + q * 16 + j;  // first of 4 output channels
+      if (m >= M || c >= a.C) continue;
+      const int gc = q * 32 + j;          // tile column of the gate values; filter at +16
+      f32x4 g = ld4(T + row * EP + gc), f = ld4(T + row * EP + gc + 16);
+      if (a.bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          g[e] += a.bias[n0 + gc + e];
+          f[e] += a.bias[n0 + gc + 16 + e];
+        }
+      }
+      if (a.epi == EPI_GATE) {
+        st4(a.aux0 + (long long)m * a.ld0 + c, g);
+        st4(a.aux0 + (long long)m * a.ld0 + a.C + c, f);
+        f32x4 z;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) z[e] = sigmoidf_(g[e]) * tanhf(f[e]);
+        st4(a.Y + (long long)m * a.ldy + c, z);
+      } else if (a.epi == EPI_GATE_TS) {
+        f32x4 z;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) z[e] = tanhf(g[e]) * sigmoidf_(f[e]);
+        st4(a.Y + (long long)m * a.ldy + c, z);
+      } else {
+        const f32x4 xr = ld4(a.aux1 + (long long)m * a.ld1 + c);
+        f32x4 y, sk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = (xr[e] + g[e]) * 0.70710678118654752f;
+        st4(a.Y + (long long)m * a.ldy + c, y);
+        float* skp = a.aux0 + (long long)m * a.ld0 + c;
+        if (a.accum) {
+          const f32x4 s0 = ld4(skp);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sk[e] = fmaf(a.alpha, f[e], s0[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sk[e] = a.alpha * f[e];
+        }
+        st4(skp, sk);
+      }
+    }
+    return;
+  }
+  for (int it = tid; it < BM * 32; it += NTHR) {
+    const int row = it >> 5, cq = it & 31;
+    const int m = m0 + row, col = n0 + cq * 4;
+    if (m >= M || col >= a.N) continue;
+    const int ne = min(4, a.N - col);
+    f32x4 v = ld4(T + row * EP + cq * 4);
+    if (a.bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e < ne) v[e] += a.bias[col + e];
+    }
+    float* y = a.Y + (long long)m * a.ldy + col;
+    if (ne == 4) {
+      if (a.epi == EPI_PLAIN) {
+        if (a.accum) v += ld4(y);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (a.relu == 1) v[e] = fmaxf(v[e], 0.f);
+          else if (a.relu == 2) v[e] = sigmoidf_(v[e]);
+        }
+        st4(y, v);
+      } else if (a.epi == EPI_ADDSCALE) {
+        const f32x4 x1 = ld4(a.aux1 + (long long)m * a.ld1 + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] += a.alpha * x1[e];
+          v[e] = a.relu == 1 ? fmaxf(v[e], 0.f) : v[e];
+        }
+        st4(y, v);
+      } else if (a.epi == EPI_RELU_MASK) {
+        const f32x4 x1 = ld4(a.aux1 + (long long)m * a.ld1 + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = x1[e] > 0.f ? v[e] : 0.f;
+        if (a.accum) v += ld4(y);
+        st4(y, v);
+      } else if (a.epi == EPI_GATE_BWD) {
+        const f32x4 g = ld4(a.aux1 + (long long)m * a.ld1 + col);
+        const f32x4 f = ld4(a.aux1 + (long long)m * a.ld1 + a.C + col);
+        f32x4 dg, df;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float sg = sigmoidf_(g[e]), th = tanhf(f[e]);
+          dg[e] = v[e] * th * sg * (1.f - sg);
+          df[e] = v[e] * sg * (1.f - th * th);
+        }
+        st4(y, dg);
+        st4(y + a.C, df);
+      }
+    } else {
+      for (int e = 0; e < ne; ++e) {
+        float w = v[e];
+        float* ye = y + e;
+        if (a.epi == EPI_PLAIN) {
+          if (a.accum) w += *ye;
+          if (a.relu == 1) w = fmaxf(w, 0.f);
+          else if (a.relu == 2) w = sigmoidf_(w);
+          *ye = w;
+        } else if (a.epi == EPI_ADDSCALE) {
+          w += a.alpha * a.aux1[(long long)m * a.ld1 + col + e];
+          *ye = a.relu == 1 ? fmaxf(w, 0.f) : w;
+        } else if (a.epi == EPI_RELU_MASK) {
+          w = a.aux1[(long long)m * a.ld1 + col + e] > 0.f ? w : 0.f;
+          *ye = a.accum ? *ye + w : w;
+        } else if (a.epi == EPI_GATE_BWD) {
+          const float g = a.aux1[(long long)m * a.ld1 + col + e];
+          const float f = a.aux1[(long long)m * a.ld1 + a.C + col + e];
+          const float sg = sigmoidf_(g), th = tanhf(f);
+          ye[0] = w * th * sg * (1.f - sg);
+          ye[a.C] = w * sg * (1.f - th * th);
+        }
+      }
+    }
   }
 }
 
@@ -818,6 +969,124 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
   }
 }
 
+// ------------------------------------------------- weight grads, bf16 operands
+// wgrad_kernel<bf16> with dy and x already rounded to bf16 in HBM (the staging rounding of
+// wgrad_kernel, so the result is bit-identical): both [32 frames][128 channels] images
+// are filled by global_load_lds_dwordx4, double-buffered with a counted vmcnt and raw
+// barriers.  The images keep wg_off's XOR swizzle (conflict-free ds_read_b64_tr_b16
+// operand reads); the DMA writes lane-linearly, so each lane fetches the chunk that the
+// swizzle maps to its slot.  a.dy / a.x point at bf16 rows here (ldy / ldx in elements).
+__device__ __forceinline__ int wg_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+__global__ __launch_bounds__(NTHR) void wgrad_b16_kernel(const WgradArgs a) {
+  constexpr int IMG = BK * 256;  // bytes per operand image (32 frames x 128 channels bf16)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int n0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
+  const int j = blockIdx.z % a.taps, s = blockIdx.z / a.taps;
+  const int mbeg = s * a.rows_per_split;
+  const int mend = min(a.M, mbeg + a.rows_per_split);
+  const int nch = mbeg < mend ? (mend - mbeg + BK - 1) / BK : 0;
+  const __bf16* dy = (const __bf16*)a.dy;
+  const __bf16* x = (const __bf16*)a.x;
+  unsigned long long zpu = (unsigned long long)(const void*)g_zero;
+  asm volatile("" : "+s"(zpu));
+  const char* zp = (const char*)zpu;
+
+  // this lane's two frame rows (glds i: row wid*8 + 4i + lane/16) and their 16-B chunks
+  int fr[2], cc[2], fb[2], ft[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    fr[i] = wid * 8 + 4 * i + (lane >> 4);
+    cc[i] = (lane & 15) ^ wg_swz(fr[i]);
+    const int m = mbeg + fr[i];
+    fb[i] = m / a.Tout;
+    ft[i] = m - fb[i] * a.Tout;
+  }
+  auto issue = [&](int ch) __attribute__((always_inline)) {
+    char* A = smem + (ch & 1) * 2 * IMG;
+    char* Bm = A + IMG;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = mbeg + ch * BK + fr[i];
+      const bool mv = m < mend;
+      const int n = n0 + cc[i] * 8, k = k0 + cc[i] * 8;
+      const void* ga = (mv && n < a.N) ? (const void*)(dy + (long long)m * a.ldy + n)
+                                       : (const void*)zp;
+      const int src = pad_src(ft[i] + a.shift0 + j * a.dil, a.Tin, a.pad);
+      const void* gb = (mv && src >= 0 && k < a.K)
+                           ? (const void*)(x + (long long)(fb[i] * a.Tin + src) * a.ldx + k)
+                           : (const void*)zp;
+      glds16(ga, A + (wid * 8 + 4 * i) * 256);
+      glds16(gb, Bm + (wid * 8 + 4 * i) * 256);
+      int nt = ft[i] + BK, nb = fb[i];  // this row slot's frame in the next chunk
+      while (nt >= a.Tout) {
+        nt -= a.Tout;
+        ++nb;
+      }
+      fb[i] = nb;
+      ft[i] = nt;
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nch > 0) issue(0);
+  for (int ch = 0; ch < nch; ++ch) {
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // chunk ch visible; every wave is done with chunk ch-1
+    if (ch + 1 < nch) issue(ch + 1);
+    const char* A = smem + (ch & 1) * 2 * IMG;
+    const char* Bm = A + IMG;
+    bf16x8 fa[4], fbv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i] = wg_frag(A, wr * 64 + i * 16, lane);
+      fbv[i] = wg_frag(Bm, wc * 64 + i * 16, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fbv[jj], acc[i][jj], 0, 0, 0);
+  }
+  if (a.splits == 1) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int k = k0 + wc * 64 + nt * 16 + (lane & 15);
+      if (k >= a.K) continue;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + wr * 64 + mt * 16 + (lane >> 4) * 4 + r;
+          if (n < a.N) {
+            float* d = a.dst + n * a.sn + k * a.sk + j * a.sj;
+            const float v = acc[mt][nt][r] * a.scale;
+            *d = a.accum ? *d + v : v;
+          }
+        }
+    }
+    return;
+  }
+  float* out = a.part + ((long long)(s * a.taps + j) * a.N) * a.K;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int k = k0 + wc * 64 + nt * 16 + (lane & 15);
+    if (k >= a.K) continue;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wr * 64 + mt * 16 + (lane >> 4) * 4 + r;
+        if (n < a.N) out[(long long)n * a.K + k] = acc[mt][nt][r];
+      }
+  }
+}
+
 // dst[n*sn + k*sk + j*sj] (+)= scale * sum_s part[s][j][n][k]   (fixed summation order)
 // grid (cdiv(K, 256), N * taps): one (tap, n) row of K per block row, coalesced over k.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
@@ -1034,6 +1303,8 @@ static int fill_gemm_args(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int
   a.ld1 = ld1;
   a.alpha = alpha;
   a.C = C;
+  auto al = [](const void* p, int ld) { return !p || ((((uintptr_t)p) & 15) == 0 && ld % 4 == 0); };
+  a.vec_out = al(Y, ldy) && al(aux0, ld0) && al(aux1, ld1) && (C % 4 == 0);
   return ENSVS_OK;
 }
 
@@ -1096,18 +1367,20 @@ ENSVS_API int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B,
       return ENSVS_E_SHAPE;
   }
   const size_t lds = (size_t)2 * BM * BK2 * 2;  // one stage (A + B images)
+  // the LDS-staged epilogue reuses the stage buffers for the fp32 output tile
+  const size_t l2 = std::max<size_t>(2 * lds, EPI_LDS), l3 = std::max<size_t>(3 * lds, EPI_LDS);
   if (stages == 2) {
     static const hipError_t e2 = hipFuncSetAttribute((const void*)conv_gemm_b16_kernel<2>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)(2 * lds));
+                                                     (int)l2);
     if (e2 != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(conv_gemm_b16_kernel<2>, grid, dim3(NTHR), 2 * lds, st, a);
+    hipLaunchKernelGGL(conv_gemm_b16_kernel<2>, grid, dim3(NTHR), l2, st, a);
   } else if (stages == 3) {
     static const hipError_t e3 = hipFuncSetAttribute((const void*)conv_gemm_b16_kernel<3>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)(3 * lds));
+                                                     (int)l3);
     if (e3 != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(conv_gemm_b16_kernel<3>, grid, dim3(NTHR), 3 * lds, st, a);
+    hipLaunchKernelGGL(conv_gemm_b16_kernel<3>, grid, dim3(NTHR), l3, st, a);
   } else {
     return ENSVS_E_ARG;
   }
@@ -1191,6 +1464,51 @@ ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx
   return ENSVS_OK;
 }
 
+
+// Weight gradient with bf16 operands (dy, x rounded to bf16 in HBM; radd folded into x).
+ENSVS_API int ensvs_conv_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, int B,
+                                    int Tout, int Tin, int N, int K, int taps, int dil, int shift0,
+                                    int pad, int splits, float* part, float* dst, long long sn,
+                                    long long sk, long long sj, int accum, float scale,
+                                    void* stream) {
+  if (B <= 0 || Tout <= 0 || N <= 0 || K <= 0 || taps <= 0 || splits <= 0) return ENSVS_E_SHAPE;
+  if (N % 8 || K % 8 || ldy % 8 || ldx % 8 || (((uintptr_t)dy | (uintptr_t)x) & 15))
+    return ENSVS_E_ARG;
+  WgradArgs a{};
+  a.dy = (const float*)dy;
+  a.x = (const float*)x;
+  a.part = part;
+  a.ldy = ldy;
+  a.ldx = ldx;
+  a.K = K;
+  a.taps = taps;
+  a.dil = dil;
+  a.shift0 = shift0;
+  a.pad = pad;
+  a.Tin = Tin;
+  a.Tout = Tout;
+  a.M = B * Tout;
+  a.N = N;
+  a.splits = splits;
+  a.rows_per_split = (cdiv(a.M, splits) + BK - 1) / BK * BK;
+  a.dst = dst;
+  a.sn = sn;
+  a.sk = sk;
+  a.sj = sj;
+  a.scale = scale;
+  a.accum = accum;
+  dim3 grid(cdiv(N, BM), cdiv(K, BN), taps * splits);
+  if (N * taps > 65535) return ENSVS_E_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(wgrad_b16_kernel, grid, dim3(NTHR), 2 * 2 * BK * 256, st, a);
+  ENSVS_CHECK_LAUNCH();
+  if (splits > 1) {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(K, 256), N * taps), dim3(256), 0, st, part,
+                       dst, splits, taps, N, K, sn, sk, sj, accum, scale);
+    ENSVS_CHECK_LAUNCH();
+  }
+  return ENSVS_OK;
+}
 
 // Batched weight repack: `descs` is a DEVICE array of `n` descriptors.
 ENSVS_API int ensvs_pack_weights(const ensvs_pack_desc* descs, int n, int max_elems, void* stream) {

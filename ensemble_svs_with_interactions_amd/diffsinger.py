@@ -149,9 +149,12 @@ class DiffNet(nn.Module):
         ds = empty(B, L * C, device=dev)
         K.gemm([K.Seg(d, C, C, pk["dp"], B)], 1, B, L * C, pk.fwd, ds, L * C,
                **pk.bias_ptr_args("dp.b"))
-        # bf16 operands: cond feeds all L gate GEMMs, so it is rounded once here (the
-        # per-block operands x + d_l and z are rounded by the GEMM's own cast pass)
-        condb = K.cast_bf16(cond, ldc, E, M) if K.bf16_operands(pk.fwd, M) else None
+        # bf16 operands: cond feeds all L gate GEMMs, so it is rounded once here; the
+        # per-block x + d_l and z are rounded by an explicit cast and, when training, kept
+        # for the bf16 weight-gradient kernels of the backward pass
+        b16 = K.bf16_operands(pk.fwd, M)
+        condb = K.cast_bf16(cond, ldc, E, M) if b16 else None
+        XB, ZB = [], []
         x = empty(M, C, device=dev)
         K.gemm([K.Seg(xin, ldx, Mc, pk["in"], T)], B, T, C, pk.fwd, x, C, relu=True,
                **pk.bias_ptr_args("in.b"))
@@ -162,9 +165,15 @@ class DiffNet(nn.Module):
             if save or z is None:
                 z = empty(M, C, device=dev)
                 gf = empty(M, 2 * C, device=dev)
-            self._gate_gemm(l, x, cond, ldc, ds, B, T, z, gf, condb=condb)
+            xb = K.cast_bf16(x, C, C, M, radd=ds[:, l * C:], radd_ld=L * C, T=T) if b16 else None
+            self._gate_gemm(l, x, cond, ldc, ds, B, T, z, gf, condb=condb, xb=xb)
+            zb = K.cast_bf16(z, C, C, M) if b16 else None
+            if save and b16:
+                XB.append(xb)
+                ZB.append(zb)
             xn = empty(M, C, device=dev) if save else x
-            K.gemm([K.Seg(z, C, C, pk[f"out{l}"], T)], B, T, 2 * C, pk.fwd, xn, C,
+            K.gemm([K.Seg(z, C, C, pk[f"out{l}"], T) if zb is None else
+                    K.Seg(zb, C, C, pk[f"out{l}"], T)], B, T, 2 * C, pk.fwd, xn, C,
                    epi=_lib.EPI_RESSKIP, aux0=S, ld0=C, aux1=x, ld1=C, accum=l > 0,
                    alpha=1.0 / math.sqrt(L), C=C, **pk.bias_ptr_args(f"o{l}.b"))
             if save:
@@ -182,17 +191,18 @@ class DiffNet(nn.Module):
         st = None
         if save:
             st = dict(xin=xin, ldx=ldx, X=X, Z=Z, GF=GF, S=S, p1=p1, demb=demb, m1=m1, mi=mi, d=d,
-                      ds=ds, cond=cond, ldc=ldc, B=B, T=T)
+                      ds=ds, cond=cond, ldc=ldc, B=B, T=T, XB=XB, ZB=ZB, condb=condb)
         return out, st
 
-    def _gate_gemm(self, l, x, cond, ldc, ds, B, T, z, gf, condb=None):
-        """Block l's fused gate GEMM (dilated conv + conditioner + sigmoid*tanh); condb:
-        cond already rounded to bf16 (shared by every block)."""
+    def _gate_gemm(self, l, x, cond, ldc, ds, B, T, z, gf, condb=None, xb=None):
+        """Block l's fused gate GEMM (dilated conv + conditioner + sigmoid*tanh); condb /
+        xb: cond and x + d_l already rounded to bf16."""
         pk = self._packs
         C, L, E = self.C, len(self.residual_layers), self.E
         dl = self.residual_layers[l].dilation
         segs = [K.Seg(x, C, C, pk[f"dil{l}"], T, taps=3, dil=dl, shift0=-dl,
-                      radd=ds[:, l * C:], radd_ld=L * C),
+                      radd=ds[:, l * C:], radd_ld=L * C) if xb is None else
+                K.Seg(xb, C, C, pk[f"dil{l}"], T, taps=3, dil=dl, shift0=-dl),
                 K.Seg(cond, ldc, E, pk[f"cond{l}"], T) if condb is None else
                 K.Seg(condb, E, E, pk[f"cond{l}"], T)]
         K.gemm(segs, B, T, 2 * C, pk.fwd, z, C, epi=_lib.EPI_GATE, aux0=gf, ld0=2 * C, C=C,
@@ -248,19 +258,29 @@ class DiffNet(nn.Module):
                           taps=3, dil=dl, shift0=-dl, xoff=l * 2 * C)], B, T, C, pk.bwd, dy, C)
             dyb = K.cast_bf16(dy, C, C, M) if (dx is None and b16) else None
             K.colsum(dy, C, T, C, dd_all, groups=B, ldo=L * C, outoff=l * C)
-            with aux.run(*([dss, dpre_all, dd_all] + ([dx] if dx is not None else []))):
+            with aux.run(*([t for t in (dss, dpre_all, dd_all, dx, dxb, dssb, dpre_b)
+                            if t is not None])):
                 w_o = blk.output_projection
+                bw = b16 and len(st["XB"]) == L  # bf16 operands saved by the forward
+                zsrc = st["ZB"][l] if bw else st["Z"][l]
                 if dx is not None:
-                    wg(w_o.weight, dx, C, st["Z"][l], C, B, T, T, C, C, scale=SQRT1_2, row0=0)
+                    wg(w_o.weight, dxb if bw else dx, C, zsrc, C, B, T, T, C, C, scale=SQRT1_2,
+                       row0=0)
                     _colsum_off(dx, C, M, C, w_o.bias, 0, SQRT1_2)
-                wg(w_o.weight, dss, C, st["Z"][l], C, B, T, T, C, C, row0=C)
+                wg(w_o.weight, dssb if bw else dss, C, zsrc, C, B, T, T, C, C, row0=C)
                 _colsum_off(dss, C, M, C, w_o.bias, C, 1.0)
                 # weight grads of the gate GEMM
-                wg(blk.dilated_conv.weight, dpre_all, L * 2 * C, st["X"][l], C, B, T, T, 2 * C,
-                   C, taps=3, dil=dl, shift0=-dl, radd=st["ds"][:, l * C:], radd_ld=L * C,
-                   dyoff=l * 2 * C)
-                wg(blk.conditioner_projection.weight, dpre_all, L * 2 * C, st["cond"], st["ldc"],
-                   B, T, T, 2 * C, E, dyoff=l * 2 * C)
+                if bw:
+                    wg(blk.dilated_conv.weight, dpre_b, L * 2 * C, st["XB"][l], C, B, T, T,
+                       2 * C, C, taps=3, dil=dl, shift0=-dl, dyoff=l * 2 * C)
+                    wg(blk.conditioner_projection.weight, dpre_b, L * 2 * C, st["condb"], E, B,
+                       T, T, 2 * C, E, dyoff=l * 2 * C)
+                else:
+                    wg(blk.dilated_conv.weight, dpre_all, L * 2 * C, st["X"][l], C, B, T, T,
+                       2 * C, C, taps=3, dil=dl, shift0=-dl, radd=st["ds"][:, l * C:],
+                       radd_ld=L * C, dyoff=l * 2 * C)
+                    wg(blk.conditioner_projection.weight, dpre_all, L * 2 * C, st["cond"],
+                       st["ldc"], B, T, T, 2 * C, E, dyoff=l * 2 * C)
                 tmpb = empty(2 * C, device=dev)
                 K.colsum(dpre_all, L * 2 * C, M, 2 * C, tmpb, yoff=l * 2 * C)
                 call("ensvs_axpy", grad_of(blk.dilated_conv.bias).data_ptr(), tmpb.data_ptr(),

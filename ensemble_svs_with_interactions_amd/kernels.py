@@ -231,11 +231,19 @@ def scratch(nfloats, device, key="part"):
 def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, sk, sj,
           accum=False, dtype=_lib.DT_BF16, radd=None, radd_ld=0, dyoff=0, xoff=0, splits=None,
           scale=1.0, dstoff=0):
+    """dst (+)= scale * dy^T x (conv/linear weight gradient).  dy and x may both be bf16
+    tensors already rounded (radd then folded into x): the glds-staged kernel, same bits."""
     M = B * Tout
     if splits is None:
         tiles = -(-N // 128) * -(-K // 128) * taps
         splits = max(1, min(64, 512 // max(tiles, 1), -(-M // 256)))
     part = scratch(splits * taps * N * K, dy.device)
+    if dy.dtype == torch.bfloat16 or x.dtype == torch.bfloat16:
+        assert dy.dtype == x.dtype == torch.bfloat16 and radd is None and dtype == _lib.DT_BF16
+        call("ensvs_conv_wgrad_bf16", dy.data_ptr() + 2 * dyoff, ldy, x.data_ptr() + 2 * xoff,
+             ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, splits, part.data_ptr(),
+             dst.data_ptr() + 4 * dstoff, sn, sk, sj, int(accum), float(scale), stream())
+        return
     call("ensvs_conv_wgrad", dy.data_ptr() + 4 * dyoff, ldy, x.data_ptr() + 4 * xoff, ldx,
          ptr(radd), radd_ld, B, Tout, Tin, N, K, taps, dil, shift0, pad, splits,
          part.data_ptr(), dst.data_ptr() + 4 * dstoff, sn, sk, sj, int(accum), float(scale),

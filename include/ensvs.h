@@ -77,6 +77,13 @@ int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx, const fl
                      int shift0, int pad, int splits, float* part, float* dst, long long sn,
                      long long sk, long long sj, int accum, float scale, int dtype, void* stream);
 
+/* ensvs_conv_wgrad with bf16 operands (dy, x already rounded to bf16, radd folded into x;
+ * N, K, ldy, ldx multiples of 8): identical bits, operands staged by global_load_lds. */
+int ensvs_conv_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, int B, int Tout,
+                          int Tin, int N, int K, int taps, int dil, int shift0, int pad, int splits,
+                          float* part, float* dst, long long sn, long long sk, long long sj,
+                          int accum, float scale, void* stream);
+
 /* Batched weight repack (descs is a DEVICE array). */
 int ensvs_pack_weights(const ensvs_pack_desc* descs, int n, int max_elems, void* stream);
 

@@ -439,6 +439,17 @@ __global__ void axpy_kernel(float* __restrict__ y, const float* __restrict__ x, 
   GRID_LOOP(i, n) y[i] += a * x[i];
 }
 
+// y[g*ystride + j] += a * x[g*xstride + j], g < count, j < n: one launch for the same-shaped
+// parameters of several layers (their gradients sit at a constant stride in the flat buffer)
+__global__ void axpy_strided_kernel(float* __restrict__ y, long long ystride,
+                                    const float* __restrict__ x, long long xstride, float a,
+                                    int n, int count) {
+  GRID_LOOP(i, (long long)n * count) {
+    const long long g = i / n, j = i - g * n;
+    y[g * ystride + j] += a * x[g * xstride + j];
+  }
+}
+
 __global__ void axpby_kernel(float* __restrict__ y, float a, const float* __restrict__ x, float b,
                              long long n) {
   GRID_LOOP(i, n) y[i] = a * y[i] + b * x[i];
@@ -722,6 +733,13 @@ ENSVS_API int ensvs_copy_cols(const float* src, int lds, float* dst, int ldd, lo
 
 ENSVS_API int ensvs_axpy(float* y, const float* x, float a, long long n, void* stream) {
   LAUNCH(axpy_kernel, n, y, x, a, n);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_axpy_strided(float* y, long long ystride, const float* x, long long xstride,
+                                 float a, int n, int count, void* stream) {
+  if (n <= 0 || count <= 0) return ENSVS_OK;
+  LAUNCH(axpy_strided_kernel, (long long)n * count, y, ystride, x, xstride, a, n, count);
   return ENSVS_OK;
 }
 

@@ -234,6 +234,9 @@ class DiffNet(nn.Module):
         dss = empty(M, C, device=dev)  # d(skip_l) = dS / sqrt(L)  (same for every block)
         K.gemm([K.Seg(dp1, C, C, pk["skip^T"], T)], B, T, C, pk.bwd, dss, C)
         dssb = K.cast_bf16(dss, C, C, M) if b16 else None
+        # d(skip_l) is the same for every block: its bias-gradient column sums once
+        tmp_dss = empty(C, device=dev)
+        K.colsum(dss, C, M, C, tmp_dss)
         dx = dxb = None
         dpre_all = empty(M, L * 2 * C, device=dev)
         dpre_b = bf(M, L * 2 * C) if b16 else None
@@ -268,7 +271,6 @@ class DiffNet(nn.Module):
                        row0=0)
                     _colsum_off(dx, C, M, C, w_o.bias, 0, SQRT1_2)
                 wg(w_o.weight, dssb if bw else dss, C, zsrc, C, B, T, T, C, C, row0=C)
-                _colsum_off(dss, C, M, C, w_o.bias, C, 1.0)
                 # weight grads of the gate GEMM
                 if bw:
                     wg(blk.dilated_conv.weight, dpre_b, L * 2 * C, st["XB"][l], C, B, T, T,
@@ -281,12 +283,6 @@ class DiffNet(nn.Module):
                        radd_ld=L * C, dyoff=l * 2 * C)
                     wg(blk.conditioner_projection.weight, dpre_all, L * 2 * C, st["cond"],
                        st["ldc"], B, T, T, 2 * C, E, dyoff=l * 2 * C)
-                tmpb = empty(2 * C, device=dev)
-                K.colsum(dpre_all, L * 2 * C, M, 2 * C, tmpb, yoff=l * 2 * C)
-                call("ensvs_axpy", grad_of(blk.dilated_conv.bias).data_ptr(), tmpb.data_ptr(),
-                     1.0, 2 * C, Ly.stream())
-                call("ensvs_axpy", grad_of(blk.conditioner_projection.bias).data_ptr(),
-                     tmpb.data_ptr(), 1.0, 2 * C, Ly.stream())
                 # diffusion projection (per-sequence rows)
                 dpj = blk.diffusion_projection
                 wg(dpj.weight, dd_all, L * C, st["d"], C, 1, B, B, C, C, dyoff=l * C)
@@ -303,6 +299,17 @@ class DiffNet(nn.Module):
                     call("ensvs_axpby_to", dxn.data_ptr(), dx.data_ptr(), SQRT1_2, dy.data_ptr(),
                          1.0, M * C, Ly.stream())
                 dx = dxn
+        # bias gradients of every block in a few launches: the gate biases (dilated conv and
+        # conditioner share the column sums of d(pre)) and the skip half of the output
+        # projection bias (the same dss column sums for every block)
+        with aux.run():
+            tmp_pre = empty(L * 2 * C, device=dev)
+            K.colsum(dpre_all, L * 2 * C, M, L * 2 * C, tmp_pre)
+            blocks = self.residual_layers
+            _axpy_blocks([grad_of(b.dilated_conv.bias) for b in blocks], tmp_pre, 2 * C, 2 * C)
+            _axpy_blocks([grad_of(b.conditioner_projection.bias) for b in blocks], tmp_pre,
+                         2 * C, 2 * C)
+            _axpy_blocks([grad_of(b.output_projection.bias)[C:] for b in blocks], tmp_dss, 0, C)
         # conditioner input grad of all blocks at once
         dcond = empty(M, E, device=dev)
         K.gemm([K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, L * 2 * C, pk["condT"], T)],
@@ -334,6 +341,19 @@ class DiffNet(nn.Module):
     def forward(self, spec, diffusion_step, cond):
         """spec (B, 1, M, T), diffusion_step (B,), cond (B, E, T) -> (B, 1, M, T)."""
         return _DiffNetFn.apply(self, spec, diffusion_step, cond, self.skip_projection.weight)
+
+
+def _axpy_blocks(dsts, x, xstride, n):
+    """dsts[g][:n] += x[g*xstride : g*xstride + n] -- one launch when the destinations sit
+    at a constant stride (the same parameter of every residual block in the flat buffer)."""
+    ptrs = [d.data_ptr() for d in dsts]
+    steps = {(b - a) // 4 for a, b in zip(ptrs, ptrs[1:])}
+    if len(steps) <= 1 and all((b - a) % 4 == 0 for a, b in zip(ptrs, ptrs[1:])):
+        call("ensvs_axpy_strided", ptrs[0], steps.pop() if steps else 0, x.data_ptr(),
+             xstride, 1.0, n, len(dsts), Ly.stream())
+        return
+    for g, d in enumerate(dsts):
+        call("ensvs_axpy", d.data_ptr(), x.data_ptr() + 4 * g * xstride, 1.0, n, Ly.stream())
 
 
 def _colsum_off(dy, ld, M, N, param, off, scale):

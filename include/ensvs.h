@@ -208,6 +208,10 @@ int ensvs_rng_advance(void* stream);
 int ensvs_copy_cols(const float* src, int lds, float* dst, int ldd, long long M, int n,
                     void* stream);
 int ensvs_axpy(float* y, const float* x, float a, long long n, void* stream);
+/* y[g*ystride + j] += a * x[g*xstride + j] for g < count, j < n (same-shaped parameters of
+ * several layers, e.g. the 20 DiffNet residual blocks' bias gradients, in one launch). */
+int ensvs_axpy_strided(float* y, long long ystride, const float* x, long long xstride, float a,
+                       int n, int count, void* stream);
 /* y = a*y + b*x ; y *= x (dropout masks) */
 int ensvs_axpby(float* y, float a, const float* x, float b, long long n, void* stream);
 /* out = a*y + b*x, bitwise the same as ensvs_axpby but out of place. */

@@ -58,6 +58,12 @@ struct GemmArgs {
   float alpha;
   int C;
   int vec_out;  // Y / aux0 / aux1 rows 16-B aligned with ld % 4 == 0: 16-B epilogue stores
+  // optional bf16 copy of what is written to Y (LDS-staged epilogue only):
+  // ybf[row*ybf_ld + col] = bf16(y + ybf_radd[(row / Tout)*ybf_radd_ld + col]) -- the next
+  // GEMM's operand, rounded exactly as ensvs_cast_bf16 would, without the extra pass
+  __bf16* ybf;
+  const float* ybf_radd;
+  int ybf_ld, ybf_radd_ld;
 };
 
 template <typename T>
@@ -123,6 +129,15 @@ __device__ __forceinline__ void xcd_tile(int& m0, int& n0) {
 
 // ---------------------------------------------------------------- epilogue
 // Shared by both forward kernels: acc holds the wave's 64x64 sub-tile (4x4 MFMA tiles).
+// d(gate), d(filter) of z = sigmoid(g) * tanh(f); contraction off so the per-element and the
+// LDS-staged epilogues round identically.
+__device__ __forceinline__ void gate_bwd_(float dz, float g, float f, float& dg, float& df) {
+#pragma clang fp contract(off)
+  const float sg = sigmoidf_(g), th = tanhf(f);
+  dg = dz * th * sg * (1.f - sg);
+  df = dz * sg * (1.f - th * th);
+}
+
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], int m0,
                                               int n0, int wr, int wc, int lane) {
   const int rbase = m0 + wr * 64 + (lane >> 4) * 4;
@@ -177,7 +192,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4]
           else if (a.relu == 2) v = sigmoidf_(v);
           *y = v;
         } else if (a.epi == EPI_ADDSCALE) {
-          v += a.alpha * a.aux1[(long long)row * a.ld1 + col];
+          v = __builtin_fmaf(a.alpha, a.aux1[(long long)row * a.ld1 + col], v);
           *y = a.relu == 1 ? fmaxf(v, 0.f) : v;
         } else if (a.epi == EPI_RELU_MASK) {
           v = a.aux1[(long long)row * a.ld1 + col] > 0.f ? v : 0.f;
@@ -185,9 +200,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4]
         } else if (a.epi == EPI_GATE_BWD) {
           const float g = a.aux1[(long long)row * a.ld1 + col];
           const float f = a.aux1[(long long)row * a.ld1 + a.C + col];
-          const float sg = sigmoidf_(g), th = tanhf(f);
-          a.Y[(long long)row * a.ldy + col] = v * th * sg * (1.f - sg);
-          a.Y[(long long)row * a.ldy + a.C + col] = v * sg * (1.f - th * th);
+          float dg, df;
+          gate_bwd_(v, g, f, dg, df);
+          a.Y[(long long)row * a.ldy + col] = dg;
+          a.Y[(long long)row * a.ldy + a.C + col] = df;
         }
       }
   }
@@ -203,6 +219,13 @@ constexpr int EPI_LDS = BM * EP * 4;
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *(f32x4*)p = v; }
+// bf16 shadow of 4 consecutive outputs (row m, columns col..col+3), see GemmArgs::ybf
+__device__ __forceinline__ void shadow4(const GemmArgs& a, int m, int col, f32x4 v) {
+  if (!a.ybf) return;
+  if (a.ybf_radd) v += ld4(a.ybf_radd + (long long)(m / a.Tout) * a.ybf_radd_ld + col);
+  *(bf16x4*)(a.ybf + (long long)m * a.ybf_ld + col) =
+      bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
 
 __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[4][4], int m0,
                                                   int n0, int wr, int wc, int lane, int tid,
@@ -243,6 +266,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = sigmoidf_(g[e]) * tanhf(f[e]);
         st4(a.Y + (long long)m * a.ldy + c, z);
+        shadow4(a, m, c, z);
       } else if (a.epi == EPI_GATE_TS) {
         f32x4 z;
 #pragma unroll
@@ -254,6 +278,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
 #pragma unroll
         for (int e = 0; e < 4; ++e) y[e] = (xr[e] + g[e]) * 0.70710678118654752f;
         st4(a.Y + (long long)m * a.ldy + c, y);
+        shadow4(a, m, c, y);
         float* skp = a.aux0 + (long long)m * a.ld0 + c;
         if (a.accum) {
           const f32x4 s0 = ld4(skp);
@@ -289,11 +314,12 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
           else if (a.relu == 2) v[e] = sigmoidf_(v[e]);
         }
         st4(y, v);
+        shadow4(a, m, col, v);
       } else if (a.epi == EPI_ADDSCALE) {
         const f32x4 x1 = ld4(a.aux1 + (long long)m * a.ld1 + col);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] += a.alpha * x1[e];
+          v[e] = __builtin_fmaf(a.alpha, x1[e], v[e]);
           v[e] = a.relu == 1 ? fmaxf(v[e], 0.f) : v[e];
         }
         st4(y, v);
@@ -309,12 +335,15 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         f32x4 dg, df;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float sg = sigmoidf_(g[e]), th = tanhf(f[e]);
-          dg[e] = v[e] * th * sg * (1.f - sg);
-          df[e] = v[e] * sg * (1.f - th * th);
+          float t0, t1;
+          gate_bwd_(v[e], g[e], f[e], t0, t1);
+          dg[e] = t0;
+          df[e] = t1;
         }
         st4(y, dg);
         st4(y + a.C, df);
+        shadow4(a, m, col, dg);
+        shadow4(a, m, a.C + col, df);
       }
     } else {
       for (int e = 0; e < ne; ++e) {
@@ -326,7 +355,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
           else if (a.relu == 2) w = sigmoidf_(w);
           *ye = w;
         } else if (a.epi == EPI_ADDSCALE) {
-          w += a.alpha * a.aux1[(long long)m * a.ld1 + col + e];
+          w = __builtin_fmaf(a.alpha, a.aux1[(long long)m * a.ld1 + col + e], w);
           *ye = a.relu == 1 ? fmaxf(w, 0.f) : w;
         } else if (a.epi == EPI_RELU_MASK) {
           w = a.aux1[(long long)m * a.ld1 + col + e] > 0.f ? w : 0.f;
@@ -334,9 +363,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         } else if (a.epi == EPI_GATE_BWD) {
           const float g = a.aux1[(long long)m * a.ld1 + col + e];
           const float f = a.aux1[(long long)m * a.ld1 + a.C + col + e];
-          const float sg = sigmoidf_(g), th = tanhf(f);
-          ye[0] = w * th * sg * (1.f - sg);
-          ye[a.C] = w * sg * (1.f - th * th);
+          gate_bwd_(w, g, f, ye[0], ye[a.C]);
         }
       }
     }
@@ -636,7 +663,7 @@ __device__ __forceinline__ TapPtrs tap_ptrs(const SegU S, int j, int Npad, int n
 }
 
 template <int STAGES>
-__global__ __launch_bounds__(NTHR) void conv_gemm_b16_kernel(const GemmArgs a) {
+__global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a) {
   static_assert(STAGES >= 2 && STAGES <= 3, "stages");
   constexpr int TILE = BM * BK2 * 2;  // bytes of one operand image (16 KB)
   constexpr int GL = 8;               // glds per thread per tile (4 A rows + 4 B rows)
@@ -746,7 +773,8 @@ __global__ __launch_bounds__(NTHR) void conv_gemm_b16_kernel(const GemmArgs a) {
   }
 #undef ISSUE
 #undef TAP_PTRS
-  gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
+  if (a.vec_out) gemm_epilogue_lds(a, acc, m0, n0, wr, wc, lane, tid, smem);
+  else gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
 }
 
 // y[m][k] = bf16(x[m][k] + radd[m / T][k]) for the bf16-activation GEMM (8 elements per thread).
@@ -1344,22 +1372,14 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
   return ENSVS_OK;
 }
 
-ENSVS_API int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N,
-                                    int Npad, const void* W, const float* bias, float* Y, int ldy,
-                                    int epi, int relu, int accum, float* aux0, int ld0,
-                                    const float* aux1, int ld1, float alpha, int C, int stages,
-                                    void* stream) {
-  GemmArgs a{};
-  const int rc = fill_gemm_args(a, segs, nseg, B, Tout, N, Npad, W, bias, Y, ldy, epi, relu,
-                                accum, aux0, ld0, aux1, ld1, alpha, C);
-  if (rc != ENSVS_OK) return rc;
+static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, int Npad,
+                      const void* W, int stages, hipStream_t st) {
   for (int s = 0; s < nseg; ++s) {
     const ensvs_conv_seg& g = segs[s];
     if (g.radd || g.pd || g.K % 8 || g.ld % 8 || ((uintptr_t)g.x & 15)) return ENSVS_E_ARG;
   }
   if (((uintptr_t)W & 15)) return ENSVS_E_ARG;
   dim3 grid(cdiv(a.M, BM), Npad / BN);
-  hipStream_t st = (hipStream_t)stream;
   for (int s = 0; s < nseg; ++s) {  // 32-bit element offsets inside the kernel
     const ensvs_conv_seg& g = segs[s];
     if ((long long)B * g.Tin * g.ld >= (1ll << 31) ||
@@ -1386,6 +1406,44 @@ ENSVS_API int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B,
   }
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N,
+                                    int Npad, const void* W, const float* bias, float* Y, int ldy,
+                                    int epi, int relu, int accum, float* aux0, int ld0,
+                                    const float* aux1, int ld1, float alpha, int C, int stages,
+                                    void* stream) {
+  GemmArgs a{};
+  const int rc = fill_gemm_args(a, segs, nseg, B, Tout, N, Npad, W, bias, Y, ldy, epi, relu,
+                                accum, aux0, ld0, aux1, ld1, alpha, C);
+  if (rc != ENSVS_OK) return rc;
+  return launch_b16(a, segs, nseg, B, Npad, W, stages, (hipStream_t)stream);
+}
+
+// ensvs_conv_gemm_bf16a plus a bf16 copy of the output for the next GEMM (see GemmArgs::ybf).
+// Only the 16-B LDS-staged epilogue writes it: output rows must be 16-B aligned with
+// ld % 4 == 0 (and N % 4 == 0, C % 4 == 0), ybf rows 8-B aligned with ybf_ld % 4 == 0.
+ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, int B, int Tout,
+                                        int N, int Npad, const void* W, const float* bias,
+                                        float* Y, int ldy, int epi, int relu, int accum,
+                                        float* aux0, int ld0, const float* aux1, int ld1,
+                                        float alpha, int C, void* ybf, int ybf_ld,
+                                        const float* ybf_radd, int ybf_radd_ld, int stages,
+                                        void* stream) {
+  GemmArgs a{};
+  const int rc = fill_gemm_args(a, segs, nseg, B, Tout, N, Npad, W, bias, Y, ldy, epi, relu,
+                                accum, aux0, ld0, aux1, ld1, alpha, C);
+  if (rc != ENSVS_OK) return rc;
+  if (ybf) {
+    if (!a.vec_out || N % 4 || ybf_ld % 4 || ((uintptr_t)ybf & 7) ||
+        (ybf_radd && (ybf_radd_ld % 4 || ((uintptr_t)ybf_radd & 15))))
+      return ENSVS_E_ARG;
+    a.ybf = (__bf16*)ybf;
+    a.ybf_ld = ybf_ld;
+    a.ybf_radd = ybf_radd;
+    a.ybf_radd_ld = ybf_radd_ld;
+  }
+  return launch_b16(a, segs, nseg, B, Npad, W, stages, (hipStream_t)stream);
 }
 
 ENSVS_API int ensvs_cast_bf16(const float* x, int ldx, const float* radd, int radd_ld, int T,

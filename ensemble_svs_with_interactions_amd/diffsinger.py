@@ -155,6 +155,7 @@ class DiffNet(nn.Module):
         b16 = K.bf16_operands(pk.fwd, M)
         condb = K.cast_bf16(cond, ldc, E, M) if b16 else None
         XB, ZB = [], []
+        xb = None
         x = empty(M, C, device=dev)
         K.gemm([K.Seg(xin, ldx, Mc, pk["in"], T)], B, T, C, pk.fwd, x, C, relu=True,
                **pk.bias_ptr_args("in.b"))
@@ -165,17 +166,24 @@ class DiffNet(nn.Module):
             if save or z is None:
                 z = empty(M, C, device=dev)
                 gf = empty(M, 2 * C, device=dev)
-            xb = K.cast_bf16(x, C, C, M, radd=ds[:, l * C:], radd_ld=L * C, T=T) if b16 else None
-            self._gate_gemm(l, x, cond, ldc, ds, B, T, z, gf, condb=condb, xb=xb)
-            zb = K.cast_bf16(z, C, C, M) if b16 else None
+            if b16 and l == 0:  # later blocks get x + d_l from the previous epilogue
+                xb = K.cast_bf16(x, C, C, M, radd=ds, radd_ld=L * C, T=T)
+            zb = empty(M, C, device=dev, dtype=torch.bfloat16) if b16 else None
+            self._gate_gemm(l, x, cond, ldc, ds, B, T, z, gf, condb=condb,
+                            xb=xb if b16 else None, zb=zb)
             if save and b16:
                 XB.append(xb)
                 ZB.append(zb)
             xn = empty(M, C, device=dev) if save else x
+            nxt = b16 and l + 1 < L
+            xbn = empty(M, C, device=dev, dtype=torch.bfloat16) if nxt else None
             K.gemm([K.Seg(z, C, C, pk[f"out{l}"], T) if zb is None else
                     K.Seg(zb, C, C, pk[f"out{l}"], T)], B, T, 2 * C, pk.fwd, xn, C,
                    epi=_lib.EPI_RESSKIP, aux0=S, ld0=C, aux1=x, ld1=C, accum=l > 0,
-                   alpha=1.0 / math.sqrt(L), C=C, **pk.bias_ptr_args(f"o{l}.b"))
+                   alpha=1.0 / math.sqrt(L), C=C, ybf=xbn, ybf_ld=C,
+                   ybf_radd=ds[:, (l + 1) * C:] if nxt else None, ybf_radd_ld=L * C,
+                   **pk.bias_ptr_args(f"o{l}.b"))
+            xb = xbn
             if save:
                 Z.append(z)
                 GF.append(gf)
@@ -194,9 +202,9 @@ class DiffNet(nn.Module):
                       ds=ds, cond=cond, ldc=ldc, B=B, T=T, XB=XB, ZB=ZB, condb=condb)
         return out, st
 
-    def _gate_gemm(self, l, x, cond, ldc, ds, B, T, z, gf, condb=None, xb=None):
+    def _gate_gemm(self, l, x, cond, ldc, ds, B, T, z, gf, condb=None, xb=None, zb=None):
         """Block l's fused gate GEMM (dilated conv + conditioner + sigmoid*tanh); condb /
-        xb: cond and x + d_l already rounded to bf16."""
+        xb: cond and x + d_l already rounded to bf16; zb receives bf16(z)."""
         pk = self._packs
         C, L, E = self.C, len(self.residual_layers), self.E
         dl = self.residual_layers[l].dilation
@@ -206,7 +214,7 @@ class DiffNet(nn.Module):
                 K.Seg(cond, ldc, E, pk[f"cond{l}"], T) if condb is None else
                 K.Seg(condb, E, E, pk[f"cond{l}"], T)]
         K.gemm(segs, B, T, 2 * C, pk.fwd, z, C, epi=_lib.EPI_GATE, aux0=gf, ld0=2 * C, C=C,
-               **pk.bias_ptr_args(f"g{l}.b"))
+               ybf=zb, ybf_ld=C, **pk.bias_ptr_args(f"g{l}.b"))
 
     def _bwd(self, st, dout):
         """dout (B*T, in_dim) -> dcond (B*T, E); parameter grads accumulated."""
@@ -251,15 +259,14 @@ class DiffNet(nn.Module):
             if dx is not None:
                 segs.insert(0, K.Seg(dxb if b16 else dx, C, C, pk[f"out{l}^Tres"], T))
             K.gemm(segs, B, T, C, pk.bwd, dpre_all, L * 2 * C, yoff=l * 2 * C,
-                   epi=_lib.EPI_GATE_BWD, aux1=st["GF"][l], ld1=2 * C, C=C)
-            if b16:
-                K.cast_bf16(dpre_all, L * 2 * C, 2 * C, M, xoff=l * 2 * C, out=dpre_b,
-                            out_ld=L * 2 * C, out_off=l * 2 * C)
+                   epi=_lib.EPI_GATE_BWD, aux1=st["GF"][l], ld1=2 * C, C=C,
+                   ybf=dpre_b[:, l * 2 * C:] if b16 else None, ybf_ld=L * 2 * C)
             # dilated conv input grad (transposed, flipped taps)
             dy = empty(M, C, device=dev)
+            dyb = bf(M, C) if (dx is None and b16) else None
             K.gemm([K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, 2 * C, pk[f"dil{l}^T"], T,
-                          taps=3, dil=dl, shift0=-dl, xoff=l * 2 * C)], B, T, C, pk.bwd, dy, C)
-            dyb = K.cast_bf16(dy, C, C, M) if (dx is None and b16) else None
+                          taps=3, dil=dl, shift0=-dl, xoff=l * 2 * C)], B, T, C, pk.bwd, dy, C,
+                   ybf=dyb, ybf_ld=C)
             K.colsum(dy, C, T, C, dd_all, groups=B, ldo=L * C, outoff=l * C)
             with aux.run(*([t for t in (dss, dpre_all, dd_all, dx, dxb, dssb, dpre_b)
                             if t is not None])):

@@ -172,12 +172,34 @@ def cast_bf16(x, ld, K, rows, xoff=0, radd=None, radd_ld=0, T=1, out=None, out_l
 
 def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: int,
          bias=None, epi=_lib.EPI_PLAIN, relu=False, accum=False, aux0=None, ld0=0, aux1=None,
-         ld1=0, alpha=0.0, C=0, yoff=0, bias_off=0):
+         ld1=0, alpha=0.0, C=0, yoff=0, bias_off=0, ybf=None, ybf_ld=0, ybf_radd=None,
+         ybf_radd_ld=0):
     """One implicit-GEMM launch (bf16-operand kernel when the A panels are bf16 or worth a
-    cast pass, register-staged kernel otherwise)."""
+    cast pass, register-staged kernel otherwise).  ybf (bf16 tensor): also receives
+    bf16(y + ybf_radd[row // Tout]) of the Y values written (PLAIN / GATE / RESSKIP:
+    the Y columns; GATE_BWD: both halves) -- from the epilogue when it can, else by a cast."""
     arr = (ConvSeg * len(segs))()
     Npad = segs[0].ref.Npad
     a16 = _bf16_act_ok(segs, W, Npad, B * Tout)
+    if ybf is not None:
+        assert ybf.dtype == torch.bfloat16 and epi in (_lib.EPI_PLAIN, _lib.EPI_GATE,
+                                                       _lib.EPI_RESSKIP, _lib.EPI_GATE_BWD)
+        yp = Y.data_ptr() + 4 * yoff
+        vec = (yp % 16 == 0 and ldy % 4 == 0 and N % 4 == 0 and C % 4 == 0 and
+               all(t is None or (t.data_ptr() % 16 == 0 and ld % 4 == 0)
+                   for t, ld in ((aux0, ld0), (aux1, ld1))) and ybf.data_ptr() % 8 == 0 and
+               ybf_ld % 4 == 0 and (ybf_radd is None or (ybf_radd.data_ptr() % 16 == 0 and
+                                                         ybf_radd_ld % 4 == 0)))
+        if not (a16 and vec):
+            gemm(segs, B, Tout, N, W, Y, ldy, bias=bias, epi=epi, relu=relu, accum=accum,
+                 aux0=aux0, ld0=ld0, aux1=aux1, ld1=ld1, alpha=alpha, C=C, yoff=yoff,
+                 bias_off=bias_off)
+            # the same rounding by a cast pass over what was written
+            width = 2 * C if epi == _lib.EPI_GATE_BWD else (
+                C if epi in (_lib.EPI_GATE, _lib.EPI_RESSKIP) else N)
+            cast_bf16(Y, ldy, width, B * Tout, xoff=yoff, radd=ybf_radd, radd_ld=ybf_radd_ld,
+                      T=Tout, out=ybf, out_ld=ybf_ld)
+            return
     keep = []
     for i, s in enumerate(segs):
         assert s.ref.Npad == Npad and s.ref.taps == s.taps and s.ref.Kp >= s.K
@@ -198,13 +220,20 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
         d.K, d.taps, d.dil, d.shift0 = s.K, s.taps, s.dil, s.shift0
         d.pad, d.Tin, d.Kp = s.pad, s.Tin, s.ref.Kp
     bptr = None if bias is None else bias.data_ptr() + 4 * bias_off
+    yptr = Y.data_ptr() + 4 * yoff
+    if ybf is not None:
+        call("ensvs_conv_gemm_bf16a_out", ctypes.addressof(arr), len(segs), B, Tout, N,
+             Npad, W.buf.data_ptr(), bptr, yptr, ldy, epi, int(relu), int(accum), ptr(aux0),
+             ld0, ptr(aux1), ld1, float(alpha), C, ybf.data_ptr(), ybf_ld, ptr(ybf_radd),
+             ybf_radd_ld, BF16_ACT["stages"], stream())
+        return
     if a16:
         call("ensvs_conv_gemm_bf16a", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,
-             W.buf.data_ptr(), bptr, Y.data_ptr() + 4 * yoff, ldy, epi, int(relu), int(accum),
+             W.buf.data_ptr(), bptr, yptr, ldy, epi, int(relu), int(accum),
              ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, BF16_ACT["stages"], stream())
     else:
         call("ensvs_conv_gemm", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,
-             W.buf.data_ptr(), W.dtype, bptr, Y.data_ptr() + 4 * yoff, ldy, epi, int(relu),
+             W.buf.data_ptr(), W.dtype, bptr, yptr, ldy, epi, int(relu),
              int(accum), ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, stream())
 
 

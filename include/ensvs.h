@@ -67,6 +67,16 @@ int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B, int Tout,
                           const void* W, const float* bias, float* Y, int ldy, int epi, int relu,
                           int accum, float* aux0, int ld0, const float* aux1, int ld1, float alpha,
                           int C, int stages, void* stream);
+/* ensvs_conv_gemm_bf16a that also writes ybf[row*ybf_ld + col] = bf16(y + ybf_radd[(row /
+ * Tout)*ybf_radd_ld + col]) for every output it writes (the next GEMM's operand, rounded as
+ * ensvs_cast_bf16 would, without that pass).  Needs 16-B output rows (ld % 4 == 0) and
+ * N % 4 == 0; returns ENSVS_E_ARG otherwise. */
+int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N,
+                              int Npad, const void* W, const float* bias, float* Y, int ldy,
+                              int epi, int relu, int accum, float* aux0, int ld0,
+                              const float* aux1, int ld1, float alpha, int C, void* ybf,
+                              int ybf_ld, const float* ybf_radd, int ybf_radd_ld, int stages,
+                              void* stream);
 /* y[m][k] = bf16(x[m][k] + radd[m / T][k]) (radd optional), K % 8 == 0. */
 int ensvs_cast_bf16(const float* x, int ldx, const float* radd, int radd_ld, int T, long long M,
                     int K, void* y, int ldy, void* stream);

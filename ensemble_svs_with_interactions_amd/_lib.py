@@ -107,6 +107,9 @@ SIGNATURES = {
     "ensvs_copy_cols": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_vp],
     "ensvs_axpy": [c_vp, c_vp, c_float, c_ll, c_vp],
     "ensvs_axpy_strided": [c_vp, c_ll, c_vp, c_ll, c_float, c_int, c_int, c_vp],
+    "ensvs_axpy_blocks2d": [c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_float, c_int, c_int, c_int,
+                            c_vp],
+    "ensvs_res_bias_grad": [c_vp, c_int, c_int, c_vp, c_ll, c_float, c_vp],
     "ensvs_axpby": [c_vp, c_float, c_vp, c_float, c_ll, c_vp],
     "ensvs_axpby_to": [c_vp, c_vp, c_float, c_vp, c_float, c_ll, c_vp],
     "ensvs_axpby_to_bf16": [c_vp, c_vp, c_vp, c_float, c_vp, c_float, c_ll, c_vp],

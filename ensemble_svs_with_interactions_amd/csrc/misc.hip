@@ -450,6 +450,32 @@ __global__ void axpy_strided_kernel(float* __restrict__ y, long long ystride,
   }
 }
 
+// y[g*ystride + r*yld + c] += a * x[g*xstride + r*xld + c]: one 2-D block per destination
+__global__ void axpy_blocks2d_kernel(float* __restrict__ y, long long ystride, long long yld,
+                                     const float* __restrict__ x, long long xstride,
+                                     long long xld, float a, int rows, int cols, int count) {
+  GRID_LOOP(i, (long long)rows * cols * count) {
+    const long long per = (long long)rows * cols;
+    const long long g = i / per, rc = i - g * per;
+    const long long r = rc / cols, c = rc - r * cols;
+    y[g * ystride + r * yld + c] += a * x[g * xstride + r * xld + c];
+  }
+}
+
+// DiffNet residual-half output-projection bias grads from the per-block column sums of the
+// dilated-conv input grads: s_l = colsum(dx_l) = a * s_l+1 + cdy[l], bias_l-1 += a * s_l
+// (dx_l = a * dx_l+1 + dy_l, a = 1/sqrt2; block l-1's residual output feeds dx_l).
+__global__ void res_bias_grad_kernel(const float* __restrict__ cdy, int L, int C,
+                                     float* __restrict__ dst, long long dstride, float a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int l = L - 1; l >= 1; --l) {
+    s = a * s + cdy[(long long)l * C + c];
+    dst[(long long)(l - 1) * dstride + c] += a * s;
+  }
+}
+
 __global__ void axpby_kernel(float* __restrict__ y, float a, const float* __restrict__ x, float b,
                              long long n) {
   GRID_LOOP(i, n) y[i] = a * y[i] + b * x[i];
@@ -740,6 +766,24 @@ ENSVS_API int ensvs_axpy_strided(float* y, long long ystride, const float* x, lo
                                  float a, int n, int count, void* stream) {
   if (n <= 0 || count <= 0) return ENSVS_OK;
   LAUNCH(axpy_strided_kernel, (long long)n * count, y, ystride, x, xstride, a, n, count);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_axpy_blocks2d(float* y, long long ystride, long long yld, const float* x,
+                                  long long xstride, long long xld, float a, int rows, int cols,
+                                  int count, void* stream) {
+  if (rows <= 0 || cols <= 0 || count <= 0) return ENSVS_OK;
+  LAUNCH(axpy_blocks2d_kernel, (long long)rows * cols * count, y, ystride, yld, x, xstride, xld,
+         a, rows, cols, count);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_res_bias_grad(const float* cdy, int L, int C, float* dst, long long dstride,
+                                  float a, void* stream) {
+  if (L <= 1 || C <= 0) return ENSVS_OK;
+  hipLaunchKernelGGL(res_bias_grad_kernel, dim3((C + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, cdy, L, C, dst, dstride, a);
+  ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
 

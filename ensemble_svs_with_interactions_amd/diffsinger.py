@@ -12,8 +12,11 @@ A DiffNet residual block (denoiser.py:54-66) is two MFMA GEMMs:
      at pack time so both land in the same lane);
   2. 1x1 output projection -> residual/skip, with (x + r)/sqrt2 and the skip sum
      (pre-scaled by 1/sqrt(L)) in the epilogue.
-Backward runs the transposed GEMMs, and the conditioner input-gradient of all L
-blocks is ONE GEMM over the concatenated pre-activation gradients (K = 2*C*L).
+Backward runs the transposed GEMMs; the conditioner input-gradient of all L
+blocks is ONE GEMM over the concatenated pre-activation gradients (K = 2*C*L), and so
+are the weight gradients whose second operand every block shares (conditioner: cond;
+skip half of the output projection: dss; diffusion projection: d) and every bias
+gradient -- one reduction over all blocks, scattered into the blocks' parameters.
 """
 import math
 
@@ -162,23 +165,34 @@ class DiffNet(nn.Module):
         S = empty(M, C, device=dev)
         X, Z, GF = [x], [], []
         z = gf = None
+        # training: the z of all blocks side by side (row stride L*C), so the backward
+        # takes the skip half of every output-projection weight gradient in one GEMM
+        ldz = L * C if save else C
+        if save:
+            Zall = empty(M, L * C, device=dev)
+            ZBall = empty(M, L * C, device=dev, dtype=torch.bfloat16) if b16 else None
         for l, blk in enumerate(self.residual_layers):
-            if save or z is None:
+            if save:
+                z = Zall[:, l * C:]
+                gf = empty(M, 2 * C, device=dev)
+            elif z is None:
                 z = empty(M, C, device=dev)
                 gf = empty(M, 2 * C, device=dev)
             if b16 and l == 0:  # later blocks get x + d_l from the previous epilogue
                 xb = K.cast_bf16(x, C, C, M, radd=ds, radd_ld=L * C, T=T)
-            zb = empty(M, C, device=dev, dtype=torch.bfloat16) if b16 else None
+            zb = None
+            if b16:
+                zb = ZBall[:, l * C:] if save else empty(M, C, device=dev, dtype=torch.bfloat16)
             self._gate_gemm(l, x, cond, ldc, ds, B, T, z, gf, condb=condb,
-                            xb=xb if b16 else None, zb=zb)
+                            xb=xb if b16 else None, zb=zb, ldz=ldz)
             if save and b16:
                 XB.append(xb)
                 ZB.append(zb)
             xn = empty(M, C, device=dev) if save else x
             nxt = b16 and l + 1 < L
             xbn = empty(M, C, device=dev, dtype=torch.bfloat16) if nxt else None
-            K.gemm([K.Seg(z, C, C, pk[f"out{l}"], T) if zb is None else
-                    K.Seg(zb, C, C, pk[f"out{l}"], T)], B, T, 2 * C, pk.fwd, xn, C,
+            K.gemm([K.Seg(z, ldz, C, pk[f"out{l}"], T) if zb is None else
+                    K.Seg(zb, ldz, C, pk[f"out{l}"], T)], B, T, 2 * C, pk.fwd, xn, C,
                    epi=_lib.EPI_RESSKIP, aux0=S, ld0=C, aux1=x, ld1=C, accum=l > 0,
                    alpha=1.0 / math.sqrt(L), C=C, ybf=xbn, ybf_ld=C,
                    ybf_radd=ds[:, (l + 1) * C:] if nxt else None, ybf_radd_ld=L * C,
@@ -199,10 +213,11 @@ class DiffNet(nn.Module):
         st = None
         if save:
             st = dict(xin=xin, ldx=ldx, X=X, Z=Z, GF=GF, S=S, p1=p1, demb=demb, m1=m1, mi=mi, d=d,
-                      ds=ds, cond=cond, ldc=ldc, B=B, T=T, XB=XB, ZB=ZB, condb=condb)
+                      ds=ds, cond=cond, ldc=ldc, B=B, T=T, XB=XB, ZB=ZB, condb=condb,
+                      Zall=Zall, ZBall=ZBall)
         return out, st
 
-    def _gate_gemm(self, l, x, cond, ldc, ds, B, T, z, gf, condb=None, xb=None, zb=None):
+    def _gate_gemm(self, l, x, cond, ldc, ds, B, T, z, gf, condb=None, xb=None, zb=None, ldz=0):
         """Block l's fused gate GEMM (dilated conv + conditioner + sigmoid*tanh); condb /
         xb: cond and x + d_l already rounded to bf16; zb receives bf16(z)."""
         pk = self._packs
@@ -213,8 +228,9 @@ class DiffNet(nn.Module):
                 K.Seg(xb, C, C, pk[f"dil{l}"], T, taps=3, dil=dl, shift0=-dl),
                 K.Seg(cond, ldc, E, pk[f"cond{l}"], T) if condb is None else
                 K.Seg(condb, E, E, pk[f"cond{l}"], T)]
-        K.gemm(segs, B, T, 2 * C, pk.fwd, z, C, epi=_lib.EPI_GATE, aux0=gf, ld0=2 * C, C=C,
-               ybf=zb, ybf_ld=C, **pk.bias_ptr_args(f"g{l}.b"))
+        ldz = ldz or C
+        K.gemm(segs, B, T, 2 * C, pk.fwd, z, ldz, epi=_lib.EPI_GATE, aux0=gf, ld0=2 * C, C=C,
+               ybf=zb, ybf_ld=ldz, **pk.bias_ptr_args(f"g{l}.b"))
 
     def _bwd(self, st, dout):
         """dout (B*T, in_dim) -> dcond (B*T, E); parameter grads accumulated."""
@@ -246,6 +262,9 @@ class DiffNet(nn.Module):
         tmp_dss = empty(C, device=dev)
         K.colsum(dss, C, M, C, tmp_dss)
         dx = dxb = None
+        bw = b16 and len(st["XB"]) == L  # bf16 operands saved by the forward
+        zsrc = st["ZB"] if bw else st["Z"]
+        ldz = L * C
         dpre_all = empty(M, L * 2 * C, device=dev)
         dpre_b = bf(M, L * 2 * C) if b16 else None
         dd_all = empty(B, L * C, device=dev)
@@ -270,30 +289,20 @@ class DiffNet(nn.Module):
             K.colsum(dy, C, T, C, dd_all, groups=B, ldo=L * C, outoff=l * C)
             with aux.run(*([t for t in (dss, dpre_all, dd_all, dx, dxb, dssb, dpre_b)
                             if t is not None])):
+                # per-block weight gradients; the ones whose second operand is shared by
+                # every block (skip half of w_o, conditioner, diffusion projection) and
+                # all bias gradients are taken for all blocks at once after the loop
                 w_o = blk.output_projection
-                bw = b16 and len(st["XB"]) == L  # bf16 operands saved by the forward
-                zsrc = st["ZB"][l] if bw else st["Z"][l]
                 if dx is not None:
-                    wg(w_o.weight, dxb if bw else dx, C, zsrc, C, B, T, T, C, C, scale=SQRT1_2,
-                       row0=0)
-                    _colsum_off(dx, C, M, C, w_o.bias, 0, SQRT1_2)
-                wg(w_o.weight, dssb if bw else dss, C, zsrc, C, B, T, T, C, C, row0=C)
-                # weight grads of the gate GEMM
+                    wg(w_o.weight, dxb if bw else dx, C, zsrc[l], ldz, B, T, T, C, C,
+                       scale=SQRT1_2, row0=0)
                 if bw:
                     wg(blk.dilated_conv.weight, dpre_b, L * 2 * C, st["XB"][l], C, B, T, T,
                        2 * C, C, taps=3, dil=dl, shift0=-dl, dyoff=l * 2 * C)
-                    wg(blk.conditioner_projection.weight, dpre_b, L * 2 * C, st["condb"], E, B,
-                       T, T, 2 * C, E, dyoff=l * 2 * C)
                 else:
                     wg(blk.dilated_conv.weight, dpre_all, L * 2 * C, st["X"][l], C, B, T, T,
                        2 * C, C, taps=3, dil=dl, shift0=-dl, radd=st["ds"][:, l * C:],
                        radd_ld=L * C, dyoff=l * 2 * C)
-                    wg(blk.conditioner_projection.weight, dpre_all, L * 2 * C, st["cond"],
-                       st["ldc"], B, T, T, 2 * C, E, dyoff=l * 2 * C)
-                # diffusion projection (per-sequence rows)
-                dpj = blk.diffusion_projection
-                wg(dpj.weight, dd_all, L * C, st["d"], C, 1, B, B, C, C, dyoff=l * C)
-                cs(dd_all, L * C, B, C, dpj.bias, yoff=l * C)
             if dx is None:
                 dx, dxb = dy, dyb
             else:
@@ -306,17 +315,52 @@ class DiffNet(nn.Module):
                     call("ensvs_axpby_to", dxn.data_ptr(), dx.data_ptr(), SQRT1_2, dy.data_ptr(),
                          1.0, M * C, Ly.stream())
                 dx = dxn
-        # bias gradients of every block in a few launches: the gate biases (dilated conv and
-        # conditioner share the column sums of d(pre)) and the skip half of the output
-        # projection bias (the same dss column sums for every block)
+        # the block-shared weight gradients and every bias gradient, each one GEMM or
+        # reduction over all blocks, then scattered into the blocks' parameters:
+        #   w_o[C:]  += dss^T [z_0 .. z_L-1]        (C x L*C)
+        #   w_cond   += [dpre_0 .. dpre_L-1]^T cond  (L*2C x E)
+        #   w_dp     += dd^T d                       (L*C x C, per-sequence rows)
+        # biases: gate (dilated conv and conditioner share the d(pre) column sums), the skip
+        # half of w_o (the same dss sums for every block), the diffusion projection (the
+        # per-sequence dd sums), and the residual half of w_o: colsum(dx_l+1), with
+        # dx_l = dx_l+1 / sqrt2 + dy_l and colsum(dy_l) the sum of dd's rows.
+        blocks = self.residual_layers
+        g_w = lambda m: [grad_of(getattr(b, m).weight) for b in blocks]  # noqa: E731
+        g_b = lambda m: [grad_of(getattr(b, m).bias) for b in blocks]  # noqa: E731
         with aux.run():
+            zall = st["ZBall"] if bw else st["Zall"]
+            tw = empty(C, L * C, device=dev)
+            K.wgrad(dssb if bw else dss, C, zall, L * C, B, T, T, C, L * C, 1, 1, 0,
+                    _lib.PAD_ZERO, tw, L * C, 1, 1, dtype=engine_gemm_dtype())
+            _axpy_blocks2d([w[C:] for w in g_w("output_projection")], tw, C, L * C, C, C)
+            tc = empty(L * 2 * C, E, device=dev)
+            K.wgrad(dpre_b if bw else dpre_all, L * 2 * C, st["condb"] if bw else st["cond"],
+                    E if bw else st["ldc"], B, T, T, L * 2 * C, E, 1, 1, 0, _lib.PAD_ZERO, tc,
+                    E, 1, 1, dtype=engine_gemm_dtype())
+            _axpy_blocks(g_w("conditioner_projection"), tc, 2 * C * E, 2 * C * E)
+            tp = empty(L * C, C, device=dev)
+            K.wgrad(dd_all, L * C, st["d"], C, 1, B, B, L * C, C, 1, 1, 0, _lib.PAD_ZERO, tp,
+                    C, 1, 1, dtype=engine_gemm_dtype())
+            _axpy_blocks(g_w("diffusion_projection"), tp, C * C, C * C)
             tmp_pre = empty(L * 2 * C, device=dev)
             K.colsum(dpre_all, L * 2 * C, M, L * 2 * C, tmp_pre)
-            blocks = self.residual_layers
-            _axpy_blocks([grad_of(b.dilated_conv.bias) for b in blocks], tmp_pre, 2 * C, 2 * C)
-            _axpy_blocks([grad_of(b.conditioner_projection.bias) for b in blocks], tmp_pre,
-                         2 * C, 2 * C)
-            _axpy_blocks([grad_of(b.output_projection.bias)[C:] for b in blocks], tmp_dss, 0, C)
+            _axpy_blocks(g_b("dilated_conv"), tmp_pre, 2 * C, 2 * C)
+            _axpy_blocks(g_b("conditioner_projection"), tmp_pre, 2 * C, 2 * C)
+            _axpy_blocks([b[C:] for b in g_b("output_projection")], tmp_dss, 0, C)
+            tdd = empty(L * C, device=dev)
+            K.colsum(dd_all, L * C, B, L * C, tdd)
+            _axpy_blocks(g_b("diffusion_projection"), tdd, C, C)
+            if L > 1:
+                bo = g_b("output_projection")
+                step = _const_step(bo)
+                if step is None:  # parameters not in one flat buffer: a contiguous copy
+                    tb = torch.zeros(L - 1, 2 * C, device=dev)
+                    call("ensvs_res_bias_grad", tdd.data_ptr(), L, C, tb.data_ptr(), 2 * C,
+                         SQRT1_2, Ly.stream())
+                    _axpy_blocks(bo[:-1], tb, 2 * C, C)
+                else:
+                    call("ensvs_res_bias_grad", tdd.data_ptr(), L, C, bo[0].data_ptr(), step,
+                         SQRT1_2, Ly.stream())
         # conditioner input grad of all blocks at once
         dcond = empty(M, E, device=dev)
         K.gemm([K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, L * 2 * C, pk["condT"], T)],
@@ -348,6 +392,28 @@ class DiffNet(nn.Module):
     def forward(self, spec, diffusion_step, cond):
         """spec (B, 1, M, T), diffusion_step (B,), cond (B, E, T) -> (B, 1, M, T)."""
         return _DiffNetFn.apply(self, spec, diffusion_step, cond, self.skip_projection.weight)
+
+
+def _const_step(dsts):
+    """Element stride between consecutive destination tensors, None if not constant."""
+    ptrs = [d.data_ptr() for d in dsts]
+    steps = {b - a for a, b in zip(ptrs, ptrs[1:])}
+    if len(steps) > 1 or any(st % 4 for st in steps):
+        return None
+    return steps.pop() // 4 if steps else 0
+
+
+def _axpy_blocks2d(dsts, x, xstride, xld, rows, cols):
+    """dsts[g] (rows x cols, contiguous) += the rows x cols block of x at g*xstride with
+    row stride xld; one launch (the destinations sit at a constant stride)."""
+    step = _const_step(dsts)
+    if step is not None:
+        call("ensvs_axpy_blocks2d", dsts[0].data_ptr(), step, cols, x.data_ptr(), xstride, xld,
+             1.0, rows, cols, len(dsts), Ly.stream())
+        return
+    for g, d in enumerate(dsts):
+        call("ensvs_axpy_blocks2d", d.data_ptr(), 0, cols, x.data_ptr() + 4 * g * xstride, 0,
+             xld, 1.0, rows, cols, 1, Ly.stream())
 
 
 def _axpy_blocks(dsts, x, xstride, n):

@@ -222,6 +222,18 @@ int ensvs_axpy(float* y, const float* x, float a, long long n, void* stream);
  * several layers, e.g. the 20 DiffNet residual blocks' bias gradients, in one launch). */
 int ensvs_axpy_strided(float* y, long long ystride, const float* x, long long xstride, float a,
                        int n, int count, void* stream);
+/* y[g*ystride + r*yld + c] += a * x[g*xstride + r*xld + c] for g < count, r < rows, c < cols
+ * (per-block views of one all-blocks weight gradient, e.g. the skip half of the 20 DiffNet
+ * output projections taken as dss^T [z_0 .. z_19]; diffsinger.py:70-110 ResidualBlock). */
+int ensvs_axpy_blocks2d(float* y, long long ystride, long long yld, const float* x,
+                        long long xstride, long long xld, float a, int rows, int cols, int count,
+                        void* stream);
+/* DiffNet residual-half output-projection bias grads: with s_l = a*s_{l+1} + cdy[l*C + c]
+ * (s = column sums of d x_l, cdy[l] = column sums of the dilated-conv input grad of block l),
+ * dst[(l-1)*dstride + c] += a*s_l for l = L-1 .. 1.  Replaces the per-block bias reduction of
+ * autograd over diffsinger.py ResidualBlock.forward's output_projection. */
+int ensvs_res_bias_grad(const float* cdy, int L, int C, float* dst, long long dstride, float a,
+                        void* stream);
 /* y = a*y + b*x ; y *= x (dropout masks) */
 int ensvs_axpby(float* y, float a, const float* x, float b, long long n, void* stream);
 /* out = a*y + b*x, bitwise the same as ensvs_axpby but out of place. */

@@ -54,7 +54,8 @@ SIGNATURES = {
                               c_float, c_vp],
     "ensvs_conv_gemm_bf16a_out": [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                                   c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_float,
-                                  c_int, c_vp, c_int, c_vp, c_int, c_int, c_vp],
+                                  c_int, c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_vp],
+    "ensvs_tile_colsum": [c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "ensvs_cast_bf16": [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_int, c_vp, c_int, c_vp],
     "ensvs_conv_wgrad": [c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_ll, c_ll, c_int,

@@ -64,6 +64,11 @@ struct GemmArgs {
   __bf16* ybf;
   const float* ybf_radd;
   int ybf_ld, ybf_radd_ld;
+  // optional per-tile column sums of the accumulator (before bias / epilogue), LDS-staged
+  // epilogue only, M % BM == 0: csum[(m0 / BM) * csum_ld + col] = rows 0..63 + rows 64..127
+  // (each half summed in row order; ensvs_tile_colsum reproduces it for other paths)
+  float* csum;
+  int csum_ld;
 };
 
 template <typename T>
@@ -215,7 +220,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4]
 // a row: one 16-B load / store per operand instead of four 4-B accesses (the per-element
 // epilogue above is store-issue bound).  Same arithmetic per element as gemm_epilogue.
 constexpr int EP = 132;
-constexpr int EPI_LDS = BM * EP * 4;
+constexpr int EPI_LDS = BM * EP * 4 + BN * 4;  // + the column-sum exchange row
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *(f32x4*)p = v; }
@@ -242,6 +247,18 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
             acc[mt][nt][r];
   __syncthreads();
   const int M = a.M;
+  if (a.csum) {  // uniform: every thread reaches the barrier
+    static_assert(NTHR == 2 * BN, "column sums: two half-tile lanes per column");
+    float* xr = T + BM * EP;
+    const int col = tid & (BN - 1), h = tid / BN;
+    const float* tc = T + (h * (BM / 2)) * EP + col;
+    float cs = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < BM / 2; ++r) cs += tc[r * EP];
+    if (h) xr[col] = cs;
+    __syncthreads();
+    if (!h && n0 + col < a.N) a.csum[(long long)(m0 / BM) * a.csum_ld + n0 + col] = cs + xr[col];
+  }
   if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
     // this tile holds 64 output channels (gate/filter interleaved by 16 in the packed columns)
     for (int it = tid; it < BM * 16; it += NTHR) {
@@ -323,6 +340,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
           v[e] = a.relu == 1 ? fmaxf(v[e], 0.f) : v[e];
         }
         st4(y, v);
+        shadow4(a, m, col, v);
       } else if (a.epi == EPI_RELU_MASK) {
         const f32x4 x1 = ld4(a.aux1 + (long long)m * a.ld1 + col);
 #pragma unroll
@@ -1428,12 +1446,19 @@ ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, in
                                         float* Y, int ldy, int epi, int relu, int accum,
                                         float* aux0, int ld0, const float* aux1, int ld1,
                                         float alpha, int C, void* ybf, int ybf_ld,
-                                        const float* ybf_radd, int ybf_radd_ld, int stages,
-                                        void* stream) {
+                                        const float* ybf_radd, int ybf_radd_ld, float* csum,
+                                        int csum_ld, int stages, void* stream) {
   GemmArgs a{};
   const int rc = fill_gemm_args(a, segs, nseg, B, Tout, N, Npad, W, bias, Y, ldy, epi, relu,
                                 accum, aux0, ld0, aux1, ld1, alpha, C);
   if (rc != ENSVS_OK) return rc;
+  if (csum) {
+    if (!a.vec_out || a.M % BM || csum_ld < N ||
+        (epi != EPI_PLAIN && epi != EPI_ADDSCALE && epi != EPI_RELU_MASK))
+      return ENSVS_E_ARG;
+    a.csum = csum;
+    a.csum_ld = csum_ld;
+  }
   if (ybf) {
     if (!a.vec_out || N % 4 || ybf_ld % 4 || ((uintptr_t)ybf & 7) ||
         (ybf_radd && (ybf_radd_ld % 4 || ((uintptr_t)ybf_radd & 15))))
@@ -1444,6 +1469,34 @@ ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, in
     a.ybf_radd_ld = ybf_radd_ld;
   }
   return launch_b16(a, segs, nseg, B, Npad, W, stages, (hipStream_t)stream);
+}
+
+// The column sums of GemmArgs::csum for a Y written by any other path: per BM-row tile,
+// rows 0..63 then rows 64..127 each in row order, then the two halves added.
+__global__ __launch_bounds__(NTHR) void tile_colsum_kernel(const float* __restrict__ y, int ldy,
+                                                           int N, float* __restrict__ out,
+                                                           int ldo) {
+  __shared__ float xr[BN];
+  const int tid = threadIdx.x, col = tid & (BN - 1), h = tid / BN;
+  const int m0 = blockIdx.x * BM, n = blockIdx.y * BN + col;
+  float cs = 0.f;
+  if (n < N) {
+    const float* p = y + (long long)(m0 + h * (BM / 2)) * ldy + n;
+    for (int r = 0; r < BM / 2; ++r) cs += p[(long long)r * ldy];
+  }
+  if (h) xr[col] = cs;
+  __syncthreads();
+  if (!h && n < N) out[(long long)blockIdx.x * ldo + n] = cs + xr[col];
+}
+
+ENSVS_API int ensvs_tile_colsum(const float* y, int ldy, int M, int N, float* out, int ldo,
+                                void* stream) {
+  if (M <= 0 || N <= 0) return ENSVS_OK;
+  if (M % BM || ldo < N) return ENSVS_E_ARG;
+  hipLaunchKernelGGL(tile_colsum_kernel, dim3(M / BM, cdiv(N, BN)), dim3(NTHR), 0,
+                     (hipStream_t)stream, y, ldy, N, out, ldo);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
 }
 
 ENSVS_API int ensvs_cast_bf16(const float* x, int ldx, const float* radd, int radd_ld, int T,

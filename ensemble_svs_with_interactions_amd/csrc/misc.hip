@@ -478,7 +478,7 @@ __global__ void res_bias_grad_kernel(const float* __restrict__ cdy, int L, int C
 
 __global__ void axpby_kernel(float* __restrict__ y, float a, const float* __restrict__ x, float b,
                              long long n) {
-  GRID_LOOP(i, n) y[i] = a * y[i] + b * x[i];
+  GRID_LOOP(i, n) y[i] = __builtin_fmaf(a, y[i], b * x[i]);
 }
 
 // out = a * y + b * x (the same expression as axpby_kernel, out of place), and an
@@ -487,7 +487,7 @@ __global__ void axpby_to_kernel(float* __restrict__ out, __bf16* __restrict__ ou
                                 const float* __restrict__ y, float a, const float* __restrict__ x,
                                 float b, long long n) {
   GRID_LOOP(i, n) {
-    const float v = a * y[i] + b * x[i];
+    const float v = __builtin_fmaf(a, y[i], b * x[i]);  // = the GEMM ADDSCALE epilogue
     out[i] = v;
     if (outb) outb[i] = (__bf16)v;
   }

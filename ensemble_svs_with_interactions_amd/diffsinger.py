@@ -268,6 +268,10 @@ class DiffNet(nn.Module):
         dpre_all = empty(M, L * 2 * C, device=dev)
         dpre_b = bf(M, L * 2 * C) if b16 else None
         dd_all = empty(B, L * C, device=dev)
+        # whole 128-frame tiles per sequence: the dgrad GEMM's epilogue also takes dy's
+        # column sums per tile (dd_tiles), reduced per sequence once after the loop
+        fuse = T % K.BM == 0
+        dd_tiles = empty(M // K.BM, L * C, device=dev) if fuse else None
         # The dgrad chain (gate_bwd GEMM -> dilated-conv^T GEMM -> next block) stays on this
         # stream; each block's weight / bias gradients go to a trailing auxiliary stream.
         aux = AuxStream(dev)
@@ -281,12 +285,22 @@ class DiffNet(nn.Module):
                    epi=_lib.EPI_GATE_BWD, aux1=st["GF"][l], ld1=2 * C, C=C,
                    ybf=dpre_b[:, l * 2 * C:] if b16 else None, ybf_ld=L * 2 * C)
             # dilated conv input grad (transposed, flipped taps)
-            dy = empty(M, C, device=dev)
-            dyb = bf(M, C) if (dx is None and b16) else None
-            K.gemm([K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, 2 * C, pk[f"dil{l}^T"], T,
-                          taps=3, dil=dl, shift0=-dl, xoff=l * 2 * C)], B, T, C, pk.bwd, dy, C,
-                   ybf=dyb, ybf_ld=C)
-            K.colsum(dy, C, T, C, dd_all, groups=B, ldo=L * C, outoff=l * C)
+            tsegs = [K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, 2 * C, pk[f"dil{l}^T"], T,
+                           taps=3, dil=dl, shift0=-dl, xoff=l * 2 * C)]
+            if fuse:
+                # dx_l = dx_l+1 / sqrt2 + dy in the epilogue (ADDSCALE, bf16 copy alongside)
+                # and dy's 128-frame tile column sums for the per-sequence sums dd
+                xnew = empty(M, C, device=dev)
+                xnewb = bf(M, C) if b16 else None
+                ep = {} if dx is None else dict(epi=_lib.EPI_ADDSCALE, aux1=dx, ld1=C,
+                                                alpha=SQRT1_2)
+                K.gemm(tsegs, B, T, C, pk.bwd, xnew, C, ybf=xnewb, ybf_ld=C, csum=dd_tiles,
+                       csum_ld=L * C, csum_off=l * C, **ep)
+            else:
+                dy = empty(M, C, device=dev)
+                dyb = bf(M, C) if (dx is None and b16) else None
+                K.gemm(tsegs, B, T, C, pk.bwd, dy, C, ybf=dyb, ybf_ld=C)
+                K.colsum(dy, C, T, C, dd_all, groups=B, ldo=L * C, outoff=l * C)
             with aux.run(*([t for t in (dss, dpre_all, dd_all, dx, dxb, dssb, dpre_b)
                             if t is not None])):
                 # per-block weight gradients; the ones whose second operand is shared by
@@ -303,7 +317,9 @@ class DiffNet(nn.Module):
                     wg(blk.dilated_conv.weight, dpre_all, L * 2 * C, st["X"][l], C, B, T, T,
                        2 * C, C, taps=3, dil=dl, shift0=-dl, radd=st["ds"][:, l * C:],
                        radd_ld=L * C, dyoff=l * 2 * C)
-            if dx is None:
+            if fuse:
+                dx, dxb = xnew, xnewb
+            elif dx is None:
                 dx, dxb = dy, dyb
             else:
                 dxn = empty(M, C, device=dev)  # out of place: the aux stream still reads dx
@@ -315,6 +331,8 @@ class DiffNet(nn.Module):
                     call("ensvs_axpby_to", dxn.data_ptr(), dx.data_ptr(), SQRT1_2, dy.data_ptr(),
                          1.0, M * C, Ly.stream())
                 dx = dxn
+        if fuse:
+            K.colsum(dd_tiles, L * C, T // K.BM, L * C, dd_all, groups=B)
         # the block-shared weight gradients and every bias gradient, each one GEMM or
         # reduction over all blocks, then scattered into the blocks' parameters:
         #   w_o[C:]  += dss^T [z_0 .. z_L-1]        (C x L*C)

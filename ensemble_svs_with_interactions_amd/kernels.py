@@ -173,15 +173,44 @@ def cast_bf16(x, ld, K, rows, xoff=0, radd=None, radd_ld=0, T=1, out=None, out_l
 def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: int,
          bias=None, epi=_lib.EPI_PLAIN, relu=False, accum=False, aux0=None, ld0=0, aux1=None,
          ld1=0, alpha=0.0, C=0, yoff=0, bias_off=0, ybf=None, ybf_ld=0, ybf_radd=None,
-         ybf_radd_ld=0):
+         ybf_radd_ld=0, csum=None, csum_ld=0, csum_off=0):
     """One implicit-GEMM launch (bf16-operand kernel when the A panels are bf16 or worth a
     cast pass, register-staged kernel otherwise).  ybf (bf16 tensor): also receives
-    bf16(y + ybf_radd[row // Tout]) of the Y values written (PLAIN / GATE / RESSKIP:
-    the Y columns; GATE_BWD: both halves) -- from the epilogue when it can, else by a cast."""
+    bf16(y + ybf_radd[row // Tout]) of the Y values written (PLAIN / GATE / RESSKIP /
+    ADDSCALE: the Y columns; GATE_BWD: both halves) -- from the epilogue when it can, else
+    by a cast.  csum (fp32, B*Tout % 128 == 0, no bias / accum / relu): per 128-row tile
+    column sums of the accumulator into csum[tile * csum_ld + csum_off + n] -- from the
+    epilogue when it can, else by ensvs_tile_colsum (the same bits)."""
     arr = (ConvSeg * len(segs))()
     Npad = segs[0].ref.Npad
-    a16 = _bf16_act_ok(segs, W, Npad, B * Tout)
-    if ybf is not None:
+    M = B * Tout
+    a16 = _bf16_act_ok(segs, W, Npad, M)
+    if csum is not None:
+        assert (M % BM == 0 and bias is None and not accum and not relu and
+                epi in (_lib.EPI_PLAIN, _lib.EPI_ADDSCALE) and ybf_radd is None)
+        yp = Y.data_ptr() + 4 * yoff
+        vec = (yp % 16 == 0 and ldy % 4 == 0 and N % 4 == 0 and
+               (aux1 is None or (aux1.data_ptr() % 16 == 0 and ld1 % 4 == 0)) and
+               (ybf is None or (ybf.data_ptr() % 8 == 0 and ybf_ld % 4 == 0)))
+        if not (a16 and vec):
+            # the accumulator through a plain Y, its tile sums, then the epilogue as a pass
+            flat = ldy == N and yoff == 0 and (aux1 is None or ld1 == N)
+            assert flat, "csum fallback needs contiguous Y / aux1"
+            acc = Y if epi == _lib.EPI_PLAIN else torch.empty(M, N, device=Y.device)
+            gemm(segs, B, Tout, N, W, acc, N)
+            call("ensvs_tile_colsum", acc.data_ptr(), N, M, N, csum.data_ptr() + 4 * csum_off,
+                 csum_ld, stream())
+            if epi == _lib.EPI_ADDSCALE:
+                if ybf is not None and ybf_ld == N:
+                    call("ensvs_axpby_to_bf16", Y.data_ptr(), ybf.data_ptr(), aux1.data_ptr(),
+                         float(alpha), acc.data_ptr(), 1.0, M * N, stream())
+                    return
+                call("ensvs_axpby_to", Y.data_ptr(), aux1.data_ptr(), float(alpha),
+                     acc.data_ptr(), 1.0, M * N, stream())
+            if ybf is not None:
+                cast_bf16(Y, N, N, M, out=ybf, out_ld=ybf_ld)
+            return
+    if ybf is not None and csum is None:
         assert ybf.dtype == torch.bfloat16 and epi in (_lib.EPI_PLAIN, _lib.EPI_GATE,
                                                        _lib.EPI_RESSKIP, _lib.EPI_GATE_BWD)
         yp = Y.data_ptr() + 4 * yoff
@@ -221,11 +250,12 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
         d.pad, d.Tin, d.Kp = s.pad, s.Tin, s.ref.Kp
     bptr = None if bias is None else bias.data_ptr() + 4 * bias_off
     yptr = Y.data_ptr() + 4 * yoff
-    if ybf is not None:
+    if ybf is not None or csum is not None:
         call("ensvs_conv_gemm_bf16a_out", ctypes.addressof(arr), len(segs), B, Tout, N,
              Npad, W.buf.data_ptr(), bptr, yptr, ldy, epi, int(relu), int(accum), ptr(aux0),
-             ld0, ptr(aux1), ld1, float(alpha), C, ybf.data_ptr(), ybf_ld, ptr(ybf_radd),
-             ybf_radd_ld, BF16_ACT["stages"], stream())
+             ld0, ptr(aux1), ld1, float(alpha), C, ptr(ybf), ybf_ld, ptr(ybf_radd),
+             ybf_radd_ld, None if csum is None else csum.data_ptr() + 4 * csum_off, csum_ld,
+             BF16_ACT["stages"], stream())
         return
     if a16:
         call("ensvs_conv_gemm_bf16a", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,

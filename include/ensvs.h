@@ -75,8 +75,13 @@ int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, int B, int T
                               int Npad, const void* W, const float* bias, float* Y, int ldy,
                               int epi, int relu, int accum, float* aux0, int ld0,
                               const float* aux1, int ld1, float alpha, int C, void* ybf,
-                              int ybf_ld, const float* ybf_radd, int ybf_radd_ld, int stages,
-                              void* stream);
+                              int ybf_ld, const float* ybf_radd, int ybf_radd_ld, float* csum,
+                              int csum_ld, int stages, void* stream);
+/* csum (optional, M % 128 == 0, PLAIN / ADDSCALE / RELU_MASK): per 128-row tile column sums
+ * of the accumulator, csum[(m / 128) * csum_ld + n] -- the DiffNet backward's per-sequence
+ * dilated-conv input-grad sums without a pass over Y.  ensvs_tile_colsum computes the same
+ * sums, bit for bit, from a Y written by any other path. */
+int ensvs_tile_colsum(const float* y, int ldy, int M, int N, float* out, int ldo, void* stream);
 /* y[m][k] = bf16(x[m][k] + radd[m / T][k]) (radd optional), K % 8 == 0. */
 int ensvs_cast_bf16(const float* x, int ldx, const float* radd, int radd_ld, int T, long long M,
                     int K, void* y, int ldy, void* stream);

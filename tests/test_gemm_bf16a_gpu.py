@@ -1,6 +1,7 @@
 """bf16-activation GEMM path (ensvs_cast_bf16 + ensvs_conv_gemm_bf16a: global_load_lds
 staging, swizzled LDS, counted vmcnt) against the register-staged bf16 kernel: identical
 bits for every epilogue, padding mode, tap/dilation, multi-segment K and ragged M/N/K."""
+import numpy as np
 import pytest
 import torch
 
@@ -103,16 +104,27 @@ def test_bf16a_epilogues_bitwise(epi):
     assert torch.equal(y0, y1) and torch.equal(a0, a1)
 
 
-@pytest.mark.parametrize("which", ["mgc", "bap"])
+@pytest.mark.parametrize("which", ["mgc", "bap", "mgc_t256"])
 def test_diffnet_bf16_operands_bitwise(which):
     """DiffNet forward + backward on the bf16-operand path (cond, dss and dpre rounded once,
-    dx rounded by its axpby, the rest by per-GEMM casts) equals the register-staged path
-    bit for bit."""
+    dx rounded by its axpby or the dgrad epilogue, the rest by per-GEMM casts) equals the
+    register-staged path bit for bit.  mgc_t256: whole 128-frame tiles per sequence, so the
+    dgrad GEMM's epilogue also produces dx_l and the tile column sums of dy (fallback:
+    ensvs_tile_colsum + axpby)."""
     from ensemble_svs_with_interactions_amd import configs, engine
     from golden_util import full_shapes, load_case
     from gpu_util import build
     engine.set_gemm_precision("bf16")
+    t256 = which == "mgc_t256"
+    which = which.split("_")[0]
     a, meta = load_case(f"diffnet_{which}")
+    if t256:  # same weights, synthetic inputs of 2 x 256 frames
+        rng = np.random.default_rng(11)
+        Mc, E = a["spec"].shape[2], a["cond"].shape[1]
+        a = dict(spec=rng.standard_normal((2, 1, Mc, 256), dtype=np.float32),
+                 cond=rng.standard_normal((2, E, 256), dtype=np.float32),
+                 t=np.array([3, 77], dtype=np.int64),
+                 R=rng.standard_normal((2, 1, Mc, 256), dtype=np.float32))
     cfg = configs.multitrack_diffusion(num_speakers=4)[f"{which}_model"]["denoise_fn"]
     B, _, Mc, T = a["spec"].shape
     E = a["cond"].shape[1]
@@ -131,3 +143,34 @@ def test_diffnet_bf16_operands_bitwise(which):
     assert torch.equal(o0, o1) and torch.equal(d0, d1)
     for k in g0:
         assert torch.equal(g0[k], g1[k]), k
+
+
+@pytest.mark.parametrize("epi", [L.EPI_PLAIN, L.EPI_ADDSCALE])
+def test_bf16a_tile_colsum_bitwise(epi):
+    """Per-128-row-tile column sums of the accumulator (and the ADDSCALE output with its bf16
+    copy) from the LDS epilogue equal the fallback (plain GEMM + ensvs_tile_colsum + axpby) bit
+    for bit, and the sums match an fp64 column sum of the plain GEMM output."""
+    torch.manual_seed(9)
+    B, T, C, N = 2, 256, 96, 64
+    x = torch.randn(B * T, C, device=DEV)
+    w = torch.randn(N, C, 3, device=DEV) / (3 * C) ** 0.5
+    pb, (r,) = _pack([w])
+    segs = [K.Seg(x, C, C, r, T, taps=3, dil=2, shift0=-2)]
+    aux1 = torch.randn(B * T, N, device=DEV)
+    ld = 3 * N
+
+    def run():
+        y = torch.empty(B * T, N, device=DEV)
+        yb = torch.empty(B * T, N, device=DEV, dtype=torch.bfloat16)
+        cs = torch.full((B * T // 128, ld), 7.0, device=DEV)
+        kw = {} if epi == L.EPI_PLAIN else dict(epi=epi, aux1=aux1, ld1=N, alpha=0.7071)
+        K.gemm(segs, B, T, N, pb, y, N, ybf=yb, ybf_ld=N, csum=cs, csum_ld=ld, csum_off=N, **kw)
+        torch.cuda.synchronize()
+        return y, yb, cs
+    (y0, b0, c0), (y1, b1, c1) = _both(run)
+    assert torch.equal(y0, y1) and torch.equal(b0, b1) and torch.equal(c0, c1)
+    assert torch.equal(b0, y0.to(torch.bfloat16))
+    assert (c0[:, :N] == 7.0).all() and (c0[:, 2 * N:] == 7.0).all()
+    acc = y0 if epi == L.EPI_PLAIN else y0 - 0.7071 * aux1
+    ref = acc.double().view(B * T // 128, 128, N).sum(1)
+    torch.testing.assert_close(c0[:, N:2 * N].double(), ref, rtol=1e-4, atol=1e-3)

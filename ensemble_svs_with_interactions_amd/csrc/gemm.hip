@@ -64,9 +64,10 @@ struct GemmArgs {
   __bf16* ybf;
   const float* ybf_radd;
   int ybf_ld, ybf_radd_ld;
-  // optional per-tile column sums of the accumulator (before bias / epilogue), LDS-staged
-  // epilogue only, M % BM == 0: csum[(m0 / BM) * csum_ld + col] = rows 0..63 + rows 64..127
-  // (each half summed in row order; ensvs_tile_colsum reproduces it for other paths)
+  // optional per-tile column sums, LDS-staged epilogue only, M % BM == 0: of the accumulator
+  // (PLAIN / ADDSCALE / RELU_MASK, before bias) or of both outputs (GATE_BWD, in Y's column
+  // space).  csum[(m0 / BM) * csum_ld + col] = sum over g = 0..7 (in order) of the sums of
+  // rows g, g+8, .., g+120 (in order); ensvs_tile_colsum reproduces it for other paths
   float* csum;
   int csum_ld;
 };
@@ -220,7 +221,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4]
 // a row: one 16-B load / store per operand instead of four 4-B accesses (the per-element
 // epilogue above is store-issue bound).  Same arithmetic per element as gemm_epilogue.
 constexpr int EP = 132;
-constexpr int EPI_LDS = BM * EP * 4 + BN * 4;  // + the column-sum exchange row
+constexpr int CS_GROUPS = NTHR / 32;  // row groups of the column sums (32 lanes per row)
+constexpr int EPI_LDS = BM * EP * 4 + CS_GROUPS * 2 * BN * 4;  // + column-sum exchange
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *(f32x4*)p = v; }
@@ -247,18 +249,6 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
             acc[mt][nt][r];
   __syncthreads();
   const int M = a.M;
-  if (a.csum) {  // uniform: every thread reaches the barrier
-    static_assert(NTHR == 2 * BN, "column sums: two half-tile lanes per column");
-    float* xr = T + BM * EP;
-    const int col = tid & (BN - 1), h = tid / BN;
-    const float* tc = T + (h * (BM / 2)) * EP + col;
-    float cs = 0.f;
-#pragma unroll 8
-    for (int r = 0; r < BM / 2; ++r) cs += tc[r * EP];
-    if (h) xr[col] = cs;
-    __syncthreads();
-    if (!h && n0 + col < a.N) a.csum[(long long)(m0 / BM) * a.csum_ld + n0 + col] = cs + xr[col];
-  }
   if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
     // this tile holds 64 output channels (gate/filter interleaved by 16 in the packed columns)
     for (int it = tid; it < BM * 16; it += NTHR) {
@@ -282,7 +272,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         f32x4 z;
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = sigmoidf_(g[e]) * tanhf(f[e]);
-        st4(a.Y + (long long)m * a.ldy + c, z);
+        if (a.Y) st4(a.Y + (long long)m * a.ldy + c, z);
         shadow4(a, m, c, z);
       } else if (a.epi == EPI_GATE_TS) {
         f32x4 z;
@@ -310,12 +300,15 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
     }
     return;
   }
+  // column sums: this thread always has columns cq*4.. and rows (tid >> 5) + 8k
+  f32x4 cs0 = {0.f, 0.f, 0.f, 0.f}, cs1 = {0.f, 0.f, 0.f, 0.f};
   for (int it = tid; it < BM * 32; it += NTHR) {
     const int row = it >> 5, cq = it & 31;
     const int m = m0 + row, col = n0 + cq * 4;
     if (m >= M || col >= a.N) continue;
     const int ne = min(4, a.N - col);
     f32x4 v = ld4(T + row * EP + cq * 4);
+    if (a.csum && a.epi != EPI_GATE_BWD) cs0 += v;
     if (a.bias) {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
@@ -358,8 +351,14 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
           dg[e] = t0;
           df[e] = t1;
         }
-        st4(y, dg);
-        st4(y + a.C, df);
+        if (a.csum) {
+          cs0 += dg;
+          cs1 += df;
+        }
+        if (a.Y) {
+          st4(y, dg);
+          st4(y + a.C, df);
+        }
         shadow4(a, m, col, dg);
         shadow4(a, m, a.C + col, df);
       }
@@ -383,6 +382,24 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
           const float f = a.aux1[(long long)m * a.ld1 + a.C + col + e];
           gate_bwd_(w, g, f, ye[0], ye[a.C]);
         }
+      }
+    }
+  }
+  if (a.csum) {  // uniform: every thread reaches the barrier
+    float* X = T + BM * EP;  // [group][2*BN]
+    const int g = tid >> 5, c4 = (tid & 31) * 4;
+    *(f32x4*)(X + g * 2 * BN + c4) = cs0;
+    *(f32x4*)(X + g * 2 * BN + BN + c4) = cs1;
+    __syncthreads();
+    const int j = tid;  // NTHR == 2 * BN: first BN the accumulator / d(gate), then d(filter)
+    const bool bwd = a.epi == EPI_GATE_BWD;
+    if (j < BN || bwd) {
+      const int c = n0 + (j & (BN - 1));
+      if (c < a.N) {
+        float t = X[j];
+#pragma unroll
+        for (int q = 1; q < CS_GROUPS; ++q) t += X[q * 2 * BN + j];
+        a.csum[(long long)(m0 / BM) * a.csum_ld + (j < BN ? c : a.C + c)] = t;
       }
     }
   }
@@ -1453,12 +1470,16 @@ ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, in
                                 accum, aux0, ld0, aux1, ld1, alpha, C);
   if (rc != ENSVS_OK) return rc;
   if (csum) {
-    if (!a.vec_out || a.M % BM || csum_ld < N ||
-        (epi != EPI_PLAIN && epi != EPI_ADDSCALE && epi != EPI_RELU_MASK))
+    if (!a.vec_out || a.M % BM || N % 4 || csum_ld < (epi == EPI_GATE_BWD ? 2 * C : N) ||
+        (epi != EPI_PLAIN && epi != EPI_ADDSCALE && epi != EPI_RELU_MASK &&
+         epi != EPI_GATE_BWD))
       return ENSVS_E_ARG;
     a.csum = csum;
     a.csum_ld = csum_ld;
   }
+  // Y may be dropped where the epilogue's other outputs are all the caller needs
+  if (!Y && !((epi == EPI_GATE && ybf) || (epi == EPI_GATE_BWD && (ybf || csum))))
+    return ENSVS_E_ARG;
   if (ybf) {
     if (!a.vec_out || N % 4 || ybf_ld % 4 || ((uintptr_t)ybf & 7) ||
         (ybf_radd && (ybf_radd_ld % 4 || ((uintptr_t)ybf_radd & 15))))
@@ -1471,29 +1492,28 @@ ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, in
   return launch_b16(a, segs, nseg, B, Npad, W, stages, (hipStream_t)stream);
 }
 
-// The column sums of GemmArgs::csum for a Y written by any other path: per BM-row tile,
-// rows 0..63 then rows 64..127 each in row order, then the two halves added.
-__global__ __launch_bounds__(NTHR) void tile_colsum_kernel(const float* __restrict__ y, int ldy,
-                                                           int N, float* __restrict__ out,
-                                                           int ldo) {
-  __shared__ float xr[BN];
-  const int tid = threadIdx.x, col = tid & (BN - 1), h = tid / BN;
-  const int m0 = blockIdx.x * BM, n = blockIdx.y * BN + col;
-  float cs = 0.f;
-  if (n < N) {
-    const float* p = y + (long long)(m0 + h * (BM / 2)) * ldy + n;
-    for (int r = 0; r < BM / 2; ++r) cs += p[(long long)r * ldy];
+// The column sums of GemmArgs::csum for a Y written by any other path, in the same order:
+// per BM-row tile and column, the 8 row groups g (rows g, g+8, ..) each summed in row order,
+// then the group sums added in order.
+__global__ __launch_bounds__(BN) void tile_colsum_kernel(const float* __restrict__ y, int ldy,
+                                                         int N, float* __restrict__ out,
+                                                         int ldo) {
+  const int m0 = blockIdx.x * BM, n = blockIdx.y * BN + threadIdx.x;
+  if (n >= N) return;
+  float t = 0.f;
+  for (int g = 0; g < CS_GROUPS; ++g) {
+    float s = 0.f;
+    for (int r = g; r < BM; r += CS_GROUPS) s += y[(long long)(m0 + r) * ldy + n];
+    t = g ? t + s : s;
   }
-  if (h) xr[col] = cs;
-  __syncthreads();
-  if (!h && n < N) out[(long long)blockIdx.x * ldo + n] = cs + xr[col];
+  out[(long long)blockIdx.x * ldo + n] = t;
 }
 
 ENSVS_API int ensvs_tile_colsum(const float* y, int ldy, int M, int N, float* out, int ldo,
                                 void* stream) {
   if (M <= 0 || N <= 0) return ENSVS_OK;
   if (M % BM || ldo < N) return ENSVS_E_ARG;
-  hipLaunchKernelGGL(tile_colsum_kernel, dim3(M / BM, cdiv(N, BN)), dim3(NTHR), 0,
+  hipLaunchKernelGGL(tile_colsum_kernel, dim3(M / BM, cdiv(N, BN)), dim3(BN), 0,
                      (hipStream_t)stream, y, ldy, N, out, ldo);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;

@@ -230,7 +230,7 @@ class DiffNet(nn.Module):
                 K.Seg(condb, E, E, pk[f"cond{l}"], T)]
         ldz = ldz or C
         K.gemm(segs, B, T, 2 * C, pk.fwd, z, ldz, epi=_lib.EPI_GATE, aux0=gf, ld0=2 * C, C=C,
-               ybf=zb, ybf_ld=ldz, **pk.bias_ptr_args(f"g{l}.b"))
+               ybf=zb, ybf_ld=ldz, keep_y=zb is None, **pk.bias_ptr_args(f"g{l}.b"))
 
     def _bwd(self, st, dout):
         """dout (B*T, in_dim) -> dcond (B*T, E); parameter grads accumulated."""
@@ -272,6 +272,7 @@ class DiffNet(nn.Module):
         # column sums per tile (dd_tiles), reduced per sequence once after the loop
         fuse = T % K.BM == 0
         dd_tiles = empty(M // K.BM, L * C, device=dev) if fuse else None
+        pre_tiles = empty(M // K.BM, L * 2 * C, device=dev) if fuse else None
         # The dgrad chain (gate_bwd GEMM -> dilated-conv^T GEMM -> next block) stays on this
         # stream; each block's weight / bias gradients go to a trailing auxiliary stream.
         aux = AuxStream(dev)
@@ -281,9 +282,13 @@ class DiffNet(nn.Module):
             segs = [K.Seg(dssb if b16 else dss, C, C, pk[f"out{l}^Tskip"], T)]
             if dx is not None:
                 segs.insert(0, K.Seg(dxb if b16 else dx, C, C, pk[f"out{l}^Tres"], T))
+            # d(pre) in bf16 for the GEMMs that read it; its fp32 copy only where an fp32
+            # consumer remains; the bias-gradient tile column sums from the epilogue
             K.gemm(segs, B, T, C, pk.bwd, dpre_all, L * 2 * C, yoff=l * 2 * C,
                    epi=_lib.EPI_GATE_BWD, aux1=st["GF"][l], ld1=2 * C, C=C,
-                   ybf=dpre_b[:, l * 2 * C:] if b16 else None, ybf_ld=L * 2 * C)
+                   ybf=dpre_b[:, l * 2 * C:] if b16 else None, ybf_ld=L * 2 * C,
+                   csum=pre_tiles, csum_ld=L * 2 * C, csum_off=l * 2 * C,
+                   keep_y=not (bw and fuse))
             # dilated conv input grad (transposed, flipped taps)
             tsegs = [K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, 2 * C, pk[f"dil{l}^T"], T,
                            taps=3, dil=dl, shift0=-dl, xoff=l * 2 * C)]
@@ -361,7 +366,10 @@ class DiffNet(nn.Module):
                     C, 1, 1, dtype=engine_gemm_dtype())
             _axpy_blocks(g_w("diffusion_projection"), tp, C * C, C * C)
             tmp_pre = empty(L * 2 * C, device=dev)
-            K.colsum(dpre_all, L * 2 * C, M, L * 2 * C, tmp_pre)
+            if fuse:
+                K.colsum(pre_tiles, L * 2 * C, M // K.BM, L * 2 * C, tmp_pre)
+            else:
+                K.colsum(dpre_all, L * 2 * C, M, L * 2 * C, tmp_pre)
             _axpy_blocks(g_b("dilated_conv"), tmp_pre, 2 * C, 2 * C)
             _axpy_blocks(g_b("conditioner_projection"), tmp_pre, 2 * C, 2 * C)
             _axpy_blocks([b[C:] for b in g_b("output_projection")], tmp_dss, 0, C)

@@ -173,25 +173,35 @@ def cast_bf16(x, ld, K, rows, xoff=0, radd=None, radd_ld=0, T=1, out=None, out_l
 def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: int,
          bias=None, epi=_lib.EPI_PLAIN, relu=False, accum=False, aux0=None, ld0=0, aux1=None,
          ld1=0, alpha=0.0, C=0, yoff=0, bias_off=0, ybf=None, ybf_ld=0, ybf_radd=None,
-         ybf_radd_ld=0, csum=None, csum_ld=0, csum_off=0):
+         ybf_radd_ld=0, csum=None, csum_ld=0, csum_off=0, keep_y=True):
     """One implicit-GEMM launch (bf16-operand kernel when the A panels are bf16 or worth a
     cast pass, register-staged kernel otherwise).  ybf (bf16 tensor): also receives
     bf16(y + ybf_radd[row // Tout]) of the Y values written (PLAIN / GATE / RESSKIP /
     ADDSCALE: the Y columns; GATE_BWD: both halves) -- from the epilogue when it can, else
     by a cast.  csum (fp32, B*Tout % 128 == 0, no bias / accum / relu): per 128-row tile
     column sums of the accumulator into csum[tile * csum_ld + csum_off + n] -- from the
-    epilogue when it can, else by ensvs_tile_colsum (the same bits)."""
+    epilogue when it can, else by ensvs_tile_colsum (the same bits); GATE_BWD: of both
+    outputs.  keep_y=False (GATE with ybf, GATE_BWD with ybf / csum): the fp32 Y is not
+    needed by the caller and the fused epilogue skips it (Y stays allocated for the
+    fallback paths, which still write it)."""
     arr = (ConvSeg * len(segs))()
     Npad = segs[0].ref.Npad
     M = B * Tout
     a16 = _bf16_act_ok(segs, W, Npad, M)
     if csum is not None:
         assert (M % BM == 0 and bias is None and not accum and not relu and
-                epi in (_lib.EPI_PLAIN, _lib.EPI_ADDSCALE) and ybf_radd is None)
+                epi in (_lib.EPI_PLAIN, _lib.EPI_ADDSCALE, _lib.EPI_GATE_BWD) and
+                ybf_radd is None)
         yp = Y.data_ptr() + 4 * yoff
-        vec = (yp % 16 == 0 and ldy % 4 == 0 and N % 4 == 0 and
+        vec = (yp % 16 == 0 and ldy % 4 == 0 and N % 4 == 0 and C % 4 == 0 and
                (aux1 is None or (aux1.data_ptr() % 16 == 0 and ld1 % 4 == 0)) and
                (ybf is None or (ybf.data_ptr() % 8 == 0 and ybf_ld % 4 == 0)))
+        if not (a16 and vec) and epi == _lib.EPI_GATE_BWD:
+            gemm(segs, B, Tout, N, W, Y, ldy, epi=epi, aux1=aux1, ld1=ld1, C=C, yoff=yoff,
+                 ybf=ybf, ybf_ld=ybf_ld)
+            call("ensvs_tile_colsum", yp, ldy, M, 2 * C, csum.data_ptr() + 4 * csum_off,
+                 csum_ld, stream())
+            return
         if not (a16 and vec):
             # the accumulator through a plain Y, its tile sums, then the epilogue as a pass
             flat = ldy == N and yoff == 0 and (aux1 is None or ld1 == N)
@@ -250,6 +260,9 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
         d.pad, d.Tin, d.Kp = s.pad, s.Tin, s.ref.Kp
     bptr = None if bias is None else bias.data_ptr() + 4 * bias_off
     yptr = Y.data_ptr() + 4 * yoff
+    if not keep_y and ((epi == _lib.EPI_GATE and ybf is not None) or
+                       (epi == _lib.EPI_GATE_BWD and (ybf is not None or csum is not None))):
+        yptr = None  # only reached on the fused-epilogue path
     if ybf is not None or csum is not None:
         call("ensvs_conv_gemm_bf16a_out", ctypes.addressof(arr), len(segs), B, Tout, N,
              Npad, W.buf.data_ptr(), bptr, yptr, ldy, epi, int(relu), int(accum), ptr(aux0),

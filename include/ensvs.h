@@ -77,10 +77,13 @@ int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, int B, int T
                               const float* aux1, int ld1, float alpha, int C, void* ybf,
                               int ybf_ld, const float* ybf_radd, int ybf_radd_ld, float* csum,
                               int csum_ld, int stages, void* stream);
-/* csum (optional, M % 128 == 0, PLAIN / ADDSCALE / RELU_MASK): per 128-row tile column sums
- * of the accumulator, csum[(m / 128) * csum_ld + n] -- the DiffNet backward's per-sequence
- * dilated-conv input-grad sums without a pass over Y.  ensvs_tile_colsum computes the same
- * sums, bit for bit, from a Y written by any other path. */
+/* csum (optional, M % 128 == 0): per 128-row tile column sums, csum[(m / 128) * csum_ld + n],
+ * of the accumulator (PLAIN / ADDSCALE / RELU_MASK, before bias) or of both GATE_BWD outputs
+ * (n < 2C, Y's column space) -- the DiffNet backward's per-sequence dilated-conv input-grad
+ * sums and gate bias gradients without a pass over Y.  Order: per column, the 8 row groups
+ * g (rows g, g+8, ..) summed in row order, then the groups in order; ensvs_tile_colsum computes
+ * the same sums, bit for bit, from a Y written by any other path.  Y may be NULL for GATE
+ * with ybf and for GATE_BWD with ybf or csum (the fp32 output is not needed). */
 int ensvs_tile_colsum(const float* y, int ldy, int M, int N, float* out, int ldo, void* stream);
 /* y[m][k] = bf16(x[m][k] + radd[m / T][k]) (radd optional), K % 8 == 0. */
 int ensvs_cast_bf16(const float* x, int ldx, const float* radd, int radd_ld, int T, long long M,

@@ -32,11 +32,12 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
 def gate_gemm_bytes(M, C, E, a_bytes):
-    """Algorithmic HBM bytes of one gate-GEMM launch: A operand (x+d and
-    cond, a_bytes each), packed weights (bf16), bias, and the fp32 outputs z (M x C) and
-    the saved gate/filter pre-activations gf (M x 2C)."""
+    """Algorithmic HBM bytes of one gate-GEMM launch as the training step issues it
+    (DESIGN.md §4): A operand (x+d and cond, a_bytes each), packed weights (bf16), bias, the
+    saved gate/filter pre-activations gf (fp32, M x 2C) and z (M x C) -- in bf16 only on the
+    bf16-operand path (the next GEMM's operand; the fp32 copy is not written), else fp32."""
     return (M * (C + E) * a_bytes + 2 * C * (3 * C + E) * 2 + 2 * C * 4 +
-            M * C * 4 + M * 2 * C * 4)
+            M * C * a_bytes + M * 2 * C * 4)
 TRAIN_FLOP_PER_FRAME = 127.5e6  # SURVEY.md §6 (torch.utils.flop_counter on the oracle)
 
 
@@ -87,15 +88,20 @@ def gate_gemm_timing(model, P, T, dev, iters=20):
         torch.cuda.synchronize()
         return s.elapsed_time(e) / 1e3 / iters
 
-    total = timed(lambda: net._gate_gemm(0, x, cond, E, ds, P, T, z, gf))
+    b16 = K.gemm_dtype_is_bf16(pk.fwd)
+    zb = torch.empty(M, C, device=dev, dtype=torch.bfloat16) if b16 else None
+    total = timed(lambda: net._gate_gemm(0, x, cond, E, ds, P, T, z, gf, zb=zb))
     dl = net.residual_layers[0].dilation
-    if K.gemm_dtype_is_bf16(pk.fwd):
+    if b16:
+        # as the training step issues it: operands already bf16 (cond rounded once for all
+        # blocks, x + d_l by the previous block's epilogue), z out in bf16 only
         xb = K.cast_bf16(x, C, C, M, radd=ds, radd_ld=L * C, T=T)
         cb = K.cast_bf16(cond, E, E, M)
         segs = [K.Seg(xb, C, C, pk["dil0"], T, taps=3, dil=dl, shift0=-dl),
                 K.Seg(cb, E, E, pk["cond0"], T)]
         gemm = timed(lambda: K.gemm(segs, P, T, 2 * C, pk.fwd, z, C, epi=_lib.EPI_GATE, aux0=gf,
-                                    ld0=2 * C, C=C, **pk.bias_ptr_args("g0.b")))
+                                    ld0=2 * C, C=C, ybf=zb, ybf_ld=C, keep_y=False,
+                                    **pk.bias_ptr_args("g0.b")))
     else:
         gemm = total
     flops = 2.0 * M * (2 * C) * (3 * C + E)

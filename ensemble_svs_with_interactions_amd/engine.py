@@ -64,10 +64,11 @@ class Branches:
         if self.on_side:
             key = (str(device), n_side)
             if key not in _SIDE_STREAMS:
-                # branch 0 (the lf0 model with its AR decoder) gets the high priority: its
-                # serial recurrences only need a few CUs and then finish early; giving it to
-                # the mgc branch instead measured slower (tools/branch_times.py)
-                _SIDE_STREAMS[key] = [torch.cuda.Stream(device, priority=-1 if i == 0 else 0)
+                # equal priorities: with the DiffNet backward's per-block launches batched,
+                # a high-priority branch (ENSVS_PRIO_BRANCH=i) measured slower -- lf0 23.5,
+                # mgc 23.4, bap 22.2 vs 22.2 ms/step for none (graph replay, 30 x 1024)
+                hi = int(os.environ.get("ENSVS_PRIO_BRANCH", "-1"))
+                _SIDE_STREAMS[key] = [torch.cuda.Stream(device, priority=-1 if i == hi else 0)
                                       for i in range(n_side)]
             self.side = _SIDE_STREAMS[key]
         else:

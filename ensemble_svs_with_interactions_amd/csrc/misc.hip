@@ -171,6 +171,7 @@ __global__ void bn_bwd_reduce_kernel(const float* __restrict__ dout, int ldd,
   float a = 0.f, bsum = 0.f;
   if (col < C) {
     const float mu = mean[g * C + col], rs = rstd[g * C + col], ga = gamma[col], be = beta[col];
+#pragma unroll 4
     for (long long r = r0 + w; r < r1; r += 4) {
       const float xh = (y[r * ldy + col] - mu) * rs;
       const float z = xh * ga + be;

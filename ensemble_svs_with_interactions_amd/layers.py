@@ -19,6 +19,9 @@ from ._lib import call, ptr
 from .engine import empty, gemm_dtype, grad_of, next_seed
 
 
+# row splits of the BatchNorm backward reduction (>= 64 rows each): 256 fills the chip
+BN_SPLITS = 256
+
 def stream():
     return torch.cuda.current_stream().cuda_stream
 
@@ -263,10 +266,11 @@ def conv_bwd(pk, conv, sv, dout, B, T, device, groups=1, first_dx=None):
         C = conv[ci].weight.shape[0]
         bn = conv[bi]
         dy = empty(M, C, device=device)
-        part = K.scratch(groups * 64 * 2 * C, device, key="bn")
+        part = K.scratch(groups * BN_SPLITS * 2 * C, device, key="bn")
         sums = empty(groups * 2 * C, device=device)
         call("ensvs_bn_bwd", d.data_ptr(), C, s["y"].data_ptr(), C, M, C, Mg, s["mean"].data_ptr(),
-             s["rstd"].data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(), part.data_ptr(), 64,
+             s["rstd"].data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(), part.data_ptr(),
+             BN_SPLITS,
              sums.data_ptr(), grad_of(bn.weight).data_ptr(), grad_of(bn.bias).data_ptr(),
              dy.data_ptr(), C, stream())
         _dbg(f"conv{li}.dout", d)

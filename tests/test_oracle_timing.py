@@ -20,7 +20,10 @@ def test_mdn_grid():
         for k in ("lp", "ls", "mu"):
             assert rel(locals()[k].grad, g("d_" + k)) < 1e-5, (key, k)
         sig, m = TO.mdn_most_probable(g("lp"), g("ls"), g("mu"))
-        assert torch.equal(sig, g("sigma")) and torch.equal(m, g("mu_best")), key
+        # component selection is exact (mu is a plain gather); sigma = exp(.) may differ by
+        # an ulp between host CPUs' vectorised exp, so it is held to 1e-6 relative
+        assert torch.equal(m, g("mu_best")), key
+        assert torch.allclose(sig, g("sigma"), rtol=1e-6, atol=0), key
         assert rel(TO.mdn_loss(g("lp"), g("ls"), g("mu"), g("tgt")), g("loss_red")) < 1e-6
 
 

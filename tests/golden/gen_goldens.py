@@ -29,6 +29,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, "/root/reference")
 sys.dont_write_bytecode = True
 
@@ -667,6 +668,60 @@ def case_onset_merge():
     save("onset_merge", arrays, meta)
 
 
+
+def case_loader():
+    from golden_util import loader_tree
+    """On-disk pair dataset (train_util.py:103-246, 439-520): file discovery and pairing,
+    SyncMultiTrackDataset items, shuffled ordered_indices, batch_by_size at several
+    world sizes and max_tokens, and the collate of a loaded batch (bit-exact)."""
+    r = rng_for("loader")
+    arrays, meta = {}, {}
+    spk_list = ["S1", "A2", "Vo1", "ritsu"]
+    for spk in spk_list:
+        for seg in ("songA_001", "songA_002", "songB_010", "x_y"):
+            if (spk, seg) in (("A2", "songA_002"), ("ritsu", "x_y")):
+                continue
+            utt = f"{spk}_{seg}"
+            n = int(r.integers(30, 220))
+            arrays[f"file::in::{utt}"] = r.standard_normal((n, 6)).astype(np.float32)
+            arrays[f"file::out::{utt}"] = r.standard_normal((n, 4)).astype(np.float32)
+            arrays[f"file::times::{utt}"] = np.sort(r.integers(0, 10**7, size=int(r.integers(3, 12))))
+    meta["spk_list"] = spk_list
+    with tempfile.TemporaryDirectory() as d:
+        dirs = loader_tree(d, arrays)
+        in_files, lengths = ref_train_util.get_filtered_files_multitrack(dirs["in"], None)
+        out_files, _ = ref_train_util.get_filtered_files_multitrack(dirs["out"], None)
+        rel_ = lambda p: os.path.relpath(p, d)  # noqa: E731
+        meta["in_pairs"] = [[rel_(a), rel_(b)] for a, b in in_files]
+        meta["out_pairs"] = [[rel_(a), rel_(b)] for a, b in out_files]
+        meta["lengths"] = [[int(a), int(b)] for a, b in lengths]
+        ds = ref_train_util.SyncMultiTrackDataset(in_files, out_files, lengths, spk_list,
+                                                  shuffle=True, allow_cache=False)
+        meta["items"] = []
+        for i in range(len(in_files)):
+            it = ds[i]
+            meta["items"].append([int(it[2]), int(it[6]), len(it[3]), len(it[7])])
+            arrays[f"item{i}::times0"] = np.asarray(it[3])
+            arrays[f"item{i}::times1"] = np.asarray(it[7])
+        meta["orders"], meta["batches"] = {}, {}
+        for seed in (0, 7):
+            np.random.seed(seed)
+            idx = ds.ordered_indices()
+            meta["orders"][str(seed)] = [int(i) for i in idx]
+            for mt in (250, 700, 2000):
+                for w in (1, 2, 3):
+                    b = ref_train_util.batch_by_size(idx, ds.num_tokens, max_tokens=mt,
+                                                     required_batch_size_multiple=w)
+                    meta["batches"][f"{seed}/{mt}/{w}"] = [[int(i) for i in x] for x in b]
+        big = meta["batches"]["7/700/1"][0]
+        out = ref_train_util.collate_fn_syncmultitrack_acoustic([ds[i] for i in big],
+                                                                reduction_factor=4)
+        meta["collate_batch"] = [int(i) for i in big]
+        for j, o in enumerate(out):
+            arrays[f"collate{j}"] = o.numpy()
+    save("loader", arrays, meta)
+
+
 def main():
     which = sys.argv[1:] or ["all"]
     run = lambda n: "all" in which or n in which  # noqa: E731
@@ -705,6 +760,8 @@ def main():
         case_vp()
     if run("onset"):
         case_onset_merge()
+    if run("loader"):
+        case_loader()
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(dict(seed=SEED, torch=torch.__version__, numpy=np.__version__,
                        reference="sarulab-speech/ensemble_svs_with_interactions @ 2025-03-21",

@@ -95,3 +95,19 @@ def rel_l2(g, ref):
 def grad_close(g, ref, rtol):
     """Relative L2 error of a gradient tensor (robust to isolated ReLU-kink flips)."""
     return rel_l2(g, ref) <= rtol
+
+def loader_tree(root, arrays):
+    """Write the on-disk dataset held in `arrays` (loader fixture) under root:
+    dump/norm/{in,out}_acoustic/<utt>-feats.npy and dump/org/in_acoustic/<utt>-times.npy.
+    Shared with tests/test_loader.py so both sides read byte-identical files."""
+    dirs = {k: os.path.join(root, "dump", a, b) for k, a, b in
+            (("in", "norm", "in_acoustic"), ("out", "norm", "out_acoustic"),
+             ("times", "org", "in_acoustic"))}
+    for d in dirs.values():
+        os.makedirs(d, exist_ok=True)
+    for key, v in arrays.items():
+        if key.startswith("file::"):
+            _, kind, utt = key.split("::")
+            suffix = "-times.npy" if kind == "times" else "-feats.npy"
+            np.save(os.path.join(dirs[kind], utt + suffix), v)
+    return dirs

@@ -259,3 +259,22 @@ class GraphedTrainStep:
         self.opt.step_count += 1
         weights_updated()
         return self.loss, self.norm
+
+
+def train_epoch(model, optimizer, feeder, logf0_diff_weight=0.0, ddp=True):
+    """The batch loop of train_loop (train_acoustic_multitrack.py:461-484, 94-100) over a
+    loader.PairBatchFeeder: each fed batch (tracks already sorted independently by
+    length, lengths = max(L0, L1)) goes through one fused train_step.  Ragged batches
+    change shape from step to step, so this runs eagerly (GraphedTrainStep is for
+    fixed-shape buckets).  Returns the per-step (loss, grad_norm) device tensors (the
+    norm copied out of the optimizer's static buffer); the host reads them only when it
+    asks."""
+    out = []
+    for b in feeder:
+        lengths = [int(v) for v in b["host_lengths"]]
+        y_sub = b["y_sub"] if logf0_diff_weight > 0 else None
+        loss, norm = train_step(model, optimizer, b["x_main"], b["x_sub"], b["y_main"],
+                                b["spk_main"], b["spk_sub"], lengths, ddp=ddp, y_sub=y_sub,
+                                logf0_diff_weight=logf0_diff_weight)
+        out.append((loss, norm.clone()))
+    return out

@@ -149,10 +149,63 @@ def test_feeder_device_copy(tree):
     batches = meta["batches"]["0/2000/1"]
     host = loader.PairBatchFeeder(ds, batches, device="cpu")
     dev = loader.PairBatchFeeder(ds, batches, device="cuda:0", prefetch=3)
-    side = torch.empty(1 << 22, device="cuda:0")
+    side = torch.zeros(1 << 22, device="cuda:0")
     for hb, db in zip(host, dev):
         side.mul_(1.0001)  # keep the consumer stream busy while copies land
         for k in ("x_main", "y_main", "spk_main", "len_main", "x_sub", "y_sub", "spk_sub",
                   "len_sub", "lengths"):
             assert db[k].device.type == "cuda"
             assert torch.equal(db[k].cpu(), hb[k]), k
+
+
+@pytest.mark.gpu
+def test_train_epoch_from_disk(tmp_path):
+    """The reference's data path end to end on the GPU: on-disk features -> pairs ->
+    dynamic batches -> feeder -> train_epoch.  Each step equals train_step on the same
+    collated, track-sorted batch with the same RNG stream (bitwise)."""
+    from ensemble_svs_with_interactions_amd import configs, engine
+    from ensemble_svs_with_interactions_amd.train import FusedAdam, train_epoch, train_step
+    from gpu_util import build
+
+    engine.set_gemm_precision("fp32")
+    a, meta = load_case("train_step_tiny")
+    Din, Dout = a["x_main"].shape[2], a["y_main"].shape[2]
+    rng = np.random.default_rng(5)
+    dirs = {k: tmp_path / "dump" / s / d for k, s, d in
+            (("in", "norm", "in_acoustic"), ("out", "norm", "out_acoustic"),
+             ("times", "org", "in_acoustic"))}
+    for d in dirs.values():
+        d.mkdir(parents=True)
+    spks = ["S", "A", "T", "B"]
+    for seg in ("song_001", "song_002"):
+        for spk in spks:
+            n = int(rng.integers(40, 72))
+            sb = data.synthetic_batch(1, n, int(rng.integers(1 << 30)), in_dim=Din,
+                                      out_dim=Dout)
+            np.save(dirs["in"] / f"{spk}_{seg}-feats.npy", sb["x_main"][0])
+            np.save(dirs["out"] / f"{spk}_{seg}-feats.npy", sb["y_main"][0])
+            np.save(dirs["times"] / f"{spk}_{seg}-times.npy", np.arange(5) * 50000)
+    np.random.seed(1)
+    ds, batches = loader.setup_multitrack_batches(str(dirs["in"]), str(dirs["out"]), spks,
+                                                  batch_max_frames=400)
+    batches = batches[:3]
+
+    def fresh():
+        model = build(configs.multitrack_diffusion(num_speakers=4, tiny=True), meta["shapes"])
+        model.vuv_model.lstm.dropout = 0.0
+        torch.manual_seed(11)
+        engine._STATE["rng"] = None
+        return model, FusedAdam(model, lr=meta["lr"])
+
+    m1, o1 = fresh()
+    got = train_epoch(m1, o1, loader.PairBatchFeeder(ds, batches, device="cuda:0"))
+    got = [(l.item(), n.item()) for l, n in got]
+    m2, o2 = fresh()
+    want = []
+    for hb in loader.PairBatchFeeder(ds, batches, device="cpu"):
+        c = lambda k: hb[k].cuda().contiguous()  # noqa: E731
+        l, n = train_step(m2, o2, c("x_main"), c("x_sub"), c("y_main"), c("spk_main"),
+                          c("spk_sub"), [int(v) for v in hb["host_lengths"]])
+        want.append((l.item(), n.item()))
+    assert len(got) == len(batches) and got == want
+    assert all(np.isfinite(v).all() for v in got)

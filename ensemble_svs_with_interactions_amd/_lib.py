@@ -137,6 +137,8 @@ SIGNATURES = {
                              c_vp, c_vp],
     "ensvs_layer_norm_bwd": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp,
                              c_int, c_vp, c_vp],
+    "ensvs_masked_mean": [c_vp, c_vp, c_ll, c_vp, c_vp, c_vp],
+    "ensvs_masked_mean_bwd": [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp],
 }
 
 # entry points returning a value instead of a status code

@@ -280,3 +280,95 @@ ENSVS_API int ensvs_layer_norm_bwd(const float* dy, int lddy, const float* x, in
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
+
+// ---------------------------------------------------------------- masked mean of the loss
+// loss.masked_select(mask).mean() of the timing train step (bin/train_multitrack.py:113-121):
+// per-block (sum, count) partials, then one block reduces them in double; out = {mean, count}.
+// The backward spreads g / count over the selected items (zeros elsewhere).
+namespace {
+constexpr int MM_THREADS = 256, MM_MAX_BLOCKS = 512;
+
+__global__ __launch_bounds__(MM_THREADS) void masked_sum_kernel(
+    const float* __restrict__ x, const unsigned char* __restrict__ m, long long n,
+    float* __restrict__ part) {
+  __shared__ float rs[MM_THREADS], rc[MM_THREADS];
+  float s = 0.f, c = 0.f;
+  for (long long i = blockIdx.x * (long long)MM_THREADS + threadIdx.x; i < n;
+       i += (long long)gridDim.x * MM_THREADS) {
+    const bool on = m[i] != 0;
+    s += on ? x[i] : 0.f;
+    c += on ? 1.f : 0.f;
+  }
+  rs[threadIdx.x] = s;
+  rc[threadIdx.x] = c;
+  __syncthreads();
+  for (int st = MM_THREADS / 2; st > 0; st >>= 1) {
+    if (threadIdx.x < st) {
+      rs[threadIdx.x] += rs[threadIdx.x + st];
+      rc[threadIdx.x] += rc[threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = rs[0];
+    part[2 * blockIdx.x + 1] = rc[0];
+  }
+}
+
+__global__ __launch_bounds__(MM_THREADS) void masked_mean_final_kernel(
+    const float* __restrict__ part, int nb, float* __restrict__ out) {
+  __shared__ double rs[MM_THREADS], rc[MM_THREADS];
+  double s = 0.0, c = 0.0;
+  for (int i = threadIdx.x; i < nb; i += MM_THREADS) {
+    s += part[2 * i];
+    c += part[2 * i + 1];
+  }
+  rs[threadIdx.x] = s;
+  rc[threadIdx.x] = c;
+  __syncthreads();
+  for (int st = MM_THREADS / 2; st > 0; st >>= 1) {
+    if (threadIdx.x < st) {
+      rs[threadIdx.x] += rs[threadIdx.x + st];
+      rc[threadIdx.x] += rc[threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = (float)(rs[0] / rc[0]);  // empty selection: 0/0 = nan, as torch's mean
+    out[1] = (float)rc[0];
+  }
+}
+
+__global__ void masked_mean_bwd_kernel(const unsigned char* __restrict__ m, long long n,
+                                       const float* __restrict__ g,
+                                       const float* __restrict__ fwd_out,
+                                       float* __restrict__ dx) {
+  const float v = g[0] / fwd_out[1];
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    dx[i] = m[i] ? v : 0.f;
+}
+}  // namespace
+
+ENSVS_API int ensvs_masked_mean(const float* x, const unsigned char* mask, long long n,
+                                float* part, float* out, void* stream) {
+  if (n < 0) return ENSVS_E_SHAPE;
+  const int nb = (int)std::max(1LL, std::min<long long>(MM_MAX_BLOCKS, (n + 4095) / 4096));
+  hipLaunchKernelGGL(masked_sum_kernel, dim3(nb), dim3(MM_THREADS), 0, (hipStream_t)stream, x,
+                     mask, n, part);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(masked_mean_final_kernel, dim3(1), dim3(MM_THREADS), 0,
+                     (hipStream_t)stream, part, nb, out);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_masked_mean_bwd(const unsigned char* mask, long long n, const float* gout,
+                                    const float* fwd_out, float* dx, void* stream) {
+  if (n <= 0) return n == 0 ? ENSVS_OK : ENSVS_E_SHAPE;
+  const int nb = (int)std::min<long long>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(masked_mean_bwd_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, mask,
+                     n, gout, fwd_out, dx);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}

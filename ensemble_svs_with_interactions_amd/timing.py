@@ -98,6 +98,35 @@ def mdn_loss(log_pi, log_sigma, mu, target, log_pi_min=-7.0, log_sigma_min=-7.0,
     return _MeanTFn.apply(loss) if reduce else loss
 
 
+
+class _MaskedMeanFn(torch.autograd.Function):
+    """loss.masked_select(mask).mean() on the device (ensvs_masked_mean); mask broadcasts
+    to the loss shape as masked_select does."""
+
+    @staticmethod
+    def forward(ctx, x, mask):
+        xc = x.contiguous().float()
+        m = mask.expand(x.shape).contiguous().to(torch.uint8)
+        out = empty(2, device=x.device)
+        part = empty(1024, device=x.device)
+        call("ensvs_masked_mean", xc.data_ptr(), m.data_ptr(), xc.numel(), part.data_ptr(),
+             out.data_ptr(), stream())
+        ctx.save_for_backward(m, out)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        m, out = ctx.saved_tensors
+        dx = empty(*m.shape, device=m.device)
+        call("ensvs_masked_mean_bwd", m.data_ptr(), m.numel(), g.contiguous().data_ptr(),
+             out.data_ptr(), dx.data_ptr(), stream())
+        return dx, None
+
+
+def masked_mean(x, mask):
+    return _MaskedMeanFn.apply(x, mask)
+
+
 @torch.no_grad()
 def mdn_get_most_probable_sigma_and_mu(log_pi, log_sigma, mu):
     """nnsvs/mdn.py:167-212 -> (sigma, mu) of the component with the largest weight."""
@@ -490,3 +519,26 @@ class _VPFn(torch.autograd.Function):
                          table.data_ptr(), stream())
         ctx.st = None
         return None, None, None, None, None
+
+
+def timing_train_step(model, optimizer, x0, x1, y, spk0, spk1, mask, train=True):
+    """train_step of bin/train_multitrack.py:46-154 for the recipe's MDN timing models
+    (MultiTrackVariancePredictor with use_mdn; duration or time-lag): forward on
+    concat(x0, x1) with both tracks' speakers, mdn_loss(reduce=False) masked by the collate's
+    note mask (mask_list[0], (B, T, 1) bool; squeezed unless the MDN is dim-wise) and
+    averaged, backward and one Adam step.  The reference's live pdb.set_trace()
+    (App. A-11) is not reproduced; its AMP grad scaler is not used (fp32); it clips
+    nothing, so pass an optimizer built with clip_norm=float("inf").  FusedAdam skips a
+    non-finite step where torch.optim.Adam would apply it.  Returns the loss (device)."""
+    if not getattr(model, "use_mdn", True):
+        raise NotImplementedError("timing_train_step: the recipe's timing models are MDN models")
+    model.train() if train else model.eval()
+    optimizer.zero_grad()
+    x = torch.cat((x0, x1), dim=2)
+    lp, ls, mu = model(x, (spk0, spk1))
+    mask_ = mask if lp.dim() == 4 else mask.squeeze(-1)
+    loss = masked_mean(mdn_loss(lp, ls, mu, y, reduce=False), mask_)
+    if train:
+        loss.backward()
+        optimizer.step()
+    return loss.detach()

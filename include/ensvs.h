@@ -321,6 +321,13 @@ int ensvs_layer_norm_fwd(const float* x, int ldx, long long M, int C, const floa
 int ensvs_layer_norm_bwd(const float* dy, int lddy, const float* x, int ldx, long long M, int C,
                          const float* gamma, const float* mean, const float* rstd, float* dx,
                          int lddx, float* dyxhat, void* stream);
+/* loss.masked_select(mask).mean() of the timing train step (bin/train_multitrack.py:113-121):
+ * out[0] = mean of x[i] over mask[i] != 0, out[1] = the count (part >= 1024 floats).  The
+ * backward writes dx[i] = mask[i] ? gout[0] / out[1] : 0. */
+int ensvs_masked_mean(const float* x, const unsigned char* mask, long long n, float* part,
+                      float* out, void* stream);
+int ensvs_masked_mean_bwd(const unsigned char* mask, long long n, const float* gout,
+                          const float* fwd_out, float* dx, void* stream);
 
 #ifdef __cplusplus
 }

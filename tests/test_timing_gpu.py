@@ -92,3 +92,52 @@ def test_variance_predictor_matches_reference(name):
         assert abs(gr.norm().item() - l2) <= 1e-4 * l2 + 1e-9, (k, gr.norm().item(), l2)
         if p + "grad::" + k in a:
             assert rel(gr, a[p + "grad::" + k]) < 1e-4, k
+
+
+@pytest.mark.parametrize("name", ["duration", "timelag"])
+def test_timing_train_step(name):
+    """bin/train_multitrack.py:46-154 through timing.timing_train_step: the masked-mean MDN
+    loss and parameter gradients equal the reference-generated ones (variance_predictor
+    golden, same dropout masks), and the first Adam step moves every parameter by
+    lr * g / (|g| + eps) (no clipping in the timing step)."""
+    from ensemble_svs_with_interactions_amd.train import FusedAdam
+
+    engine.set_gemm_precision("fp32")
+    a, meta = load_case("variance_predictor")
+    m, p = meta[name], name + "::"
+    model = timing.MultiTrackVariancePredictor(**m["cfg"])
+    model.load_state_dict(params_from_shapes(m["shapes"]))
+    model = model.cuda()
+    g = lambda k: torch.from_numpy(a[p + k]).cuda()  # noqa: E731
+    x, s0, s1 = g("x"), g("s0"), g("s1")
+    B, T, D2 = x.shape
+    x0, x1 = x[:, :, : D2 // 2].contiguous(), x[:, :, D2 // 2:].contiguous()
+    model._replay_masks = [g(f"mask{i}").transpose(1, 2).contiguous().view(-1)
+                           for i in range(m["cfg"]["num_layers"])]
+    lengths = torch.from_numpy(a[p + "lengths"]).cuda()
+    mask = (torch.arange(T, device="cuda")[None, :] < lengths[:, None]).unsqueeze(-1)
+    lr = 1e-3
+    opt = FusedAdam(model, lr=lr, clip_norm=float("inf"))
+    before = {k: v.detach().clone() for k, v in model.named_parameters()}
+    loss = timing.timing_train_step(model, opt, x0, x1, g("y"), s0, s1, mask)
+    assert rel(loss.cpu(), a[p + "loss"]) < 1e-5
+    for k, (s, ab, l2) in m["grad_summary"].items():
+        gr = dict(model.named_parameters())[k].grad.double().cpu()
+        assert abs(gr.norm().item() - l2) <= 1e-4 * l2 + 1e-9, (k, gr.norm().item(), l2)
+    for k, v in model.named_parameters():
+        gr = v.grad.detach()
+        want = before[k] - lr * gr / (gr.abs() + 1e-8)
+        assert torch.allclose(v.detach(), want, rtol=0, atol=1e-6), k
+
+
+def test_masked_mean_matches_masked_select():
+    x = torch.randn(3, 37, 2, device="cuda")
+    mask = torch.rand(3, 37, 1, device="cuda") < 0.6
+    xr = x.clone().requires_grad_()
+    got = timing.masked_mean(xr, mask)
+    want = x.masked_select(mask).mean()
+    assert rel(got.detach().cpu(), want.cpu()) < 1e-6
+    got.backward()
+    ref = mask.expand_as(x).float() / mask.expand_as(x).sum()
+    assert torch.allclose(xr.grad, ref, rtol=1e-6, atol=0)
+    assert torch.isnan(timing.masked_mean(x, torch.zeros_like(mask)))

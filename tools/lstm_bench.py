@@ -7,7 +7,11 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ensemble_svs_with_interactions_amd import data  # noqa: E402
+from ensemble_svs_with_interactions_amd import _lib  # noqa: E402
 from ensemble_svs_with_interactions_amd._lib import call  # noqa: E402
+
+if len(sys.argv) > 1:  # A/B timing against another build of the library
+    _lib.LIB_PATH = sys.argv[1]
 
 B, T = 30, 1024
 lengths = data.synthetic_batch(B, T, 1000)["lengths"].tolist()

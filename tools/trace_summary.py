@@ -30,7 +30,7 @@ def main(path):
     per_name = collections.defaultdict(lambda: [0.0, 0])
     for s, e, n, q in win:
         per_q[q] += (e - s) / 1e3
-        short = n.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+        short = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
         per_name[short][0] += (e - s) / 1e3
         per_name[short][1] += 1
     for q, b in sorted(per_q.items()):
@@ -46,7 +46,7 @@ def main(path):
             cur_e = max(cur_e, e)
     busy += cur_e - cur_s
     print(f"  GPU busy (any kernel): {busy / 1e3:.0f} us ({busy / 1e3 / wall * 100:.1f}%)")
-    for n, (t, c) in sorted(per_name.items(), key=lambda kv: -kv[1][0])[:20]:
+    for n, (t, c) in sorted(per_name.items(), key=lambda kv: -kv[1][0])[:30]:
         print(f"  {t:8.0f} us {c:5d}x  {n[:90]}")
 
 

@@ -35,11 +35,15 @@ namespace {
 // is bound by its dependent dot-product chain and prefers 1024.
 template <int H> struct Geo {
   static constexpr int KPF = H == 64 ? 8 : 4, KPB = H >= 64 ? 8 : 4;
-  static constexpr int TF = H * KPF, TB = H * KPB;  // threads
+  // bwd units per lane group: at H=128 one group of KPB lanes serves two units, so each
+  // dG value read from LDS feeds two dot products (the step is bound by LDS data return:
+  // lanes x 4H/KPB floats per step, halved with the lane count)
+  static constexpr int UPB = H >= 128 ? 2 : 1;
+  static constexpr int TF = H * KPF, TB = H * KPB / UPB;  // threads
   static constexpr int Q = H / KPF;                 // fwd: h elements per lane
   static constexpr int QB = 4 * H / KPB;            // bwd: dG elements per lane
-  // steps per staged chunk (bwd H=128: 8, keeping its prefetch within 128 VGPRs)
-  static constexpr int CHF = 16, CHB = H >= 128 ? 8 : 16;
+  // steps per staged chunk (bwd H=128: 4, keeping its prefetch next to 2 x 64 weights)
+  static constexpr int CHF = 16, CHB = H >= 128 ? 4 : 16;
   // The exchanged vectors (h: KPF parts of Q, dG: KPB parts of QB) are stored with a
   // 16-B pad after each part, so the distinct addresses one wave reads per
   // ds_read_b128 fall in distinct banks.
@@ -218,6 +222,7 @@ __global__ __launch_bounds__(Geo<H>::TB) void lstm_bwd_kernel(
     float* __restrict__ dg, int lddg) {           // [B*T][lddg], dir d pre-act grads at d*4H + g*H + u
   using G = Geo<H>;
   constexpr int KP = G::KPB, QB = G::QB, NT = G::TB, IW = 7 * H, GW = 4 * H, CH = G::CHB;
+  constexpr int UP = G::UPB, HU = H / UP;  // units per lane group, group count
   constexpr int NIN = CH * IW / 4;                 // float4 per input chunk
   constexpr int PF = (NIN + NT - 1) / NT;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -225,15 +230,22 @@ __global__ __launch_bounds__(Geo<H>::TB) void lstm_bwd_kernel(
   float* gin = gbuf + 2 * G::GBUF;  // [CH][7H]: i f g o c (row t), dy (row t), c (previous step)
   float* out = gin + CH * IW;     // [CH][4H]
   const int b = blockIdx.x, dir = blockIdx.y;
-  const int tid = threadIdx.x, u = tid / KP, q = tid % KP, gq = q & 3;
+  // lane group grp serves units grp + k*HU (k < UP); lane q evaluates gate q&3 of unit
+  // uq (UP = 2: lanes 0-3 the first unit, 4-7 the second) and holds, for every unit of
+  // its group, column u of part q of W_hh (QB rows)
+  const int tid = threadIdx.x, grp = tid / KP, q = tid % KP, gq = q & 3;
+  const int uk = UP == 1 ? 0 : q / (KP / UP), u = grp + uk * HU;
   const int L = (int)lengths[b];
   const float* W = dir ? whh1 : whh0;
 
-  float w[QB];
+  float w[UP][QB];
 #pragma unroll
-  for (int j = 0; j < QB; ++j) w[j] = W[(long long)(q * QB + j) * H + u];
-  settle(w);
-  const int f = gq * H + u;                      // this lane's gate gradient (q < 4)
+  for (int k = 0; k < UP; ++k) {
+#pragma unroll
+    for (int j = 0; j < QB; ++j) w[k][j] = W[(long long)(q * QB + j) * H + grp + k * HU];
+    settle(w[k]);
+  }
+  const int f = gq * H + u;                      // this lane's gate gradient
   const int gslot = (f / QB) * G::GP + f % QB;
 
   const long long rowb = (long long)b * T;
@@ -302,16 +314,26 @@ __global__ __launch_bounds__(Geo<H>::TB) void lstm_bwd_kernel(
       const float dgs[4] = {d_i, d_f, d_g, d_o};
       const float mine = pick4(dgs, gq);
       float* gb = gbuf + (s & 1) * G::GBUF;
-      if (q < 4) {
+      if (UP == 2 || q < 4) {
         gb[gslot] = mine;
         out[st * GW + f] = mine;
       }
       __syncthreads();
       const float* gp = gb + q * G::GP;
-      float p[4] = {0.f, 0.f, 0.f, 0.f};  // 4 chains: the FMA latency, not issue, bounds one
+      // 4 chains per unit: the FMA latency, not issue, bounds one
+      float p[UP][4];
 #pragma unroll
-      for (int j = 0; j < QB; ++j) p[j & 3] = fmaf(w[j], gp[j], p[j & 3]);
-      dhr = unit_sum<KP>((p[0] + p[1]) + (p[2] + p[3]));
+      for (int k = 0; k < UP; ++k) p[k][0] = p[k][1] = p[k][2] = p[k][3] = 0.f;
+#pragma unroll
+      for (int j = 0; j < QB; ++j) {
+        const float gv = gp[j];
+#pragma unroll
+        for (int k = 0; k < UP; ++k) p[k][j & 3] = fmaf(w[k][j], gv, p[k][j & 3]);
+      }
+      float dsum[UP];
+#pragma unroll
+      for (int k = 0; k < UP; ++k) dsum[k] = unit_sum<KP>((p[k][0] + p[k][1]) + (p[k][2] + p[k][3]));
+      dhr = UP == 1 ? dsum[0] : (uk == 0 ? dsum[0] : dsum[UP - 1]);
     }
     __syncthreads();
     if (ch + 1 < nch) store_in();

@@ -452,11 +452,8 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
         return out
 
     # ------------------------------------------------------------------ training
-    def _train_fwd(self, x_main, x_sub, y_main, spk0, spk1, lengths, draws=None):
-        """One training forward.  x_* (B, T, in_dim), y_main (B, T, out_dim) contiguous fp32
-        device tensors.  Returns (outputs dict of (B*T, .) tensors, state)."""
+    def _fwd_prologue(self, x_main, x_sub, y_main, spk0, spk1, lengths, draws):
         self._set_lf0_params()
-        draws = draws or {}
         B, T, D = x_main.shape
         Dy = y_main.shape[2]
         dev = x_main.device
@@ -464,69 +461,86 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
         (s0, i0), (s1, i1) = self._spk_vectors(spk0, spk1, B)
         E = s0.shape[1]
         o = self._stream_cols()
-        enc_src = [(x_main, D, 0, D), (y_main, Dy, o[1], o[2] - o[1])]
+        st = dict(i0=i0, i1=i1, B=B, T=T, E=E, lens_host=lens_host, lens_dev=lens_dev)
+        c = dict(x_main=x_main, x_sub=x_sub, y_main=y_main, D=D, Dy=Dy, o=o, s0=s0, s1=s1,
+                 draws=draws or {}, enc_src=[(x_main, D, 0, D), (y_main, Dy, o[1], o[2] - o[1])])
+        return c, st
+
+    def _fwd_branch(self, i, c, outs, st):
+        """Forward of branch i (0 lf0, 1 mgc, 2 bap, 3 V/UV) into outs / st."""
+        B, T, E, lens_dev = st["B"], st["T"], st["E"], st["lens_dev"]
+        x_main, x_sub, y_main, D, Dy, o = c["x_main"], c["x_sub"], c["y_main"], c["D"], c["Dy"], c["o"]
+        s0, s1, draws = c["s0"], c["s1"], c["draws"]
+        if i == 0:
+            lf0, res, st["lf0"] = self.lf0_model._fwd(x_main, x_sub, D, B, T, lens_dev, s0, s1, E,
+                                                      masks=draws.get("lf0_main"))
+            outs.update(lf0=lf0, lf0_residual=res)
+            if self.output_subtrack:
+                # sub-track call with its outputs (multistream.py:1649-1651, 1759-1768):
+                # the lf0 prediction the interaction loss compares with the main one.
+                # Same stream as the main call: BatchNorm running statistics are
+                # updated main-then-sub, as in the reference.
+                lf0_s, res_s, st["lf0_sub"] = self.lf0_model._fwd(
+                    x_sub, x_main, D, B, T, lens_dev, s1, s0, E, masks=draws.get("lf0_sub"))
+                outs.update(lf0_sub=lf0_s, lf0_residual_sub=res_s)
+            elif self.training:
+                # sub-track call (outputs unused without output_subtrack): BN statistics
+                self.lf0_model._bn_only(x_sub, x_main, D, B, T, s1, s0, E)
+        elif i == 1:
+            nm, rm, st["mgc"] = self.mgc_model._fwd(c["enc_src"], B, T, lens_dev, (y_main, Dy, o[0]),
+                                                    s0, E, t=draws.get("mgc_t"),
+                                                    noise=draws.get("mgc_noise"))
+            outs.update(mgc_noise=nm, mgc_recon=rm)
+        elif i == 2:
+            nb, rb, st["bap"] = self.bap_model._fwd(c["enc_src"], B, T, lens_dev, (y_main, Dy, o[3]),
+                                                    s0, E, t=draws.get("bap_t"),
+                                                    noise=draws.get("bap_noise"))
+            outs.update(bap_noise=nb, bap_recon=rb)
+        else:
+            outs["vuv"], st["vuv"] = self.vuv_model._fwd(self._vuv_sources(x_main, D, y_main, Dy),
+                                                         B, T, lens_dev, s0, E,
+                                                         lstm_masks=draws.get("vuv_lstm"))
+
+    def _train_fwd(self, x_main, x_sub, y_main, spk0, spk1, lengths, draws=None):
+        """One training forward.  x_* (B, T, in_dim), y_main (B, T, out_dim) contiguous fp32
+        device tensors.  Returns (outputs dict of (B*T, .) tensors, state)."""
+        c, st = self._fwd_prologue(x_main, x_sub, y_main, spk0, spk1, lengths, draws)
+        outs = {}
         # The four branches are independent until the loss: concurrent HIP streams
         # (the recurrences alone occupy only 2*B workgroups each).
-        with Branches(dev) as br:
-            with br.on(0):
-                lf0, res, st_lf0 = self.lf0_model._fwd(x_main, x_sub, D, B, T, lens_dev, s0, s1,
-                                                       E, masks=draws.get("lf0_main"))
-                if self.output_subtrack:
-                    # sub-track call with its outputs (multistream.py:1649-1651, 1759-1768):
-                    # the lf0 prediction the interaction loss compares with the main one.
-                    # Same stream as the main call: BatchNorm running statistics are
-                    # updated main-then-sub, as in the reference.
-                    lf0_s, res_s, st_lf0_s = self.lf0_model._fwd(
-                        x_sub, x_main, D, B, T, lens_dev, s1, s0, E, masks=draws.get("lf0_sub"))
-                elif self.training:
-                    # sub-track call (outputs unused without output_subtrack): BN statistics
-                    self.lf0_model._bn_only(x_sub, x_main, D, B, T, s1, s0, E)
-            with br.on(1):
-                nm, rm, st_mgc = self.mgc_model._fwd(enc_src, B, T, lens_dev, (y_main, Dy, o[0]),
-                                                     s0, E, t=draws.get("mgc_t"),
-                                                     noise=draws.get("mgc_noise"))
-            with br.on(2):
-                nb, rb, st_bap = self.bap_model._fwd(enc_src, B, T, lens_dev, (y_main, Dy, o[3]),
-                                                     s0, E, t=draws.get("bap_t"),
-                                                     noise=draws.get("bap_noise"))
-            with br.on(3):
-                vuv, st_vuv = self.vuv_model._fwd(self._vuv_sources(x_main, D, y_main, Dy), B, T,
-                                                  lens_dev, s0, E,
-                                                  lstm_masks=draws.get("vuv_lstm"))
-        outs = dict(mgc_noise=nm, mgc_recon=rm, lf0=lf0, vuv=vuv, bap_noise=nb, bap_recon=rb,
-                    lf0_residual=res)
-        st = dict(lf0=st_lf0, mgc=st_mgc, bap=st_bap, vuv=st_vuv, i0=i0, i1=i1, B=B, T=T, E=E,
-                  lens_host=lens_host, lens_dev=lens_dev)
-        if self.output_subtrack:
-            outs.update(lf0_sub=lf0_s, lf0_residual_sub=res_s)
-            st["lf0_sub"] = st_lf0_s
+        with Branches(x_main.device) as br:
+            for i in range(4):
+                with br.on(i):
+                    self._fwd_branch(i, c, outs, st)
         return outs, st
 
-    def _train_bwd(self, st, g):
-        """g: dict of grads (B*T, .) for mgc_recon, lf0, vuv, bap_recon [, lf0_residual]
-        [, lf0_sub, lf0_residual_sub (output_subtrack)]."""
+    def _bwd_branch(self, i, st, g, dsp):
+        """Backward of branch i from its output grads g; its speaker-vector grads -> dsp."""
+        if i == 0:
+            dmain, dsub, _ = self.lf0_model._bwd(st["lf0"], g["lf0"], g.get("lf0_residual"))
+            dsp["lf0"], dsp["lf0_sub_in"] = dmain, dsub
+            if st.get("lf0_sub") is not None and (g.get("lf0_sub") is not None or
+                                                  g.get("lf0_residual_sub") is not None):
+                gs = g.get("lf0_sub")
+                if gs is None:
+                    gs = torch.zeros(st["B"] * st["T"], device=st["lens_dev"].device)
+                dsp["lf0_sub"], _, _ = self.lf0_model._bwd(st["lf0_sub"], gs,
+                                                           g.get("lf0_residual_sub"))
+        elif i == 1:
+            dsp["mgc"] = self.mgc_model._bwd(st["mgc"], g["mgc_recon"])
+        elif i == 2:
+            dsp["bap"] = self.bap_model._bwd(st["bap"], g["bap_recon"])
+        else:
+            _, dsp["vuv"] = self.vuv_model._bwd(st["vuv"], g["vuv"], want_spk=True)
+
+    def _bwd_epilogue(self, st, dsp):
+        """Speaker-embedding gradient: the branch contributions, summed after the join."""
         B, E = st["B"], st["E"]
         dev = st["lens_dev"].device
-        dsc = None
-        with Branches(dev) as br:  # same branch -> stream assignment as _train_fwd
-            with br.on(0):
-                dmain, dsub, _ = self.lf0_model._bwd(st["lf0"], g["lf0"], g.get("lf0_residual"))
-                if st.get("lf0_sub") is not None and (g.get("lf0_sub") is not None or
-                                                      g.get("lf0_residual_sub") is not None):
-                    gs = g.get("lf0_sub")
-                    if gs is None:
-                        gs = torch.zeros(B * st["T"], device=dev)
-                    dsc, _, _ = self.lf0_model._bwd(st["lf0_sub"], gs, g.get("lf0_residual_sub"))
-            with br.on(1):
-                dsp_m = self.mgc_model._bwd(st["mgc"], g["mgc_recon"])
-            with br.on(2):
-                dsp_b = self.bap_model._bwd(st["bap"], g["bap_recon"])
-            with br.on(3):
-                _, dsp_v = self.vuv_model._bwd(st["vuv"], g["vuv"], want_spk=True)
-        # speaker-embedding gradient: the four branch contributions, summed after the join
+        dsc, dsub = dsp.get("lf0_sub"), dsp["lf0_sub_in"]
         ds0 = torch.zeros(B, E, device=dev)
-        for dsp in (dsp_m, dsp_b, dsp_v, dmain) + ((dsc,) if dsc is not None else ()):
-            call("ensvs_axpy", ds0.data_ptr(), dsp.data_ptr(), 1.0, B * E, Ly.stream())
+        for k in ("mgc", "bap", "vuv", "lf0") + (("lf0_sub",) if dsc is not None else ()):
+            call("ensvs_axpy", ds0.data_ptr(), dsp[k].data_ptr(), 1.0, B * E, Ly.stream())
         if dsc is not None:  # the sub call's fused input holds both speaker vectors too
             call("ensvs_axpy", dsub.data_ptr(), dsc.data_ptr(), 1.0, B * E, Ly.stream())
         table = grad_of(self.speaker_embedding.emb.weight)
@@ -534,6 +548,37 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
              Ly.stream())
         call("ensvs_spk_scatter", dsub.data_ptr(), B, E, st["i1"].data_ptr(), table.data_ptr(),
              Ly.stream())
+
+    def _train_bwd(self, st, g):
+        """g: dict of grads (B*T, .) for mgc_recon, lf0, vuv, bap_recon [, lf0_residual]
+        [, lf0_sub, lf0_residual_sub (output_subtrack)]."""
+        dsp = {}
+        with Branches(st["lens_dev"].device) as br:  # same branch -> stream assignment as _train_fwd
+            for i in range(4):
+                with br.on(i):
+                    self._bwd_branch(i, st, g, dsp)
+        self._bwd_epilogue(st, dsp)
+
+    def _train_fused(self, x_main, x_sub, y_main, spk0, spk1, lengths, draws, branch_loss):
+        """Training forward + loss gradient + backward with each branch end to end on its
+        own stream: a branch's loss gradient needs only its own outputs (the masked L1
+        normaliser is known on the host), so its backward starts when its forward ends,
+        not when the slowest forward does.  branch_loss(i, outs, st) -> (partial loss
+        (1,) tensor, grads dict of branch i); the partial losses are summed after the
+        join.  Returns (loss, outs)."""
+        c, st = self._fwd_prologue(x_main, x_sub, y_main, spk0, spk1, lengths, draws)
+        outs, dsp, parts = {}, {}, {}
+        with Branches(x_main.device) as br:
+            for i in range(4):
+                with br.on(i):
+                    self._fwd_branch(i, c, outs, st)
+                    parts[i], g = branch_loss(i, outs, st)
+                    self._bwd_branch(i, st, g, dsp)
+        loss = parts[0]
+        for i in (1, 2, 3):
+            call("ensvs_axpy", loss.data_ptr(), parts[i].data_ptr(), 1.0, 1, Ly.stream())
+        self._bwd_epilogue(st, dsp)
+        return loss, outs
 
     # ------------------------------------------------------------------ inference
     def _infer(self, x_main, x_sub, spk0, spk1, lengths, noises=None, masks=None, graph=None):

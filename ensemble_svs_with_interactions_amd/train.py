@@ -81,12 +81,15 @@ class FusedAdam:
         weights_updated()
 
 
-def masked_l1(preds, targets, lengths_dev, n_valid_frames, B, T, grad_scale=1.0):
+def masked_l1(preds, targets, lengths_dev, n_valid_frames, B, T, grad_scale=1.0,
+              total_cols=None):
     """Masked L1 summed over streams / element count, with its gradient.
 
     preds/targets: lists of (tensor, ld, col) with stream widths.  Returns
     (loss (1,) device tensor, list of grad tensors (B*T, n)).  The gradients are
     additionally multiplied by ``grad_scale`` (1/world under data parallelism).
+    total_cols: the element count's stream width when these streams are part of a
+    larger loss (default: their own widths).
     """
     ns = len(preds)
     dev = preds[0][0].device
@@ -107,7 +110,7 @@ def masked_l1(preds, targets, lengths_dev, n_valid_frames, B, T, grad_scale=1.0)
         pg[i] = g.data_ptr()
         la[i], lb[i], lg[i], nn_[i] = lda, ldb, n, n
         total += n
-    N = n_valid_frames * total
+    N = n_valid_frames * (total if total_cols is None else total_cols)
     part = empty(1024, device=dev)
     loss = empty(1, device=dev)
     call("ensvs_masked_l1", ctypes.addressof(pa), ctypes.addressof(pb), ctypes.addressof(pg),
@@ -156,6 +159,11 @@ def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, 
     """zero_grad + forward + masked L1 (+ interaction loss) + backward into the flat grads."""
     model.train()
     optimizer.zero_grad()
+    if logf0_diff_weight > 0.0 and (not model.output_subtrack or y_sub is None):
+        raise ValueError("logf0_diff_weight > 0 needs output_subtrack=True and y_sub")
+    if _STATE_FUSED["on"]:
+        return _loss_and_grads_fused(model, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
+                                     draws, ddp, y_sub, logf0_diff_weight)
     outs, st = model._train_fwd(x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws)
     B, T = st["B"], st["T"]
     Dy = y_main.shape[2]
@@ -181,6 +189,60 @@ def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, 
              g["lf0"].data_ptr(), g_sub.data_ptr(), Ly.stream())
         g["lf0_sub"] = g_sub
     model._train_bwd(st, g)
+    return loss
+
+
+# Per-branch fused schedule (forward -> loss gradient -> backward of each branch on its own
+# stream, acoustic_models._train_fused).  Off by default: measured 22.3 vs 22.0 ms/step for
+# the forward-all / loss / backward-all schedule (graph replay, 30 x 1024) -- the short
+# branches' backward then contends with the mgc forward, the longest chain.
+# ENSVS_FUSED_BRANCHES=1 turns it on.
+import os as _os  # noqa: E402
+_STATE_FUSED = {"on": _os.environ.get("ENSVS_FUSED_BRANCHES", "0") == "1"}
+
+
+def set_fused_branches(on: bool):
+    _STATE_FUSED["on"] = bool(on)
+
+
+def _loss_and_grads_fused(model, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws,
+                          ddp, y_sub, logf0_diff_weight):
+    """The loss of _loss_and_grads split by branch: each branch's masked L1 over its own
+    streams with the whole loss's element count (same gradients, elementwise), the
+    interaction loss inside the lf0 branch; partial losses summed after the join."""
+    Dy = y_main.shape[2]
+    o = model._stream_cols()
+    nm, nb = model.stream_sizes[0], model.stream_sizes[3]
+    W = world_size() if ddp else 1
+    total = nm + 1 + 1 + nb
+
+    def branch_loss(i, outs, st):
+        B, T = st["B"], st["T"]
+        nvalid = sum(st["lens_host"])
+        if i == 1:
+            pt = [(outs["mgc_recon"], nm, 0, nm)], [(outs["mgc_noise"], nm, 0)], "mgc_recon"
+        elif i == 2:
+            pt = [(outs["bap_recon"], nb, 0, nb)], [(outs["bap_noise"], nb, 0)], "bap_recon"
+        elif i == 3:
+            pt = [(outs["vuv"], 1, 0, 1)], [(y_main, Dy, o[2])], "vuv"
+        else:
+            pt = [(outs["lf0"], 1, 0, 1)], [(y_main, Dy, o[1])], "lf0"
+        loss, (gi,) = masked_l1(pt[0], pt[1], st["lens_dev"], nvalid, B, T, grad_scale=1.0 / W,
+                                total_cols=total)
+        g = {pt[2]: gi.view(-1) if i == 0 else gi}
+        if i == 0 and logf0_diff_weight > 0.0:
+            ys = y_sub.contiguous().float()
+            g_sub = empty(B * T, device=y_main.device)
+            part = empty(1024, device=y_main.device)
+            call("ensvs_lf0_interaction", outs["lf0"].data_ptr(), outs["lf0_sub"].data_ptr(),
+                 y_main.data_ptr(), ys.data_ptr(), Dy, o[1], o[2], st["lens_dev"].data_ptr(), B,
+                 T, float(logf0_diff_weight), 1.0 / W, part.data_ptr(), loss.data_ptr(),
+                 g["lf0"].data_ptr(), g_sub.data_ptr(), Ly.stream())
+            g["lf0_sub"] = g_sub
+        return loss, g
+
+    loss, _ = model._train_fused(x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws,
+                                 branch_loss)
     return loss
 
 

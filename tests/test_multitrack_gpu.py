@@ -176,3 +176,36 @@ def test_concurrent_branches_bitwise_equal_serial(prec):
     assert torch.equal(res[0][1], res[1][1])
     for k in res[0][2]:
         assert torch.equal(res[0][2][k], res[1][2][k]), k
+
+
+@pytest.mark.parametrize("case", ["train_step_tiny", "train_step_tiny_il"])
+def test_fused_branch_schedule_matches(case):
+    """train.set_fused_branches(True) (each branch's forward, loss gradient and backward on
+    its own stream) gives the same gradients bit for bit, and the loss up to the order of
+    its per-branch partial sums, as the forward-all / loss / backward-all schedule."""
+    from ensemble_svs_with_interactions_amd.train import set_fused_branches
+
+    engine.set_gemm_precision("fp32")
+    a, meta = load_case(case)
+    w_il = meta.get("logf0_diff_weight", 0.0)
+    xm, xs, ym, s0, s1, lens = _batch(a)
+    ysub = torch.from_numpy(a["y_sub"]).cuda().contiguous()
+    B, T = xm.shape[:2]
+    res = []
+    try:
+        for fused in (False, True):
+            set_fused_branches(fused)
+            model = build(configs.multitrack_diffusion(num_speakers=4, tiny=True,
+                                                       output_subtrack=w_il > 0), meta["shapes"])
+            model.vuv_model.lstm.dropout = 0.0
+            opt = FusedAdam(model, lr=meta["lr"])
+            loss, norm = train_step(model, opt, xm, xs, ym, s0, s1, lens,
+                                    draws=_draws(a, "draw0::", B, T), y_sub=ysub,
+                                    logf0_diff_weight=w_il)
+            torch.cuda.synchronize()
+            res.append((loss.item(), opt.gflat.clone()))
+    finally:
+        set_fused_branches(False)
+    assert abs(res[0][0] - res[1][0]) <= 1e-6 * abs(res[0][0])
+    assert torch.equal(res[0][1], res[1][1])
+    assert abs(res[1][0] - meta["losses"][0]) < 1e-5 * abs(meta["losses"][0])

@@ -11,6 +11,8 @@ Same constructor arguments, forward/inference signatures, prediction types
 and state_dict keys as the reference; ``_target_`` strings are the only change
 a recipe needs (configs.py).
 """
+import os
+
 import torch
 from torch import nn
 
@@ -22,6 +24,12 @@ from .base import BaseModel, PredictionType
 from .engine import Branches, ModulePacks, _sig, empty, grad_of, lengths_pair
 from .model import init_weights
 
+
+
+# Backward schedule option: the V/UV branch's backward starts after the mgc DiffNet
+# backward (ENSVS_VUV_AFTER_MGC=1).  Off: measured 24.9 vs 22.2 ms/step (graph replay,
+# 30 x 1024) -- the V/UV recurrences then lengthen the tail instead of filling it.
+_VUV_AFTER_MGC = {"on": os.environ.get("ENSVS_VUV_AFTER_MGC", "0") == "1"}
 
 class ZoneOutCell(nn.Module):
     """nnsvs/tacotron/decoder.py:20-48 (container).  The recipe uses zoneout 0, for which
@@ -527,10 +535,21 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
                 dsp["lf0_sub"], _, _ = self.lf0_model._bwd(st["lf0_sub"], gs,
                                                            g.get("lf0_residual_sub"))
         elif i == 1:
-            dsp["mgc"] = self.mgc_model._bwd(st["mgc"], g["mgc_recon"])
+            hook = None
+            if _VUV_AFTER_MGC["on"] and torch.cuda.is_available() and g["mgc_recon"].is_cuda:
+                ev = torch.cuda.Event()
+                dsp["_mgc_denoiser_done"] = ev
+                hook = lambda: ev.record(torch.cuda.current_stream())  # noqa: E731
+            dsp["mgc"] = self.mgc_model._bwd(st["mgc"], g["mgc_recon"], after_denoiser=hook)
         elif i == 2:
             dsp["bap"] = self.bap_model._bwd(st["bap"], g["bap_recon"])
         else:
+            ev = dsp.get("_mgc_denoiser_done")
+            if ev is not None:
+                # the V/UV backward (LSTM recurrences on 2B workgroups) waits for the mgc
+                # DiffNet backward so that it overlaps the mgc encoder's recurrences at the
+                # tail of the step instead of contending with the DiffNet GEMMs
+                torch.cuda.current_stream().wait_event(ev)
             _, dsp["vuv"] = self.vuv_model._bwd(st["vuv"], g["vuv"], want_spk=True)
 
     def _bwd_epilogue(self, st, dsp):

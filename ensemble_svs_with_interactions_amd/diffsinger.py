@@ -570,8 +570,12 @@ class GaussianDiffusion(BaseModel):
         xr, dst = self.denoise_fn._fwd(xn, Mc, t, cond, E, B, T, save=save)
         return noise, xr, dict(est=est, dst=dst)
 
-    def _bwd(self, st, dxr):
+    def _bwd(self, st, dxr, after_denoiser=None):
+        """after_denoiser: called between the DiffNet and the encoder backward (the step
+        schedule records a stream event there)."""
         dcond = self.denoise_fn._bwd(st["dst"], dxr)
+        if after_denoiser is not None:
+            after_denoiser()
         _, dspk = self.encoder._bwd(st["est"], dcond, want_spk=True)
         return dspk
 

@@ -123,8 +123,10 @@ def synth_rtf(model, dev, T=2000, parts=6, reps=3):
     """Synthesis real-time factor (BASELINE metric part 2): elapsed /
     audio seconds (svs.py:449-452, 581-582) of acoustic inference (pad_inference_multitrack,
     free-running AR log-F0, 100-step reverse diffusion for mgc and bap, V/UV) + the uSFGAN
-    generator on its output, for one (main, sub) pair of T frames (5 ms) and for a
-    `parts`-part ensemble (every part paired with its neighbour) batched in one pass.
+    generator on its output, for one (main, sub) pair of T frames (5 ms), for a
+    `parts`-part ensemble (every part paired with its neighbour) batched in one pass, and
+    for the reference's ordered-pair sweep (synthesis_multitrack.py:113-118: every part
+    with every partner, itself included: parts^2 pairs) batched in one pass.
     Host glue of the reference (scalers, pyworld aperiodicity codec, gen.py:1637-1694) is
     replaced by identity scalers on synthetic data."""
     from ensemble_svs_with_interactions_amd import usfgan
@@ -136,7 +138,8 @@ def synth_rtf(model, dev, T=2000, parts=6, reps=3):
     model.eval()
     sc, mu = configs.LF0_STATS["out_lf0_scale"], configs.LF0_STATS["out_lf0_mean"]
     out = {}
-    for name, B in (("pair", 1), (f"ensemble_{parts}part", parts)):
+    for name, B in (("pair", 1), (f"ensemble_{parts}part", parts),
+                    (f"n2_sweep_{parts}part", parts * parts)):
         b = data.synthetic_batch(B, T, 4242 + B)
         g = lambda k: torch.from_numpy(b[k]).to(dev).contiguous()  # noqa: E731
         xm, xs, s0, s1 = g("x_main"), g("x_sub"), g("spk_main"), g("spk_sub")

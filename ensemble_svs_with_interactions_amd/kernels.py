@@ -4,6 +4,7 @@ Everything here only moves pointers and sizes; all arithmetic happens in the
 HIP kernels of ``csrc/``.  Tensors are fp32, channels-last frame rows.
 """
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -140,8 +141,12 @@ class Seg:
 
 # bf16-operand GEMMs: activations rounded to bf16 in HBM by one cast pass (radd fused),
 # then both operands staged by global_load_lds (ensvs_conv_gemm_bf16a).  Same bits as the
-# register-staged kernel; pays where the A tile is re-read (several N tiles or taps).
-BF16_ACT = {"on": True, "stages": 2, "min_reuse": 2, "min_rows": 8192}
+# register-staged kernel; pays where the A tile is re-read (several N tiles or taps) --
+# at every row count: at M = 2 000 (one pair of 10 s in the reverse diffusion) a
+# register-staged DiffNet GEMM launch averaged 33 us against ~10 us here (pair inference
+# 185 -> 102 ms), so there is no row threshold by default (ENSVS_BF16_MIN_ROWS sets one).
+BF16_ACT = {"on": True, "stages": 2, "min_reuse": 2,
+            "min_rows": int(os.environ.get("ENSVS_BF16_MIN_ROWS", "0"))}
 
 
 def _bf16_act_ok(segs, W, Npad, M):

@@ -21,7 +21,7 @@ from . import kernels as K
 from . import layers as Ly
 from ._lib import call, ptr
 from .base import BaseModel, PredictionType
-from .engine import Branches, ModulePacks, _sig, empty, grad_of, lengths_pair
+from .engine import Branches, GradCapture, ModulePacks, _sig, empty, grad_of, lengths_pair
 from .model import init_weights
 
 
@@ -333,12 +333,12 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
             raise NotImplementedError("teacher-forced lf0 decoding is not used by the "
                                       "multi-track diffusion model (multistream.py:1646-1651)")
         return _Lf0Fn.apply(self, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths,
-                            self.fc_in.weight)
+                            *self.parameters())
 
 
 class _Lf0Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, mod, x_main, x_sub, s0, s1, lengths, anchor):
+    def forward(ctx, mod, x_main, x_sub, s0, s1, lengths, *params):
         from .model import _spk_args
         B, T, D = x_main.shape
         x_main = x_main.contiguous().float()
@@ -349,7 +349,7 @@ class _Lf0Fn(torch.autograd.Function):
         if f0 is not None or f1 is not None or ld0 != ld1:
             raise NotImplementedError("per-frame speaker embeddings are not on the path")
         lf0, res, st = mod._fwd(x_main, x_sub, D, B, T, lens_dev, p0, p1, ld0)
-        ctx.mod, ctx.st = mod, st
+        ctx.mod, ctx.st, ctx.params = mod, st, params
         ctx.needs = (s0 is not None and s0.requires_grad, s1 is not None and s1.requires_grad)
         return lf0.view(B, T, 1), res.view(B, T, 1)
 
@@ -360,12 +360,13 @@ class _Lf0Fn(torch.autograd.Function):
         dev = st["y"].device
         glf0 = glf0.contiguous().view(-1) if glf0 is not None else torch.zeros(B * T, device=dev)
         gres = gres.contiguous().view(-1) if gres is not None else None
-        _, _, dX0 = ctx.mod._bwd(st, glf0, gres, want_spk=False)
-        ctx.st = None
+        with GradCapture(ctx.params) as gc:
+            _, _, dX0 = ctx.mod._bwd(st, glf0, gres, want_spk=False)
+        ctx.st = ctx.params = None
         # per-frame grad of each (expanded) speaker embedding = grad of the fused input
         d = dX0.view(B, T, -1)
         return (None, None, None, d if ctx.needs[0] else None, d if ctx.needs[1] else None,
-                None, None)
+                None) + gc.grads(ctx.needs_input_grad[6:])
 
 
 class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
@@ -648,7 +649,7 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
                               spks_list[0], spks_list[1], lengths)
             return out, out
         outs = _MultiTrackFn.apply(self, x_main, x_sub, ys[0], spks_list[0], spks_list[1],
-                                   lengths, self.speaker_embedding.emb.weight)
+                                   lengths, *self.parameters())
         nm, rm, lf0, vuv, nb, rb, res = outs[:7]
         main = (((nm, rm), lf0, vuv, (nb, rb)), res)
         if not self.output_subtrack:
@@ -684,13 +685,13 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
 
 class _MultiTrackFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, mod, x_main, x_sub, y_main, spk0, spk1, lengths, anchor):
+    def forward(ctx, mod, x_main, x_sub, y_main, spk0, spk1, lengths, *params):
         B, T, _ = x_main.shape
         # _replay_draws (tests only): random draws to replay, as train_step(draws=...)
         outs, st = mod._train_fwd(x_main.contiguous().float(), x_sub.contiguous().float(),
                                   y_main.contiguous().float(), spk0, spk1, lengths,
                                   getattr(mod, "_replay_draws", None))
-        ctx.mod, ctx.st = mod, st
+        ctx.mod, ctx.st, ctx.params = mod, st, params
         ctx.mark_non_differentiable(outs["mgc_noise"], outs["bap_noise"])
         v = lambda t: t.view(B, T, -1)  # noqa: E731
         ret = (v(outs["mgc_noise"]), v(outs["mgc_recon"]), v(outs["lf0"]), v(outs["vuv"]),
@@ -718,6 +719,7 @@ class _MultiTrackFn(torch.autograd.Function):
             g["lf0_sub"] = g_sub[0].contiguous().view(-1)
         if g_sub and g_sub[1] is not None:
             g["lf0_residual_sub"] = g_sub[1].contiguous().view(-1)
-        ctx.mod._train_bwd(st, g)
-        ctx.st = None
-        return (None,) * 8
+        with GradCapture(ctx.params) as gc:
+            ctx.mod._train_bwd(st, g)
+        ctx.st = ctx.params = None
+        return (None,) * 7 + gc.grads(ctx.needs_input_grad[7:])

@@ -29,7 +29,7 @@ from . import kernels as K
 from . import layers as Ly
 from ._lib import call
 from .base import BaseModel, PredictionType
-from .engine import AuxStream, ModulePacks, empty, grad_of, lengths_pair, next_seed
+from .engine import GradCapture, ModulePacks, empty, grad_of, lengths_pair, next_seed
 from .engine import gemm_dtype as engine_gemm_dtype
 
 SQRT1_2 = 1.0 / math.sqrt(2.0)
@@ -273,9 +273,6 @@ class DiffNet(nn.Module):
         fuse = T % K.BM == 0
         dd_tiles = empty(M // K.BM, L * C, device=dev) if fuse else None
         pre_tiles = empty(M // K.BM, L * 2 * C, device=dev) if fuse else None
-        # The dgrad chain (gate_bwd GEMM -> dilated-conv^T GEMM -> next block) stays on this
-        # stream; each block's weight / bias gradients go to a trailing auxiliary stream.
-        aux = AuxStream(dev)
         for l in reversed(range(L)):
             blk = self.residual_layers[l]
             dl = blk.dilation
@@ -306,28 +303,26 @@ class DiffNet(nn.Module):
                 dyb = bf(M, C) if (dx is None and b16) else None
                 K.gemm(tsegs, B, T, C, pk.bwd, dy, C, ybf=dyb, ybf_ld=C)
                 K.colsum(dy, C, T, C, dd_all, groups=B, ldo=L * C, outoff=l * C)
-            with aux.run(*([t for t in (dss, dpre_all, dd_all, dx, dxb, dssb, dpre_b)
-                            if t is not None])):
-                # per-block weight gradients; the ones whose second operand is shared by
-                # every block (skip half of w_o, conditioner, diffusion projection) and
-                # all bias gradients are taken for all blocks at once after the loop
-                w_o = blk.output_projection
-                if dx is not None:
-                    wg(w_o.weight, dxb if bw else dx, C, zsrc[l], ldz, B, T, T, C, C,
-                       scale=SQRT1_2, row0=0)
-                if bw:
-                    wg(blk.dilated_conv.weight, dpre_b, L * 2 * C, st["XB"][l], C, B, T, T,
-                       2 * C, C, taps=3, dil=dl, shift0=-dl, dyoff=l * 2 * C)
-                else:
-                    wg(blk.dilated_conv.weight, dpre_all, L * 2 * C, st["X"][l], C, B, T, T,
-                       2 * C, C, taps=3, dil=dl, shift0=-dl, radd=st["ds"][:, l * C:],
-                       radd_ld=L * C, dyoff=l * 2 * C)
+            # per-block weight gradients; the ones whose second operand is shared by
+            # every block (skip half of w_o, conditioner, diffusion projection) and
+            # all bias gradients are taken for all blocks at once after the loop
+            w_o = blk.output_projection
+            if dx is not None:
+                wg(w_o.weight, dxb if bw else dx, C, zsrc[l], ldz, B, T, T, C, C,
+                   scale=SQRT1_2, row0=0)
+            if bw:
+                wg(blk.dilated_conv.weight, dpre_b, L * 2 * C, st["XB"][l], C, B, T, T,
+                   2 * C, C, taps=3, dil=dl, shift0=-dl, dyoff=l * 2 * C)
+            else:
+                wg(blk.dilated_conv.weight, dpre_all, L * 2 * C, st["X"][l], C, B, T, T,
+                   2 * C, C, taps=3, dil=dl, shift0=-dl, radd=st["ds"][:, l * C:],
+                   radd_ld=L * C, dyoff=l * 2 * C)
             if fuse:
                 dx, dxb = xnew, xnewb
             elif dx is None:
                 dx, dxb = dy, dyb
             else:
-                dxn = empty(M, C, device=dev)  # out of place: the aux stream still reads dx
+                dxn = empty(M, C, device=dev)  # out of place: the weight gradient reads dx
                 if b16:
                     dxb = bf(M, C)
                     call("ensvs_axpby_to_bf16", dxn.data_ptr(), dxb.data_ptr(), dx.data_ptr(),
@@ -350,43 +345,42 @@ class DiffNet(nn.Module):
         blocks = self.residual_layers
         g_w = lambda m: [grad_of(getattr(b, m).weight) for b in blocks]  # noqa: E731
         g_b = lambda m: [grad_of(getattr(b, m).bias) for b in blocks]  # noqa: E731
-        with aux.run():
-            zall = st["ZBall"] if bw else st["Zall"]
-            tw = empty(C, L * C, device=dev)
-            K.wgrad(dssb if bw else dss, C, zall, L * C, B, T, T, C, L * C, 1, 1, 0,
-                    _lib.PAD_ZERO, tw, L * C, 1, 1, dtype=engine_gemm_dtype())
-            _axpy_blocks2d([w[C:] for w in g_w("output_projection")], tw, C, L * C, C, C)
-            tc = empty(L * 2 * C, E, device=dev)
-            K.wgrad(dpre_b if bw else dpre_all, L * 2 * C, st["condb"] if bw else st["cond"],
-                    E if bw else st["ldc"], B, T, T, L * 2 * C, E, 1, 1, 0, _lib.PAD_ZERO, tc,
-                    E, 1, 1, dtype=engine_gemm_dtype())
-            _axpy_blocks(g_w("conditioner_projection"), tc, 2 * C * E, 2 * C * E)
-            tp = empty(L * C, C, device=dev)
-            K.wgrad(dd_all, L * C, st["d"], C, 1, B, B, L * C, C, 1, 1, 0, _lib.PAD_ZERO, tp,
-                    C, 1, 1, dtype=engine_gemm_dtype())
-            _axpy_blocks(g_w("diffusion_projection"), tp, C * C, C * C)
-            tmp_pre = empty(L * 2 * C, device=dev)
-            if fuse:
-                K.colsum(pre_tiles, L * 2 * C, M // K.BM, L * 2 * C, tmp_pre)
+        zall = st["ZBall"] if bw else st["Zall"]
+        tw = empty(C, L * C, device=dev)
+        K.wgrad(dssb if bw else dss, C, zall, L * C, B, T, T, C, L * C, 1, 1, 0,
+                _lib.PAD_ZERO, tw, L * C, 1, 1, dtype=engine_gemm_dtype())
+        _axpy_blocks2d([w[C:] for w in g_w("output_projection")], tw, C, L * C, C, C)
+        tc = empty(L * 2 * C, E, device=dev)
+        K.wgrad(dpre_b if bw else dpre_all, L * 2 * C, st["condb"] if bw else st["cond"],
+                E if bw else st["ldc"], B, T, T, L * 2 * C, E, 1, 1, 0, _lib.PAD_ZERO, tc,
+                E, 1, 1, dtype=engine_gemm_dtype())
+        _axpy_blocks(g_w("conditioner_projection"), tc, 2 * C * E, 2 * C * E)
+        tp = empty(L * C, C, device=dev)
+        K.wgrad(dd_all, L * C, st["d"], C, 1, B, B, L * C, C, 1, 1, 0, _lib.PAD_ZERO, tp,
+                C, 1, 1, dtype=engine_gemm_dtype())
+        _axpy_blocks(g_w("diffusion_projection"), tp, C * C, C * C)
+        tmp_pre = empty(L * 2 * C, device=dev)
+        if fuse:
+            K.colsum(pre_tiles, L * 2 * C, M // K.BM, L * 2 * C, tmp_pre)
+        else:
+            K.colsum(dpre_all, L * 2 * C, M, L * 2 * C, tmp_pre)
+        _axpy_blocks(g_b("dilated_conv"), tmp_pre, 2 * C, 2 * C)
+        _axpy_blocks(g_b("conditioner_projection"), tmp_pre, 2 * C, 2 * C)
+        _axpy_blocks([b[C:] for b in g_b("output_projection")], tmp_dss, 0, C)
+        tdd = empty(L * C, device=dev)
+        K.colsum(dd_all, L * C, B, L * C, tdd)
+        _axpy_blocks(g_b("diffusion_projection"), tdd, C, C)
+        if L > 1:
+            bo = g_b("output_projection")
+            step = _const_step(bo)
+            if step is None:  # parameters not in one flat buffer: a contiguous copy
+                tb = torch.zeros(L - 1, 2 * C, device=dev)
+                call("ensvs_res_bias_grad", tdd.data_ptr(), L, C, tb.data_ptr(), 2 * C,
+                     SQRT1_2, Ly.stream())
+                _axpy_blocks(bo[:-1], tb, 2 * C, C)
             else:
-                K.colsum(dpre_all, L * 2 * C, M, L * 2 * C, tmp_pre)
-            _axpy_blocks(g_b("dilated_conv"), tmp_pre, 2 * C, 2 * C)
-            _axpy_blocks(g_b("conditioner_projection"), tmp_pre, 2 * C, 2 * C)
-            _axpy_blocks([b[C:] for b in g_b("output_projection")], tmp_dss, 0, C)
-            tdd = empty(L * C, device=dev)
-            K.colsum(dd_all, L * C, B, L * C, tdd)
-            _axpy_blocks(g_b("diffusion_projection"), tdd, C, C)
-            if L > 1:
-                bo = g_b("output_projection")
-                step = _const_step(bo)
-                if step is None:  # parameters not in one flat buffer: a contiguous copy
-                    tb = torch.zeros(L - 1, 2 * C, device=dev)
-                    call("ensvs_res_bias_grad", tdd.data_ptr(), L, C, tb.data_ptr(), 2 * C,
-                         SQRT1_2, Ly.stream())
-                    _axpy_blocks(bo[:-1], tb, 2 * C, C)
-                else:
-                    call("ensvs_res_bias_grad", tdd.data_ptr(), L, C, bo[0].data_ptr(), step,
-                         SQRT1_2, Ly.stream())
+                call("ensvs_res_bias_grad", tdd.data_ptr(), L, C, bo[0].data_ptr(), step,
+                     SQRT1_2, Ly.stream())
         # conditioner input grad of all blocks at once
         dcond = empty(M, E, device=dev)
         K.gemm([K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, L * 2 * C, pk["condT"], T)],
@@ -411,13 +405,12 @@ class DiffNet(nn.Module):
         ip = self.input_projection
         wg(ip.weight, dpre0, C, st["xin"], st["ldx"], B, T, T, C, Mc)
         cs(dpre0, C, M, C, ip.bias)
-        aux.join()
         return dcond
 
     # ---------------------------------------------------------------- reference API
     def forward(self, spec, diffusion_step, cond):
         """spec (B, 1, M, T), diffusion_step (B,), cond (B, E, T) -> (B, 1, M, T)."""
-        return _DiffNetFn.apply(self, spec, diffusion_step, cond, self.skip_projection.weight)
+        return _DiffNetFn.apply(self, spec, diffusion_step, cond, *self.parameters())
 
 
 def _const_step(dsts):
@@ -463,7 +456,7 @@ def _colsum_off(dy, ld, M, N, param, off, scale):
 
 class _DiffNetFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, mod, spec, t, cond, anchor):
+    def forward(ctx, mod, spec, t, cond, *params):
         B, _, Mc, T = spec.shape
         E = cond.shape[1]
         # reference layouts are (B, C, T); the kernels use frame rows (B*T, C)
@@ -471,7 +464,7 @@ class _DiffNetFn(torch.autograd.Function):
         cnd = cond.transpose(1, 2).contiguous().view(B * T, E)
         t = t.to(device=spec.device, dtype=torch.int64).contiguous()
         out, st = mod._fwd(xin, Mc, t, cnd, E, B, T)
-        ctx.mod, ctx.st = mod, st
+        ctx.mod, ctx.st, ctx.params = mod, st, params
         ctx.dims = (B, Mc, T, E)
         return out.view(B, T, Mc).transpose(1, 2).unsqueeze(1)
 
@@ -479,9 +472,11 @@ class _DiffNetFn(torch.autograd.Function):
     def backward(ctx, g):
         B, Mc, T, E = ctx.dims
         dout = g[:, 0].transpose(1, 2).contiguous().view(B * T, Mc)
-        dcond = ctx.mod._bwd(ctx.st, dout)
-        ctx.st = None
-        return None, None, None, dcond.view(B, T, E).transpose(1, 2), None
+        with GradCapture(ctx.params) as gc:
+            dcond = ctx.mod._bwd(ctx.st, dout)
+        ctx.st = ctx.params = None
+        return (None, None, None, dcond.view(B, T, E).transpose(1, 2)) + \
+            gc.grads(ctx.needs_input_grad[4:])
 
 
 def linear_beta_schedule(timesteps, min_beta=1e-4, max_beta=0.06):
@@ -680,8 +675,7 @@ class GaussianDiffusion(BaseModel):
 
     # ---------------------------------------------------------------- reference API
     def forward(self, cond, lengths=None, y=None, spk_embs=None):
-        return _DiffusionFn.apply(self, cond, y, spk_embs, lengths, self.betas,
-                                  self.denoise_fn.skip_projection.weight)
+        return _DiffusionFn.apply(self, cond, y, spk_embs, lengths, *self.parameters())
 
     def inference(self, cond, lengths=None, spk_embs=None):
         B, T, D = cond.shape
@@ -695,7 +689,7 @@ class GaussianDiffusion(BaseModel):
 
 class _DiffusionFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, mod, cond, y, spk_embs, lengths, _buf, anchor):
+    def forward(ctx, mod, cond, y, spk_embs, lengths, *params):
         B, T, D = cond.shape
         cond = cond.contiguous().float()
         y = y.contiguous().float()
@@ -704,7 +698,7 @@ class _DiffusionFn(torch.autograd.Function):
         spk, spk_ld, _ = _spk_args(spk_embs, B, T)
         noise, xr, st = mod._fwd([(cond, D, 0, D)], B, T, lens_dev, (y, y.shape[2], 0), spk,
                                  spk_ld)
-        ctx.mod, ctx.st, ctx.dims = mod, st, (B, T)
+        ctx.mod, ctx.st, ctx.dims, ctx.params = mod, st, (B, T), params
         ctx.spk_needs = spk_embs is not None and spk_embs.requires_grad
         ctx.mark_non_differentiable(noise)
         return noise.view(B, T, -1), xr.view(B, T, -1)
@@ -713,8 +707,9 @@ class _DiffusionFn(torch.autograd.Function):
     def backward(ctx, gnoise, gxr):
         B, T = ctx.dims
         st = ctx.st
-        dcond = ctx.mod.denoise_fn._bwd(st["dst"], gxr.contiguous().view(B * T, -1))
-        dX0, _ = ctx.mod.encoder._bwd(st["est"], dcond, want_spk=False)
-        ctx.st = None
+        with GradCapture(ctx.params) as gc:
+            dcond = ctx.mod.denoise_fn._bwd(st["dst"], gxr.contiguous().view(B * T, -1))
+            dX0, _ = ctx.mod.encoder._bwd(st["est"], dcond, want_spk=False)
+        ctx.st = ctx.params = None
         dspk = dX0.view(B, T, -1) if ctx.spk_needs else None
-        return None, None, None, dspk, None, None, None
+        return (None, None, None, dspk, None) + gc.grads(ctx.needs_input_grad[5:])

@@ -17,8 +17,7 @@ import torch
 from . import _lib
 from .kernels import PackedBuffer
 
-_STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None, "concurrent": True,
-          "aux": os.environ.get("ENSVS_AUX", "0") == "1", "aux_pending": []}
+_STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None, "concurrent": True}
 _SIDE_STREAMS = {}
 # Dev instrumentation: set to a list to collect (branch, start_event, end_event) per
 # branch region (tools/branch_times.py); None = off.
@@ -80,7 +79,6 @@ class Branches:
             ev = self.main.record_event()
             for s in self.side:
                 s.wait_event(ev)
-            _STATE["aux_pending"].append([])
         return self
 
     def on(self, i):
@@ -97,58 +95,7 @@ class Branches:
         if self.on_side:
             for s in self.side:
                 self.main.wait_stream(s)
-            # auxiliary streams forked inside the branches join here, into the stream the
-            # branches forked from (joining them into a branch stream instead crashes HIP
-            # graph capture on ROCm 7: tools/debug_graph_nested.py)
-            for aux in _STATE["aux_pending"].pop():
-                self.main.wait_stream(aux.stream)
-                aux.keep = []
         return False
-
-
-_AUX_STREAMS = {}
-
-
-class AuxStream:
-    """(Off by default -- ENSVS_AUX=1 enables it: with 4 hardware queues the extra streams
-    share queues with the other branches, and HIP graph replay of the resulting topology
-    measured slower, 55-61 ms vs 32 ms per step.)
-
-    Off-critical-path work (weight gradients) on an auxiliary HIP stream that trails the
-    current stream: each ``with aux.run(*tensors):`` block starts after everything issued so
-    far on the current stream and overlaps what the current stream issues next.  Tensors
-    named there are referenced until ``join()`` (which makes the current stream wait for the
-    auxiliary one), so their memory is not reused under the auxiliary stream -- no
-    record_stream, which is also safe inside graph capture.  Serial schedule: in place."""
-
-    def __init__(self, device):
-        self.on = _STATE["concurrent"] and _STATE["aux"] and torch.cuda.is_available()
-        self.keep = []
-        if self.on:
-            self.main = torch.cuda.current_stream(device)
-            key = (str(device), self.main.cuda_stream)
-            if key not in _AUX_STREAMS:
-                _AUX_STREAMS[key] = torch.cuda.Stream(device)
-            self.stream = _AUX_STREAMS[key]
-
-    def run(self, *tensors):
-        import contextlib
-        if not self.on:
-            return contextlib.nullcontext()
-        self.keep.extend(tensors)
-        self.stream.wait_event(self.main.record_event())
-        return torch.cuda.stream(self.stream)
-
-    def join(self):
-        """Inside Branches: deferred to the branches' join; otherwise the current stream
-        waits for the auxiliary one now."""
-        if not self.on:
-            return
-        if _STATE["aux_pending"]:
-            _STATE["aux_pending"][-1].append(self)
-        else:
-            self.main.wait_stream(self.stream)
-            self.keep = []
 
 
 def next_seed() -> int:
@@ -188,6 +135,45 @@ def grad_of(p: torch.Tensor) -> torch.Tensor:
             g.zero_()
         p.grad = g
     return p.grad
+
+
+class GradCapture:
+    """Routes the parameter gradients that backward kernels write (through ``grad_of``)
+    into fresh buffers that an autograd ``Function.backward`` RETURNS, instead of into
+    ``p.grad``.  Autograd then accumulates them into ``p.grad`` itself, so
+    DistributedDataParallel's per-parameter hooks fire and ``GradScaler.unscale_`` /
+    ``clip_grad_norm_`` see ordinary gradients (the reference's own train_step,
+    train_acoustic_multitrack.py:93-100, 358-380).  The fused ``train.train_step``
+    does not go through autograd and writes ``p.grad`` directly.
+
+    Buffers are laid out like ``flatten_parameters`` (64-element aligned, module order),
+    so kernels that address several blocks' gradients at a constant stride still can."""
+
+    def __init__(self, params, align: int = 64):
+        self.params = list(params)
+        sizes = [(p.numel() + align - 1) // align * align for p in self.params]
+        dev = self.params[0].device
+        self.buf = torch.zeros(max(sum(sizes), 1), dtype=torch.float32, device=dev)
+        self.views, o = [], 0
+        for p, n in zip(self.params, sizes):
+            self.views.append(self.buf[o:o + p.numel()].view_as(p))
+            o += n
+
+    def __enter__(self):
+        self.saved = [p.grad for p in self.params]
+        for p, v in zip(self.params, self.views):
+            p.grad = v
+        return self
+
+    def __exit__(self, *exc):
+        for p, g in zip(self.params, self.saved):
+            p.grad = g
+        self.saved = None
+        return False
+
+    def grads(self, needs):
+        """Per-parameter gradients for Function.backward (None where not needed)."""
+        return tuple(v if n else None for v, n in zip(self.views, needs))
 
 
 def flatten_parameters(module: torch.nn.Module, align: int = 64):

@@ -152,14 +152,29 @@ BF16_ACT = {"on": True, "stages": 2,
             "min_rows": int(os.environ.get("ENSVS_BF16_MIN_ROWS", "0"))}
 
 
+def _castable(s):
+    """ensvs_cast_bf16's operand contract (gemm.hip): K % 8, ld % 4, 16-B aligned rows and
+    radd; an fp32 segment that misses it stays on the register-staged kernel."""
+    ok = s.pd is None and s.K % 8 == 0 and s.ld % 4 == 0 and \
+        (s.x.data_ptr() + 4 * s.xoff) % 16 == 0
+    if s.radd is not None:
+        ok = ok and s.radd_ld % 4 == 0 and s.radd.data_ptr() % 16 == 0
+    return ok
+
+
 def _bf16_act_ok(segs, W, Npad, M):
     if any(s.x.dtype == torch.bfloat16 for s in segs):  # operands already rounded
         assert W.dtype == _lib.DT_BF16 and all(s.pd is None and s.K % 8 == 0 for s in segs)
         assert all(s.radd is None for s in segs if s.x.dtype == torch.bfloat16)
+        for s in segs:  # ensvs_conv_gemm_bf16a's contract: a caller-side layout error
+            if s.x.dtype == torch.bfloat16 and (s.ld % 8 or (s.x.data_ptr() + 2 * s.xoff) % 16):
+                raise ValueError("bf16 GEMM operand needs ld % 8 == 0 and 16-B aligned rows")
+            if s.x.dtype != torch.bfloat16 and not _castable(s):
+                raise ValueError("fp32 segment beside bf16 operands is not castable")
         return True
     if not BF16_ACT["on"] or W.dtype != _lib.DT_BF16 or M < BF16_ACT["min_rows"]:
         return False
-    if any(s.pd is not None or s.K % 8 for s in segs):
+    if not all(_castable(s) for s in segs):
         return False
     return max(s.taps for s in segs) * (Npad // 128) >= BF16_ACT["min_reuse"]
 

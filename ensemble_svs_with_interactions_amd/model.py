@@ -12,7 +12,7 @@ from torch import nn
 
 from . import layers as Ly
 from .base import BaseModel, PredictionType
-from .engine import ModulePacks, empty, lengths_pair
+from .engine import GradCapture, ModulePacks, empty, lengths_pair
 
 
 def init_weights(net, init_type="normal", init_gain=0.02):
@@ -192,7 +192,7 @@ class FFConvLSTM(BaseModel):
     def forward(self, x, lengths=None, y=None, spk_embs=None):
         B, T, _ = x.shape
         x = x.contiguous().float()
-        return _FFConvLSTMFn.apply(self, x, spk_embs, lengths, self.fc.weight)
+        return _FFConvLSTMFn.apply(self, x, spk_embs, lengths, *self.parameters())
 
     def inference(self, x, lengths=None, spk_embs=None):
         return self(x, lengths, spk_embs=spk_embs)
@@ -210,7 +210,7 @@ def _spk_args(spk_embs, B, T):
 
 class _FFConvLSTMFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, mod, x, spk_embs, lengths, anchor):
+    def forward(ctx, mod, x, spk_embs, lengths, *params):
         B, T, D = x.shape
         dev = x.device
         lens_host, lens_dev = lengths_pair(lengths, B, T, dev)
@@ -219,7 +219,7 @@ class _FFConvLSTMFn(torch.autograd.Function):
             raise NotImplementedError("per-frame speaker embeddings are not on the path")
         out, st = mod._fwd([(x, D, 0, D)], B, T, lens_dev, spk, spk_ld,
                            save=torch.is_grad_enabled() or True)
-        ctx.mod, ctx.st = mod, st
+        ctx.mod, ctx.st, ctx.params = mod, st, params
         ctx.spk_needs = spk_embs is not None and spk_embs.requires_grad
         Tm = max(lens_host)
         out = out.view(B, T, -1)
@@ -234,7 +234,8 @@ class _FFConvLSTMFn(torch.autograd.Function):
             gg = torch.zeros(B, T, g.shape[2], device=g.device)
             gg[:, :g.shape[1]] = g
             g = gg
-        dX0, _ = ctx.mod._bwd(st, g.view(B * T, -1), want_spk=False)
+        with GradCapture(ctx.params) as gc:
+            dX0, _ = ctx.mod._bwd(st, g.view(B * T, -1), want_spk=False)
         dspk = dX0.view(B, T, -1) if ctx.spk_needs else None
-        ctx.st = None
-        return None, None, dspk, None, None
+        ctx.st = ctx.params = None
+        return (None, None, dspk, None) + gc.grads(ctx.needs_input_grad[4:])

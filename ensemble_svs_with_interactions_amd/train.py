@@ -33,6 +33,10 @@ class FusedAdam:
             raise NotImplementedError("weight_decay != 0 (recipe uses 0.0)")
         if not hasattr(model, "_ensvs_flat"):
             flatten_parameters(model)
+        if world_size() > 1:
+            # DDP(model) broadcasts rank 0's parameters and buffers when it is built
+            # (train_util.py:1446); the fused data-parallel step starts from the same state
+            broadcast_state(model)
         self.model = model
         self.flat, self.gflat = model._ensvs_flat
         self.m = torch.zeros_like(self.flat)
@@ -124,6 +128,24 @@ def world_size(group=None):
     if not (dist.is_available() and dist.is_initialized()):
         return 1
     return dist.get_world_size(group)
+
+
+def broadcast_state(model, src=0, group=None):
+    """Rank ``src``'s parameters (one broadcast of the flat buffer) and buffers (BatchNorm
+    running statistics, diffusion schedules) to every rank, as DistributedDataParallel's
+    constructor does (``_sync_module_states``)."""
+    import torch.distributed as dist
+    if world_size(group) == 1:
+        return
+    flat = getattr(model, "_ensvs_flat", None)
+    if flat is not None:
+        dist.broadcast(flat[0], src, group=group)
+    else:
+        for p in model.parameters():
+            dist.broadcast(p.data, src, group=group)
+    for b in model.buffers():
+        dist.broadcast(b, src, group=group)
+    weights_updated()
 
 
 def allreduce_grads(gflat, group=None):
@@ -303,8 +325,16 @@ class GraphedTrainStep:
         self.opt.step()
         return loss
 
-    def step(self, draws=None, **batch):
-        """One training step (replay).  Returns the static (loss, grad_norm) tensors."""
+    def step(self, draws=None, lengths=None, **batch):
+        """One training step (replay).  Returns the static (loss, grad_norm) tensors.
+
+        The valid lengths are part of the captured graph (the masked-L1 element count and
+        the packed recurrences' bounds): a batch must have exactly the captured lengths
+        (bucketed batches of identical lengths); passing different ``lengths`` raises."""
+        if lengths is not None and [int(v) for v in lengths] != self.lengths:
+            raise ValueError("GraphedTrainStep: lengths differ from the captured ones "
+                             f"({list(lengths)[:4]}... vs {self.lengths[:4]}...); capture "
+                             "another GraphedTrainStep for this bucket")
         for k, v in (draws or {}).items():
             if self.draws is None or self.draws[k].shape != v.shape:
                 raise ValueError(f"draws[{k}]: not captured with this shape")

@@ -8,24 +8,20 @@ pairs = 30 pairs x 1024 frames of synthetic features.
 GEMMs run on bf16 MFMA with fp32 accumulation; everything else fp32.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-Multi-GPU: one process per GPU via torch.distributed.run, RCCL gradient
+Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) each rank
+runs directly; `python bench.py --gpus N` without it starts torch.distributed.run with N
+ranks itself (before anything touches the GPU) and exits with its status.  RCCL gradient
 all-reduce, pairs sharded per rank (weak scaling).
 """
 import argparse
 import json
-import math
 import os
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-from ensemble_svs_with_interactions_amd import configs, data, engine  # noqa: E402
-from ensemble_svs_with_interactions_amd.train import FusedAdam, GraphedTrainStep, train_step  # noqa: E402,E501
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -39,6 +35,30 @@ def gate_gemm_bytes(M, C, E, a_bytes):
     return (M * (C + E) * a_bytes + 2 * C * (3 * C + E) * 2 + 2 * C * 4 +
             M * C * a_bytes + M * 2 * C * 4)
 TRAIN_FLOP_PER_FRAME = 127.5e6  # SURVEY.md §6 (torch.utils.flop_counter on the oracle)
+
+
+def _imports():
+    """Package imports (they load libensvs.so): only after the launcher decision."""
+    global np, torch, configs, data, engine, FusedAdam, GraphedTrainStep, train_step
+    import numpy as np  # noqa: F811
+    import torch  # noqa: F811
+    from ensemble_svs_with_interactions_amd import configs, data, engine  # noqa: F811
+    from ensemble_svs_with_interactions_amd.train import (FusedAdam, GraphedTrainStep,  # noqa
+                                                          train_step)
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` outside torch.distributed.run: start N ranks (one per GPU) as a
+    child torch.distributed.run on 127.0.0.1 and return its exit status."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
 
 
 def parse():
@@ -55,7 +75,10 @@ def parse():
                     help="run the lf0/mgc/bap/vuv branches serially (no side streams)")
     ap.add_argument("--eager", action="store_true",
                     help="issue every kernel from the host each step (no HIP graph replay)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-config2", action="store_true",
+                    help="skip the single-track (BASELINE config 2) training leg")
+    ap.add_argument("--cpu-pairs", type=int, default=10)
+    ap.add_argument("--cpu-frames", type=int, default=1024)
     return ap.parse_args()
 
 
@@ -158,17 +181,35 @@ def synth_rtf(model, dev, T=2000, parts=6, reps=3):
         tv, wav = _median_time(lambda: vocoder(feats), reps)
         assert torch.isfinite(wav).all()
         sec = T * 0.005
-        out[name] = dict(rtf=(ta + tv) / sec, acoustic_ms=ta * 1e3, vocoder_ms=tv * 1e3,
-                         tracks=B, samples_per_track=int(wav.shape[-1]))
+        # rtf: wall-clock / seconds of the song (the whole ensemble rendered);
+        # rtf_per_track: wall-clock / seconds of synthesized audio (B tracks), the
+        # reference's per-synthesis definition (svs.py:449-452, 581-582)
+        out[name] = dict(rtf=(ta + tv) / sec, rtf_per_track=(ta + tv) / (B * sec),
+                         acoustic_ms=ta * 1e3, vocoder_ms=tv * 1e3, tracks=B,
+                         samples_per_track=int(wav.shape[-1]))
     model.train()
     return dict(metric="synth RTF (acoustic inference + uSFGAN) / audio seconds",
                 frames=T, audio_s=T * 0.005, diffusion_steps=100, higher_is_better=False,
                 dtype=engine.gemm_precision(), **out)
 
 
-def cpu_baseline(args, budget_s):
-    """The oracle (CPU PyTorch restatement of the reference, fused CPU LSTM) on host
-    cores: full-size model, bounded sample of the same workload."""
+def _cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for ln in out.splitlines():
+            if ln.startswith("Model name"):
+                return ln.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(args):
+    """The oracle (CPU PyTorch restatement of the reference, fused CPU LSTM) on the host
+    cores, BASELINE.md §3: full-size model, P pairs x T frames fp32 (10 x
+    1024), median of 5 steps after 2 warm-up steps.  tools/cpu_baseline_check.py pins its
+    speed to the reference's own train_step."""
     from oracle import ensvs_oracle as O
     from oracle.weights import seeded_state_dict
     cores = os.cpu_count() or 1
@@ -188,16 +229,15 @@ def cpu_baseline(args, budget_s):
             P[pre + k] = v
     trainable = [k for k in P if "running" not in k and k.rsplit(".", 1)[-1] not in
                  O.diffusion_schedule()]
-    Pp, T = 6, 1024
+    Pp, T = args.cpu_pairs, args.cpu_frames
     b = data.synthetic_batch(Pp, T, 7)
     x = (torch.from_numpy(b["x_main"]), torch.from_numpy(b["x_sub"]))
     y = (torch.from_numpy(b["y_main"]), torch.from_numpy(b["y_sub"]))
     spk = (torch.from_numpy(b["spk_main"]), torch.from_numpy(b["spk_sub"]))
     rng = torch.Generator().manual_seed(3)
     state, times = {}, []
-    t_start = time.time()
-    step = 0
-    while True:
+    warm, timed = 2, 5
+    for step in range(warm + timed):
         for k in trainable:
             P[k] = P[k].detach().requires_grad_()
         draws = dict(
@@ -218,26 +258,65 @@ def cpu_baseline(args, budget_s):
         O.clip_and_adam(params, grads, state, step=step + 1)
         P.update(params)
         times.append(time.time() - t0)
-        step += 1
-        if time.time() - t_start > budget_s and step >= 3:
-            break
-    sec = float(np.median(times[1:]))
+    sec = float(np.median(times[warm:]))
     return dict(value=Pp * T / sec, unit="main-track frames/s", cores=cores, kind="port",
+                cpu_model=_cpu_model(),
                 sample=f"oracle (CPU PyTorch restatement, fused CPU LSTM) full-size model, "
-                       f"{Pp} pairs x {T} frames fp32, median of {len(times) - 1} steps "
-                       f"after 1 warm-up ({sum(times):.1f} s of CPU work)")
+                       f"{Pp} pairs x {T} frames fp32, median of {timed} steps after {warm} "
+                       f"warm-up ({sum(times):.1f} s of CPU work)")
+
+
+def config2_train(args, dev):
+    """BASELINE config 2: single-track NPSSMDNMultistreamParametricModel (teacher-forced
+    lf0 decoder, both diffusions, V/UV) training steps, same per-GPU workload (pairs ->
+    utterances x frames), graph replay, bf16 GEMM operands."""
+    from ensemble_svs_with_interactions_amd.train import train_step_single
+    torch.manual_seed(20250322)
+    model = configs.instantiate(configs.singletrack_diffusion()).to(dev)
+    opt = FusedAdam(model, lr=1e-4, clip_norm=1.0)
+    P, T = args.pairs, args.frames
+    b = data.synthetic_batch(P, T, 2000)
+    g = lambda k: torch.from_numpy(b[k]).to(dev).contiguous()  # noqa: E731
+    x, y = g("x_main"), g("y_main")
+    lens = b["lengths"].tolist()
+    if args.eager:
+        def step():
+            return train_step_single(model, opt, x, y, lens)
+        step()
+    else:
+        step = GraphedTrainStep(model, opt, x, None, y, None, None, lens, warmup=1).step
+    for _ in range(max(0, args.warmup - 1)):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for _ in range(args.steps):
+        loss, norm = step()
+    torch.cuda.synchronize()
+    el = time.time() - t0
+    return dict(metric="single-track acoustic-model train frames/sec (BASELINE config 2)",
+                value=P * T * args.steps / el, unit="frames/s", ms_per_step=el / args.steps * 1e3,
+                steps=args.steps, utterances=P, frames=T, dtype=engine.gemm_precision(),
+                train_loss=loss.item(), grad_norm=norm.item(),
+                model="NPSSMDNMultistreamParametricModel (acoustic_nnsvs_world_multi_ar_f0_"
+                      "diff_mgcbap.yaml)")
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    _imports()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    backend = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()
+        backend = dist.get_backend()
     engine.set_gemm_precision(args.precision)
     engine.set_concurrency(not args.serial)
     torch.manual_seed(20250321)
@@ -301,6 +380,8 @@ def main():
                                "Model (multitrack_acoustic_nnsvs_world_multi_ar_f0_diff_mgcbap)",
                    "pairs_per_gpu": P, "frames_per_pair": T, "global_batch_pairs": P * world,
                    "parallelism": f"dp{world}",
+                   "process_group": {"backend": backend, "world_size": world} if world > 1
+                   else None,
                    "execution": "eager" if args.eager else "hip-graph replay"},
         "train_loss": loss_v, "grad_norm": norm_v,
         "model_tflops_per_s": value * TRAIN_FLOP_PER_FRAME / 1e12,
@@ -315,19 +396,23 @@ def main():
                      "mfma_frac": achieved / (PEAK_BF16_TFLOPS if args.precision == "bf16"
                                               else 157.3),
                      "launch_us": sec * 1e6, "call_us_incl_operand_casts": sec_call * 1e6,
-                     "traffic": _traffic()},
+                     "traffic": _traffic(),
+                     "traffic_source": "profiles/gate_gemm_pmc.json (rocprofv3 --pmc FETCH_SIZE"
+                                       " x2 + WRITE_SIZE, separate passes; not this run)"},
     }
-    if not args.no_synth:
+    if not args.no_config2 and world == 1:
+        out["config2"] = config2_train(args, dev)
+    if not args.no_synth and world == 1:
         out["synth"] = synth_rtf(model, dev)
-    if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+    if not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(out), flush=True)
 
 
 def _traffic():
-    """HBM bytes per launch of the gate GEMM from the committed rocprofv3 PMC pass, if any
-    (tools/gate_gemm_pmc.json travels with the tree; profiles/ holds the same summary)."""
-    p = os.path.join(ROOT, "tools", "gate_gemm_pmc.json")
+    """HBM bytes per launch of the gate GEMM from the committed rocprofv3 PMC pass
+    (profiles/gate_gemm_pmc.json, written by tools/profile_round.sh), if any."""
+    p = os.path.join(ROOT, "profiles", "gate_gemm_pmc.json")
     if os.path.exists(p):
         with open(p) as f:
             return json.load(f).get("hbm_bytes_per_launch")

@@ -69,10 +69,10 @@ SIGNATURES = {
                        c_vp],
     "ensvs_ardec_pack": [c_vp, c_int, c_vp, c_vp, c_vp],
     "ensvs_ardec_fwd": [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
-                        c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp, c_vp, c_vp,
-                        c_vp, c_vp, c_vp, c_vp, c_vp],
-    "ensvs_ardec_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_float,
-                        c_float, c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+                        c_vp, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp,
+                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ensvs_ardec_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
+                        c_float, c_float, c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ensvs_downsample_fwd": [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp,
                              c_vp, c_int, c_int, c_vp, c_int, c_vp],
     "ensvs_downsample_bwd": [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_int,

@@ -82,11 +82,19 @@ class ResF0NonAttentiveDecoder(BaseModel):
         return True
 
 
-class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
-    """tacotron_f0.py:757-991: cross-singer log-F0 model (additive main+sub fusion)."""
+class BiLSTMResF0NonAttentiveDecoder(BaseModel):
+    """tacotron_f0.py:528-756: FF + Conv/BN + bi-LSTM encoder and the residual-F0
+    autoregressive decoder, single track (BASELINE config 2's log-F0 model).
+
+    The decoder is teacher-forced when targets are given (the single-track model in
+    training, multistream.py:1158; tacotron_f0.py:156-159, 226-228) and free-running
+    otherwise; both run in the persistent ardec kernels.  The multi-track subclass adds
+    the second track (additive main + sub fusion)."""
+
+    _NTRACKS = 1
 
     def __init__(self, in_dim=512, ff_hidden_dim=2048, conv_hidden_dim=1024, lstm_hidden_dim=256,
-                 num_lstm_layers=2, dropout=0.0, out_dim=80, num_speaker=15, decoder_layers=2,
+                 num_lstm_layers=2, dropout=0.0, out_dim=80, decoder_layers=2,
                  decoder_hidden_dim=1024, prenet_layers=2, prenet_hidden_dim=256,
                  prenet_dropout=0.5, zoneout=0.1, reduction_factor=1, downsample_by_conv=False,
                  scaled_tanh=True, in_lf0_idx=300, in_lf0_min=5.3936276, in_lf0_max=6.491111,
@@ -95,8 +103,21 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
                  sampling_mode="mean", in_ph_start_idx: int = 1, in_ph_end_idx: int = 50,
                  embed_dim=None, init_type="none"):
         super().__init__()
+        self._build(in_dim, ff_hidden_dim, conv_hidden_dim, lstm_hidden_dim, num_lstm_layers,
+                    dropout, out_dim, decoder_layers, decoder_hidden_dim, prenet_layers,
+                    prenet_hidden_dim, prenet_dropout, zoneout, reduction_factor,
+                    downsample_by_conv, scaled_tanh, in_lf0_idx, in_lf0_min, in_lf0_max,
+                    out_lf0_idx, out_lf0_mean, out_lf0_scale, use_mdn, in_ph_start_idx,
+                    in_ph_end_idx, embed_dim, init_type)
+
+    def _build(self, in_dim, ff_hidden_dim, conv_hidden_dim, lstm_hidden_dim, num_lstm_layers,
+               dropout, out_dim, decoder_layers, decoder_hidden_dim, prenet_layers,
+               prenet_hidden_dim, prenet_dropout, zoneout, reduction_factor, downsample_by_conv,
+               scaled_tanh, in_lf0_idx, in_lf0_min, in_lf0_max, out_lf0_idx, out_lf0_mean,
+               out_lf0_scale, use_mdn, in_ph_start_idx, in_ph_end_idx, embed_dim, init_type):
         if use_mdn or embed_dim is None:
             raise NotImplementedError("use_mdn / no phoneme embedding are not on the path")
+        nt = self._NTRACKS
         self.reduction_factor = reduction_factor
         self.in_lf0_idx = in_lf0_idx
         self.in_lf0_min = in_lf0_min
@@ -116,8 +137,9 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
             nn.Linear(embed_dim, ff_hidden_dim), nn.ReLU(),
             nn.Linear(ff_hidden_dim, ff_hidden_dim), nn.ReLU(),
             nn.Linear(ff_hidden_dim, ff_hidden_dim), nn.ReLU())
+        # the score log-F0 column of every track joins the conv input (ff + 1 or ff + 2)
         self.conv = nn.Sequential(
-            nn.ReflectionPad1d(3), nn.Conv1d(ff_hidden_dim + 2, conv_hidden_dim, 7, padding=0),
+            nn.ReflectionPad1d(3), nn.Conv1d(ff_hidden_dim + nt, conv_hidden_dim, 7, padding=0),
             nn.BatchNorm1d(conv_hidden_dim), nn.ReLU(),
             nn.ReflectionPad1d(3), nn.Conv1d(conv_hidden_dim, conv_hidden_dim, 7, padding=0),
             nn.BatchNorm1d(conv_hidden_dim), nn.ReLU(),
@@ -125,20 +147,26 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
             nn.BatchNorm1d(conv_hidden_dim), nn.ReLU())
         self.lstm = nn.LSTM(conv_hidden_dim, lstm_hidden_dim, num_lstm_layers, bidirectional=True,
                             batch_first=True, dropout=dropout)
-        decoder_in_dim = 2 * lstm_hidden_dim + 2
+        # decoder input = [bi-LSTM out, score lf0 of every track]; the residual is added to
+        # the main track's score (in_lf0_idx -1 / -2: tacotron_f0.py:674, 896)
+        decoder_in_dim = 2 * lstm_hidden_dim + nt
         self.decoder = ResF0NonAttentiveDecoder(
             in_dim=decoder_in_dim, out_dim=out_dim, layers=decoder_layers,
             hidden_dim=decoder_hidden_dim, prenet_layers=prenet_layers,
             prenet_hidden_dim=prenet_hidden_dim, prenet_dropout=prenet_dropout, zoneout=zoneout,
             reduction_factor=reduction_factor, downsample_by_conv=downsample_by_conv,
-            scaled_tanh=scaled_tanh, in_lf0_idx=-2, in_lf0_min=in_lf0_min, in_lf0_max=in_lf0_max,
-            out_lf0_idx=out_lf0_idx, out_lf0_mean=out_lf0_mean, out_lf0_scale=out_lf0_scale)
+            scaled_tanh=scaled_tanh, in_lf0_idx=-nt, in_lf0_min=in_lf0_min,
+            in_lf0_max=in_lf0_max, out_lf0_idx=out_lf0_idx, out_lf0_mean=out_lf0_mean,
+            out_lf0_scale=out_lf0_scale)
         init_weights(self, init_type)
         self._packs = ModulePacks()
         self._ar = None
 
     def is_autoregressive(self):
         return True
+
+    def prediction_type(self):
+        return PredictionType.DETERMINISTIC
 
     def has_residual_lf0_prediction(self):
         return True
@@ -154,9 +182,10 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
         Ly.phoneme_input_register(pk, self.emb, self.fc_in)
         Ly.ff_register(pk, self.ff)
         F = self.ff[4].weight.shape[0]
-        Ly.conv_register(pk, self.conv, first_cols=[("ff", (0, F)), ("s0", (F, F + 1)),
-                                                    ("s1", (F + 1, F + 2))],
-                         first_bwd_cols=["ff"])
+        cols = [("ff", (0, F)), ("s0", (F, F + 1))]
+        if self._NTRACKS == 2:
+            cols.append(("s1", (F + 1, F + 2)))
+        Ly.conv_register(pk, self.conv, first_cols=cols, first_bwd_cols=["ff"])
         Ly.lstm_register(pk, self.lstm)
         cell = self.decoder.lstm[0].cell
         Ce = self.decoder.conv_downsample.weight.shape[0]
@@ -186,15 +215,15 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
         return self._ar[1]
 
     # ------------------------------------------------------------------ kernels
-    def _embed(self, pk, x0, x1, ld, B, T, s0, s1, spk_ld, dev):
-        """x = (emb + fc_in + spk)(track 0) + (same)(track 1)   (tacotron_f0.py:929-965)."""
+    def _embed(self, pk, xs, ld, B, T, spks, spk_ld, dev):
+        """x = sum over tracks of (emb + fc_in + spk)   (tacotron_f0.py:710-726, 929-965)."""
         M = B * T
         ph0, ph1 = self.in_ph_start_idx, self.in_ph_end_idx
         E = self.embed_dim
         Y = empty(M, E, device=dev)
         saved = []
         ids = []
-        for k, x in enumerate((x0, x1)):
+        for k, x in enumerate(xs):
             ph_src, X, Kin, ldx = Ly.gather_input([(x, ld, 0, ld)], ph0, ph1, M, dev)
             idv = torch.empty(M, dtype=torch.int32, device=dev)
             t, lds, off = ph_src
@@ -204,36 +233,42 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
                    **pk.bias_ptr_args("fc_in.b"))
             saved.append(dict(ids=idv, X=X, Kin=Kin, ldx=ldx))
             ids.append(idv)
+        two = len(xs) == 2
         call("ensvs_embed_add", Y.data_ptr(), E, M, E, T, self.emb.weight.data_ptr(),
-             ids[0].data_ptr(), ids[1].data_ptr(), ptr(s0), ptr(s1), spk_ld, Ly.stream())
+             ids[0].data_ptr(), ids[1].data_ptr() if two else None, ptr(spks[0]),
+             ptr(spks[1]) if two else None, spk_ld, Ly.stream())
         return Y, saved
 
-    def _fwd(self, x_main, x_sub, ld, B, T, lens_dev, s_main, s_sub, spk_ld, masks=None,
-             training=None, save=True):
-        """Main-track call of the lf0 model.  Returns (lf0 (B*T,), res (B*T,), state)."""
+    def _fwd(self, xs, ld, B, T, lens_dev, spks=(None, None), spk_ld=0, masks=None,
+             training=None, save=True, teacher=None):
+        """xs: [x_main] or [x_main, x_sub] (B*T rows of ld floats); spks: per-sequence speaker
+        vectors (or None); teacher: (targets, ld, col) of the normalised log-F0 target for
+        teacher forcing, None = free-running.  Returns (lf0 (B*T,), res (B*T,), state)."""
         self._set_lf0_params()
         training = self.training if training is None else training
         pk = self._packs.ensure(self, self._register)
         dev = self.fc_in.weight.device
         M = B * T
         li = self.in_lf0_idx
-        X0, esv = self._embed(pk, x_main, x_sub, ld, B, T, s_main, s_sub, spk_ld, dev)
+        X0, esv = self._embed(pk, xs, ld, B, T, spks, spk_ld, dev)
         hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
         F = hs[2].shape[1]
-        a, csv = Ly.conv_fwd(pk, self.conv, [("ff", hs[2], F, F, 0), ("s0", x_main, ld, 1, li),
-                                             ("s1", x_sub, ld, 1, li)], B, T, dev, training,
-                             save=save)
+        segs = [("ff", hs[2], F, F, 0), ("s0", xs[0], ld, 1, li)]
+        if len(xs) == 2:
+            segs.append(("s1", xs[1], ld, 1, li))
+        a, csv = Ly.conv_fwd(pk, self.conv, segs, B, T, dev, training, save=save)
         C = a.shape[1]
         y, lsv = Ly.lstm_fwd(pk, self.lstm, a, C, B, T, lens_dev, dev, None, save=save)
         dec = self.decoder
         cell = dec.lstm[0].cell
         H = cell.hidden_size
         Hl2 = y.shape[1]
-        Ce = Hl2 + 2
+        Ce = Hl2 + len(xs)
         Tr = T // 4
         e = empty(B * Tr, Ce, device=dev)
-        call("ensvs_downsample_fwd", y.data_ptr(), Hl2, Hl2, x_main.data_ptr() + 4 * li, ld, 1,
-             x_sub.data_ptr() + 4 * li, ld, 1, dec.conv_downsample.weight.data_ptr(),
+        x1 = xs[1].data_ptr() + 4 * li if len(xs) == 2 else None
+        call("ensvs_downsample_fwd", y.data_ptr(), Hl2, Hl2, xs[0].data_ptr() + 4 * li, ld, 1,
+             x1, ld, 1, dec.conv_downsample.weight.data_ptr(),
              dec.conv_downsample.bias.data_ptr(), B, T, e.data_ptr(), Ce, Ly.stream())
         gx = empty(B * Tr, 4 * H, device=dev)
         K.gemm([K.Seg(e, Ce, Ce, pk["dec_ih_e"], Tr)], B, Tr, 4 * H, pk.fwd, gx, 4 * H,
@@ -250,35 +285,25 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
         sh = empty(B * Tr, H, device=dev)
         so = empty(B * Tr, 4, device=dev)
         sp = empty(B * Tr, device=dev)
+        tptr, tld = (None, 0) if teacher is None else \
+            (teacher[0].data_ptr() + 4 * teacher[2], teacher[1])
         call("ensvs_ardec_fwd", gx.data_ptr(), 4 * H, ofx.data_ptr(), 4, wpf.data_ptr(),
              wih_p.data_ptr(), dec.feat_out.weight.data_ptr(), dec.feat_out.weight.shape[1],
-             x_main.data_ptr() + 4 * li, ld, masks.data_ptr(), B, T, H, float(dec.in_lf0_min),
-             float(dec.in_lf0_max), float(dec.out_lf0_mean), float(dec.out_lf0_scale),
-             lf0.data_ptr(), res.data_ptr(), sg.data_ptr(), sc.data_ptr(), sh.data_ptr(),
-             so.data_ptr(), sp.data_ptr(), Ly.stream())
+             xs[0].data_ptr() + 4 * li, ld, masks.data_ptr(), tptr, tld, B, T, H,
+             float(dec.in_lf0_min), float(dec.in_lf0_max), float(dec.out_lf0_mean),
+             float(dec.out_lf0_scale), lf0.data_ptr(), res.data_ptr(), sg.data_ptr(),
+             sc.data_ptr(), sh.data_ptr(), so.data_ptr(), sp.data_ptr(), Ly.stream())
         st = None
         if save:
             st = dict(X0=X0, esv=esv, hs=hs, csv=csv, lsv=lsv, y=y, e=e, masks=masks, sg=sg,
-                      sc=sc, sh=sh, so=so, sp=sp, B=B, T=T, lens=lens_dev, x_main=x_main,
-                      x_sub=x_sub, ld=ld)
+                      sc=sc, sh=sh, so=so, sp=sp, B=B, T=T, lens=lens_dev, xs=xs, ld=ld,
+                      teacher=teacher is not None)
         return lf0, res, st
 
-    def _bn_only(self, x_main, x_sub, ld, B, T, s_main, s_sub, spk_ld):
-        """Forward of a call whose outputs are unused in training (the sub-track call with
-        output_subtrack=False, multistream.py:1649-1651): only its BatchNorm running-statistic
-        updates are observable, so only embed + FF + the conv/BN stack run."""
-        pk = self._packs.ensure(self, self._register)
-        dev = self.fc_in.weight.device
-        li = self.in_lf0_idx
-        X0, _ = self._embed(pk, x_main, x_sub, ld, B, T, s_main, s_sub, spk_ld, dev)
-        hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
-        F = hs[2].shape[1]
-        Ly.conv_fwd(pk, self.conv, [("ff", hs[2], F, F, 0), ("s0", x_main, ld, 1, li),
-                                    ("s1", x_sub, ld, 1, li)], B, T, dev, True, save=False)
-
     def _bwd(self, st, dlf0, dres=None, want_spk=True):
-        """dlf0 / dres: (B*T,) grads of the lf0 / residual outputs.  Returns per-sequence
-        grads of the main / sub speaker vectors (B, E) each."""
+        """dlf0 / dres: (B*T,) grads of the lf0 / residual outputs.  Returns (per-sequence
+        speaker-vector grads of the main and sub track (B, E) -- the same tensor: the
+        fused input holds both -- or None, the input grad dX0 (B*T, E))."""
         pk = self._packs
         dev = dlf0.device
         B, T = st["B"], st["T"]
@@ -287,14 +312,15 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
         cell = dec.lstm[0].cell
         H = cell.hidden_size
         Ce = st["e"].shape[1]
+        xs = st["xs"]
         wpf, wpb, wih_p = self._ar_prepare()
         dg = empty(B * Tr, 4 * H, device=dev)
         do4 = empty(B * Tr, 4, device=dev)
         call("ensvs_ardec_bwd", dlf0.data_ptr(), ptr(dres), wpb.data_ptr(), wih_p.data_ptr(),
              dec.feat_out.weight.data_ptr(), dec.feat_out.weight.shape[1], st["masks"].data_ptr(),
-             B, T, H, float(dec.in_lf0_min), float(dec.in_lf0_max), float(dec.out_lf0_mean),
-             float(dec.out_lf0_scale), st["sg"].data_ptr(), st["sc"].data_ptr(),
-             st["so"].data_ptr(), dg.data_ptr(), do4.data_ptr(), Ly.stream())
+             int(st["teacher"]), B, T, H, float(dec.in_lf0_min), float(dec.in_lf0_max),
+             float(dec.out_lf0_mean), float(dec.out_lf0_scale), st["sg"].data_ptr(),
+             st["sc"].data_ptr(), st["so"].data_ptr(), dg.data_ptr(), do4.data_ptr(), Ly.stream())
         wg = Ly.wgrad_into
         # decoder weights
         wg(cell.weight_hh, dg, 4 * H, st["sh"], H, B, Tr, Tr, 4 * H, H, shift0=-1)
@@ -310,9 +336,10 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
         Hl2 = st["y"].shape[1]
         dy = empty(M, Hl2, device=dev)
         li = self.in_lf0_idx
+        x1 = xs[1].data_ptr() + 4 * li if len(xs) == 2 else None
         call("ensvs_downsample_bwd", de.data_ptr(), Ce, st["y"].data_ptr(), Hl2, Hl2,
-             st["x_main"].data_ptr() + 4 * li, st["ld"], 1, st["x_sub"].data_ptr() + 4 * li,
-             st["ld"], 1, dec.conv_downsample.weight.data_ptr(), B, T, dy.data_ptr(), Hl2,
+             xs[0].data_ptr() + 4 * li, st["ld"], 1, x1, st["ld"], 1,
+             dec.conv_downsample.weight.data_ptr(), B, T, dy.data_ptr(), Hl2,
              grad_of(dec.conv_downsample.weight).data_ptr(),
              grad_of(dec.conv_downsample.bias).data_ptr(), Ly.stream())
         # encoder
@@ -324,32 +351,117 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BaseModel):
         dspk = torch.zeros(B, E, device=dev) if want_spk else None
         for k, sv in enumerate(st["esv"]):
             Ly.embed_bwd(self.emb, self.fc_in, sv, dX0, B, T, dspk if k == 0 else None)
-        # both tracks' speaker vectors receive the same per-sequence sum
         return dspk, dspk, dX0
+
+    def _pad_infer(self, xs, ld, B, T, lens_host, masks=None):
+        """pad_inference (acoustic_models/util.py:60-151) of the lf0 model alone, as the
+        single-track model's inference calls it (multistream.py:1152): replicate-pad r frames
+        (r - max(L) % r, never 0), free-running forward in eval mode, trim.  Returns
+        lf0 (B*T,) of the unpadded frames."""
+        r = self.reduction_factor
+        pad = r - max(lens_host) % r
+        dev = xs[0].device
+        D = ld
+        xps = [_replicate_pad(x, B, T, D, pad) for x in xs]
+        _, lens_dev = lengths_pair([v + pad for v in lens_host], B, T + pad, dev)
+        lf0, _, _ = self._fwd(xps, D, B, T + pad, lens_dev, masks=masks, training=False,
+                              save=False)
+        out = empty(B * T, device=dev)
+        call("ensvs_copy_cols", lf0.data_ptr(), T + pad, out.data_ptr(), T, B, T, Ly.stream())
+        return out
+
+    # ---------------------------------------------------------------- reference API
+    def forward(self, x, lengths=None, y=None, spk_embs=None):
+        return _Lf0Fn.apply(self, x, None, spk_embs, None, lengths, y, *self.parameters())
+
+    def inference(self, x, lengths=None, spk_embs=None):
+        if spk_embs is not None:
+            raise NotImplementedError("speaker embeddings at lf0 inference are not on the path")
+        B, T, D = x.shape
+        lens = [int(v) for v in (lengths if lengths is not None else [T] * B)]
+        x = x.contiguous().float()
+        return self._pad_infer([x], D, B, T, lens).view(B, T, 1)
+
+
+def _replicate_pad(x, B, T, D, pad):
+    """F.pad(x, (0, 0, 0, pad), mode="replicate") of a (B, T, D) fp32 tensor."""
+    xp = empty(B, T + pad, D, device=x.device)
+    call("ensvs_copy_cols", x.data_ptr(), T * D, xp.data_ptr(), (T + pad) * D, B, T * D,
+         Ly.stream())
+    for k in range(pad):  # replicate the last frame
+        call("ensvs_copy_cols", x.data_ptr() + 4 * (T - 1) * D, T * D,
+             xp.data_ptr() + 4 * (T + k) * D, (T + pad) * D, B, D, Ly.stream())
+    return xp
+
+
+class MultiTrackBiLSTMResF0NonAttentiveDecoder(BiLSTMResF0NonAttentiveDecoder):
+    """tacotron_f0.py:757-991: cross-singer log-F0 model (additive main+sub fusion)."""
+
+    _NTRACKS = 2
+
+    def __init__(self, in_dim=512, ff_hidden_dim=2048, conv_hidden_dim=1024, lstm_hidden_dim=256,
+                 num_lstm_layers=2, dropout=0.0, out_dim=80, num_speaker=15, decoder_layers=2,
+                 decoder_hidden_dim=1024, prenet_layers=2, prenet_hidden_dim=256,
+                 prenet_dropout=0.5, zoneout=0.1, reduction_factor=1, downsample_by_conv=False,
+                 scaled_tanh=True, in_lf0_idx=300, in_lf0_min=5.3936276, in_lf0_max=6.491111,
+                 out_lf0_idx=180, out_lf0_mean=5.953093881972361,
+                 out_lf0_scale=0.23435173188961034, use_mdn=False, num_gaussians=4,
+                 sampling_mode="mean", in_ph_start_idx: int = 1, in_ph_end_idx: int = 50,
+                 embed_dim=None, init_type="none"):
+        BaseModel.__init__(self)
+        self._build(in_dim, ff_hidden_dim, conv_hidden_dim, lstm_hidden_dim, num_lstm_layers,
+                    dropout, out_dim, decoder_layers, decoder_hidden_dim, prenet_layers,
+                    prenet_hidden_dim, prenet_dropout, zoneout, reduction_factor,
+                    downsample_by_conv, scaled_tanh, in_lf0_idx, in_lf0_min, in_lf0_max,
+                    out_lf0_idx, out_lf0_mean, out_lf0_scale, use_mdn, in_ph_start_idx,
+                    in_ph_end_idx, embed_dim, init_type)
+
+    def _bn_only(self, x_main, x_sub, ld, B, T, s_main, s_sub, spk_ld):
+        """Forward of a call whose outputs are unused in training (the sub-track call with
+        output_subtrack=False, multistream.py:1649-1651): only its BatchNorm running-statistic
+        updates are observable, so only embed + FF + the conv/BN stack run."""
+        pk = self._packs.ensure(self, self._register)
+        dev = self.fc_in.weight.device
+        li = self.in_lf0_idx
+        X0, _ = self._embed(pk, [x_main, x_sub], ld, B, T, [s_main, s_sub], spk_ld, dev)
+        hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
+        F = hs[2].shape[1]
+        Ly.conv_fwd(pk, self.conv, [("ff", hs[2], F, F, 0), ("s0", x_main, ld, 1, li),
+                                    ("s1", x_sub, ld, 1, li)], B, T, dev, True, save=False)
 
     # ---------------------------------------------------------------- reference API
     def forward(self, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths=None, y=None):
-        if y is not None:
-            raise NotImplementedError("teacher-forced lf0 decoding is not used by the "
-                                      "multi-track diffusion model (multistream.py:1646-1651)")
-        return _Lf0Fn.apply(self, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths,
+        return _Lf0Fn.apply(self, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths, y,
                             *self.parameters())
+
+    def inference(self, *args, **kwargs):
+        raise NotImplementedError("the multi-track model calls the lf0 model's forward "
+                                  "(multistream.py:1646-1651)")
 
 
 class _Lf0Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, mod, x_main, x_sub, s0, s1, lengths, *params):
+    def forward(ctx, mod, x_main, x_sub, s0, s1, lengths, y, *params):
         from .model import _spk_args
         B, T, D = x_main.shape
-        x_main = x_main.contiguous().float()
-        x_sub = x_sub.contiguous().float()
+        xs = [x_main.contiguous().float()]
+        if x_sub is not None:
+            xs.append(x_sub.contiguous().float())
         _, lens_dev = lengths_pair(lengths, B, T, x_main.device)
         p0, ld0, f0 = _spk_args(s0, B, T)
         p1, ld1, f1 = _spk_args(s1, B, T)
-        if f0 is not None or f1 is not None or ld0 != ld1:
+        if f0 is not None or f1 is not None or (s1 is not None and ld0 != ld1):
             raise NotImplementedError("per-frame speaker embeddings are not on the path")
-        lf0, res, st = mod._fwd(x_main, x_sub, D, B, T, lens_dev, p0, p1, ld0)
+        teacher = None
+        if y is not None:
+            if y.shape[1] != T:
+                raise ValueError("decoder targets must have the input's frame count "
+                                 "(tacotron_f0.py:139)")
+            yc = y.contiguous().float()
+            teacher = (yc, yc.shape[2], mod.decoder.out_lf0_idx)
+        lf0, res, st = mod._fwd(xs, D, B, T, lens_dev, (p0, p1), ld0, teacher=teacher)
         ctx.mod, ctx.st, ctx.params = mod, st, params
+        ctx.keep = teacher
         ctx.needs = (s0 is not None and s0.requires_grad, s1 is not None and s1.requires_grad)
         return lf0.view(B, T, 1), res.view(B, T, 1)
 
@@ -362,47 +474,22 @@ class _Lf0Fn(torch.autograd.Function):
         gres = gres.contiguous().view(-1) if gres is not None else None
         with GradCapture(ctx.params) as gc:
             _, _, dX0 = ctx.mod._bwd(st, glf0, gres, want_spk=False)
-        ctx.st = ctx.params = None
+        ctx.st = ctx.params = ctx.keep = None
         # per-frame grad of each (expanded) speaker embedding = grad of the fused input
         d = dX0.view(B, T, -1)
         return (None, None, None, d if ctx.needs[0] else None, d if ctx.needs[1] else None,
-                None) + gc.grads(ctx.needs_input_grad[6:])
+                None, None) + gc.grads(ctx.needs_input_grad[7:])
 
 
-class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
-    """multistream.py:1482-1778: pairwise (main, sub) ensemble diffusion model."""
+class _MultistreamHybrid(BaseModel):
+    """Kernel orchestration shared by the single-track and the pairwise multi-track NPSS
+    multistream models: four branches (lf0, mgc, bap, V/UV) on concurrent HIP streams,
+    their backward, and the reverse-diffusion inference.  ``_MULTI`` selects the
+    multi-track variant (second track, speaker embeddings, free-running lf0 decoder in
+    training) or the single-track one (no speaker, teacher-forced lf0 decoder)."""
 
-    def __init__(self, in_dim: int, out_dim: int, stream_sizes: list, reduction_factor: int,
-                 lf0_model: nn.Module, mgc_model: nn.Module, bap_model: nn.Module,
-                 vuv_model: nn.Module, speaker_embedding: nn.Module, in_rest_idx=0, in_lf0_idx=51,
-                 in_lf0_min=5.3936276, in_lf0_max=6.491111, out_lf0_idx=60,
-                 out_lf0_mean=5.953093881972361, out_lf0_scale=0.23435173188961034,
-                 vuv_model_bap_conditioning=True, vuv_model_bap0_conditioning=False,
-                 vuv_model_lf0_conditioning=True, vuv_model_mgc_conditioning=False,
-                 output_subtrack=False):
-        super().__init__()
-        self.in_dim = in_dim
-        self.out_dim = out_dim
-        self.stream_sizes = stream_sizes
-        self.reduction_factor = reduction_factor
-        self.vuv_model_bap_conditioning = vuv_model_bap_conditioning
-        self.vuv_model_bap0_conditioning = vuv_model_bap0_conditioning
-        self.vuv_model_lf0_conditioning = vuv_model_lf0_conditioning
-        self.vuv_model_mgc_conditioning = vuv_model_mgc_conditioning
-        self.output_subtrack = output_subtrack
-        assert len(stream_sizes) in [4]
-        self.lf0_model = lf0_model
-        self.mgc_model = mgc_model
-        self.bap_model = bap_model
-        self.vuv_model = vuv_model
-        self.speaker_embedding = speaker_embedding
-        self.in_rest_idx = in_rest_idx
-        self.in_lf0_idx = in_lf0_idx
-        self.in_lf0_min = in_lf0_min
-        self.in_lf0_max = in_lf0_max
-        self.out_lf0_idx = out_lf0_idx
-        self.out_lf0_mean = out_lf0_mean
-        self.out_lf0_scale = out_lf0_scale
+    _MULTI = True
+    output_subtrack = False
 
     def _set_lf0_params(self):
         if hasattr(self.lf0_model, "out_lf0_mean"):
@@ -413,9 +500,6 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
 
     def prediction_type(self):
         return PredictionType.MULTISTREAM_HYBRID
-
-    def is_autoregressive(self):
-        return True  # the lf0 model is autoregressive
 
     def has_residual_lf0_prediction(self):
         return True
@@ -467,8 +551,12 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
         Dy = y_main.shape[2]
         dev = x_main.device
         lens_host, lens_dev = lengths_pair(lengths, B, T, dev)
-        (s0, i0), (s1, i1) = self._spk_vectors(spk0, spk1, B)
-        E = s0.shape[1]
+        if self._MULTI:
+            (s0, i0), (s1, i1) = self._spk_vectors(spk0, spk1, B)
+            E = s0.shape[1]
+        else:  # single track: no speaker embedding
+            s0 = i0 = s1 = i1 = None
+            E = 0
         o = self._stream_cols()
         st = dict(i0=i0, i1=i1, B=B, T=T, E=E, lens_host=lens_host, lens_dev=lens_dev)
         c = dict(x_main=x_main, x_sub=x_sub, y_main=y_main, D=D, Dy=Dy, o=o, s0=s0, s1=s1,
@@ -480,9 +568,15 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
         B, T, E, lens_dev = st["B"], st["T"], st["E"], st["lens_dev"]
         x_main, x_sub, y_main, D, Dy, o = c["x_main"], c["x_sub"], c["y_main"], c["D"], c["Dy"], c["o"]
         s0, s1, draws = c["s0"], c["s1"], c["draws"]
-        if i == 0:
-            lf0, res, st["lf0"] = self.lf0_model._fwd(x_main, x_sub, D, B, T, lens_dev, s0, s1, E,
-                                                      masks=draws.get("lf0_main"))
+        if i == 0 and not self._MULTI:
+            # single track: lf0 model with the lf0 target stream (multistream.py:1158)
+            lf0, res, st["lf0"] = self.lf0_model._fwd([x_main], D, B, T, lens_dev,
+                                                      masks=draws.get("lf0_main"),
+                                                      teacher=(y_main, Dy, o[1]))
+            outs.update(lf0=lf0, lf0_residual=res)
+        elif i == 0:
+            lf0, res, st["lf0"] = self.lf0_model._fwd([x_main, x_sub], D, B, T, lens_dev,
+                                                      (s0, s1), E, masks=draws.get("lf0_main"))
             outs.update(lf0=lf0, lf0_residual=res)
             if self.output_subtrack:
                 # sub-track call with its outputs (multistream.py:1649-1651, 1759-1768):
@@ -490,7 +584,7 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
                 # Same stream as the main call: BatchNorm running statistics are
                 # updated main-then-sub, as in the reference.
                 lf0_s, res_s, st["lf0_sub"] = self.lf0_model._fwd(
-                    x_sub, x_main, D, B, T, lens_dev, s1, s0, E, masks=draws.get("lf0_sub"))
+                    [x_sub, x_main], D, B, T, lens_dev, (s1, s0), E, masks=draws.get("lf0_sub"))
                 outs.update(lf0_sub=lf0_s, lf0_residual_sub=res_s)
             elif self.training:
                 # sub-track call (outputs unused without output_subtrack): BN statistics
@@ -525,7 +619,10 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
 
     def _bwd_branch(self, i, st, g, dsp):
         """Backward of branch i from its output grads g; its speaker-vector grads -> dsp."""
-        if i == 0:
+        spk = self._MULTI
+        if i == 0 and not spk:
+            self.lf0_model._bwd(st["lf0"], g["lf0"], g.get("lf0_residual"), want_spk=False)
+        elif i == 0:
             dmain, dsub, _ = self.lf0_model._bwd(st["lf0"], g["lf0"], g.get("lf0_residual"))
             dsp["lf0"], dsp["lf0_sub_in"] = dmain, dsub
             if st.get("lf0_sub") is not None and (g.get("lf0_sub") is not None or
@@ -541,9 +638,10 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
                 ev = torch.cuda.Event()
                 dsp["_mgc_denoiser_done"] = ev
                 hook = lambda: ev.record(torch.cuda.current_stream())  # noqa: E731
-            dsp["mgc"] = self.mgc_model._bwd(st["mgc"], g["mgc_recon"], after_denoiser=hook)
+            dsp["mgc"] = self.mgc_model._bwd(st["mgc"], g["mgc_recon"], after_denoiser=hook,
+                                             want_spk=spk)
         elif i == 2:
-            dsp["bap"] = self.bap_model._bwd(st["bap"], g["bap_recon"])
+            dsp["bap"] = self.bap_model._bwd(st["bap"], g["bap_recon"], want_spk=spk)
         else:
             ev = dsp.get("_mgc_denoiser_done")
             if ev is not None:
@@ -551,10 +649,12 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
                 # DiffNet backward so that it overlaps the mgc encoder's recurrences at the
                 # tail of the step instead of contending with the DiffNet GEMMs
                 torch.cuda.current_stream().wait_event(ev)
-            _, dsp["vuv"] = self.vuv_model._bwd(st["vuv"], g["vuv"], want_spk=True)
+            _, dsp["vuv"] = self.vuv_model._bwd(st["vuv"], g["vuv"], want_spk=spk)
 
     def _bwd_epilogue(self, st, dsp):
         """Speaker-embedding gradient: the branch contributions, summed after the join."""
+        if not self._MULTI:
+            return
         B, E = st["B"], st["E"]
         dev = st["lens_dev"].device
         dsc, dsub = dsp.get("lf0_sub"), dsp["lf0_sub_in"]
@@ -607,11 +707,17 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
         self._set_lf0_params()
         B, T, D = x_main.shape
         dev = x_main.device
-        _, lens_dev = lengths_pair(lengths, B, T, dev)
-        (s0, _), (s1, _) = self._spk_vectors(spk0, spk1, B)
-        E = s0.shape[1]
-        lf0, _, _ = self.lf0_model._fwd(x_main, x_sub, D, B, T, lens_dev, s0, s1, E,
-                                        masks=masks, training=False, save=False)
+        lens_host, lens_dev = lengths_pair(lengths, B, T, dev)
+        if self._MULTI:
+            (s0, _), (s1, _) = self._spk_vectors(spk0, spk1, B)
+            E = s0.shape[1]
+            lf0, _, _ = self.lf0_model._fwd([x_main, x_sub], D, B, T, lens_dev, (s0, s1), E,
+                                            masks=masks, training=False, save=False)
+        else:
+            # single track: lf0_model.inference, itself pad_inference (multistream.py:1152),
+            # i.e. r more replicated frames on the already padded input, then trimmed
+            s0, E = None, 0
+            lf0 = self.lf0_model._pad_infer([x_main], D, B, T, lens_host, masks=masks)
         o = self._stream_cols()
         Dy = self.out_dim
         out = empty(B * T, Dy, device=dev)
@@ -640,6 +746,45 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
         call("ensvs_copy_cols", vuv.data_ptr(), 1, out.data_ptr() + 4 * o[2], Dy, B * T, 1,
              Ly.stream())
         return out.view(B, T, Dy)
+
+
+class MultiTrackNPSSMDNMultistreamParametricModel(_MultistreamHybrid):
+    """multistream.py:1482-1778: pairwise (main, sub) ensemble diffusion model."""
+
+    def __init__(self, in_dim: int, out_dim: int, stream_sizes: list, reduction_factor: int,
+                 lf0_model: nn.Module, mgc_model: nn.Module, bap_model: nn.Module,
+                 vuv_model: nn.Module, speaker_embedding: nn.Module, in_rest_idx=0, in_lf0_idx=51,
+                 in_lf0_min=5.3936276, in_lf0_max=6.491111, out_lf0_idx=60,
+                 out_lf0_mean=5.953093881972361, out_lf0_scale=0.23435173188961034,
+                 vuv_model_bap_conditioning=True, vuv_model_bap0_conditioning=False,
+                 vuv_model_lf0_conditioning=True, vuv_model_mgc_conditioning=False,
+                 output_subtrack=False):
+        super().__init__()
+        self.in_dim = in_dim
+        self.out_dim = out_dim
+        self.stream_sizes = stream_sizes
+        self.reduction_factor = reduction_factor
+        self.vuv_model_bap_conditioning = vuv_model_bap_conditioning
+        self.vuv_model_bap0_conditioning = vuv_model_bap0_conditioning
+        self.vuv_model_lf0_conditioning = vuv_model_lf0_conditioning
+        self.vuv_model_mgc_conditioning = vuv_model_mgc_conditioning
+        self.output_subtrack = output_subtrack
+        assert len(stream_sizes) in [4]
+        self.lf0_model = lf0_model
+        self.mgc_model = mgc_model
+        self.bap_model = bap_model
+        self.vuv_model = vuv_model
+        self.speaker_embedding = speaker_embedding
+        self.in_rest_idx = in_rest_idx
+        self.in_lf0_idx = in_lf0_idx
+        self.in_lf0_min = in_lf0_min
+        self.in_lf0_max = in_lf0_max
+        self.out_lf0_idx = out_lf0_idx
+        self.out_lf0_mean = out_lf0_mean
+        self.out_lf0_scale = out_lf0_scale
+
+    def is_autoregressive(self):
+        return True  # the lf0 model is autoregressive
 
     # ---------------------------------------------------------------- reference API
     def forward(self, x_main, x_sub, spks_list, lengths=None, ys=None):
@@ -683,12 +828,84 @@ class MultiTrackNPSSMDNMultistreamParametricModel(BaseModel):
         return out[:, :-pad]
 
 
+class NPSSMDNMultistreamParametricModel(_MultistreamHybrid):
+    """multistream.py:1025-1243: single-track NPSS multistream model (BASELINE config 2 with
+    the recipe's diffusion config acoustic_nnsvs_world_multi_ar_f0_diff_mgcbap.yaml):
+    teacher-forced residual-F0 model, mgc / bap GaussianDiffusion conditioned on
+    [x, lf0] (ground truth in training), V/UV conditioned per the vuv_model_* flags."""
+
+    _MULTI = False
+
+    def __init__(self, in_dim: int, out_dim: int, stream_sizes: list, reduction_factor: int,
+                 lf0_model: nn.Module, mgc_model: nn.Module, bap_model: nn.Module,
+                 vuv_model: nn.Module, in_rest_idx=0, in_lf0_idx=51, in_lf0_min=5.3936276,
+                 in_lf0_max=6.491111, out_lf0_idx=60, out_lf0_mean=5.953093881972361,
+                 out_lf0_scale=0.23435173188961034, vuv_model_bap_conditioning=True,
+                 vuv_model_bap0_conditioning=False, vuv_model_lf0_conditioning=True,
+                 vuv_model_mgc_conditioning=False):
+        super().__init__()
+        self.in_dim = in_dim
+        self.out_dim = out_dim
+        self.stream_sizes = stream_sizes
+        self.reduction_factor = reduction_factor
+        self.vuv_model_bap_conditioning = vuv_model_bap_conditioning
+        self.vuv_model_bap0_conditioning = vuv_model_bap0_conditioning
+        self.vuv_model_lf0_conditioning = vuv_model_lf0_conditioning
+        self.vuv_model_mgc_conditioning = vuv_model_mgc_conditioning
+        assert len(stream_sizes) in [4]
+        if not isinstance(lf0_model, BiLSTMResF0NonAttentiveDecoder) or \
+                isinstance(lf0_model, MultiTrackBiLSTMResF0NonAttentiveDecoder):
+            raise NotImplementedError("lf0_model: BiLSTMResF0NonAttentiveDecoder (recipe)")
+        self.lf0_model = lf0_model
+        self.mgc_model = mgc_model
+        self.bap_model = bap_model
+        self.vuv_model = vuv_model
+        self.in_rest_idx = in_rest_idx
+        self.in_lf0_idx = in_lf0_idx
+        self.in_lf0_min = in_lf0_min
+        self.in_lf0_max = in_lf0_max
+        self.out_lf0_idx = out_lf0_idx
+        self.out_lf0_mean = out_lf0_mean
+        self.out_lf0_scale = out_lf0_scale
+
+    def is_autoregressive(self):
+        return (self.mgc_model.is_autoregressive() or self.lf0_model.is_autoregressive()
+                or self.vuv_model.is_autoregressive() or self.bap_model.is_autoregressive())
+
+    # ---------------------------------------------------------------- reference API
+    def forward(self, x, lengths=None, y=None):
+        """multistream.py:1133-1233: training (teacher forcing) when y is given, else the
+        inference cascade on x as is; returns ((mgc, lf0, vuv, bap), lf0_residual) /
+        (out, out)."""
+        assert x.shape[-1] == self.in_dim
+        if y is None:
+            out = self._infer(x.contiguous().float(), None, None, None, lengths)
+            return out, out
+        outs = _MultiTrackFn.apply(self, x, None, y, None, None, lengths, *self.parameters())
+        nm, rm, lf0, vuv, nb, rb, res = outs[:7]
+        return ((nm, rm), lf0, vuv, (nb, rb)), res
+
+    def inference(self, x, lengths=None, draws=None):
+        """pad_inference(mdn=True) (acoustic_models/util.py:60-141): replicate-pad
+        r - max(L) % r frames (never 0), forward(y=None), trim; returns (mu, sigma) = (out,
+        out).  ``draws`` (tests only): dict(noises=..., masks=...) replayed draws."""
+        r = self.reduction_factor
+        B, T, D = x.shape
+        lens = [int(v) for v in (lengths if lengths is not None else [T] * B)]
+        pad = r - max(lens) % r
+        xp = _replicate_pad(x.contiguous().float(), B, T, D, pad)
+        out = self._infer(xp, None, None, None, [v + pad for v in lens], **(draws or {}))
+        mu = out[:, :-pad]
+        return mu, mu
+
+
 class _MultiTrackFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, mod, x_main, x_sub, y_main, spk0, spk1, lengths, *params):
         B, T, _ = x_main.shape
         # _replay_draws (tests only): random draws to replay, as train_step(draws=...)
-        outs, st = mod._train_fwd(x_main.contiguous().float(), x_sub.contiguous().float(),
+        outs, st = mod._train_fwd(x_main.contiguous().float(),
+                                  None if x_sub is None else x_sub.contiguous().float(),
                                   y_main.contiguous().float(), spk0, spk1, lengths,
                                   getattr(mod, "_replay_draws", None))
         ctx.mod, ctx.st, ctx.params = mod, st, params

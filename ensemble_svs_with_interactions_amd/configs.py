@@ -18,6 +18,10 @@ REFERENCE_TARGETS = {
         "nnsvs.acoustic_models.MultiTrackNPSSMDNMultistreamParametricModel",
     f"{PKG}.acoustic_models.MultiTrackBiLSTMResF0NonAttentiveDecoder":
         "nnsvs.acoustic_models.MultiTrackBiLSTMResF0NonAttentiveDecoder",
+    f"{PKG}.acoustic_models.NPSSMDNMultistreamParametricModel":
+        "nnsvs.acoustic_models.NPSSMDNMultistreamParametricModel",
+    f"{PKG}.acoustic_models.BiLSTMResF0NonAttentiveDecoder":
+        "nnsvs.acoustic_models.BiLSTMResF0NonAttentiveDecoder",
     f"{PKG}.diffsinger.GaussianDiffusion": "nnsvs.diffsinger.GaussianDiffusion",
     f"{PKG}.diffsinger.DiffNet": "nnsvs.diffsinger.DiffNet",
     f"{PKG}.model.FFConvLSTM": "nnsvs.model.FFConvLSTM",
@@ -116,6 +120,19 @@ def multitrack_diffusion(num_speakers=4, tiny=False, vuv_dropout=0.1, output_sub
         },
     }
     cfg.update(LF0_STATS)
+    return cfg
+
+
+def singletrack_diffusion(tiny=False, vuv_dropout=0.1):
+    """BASELINE config 2: the single-track diffusion acoustic model,
+    recipes/jaCappella_ritsu/dev-48k-world-multitrack/conf/train_acoustic/model/
+    acoustic_nnsvs_world_multi_ar_f0_diff_mgcbap.yaml (netG): the multi-track config's
+    sub-models without the second track and the speaker embedding."""
+    cfg = multitrack_diffusion(tiny=tiny, vuv_dropout=vuv_dropout)
+    cfg["_target_"] = f"{PKG}.acoustic_models.NPSSMDNMultistreamParametricModel"
+    for k in ("speaker_embedding", "output_subtrack"):
+        cfg.pop(k)
+    cfg["lf0_model"]["_target_"] = f"{PKG}.acoustic_models.BiLSTMResF0NonAttentiveDecoder"
     return cfg
 
 

@@ -63,6 +63,7 @@ __global__ __launch_bounds__(4 * H) void ardec_fwd_kernel(
     const float* __restrict__ wfo, int ldwfo,   // W_fo [4][ldwfo], cols [0, H)
     const float* __restrict__ score, int lds,   // raw score lf0 at score[(b*T + f)*lds]
     const float* __restrict__ mask,             // [B][Tr] scaled keep mask
+    const float* __restrict__ teach, int ldt,   // teacher forcing: targets[(b*T + f)*ldt]
     int T, ArConsts k,
     float* __restrict__ lf0, float* __restrict__ res,   // [B*T]
     float* __restrict__ sg, float* __restrict__ sc, float* __restrict__ sh,  // [B*Tr][4H|H|H]
@@ -143,8 +144,14 @@ __global__ __launch_bounds__(4 * H) void ardec_fwd_kernel(
       so[row * 4 + r] = ov;
     }
     if (tid == 0) sp[row] = p;
-    prev = l;  // r == 3 for tid >= 3
-    prev = __shfl(prev, 3);
+    if (teach) {
+      // teacher forcing (tacotron_f0.py:156-159, 226-228): the next input is the target
+      // of this step's last frame, decoder_targets[:, t] = targets[:, 4t + 3]
+      prev = teach[((long long)b * T + 4 * t + 3) * ldt];
+    } else {
+      prev = l;  // r == 3 for tid >= 3
+      prev = __shfl(prev, 3);
+    }
   }
 }
 
@@ -154,7 +161,7 @@ __global__ __launch_bounds__(4 * H) void ardec_bwd_kernel(
     const float* __restrict__ wpb,              // packed transposed W_hh
     const float* __restrict__ wih_p,            // [4H]
     const float* __restrict__ wfo, int ldwfo,   // W_fo [4][ldwfo]
-    const float* __restrict__ mask, int T, ArConsts k,
+    const float* __restrict__ mask, int teacher, int T, ArConsts k,
     const float* __restrict__ sg, const float* __restrict__ sc, const float* __restrict__ so,
     float* __restrict__ dg,                     // [B*Tr][4H]
     float* __restrict__ do4) {                  // [B*Tr][4]
@@ -221,7 +228,8 @@ __global__ __launch_bounds__(4 * H) void ardec_bwd_kernel(
     float dp = 0.f;
 #pragma unroll
     for (int w2 = 0; w2 < NW; ++w2) dp += red[t & 1][w2];
-    dprev = dp * mask[row];
+    // teacher forcing: the step input is a target, not the previous output
+    dprev = teacher ? 0.f : dp * mask[row];
   }
 }
 
@@ -309,21 +317,23 @@ __global__ void downsample_wgrad_kernel(DsArgs a, const float* __restrict__ de, 
 template <int H>
 int fwd_launch(const float* gx, int ldgx, const float* ofx, int ldo, const float* wpf,
                const float* wih_p, const float* wfo, int ldwfo, const float* score, int lds,
-               const float* mask, int B, int T, ArConsts k, float* lf0, float* res, float* sg,
-               float* sc, float* sh, float* so, float* sp, hipStream_t st) {
+               const float* mask, const float* teach, int ldt, int B, int T, ArConsts k,
+               float* lf0, float* res, float* sg, float* sc, float* sh, float* so, float* sp,
+               hipStream_t st) {
   hipLaunchKernelGGL(ardec_fwd_kernel<H>, dim3(B), dim3(4 * H), 0, st, gx, ldgx, ofx, ldo, wpf,
-                     wih_p, wfo, ldwfo, score, lds, mask, T, k, lf0, res, sg, sc, sh, so, sp);
+                     wih_p, wfo, ldwfo, score, lds, mask, teach, ldt, T, k, lf0, res, sg, sc, sh,
+                     so, sp);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
 
 template <int H>
 int bwd_launch(const float* glf0, const float* gres, const float* wpb, const float* wih_p,
-               const float* wfo, int ldwfo, const float* mask, int B, int T, ArConsts k,
-               const float* sg, const float* sc, const float* so, float* dg, float* do4,
-               hipStream_t st) {
+               const float* wfo, int ldwfo, const float* mask, int teacher, int B, int T,
+               ArConsts k, const float* sg, const float* sc, const float* so, float* dg,
+               float* do4, hipStream_t st) {
   hipLaunchKernelGGL(ardec_bwd_kernel<H>, dim3(B), dim3(4 * H), 0, st, glf0, gres, wpb, wih_p, wfo,
-                     ldwfo, mask, T, k, sg, sc, so, dg, do4);
+                     ldwfo, mask, teacher, T, k, sg, sc, so, dg, do4);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
@@ -341,7 +351,8 @@ ENSVS_API int ensvs_ardec_pack(const float* whh, int H, float* wpf, float* wpb, 
 
 ENSVS_API int ensvs_ardec_fwd(const float* gx, int ldgx, const float* ofx, int ldo,
                               const float* wpf, const float* wih_p, const float* wfo, int ldwfo,
-                              const float* score, int lds, const float* mask, int B, int T, int H,
+                              const float* score, int lds, const float* mask,
+                              const float* teach, int ldt, int B, int T, int H,
                               float in_min, float in_max, float mean, float scale, float* lf0,
                               float* res, float* sg, float* sc, float* sh, float* so, float* sp,
                               void* stream) {
@@ -349,29 +360,30 @@ ENSVS_API int ensvs_ardec_fwd(const float* gx, int ldgx, const float* ofx, int l
   ArConsts k{in_min, in_max, mean, scale};
   hipStream_t st = (hipStream_t)stream;
   switch (H) {
-    case 16: return fwd_launch<16>(gx, ldgx, ofx, ldo, wpf, wih_p, wfo, ldwfo, score, lds, mask, B, T, k, lf0, res, sg, sc, sh, so, sp, st);
-    case 32: return fwd_launch<32>(gx, ldgx, ofx, ldo, wpf, wih_p, wfo, ldwfo, score, lds, mask, B, T, k, lf0, res, sg, sc, sh, so, sp, st);
-    case 64: return fwd_launch<64>(gx, ldgx, ofx, ldo, wpf, wih_p, wfo, ldwfo, score, lds, mask, B, T, k, lf0, res, sg, sc, sh, so, sp, st);
-    case 128: return fwd_launch<128>(gx, ldgx, ofx, ldo, wpf, wih_p, wfo, ldwfo, score, lds, mask, B, T, k, lf0, res, sg, sc, sh, so, sp, st);
-    case 256: return fwd_launch<256>(gx, ldgx, ofx, ldo, wpf, wih_p, wfo, ldwfo, score, lds, mask, B, T, k, lf0, res, sg, sc, sh, so, sp, st);
+    case 16: return fwd_launch<16>(gx, ldgx, ofx, ldo, wpf, wih_p, wfo, ldwfo, score, lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, so, sp, st);
+    case 32: return fwd_launch<32>(gx, ldgx, ofx, ldo, wpf, wih_p, wfo, ldwfo, score, lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, so, sp, st);
+    case 64: return fwd_launch<64>(gx, ldgx, ofx, ldo, wpf, wih_p, wfo, ldwfo, score, lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, so, sp, st);
+    case 128: return fwd_launch<128>(gx, ldgx, ofx, ldo, wpf, wih_p, wfo, ldwfo, score, lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, so, sp, st);
+    case 256: return fwd_launch<256>(gx, ldgx, ofx, ldo, wpf, wih_p, wfo, ldwfo, score, lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, so, sp, st);
     default: return ENSVS_E_SHAPE;
   }
 }
 
 ENSVS_API int ensvs_ardec_bwd(const float* glf0, const float* gres, const float* wpb,
                               const float* wih_p, const float* wfo, int ldwfo, const float* mask,
-                              int B, int T, int H, float in_min, float in_max, float mean,
+                              int teacher, int B, int T, int H, float in_min, float in_max,
+                              float mean,
                               float scale, const float* sg, const float* sc, const float* so,
                               float* dg, float* do4, void* stream) {
   if (T % 4 != 0) return ENSVS_E_SHAPE;
   ArConsts k{in_min, in_max, mean, scale};
   hipStream_t st = (hipStream_t)stream;
   switch (H) {
-    case 16: return bwd_launch<16>(glf0, gres, wpb, wih_p, wfo, ldwfo, mask, B, T, k, sg, sc, so, dg, do4, st);
-    case 32: return bwd_launch<32>(glf0, gres, wpb, wih_p, wfo, ldwfo, mask, B, T, k, sg, sc, so, dg, do4, st);
-    case 64: return bwd_launch<64>(glf0, gres, wpb, wih_p, wfo, ldwfo, mask, B, T, k, sg, sc, so, dg, do4, st);
-    case 128: return bwd_launch<128>(glf0, gres, wpb, wih_p, wfo, ldwfo, mask, B, T, k, sg, sc, so, dg, do4, st);
-    case 256: return bwd_launch<256>(glf0, gres, wpb, wih_p, wfo, ldwfo, mask, B, T, k, sg, sc, so, dg, do4, st);
+    case 16: return bwd_launch<16>(glf0, gres, wpb, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc, so, dg, do4, st);
+    case 32: return bwd_launch<32>(glf0, gres, wpb, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc, so, dg, do4, st);
+    case 64: return bwd_launch<64>(glf0, gres, wpb, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc, so, dg, do4, st);
+    case 128: return bwd_launch<128>(glf0, gres, wpb, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc, so, dg, do4, st);
+    case 256: return bwd_launch<256>(glf0, gres, wpb, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc, so, dg, do4, st);
     default: return ENSVS_E_SHAPE;
   }
 }

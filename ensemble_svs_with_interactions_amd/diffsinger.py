@@ -565,13 +565,14 @@ class GaussianDiffusion(BaseModel):
         xr, dst = self.denoise_fn._fwd(xn, Mc, t, cond, E, B, T, save=save)
         return noise, xr, dict(est=est, dst=dst)
 
-    def _bwd(self, st, dxr, after_denoiser=None):
+    def _bwd(self, st, dxr, after_denoiser=None, want_spk=True):
         """after_denoiser: called between the DiffNet and the encoder backward (the step
-        schedule records a stream event there)."""
+        schedule records a stream event there).  Returns the per-sequence speaker-vector
+        gradient (B, E) when want_spk."""
         dcond = self.denoise_fn._bwd(st["dst"], dxr)
         if after_denoiser is not None:
             after_denoiser()
-        _, dspk = self.encoder._bwd(st["est"], dcond, want_spk=True)
+        _, dspk = self.encoder._bwd(st["est"], dcond, want_spk=want_spk)
         return dspk
 
     def _schedule_host(self):

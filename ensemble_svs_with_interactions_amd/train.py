@@ -176,6 +176,15 @@ def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengt
     return loss, optimizer.norm
 
 
+def train_step_single(model, optimizer, x, y, lengths, draws=None, ddp=True):
+    """One training step of the single-track NPSSMDNMultistreamParametricModel (BASELINE
+    config 2; nnsvs/bin/train_acoustic.py:33-274 with feats_criterion l1, pitch_reg_weight 0):
+    forward with teacher forcing, masked L1 over all streams / element count, backward,
+    clip, Adam.  lengths: per-sequence valid frames (sorted descending, train_acoustic.py:
+    :343).  Returns (loss, grad_norm) device tensors."""
+    return train_step(model, optimizer, x, None, y, None, None, lengths, draws=draws, ddp=ddp)
+
+
 def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws,
                     ddp, y_sub, logf0_diff_weight):
     """zero_grad + forward + masked L1 (+ interaction loss) + backward into the flat grads."""
@@ -293,8 +302,9 @@ class GraphedTrainStep:
         self.lengths = [int(v) for v in lengths]
         self.kw = dict(y_sub=None if y_sub is None else y_sub.clone(),
                        logf0_diff_weight=logf0_diff_weight)
-        self.inputs = dict(x_main=x_main.clone(), x_sub=x_sub.clone(), y_main=y_main.clone(),
-                           spk_main=spk_main.clone(), spk_sub=spk_sub.clone())
+        cl = lambda t: None if t is None else t.clone()  # noqa: E731 (single track: None)
+        self.inputs = dict(x_main=cl(x_main), x_sub=cl(x_sub), y_main=cl(y_main),
+                           spk_main=cl(spk_main), spk_sub=cl(spk_sub))
         dev = x_main.device
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))

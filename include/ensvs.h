@@ -125,17 +125,21 @@ int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* w
                    const long long* lengths, int B, int T, int H, const float* saved, float* dg,
                    int lddg, void* stream);
 
-/* Free-running residual-F0 AR decoder (acoustic_models/tacotron_f0.py:126-237 with
- * ZoneOutCell(LSTMCell), tacotron/decoder.py:20-48).  H in {16,...,256}, T % 4 == 0. */
+/* Residual-F0 AR decoder (acoustic_models/tacotron_f0.py:126-237 with
+ * ZoneOutCell(LSTMCell), tacotron/decoder.py:20-48).  H in {16,...,256}, T % 4 == 0.
+ * teach == NULL: free-running (the multi-track diffusion model, multistream.py:1646-1651,
+ * and every inference); teach != NULL: teacher forcing on targets[(b*T + f)*ldt]
+ * (BiLSTMResF0NonAttentiveDecoder in training, multistream.py:1158); the backward then
+ * takes teacher = 1 (no gradient through the previous output). */
 int ensvs_ardec_pack(const float* whh, int H, float* wpf, float* wpb, void* stream);
 int ensvs_ardec_fwd(const float* gx, int ldgx, const float* ofx, int ldo, const float* wpf,
                     const float* wih_p, const float* wfo, int ldwfo, const float* score, int lds,
-                    const float* mask, int B, int T, int H, float in_min, float in_max, float mean,
-                    float scale, float* lf0, float* res, float* sg, float* sc, float* sh,
-                    float* so, float* sp, void* stream);
+                    const float* mask, const float* teach, int ldt, int B, int T, int H,
+                    float in_min, float in_max, float mean, float scale, float* lf0, float* res,
+                    float* sg, float* sc, float* sh, float* so, float* sp, void* stream);
 int ensvs_ardec_bwd(const float* glf0, const float* gres, const float* wpb, const float* wih_p,
-                    const float* wfo, int ldwfo, const float* mask, int B, int T, int H,
-                    float in_min, float in_max, float mean, float scale, const float* sg,
+                    const float* wfo, int ldwfo, const float* mask, int teacher, int B, int T,
+                    int H, float in_min, float in_max, float mean, float scale, const float* sg,
                     const float* sc, const float* so, float* dg, float* do4, void* stream);
 /* Depthwise Conv1d(k=4, s=4, groups=C) down-sampling (tacotron_f0.py:104-111,161-164). */
 int ensvs_downsample_fwd(const float* p0, int ld0, int n0, const float* p1, int ld1, int n1,

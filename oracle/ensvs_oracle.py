@@ -196,13 +196,15 @@ def ffconvlstm(P, prefix, cfg, x, lengths, spk_embs=None, training=True, bn_upda
     return linear(P, prefix + "fc", out)
 
 
-def resf0_decoder(P, prefix, cfg, enc, dropout_masks):
-    """ResF0NonAttentiveDecoder.forward, free-running (decoder_targets=None).
+def resf0_decoder(P, prefix, cfg, enc, dropout_masks, targets=None):
+    """ResF0NonAttentiveDecoder.forward, free-running (decoder_targets=None) or
+    teacher-forced (``targets`` (B, T, out_dim)).
 
     nnsvs/acoustic_models/tacotron_f0.py:126-237 with prenet_layers=0,
     one ZoneOutCell(LSTMCell) layer with zoneout 0, reduction factor r.
     ``dropout_masks``: (B, T/r, out_dim) scaled keep masks of the always-on
-    F.dropout(prev_out, 0.5, training=True) at :191.
+    F.dropout(prev_out, 0.5, training=True) at :191.  Teacher forcing feeds
+    targets[:, r-1::r] (:156-159) as the next step's input (:226-228).
     """
     r = cfg["reduction_factor"]
     lf0_score = enc[:, :, cfg["in_lf0_idx"]].unsqueeze(-1)
@@ -233,7 +235,7 @@ def resf0_decoder(P, prefix, cfg, enc, dropout_masks):
         out[:, cfg["out_lf0_idx"], :] = pred.squeeze(1)
         outs.append(out)
         res.append(lf0_res)
-        prev = out[:, :, -1]
+        prev = out[:, :, -1] if targets is None else targets[:, r - 1::r][:, t]
     return torch.cat(outs, 2).transpose(1, 2), torch.cat(res, 2).transpose(1, 2)
 
 
@@ -254,6 +256,31 @@ def lf0_model(P, prefix, cfg, x_main, x_sub, spk_main, spk_sub, lengths, dropout
     dcfg = dict(cfg)
     dcfg["in_lf0_idx"] = -2  # tacotron_f0.py:896
     return resf0_decoder(P, prefix + "decoder.", dcfg, out, dropout_masks)
+
+
+def bilstm_lf0_model(P, prefix, cfg, x, lengths, dropout_masks, y=None, training=True,
+                     bn_updates=None, fast=False, relu_masks=None, spk_embs=None):
+    """BiLSTMResF0NonAttentiveDecoder.forward (tacotron_f0.py:706-744), single track:
+    embed (+ spk) -> FF -> [., score lf0] -> conv/BN -> packed bi-LSTM -> [., score lf0]
+    -> decoder (teacher-forced when y is given)."""
+    li = cfg["in_lf0_idx"]
+    s = x[:, :, li].unsqueeze(-1)
+    h = phoneme_embed(P, prefix, x, cfg["in_ph_start_idx"], cfg["in_ph_end_idx"])
+    if spk_embs is not None:
+        h = h + spk_embs
+    out = ff_stack(P, prefix, h, relu_masks)
+    out = torch.cat([out, s], -1)
+    out = conv_stack(P, prefix, out, training, bn_updates, masks=relu_masks)
+    out = bilstm(P, prefix, out, lengths, cfg["num_lstm_layers"], None, fast)
+    out = torch.cat([out, s[:, :out.shape[1]]], -1)
+    dcfg = dict(cfg)
+    dcfg["in_lf0_idx"] = -1  # tacotron_f0.py:674
+    return resf0_decoder(P, prefix + "decoder.", dcfg, out, dropout_masks, targets=y)
+
+
+def replicate_pad(x, pad):
+    """F.pad(x, (0, 0, 0, pad), mode="replicate") on (B, T, C)."""
+    return torch.cat([x, x[:, -1:].expand(x.shape[0], pad, x.shape[2])], 1)
 
 
 # -------------------------------------------------------------- diffusion
@@ -416,6 +443,72 @@ def model_forward(P, cfg, x_main, x_sub, spks, lengths, ys, draws, training=True
     if with_sub:
         return ((mgc, lf0_main, vuv, bap), lf0_res_main), lf0_sub
     return (mgc, lf0_main, vuv, bap), lf0_res_main
+
+
+def model_forward_single(P, cfg, x, lengths, y, draws, training=True, bn_updates=None,
+                         fast=False):
+    """NPSSMDNMultistreamParametricModel.forward, training branch (multistream.py:1133-1233):
+    teacher-forced lf0 model, mgc/bap GaussianDiffusion on [x, y_lf0], V/UV on
+    [x, (y_mgc), (y_lf0), (y_bap)].  draws: 'lf0_main' AR dropout masks, 'mgc_t',
+    'mgc_noise', 'bap_t', 'bap_noise', 'vuv_lstm'."""
+    lcfg = dict(cfg["lf0_model"])
+    for k in ("in_lf0_min", "in_lf0_max", "out_lf0_mean", "out_lf0_scale"):
+        lcfg[k] = cfg[k]  # _set_lf0_params, multistream.py:1110-1117
+    y_mgc, y_lf0, y_vuv, y_bap = split_streams(y, cfg["stream_sizes"])
+    lf0, lf0_res = bilstm_lf0_model(P, "lf0_model.", lcfg, x, lengths, draws["lf0_main"], y_lf0,
+                                    training, bn_updates, fast)
+    cin = torch.cat([x, y_lf0], -1)
+    mgc = gaussian_diffusion_forward(P, "mgc_model.", cfg["mgc_model"], cin, lengths, y_mgc,
+                                     None, draws["mgc_t"], draws["mgc_noise"], training,
+                                     bn_updates, fast)
+    bap = gaussian_diffusion_forward(P, "bap_model.", cfg["bap_model"], cin, lengths, y_bap,
+                                     None, draws["bap_t"], draws["bap_noise"], training,
+                                     bn_updates, fast)
+    vuv_in = [x]
+    if cfg.get("vuv_model_mgc_conditioning", False):
+        vuv_in.append(y_mgc)
+    if cfg.get("vuv_model_lf0_conditioning", True):
+        vuv_in.append(y_lf0)
+    if cfg.get("vuv_model_bap_conditioning", True):
+        vuv_in.append(y_bap[:, :, 0:1] if cfg.get("vuv_model_bap0_conditioning") else y_bap)
+    vuv = ffconvlstm(P, "vuv_model.", cfg["vuv_model"], torch.cat(vuv_in, -1), lengths, None,
+                     training, bn_updates, draws.get("vuv_lstm"), fast)
+    return (mgc, lf0, vuv, bap), lf0_res
+
+
+def model_inference_single(P, cfg, x, lengths, masks, noises_mgc, noises_bap, fast=False):
+    """NPSSMDNMultistreamParametricModel.inference = pad_inference(mdn=True)
+    (acoustic_models/util.py:60-141) around forward(y=None) (multistream.py:1150-1231),
+    whose lf0_model.inference pads r frames more (:1152).  masks: AR dropout masks of the
+    doubly padded lf0 call; noises_*: (K+1, B, 1, M, T+pad) reverse-diffusion draws.
+    Returns (out, out) trimmed to T frames."""
+    r = cfg["reduction_factor"]
+    lcfg = dict(cfg["lf0_model"])
+    for k in ("in_lf0_min", "in_lf0_max", "out_lf0_mean", "out_lf0_scale"):
+        lcfg[k] = cfg[k]
+    lengths = [int(v) for v in lengths]
+    pad, lens1 = pad_inference_lengths(lengths, r)
+    xp = replicate_pad(x, pad)
+    pad2, lens2 = pad_inference_lengths(lens1, r)
+    lf0, _ = bilstm_lf0_model(P, "lf0_model.", lcfg, replicate_pad(xp, pad2), lens2, masks,
+                              None, False, None, fast)
+    lf0 = lf0[:, :-pad2]
+    cin = torch.cat([xp, lf0], -1)
+    mgc = gaussian_diffusion_inference(P, "mgc_model.", cfg["mgc_model"], cin, lens1, None,
+                                       noises_mgc, fast)
+    bap = gaussian_diffusion_inference(P, "bap_model.", cfg["bap_model"], cin, lens1, None,
+                                       noises_bap, fast)
+    vuv_in = [xp]
+    if cfg.get("vuv_model_mgc_conditioning", False):
+        vuv_in.append(mgc)
+    if cfg.get("vuv_model_lf0_conditioning", True):
+        vuv_in.append(lf0)
+    if cfg.get("vuv_model_bap_conditioning", True):
+        vuv_in.append(bap[:, :, 0:1] if cfg.get("vuv_model_bap0_conditioning") else bap)
+    vuv = ffconvlstm(P, "vuv_model.", cfg["vuv_model"], torch.cat(vuv_in, -1), lens1, None,
+                     False, None, None, fast)
+    out = torch.cat([mgc, lf0, vuv, bap], -1)[:, :-pad]
+    return out, out
 
 
 def lf0_interaction_loss(lf0_main, lf0_sub, y_main, y_sub, lengths, stream_sizes):

@@ -414,6 +414,112 @@ def case_model_inference_tiny():
     save("model_inference_tiny", arrays, meta)
 
 
+def st_draws(name, P, T):
+    r = rng_for(name)
+    return dict(lf0_main=ar_masks(name + "_lm", P, T // 4),
+                mgc_t=r.integers(0, 100, size=P).astype(np.int64),
+                mgc_noise=r.standard_normal((P, 1, 60, T)).astype(np.float32),
+                bap_t=r.integers(0, 100, size=P).astype(np.int64),
+                bap_noise=r.standard_normal((P, 1, 5, T)).astype(np.float32))
+
+
+def st_queue(d, T):
+    DROP.queue = [T_(d["lf0_main"][:, t]) for t in range(T // 4)]
+    return inject_diffusion(ints=[T_(d["mgc_t"]), T_(d["bap_t"])],
+                            normals=[T_(d["mgc_noise"]), T_(d["bap_noise"])])
+
+
+def case_st_forward_full():
+    """BASELINE config 2: single-track NPSSMDNMultistreamParametricModel (multistream.py:
+    1025-1243) training forward at full size, teacher-forced lf0 decoder."""
+    model, shapes = build_ref(configs.singletrack_diffusion())
+    model.train()
+    model.vuv_model.lstm.dropout = 0.0
+    P, T = 2, 32
+    batch = data.synthetic_batch(P, T, SEED + 29, lengths=[32, 28])
+    d = st_draws("st_fwd_full", P, T)
+    with st_queue(d, T):
+        (mgc, lf0, vuv, bap), res = model(T_(batch["x_main"]), T_(batch["lengths"]),
+                                          T_(batch["y_main"]))
+    assert not DROP.queue
+    arrays = dict(x=batch["x_main"], y=batch["y_main"], lengths=batch["lengths"],
+                  **{"draw::" + k: v for k, v in d.items()},
+                  mgc_noise_out=mgc[0].detach().numpy(), mgc_recon=mgc[1].detach().numpy(),
+                  lf0=lf0.detach().numpy(), vuv=vuv.detach().numpy(),
+                  bap_noise_out=bap[0].detach().numpy(), bap_recon=bap[1].detach().numpy(),
+                  res=res.detach().numpy())
+    save("st_forward_full", arrays, dict(shapes={k: list(v) for k, v in shapes.items()}))
+
+
+def case_st_train_tiny(steps=2, lr=1e-3):
+    """2 steps of the reference single-track train_step (nnsvs/bin/train_acoustic.py:33-274,
+    feats_criterion l1, no AMP) on the tiny single-track config."""
+    from nnsvs.bin.train_acoustic import train_step as ref_st_train_step
+    model, shapes = build_ref(configs.singletrack_diffusion(tiny=True))
+    model.vuv_model.lstm.dropout = 0.0
+    P, T = 3, 48
+    batch = data.synthetic_batch(P, T, SEED + 31, lengths=[48, 40, 32])
+    opt = torch.optim.Adam(model.parameters(), lr=lr, betas=(0.9, 0.999), weight_decay=0.0)
+    model_config = types.SimpleNamespace(stream_sizes=[60, 1, 1, 5])
+    optim_config = types.SimpleNamespace(clip_norm=1.0)
+    logger = logging.getLogger("golden")
+    before = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    arrays = dict(x=batch["x_main"], y=batch["y_main"], lengths=batch["lengths"])
+    meta = dict(shapes={k: list(v) for k, v in shapes.items()}, lr=lr, steps=steps)
+    losses, norms = [], []
+    for s in range(steps):
+        d = st_draws(f"st_tiny_step{s}", P, T)
+        for k, v in d.items():
+            arrays[f"draw{s}::{k}"] = v
+        with st_queue(d, T):
+            loss, metrics = ref_st_train_step(
+                logger, model, model_config, optim_config, opt, None, True, T_(batch["x_main"]),
+                T_(batch["y_main"]), T_(batch["lengths"]), None, feats_criterion="l1",
+                pitch_reg_dyn_ws=1.0, pitch_reg_weight=0.0, stream_wise_loss=False)
+        losses.append(float(loss))
+        norms.append(float(metrics["GradNorm"]))
+        if s == 0:
+            after = {k: v.detach().clone() for k, v in model.state_dict().items()}
+            for k in after:
+                if after[k].dtype == torch.float32:
+                    arrays[f"delta0::{k}"] = (after[k] - before[k]).numpy()
+    for k, v in model.state_dict().items():
+        if v.dtype == torch.float32:
+            arrays[f"final::{k}"] = v.numpy()
+    meta.update(losses=losses, grad_norms=norms)
+    save("st_train_step_tiny", arrays, meta)
+
+
+def case_st_inference_tiny():
+    """Single-track inference: pad_inference(mdn=True) around forward(y=None), whose
+    lf0_model.inference pads r frames more (multistream.py:1152), T mod 4 = 0..3."""
+    model, shapes = build_ref(configs.singletrack_diffusion(tiny=True))
+    model.eval()
+    arrays, meta = {}, {}
+    for T in (28, 29, 30, 31):
+        batch = data.synthetic_batch(1, T, SEED + 37 + T)
+        pad = 4 - T % 4
+        Tp = T + pad
+        Tpp = Tp + 4
+        r = rng_for(f"st_inf_tiny_{T}")
+        masks = ar_masks(f"st_inf_tiny_masks_{T}", 1, Tpp // 4)
+        nm = r.standard_normal((101, 1, 1, 60, Tp)).astype(np.float32)
+        nb = r.standard_normal((101, 1, 1, 5, Tp)).astype(np.float32)
+        DROP.queue = [T_(masks[0:1, t]) for t in range(Tpp // 4)]
+        with torch.no_grad(), inject_diffusion(normals=[T_(n) for n in nm] + [T_(n) for n in nb]):
+            mu, sigma = model.inference(T_(batch["x_main"]), T_(batch["lengths"]))
+        assert not DROP.queue and torch.equal(mu, sigma)
+        arrays[f"T{T}::x"] = batch["x_main"]
+        arrays[f"T{T}::lengths"] = batch["lengths"]
+        arrays[f"T{T}::masks"] = masks
+        arrays[f"T{T}::noise_mgc"] = nm
+        arrays[f"T{T}::noise_bap"] = nb
+        arrays[f"T{T}::out"] = mu.numpy()
+        meta[f"T{T}"] = dict(pad=pad, out_shape=list(mu.shape))
+    meta["shapes"] = {k: list(v) for k, v in shapes.items()}
+    save("st_inference_tiny", arrays, meta)
+
+
 def case_data_path():
     """Integer/byte fixtures: pairing, collation, masks (bit-exact)."""
     r = rng_for("data_path")
@@ -748,6 +854,10 @@ def main():
         case_train_step_tiny(logf0_diff_weight=0.5, name="train_step_tiny_il")
     if run("inference_tiny"):
         case_model_inference_tiny()
+    if run("st"):
+        case_st_forward_full()
+        case_st_train_tiny()
+        case_st_inference_tiny()
     if run("data"):
         case_data_path()
     if run("usfgan"):

@@ -1,0 +1,167 @@
+"""Data-parallel product step at world size 2 on one MI355X (two processes, gloo over CUDA
+tensors; the bench's N-GPU runs use RCCL with the same code).
+
+Pairs are split x[rank::W] (train_util.py:1176-1182).  Per rank:
+  1. FusedAdam broadcasts rank 0's state (as DDP's constructor does): ranks seeded
+     differently start equal.
+  2. train.train_step (ddp): the flat gradient after the all-reduce equals the mean of the
+     ranks' own (pre-reduce, 1/W-scaled) shard gradients, and the updated parameters are
+     identical on both ranks.
+  3. GraphedTrainStep: the same relation on graph replays (the all-reduce runs between the
+     two captured graphs).
+  4. torch DistributedDataParallel(model) around the drop-in model with the reference-style
+     autograd step: DDP's hooks average the gradients that Function.backward returns, and
+     the result equals the fused data-parallel gradient of the same shards.
+BatchNorm statistics stay per rank, as in the reference (no SyncBN).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+W = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, port, out_dir):
+    import sys
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    sys.path.insert(0, here)
+    from ensemble_svs_with_interactions_amd import configs, data, engine, train
+    from golden_util import load_case
+    from gpu_util import build
+    from test_dropin_gpu import _reference_style_loss
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=W)
+    res = {}
+    try:
+        engine.set_gemm_precision("fp32")
+        a, meta = load_case("train_step_tiny")
+        cfg = configs.multitrack_diffusion(num_speakers=4, tiny=True)
+        b = data.synthetic_batch(4, 32, 77)
+        (mine,) = data.shard_pairs([list(range(4))], rank, W)
+        sel = np.asarray(mine)
+        g = lambda k: torch.from_numpy(np.ascontiguousarray(b[k][sel])).cuda()  # noqa: E731
+        xm, xs, ym, ys, s0, s1 = (g(k) for k in ("x_main", "x_sub", "y_main", "y_sub",
+                                                  "spk_main", "spk_sub"))
+        lens = b["lengths"][sel].tolist()
+        Bs, T = xm.shape[:2]
+        gen = torch.Generator().manual_seed(100 + rank)
+        draws = dict(lf0_main=(torch.rand(Bs * T // 4, generator=gen) > 0.5).float().cuda() * 2,
+                     lf0_sub=(torch.rand(Bs * T // 4, generator=gen) > 0.5).float().cuda() * 2,
+                     mgc_t=torch.randint(0, 100, (Bs,), generator=gen).cuda(),
+                     bap_t=torch.randint(0, 100, (Bs,), generator=gen).cuda(),
+                     mgc_noise=torch.randn(Bs * T, 60, generator=gen).cuda(),
+                     bap_noise=torch.randn(Bs * T, 5, generator=gen).cuda())
+
+        def gather(t):
+            out = [torch.zeros_like(t.cpu()) for _ in range(W)]
+            dist.all_gather(out, t.detach().cpu().contiguous())
+            return out
+
+        # record each rank's own gradient right before the exchange
+        pre = []
+        orig = train.allreduce_grads
+
+        def spy(gflat, group=None):
+            pre.append(gflat.detach().clone())
+            return orig(gflat, group)
+        train.allreduce_grads = spy
+
+        def check_mean(opt, tag):
+            mine_pre = pre[-1]
+            allpre = gather(mine_pre)
+            mean = sum(allpre)  # each rank's gradient is already scaled by 1/W
+            got = opt.gflat.detach().cpu()
+            res[tag + "_grad_err"] = ((got - mean).norm() / mean.norm()).item()
+            res[tag + "_rank_grads_differ"] = float((allpre[0] - allpre[1]).abs().max())
+            flats = gather(opt.flat)
+            res[tag + "_param_mismatch"] = float((flats[0] - flats[1]).abs().max())
+
+        # 1 + 2: broadcast at init, fused step
+        torch.manual_seed(1234 + rank)  # ranks initialise differently on purpose
+        model = configs.instantiate(cfg).cuda()
+        model.vuv_model.lstm.dropout = 0.0
+        opt = train.FusedAdam(model, lr=1e-3)
+        flats = gather(opt.flat)
+        res["init_param_mismatch"] = float((flats[0] - flats[1]).abs().max())
+        loss, norm = train.train_step(model, opt, xm, xs, ym, s0, s1, lens, draws=draws)
+        torch.cuda.synchronize()
+        check_mean(opt, "fused")
+        fused_grad = opt.gflat.detach().cpu().clone()
+
+        # 3: graph-replayed data-parallel steps
+        gstep = train.GraphedTrainStep(model, opt, xm, xs, ym, s0, s1, lens, warmup=1)
+        for _ in range(2):
+            gstep.step()
+        torch.cuda.synchronize()
+        check_mean(opt, "graph")
+        train.allreduce_grads = orig
+
+        # 4: torch DDP around the drop-in model, reference-style autograd step
+        torch.manual_seed(0)
+        ref = build(cfg, meta["shapes"])
+        ref.vuv_model.lstm.dropout = 0.0
+        torch.manual_seed(0)
+        fz = build(cfg, meta["shapes"])
+        fz.vuv_model.lstm.dropout = 0.0
+        fopt = train.FusedAdam(fz, lr=1e-3)
+        train._loss_and_grads(fz, fopt, xm, xs, ym, s0, s1, lens, draws, True, None, 0.0)
+        train.allreduce_grads(fopt.gflat)
+        ddp = torch.nn.parallel.DistributedDataParallel(ref, device_ids=[0])
+        ref.train()
+        ref._replay_draws = draws
+        for p in ref.parameters():
+            p.grad = None
+        lengths = torch.tensor(lens, device="cuda")
+        # DDP averages; the reference's loss is per-rank (not 1/W scaled)
+        loss = _reference_style_loss(ddp, xm, xs, ym, ys, (s0, s1), lengths, 0.0,
+                                     cfg["stream_sizes"])
+        loss.backward()
+        torch.cuda.synchronize()
+        num = den = 0.0
+        for (k, p), (k2, q) in zip(ref.named_parameters(), fz.named_parameters()):
+            assert k == k2
+            num += ((p.grad - q.grad) ** 2).sum().item()
+            den += (q.grad ** 2).sum().item()
+        res["ddp_grad_err"] = (num / den) ** 0.5
+        res["fused_grad_norm"] = float(fused_grad.norm())
+    finally:
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), **{k: np.float64(v) for k, v in res.items()})
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_data_parallel_world2_product_step(tmp_path):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_rank, args=(r, port, str(tmp_path))) for r in range(W)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(280)
+        if p.exitcode is None:
+            p.kill()
+        assert p.exitcode == 0, f"rank exited with {p.exitcode}"
+    for r in range(W):
+        z = dict(np.load(tmp_path / f"r{r}.npz"))
+        print(r, {k: float(v) for k, v in z.items()})
+        assert z["init_param_mismatch"] == 0.0
+        for tag in ("fused", "graph"):
+            assert z[tag + "_grad_err"] < 1e-6, (tag, z[tag + "_grad_err"])
+            assert z[tag + "_param_mismatch"] == 0.0, tag
+            assert z[tag + "_rank_grads_differ"] > 0.0, tag  # the shards really differ
+        assert z["ddp_grad_err"] < 1e-5, z["ddp_grad_err"]

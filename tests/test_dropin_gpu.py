@@ -87,3 +87,68 @@ def test_reference_style_step_equals_fused(case):
     assert abs(l_fused - l_ref) <= 1e-6 * abs(l_ref)
     err = ((g_fused - g_ref).norm() / g_ref.norm()).item()
     assert err < 1e-5, err
+
+
+def test_reference_step_amp_gradscaler_equals_fused():
+    """The reference's own step shape (train_acoustic_multitrack.py:93-184, 358-380):
+    prediction_type() dispatch, fp16 autocast around the forward, GradScaler scale ->
+    backward -> unscale_ -> clip_grad_norm_ -> step -> update, torch.optim.Adam.  Parameter
+    gradients come back through autograd (Function.backward returns them), so GradScaler
+    and clip_grad_norm_ see them; the result equals the fused step."""
+    from ensemble_svs_with_interactions_amd.base import PredictionType
+    engine.set_gemm_precision("fp32")
+    a, meta = load_case("train_step_tiny")
+    cfg = configs.multitrack_diffusion(num_speakers=4, tiny=True)
+    g = lambda k: torch.from_numpy(a[k]).cuda().contiguous()  # noqa: E731
+    xm, xs, ym, ys, s0, s1 = g("x_main"), g("x_sub"), g("y_main"), g("y_sub"), g("spk_main"), \
+        g("spk_sub")
+    lengths = torch.from_numpy(a["lengths"]).cuda()
+    B, T = xm.shape[:2]
+    draws = _draws(a, B, T)
+    lr = meta["lr"]
+
+    # reference-style
+    model = build(cfg, meta["shapes"])
+    model.vuv_model.lstm.dropout = 0.0
+    p0 = {k: v.detach().clone() for k, v in model.named_parameters()}
+    opt = torch.optim.Adam(model.parameters(), lr=lr, betas=(0.9, 0.999), weight_decay=0.0)
+    scaler = torch.amp.GradScaler("cuda")
+    model.train()
+    opt.zero_grad()
+    model._replay_draws = draws
+    assert model.prediction_type() == PredictionType.MULTISTREAM_HYBRID
+    with torch.autocast("cuda", dtype=torch.float16):
+        loss = _reference_style_loss(model, xm, xs, ym, ys, (s0, s1), lengths, 0.0,
+                                     cfg["stream_sizes"])
+    scaler.scale(loss).backward()
+    scaler.unscale_(opt)
+    grads = {k: p.grad.detach().clone() for k, p in model.named_parameters()}
+    gn = torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+    scaler.step(opt)
+    scaler.update()
+    torch.cuda.synchronize()
+    assert all(v is not None for v in grads.values())
+    after_ref = {k: v.detach().clone() for k, v in model.named_parameters()}
+
+    # fused
+    model2 = build(cfg, meta["shapes"])
+    model2.vuv_model.lstm.dropout = 0.0
+    opt2 = FusedAdam(model2, lr=lr)
+    loss2, norm2 = train_step(model2, opt2, xm, xs, ym, s0, s1, a["lengths"].tolist(),
+                              draws=draws)
+    torch.cuda.synchronize()
+    assert abs(loss.item() - loss2.item()) <= 1e-6 * abs(loss2.item())
+    assert abs(gn.item() - norm2.item()) <= 1e-5 * norm2.item()
+    g2 = {k: p.grad.detach() for k, p in model2.named_parameters()}
+    num = sum(((grads[k] - g2[k]) ** 2).sum().item() for k in grads) ** 0.5
+    den = sum((g2[k] ** 2).sum().item() for k in grads) ** 0.5
+    assert num / den < 1e-5, num / den
+    bad = []
+    for k, p in model2.named_parameters():
+        d_ref = after_ref[k] - p0[k]
+        d_f = p.detach() - p0[k]
+        gk = g2[k].abs()
+        err = (d_ref - d_f).abs().masked_fill(gk < 1e-7 * (1.0 + gk.max()), 0.0)
+        if (err > 0.1 * lr).float().mean().item() > 0.02:
+            bad.append(k)
+    assert not bad, bad[:5]

@@ -38,7 +38,7 @@ def test_lf0_model_matches_reference():
     s1 = torch.from_numpy(a["spk_sub"]).cuda().view(B, -1).contiguous()
     lens = torch.tensor(a["lengths"].tolist(), device="cuda")
     masks = torch.from_numpy(a["masks"]).cuda().view(-1).contiguous()
-    lf0, res, st = mod._fwd(xm, xs, D, B, T, lens, s0, s1, s0.shape[1], masks=masks)
+    lf0, res, st = mod._fwd([xm, xs], D, B, T, lens, (s0, s1), s0.shape[1], masks=masks)
     R1 = torch.from_numpy(a["R1"]).cuda().view(-1).contiguous()
     R2 = torch.from_numpy(a["R2"]).cuda().view(-1).contiguous()
     d0, d1, _ = mod._bwd(st, R1, R2)

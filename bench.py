@@ -142,30 +142,70 @@ def _median_time(fn, reps):
     return float(np.median(ts)), out
 
 
+ACOUSTIC_INFER_FLOP_PER_FRAME = 3.01e9  # 100 reverse-diffusion steps
+VOCODER_FLOP_PER_FRAME = 4.68e6 * 240   # uSFGAN 4.68 MFLOP/sample x 240 samples/frame
+
+
+def _timing_models(dev):
+    """The recipe's multi-track time-lag and duration MDN models (random init) and scalers
+    fitted on synthetic statistics (the reference fits them on the corpus)."""
+    from ensemble_svs_with_interactions_amd import scalers
+    rng = np.random.default_rng(11)
+    out = {}
+    for name, mu, sd in (("timelag", 0.0, 3.0), ("duration", 12.0, 6.0)):
+        m = configs.instantiate(configs.multitrack_timing(name, num_speaker=4)).to(dev).eval()
+        fit = rng.random((1000, 82))
+        ins = scalers.MinMaxScaler(-fit.min(0) / np.ptp(fit, 0), 1.0 / np.ptp(fit, 0),
+                                   fit.min(0), fit.max(0))
+        outs = scalers.StandardScaler(np.array([mu]), np.array([sd * sd]))
+        out[name] = (m, (ins, outs))
+    return out
+
+
 def synth_rtf(model, dev, T=2000, parts=6, reps=3):
-    """Synthesis real-time factor (BASELINE metric part 2): elapsed /
-    audio seconds (svs.py:449-452, 581-582) of acoustic inference (pad_inference_multitrack,
-    free-running AR log-F0, 100-step reverse diffusion for mgc and bap, V/UV) + the uSFGAN
-    generator on its output, for one (main, sub) pair of T frames (5 ms), for a
-    `parts`-part ensemble (every part paired with its neighbour) batched in one pass, and
-    for the reference's ordered-pair sweep (synthesis_multitrack.py:113-118: every part
-    with every partner, itself included: parts^2 pairs) batched in one pass.
-    Host glue of the reference (scalers, pyworld aperiodicity codec, gen.py:1637-1694) is
-    replaced by identity scalers on synthetic data."""
-    from ensemble_svs_with_interactions_amd import usfgan
+    """Synthesis real-time factor (BASELINE metric part 2 and config 5):
+    elapsed / audio seconds (svs.py:449-452, 581-582) of the pipeline of
+    synthesis_multitrack.py:113-288 -- timing inference (time-lag + duration MDN models with
+    the onset merge and duration fitting of gen.py:214-1006, per ordered pair), acoustic
+    inference (pad_inference_multitrack, free-running AR log-F0, 100-step reverse diffusion
+    for mgc and bap, V/UV) and the uSFGAN generator -- for one (main, sub) pair of T frames
+    (5 ms), for a `parts`-part ensemble (every part paired with its neighbour) batched in
+    one acoustic/vocoder pass, and for the reference's ordered-pair sweep (every part with
+    every partner, itself included: parts^2 pairs).  The acoustic input frames are
+    synthetic features of the song length (the reference's ground-truth-duration path:
+    its predicted-timing path fails, Appendix A-12); timing runs on synthetic score tracks
+    and its output labels are not fed back into frame features (nnmnkwii frame feature
+    extraction is out of scope).  Scalers and the pyworld codec of gen.py:1637-1694 are
+    replaced by identity statistics on synthetic data."""
+    from ensemble_svs_with_interactions_amd import synthesis, usfgan
     torch.manual_seed(7)
     voc = configs.instantiate(configs.usfgan_generator()).to(dev)
     voc.remove_weight_norm()  # as load_vocoder does (nnsvs/util.py:412-414)
     wrapper = usfgan.USFGANWrapper({"data": dict(configs.USFGAN_DATA),
                                     "generator": {"aux_context_window": 2}}, voc)
+    tm = _timing_models(dev)
+    score = data.synthetic_score(99, parts, T)
+    spk_of = [p % 4 for p in range(parts)]
     model.eval()
     sc, mu = configs.LF0_STATS["out_lf0_scale"], configs.LF0_STATS["out_lf0_mean"]
     out = {}
-    for name, B in (("pair", 1), (f"ensemble_{parts}part", parts),
-                    (f"n2_sweep_{parts}part", parts * parts)):
+    for name, pairs in (("pair", [(0, 1)]),
+                        (f"ensemble_{parts}part", [(i, (i + 1) % parts) for i in range(parts)]),
+                        (f"n2_sweep_{parts}part", [(i, j) for i in range(parts)
+                                                   for j in range(parts)])):
+        B = len(pairs)
         b = data.synthetic_batch(B, T, 4242 + B)
         g = lambda k: torch.from_numpy(b[k]).to(dev).contiguous()  # noqa: E731
         xm, xs, s0, s1 = g("x_main"), g("x_sub"), g("spk_main"), g("spk_sub")
+
+        def timing():
+            res = []
+            for i, j in pairs:
+                res.append(synthesis.predict_timing_multitrack(
+                    tm["timelag"][0], tm["duration"][0], [score[i], score[j]],
+                    [spk_of[i], spk_of[j]], tm["timelag"][1], tm["duration"][1],
+                    device=dev))
+            return res
 
         def acoustic():
             return model.inference(xm, xs, spks=(s0, s1), lengths=[T] * B)
@@ -175,22 +215,83 @@ def synth_rtf(model, dev, T=2000, parts=6, reps=3):
             aux = torch.cat([feats[:, :, :60], feats[:, :, 62:67]], -1)
             return wrapper.inference_batch(f0, aux)
 
-        feats = acoustic()  # warm-up (weight packing)
+        timing()
+        feats = acoustic()  # warm-up (weight packing, graph capture)
         vocoder(feats)
+        tt, _ = _median_time(timing, reps)
         ta, feats = _median_time(acoustic, reps)
         tv, wav = _median_time(lambda: vocoder(feats), reps)
         assert torch.isfinite(wav).all()
         sec = T * 0.005
+        flops = B * T * (ACOUSTIC_INFER_FLOP_PER_FRAME + VOCODER_FLOP_PER_FRAME)
         # rtf: wall-clock / seconds of the song (the whole ensemble rendered);
         # rtf_per_track: wall-clock / seconds of synthesized audio (B tracks), the
         # reference's per-synthesis definition (svs.py:449-452, 581-582)
-        out[name] = dict(rtf=(ta + tv) / sec, rtf_per_track=(ta + tv) / (B * sec),
-                         acoustic_ms=ta * 1e3, vocoder_ms=tv * 1e3, tracks=B,
-                         samples_per_track=int(wav.shape[-1]))
+        out[name] = dict(rtf=(tt + ta + tv) / sec, rtf_per_track=(tt + ta + tv) / (B * sec),
+                         timing_ms=tt * 1e3, acoustic_ms=ta * 1e3, vocoder_ms=tv * 1e3,
+                         tracks=B, samples_per_track=int(wav.shape[-1]),
+                         model_tflops_per_s=flops / (ta + tv) / 1e12)
     model.train()
-    return dict(metric="synth RTF (acoustic inference + uSFGAN) / audio seconds",
+    ens = out[f"ensemble_{parts}part"]
+    achieved = ens["model_tflops_per_s"]
+    return dict(metric="synth RTF (timing + acoustic inference + uSFGAN) / audio seconds",
                 frames=T, audio_s=T * 0.005, diffusion_steps=100, higher_is_better=False,
-                dtype=engine.gemm_precision(), **out)
+                dtype=engine.gemm_precision(), **out,
+                roofline={"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
+                          "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
+                          "traffic": None,
+                          "work": f"ensemble_{parts}part acoustic inference "
+                                  f"({ACOUSTIC_INFER_FLOP_PER_FRAME / 1e9:.2f} GFLOP/frame) + "
+                                  f"uSFGAN ({VOCODER_FLOP_PER_FRAME / 1e9:.2f} GFLOP/frame), "
+                                  "GEMM/conv FLOPs of the whole pipeline over its wall time"})
+
+
+def cpu_synth_baseline(T=400):
+    """The oracle's synthesis of one (main, sub) pair on the host cores: multi-track
+    acoustic inference (100 reverse-diffusion steps) + uSFGAN, full-size random weights,
+    T frames; RTF = elapsed / (T * 5 ms).  Bounded sample (the reference probe: acoustic
+    RTF 0.776 at T = 2000, uSFGAN 0.70 at 1 s)."""
+    from oracle import ensvs_oracle as O
+    from oracle import usfgan_oracle as U
+    from oracle.weights import seeded_state_dict
+    cfg = configs.multitrack_diffusion(num_speakers=4)
+    m = configs.instantiate(cfg)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    del m
+    P = {k: torch.from_numpy(v) for k, v in seeded_state_dict(shapes, 1).items()}
+    for pre in ("mgc_model.", "bap_model."):
+        for k, v in O.diffusion_schedule().items():
+            P[pre + k] = v
+    vm = configs.instantiate(configs.usfgan_generator())
+    vshapes = {k: tuple(v.shape) for k, v in vm.state_dict().items()}
+    del vm
+    PV = {k: torch.from_numpy(v) for k, v in seeded_state_dict(vshapes, 2).items()}
+    b = data.synthetic_batch(1, T, 5)
+    rng = torch.Generator().manual_seed(5)
+    Tp = T + 4 - T % 4
+    t0 = time.time()
+    with torch.no_grad():
+        feats = O.model_inference(
+            P, cfg, torch.from_numpy(b["x_main"]), torch.from_numpy(b["x_sub"]),
+            (torch.from_numpy(b["spk_main"]), torch.from_numpy(b["spk_sub"])), [T],
+            (torch.rand(1, Tp // 4, 1, generator=rng) < 0.5).float() * 2,
+            torch.randn(101, 1, 1, 60, Tp, generator=rng),
+            torch.randn(101, 1, 1, 5, Tp, generator=rng), fast=True)
+        ta = time.time() - t0
+        sc, mu = configs.LF0_STATS["out_lf0_scale"], configs.LF0_STATS["out_lf0_mean"]
+        f0 = torch.exp(feats[0, :, 60:61] * sc + mu).numpy()
+        aux = torch.cat([feats[0, :, :60], feats[0, :, 62:67]], -1)
+        L = T * configs.USFGAN_DATA["hop_size"]
+        t1 = time.time()
+        wav = U.usfgan_inference(PV, f0, aux, torch.randn(1, 1, L, generator=rng),
+                                 torch.randn(1, 1, L, generator=rng))
+        tv = time.time() - t1
+    assert torch.isfinite(wav).all()
+    sec = T * 0.005
+    return dict(value=(ta + tv) / sec, unit="RTF (lower is better)",
+                cores=torch.get_num_threads(), kind="port", acoustic_s=ta, vocoder_s=tv,
+                sample=f"oracle multi-track pair inference (100 diffusion steps) + uSFGAN "
+                       f"oracle, {T} frames = {sec:.1f} s of audio, fp32, one run")
 
 
 def _cpu_model():
@@ -406,6 +507,8 @@ def main():
         out["synth"] = synth_rtf(model, dev)
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(args)
+        if "synth" in out:
+            out["synth"]["cpu_baseline"] = cpu_synth_baseline()
     print(json.dumps(out), flush=True)
 
 

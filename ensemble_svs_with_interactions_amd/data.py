@@ -219,3 +219,33 @@ def shard_pairs(batches, rank, world):
     if world == 1:
         return [list(x) for x in batches]
     return [list(x[rank::world]) for x in batches if len(x) % world == 0]
+
+
+def synthetic_score(seed, parts, T, note_dim=82, frame_period=5):
+    """Synthetic score tracks of a `parts`-part song of T frames for the timing models
+    (config 5 bench): notes on a shared 100-frame onset grid (0.5 s; every part takes ~70 %
+    of the grid points, so onsets tie across parts), 1-3 phoneme labels per note sharing
+    the note onset (get_note_indices groups labels by onset), ~15 % silence notes.
+    Per part: dict(start, end (HTS units, int64), contexts, ph_feats (N, note_dim) float32,
+    note_feats (one row per note))."""
+    rng = np.random.default_rng(seed)
+    shift = int(frame_period * 1e4)
+    grid = np.arange(0, T, 100)
+    tracks = []
+    for _ in range(parts):
+        on = grid[rng.random(len(grid)) < 0.7]
+        if len(on) == 0 or on[0] != 0:
+            on = np.concatenate(([0], on))
+        start, end, ctx, first = [], [], [], []
+        for k, o in enumerate(on):
+            nxt = on[k + 1] if k + 1 < len(on) else T
+            sil = rng.random() < 0.15
+            first.append(len(start))
+            for _ in range(1 if sil else int(rng.integers(1, 4))):
+                start.append(int(o) * shift)
+                end.append(int(nxt) * shift)
+                ctx.append("x-sil+y@1" if sil else "x-a+y@1")
+        ph = rng.random((len(start), note_dim)).astype(np.float32)
+        tracks.append(dict(start=np.asarray(start, np.int64), end=np.asarray(end, np.int64),
+                           contexts=ctx, ph_feats=ph, note_feats=ph[first]))
+    return tracks

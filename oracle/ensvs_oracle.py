@@ -476,6 +476,41 @@ def model_forward_single(P, cfg, x, lengths, y, draws, training=True, bn_updates
     return (mgc, lf0, vuv, bap), lf0_res
 
 
+def model_inference(P, cfg, x_main, x_sub, spks, lengths, masks, noises_mgc, noises_bap,
+                    fast=False):
+    """MultiTrackNPSSMDNMultistreamParametricModel.inference (multistream.py:1770-1778):
+    pad_inference_multitrack (acoustic_models/util.py:154-188: r - max(L) % r replicated
+    frames, never 0) around forward(ys=None) (:1594-1757) in eval mode.  masks: AR-decoder
+    dropout masks of the main-track lf0 call (the sub-track call's outputs are unused);
+    noises_*: (K+1, B, 1, M, T+pad).  Returns the main track's (B, T, 67)."""
+    r = cfg["reduction_factor"]
+    lcfg = dict(cfg["lf0_model"])
+    for k in ("in_lf0_min", "in_lf0_max", "out_lf0_mean", "out_lf0_scale"):
+        lcfg[k] = cfg[k]
+    pad, lens = pad_inference_lengths([int(v) for v in lengths], r)
+    xm, xs = replicate_pad(x_main, pad), replicate_pad(x_sub, pad)
+    emb = P["speaker_embedding.emb.weight"]
+    T = xm.shape[1]
+    s0 = F.embedding(spks[0], emb).expand(-1, T, -1)
+    s1 = F.embedding(spks[1], emb).expand(-1, T, -1)
+    lf0, _ = lf0_model(P, "lf0_model.", lcfg, xm, xs, s0, s1, lens, masks, False, None, fast)
+    cin = torch.cat([xm, lf0], -1)
+    mgc = gaussian_diffusion_inference(P, "mgc_model.", cfg["mgc_model"], cin, lens, s0,
+                                       noises_mgc, fast)
+    bap = gaussian_diffusion_inference(P, "bap_model.", cfg["bap_model"], cin, lens, s0,
+                                       noises_bap, fast)
+    vuv_in = [xm]
+    if cfg.get("vuv_model_mgc_conditioning", False):
+        vuv_in.append(mgc)
+    if cfg.get("vuv_model_lf0_conditioning", True):
+        vuv_in.append(lf0)
+    if cfg.get("vuv_model_bap_conditioning", True):
+        vuv_in.append(bap[:, :, 0:1] if cfg.get("vuv_model_bap0_conditioning") else bap)
+    vuv = ffconvlstm(P, "vuv_model.", cfg["vuv_model"], torch.cat(vuv_in, -1), lens, s0,
+                     False, None, None, fast)
+    return torch.cat([mgc, lf0, vuv, bap], -1)[:, :-pad]
+
+
 def model_inference_single(P, cfg, x, lengths, masks, noises_mgc, noises_bap, fast=False):
     """NPSSMDNMultistreamParametricModel.inference = pad_inference(mdn=True)
     (acoustic_models/util.py:60-141) around forward(y=None) (multistream.py:1150-1231),

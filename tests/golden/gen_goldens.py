@@ -520,6 +520,112 @@ def case_st_inference_tiny():
     save("st_inference_tiny", arrays, meta)
 
 
+class FakeLabels:
+    """Test-side stand-in for nnmnkwii's HTSLabelFile in the timing-inference golden: it only
+    CARRIES data (start/end times, context strings, per-label feature rows returned by the
+    patched fe.linguistic_features); every arithmetic step is the reference's own."""
+
+    def __init__(self, start, end, contexts, feats):
+        self.start_times = list(start)
+        self.end_times = list(end)
+        self.contexts = list(contexts)
+        self.feats = np.asarray(feats, dtype=np.float32)
+        self.frame_shift = 50000
+
+    def round_(self):
+        return self
+
+    def __len__(self):
+        return len(self.start_times)
+
+    def __getitem__(self, idx):
+        idx = list(idx)
+        return FakeLabels([self.start_times[i] for i in idx], [self.end_times[i] for i in idx],
+                          [self.contexts[i] for i in idx], self.feats[idx])
+
+
+def timing_track(r, n_notes, D, grid):
+    """A synthetic score track: notes on a coarse onset grid (ties with the other track),
+    1-3 phonemes per note sharing the note's onset (as get_note_indices expects), a silence
+    note now and then.  Times in HTS units (5 ms frame = 50 000)."""
+    onsets = np.sort(r.choice(np.arange(0, grid), size=n_notes, replace=False)) * 10 * 50000
+    start, end, ctx = [], [], []
+    for k, o in enumerate(onsets):
+        nxt = onsets[k + 1] if k + 1 < n_notes else o + 10 * 50000
+        sil = r.random() < 0.15
+        nph = 1 if sil else int(r.integers(1, 4))
+        for _ in range(nph):
+            start.append(int(o))
+            end.append(int(nxt))
+            ctx.append("x-sil+y@1" if sil else "x-a+y@1")
+    feats = r.random((len(start), D)).astype(np.float32) * 4 - 1
+    return start, end, ctx, feats
+
+
+def case_timing_inference():
+    """predict_timelag_multitrack (gen.py:214-416) and predict_duration_multitrack
+    (gen.py:551-720) of the reference on two synthetic score tracks, with the recipe's
+    MDN time-lag / duration models (seeded weights) and fitted sklearn scalers."""
+    import nnsvs.gen as ref_gen
+    from nnsvs.model import MultiTrackVariancePredictor as RefVP
+    from sklearn.preprocessing import MinMaxScaler, StandardScaler
+    ref_gen.fe = types.SimpleNamespace(
+        linguistic_features=lambda labels, *a, **k: np.asarray(labels.feats))
+    r = rng_for("timing_inference")
+    D = 82
+    arrays, meta = {}, {"cases": []}
+    models = {}
+    for name in ("timelag", "duration"):
+        cfg = configs.multitrack_timing(name, num_speaker=3)
+        cfg = {k: v for k, v in cfg.items() if k != "_target_"}
+        torch.manual_seed(0)
+        m = RefVP(**cfg)
+        shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in
+                           seeded_state_dict(shapes, SEED).items()})
+        m.eval()
+        models[name] = m
+        fit = r.random((500, D)) * 5 - 2
+        ins = MinMaxScaler().fit(fit)
+        outs = StandardScaler().fit(r.standard_normal((500, 1)) * 7 + (1 if name == "timelag" else 9))
+        models[name + "_sc"] = (ins, outs)
+        for k in ("min_", "scale_", "data_min_", "data_max_"):
+            arrays[f"{name}::in::{k}"] = getattr(ins, k)
+        for k in ("mean_", "var_", "scale_"):
+            arrays[f"{name}::out::{k}"] = getattr(outs, k)
+    conf = types.SimpleNamespace(has_dynamic_features=[False])
+    for case in range(3):
+        tr = [timing_track(r, int(r.integers(6, 14)), D, 30) for _ in range(2)]
+        labs = [FakeLabels(*t) for t in tr]
+        spk = [int(r.integers(0, 3)) for _ in range(2)]
+        spks = [torch.IntTensor([spk[0]]), torch.IntTensor([spk[1]])]
+        lag, lag_eval, mask = ref_gen.predict_timelag_multitrack(
+            "cpu", labs, spks, models["timelag"], conf, models["timelag_sc"][0],
+            models["timelag_sc"][1], {}, {}, pitch_indices=[], log_f0_conditioning=False,
+            force_clip_input_features=True)
+        labs = [FakeLabels(*t) for t in tr]
+        mu, sig = ref_gen.predict_duration_multitrack(
+            "cpu", labs, spks, models["duration"], conf, models["duration_sc"][0],
+            models["duration_sc"][1], {}, {}, pitch_indices=[], log_f0_conditioning=False,
+            force_clip_input_features=True)
+        p = f"c{case}::"
+        for t in range(2):
+            arrays[p + f"start{t}"] = np.asarray(tr[t][0], dtype=np.int64)
+            arrays[p + f"end{t}"] = np.asarray(tr[t][1], dtype=np.int64)
+            arrays[p + f"sil{t}"] = np.asarray(["sil" in c for c in tr[t][2]])
+            arrays[p + f"feats{t}"] = tr[t][3]
+        arrays[p + "spk"] = np.asarray(spk)
+        arrays[p + "lag"] = np.asarray(lag)
+        arrays[p + "lag_eval"] = np.asarray(lag_eval)
+        arrays[p + "mask"] = np.asarray(mask)
+        arrays[p + "dur_mu"] = np.asarray(mu)
+        arrays[p + "dur_sigma_sq"] = np.asarray(sig)
+        meta["cases"].append(case)
+    meta["shapes"] = {n: {k: list(v.shape) for k, v in models[n].state_dict().items()}
+                      for n in ("timelag", "duration")}
+    save("timing_inference", arrays, meta)
+
+
 def case_data_path():
     """Integer/byte fixtures: pairing, collation, masks (bit-exact)."""
     r = rng_for("data_path")
@@ -858,6 +964,8 @@ def main():
         case_st_forward_full()
         case_st_train_tiny()
         case_st_inference_tiny()
+    if run("timing_inf"):
+        case_timing_inference()
     if run("data"):
         case_data_path()
     if run("usfgan"):

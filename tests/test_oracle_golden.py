@@ -208,3 +208,18 @@ def test_usfgan_pd_indexing_bitexact():
         xP, xF = U.pd_indexing(x, T_(a["d"]).view(1, 1, -1), dil)
         assert np.array_equal(n1 - xP.numpy().reshape(-1).astype(np.int64), a[f"offP{dil}"])
         assert np.array_equal(xF.numpy().reshape(-1).astype(np.int64) - n1, a[f"offF{dil}"])
+
+
+def test_model_inference_tiny():
+    """MultiTrackNPSSMDN...inference (pad_inference_multitrack) at T mod 4 = 0..3."""
+    a, meta = load_case("model_inference_tiny")
+    cfg = configs.multitrack_diffusion(num_speakers=4, tiny=True)
+    P = params_from_shapes(meta["shapes"])
+    for T in (28, 29, 30, 31):
+        g = lambda k: T_(a[f"T{T}::{k}"])  # noqa: E731
+        with torch.no_grad():
+            out = O.model_inference(P, cfg, g("x_main"), g("x_sub"),
+                                    (g("spk_main"), g("spk_sub")), a[f"T{T}::lengths"],
+                                    g("masks")[0:1], g("noise_mgc"), g("noise_bap"))
+        assert list(out.shape) == meta[f"T{T}"]["out_shape"]
+        assert rel(out, a[f"T{T}::out"]) < 1e-4, T

@@ -29,11 +29,12 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 def gate_gemm_bytes(M, C, E, a_bytes):
     """Algorithmic HBM bytes of one gate-GEMM launch as the training step issues it
-    (DESIGN.md §4): A operand (x+d and cond, a_bytes each), packed weights (bf16), bias, the
-    saved gate/filter pre-activations gf (fp32, M x 2C) and z (M x C) -- in bf16 only on the
-    bf16-operand path (the next GEMM's operand; the fp32 copy is not written), else fp32."""
+    (DESIGN.md §3): A operand (x+d and cond, a_bytes each), packed weights (bf16), bias, the
+    saved gate/filter pre-activations gf (M x 2C) and z (M x C) -- both in bf16 on the
+    bf16 path (z: the next GEMM's operand, no fp32 copy; gf: the backward's save), fp32
+    otherwise."""
     return (M * (C + E) * a_bytes + 2 * C * (3 * C + E) * 2 + 2 * C * 4 +
-            M * C * a_bytes + M * 2 * C * 4)
+            M * C * a_bytes + M * 2 * C * a_bytes)
 TRAIN_FLOP_PER_FRAME = 127.5e6  # SURVEY.md §6 (torch.utils.flop_counter on the oracle)
 
 
@@ -97,8 +98,9 @@ def gate_gemm_timing(model, P, T, dev, iters=20):
     cond = torch.randn(M, E, device=dev, generator=g)
     ds = torch.randn(P, L * C, device=dev, generator=g)
     z = torch.empty(M, C, device=dev)
-    gf = torch.empty(M, 2 * C, device=dev)
     pk = net._packs.ensure(net, net._register)
+    gf = torch.empty(M, 2 * C, device=dev,
+                     dtype=torch.bfloat16 if K.gemm_dtype_is_bf16(pk.fwd) else torch.float32)
 
     def timed(fn):
         for _ in range(3):

@@ -32,6 +32,8 @@ enum {
   EPI_ADDSCALE = 4,  // Y = alpha * aux1 + acc + bias
   EPI_RELU_MASK = 5, // Y = (accum ? Y : 0) + (aux1 > 0 ? acc + bias : 0)   (ReLU backward)
   EPI_GATE_TS = 6,   // uSFGAN: xa/xb interleaved by 16 -> z = tanh(xa)*sigmoid(xb)
+  EPI_AUX0_BF16 = 256,  // flag: GATE writes its gate/filter save (aux0) in bf16
+  EPI_AUX1_BF16 = 512,  // flag: GATE_BWD reads the gate/filter save (aux1) in bf16
 };
 // `relu` of EPI_PLAIN / EPI_ADDSCALE selects the output activation: 1 ReLU, 2 sigmoid.
 
@@ -57,6 +59,9 @@ struct GemmArgs {
   int ld0, ld1;
   float alpha;
   int C;
+  // GATE saves its gate/filter pre-activations to aux0 in bf16, GATE_BWD reads them from
+  // aux1 in bf16 (C ABI: bits EPI_AUX0_BF16 / EPI_AUX1_BF16 of `epi`)
+  int aux0_bf, aux1_bf;
   int vec_out;  // Y / aux0 / aux1 rows 16-B aligned with ld % 4 == 0: 16-B epilogue stores
   // optional bf16 copy of what is written to Y (LDS-staged epilogue only):
   // ybf[row*ybf_ld + col] = bf16(y + ybf_radd[(row / Tout)*ybf_radd_ld + col]) -- the next
@@ -144,6 +149,28 @@ __device__ __forceinline__ void gate_bwd_(float dz, float g, float f, float& dg,
   df = dz * sg * (1.f - th * th);
 }
 
+// one gate/filter pre-activation, fp32 or bf16 (GemmArgs::aux0_bf / aux1_bf)
+__device__ __forceinline__ void st_aux0(const GemmArgs& a, long long i, float v) {
+  if (a.aux0_bf) ((__bf16*)a.aux0)[i] = (__bf16)v;
+  else a.aux0[i] = v;
+}
+__device__ __forceinline__ float ld_aux1(const GemmArgs& a, long long i) {
+  return a.aux1_bf ? (float)((const __bf16*)a.aux1)[i] : a.aux1[i];
+}
+__device__ __forceinline__ void st4_aux0(const GemmArgs& a, long long i, f32x4 v) {
+  if (a.aux0_bf)
+    *(bf16x4*)((__bf16*)a.aux0 + i) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  else
+    *(f32x4*)(a.aux0 + i) = v;
+}
+__device__ __forceinline__ f32x4 ld4_aux1(const GemmArgs& a, long long i) {
+  if (a.aux1_bf) {
+    const bf16x4 v = *(const bf16x4*)((const __bf16*)a.aux1 + i);
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  }
+  return *(const f32x4*)(a.aux1 + i);
+}
+
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], int m0,
                                               int n0, int wr, int wc, int lane) {
   const int rbase = m0 + wr * 64 + (lane >> 4) * 4;
@@ -164,8 +191,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4]
           const float v0 = acc[mt][2 * p][r] + b0;
           const float v1 = acc[mt][2 * p + 1][r] + b1;
           if (a.epi == EPI_GATE) {
-            a.aux0[(long long)row * a.ld0 + c] = v0;
-            a.aux0[(long long)row * a.ld0 + a.C + c] = v1;
+            st_aux0(a, (long long)row * a.ld0 + c, v0);
+            st_aux0(a, (long long)row * a.ld0 + a.C + c, v1);
             a.Y[(long long)row * a.ldy + c] = sigmoidf_(v0) * tanhf(v1);
           } else if (a.epi == EPI_GATE_TS) {
             a.Y[(long long)row * a.ldy + c] = tanhf(v0) * sigmoidf_(v1);
@@ -204,8 +231,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4]
           v = a.aux1[(long long)row * a.ld1 + col] > 0.f ? v : 0.f;
           *y = a.accum ? *y + v : v;
         } else if (a.epi == EPI_GATE_BWD) {
-          const float g = a.aux1[(long long)row * a.ld1 + col];
-          const float f = a.aux1[(long long)row * a.ld1 + a.C + col];
+          const float g = ld_aux1(a, (long long)row * a.ld1 + col);
+          const float f = ld_aux1(a, (long long)row * a.ld1 + a.C + col);
           float dg, df;
           gate_bwd_(v, g, f, dg, df);
           a.Y[(long long)row * a.ldy + col] = dg;
@@ -267,8 +294,8 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         }
       }
       if (a.epi == EPI_GATE) {
-        st4(a.aux0 + (long long)m * a.ld0 + c, g);
-        st4(a.aux0 + (long long)m * a.ld0 + a.C + c, f);
+        st4_aux0(a, (long long)m * a.ld0 + c, g);
+        st4_aux0(a, (long long)m * a.ld0 + a.C + c, f);
         f32x4 z;
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = sigmoidf_(g[e]) * tanhf(f[e]);
@@ -341,8 +368,8 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         if (a.accum) v += ld4(y);
         st4(y, v);
       } else if (a.epi == EPI_GATE_BWD) {
-        const f32x4 g = ld4(a.aux1 + (long long)m * a.ld1 + col);
-        const f32x4 f = ld4(a.aux1 + (long long)m * a.ld1 + a.C + col);
+        const f32x4 g = ld4_aux1(a, (long long)m * a.ld1 + col);
+        const f32x4 f = ld4_aux1(a, (long long)m * a.ld1 + a.C + col);
         f32x4 dg, df;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -378,8 +405,8 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
           w = a.aux1[(long long)m * a.ld1 + col + e] > 0.f ? w : 0.f;
           *ye = a.accum ? *ye + w : w;
         } else if (a.epi == EPI_GATE_BWD) {
-          const float g = a.aux1[(long long)m * a.ld1 + col + e];
-          const float f = a.aux1[(long long)m * a.ld1 + a.C + col + e];
+          const float g = ld_aux1(a, (long long)m * a.ld1 + col + e);
+          const float f = ld_aux1(a, (long long)m * a.ld1 + a.C + col + e);
           gate_bwd_(w, g, f, ye[0], ye[a.C]);
         }
       }
@@ -810,6 +837,278 @@ __global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a
 #undef TAP_PTRS
   if (a.vec_out) gemm_epilogue_lds(a, acc, m0, n0, wr, wc, lane, tid, smem);
   else gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
+}
+
+// ------------------------------------------------------ 256 x 256 bf16-operand GEMM
+// The large-M launches of the step (DiffNet gate / res-skip GEMMs at 30 k frames) are
+// bound by what the CUs pull from L2 into LDS (~70 GB/s per CU, MI355X_MICROARCH.md
+// "Indexed rows"): a 128 x 128 tile moves 32 KB per 64-deep K step for 2 MFLOP, a 256 x 256
+// tile 64 KB for 8 MFLOP -- half the L2 -> LDS bytes per FLOP.  8 waves (2 x 4), each a
+// 128 x 64 sub-tile of 8 x 4 v_mfma_f32_16x16x32_bf16 accumulators; both operand images
+// staged by global_load_lds with the same swizzle and per-tap staging pointers as the
+// 128 x 128 kernel; two stages (128 KB of LDS, one workgroup per CU: a K step is 2 x 64
+// MFMAs per SIMD, long enough to cover the L2 latency of the next step's loads).  The
+// epilogue stages the fp32 tile through LDS in four 64-row chunks and runs the same
+// per-element arithmetic as gemm_epilogue_lds (no column sums).
+constexpr int BMB = 256, BNB = 256, NTHRB = 512, EPB = BNB + 4, CHR = 64;
+
+__device__ __forceinline__ void xcd_tile_big(int& m0, int& n0) {
+  const int nM = gridDim.x, nN = gridDim.y, total = nM * nN;
+  const int orig = blockIdx.x + blockIdx.y * nM;
+  const int xcd = orig & 7, q = total >> 3, r = total & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  m0 = (wg / nN) * BMB;
+  n0 = (wg % nN) * BNB;
+}
+
+// one staged chunk: rows [0, CHR) of T are output rows mb.., columns [0, BNB) are n0..
+__device__ __forceinline__ void epilogue_chunk_big(const GemmArgs& a, const float* T, int mb,
+                                                   int n0, int tid) {
+  const int M = a.M;
+  if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
+    // BNB / 2 output channels per row: gate/filter interleaved by 16 in the packed columns
+    for (int it = tid; it < CHR * (BNB / 8); it += NTHRB) {
+      const int row = it / (BNB / 8), q4 = it % (BNB / 8);
+      const int m = mb + row;
+      const int q = q4 >> 2, j = (q4 & 3) * 4;
+      const int c = n0 / 2 + q * 16 + j;
+      if (m >= M || c >= a.C) continue;
+      const int gc = q * 32 + j;
+      f32x4 g = ld4(T + row * EPB + gc), f = ld4(T + row * EPB + gc + 16);
+      if (a.bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          g[e] += a.bias[n0 + gc + e];
+          f[e] += a.bias[n0 + gc + 16 + e];
+        }
+      }
+      if (a.epi == EPI_GATE) {
+        st4_aux0(a, (long long)m * a.ld0 + c, g);
+        st4_aux0(a, (long long)m * a.ld0 + a.C + c, f);
+        f32x4 z;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) z[e] = sigmoidf_(g[e]) * tanhf(f[e]);
+        if (a.Y) st4(a.Y + (long long)m * a.ldy + c, z);
+        shadow4(a, m, c, z);
+      } else if (a.epi == EPI_GATE_TS) {
+        f32x4 z;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) z[e] = tanhf(g[e]) * sigmoidf_(f[e]);
+        st4(a.Y + (long long)m * a.ldy + c, z);
+      } else {
+        const f32x4 xr = ld4(a.aux1 + (long long)m * a.ld1 + c);
+        f32x4 y, sk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = (xr[e] + g[e]) * 0.70710678118654752f;
+        st4(a.Y + (long long)m * a.ldy + c, y);
+        shadow4(a, m, c, y);
+        float* skp = a.aux0 + (long long)m * a.ld0 + c;
+        if (a.accum) {
+          const f32x4 s0 = ld4(skp);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sk[e] = fmaf(a.alpha, f[e], s0[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sk[e] = a.alpha * f[e];
+        }
+        st4(skp, sk);
+      }
+    }
+    return;
+  }
+  for (int it = tid; it < CHR * (BNB / 4); it += NTHRB) {
+    const int row = it / (BNB / 4), cq = it % (BNB / 4);
+    const int m = mb + row, col = n0 + cq * 4;
+    if (m >= M || col >= a.N) continue;
+    const int ne = min(4, a.N - col);
+    f32x4 v = ld4(T + row * EPB + cq * 4);
+    if (a.bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e < ne) v[e] += a.bias[col + e];
+    }
+    float* y = a.Y + (long long)m * a.ldy + col;
+    if (ne == 4) {
+      if (a.epi == EPI_PLAIN) {
+        if (a.accum) v += ld4(y);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (a.relu == 1) v[e] = fmaxf(v[e], 0.f);
+          else if (a.relu == 2) v[e] = sigmoidf_(v[e]);
+        }
+        st4(y, v);
+        shadow4(a, m, col, v);
+      } else if (a.epi == EPI_ADDSCALE) {
+        const f32x4 x1 = ld4(a.aux1 + (long long)m * a.ld1 + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = __builtin_fmaf(a.alpha, x1[e], v[e]);
+          v[e] = a.relu == 1 ? fmaxf(v[e], 0.f) : v[e];
+        }
+        st4(y, v);
+        shadow4(a, m, col, v);
+      } else if (a.epi == EPI_RELU_MASK) {
+        const f32x4 x1 = ld4(a.aux1 + (long long)m * a.ld1 + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = x1[e] > 0.f ? v[e] : 0.f;
+        if (a.accum) v += ld4(y);
+        st4(y, v);
+      } else if (a.epi == EPI_GATE_BWD) {
+        const f32x4 g = ld4_aux1(a, (long long)m * a.ld1 + col);
+        const f32x4 f = ld4_aux1(a, (long long)m * a.ld1 + a.C + col);
+        f32x4 dg, df;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t0, t1;
+          gate_bwd_(v[e], g[e], f[e], t0, t1);
+          dg[e] = t0;
+          df[e] = t1;
+        }
+        if (a.Y) {
+          st4(y, dg);
+          st4(y + a.C, df);
+        }
+        shadow4(a, m, col, dg);
+        shadow4(a, m, a.C + col, df);
+      }
+    } else {
+      for (int e = 0; e < ne; ++e) {
+        float w = v[e];
+        float* ye = y + e;
+        if (a.epi == EPI_PLAIN) {
+          if (a.accum) w += *ye;
+          if (a.relu == 1) w = fmaxf(w, 0.f);
+          else if (a.relu == 2) w = sigmoidf_(w);
+          *ye = w;
+        } else if (a.epi == EPI_ADDSCALE) {
+          w = __builtin_fmaf(a.alpha, a.aux1[(long long)m * a.ld1 + col + e], w);
+          *ye = a.relu == 1 ? fmaxf(w, 0.f) : w;
+        } else if (a.epi == EPI_RELU_MASK) {
+          w = a.aux1[(long long)m * a.ld1 + col + e] > 0.f ? w : 0.f;
+          *ye = a.accum ? *ye + w : w;
+        } else if (a.epi == EPI_GATE_BWD) {
+          const float g = ld_aux1(a, (long long)m * a.ld1 + col + e);
+          const float f = ld_aux1(a, (long long)m * a.ld1 + a.C + col + e);
+          gate_bwd_(w, g, f, ye[0], ye[a.C]);
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(NTHRB) void conv_gemm_b16_big_kernel(const GemmArgs a) {
+  constexpr int TILE_A = BMB * BK2 * 2;  // 32 KB
+  constexpr int STAGE = TILE_A + BNB * BK2 * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  int m0, n0;
+  xcd_tile_big(m0, n0);
+  const int M = a.M, Tout = a.Tout, Npad = a.Npad;
+  const int nseg = a.nseg;
+  const SegU S0 = seg_u(a.seg[0], a.W);
+  const SegU S1 = nseg > 1 ? seg_u(a.seg[1], a.W) : S0;
+  const SegU S2 = nseg > 2 ? seg_u(a.seg[2], a.W) : S0;
+  const int nit = S0.nk * S0.taps + (nseg > 1 ? S1.nk * S1.taps : 0) +
+                  (nseg > 2 ? S2.nk * S2.taps : 0);
+  // staging: wave wid fills rows wid*32 .. +31 of both images, 4 glds (8 rows each) per image
+  const int rl = wid * 32 + (lane >> 3), slot = lane & 7;
+  const int cq = swz(rl, slot), cq8a = cq * 8, cq8b = (cq ^ 4) * 8;
+  int bt[4], tt[4];
+  unsigned okm = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + rl + 8 * i;
+    const bool ok = m < M;
+    bt[i] = ok ? m / Tout : 0;
+    tt[i] = ok ? m - bt[i] * Tout : 0;
+    okm |= ok ? (1u << i) : 0u;
+  }
+  unsigned long long zpu = (unsigned long long)(const void*)g_zero;
+  asm volatile("" : "+s"(zpu));
+  const char* zp = (const char*)zpu;
+  const int c8[4] = {cq8a, cq8b, cq8a, cq8b};
+  int qs = 0, qj = 0, qkc = 0;
+#define TAP_PTRS(S) \
+  tap_ptrs(S, qj, Npad, n0, rl, cq8a, cq8b, bt[0], bt[1], bt[2], bt[3], tt[0], tt[1], tt[2], tt[3], okm)
+  TapPtrs P = TAP_PTRS(S0);
+#define ISSUE_BIG(it)                                                                    \
+  do {                                                                                   \
+    char* As_ = smem + ((it) & 1) * STAGE + wid * 32 * 128;                              \
+    const int kb_ = qkc * BK2;                                                           \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                      \
+      const bool oa = ((P.va >> i) & 1) && kb_ + c8[i] < P.K;                            \
+      glds16(oa ? (const void*)(P.pa[i] + kb_ * 2) : (const void*)zp, As_ + i * 1024);   \
+    }                                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                      \
+      const bool ob = kb_ + c8[i] < P.Kp;                                                \
+      glds16(ob ? (const void*)(P.pb[i] + kb_ * 2) : (const void*)zp,                    \
+             As_ + TILE_A + i * 1024);                                                   \
+    }                                                                                    \
+    const int nks_ = qs == 0 ? S0.nk : (qs == 1 ? S1.nk : S2.nk);                        \
+    const int taps_ = qs == 0 ? S0.taps : (qs == 1 ? S1.taps : S2.taps);                 \
+    if (++qkc == nks_) {                                                                 \
+      qkc = 0;                                                                           \
+      if (++qj == taps_) {                                                               \
+        qj = 0;                                                                          \
+        ++qs;                                                                            \
+      }                                                                                  \
+      if (qs < nseg) P = qs == 0 ? TAP_PTRS(S0) : (qs == 1 ? TAP_PTRS(S1) : TAP_PTRS(S2)); \
+    }                                                                                    \
+  } while (0)
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nit > 0) ISSUE_BIG(0);
+  const int arow = lane & 15, kq = lane >> 4;
+  const int ra = wr * 128 + arow, rbr = wc * 64 + arow;
+  const int oa0 = ra * 128 + swz(ra, kq) * 16, oa1 = ra * 128 + swz(ra, kq + 4) * 16;
+  const int ob0 = TILE_A + rbr * 128 + swz(rbr, kq) * 16;
+  const int ob1 = TILE_A + rbr * 128 + swz(rbr, kq + 4) * 16;
+  for (int it = 0; it < nit; ++it) {
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // tile `it` visible; every wave is done with tile it-1
+    if (it + 1 < nit) ISSUE_BIG(it + 1);
+    const char* St = smem + (it & 1) * STAGE;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = *(const bf16x8*)(St + (h ? ob1 : ob0) + j * 2048);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 fa = *(const bf16x8*)(St + (h ? oa1 : oa0) + i * 2048);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+#undef ISSUE_BIG
+#undef TAP_PTRS
+  // epilogue: four 64-row chunks staged through LDS (row stride EPB floats)
+  float* T = (float*)smem;
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < BMB / CHR; ++c) {
+    if (wr == (c >> 1)) {
+#pragma unroll
+      for (int mt2 = 0; mt2 < 4; ++mt2)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            T[(mt2 * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] =
+                acc[(c & 1) * 4 + mt2][nt][r];
+    }
+    __syncthreads();
+    epilogue_chunk_big(a, T, m0 + c * CHR, n0, tid);
+    __syncthreads();
+  }
 }
 
 // y[m][k] = bf16(x[m][k] + radd[m / T][k]) for the bf16-activation GEMM (8 elements per thread).
@@ -1348,6 +1647,11 @@ static int fill_gemm_args(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int
     a.seg[s].vec = (g.K % 4 == 0) && (g.ld % 4 == 0) && (((uintptr_t)g.x & 15) == 0) &&
                    (!g.radd || ((g.radd_ld % 4 == 0) && (((uintptr_t)g.radd & 15) == 0)));
   }
+  // epi bits 8 / 9: aux0 / aux1 hold bf16 (only the gate save and its backward read)
+  a.aux0_bf = (epi & EPI_AUX0_BF16) ? 1 : 0;
+  a.aux1_bf = (epi & EPI_AUX1_BF16) ? 1 : 0;
+  epi &= 0xff;
+  if ((a.aux0_bf && epi != EPI_GATE) || (a.aux1_bf && epi != EPI_GATE_BWD)) return ENSVS_E_ARG;
   a.nseg = nseg;
   a.Tout = Tout;
   a.M = B * Tout;
@@ -1367,7 +1671,9 @@ static int fill_gemm_args(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int
   a.alpha = alpha;
   a.C = C;
   auto al = [](const void* p, int ld) { return !p || ((((uintptr_t)p) & 15) == 0 && ld % 4 == 0); };
-  a.vec_out = al(Y, ldy) && al(aux0, ld0) && al(aux1, ld1) && (C % 4 == 0);
+  auto al8 = [](const void* p, int ld) { return !p || ((((uintptr_t)p) & 7) == 0 && ld % 4 == 0); };
+  a.vec_out = al(Y, ldy) && (a.aux0_bf ? al8(aux0, ld0) : al(aux0, ld0)) &&
+              (a.aux1_bf ? al8(aux1, ld1) : al(aux1, ld1)) && (C % 4 == 0);
   return ENSVS_OK;
 }
 
@@ -1407,6 +1713,20 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
   return ENSVS_OK;
 }
 
+// The 256 x 256 kernel takes a bf16-operand launch when it fills the chip with whole
+// tiles (>= 192 workgroups of 256 x 256), its LDS epilogue applies (16-B rows, no column
+// sums) and the padded N is a multiple of 256; ENSVS_BIG_TILE=0 disables it.
+static int g_big_tile = -1;  // -1: not read yet (ENSVS_BIG_TILE, default on)
+
+static bool use_big_tile(const GemmArgs& a) {
+  if (g_big_tile < 0) {
+    const char* e = getenv("ENSVS_BIG_TILE");
+    g_big_tile = e ? atoi(e) : 1;
+  }
+  if (!g_big_tile || a.csum || !a.vec_out || a.Npad % BNB) return false;
+  return (long long)cdiv(a.M, BMB) * (a.Npad / BNB) >= 192;
+}
+
 static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, int Npad,
                       const void* W, int stages, hipStream_t st) {
   for (int s = 0; s < nseg; ++s) {
@@ -1420,6 +1740,17 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     if ((long long)B * g.Tin * g.ld >= (1ll << 31) ||
         (long long)g.taps * Npad * g.Kp >= (1ll << 30))
       return ENSVS_E_SHAPE;
+  }
+  if (use_big_tile(a)) {
+    const size_t lb = (size_t)2 * (BMB + BNB) * BK2 * 2;  // two stages of both images
+    static const hipError_t eb = hipFuncSetAttribute((const void*)conv_gemm_b16_big_kernel,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)lb);
+    if (eb != hipSuccess) return ENSVS_E_HIP;
+    hipLaunchKernelGGL(conv_gemm_b16_big_kernel, dim3(cdiv(a.M, BMB), Npad / BNB),
+                       dim3(NTHRB), lb, st, a);
+    ENSVS_CHECK_LAUNCH();
+    return ENSVS_OK;
   }
   const size_t lds = (size_t)2 * BM * BK2 * 2;  // one stage (A + B images)
   // the LDS-staged epilogue reuses the stage buffers for the fp32 output tile
@@ -1440,6 +1771,11 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     return ENSVS_E_ARG;
   }
   ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_set_big_tile(int on) {
+  g_big_tile = on ? 1 : 0;
   return ENSVS_OK;
 }
 
@@ -1470,15 +1806,15 @@ ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, in
                                 accum, aux0, ld0, aux1, ld1, alpha, C);
   if (rc != ENSVS_OK) return rc;
   if (csum) {
-    if (!a.vec_out || a.M % BM || N % 4 || csum_ld < (epi == EPI_GATE_BWD ? 2 * C : N) ||
-        (epi != EPI_PLAIN && epi != EPI_ADDSCALE && epi != EPI_RELU_MASK &&
-         epi != EPI_GATE_BWD))
+    if (!a.vec_out || a.M % BM || N % 4 || csum_ld < (a.epi == EPI_GATE_BWD ? 2 * C : N) ||
+        (a.epi != EPI_PLAIN && a.epi != EPI_ADDSCALE && a.epi != EPI_RELU_MASK &&
+         a.epi != EPI_GATE_BWD))
       return ENSVS_E_ARG;
     a.csum = csum;
     a.csum_ld = csum_ld;
   }
   // Y may be dropped where the epilogue's other outputs are all the caller needs
-  if (!Y && !((epi == EPI_GATE && ybf) || (epi == EPI_GATE_BWD && (ybf || csum))))
+  if (!Y && !((a.epi == EPI_GATE && ybf) || (a.epi == EPI_GATE_BWD && (ybf || csum))))
     return ENSVS_E_ARG;
   if (ybf) {
     if (!a.vec_out || N % 4 || ybf_ld % 4 || ((uintptr_t)ybf & 7) ||

@@ -171,13 +171,16 @@ class DiffNet(nn.Module):
         if save:
             Zall = empty(M, L * C, device=dev)
             ZBall = empty(M, L * C, device=dev, dtype=torch.bfloat16) if b16 else None
+        # the gate/filter pre-activations the backward reads: bf16 on the bf16 path (half
+        # the epilogue's HBM writes; the backward's bf16-operand GEMMs round them anyway)
+        gdt = torch.bfloat16 if b16 else torch.float32
         for l, blk in enumerate(self.residual_layers):
             if save:
                 z = Zall[:, l * C:]
-                gf = empty(M, 2 * C, device=dev)
+                gf = empty(M, 2 * C, device=dev, dtype=gdt)
             elif z is None:
                 z = empty(M, C, device=dev)
-                gf = empty(M, 2 * C, device=dev)
+                gf = empty(M, 2 * C, device=dev, dtype=gdt)
             if b16 and l == 0:  # later blocks get x + d_l from the previous epilogue
                 xb = K.cast_bf16(x, C, C, M, radd=ds, radd_ld=L * C, T=T)
             zb = None

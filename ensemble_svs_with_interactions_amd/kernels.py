@@ -179,6 +179,12 @@ def _bf16_act_ok(segs, W, Npad, M):
     return max(s.taps for s in segs) * (Npad // 128) >= BF16_ACT["min_reuse"]
 
 
+def set_big_tile(on: bool):
+    """Route large-M bf16-operand GEMMs to the 256 x 256-tile kernel (default) or keep them
+    on the 128 x 128 kernel; both give identical bits."""
+    _lib.call("ensvs_set_big_tile", int(bool(on)))
+
+
 def gemm_dtype_is_bf16(W):
     return W.dtype == _lib.DT_BF16
 
@@ -209,6 +215,12 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
     fallback paths, which still write it)."""
     arr = (ConvSeg * len(segs))()
     Npad = segs[0].ref.Npad
+    # C-ABI epilogue flags: a bf16 gate/filter save (DiffNet production path)
+    ep = epi
+    if aux0 is not None and aux0.dtype == torch.bfloat16:
+        ep |= _lib.EPI_AUX0_BF16
+    if aux1 is not None and aux1.dtype == torch.bfloat16:
+        ep |= _lib.EPI_AUX1_BF16
     M = B * Tout
     a16 = _bf16_act_ok(segs, W, Npad, M)
     if csum is not None:
@@ -288,18 +300,18 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
         yptr = None  # only reached on the fused-epilogue path
     if ybf is not None or csum is not None:
         call("ensvs_conv_gemm_bf16a_out", ctypes.addressof(arr), len(segs), B, Tout, N,
-             Npad, W.buf.data_ptr(), bptr, yptr, ldy, epi, int(relu), int(accum), ptr(aux0),
+             Npad, W.buf.data_ptr(), bptr, yptr, ldy, ep, int(relu), int(accum), ptr(aux0),
              ld0, ptr(aux1), ld1, float(alpha), C, ptr(ybf), ybf_ld, ptr(ybf_radd),
              ybf_radd_ld, None if csum is None else csum.data_ptr() + 4 * csum_off, csum_ld,
              BF16_ACT["stages"], stream())
         return
     if a16:
         call("ensvs_conv_gemm_bf16a", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,
-             W.buf.data_ptr(), bptr, yptr, ldy, epi, int(relu), int(accum),
+             W.buf.data_ptr(), bptr, yptr, ldy, ep, int(relu), int(accum),
              ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, BF16_ACT["stages"], stream())
     else:
         call("ensvs_conv_gemm", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,
-             W.buf.data_ptr(), W.dtype, bptr, yptr, ldy, epi, int(relu),
+             W.buf.data_ptr(), W.dtype, bptr, yptr, ldy, ep, int(relu),
              int(accum), ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, stream())
 
 

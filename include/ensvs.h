@@ -22,7 +22,10 @@ enum { ENSVS_STATUS_OK = 0, ENSVS_STATUS_E_SHAPE = 1, ENSVS_STATUS_E_DTYPE = 2,
 enum { ENSVS_PAD_ZERO = 0, ENSVS_PAD_REFLECT = 1, ENSVS_PAD_REPLICATE = 2 };
 enum { ENSVS_DT_F32 = 0, ENSVS_DT_BF16 = 1 };
 enum { ENSVS_EPI_PLAIN = 0, ENSVS_EPI_GATE = 1, ENSVS_EPI_RESSKIP = 2, ENSVS_EPI_GATE_BWD = 3,
-       ENSVS_EPI_ADDSCALE = 4, ENSVS_EPI_RELU_MASK = 5, ENSVS_EPI_GATE_TS = 6 };
+       ENSVS_EPI_ADDSCALE = 4, ENSVS_EPI_RELU_MASK = 5, ENSVS_EPI_GATE_TS = 6,
+       /* flags or-ed into `epi`: the DiffNet gate/filter save in bf16 (GATE writes aux0,
+        * GATE_BWD reads aux1 as bf16 rows; the production bf16 path) */
+       ENSVS_EPI_AUX0_BF16 = 256, ENSVS_EPI_AUX1_BF16 = 512 };
 
 /* One K-segment of the implicit-GEMM activation operand. */
 typedef struct ensvs_conv_seg {
@@ -63,6 +66,10 @@ int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N
  * K multiples of 8, 16-B aligned, radd and pd NULL) -- ensvs_cast_bf16 output, which
  * holds the rounding ensvs_conv_gemm applies while staging, so both give identical bits.
  * Operands are staged by global_load_lds, `stages` (2 or 3) 64-deep K tiles.  wdtype is bf16. */
+/* Large-M bf16-operand launches (>= 192 tiles of 256 x 256, padded N % 256 == 0, no column
+ * sums) run a 256 x 256-tile kernel with the same accumulation order (bitwise equal);
+ * on = 0 keeps the 128 x 128 kernel (default: ENSVS_BIG_TILE, else on). */
+int ensvs_set_big_tile(int on);
 int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N, int Npad,
                           const void* W, const float* bias, float* Y, int ldy, int epi, int relu,
                           int accum, float* aux0, int ld0, const float* aux1, int ld1, float alpha,

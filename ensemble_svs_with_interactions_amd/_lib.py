@@ -21,6 +21,7 @@ PAD_ZERO, PAD_REFLECT, PAD_REPLICATE = 0, 1, 2
 DT_F32, DT_BF16 = 0, 1
 EPI_PLAIN, EPI_GATE, EPI_RESSKIP, EPI_GATE_BWD, EPI_ADDSCALE, EPI_RELU_MASK = 0, 1, 2, 3, 4, 5
 EPI_GATE_TS = 6
+EPI_NONE = 7  # measurement only: the GEMM main loop without any output
 EPI_AUX0_BF16, EPI_AUX1_BF16 = 256, 512  # flags or-ed into epi (include/ensvs.h)
 ACT_RELU, ACT_SIGMOID = 1, 2
 
@@ -56,7 +57,7 @@ SIGNATURES = {
     "ensvs_conv_gemm_bf16a_out": [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                                   c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_float,
                                   c_int, c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_vp],
-    "ensvs_set_big_tile": [c_int],
+    "ensvs_set_big_tile": [c_int, c_int],
     "ensvs_tile_colsum": [c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "ensvs_cast_bf16": [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_int, c_vp, c_int, c_vp],
     "ensvs_conv_wgrad": [c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,

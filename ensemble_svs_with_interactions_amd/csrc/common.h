@@ -50,4 +50,23 @@ __device__ __forceinline__ int pad_src(int s, int n, int mode) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
+// Fast gated-activation math for GEMM epilogues: hardware v_exp_f32 / v_rcp_f32 (about
+// 1 ulp each) instead of IEEE division and libm tanhf (the DiffNet gate epilogue was
+// VALU-bound on them).  tanh uses an odd polynomial below |x| = 1/16, where (1 - e)/(1 + e)
+// would cancel, and saturates past |x| = 15.
+__device__ __forceinline__ float fexpn_(float x) {  // exp(-x)
+  return __builtin_amdgcn_exp2f(-1.44269504088896341f * x);
+}
+__device__ __forceinline__ float fsigmoid_(float x) {
+  return __builtin_amdgcn_rcpf(1.f + fexpn_(x));
+}
+__device__ __forceinline__ float ftanh_(float x) {
+  const float xc = fminf(fmaxf(x, -15.f), 15.f);
+  const float e = fexpn_(2.f * xc);
+  const float big = (1.f - e) * __builtin_amdgcn_rcpf(1.f + e);
+  const float x2 = x * x;
+  const float small = x * (1.f + x2 * (-0.333333333f + x2 * 0.133333333f));
+  return fabsf(x) < 0.0625f ? small : big;
+}
+
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }

@@ -32,6 +32,7 @@ enum {
   EPI_ADDSCALE = 4,  // Y = alpha * aux1 + acc + bias
   EPI_RELU_MASK = 5, // Y = (accum ? Y : 0) + (aux1 > 0 ? acc + bias : 0)   (ReLU backward)
   EPI_GATE_TS = 6,   // uSFGAN: xa/xb interleaved by 16 -> z = tanh(xa)*sigmoid(xb)
+  EPI_NONE = 7,      // measurement only (tools/gate_probe.py): no output at all
   EPI_AUX0_BF16 = 256,  // flag: GATE writes its gate/filter save (aux0) in bf16
   EPI_AUX1_BF16 = 512,  // flag: GATE_BWD reads the gate/filter save (aux1) in bf16
 };
@@ -144,7 +145,7 @@ __device__ __forceinline__ void xcd_tile(int& m0, int& n0) {
 // LDS-staged epilogues round identically.
 __device__ __forceinline__ void gate_bwd_(float dz, float g, float f, float& dg, float& df) {
 #pragma clang fp contract(off)
-  const float sg = sigmoidf_(g), th = tanhf(f);
+  const float sg = fsigmoid_(g), th = ftanh_(f);
   dg = dz * th * sg * (1.f - sg);
   df = dz * sg * (1.f - th * th);
 }
@@ -173,6 +174,10 @@ __device__ __forceinline__ f32x4 ld4_aux1(const GemmArgs& a, long long i) {
 
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], int m0,
                                               int n0, int wr, int wc, int lane) {
+  if (a.epi == EPI_NONE) {  // keep the accumulators live: one impossible store
+    if (acc[0][0][0] == 12345.678f && m0 < 0) a.Y[0] = acc[3][3][3];
+    return;
+  }
   const int rbase = m0 + wr * 64 + (lane >> 4) * 4;
   if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
 #pragma unroll
@@ -193,9 +198,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4 (&acc)[4]
           if (a.epi == EPI_GATE) {
             st_aux0(a, (long long)row * a.ld0 + c, v0);
             st_aux0(a, (long long)row * a.ld0 + a.C + c, v1);
-            a.Y[(long long)row * a.ldy + c] = sigmoidf_(v0) * tanhf(v1);
+            a.Y[(long long)row * a.ldy + c] = fsigmoid_(v0) * ftanh_(v1);
           } else if (a.epi == EPI_GATE_TS) {
-            a.Y[(long long)row * a.ldy + c] = tanhf(v0) * sigmoidf_(v1);
+            a.Y[(long long)row * a.ldy + c] = ftanh_(v0) * fsigmoid_(v1);
           } else {
             const float xr = a.aux1[(long long)row * a.ld1 + c];
             a.Y[(long long)row * a.ldy + c] = (xr + v0) * 0.70710678118654752f;
@@ -264,6 +269,10 @@ __device__ __forceinline__ void shadow4(const GemmArgs& a, int m, int col, f32x4
 __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[4][4], int m0,
                                                   int n0, int wr, int wc, int lane, int tid,
                                                   char* smem) {
+  if (a.epi == EPI_NONE) {
+    gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
+    return;
+  }
   float* T = (float*)smem;
   __syncthreads();  // every wave is done with the K-loop images
 #pragma unroll
@@ -298,13 +307,13 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         st4_aux0(a, (long long)m * a.ld0 + a.C + c, f);
         f32x4 z;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) z[e] = sigmoidf_(g[e]) * tanhf(f[e]);
+        for (int e = 0; e < 4; ++e) z[e] = fsigmoid_(g[e]) * ftanh_(f[e]);
         if (a.Y) st4(a.Y + (long long)m * a.ldy + c, z);
         shadow4(a, m, c, z);
       } else if (a.epi == EPI_GATE_TS) {
         f32x4 z;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) z[e] = tanhf(g[e]) * sigmoidf_(f[e]);
+        for (int e = 0; e < 4; ++e) z[e] = ftanh_(g[e]) * fsigmoid_(f[e]);
         st4(a.Y + (long long)m * a.ldy + c, z);
       } else {
         const f32x4 xr = ld4(a.aux1 + (long long)m * a.ld1 + c);
@@ -818,20 +827,25 @@ __global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a
     // (both 32-halves always: a zero half adds exact zeros, and a data-dependent skip
     // makes hipcc move the accumulators out of AGPRs every iteration)
     const char* St = smem + (it % STAGES) * 2 * TILE;
+    // all 16 fragment reads of the K step first, then its 32 MFMAs: the scheduler would
+    // otherwise sink each read next to its first MFMA behind an lgkmcnt(0) wait
+    bf16x8 fa[2][4], fb[2][4];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      bf16x8 fa[4], fb[4];
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        fa[i] = *(const bf16x8*)(St + (h ? oa1 : oa0) + i * 2048);
-        fb[i] = *(const bf16x8*)(St + (h ? ob1 : ob0) + i * 2048);
+        fa[h][i] = *(const bf16x8*)(St + (h ? oa1 : oa0) + i * 2048);
+        fb[h][i] = *(const bf16x8*)(St + (h ? ob1 : ob0) + i * 2048);
       }
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // DS reads
+    __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);  // MFMAs
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[h][i], fb[h][j], acc[i][j], 0, 0, 0);
   }
 #undef ISSUE
 #undef TAP_PTRS
@@ -865,6 +879,10 @@ __device__ __forceinline__ void xcd_tile_big(int& m0, int& n0) {
 __device__ __forceinline__ void epilogue_chunk_big(const GemmArgs& a, const float* T, int mb,
                                                    int n0, int tid) {
   const int M = a.M;
+  if (a.epi == EPI_NONE) {
+    if (T[tid] == 12345.678f && mb < 0) a.Y[0] = T[tid + 1];
+    return;
+  }
   if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
     // BNB / 2 output channels per row: gate/filter interleaved by 16 in the packed columns
     for (int it = tid; it < CHR * (BNB / 8); it += NTHRB) {
@@ -887,13 +905,13 @@ __device__ __forceinline__ void epilogue_chunk_big(const GemmArgs& a, const floa
         st4_aux0(a, (long long)m * a.ld0 + a.C + c, f);
         f32x4 z;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) z[e] = sigmoidf_(g[e]) * tanhf(f[e]);
+        for (int e = 0; e < 4; ++e) z[e] = fsigmoid_(g[e]) * ftanh_(f[e]);
         if (a.Y) st4(a.Y + (long long)m * a.ldy + c, z);
         shadow4(a, m, c, z);
       } else if (a.epi == EPI_GATE_TS) {
         f32x4 z;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) z[e] = tanhf(g[e]) * sigmoidf_(f[e]);
+        for (int e = 0; e < 4; ++e) z[e] = ftanh_(g[e]) * fsigmoid_(f[e]);
         st4(a.Y + (long long)m * a.ldy + c, z);
       } else {
         const f32x4 xr = ld4(a.aux1 + (long long)m * a.ld1 + c);
@@ -1076,16 +1094,18 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_big_kernel(const GemmArgs
     const char* St = smem + (it & 1) * STAGE;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      bf16x8 fb[4];
+      bf16x8 fa[8], fb[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) fb[j] = *(const bf16x8*)(St + (h ? ob1 : ob0) + j * 2048);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bf16x8 fa = *(const bf16x8*)(St + (h ? oa1 : oa0) + i * 2048);
+      for (int i = 0; i < 8; ++i) fa[i] = *(const bf16x8*)(St + (h ? oa1 : oa0) + i * 2048);
+      __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // DS reads first
+      __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);  // then the MFMAs
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[j], acc[i][j], 0, 0, 0);
-      }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
   }
 #undef ISSUE_BIG
@@ -1107,6 +1127,174 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_big_kernel(const GemmArgs
     }
     __syncthreads();
     epilogue_chunk_big(a, T, m0 + c * CHR, n0, tid);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------- 256 x 256, 32-deep K steps, S-stage ring
+// Measured on the gate GEMM (tools/gate_probe.py, rocprofv3 PMC): the 64-deep two-stage
+// kernels above wait on their LDS-DMA loads (SQ_WAIT_ANY 45 % of wave cycles, MFMA busy
+// 21 %) at ~18 GB/s per CU -- the rate that 64 KB in flight per CU sustains at ~3.5 us
+// of load latency under full-chip load, for both tile shapes.  Throughput follows bytes
+// in flight, so this kernel keeps S - 1 32-deep stages of both operand images in flight
+// (S = 5: 128 KB of 160 KB LDS) with the 256 x 256 tile's L2 -> LDS bytes per FLOP.
+// 64-B LDS rows: the 16-B chunk c of row r sits in slot c ^ ((r >> 1) & 3), conflict-free
+// for the MFMA fragment reads (ds_read_b128 lane groups, MI355X_MICROARCH.md §LDS); the
+// DMA writes stay lane-linear, each lane fetching the chunk its slot holds.
+constexpr int BK3 = 32;
+
+template <int N>
+__device__ __forceinline__ void wait_vm_n() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+}
+
+struct TapPtrs2 {
+  const char* pa[2];
+  const char* pb[2];
+  unsigned va;
+  int K, Kp;
+};
+
+__device__ __forceinline__ TapPtrs2 tap_ptrs2(const SegU S, int j, int Npad, int n0, int r0,
+                                              int c8, const int b0, const int b1, const int t0,
+                                              const int t1, unsigned okm) {
+  TapPtrs2 P;
+  const int bt[2] = {b0, b1}, tt[2] = {t0, t1};
+  const int shj = S.shift0 + j * S.dil;
+  P.va = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ts = tt[i] + shj;
+    const int src = S.pad == PAD_ZERO ? ((unsigned)ts < (unsigned)S.Tin ? ts : -1)
+                                      : pad_src(ts, S.Tin, S.pad);
+    const bool ok = ((okm >> i) & 1) && src >= 0;
+    P.va |= ok ? (1u << i) : 0u;
+    P.pa[i] = (const char*)(S.x + (unsigned)((bt[i] * S.Tin + (ok ? src : 0)) * S.ld + c8));
+    P.pb[i] = S.w + ((unsigned)((j * Npad + n0 + r0 + 16 * i) * S.Kp + c8)) * 2;
+  }
+  P.K = S.K;
+  P.Kp = S.Kp;
+  return P;
+}
+
+template <int STAGES>
+__global__ __launch_bounds__(NTHRB) void conv_gemm_b16_ring_kernel(const GemmArgs a) {
+  static_assert(STAGES >= 3 && STAGES <= 5, "stages");
+  constexpr int IMG = BMB * BK3 * 2;   // 16 KB: one operand image of one stage
+  constexpr int STAGE = 2 * IMG;
+  constexpr int GL = 4;                // glds per thread per stage (2 A rows + 2 B rows)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  int m0, n0;
+  xcd_tile_big(m0, n0);
+  const int M = a.M, Tout = a.Tout, Npad = a.Npad;
+  const int nseg = a.nseg;
+  const SegU S0 = seg_u(a.seg[0], a.W);
+  const SegU S1 = nseg > 1 ? seg_u(a.seg[1], a.W) : S0;
+  const SegU S2 = nseg > 2 ? seg_u(a.seg[2], a.W) : S0;
+  auto nk3 = [](const SegU& S) { return (S.K + BK3 - 1) / BK3; };
+  const int k0 = uni(nk3(S0)), k1 = uni(nk3(S1)), k2 = uni(nk3(S2));
+  const int nit = k0 * S0.taps + (nseg > 1 ? k1 * S1.taps : 0) + (nseg > 2 ? k2 * S2.taps : 0);
+  // staging: wave wid fills the 1-KB pieces 2*wid and 2*wid + 1 (16 rows each) of both
+  // images: rows r0 = 32*wid + lane/4 and r0 + 16; lane slot lane & 3 holds chunk c
+  const int r0 = wid * 32 + (lane >> 2);
+  const int c = (lane & 3) ^ (((lane >> 2) >> 1) & 3), c8 = c * 8;
+  int bt[2], tt[2];
+  unsigned okm = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + r0 + 16 * i;
+    const bool ok = m < M;
+    bt[i] = ok ? m / Tout : 0;
+    tt[i] = ok ? m - bt[i] * Tout : 0;
+    okm |= ok ? (1u << i) : 0u;
+  }
+  unsigned long long zpu = (unsigned long long)(const void*)g_zero;
+  asm volatile("" : "+s"(zpu));
+  const char* zp = (const char*)zpu;
+  int qs = 0, qj = 0, qkc = 0;
+#define TAP_PTRS2(S) tap_ptrs2(S, qj, Npad, n0, r0, c8, bt[0], bt[1], tt[0], tt[1], okm)
+  TapPtrs2 P = TAP_PTRS2(S0);
+#define ISSUE_RING(it)                                                                   \
+  do {                                                                                   \
+    char* As_ = smem + ((it) % STAGES) * STAGE + wid * 2048;                             \
+    const int kb_ = qkc * BK3;                                                           \
+    const bool in_ = kb_ + c8 < P.K, inb_ = kb_ + c8 < P.Kp;                             \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                      \
+      const bool oa = ((P.va >> i) & 1) && in_;                                          \
+      glds16(oa ? (const void*)(P.pa[i] + kb_ * 2) : (const void*)zp, As_ + i * 1024);   \
+    }                                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                        \
+      glds16(inb_ ? (const void*)(P.pb[i] + kb_ * 2) : (const void*)zp,                  \
+             As_ + IMG + i * 1024);                                                      \
+    const int nks_ = qs == 0 ? k0 : (qs == 1 ? k1 : k2);                                 \
+    const int taps_ = qs == 0 ? S0.taps : (qs == 1 ? S1.taps : S2.taps);                 \
+    if (++qkc == nks_) {                                                                 \
+      qkc = 0;                                                                           \
+      if (++qj == taps_) {                                                               \
+        qj = 0;                                                                          \
+        ++qs;                                                                            \
+      }                                                                                  \
+      if (qs < nseg) P = qs == 0 ? TAP_PTRS2(S0) : (qs == 1 ? TAP_PTRS2(S1) : TAP_PTRS2(S2)); \
+    }                                                                                    \
+  } while (0)
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int p = 0; p < STAGES - 1; ++p)
+    if (p < nit) ISSUE_RING(p);
+  const int arow = lane & 15, kq = lane >> 4;
+  const int sw = (kq ^ ((arow >> 1) & 3)) * 16;  // rows + 16 i keep the slot
+  const int oa = (wr * 128 + arow) * 64 + sw, ob = IMG + (wc * 64 + arow) * 64 + sw;
+  for (int it = 0; it < nit; ++it) {
+    const int ahead = min(STAGES - 2, nit - 1 - it);  // stages issued after tile `it`
+    if (ahead >= 3) wait_vm_n<3 * GL>();
+    else if (ahead == 2) wait_vm_n<2 * GL>();
+    else if (ahead == 1) wait_vm_n<GL>();
+    else wait_vm_n<0>();
+    __builtin_amdgcn_s_barrier();  // tile `it` visible; every wave is done with tile it-1
+    if (it + STAGES - 1 < nit) ISSUE_RING(it + STAGES - 1);
+    const char* St = smem + (it % STAGES) * STAGE;
+    bf16x8 fa[8], fb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = *(const bf16x8*)(St + ob + j * 1024);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = *(const bf16x8*)(St + oa + i * 1024);
+    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  }
+#undef ISSUE_RING
+#undef TAP_PTRS2
+  float* T = (float*)smem;
+  __syncthreads();
+#pragma unroll
+  for (int cch = 0; cch < BMB / CHR; ++cch) {
+    if (wr == (cch >> 1)) {
+#pragma unroll
+      for (int mt2 = 0; mt2 < 4; ++mt2)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            T[(mt2 * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] =
+                acc[(cch & 1) * 4 + mt2][nt][r];
+    }
+    __syncthreads();
+    epilogue_chunk_big(a, T, m0 + cch * CHR, n0, tid);
     __syncthreads();
   }
 }
@@ -1716,12 +1904,18 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
 // The 256 x 256 kernel takes a bf16-operand launch when it fills the chip with whole
 // tiles (>= 192 workgroups of 256 x 256), its LDS epilogue applies (16-B rows, no column
 // sums) and the padded N is a multiple of 256; ENSVS_BIG_TILE=0 disables it.
-static int g_big_tile = -1;  // -1: not read yet (ENSVS_BIG_TILE, default on)
+// -1: not read yet (ENSVS_BIG_TILE, default 2): 0 off, 1 the 32-deep ring kernel with
+// g_big_stages stages (ENSVS_BIG_STAGES, default 5), 2 the 64-deep two-stage kernel.
+// Gate GEMM (tools/gate_probe.py): 2 -> 44.8 us, 1 (5 / 4 / 3 stages) -> 53.3 / 53.0 /
+// 50.2 us, 0 (128 x 128) -> 51.0 us: more LDS stages in flight did not pay.
+static int g_big_tile = -1, g_big_stages = 5;
 
 static bool use_big_tile(const GemmArgs& a) {
   if (g_big_tile < 0) {
     const char* e = getenv("ENSVS_BIG_TILE");
-    g_big_tile = e ? atoi(e) : 1;
+    g_big_tile = e ? atoi(e) : 2;
+    const char* s = getenv("ENSVS_BIG_STAGES");
+    if (s) g_big_stages = atoi(s);
   }
   if (!g_big_tile || a.csum || !a.vec_out || a.Npad % BNB) return false;
   return (long long)cdiv(a.M, BMB) * (a.Npad / BNB) >= 192;
@@ -1742,13 +1936,30 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
       return ENSVS_E_SHAPE;
   }
   if (use_big_tile(a)) {
-    const size_t lb = (size_t)2 * (BMB + BNB) * BK2 * 2;  // two stages of both images
-    static const hipError_t eb = hipFuncSetAttribute((const void*)conv_gemm_b16_big_kernel,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)lb);
-    if (eb != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(conv_gemm_b16_big_kernel, dim3(cdiv(a.M, BMB), Npad / BNB),
-                       dim3(NTHRB), lb, st, a);
+    const dim3 grid_b(cdiv(a.M, BMB), Npad / BNB);
+    if (g_big_tile == 2) {
+      const size_t lb = (size_t)2 * (BMB + BNB) * BK2 * 2;  // two stages of both images
+      static const hipError_t eb = hipFuncSetAttribute(
+          (const void*)conv_gemm_b16_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+          (int)lb);
+      if (eb != hipSuccess) return ENSVS_E_HIP;
+      hipLaunchKernelGGL(conv_gemm_b16_big_kernel, grid_b, dim3(NTHRB), lb, st, a);
+    } else {
+#define RING(S)                                                                           \
+  do {                                                                                    \
+    const size_t lr = std::max<size_t>((size_t)(S) * 2 * BMB * BK3 * 2,                   \
+                                       (size_t)CHR * EPB * 4);                            \
+    static const hipError_t er = hipFuncSetAttribute(                                     \
+        (const void*)conv_gemm_b16_ring_kernel<S>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+        (int)lr);                                                                         \
+    if (er != hipSuccess) return ENSVS_E_HIP;                                             \
+    hipLaunchKernelGGL(conv_gemm_b16_ring_kernel<S>, grid_b, dim3(NTHRB), lr, st, a);     \
+  } while (0)
+      if (g_big_stages == 3) RING(3);
+      else if (g_big_stages == 4) RING(4);
+      else RING(5);
+#undef RING
+    }
     ENSVS_CHECK_LAUNCH();
     return ENSVS_OK;
   }
@@ -1774,8 +1985,10 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
   return ENSVS_OK;
 }
 
-ENSVS_API int ensvs_set_big_tile(int on) {
-  g_big_tile = on ? 1 : 0;
+ENSVS_API int ensvs_set_big_tile(int mode, int stages) {
+  if (mode < 0 || mode > 2 || (stages != 0 && (stages < 3 || stages > 5))) return ENSVS_E_ARG;
+  g_big_tile = mode;
+  if (stages) g_big_stages = stages;
   return ENSVS_OK;
 }
 

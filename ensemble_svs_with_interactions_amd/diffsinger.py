@@ -173,7 +173,7 @@ class DiffNet(nn.Module):
             ZBall = empty(M, L * C, device=dev, dtype=torch.bfloat16) if b16 else None
         # the gate/filter pre-activations the backward reads: bf16 on the bf16 path (half
         # the epilogue's HBM writes; the backward's bf16-operand GEMMs round them anyway)
-        gdt = torch.bfloat16 if b16 else torch.float32
+        gdt = torch.bfloat16 if K.gemm_dtype_is_bf16(pk.fwd) else torch.float32
         for l, blk in enumerate(self.residual_layers):
             if save:
                 z = Zall[:, l * C:]

@@ -179,10 +179,11 @@ def _bf16_act_ok(segs, W, Npad, M):
     return max(s.taps for s in segs) * (Npad // 128) >= BF16_ACT["min_reuse"]
 
 
-def set_big_tile(on: bool):
-    """Route large-M bf16-operand GEMMs to the 256 x 256-tile kernel (default) or keep them
-    on the 128 x 128 kernel; both give identical bits."""
-    _lib.call("ensvs_set_big_tile", int(bool(on)))
+def set_big_tile(mode, stages=0):
+    """Route large-M bf16-operand GEMMs to a 256 x 256-tile kernel (mode 2: 64-deep
+    two-stage, the default; 1: 32-deep LDS ring of `stages` stages) or keep them on the
+    128 x 128 kernel (0 / False); all give identical bits."""
+    _lib.call("ensvs_set_big_tile", int(mode), int(stages))
 
 
 def gemm_dtype_is_bf16(W):

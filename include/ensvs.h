@@ -67,9 +67,11 @@ int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N
  * holds the rounding ensvs_conv_gemm applies while staging, so both give identical bits.
  * Operands are staged by global_load_lds, `stages` (2 or 3) 64-deep K tiles.  wdtype is bf16. */
 /* Large-M bf16-operand launches (>= 192 tiles of 256 x 256, padded N % 256 == 0, no column
- * sums) run a 256 x 256-tile kernel with the same accumulation order (bitwise equal);
- * on = 0 keeps the 128 x 128 kernel (default: ENSVS_BIG_TILE, else on). */
-int ensvs_set_big_tile(int on);
+ * sums) run a 256 x 256-tile kernel with the same accumulation order (bitwise equal).
+ * mode 0: keep the 128 x 128 kernel; 1: 32-deep K steps on a `stages`-deep LDS ring
+ * (3..5; 0 keeps the current count); 2: 64-deep two-stage kernel.  Defaults: ENSVS_BIG_TILE
+ * (2), ENSVS_BIG_STAGES (5). */
+int ensvs_set_big_tile(int mode, int stages);
 int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N, int Npad,
                           const void* W, const float* bias, float* Y, int ldy, int epi, int relu,
                           int accum, float* aux0, int ld0, const float* aux1, int ld1, float alpha,

@@ -21,15 +21,16 @@ def _pack(ws):
     return pb, refs
 
 
-def _both(run):
+def _both(run, mode=2, stages=0):
+    """run() on the 128 x 128 kernel, then on the 256 x 256 kernel `mode` / `stages`."""
     outs = []
     try:
-        for big in (False, True):
-            K.set_big_tile(big)
+        for m, st in ((0, 0), (mode, stages)):
+            K.set_big_tile(m, st)
             outs.append(run())
             torch.cuda.synchronize()
     finally:
-        K.set_big_tile(True)
+        K.set_big_tile(2, 5)
     return outs
 
 
@@ -42,6 +43,16 @@ def _bf(t):
                                  L.EPI_RELU_MASK])
 @pytest.mark.parametrize("B,T", [(30, 1024), (30, 1000)])
 def test_big_tile_epilogues_bitwise(epi, B, T):
+    _epilogue_case(epi, B, T, 2, 0)
+
+
+@pytest.mark.parametrize("mode,stages", [(1, 3), (1, 4), (1, 5)])
+def test_big_tile_variants_bitwise(mode, stages):
+    _epilogue_case("gate_bf16", 30, 1000, mode, stages)
+    _epilogue_case(L.EPI_RESSKIP, 30, 1024, mode, stages)
+
+
+def _epilogue_case(epi, B, T, mode, stages):
     torch.manual_seed(11)
     C, E = 256, 256
     M = B * T
@@ -77,12 +88,12 @@ def test_big_tile_epilogues_bitwise(epi, B, T):
             kw = dict(epi=L.EPI_GATE_BWD, aux1=a1, ld1=N, C=C, ybf=ybf, ybf_ld=N)
             Nn = C
         elif epi == L.EPI_ADDSCALE:
-            kw = dict(epi=epi, aux1=aux1, ld1=N, alpha=0.25, ybf=ybf, ybf_ld=N)
+            kw = dict(epi=epi, aux1=aux1, ld1=N, alpha=0.25, relu=True)
         else:
             kw = dict(epi=epi, aux1=aux1, ld1=N, accum=True)
         K.gemm(segs, B, T, Nn, pb, y, N, **kw)
         return y, aux0, ybf
-    (y0, a0, b0), (y1, a1_, b1) = _both(run)
+    (y0, a0, b0), (y1, a1_, b1) = _both(run, mode, stages)
     assert torch.equal(y0, y1)
     assert torch.equal(a0, a1_)
     assert torch.equal(b0, b1)
@@ -93,7 +104,7 @@ def test_big_tile_three_segments_reflect():
     torch.manual_seed(5)
     B, T = 40, 1024
     M = B * T
-    specs = [(128, 7, 1, L.PAD_REFLECT), (64, 1, 1, L.PAD_ZERO), (32, 3, 2, L.PAD_REPLICATE)]
+    specs = [(128, 7, 1, L.PAD_REFLECT), (40, 1, 1, L.PAD_ZERO), (72, 3, 2, L.PAD_REPLICATE)]
     xs, ws = [], []
     N = 768
     for (Kc, taps, dil, pad) in specs:

@@ -142,10 +142,29 @@ SIGNATURES = {
                              c_int, c_vp, c_vp],
     "ensvs_masked_mean": [c_vp, c_vp, c_ll, c_vp, c_vp, c_vp],
     "ensvs_masked_mean_bwd": [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp],
+    "ensvs_bgemm": [c_vp, c_ll, c_ll, c_ll, c_ll, c_vp, c_ll, c_ll, c_ll, c_ll, c_vp, c_ll, c_ll,
+                    c_ll, c_ll, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_vp],
+    "ensvs_div": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_float, c_vp],
+    "ensvs_attn_softmax": [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
+                           c_vp, c_vp, c_vp],
+    "ensvs_attn_relv": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "ensvs_attn_band_dot": [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "ensvs_attn_table_grad_workspace": [c_int, c_int],
+    "ensvs_attn_table_grad": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
+                              c_int, c_vp],
+    "ensvs_attn_softmax_bwd": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],
+    "ensvs_attn_band_rows": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "ensvs_mask_rows": [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "ensvs_stride_rows": [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                          c_vp],
+    "ensvs_dwdown_fwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "ensvs_dwdown_bwd": [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int,
+                         c_int, c_vp],
 }
 
 # entry points returning a value instead of a status code
-RESTYPES = {"ensvs_embed_bwd_workspace": c_ll, "ensvs_usf_source_workspace": c_ll}
+RESTYPES = {"ensvs_embed_bwd_workspace": c_ll, "ensvs_usf_source_workspace": c_ll,
+            "ensvs_attn_table_grad_workspace": c_ll}
 
 _lib = None
 

@@ -32,6 +32,7 @@ REFERENCE_TARGETS = {
         "nnsvs.usfgan.models.generator.ParallelHnUSFGANGenerator",
     f"{PKG}.timing.MultiTrackVariancePredictor": "nnsvs.model.MultiTrackVariancePredictor",
     f"{PKG}.timing.MDN": "nnsvs.model.MDN",
+    f"{PKG}.transformer.TransformerEncoder": "nnsvs.model.TransformerEncoder",
 }
 
 

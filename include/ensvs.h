@@ -342,6 +342,54 @@ int ensvs_masked_mean(const float* x, const unsigned char* mask, long long n, fl
 int ensvs_masked_mean_bwd(const unsigned char* mask, long long n, const float* gout,
                           const float* fwd_out, float* dx, void* stream);
 
+/* ---- Transformer encoder (model.py:1540-1671, transformer/encoder.py:82-142,
+ * transformer/attentions.py:22-214; attention.hip).  Replaces MultiHeadAttention.attention's
+ * torch.matmul / softmax / relative-position reshapes (attentions.py:86-135) and their
+ * autograd.  Q / K / V are frame rows [(b*T + t)*ld + h*dk + d]; scores [(b*H + h)][T][T]. */
+/* Batched fp32 GEMM C[z](m,n) (=|+=) alpha sum_k A[z](m,k) B[z](k,n), z = zb*H + zh, every
+ * operand addressed base + zb*sb + zh*sh + row*sr + col*sc (the per-head score / context
+ * products and their transposes). */
+int ensvs_bgemm(const float* a, long long asb, long long ash, long long asr, long long asc,
+                const float* b, long long bsb, long long bsh, long long bsr, long long bsc,
+                float* c, long long csb, long long csh, long long csr, long long csc, int Bn,
+                int H, int M, int N, int K, float alpha, int accum, void* stream);
+/* y = x / s (the query scaling query / sqrt(k_channels), attentions.py:93). */
+int ensvs_div(const float* x, int ldx, float* y, int ldy, long long M, int C, float s,
+              void* stream);
+/* S += relative-key logits qs_i . ek[j-i+w] (|j-i| <= w), masked_fill(-1e4) where i or j is
+ * past the length, softmax over j in place; keep (dropout keep-mask, scaled) -> Pd = P*keep. */
+int ensvs_attn_softmax(float* S, const float* qs, int ldq, const float* ek,
+                       const long long* lens, int B, int H, int T, int dk, int w,
+                       const float* keep, float* Pd, void* stream);
+/* O += sum_{|j-i|<=w} P[i][j] ev[j-i+w] (_matmul_with_relative_values, attentions.py:124-131) */
+int ensvs_attn_relv(const float* P, const float* ev, float* O, int ldo, int B, int H, int T,
+                    int dk, int w, void* stream);
+/* D[row][i+r-w] += vec_i . tab[r] (band of dO ev^T in the backward) */
+int ensvs_attn_band_dot(float* D, const float* vec, int ldv, const float* tab, int B, int H,
+                        int T, int dk, int w, void* stream);
+long long ensvs_attn_table_grad_workspace(int dk, int w);
+/* out[r][d] (+)= sum over rows A[row][i+r-w] X_i[d]: emb_rel_v / emb_rel_k gradients */
+int ensvs_attn_table_grad(const float* A, const float* X, int ldx, int B, int H, int T, int dk,
+                          int w, float* part, float* out, int accum, void* stream);
+/* in place dS = P (dPd*keep - sum_j P dPd*keep), 0 at masked scores */
+int ensvs_attn_softmax_bwd(float* dS, const float* P, const float* keep, const long long* lens,
+                           int B, int H, int T, void* stream);
+/* out_i += sum_r A[row][i+r-w] tab[r] (relative-key part of dQ) */
+int ensvs_attn_band_rows(const float* A, const float* tab, float* out, int ldo, int B, int H,
+                         int T, int dk, int w, void* stream);
+/* y = x * x_mask (sequence_mask of lengths over frame rows; y may alias x) */
+int ensvs_mask_rows(const float* x, int ldx, float* y, int ldy, int B, int T, int C,
+                    const long long* lens, void* stream);
+/* x[:, off::r] (bwd = 0) / its scatter-back with zeros (bwd = 1), model.py:1660 */
+int ensvs_stride_rows(const float* x, int ldx, float* y, int ldy, int B, int T, int C, int r,
+                      int off, int bwd, void* stream);
+/* conv_downsample: depthwise Conv1d(C, C, r, stride=r, groups=C) (model.py:1610-1617), and
+ * its backward: dx, and prod[b*Tp+tp][c*r+k] = dy*x whose column sums are dw. */
+int ensvs_dwdown_fwd(const float* x, int ldx, const float* w, const float* bias, float* y,
+                     int ldy, int B, int T, int C, int r, void* stream);
+int ensvs_dwdown_bwd(const float* dy, int ldy, const float* x, int ldx, const float* w,
+                     float* dx, int lddx, float* prod, int B, int T, int C, int r, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -603,3 +603,95 @@ def pad_inference_lengths(lengths, r):
     mod = max(lengths) % r
     pad = r - mod
     return pad, [int(v) + pad for v in lengths]
+
+
+# ---------------------------------------------------- Transformer encoder (row a14)
+
+def rel_attention(q, k, v, ek, ev, lengths, w, keep=None):
+    """nnsvs/transformer/attentions.py:86-135 restated with an explicit band: q, k, v
+    (B, H, T, dk); ek / ev (1, 2w+1, dk) shared by the heads.  scores[i, j] gets
+    qs_i . ek[j-i+w] for |j-i| <= w (what _relative_position_to_absolute_position
+    produces), masked_fill(-1e4) outside the lengths, softmax, optional dropout keep-mask,
+    and the context picks up sum_j p[i, j] ev[j-i+w] over the same band."""
+    B, H, T, dk = q.shape
+    qs = q / math.sqrt(dk)
+    scores = qs @ k.transpose(-2, -1)
+    i = torch.arange(T)[:, None]
+    j = torch.arange(T)[None, :]
+    rel = j - i + w
+    band = (rel >= 0) & (rel <= 2 * w)
+    relc = rel.clamp(0, 2 * w)
+    logits = qs @ ek[0].t()  # (B, H, T, 2w+1)
+    scores = scores + torch.where(band, torch.gather(
+        logits, 3, relc.expand(B, H, T, T)), torch.zeros((), dtype=q.dtype))
+    valid = make_non_pad_mask(lengths, T)
+    mask = valid[:, None, :, None] & valid[:, None, None, :]
+    scores = scores.masked_fill(~mask, -1e4)
+    p = torch.softmax(scores, dim=-1)
+    if keep is not None:
+        p = p * keep
+    out = p @ v
+    # relative weights: pw[i, r] = p[i, i + r - w]
+    pw = torch.zeros(B, H, T, 2 * w + 1, dtype=q.dtype)
+    pw = pw.scatter_add(3, relc.expand(B, H, T, T), torch.where(band, p, torch.zeros((),
+                                                                                  dtype=q.dtype)))
+    return out + pw @ ev[0]
+
+
+def transformer_encoder(P, cfg, x, lengths, keeps=None):
+    """nnsvs/model.py:1625-1671 + transformer/encoder.py:24-142 on (B, T, in_dim) -> (B,
+    T'*r, out_dim).  keeps: optional dict of dropout keep-masks keyed like the module path
+    ('L{i}.attn_p', 'L{i}.attn_y', 'L{i}.ffn_h', 'L{i}.ffn_y'); None -> no dropout."""
+    keeps = keeps or {}
+    H, nl = cfg.get("num_heads", 2), cfg.get("num_layers", 2)
+    kz, r = cfg.get("kernel_size", 3), cfg.get("reduction_factor", 1)
+    w = 4  # Encoder's window_size default (encoder.py:91)
+    lengths = torch.as_tensor(lengths, dtype=torch.int64)
+    if cfg.get("embed_dim") is not None:
+        x = phoneme_embed(P, "", x, cfg.get("in_ph_start_idx", 1), cfg.get("in_ph_end_idx", 50))
+    if r > 1:
+        lengths = lengths // r
+        if cfg.get("downsample_by_conv", False):
+            x = F.conv1d(x.transpose(1, 2), P["conv_downsample.weight"],
+                         P["conv_downsample.bias"], stride=r, groups=x.shape[-1]).transpose(1, 2)
+        else:
+            x = x[:, r - 1::r]
+    h = linear(P, "fc", x)  # (B, T, C)
+    B, T, C = h.shape
+    m = make_non_pad_mask(lengths, T)[:, :, None].to(h.dtype)
+    h = h * m
+    dk = C // H
+    pl, pr = (kz - 1) // 2, kz // 2
+
+    def conv(name, t):  # Conv1d over frames, "same" zero padding
+        y = F.conv1d(F.pad(t.transpose(1, 2), (pl, pr)), P[name + ".weight"], P[name + ".bias"])
+        return y.transpose(1, 2)
+
+    def proj(name, t):
+        return F.linear(t, P[name + ".weight"][:, :, 0], P[name + ".bias"])
+
+    def heads(t):
+        return t.view(B, T, H, dk).transpose(1, 2)
+
+    def ln(name, t):
+        return F.layer_norm(t, (C,), P[name + ".gamma"], P[name + ".beta"], 1e-5)
+
+    for i in range(nl):
+        a = f"encoder.attn_layers.{i}."
+        q, k_, v = (heads(proj(a + "conv_" + n, h)) for n in "qkv")
+        o = rel_attention(q, k_, v, P[a + "emb_rel_k"], P[a + "emb_rel_v"], lengths, w,
+                          keeps.get(f"L{i}.attn_p"))
+        y = proj(a + "conv_o", o.transpose(1, 2).reshape(B, T, C))
+        if f"L{i}.attn_y" in keeps:
+            y = y * keeps[f"L{i}.attn_y"]
+        h = ln(f"encoder.norm_layers_1.{i}", h + y)
+        f = f"encoder.ffn_layers.{i}."
+        z = torch.relu(conv(f + "conv_1", h * m))
+        if f"L{i}.ffn_h" in keeps:
+            z = z * keeps[f"L{i}.ffn_h"]
+        y = conv(f + "conv_2", z * m) * m
+        if f"L{i}.ffn_y" in keeps:
+            y = y * keeps[f"L{i}.ffn_y"]
+        h = ln(f"encoder.norm_layers_2.{i}", h + y)
+    h = h * m
+    return linear(P, "fc_out", h).view(B, -1, cfg["out_dim"])

@@ -40,6 +40,8 @@ def seeded_value(key, shape, seed, shapes):
         H = shapes[hkey][1] if hkey in shapes else shape[0] // 4
         k = 1.0 / np.sqrt(H)
         return rng.uniform(-k, k, shape).astype(np.float32)
+    if leaf == "gamma":  # LayerNorm scale of the Transformer encoder (encoder.py:15)
+        return (1.0 + 0.1 * rng.standard_normal(shape)).astype(np.float32)
     if key.endswith("emb.weight"):
         return (0.3 * rng.standard_normal(shape)).astype(np.float32)
     if len(shape) >= 2:

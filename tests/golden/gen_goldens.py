@@ -849,6 +849,63 @@ def case_vp():
     save("variance_predictor", arrays, meta)
 
 
+TRANSFORMER_CASES = (
+    # name, constructor kwargs, B, T, lengths
+    ("base", dict(in_dim=20, out_dim=5, hidden_dim=16, attention_dim=24, num_heads=2,
+                  num_layers=2, kernel_size=3, dropout=0.0), 2, 37, [37, 30]),
+    ("embed", dict(in_dim=20, out_dim=3, hidden_dim=16, attention_dim=12, num_heads=4,
+                   num_layers=1, kernel_size=1, dropout=0.0, embed_dim=8, in_ph_start_idx=2,
+                   in_ph_end_idx=12), 3, 29, [29, 17, 5]),
+    ("rf4_stride", dict(in_dim=12, out_dim=4, hidden_dim=32, attention_dim=40, num_heads=2,
+                        num_layers=2, kernel_size=4, dropout=0.0, reduction_factor=4), 2, 70,
+     [70, 45]),
+    ("rf2_conv", dict(in_dim=12, out_dim=4, hidden_dim=16, attention_dim=16, num_heads=1,
+                      num_layers=1, kernel_size=3, dropout=0.0, reduction_factor=2,
+                      downsample_by_conv=True), 2, 41, [41, 20]),
+    ("short", dict(in_dim=6, out_dim=2, hidden_dim=8, attention_dim=8, num_heads=2,
+                   num_layers=1, kernel_size=3, dropout=0.0), 2, 3, [3, 2]),
+)
+
+
+def case_transformer():
+    """nnsvs.model.TransformerEncoder (model.py:1540-1671; transformer/encoder.py,
+    attentions.py) on ragged batches: phoneme embedding, reduction factor (stride and conv
+    downsampling), even FFN kernel (asymmetric "same" padding), T below the relative window.
+    Training-mode forward (dropout 0) + backward of sum(out * R): output, input grad and every
+    parameter grad."""
+    from nnsvs.model import TransformerEncoder as RefTE
+    arrays, meta = {}, {}
+    for name, cfg, B, T, lengths in TRANSFORMER_CASES:
+        torch.manual_seed(0)
+        model = RefTE(**cfg)
+        shapes = {k: tuple(v.shape) for k, v in model.state_dict().items()}
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in
+                               seeded_state_dict(shapes, SEED).items()})
+        r = rng_for("transformer_" + name)
+        x = r.standard_normal((B, T, cfg["in_dim"])).astype(np.float32)
+        if cfg.get("embed_dim"):
+            p0, p1 = cfg["in_ph_start_idx"], cfg["in_ph_end_idx"]
+            x[:, :, p0:p1] = 0.0
+            ids = r.integers(0, p1 - p0, size=(B, T))
+            for b in range(B):
+                x[b, np.arange(T), p0 + ids[b]] = 1.0
+        model.train()
+        xt = T_(x).requires_grad_()
+        out = model(xt, T_(np.array(lengths, dtype=np.int64)))
+        R = r.standard_normal(tuple(out.shape)).astype(np.float32)
+        (out * T_(R)).sum().backward()
+        p = name + "::"
+        arrays.update({p + "x": x, p + "R": R, p + "out": out.detach().numpy(),
+                       p + "dx": xt.grad.numpy(), p + "lengths": np.array(lengths)})
+        for k, prm in model.named_parameters():
+            arrays[p + "grad::" + k] = prm.grad.numpy()
+        model.eval()
+        with torch.no_grad():
+            arrays[p + "eval_out"] = model(T_(x), T_(np.array(lengths, dtype=np.int64))).numpy()
+        meta[name] = dict(cfg=cfg, B=B, T=T, shapes={k: list(v) for k, v in shapes.items()})
+    save("transformer", arrays, meta)
+
+
 def case_onset_merge():
     """Timing-path onset merge (collate_fn_syncmultitrack, train_util.py:776-934): two
     tracks' note rows aligned by onset time, with ties, empty overlaps and ragged ends
@@ -976,6 +1033,8 @@ def main():
         case_mdn()
     if run("vp"):
         case_vp()
+    if run("transformer"):
+        case_transformer()
     if run("onset"):
         case_onset_merge()
     if run("loader"):

@@ -19,6 +19,7 @@ import os
 import subprocess
 import sys
 import time
+import types
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -36,6 +37,11 @@ def gate_gemm_bytes(M, C, E, a_bytes):
     return (M * (C + E) * a_bytes + 2 * C * (3 * C + E) * 2 + 2 * C * 4 +
             M * C * a_bytes + M * 2 * C * a_bytes)
 TRAIN_FLOP_PER_FRAME = 127.5e6  # SURVEY.md §6 (torch.utils.flop_counter on the oracle)
+# postprocess_acoustic settings of the recipe's synthesis config
+# (nnsvs/bin/conf/synthesis/synthesis/world_gv_usfgan.yaml)
+SYNTH_POST = dict(frame_period=5, post_filter_type="gv", trajectory_smoothing=True,
+                  trajectory_smoothing_cutoff=50, trajectory_smoothing_cutoff_f0=20,
+                  vuv_threshold=0.3)
 
 
 def _imports():
@@ -170,16 +176,19 @@ def synth_rtf(model, dev, T=2000, parts=6, reps=3):
     synthesis_multitrack.py:113-288 -- timing inference (time-lag + duration MDN models with
     the onset merge and duration fitting of gen.py:214-1006, per ordered pair), acoustic
     inference (pad_inference_multitrack, free-running AR log-F0, 100-step reverse diffusion
-    for mgc and bap, V/UV) and the uSFGAN generator -- for one (main, sub) pair of T frames
+    for mgc and bap, V/UV), the output inverse scaling + postprocess_acoustic (GV,
+    WORLD F0 stream, trajectory smoothing; gen.py:1299, 1314-1530) + predict_waveform's
+    uSFGAN input preparation (aperiodicity codec round trip, f0; gen.py:1637-1694) and the
+    uSFGAN generator -- for one (main, sub) pair of T frames
     (5 ms), for a `parts`-part ensemble (every part paired with its neighbour) batched in
     one acoustic/vocoder pass, and for the reference's ordered-pair sweep (every part with
     every partner, itself included: parts^2 pairs).  The acoustic input frames are
     synthetic features of the song length (the reference's ground-truth-duration path:
     its predicted-timing path fails, Appendix A-12); timing runs on synthetic score tracks
     and its output labels are not fed back into frame features (nnmnkwii frame feature
-    extraction is out of scope).  Scalers and the pyworld codec of gen.py:1637-1694 are
-    replaced by identity statistics on synthetic data."""
-    from ensemble_svs_with_interactions_amd import synthesis, usfgan
+    extraction is out of scope; the score-pitch column of the input features stands in for
+    the note frames).  Scaler statistics are synthetic."""
+    from ensemble_svs_with_interactions_amd import postprocess, scalers, synthesis, usfgan
     torch.manual_seed(7)
     voc = configs.instantiate(configs.usfgan_generator()).to(dev)
     voc.remove_weight_norm()  # as load_vocoder does (nnsvs/util.py:412-414)
@@ -190,6 +199,13 @@ def synth_rtf(model, dev, T=2000, parts=6, reps=3):
     spk_of = [p % 4 for p in range(parts)]
     model.eval()
     sc, mu = configs.LF0_STATS["out_lf0_scale"], configs.LF0_STATS["out_lf0_mean"]
+    # output statistics: unit variance except the log-F0 stream (synthetic; var_ doubles as
+    # the GV target of the mgc post-filter)
+    mean_, var_ = np.zeros(67), np.full(67, 0.25)
+    mean_[60], var_[60] = mu, sc * sc
+    out_scaler = scalers.StandardScaler(mean_, var_)
+    stream_cfg = types.SimpleNamespace(stream_sizes=[60, 1, 1, 5], num_windows=1,
+                                       has_dynamic_features=[False] * 4)
     out = {}
     for name, pairs in (("pair", [(0, 1)]),
                         (f"ensemble_{parts}part", [(i, (i + 1) % parts) for i in range(parts)]),
@@ -213,9 +229,24 @@ def synth_rtf(model, dev, T=2000, parts=6, reps=3):
             return model.inference(xm, xs, spks=(s0, s1), lengths=[T] * B)
 
         def vocoder(feats):
-            f0 = torch.exp(feats[:, :, 60] * sc + mu)  # de-normalised continuous log-F0
-            aux = torch.cat([feats[:, :, :60], feats[:, :, 62:67]], -1)
-            return wrapper.inference_batch(f0, aux)
+            # predict_acoustic's inverse scaling (gen.py:1299), postprocess_acoustic
+            # (gen.py:1314-1530: GV on note frames, WORLD F0 stream, 50 / 20 Hz trajectory
+            # smoothing, bap clip) and predict_waveform's uSFGAN inputs (gen.py:1637-1694)
+            # per track on the device, then one batched generator pass
+            f0s, auxs = [], []
+            for bi in range(B):
+                f = feats[bi].clone()
+                postprocess.inverse_transform(out_scaler, f)
+                streams = postprocess.postprocess_acoustic(
+                    dev, f, xm[bi], {}, {}, stream_cfg, out_scaler, pitch_idx=51,
+                    **SYNTH_POST)
+                f0, aux = postprocess.usfgan_inputs(
+                    *streams, sine_f0_type=configs.USFGAN_DATA["sine_f0_type"],
+                    vuv_threshold=SYNTH_POST["vuv_threshold"])
+                f0s.append(f0)
+                auxs.append(aux)
+            return wrapper.inference_batch(torch.cat(f0s, 1).t().contiguous(),
+                                           torch.stack(auxs))
 
         timing()
         feats = acoustic()  # warm-up (weight packing, graph capture)

@@ -160,6 +160,11 @@ SIGNATURES = {
     "ensvs_dwdown_fwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp],
     "ensvs_dwdown_bwd": [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int,
                          c_int, c_vp],
+    "ensvs_gv_scale": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp],
+    "ensvs_world_lf0": [c_vp, c_int, c_vp, c_int, c_int, c_float, c_float, c_vp, c_vp],
+    "ensvs_filtfilt": [c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp],
+    "ensvs_bap_post": [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "ensvs_scale_cols": [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp],
 }
 
 # entry points returning a value instead of a status code

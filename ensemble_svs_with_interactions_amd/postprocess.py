@@ -1,0 +1,219 @@
+"""Post-acoustic feature processing on the device.
+
+Drop-in for nnsvs.gen.postprocess_acoustic (gen.py:1314-1530) and the uSFGAN input
+preparation of predict_waveform (gen.py:1637-1694) as the multi-track synthesis driver calls
+them (synthesis_multitrack.py:221-259 with nnsvs/bin/conf/synthesis/synthesis/
+world_gv_usfgan.yaml): GV variance scaling of the note frames, the WORLD static F0 stream
+(V/UV threshold, interpolation over unvoiced frames), trajectory smoothing (zero-phase
+Butterworth), the band-aperiodicity clip, then the WORLD aperiodicity codec round trip,
+continuous / voiced F0 and the vocoder input scaler.  The features stay in HBM between the
+acoustic model and the vocoder; every step is a kernel of postprocess.hip.
+
+Interface deviation: the reference recomputes the frame-level linguistic features from HTS
+labels with nnmnkwii (fe.linguistic_features), which this image does not have; here the
+``duration_modified_labels`` argument takes those frame-level features directly (an array
+(T, D_ling); only the score-pitch column get_pitch_index(binary_dict, numeric_dict) is read).
+Filter design (scipy.signal.butter / lfilter_zi, a handful of float64 coefficients) runs on
+the host once per cutoff.
+"""
+import numpy as np
+import torch
+
+from ._lib import call
+
+_FILTERS = {}
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def get_pitch_index(binary_dict, numeric_dict):
+    """nnsvs/io/hts.py:48-65: column of the first numeric question whose pattern starts with
+    /E (the score pitch), after the binary questions."""
+    idx = 0
+    pitch_idx = len(binary_dict)
+    while idx < len(numeric_dict):
+        if numeric_dict[idx][1].pattern.startswith("/E"):
+            pitch_idx = pitch_idx + idx
+            break
+        idx += 1
+    return pitch_idx
+
+
+def _dev_f32(x, device):
+    if isinstance(x, torch.Tensor):
+        return x.detach().to(device=device, dtype=torch.float32).contiguous().clone()
+    return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(device)
+
+
+def _filter(fs, cutoff, N=5, device="cuda"):
+    """Butterworth lowpass (b | a) and lfilter_zi on the device, cached per design."""
+    key = (int(fs), float(cutoff), int(N), str(torch.device(device)))
+    f = _FILTERS.get(key)
+    if f is None:
+        from scipy import signal
+        b, a = signal.butter(N, [cutoff / (fs // 2)], "lowpass")  # dsp.py:21-25
+        zi = signal.lfilter_zi(b, a)
+        ba = torch.from_numpy(np.concatenate([b, a]).astype(np.float64)).to(device)
+        f = _FILTERS[key] = (ba, torch.from_numpy(zi.astype(np.float64)).to(device), len(b),
+                             max(len(a), len(b)) * (N // 2 + 1))
+    return f
+
+
+def lowpass_filter(x, fs, cutoff=5, N=5, ld=None, C=None, T=None):
+    """nnsvs/dsp.py:10-33 on device columns, in place: x (T,) or (T, C) float32 (or a raw
+    view given by ld / C / T).  Sequences no longer than the guard are left as they are."""
+    ba, zi, nb, guard = _filter(fs, cutoff, N, x.device)
+    if T is None:
+        T = x.shape[0]
+        C = 1 if x.dim() == 1 else x.shape[1]
+        ld = 1 if x.dim() == 1 else x.stride(0)
+    padlen = 3 * nb
+    if T <= guard:
+        return x
+    work = torch.empty(C * (T + 2 * padlen), dtype=torch.float64, device=x.device)
+    call("ensvs_filtfilt", x.data_ptr(), ld, T, C, ba.data_ptr(), nb, zi.data_ptr(), padlen,
+         guard, work.data_ptr(), stream())
+    return x
+
+
+def variance_scaling(gv, feats, offset=2, note_mask=None):
+    """nnsvs/postfilters.py:9-46 in place on device rows feats (T, D); note_mask (T,) bool
+    (None: every frame) selects the note frames whose statistics are matched to gv."""
+    T, D = feats.shape
+    if note_mask is None:
+        note = torch.ones(T, dtype=torch.uint8, device=feats.device)
+    else:
+        note = note_mask.to(device=feats.device, dtype=torch.uint8).contiguous()
+    g = torch.as_tensor(np.asarray(gv, dtype=np.float64).reshape(-1)[:D]).to(feats.device)
+    call("ensvs_gv_scale", feats.data_ptr(), feats.stride(0), T, D, offset, note.data_ptr(),
+         g.data_ptr(), stream())
+    return feats
+
+
+def scale_cols(x, a, b, mode):
+    """sklearn scaler arithmetic on device rows (see ensvs_scale_cols)."""
+    T, C = x.shape
+    dev = x.device
+    a_ = torch.as_tensor(np.asarray(a, dtype=np.float64).reshape(-1)).to(dev)
+    b_ = torch.as_tensor(np.asarray(b, dtype=np.float64).reshape(-1)).to(dev)
+    call("ensvs_scale_cols", x.data_ptr(), x.stride(0), T, C, a_.data_ptr(), b_.data_ptr(),
+         int(mode), stream())
+    return x
+
+
+def inverse_transform(scaler, x):
+    """scaler.inverse_transform on device rows, in place (StandardScaler / MinMaxScaler)."""
+    if getattr(scaler, "kind", None) == "minmax" or hasattr(scaler, "data_min_"):
+        return scale_cols(x, scaler.scale_, scaler.min_, 1)
+    return scale_cols(x, scaler.scale_, scaler.mean_, 0)
+
+
+def transform(scaler, x):
+    if getattr(scaler, "kind", None) == "minmax" or hasattr(scaler, "data_min_"):
+        return scale_cols(x, scaler.scale_, scaler.min_, 0)
+    return scale_cols(x, scaler.scale_, scaler.mean_, 1)
+
+
+@torch.no_grad()
+def postprocess_acoustic(device, acoustic_features, duration_modified_labels, binary_dict,
+                         numeric_dict, acoustic_config, acoustic_out_static_scaler,
+                         postfilter_model=None, postfilter_config=None,
+                         postfilter_out_scaler=None, sample_rate=48000, frame_period=5,
+                         relative_f0=False, feature_type="world", post_filter_type="gv",
+                         trajectory_smoothing=True, trajectory_smoothing_cutoff=50,
+                         trajectory_smoothing_cutoff_f0=20, vuv_threshold=0.5,
+                         f0_shift_in_cent=0, vibrato_scale=1.0, force_fix_vuv=False,
+                         fill_silence_to_rest=False, pitch_idx=None):
+    """gen.py:1314-1530 -> (mgc, lf0, vuv, bap) device tensors (T, d).
+
+    duration_modified_labels: the frame-level linguistic features (T, D_ling) (see the module
+    docstring).  Supported: feature_type "world" with static streams (mgc, lf0, vuv, bap),
+    post_filter_type "gv" (or "nnsvs" without a model, which the reference treats as "gv"),
+    relative_f0 False, no vibrato streams -- the recipe's synthesis settings."""
+    if feature_type != "world":
+        raise NotImplementedError("feature_type 'melf0' is not in the multi-track recipe")
+    if relative_f0:
+        raise NotImplementedError("relative_f0 needs librosa.midi_to_hz (not in the recipe)")
+    if force_fix_vuv or fill_silence_to_rest:
+        raise NotImplementedError("force_fix_vuv / fill_silence_to_rest read HTS question "
+                                  "names (off in the recipe's synthesis config)")
+    if post_filter_type == "merlin" or (post_filter_type == "nnsvs" and
+                                        postfilter_model is not None):
+        raise NotImplementedError(f"post_filter_type {post_filter_type!r} with a model / "
+                                  "pysptk is not in the multi-track synthesis path")
+    if np.any(acoustic_config.has_dynamic_features):
+        raise NotImplementedError("dynamic features (MLPG) are not in the recipe")
+    sizes = [int(v) for v in acoustic_config.stream_sizes]
+    if len(sizes) != 4:
+        raise NotImplementedError("vibrato streams are not in the recipe")
+    if isinstance(duration_modified_labels, (np.ndarray, torch.Tensor)):
+        ling = duration_modified_labels
+    else:
+        raise TypeError("duration_modified_labels: pass the frame-level linguistic features "
+                        "(nnmnkwii label parsing is not part of this package)")
+    dev = torch.device(device)
+    feats = _dev_f32(acoustic_features, dev)
+    T, D = feats.shape
+    assert D == sum(sizes)
+    if pitch_idx is None:
+        pitch_idx = get_pitch_index(binary_dict, numeric_dict)
+    ling_t = ling if isinstance(ling, torch.Tensor) else torch.from_numpy(np.asarray(ling))
+    score = ling_t[:, pitch_idx].to(dev)
+    if post_filter_type in ("gv", "nnsvs"):
+        m = sizes[0]
+        gv = np.asarray(acoustic_out_static_scaler.var_, dtype=np.float64).reshape(-1)[:m]
+        variance_scaling(gv, feats[:, :m], offset=2, note_mask=score > 0)
+    o = np.cumsum([0] + sizes)
+    lf0, vuv = feats[:, o[1]:o[2]], feats[:, o[2]:o[3]]
+    shift = f0_shift_in_cent * np.log(2) / 1200 if f0_shift_in_cent != 0 else 0.0
+    work = torch.empty(T, device=dev)
+    call("ensvs_world_lf0", lf0.data_ptr(), D, vuv.data_ptr(), D, T, float(vuv_threshold),
+         float(shift), work.data_ptr(), stream())
+    if trajectory_smoothing:
+        modfs = int(1 / (frame_period * 0.001))
+        _lp_cols(feats, o[1], sizes[1], T, D, modfs, trajectory_smoothing_cutoff_f0)
+        _lp_cols(feats, o[0], sizes[0], T, D, modfs, trajectory_smoothing_cutoff)
+        _lp_cols(feats, o[3], sizes[3], T, D, modfs, trajectory_smoothing_cutoff)
+    if not sizes[3] > 5:  # use_mcep_aperiodicity (gen.py:1519-1522)
+        call("ensvs_bap_post", feats.data_ptr() + 4 * int(o[3]), D, T, sizes[3], 1, 0, stream())
+    return tuple(feats[:, o[i]:o[i + 1]] for i in range(4))
+
+
+def _lp_cols(feats, c0, C, T, D, fs, cutoff):
+    ba, zi, nb, guard = _filter(fs, cutoff, 5, feats.device)
+    if T <= guard:
+        return
+    padlen = 3 * nb
+    work = torch.empty(C * (T + 2 * padlen), dtype=torch.float64, device=feats.device)
+    call("ensvs_filtfilt", feats.data_ptr() + 4 * int(c0), D, T, C, ba.data_ptr(), nb,
+         zi.data_ptr(), padlen, guard, work.data_ptr(), stream())
+
+
+@torch.no_grad()
+def usfgan_inputs(mgc, lf0, vuv, bap, vocoder_in_scaler=None, sine_f0_type="f0",
+                  vuv_threshold=0.5):
+    """predict_waveform's uSFGAN branch up to the generator (gen.py:1637-1694), on device
+    streams (T, d): the WORLD band-aperiodicity codec round trip with the unvoiced fill and
+    clip (restated from WORLD d4c.cpp; pyworld is not in this image: parity unpinned),
+    aux = vocoder_in_scaler.transform([mgc, bap]), f0 = exp(lf0) (0 where vuv < threshold
+    for sine_f0_type 'f0').  Returns (f0 (T, 1), aux (T, d_mgc + d_bap))."""
+    T = mgc.shape[0]
+    dev = mgc.device
+    dm, db = mgc.shape[1], bap.shape[1]
+    aux = torch.empty(T, dm + db, device=dev)
+    call("ensvs_copy_cols", mgc.data_ptr(), mgc.stride(0), aux.data_ptr(), dm + db, T, dm,
+         stream())
+    call("ensvs_copy_cols", bap.data_ptr(), bap.stride(0), aux.data_ptr() + 4 * dm, dm + db, T,
+         db, stream())
+    if db <= 5:
+        call("ensvs_bap_post", aux.data_ptr() + 4 * dm, dm + db, T, db, 0, 1, stream())
+    else:
+        raise NotImplementedError("mel-cepstral aperiodicity (pysptk) is not in the recipe")
+    if vocoder_in_scaler is not None:
+        transform(vocoder_in_scaler, aux)
+    f0 = torch.exp(lf0.float())
+    if sine_f0_type == "f0":
+        f0 = torch.where(vuv < vuv_threshold, torch.zeros_like(f0), f0)
+    return f0.contiguous(), aux

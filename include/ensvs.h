@@ -390,6 +390,31 @@ int ensvs_dwdown_fwd(const float* x, int ldx, const float* w, const float* bias,
 int ensvs_dwdown_bwd(const float* dy, int ldy, const float* x, int ldx, const float* w,
                      float* dx, int lddx, float* prod, int B, int T, int C, int r, void* stream);
 
+/* ---- Post-acoustic feature processing (gen.py postprocess_acoustic :1314-1530; row f4;
+ * postprocess.hip).  Frame rows [t*ld + c], in place. */
+/* variance_scaling (postfilters.py:9-46) of columns [offset, D) over the frames with
+ * note[t] != 0 (get_note_frame_indices, io/hts.py:29-45); gv: float64 [D] (scaler var_). */
+int ensvs_gv_scale(float* x, int ld, int T, int D, int offset, const unsigned char* note,
+                   const double* gv, void* stream);
+/* gen_spsvs_static_features' F0 stream (gen.py:1988-2016, relative_f0 = False): vuv
+ * threshold, exp/log round trip, nnmnkwii interp1d(slinear) over unvoiced frames, + shift.
+ * work: T floats. */
+int ensvs_world_lf0(float* lf0, int ldl, const float* vuv, int ldv, int T, float thr,
+                    float shift, float* work, void* stream);
+/* lowpass_filter (dsp.py:10-33): scipy.signal.filtfilt(b, a, x) per column, float64; ba =
+ * [b | a] (nb each), zi = lfilter_zi(b, a) (nb - 1), padlen = 3 nb; columns are left unchanged
+ * when T <= guard.  work: C * (T + 2 padlen) doubles. */
+int ensvs_filtfilt(float* x, int ld, int T, int C, const double* ba, int nb, const double* zi,
+                   int padlen, int guard, double* work, void* stream);
+/* bap clip [-60, 0] (gen.py:1520-1522) and the WORLD aperiodicity codec round trip before
+ * uSFGAN (gen.py:1649-1670). */
+int ensvs_bap_post(float* bap, int ld, int T, int D, int clip, int codec, void* stream);
+/* sklearn scaler arithmetic in place (float32 data, float64 statistics a, b per column):
+ * mode 0 x = x*a + b (StandardScaler.inverse_transform, gen.py:1299; MinMaxScaler.transform),
+ * mode 1 x = (x - b)/a (StandardScaler.transform: the vocoder input scaler, gen.py:1678-1684). */
+int ensvs_scale_cols(float* x, int ld, int T, int C, const double* a, const double* b, int mode,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

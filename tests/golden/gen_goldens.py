@@ -906,6 +906,65 @@ def case_transformer():
     save("transformer", arrays, meta)
 
 
+POSTPROCESS_CASES = (
+    # name, T, note fraction, voiced fraction
+    ("song", 1500, 0.8, 0.7),
+    ("short", 15, 1.0, 0.6),      # below lowpass_filter's length guard (18)
+    ("edge", 19, 0.5, 0.5),       # just above it
+    ("unvoiced", 300, 0.6, 0.0),  # no voiced frame: interp1d returns its input
+    ("nonote", 240, 0.0, 0.8),    # no note frame: variance_scaling returns its input
+)
+
+
+def case_postprocess():
+    """postprocess_acoustic (gen.py:1314-1530) with the recipe's synthesis settings
+    (conf/synthesis/synthesis/world_gv_usfgan.yaml: gv post-filter, trajectory smoothing
+    50 / 20 Hz, vuv_threshold 0.3, relative_f0 false).  Absent dependencies patched in:
+    the frame-level linguistic features are given (fe.linguistic_features returns them;
+    only the score-pitch column is read) and nnmnkwii's interp1d is the oracle's restatement
+    (parity of that piece unpinned)."""
+    import re
+    import nnsvs.gen as ref_gen
+    from oracle import postprocess_oracle as PO
+    arrays, meta = {}, {"cases": []}
+    cfg = types.SimpleNamespace(stream_sizes=[60, 1, 1, 5],
+                                has_dynamic_features=[False, False, False, False],
+                                num_windows=1)
+    r = rng_for("postprocess")
+    gv = (0.02 + r.random(67)) ** 2
+    scaler = types.SimpleNamespace(var_=gv)
+    numeric_dict = {0: ("e1", re.compile(r"/E:(\d+)"))}
+    saved = (ref_gen.fe, ref_gen.interp1d)
+    try:
+        ref_gen.interp1d = PO.interp1d
+        for name, T, note_frac, voiced_frac in POSTPROCESS_CASES:
+            runs = lambda frac: np.repeat(r.random(T // 10 + 1) < frac, 10)[:T]  # noqa: E731
+            score = np.where(runs(note_frac), r.integers(55, 80, size=T), 0).astype(np.float32)
+            x = np.empty((T, 67), dtype=np.float32)
+            x[:, :60] = (r.standard_normal((T, 60)) * np.linspace(2.0, 0.1, 60)).astype(
+                np.float32) + np.cumsum(r.standard_normal((T, 1)), 0).astype(np.float32) * .05
+            x[:, 60] = (5.5 + 0.3 * np.sin(np.arange(T) / 17.0) + 0.05 * r.standard_normal(T))
+            x[:, 61] = np.where(runs(voiced_frac), 0.5 + 0.5 * r.random(T), 0.3 * r.random(T))
+            x[:, 62:] = (-25.0 + 30.0 * r.standard_normal((T, 5))).astype(np.float32)
+            ling = score[:, None].copy()
+            ref_gen.fe = types.SimpleNamespace(linguistic_features=lambda *a, **k: ling)
+            out = ref_gen.postprocess_acoustic(
+                "cpu", x.copy(), None, {}, numeric_dict, cfg, scaler, sample_rate=48000,
+                frame_period=5, relative_f0=False, feature_type="world", post_filter_type="gv",
+                trajectory_smoothing=True, trajectory_smoothing_cutoff=50,
+                trajectory_smoothing_cutoff_f0=20, vuv_threshold=0.3, f0_shift_in_cent=0,
+                vibrato_scale=1.0, force_fix_vuv=False)
+            p = name + "::"
+            arrays.update({p + "x": x, p + "score": score})
+            for k, v in zip(("mgc", "lf0", "vuv", "bap"), out):
+                arrays[p + k] = np.asarray(v)
+            meta["cases"].append(name)
+    finally:
+        ref_gen.fe, ref_gen.interp1d = saved
+    arrays["gv"] = gv
+    save("postprocess", arrays, meta)
+
+
 def case_onset_merge():
     """Timing-path onset merge (collate_fn_syncmultitrack, train_util.py:776-934): two
     tracks' note rows aligned by onset time, with ties, empty overlaps and ragged ends
@@ -1035,6 +1094,8 @@ def main():
         case_vp()
     if run("transformer"):
         case_transformer()
+    if run("postprocess"):
+        case_postprocess()
     if run("onset"):
         case_onset_merge()
     if run("loader"):

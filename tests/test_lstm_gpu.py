@@ -2,7 +2,9 @@
 (fp32 CPU, packed bidirectional, as FFConvLSTM / the lf0 encoder use it: nnsvs/model.py:862-869,
 914-916), for every hidden size the C-ABI dispatches, with lengths that end inside, at and
 one past a staging chunk (16 steps; 8 for the H=128 backward) and a length-1 sequence.
-Tolerances (fp32): outputs rel 1e-5, gradients rel 1e-4."""
+Tolerances (fp32): outputs rel 1e-5, gradients rel 1e-4; at the bench's T = 1024 and the
+long-sequence T = 4096 outputs rel 1e-4, gradients rel 1e-3 (4096 serial
+steps of fp32 rounding in different orders)."""
 import pytest
 import torch
 from torch.nn.utils.rnn import pack_padded_sequence, pad_packed_sequence
@@ -15,9 +17,16 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("H", [8, 16, 32, 64, 128])
 def test_lstm_recurrence_matches_torch(H):
-    torch.manual_seed(H)
-    B, T, I = 5, 37, 24
-    lengths = [37, 17, 16, 9, 1]
+    _check(H, 5, 37, 24, [37, 17, 16, 9, 1], 1e-5, 1e-4)
+
+
+@pytest.mark.parametrize("H,T", [(128, 1024), (64, 1024), (128, 4096), (64, 4096)])
+def test_lstm_long_sequences_match_torch(H, T):
+    _check(H, 3, T, 16, [T, T - 333, T // 2 + 1], 1e-4, 1e-3)
+
+
+def _check(H, B, T, I, lengths, tol_y, tol_g):
+    torch.manual_seed(H + T)
     lstm = torch.nn.LSTM(I, H, batch_first=True, bidirectional=True)
     x = torch.randn(B, T, I, requires_grad=True)
     out, _ = lstm(pack_padded_sequence(x, lengths, batch_first=True, enforce_sorted=False))
@@ -38,7 +47,7 @@ def test_lstm_recurrence_matches_torch(H):
     saved = torch.empty(B * T * 2 * 5 * H, device=dev)
     assert call("ensvs_lstm_fwd", gx_d.data_ptr(), 8 * H, whh[0].data_ptr(), whh[1].data_ptr(),
                 lens.data_ptr(), B, T, H, y.data_ptr(), 2 * H, saved.data_ptr(), st) in (0, None)
-    assert rel(y.cpu().view(B, T, 2 * H), y_ref.detach()) < 1e-5
+    assert rel(y.cpu().view(B, T, 2 * H), y_ref.detach()) < tol_y
 
     dg = torch.empty(B * T, 8 * H, device=dev)
     gy_d = gy.reshape(B * T, 2 * H).contiguous().to(dev)
@@ -48,7 +57,7 @@ def test_lstm_recurrence_matches_torch(H):
     hy = y.cpu().view(B, T, 2 * H)
     for d, s in enumerate(("", "_reverse")):
         g = dg[:, :, 4 * H * d:4 * H * (d + 1)]
-        assert torch.all(g[1, 17:] == 0)  # padded frames
+        assert torch.all(g[1, lengths[1]:] == 0)  # padded frames
         # h_{t-1} in processing order (zero state at the sequence start)
         h = hy[:, :, H * d:H * (d + 1)]
         hp = torch.zeros_like(h)
@@ -58,8 +67,8 @@ def test_lstm_recurrence_matches_torch(H):
             else:
                 hp[b, :L - 1] = h[b, 1:L]
         dwhh = torch.einsum("btg,bth->gh", g, hp)
-        assert rel(dwhh, P["weight_hh_l0" + s].grad) < 1e-4, s
-        assert rel(g.sum((0, 1)), P["bias_hh_l0" + s].grad) < 1e-4, s
+        assert rel(dwhh, P["weight_hh_l0" + s].grad) < tol_g, s
+        assert rel(g.sum((0, 1)), P["bias_hh_l0" + s].grad) < tol_g, s
     dx = sum(dg[:, :, 4 * H * d:4 * H * (d + 1)] @ P["weight_ih_l0" + s].detach()
              for d, s in enumerate(("", "_reverse")))
-    assert rel(dx, x.grad) < 1e-4
+    assert rel(dx, x.grad) < tol_g

@@ -29,7 +29,7 @@ from . import kernels as K
 from . import layers as Ly
 from ._lib import call
 from .base import BaseModel, PredictionType
-from .engine import GradCapture, ModulePacks, empty, grad_of, lengths_pair, next_seed
+from .engine import GradCapture, ModulePacks, aux_stream, empty, grad_of, lengths_pair, next_seed
 from .engine import gemm_dtype as engine_gemm_dtype
 
 SQRT1_2 = 1.0 / math.sqrt(2.0)
@@ -265,6 +265,7 @@ class DiffNet(nn.Module):
         tmp_dss = empty(C, device=dev)
         K.colsum(dss, C, M, C, tmp_dss)
         dx = dxb = None
+        later = []
         bw = b16 and len(st["XB"]) == L  # bf16 operands saved by the forward
         zsrc = st["ZB"] if bw else st["Z"]
         ldz = L * C
@@ -306,20 +307,23 @@ class DiffNet(nn.Module):
                 dyb = bf(M, C) if (dx is None and b16) else None
                 K.gemm(tsegs, B, T, C, pk.bwd, dy, C, ybf=dyb, ybf_ld=C)
                 K.colsum(dy, C, T, C, dd_all, groups=B, ldo=L * C, outoff=l * C)
-            # per-block weight gradients; the ones whose second operand is shared by
-            # every block (skip half of w_o, conditioner, diffusion projection) and
-            # all bias gradients are taken for all blocks at once after the loop
+            # per-block weight gradients (deferred: they run after the conditioner input
+            # gradient, off the critical path); the ones whose second operand is shared by
+            # every block (skip half of w_o, conditioner, diffusion projection) and all
+            # bias gradients are taken for all blocks at once after the loop
             w_o = blk.output_projection
             if dx is not None:
-                wg(w_o.weight, dxb if bw else dx, C, zsrc[l], ldz, B, T, T, C, C,
-                   scale=SQRT1_2, row0=0)
+                later.append(lambda w=w_o.weight, g=(dxb if bw else dx), z=zsrc[l]:
+                             wg(w, g, C, z, ldz, B, T, T, C, C, scale=SQRT1_2, row0=0))
             if bw:
-                wg(blk.dilated_conv.weight, dpre_b, L * 2 * C, st["XB"][l], C, B, T, T,
-                   2 * C, C, taps=3, dil=dl, shift0=-dl, dyoff=l * 2 * C)
+                later.append(lambda w=blk.dilated_conv.weight, x_=st["XB"][l], dl=dl, l=l:
+                             wg(w, dpre_b, L * 2 * C, x_, C, B, T, T, 2 * C, C, taps=3,
+                                dil=dl, shift0=-dl, dyoff=l * 2 * C))
             else:
-                wg(blk.dilated_conv.weight, dpre_all, L * 2 * C, st["X"][l], C, B, T, T,
-                   2 * C, C, taps=3, dil=dl, shift0=-dl, radd=st["ds"][:, l * C:],
-                   radd_ld=L * C, dyoff=l * 2 * C)
+                later.append(lambda w=blk.dilated_conv.weight, x_=st["X"][l], dl=dl, l=l:
+                             wg(w, dpre_all, L * 2 * C, x_, C, B, T, T, 2 * C, C, taps=3,
+                                dil=dl, shift0=-dl, radd=st["ds"][:, l * C:], radd_ld=L * C,
+                                dyoff=l * 2 * C))
             if fuse:
                 dx, dxb = xnew, xnewb
             elif dx is None:
@@ -334,6 +338,32 @@ class DiffNet(nn.Module):
                     call("ensvs_axpby_to", dxn.data_ptr(), dx.data_ptr(), SQRT1_2, dy.data_ptr(),
                          1.0, M * C, Ly.stream())
                 dx = dxn
+        # conditioner input grad of all blocks at once: the only output the encoder's
+        # backward waits for
+        dcond = empty(M, E, device=dev)
+        K.gemm([K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, L * 2 * C, pk["condT"], T)],
+               B, T, E, pk.bwd, dcond, E)
+        # everything below produces parameter gradients only: an auxiliary stream of the
+        # enclosing branch set (engine.aux_stream) runs it beside the encoder's backward
+        with aux_stream(keep=(later, st, dout, dx, dxb, dss, dssb, tmp_dss, dpre_all, dpre_b,
+                              dd_all, dd_tiles, pre_tiles)):
+            for f in later:
+                f()
+            self._bwd_param_tail(st, dout, dx, dss, dssb, tmp_dss, dpre_all, dpre_b, dd_all,
+                                 dd_tiles, pre_tiles, fuse, bw, b16)
+        return dcond
+
+    def _bwd_param_tail(self, st, dout, dx, dss, dssb, tmp_dss, dpre_all, dpre_b, dd_all,
+                        dd_tiles, pre_tiles, fuse, bw, b16):
+        """The block-shared weight gradients, every bias gradient, the step-embedding MLP
+        and the input projection (parameter gradients only)."""
+        pk = self._packs
+        dev = dout.device
+        C, L, E, Mc = self.C, len(self.residual_layers), self.E, self.in_dim
+        B, T = st["B"], st["T"]
+        M = B * T
+        wg = Ly.wgrad_into
+        cs = Ly.colsum_into
         if fuse:
             K.colsum(dd_tiles, L * C, T // K.BM, L * C, dd_all, groups=B)
         # the block-shared weight gradients and every bias gradient, each one GEMM or
@@ -384,10 +414,6 @@ class DiffNet(nn.Module):
             else:
                 call("ensvs_res_bias_grad", tdd.data_ptr(), L, C, bo[0].data_ptr(), step,
                      SQRT1_2, Ly.stream())
-        # conditioner input grad of all blocks at once
-        dcond = empty(M, E, device=dev)
-        K.gemm([K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, L * 2 * C, pk["condT"], T)],
-               B, T, E, pk.bwd, dcond, E)
         # step-embedding MLP
         ddv = empty(B, C, device=dev)
         K.gemm([K.Seg(dd_all, L * C, L * C, pk["dpT"], B)], 1, B, C, pk.bwd, ddv, C)
@@ -408,7 +434,6 @@ class DiffNet(nn.Module):
         ip = self.input_projection
         wg(ip.weight, dpre0, C, st["xin"], st["ldx"], B, T, T, C, Mc)
         cs(dpre0, C, M, C, ip.bias)
-        return dcond
 
     # ---------------------------------------------------------------- reference API
     def forward(self, spec, diffusion_step, cond):

@@ -17,8 +17,11 @@ import torch
 from . import _lib
 from .kernels import PackedBuffer
 
-_STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None, "concurrent": True}
+_STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None, "concurrent": True,
+          "aux": os.environ.get("ENSVS_AUX_WGRAD", "0") != "0"}
 _SIDE_STREAMS = {}
+_AUX_STREAMS = {}
+_ACTIVE_BRANCHES = []
 # Dev instrumentation: set to a list to collect (branch, start_event, end_event) per
 # branch region (tools/branch_times.py); None = off.
 BRANCH_TIMES = None
@@ -74,12 +77,30 @@ class Branches:
             self.side = []
 
     def __enter__(self):
+        self.aux_used = []
+        self.keep = []
         if self.on_side:
             self.main = torch.cuda.current_stream(self.device)
             ev = self.main.record_event()
             for s in self.side:
                 s.wait_event(ev)
+        _ACTIVE_BRANCHES.append(self)
         return self
+
+    def aux(self):
+        """Fork an auxiliary stream from the current (branch) stream for work that only
+        produces parameter gradients; it is joined into the MAIN stream at exit.  (Joining
+        a nested fork back into its parent branch stream instead makes hipStreamEndCapture
+        segfault under HIP-graph capture on ROCm 7.2: tools/graph_fork_probe.py, DESIGN.md
+        §5.)"""
+        k = len(self.aux_used)
+        key = (str(self.device), k)
+        if key not in _AUX_STREAMS:
+            _AUX_STREAMS[key] = torch.cuda.Stream(self.device)
+        s = _AUX_STREAMS[key]
+        s.wait_event(torch.cuda.current_stream(self.device).record_event())
+        self.aux_used.append(s)
+        return torch.cuda.stream(s)
 
     def on(self, i):
         import contextlib
@@ -92,10 +113,35 @@ class Branches:
         return _timed(ctx, i)
 
     def __exit__(self, *exc):
+        _ACTIVE_BRANCHES.pop()
         if self.on_side:
-            for s in self.side:
+            for s in self.side + self.aux_used:
                 self.main.wait_stream(s)
+        # tensors an auxiliary stream reads were allocated on a branch stream: released only
+        # now, after the join, so the allocator cannot hand their blocks to later branch work
+        # while the auxiliary stream may still read them
+        self.keep = []
         return False
+
+
+def aux_stream(keep=()):
+    """Context for launches off a branch's critical path (weight / bias gradients): an
+    auxiliary stream forked from the current stream and joined at the end of the enclosing
+    Branches, or inline when branches run serially or auxiliary streams are off (the
+    default: ENSVS_AUX_WGRAD=1 turns them on; the DiffNet weight gradients beside the
+    encoder backward measured 24.8 vs 21.4 ms/step at 4 and at 8 hardware queues --
+    the recurrences slow down under the extra GEMM traffic).  ``keep``: objects
+    holding the tensors the enclosed launches read, kept alive until that join."""
+    import contextlib
+    if not _STATE["aux"] or not _ACTIVE_BRANCHES or not _ACTIVE_BRANCHES[-1].on_side:
+        return contextlib.nullcontext()
+    br = _ACTIVE_BRANCHES[-1]
+    br.keep.append(keep)
+    return br.aux()
+
+
+def set_aux_streams(on: bool):
+    _STATE["aux"] = bool(on)
 
 
 def next_seed() -> int:

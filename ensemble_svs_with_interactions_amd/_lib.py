@@ -50,14 +50,16 @@ SIGNATURES = {
                         c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_float, c_int, c_vp],
     "ensvs_conv_gemm_bf16a": [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
                               c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_float, c_int,
-                              c_int, c_vp],
+                              c_int, c_vp, c_ll, c_vp],
     "ensvs_conv_wgrad_bf16": [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_ll, c_ll, c_int,
                               c_float, c_vp],
     "ensvs_conv_gemm_bf16a_out": [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                                   c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_float,
-                                  c_int, c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_vp],
+                                  c_int, c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_vp,
+                                  c_ll, c_vp],
     "ensvs_set_big_tile": [c_int, c_int],
+    "ensvs_set_dual_small": [c_int],
     "ensvs_tile_colsum": [c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "ensvs_cast_bf16": [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_int, c_vp, c_int, c_vp],
     "ensvs_conv_wgrad": [c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,

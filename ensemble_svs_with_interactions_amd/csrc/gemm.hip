@@ -64,6 +64,10 @@ struct GemmArgs {
   // aux1 in bf16 (C ABI: bits EPI_AUX0_BF16 / EPI_AUX1_BF16 of `epi`)
   int aux0_bf, aux1_bf;
   int vec_out;  // Y / aux0 / aux1 rows 16-B aligned with ld % 4 == 0: 16-B epilogue stores
+  // GATE / RESSKIP: every bf16 output (gate/filter save, ybf) 16-B aligned with ld % 8 == 0:
+  // 8 channels per thread, 16-B bf16 stores (the 8-B ones made the epilogue store-issue
+  // bound)
+  int gate8;
   // optional bf16 copy of what is written to Y (LDS-staged epilogue only):
   // ybf[row*ybf_ld + col] = bf16(y + ybf_radd[(row / Tout)*ybf_radd_ld + col]) -- the next
   // GEMM's operand, rounded exactly as ensvs_cast_bf16 would, without the extra pass
@@ -76,6 +80,13 @@ struct GemmArgs {
   // rows g, g+8, .., g+120 (in order); ensvs_tile_colsum reproduces it for other paths
   float* csum;
   int csum_ld;
+  // split-K (small M, bf16-operand 128 x 128 kernel): workgroup z takes K-steps
+  // [nit * z / ksplit, nit * (z + 1) / ksplit) and stores its raw accumulator tile to
+  // part[(z * M + row) * Npad + col]; splitk_epilogue_kernel sums the slices in z order and
+  // runs the LDS-staged epilogue
+  float* part;
+  long long part_floats;
+  int ksplit;
 };
 
 template <typename T>
@@ -266,41 +277,153 @@ __device__ __forceinline__ void shadow4(const GemmArgs& a, int m, int col, f32x4
       bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
 }
 
+// NT threads share the element loops; only the waves with write_acc stage their
+// accumulators (the 8-wave small-M kernel: the K-group that holds the reduced tile).
+// 8 consecutive channels: bf16 copies as one 16-B store
+__device__ __forceinline__ void st8_bf(__bf16* p, f32x4 lo, f32x4 hi) {
+  *(bf16x8*)p = bf16x8{(__bf16)lo[0], (__bf16)lo[1], (__bf16)lo[2], (__bf16)lo[3],
+                       (__bf16)hi[0], (__bf16)hi[1], (__bf16)hi[2], (__bf16)hi[3]};
+}
+__device__ __forceinline__ void shadow8(const GemmArgs& a, int m, int col, f32x4 lo, f32x4 hi) {
+  if (!a.ybf) return;
+  if (a.ybf_radd) {
+    const float* r = a.ybf_radd + (long long)(m / a.Tout) * a.ybf_radd_ld + col;
+    lo += ld4(r);
+    hi += ld4(r + 4);
+  }
+  st8_bf(a.ybf + (long long)m * a.ybf_ld + col, lo, hi);
+}
+__device__ __forceinline__ void st8_aux0(const GemmArgs& a, long long i, f32x4 lo, f32x4 hi) {
+  if (a.aux0_bf) {
+    st8_bf((__bf16*)a.aux0 + i, lo, hi);
+  } else {
+    st4(a.aux0 + i, lo);
+    st4(a.aux0 + i + 4, hi);
+  }
+}
+
+// One row's 8 gate/filter channel pairs (GATE / GATE_TS epilogue): t points at the row's
+// staged accumulator tile, gc the tile column of the first gate value (filter +16), c the
+// first output channel.  (No global operand loads besides the bias, an L1 hit; the bias is
+// not held across rows: the 256 x 256 kernel keeps half its accumulators live here.)
+__device__ __forceinline__ void gate_row8(const GemmArgs& a, const float* t, int n0, int gc,
+                                          int m, int c) {
+  f32x4 g0 = ld4(t + gc), g1 = ld4(t + gc + 4), f0 = ld4(t + gc + 16), f1 = ld4(t + gc + 20);
+  if (a.bias) {
+    g0 += ld4(a.bias + n0 + gc);
+    g1 += ld4(a.bias + n0 + gc + 4);
+    f0 += ld4(a.bias + n0 + gc + 16);
+    f1 += ld4(a.bias + n0 + gc + 20);
+  }
+  f32x4 z0, z1;
+  if (a.epi == EPI_GATE) {
+    st8_aux0(a, (long long)m * a.ld0 + c, g0, g1);
+    st8_aux0(a, (long long)m * a.ld0 + a.C + c, f0, f1);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      z0[e] = fsigmoid_(g0[e]) * ftanh_(f0[e]);
+      z1[e] = fsigmoid_(g1[e]) * ftanh_(f1[e]);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      z0[e] = ftanh_(g0[e]) * fsigmoid_(f0[e]);
+      z1[e] = ftanh_(g1[e]) * fsigmoid_(f1[e]);
+    }
+  }
+  if (a.Y) {
+    st4(a.Y + (long long)m * a.ldy + c, z0);
+    st4(a.Y + (long long)m * a.ldy + c + 4, z1);
+  }
+  if (a.epi == EPI_GATE) shadow8(a, m, c, z0, z1);
+}
+
+// 8-channel GATE / GATE_TS rows of a staged tile: NTT threads, tile rows [0, ROWS), T row
+// stride ldT, ROWW 8-channel groups (threads) per row.
+template <int NTT, int ROWS, int ROWW>
+__device__ __forceinline__ void gate_tile8(const GemmArgs& a, const float* T, int ldT, int mb,
+                                           int n0, int tid) {
+  constexpr int NI = ROWS * ROWW / NTT;
+  static_assert(NTT % ROWW == 0 && NI >= 1, "gate8 geometry");
+  const int q8 = tid % ROWW, q = q8 >> 1, j = (q8 & 1) * 8;
+  const int c = n0 / 2 + q * 16 + j;
+  const int gc = q * 32 + j;
+  if (c >= a.C) return;
+#pragma unroll 1
+  for (int k = 0; k < NI; ++k) {
+    const int row = tid / ROWW + k * (NTT / ROWW);
+    const int m = mb + row;
+    if (m >= a.M) continue;
+    gate_row8(a, T + row * ldT, n0, gc, m, c);
+  }
+}
+
+template <int NT = NTHR>
 __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[4][4], int m0,
                                                   int n0, int wr, int wc, int lane, int tid,
-                                                  char* smem) {
+                                                  char* smem, bool write_acc = true) {
   if (a.epi == EPI_NONE) {
-    gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
+    if (write_acc) gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
     return;
   }
   float* T = (float*)smem;
   __syncthreads();  // every wave is done with the K-loop images
+  if (write_acc) {
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+      for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        T[(wr * 64 + mt * 16 + (lane >> 4) * 4 + r) * EP + wc * 64 + nt * 16 + (lane & 15)] =
-            acc[mt][nt][r];
+        for (int r = 0; r < 4; ++r)
+          T[(wr * 64 + mt * 16 + (lane >> 4) * 4 + r) * EP + wc * 64 + nt * 16 + (lane & 15)] =
+              acc[mt][nt][r];
+  }
   __syncthreads();
   const int M = a.M;
+  constexpr int EB = 2;  // rows whose operands are in flight together (register budget)
+  // Every thread keeps one column group across its rows (NT is a multiple of 32), so the
+  // bias is read once, and all of a thread's global operand loads (residual, skip, Y,
+  // gate/filter save) are issued before its first store: with the loads after the stores
+  // the compiler cannot reorder them (possible aliasing) and each row paid a full L2 / HBM
+  // latency -- 12 of 18 us of a 2 000-row GEMM (tools/small_gemm_probe.py).
+  if (a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS)) {
+    gate_tile8<NT, BM, 8>(a, T, EP, m0, n0, tid);  // 64 channels per row: 8 threads
+    return;
+  }
   if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
     // this tile holds 64 output channels (gate/filter interleaved by 16 in the packed columns)
-    for (int it = tid; it < BM * 16; it += NTHR) {
-      const int row = it >> 4, q4 = it & 15;
+    constexpr int NI = BM * 16 / NT;
+    const int q4 = tid & 15, q = q4 >> 2, j = (q4 & 3) * 4;
+    const int c = n0 / 2 + q * 16 + j;  // first of 4 output channels
+    const int gc = q * 32 + j;          // tile column of the gate values; filter at +16
+    if (c >= a.C) return;
+    f32x4 bg = {0.f, 0.f, 0.f, 0.f}, bfl = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias) {
+      bg = ld4(a.bias + n0 + gc);
+      bfl = ld4(a.bias + n0 + gc + 16);
+    }
+    static_assert(NI % EB == 0, "rows per thread in batches of EB");
+#pragma unroll 1
+    for (int kb = 0; kb < NI; kb += EB) {
+    f32x4 xr[EB], s0[EB];
+    if (a.epi == EPI_RESSKIP) {
+#pragma unroll
+      for (int k = 0; k < EB; ++k) {
+        const int m = m0 + (tid >> 4) + (kb + k) * (NT / 16);
+        if (m >= M) continue;
+        xr[k] = ld4(a.aux1 + (long long)m * a.ld1 + c);
+        if (a.accum) s0[k] = ld4(a.aux0 + (long long)m * a.ld0 + c);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < EB; ++k) {
+      const int row = (tid >> 4) + (kb + k) * (NT / 16);
       const int m = m0 + row;
-      const int q = q4 >> 2, j = (q4 & 3) * 4;
-      const int c = n0 / 2 + q * 16 + j;  // first of 4 output channels
-      if (m >= M || c >= a.C) continue;
-      const int gc = q * 32 + j;          // tile column of the gate values; filter at +16
+      if (m >= M) continue;
       f32x4 g = ld4(T + row * EP + gc), f = ld4(T + row * EP + gc + 16);
       if (a.bias) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          g[e] += a.bias[n0 + gc + e];
-          f[e] += a.bias[n0 + gc + 16 + e];
-        }
+        g += bg;
+        f += bfl;
       }
       if (a.epi == EPI_GATE) {
         st4_aux0(a, (long long)m * a.ld0 + c, g);
@@ -316,112 +439,139 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         for (int e = 0; e < 4; ++e) z[e] = ftanh_(g[e]) * fsigmoid_(f[e]);
         st4(a.Y + (long long)m * a.ldy + c, z);
       } else {
-        const f32x4 xr = ld4(a.aux1 + (long long)m * a.ld1 + c);
         f32x4 y, sk;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (xr[e] + g[e]) * 0.70710678118654752f;
+        for (int e = 0; e < 4; ++e) y[e] = (xr[k][e] + g[e]) * 0.70710678118654752f;
         st4(a.Y + (long long)m * a.ldy + c, y);
         shadow4(a, m, c, y);
-        float* skp = a.aux0 + (long long)m * a.ld0 + c;
         if (a.accum) {
-          const f32x4 s0 = ld4(skp);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) sk[e] = fmaf(a.alpha, f[e], s0[e]);
+          for (int e = 0; e < 4; ++e) sk[e] = fmaf(a.alpha, f[e], s0[k][e]);
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e) sk[e] = a.alpha * f[e];
         }
-        st4(skp, sk);
+        st4(a.aux0 + (long long)m * a.ld0 + c, sk);
       }
+    }
     }
     return;
   }
   // column sums: this thread always has columns cq*4.. and rows (tid >> 5) + 8k
   f32x4 cs0 = {0.f, 0.f, 0.f, 0.f}, cs1 = {0.f, 0.f, 0.f, 0.f};
-  for (int it = tid; it < BM * 32; it += NTHR) {
-    const int row = it >> 5, cq = it & 31;
-    const int m = m0 + row, col = n0 + cq * 4;
-    if (m >= M || col >= a.N) continue;
+  {
+    constexpr int NI = BM * 32 / NT;
+    const int cq = tid & 31, col = n0 + cq * 4;
     const int ne = min(4, a.N - col);
-    f32x4 v = ld4(T + row * EP + cq * 4);
-    if (a.csum && a.epi != EPI_GATE_BWD) cs0 += v;
-    if (a.bias) {
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias && ne > 0) {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        if (e < ne) v[e] += a.bias[col + e];
+        if (e < ne) bv[e] = a.bias[col + e];
     }
-    float* y = a.Y + (long long)m * a.ldy + col;
-    if (ne == 4) {
-      if (a.epi == EPI_PLAIN) {
-        if (a.accum) v += ld4(y);
+    const bool want1 = (a.epi == EPI_PLAIN && a.accum) || a.epi == EPI_ADDSCALE ||
+                       a.epi == EPI_RELU_MASK || a.epi == EPI_GATE_BWD;
+    const bool want2 = (a.epi == EPI_RELU_MASK && a.accum) || a.epi == EPI_GATE_BWD;
+    static_assert(NI % EB == 0, "rows per thread in batches of EB");
+#pragma unroll 1
+    for (int kb = 0; kb < NI; kb += EB) {
+    // operands of these rows, loaded before any of their stores
+    f32x4 p1[EB], p2[EB];
+    if (ne == 4 && (want1 || want2)) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (a.relu == 1) v[e] = fmaxf(v[e], 0.f);
-          else if (a.relu == 2) v[e] = sigmoidf_(v[e]);
-        }
-        st4(y, v);
-        shadow4(a, m, col, v);
-      } else if (a.epi == EPI_ADDSCALE) {
-        const f32x4 x1 = ld4(a.aux1 + (long long)m * a.ld1 + col);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = __builtin_fmaf(a.alpha, x1[e], v[e]);
-          v[e] = a.relu == 1 ? fmaxf(v[e], 0.f) : v[e];
-        }
-        st4(y, v);
-        shadow4(a, m, col, v);
-      } else if (a.epi == EPI_RELU_MASK) {
-        const f32x4 x1 = ld4(a.aux1 + (long long)m * a.ld1 + col);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = x1[e] > 0.f ? v[e] : 0.f;
-        if (a.accum) v += ld4(y);
-        st4(y, v);
-      } else if (a.epi == EPI_GATE_BWD) {
-        const f32x4 g = ld4_aux1(a, (long long)m * a.ld1 + col);
-        const f32x4 f = ld4_aux1(a, (long long)m * a.ld1 + a.C + col);
-        f32x4 dg, df;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float t0, t1;
-          gate_bwd_(v[e], g[e], f[e], t0, t1);
-          dg[e] = t0;
-          df[e] = t1;
-        }
-        if (a.csum) {
-          cs0 += dg;
-          cs1 += df;
-        }
-        if (a.Y) {
-          st4(y, dg);
-          st4(y + a.C, df);
-        }
-        shadow4(a, m, col, dg);
-        shadow4(a, m, a.C + col, df);
-      }
-    } else {
-      for (int e = 0; e < ne; ++e) {
-        float w = v[e];
-        float* ye = y + e;
+      for (int k = 0; k < EB; ++k) {
+        const int m = m0 + (tid >> 5) + (kb + k) * (NT / 32);
+        if (m >= M) continue;
+        const float* y = a.Y + (long long)m * a.ldy + col;
         if (a.epi == EPI_PLAIN) {
-          if (a.accum) w += *ye;
-          if (a.relu == 1) w = fmaxf(w, 0.f);
-          else if (a.relu == 2) w = sigmoidf_(w);
-          *ye = w;
-        } else if (a.epi == EPI_ADDSCALE) {
-          w = __builtin_fmaf(a.alpha, a.aux1[(long long)m * a.ld1 + col + e], w);
-          *ye = a.relu == 1 ? fmaxf(w, 0.f) : w;
-        } else if (a.epi == EPI_RELU_MASK) {
-          w = a.aux1[(long long)m * a.ld1 + col + e] > 0.f ? w : 0.f;
-          *ye = a.accum ? *ye + w : w;
+          p1[k] = ld4(y);
         } else if (a.epi == EPI_GATE_BWD) {
-          const float g = ld_aux1(a, (long long)m * a.ld1 + col + e);
-          const float f = ld_aux1(a, (long long)m * a.ld1 + a.C + col + e);
-          gate_bwd_(w, g, f, ye[0], ye[a.C]);
+          p1[k] = ld4_aux1(a, (long long)m * a.ld1 + col);
+          p2[k] = ld4_aux1(a, (long long)m * a.ld1 + a.C + col);
+        } else {
+          p1[k] = ld4(a.aux1 + (long long)m * a.ld1 + col);
+          if (want2) p2[k] = ld4(y);
         }
       }
+    }
+#pragma unroll
+    for (int k = 0; k < EB; ++k) {
+      const int row = (tid >> 5) + (kb + k) * (NT / 32);
+      const int m = m0 + row;
+      if (m >= M || ne <= 0) continue;
+      f32x4 v = ld4(T + row * EP + cq * 4);
+      if (a.csum && a.epi != EPI_GATE_BWD) cs0 += v;
+      if (a.bias) v += bv;
+      float* y = a.Y + (long long)m * a.ldy + col;
+      if (ne == 4) {
+        if (a.epi == EPI_PLAIN) {
+          if (a.accum) v += p1[k];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (a.relu == 1) v[e] = fmaxf(v[e], 0.f);
+            else if (a.relu == 2) v[e] = sigmoidf_(v[e]);
+          }
+          st4(y, v);
+          shadow4(a, m, col, v);
+        } else if (a.epi == EPI_ADDSCALE) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = __builtin_fmaf(a.alpha, p1[k][e], v[e]);
+            v[e] = a.relu == 1 ? fmaxf(v[e], 0.f) : v[e];
+          }
+          st4(y, v);
+          shadow4(a, m, col, v);
+        } else if (a.epi == EPI_RELU_MASK) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = p1[k][e] > 0.f ? v[e] : 0.f;
+          if (a.accum) v += p2[k];
+          st4(y, v);
+        } else if (a.epi == EPI_GATE_BWD) {
+          f32x4 dg, df;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float t0, t1;
+            gate_bwd_(v[e], p1[k][e], p2[k][e], t0, t1);
+            dg[e] = t0;
+            df[e] = t1;
+          }
+          if (a.csum) {
+            cs0 += dg;
+            cs1 += df;
+          }
+          if (a.Y) {
+            st4(y, dg);
+            st4(y + a.C, df);
+          }
+          shadow4(a, m, col, dg);
+          shadow4(a, m, a.C + col, df);
+        }
+      } else {
+        for (int e = 0; e < ne; ++e) {
+          float w = v[e];
+          float* ye = y + e;
+          if (a.epi == EPI_PLAIN) {
+            if (a.accum) w += *ye;
+            if (a.relu == 1) w = fmaxf(w, 0.f);
+            else if (a.relu == 2) w = sigmoidf_(w);
+            *ye = w;
+          } else if (a.epi == EPI_ADDSCALE) {
+            w = __builtin_fmaf(a.alpha, a.aux1[(long long)m * a.ld1 + col + e], w);
+            *ye = a.relu == 1 ? fmaxf(w, 0.f) : w;
+          } else if (a.epi == EPI_RELU_MASK) {
+            w = a.aux1[(long long)m * a.ld1 + col + e] > 0.f ? w : 0.f;
+            *ye = a.accum ? *ye + w : w;
+          } else if (a.epi == EPI_GATE_BWD) {
+            const float g = ld_aux1(a, (long long)m * a.ld1 + col + e);
+            const float f = ld_aux1(a, (long long)m * a.ld1 + a.C + col + e);
+            gate_bwd_(w, g, f, ye[0], ye[a.C]);
+          }
+        }
+      }
+    }
     }
   }
-  if (a.csum) {  // uniform: every thread reaches the barrier
+  if (NT == NTHR && a.csum) {  // uniform: every thread reaches the barrier
     float* X = T + BM * EP;  // [group][2*BN]
     const int g = tid >> 5, c4 = (tid & 31) * 4;
     *(f32x4*)(X + g * 2 * BN + c4) = cs0;
@@ -773,9 +923,26 @@ __global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a
   const int c8[4] = {cq8a, cq8b, cq8a, cq8b};
 
   int qs = 0, qj = 0, qkc = 0;  // staging cursor (segment, tap, k-step)
+  int nloc = nit;
+  if (a.ksplit > 1) {  // this split's K-steps: advance the cursor to the first one
+    const int z = blockIdx.z;
+    const int i0 = (int)((long long)nit * z / a.ksplit);
+    nloc = (int)((long long)nit * (z + 1) / a.ksplit) - i0;
+    for (int i = 0; i < i0; ++i) {
+      const int nks_ = qs == 0 ? S0.nk : (qs == 1 ? S1.nk : S2.nk);
+      const int taps_ = qs == 0 ? S0.taps : (qs == 1 ? S1.taps : S2.taps);
+      if (++qkc == nks_) {
+        qkc = 0;
+        if (++qj == taps_) {
+          qj = 0;
+          ++qs;
+        }
+      }
+    }
+  }
 #define TAP_PTRS(S) \
   tap_ptrs(S, qj, Npad, n0, rl, cq8a, cq8b, bt[0], bt[1], bt[2], bt[3], tt[0], tt[1], tt[2], tt[3], okm)
-  TapPtrs P = TAP_PTRS(S0);
+  TapPtrs P = qs == 0 ? TAP_PTRS(S0) : (qs == 1 ? TAP_PTRS(S1) : TAP_PTRS(S2));
 #define ISSUE(it)                                                                        \
   do {                                                                                   \
     char* As_ = smem + ((it) % STAGES) * 2 * TILE + wid * 32 * 128;                      \
@@ -809,21 +976,21 @@ __global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a
 
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
-    if (p < nit) ISSUE(p);
+    if (p < nloc) ISSUE(p);
   const int arow = lane & 15, kq = lane >> 4;
   // fragment read offsets: rows ra + 16i share swz(ra, .), so i only adds 2048 B
   const int ra = wr * 64 + arow, rbr = wc * 64 + arow;
   const int oa0 = ra * 128 + swz(ra, kq) * 16, oa1 = ra * 128 + swz(ra, kq + 4) * 16;
   const int ob0 = TILE + rbr * 128 + swz(rbr, kq) * 16, ob1 = TILE + rbr * 128 + swz(rbr, kq + 4) * 16;
-  for (int it = 0; it < nit; ++it) {
+  for (int it = 0; it < nloc; ++it) {
     if constexpr (STAGES == 3) {
-      if (it + 1 < nit) wait_vm<GL>();
+      if (it + 1 < nloc) wait_vm<GL>();
       else wait_vm<0>();
     } else {
       wait_vm<0>();
     }
     __builtin_amdgcn_s_barrier();  // tile `it` visible; every wave is done with tile it-1
-    if (it + STAGES - 1 < nit) ISSUE(it + STAGES - 1);
+    if (it + STAGES - 1 < nloc) ISSUE(it + STAGES - 1);
     // (both 32-halves always: a zero half adds exact zeros, and a data-dependent skip
     // makes hipcc move the accumulators out of AGPRs every iteration)
     const char* St = smem + (it % STAGES) * 2 * TILE;
@@ -849,8 +1016,179 @@ __global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a
   }
 #undef ISSUE
 #undef TAP_PTRS
+  if (a.ksplit > 1) {  // raw partial tile of this K split
+    float* pz = a.part + (long long)blockIdx.z * M * Npad;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          pz[(long long)row * Npad + n0 + wc * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+      }
+    return;
+  }
   if (a.vec_out) gemm_epilogue_lds(a, acc, m0, n0, wr, wc, lane, tid, smem);
   else gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
+}
+
+// ------------------------------------------- 128 x 128, two K-groups of 4 waves (small M)
+// Small-M launches (a 2 000-frame reverse-diffusion GEMM is 64 tiles: a quarter of the CUs)
+// are bound by what ONE workgroup issues per K-step -- 8 LDS-DMA pieces and 32 MFMAs per
+// wave (MI355X_MICROARCH.md: a DMA piece costs 60-185 issue cycles) -- not by load
+// latency (three stages measured 3 % faster than two) or bytes.  Here 8 waves form two
+// K-groups: group g stages and multiplies K-steps g, g+2, g+4, .. into its own 64 x 64
+// sub-tile accumulators (its own half of each LDS stage), so a tile's K loop takes half the
+// per-wave issue; the groups' tiles are added through LDS (acc0 + acc1: the sum differs from
+// the one-group order only by fp32 rounding) and all 8 waves run the LDS-staged epilogue.
+constexpr int NTHR2 = 2 * NTHR;
+
+__global__ __launch_bounds__(NTHR2) void conv_gemm_b16_dual_kernel(const GemmArgs a) {
+  constexpr int TILE = BM * BK2 * 2;      // bytes of one operand image (16 KB)
+  constexpr int GSET = 2 * TILE;          // one K-group's A + B images
+  constexpr int STAGE = 2 * GSET;         // both groups
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
+  const int kg = wid >> 2, w4 = wid & 3;  // K-group, wave within the group
+  const int wr = w4 >> 1, wc = w4 & 1;
+  int m0, n0;
+  xcd_tile(m0, n0);
+  const int M = a.M, Tout = a.Tout, Npad = a.Npad;
+  const int nseg = a.nseg;
+  const SegU S0 = seg_u(a.seg[0], a.W);
+  const SegU S1 = nseg > 1 ? seg_u(a.seg[1], a.W) : S0;
+  const SegU S2 = nseg > 2 ? seg_u(a.seg[2], a.W) : S0;
+  const int nit = S0.nk * S0.taps + (nseg > 1 ? S1.nk * S1.taps : 0) +
+                  (nseg > 2 ? S2.nk * S2.taps : 0);
+  const int nmine = (nit - kg + 1) / 2;  // K-steps kg, kg+2, ..
+  const int npair = (nit + 1) / 2;
+
+  const int rl = w4 * 32 + (lane >> 3), slot = lane & 7;
+  const int cq = swz(rl, slot), cq8a = cq * 8, cq8b = (cq ^ 4) * 8;
+  int bt[4], tt[4];
+  unsigned okm = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + rl + 8 * i;
+    const bool ok = m < M;
+    bt[i] = ok ? m / Tout : 0;
+    tt[i] = ok ? m - bt[i] * Tout : 0;
+    okm |= ok ? (1u << i) : 0u;
+  }
+  unsigned long long zpu = (unsigned long long)(const void*)g_zero;
+  asm volatile("" : "+s"(zpu));
+  const char* zp = (const char*)zpu;
+  const int c8[4] = {cq8a, cq8b, cq8a, cq8b};
+
+  int qs = 0, qj = 0, qkc = 0;
+#define ADV()                                                                      \
+  do {                                                                             \
+    const int nks_ = qs == 0 ? S0.nk : (qs == 1 ? S1.nk : S2.nk);                  \
+    const int taps_ = qs == 0 ? S0.taps : (qs == 1 ? S1.taps : S2.taps);           \
+    if (++qkc == nks_) {                                                           \
+      qkc = 0;                                                                     \
+      if (++qj == taps_) {                                                         \
+        qj = 0;                                                                    \
+        ++qs;                                                                      \
+      }                                                                            \
+    }                                                                              \
+  } while (0)
+  if (kg == 1 && nit > 0) ADV();  // group 1 starts at K-step 1
+#define TAP_PTRS(S) \
+  tap_ptrs(S, qj, Npad, n0, rl, cq8a, cq8b, bt[0], bt[1], bt[2], bt[3], tt[0], tt[1], tt[2], tt[3], okm)
+  TapPtrs P = qs == 0 ? TAP_PTRS(S0) : (qs == 1 ? TAP_PTRS(S1) : TAP_PTRS(S2));
+  // issue this group's next K-step into stage `st`, then step the cursor over the other
+  // group's K-step (pointers rebuilt when a tap / segment boundary is crossed)
+#define ISSUE2(st)                                                                       \
+  do {                                                                                   \
+    char* As_ = smem + (st) * STAGE + kg * GSET + w4 * 32 * 128;                         \
+    const int kb_ = qkc * BK2;                                                           \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                      \
+      const bool oa = ((P.va >> i) & 1) && kb_ + c8[i] < P.K;                            \
+      glds16(oa ? (const void*)(P.pa[i] + kb_ * 2) : (const void*)zp, As_ + i * 1024);   \
+    }                                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                      \
+      const bool ob = kb_ + c8[i] < P.Kp;                                                \
+      glds16(ob ? (const void*)(P.pb[i] + kb_ * 2) : (const void*)zp,                    \
+             As_ + TILE + i * 1024);                                                     \
+    }                                                                                    \
+    const int qs0_ = qs, qj0_ = qj;                                                      \
+    ADV();                                                                               \
+    if (qs < nseg) ADV();                                                                \
+    if (qs < nseg && (qs != qs0_ || qj != qj0_))                                         \
+      P = qs == 0 ? TAP_PTRS(S0) : (qs == 1 ? TAP_PTRS(S1) : TAP_PTRS(S2));              \
+  } while (0)
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nmine > 0) ISSUE2(0);
+  const int arow = lane & 15, kq = lane >> 4;
+  const int ra = wr * 64 + arow, rbr = wc * 64 + arow;
+  const int oa0 = ra * 128 + swz(ra, kq) * 16, oa1 = ra * 128 + swz(ra, kq + 4) * 16;
+  const int ob0 = TILE + rbr * 128 + swz(rbr, kq) * 16, ob1 = TILE + rbr * 128 + swz(rbr, kq + 4) * 16;
+  for (int p = 0; p < npair; ++p) {
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // pair p visible; every wave is done with pair p-1
+    if (p + 1 < nmine) ISSUE2((p + 1) & 1);
+    if (p < nmine) {
+      const char* St = smem + (p & 1) * STAGE + kg * GSET;
+      bf16x8 fa[2][4], fb[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          fa[h][i] = *(const bf16x8*)(St + (h ? oa1 : oa0) + i * 2048);
+          fb[h][i] = *(const bf16x8*)(St + (h ? ob1 : ob0) + i * 2048);
+        }
+      __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[h][i], fb[h][j], acc[i][j], 0, 0, 0);
+    }
+  }
+#undef ISSUE2
+#undef TAP_PTRS
+#undef ADV
+  // group 1's tile through LDS into group 0's accumulators
+  float* T = (float*)smem;
+  __syncthreads();
+  if (kg == 1) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          T[(wr * 64 + mt * 16 + (lane >> 4) * 4 + r) * EP + wc * 64 + nt * 16 + (lane & 15)] =
+              acc[mt][nt][r];
+  }
+  __syncthreads();
+  if (kg == 0) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[mt][nt][r] +=
+              T[(wr * 64 + mt * 16 + (lane >> 4) * 4 + r) * EP + wc * 64 + nt * 16 + (lane & 15)];
+  }
+  if (a.vec_out) {
+    gemm_epilogue_lds<NTHR2>(a, acc, m0, n0, wr, wc, lane, tid, smem, kg == 0);
+  } else if (kg == 0) {
+    gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
+  }
 }
 
 // ------------------------------------------------------ 256 x 256 bf16-operand GEMM
@@ -879,26 +1217,50 @@ __device__ __forceinline__ void xcd_tile_big(int& m0, int& n0) {
 __device__ __forceinline__ void epilogue_chunk_big(const GemmArgs& a, const float* T, int mb,
                                                    int n0, int tid) {
   const int M = a.M;
+  constexpr int EB = 2;  // rows whose operands are in flight together (register budget)
   if (a.epi == EPI_NONE) {
     if (T[tid] == 12345.678f && mb < 0) a.Y[0] = T[tid + 1];
     return;
   }
+  // as gemm_epilogue_lds: a fixed column group per thread, bias read once, every global
+  // operand load of the thread's rows issued before its first store
+  if (a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS)) {
+    gate_tile8<NTHRB, CHR, BNB / 16>(a, T, EPB, mb, n0, tid);  // 128 channels: 16 threads
+    return;
+  }
   if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
     // BNB / 2 output channels per row: gate/filter interleaved by 16 in the packed columns
-    for (int it = tid; it < CHR * (BNB / 8); it += NTHRB) {
-      const int row = it / (BNB / 8), q4 = it % (BNB / 8);
+    constexpr int NI = CHR * (BNB / 8) / NTHRB;
+    const int q4 = tid % (BNB / 8), q = q4 >> 2, j = (q4 & 3) * 4;
+    const int c = n0 / 2 + q * 16 + j;
+    const int gc = q * 32 + j;
+    if (c >= a.C) return;
+    f32x4 bg = {0.f, 0.f, 0.f, 0.f}, bfl = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias) {
+      bg = ld4(a.bias + n0 + gc);
+      bfl = ld4(a.bias + n0 + gc + 16);
+    }
+#pragma unroll 1
+    for (int kb = 0; kb < NI; kb += EB) {
+    f32x4 xr[EB], s0[EB];
+    if (a.epi == EPI_RESSKIP) {
+#pragma unroll
+      for (int k = 0; k < EB; ++k) {
+        const int m = mb + tid / (BNB / 8) + (kb + k) * (NTHRB / (BNB / 8));
+        if (m >= M) continue;
+        xr[k] = ld4(a.aux1 + (long long)m * a.ld1 + c);
+        if (a.accum) s0[k] = ld4(a.aux0 + (long long)m * a.ld0 + c);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < EB; ++k) {
+      const int row = tid / (BNB / 8) + (kb + k) * (NTHRB / (BNB / 8));
       const int m = mb + row;
-      const int q = q4 >> 2, j = (q4 & 3) * 4;
-      const int c = n0 / 2 + q * 16 + j;
-      if (m >= M || c >= a.C) continue;
-      const int gc = q * 32 + j;
+      if (m >= M) continue;
       f32x4 g = ld4(T + row * EPB + gc), f = ld4(T + row * EPB + gc + 16);
       if (a.bias) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          g[e] += a.bias[n0 + gc + e];
-          f[e] += a.bias[n0 + gc + 16 + e];
-        }
+        g += bg;
+        f += bfl;
       }
       if (a.epi == EPI_GATE) {
         st4_aux0(a, (long long)m * a.ld0 + c, g);
@@ -914,41 +1276,69 @@ __device__ __forceinline__ void epilogue_chunk_big(const GemmArgs& a, const floa
         for (int e = 0; e < 4; ++e) z[e] = ftanh_(g[e]) * fsigmoid_(f[e]);
         st4(a.Y + (long long)m * a.ldy + c, z);
       } else {
-        const f32x4 xr = ld4(a.aux1 + (long long)m * a.ld1 + c);
         f32x4 y, sk;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (xr[e] + g[e]) * 0.70710678118654752f;
+        for (int e = 0; e < 4; ++e) y[e] = (xr[k][e] + g[e]) * 0.70710678118654752f;
         st4(a.Y + (long long)m * a.ldy + c, y);
         shadow4(a, m, c, y);
-        float* skp = a.aux0 + (long long)m * a.ld0 + c;
         if (a.accum) {
-          const f32x4 s0 = ld4(skp);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) sk[e] = fmaf(a.alpha, f[e], s0[e]);
+          for (int e = 0; e < 4; ++e) sk[e] = fmaf(a.alpha, f[e], s0[k][e]);
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e) sk[e] = a.alpha * f[e];
         }
-        st4(skp, sk);
+        st4(a.aux0 + (long long)m * a.ld0 + c, sk);
       }
+    }
     }
     return;
   }
-  for (int it = tid; it < CHR * (BNB / 4); it += NTHRB) {
-    const int row = it / (BNB / 4), cq = it % (BNB / 4);
-    const int m = mb + row, col = n0 + cq * 4;
-    if (m >= M || col >= a.N) continue;
-    const int ne = min(4, a.N - col);
-    f32x4 v = ld4(T + row * EPB + cq * 4);
-    if (a.bias) {
+  constexpr int NI = CHR * (BNB / 4) / NTHRB;
+  const int cq = tid % (BNB / 4), col = n0 + cq * 4;
+  const int ne = min(4, a.N - col);
+  if (ne <= 0) return;
+  f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+  if (a.bias) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (e < ne) v[e] += a.bias[col + e];
+    for (int e = 0; e < 4; ++e)
+      if (e < ne) bv[e] = a.bias[col + e];
+  }
+  const bool want1 = (a.epi == EPI_PLAIN && a.accum) || a.epi == EPI_ADDSCALE ||
+                     a.epi == EPI_RELU_MASK || a.epi == EPI_GATE_BWD;
+  const bool want2 = (a.epi == EPI_RELU_MASK && a.accum) || a.epi == EPI_GATE_BWD;
+  static_assert(NI % EB == 0, "rows per thread in batches of EB");
+#pragma unroll 1
+  for (int kb = 0; kb < NI; kb += EB) {
+  f32x4 p1[EB], p2[EB];
+  if (ne == 4 && (want1 || want2)) {
+#pragma unroll
+    for (int k = 0; k < EB; ++k) {
+      const int m = mb + tid / (BNB / 4) + (kb + k) * (NTHRB / (BNB / 4));
+      if (m >= M) continue;
+      const float* y = a.Y + (long long)m * a.ldy + col;
+      if (a.epi == EPI_PLAIN) {
+        p1[k] = ld4(y);
+      } else if (a.epi == EPI_GATE_BWD) {
+        p1[k] = ld4_aux1(a, (long long)m * a.ld1 + col);
+        p2[k] = ld4_aux1(a, (long long)m * a.ld1 + a.C + col);
+      } else {
+        p1[k] = ld4(a.aux1 + (long long)m * a.ld1 + col);
+        if (want2) p2[k] = ld4(y);
+      }
     }
+  }
+#pragma unroll
+  for (int k = 0; k < EB; ++k) {
+    const int row = tid / (BNB / 4) + (kb + k) * (NTHRB / (BNB / 4));
+    const int m = mb + row;
+    if (m >= M) continue;
+    f32x4 v = ld4(T + row * EPB + cq * 4);
+    if (a.bias) v += bv;
     float* y = a.Y + (long long)m * a.ldy + col;
     if (ne == 4) {
       if (a.epi == EPI_PLAIN) {
-        if (a.accum) v += ld4(y);
+        if (a.accum) v += p1[k];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           if (a.relu == 1) v[e] = fmaxf(v[e], 0.f);
@@ -957,28 +1347,24 @@ __device__ __forceinline__ void epilogue_chunk_big(const GemmArgs& a, const floa
         st4(y, v);
         shadow4(a, m, col, v);
       } else if (a.epi == EPI_ADDSCALE) {
-        const f32x4 x1 = ld4(a.aux1 + (long long)m * a.ld1 + col);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = __builtin_fmaf(a.alpha, x1[e], v[e]);
+          v[e] = __builtin_fmaf(a.alpha, p1[k][e], v[e]);
           v[e] = a.relu == 1 ? fmaxf(v[e], 0.f) : v[e];
         }
         st4(y, v);
         shadow4(a, m, col, v);
       } else if (a.epi == EPI_RELU_MASK) {
-        const f32x4 x1 = ld4(a.aux1 + (long long)m * a.ld1 + col);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = x1[e] > 0.f ? v[e] : 0.f;
-        if (a.accum) v += ld4(y);
+        for (int e = 0; e < 4; ++e) v[e] = p1[k][e] > 0.f ? v[e] : 0.f;
+        if (a.accum) v += p2[k];
         st4(y, v);
       } else if (a.epi == EPI_GATE_BWD) {
-        const f32x4 g = ld4_aux1(a, (long long)m * a.ld1 + col);
-        const f32x4 f = ld4_aux1(a, (long long)m * a.ld1 + a.C + col);
         f32x4 dg, df;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float t0, t1;
-          gate_bwd_(v[e], g[e], f[e], t0, t1);
+          gate_bwd_(v[e], p1[k][e], p2[k][e], t0, t1);
           dg[e] = t0;
           df[e] = t1;
         }
@@ -1011,6 +1397,7 @@ __device__ __forceinline__ void epilogue_chunk_big(const GemmArgs& a, const floa
         }
       }
     }
+  }
   }
 }
 
@@ -1113,22 +1500,50 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_big_kernel(const GemmArgs
   // epilogue: four 64-row chunks staged through LDS (row stride EPB floats)
   float* T = (float*)smem;
   __syncthreads();
-#pragma unroll
+  // (the chunk loop is not unrolled -- its body is large -- so the accumulator half is
+  // picked by a branch with static indices, never by a runtime index into acc)
+#define STAGE_HALF(H)                                                                     \
+  _Pragma("unroll") for (int mt2 = 0; mt2 < 4; ++mt2)                                     \
+  _Pragma("unroll") for (int nt = 0; nt < 4; ++nt)                                        \
+  _Pragma("unroll") for (int r = 0; r < 4; ++r)                                           \
+      T[(mt2 * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] =        \
+          acc[(H) * 4 + mt2][nt][r]
+#pragma unroll 1
   for (int c = 0; c < BMB / CHR; ++c) {
     if (wr == (c >> 1)) {
-#pragma unroll
-      for (int mt2 = 0; mt2 < 4; ++mt2)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            T[(mt2 * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] =
-                acc[(c & 1) * 4 + mt2][nt][r];
+      if (c & 1) {
+        STAGE_HALF(1);
+      } else {
+        STAGE_HALF(0);
+      }
     }
     __syncthreads();
     epilogue_chunk_big(a, T, m0 + c * CHR, n0, tid);
     __syncthreads();
   }
+#undef STAGE_HALF
+}
+
+// Split-K reduction + epilogue: 64 rows x 256 columns per block, the ksplit partial slices
+// summed in slice order into an LDS tile (columns past Npad read as zero), then the same
+// per-element epilogue as the 256 x 256 kernel.
+__global__ __launch_bounds__(NTHRB) void splitk_epilogue_kernel(const GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* T = (float*)smem;
+  const int mb = blockIdx.x * CHR, n0 = blockIdx.y * BNB, tid = threadIdx.x;
+  const int M = a.M, Npad = a.Npad;
+  for (int e = tid; e < CHR * (BNB / 4); e += NTHRB) {
+    const int row = e / (BNB / 4), c4 = e % (BNB / 4);
+    const int m = mb + row, n = n0 + c4 * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (m < M && n < Npad) {
+      for (int z = 0; z < a.ksplit; ++z)
+        v += *(const f32x4*)(a.part + ((long long)z * M + m) * Npad + n);
+    }
+    *(f32x4*)(T + row * EPB + c4 * 4) = v;
+  }
+  __syncthreads();
+  epilogue_chunk_big(a, T, mb, n0, tid);
 }
 
 // ---------------------------------------- 256 x 256, 32-deep K steps, S-stage ring
@@ -1281,22 +1696,26 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_ring_kernel(const GemmArg
 #undef TAP_PTRS2
   float* T = (float*)smem;
   __syncthreads();
-#pragma unroll
+#define STAGE_HALF(H)                                                                     \
+  _Pragma("unroll") for (int mt2 = 0; mt2 < 4; ++mt2)                                     \
+  _Pragma("unroll") for (int nt = 0; nt < 4; ++nt)                                        \
+  _Pragma("unroll") for (int r = 0; r < 4; ++r)                                           \
+      T[(mt2 * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] =        \
+          acc[(H) * 4 + mt2][nt][r]
+#pragma unroll 1
   for (int cch = 0; cch < BMB / CHR; ++cch) {
     if (wr == (cch >> 1)) {
-#pragma unroll
-      for (int mt2 = 0; mt2 < 4; ++mt2)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            T[(mt2 * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] =
-                acc[(cch & 1) * 4 + mt2][nt][r];
+      if (cch & 1) {
+        STAGE_HALF(1);
+      } else {
+        STAGE_HALF(0);
+      }
     }
     __syncthreads();
     epilogue_chunk_big(a, T, m0 + cch * CHR, n0, tid);
     __syncthreads();
   }
+#undef STAGE_HALF
 }
 
 // y[m][k] = bf16(x[m][k] + radd[m / T][k]) for the bf16-activation GEMM (8 elements per thread).
@@ -1862,6 +2281,12 @@ static int fill_gemm_args(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int
   auto al8 = [](const void* p, int ld) { return !p || ((((uintptr_t)p) & 7) == 0 && ld % 4 == 0); };
   a.vec_out = al(Y, ldy) && (a.aux0_bf ? al8(aux0, ld0) : al(aux0, ld0)) &&
               (a.aux1_bf ? al8(aux1, ld1) : al(aux1, ld1)) && (C % 4 == 0);
+  static const int gate8_on = [] {
+    const char* e = getenv("ENSVS_GATE8");  // A/B switch for the 8-channel gate epilogue
+    return e ? atoi(e) : 1;
+  }();
+  a.gate8 = gate8_on && a.vec_out && C % 8 == 0 &&
+            (!a.aux0_bf || (((uintptr_t)aux0 & 15) == 0 && ld0 % 8 == 0));
   return ENSVS_OK;
 }
 
@@ -1909,6 +2334,11 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
 // Gate GEMM (tools/gate_probe.py): 2 -> 44.8 us, 1 (5 / 4 / 3 stages) -> 53.3 / 53.0 /
 // 50.2 us, 0 (128 x 128) -> 51.0 us: more LDS stages in flight did not pay.
 static int g_big_tile = -1, g_big_stages = 5;
+// split-K fills about this many workgroups (ENSVS_SPLITK=0 turns it off)
+static const int SPLITK_TARGET = 256;
+// launches of fewer than 128 tiles of 128 x 128 run the two-K-group kernel (-1: not read
+// yet; ENSVS_DUAL_SMALL, default 1; ensvs_set_dual_small)
+static int g_dual_small = -1;
 
 static bool use_big_tile(const GemmArgs& a) {
   if (g_big_tile < 0) {
@@ -1963,9 +2393,40 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     ENSVS_CHECK_LAUNCH();
     return ENSVS_OK;
   }
+  // small M: split K over up to 8 workgroups per output tile so the launch fills the chip
+  // (a 2 000-frame DiffNet GEMM is 64 tiles of 128 x 128; each tile's 16 K-steps would run
+  // serially on one CU).  Needs a caller workspace for ksplit x M x Npad fp32 partials.
+  static const bool splitk_on = [] {
+    const char* e = getenv("ENSVS_SPLITK");
+    return !(e && e[0] == '0');
+  }();
+  if (splitk_on && a.part && !a.csum && a.vec_out && a.epi != EPI_NONE) {
+    const long long tiles = (long long)grid.x * grid.y;
+    int nit = 0;
+    for (int s = 0; s < nseg; ++s) nit += cdiv(segs[s].K, BK2) * segs[s].taps;
+    int S = (int)std::min<long long>(8, (SPLITK_TARGET + tiles - 1) / tiles);
+    S = std::min(S, nit / 2);
+    while (S > 1 && (long long)S * a.M * Npad > a.part_floats) --S;
+    if (S > 1 && tiles < SPLITK_TARGET / 2) a.ksplit = S;
+  }
   const size_t lds = (size_t)2 * BM * BK2 * 2;  // one stage (A + B images)
   // the LDS-staged epilogue reuses the stage buffers for the fp32 output tile
   const size_t l2 = std::max<size_t>(2 * lds, EPI_LDS), l3 = std::max<size_t>(3 * lds, EPI_LDS);
+  if (a.ksplit > 1) grid.z = a.ksplit;
+  if (g_dual_small < 0) {
+    const char* e = getenv("ENSVS_DUAL_SMALL");
+    g_dual_small = e ? atoi(e) : 1;
+  }
+  if (g_dual_small && a.ksplit <= 1 && !a.csum && (long long)grid.x * grid.y < 128) {
+    const size_t ld2 = std::max<size_t>(4 * lds, EPI_LDS);  // 2 stages x 2 K-groups
+    static const hipError_t ed = hipFuncSetAttribute(
+        (const void*)conv_gemm_b16_dual_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)ld2);
+    if (ed != hipSuccess) return ENSVS_E_HIP;
+    hipLaunchKernelGGL(conv_gemm_b16_dual_kernel, grid, dim3(NTHR2), ld2, st, a);
+    ENSVS_CHECK_LAUNCH();
+    return ENSVS_OK;
+  }
   if (stages == 2) {
     static const hipError_t e2 = hipFuncSetAttribute((const void*)conv_gemm_b16_kernel<2>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1982,6 +2443,20 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     return ENSVS_E_ARG;
   }
   ENSVS_CHECK_LAUNCH();
+  if (a.ksplit > 1) {
+    const size_t le = (size_t)CHR * EPB * 4;
+    static const hipError_t ee = hipFuncSetAttribute(
+        (const void*)splitk_epilogue_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)le);
+    if (ee != hipSuccess) return ENSVS_E_HIP;
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(cdiv(a.M, CHR), cdiv(Npad, BNB)),
+                       dim3(NTHRB), le, st, a);
+    ENSVS_CHECK_LAUNCH();
+  }
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_set_dual_small(int on) {
+  g_dual_small = on ? 1 : 0;
   return ENSVS_OK;
 }
 
@@ -1996,11 +2471,13 @@ ENSVS_API int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B,
                                     int Npad, const void* W, const float* bias, float* Y, int ldy,
                                     int epi, int relu, int accum, float* aux0, int ld0,
                                     const float* aux1, int ld1, float alpha, int C, int stages,
-                                    void* stream) {
+                                    float* part, long long part_floats, void* stream) {
   GemmArgs a{};
   const int rc = fill_gemm_args(a, segs, nseg, B, Tout, N, Npad, W, bias, Y, ldy, epi, relu,
                                 accum, aux0, ld0, aux1, ld1, alpha, C);
   if (rc != ENSVS_OK) return rc;
+  a.part = part;
+  a.part_floats = part ? part_floats : 0;
   return launch_b16(a, segs, nseg, B, Npad, W, stages, (hipStream_t)stream);
 }
 
@@ -2013,11 +2490,14 @@ ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, in
                                         float* aux0, int ld0, const float* aux1, int ld1,
                                         float alpha, int C, void* ybf, int ybf_ld,
                                         const float* ybf_radd, int ybf_radd_ld, float* csum,
-                                        int csum_ld, int stages, void* stream) {
+                                        int csum_ld, int stages, float* part,
+                                        long long part_floats, void* stream) {
   GemmArgs a{};
   const int rc = fill_gemm_args(a, segs, nseg, B, Tout, N, Npad, W, bias, Y, ldy, epi, relu,
                                 accum, aux0, ld0, aux1, ld1, alpha, C);
   if (rc != ENSVS_OK) return rc;
+  a.part = part;
+  a.part_floats = part ? part_floats : 0;
   if (csum) {
     if (!a.vec_out || a.M % BM || N % 4 || csum_ld < (a.epi == EPI_GATE_BWD ? 2 * C : N) ||
         (a.epi != EPI_PLAIN && a.epi != EPI_ADDSCALE && a.epi != EPI_RELU_MASK &&
@@ -2037,6 +2517,7 @@ ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, in
     a.ybf_ld = ybf_ld;
     a.ybf_radd = ybf_radd;
     a.ybf_radd_ld = ybf_radd_ld;
+    a.gate8 = a.gate8 && ((uintptr_t)ybf & 15) == 0 && ybf_ld % 8 == 0;
   }
   return launch_b16(a, segs, nseg, B, Npad, W, stages, (hipStream_t)stream);
 }

@@ -148,8 +148,15 @@ class Seg:
 # Single-reuse GEMMs (one tap, one N tile) stay register-staged: ENSVS_BF16_MIN_REUSE=1
 # measured 22.0 vs 21.9 ms/step and ensemble RTF 0.0305 vs 0.0294.
 BF16_ACT = {"on": True, "stages": 2,
+            "stages_small": int(os.environ.get("ENSVS_STAGES_SMALL", "2")),
             "min_reuse": int(os.environ.get("ENSVS_BF16_MIN_REUSE", "2")),
             "min_rows": int(os.environ.get("ENSVS_BF16_MIN_ROWS", "0"))}
+
+
+# Small-M bf16-operand GEMMs split their K-steps over up to max_split workgroups per output
+# tile (ensvs_conv_gemm_bf16a: part / part_floats) when the launch has fewer than max_tiles
+# tiles; ENSVS_SPLITK=0 turns it off.
+SPLITK = {"on": os.environ.get("ENSVS_SPLITK", "0") != "0", "max_split": 8, "max_tiles": 128}
 
 
 def _castable(s):
@@ -184,6 +191,12 @@ def set_big_tile(mode, stages=0):
     two-stage, the default; 1: 32-deep LDS ring of `stages` stages) or keep them on the
     128 x 128 kernel (0 / False); all give identical bits."""
     _lib.call("ensvs_set_big_tile", int(mode), int(stages))
+
+
+def set_dual_small(on):
+    """Small-M bf16-operand launches (< 128 tiles) on the two-K-group kernel (default) or
+    the one-group kernel (the register-staged kernel's bits)."""
+    _lib.call("ensvs_set_dual_small", int(bool(on)))
 
 
 def gemm_dtype_is_bf16(W):
@@ -299,17 +312,25 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
     if not keep_y and ((epi == _lib.EPI_GATE and ybf is not None) or
                        (epi == _lib.EPI_GATE_BWD and (ybf is not None or csum is not None))):
         yptr = None  # only reached on the fused-epilogue path
+    # split-K workspace for small-M launches (fewer than 128 output tiles of 128 x 128)
+    part, part_n = None, 0
+    small = -(-M // BM) * (Npad // BM) < SPLITK["max_tiles"]
+    stages = BF16_ACT["stages_small"] if small else BF16_ACT["stages"]
+    if a16 and csum is None and SPLITK["on"] and small:
+        part_n = SPLITK["max_split"] * M * Npad
+        part = scratch(part_n, segs[0].x.device, key="splitk")
     if ybf is not None or csum is not None:
         call("ensvs_conv_gemm_bf16a_out", ctypes.addressof(arr), len(segs), B, Tout, N,
              Npad, W.buf.data_ptr(), bptr, yptr, ldy, ep, int(relu), int(accum), ptr(aux0),
              ld0, ptr(aux1), ld1, float(alpha), C, ptr(ybf), ybf_ld, ptr(ybf_radd),
              ybf_radd_ld, None if csum is None else csum.data_ptr() + 4 * csum_off, csum_ld,
-             BF16_ACT["stages"], stream())
+             stages, ptr(part), part_n, stream())
         return
     if a16:
         call("ensvs_conv_gemm_bf16a", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,
              W.buf.data_ptr(), bptr, yptr, ldy, ep, int(relu), int(accum),
-             ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, BF16_ACT["stages"], stream())
+             ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, stages, ptr(part),
+             part_n, stream())
     else:
         call("ensvs_conv_gemm", ctypes.addressof(arr), len(segs), B, Tout, N, Npad,
              W.buf.data_ptr(), W.dtype, bptr, yptr, ldy, ep, int(relu),

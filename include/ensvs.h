@@ -72,10 +72,20 @@ int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N
  * (3..5; 0 keeps the current count); 2: 64-deep two-stage kernel.  Defaults: ENSVS_BIG_TILE
  * (2), ENSVS_BIG_STAGES (5). */
 int ensvs_set_big_tile(int mode, int stages);
+/* Launches of fewer than 128 output tiles (small M) run a 128 x 128 kernel with two K-groups
+ * of 4 waves (each group half of the K-steps, tiles added through LDS; default on,
+ * ENSVS_DUAL_SMALL); 0 keeps them on the one-group kernel (the same bits as the register-
+ * staged kernel). */
+int ensvs_set_dual_small(int on);
+/* part / part_floats (optional, may be NULL / 0): fp32 workspace for split-K.  Launches of
+ * fewer than 128 output tiles (small M: the 2 000-frame reverse-diffusion GEMMs) split their
+ * K-steps over up to 8 workgroups per tile when part holds ksplit x M x Npad floats; the
+ * slices are summed in a fixed order by a second kernel that runs the epilogue
+ * (deterministic; ENSVS_SPLITK=0 disables). */
 int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N, int Npad,
                           const void* W, const float* bias, float* Y, int ldy, int epi, int relu,
                           int accum, float* aux0, int ld0, const float* aux1, int ld1, float alpha,
-                          int C, int stages, void* stream);
+                          int C, int stages, float* part, long long part_floats, void* stream);
 /* ensvs_conv_gemm_bf16a that also writes ybf[row*ybf_ld + col] = bf16(y + ybf_radd[(row /
  * Tout)*ybf_radd_ld + col]) for every output it writes (the next GEMM's operand, rounded as
  * ensvs_cast_bf16 would, without that pass).  Needs 16-B output rows (ld % 4 == 0) and
@@ -85,7 +95,8 @@ int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, int B, int T
                               int epi, int relu, int accum, float* aux0, int ld0,
                               const float* aux1, int ld1, float alpha, int C, void* ybf,
                               int ybf_ld, const float* ybf_radd, int ybf_radd_ld, float* csum,
-                              int csum_ld, int stages, void* stream);
+                              int csum_ld, int stages, float* part, long long part_floats,
+                              void* stream);
 /* csum (optional, M % 128 == 0): per 128-row tile column sums, csum[(m / 128) * csum_ld + n],
  * of the accumulator (PLAIN / ADDSCALE / RELU_MASK, before bias) or of both GATE_BWD outputs
  * (n < 2C, Y's column space) -- the DiffNet backward's per-sequence dilated-conv input-grad

@@ -22,10 +22,14 @@ def _pack(ws):
 
 
 def _both(run):
-    """run() with the bf16-activation path forced off, then forced on."""
+    """run() with the bf16-activation path forced off, then forced on (split-K off: these
+    compare the staging paths of one accumulation order; test_splitk_* cover split-K)."""
     saved = dict(K.BF16_ACT)
+    split = K.SPLITK["on"]
     outs = []
     try:
+        K.SPLITK["on"] = False
+        K.set_dual_small(False)
         for on in (False, True):
             K.BF16_ACT.update(on=on, min_reuse=1, min_rows=0)
             outs.append(run())
@@ -33,6 +37,8 @@ def _both(run):
     finally:
         K.BF16_ACT.clear()
         K.BF16_ACT.update(saved)
+        K.SPLITK["on"] = split
+        K.set_dual_small(True)
     return outs
 
 
@@ -174,3 +180,73 @@ def test_bf16a_tile_colsum_bitwise(epi):
     acc = y0 if epi == L.EPI_PLAIN else y0 - 0.7071 * aux1
     ref = acc.double().view(B * T // 128, 128, N).sum(1)
     torch.testing.assert_close(c0[:, N:2 * N].double(), ref, rtol=1e-4, atol=1e-3)
+
+
+def _close(a, b, rtol):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item() < rtol
+
+
+@pytest.mark.parametrize("epi", [L.EPI_PLAIN, L.EPI_GATE, "gate_bf16", L.EPI_RESSKIP,
+                                 L.EPI_GATE_BWD, L.EPI_ADDSCALE, L.EPI_RELU_MASK])
+def test_splitk_and_dual_match_unsplit(epi):
+    """Small-M launches (2 x 1002 frames: 64 tiles, 16 K-steps) on the two-K-group kernel
+    (the default) and with split-K (4 K splits): the same results as the one-group kernel up
+    to fp32 summation order (rel 1e-5; bf16 copies within one bf16 rounding), every epilogue
+    and bf16 output copy, and bit-identical from run to run."""
+    torch.manual_seed(21)
+    B, T, C, E = 2, 1002, 256, 256
+    M, N = B * T, 2 * C
+    x = torch.randn(M, C, device=DEV).to(torch.bfloat16)
+    cond = torch.randn(M, E, device=DEV).to(torch.bfloat16)
+    wd = torch.randn(N, C, 3, device=DEV) / (3 * C) ** 0.5
+    wc = torch.randn(N, E, 1, device=DEV) / E ** 0.5
+    pb, (rd, rc) = _pack([wd, wc])
+    segs = [K.Seg(x, C, C, rd, T, taps=3, dil=4, shift0=-4), K.Seg(cond, E, E, rc, T)]
+    bias = torch.randn(N, device=DEV)
+    aux1 = torch.randn(M, N, device=DEV)
+    radd = torch.randn(B, C, device=DEV)
+
+    def run():
+        g = torch.Generator(DEV).manual_seed(4)
+        y = torch.randn(M, N, device=DEV, generator=g)
+        aux0 = torch.randn(M, N, device=DEV, generator=g)
+        ybf = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+        Nn, kw = N, dict(bias=bias)
+        if epi == L.EPI_PLAIN:
+            kw.update(relu=True, accum=True, ybf=ybf, ybf_ld=N)
+        elif epi in (L.EPI_GATE, "gate_bf16"):
+            if epi == "gate_bf16":
+                aux0 = aux0.to(torch.bfloat16)
+            kw.update(epi=L.EPI_GATE, aux0=aux0, ld0=N, C=C, ybf=ybf, ybf_ld=C)
+        elif epi == L.EPI_RESSKIP:
+            kw.update(epi=epi, aux0=aux0, ld0=C, aux1=aux1, ld1=C, C=C, alpha=0.5, accum=True,
+                      ybf=ybf, ybf_ld=C, ybf_radd=radd, ybf_radd_ld=C)
+        elif epi == L.EPI_GATE_BWD:
+            kw = dict(epi=epi, aux1=aux1, ld1=N, C=C, ybf=ybf, ybf_ld=N)
+            Nn = C
+        elif epi == L.EPI_ADDSCALE:
+            kw = dict(epi=epi, aux1=aux1, ld1=N, alpha=0.25)
+        else:
+            kw = dict(epi=epi, aux1=aux1, ld1=N, accum=True)
+        K.gemm(segs, B, T, Nn, pb, y, N, **kw)
+        torch.cuda.synchronize()
+        return y, aux0, ybf
+    split = K.SPLITK["on"]
+    try:
+        K.SPLITK["on"] = False
+        K.set_dual_small(False)
+        ref = run()
+        K.set_dual_small(True)
+        dual = [run(), run()]
+        K.SPLITK["on"] = True
+        spl = [run(), run()]
+    finally:
+        K.SPLITK["on"] = split
+        K.set_dual_small(True)
+    for (y1, a1, b1), (y2, a2, b2) in (dual, spl):
+        assert torch.equal(y1, y2) and torch.equal(a1, a2) and torch.equal(b1, b2)
+        y0, a0, b0 = ref
+        assert _close(y1, y0, 1e-5)
+        assert _close(a1, a0, 1e-2 if a0.dtype == torch.bfloat16 else 1e-5)
+        assert _close(b1.float(), b0.float(), 1e-2)

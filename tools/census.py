@@ -1,0 +1,100 @@
+"""Per-launch census of one training step (dev tool): every libensvs entry point of one eager,
+serial bench step (30 pairs x 1024 frames) timed with HIP events and tagged with the GEMM /
+weight-gradient shape that issued it; aggregated by (entry point, shape), largest total
+first.   python tools/census.py [rows]
+"""
+import collections
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ensemble_svs_with_interactions_amd import _lib, configs, data, engine  # noqa: E402
+from ensemble_svs_with_interactions_amd import kernels as K  # noqa: E402
+from ensemble_svs_with_interactions_amd.train import FusedAdam, train_step  # noqa: E402
+
+ROWS = int(sys.argv[1]) if len(sys.argv) > 1 else 45
+REC = []
+TAG = [None]
+ON = [False]
+orig_call = _lib.call
+
+
+def call(name, *args):
+    if not ON[0]:
+        return orig_call(name, *args)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    orig_call(name, *args)
+    e.record()
+    REC.append((name, TAG[0], s, e))
+
+
+def tagged(fn, fmt):
+    def w(*a, **k):
+        old = TAG[0]
+        TAG[0] = fmt(*a, **k)
+        try:
+            return fn(*a, **k)
+        finally:
+            TAG[0] = old
+    return w
+
+
+def gemm_tag(segs, B, Tout, N, W, Y, ldy, **k):
+    sg = "+".join(f"{s.K}x{s.taps}{'b' if s.x.dtype == torch.bfloat16 else 'f'}" for s in segs)
+    return f"gemm M={B * Tout} N={N} K=[{sg}] epi={k.get('epi', 0)}"
+
+
+def wgrad_tag(dy, ldy, x, ldx, B, Tout, Tin, N, Kc, taps, *a, **k):
+    return (f"wgrad M={B * Tout} N={N} K={Kc}x{taps} "
+            f"{'b' if dy.dtype == torch.bfloat16 else 'f'}")
+
+
+import importlib  # noqa: E402
+import pkgutil  # noqa: E402
+import ensemble_svs_with_interactions_amd as pkg  # noqa: E402
+
+for m in [m for m in pkgutil.iter_modules(pkg.__path__) if not m.name.startswith("lib")]:
+    mod = importlib.import_module(f"{pkg.__name__}.{m.name}")
+    if getattr(mod, "call", None) is orig_call:
+        mod.call = call
+_lib.call = call
+K.gemm = tagged(K.gemm, gemm_tag)
+K.wgrad = tagged(K.wgrad, wgrad_tag)
+
+
+def main():
+    dev = torch.device("cuda")
+    engine.set_concurrency(False)
+    torch.manual_seed(20250321)
+    model = configs.instantiate(configs.multitrack_diffusion(num_speakers=4)).to(dev)
+    opt = FusedAdam(model, lr=1e-4, clip_norm=1.0)
+    P, T = 30, 1024
+    b = data.synthetic_batch(P, T, 1000)
+    g = lambda k: torch.from_numpy(b[k]).to(dev).contiguous()  # noqa: E731
+    xm, xs, ym, s0, s1 = g("x_main"), g("x_sub"), g("y_main"), g("spk_main"), g("spk_sub")
+    lens = b["lengths"].tolist()
+    for _ in range(2):
+        train_step(model, opt, xm, xs, ym, s0, s1, lens)
+    torch.cuda.synchronize()
+    ON[0] = True
+    train_step(model, opt, xm, xs, ym, s0, s1, lens)
+    torch.cuda.synchronize()
+    ON[0] = False
+    agg = collections.defaultdict(lambda: [0, 0.0])
+    tot = 0.0
+    for name, tag, s, e in REC:
+        ms = s.elapsed_time(e)
+        a = agg[(name, tag)]
+        a[0] += 1
+        a[1] += ms
+        tot += ms
+    print(f"{len(REC)} launches, {tot:.2f} ms (event-bracketed, serial eager step)")
+    for (name, tag), (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:ROWS]:
+        print(f"{ms:8.3f} ms {n:4d}x {ms / n * 1e3:8.1f} us  {name:28s} {tag or ''}")
+
+
+if __name__ == "__main__":
+    main()

@@ -521,7 +521,7 @@ def main():
         "model_tflops_per_s": value * TRAIN_FLOP_PER_FRAME / 1e12,
         # The gate GEMM's binding roof is HBM: 126.9 MB / 8 TB/s = 15.9 us > 32.2 GFLOP /
         # 2.5 PFLOP/s = 12.9 us (arithmetic intensity 254 FLOP/B < ridge 312).
-        "roofline": {"kernel": "conv_gemm_b16_kernel<2> (mgc DiffNet block gate GEMM, "
+        "roofline": {"kernel": "conv_gemm_b16_big_kernel (256x256 tile; mgc DiffNet block gate GEMM, "
                                f"M={P * T} N=512 K=1024, bf16 operands)"
                                if args.precision == "bf16" else "conv_gemm_kernel<float>",
                      "bound": "hbm", "achieved": gbytes / sec / 1e9, "peak": PEAK_HBM_GBS,

@@ -70,8 +70,10 @@ SIGNATURES = {
                      c_int, c_vp],
     "ensvs_lstm_fwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp,
                        c_vp],
+    "ensvs_lstm_bwd_work_floats": [c_int, c_int],
+    "ensvs_lstm_set_step": [c_int],
     "ensvs_lstm_bwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int,
-                       c_vp],
+                       c_vp, c_ll, c_vp],
     "ensvs_ardec_pack": [c_vp, c_int, c_vp, c_vp, c_vp],
     "ensvs_ardec_fwd": [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
                         c_vp, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp,
@@ -171,7 +173,7 @@ SIGNATURES = {
 
 # entry points returning a value instead of a status code
 RESTYPES = {"ensvs_embed_bwd_workspace": c_ll, "ensvs_usf_source_workspace": c_ll,
-            "ensvs_attn_table_grad_workspace": c_ll}
+            "ensvs_attn_table_grad_workspace": c_ll, "ensvs_lstm_bwd_work_floats": c_ll}
 
 _lib = None
 

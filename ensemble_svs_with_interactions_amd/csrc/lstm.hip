@@ -373,12 +373,308 @@ int launch_bwd(const float* dy, int lddy, const float* w0, const float* w1,
   return ENSVS_OK;
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Any hidden size (the encoders' H = 256 / 512, the bap decoder's H = 62): one launch per
+// time step over all sequences and both directions.  W_hh (1-4 MB per direction in fp32)
+// does not fit one CU's registers or LDS, so the step's dot products are spread over
+// ceil(H/U) x 2 workgroups, each owning U hidden units (their 4 gate rows of W_hh, read
+// from L2) for every sequence; the kernel boundary is the step's grid-wide barrier, and the
+// previous step's h / c (forward) and dG (backward) are read back from the outputs.  A
+// thread owns 4 sequences x (4 gates x U units) accumulators over one K slice (K = H
+// forward, 4H backward); slices are summed through LDS, then one thread per (sequence,
+// unit) applies the cell.  Sequence b's step s is its forward step s (row s forward, row
+// L_b-1-s reverse); backward launch p is step s = L_b-1-p.
+constexpr int SNT = 256;
+
+__device__ __forceinline__ long long step_row(int b, int T, int L, int dir, int s) {
+  return (long long)b * T + (dir ? L - 1 - s : s);
+}
+__device__ __forceinline__ void step_geo(int B, int& RB, int& KS) {
+  RB = (B + 3) / 4;
+  KS = 1;
+  while (RB * KS * 2 <= SNT) KS *= 2;
+}
+
+template <int U, bool VEC>
+__global__ __launch_bounds__(SNT) void lstm_step_fwd_kernel(
+    const float* __restrict__ gx, int ldg, const float* __restrict__ whh0,
+    const float* __restrict__ whh1, const long long* __restrict__ lengths, int B, int T, int H,
+    float* __restrict__ y, int ldy, float* __restrict__ sv, int s) {
+  __shared__ float part[SNT * 16 * U];  // [KS][4 RB][4][U]
+  const int dir = blockIdx.y, j0 = blockIdx.x * U, tid = threadIdx.x;
+  const float* W = dir ? whh1 : whh0;
+  int RB, KS;
+  step_geo(B, RB, KS);
+  const int kc = ((H + KS - 1) / KS + 3) & ~3;
+  const int BR = RB * 4;
+  for (int it = tid; it < RB * KS; it += SNT) {
+    const int rb = it / KS, ks = it % KS;
+    const int k0 = ks * kc, k1 = min(H, k0 + kc);
+    float acc[4][4][U];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[r][g][u] = 0.f;
+    const float* hp[4];
+    bool any = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = rb * 4 + r;
+      const int L = b < B ? (int)lengths[b] : 0;
+      const bool on = s > 0 && s < L;
+      hp[r] = on ? y + step_row(b, T, L, dir, s - 1) * ldy + dir * H : nullptr;
+      any |= on;
+    }
+    if (any) {
+      const float* wr[4][U];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int u = 0; u < U; ++u) wr[g][u] = W + (long long)(g * H + min(j0 + u, H - 1)) * H;
+      if constexpr (VEC) {
+        for (int k = k0; k < k1; k += 4) {
+          f32x4 hv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            hv[r] = hp[r] ? *(const f32x4*)(hp[r] + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const f32x4 wv = *(const f32x4*)(wr[g][u] + k);
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[r][g][u] = fmaf(hv[r][e], wv[e], acc[r][g][u]);
+            }
+        }
+      } else {
+        for (int k = k0; k < k1; ++k) {
+          float hv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hv[r] = hp[r] ? hp[r][k] : 0.f;
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const float wv = wr[g][u][k];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[r][g][u] = fmaf(hv[r], wv, acc[r][g][u]);
+            }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int u = 0; u < U; ++u) part[((ks * BR + rb * 4 + r) * 4 + g) * U + u] = acc[r][g][u];
+  }
+  __syncthreads();
+  const int G4 = 4 * H;
+  for (int it = tid; it < B * U; it += SNT) {
+    const int b = it / U, u = it % U, j = j0 + u;
+    if (j >= H) continue;
+    const int L = (int)lengths[b];
+    if (s == 0)  // pad_packed_sequence: zero outputs past the sequence end
+      for (int t = L; t < T; ++t) y[((long long)b * T + t) * ldy + dir * H + j] = 0.f;
+    if (s >= L) continue;
+    const long long row = step_row(b, T, L, dir, s);
+    float pre[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float a = 0.f;
+      for (int ks = 0; ks < KS; ++ks) a += part[((ks * BR + b) * 4 + g) * U + u];
+      pre[g] = gx[row * ldg + dir * G4 + g * H + j] + a;
+    }
+    const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanh_fast(pre[2]), og = sigm(pre[3]);
+    const float cp = s > 0 ? sv[(step_row(b, T, L, dir, s - 1) * 2 + dir) * 5 * H + 4 * H + j] : 0.f;
+    const float c = fg * cp + ig * gg;
+    const float h = og * tanh_fast(c);
+    y[row * ldy + dir * H + j] = h;
+    float* o = sv + (row * 2 + dir) * 5 * H + j;
+    o[0] = ig;
+    o[H] = fg;
+    o[2 * H] = gg;
+    o[3 * H] = og;
+    o[4 * H] = c;
+  }
+}
+
+template <int U, bool VEC>
+__global__ __launch_bounds__(SNT) void lstm_step_bwd_kernel(
+    const float* __restrict__ dy, int lddy, const float* __restrict__ whh0,
+    const float* __restrict__ whh1, const long long* __restrict__ lengths, int B, int T, int H,
+    const float* __restrict__ sv, float* __restrict__ dg, int lddg, float* __restrict__ dcs,
+    int p) {
+  __shared__ float part[SNT * 4 * U];  // [KS][4 RB][U]
+  const int dir = blockIdx.y, j0 = blockIdx.x * U, tid = threadIdx.x;
+  const float* W = dir ? whh1 : whh0;
+  const int G4 = 4 * H;
+  int RB, KS;
+  step_geo(B, RB, KS);
+  const int kc = ((G4 + KS - 1) / KS + 3) & ~3;
+  const int BR = RB * 4;
+  if (p > 0) {
+    for (int it = tid; it < RB * KS; it += SNT) {
+      const int rb = it / KS, ks = it % KS;
+      const int k0 = ks * kc, k1 = min(G4, k0 + kc);
+      float acc[4][U];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[r][u] = 0.f;
+      const float* gp[4];
+      bool any = false;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = rb * 4 + r;
+        const int L = b < B ? (int)lengths[b] : 0;
+        const int sb = L - 1 - p;  // this launch's step; dG of step sb + 1 was the last one
+        gp[r] = sb >= 0 ? dg + step_row(b, T, L, dir, sb + 1) * lddg + dir * G4 : nullptr;
+        any |= sb >= 0;
+      }
+      if (any) {
+        int jc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) jc[u] = min(j0 + u, H - 1);
+        if constexpr (VEC) {
+          for (int k = k0; k < k1; k += 4) {
+            f32x4 gv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              gv[r] = gp[r] ? *(const f32x4*)(gp[r] + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float* wrow = W + (long long)(k + e) * H;
+#pragma unroll
+              for (int u = 0; u < U; ++u) {
+                const float wv = wrow[jc[u]];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[r][u] = fmaf(gv[r][e], wv, acc[r][u]);
+              }
+            }
+          }
+        } else {
+          for (int k = k0; k < k1; ++k) {
+            const float* wrow = W + (long long)k * H;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const float wv = wrow[jc[u]];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[r][u] = fmaf(gp[r] ? gp[r][k] : 0.f, wv, acc[r][u]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u) part[(ks * BR + rb * 4 + r) * U + u] = acc[r][u];
+    }
+    __syncthreads();
+  }
+  for (int it = tid; it < B * U; it += SNT) {
+    const int b = it / U, u = it % U, j = j0 + u;
+    if (j >= H) continue;
+    const int L = (int)lengths[b];
+    if (p == 0)  // zero gate gradients past the sequence end
+      for (int t = L; t < T; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dg[((long long)b * T + t) * lddg + dir * G4 + g * H + j] = 0.f;
+    const int s = L - 1 - p;
+    if (s < 0) continue;
+    const long long row = step_row(b, T, L, dir, s);
+    float dhr = 0.f;
+    if (p > 0)
+      for (int ks = 0; ks < KS; ++ks) dhr += part[(ks * BR + b) * U + u];
+    const float* in = sv + (row * 2 + dir) * 5 * H + j;
+    const float ig = in[0], fg = in[H], gg = in[2 * H], og = in[3 * H], ct = in[4 * H];
+    const float cp = s > 0 ? sv[(step_row(b, T, L, dir, s - 1) * 2 + dir) * 5 * H + 4 * H + j] : 0.f;
+    float* dcp = dcs + ((long long)dir * B + b) * H + j;
+    const float dc = p > 0 ? *dcp : 0.f;
+    const float dh = dy[row * lddy + dir * H + j] + dhr;
+    const float tc = tanh_fast(ct);
+    const float dcc = dc + dh * og * (1.f - tc * tc);
+    float* o = dg + row * lddg + dir * G4 + j;
+    o[0] = dcc * gg * ig * (1.f - ig);
+    o[H] = dcc * cp * fg * (1.f - fg);
+    o[2 * H] = dcc * ig * (1.f - gg * gg);
+    o[3 * H] = dh * tc * og * (1.f - og);
+    *dcp = dcc * fg;
+  }
+}
+
+template <int U, bool VEC>
+int launch_step_fwd(const float* gx, int ldg, const float* w0, const float* w1,
+                    const long long* lengths, int B, int T, int H, float* y, int ldy, float* sv,
+                    hipStream_t st) {
+  const dim3 grid((H + U - 1) / U, 2);
+  for (int s = 0; s < T; ++s) {
+    hipLaunchKernelGGL((lstm_step_fwd_kernel<U, VEC>), grid, dim3(SNT), 0, st, gx, ldg, w0, w1,
+                       lengths, B, T, H, y, ldy, sv, s);
+    ENSVS_CHECK_LAUNCH();
+  }
+  return ENSVS_OK;
+}
+
+template <int U, bool VEC>
+int launch_step_bwd(const float* dy, int lddy, const float* w0, const float* w1,
+                    const long long* lengths, int B, int T, int H, const float* sv, float* dg,
+                    int lddg, float* dcs, hipStream_t st) {
+  const dim3 grid((H + U - 1) / U, 2);
+  for (int p = 0; p < T; ++p) {
+    hipLaunchKernelGGL((lstm_step_bwd_kernel<U, VEC>), grid, dim3(SNT), 0, st, dy, lddy, w0, w1,
+                       lengths, B, T, H, sv, dg, lddg, dcs, p);
+    ENSVS_CHECK_LAUNCH();
+  }
+  return ENSVS_OK;
+}
+
+int g_force_step = -1;  // ENSVS_LSTM_STEP=1: the per-step kernels at every H (tests)
+bool use_step(int H) {
+  if (g_force_step < 0) {
+    const char* e = getenv("ENSVS_LSTM_STEP");
+    g_force_step = e ? atoi(e) : 0;
+  }
+  return g_force_step || !(H == 8 || H == 16 || H == 32 || H == 64 || H == 128);
+}
+
+int step_fwd(const float* gx, int ldg, const float* w0, const float* w1, const long long* lengths,
+             int B, int T, int H, float* y, int ldy, float* sv, hipStream_t st) {
+  if (H <= 0 || B <= 0 || T <= 0 || B > 4 * SNT) return ENSVS_E_SHAPE;
+  const bool vec = H % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)y | (uintptr_t)w0 | (uintptr_t)w1) % 16 == 0;
+  if (H >= 512)
+    return vec ? launch_step_fwd<4, true>(gx, ldg, w0, w1, lengths, B, T, H, y, ldy, sv, st)
+               : launch_step_fwd<4, false>(gx, ldg, w0, w1, lengths, B, T, H, y, ldy, sv, st);
+  return vec ? launch_step_fwd<2, true>(gx, ldg, w0, w1, lengths, B, T, H, y, ldy, sv, st)
+             : launch_step_fwd<2, false>(gx, ldg, w0, w1, lengths, B, T, H, y, ldy, sv, st);
+}
+
+int step_bwd(const float* dy, int lddy, const float* w0, const float* w1, const long long* lengths,
+             int B, int T, int H, const float* sv, float* dg, int lddg, float* work,
+             long long work_floats, hipStream_t st) {
+  if (H <= 0 || B <= 0 || T <= 0 || B > 4 * SNT) return ENSVS_E_SHAPE;
+  if (!work || work_floats < 2LL * B * H) return ENSVS_E_ARG;
+  const bool vec = lddg % 4 == 0 && ((uintptr_t)dg % 16) == 0;
+  if (H >= 512)
+    return vec ? launch_step_bwd<4, true>(dy, lddy, w0, w1, lengths, B, T, H, sv, dg, lddg, work, st)
+               : launch_step_bwd<4, false>(dy, lddy, w0, w1, lengths, B, T, H, sv, dg, lddg, work, st);
+  return vec ? launch_step_bwd<2, true>(dy, lddy, w0, w1, lengths, B, T, H, sv, dg, lddg, work, st)
+             : launch_step_bwd<2, false>(dy, lddy, w0, w1, lengths, B, T, H, sv, dg, lddg, work, st);
+}
+
 }  // namespace
 
 ENSVS_API int ensvs_lstm_fwd(const float* gx, int ldg, const float* whh_f, const float* whh_r,
                              const long long* lengths, int B, int T, int H, float* y, int ldy,
                              float* saved, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (use_step(H)) return step_fwd(gx, ldg, whh_f, whh_r, lengths, B, T, H, y, ldy, saved, st);
   switch (H) {
     case 8: return launch_fwd<8>(gx, ldg, whh_f, whh_r, lengths, B, T, y, ldy, saved, st);
     case 16: return launch_fwd<16>(gx, ldg, whh_f, whh_r, lengths, B, T, y, ldy, saved, st);
@@ -389,10 +685,22 @@ ENSVS_API int ensvs_lstm_fwd(const float* gx, int ldg, const float* whh_f, const
   }
 }
 
+ENSVS_API int ensvs_lstm_set_step(int force) {
+  g_force_step = force;
+  return ENSVS_OK;
+}
+
+ENSVS_API long long ensvs_lstm_bwd_work_floats(int B, int H) {
+  return use_step(H) ? 2LL * B * H : 0;
+}
+
 ENSVS_API int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* whh_r,
                              const long long* lengths, int B, int T, int H, const float* saved,
-                             float* dg, int lddg, void* stream) {
+                             float* dg, int lddg, float* work, long long work_floats,
+                             void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (use_step(H))
+    return step_bwd(dy, lddy, whh_f, whh_r, lengths, B, T, H, saved, dg, lddg, work, work_floats, st);
   switch (H) {
     case 8: return launch_bwd<8>(dy, lddy, whh_f, whh_r, lengths, B, T, saved, dg, lddg, st);
     case 16: return launch_bwd<16>(dy, lddy, whh_f, whh_r, lengths, B, T, saved, dg, lddg, st);

@@ -15,7 +15,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
-from ._lib import call, ptr
+from ._lib import call, ptr, query
 from .engine import empty, gemm_dtype, grad_of, next_seed
 
 
@@ -352,9 +352,11 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
         s = sv[l]
         Kc = getattr(lstm, f"weight_ih_l{l}").shape[1]
         dg = empty(M, 8 * H, device=device)
+        nw = query("ensvs_lstm_bwd_work_floats", B, H)
+        work = empty(max(nw, 1), device=device)
         call("ensvs_lstm_bwd", d.data_ptr(), 2 * H, getattr(lstm, f"weight_hh_l{l}").data_ptr(),
              getattr(lstm, f"weight_hh_l{l}_reverse").data_ptr(), lens_dev.data_ptr(), B, T, H,
-             s["saved"].data_ptr(), dg.data_ptr(), 8 * H, stream())
+             s["saved"].data_ptr(), dg.data_ptr(), 8 * H, work.data_ptr(), nw, stream())
         for di, sfx in enumerate(("", "_reverse")):
             wgrad_into(getattr(lstm, f"weight_ih_l{l}{sfx}"), dg, 8 * H, s["x"], s["ldx"], B, T, T,
                        4 * H, Kc, dyoff=di * 4 * H)

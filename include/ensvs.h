@@ -136,14 +136,22 @@ int ensvs_colsum(const float* y, int ld, int M, int groups, int N, const float* 
  * by ensvs_conv_gemm into gx [B*T][ldg], dir d gates at cols d*4H + {i,f,g,o}*H).
  * Replaces the time loop of nn.LSTM(bidirectional=True) over pack_padded_sequence:
  * nnsvs/model.py:862-869,914-916 and acoustic_models/tacotron_f0.py:876-883,981-983.
- * H in {8,16,32,64,128}; saved holds [B*T][2][5H]. */
+ * Any H >= 1: H in {8,16,32,64,128} runs one persistent workgroup per (sequence,
+ * direction); other sizes (the encoders' 256 / 512, the bap decoder's 62 of
+ * MultiTrackMultistreamSeparateF0ParametricModel, nnsvs/model.py:1483-1490,861-869) one
+ * launch per time step over ceil(H/U) x 2 workgroups.  saved holds [B*T][2][5H]. */
 int ensvs_lstm_fwd(const float* gx, int ldg, const float* whh_f, const float* whh_r,
                    const long long* lengths, int B, int T, int H, float* y, int ldy, float* saved,
                    void* stream);
+/* Workspace floats ensvs_lstm_bwd needs for (B, H): 2*B*H (cell-gradient carry) for the
+ * per-step kernels, 0 for the persistent ones. */
+long long ensvs_lstm_bwd_work_floats(int B, int H);
+/* Test knob: force != 0 runs the per-step kernels at every H (default: ENSVS_LSTM_STEP). */
+int ensvs_lstm_set_step(int force);
 /* Backward through time: pre-activation gate gradients dg [B*T][lddg] (zero past L_b). */
 int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* whh_r,
                    const long long* lengths, int B, int T, int H, const float* saved, float* dg,
-                   int lddg, void* stream);
+                   int lddg, float* work, long long work_floats, void* stream);
 
 /* Residual-F0 AR decoder (acoustic_models/tacotron_f0.py:126-237 with
  * ZoneOutCell(LSTMCell), tacotron/decoder.py:20-48).  H in {16,...,256}, T % 4 == 0.

@@ -1,6 +1,7 @@
 """LSTM recurrence kernels (ensvs_lstm_fwd / ensvs_lstm_bwd, lstm.hip) against torch.nn.LSTM
 (fp32 CPU, packed bidirectional, as FFConvLSTM / the lf0 encoder use it: nnsvs/model.py:862-869,
-914-916), for every hidden size the C-ABI dispatches, with lengths that end inside, at and
+914-916), for every hidden size the C-ABI dispatches (persistent kernels at H = 8..128; the per-step
+kernels at the SeparateF0 model's H = 62 / 256 / 512, and forced at H = 16 / 64), with lengths that end inside, at and
 one past a staging chunk (16 steps; 8 for the H=128 backward) and a length-1 sequence.
 Tolerances (fp32): outputs rel 1e-5, gradients rel 1e-4; at the bench's T = 1024 and the
 long-sequence T = 4096 outputs rel 1e-4, gradients rel 1e-3 (4096 serial
@@ -9,7 +10,7 @@ import pytest
 import torch
 from torch.nn.utils.rnn import pack_padded_sequence, pad_packed_sequence
 
-from ensemble_svs_with_interactions_amd._lib import call
+from ensemble_svs_with_interactions_amd._lib import call, query
 from golden_util import rel
 
 pytestmark = pytest.mark.gpu
@@ -23,6 +24,30 @@ def test_lstm_recurrence_matches_torch(H):
 @pytest.mark.parametrize("H,T", [(128, 1024), (64, 1024), (128, 4096), (64, 4096)])
 def test_lstm_long_sequences_match_torch(H, T):
     _check(H, 3, T, 16, [T, T - 333, T // 2 + 1], 1e-4, 1e-3)
+
+
+@pytest.mark.parametrize("H", [62, 256, 512, 3])
+def test_lstm_step_kernels_match_torch(H):
+    """Per-step kernels (any H): the SeparateF0 recipe model's encoder (512), mgc decoder (256)
+    and bap decoder (62); H = 3 for the scalar path's bounds."""
+    _check(H, 5, 37, 24, [37, 17, 16, 9, 1], 1e-5, 1e-4)
+
+
+@pytest.mark.parametrize("H", [16, 64])
+def test_lstm_step_kernels_forced_match_torch(H):
+    call("ensvs_lstm_set_step", 1)
+    try:
+        _check(H, 5, 37, 24, [37, 17, 16, 9, 1], 1e-5, 1e-4)
+    finally:
+        call("ensvs_lstm_set_step", 0)
+
+
+def test_lstm_step_kernels_long_and_wide_batch():
+    """T = 1024 at H = 256 (the mgc decoder), 61 sequences (more than one 4-row group per
+    thread slice, ragged)."""
+    _check(256, 3, 1024, 16, [1024, 691, 513], 1e-4, 1e-3)
+    lens = [37 - (i % 37) for i in range(61)]
+    _check(64 + 6, 61, 37, 8, lens, 1e-5, 1e-4)
 
 
 def _check(H, B, T, I, lengths, tol_y, tol_g):
@@ -51,13 +76,17 @@ def _check(H, B, T, I, lengths, tol_y, tol_g):
 
     dg = torch.empty(B * T, 8 * H, device=dev)
     gy_d = gy.reshape(B * T, 2 * H).contiguous().to(dev)
+    nw = query("ensvs_lstm_bwd_work_floats", B, H)
+    work = torch.empty(max(nw, 1), device=dev)
     call("ensvs_lstm_bwd", gy_d.data_ptr(), 2 * H, whh[0].data_ptr(), whh[1].data_ptr(),
-         lens.data_ptr(), B, T, H, saved.data_ptr(), dg.data_ptr(), 8 * H, st)
+         lens.data_ptr(), B, T, H, saved.data_ptr(), dg.data_ptr(), 8 * H, work.data_ptr(), nw, st)
     dg = dg.cpu().view(B, T, 8 * H)
     hy = y.cpu().view(B, T, 2 * H)
     for d, s in enumerate(("", "_reverse")):
         g = dg[:, :, 4 * H * d:4 * H * (d + 1)]
-        assert torch.all(g[1, lengths[1]:] == 0)  # padded frames
+        for b, L in enumerate(lengths):
+            assert torch.all(g[b, L:] == 0)  # padded frames
+            assert torch.all(hy[b, L:] == 0)
         # h_{t-1} in processing order (zero state at the sequence start)
         h = hy[:, :, H * d:H * (d + 1)]
         hp = torch.zeros_like(h)

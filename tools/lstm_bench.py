@@ -18,20 +18,22 @@ lengths = data.synthetic_batch(B, T, 1000)["lengths"].tolist()
 dev = "cuda"
 st = torch.cuda.current_stream().cuda_stream
 lens = torch.tensor(lengths, dtype=torch.int64, device=dev)
-for H in (8, 16, 64, 128):
+for H in (8, 16, 64, 128, 62, 256, 512):
     gx = torch.randn(B * T, 8 * H, device=dev)
     w = [torch.randn(4 * H, H, device=dev) * 0.1 for _ in range(2)]
     y = torch.empty(B * T, 2 * H, device=dev)
     sv = torch.empty(B * T * 10 * H, device=dev)
     dy = torch.randn(B * T, 2 * H, device=dev)
     dg = torch.empty(B * T, 8 * H, device=dev)
+    nw = _lib.query("ensvs_lstm_bwd_work_floats", B, H)
+    work = torch.empty(max(nw, 1), device=dev)
     res = {}
     for name, fn in (("fwd", lambda: call("ensvs_lstm_fwd", gx.data_ptr(), 8 * H, w[0].data_ptr(),
                                            w[1].data_ptr(), lens.data_ptr(), B, T, H, y.data_ptr(),
                                            2 * H, sv.data_ptr(), st)),
                      ("bwd", lambda: call("ensvs_lstm_bwd", dy.data_ptr(), 2 * H, w[0].data_ptr(),
                                            w[1].data_ptr(), lens.data_ptr(), B, T, H, sv.data_ptr(),
-                                           dg.data_ptr(), 8 * H, st))):
+                                           dg.data_ptr(), 8 * H, work.data_ptr(), nw, st))):
         for _ in range(3):
             fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -95,6 +95,7 @@ def gate_gemm_timing(model, P, T, dev, iters=20):
 
     Returns (GEMM kernel seconds, seconds of the whole gate-GEMM call including the
     fp32 -> bf16 operand casts (ensvs_cast_bf16 of x + d and of cond), flops)."""
+    import torch
     from ensemble_svs_with_interactions_amd import _lib, kernels as K
     net = model.mgc_model.denoise_fn
     C, E, L = net.C, net.E, len(net.residual_layers)

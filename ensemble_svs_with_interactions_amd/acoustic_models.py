@@ -651,6 +651,19 @@ class _MultistreamHybrid(BaseModel):
                 torch.cuda.current_stream().wait_event(ev)
             _, dsp["vuv"] = self.vuv_model._bwd(st["vuv"], g["vuv"], want_spk=spk)
 
+    def _l1_terms(self, outs, y_main):
+        """The masked-L1 terms of the multistream-hybrid loss (train_acoustic_multitrack.py:
+        120-173): diffusion noise vs its prediction for mgc / bap, lf0 and V/UV vs the
+        targets.  Returns (preds, targets, grad keys) for train.masked_l1."""
+        Dy = y_main.shape[2]
+        o = self._stream_cols()
+        nm, nb = self.stream_sizes[0], self.stream_sizes[3]
+        preds = [(outs["mgc_recon"], nm, 0, nm), (outs["lf0"], 1, 0, 1), (outs["vuv"], 1, 0, 1),
+                 (outs["bap_recon"], nb, 0, nb)]
+        targets = [(outs["mgc_noise"], nm, 0), (y_main, Dy, o[1]), (y_main, Dy, o[2]),
+                   (outs["bap_noise"], nb, 0)]
+        return preds, targets, ["mgc_recon", "lf0", "vuv", "bap_recon"]
+
     def _bwd_epilogue(self, st, dsp):
         """Speaker-embedding gradient: the branch contributions, summed after the join."""
         if not self._MULTI:
@@ -897,6 +910,326 @@ class NPSSMDNMultistreamParametricModel(_MultistreamHybrid):
         out = self._infer(xp, None, None, None, [v + pad for v in lens], **(draws or {}))
         mu = out[:, :-pad]
         return mu, mu
+
+
+class MultiTrackMultistreamSeparateF0ParametricModel(_MultistreamHybrid):
+    """multistream.py:348-577: the recipe's default pairwise model (config.yaml:93-95,
+    multitrack_acoustic_nnsvs_world_multi_ar_f0.yaml).  The cross-singer log-F0 model (main
+    and sub call), the concatenation-fusion MultiTrackLSTMEncoder, and FFConvLSTM mgc / V/UV
+    / bap decoders on [encoder out, rest flag, lf0] (ground-truth lf0 under
+    lf0_teacher_forcing in training, the predicted one otherwise).
+
+    Reference quirks kept: the sub-track decoders read the MAIN track's decoder input
+    (multistream.py:519-521), so the sub outputs differ from the main ones only by the LSTM
+    dropout draws and the log-F0 stream; the sub track's encoder output is never read
+    (multistream.py:490-492, 507-510) and is not computed here.  The fused train step
+    (train.train_step; loss on the main outputs) runs the unobservable sub calls only for
+    their BatchNorm running-statistic updates: the lf0 model's conv stack on the sub input,
+    and for the decoders a second update with the main call's batch statistics (same input)."""
+
+    _MULTI = True
+    _train_fused = None  # the per-branch fused schedule is the diffusion model's
+
+    def __init__(self, in_dim: int, out_dim: int, stream_sizes: list, reduction_factor: int,
+                 encoder: nn.Module, mgc_model: nn.Module, lf0_model: nn.Module,
+                 vuv_model: nn.Module, bap_model: nn.Module, speaker_embedding: nn.Module,
+                 vib_model: nn.Module = None, vib_flags_model: nn.Module = None, in_rest_idx=1,
+                 in_lf0_idx=300, in_lf0_min=5.3936276, in_lf0_max=6.491111, out_lf0_idx=180,
+                 out_lf0_mean=5.953093881972361, out_lf0_scale=0.23435173188961034,
+                 lf0_teacher_forcing=True):
+        super().__init__()
+        from .model import FFConvLSTM, MultiTrackLSTMEncoder
+        self.in_dim = in_dim
+        self.out_dim = out_dim
+        self.stream_sizes = stream_sizes
+        self.reduction_factor = reduction_factor
+        self.lf0_teacher_forcing = lf0_teacher_forcing
+        assert len(stream_sizes) in [4]
+        if vib_model is not None or vib_flags_model is not None:
+            raise NotImplementedError("vib_model / vib_flags_model (deprecated in the reference)")
+        if not isinstance(lf0_model, MultiTrackBiLSTMResF0NonAttentiveDecoder):
+            raise NotImplementedError("lf0_model: MultiTrackBiLSTMResF0NonAttentiveDecoder")
+        if encoder is not None and not isinstance(encoder, MultiTrackLSTMEncoder):
+            raise NotImplementedError("encoder: MultiTrackLSTMEncoder (recipe) or None")
+        for m in (mgc_model, vuv_model, bap_model):
+            if not isinstance(m, FFConvLSTM):
+                raise NotImplementedError("mgc / vuv / bap models: FFConvLSTM (recipe)")
+        self.encoder = encoder
+        if self.encoder is not None:
+            assert not encoder.is_autoregressive()
+        self.mgc_model = mgc_model
+        self.lf0_model = lf0_model
+        self.vuv_model = vuv_model
+        self.bap_model = bap_model
+        self.speaker_embedding = speaker_embedding
+        self.in_rest_idx = in_rest_idx
+        self.in_lf0_idx = in_lf0_idx
+        self.in_lf0_min = in_lf0_min
+        self.in_lf0_max = in_lf0_max
+        self.out_lf0_idx = out_lf0_idx
+        self.out_lf0_mean = out_lf0_mean
+        self.out_lf0_scale = out_lf0_scale
+
+    def prediction_type(self):
+        return PredictionType.DETERMINISTIC  # BaseModel's default (nnsvs/base.py:128-136)
+
+    def is_autoregressive(self):
+        return (self.mgc_model.is_autoregressive() or self.lf0_model.is_autoregressive()
+                or self.vuv_model.is_autoregressive() or self.bap_model.is_autoregressive())
+
+    def _decoders(self):
+        return (("mgc", self.mgc_model), ("vuv", self.vuv_model), ("bap", self.bap_model))
+
+    # ------------------------------------------------------------------ core
+    def _fwd_core(self, x_main, x_sub, y_main, y_sub, spk0, spk1, lengths, training,
+                  want_sub, draws=None, save=True, sub_decoders=None):
+        """x_*: (B, T, in_dim) fp32 contiguous; y_*: (B, T, out_dim) targets or None;
+        want_sub: the sub-track lf0 call with outputs; sub_decoders (default want_sub): the
+        sub-track decoder calls.  Returns (outputs dict of (B*T, .) tensors, state)."""
+        sub_decoders = want_sub if sub_decoders is None else sub_decoders
+        self._set_lf0_params()
+        B, T, D = x_main.shape
+        dev = x_main.device
+        lens_host, lens_dev = lengths_pair(lengths, B, T, dev)
+        if max(lens_host) != T:
+            raise ValueError("max(lengths) must equal the frame count (multistream.py:495-510 "
+                             "concatenates T-frame rest flags with the packed outputs)")
+        (s0, i0), (s1, i1) = self._spk_vectors(spk0, spk1, B)
+        E = s0.shape[1]
+        o = self._stream_cols()
+        Dy = self.out_dim
+        dr = draws or {}
+        teach = self.lf0_teacher_forcing and y_main is not None
+        M = B * T
+        outs = {}
+        st = dict(i0=i0, i1=i1, B=B, T=T, E=E, lens_host=lens_host, lens_dev=lens_dev,
+                  teach=teach, want_sub=want_sub)
+        if self.encoder is not None:
+            N = self.encoder.out_dim
+            Din = N + 2
+            X = empty(M, (Din + 3) // 4 * 4, device=dev)
+        # phase 1: the lf0 model (main and sub calls) beside the encoder
+        with Branches(dev) as br:
+            with br.on(0):
+                tm = None if y_main is None else (y_main, Dy, o[1])
+                outs["lf0"], outs["lf0_residual"], st["lf0"] = self.lf0_model._fwd(
+                    [x_main, x_sub], D, B, T, lens_dev, (s0, s1), E,
+                    masks=dr.get("lf0_main"), training=training, save=save, teacher=tm)
+                if want_sub:
+                    ts = None if y_sub is None else (y_sub, Dy, o[1])
+                    outs["lf0_sub"], outs["lf0_residual_sub"], st["lf0_sub"] = \
+                        self.lf0_model._fwd([x_sub, x_main], D, B, T, lens_dev, (s1, s0), E,
+                                            masks=dr.get("lf0_sub"), training=training,
+                                            save=save, teacher=ts)
+                elif training:
+                    self.lf0_model._bn_only(x_sub, x_main, D, B, T, s1, s0, E)
+            if self.encoder is not None:
+                _, st["enc"] = self.encoder._fwd(x_main, x_sub, D, B, T, lens_dev, (s0, s1), E,
+                                                 training=training, save=save,
+                                                 lstm_masks=dr.get("enc_lstm"),
+                                                 out=(X, X.shape[1]))
+        if self.encoder is not None:
+            # [encoder out, rest flag, lf0] (multistream.py:495-510)
+            call("ensvs_copy_cols", x_main.data_ptr() + 4 * self.in_rest_idx, D,
+                 X.data_ptr() + 4 * N, X.shape[1], M, 1, Ly.stream())
+            lsrc, lld = (y_main.data_ptr() + 4 * o[1], Dy) if teach else \
+                (outs["lf0"].data_ptr(), 1)
+            call("ensvs_copy_cols", lsrc, lld, X.data_ptr() + 4 * (N + 1), X.shape[1], M, 1,
+                 Ly.stream())
+            src = [(X, X.shape[1], 0, Din)]
+        else:
+            src = [(x_main, D, 0, D)]
+        st["X"] = src
+        # phase 2: the three decoders (sub calls on the same input: multistream.py:519-521)
+        with Branches(dev) as br:
+            for bi, (name, m) in enumerate(self._decoders()):
+                with br.on(bi):
+                    outs[name], st[name] = m._fwd(
+                        src, B, T, lens_dev, training=training, save=save,
+                        lstm_masks=dr.get(f"{name}_lstm"),
+                        bn_updates=1 if sub_decoders or not training else 2)
+                    if sub_decoders:
+                        outs[name + "_sub"], st[name + "_sub"] = m._fwd(
+                            src, B, T, lens_dev, training=training, save=save,
+                            lstm_masks=dr.get(f"{name}_sub_lstm"))
+        return outs, st
+
+    def _bwd_core(self, st, g):
+        """g: grads (B*T, .) keyed like the outputs (missing = zero)."""
+        B, T, E = st["B"], st["T"], st["E"]
+        M = B * T
+        dev = st["lens_dev"].device
+        dX = {}
+        with Branches(dev) as br:
+            for bi, (name, m) in enumerate(self._decoders()):
+                with br.on(bi):
+                    acc = None
+                    for key in (name, name + "_sub"):
+                        if key not in st or g.get(key) is None:
+                            continue
+                        d, _ = m._bwd(st[key], g[key].contiguous())
+                        if acc is None:
+                            acc = d
+                        else:
+                            call("ensvs_axpy", acc.data_ptr(), d.data_ptr(), 1.0, d.numel(),
+                                 Ly.stream())
+                    dX[name] = acc
+        parts = [d for d in dX.values() if d is not None]
+        dsum = None
+        if parts:
+            dsum = parts[0]
+            for d in parts[1:]:
+                call("ensvs_axpy", dsum.data_ptr(), d.data_ptr(), 1.0, d.numel(), Ly.stream())
+        enc = self.encoder is not None
+        glf0 = g.get("lf0")
+        if glf0 is None:
+            glf0 = torch.zeros(M, device=dev)
+        if enc and dsum is not None and not st["teach"]:
+            # predicted lf0 fed the decoders: its column of the decoder-input gradient
+            N = self.encoder.out_dim
+            gl = empty(M, device=dev)
+            call("ensvs_copy_cols", dsum.data_ptr() + 4 * (N + 1), dsum.shape[1], gl.data_ptr(),
+                 1, M, 1, Ly.stream())
+            call("ensvs_axpy", gl.data_ptr(), glf0.contiguous().data_ptr(), 1.0, M, Ly.stream())
+            glf0 = gl
+        dsp = {}
+        with Branches(dev) as br:
+            with br.on(0):
+                dsp["lf0"], _, _ = self.lf0_model._bwd(st["lf0"], glf0.contiguous().view(-1),
+                                                       g.get("lf0_residual"))
+                if "lf0_sub" in st and (g.get("lf0_sub") is not None or
+                                        g.get("lf0_residual_sub") is not None):
+                    gs = g.get("lf0_sub")
+                    if gs is None:
+                        gs = torch.zeros(M, device=dev)
+                    dsp["lf0_sub"], _, _ = self.lf0_model._bwd(
+                        st["lf0_sub"], gs.contiguous().view(-1), g.get("lf0_residual_sub"))
+            if enc and dsum is not None:
+                dsp["enc0"], dsp["enc1"], _ = self.encoder._bwd(
+                    st["enc"], dsum, ld=dsum.shape[1], want_spk=True)
+        # speaker vectors: the lf0 calls' fused input holds both tracks' vectors
+        ds = [torch.zeros(B, E, device=dev) for _ in range(2)]
+        for k in range(2):
+            for key in ("lf0", "lf0_sub", "enc0" if k == 0 else "enc1"):
+                if dsp.get(key) is not None:
+                    call("ensvs_axpy", ds[k].data_ptr(), dsp[key].data_ptr(), 1.0, B * E,
+                         Ly.stream())
+        table = grad_of(self.speaker_embedding.emb.weight)
+        call("ensvs_spk_scatter", ds[0].data_ptr(), B, E, st["i0"].data_ptr(), table.data_ptr(),
+             Ly.stream())
+        call("ensvs_spk_scatter", ds[1].data_ptr(), B, E, st["i1"].data_ptr(), table.data_ptr(),
+             Ly.stream())
+
+    def _assemble(self, outs, sfx=""):
+        """cat([mgc, lf0, vuv, bap], -1) (multistream.py:559-560) as (B*T, out_dim)."""
+        o = self._stream_cols()
+        Dy = self.out_dim
+        M = outs["mgc" + sfx].shape[0]
+        out = empty(M, Dy, device=outs["mgc" + sfx].device)
+        for k, name in enumerate(("mgc", "lf0", "vuv", "bap")):
+            n = o[k + 1] - o[k]
+            call("ensvs_copy_cols", outs[name + sfx].data_ptr(), n, out.data_ptr() + 4 * o[k], Dy,
+                 M, n, Ly.stream())
+        return out
+
+    def _split(self, g, sfx, into):
+        """Per-stream contiguous grads of a (B*T, out_dim) output grad."""
+        o = self._stream_cols()
+        Dy = self.out_dim
+        M = g.shape[0]
+        for k, name in enumerate(("mgc", "lf0", "vuv", "bap")):
+            n = o[k + 1] - o[k]
+            d = empty(M, n, device=g.device)
+            call("ensvs_copy_cols", g.data_ptr() + 4 * o[k], Dy, d.data_ptr(), n, M, n,
+                 Ly.stream())
+            into[name + sfx] = d.view(-1) if name == "lf0" else d
+
+    # ------------------------------------------------------------------ fused train step
+    def _train_fwd(self, x_main, x_sub, y_main, spk0, spk1, lengths, draws=None):
+        return self._fwd_core(x_main, x_sub, y_main, None, spk0, spk1, lengths, True, False,
+                              draws)
+
+    def _train_bwd(self, st, g):
+        self._bwd_core(st, g)
+
+    def _l1_terms(self, outs, y_main):
+        """The reference's deterministic loss (train_acoustic_multitrack.py:197-238,
+        stream_wise_loss false): L1 of the whole main output against the main targets,
+        mean over valid frames x out_dim."""
+        o = self._stream_cols()
+        Dy = y_main.shape[2]
+        preds, targets, keys = [], [], []
+        for k, name in enumerate(("mgc", "lf0", "vuv", "bap")):
+            n = o[k + 1] - o[k]
+            preds.append((outs[name], n, 0, n))
+            targets.append((y_main, Dy, o[k]))
+            keys.append(name)
+        return preds, targets, keys
+
+    # ------------------------------------------------------------------ inference
+    def _infer(self, x_main, x_sub, spk0, spk1, lengths, masks=None):
+        """multistream.py:447-567 with ys=None: (out_main, out_sub) (B, T, out_dim); the
+        sub output's mgc / V/UV / bap equal the main ones (same input, no dropout).
+        masks (tests only): dict(lf0_main=..., lf0_sub=...) AR prenet keep-masks to replay."""
+        B, T, _ = x_main.shape
+        outs, _ = self._fwd_core(x_main, x_sub, None, None, spk0, spk1, lengths, False, True,
+                                 masks, save=False, sub_decoders=False)
+        for name, _m in self._decoders():
+            outs[name + "_sub"] = outs[name]
+        return self._assemble(outs).view(B, T, -1), self._assemble(outs, "_sub").view(B, T, -1)
+
+    # ---------------------------------------------------------------- reference API
+    def forward(self, x_main, x_sub, spks_list, lengths=None, ys=None):
+        assert x_main.shape[-1] == self.in_dim
+        if ys is None:
+            return self._infer(x_main.contiguous().float(), x_sub.contiguous().float(),
+                               spks_list[0], spks_list[1], lengths)
+        om, rm, os_, rs = _SeparateF0Fn.apply(self, x_main, x_sub, ys[0], ys[1], spks_list[0],
+                                              spks_list[1], lengths, *self.parameters())
+        return (om, rm), (os_, rs)
+
+    def inference(self, x_main, x_sub, spks=None, lengths=None, draws=None):
+        """pad_inference_multitrack (acoustic_models/util.py:154-188): replicate-pad r -
+        max(L) % r frames (r when divisible), forward, main output, trim.  draws (tests
+        only): dict(lf0_main=..., lf0_sub=...) AR prenet keep-masks to replay."""
+        r = self.reduction_factor
+        B, T, D = x_main.shape
+        lens = [int(v) for v in (lengths if lengths is not None else [T] * B)]
+        pad = r - max(lens) % r
+        xm = _replicate_pad(x_main.contiguous().float(), B, T, D, pad)
+        xs = _replicate_pad(x_sub.contiguous().float(), B, T, D, pad)
+        out, _ = self._infer(xm, xs, spks[0], spks[1], [v + pad for v in lens], masks=draws)
+        return out[:, :-pad]
+
+
+class _SeparateF0Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mod, x_main, x_sub, y_main, y_sub, spk0, spk1, lengths, *params):
+        B, T, _ = x_main.shape
+        f = lambda t: t.contiguous().float()  # noqa: E731
+        outs, st = mod._fwd_core(f(x_main), f(x_sub), f(y_main), f(y_sub), spk0, spk1, lengths,
+                                 mod.training, True, getattr(mod, "_replay_draws", None))
+        ctx.mod, ctx.st, ctx.params = mod, st, params
+        v = lambda t: t.view(B, T, -1)  # noqa: E731
+        return (v(mod._assemble(outs)), v(outs["lf0_residual"]), v(mod._assemble(outs, "_sub")),
+                v(outs["lf0_residual_sub"]))
+
+    @staticmethod
+    def backward(ctx, g_om, g_rm, g_os, g_rs):
+        mod, st = ctx.mod, ctx.st
+        B, T = st["B"], st["T"]
+        g = {}
+        for gg, sfx in ((g_om, ""), (g_os, "_sub")):
+            if gg is not None:
+                mod._split(gg.contiguous().view(B * T, -1), sfx, g)
+        if g_rm is not None:
+            g["lf0_residual"] = g_rm.contiguous().view(-1)
+        if g_rs is not None:
+            g["lf0_residual_sub"] = g_rs.contiguous().view(-1)
+        with GradCapture(ctx.params) as gc:
+            mod._bwd_core(st, g)
+        ctx.st = ctx.params = None
+        return (None,) * 8 + gc.grads(ctx.needs_input_grad[8:])
 
 
 class _MultiTrackFn(torch.autograd.Function):

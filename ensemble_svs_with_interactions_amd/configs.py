@@ -33,6 +33,9 @@ REFERENCE_TARGETS = {
     f"{PKG}.timing.MultiTrackVariancePredictor": "nnsvs.model.MultiTrackVariancePredictor",
     f"{PKG}.timing.MDN": "nnsvs.model.MDN",
     f"{PKG}.transformer.TransformerEncoder": "nnsvs.model.TransformerEncoder",
+    f"{PKG}.acoustic_models.MultiTrackMultistreamSeparateF0ParametricModel":
+        "nnsvs.acoustic_models.MultiTrackMultistreamSeparateF0ParametricModel",
+    f"{PKG}.model.MultiTrackLSTMEncoder": "nnsvs.model.MultiTrackLSTMEncoder",
 }
 
 
@@ -134,6 +137,45 @@ def singletrack_diffusion(tiny=False, vuv_dropout=0.1):
     for k in ("speaker_embedding", "output_subtrack"):
         cfg.pop(k)
     cfg["lf0_model"]["_target_"] = f"{PKG}.acoustic_models.BiLSTMResF0NonAttentiveDecoder"
+    return cfg
+
+
+def multitrack_separate_f0(num_speakers=3, tiny=False):
+    """The recipe's default acoustic model (config.yaml:93-95):
+    recipes/jaCappella_ritsu/dev-48k-world-multitrack/conf/train_acoustic/model/
+    multitrack_acoustic_nnsvs_world_multi_ar_f0.yaml (netG).  tiny: same topology, small
+    widths (hidden sizes off the persistent-kernel set, so the per-step LSTM kernels run)."""
+    base = multitrack_diffusion(num_speakers=num_speakers, tiny=tiny)
+    E = base["speaker_embedding"]["embedding_dim"]
+    if tiny:
+        enc = dict(hidden=20, out=32)
+        dec = dict(mgc=(32, 16, 12), vuv=(16, 8, 8), bap=(16, 8, 6))
+    else:
+        enc = dict(hidden=512, out=1024)
+        dec = dict(mgc=(1024, 512, 256), vuv=(256, 128, 64), bap=(256, 128, 62))
+    Din = enc["out"] + 2
+
+    def decoder(name, out_dim, dropout):
+        ff, conv, lstm = dec[name]
+        return {"_target_": f"{PKG}.model.FFConvLSTM", "in_dim": Din, "ff_hidden_dim": ff,
+                "conv_hidden_dim": conv, "lstm_hidden_dim": lstm, "num_lstm_layers": 2,
+                "bidirectional": True, "out_dim": out_dim, "dropout": dropout}
+    cfg = {
+        "_target_": f"{PKG}.acoustic_models.MultiTrackMultistreamSeparateF0ParametricModel",
+        "in_dim": 86, "out_dim": 67, "stream_sizes": [60, 1, 1, 5], "reduction_factor": 4,
+        "in_rest_idx": 0, "in_lf0_idx": 51, "out_lf0_idx": 60,
+        "lf0_model": base["lf0_model"],
+        "encoder": {"_target_": f"{PKG}.model.MultiTrackLSTMEncoder", "in_dim": 86,
+                    "in_ph_start_idx": 3, "in_ph_end_idx": 50, "embed_dim": E,
+                    "hidden_dim": enc["hidden"], "out_dim": enc["out"], "num_layers": 3,
+                    "dropout": 0.0, "bidirectional": True, "init_type": "kaiming_normal"},
+        "mgc_model": decoder("mgc", 60, 0.1),
+        "vuv_model": decoder("vuv", 1, 0.1),
+        "bap_model": decoder("bap", 5, 0.0),
+        "speaker_embedding": base["speaker_embedding"],
+        "vib_model": None, "vib_flags_model": None,
+    }
+    cfg.update(LF0_STATS)
     return cfg
 
 

@@ -109,34 +109,41 @@ def gather_input(sources, ph0, ph1, M, device):
     return ph_src, X, Kin, ldx
 
 
-def embed_fwd(pk, emb_weight, sources, ph0, ph1, B, T, spk_seq=None, spk_ld=0, device=None):
-    """x = emb(argmax onehot) + fc_in(other cols) [+ spk]  -> (M, E); returns saved dict."""
+def embed_fwd(pk, emb_weight, sources, ph0, ph1, B, T, spk_seq=None, spk_ld=0, device=None,
+              out=None):
+    """x = emb(argmax onehot) + fc_in(other cols) [+ spk]  -> (M, E); returns saved dict.
+    out: (tensor, ld, col) to write into a column range of a wider buffer instead."""
     M = B * T
     ph_src, X, Kin, ldx = gather_input(sources, ph0, ph1, M, device)
     ids = torch.empty(M, dtype=torch.int32, device=device)
     t, ld, off = ph_src
     call("ensvs_phoneme_ids", t.data_ptr() + 4 * off, ld, M, 0, ph1 - ph0, ids.data_ptr(), stream())
     E = emb_weight.shape[1]
-    Y = empty(M, E, device=device)
-    K.gemm([K.Seg(X, ldx, Kin, pk["fc_in"], T)], B, T, E, pk.fwd, Y, E,
+    if out is None:
+        Y, ldY, col = empty(M, E, device=device), E, 0
+    else:
+        Y, ldY, col = out
+    K.gemm([K.Seg(X, ldx, Kin, pk["fc_in"], T)], B, T, E, pk.fwd, Y, ldY, yoff=col,
            **pk.bias_ptr_args("fc_in.b"))
-    call("ensvs_embed_add", Y.data_ptr(), E, M, E, T, emb_weight.data_ptr(), ids.data_ptr(), None,
-         ptr(spk_seq), None, spk_ld, stream())
+    call("ensvs_embed_add", Y.data_ptr() + 4 * col, ldY, M, E, T, emb_weight.data_ptr(),
+         ids.data_ptr(), None, ptr(spk_seq), None, spk_ld, stream())
     return Y, dict(ids=ids, X=X, Kin=Kin, ldx=ldx)
 
 
-def embed_bwd(emb_mod, fc_in, sv, dY, B, T, dspk_seq=None):
-    """Grads of emb / fc_in (and per-sequence speaker vectors, summed over frames)."""
+def embed_bwd(emb_mod, fc_in, sv, dY, B, T, dspk_seq=None, ld=None, col=0):
+    """Grads of emb / fc_in (and per-sequence speaker vectors, summed over frames).
+    dY: (M, E), or columns [col, col + E) of a (M, ld) buffer."""
     M = B * T
-    E = dY.shape[1]
+    E = emb_mod.weight.shape[1]
+    ld = E if ld is None else ld
     V = emb_mod.weight.shape[0]
     part = K.scratch(_lib.query("ensvs_embed_bwd_workspace", M, E, V), dY.device, key="emb")
-    call("ensvs_embed_bwd", dY.data_ptr(), E, M, E, sv["ids"].data_ptr(), V, part.data_ptr(),
-         grad_of(emb_mod.weight).data_ptr(), stream())
-    wgrad_into(fc_in.weight, dY, E, sv["X"], sv["ldx"], B, T, T, E, sv["Kin"])
-    colsum_into(dY, E, M, E, fc_in.bias)
+    call("ensvs_embed_bwd", dY.data_ptr() + 4 * col, ld, M, E, sv["ids"].data_ptr(), V,
+         part.data_ptr(), grad_of(emb_mod.weight).data_ptr(), stream())
+    wgrad_into(fc_in.weight, dY, ld, sv["X"], sv["ldx"], B, T, T, E, sv["Kin"], dyoff=col)
+    colsum_into(dY, ld, M, E, fc_in.bias, yoff=col)
     if dspk_seq is not None:
-        K.colsum(dY, E, T, E, dspk_seq, groups=B, accum=True)
+        K.colsum(dY, ld, T, E, dspk_seq, groups=B, accum=True, yoff=col)
 
 
 # ----------------------------------------------------------------- FF stack
@@ -207,8 +214,10 @@ def conv_register(pk, conv, first_cols=None, first_bwd_cols=None):
 
 
 def conv_fwd(pk, conv, first_segs, B, T, device, training, groups=1, save=True,
-             update_running=True):
-    """first_segs: list of (name, tensor, ld, K, xoff) for conv.1.  Returns (out, saved)."""
+             update_running=True, running_updates=1):
+    """first_segs: list of (name, tensor, ld, K, xoff) for conv.1.  Returns (out, saved).
+    running_updates: BatchNorm running-statistic updates with this batch's statistics (2
+    stands for a second call of the stack on the same input whose outputs are unused)."""
     M = B * T
     Mg = M // groups
     sv = []
@@ -231,11 +240,12 @@ def conv_fwd(pk, conv, first_segs, B, T, device, training, groups=1, save=True,
             K.colsum(y, C, Mg, C, mean, groups=groups, scale=1.0 / Mg)
             K.colsum(y, C, Mg, C, var, groups=groups, mean=mean, scale=1.0 / Mg)
             upd = int(update_running and bn.track_running_stats)
-            call("ensvs_bn_finalize", mean.data_ptr(), var.data_ptr(), groups, C, Mg,
-                 float(bn.eps), rstd.data_ptr(), bn.running_mean.data_ptr(),
-                 bn.running_var.data_ptr(), float(bn.momentum), upd, stream())
-            if upd:
-                bn.num_batches_tracked.add_(groups)
+            for _ in range(max(1, running_updates if upd else 1)):
+                call("ensvs_bn_finalize", mean.data_ptr(), var.data_ptr(), groups, C, Mg,
+                     float(bn.eps), rstd.data_ptr(), bn.running_mean.data_ptr(),
+                     bn.running_var.data_ptr(), float(bn.momentum), upd, stream())
+                if upd:
+                    bn.num_batches_tracked.add_(groups)
             Mg_apply = Mg
         else:
             # eval: running statistics, one group

@@ -99,13 +99,16 @@ class FFConvLSTM(BaseModel):
         self.num_vocab = in_ph_end_idx - in_ph_start_idx
         self.embed_dim = embed_dim
         self.use_mdn = use_mdn
-        if embed_dim is None:
-            raise NotImplementedError("FFConvLSTM without phoneme embedding is not on the path")
-        assert in_dim > self.num_vocab
-        self.emb = nn.Embedding(self.num_vocab, embed_dim)
-        self.fc_in = nn.Linear(in_dim - self.num_vocab, embed_dim)
+        if embed_dim is not None:
+            assert in_dim > self.num_vocab
+            self.emb = nn.Embedding(self.num_vocab, embed_dim)
+            self.fc_in = nn.Linear(in_dim - self.num_vocab, embed_dim)
+            ff_in_dim = embed_dim
+        else:
+            # the SeparateF0 recipe model's decoders read [encoder out, rest flag, lf0]
+            ff_in_dim = in_dim
         self.ff = nn.Sequential(
-            nn.Linear(embed_dim, ff_hidden_dim), nn.ReLU(),
+            nn.Linear(ff_in_dim, ff_hidden_dim), nn.ReLU(),
             nn.Linear(ff_hidden_dim, ff_hidden_dim), nn.ReLU(),
             nn.Linear(ff_hidden_dim, ff_hidden_dim), nn.ReLU(),
         )
@@ -130,7 +133,8 @@ class FFConvLSTM(BaseModel):
 
     # ---- kernels -----------------------------------------------------------------
     def _register(self, pk):
-        Ly.phoneme_input_register(pk, self.emb, self.fc_in)
+        if self.embed_dim is not None:
+            Ly.phoneme_input_register(pk, self.emb, self.fc_in)
         Ly.ff_register(pk, self.ff)
         Ly.conv_register(pk, self.conv)
         Ly.lstm_register(pk, self.lstm)
@@ -138,18 +142,24 @@ class FFConvLSTM(BaseModel):
         pk.bias_vec("fc.b", self.fc.bias)
 
     def _fwd(self, sources, B, T, lens_dev, spk_seq=None, spk_ld=0, training=None,
-             lstm_masks=None, save=True):
-        """sources: [(tensor, ld, col_offset, ncols)] of the logical input columns.
+             lstm_masks=None, save=True, bn_updates=1):
+        """sources: [(tensor, ld, col_offset, ncols)] of the logical input columns (without
+        phoneme embedding: one (X, ldx, 0, in_dim) source is read in place).
         Returns (out (B*T, out_dim), saved state)."""
         training = self.training if training is None else training
         pk = self._packs.ensure(self, self._register)
         dev = self.fc.weight.device
-        X0, esv = Ly.embed_fwd(pk, self.emb.weight, sources, self.in_ph_start_idx,
-                               self.in_ph_end_idx, B, T, spk_seq, spk_ld, dev)
+        if self.embed_dim is not None:
+            X0, esv = Ly.embed_fwd(pk, self.emb.weight, sources, self.in_ph_start_idx,
+                                   self.in_ph_end_idx, B, T, spk_seq, spk_ld, dev)
+        else:
+            if spk_seq is not None:
+                raise NotImplementedError("FFConvLSTM(embed_dim=None) with spk_embs")
+            X0, esv = _plain_input(sources, self.in_dim, B * T, dev), None
         hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
         F = hs[2].shape[1]
         a, csv = Ly.conv_fwd(pk, self.conv, [("", hs[2], F, F, 0)], B, T, dev, training,
-                             save=save)
+                             save=save, running_updates=bn_updates)
         if training and self.lstm.dropout > 0 and lstm_masks is None:
             lstm_masks = [Ly.dropout_mask(B * T * 2 * self.lstm.hidden_size, self.lstm.dropout,
                                           dev)
@@ -183,6 +193,8 @@ class FFConvLSTM(BaseModel):
         (dh3,) = Ly.conv_bwd(pk, self.conv, st["csv"], da, B, T, dev, first_dx=[("", F)])
         dX0 = Ly.ff_bwd(pk, self.ff, st["X0"], st["hs"], dh3, B, T, dev)
         dspk = None
+        if self.embed_dim is None:
+            return dX0, None
         if want_spk:
             dspk = torch.zeros(B, self.embed_dim, device=dev)
         Ly.embed_bwd(self.emb, self.fc_in, st["esv"], dX0, B, T, dspk)
@@ -196,6 +208,17 @@ class FFConvLSTM(BaseModel):
 
     def inference(self, x, lengths=None, spk_embs=None):
         return self(x, lengths, spk_embs=spk_embs)
+
+
+def _plain_input(sources, D, M, device):
+    """The logical input columns as one (M, ldx) buffer (ldx = D rounded up to 4): the
+    single source itself when it is already such a buffer, else a gathered copy."""
+    if len(sources) == 1:
+        t, ld, off, n = sources[0]
+        if off == 0 and n == D and t.dim() == 2 and t.shape[1] == ld and ld % 4 == 0:
+            return t
+    _, X, _, _ = Ly.gather_input(sources, D, D, M, device)
+    return X
 
 
 def _spk_args(spk_embs, B, T):
@@ -239,3 +262,141 @@ class _FFConvLSTMFn(torch.autograd.Function):
         dspk = dX0.view(B, T, -1) if ctx.spk_needs else None
         ctx.st = ctx.params = None
         return (None, None, dspk, None) + gc.grads(ctx.needs_input_grad[4:])
+
+
+class MultiTrackLSTMEncoder(BaseModel):
+    """nnsvs/model.py:1435-1537: the concatenation-fusion encoder of the SeparateF0 recipe
+    model.  Each track's input becomes emb(argmax one-hot phoneme) + fc_in(other columns)
+    + its speaker vector, written side by side into one (M, 2E) buffer (the reference's
+    torch.concat, model.py:1527-1529), then the packed bidirectional LSTM (H = 512 in the
+    recipe: the per-step recurrence kernels) and hidden2out."""
+
+    def __init__(self, in_dim: int, hidden_dim: int, out_dim: int, num_layers: int = 1,
+                 bidirectional: bool = True, dropout: float = 0.0, init_type: str = "none",
+                 in_ph_start_idx: int = 1, in_ph_end_idx: int = 50, embed_dim=None):
+        super().__init__()
+        self.in_dim = in_dim
+        self.in_ph_start_idx = in_ph_start_idx
+        self.in_ph_end_idx = in_ph_end_idx
+        self.num_vocab = in_ph_end_idx - in_ph_start_idx
+        self.embed_dim = embed_dim
+        if embed_dim is None:
+            # the reference adds the speaker vectors to its caller's inputs in place
+            # (model.py:1527-1528); the recipe always embeds (embed_dim 256)
+            raise NotImplementedError("MultiTrackLSTMEncoder(embed_dim=None)")
+        if not bidirectional:
+            raise NotImplementedError("MultiTrackLSTMEncoder(bidirectional=False)")
+        assert in_dim > self.num_vocab
+        self.emb = nn.Embedding(self.num_vocab, embed_dim)
+        self.fc_in = nn.Linear(in_dim - self.num_vocab, embed_dim)
+        self.num_layers = num_layers
+        self.lstm = nn.LSTM(embed_dim * 2, hidden_dim, num_layers, bidirectional=True,
+                            batch_first=True, dropout=dropout)
+        self.hidden2out = nn.Linear(2 * hidden_dim, out_dim)
+        init_weights(self, init_type)
+        self._packs = ModulePacks()
+
+    @property
+    def out_dim(self):
+        return self.hidden2out.out_features
+
+    def _register(self, pk):
+        Ly.phoneme_input_register(pk, self.emb, self.fc_in)
+        Ly.lstm_register(pk, self.lstm)
+        pk.linear("h2o", self.hidden2out.weight)
+        pk.bias_vec("h2o.b", self.hidden2out.bias)
+
+    def _fwd(self, x_main, x_sub, D, B, T, lens_dev, spks=(None, None), spk_ld=0,
+             training=None, lstm_masks=None, save=True, out=None):
+        """x_main / x_sub: (B*T, D) rows (ld D); spks: per-sequence speaker vectors (B rows of
+        stride spk_ld) or None; out: (buffer, ld) to write the (B*T, out_dim) output into the
+        first columns of a wider buffer.  Returns (out, saved state)."""
+        training = self.training if training is None else training
+        pk = self._packs.ensure(self, self._register)
+        dev = self.hidden2out.weight.device
+        E = self.embed_dim
+        X = empty(B * T, 2 * E, device=dev)
+        esv = []
+        for k, x in enumerate((x_main, x_sub)):
+            _, sv = Ly.embed_fwd(pk, self.emb.weight, [(x, D, 0, D)], self.in_ph_start_idx,
+                                 self.in_ph_end_idx, B, T, spks[k], spk_ld, dev,
+                                 out=(X, 2 * E, k * E))
+            esv.append(sv)
+        H = self.lstm.hidden_size
+        if training and self.lstm.dropout > 0 and lstm_masks is None:
+            lstm_masks = [Ly.dropout_mask(B * T * 2 * H, self.lstm.dropout, dev)
+                          for _ in range(self.num_layers - 1)]
+        y, lsv = Ly.lstm_fwd(pk, self.lstm, X, 2 * E, B, T, lens_dev, dev,
+                             lstm_masks if training else None, save=save)
+        N = self.out_dim
+        out, ldo = (empty(B * T, N, device=dev), N) if out is None else out
+        Ly.K.gemm([Ly.K.Seg(y, 2 * H, 2 * H, pk["h2o"], T)], B, T, N, pk.fwd, out, ldo,
+                  **pk.bias_ptr_args("h2o.b"))
+        st = dict(X=X, esv=esv, lsv=lsv, y=y, B=B, T=T, lens=lens_dev) if save else None
+        return out, st
+
+    def _bwd(self, st, dout, ld=None, want_spk=True):
+        """dout: (B*T, out_dim) rows of stride ld.  Accumulates parameter grads; returns the
+        per-sequence speaker-vector grads (dspk_main, dspk_sub) (B, E) (or None) and the
+        grad of the fused (B*T, 2E) LSTM input."""
+        pk = self._packs
+        dev = dout.device
+        B, T = st["B"], st["T"]
+        M = B * T
+        N = self.out_dim
+        ld = N if ld is None else ld
+        H2 = 2 * self.lstm.hidden_size
+        E = self.embed_dim
+        Ly.wgrad_into(self.hidden2out.weight, dout, ld, st["y"], H2, B, T, T, N, H2)
+        Ly.colsum_into(dout, ld, M, N, self.hidden2out.bias)
+        dy = empty(M, H2, device=dev)
+        Ly.K.gemm([Ly.K.Seg(dout, ld, N, pk["h2o^T"], T)], B, T, H2, pk.bwd, dy, H2)
+        dX = Ly.lstm_bwd(pk, self.lstm, st["lsv"], dy, B, T, st["lens"], dev)
+        dspk = [torch.zeros(B, E, device=dev) if want_spk else None for _ in range(2)]
+        for k in range(2):
+            Ly.embed_bwd(self.emb, self.fc_in, st["esv"][k], dX, B, T, dspk[k], ld=2 * E,
+                         col=k * E)
+        return dspk[0], dspk[1], dX
+
+    # ---- reference API -----------------------------------------------------------
+    def forward(self, x_main, x_sub, spk_embs, lengths, y=None):
+        return _LSTMEncFn.apply(self, x_main, x_sub, spk_embs[0], spk_embs[1], lengths,
+                                *self.parameters())
+
+
+class _LSTMEncFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mod, x_main, x_sub, s0, s1, lengths, *params):
+        B, T, D = x_main.shape
+        dev = x_main.device
+        lens_host, lens_dev = lengths_pair(lengths, B, T, dev)
+        p0, ld0, f0 = _spk_args(s0, B, T)
+        p1, ld1, f1 = _spk_args(s1, B, T)
+        if f0 is not None or f1 is not None or ld0 != ld1:
+            raise NotImplementedError("per-frame speaker embeddings are not on the path")
+        xm = x_main.contiguous().float()
+        xs = x_sub.contiguous().float()
+        out, st = mod._fwd(xm, xs, D, B, T, lens_dev, (p0, p1), ld0)
+        ctx.mod, ctx.st, ctx.params = mod, st, params
+        ctx.needs = (s0 is not None and s0.requires_grad, s1 is not None and s1.requires_grad)
+        Tm = max(lens_host)
+        out = out.view(B, T, -1)
+        return out[:, :Tm] if Tm < T else out
+
+    @staticmethod
+    def backward(ctx, g):
+        st = ctx.st
+        B, T = st["B"], st["T"]
+        g = g.contiguous()
+        if g.shape[1] < T:
+            gg = torch.zeros(B, T, g.shape[2], device=g.device)
+            gg[:, :g.shape[1]] = g
+            g = gg
+        with GradCapture(ctx.params) as gc:
+            _, _, dX = ctx.mod._bwd(st, g.view(B * T, -1), want_spk=False)
+        ctx.st = ctx.params = None
+        # per-frame grad of each (expanded) speaker input = its half of the fused input grad
+        E = ctx.mod.embed_dim
+        d = dX.view(B, T, 2 * E)
+        out = [d[:, :, k * E:(k + 1) * E] if need else None for k, need in enumerate(ctx.needs)]
+        return (None, None, None, out[0], out[1], None) + gc.grads(ctx.needs_input_grad[6:])

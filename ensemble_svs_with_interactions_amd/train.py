@@ -191,23 +191,20 @@ def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, 
     model.train()
     optimizer.zero_grad()
     if logf0_diff_weight > 0.0 and (not model.output_subtrack or y_sub is None):
-        raise ValueError("logf0_diff_weight > 0 needs output_subtrack=True and y_sub")
-    if _STATE_FUSED["on"]:
+        raise ValueError("logf0_diff_weight > 0 needs output_subtrack=True and y_sub (the "
+                         "SeparateF0 model: through its forward, with autograd)")
+    if _STATE_FUSED["on"] and getattr(model, "_train_fused", None) is not None:
         return _loss_and_grads_fused(model, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
                                      draws, ddp, y_sub, logf0_diff_weight)
     outs, st = model._train_fwd(x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws)
     B, T = st["B"], st["T"]
     Dy = y_main.shape[2]
     o = model._stream_cols()
-    nm, nb = model.stream_sizes[0], model.stream_sizes[3]
-    preds = [(outs["mgc_recon"], nm, 0, nm), (outs["lf0"], 1, 0, 1), (outs["vuv"], 1, 0, 1),
-             (outs["bap_recon"], nb, 0, nb)]
-    targets = [(outs["mgc_noise"], nm, 0), (y_main, Dy, o[1]), (y_main, Dy, o[2]),
-               (outs["bap_noise"], nb, 0)]
+    preds, targets, keys = model._l1_terms(outs, y_main)
     W = world_size() if ddp else 1
-    loss, (g_m, g_l, g_v, g_b) = masked_l1(preds, targets, st["lens_dev"], sum(st["lens_host"]),
-                                           B, T, grad_scale=1.0 / W)
-    g = dict(mgc_recon=g_m, lf0=g_l.view(-1), vuv=g_v, bap_recon=g_b)
+    loss, grads = masked_l1(preds, targets, st["lens_dev"], sum(st["lens_host"]), B, T,
+                            grad_scale=1.0 / W)
+    g = {k: gi.view(-1) if k == "lf0" else gi for k, gi in zip(keys, grads)}
     if logf0_diff_weight > 0.0:
         if not model.output_subtrack or y_sub is None:
             raise ValueError("logf0_diff_weight > 0 needs output_subtrack=True and y_sub")

@@ -240,8 +240,10 @@ def resf0_decoder(P, prefix, cfg, enc, dropout_masks, targets=None):
 
 
 def lf0_model(P, prefix, cfg, x_main, x_sub, spk_main, spk_sub, lengths, dropout_masks,
-              training=True, bn_updates=None, fast=False, relu_masks=None):
-    """MultiTrackBiLSTMResF0NonAttentiveDecoder.forward (tacotron_f0.py:924-991)."""
+              training=True, bn_updates=None, fast=False, relu_masks=None, y=None):
+    """MultiTrackBiLSTMResF0NonAttentiveDecoder.forward (tacotron_f0.py:924-991); y: the
+    normalised log-F0 target (B, T, 1) for teacher forcing (the SeparateF0 model,
+    multistream.py:479-484), None = free-running."""
     li = cfg["in_lf0_idx"]
     s_main = x_main[:, :, li].unsqueeze(-1)
     s_sub = x_sub[:, :, li].unsqueeze(-1)
@@ -255,7 +257,7 @@ def lf0_model(P, prefix, cfg, x_main, x_sub, spk_main, spk_sub, lengths, dropout
     out = torch.cat([out, s_main[:, :out.shape[1]], s_sub[:, :out.shape[1]]], -1)
     dcfg = dict(cfg)
     dcfg["in_lf0_idx"] = -2  # tacotron_f0.py:896
-    return resf0_decoder(P, prefix + "decoder.", dcfg, out, dropout_masks)
+    return resf0_decoder(P, prefix + "decoder.", dcfg, out, dropout_masks, targets=y)
 
 
 def bilstm_lf0_model(P, prefix, cfg, x, lengths, dropout_masks, y=None, training=True,
@@ -695,3 +697,68 @@ def transformer_encoder(P, cfg, x, lengths, keeps=None):
         h = ln(f"encoder.norm_layers_2.{i}", h + y)
     h = h * m
     return linear(P, "fc_out", h).view(B, -1, cfg["out_dim"])
+
+
+# ------------------------------------------------- SeparateF0 recipe model
+
+def lstm_encoder(P, prefix, cfg, x_main, x_sub, spk_main, spk_sub, lengths, fast=False,
+                 layer_dropout_masks=None):
+    """MultiTrackLSTMEncoder.forward (nnsvs/model.py:1494-1537): each track's phoneme
+    embedding + its speaker vector, concatenated, packed bi-LSTM, hidden2out."""
+    a = phoneme_embed(P, prefix, x_main, cfg["in_ph_start_idx"], cfg["in_ph_end_idx"]) + spk_main
+    b = phoneme_embed(P, prefix, x_sub, cfg["in_ph_start_idx"], cfg["in_ph_end_idx"]) + spk_sub
+    out = bilstm(P, prefix, torch.cat([a, b], -1), lengths, cfg["num_layers"],
+                 layer_dropout_masks, fast)
+    return linear(P, prefix + "hidden2out", out)
+
+
+def separate_f0_forward(P, cfg, x_main, x_sub, spks, lengths, ys, draws, training=True,
+                        bn_updates=None, fast=False):
+    """MultiTrackMultistreamSeparateF0ParametricModel.forward (multistream.py:447-567).
+
+    ys: [y_main, y_sub] targets (teacher forcing) or None (inference branch).  draws:
+    'lf0_main' / 'lf0_sub' AR dropout masks, optional '<mgc|vuv|bap>[_sub]_lstm' LSTM
+    inter-layer masks.  The sub-track decoders read the MAIN decoder input (:519-521).
+    Returns ((out_main, res_main), (out_sub, res_sub)) with ys, (out_main, out_sub) without.
+    """
+    lcfg = dict(cfg["lf0_model"])
+    for k in ("in_lf0_min", "in_lf0_max", "out_lf0_mean", "out_lf0_scale"):
+        lcfg[k] = cfg[k]  # _set_lf0_params, multistream.py:430-437
+    sizes = cfg["stream_sizes"]
+    emb = P["speaker_embedding.emb.weight"]
+    T = x_main.shape[1]
+    s0 = F.embedding(spks[0], emb).expand(-1, T, -1)
+    s1 = F.embedding(spks[1], emb).expand(-1, T, -1)
+    y_lf0 = [None, None] if ys is None else [split_streams(y, sizes)[1] for y in ys]
+    lf0_m, res_m = lf0_model(P, "lf0_model.", lcfg, x_main, x_sub, s0, s1, lengths,
+                             draws["lf0_main"], training, bn_updates, fast, y=y_lf0[0])
+    lf0_s, res_s = lf0_model(P, "lf0_model.", lcfg, x_sub, x_main, s1, s0, lengths,
+                             draws["lf0_sub"], training, bn_updates, fast, y=y_lf0[1])
+    enc = lstm_encoder(P, "encoder.", cfg["encoder"], x_main, x_sub, s0, s1, lengths, fast)
+    ri = cfg["in_rest_idx"]
+    teach = cfg.get("lf0_teacher_forcing", True) and ys is not None
+    din = torch.cat([enc, x_main[:, :, ri:ri + 1], y_lf0[0] if teach else lf0_m], -1)
+    dec = {}
+    for name in ("mgc", "vuv", "bap"):
+        for sfx in ("", "_sub"):
+            dec[name + sfx] = ffconvlstm(P, f"{name}_model.", cfg[f"{name}_model"], din, lengths,
+                                         None, training, bn_updates,
+                                         draws.get(f"{name}{sfx}_lstm"), fast)
+    out_m = torch.cat([dec["mgc"], lf0_m, dec["vuv"], dec["bap"]], -1)
+    out_s = torch.cat([dec["mgc_sub"], lf0_s, dec["vuv_sub"], dec["bap_sub"]], -1)
+    if ys is None:
+        return out_m, out_s
+    return (out_m, res_m), (out_s, res_s)
+
+
+def separate_f0_inference(P, cfg, x_main, x_sub, spks, lengths, masks_main, masks_sub,
+                          fast=False):
+    """pad_inference_multitrack (acoustic_models/util.py:154-188) around forward(ys=None)
+    in eval mode: the main output, trimmed."""
+    r = cfg["reduction_factor"]
+    pad, lens = pad_inference_lengths([int(v) for v in lengths], r)
+    xm, xs = replicate_pad(x_main, pad), replicate_pad(x_sub, pad)
+    out, _ = separate_f0_forward(P, cfg, xm, xs, spks, lens, None,
+                                 dict(lf0_main=masks_main, lf0_sub=masks_sub), training=False,
+                                 fast=fast)
+    return out[:, :-pad]

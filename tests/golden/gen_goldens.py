@@ -414,6 +414,133 @@ def case_model_inference_tiny():
     save("model_inference_tiny", arrays, meta)
 
 
+def sf0_ref(tiny):
+    """The SeparateF0 recipe model with the decoders' / encoder's nn.LSTM inter-layer
+    dropout off (torch's C++ RNG cannot be replayed; module docstring)."""
+    model, shapes = build_ref(configs.multitrack_separate_f0(num_speakers=4, tiny=tiny))
+    for m in (model.mgc_model, model.vuv_model, model.bap_model, model.encoder):
+        m.lstm.dropout = 0.0
+    return model, shapes
+
+
+def sf0_queue(d, T):
+    DROP.queue = [T_(d["lf0_main"][:, t]) for t in range(T // 4)] + \
+                 [T_(d["lf0_sub"][:, t]) for t in range(T // 4)]
+
+
+def case_sf0_forward(tiny, P, T, lengths, name):
+    """MultiTrackMultistreamSeparateF0ParametricModel.forward in training mode (teacher
+    forcing) through the reference API, then backward of sum(out_main * R0 + res_main * R1
+    + out_sub * R2 + res_sub * R3): outputs, BatchNorm running statistics after the call and
+    the parameter gradients (all of them for the tiny model, summaries for the full one)."""
+    model, shapes = sf0_ref(tiny)
+    model.train()
+    batch = data.synthetic_batch(P, T, SEED + 29, lengths=lengths)
+    d = dict(lf0_main=ar_masks(name + "_lm", P, T // 4), lf0_sub=ar_masks(name + "_ls", P, T // 4))
+    sf0_queue(d, T)
+    model.zero_grad()
+    (om, rm), (os_, rs) = model(T_(batch["x_main"]), T_(batch["x_sub"]),
+                                (T_(batch["spk_main"]).int(), T_(batch["spk_sub"]).int()),
+                                lengths=T_(batch["lengths"]),
+                                ys=[T_(batch["y_main"]), T_(batch["y_sub"])])
+    assert not DROP.queue
+    r = rng_for(name)
+    Rs = [r.standard_normal(tuple(t.shape)).astype(np.float32) for t in (om, rm, os_, rs)]
+    sum((t * T_(R)).sum() for t, R in zip((om, rm, os_, rs), Rs)).backward()
+    arrays = dict(**{k: v for k, v in batch.items()}, **{"draw::" + k: v for k, v in d.items()},
+                  out_main=om.detach().numpy(), res_main=rm.detach().numpy(),
+                  out_sub=os_.detach().numpy(), res_sub=rs.detach().numpy(),
+                  **{f"R{i}": R for i, R in enumerate(Rs)})
+    for k, v in model.state_dict().items():
+        if "running" in k:
+            arrays["bn::" + k] = v.numpy().copy()
+    if tiny:
+        for k, p_ in model.named_parameters():
+            arrays["grad::" + k] = (p_.grad if p_.grad is not None
+                                    else torch.zeros_like(p_)).numpy()
+    meta = dict(shapes={k: list(v) for k, v in shapes.items()}, grad_summary=grad_summary(model),
+                lengths=list(lengths))
+    save(name, arrays, meta)
+
+
+def case_sf0_train_tiny(steps=2, lr=1e-3):
+    """Two reference train steps (train_acoustic_multitrack.py:40-392: deterministic-loss
+    branch, feats_criterion l1, clip 1.0, Adam) of the tiny SeparateF0 model."""
+    model, shapes = sf0_ref(True)
+    P, T = 3, 48
+    batch = data.synthetic_batch(P, T, SEED + 31, lengths=[48, 40, 32])
+    opt = torch.optim.Adam(model.parameters(), lr=lr, betas=(0.9, 0.999), weight_decay=0.0)
+    model_config = types.SimpleNamespace(stream_sizes=[60, 1, 1, 5])
+    optim_config = types.SimpleNamespace(clip_norm=1.0)
+    logger = logging.getLogger("golden")
+    before = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    arrays = dict(**{k: v for k, v in batch.items()})
+    meta = dict(shapes={k: list(v) for k, v in shapes.items()}, lr=lr, steps=steps)
+    losses, norms = [], []
+    for s in range(steps):
+        d = dict(lf0_main=ar_masks(f"sf0_step{s}_lm", P, T // 4),
+                 lf0_sub=ar_masks(f"sf0_step{s}_ls", P, T // 4))
+        for k, v in d.items():
+            arrays[f"draw{s}::{k}"] = v
+        norm_box = {}
+        orig = torch.nn.utils.clip_grad_norm_
+
+        def clip(params, max_norm, *a, **k):
+            n = orig(params, max_norm, *a, **k)
+            norm_box["n"] = float(n)
+            return n
+        torch.nn.utils.clip_grad_norm_ = clip
+        try:
+            sf0_queue(d, T)
+            loss, _ = ref_train_step(
+                logger, model, model_config, optim_config, opt, None, True,
+                (T_(batch["x_main"]), T_(batch["x_sub"])),
+                [T_(batch["y_main"]), T_(batch["y_sub"])],
+                (T_(batch["spk_main"]).int(), T_(batch["spk_sub"]).int()),
+                (T_(batch["lengths"]), T_(batch["lengths"])),
+                None, None, feats_criterion="l1", pitch_reg_weight=0.0,
+                logf0_diff_weight=0.0, mgc_diff_weight=0.0)
+            assert not DROP.queue
+        finally:
+            torch.nn.utils.clip_grad_norm_ = orig
+        losses.append(float(loss))
+        norms.append(norm_box["n"])
+        if s == 0:
+            after = {k: v.detach().clone() for k, v in model.state_dict().items()}
+            for k in after:
+                if after[k].dtype == torch.float32:
+                    arrays[f"delta0::{k}"] = (after[k] - before[k]).numpy()
+    for k, v in model.state_dict().items():
+        if v.dtype == torch.float32:
+            arrays[f"final::{k}"] = v.numpy()
+    meta.update(losses=losses, grad_norms=norms)
+    save("sf0_train_tiny", arrays, meta)
+
+
+def case_sf0_inference_tiny():
+    model, shapes = sf0_ref(True)
+    model.eval()
+    arrays, meta = {}, {}
+    for T in (29, 32):
+        batch = data.synthetic_batch(2, T, SEED + 37 + T, lengths=[T, T - 5])
+        pad = 4 - T % 4
+        Tp = T + pad
+        masks = ar_masks(f"sf0_inf_{T}_lm", 2, Tp // 4), ar_masks(f"sf0_inf_{T}_ls", 2, Tp // 4)
+        sf0_queue(dict(lf0_main=masks[0], lf0_sub=masks[1]), Tp)
+        with torch.no_grad():
+            out = model.inference(T_(batch["x_main"]), T_(batch["x_sub"]),
+                                  spks=(T_(batch["spk_main"]).int(), T_(batch["spk_sub"]).int()),
+                                  lengths=T_(batch["lengths"]))
+        assert not DROP.queue
+        for k in ("x_main", "x_sub", "spk_main", "spk_sub", "lengths"):
+            arrays[f"T{T}::{k}"] = batch[k]
+        arrays[f"T{T}::masks_main"] = masks[0]
+        arrays[f"T{T}::masks_sub"] = masks[1]
+        arrays[f"T{T}::out"] = out.numpy()
+        meta[f"T{T}"] = dict(pad=pad, out_shape=list(out.shape))
+    save("sf0_inference_tiny", arrays, meta)
+
+
 def st_draws(name, P, T):
     r = rng_for(name)
     return dict(lf0_main=ar_masks(name + "_lm", P, T // 4),
@@ -1100,6 +1227,11 @@ def main():
         case_onset_merge()
     if run("loader"):
         case_loader()
+    if run("sf0"):
+        case_sf0_forward(True, 3, 40, [40, 33, 21], "sf0_forward_tiny")
+        case_sf0_forward(False, 2, 32, [32, 28], "sf0_forward_full")
+        case_sf0_train_tiny()
+        case_sf0_inference_tiny()
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(dict(seed=SEED, torch=torch.__version__, numpy=np.__version__,
                        reference="sarulab-speech/ensemble_svs_with_interactions @ 2025-03-21",

@@ -7,7 +7,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libensvs.so")
+# ENSVS_LIB: another in-tree build of the same ABI, for A/B timing of a kernel change
+# (tools/ab_lib.sh); the default is the package's own libensvs.so
+LIB_PATH = os.environ.get("ENSVS_LIB") or os.path.join(_HERE, "libensvs.so")
 
 c_int = ctypes.c_int
 c_ll = ctypes.c_longlong

@@ -1941,11 +1941,31 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
 // ------------------------------------------------- weight grads, bf16 operands
 // wgrad_kernel<bf16> with dy and x already rounded to bf16 in HBM (the staging rounding of
 // wgrad_kernel, so the result is bit-identical): both [32 frames][128 channels] images
-// are filled by global_load_lds_dwordx4, double-buffered with a counted vmcnt and raw
-// barriers.  The images keep wg_off's XOR swizzle (conflict-free ds_read_b64_tr_b16
+// are filled by global_load_lds_dwordx4 into a WNS-slot ring (64 KB of LDS; WNS - 1 chunks,
+// 48 KB, in flight per workgroup, 96 KB per CU at two workgroups: a 32-frame chunk is only 16 MFMAs
+// per wave, so one chunk in flight left every chunk's L2 latency exposed), with a counted
+// vmcnt and raw barriers.  The images keep wg_off's XOR swizzle (conflict-free ds_read_b64_tr_b16
 // operand reads); the DMA writes lane-linearly, so each lane fetches the chunk that the
 // swizzle maps to its slot.  a.dy / a.x point at bf16 rows here (ldy / ldx in elements).
 __device__ __forceinline__ int wg_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+// wg_frag's two transposed reads issued by inline asm.  The builtin's LDS read makes the
+// compiler drain every outstanding global_load_lds first (s_waitcnt vmcnt(0) in front of
+// it: it cannot tell the read from the ring slots being filled), which serialised each
+// chunk's DMA with the MFMAs.  The caller waits with a counted lgkmcnt that takes the
+// destination registers as operands, so nothing reads them earlier.
+typedef __attribute__((address_space(3))) char lds_char;
+__device__ __forceinline__ void wg_frag_issue(const char* img, int c0, int lane, bf16x4& lo,
+                                              bf16x4& hi) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int ch = (c0 >> 3) + (p >> 1);
+  const unsigned base = (unsigned)(size_t)(const lds_char*)img;
+  const unsigned o0 = base + wg_off(8 * g + q, ch) + 8 * (p & 1);
+  const unsigned o1 = base + wg_off(8 * g + 4 + q, ch) + 8 * (p & 1);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(o0) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(o1) : "memory");
+}
+constexpr int WNS = 4;  // wgrad_b16 ring slots (static_assert below: wait counts cover WNS-2)
+static_assert(WNS >= 2 && WNS - 2 <= 2, "wgrad_b16 waits for at most 2 chunks ahead");
 
 __global__ __launch_bounds__(NTHR) void wgrad_b16_kernel(const WgradArgs a) {
   constexpr int IMG = BK * 256;  // bytes per operand image (32 frames x 128 channels bf16)
@@ -1974,7 +1994,7 @@ __global__ __launch_bounds__(NTHR) void wgrad_b16_kernel(const WgradArgs a) {
     ft[i] = m - fb[i] * a.Tout;
   }
   auto issue = [&](int ch) __attribute__((always_inline)) {
-    char* A = smem + (ch & 1) * 2 * IMG;
+    char* A = smem + (ch % WNS) * 2 * IMG;
     char* Bm = A + IMG;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -2003,24 +2023,45 @@ __global__ __launch_bounds__(NTHR) void wgrad_b16_kernel(const WgradArgs a) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (nch > 0) issue(0);
+  // 4 DMA instructions per lane and chunk: chunk ch has landed once at most 4 * (chunks
+  // issued after it) remain outstanding
+#pragma unroll
+  for (int c = 0; c < WNS - 1; ++c)
+    if (c < nch) issue(c);
   for (int ch = 0; ch < nch; ++ch) {
-    wait_vm<0>();
-    __builtin_amdgcn_s_barrier();  // chunk ch visible; every wave is done with chunk ch-1
-    if (ch + 1 < nch) issue(ch + 1);
-    const char* A = smem + (ch & 1) * 2 * IMG;
+    const int ahead = min(WNS - 2, nch - 1 - ch);
+    if (ahead >= 2) wait_vm_n<8>();
+    else if (ahead == 1) wait_vm_n<4>();
+    else wait_vm_n<0>();
+    // chunk ch visible to every wave; every wave is done with chunk ch-1, whose slot the
+    // next issue refills
+    __builtin_amdgcn_s_barrier();
+    if (ch + WNS - 1 < nch) issue(ch + WNS - 1);
+    const char* A = smem + (ch % WNS) * 2 * IMG;
     const char* Bm = A + IMG;
-    bf16x8 fa[4], fbv[4];
+    // B fragments, then A fragment rows; row i's MFMAs start once its reads have returned
+    bf16x4 blo[4], bhi[4], alo[4], ahi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wg_frag_issue(Bm, wc * 64 + i * 16, lane, blo[i], bhi[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wg_frag_issue(A, wr * 64 + i * 16, lane, alo[i], ahi[i]);
+    asm volatile("s_waitcnt lgkmcnt(6)"
+                 : "+v"(blo[0]), "+v"(bhi[0]), "+v"(blo[1]), "+v"(bhi[1]), "+v"(blo[2]),
+                   "+v"(bhi[2]), "+v"(blo[3]), "+v"(bhi[3]), "+v"(alo[0]), "+v"(ahi[0]));
+    bf16x8 fbv[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+      fbv[jj] = __builtin_shufflevector(blo[jj], bhi[jj], 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      fa[i] = wg_frag(A, wr * 64 + i * 16, lane);
-      fbv[i] = wg_frag(Bm, wc * 64 + i * 16, lane);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
+      if (i == 1) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(alo[1]), "+v"(ahi[1]));
+      if (i == 2) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(alo[2]), "+v"(ahi[2]));
+      if (i == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(alo[3]), "+v"(ahi[3]));
+      const bf16x8 fa = __builtin_shufflevector(alo[i], ahi[i], 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
-        acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fbv[jj], acc[i][jj], 0, 0, 0);
+        acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fbv[jj], acc[i][jj], 0, 0, 0);
+    }
   }
   if (a.splits == 1) {
 #pragma unroll
@@ -2661,7 +2702,7 @@ ENSVS_API int ensvs_conv_wgrad_bf16(const void* dy, int ldy, const void* x, int 
   dim3 grid(cdiv(N, BM), cdiv(K, BN), taps * splits);
   if (N * taps > 65535) return ENSVS_E_SHAPE;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(wgrad_b16_kernel, grid, dim3(NTHR), 2 * 2 * BK * 256, st, a);
+  hipLaunchKernelGGL(wgrad_b16_kernel, grid, dim3(NTHR), WNS * 2 * BK * 256, st, a);
   ENSVS_CHECK_LAUNCH();
   if (splits > 1) {
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(K, 256), N * taps), dim3(256), 0, st, part,

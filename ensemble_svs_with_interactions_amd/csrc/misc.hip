@@ -193,22 +193,44 @@ __global__ void bn_bwd_reduce_kernel(const float* __restrict__ dout, int ldd,
 }
 
 // sums[g][0|1][c] = sum_s part; dgamma[c] += sum_g sums1, dbeta[c] += sum_g sums0
-__global__ void bn_bwd_final_kernel(const float* __restrict__ part, int S, int G, int C,
-                                    float* __restrict__ sums, float* __restrict__ dgamma,
-                                    float* __restrict__ dbeta) {
+// grid (ceil(C/64), G), 1024 threads: 16 lane rows split the S partials of 64 channels
+// (s = row, row + 16, ...), then fold in a fixed order; one workgroup per group g (a
+// single-workgroup serial sum over S ~ 480 splits took 63 us on the branch's chain).
+__global__ __launch_bounds__(1024) void bn_bwd_final_kernel(
+    const float* __restrict__ part, int S, int C, float* __restrict__ sums) {  // sums[g][2][C]
+  __shared__ double red[2][16][65];
+  const int cl = threadIdx.x & 63, row = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, g = blockIdx.y;
+  double a = 0.0, b = 0.0;
+  if (c < C)
+    for (int s = row; s < S; s += 16) {
+      a += part[(((long long)g * S + s) * 2) * C + c];
+      b += part[(((long long)g * S + s) * 2 + 1) * C + c];
+    }
+  red[0][row][cl] = a;
+  red[1][row][cl] = b;
+  __syncthreads();
+  if (row == 0 && c < C) {
+    double ta = 0.0, tb = 0.0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      ta += red[0][r][cl];
+      tb += red[1][r][cl];
+    }
+    sums[(g * 2) * C + c] = (float)ta;
+    sums[(g * 2 + 1) * C + c] = (float)tb;
+  }
+}
+
+// dgamma[c] += sum_g sum dz*xhat, dbeta[c] += sum_g sum dz (groups in order)
+__global__ void bn_param_grad_kernel(const float* __restrict__ sums, int G, int C,
+                                     float* __restrict__ dgamma, float* __restrict__ dbeta) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double tg = 0.0, tb = 0.0;
   for (int g = 0; g < G; ++g) {
-    double a = 0.0, b = 0.0;
-    for (int s = 0; s < S; ++s) {
-      a += part[(((long long)g * S + s) * 2) * C + c];
-      b += part[(((long long)g * S + s) * 2 + 1) * C + c];
-    }
-    sums[(g * 2) * C + c] = (float)a;
-    sums[(g * 2 + 1) * C + c] = (float)b;
-    tb += a;
-    tg += b;
+    tb += sums[(g * 2) * C + c];
+    tg += sums[(g * 2 + 1) * C + c];
   }
   dgamma[c] += (float)tg;
   dbeta[c] += (float)tb;
@@ -653,8 +675,11 @@ ENSVS_API int ensvs_bn_bwd(const float* dout, int ldd, const float* y, int ldy, 
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(cdiv(C, 64), S, G), dim3(256), 0, st, dout, ldd, y,
                      ldy, Mg, C, mean, rstd, gamma, beta, rps, part);
   ENSVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, part, S, G, C, sums,
-                     dgamma, dbeta);
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, 64), G), dim3(1024), 0, st, part, S, C,
+                     sums);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_param_grad_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, G, C, dgamma,
+                     dbeta);
   ENSVS_CHECK_LAUNCH();
   LAUNCH(bn_bwd_apply_kernel, M * C, dout, ldd, y, ldy, M, C, Mg, mean, rstd, gamma, beta, sums, dy,
          lddy);

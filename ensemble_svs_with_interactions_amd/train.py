@@ -221,12 +221,12 @@ def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, 
 
 
 # Per-branch fused schedule (forward -> loss gradient -> backward of each branch on its own
-# stream, acoustic_models._train_fused).  Off by default: measured 22.3 vs 22.0 ms/step for
-# the forward-all / loss / backward-all schedule (graph replay, 30 x 1024) -- the short
-# branches' backward then contends with the mgc forward, the longest chain.
-# ENSVS_FUSED_BRANCHES=1 turns it on.
+# stream, acoustic_models._train_fused), the default: with 8 hardware queues it measured
+# 20.4 vs 20.6 ms/step for the forward-all / loss / backward-all schedule (graph replay,
+# 30 x 1024; with 4 queues it was 22.3 vs 22.0).  Same gradients bitwise; the loss is the
+# sum of the branches' partial losses.  ENSVS_FUSED_BRANCHES=0 turns it off.
 import os as _os  # noqa: E402
-_STATE_FUSED = {"on": _os.environ.get("ENSVS_FUSED_BRANCHES", "0") == "1"}
+_STATE_FUSED = {"on": _os.environ.get("ENSVS_FUSED_BRANCHES", "1") == "1"}
 
 
 def set_fused_branches(on: bool):

@@ -680,14 +680,21 @@ class GaussianDiffusion(BaseModel):
             # warm-up outside capture (packs the weights, reads the schedule to the host)
             self.denoise_fn._packs.ensure(self.denoise_fn, self.denoise_fn._register)
             self._schedule_host()
-            side = torch.cuda.Stream(dev)
-            side.wait_stream(torch.cuda.current_stream(dev))
+            # captured on the stream it is replayed on (a branch stream of the inference):
+            # captured on a fresh pool stream, the mgc and bap graphs replayed serially
+            # whenever those capture streams shared a hardware queue (pair inference 116
+            # vs 84 ms after a training step had drawn pool streams first)
+            cur = torch.cuda.current_stream(dev)
+            side = cur if cur.cuda_stream != 0 else torch.cuda.Stream(dev)
+            if side is not cur:
+                side.wait_stream(cur)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.stream(side), torch.cuda.graph(g, stream=side):
                 call("ensvs_copy_cols", nz[0].data_ptr(), Mc, st["x"].data_ptr(), Mc, M, Mc,
                      Ly.stream())
                 self._reverse(st["x"], st["cond"], E, B, T, lambda k: nz[k + 1], st["steps"])
-            torch.cuda.current_stream(dev).wait_stream(side)
+            if side is not cur:
+                cur.wait_stream(side)
             st["graph"] = g
             cache[(B, T, E, str(dev))] = ent = st
         call("ensvs_copy_cols", cond.data_ptr(), E, ent["cond"].data_ptr(), E, M, E, Ly.stream())

@@ -44,6 +44,30 @@ class _timed:
         return self.ctx.__exit__(*exc)
 
 
+def branch_streams(device, n_side=3):
+    """The side streams of Branches(device, n_side), created on first use, each given its
+    first command at once.  HIP binds a stream to a hardware queue when the stream is first
+    used: side streams first used inside GraphedTrainStep's warm-up (on its capture stream)
+    left the two reverse-diffusion graphs of every later inference unable to overlap (pair
+    inference 116 ms, slower than the serial 109 ms); created and touched before the
+    capture stream (GraphedTrainStep calls this first): 83 ms
+    (tools/infer_streams_probe.py)."""
+    key = (str(device), n_side)
+    if key not in _SIDE_STREAMS:
+        # equal priorities: with the DiffNet backward's per-block launches batched, a
+        # high-priority branch (ENSVS_PRIO_BRANCH=i) measured slower -- lf0 23.5, mgc 23.4,
+        # bap 22.2 vs 22.2 ms/step for none (graph replay, 30 x 1024)
+        hi = int(os.environ.get("ENSVS_PRIO_BRANCH", "-1"))
+        _SIDE_STREAMS[key] = [torch.cuda.Stream(device, priority=-1 if i == hi else 0)
+                              for i in range(n_side)]
+        if os.environ.get("ENSVS_TOUCH_STREAMS", "1") == "1":
+            cur = torch.cuda.current_stream(device)
+            for s in _SIDE_STREAMS[key]:  # first command on each side stream now
+                s.wait_stream(cur)
+                cur.wait_stream(s)
+    return _SIDE_STREAMS[key]
+
+
 def set_concurrency(on: bool):
     """Run the independent branches of the step (lf0 / mgc / bap / vuv) on their own HIP
     streams (default) or serially on the current stream."""
@@ -63,18 +87,7 @@ class Branches:
     def __init__(self, device, n_side=3):
         self.device = device
         self.on_side = _STATE["concurrent"] and torch.cuda.is_available()
-        if self.on_side:
-            key = (str(device), n_side)
-            if key not in _SIDE_STREAMS:
-                # equal priorities: with the DiffNet backward's per-block launches batched,
-                # a high-priority branch (ENSVS_PRIO_BRANCH=i) measured slower -- lf0 23.5,
-                # mgc 23.4, bap 22.2 vs 22.2 ms/step for none (graph replay, 30 x 1024)
-                hi = int(os.environ.get("ENSVS_PRIO_BRANCH", "-1"))
-                _SIDE_STREAMS[key] = [torch.cuda.Stream(device, priority=-1 if i == hi else 0)
-                                      for i in range(n_side)]
-            self.side = _SIDE_STREAMS[key]
-        else:
-            self.side = []
+        self.side = branch_streams(device, n_side) if self.on_side else []
 
     def __enter__(self):
         self.aux_used = []

@@ -14,7 +14,8 @@ import torch
 
 from . import layers as Ly
 from ._lib import call
-from .engine import empty, flatten_parameters, weights_updated
+from .engine import branch_streams, empty, flatten_parameters, weights_updated
+from .engine import _STATE as _ENGINE_STATE
 
 
 class FusedAdam:
@@ -303,6 +304,8 @@ class GraphedTrainStep:
         self.inputs = dict(x_main=cl(x_main), x_sub=cl(x_sub), y_main=cl(y_main),
                            spk_main=cl(spk_main), spk_sub=cl(spk_sub))
         dev = x_main.device
+        if _ENGINE_STATE["concurrent"]:
+            branch_streams(dev)  # before the capture stream (engine.branch_streams)
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):

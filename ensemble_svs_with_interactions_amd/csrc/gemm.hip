@@ -2300,6 +2300,31 @@ static int fill_gemm_args(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int
   a.aux1_bf = (epi & EPI_AUX1_BF16) ? 1 : 0;
   epi &= 0xff;
   if ((a.aux0_bf && epi != EPI_GATE) || (a.aux1_bf && epi != EPI_GATE_BWD)) return ENSVS_E_ARG;
+  // each epilogue's output / operand widths: an inconsistent set would index past the
+  // caller's rows (the kernels trust these)
+  switch (epi) {
+    case EPI_PLAIN:
+      if (Y && ldy < N) return ENSVS_E_SHAPE;
+      break;
+    case EPI_GATE:
+    case EPI_GATE_TS:
+    case EPI_RESSKIP:  // N = 2C interleaved pairs -> C output channels
+      if (C <= 0 || N != 2 * C || (Y && ldy < C)) return ENSVS_E_SHAPE;
+      if (epi == EPI_GATE && aux0 && ld0 < 2 * C) return ENSVS_E_SHAPE;
+      if (epi == EPI_RESSKIP && (!Y || !aux0 || !aux1 || ld0 < C || ld1 < C)) return ENSVS_E_ARG;
+      break;
+    case EPI_GATE_BWD:  // N = C channels of dz -> 2C pre-activation gradients
+      if (C <= 0 || N != C || !aux1 || ld1 < 2 * C || (Y && ldy < 2 * C)) return ENSVS_E_SHAPE;
+      break;
+    case EPI_ADDSCALE:
+    case EPI_RELU_MASK:
+      if (!Y || !aux1 || ldy < N || ld1 < N) return ENSVS_E_ARG;
+      break;
+    case EPI_NONE:
+      break;
+    default:
+      return ENSVS_E_ARG;
+  }
   a.nseg = nseg;
   a.Tout = Tout;
   a.M = B * Tout;

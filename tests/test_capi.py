@@ -59,3 +59,27 @@ def test_library_newer_than_sources():
 def test_workspace_query():
     # 1000 frames -> 4 chunks of 256 frames, each a V x C partial table
     assert _lib.query("ensvs_embed_bwd_workspace", 1000, 256, 47) == 4 * 47 * 256
+
+
+def test_gemm_rejects_inconsistent_epilogue_shapes():
+    """Argument validation runs before any launch (no GPU needed): epilogue widths that
+    would index past the caller's rows come back as E_SHAPE / E_ARG, not as a fault."""
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    seg = (_lib.ConvSeg * 1)()
+    seg[0].x = 16
+    seg[0].ld, seg[0].K, seg[0].taps, seg[0].Tin, seg[0].Kp = 256, 256, 1, 64, 256
+    f = lib.ensvs_conv_gemm
+    f.restype = ctypes.c_int
+    P = ctypes.c_void_p
+    # GATE_BWD expands C channels of dz into 2C outputs: N must equal C
+    rc = f(seg, 1, 1, 64, 512, 512, P(16), 1, None, P(16), 512, _lib.EPI_GATE_BWD, 0, 0, None,
+           0, P(16), 512, ctypes.c_float(0.0), 256, None)
+    assert rc == 1
+    # GATE: N = 2C interleaved gate/filter pairs
+    rc = f(seg, 1, 1, 64, 256, 256, P(16), 1, None, P(16), 256, _lib.EPI_GATE, 0, 0, P(16),
+           512, None, 0, ctypes.c_float(0.0), 256, None)
+    assert rc == 1
+    # RESSKIP needs its residual and skip operands
+    rc = f(seg, 1, 1, 64, 512, 512, P(16), 1, None, P(16), 256, _lib.EPI_RESSKIP, 0, 0, None,
+           0, None, 0, ctypes.c_float(0.0), 256, None)
+    assert rc == 4

@@ -314,13 +314,25 @@ __global__ void downsample_wgrad_kernel(DsArgs a, const float* __restrict__ de, 
   if (threadIdx.x == 4) db[c] += red[4][0];
 }
 
+// The decoder workgroup reserves its CU's LDS (lstm.hip excl_lds; ENSVS_LSTM_EXCLUSIVE=0: off)
+static size_t ar_excl_lds() {
+  static const int on = [] {
+    const char* e = getenv("ENSVS_LSTM_EXCLUSIVE");
+    return e ? atoi(e) : 1;
+  }();
+  return on ? 96 * 1024 : 0;  // + the static LDS: no 64 KB GEMM workgroup fits beside it
+}
+
 template <int H>
 int fwd_launch(const float* gx, int ldgx, const float* ofx, int ldo, const float* wpf,
                const float* wih_p, const float* wfo, int ldwfo, const float* score, int lds,
                const float* mask, const float* teach, int ldt, int B, int T, ArConsts k,
                float* lf0, float* res, float* sg, float* sc, float* sh, float* so, float* sp,
                hipStream_t st) {
-  hipLaunchKernelGGL(ardec_fwd_kernel<H>, dim3(B), dim3(4 * H), 0, st, gx, ldgx, ofx, ldo, wpf,
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)ardec_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+  if (attr != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(ardec_fwd_kernel<H>, dim3(B), dim3(4 * H), ar_excl_lds(), st, gx, ldgx, ofx, ldo, wpf,
                      wih_p, wfo, ldwfo, score, lds, mask, teach, ldt, T, k, lf0, res, sg, sc, sh,
                      so, sp);
   ENSVS_CHECK_LAUNCH();
@@ -332,7 +344,10 @@ int bwd_launch(const float* glf0, const float* gres, const float* wpb, const flo
                const float* wfo, int ldwfo, const float* mask, int teacher, int B, int T,
                ArConsts k, const float* sg, const float* sc, const float* so, float* dg,
                float* do4, hipStream_t st) {
-  hipLaunchKernelGGL(ardec_bwd_kernel<H>, dim3(B), dim3(4 * H), 0, st, glf0, gres, wpb, wih_p, wfo,
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)ardec_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+  if (attr != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(ardec_bwd_kernel<H>, dim3(B), dim3(4 * H), ar_excl_lds(), st, glf0, gres, wpb, wih_p, wfo,
                      ldwfo, mask, teacher, T, k, sg, sc, so, dg, do4);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;

@@ -343,16 +343,29 @@ __global__ __launch_bounds__(Geo<H>::TB) void lstm_bwd_kernel(
   }
 }
 
+// Each persistent recurrence workgroup reserves its CU's whole LDS, so no GEMM workgroup
+// of a concurrent branch stream lands beside it (a co-resident GEMM stretches the
+// latency-bound step): 20.8 vs 21.3 ms per training step (profiles/r2_schedule_ab.txt).
+// ENSVS_LSTM_EXCLUSIVE=0 turns it off.  Read once.
+static size_t excl_lds(size_t need) {
+  static const int on = [] {
+    const char* e = getenv("ENSVS_LSTM_EXCLUSIVE");
+    return e ? atoi(e) : 1;
+  }();
+  return on ? std::max<size_t>(need, 160 * 1024) : need;
+}
+
 template <int H>
 int launch_fwd(const float* gx, int ldg, const float* w0, const float* w1,
                const long long* lengths, int B, int T, float* y, int ldy, float* sv,
                hipStream_t st) {
   if (ldg % 4 || ldy % 4 || ((uintptr_t)gx | (uintptr_t)y | (uintptr_t)sv) % 16)
     return ENSVS_E_ARG;
+  const size_t lds = excl_lds(Geo<H>::FWD_LDS);
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)lstm_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, Geo<H>::FWD_LDS);
+      (const void*)lstm_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return ENSVS_E_HIP;
-  hipLaunchKernelGGL(lstm_fwd_kernel<H>, dim3(B, 2), dim3(Geo<H>::TF), Geo<H>::FWD_LDS, st,
+  hipLaunchKernelGGL(lstm_fwd_kernel<H>, dim3(B, 2), dim3(Geo<H>::TF), lds, st,
                      gx, ldg, w0, w1, lengths, T, y, ldy, sv);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
@@ -364,10 +377,11 @@ int launch_bwd(const float* dy, int lddy, const float* w0, const float* w1,
                hipStream_t st) {
   if (lddy % 4 || lddg % 4 || ((uintptr_t)dy | (uintptr_t)sv | (uintptr_t)dg) % 16)
     return ENSVS_E_ARG;
+  const size_t lds = excl_lds(Geo<H>::BWD_LDS);
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)lstm_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, Geo<H>::BWD_LDS);
+      (const void*)lstm_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return ENSVS_E_HIP;
-  hipLaunchKernelGGL(lstm_bwd_kernel<H>, dim3(B, 2), dim3(Geo<H>::TB), Geo<H>::BWD_LDS, st,
+  hipLaunchKernelGGL(lstm_bwd_kernel<H>, dim3(B, 2), dim3(Geo<H>::TB), lds, st,
                      dy, lddy, w0, w1, lengths, T, sv, dg, lddg);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;

@@ -60,9 +60,16 @@ def branch_streams(device, n_side=3):
         hi = int(os.environ.get("ENSVS_PRIO_BRANCH", "-1"))
         _SIDE_STREAMS[key] = [torch.cuda.Stream(device, priority=-1 if i == hi else 0)
                               for i in range(n_side)]
+        new = list(_SIDE_STREAMS[key])
+        if _STATE["aux"]:  # the auxiliary weight-gradient streams too (Branches.aux)
+            for k in range(2):
+                ak = (str(device), k)
+                if ak not in _AUX_STREAMS:
+                    _AUX_STREAMS[ak] = torch.cuda.Stream(device)
+                    new.append(_AUX_STREAMS[ak])
         if os.environ.get("ENSVS_TOUCH_STREAMS", "1") == "1":
             cur = torch.cuda.current_stream(device)
-            for s in _SIDE_STREAMS[key]:  # first command on each side stream now
+            for s in new:  # first command on each new stream now
                 s.wait_stream(cur)
                 cur.wait_stream(s)
     return _SIDE_STREAMS[key]

@@ -6,6 +6,6 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 rm -f gpurun_out/ab.txt
 while read -r n rest; do
   [ -z "$n" ] && continue
-  env $rest timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-synth --no-cpu-baseline --no-config2 > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err || exit 1
+  env $rest timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-synth --no-cpu-baseline --no-config2 $BENCH_ARGS > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err || exit 1
   python3 -c "import json; d=json.load(open('gpurun_out/ab_$n.json')); print('$n', round(d['ms_per_step'],2))" >> gpurun_out/ab.txt
 done < "$1"

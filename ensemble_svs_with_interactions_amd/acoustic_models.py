@@ -633,11 +633,15 @@ class _MultistreamHybrid(BaseModel):
                 dsp["lf0_sub"], _, _ = self.lf0_model._bwd(st["lf0_sub"], gs,
                                                            g.get("lf0_residual_sub"))
         elif i == 1:
-            hook = None
+            hooks = []
             if _VUV_AFTER_MGC["on"] and torch.cuda.is_available() and g["mgc_recon"].is_cuda:
                 ev = torch.cuda.Event()
                 dsp["_mgc_denoiser_done"] = ev
-                hook = lambda: ev.record(torch.cuda.current_stream())  # noqa: E731
+                hooks.append(lambda: ev.record(torch.cuda.current_stream()))
+            if dsp.get("_reduce") is not None:
+                red = dsp["_reduce"]
+                hooks.append(lambda: red("mgc_denoiser"))
+            hook = (lambda: [h() for h in hooks]) if hooks else None  # noqa: E731
             dsp["mgc"] = self.mgc_model._bwd(st["mgc"], g["mgc_recon"], after_denoiser=hook,
                                              want_spk=spk)
         elif i == 2:
@@ -692,21 +696,29 @@ class _MultistreamHybrid(BaseModel):
                     self._bwd_branch(i, st, g, dsp)
         self._bwd_epilogue(st, dsp)
 
-    def _train_fused(self, x_main, x_sub, y_main, spk0, spk1, lengths, draws, branch_loss):
+    def _train_fused(self, x_main, x_sub, y_main, spk0, spk1, lengths, draws, branch_loss,
+                     reduce_hook=None):
         """Training forward + loss gradient + backward with each branch end to end on its
         own stream: a branch's loss gradient needs only its own outputs (the masked L1
         normaliser is known on the host), so its backward starts when its forward ends,
         not when the slowest forward does.  branch_loss(i, outs, st) -> (partial loss
         (1,) tensor, grads dict of branch i); the partial losses are summed after the
-        join.  Returns (loss, outs)."""
+        join.  reduce_hook(tag): called on the branch's stream where a parameter group's
+        gradients are final ("lf0", "mgc_denoiser", "mgc", "bap", "vuv";
+        train.BucketedAllReduce).  Returns (loss, outs)."""
         c, st = self._fwd_prologue(x_main, x_sub, y_main, spk0, spk1, lengths, draws)
         outs, dsp, parts = {}, {}, {}
+        if reduce_hook is not None:
+            dsp["_reduce"] = reduce_hook
+        tags = ("lf0", "mgc", "bap", "vuv")
         with Branches(x_main.device) as br:
             for i in range(4):
                 with br.on(i):
                     self._fwd_branch(i, c, outs, st)
                     parts[i], g = branch_loss(i, outs, st)
                     self._bwd_branch(i, st, g, dsp)
+                    if reduce_hook is not None:
+                        reduce_hook(tags[i])
         loss = parts[0]
         for i in (1, 2, 3):
             call("ensvs_axpy", loss.data_ptr(), parts[i].data_ptr(), 1.0, 1, Ly.stream())

@@ -9,12 +9,13 @@ RCCL gradient all-reduce (data parallel over pairs), global-norm clipping,
 non-finite skip and Adam — every arithmetic op in libensvs.so, no host sync.
 """
 import ctypes
+from os import environ as _os_env
 
 import torch
 
 from . import layers as Ly
 from ._lib import call
-from .engine import branch_streams, empty, flatten_parameters, weights_updated
+from .engine import branch_streams, empty, flatten_parameters, grad_of, weights_updated
 from .engine import _STATE as _ENGINE_STATE
 
 
@@ -161,6 +162,73 @@ def allreduce_grads(gflat, group=None):
     dist.all_reduce(gflat, op=dist.ReduceOp.SUM, group=group)
 
 
+class BucketedAllReduce:
+    """Data-parallel gradient exchange overlapped with the backward: the flat gradient
+    buffer is all-reduced (SUM, async RCCL collectives) in buckets = the flat ranges of
+    the parameter groups whose gradients are final at known points of the fused per-branch
+    schedule -- the lf0, bap and V/UV models when their branch's backward ends, the mgc
+    DiffNet once its backward is done (before the mgc encoder's: the longest tail of the
+    step), the mgc encoder at the end of its branch, everything else (speaker embedding)
+    after the join.  Each launch is issued on the branch's stream (the collective waits for
+    that branch only) in the same host order on every rank; ``finish`` makes the current
+    stream wait for all of them.  Same sums as one all-reduce of the whole buffer
+    (element-wise); alignment pads between parameters are zeros and ride along."""
+
+    def __init__(self, model, gflat, group=None, align=64):
+        self.gflat, self.group, self.works = gflat, group, []
+        base, n = gflat.data_ptr(), gflat.numel()
+
+        def rng(params):
+            spans = sorted(((grad_of(p).data_ptr() - base) // 4,
+                            (grad_of(p).data_ptr() - base) // 4 + p.numel()) for p in params)
+            out = []
+            for a, b in spans:
+                assert 0 <= a and b <= n, "parameter gradient outside the flat buffer"
+                if out and a <= -(-out[-1][1] // align) * align:
+                    out[-1][1] = max(out[-1][1], b)
+                else:
+                    out.append([a, b])
+            return [tuple(r) for r in out]
+
+        den = list(model.mgc_model.denoise_fn.parameters())
+        den_ids = {id(p) for p in den}
+        groups = {"lf0": list(model.lf0_model.parameters()), "mgc_denoiser": den,
+                  "mgc": [p for p in model.mgc_model.parameters() if id(p) not in den_ids],
+                  "bap": list(model.bap_model.parameters()),
+                  "vuv": list(model.vuv_model.parameters())}
+        seen = {id(p) for ps in groups.values() for p in ps}
+        groups["rest"] = [p for p in model.parameters() if id(p) not in seen]
+        self.buckets = {k: rng(v) for k, v in groups.items() if v}
+
+    def launch(self, tag):
+        import torch.distributed as dist
+        for a, b in self.buckets.get(tag, ()):
+            self.works.append(dist.all_reduce(self.gflat[a:b], op=dist.ReduceOp.SUM,
+                                              group=self.group, async_op=True))
+
+    def finish(self):
+        self.launch("rest")
+        for w in self.works:
+            w.wait()
+        self.works = []
+
+
+# overlapped bucketed all-reduce in the eager fused step (W > 1); ENSVS_OVERLAP_ALLREDUCE=0:
+# one all-reduce of the whole buffer after the backward
+_STATE_OVERLAP = {"on": _os_env.get("ENSVS_OVERLAP_ALLREDUCE", "1") == "1"}
+
+
+def set_overlap_allreduce(on: bool):
+    _STATE_OVERLAP["on"] = bool(on)
+
+
+def _bucketed(model, optimizer):
+    br = getattr(optimizer, "_bucketed", None)
+    if br is None or br.gflat is not optimizer.gflat:
+        br = optimizer._bucketed = BucketedAllReduce(model, optimizer.gflat)
+    return br
+
+
 def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws=None,
                ddp=True, y_sub=None, logf0_diff_weight=0.0):
     """One training step on a (main, sub) pair batch.  Returns (loss, grad_norm) device tensors.
@@ -170,9 +238,10 @@ def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengt
     (train_acoustic_multitrack.py:175-182, 296; needs the output_subtrack model and y_sub).
     """
     loss = _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
-                           draws, ddp, y_sub, logf0_diff_weight)
-    if ddp and world_size() > 1:
+                           draws, ddp, y_sub, logf0_diff_weight, overlap=True)
+    if ddp and world_size() > 1 and not getattr(optimizer, "_reduced", False):
         allreduce_grads(optimizer.gflat)
+    optimizer._reduced = False
     optimizer.step()
     return loss, optimizer.norm
 
@@ -187,7 +256,7 @@ def train_step_single(model, optimizer, x, y, lengths, draws=None, ddp=True):
 
 
 def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws,
-                    ddp, y_sub, logf0_diff_weight):
+                    ddp, y_sub, logf0_diff_weight, overlap=False):
     """zero_grad + forward + masked L1 (+ interaction loss) + backward into the flat grads."""
     model.train()
     optimizer.zero_grad()
@@ -195,8 +264,17 @@ def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, 
         raise ValueError("logf0_diff_weight > 0 needs output_subtrack=True and y_sub (the "
                          "SeparateF0 model: through its forward, with autograd)")
     if _STATE_FUSED["on"] and getattr(model, "_train_fused", None) is not None:
-        return _loss_and_grads_fused(model, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
-                                     draws, ddp, y_sub, logf0_diff_weight)
+        reducer = None
+        if (overlap and ddp and _STATE_OVERLAP["on"] and world_size() > 1 and
+                getattr(model, "mgc_model", None) is not None and
+                hasattr(model.mgc_model, "denoise_fn")):
+            reducer = _bucketed(model, optimizer)
+        loss = _loss_and_grads_fused(model, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
+                                     draws, ddp, y_sub, logf0_diff_weight, reducer)
+        if reducer is not None:
+            reducer.finish()
+            optimizer._reduced = True
+        return loss
     outs, st = model._train_fwd(x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws)
     B, T = st["B"], st["T"]
     Dy = y_main.shape[2]
@@ -235,7 +313,7 @@ def set_fused_branches(on: bool):
 
 
 def _loss_and_grads_fused(model, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws,
-                          ddp, y_sub, logf0_diff_weight):
+                          ddp, y_sub, logf0_diff_weight, reducer=None):
     """The loss of _loss_and_grads split by branch: each branch's masked L1 over its own
     streams with the whole loss's element count (same gradients, elementwise), the
     interaction loss inside the lf0 branch; partial losses summed after the join."""
@@ -271,7 +349,8 @@ def _loss_and_grads_fused(model, x_main, x_sub, y_main, spk_main, spk_sub, lengt
         return loss, g
 
     loss, _ = model._train_fused(x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws,
-                                 branch_loss)
+                                 branch_loss, reduce_hook=None if reducer is None else
+                                 reducer.launch)
     return loss
 
 

@@ -91,17 +91,36 @@ def _rank(rank, port, out_dir):
             flats = gather(opt.flat)
             res[tag + "_param_mismatch"] = float((flats[0] - flats[1]).abs().max())
 
-        # 1 + 2: broadcast at init, fused step
+        # 1 + 2: broadcast at init, fused step (one all-reduce of the whole buffer)
         torch.manual_seed(1234 + rank)  # ranks initialise differently on purpose
         model = configs.instantiate(cfg).cuda()
         model.vuv_model.lstm.dropout = 0.0
         opt = train.FusedAdam(model, lr=1e-3)
         flats = gather(opt.flat)
         res["init_param_mismatch"] = float((flats[0] - flats[1]).abs().max())
+        train.set_overlap_allreduce(False)
         loss, norm = train.train_step(model, opt, xm, xs, ym, s0, s1, lens, draws=draws)
         torch.cuda.synchronize()
         check_mean(opt, "fused")
         fused_grad = opt.gflat.detach().cpu().clone()
+
+        # 2b: the same step with the bucketed all-reduce overlapped with the backward
+        # (train.BucketedAllReduce): the same reduced gradient, no whole-buffer all-reduce
+        torch.manual_seed(1234 + rank)
+        m2 = configs.instantiate(cfg).cuda()
+        m2.vuv_model.lstm.dropout = 0.0
+        o2 = train.FusedAdam(m2, lr=1e-3)
+        train.set_overlap_allreduce(True)
+        n_before = len(pre)
+        train.train_step(m2, o2, xm, xs, ym, s0, s1, lens, draws=draws)
+        torch.cuda.synchronize()
+        res["overlap_whole_buffer_calls"] = len(pre) - n_before
+        res["overlap_grad_err"] = float((o2.gflat.detach().cpu() - fused_grad).abs().max() /
+                                        fused_grad.abs().max())
+        res["overlap_buckets"] = sum(len(v) for v in o2._bucketed.buckets.values())
+        flats2 = gather(o2.flat)
+        res["overlap_param_mismatch"] = float((flats2[0] - flats2[1]).abs().max())
+        del m2, o2
 
         # 3: graph-replayed data-parallel steps
         gstep = train.GraphedTrainStep(model, opt, xm, xs, ym, s0, s1, lens, warmup=1)
@@ -164,4 +183,9 @@ def test_data_parallel_world2_product_step(tmp_path):
             assert z[tag + "_grad_err"] < 1e-6, (tag, z[tag + "_grad_err"])
             assert z[tag + "_param_mismatch"] == 0.0, tag
             assert z[tag + "_rank_grads_differ"] > 0.0, tag  # the shards really differ
+        # bucketed all-reduce overlapped with the backward: same reduced gradient (2 ranks:
+        # a + b either way), equal parameters on both ranks, no whole-buffer collective
+        assert z["overlap_grad_err"] < 1e-6, z["overlap_grad_err"]
+        assert z["overlap_param_mismatch"] == 0.0
+        assert z["overlap_whole_buffer_calls"] == 0 and z["overlap_buckets"] >= 6
         assert z["ddp_grad_err"] < 1e-5, z["ddp_grad_err"]

@@ -67,6 +67,7 @@ SIGNATURES = {
                                   c_ll, c_vp],
     "ensvs_set_big_tile": [c_int, c_int],
     "ensvs_set_dual_small": [c_int],
+    "ensvs_set_small": [c_int],
     "ensvs_tile_colsum": [c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "ensvs_cast_bf16": [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_int, c_vp, c_int, c_vp],
     "ensvs_conv_wgrad": [c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -109,6 +110,8 @@ SIGNATURES = {
     "ensvs_q_sample": [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_float,
                        c_vp, c_int, c_vp],
     "ensvs_p_sample": [c_vp, c_vp, c_vp, c_ll, c_float, c_float, c_float, c_float, c_float, c_vp],
+    "ensvs_p_sample_bf16": [c_vp, c_vp, c_vp, c_ll, c_int, c_float, c_float, c_float, c_float,
+                            c_float, c_vp, c_int, c_vp],
     "ensvs_masked_l1": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int,
                         c_float, c_float, c_vp, c_vp, c_vp],
     "ensvs_lf0_interaction": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_int,

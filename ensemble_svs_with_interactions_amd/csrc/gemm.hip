@@ -269,6 +269,13 @@ constexpr int EPI_LDS = BM * EP * 4 + CS_GROUPS * 2 * BN * 4;  // + column-sum e
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *(f32x4*)p = v; }
+// the same with the per-sequence add already loaded (rr)
+__device__ __forceinline__ void shadow4r(const GemmArgs& a, int m, int col, f32x4 v, f32x4 rr) {
+  if (!a.ybf) return;
+  if (a.ybf_radd) v += rr;
+  *(bf16x4*)(a.ybf + (long long)m * a.ybf_ld + col) =
+      bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
 // bf16 shadow of 4 consecutive outputs (row m, columns col..col+3), see GemmArgs::ybf
 __device__ __forceinline__ void shadow4(const GemmArgs& a, int m, int col, f32x4 v) {
   if (!a.ybf) return;
@@ -304,16 +311,18 @@ __device__ __forceinline__ void st8_aux0(const GemmArgs& a, long long i, f32x4 l
 
 // One row's 8 gate/filter channel pairs (GATE / GATE_TS epilogue): t points at the row's
 // staged accumulator tile, gc the tile column of the first gate value (filter +16), c the
-// first output channel.  (No global operand loads besides the bias, an L1 hit; the bias is
-// not held across rows: the 256 x 256 kernel keeps half its accumulators live here.)
-__device__ __forceinline__ void gate_row8(const GemmArgs& a, const float* t, int n0, int gc,
-                                          int m, int c) {
+// first output channel, bb the 16 bias values of those columns (read once per thread, or
+// null when the staged tile already holds acc + bias).  No global loads here: on gfx950
+// vmcnt counts stores too, so a load issued after a row's stores (the bias, formerly
+// re-read per row) waits for all of them -- one full store round trip per row.
+__device__ __forceinline__ void gate_row8(const GemmArgs& a, const float* t, int gc, int m,
+                                          int c, const f32x4* bb) {
   f32x4 g0 = ld4(t + gc), g1 = ld4(t + gc + 4), f0 = ld4(t + gc + 16), f1 = ld4(t + gc + 20);
-  if (a.bias) {
-    g0 += ld4(a.bias + n0 + gc);
-    g1 += ld4(a.bias + n0 + gc + 4);
-    f0 += ld4(a.bias + n0 + gc + 16);
-    f1 += ld4(a.bias + n0 + gc + 20);
+  if (bb) {
+    g0 += bb[0];
+    g1 += bb[1];
+    f0 += bb[2];
+    f1 += bb[3];
   }
   f32x4 z0, z1;
   if (a.epi == EPI_GATE) {
@@ -339,8 +348,9 @@ __device__ __forceinline__ void gate_row8(const GemmArgs& a, const float* t, int
 }
 
 // 8-channel GATE / GATE_TS rows of a staged tile: NTT threads, tile rows [0, ROWS), T row
-// stride ldT, ROWW 8-channel groups (threads) per row.
-template <int NTT, int ROWS, int ROWW>
+// stride ldT, ROWW 8-channel groups (threads) per row.  BIAS_IN_T: the staged tile already
+// holds acc + bias (the 256 x 256 kernel adds it while staging).
+template <int NTT, int ROWS, int ROWW, bool BIAS_IN_T = false>
 __device__ __forceinline__ void gate_tile8(const GemmArgs& a, const float* T, int ldT, int mb,
                                            int n0, int tid) {
   constexpr int NI = ROWS * ROWW / NTT;
@@ -349,12 +359,70 @@ __device__ __forceinline__ void gate_tile8(const GemmArgs& a, const float* T, in
   const int c = n0 / 2 + q * 16 + j;
   const int gc = q * 32 + j;
   if (c >= a.C) return;
+  f32x4 bb[4];
+  const bool hb = !BIAS_IN_T && a.bias;
+  if (hb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bb[i] = ld4(a.bias + n0 + gc + (i >> 1) * 16 + (i & 1) * 4);
+  }
 #pragma unroll 1
   for (int k = 0; k < NI; ++k) {
     const int row = tid / ROWW + k * (NTT / ROWW);
     const int m = mb + row;
     if (m >= a.M) continue;
-    gate_row8(a, T + row * ldT, n0, gc, m, c);
+    gate_row8(a, T + row * ldT, gc, m, c, hb ? bb : nullptr);
+  }
+}
+
+// RESSKIP epilogue operands of one row (residual input x, running skip sum, the next
+// block's per-sequence add for the bf16 copy), loaded a batch of rows AHEAD of the
+// previous batch's stores: vmcnt counts loads and stores in issue order, so a load issued
+// after stores can only be waited for together with them.
+struct RsOps {
+  f32x4 xr, s0, rr;
+};
+__device__ __forceinline__ void rs_load(const GemmArgs& a, int m, int c, RsOps& o) {
+  if (m >= a.M) return;
+  o.xr = ld4(a.aux1 + (long long)m * a.ld1 + c);
+  if (a.accum) o.s0 = ld4(a.aux0 + (long long)m * a.ld0 + c);
+  if (a.ybf && a.ybf_radd) o.rr = ld4(a.ybf_radd + (long long)(m / a.Tout) * a.ybf_radd_ld + c);
+}
+// x' = (x + r) / sqrt2 to Y (+ its bf16 copy with the next block's add), skip (+)= alpha * s
+__device__ __forceinline__ void rs_store(const GemmArgs& a, int m, int c, f32x4 g, f32x4 f,
+                                         const RsOps& o) {
+  f32x4 y, sk;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) y[e] = (o.xr[e] + g[e]) * 0.70710678118654752f;
+  st4(a.Y + (long long)m * a.ldy + c, y);
+  if (a.ybf) {
+    f32x4 v = y;
+    if (a.ybf_radd) v += o.rr;
+    *(bf16x4*)(a.ybf + (long long)m * a.ybf_ld + c) =
+        bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  }
+  if (a.accum) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sk[e] = fmaf(a.alpha, f[e], o.s0[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sk[e] = a.alpha * f[e];
+  }
+  st4(a.aux0 + (long long)m * a.ld0 + c, sk);
+}
+
+// operands of one row of the PLAIN (accum) / ADDSCALE / RELU_MASK / GATE_BWD epilogues
+__device__ __forceinline__ void gen_load(const GemmArgs& a, int m, int col, bool want2, f32x4& p1,
+                                         f32x4& p2) {
+  if (m >= a.M) return;
+  const float* y = a.Y + (long long)m * a.ldy + col;
+  if (a.epi == EPI_PLAIN) {
+    p1 = ld4(y);
+  } else if (a.epi == EPI_GATE_BWD) {
+    p1 = ld4_aux1(a, (long long)m * a.ld1 + col);
+    p2 = ld4_aux1(a, (long long)m * a.ld1 + a.C + col);
+  } else {
+    p1 = ld4(a.aux1 + (long long)m * a.ld1 + col);
+    if (want2) p2 = ld4(y);
   }
 }
 
@@ -380,7 +448,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
   }
   __syncthreads();
   const int M = a.M;
-  constexpr int EB = 2;  // rows whose operands are in flight together (register budget)
+  constexpr int EB = 1;  // rows per operand batch (one batch ahead in flight: register budget)
   // Every thread keeps one column group across its rows (NT is a multiple of 32), so the
   // bias is read once, and all of a thread's global operand loads (residual, skip, Y,
   // gate/filter save) are issued before its first store: with the loads after the stores
@@ -403,17 +471,17 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
       bfl = ld4(a.bias + n0 + gc + 16);
     }
     static_assert(NI % EB == 0, "rows per thread in batches of EB");
-#pragma unroll 1
-    for (int kb = 0; kb < NI; kb += EB) {
-    f32x4 xr[EB], s0[EB];
+    RsOps cur[EB], nxt[EB];
     if (a.epi == EPI_RESSKIP) {
 #pragma unroll
-      for (int k = 0; k < EB; ++k) {
-        const int m = m0 + (tid >> 4) + (kb + k) * (NT / 16);
-        if (m >= M) continue;
-        xr[k] = ld4(a.aux1 + (long long)m * a.ld1 + c);
-        if (a.accum) s0[k] = ld4(a.aux0 + (long long)m * a.ld0 + c);
-      }
+      for (int k = 0; k < EB; ++k) rs_load(a, m0 + (tid >> 4) + k * (NT / 16), c, cur[k]);
+    }
+#pragma unroll 1
+    for (int kb = 0; kb < NI; kb += EB) {
+    if (a.epi == EPI_RESSKIP && kb + EB < NI) {
+#pragma unroll
+      for (int k = 0; k < EB; ++k)
+        rs_load(a, m0 + (tid >> 4) + (kb + EB + k) * (NT / 16), c, nxt[k]);
     }
 #pragma unroll
     for (int k = 0; k < EB; ++k) {
@@ -425,7 +493,9 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         g += bg;
         f += bfl;
       }
-      if (a.epi == EPI_GATE) {
+      if (a.epi == EPI_RESSKIP) {
+        rs_store(a, m, c, g, f, cur[k]);
+      } else if (a.epi == EPI_GATE) {
         st4_aux0(a, (long long)m * a.ld0 + c, g);
         st4_aux0(a, (long long)m * a.ld0 + a.C + c, f);
         f32x4 z;
@@ -438,22 +508,10 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = ftanh_(g[e]) * fsigmoid_(f[e]);
         st4(a.Y + (long long)m * a.ldy + c, z);
-      } else {
-        f32x4 y, sk;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (xr[k][e] + g[e]) * 0.70710678118654752f;
-        st4(a.Y + (long long)m * a.ldy + c, y);
-        shadow4(a, m, c, y);
-        if (a.accum) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) sk[e] = fmaf(a.alpha, f[e], s0[k][e]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) sk[e] = a.alpha * f[e];
-        }
-        st4(a.aux0 + (long long)m * a.ld0 + c, sk);
       }
     }
+#pragma unroll
+    for (int k = 0; k < EB; ++k) cur[k] = nxt[k];
     }
     return;
   }
@@ -473,26 +531,20 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
                        a.epi == EPI_RELU_MASK || a.epi == EPI_GATE_BWD;
     const bool want2 = (a.epi == EPI_RELU_MASK && a.accum) || a.epi == EPI_GATE_BWD;
     static_assert(NI % EB == 0, "rows per thread in batches of EB");
+    // operands of a batch of rows, loaded before the previous batch's stores
+    const bool wl = ne == 4 && (want1 || want2);
+    f32x4 p1[EB], p2[EB], q1[EB], q2[EB];
+    if (wl) {
+#pragma unroll
+      for (int k = 0; k < EB; ++k)
+        gen_load(a, m0 + (tid >> 5) + k * (NT / 32), col, want2, p1[k], p2[k]);
+    }
 #pragma unroll 1
     for (int kb = 0; kb < NI; kb += EB) {
-    // operands of these rows, loaded before any of their stores
-    f32x4 p1[EB], p2[EB];
-    if (ne == 4 && (want1 || want2)) {
+    if (wl && kb + EB < NI) {
 #pragma unroll
-      for (int k = 0; k < EB; ++k) {
-        const int m = m0 + (tid >> 5) + (kb + k) * (NT / 32);
-        if (m >= M) continue;
-        const float* y = a.Y + (long long)m * a.ldy + col;
-        if (a.epi == EPI_PLAIN) {
-          p1[k] = ld4(y);
-        } else if (a.epi == EPI_GATE_BWD) {
-          p1[k] = ld4_aux1(a, (long long)m * a.ld1 + col);
-          p2[k] = ld4_aux1(a, (long long)m * a.ld1 + a.C + col);
-        } else {
-          p1[k] = ld4(a.aux1 + (long long)m * a.ld1 + col);
-          if (want2) p2[k] = ld4(y);
-        }
-      }
+      for (int k = 0; k < EB; ++k)
+        gen_load(a, m0 + (tid >> 5) + (kb + EB + k) * (NT / 32), col, want2, q1[k], q2[k]);
     }
 #pragma unroll
     for (int k = 0; k < EB; ++k) {
@@ -568,6 +620,11 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
           }
         }
       }
+    }
+#pragma unroll
+    for (int k = 0; k < EB; ++k) {
+      p1[k] = q1[k];
+      p2[k] = q2[k];
     }
     }
   }
@@ -1213,56 +1270,102 @@ __device__ __forceinline__ void xcd_tile_big(int& m0, int& n0) {
   n0 = (wg % nN) * BNB;
 }
 
-// one staged chunk: rows [0, CHR) of T are output rows mb.., columns [0, BNB) are n0..
-__device__ __forceinline__ void epilogue_chunk_big(const GemmArgs& a, const float* T, int mb,
-                                                   int n0, int tid) {
+// Operands of one batch of EB epilogue rows, loaded ahead of the previous batch's stores
+// (vmcnt counts loads and stores in issue order: a load issued after stores is waited for
+// together with them).  RESSKIP: x = residual input, y = running skip sum, z = the next
+// block's per-sequence add; other epilogues: x, y = their p1, p2 operands, z = the per-
+// sequence add of the bf16 copy (PLAIN / ADDSCALE).
+constexpr int EBB = 1;  // rows whose operands are in flight together (register budget: the
+                        // waves of the second row half still hold 128 accumulators)
+template <int EB>
+struct EpiPreT {
+  f32x4 x[EB], y[EB], z[EB];
+};
+using EpiPre = EpiPreT<EBB>;
+__device__ __forceinline__ bool big_pairs(const GemmArgs& a) {
+  return a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS;
+}
+// loads batch kb (rows kb .. kb + EB - 1 of this thread) of the chunk at mb into p
+template <int COLS, int NT, int EB = EBB>
+__device__ __forceinline__ void epi_pre(const GemmArgs& a, int mb, int n0, int tid, int kb,
+                                        EpiPreT<EB>& p) {
+  if (a.epi == EPI_RESSKIP) {
+    const int q4 = tid % (COLS / 8), c = n0 / 2 + (q4 >> 2) * 16 + (q4 & 3) * 4;
+    if (c >= a.C) return;
+#pragma unroll
+    for (int k = 0; k < EB; ++k) {
+      RsOps o;
+      rs_load(a, mb + tid / (COLS / 8) + (kb + k) * (NT / (COLS / 8)), c, o);
+      p.x[k] = o.xr;
+      p.y[k] = o.s0;
+      p.z[k] = o.rr;
+    }
+    return;
+  }
+  if (big_pairs(a)) return;
+  const bool want1 = (a.epi == EPI_PLAIN && a.accum) || a.epi == EPI_ADDSCALE ||
+                     a.epi == EPI_RELU_MASK || a.epi == EPI_GATE_BWD;
+  const bool want2 = (a.epi == EPI_RELU_MASK && a.accum) || a.epi == EPI_GATE_BWD;
+  const bool wr = a.ybf && a.ybf_radd && (a.epi == EPI_PLAIN || a.epi == EPI_ADDSCALE);
+  const int col = n0 + (tid % (COLS / 4)) * 4;
+  if (!(want1 || want2 || wr) || a.N - col < 4) return;
+#pragma unroll
+  for (int k = 0; k < EB; ++k) {
+    const int m = mb + tid / (COLS / 4) + (kb + k) * (NT / (COLS / 4));
+    if (want1 || want2) gen_load(a, m, col, want2, p.x[k], p.y[k]);
+    if (wr && m < a.M) p.z[k] = ld4(a.ybf_radd + (long long)(m / a.Tout) * a.ybf_radd_ld + col);
+  }
+}
+
+// One staged tile (or chunk of one): rows [0, ROWS) of T (row stride LDT) are output rows
+// mb.., columns [0, COLS) are n0.., NT threads.
+// BIAS_IN_T: T already holds acc + bias.  pre holds this chunk's first batch of operands on
+// entry; the last batch loads the next chunk's first batch (unless `last`) before its stores.
+template <int ROWS, int COLS, int NT, int LDT, bool BIAS_IN_T, int EB = EBB>
+__device__ __forceinline__ void epilogue_tile(const GemmArgs& a, const float* T, int mb, int n0,
+                                              int tid, bool last, EpiPreT<EB>& pre) {
   const int M = a.M;
-  constexpr int EB = 2;  // rows whose operands are in flight together (register budget)
   if (a.epi == EPI_NONE) {
     if (T[tid] == 12345.678f && mb < 0) a.Y[0] = T[tid + 1];
     return;
   }
-  // as gemm_epilogue_lds: a fixed column group per thread, bias read once, every global
-  // operand load of the thread's rows issued before its first store
+  const bool hb = !BIAS_IN_T && a.bias;
   if (a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS)) {
-    gate_tile8<NTHRB, CHR, BNB / 16>(a, T, EPB, mb, n0, tid);  // 128 channels: 16 threads
+    gate_tile8<NT, ROWS, COLS / 16, BIAS_IN_T>(a, T, LDT, mb, n0, tid);
     return;
   }
-  if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
-    // BNB / 2 output channels per row: gate/filter interleaved by 16 in the packed columns
-    constexpr int NI = CHR * (BNB / 8) / NTHRB;
-    const int q4 = tid % (BNB / 8), q = q4 >> 2, j = (q4 & 3) * 4;
+  if (big_pairs(a)) {
+    // COLS / 2 output channels per row: gate/filter interleaved by 16 in the packed columns
+    constexpr int NI = ROWS * (COLS / 8) / NT;
+    const int q4 = tid % (COLS / 8), q = q4 >> 2, j = (q4 & 3) * 4;
     const int c = n0 / 2 + q * 16 + j;
     const int gc = q * 32 + j;
     if (c >= a.C) return;
     f32x4 bg = {0.f, 0.f, 0.f, 0.f}, bfl = {0.f, 0.f, 0.f, 0.f};
-    if (a.bias) {
+    if (hb) {
       bg = ld4(a.bias + n0 + gc);
       bfl = ld4(a.bias + n0 + gc + 16);
     }
 #pragma unroll 1
     for (int kb = 0; kb < NI; kb += EB) {
-    f32x4 xr[EB], s0[EB];
+    EpiPreT<EB> cur = pre;
     if (a.epi == EPI_RESSKIP) {
-#pragma unroll
-      for (int k = 0; k < EB; ++k) {
-        const int m = mb + tid / (BNB / 8) + (kb + k) * (NTHRB / (BNB / 8));
-        if (m >= M) continue;
-        xr[k] = ld4(a.aux1 + (long long)m * a.ld1 + c);
-        if (a.accum) s0[k] = ld4(a.aux0 + (long long)m * a.ld0 + c);
-      }
+      if (kb + EB < NI) epi_pre<COLS, NT, EB>(a, mb, n0, tid, kb + EB, pre);
+      else if (!last) epi_pre<COLS, NT, EB>(a, mb + ROWS, n0, tid, 0, pre);
     }
 #pragma unroll
     for (int k = 0; k < EB; ++k) {
-      const int row = tid / (BNB / 8) + (kb + k) * (NTHRB / (BNB / 8));
+      const int row = tid / (COLS / 8) + (kb + k) * (NT / (COLS / 8));
       const int m = mb + row;
       if (m >= M) continue;
-      f32x4 g = ld4(T + row * EPB + gc), f = ld4(T + row * EPB + gc + 16);
-      if (a.bias) {
+      f32x4 g = ld4(T + row * LDT + gc), f = ld4(T + row * LDT + gc + 16);
+      if (hb) {
         g += bg;
         f += bfl;
       }
-      if (a.epi == EPI_GATE) {
+      if (a.epi == EPI_RESSKIP) {
+        rs_store(a, m, c, g, f, RsOps{cur.x[k], cur.y[k], cur.z[k]});
+      } else if (a.epi == EPI_GATE) {
         st4_aux0(a, (long long)m * a.ld0 + c, g);
         st4_aux0(a, (long long)m * a.ld0 + a.C + c, f);
         f32x4 z;
@@ -1270,101 +1373,70 @@ __device__ __forceinline__ void epilogue_chunk_big(const GemmArgs& a, const floa
         for (int e = 0; e < 4; ++e) z[e] = fsigmoid_(g[e]) * ftanh_(f[e]);
         if (a.Y) st4(a.Y + (long long)m * a.ldy + c, z);
         shadow4(a, m, c, z);
-      } else if (a.epi == EPI_GATE_TS) {
+      } else {
         f32x4 z;
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = ftanh_(g[e]) * fsigmoid_(f[e]);
         st4(a.Y + (long long)m * a.ldy + c, z);
-      } else {
-        f32x4 y, sk;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (xr[k][e] + g[e]) * 0.70710678118654752f;
-        st4(a.Y + (long long)m * a.ldy + c, y);
-        shadow4(a, m, c, y);
-        if (a.accum) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) sk[e] = fmaf(a.alpha, f[e], s0[k][e]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) sk[e] = a.alpha * f[e];
-        }
-        st4(a.aux0 + (long long)m * a.ld0 + c, sk);
       }
     }
     }
     return;
   }
-  constexpr int NI = CHR * (BNB / 4) / NTHRB;
-  const int cq = tid % (BNB / 4), col = n0 + cq * 4;
+  constexpr int NI = ROWS * (COLS / 4) / NT;
+  const int cq = tid % (COLS / 4), col = n0 + cq * 4;
   const int ne = min(4, a.N - col);
   if (ne <= 0) return;
   f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-  if (a.bias) {
+  if (hb) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (e < ne) bv[e] = a.bias[col + e];
   }
-  const bool want1 = (a.epi == EPI_PLAIN && a.accum) || a.epi == EPI_ADDSCALE ||
-                     a.epi == EPI_RELU_MASK || a.epi == EPI_GATE_BWD;
-  const bool want2 = (a.epi == EPI_RELU_MASK && a.accum) || a.epi == EPI_GATE_BWD;
   static_assert(NI % EB == 0, "rows per thread in batches of EB");
 #pragma unroll 1
   for (int kb = 0; kb < NI; kb += EB) {
-  f32x4 p1[EB], p2[EB];
-  if (ne == 4 && (want1 || want2)) {
-#pragma unroll
-    for (int k = 0; k < EB; ++k) {
-      const int m = mb + tid / (BNB / 4) + (kb + k) * (NTHRB / (BNB / 4));
-      if (m >= M) continue;
-      const float* y = a.Y + (long long)m * a.ldy + col;
-      if (a.epi == EPI_PLAIN) {
-        p1[k] = ld4(y);
-      } else if (a.epi == EPI_GATE_BWD) {
-        p1[k] = ld4_aux1(a, (long long)m * a.ld1 + col);
-        p2[k] = ld4_aux1(a, (long long)m * a.ld1 + a.C + col);
-      } else {
-        p1[k] = ld4(a.aux1 + (long long)m * a.ld1 + col);
-        if (want2) p2[k] = ld4(y);
-      }
-    }
-  }
+  EpiPreT<EB> cur = pre;
+  if (kb + EB < NI) epi_pre<COLS, NT, EB>(a, mb, n0, tid, kb + EB, pre);
+  else if (!last) epi_pre<COLS, NT, EB>(a, mb + ROWS, n0, tid, 0, pre);
 #pragma unroll
   for (int k = 0; k < EB; ++k) {
-    const int row = tid / (BNB / 4) + (kb + k) * (NTHRB / (BNB / 4));
+    const int row = tid / (COLS / 4) + (kb + k) * (NT / (COLS / 4));
     const int m = mb + row;
     if (m >= M) continue;
-    f32x4 v = ld4(T + row * EPB + cq * 4);
-    if (a.bias) v += bv;
+    f32x4 v = ld4(T + row * LDT + cq * 4);
+    if (hb) v += bv;
+    const f32x4 p1 = cur.x[k], p2 = cur.y[k];
     float* y = a.Y + (long long)m * a.ldy + col;
     if (ne == 4) {
       if (a.epi == EPI_PLAIN) {
-        if (a.accum) v += p1[k];
+        if (a.accum) v += p1;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           if (a.relu == 1) v[e] = fmaxf(v[e], 0.f);
           else if (a.relu == 2) v[e] = sigmoidf_(v[e]);
         }
         st4(y, v);
-        shadow4(a, m, col, v);
+        shadow4r(a, m, col, v, cur.z[k]);
       } else if (a.epi == EPI_ADDSCALE) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = __builtin_fmaf(a.alpha, p1[k][e], v[e]);
+          v[e] = __builtin_fmaf(a.alpha, p1[e], v[e]);
           v[e] = a.relu == 1 ? fmaxf(v[e], 0.f) : v[e];
         }
         st4(y, v);
-        shadow4(a, m, col, v);
+        shadow4r(a, m, col, v, cur.z[k]);
       } else if (a.epi == EPI_RELU_MASK) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = p1[k][e] > 0.f ? v[e] : 0.f;
-        if (a.accum) v += p2[k];
+        for (int e = 0; e < 4; ++e) v[e] = p1[e] > 0.f ? v[e] : 0.f;
+        if (a.accum) v += p2;
         st4(y, v);
       } else if (a.epi == EPI_GATE_BWD) {
         f32x4 dg, df;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float t0, t1;
-          gate_bwd_(v[e], p1[k][e], p2[k][e], t0, t1);
+          gate_bwd_(v[e], p1[e], p2[e], t0, t1);
           dg[e] = t0;
           df[e] = t1;
         }
@@ -1401,6 +1473,18 @@ __device__ __forceinline__ void epilogue_chunk_big(const GemmArgs& a, const floa
   }
 }
 
+// per-lane bias of the wave's accumulator columns (nt = 0..3), added while staging
+__device__ __forceinline__ void big_bias(const GemmArgs& a, int n0, int wc, int lane, float (&bs)[4]) {
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int n = n0 + wc * 64 + nt * 16 + (lane & 15);
+    bs[nt] = a.bias && n < a.N ? a.bias[n] : 0.f;
+  }
+}
+
+// GATE8: the launch runs the 16-B gate epilogue (the DiffNet gate GEMM), compiled without
+// the other epilogues' operand registers
+template <bool GATE8>
 __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_big_kernel(const GemmArgs a) {
   constexpr int TILE_A = BMB * BK2 * 2;  // 32 KB
   constexpr int STAGE = TILE_A + BNB * BK2 * 2;
@@ -1497,7 +1581,13 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_big_kernel(const GemmArgs
   }
 #undef ISSUE_BIG
 #undef TAP_PTRS
-  // epilogue: four 64-row chunks staged through LDS (row stride EPB floats)
+  // epilogue: four 64-row chunks staged through LDS (row stride EPB floats) with the bias
+  // added while staging; the first chunk's epilogue operands are loaded before any store
+  float bs[4];
+  const bool bias_st = a.bias != nullptr;
+  if (bias_st) big_bias(a, n0, wc, lane, bs);
+  EpiPre pre;
+  if (!GATE8) epi_pre<BNB, NTHRB>(a, m0, n0, tid, 0, pre);
   float* T = (float*)smem;
   __syncthreads();
   // (the chunk loop is not unrolled -- its body is large -- so the accumulator half is
@@ -1507,7 +1597,7 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_big_kernel(const GemmArgs
   _Pragma("unroll") for (int nt = 0; nt < 4; ++nt)                                        \
   _Pragma("unroll") for (int r = 0; r < 4; ++r)                                           \
       T[(mt2 * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] =        \
-          acc[(H) * 4 + mt2][nt][r]
+          bias_st ? acc[(H) * 4 + mt2][nt][r] + bs[nt] : acc[(H) * 4 + mt2][nt][r]
 #pragma unroll 1
   for (int c = 0; c < BMB / CHR; ++c) {
     if (wr == (c >> 1)) {
@@ -1518,7 +1608,8 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_big_kernel(const GemmArgs
       }
     }
     __syncthreads();
-    epilogue_chunk_big(a, T, m0 + c * CHR, n0, tid);
+    if (GATE8) gate_tile8<NTHRB, CHR, BNB / 16, true>(a, T, EPB, m0 + c * CHR, n0, tid);
+    else epilogue_tile<CHR, BNB, NTHRB, EPB, true>(a, T, m0 + c * CHR, n0, tid, c == BMB / CHR - 1, pre);
     __syncthreads();
   }
 #undef STAGE_HALF
@@ -1542,8 +1633,10 @@ __global__ __launch_bounds__(NTHRB) void splitk_epilogue_kernel(const GemmArgs a
     }
     *(f32x4*)(T + row * EPB + c4 * 4) = v;
   }
+  EpiPre pre;
+  epi_pre<BNB, NTHRB>(a, mb, n0, tid, 0, pre);
   __syncthreads();
-  epilogue_chunk_big(a, T, mb, n0, tid);
+  epilogue_tile<CHR, BNB, NTHRB, EPB, false>(a, T, mb, n0, tid, true, pre);
 }
 
 // ---------------------------------------- 256 x 256, 32-deep K steps, S-stage ring
@@ -1694,6 +1787,8 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_ring_kernel(const GemmArg
   }
 #undef ISSUE_RING
 #undef TAP_PTRS2
+  EpiPre pre;
+  epi_pre<BNB, NTHRB>(a, m0, n0, tid, 0, pre);
   float* T = (float*)smem;
   __syncthreads();
 #define STAGE_HALF(H)                                                                     \
@@ -1712,10 +1807,196 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_ring_kernel(const GemmArg
       }
     }
     __syncthreads();
-    epilogue_chunk_big(a, T, m0 + cch * CHR, n0, tid);
+    epilogue_tile<CHR, BNB, NTHRB, EPB, false>(a, T, m0 + cch * CHR, n0, tid, cch == BMB / CHR - 1, pre);
     __syncthreads();
   }
 #undef STAGE_HALF
+}
+
+// ------------------------------------------------- 64 x 64 bf16-operand GEMM (small M)
+// The reverse diffusion's DiffNet GEMMs have M = 2 000 frame rows: 16 x 4 tiles of 128 x 128
+// keep 64 CUs busy, each walking a 16-step K loop at one L2 round trip per step.  64 x 64
+// tiles give 32 x 8 = 256 workgroups (the whole chip) whose operands sit in the XCD's L2
+// (activations 1-2 MB bf16, weights 1 MB); each workgroup keeps SMS - 1 K-steps of both
+// images in flight (an L2-resident LDS-DMA stream runs at ~70 GB/s per CU with 64-72 KiB in
+// flight, MI355X_MICROARCH.md "Indexed rows"), so a 1 024-deep tile streams its 256 KB in
+// ~4 us.  4 waves in 2 x 2, each a 32 x 32 sub-tile (2 x 2 v_mfma_f32_16x16x32_bf16) over the
+// full K loop: every output element accumulates its K-steps in the same order as the 128 x
+// 128 kernels, so the results are bit-identical to them.  Same LDS image / swizzle / staging
+// pointers; the epilogue stages the fp32 tile through LDS (epilogue_tile).
+constexpr int BMS = 64, BNS = 64, EPS = BNS + 4;
+
+__device__ __forceinline__ void xcd_tile_small(int& m0, int& n0) {
+  const int nM = gridDim.x, nN = gridDim.y, total = nM * nN;
+  const int orig = blockIdx.x + blockIdx.y * nM;
+  const int xcd = orig & 7, q = total >> 3, r = total & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  m0 = (wg / nN) * BMS;
+  n0 = (wg % nN) * BNS;
+}
+
+// staging pointers of this lane's 2 A rows (rl, rl + 8) and 2 B rows of one (segment, tap)
+struct TapPtrsS {
+  const char* pa[2];
+  const char* pb[2];
+  unsigned va;
+  int K, Kp;
+};
+
+__device__ __forceinline__ TapPtrsS tap_ptrs_s(const SegU S, int j, int Npad, int n0, int rl,
+                                               int cq8a, int cq8b, const int b0, const int b1,
+                                               const int t0, const int t1, unsigned okm) {
+  TapPtrsS P;
+  const int bt[2] = {b0, b1}, tt[2] = {t0, t1};
+  const int shj = S.shift0 + j * S.dil;
+  P.va = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c8 = i ? cq8b : cq8a;
+    const int ts = tt[i] + shj;
+    const int src = S.pad == PAD_ZERO ? ((unsigned)ts < (unsigned)S.Tin ? ts : -1)
+                                      : pad_src(ts, S.Tin, S.pad);
+    const bool ok = ((okm >> i) & 1) && src >= 0;
+    P.va |= ok ? (1u << i) : 0u;
+    P.pa[i] = (const char*)(S.x + (unsigned)((bt[i] * S.Tin + (ok ? src : 0)) * S.ld + c8));
+    P.pb[i] = S.w + ((unsigned)((j * Npad + n0 + rl + 8 * i) * S.Kp + c8)) * 2;
+  }
+  P.K = S.K;
+  P.Kp = S.Kp;
+  return P;
+}
+
+template <int SMS>
+__global__ __launch_bounds__(NTHR) void conv_gemm_b16_small_kernel(const GemmArgs a) {
+  static_assert(SMS >= 2 && SMS <= 5, "stages (waits are counted up to 3 stages ahead)");
+  constexpr int IMG = BMS * BK2 * 2;  // 8 KB: one operand image of one stage
+  constexpr int STAGE = 2 * IMG;
+  constexpr int GL = 4;               // glds per thread per stage (2 A rows + 2 B rows)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  int m0, n0;
+  xcd_tile_small(m0, n0);
+  const int M = a.M, Tout = a.Tout, Npad = a.Npad;
+  const int nseg = a.nseg;
+  const SegU S0 = seg_u(a.seg[0], a.W);
+  const SegU S1 = nseg > 1 ? seg_u(a.seg[1], a.W) : S0;
+  const SegU S2 = nseg > 2 ? seg_u(a.seg[2], a.W) : S0;
+  const int nit = S0.nk * S0.taps + (nseg > 1 ? S1.nk * S1.taps : 0) +
+                  (nseg > 2 ? S2.nk * S2.taps : 0);
+  // wave wid fills rows wid*16 + lane/8 + 8i (i = 0, 1) of both images
+  const int rl = wid * 16 + (lane >> 3), slot = lane & 7;
+  const int cq = swz(rl, slot), cq8a = cq * 8, cq8b = (cq ^ 4) * 8;
+  int bt[2], tt[2];
+  unsigned okm = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + rl + 8 * i;
+    const bool ok = m < M;
+    bt[i] = ok ? m / Tout : 0;
+    tt[i] = ok ? m - bt[i] * Tout : 0;
+    okm |= ok ? (1u << i) : 0u;
+  }
+  unsigned long long zpu = (unsigned long long)(const void*)g_zero;
+  asm volatile("" : "+s"(zpu));
+  const char* zp = (const char*)zpu;
+  int qs = 0, qj = 0, qkc = 0;
+#define TAP_PTRS_S(S) tap_ptrs_s(S, qj, Npad, n0, rl, cq8a, cq8b, bt[0], bt[1], tt[0], tt[1], okm)
+  TapPtrsS P = TAP_PTRS_S(S0);
+#define ISSUE_S(it)                                                                      \
+  do {                                                                                   \
+    char* As_ = smem + ((it) % SMS) * STAGE + wid * 16 * 128;                            \
+    const int kb_ = qkc * BK2;                                                           \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                      \
+      const bool oa = ((P.va >> i) & 1) && kb_ + (i ? cq8b : cq8a) < P.K;                \
+      glds16(oa ? (const void*)(P.pa[i] + kb_ * 2) : (const void*)zp, As_ + i * 1024);   \
+    }                                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                      \
+      const bool ob = kb_ + (i ? cq8b : cq8a) < P.Kp;                                    \
+      glds16(ob ? (const void*)(P.pb[i] + kb_ * 2) : (const void*)zp,                    \
+             As_ + IMG + i * 1024);                                                      \
+    }                                                                                    \
+    const int nks_ = qs == 0 ? S0.nk : (qs == 1 ? S1.nk : S2.nk);                        \
+    const int taps_ = qs == 0 ? S0.taps : (qs == 1 ? S1.taps : S2.taps);                 \
+    if (++qkc == nks_) {                                                                 \
+      qkc = 0;                                                                           \
+      if (++qj == taps_) {                                                               \
+        qj = 0;                                                                          \
+        ++qs;                                                                            \
+      }                                                                                  \
+      if (qs < nseg) P = qs == 0 ? TAP_PTRS_S(S0) : (qs == 1 ? TAP_PTRS_S(S1) : TAP_PTRS_S(S2)); \
+    }                                                                                    \
+  } while (0)
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < SMS - 1; ++p)
+    if (p < nit) ISSUE_S(p);
+  // the epilogue's global operands (bias, residual / skip rows, per-sequence adds) are
+  // loaded now, behind the K loop, instead of as a dependent round trip after it: at
+  // M = 2 000 a launch is a few K-steps long and such round trips set its duration
+  float bs[2] = {0.f, 0.f};
+  const bool bias_st = a.bias != nullptr;
+  if (bias_st) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wc * 32 + j * 16 + (lane & 15);
+      bs[j] = n < a.N ? a.bias[n] : 0.f;
+    }
+  }
+  EpiPreT<2> pre;
+  epi_pre<BNS, NTHR, 2>(a, m0, n0, tid, 0, pre);
+  const int arow = lane & 15, kq = lane >> 4;
+  const int ra = wr * 32 + arow, rbr = wc * 32 + arow;
+  const int oa0 = ra * 128 + swz(ra, kq) * 16, oa1 = ra * 128 + swz(ra, kq + 4) * 16;
+  const int ob0 = IMG + rbr * 128 + swz(rbr, kq) * 16;
+  const int ob1 = IMG + rbr * 128 + swz(rbr, kq + 4) * 16;
+  for (int it = 0; it < nit; ++it) {
+    const int ahead = min(SMS - 2, nit - 1 - it);  // stages issued after tile `it`
+    if (ahead >= 3) wait_vm_n<3 * GL>();
+    else if (ahead == 2) wait_vm_n<2 * GL>();
+    else if (ahead == 1) wait_vm_n<GL>();
+    else wait_vm_n<0>();
+    __builtin_amdgcn_s_barrier();  // tile `it` visible; every wave is done with tile it-1
+    if (it + SMS - 1 < nit) ISSUE_S(it + SMS - 1);
+    const char* St = smem + (it % SMS) * STAGE;
+    bf16x8 fa[2][2], fb[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        fa[h][i] = *(const bf16x8*)(St + (h ? oa1 : oa0) + i * 2048);
+        fb[h][i] = *(const bf16x8*)(St + (h ? ob1 : ob0) + i * 2048);
+      }
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // DS reads
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);  // MFMAs
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[h][i], fb[h][j], acc[i][j], 0, 0, 0);
+  }
+#undef ISSUE_S
+#undef TAP_PTRS_S
+  // epilogue: acc + bias staged through LDS as an fp32 tile
+  float* T = (float*)smem;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        T[(wr * 32 + i * 16 + (lane >> 4) * 4 + r) * EPS + wc * 32 + j * 16 + (lane & 15)] =
+            bias_st ? acc[i][j][r] + bs[j] : acc[i][j][r];
+  __syncthreads();
+  epilogue_tile<BMS, BNS, NTHR, EPS, true, 2>(a, T, m0, n0, tid, true, pre);
 }
 
 // y[m][k] = bf16(x[m][k] + radd[m / T][k]) for the bf16-activation GEMM (8 elements per thread).
@@ -2405,6 +2686,9 @@ static const int SPLITK_TARGET = 256;
 // launches of fewer than 128 tiles of 128 x 128 run the two-K-group kernel (-1: not read
 // yet; ENSVS_DUAL_SMALL, default 1; ensvs_set_dual_small)
 static int g_dual_small = -1;
+// launches of fewer than 128 tiles of 128 x 128 run the 64 x 64-tile kernel (-1: not read yet;
+// ENSVS_SMALL, default 1; ensvs_set_small); it takes precedence over split-K and dual
+static int g_small = -1;
 
 static bool use_big_tile(const GemmArgs& a) {
   if (g_big_tile < 0) {
@@ -2421,7 +2705,10 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
                       const void* W, int stages, hipStream_t st) {
   for (int s = 0; s < nseg; ++s) {
     const ensvs_conv_seg& g = segs[s];
-    if (g.radd || g.pd || g.K % 8 || g.ld % 8 || ((uintptr_t)g.x & 15)) return ENSVS_E_ARG;
+    // K % 8 != 0: the caller zero-pads the operand rows to a multiple of 8 within ld (the
+    // last 16-B chunk reads the padding; the packed weights are zero there anyway)
+    if (g.radd || g.pd || g.ld % 8 || g.ld < ((g.K + 7) & ~7) || ((uintptr_t)g.x & 15))
+      return ENSVS_E_ARG;
   }
   if (((uintptr_t)W & 15)) return ENSVS_E_ARG;
   dim3 grid(cdiv(a.M, BM), Npad / BN);
@@ -2436,10 +2723,16 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     if (g_big_tile == 2) {
       const size_t lb = (size_t)2 * (BMB + BNB) * BK2 * 2;  // two stages of both images
       static const hipError_t eb = hipFuncSetAttribute(
-          (const void*)conv_gemm_b16_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-          (int)lb);
-      if (eb != hipSuccess) return ENSVS_E_HIP;
-      hipLaunchKernelGGL(conv_gemm_b16_big_kernel, grid_b, dim3(NTHRB), lb, st, a);
+          (const void*)conv_gemm_b16_big_kernel<false>,
+          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+      static const hipError_t eg = hipFuncSetAttribute(
+          (const void*)conv_gemm_b16_big_kernel<true>,
+          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+      if (eb != hipSuccess || eg != hipSuccess) return ENSVS_E_HIP;
+      if (a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS))
+        hipLaunchKernelGGL(conv_gemm_b16_big_kernel<true>, grid_b, dim3(NTHRB), lb, st, a);
+      else
+        hipLaunchKernelGGL(conv_gemm_b16_big_kernel<false>, grid_b, dim3(NTHRB), lb, st, a);
     } else {
 #define RING(S)                                                                           \
   do {                                                                                    \
@@ -2456,6 +2749,35 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
       else RING(5);
 #undef RING
     }
+    ENSVS_CHECK_LAUNCH();
+    return ENSVS_OK;
+  }
+  // small M (fewer than 128 tiles of 128 x 128): the 64 x 64-tile kernel fills the chip
+  if (g_small < 0) {
+    const char* e = getenv("ENSVS_SMALL");
+    g_small = e ? atoi(e) : 1;
+  }
+  if (g_small && !a.csum && a.vec_out && Npad % BNS == 0 &&
+      (long long)grid.x * grid.y < 128) {
+    static const int sms = [] {
+      const char* e = getenv("ENSVS_SMALL_STAGES");
+      const int v = e ? atoi(e) : 5;
+      return v < 3 ? 3 : (v > 5 ? 5 : v);
+    }();
+    const dim3 gs(cdiv(a.M, BMS), Npad / BNS);
+#define SMALL(S)                                                                          \
+  do {                                                                                    \
+    const size_t ls = std::max<size_t>((size_t)(S) * 2 * BMS * BK2 * 2, (size_t)BMS * EPS * 4); \
+    static const hipError_t es = hipFuncSetAttribute(                                     \
+        (const void*)conv_gemm_b16_small_kernel<S>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+        (int)ls);                                                                         \
+    if (es != hipSuccess) return ENSVS_E_HIP;                                             \
+    hipLaunchKernelGGL(conv_gemm_b16_small_kernel<S>, gs, dim3(NTHR), ls, st, a);         \
+  } while (0)
+    if (sms == 3) SMALL(3);
+    else if (sms == 4) SMALL(4);
+    else SMALL(5);
+#undef SMALL
     ENSVS_CHECK_LAUNCH();
     return ENSVS_OK;
   }
@@ -2518,6 +2840,11 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
                        dim3(NTHRB), le, st, a);
     ENSVS_CHECK_LAUNCH();
   }
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_set_small(int on) {
+  g_small = on ? 1 : 0;
   return ENSVS_OK;
 }
 

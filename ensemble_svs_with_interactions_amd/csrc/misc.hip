@@ -322,6 +322,31 @@ __global__ void p_sample_kernel(float* __restrict__ x, const float* __restrict__
   }
 }
 
+// p_sample over M rows of Mc channels that also writes the next DiffNet input projection's
+// bf16 operand: xb[m][k] = bf16(x[m][k]) for k < Mc, 0 for Mc <= k < ldb (the K padding the
+// 16-B operand chunks read).  eps == nullptr: no update, only the copy (the first step's x).
+__global__ void p_sample_bf16_kernel(float* __restrict__ x, const float* __restrict__ eps,
+                                     const float* __restrict__ noise, long long M, int Mc,
+                                     float sra, float srm1, float c1, float c2, float sigma,
+                                     __bf16* __restrict__ xb, int ldb) {
+  GRID_LOOP(i, M * ldb) {
+    const long long m = i / ldb;
+    const int k = (int)(i - m * ldb);
+    float v = 0.f;
+    if (k < Mc) {
+      const long long j = m * Mc + k;
+      v = x[j];
+      if (eps) {
+        float xr = sra * v - srm1 * eps[j];
+        xr = fminf(fmaxf(xr, -1.f), 1.f);
+        v = (c1 * xr + c2 * v) + sigma * noise[j];
+        x[j] = v;
+      }
+    }
+    xb[i] = (__bf16)v;
+  }
+}
+
 // ------------------------------------------------------------- loss
 struct LossStream {
   const float* a;  // prediction (or x_recon)
@@ -711,6 +736,15 @@ ENSVS_API int ensvs_q_sample(const float* y, int ldy, const float* noise, int ld
 ENSVS_API int ensvs_p_sample(float* x, const float* eps, const float* noise, long long n, float sra,
                              float srm1, float c1, float c2, float sigma, void* stream) {
   LAUNCH(p_sample_kernel, n, x, eps, noise, n, sra, srm1, c1, c2, sigma);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_p_sample_bf16(float* x, const float* eps, const float* noise, long long M,
+                                  int Mc, float sra, float srm1, float c1, float c2, float sigma,
+                                  void* xb, int ldb, void* stream) {
+  if (ldb < Mc || ldb % 8 || ((uintptr_t)xb & 15)) return ENSVS_E_ARG;
+  LAUNCH(p_sample_bf16_kernel, M * ldb, x, eps, noise, M, Mc, sra, srm1, c1, c2, sigma,
+         (__bf16*)xb, ldb);
   return ENSVS_OK;
 }
 

@@ -154,10 +154,12 @@ class DiffNet(nn.Module):
                **pk.bias_ptr_args("dp.b"))
         return demb, m1, mi, d, ds
 
-    def _fwd(self, xin, ldx, t, cond, ldc, B, T, save=True, ds=None):
+    def _fwd(self, xin, ldx, t, cond, ldc, B, T, save=True, ds=None, xinb=None, condb=None):
         """xin (B*T, in_dim) noisy spec, t (B,) int64 (device), cond (B*T, E).  ds: the
         step embedding's block projections (B, L*C) when precomputed (the reverse process
-        embeds all K steps at once; inference only).
+        embeds all K steps at once; inference only).  bf16 operands only (inference): xinb
+        the bf16 copy of xin (row stride a multiple of 8, zero K padding: p_sample_bf16),
+        condb the bf16 copy of cond (the reverse process rounds it once, not per step).
         Returns (out (B*T, in_dim), saved state)."""
         pk = self._packs.ensure(self, self._register)
         dev = xin.device
@@ -172,11 +174,15 @@ class DiffNet(nn.Module):
         # per-block x + d_l and z are rounded by an explicit cast and, when training, kept
         # for the bf16 weight-gradient kernels of the backward pass
         b16 = K.bf16_operands(pk.fwd, M)
-        condb = K.cast_bf16(cond, ldc, E, M) if b16 else None
+        if b16 and condb is None:
+            condb = K.cast_bf16(cond, ldc, E, M)
         XB, ZB = [], []
-        xb = None
         x = empty(M, C, device=dev)
-        K.gemm([K.Seg(xin, ldx, Mc, pk["in"], T)], B, T, C, pk.fwd, x, C, relu=True,
+        # block 0's bf16 operand x + d_0 comes from the input projection's epilogue
+        xb = empty(M, C, device=dev, dtype=torch.bfloat16) if b16 else None
+        K.gemm([K.Seg(xin, ldx, Mc, pk["in"], T) if xinb is None else
+                K.Seg(xinb, xinb.shape[1], Mc, pk["in"], T)], B, T, C, pk.fwd, x, C,
+               relu=True, ybf=xb, ybf_ld=C, ybf_radd=ds if b16 else None, ybf_radd_ld=L * C,
                **pk.bias_ptr_args("in.b"))
         S = empty(M, C, device=dev)
         X, Z, GF = [x], [], []
@@ -197,9 +203,7 @@ class DiffNet(nn.Module):
             elif z is None:
                 z = empty(M, C, device=dev)
                 gf = empty(M, 2 * C, device=dev, dtype=gdt)
-            if b16 and l == 0:  # later blocks get x + d_l from the previous epilogue
-                xb = K.cast_bf16(x, C, C, M, radd=ds, radd_ld=L * C, T=T)
-            zb = None
+            zb = None  # (xb: x + d_l from the previous epilogue)
             if b16:
                 zb = ZBall[:, l * C:] if save else empty(M, C, device=dev, dtype=torch.bfloat16)
             self._gate_gemm(l, x, cond, ldc, ds, B, T, z, gf, condb=condb,
@@ -224,10 +228,12 @@ class DiffNet(nn.Module):
                     X.append(xn)
             x = xn
         p1 = empty(M, C, device=dev)
+        p1b = empty(M, C, device=dev, dtype=torch.bfloat16) if b16 else None
         K.gemm([K.Seg(S, C, C, pk["skip"], T)], B, T, C, pk.fwd, p1, C, relu=True,
-               **pk.bias_ptr_args("skip.b"))
+               ybf=p1b, ybf_ld=C, **pk.bias_ptr_args("skip.b"))
         out = empty(M, Mc, device=dev)
-        K.gemm([K.Seg(p1, C, C, pk["outp"], T)], B, T, Mc, pk.fwd, out, Mc,
+        K.gemm([K.Seg(p1, C, C, pk["outp"], T) if p1b is None else
+                K.Seg(p1b, C, C, pk["outp"], T)], B, T, Mc, pk.fwd, out, Mc,
                **pk.bias_ptr_args("outp.b"))
         st = None
         if save:
@@ -647,13 +653,27 @@ class GaussianDiffusion(BaseModel):
         # the step embedding depends on t only: all K steps in one pass (5 launches instead
         # of 5 per step)
         dn = self.denoise_fn
-        dn._packs.ensure(dn, dn._register)
+        pk = dn._packs.ensure(dn, dn._register)
         ds_all = dn._step_embed(steps.reshape(-1), K_ * B)[4]
         LC = ds_all.shape[1]
+        # bf16 operands: cond rounded once for all K steps; x_t's bf16 copy (K padded to a
+        # multiple of 8 with zeros) written by each p_sample for the next step's input GEMM
+        b16 = K.bf16_operands(pk.fwd, M)
+        condb = xb = None
+        if b16:
+            condb = K.cast_bf16(cond, E, E, M)
+            xb = empty(M, -(-Mc // 8) * 8, device=dev, dtype=torch.bfloat16)
+            call("ensvs_p_sample_bf16", x.data_ptr(), None, None, M, Mc, 0.0, 0.0, 0.0, 0.0,
+                 0.0, xb.data_ptr(), xb.shape[1], Ly.stream())
         for k, i in enumerate(reversed(range(K_))):
             eps, _ = dn._fwd(x, Mc, steps[k], cond, E, B, T, save=False,
-                             ds=ds_all[k * B:(k + 1) * B].view(B, LC))
+                             ds=ds_all[k * B:(k + 1) * B].view(B, LC), xinb=xb, condb=condb)
             sigma = 0.0 if i == 0 else math.exp(0.5 * lv[i])
+            if b16:
+                call("ensvs_p_sample_bf16", x.data_ptr(), eps.data_ptr(), noise_at(k).data_ptr(),
+                     M, Mc, sra[i], srm1[i], c1[i], c2[i], sigma, xb.data_ptr(), xb.shape[1],
+                     Ly.stream())
+                continue
             call("ensvs_p_sample", x.data_ptr(), eps.data_ptr(), noise_at(k).data_ptr(), M * Mc,
                  sra[i], srm1[i], c1[i], c2[i], sigma, Ly.stream())
         call("ensvs_axpby", x.data_ptr(), float(self.norm_scale), x.data_ptr(), 0.0, M * Mc,

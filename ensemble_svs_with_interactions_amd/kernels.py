@@ -171,11 +171,13 @@ def _castable(s):
 
 def _bf16_act_ok(segs, W, Npad, M):
     if any(s.x.dtype == torch.bfloat16 for s in segs):  # operands already rounded
-        assert W.dtype == _lib.DT_BF16 and all(s.pd is None and s.K % 8 == 0 for s in segs)
+        assert W.dtype == _lib.DT_BF16 and all(s.pd is None for s in segs)
         assert all(s.radd is None for s in segs if s.x.dtype == torch.bfloat16)
         for s in segs:  # ensvs_conv_gemm_bf16a's contract: a caller-side layout error
-            if s.x.dtype == torch.bfloat16 and (s.ld % 8 or (s.x.data_ptr() + 2 * s.xoff) % 16):
-                raise ValueError("bf16 GEMM operand needs ld % 8 == 0 and 16-B aligned rows")
+            if s.x.dtype == torch.bfloat16 and (s.ld % 8 or (s.x.data_ptr() + 2 * s.xoff) % 16
+                                                or s.ld < -(-s.K // 8) * 8):
+                raise ValueError("bf16 GEMM operand needs ld % 8 == 0 and 16-B aligned rows "
+                                 "(K % 8 != 0: zero-padded to a multiple of 8 within ld)")
             if s.x.dtype != torch.bfloat16 and not _castable(s):
                 raise ValueError("fp32 segment beside bf16 operands is not castable")
         return True
@@ -191,6 +193,12 @@ def set_big_tile(mode, stages=0):
     two-stage, the default; 1: 32-deep LDS ring of `stages` stages) or keep them on the
     128 x 128 kernel (0 / False); all give identical bits."""
     _lib.call("ensvs_set_big_tile", int(mode), int(stages))
+
+
+def set_small(on):
+    """Small-M bf16-operand launches (< 128 tiles of 128 x 128) on the 64 x 64-tile kernel
+    (default; the one-group kernel's bits) or on the dual / split-K / one-group kernels."""
+    _lib.call("ensvs_set_small", int(bool(on)))
 
 
 def set_dual_small(on):

@@ -77,11 +77,17 @@ int ensvs_set_big_tile(int mode, int stages);
  * ENSVS_DUAL_SMALL); 0 keeps them on the one-group kernel (the same bits as the register-
  * staged kernel). */
 int ensvs_set_dual_small(int on);
+/* Launches of fewer than 128 output tiles of 128 x 128 (small M: the 2 000-frame reverse-
+ * diffusion GEMMs) run a 64 x 64-tile kernel that fills the chip (default on, ENSVS_SMALL; it
+ * takes precedence over the two-K-group kernel and split-K); same accumulation order as the
+ * one-group kernel, so the same bits.  0 turns it off. */
+int ensvs_set_small(int on);
 /* part / part_floats (optional, may be NULL / 0): fp32 workspace for split-K.  Launches of
  * fewer than 128 output tiles (small M: the 2 000-frame reverse-diffusion GEMMs) split their
  * K-steps over up to 8 workgroups per tile when part holds ksplit x M x Npad floats; the
  * slices are summed in a fixed order by a second kernel that runs the epilogue
- * (deterministic; ENSVS_SPLITK=0 disables). */
+ * (deterministic; ENSVS_SPLITK=0 disables).  Operand rows: bf16, ld % 8 == 0, 16-B aligned;
+ * a segment with K % 8 != 0 has its rows zero-padded to a multiple of 8 within ld. */
 int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N, int Npad,
                           const void* W, const float* bias, float* Y, int ldy, int epi, int relu,
                           int accum, float* aux0, int ld0, const float* aux1, int ld1, float alpha,
@@ -221,6 +227,12 @@ int ensvs_q_sample(const float* y, int ldy, const float* noise, int ldn, const l
                    float* xn, int ldx, void* stream);
 int ensvs_p_sample(float* x, const float* eps, const float* noise, long long n, float sra,
                    float srm1, float c1, float c2, float sigma, void* stream);
+/* p_sample over x [M][Mc] that also writes the next denoiser input's bf16 GEMM operand
+ * xb [M][ldb] (ldb % 8 == 0, >= Mc; columns Mc..ldb-1 zero: the operand's K padding).
+ * eps == NULL: x unchanged, only the copy (the draw x_K before the first step). */
+int ensvs_p_sample_bf16(float* x, const float* eps, const float* noise, long long M, int Mc,
+                        float sra, float srm1, float c1, float c2, float sigma, void* xb,
+                        int ldb, void* stream);
 /* Masked L1 loss summed over streams / N with its gradient fused
  * (bin/train_acoustic_multitrack.py:115-173).  loss = invN * sum|a-b| over valid
  * frames; ga = gscale * invN * sign(a-b) (0 on padding).  gscale = 1/world folds the

@@ -190,8 +190,9 @@ def _close(a, b, rtol):
 @pytest.mark.parametrize("epi", [L.EPI_PLAIN, L.EPI_GATE, "gate_bf16", L.EPI_RESSKIP,
                                  L.EPI_GATE_BWD, L.EPI_ADDSCALE, L.EPI_RELU_MASK])
 def test_splitk_and_dual_match_unsplit(epi):
-    """Small-M launches (2 x 1002 frames: 64 tiles, 16 K-steps) on the two-K-group kernel
-    (the default) and with split-K (4 K splits): the same results as the one-group kernel up
+    """Small-M launches (2 x 1002 frames: 64 tiles, 16 K-steps): the 64 x 64-tile kernel (the
+    default) bit-identical to the one-group kernel; the two-K-group kernel and split-K (4 K
+    splits): the same results as the one-group kernel up
     to fp32 summation order (rel 1e-5; bf16 copies within one bf16 rounding), every epilogue
     and bf16 output copy, and bit-identical from run to run."""
     torch.manual_seed(21)
@@ -235,8 +236,12 @@ def test_splitk_and_dual_match_unsplit(epi):
     split = K.SPLITK["on"]
     try:
         K.SPLITK["on"] = False
+        K.set_small(False)
         K.set_dual_small(False)
         ref = run()
+        K.set_small(True)
+        small = run()
+        K.set_small(False)
         K.set_dual_small(True)
         dual = [run(), run()]
         K.SPLITK["on"] = True
@@ -244,6 +249,10 @@ def test_splitk_and_dual_match_unsplit(epi):
     finally:
         K.SPLITK["on"] = split
         K.set_dual_small(True)
+        K.set_small(True)
+    # the 64 x 64-tile kernel: the one-group kernel's accumulation order, identical bits
+    for t0, t1 in zip(ref, small):
+        assert torch.equal(t0, t1)
     for (y1, a1, b1), (y2, a2, b2) in (dual, spl):
         assert torch.equal(y1, y2) and torch.equal(a1, a2) and torch.equal(b1, b2)
         y0, a0, b0 = ref

@@ -1,7 +1,9 @@
 """Per-launch census of one training step (dev tool): every libensvs entry point of one eager,
 serial bench step (30 pairs x 1024 frames) timed with HIP events and tagged with the GEMM /
 weight-gradient shape that issued it; aggregated by (entry point, shape), largest total
-first.   python tools/census.py [rows]
+first.   python tools/census.py [rows] [synth]
+synth: the mgc DiffNet's 100-step reverse diffusion of one (main, sub) pair at 2 000 frames
+(eager, the launches the inference graph captures) instead of the training step.
 """
 import collections
 import os
@@ -15,6 +17,7 @@ from ensemble_svs_with_interactions_amd import kernels as K  # noqa: E402
 from ensemble_svs_with_interactions_amd.train import FusedAdam, train_step  # noqa: E402
 
 ROWS = int(sys.argv[1]) if len(sys.argv) > 1 else 45
+SYNTH = len(sys.argv) > 2 and sys.argv[2] == "synth"
 REC = []
 TAG = [None]
 ON = [False]
@@ -65,9 +68,28 @@ K.gemm = tagged(K.gemm, gemm_tag)
 K.wgrad = tagged(K.wgrad, wgrad_tag)
 
 
+def run_synth(dev):
+    model = configs.instantiate(configs.multitrack_diffusion(num_speakers=4)).to(dev).eval()
+    gd = model.mgc_model
+    B, T = 1, 2004
+    E = gd.denoise_fn.E
+    cond = torch.randn(B * T, E, device=dev)
+    x = torch.randn(B * T, gd.out_dim, device=dev)
+    noise = torch.randn(B * T, gd.out_dim, device=dev)
+    gd._reverse(x, cond, E, B, T, lambda k: noise)
+    torch.cuda.synchronize()
+    ON[0] = True
+    gd._reverse(x, cond, E, B, T, lambda k: noise)
+    torch.cuda.synchronize()
+    ON[0] = False
+
+
 def main():
     dev = torch.device("cuda")
     engine.set_concurrency(False)
+    if SYNTH:
+        run_synth(dev)
+        return report()
     torch.manual_seed(20250321)
     model = configs.instantiate(configs.multitrack_diffusion(num_speakers=4)).to(dev)
     opt = FusedAdam(model, lr=1e-4, clip_norm=1.0)
@@ -83,6 +105,10 @@ def main():
     train_step(model, opt, xm, xs, ym, s0, s1, lens)
     torch.cuda.synchronize()
     ON[0] = False
+    report()
+
+
+def report():
     agg = collections.defaultdict(lambda: [0, 0.0])
     tot = 0.0
     for name, tag, s, e in REC:
@@ -91,7 +117,8 @@ def main():
         a[0] += 1
         a[1] += ms
         tot += ms
-    print(f"{len(REC)} launches, {tot:.2f} ms (event-bracketed, serial eager step)")
+    print(f"{len(REC)} launches, {tot:.2f} ms (event-bracketed, serial eager "
+          f"{'reverse diffusion' if SYNTH else 'step'})")
     for (name, tag), (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:ROWS]:
         print(f"{ms:8.3f} ms {n:4d}x {ms / n * 1e3:8.1f} us  {name:28s} {tag or ''}")
 

@@ -1483,7 +1483,8 @@ __device__ __forceinline__ void big_bias(const GemmArgs& a, int n0, int wc, int 
 }
 
 // GATE8: the launch runs the 16-B gate epilogue (the DiffNet gate GEMM), compiled without
-// the other epilogues' operand registers
+// the other epilogues' operand registers.  (An activation image three slots deep, issued two
+// K-steps ahead -- 96 KB in flight in all 160 KB of LDS -- measured slower: 47.9 vs 43.6 us.)
 template <bool GATE8>
 __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_big_kernel(const GemmArgs a) {
   constexpr int TILE_A = BMB * BK2 * 2;  // 32 KB
@@ -2721,18 +2722,19 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
   if (use_big_tile(a)) {
     const dim3 grid_b(cdiv(a.M, BMB), Npad / BNB);
     if (g_big_tile == 2) {
-      const size_t lb = (size_t)2 * (BMB + BNB) * BK2 * 2;  // two stages of both images
-      static const hipError_t eb = hipFuncSetAttribute(
-          (const void*)conv_gemm_b16_big_kernel<false>,
-          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
-      static const hipError_t eg = hipFuncSetAttribute(
-          (const void*)conv_gemm_b16_big_kernel<true>,
-          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
-      if (eb != hipSuccess || eg != hipSuccess) return ENSVS_E_HIP;
-      if (a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS))
-        hipLaunchKernelGGL(conv_gemm_b16_big_kernel<true>, grid_b, dim3(NTHRB), lb, st, a);
-      else
-        hipLaunchKernelGGL(conv_gemm_b16_big_kernel<false>, grid_b, dim3(NTHRB), lb, st, a);
+      const bool gate = a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS);
+#define BIG(G)                                                                            \
+  do {                                                                                    \
+    const size_t lb = (size_t)2 * (BMB + BNB) * BK2 * 2;  /* two stages of both images */ \
+    static const hipError_t eb = hipFuncSetAttribute(                                     \
+        (const void*)conv_gemm_b16_big_kernel<G>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+        (int)lb);                                                                         \
+    if (eb != hipSuccess) return ENSVS_E_HIP;                                             \
+    hipLaunchKernelGGL(conv_gemm_b16_big_kernel<G>, grid_b, dim3(NTHRB), lb, st, a);      \
+  } while (0)
+      if (gate) BIG(true);
+      else BIG(false);
+#undef BIG
     } else {
 #define RING(S)                                                                           \
   do {                                                                                    \

@@ -344,7 +344,7 @@ __device__ __forceinline__ void gate_row8(const GemmArgs& a, const float* t, int
     st4(a.Y + (long long)m * a.ldy + c, z0);
     st4(a.Y + (long long)m * a.ldy + c + 4, z1);
   }
-  if (a.epi == EPI_GATE) shadow8(a, m, c, z0, z1);
+  shadow8(a, m, c, z0, z1);
 }
 
 // 8-channel GATE / GATE_TS rows of a staged tile: NTT threads, tile rows [0, ROWS), T row
@@ -507,7 +507,8 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         f32x4 z;
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = ftanh_(g[e]) * fsigmoid_(f[e]);
-        st4(a.Y + (long long)m * a.ldy + c, z);
+        if (a.Y) st4(a.Y + (long long)m * a.ldy + c, z);
+        shadow4(a, m, c, z);
       }
     }
 #pragma unroll
@@ -915,21 +916,27 @@ struct TapPtrs {
   int K, Kp;    // wave-uniform
 };
 
+// pd: segment 0 of an uSFGAN adaptive block -- tap j of row i reads the pitch-dependent row
+// pd_src(d_i, pdil, t_i, Tin, j) (d0..d3: the staged rows' dilation factors)
 __device__ __forceinline__ TapPtrs tap_ptrs(const SegU S, int j, int Npad, int n0, int rl,
                                             int cq8a, int cq8b, const int b0, const int b1,
                                             const int b2, const int b3, const int t0,
                                             const int t1, const int t2, const int t3,
-                                            unsigned okm) {
+                                            unsigned okm, bool pd = false, float d0 = 0.f,
+                                            float d1 = 0.f, float d2 = 0.f, float d3 = 0.f,
+                                            float pdil = 0.f) {
   TapPtrs P;
   const int bt[4] = {b0, b1, b2, b3}, tt[4] = {t0, t1, t2, t3};
+  const float dd[4] = {d0, d1, d2, d3};
   const int shj = S.shift0 + j * S.dil;
   P.va = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c8 = (i & 1) ? cq8b : cq8a;
     const int ts = tt[i] + shj;
-    const int src = S.pad == PAD_ZERO ? ((unsigned)ts < (unsigned)S.Tin ? ts : -1)
-                                      : pad_src(ts, S.Tin, S.pad);
+    const int src = pd ? pd_src(dd[i], pdil, tt[i], S.Tin, j)
+                       : S.pad == PAD_ZERO ? ((unsigned)ts < (unsigned)S.Tin ? ts : -1)
+                                           : pad_src(ts, S.Tin, S.pad);
     const bool ok = ((okm >> i) & 1) && src >= 0;
     P.va |= ok ? (1u << i) : 0u;
     P.pa[i] = (const char*)(S.x + (unsigned)((bt[i] * S.Tin + (ok ? src : 0)) * S.ld + c8));
@@ -972,6 +979,14 @@ __global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a
     tt[i] = ok ? m - bt[i] * Tout : 0;
     okm |= ok ? (1u << i) : 0u;
   }
+  // uSFGAN adaptive block: segment 0 gathers pitch-dependent rows (the staged rows' factors)
+  const bool hpd = a.seg[0].pd != nullptr;
+  float pdv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (hpd) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pdv[i] = ((okm >> i) & 1) ? a.seg[0].pd[m0 + rl + 8 * i] : 0.f;
+  }
+  const float pdil = (float)a.seg[0].pd_dil;
   // g_zero's address, opaque to the compiler: it would otherwise re-load it from the GOT
   // (s_load + lgkmcnt wait) at every use inside the K loop
   unsigned long long zpu = (unsigned long long)(const void*)g_zero;
@@ -998,7 +1013,8 @@ __global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a
     }
   }
 #define TAP_PTRS(S) \
-  tap_ptrs(S, qj, Npad, n0, rl, cq8a, cq8b, bt[0], bt[1], bt[2], bt[3], tt[0], tt[1], tt[2], tt[3], okm)
+  tap_ptrs(S, qj, Npad, n0, rl, cq8a, cq8b, bt[0], bt[1], bt[2], bt[3], tt[0], tt[1], tt[2], tt[3], okm, \
+           &(S) == &S0 && hpd, pdv[0], pdv[1], pdv[2], pdv[3], pdil)
   TapPtrs P = qs == 0 ? TAP_PTRS(S0) : (qs == 1 ? TAP_PTRS(S1) : TAP_PTRS(S2));
 #define ISSUE(it)                                                                        \
   do {                                                                                   \
@@ -1377,7 +1393,8 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs& a, const float* T,
         f32x4 z;
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = ftanh_(g[e]) * fsigmoid_(f[e]);
-        st4(a.Y + (long long)m * a.ldy + c, z);
+        if (a.Y) st4(a.Y + (long long)m * a.ldy + c, z);
+        shadow4(a, m, c, z);
       }
     }
     }
@@ -2020,6 +2037,23 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict_
     *(bf16x8*)(y + m * ldy + k) = bf16x8{(__bf16)v0[0], (__bf16)v0[1], (__bf16)v0[2],
                                          (__bf16)v0[3], (__bf16)v1[0], (__bf16)v1[1],
                                          (__bf16)v1[2], (__bf16)v1[3]};
+  }
+}
+
+// K % 8 != 0 (the uSFGAN auxiliary features, K = 65): y[m][k] = bf16(x[m][k]) for k < K and
+// 0 up to the next multiple of 8 -- the zero K padding the 16-B operand chunks read.
+__global__ __launch_bounds__(256) void cast_bf16_pad_kernel(const float* __restrict__ x, int ldx,
+                                                            long long M, int K, int K8,
+                                                            __bf16* __restrict__ y, int ldy) {
+  const long long n = M * K8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / K8;
+    const int k = (int)(i - m * K8) * 8;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (__bf16)(k + e < K ? x[m * ldx + k + e] : 0.f);
+    *(bf16x8*)(y + m * ldy + k) = o;
   }
 }
 
@@ -2708,18 +2742,20 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     const ensvs_conv_seg& g = segs[s];
     // K % 8 != 0: the caller zero-pads the operand rows to a multiple of 8 within ld (the
     // last 16-B chunk reads the padding; the packed weights are zero there anyway)
-    if (g.radd || g.pd || g.ld % 8 || g.ld < ((g.K + 7) & ~7) || ((uintptr_t)g.x & 15))
+    // (pd: segment 0 only, checked by fill_gemm_args; the 128 x 128 kernel gathers it)
+    if (g.radd || g.ld % 8 || g.ld < ((g.K + 7) & ~7) || ((uintptr_t)g.x & 15))
       return ENSVS_E_ARG;
   }
   if (((uintptr_t)W & 15)) return ENSVS_E_ARG;
   dim3 grid(cdiv(a.M, BM), Npad / BN);
+  const bool has_pd = segs[0].pd != nullptr;
   for (int s = 0; s < nseg; ++s) {  // 32-bit element offsets inside the kernel
     const ensvs_conv_seg& g = segs[s];
     if ((long long)B * g.Tin * g.ld >= (1ll << 31) ||
         (long long)g.taps * Npad * g.Kp >= (1ll << 30))
       return ENSVS_E_SHAPE;
   }
-  if (use_big_tile(a)) {
+  if (!has_pd && use_big_tile(a)) {
     const dim3 grid_b(cdiv(a.M, BMB), Npad / BNB);
     if (g_big_tile == 2) {
       const bool gate = a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS);
@@ -2754,19 +2790,21 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     ENSVS_CHECK_LAUNCH();
     return ENSVS_OK;
   }
-  // small M (fewer than 128 tiles of 128 x 128): the 64 x 64-tile kernel fills the chip
+  // small M (fewer than 128 tiles of 128 x 128): the 64 x 64-tile kernel fills the chip; it
+  // also takes N <= 64 at any M (a 128-wide tile would leave half its columns and half the
+  // epilogue threads idle: the uSFGAN block output GEMMs, 480 000 x 64)
   if (g_small < 0) {
     const char* e = getenv("ENSVS_SMALL");
     g_small = e ? atoi(e) : 1;
   }
-  if (g_small && !a.csum && a.vec_out && Npad % BNS == 0 &&
-      (long long)grid.x * grid.y < 128) {
+  if (g_small && !has_pd && !a.csum && a.vec_out && Npad % BNS == 0 &&
+      ((long long)grid.x * grid.y < 128 || a.N <= BNS)) {
     static const int sms = [] {
       const char* e = getenv("ENSVS_SMALL_STAGES");
       const int v = e ? atoi(e) : 5;
       return v < 3 ? 3 : (v > 5 ? 5 : v);
     }();
-    const dim3 gs(cdiv(a.M, BMS), Npad / BNS);
+    const dim3 gs(cdiv(a.M, BMS), a.N <= BNS ? 1 : Npad / BNS);
 #define SMALL(S)                                                                          \
   do {                                                                                    \
     const size_t ls = std::max<size_t>((size_t)(S) * 2 * BMS * BK2 * 2, (size_t)BMS * EPS * 4); \
@@ -2790,7 +2828,7 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     const char* e = getenv("ENSVS_SPLITK");
     return !(e && e[0] == '0');
   }();
-  if (splitk_on && a.part && !a.csum && a.vec_out && a.epi != EPI_NONE) {
+  if (splitk_on && !has_pd && a.part && !a.csum && a.vec_out && a.epi != EPI_NONE) {
     const long long tiles = (long long)grid.x * grid.y;
     int nit = 0;
     for (int s = 0; s < nseg; ++s) nit += cdiv(segs[s].K, BK2) * segs[s].taps;
@@ -2807,7 +2845,8 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     const char* e = getenv("ENSVS_DUAL_SMALL");
     g_dual_small = e ? atoi(e) : 1;
   }
-  if (g_dual_small && a.ksplit <= 1 && !a.csum && (long long)grid.x * grid.y < 128) {
+  if (g_dual_small && !has_pd && a.ksplit <= 1 && !a.csum &&
+      (long long)grid.x * grid.y < 128) {
     const size_t ld2 = std::max<size_t>(4 * lds, EPI_LDS);  // 2 stages x 2 K-groups
     static const hipError_t ed = hipFuncSetAttribute(
         (const void*)conv_gemm_b16_dual_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2902,7 +2941,8 @@ ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, in
     a.csum_ld = csum_ld;
   }
   // Y may be dropped where the epilogue's other outputs are all the caller needs
-  if (!Y && !((a.epi == EPI_GATE && ybf) || (a.epi == EPI_GATE_BWD && (ybf || csum))))
+  if (!Y && !(((a.epi == EPI_GATE || a.epi == EPI_GATE_TS) && ybf) ||
+              (a.epi == EPI_GATE_BWD && (ybf || csum))))
     return ENSVS_E_ARG;
   if (ybf) {
     if (!a.vec_out || N % 4 || ybf_ld % 4 || ((uintptr_t)ybf & 7) ||
@@ -2947,6 +2987,16 @@ ENSVS_API int ensvs_tile_colsum(const float* y, int ldy, int M, int N, float* ou
 ENSVS_API int ensvs_cast_bf16(const float* x, int ldx, const float* radd, int radd_ld, int T,
                               long long M, int K, void* y, int ldy, void* stream) {
   if (M <= 0 || K <= 0) return ENSVS_OK;
+  if (K % 8 && !radd) {  // zero-padded copy (a K % 8 != 0 operand of the bf16 kernels)
+    const int K8 = (K + 7) / 8;
+    if (ldy % 8 || ldy < 8 * K8 || ldx < K || ((uintptr_t)y & 15)) return ENSVS_E_ARG;
+    const long long n = M * K8;
+    const int blocks = (int)std::min<long long>(8192, (n + 255) / 256);
+    hipLaunchKernelGGL(cast_bf16_pad_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x,
+                       ldx, M, K, K8, (__bf16*)y, ldy);
+    ENSVS_CHECK_LAUNCH();
+    return ENSVS_OK;
+  }
   if (K % 8 || ldx % 4 || ldy % 8 || (radd && (radd_ld % 4 || T <= 0)) ||
       (((uintptr_t)x | (uintptr_t)y | (uintptr_t)radd) & 15))
     return ENSVS_E_ARG;

@@ -171,7 +171,10 @@ def _castable(s):
 
 def _bf16_act_ok(segs, W, Npad, M):
     if any(s.x.dtype == torch.bfloat16 for s in segs):  # operands already rounded
-        assert W.dtype == _lib.DT_BF16 and all(s.pd is None for s in segs)
+        # (a pitch-dependent segment: segment 0, already bf16 -- the 128 x 128 kernel gathers it)
+        assert W.dtype == _lib.DT_BF16 and all(s.pd is None or (i == 0 and s.x.dtype ==
+                                                                torch.bfloat16)
+                                               for i, s in enumerate(segs))
         assert all(s.radd is None for s in segs if s.x.dtype == torch.bfloat16)
         for s in segs:  # ensvs_conv_gemm_bf16a's contract: a caller-side layout error
             if s.x.dtype == torch.bfloat16 and (s.ld % 8 or (s.x.data_ptr() + 2 * s.xoff) % 16
@@ -279,7 +282,8 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
             return
     if ybf is not None and csum is None:
         assert ybf.dtype == torch.bfloat16 and epi in (_lib.EPI_PLAIN, _lib.EPI_GATE,
-                                                       _lib.EPI_RESSKIP, _lib.EPI_GATE_BWD)
+                                                       _lib.EPI_RESSKIP, _lib.EPI_GATE_BWD,
+                                                       _lib.EPI_GATE_TS, _lib.EPI_ADDSCALE)
         yp = Y.data_ptr() + 4 * yoff
         vec = (yp % 16 == 0 and ldy % 4 == 0 and N % 4 == 0 and C % 4 == 0 and
                all(t is None or (t.data_ptr() % 16 == 0 and ld % 4 == 0)
@@ -292,7 +296,7 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
                  bias_off=bias_off)
             # the same rounding by a cast pass over what was written
             width = 2 * C if epi == _lib.EPI_GATE_BWD else (
-                C if epi in (_lib.EPI_GATE, _lib.EPI_RESSKIP) else N)
+                C if epi in (_lib.EPI_GATE, _lib.EPI_RESSKIP, _lib.EPI_GATE_TS) else N)
             cast_bf16(Y, ldy, width, B * Tout, xoff=yoff, radd=ybf_radd, radd_ld=ybf_radd_ld,
                       T=Tout, out=ybf, out_ld=ybf_ld)
             return
@@ -317,7 +321,7 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
         d.pad, d.Tin, d.Kp = s.pad, s.Tin, s.ref.Kp
     bptr = None if bias is None else bias.data_ptr() + 4 * bias_off
     yptr = Y.data_ptr() + 4 * yoff
-    if not keep_y and ((epi == _lib.EPI_GATE and ybf is not None) or
+    if not keep_y and ((epi in (_lib.EPI_GATE, _lib.EPI_GATE_TS) and ybf is not None) or
                        (epi == _lib.EPI_GATE_BWD and (ybf is not None or csum is not None))):
         yptr = None  # only reached on the fused-epilogue path
     # split-K workspace for small-M launches (fewer than 128 output tiles of 128 x 128)

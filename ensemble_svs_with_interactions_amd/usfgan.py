@@ -426,27 +426,38 @@ class ParallelHnUSFGANGenerator(nn.Module):
         return prep
 
     # ---- kernels ------------------------------------------------------------------
-    def _blocks(self, P, name, x, c, ldc, d, B, L, z, relu_last=False):
+    def _blocks(self, P, name, x, c, ldc, d, B, L, z, relu_last=False, xb=None, cb=None,
+                zb=None):
+        """The network's residual blocks on x in place.  bf16 operands (xb, cb, zb given): the
+        blocks read x's bf16 copy xb (kept current by each output GEMM's epilogue), the
+        auxiliary features' zero-padded bf16 copy cb and z's bf16 copy zb -- the rounding
+        the register-staged kernel applies while staging, so the same bits, without an fp32
+        z round trip or an fp32 re-read of the features per block."""
         net = getattr(self, name)
-        R, Gh = self.n_ch, self.gate_channels // 2
+        R, Gh, Ca = self.n_ch, self.gate_channels // 2, self.aux_channels
         nb = len(net.conv_dilated)
+        xs = x if xb is None else xb
         for i, (mode, dil) in enumerate(zip(net.block_modes, net.dilations)):
             key = f"{name}.{i}"
             if mode:
-                seg0 = K.Seg(x, R, R, P.ref[key + ".g"], L, taps=3, pd=d, pd_dil=dil)
+                seg0 = K.Seg(xs, R, R, P.ref[key + ".g"], L, taps=3, pd=d, pd_dil=dil)
             else:
                 if dil >= L:
                     raise ValueError(f"reflect padding {dil} needs more than {dil} samples")
-                seg0 = K.Seg(x, R, R, P.ref[key + ".g"], L, taps=3, dil=dil, shift0=-dil,
+                seg0 = K.Seg(xs, R, R, P.ref[key + ".g"], L, taps=3, dil=dil, shift0=-dil,
                              pad=_lib.PAD_REFLECT)
-            K.gemm([seg0, K.Seg(c, ldc, ldc, P.ref[key + ".aux"], L)], B, L, 2 * Gh, P.fwd, z,
-                   Gh, epi=_lib.EPI_GATE_TS, C=Gh, **P.bias(key + ".g"))
-            K.gemm([K.Seg(z, Gh, Gh, P.ref[key + ".out"], L)], B, L, R, P.fwd, x, R,
+            seg1 = (K.Seg(c, ldc, ldc, P.ref[key + ".aux"], L) if cb is None else
+                    K.Seg(cb, cb.shape[1], Ca, P.ref[key + ".aux"], L))
+            K.gemm([seg0, seg1], B, L, 2 * Gh, P.fwd, z, Gh, epi=_lib.EPI_GATE_TS, C=Gh,
+                   ybf=zb, ybf_ld=Gh, keep_y=zb is None, **P.bias(key + ".g"))
+            K.gemm([K.Seg(z, Gh, Gh, P.ref[key + ".out"], L) if zb is None else
+                    K.Seg(zb, Gh, Gh, P.ref[key + ".out"], L)], B, L, R, P.fwd, x, R,
                    epi=_lib.EPI_ADDSCALE, aux1=x, ld1=R, alpha=SQRT1_2,
-                   relu=relu_last and i == nb - 1, **P.bias(key + ".out"))
+                   relu=relu_last and i == nb - 1, ybf=xb, ybf_ld=R, **P.bias(key + ".out"))
 
     def _conv_last(self, P, xr, B, L, dev):
-        """conv_last on an already ReLU'd input (generator.py:461-466)."""
+        """conv_last on an already ReLU'd input (generator.py:461-466); xr fp32 or its bf16
+        copy."""
         R = self.n_ch
         t = empty(B * L, R, device=dev)
         K.gemm([K.Seg(xr, R, R, P.ref["last1"], L)], B, L, R, P.fwd, t, R, relu=True,
@@ -491,21 +502,33 @@ class ParallelHnUSFGANGenerator(nn.Module):
             a, lda, Kin = out, R, R
         h = empty(M, R, device=dev)
         n = empty(M, R, device=dev)
+        # inference with bf16 operands: the residual streams' bf16 copies ride along in the
+        # epilogues, the auxiliary features are rounded once (zero K padding) for all blocks
+        b16 = not keep and K.bf16_operands(P.fwd, M)
+        hb = nb_ = cb = zb = None
+        if b16:
+            hb = empty(M, R, device=dev, dtype=torch.bfloat16)
+            nb_ = empty(M, R, device=dev, dtype=torch.bfloat16)
+            zb = empty(M, Gh, device=dev, dtype=torch.bfloat16)
+            cb = empty(M, -(-Ca // 8) * 8, device=dev, dtype=torch.bfloat16)
+            K.cast_bf16(c, ldc, Ca, M, out=cb, out_ld=cb.shape[1])
         K.gemm([K.Seg(xsrc, 2, 1, P.ref["first_sine"], L)], B, L, R, P.fwd, h, R,
-               **P.bias("first_sine"))
+               ybf=hb, ybf_ld=R, **P.bias("first_sine"))
         K.gemm([K.Seg(xsrc, 2, 1, P.ref["first_noise"], L, xoff=1)], B, L, R, P.fwd, n, R,
-               **P.bias("first_noise"))
+               ybf=nb_, ybf_ld=R, **P.bias("first_noise"))
         z = empty(M, Gh, device=dev)
-        self._blocks(P, "harmonic_network", h, c, ldc, d, B, L, z)
-        self._blocks(P, "noise_network", n, c, ldc, d, B, L, z)
+        self._blocks(P, "harmonic_network", h, c, ldc, d, B, L, z, xb=hb, cb=cb, zb=zb)
+        self._blocks(P, "noise_network", n, c, ldc, d, B, L, z, xb=nb_, cb=cb, zb=zb)
         s = empty(M, R, device=dev)
         call("ensvs_usf_mix", a.data_ptr(), h.data_ptr(), n.data_ptr(), s.data_ptr(), M * R,
              int(keep), stream())
         if not keep:
             # inference: the filter runs in place on s, its last block emits ReLU(x) for
             # conv_last
-            self._blocks(P, "filter_network", s, c, ldc, d, B, L, z, relu_last=True)
-            return self._conv_last(P, s, B, L, dev)
+            sb = K.cast_bf16(s, R, R, M) if b16 else None
+            self._blocks(P, "filter_network", s, c, ldc, d, B, L, z, relu_last=True, xb=sb,
+                         cb=cb, zb=zb)
+            return self._conv_last(P, s if sb is None else sb, B, L, dev)
         x = empty(M, R, device=dev)
         call("ensvs_copy_cols", s.data_ptr(), R, x.data_ptr(), R, M, R, stream())
         self._blocks(P, "filter_network", x, c, ldc, d, B, L, z, relu_last=True)

@@ -111,7 +111,8 @@ int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, int B, int T
  * the same sums, bit for bit, from a Y written by any other path.  Y may be NULL for GATE
  * with ybf and for GATE_BWD with ybf or csum (the fp32 output is not needed). */
 int ensvs_tile_colsum(const float* y, int ldy, int M, int N, float* out, int ldo, void* stream);
-/* y[m][k] = bf16(x[m][k] + radd[m / T][k]) (radd optional), K % 8 == 0. */
+/* y[m][k] = bf16(x[m][k] + radd[m / T][k]) (radd optional), K % 8 == 0; without radd K may
+ * be any size: columns K .. 8*ceil(K/8) - 1 of y are then zero (ldy >= that width). */
 int ensvs_cast_bf16(const float* x, int ldx, const float* radd, int radd_ld, int T, long long M,
                     int K, void* y, int ldy, void* stream);
 

@@ -141,3 +141,37 @@ def test_bf16_generator():
         assert e < 5e-2
     finally:
         engine.set_gemm_precision("fp32")
+
+
+def test_bf16_operand_copies_bitwise():
+    """Inference on bf16 operand copies (the residual streams' copies from the output-GEMM
+    epilogues, the zero-padded auxiliary features rounded once, z in bf16 only, the
+    pitch-dependent gather on the bf16 copy) = the register-staged kernels that round the
+    fp32 operands while staging: identical waveform bits, full-size generator (bench config),
+    two tracks."""
+    engine.set_gemm_precision("bf16")
+    saved = dict(K.BF16_ACT)
+    try:
+        torch.manual_seed(9)
+        gen = configs.instantiate(configs.usfgan_generator()).cuda()
+        gen.remove_weight_norm()
+        wr = USFGANWrapper({"data": dict(configs.USFGAN_DATA),
+                            "generator": {"aux_context_window": 2}}, gen)
+        T = 60
+        f0 = 150.0 + 100.0 * torch.rand(2, T, device="cuda")
+        f0[:, 10:14] = 0.0  # unvoiced frames
+        aux = torch.randn(2, T, gen.aux_channels, device="cuda")
+        L = T * 240
+        g = torch.Generator(device="cuda").manual_seed(4)
+        nz = [torch.randn(2, L, device="cuda", generator=g) for _ in range(2)]
+        outs = []
+        for on in (False, True):
+            K.BF16_ACT.update(on=on)
+            outs.append(wr.inference_batch(f0, aux, noises=nz))
+            torch.cuda.synchronize()
+        assert torch.isfinite(outs[1]).all()
+        assert torch.equal(outs[0], outs[1])
+    finally:
+        K.BF16_ACT.clear()
+        K.BF16_ACT.update(saved)
+        engine.set_gemm_precision("fp32")

@@ -3,7 +3,8 @@ serial bench step (30 pairs x 1024 frames) timed with HIP events and tagged with
 weight-gradient shape that issued it; aggregated by (entry point, shape), largest total
 first.   python tools/census.py [rows] [synth]
 synth: the mgc DiffNet's 100-step reverse diffusion of one (main, sub) pair at 2 000 frames
-(eager, the launches the inference graph captures) instead of the training step.
+(eager, the launches the inference graph captures) instead of the training step; voc: one
+uSFGAN generator pass over one 2 000-frame track (480 000 samples).
 """
 import collections
 import os
@@ -18,6 +19,7 @@ from ensemble_svs_with_interactions_amd.train import FusedAdam, train_step  # no
 
 ROWS = int(sys.argv[1]) if len(sys.argv) > 1 else 45
 SYNTH = len(sys.argv) > 2 and sys.argv[2] == "synth"
+VOC = len(sys.argv) > 2 and sys.argv[2] == "voc"
 REC = []
 TAG = [None]
 ON = [False]
@@ -84,9 +86,29 @@ def run_synth(dev):
     ON[0] = False
 
 
+def run_voc(dev):
+    from ensemble_svs_with_interactions_amd import usfgan
+    voc = configs.instantiate(configs.usfgan_generator()).to(dev)
+    voc.remove_weight_norm()
+    wrapper = usfgan.USFGANWrapper({"data": dict(configs.USFGAN_DATA),
+                                    "generator": {"aux_context_window": 2}}, voc)
+    T = 2000
+    f0 = 200.0 + 20.0 * torch.rand(1, T, device=dev)
+    aux = torch.randn(1, T, voc.aux_channels, device=dev)
+    wrapper.inference_batch(f0, aux)
+    torch.cuda.synchronize()
+    ON[0] = True
+    wrapper.inference_batch(f0, aux)
+    torch.cuda.synchronize()
+    ON[0] = False
+
+
 def main():
     dev = torch.device("cuda")
     engine.set_concurrency(False)
+    if VOC:
+        run_voc(dev)
+        return report()
     if SYNTH:
         run_synth(dev)
         return report()
@@ -118,7 +140,7 @@ def report():
         a[1] += ms
         tot += ms
     print(f"{len(REC)} launches, {tot:.2f} ms (event-bracketed, serial eager "
-          f"{'reverse diffusion' if SYNTH else 'step'})")
+          f"{'reverse diffusion' if SYNTH else ('vocoder' if VOC else 'step')})")
     for (name, tag), (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:ROWS]:
         print(f"{ms:8.3f} ms {n:4d}x {ms / n * 1e3:8.1f} us  {name:28s} {tag or ''}")
 

@@ -68,6 +68,7 @@ SIGNATURES = {
     "ensvs_set_big_tile": [c_int, c_int],
     "ensvs_set_dual_small": [c_int],
     "ensvs_set_small": [c_int],
+    "ensvs_set_recurrence_exclusive": [c_int],
     "ensvs_tile_colsum": [c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "ensvs_cast_bf16": [c_vp, c_int, c_vp, c_int, c_int, c_ll, c_int, c_vp, c_int, c_vp],
     "ensvs_conv_wgrad": [c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,

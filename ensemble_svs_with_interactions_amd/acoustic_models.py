@@ -31,6 +31,19 @@ from .model import init_weights
 # 30 x 1024) -- the V/UV recurrences then lengthen the tail instead of filling it.
 _VUV_AFTER_MGC = {"on": os.environ.get("ENSVS_VUV_AFTER_MGC", "0") == "1"}
 
+
+# Step schedule of the fused branches (0 lf0, 1 mgc, 2 bap, 3 vuv; profiles/r2_schedule_ab.txt).
+# BRANCH_AFTER {branch: branch whose forward must finish first}: the bap branch starts when
+# the mgc forward ends, so mgc -- the critical branch (13.9 ms alone) -- runs its forward
+# beside the latency-bound lf0 / vuv chains only (ENSVS_BRANCH_AFTER, "" = all at once:
+# 20.9 vs 21.2 ms/step).  EXCL_BRANCHES: branches whose recurrence workgroups reserve their
+# CU's LDS (the lf0 and mgc chains; bap / vuv LSTM workgroups share CUs with GEMMs:
+# 20.8 vs 21.0 ms/step; ENSVS_EXCL_BRANCHES).
+BRANCH_AFTER = {int(b): int(a) for b, a in (kv.split(":") for kv in
+                os.environ.get("ENSVS_BRANCH_AFTER", "2:1").split(",") if kv)}
+EXCL_BRANCHES = {int(v) for v in os.environ.get("ENSVS_EXCL_BRANCHES", "0,1").split(",")
+                 if v}
+
 class ZoneOutCell(nn.Module):
     """nnsvs/tacotron/decoder.py:20-48 (container).  The recipe uses zoneout 0, for which
     the cell output is exactly the LSTMCell output in train and eval modes."""
@@ -711,14 +724,25 @@ class _MultistreamHybrid(BaseModel):
         if reduce_hook is not None:
             dsp["_reduce"] = reduce_hook
         tags = ("lf0", "mgc", "bap", "vuv")
+        fwd_done = {}
         with Branches(x_main.device) as br:
             for i in range(4):
                 with br.on(i):
+                    if len(EXCL_BRANCHES) < 4:
+                        call("ensvs_set_recurrence_exclusive", int(i in EXCL_BRANCHES))
+                    # schedule knob: branch i starts after branch a's forward (BRANCH_AFTER)
+                    a = BRANCH_AFTER.get(i)
+                    if a is not None and a in fwd_done:
+                        torch.cuda.current_stream().wait_event(fwd_done[a])
                     self._fwd_branch(i, c, outs, st)
+                    if i in BRANCH_AFTER.values():
+                        fwd_done[i] = torch.cuda.current_stream().record_event()
                     parts[i], g = branch_loss(i, outs, st)
                     self._bwd_branch(i, st, g, dsp)
                     if reduce_hook is not None:
                         reduce_hook(tags[i])
+        if len(EXCL_BRANCHES) < 4:
+            call("ensvs_set_recurrence_exclusive", 1)
         loss = parts[0]
         for i in (1, 2, 3):
             call("ensvs_axpy", loss.data_ptr(), parts[i].data_ptr(), 1.0, 1, Ly.stream())

@@ -314,13 +314,10 @@ __global__ void downsample_wgrad_kernel(DsArgs a, const float* __restrict__ de, 
   if (threadIdx.x == 4) db[c] += red[4][0];
 }
 
-// The decoder workgroup reserves its CU's LDS (lstm.hip excl_lds; ENSVS_LSTM_EXCLUSIVE=0: off)
+// The decoder workgroup reserves its CU's LDS (lstm.hip ensvs_rec_exclusive: ENSVS_LSTM_EXCLUSIVE,
+// ensvs_set_recurrence_exclusive)
 static size_t ar_excl_lds() {
-  static const int on = [] {
-    const char* e = getenv("ENSVS_LSTM_EXCLUSIVE");
-    return e ? atoi(e) : 1;
-  }();
-  return on ? 96 * 1024 : 0;  // + the static LDS: no 64 KB GEMM workgroup fits beside it
+  return ensvs_rec_exclusive() ? 96 * 1024 : 0;  // + the static LDS: no 64 KB GEMM workgroup fits beside it
 }
 
 template <int H>

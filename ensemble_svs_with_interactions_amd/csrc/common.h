@@ -14,6 +14,7 @@
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 enum {
   ENSVS_OK = 0,
@@ -70,3 +71,6 @@ __device__ __forceinline__ float ftanh_(float x) {
 }
 
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// whether persistent recurrence workgroups reserve their CU's LDS (lstm.hip)
+int ensvs_rec_exclusive();

@@ -2733,7 +2733,11 @@ static bool use_big_tile(const GemmArgs& a) {
     if (s) g_big_stages = atoi(s);
   }
   if (!g_big_tile || a.csum || !a.vec_out || a.Npad % BNB) return false;
-  return (long long)cdiv(a.M, BMB) * (a.Npad / BNB) >= 192;
+  static const int min_tiles = [] {  // ENSVS_BIG_MIN_TILES: A/B knob of the row threshold
+    const char* e = getenv("ENSVS_BIG_MIN_TILES");
+    return e ? atoi(e) : 192;
+  }();
+  return (long long)cdiv(a.M, BMB) * (a.Npad / BNB) >= min_tiles;
 }
 
 static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, int Npad,

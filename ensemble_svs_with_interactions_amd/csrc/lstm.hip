@@ -28,6 +28,15 @@
 #include "common.h"
 #include "ensvs.h"
 
+static int g_rec_excl = -1;
+int ensvs_rec_exclusive() {  // (common.h)
+  if (g_rec_excl < 0) {
+    const char* e = getenv("ENSVS_LSTM_EXCLUSIVE");
+    g_rec_excl = e ? atoi(e) : 1;
+  }
+  return g_rec_excl;
+}
+
 namespace {
 
 // Lanes per unit (KPF forward, KPB backward; measured on MI355X at 30 x 1024 frames):
@@ -238,12 +247,19 @@ __global__ __launch_bounds__(Geo<H>::TB) void lstm_bwd_kernel(
   const int L = (int)lengths[b];
   const float* W = dir ? whh1 : whh0;
 
+  static_assert(QB % 4 == 0, "bwd K-part in quads");
   float w[UP][QB];
 #pragma unroll
   for (int k = 0; k < UP; ++k) {
 #pragma unroll
     for (int j = 0; j < QB; ++j) w[k][j] = W[(long long)(q * QB + j) * H + grp + k * HU];
     settle(w[k]);
+  }
+  // UP = 1: weight rows (j, j + 1) as v_pk_fma_f32 operand pairs
+  f32x2 w2[UP == 1 ? QB / 2 : 1];
+  if constexpr (UP == 1) {
+#pragma unroll
+    for (int j = 0; j < QB; j += 2) w2[j / 2] = f32x2{w[0][j], w[0][j + 1]};
   }
   const int f = gq * H + u;                      // this lane's gate gradient
   const int gslot = (f / QB) * G::GP + f % QB;
@@ -321,14 +337,30 @@ __global__ __launch_bounds__(Geo<H>::TB) void lstm_bwd_kernel(
       __syncthreads();
       const float* gp = gb + q * G::GP;
       // 4 chains per unit: the FMA latency, not issue, bounds one
+      // UP = 1: chains (0, 1) and (2, 3) as v_pk_fma_f32 pairs (the same fmaf sequence per
+      // chain, half the VALU issue: H = 64 548 vs 629 ns/step); UP = 2 stays scalar (its
+      // 128 weight registers leave no room for the pairs: 1 224 vs 1 180 ns/step packed)
       float p[UP][4];
+      if constexpr (UP == 2) {
 #pragma unroll
-      for (int k = 0; k < UP; ++k) p[k][0] = p[k][1] = p[k][2] = p[k][3] = 0.f;
+        for (int k = 0; k < UP; ++k) p[k][0] = p[k][1] = p[k][2] = p[k][3] = 0.f;
 #pragma unroll
-      for (int j = 0; j < QB; ++j) {
-        const float gv = gp[j];
+        for (int j = 0; j < QB; ++j) {
+          const float gv = gp[j];
 #pragma unroll
-        for (int k = 0; k < UP; ++k) p[k][j & 3] = fmaf(w[k][j], gv, p[k][j & 3]);
+          for (int k = 0; k < UP; ++k) p[k][j & 3] = fmaf(w[k][j], gv, p[k][j & 3]);
+        }
+      } else {
+        f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < QB; j += 4) {
+          a01 = __builtin_elementwise_fma(w2[j / 2], f32x2{gp[j], gp[j + 1]}, a01);
+          a23 = __builtin_elementwise_fma(w2[j / 2 + 1], f32x2{gp[j + 2], gp[j + 3]}, a23);
+        }
+        p[0][0] = a01.x;
+        p[0][1] = a01.y;
+        p[0][2] = a23.x;
+        p[0][3] = a23.y;
       }
       float dsum[UP];
 #pragma unroll
@@ -346,13 +378,10 @@ __global__ __launch_bounds__(Geo<H>::TB) void lstm_bwd_kernel(
 // Each persistent recurrence workgroup reserves its CU's whole LDS, so no GEMM workgroup
 // of a concurrent branch stream lands beside it (a co-resident GEMM stretches the
 // latency-bound step): 20.8 vs 21.3 ms per training step (profiles/r2_schedule_ab.txt).
-// ENSVS_LSTM_EXCLUSIVE=0 turns it off.  Read once.
+// ENSVS_LSTM_EXCLUSIVE=0 turns it off; ensvs_set_recurrence_exclusive switches it per
+// launch (the caller's branch schedule; read at launch, so a captured graph keeps it).
 static size_t excl_lds(size_t need) {
-  static const int on = [] {
-    const char* e = getenv("ENSVS_LSTM_EXCLUSIVE");
-    return e ? atoi(e) : 1;
-  }();
-  return on ? std::max<size_t>(need, 160 * 1024) : need;
+  return ensvs_rec_exclusive() ? std::max<size_t>(need, 160 * 1024) : need;
 }
 
 template <int H>
@@ -683,6 +712,11 @@ int step_bwd(const float* dy, int lddy, const float* w0, const float* w1, const 
 }
 
 }  // namespace
+
+ENSVS_API int ensvs_set_recurrence_exclusive(int on) {
+  g_rec_excl = on ? 1 : 0;
+  return ENSVS_OK;
+}
 
 ENSVS_API int ensvs_lstm_fwd(const float* gx, int ldg, const float* whh_f, const float* whh_r,
                              const long long* lengths, int B, int T, int H, float* y, int ldy,

@@ -82,6 +82,10 @@ int ensvs_set_dual_small(int on);
  * takes precedence over the two-K-group kernel and split-K); same accumulation order as the
  * one-group kernel, so the same bits.  0 turns it off. */
 int ensvs_set_small(int on);
+/* Persistent recurrence workgroups (LSTM, AR decoder) reserve their CU's LDS so no GEMM
+ * workgroup of a concurrent stream lands beside them (default on, ENSVS_LSTM_EXCLUSIVE);
+ * read at each launch, so a caller can choose per branch. */
+int ensvs_set_recurrence_exclusive(int on);
 /* part / part_floats (optional, may be NULL / 0): fp32 workspace for split-K.  Launches of
  * fewer than 128 output tiles (small M: the 2 000-frame reverse-diffusion GEMMs) split their
  * K-steps over up to 8 workgroups per tile when part holds ksplit x M x Npad floats; the

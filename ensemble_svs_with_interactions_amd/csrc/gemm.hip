@@ -947,8 +947,18 @@ __device__ __forceinline__ TapPtrs tap_ptrs(const SegU S, int j, int Npad, int n
   return P;
 }
 
-template <int STAGES>
-__global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a) {
+// FUSE (the uSFGAN residual block, usf_block_kernel): a is the block's gate GEMM (GATE_TS,
+// all 128 gate/filter columns in this tile), a2 its output projection (ADDSCALE on the
+// residual stream): z = tanh(gate) * sigmoid(filter) goes from the accumulators to a bf16
+// LDS image (the rounding of z's bf16 copy), the 128 x 64 output GEMM reads it there and
+// the weights from global memory, and a2's epilogue updates the residual stream -- no z
+// round trip through HBM, one launch per block instead of two.
+__device__ __forceinline__ void usf_block_tail(const GemmArgs& a, const GemmArgs& a2,
+                                               f32x4 (&acc)[4][4], char* smem, int tid, int lane,
+                                               int wr, int wc, int m0);
+
+template <int STAGES, bool FUSE>
+__device__ __forceinline__ void b16_body(const GemmArgs& a, const GemmArgs& a2) {
   static_assert(STAGES >= 2 && STAGES <= 3, "stages");
   constexpr int TILE = BM * BK2 * 2;  // bytes of one operand image (16 KB)
   constexpr int GL = 8;               // glds per thread per tile (4 A rows + 4 B rows)
@@ -1089,6 +1099,10 @@ __global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a
   }
 #undef ISSUE
 #undef TAP_PTRS
+  if constexpr (FUSE) {
+    usf_block_tail(a, a2, acc, smem, tid, lane, wr, wc, m0);
+    return;
+  }
   if (a.ksplit > 1) {  // raw partial tile of this K split
     float* pz = a.part + (long long)blockIdx.z * M * Npad;
 #pragma unroll
@@ -1105,6 +1119,15 @@ __global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a
   }
   if (a.vec_out) gemm_epilogue_lds(a, acc, m0, n0, wr, wc, lane, tid, smem);
   else gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
+}
+
+template <int STAGES>
+__global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a) {
+  b16_body<STAGES, false>(a, a);
+}
+
+__global__ __launch_bounds__(NTHR, 2) void usf_block_kernel(const GemmArgs a, const GemmArgs a2) {
+  b16_body<2, true>(a, a2);
 }
 
 // ------------------------------------------- 128 x 128, two K-groups of 4 waves (small M)
@@ -1488,6 +1511,81 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs& a, const float* T,
     }
   }
   }
+}
+
+// The fused uSFGAN block's second half (b16_body<.., true>): acc holds this wave's 64 x 64
+// part of the 128 x 128 gate/filter tile (n0 = 0: packed column group q = 2 wc + p holds the
+// gate of channels 16 q .. 16 q + 15, then their filter).
+__device__ __forceinline__ void usf_block_tail(const GemmArgs& a, const GemmArgs& a2,
+                                               f32x4 (&acc)[4][4], char* smem, int tid, int lane,
+                                               int wr, int wc, int m0) {
+  const int l16 = lane & 15, kq = lane >> 4;
+  // output-projection weight fragments straight from global memory (8 KB, L2-resident):
+  // rows n = wc*32 + 16 j + l16, k chunk h*4 + kq of the packed [Npad][Kp = 64] image
+  const __bf16* W2 = (const __bf16*)a2.W + a2.seg[0].wofs;
+  const int kp2 = a2.seg[0].Kp;
+  bf16x8 fb[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      fb[h][j] = *(const bf16x8*)(W2 + (long long)(wc * 32 + 16 * j + l16) * kp2 + h * 32 + kq * 8);
+  float bg[2] = {0.f, 0.f}, bfl[2] = {0.f, 0.f};
+  if (a.bias) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      bg[p] = a.bias[wc * 64 + p * 32 + l16];
+      bfl[p] = a.bias[wc * 64 + p * 32 + 16 + l16];
+    }
+  }
+  EpiPreT<2> pre;
+  epi_pre<64, NTHR, 2>(a2, m0, 0, tid, 0, pre);  // a2 has 64 output columns: its first batch
+  // z = tanh(g) * sigmoid(f) in bf16 into the [128][64] swizzled A image of the second GEMM
+  __syncthreads();  // every wave is done with the K loop's images
+  char* A2 = smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 64 + i * 16 + kq * 4 + r, ch = wc * 32 + p * 16 + l16;
+        const float g = acc[i][2 * p][r] + bg[p], f = acc[i][2 * p + 1][r] + bfl[p];
+        const float z = ftanh_(g) * fsigmoid_(f);
+        *(__bf16*)(A2 + row * 128 + swz(row, ch >> 3) * 16 + (ch & 7) * 2) = (__bf16)z;
+      }
+  __syncthreads();
+  // out = z W_out^T: 128 x 64, waves 2 x 2 of 64 x 32 (4 x 2 MFMA tiles), K = 64
+  f32x4 acc2[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ra = wr * 64 + l16;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bf16x8 fa[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      fa[i] = *(const bf16x8*)(A2 + (ra + 16 * i) * 128 + swz(ra, kq + 4 * h) * 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[h][j], acc2[i][j], 0, 0, 0);
+  }
+  // a2's epilogue (ADDSCALE on the residual stream + its bf16 copy) over an LDS-staged tile
+  constexpr int LT = 64 + 4;
+  float* T = (float*)(smem + 16384);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        T[(wr * 64 + i * 16 + kq * 4 + r) * LT + wc * 32 + j * 16 + l16] = acc2[i][j][r];
+  __syncthreads();
+  epilogue_tile<BM, 64, NTHR, LT, false, 2>(a2, T, m0, 0, tid, true, pre);
 }
 
 // per-lane bias of the wave's accumulator columns (nt = 0..3), added while staging
@@ -2959,6 +3057,57 @@ ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, in
     a.gate8 = a.gate8 && ((uintptr_t)ybf & 15) == 0 && ybf_ld % 8 == 0;
   }
   return launch_b16(a, segs, nseg, B, Npad, W, stages, (hipStream_t)stream);
+}
+
+// One uSFGAN residual block (usfgan/layers/residual_block.py: gated dilated / pitch-dependent
+// conv + aux conv, tanh * sigmoid, 1x1 output conv, (x + out) / sqrt 2) as one launch of
+// usf_block_kernel: segs = the gate GEMM's bf16 segments (x's copy, taps 3, optional pd; the
+// aux features' copy), W packed bf16 ([2C = 128 gate/filter columns interleaved by 16] and
+// the output conv at wofs2 as [Npad >= 64][Kp2 = 64]); x [M][ldx] fp32 updated in place,
+// xb its bf16 copy (optional).  Same bits as the two-GEMM path with a bf16 z copy.
+ENSVS_API int ensvs_usf_block(const ensvs_conv_seg* segs, int nseg, int B, int Tout,
+                              const void* W, const float* bias1, int C, long long wofs2, int Kp2,
+                              const float* bias2, float* x, int ldx, float alpha, int relu,
+                              void* xb, int xb_ld, void* stream) {
+  if (C != 64 || Kp2 != 64 || nseg < 1) return ENSVS_E_SHAPE;
+  GemmArgs a{}, a2{};
+  int rc = fill_gemm_args(a, segs, nseg, B, Tout, 2 * C, BN, W, bias1, nullptr, 0, EPI_GATE_TS, 0,
+                          0, nullptr, 0, nullptr, 0, 0.f, C);
+  if (rc != ENSVS_OK) return rc;
+  ensvs_conv_seg z{};
+  z.x = x;
+  z.ld = C;
+  z.K = C;
+  z.taps = 1;
+  z.dil = 1;
+  z.pad = PAD_ZERO;
+  z.Tin = Tout;
+  z.Kp = Kp2;
+  z.wofs = wofs2;
+  rc = fill_gemm_args(a2, &z, 1, B, Tout, 64, BN, W, bias2, x, ldx, EPI_ADDSCALE, relu, 0, nullptr,
+                      0, x, ldx, alpha, C);
+  if (rc != ENSVS_OK) return rc;
+  if (!a2.vec_out || ((uintptr_t)W & 15)) return ENSVS_E_ARG;
+  if (xb) {
+    if (xb_ld % 4 || ((uintptr_t)xb & 7)) return ENSVS_E_ARG;
+    a2.ybf = (__bf16*)xb;
+    a2.ybf_ld = xb_ld;
+  }
+  for (int s = 0; s < nseg; ++s) {  // the bf16 operand contract of launch_b16
+    const ensvs_conv_seg& g = segs[s];
+    if (g.radd || g.ld % 8 || g.ld < ((g.K + 7) & ~7) || ((uintptr_t)g.x & 15))
+      return ENSVS_E_ARG;
+    if ((long long)B * g.Tin * g.ld >= (1ll << 31) || (long long)g.taps * BN * g.Kp >= (1ll << 30))
+      return ENSVS_E_SHAPE;
+  }
+  const size_t lds = (size_t)2 * 2 * BM * BK2 * 2;  // two stages of both images (64 KB)
+  static const hipError_t e = hipFuncSetAttribute(
+      (const void*)usf_block_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(usf_block_kernel, dim3(cdiv(a.M, BM), 1), dim3(NTHR), lds,
+                     (hipStream_t)stream, a, a2);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
 }
 
 // The column sums of GemmArgs::csum for a Y written by any other path, in the same order:

@@ -233,7 +233,42 @@ __global__ void scale_cols_kernel(float* x, int ld, long long n, int C, const do
   }
 }
 
+// note[t] = score[t] > 0 (gen.py:1339-1340: GV on note frames, score = the linguistic
+// features' pitch column)
+__global__ void note_mask_kernel(const float* score, int lds, int T, unsigned char* note) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < T; t += gridDim.x * blockDim.x)
+    note[t] = score[(long long)t * lds] > 0.f ? 1 : 0;
+}
+
+// f0[t] = exp(lf0[t]), 0 where vuv[t] < thr when zero_unvoiced (gen.py:1662-1666, sine_f0_type
+// "f0"); expf: torch.exp's float32 arithmetic
+__global__ void f0_from_lf0_kernel(const float* lf0, int ldl, const float* vuv, int ldv, int T,
+                                   float thr, int zero_unvoiced, float* f0) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < T; t += gridDim.x * blockDim.x) {
+    const float e = expf(lf0[(long long)t * ldl]);
+    f0[t] = zero_unvoiced && vuv[(long long)t * ldv] < thr ? 0.f : e;
+  }
+}
+
 }  // namespace
+
+ENSVS_API int ensvs_note_mask(const float* score, int lds, int T, unsigned char* note,
+                              void* stream) {
+  if (T <= 0) return ENSVS_E_SHAPE;
+  hipLaunchKernelGGL(note_mask_kernel, dim3(cdiv(T, 256)), dim3(256), 0, (hipStream_t)stream,
+                     score, lds, T, note);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_f0_from_lf0(const float* lf0, int ldl, const float* vuv, int ldv, int T,
+                                float thr, int zero_unvoiced, float* f0, void* stream) {
+  if (T <= 0) return ENSVS_E_SHAPE;
+  hipLaunchKernelGGL(f0_from_lf0_kernel, dim3(cdiv(T, 256)), dim3(256), 0, (hipStream_t)stream,
+                     lf0, ldl, vuv, ldv, T, thr, zero_unvoiced, f0);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
 
 ENSVS_API int ensvs_scale_cols(float* x, int ld, int T, int C, const double* a, const double* b,
                                int mode, void* stream) {

@@ -349,6 +349,28 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
              int(accum), ptr(aux0), ld0, ptr(aux1), ld1, float(alpha), C, stream())
 
 
+def usf_block(segs: List[Seg], B, Tout, W: PackedBuffer, C, ref2, x, ldx, alpha, relu=False,
+              xb=None, bias=None, bias_off=0, bias2=None, bias2_off=0):
+    """One uSFGAN residual block in one launch (ensvs_usf_block): the gate GEMM over the
+    bf16 segments segs (packed 2C = 128 gate/filter columns), z on chip, the output conv
+    ref2 and x = alpha * x + out + bias2 in place (+ its bf16 copy xb).  The same bits as
+    gemm(.., EPI_GATE_TS, ybf=z copy) followed by gemm(.., EPI_ADDSCALE) on that copy."""
+    arr = (ConvSeg * len(segs))()
+    for d, sg in zip(arr, segs):
+        assert sg.x.dtype == torch.bfloat16 and sg.radd is None and sg.ref.taps == sg.taps
+        d.x = sg.x.data_ptr() + 2 * sg.xoff
+        d.ld, d.radd, d.radd_ld = sg.ld, None, 0
+        d.pd = None if sg.pd is None else sg.pd.data_ptr()
+        d.pd_dil = sg.pd_dil
+        d.wofs = sg.ref.offset
+        d.K, d.taps, d.dil, d.shift0 = sg.K, sg.taps, sg.dil, sg.shift0
+        d.pad, d.Tin, d.Kp = sg.pad, sg.Tin, sg.ref.Kp
+    call("ensvs_usf_block", ctypes.addressof(arr), len(segs), B, Tout, W.buf.data_ptr(),
+         None if bias is None else bias.data_ptr() + 4 * bias_off, C, ref2.offset, ref2.Kp,
+         None if bias2 is None else bias2.data_ptr() + 4 * bias2_off, x.data_ptr(), ldx,
+         float(alpha), int(bool(relu)), ptr(xb), 0 if xb is None else xb.shape[1], stream())
+
+
 def bf16_operands(W, M):
     """Whether GEMMs on these packed weights with M rows take pre-rounded bf16 operands
     (callers then round an operand shared by several GEMMs once, instead of per GEMM)."""

@@ -78,15 +78,40 @@ def lowpass_filter(x, fs, cutoff=5, N=5, ld=None, C=None, T=None):
     return x
 
 
+_CONST = {}
+
+
+def _dev_f64(v, device):
+    """Device fp64 copy of a host constant (scaler statistics, GV), cached by content: the
+    per-track synthesis loop would otherwise pay a pageable host-to-device copy -- a host
+    round trip -- per call."""
+    a = np.ascontiguousarray(np.asarray(v, dtype=np.float64).reshape(-1))
+    key = (a.tobytes(), str(torch.device(device)))
+    t = _CONST.get(key)
+    if t is None:
+        t = _CONST[key] = torch.from_numpy(a.copy()).to(device)
+    return t
+
+
+def note_mask(score_col, T):
+    """(T,) uint8 note-frame mask score > 0 of a device column view (ensvs_note_mask)."""
+    note = torch.empty(T, dtype=torch.uint8, device=score_col.device)
+    call("ensvs_note_mask", score_col.data_ptr(), score_col.stride(0), T, note.data_ptr(),
+         stream())
+    return note
+
+
 def variance_scaling(gv, feats, offset=2, note_mask=None):
-    """nnsvs/postfilters.py:9-46 in place on device rows feats (T, D); note_mask (T,) bool
-    (None: every frame) selects the note frames whose statistics are matched to gv."""
+    """nnsvs/postfilters.py:9-46 in place on device rows feats (T, D); note_mask (T,) bool or
+    uint8 (None: every frame) selects the note frames whose statistics are matched to gv."""
     T, D = feats.shape
     if note_mask is None:
         note = torch.ones(T, dtype=torch.uint8, device=feats.device)
+    elif note_mask.dtype == torch.uint8 and note_mask.is_contiguous():
+        note = note_mask
     else:
         note = note_mask.to(device=feats.device, dtype=torch.uint8).contiguous()
-    g = torch.as_tensor(np.asarray(gv, dtype=np.float64).reshape(-1)[:D]).to(feats.device)
+    g = _dev_f64(np.asarray(gv, dtype=np.float64).reshape(-1)[:D], feats.device)
     call("ensvs_gv_scale", feats.data_ptr(), feats.stride(0), T, D, offset, note.data_ptr(),
          g.data_ptr(), stream())
     return feats
@@ -96,8 +121,8 @@ def scale_cols(x, a, b, mode):
     """sklearn scaler arithmetic on device rows (see ensvs_scale_cols)."""
     T, C = x.shape
     dev = x.device
-    a_ = torch.as_tensor(np.asarray(a, dtype=np.float64).reshape(-1)).to(dev)
-    b_ = torch.as_tensor(np.asarray(b, dtype=np.float64).reshape(-1)).to(dev)
+    a_ = _dev_f64(a, dev)
+    b_ = _dev_f64(b, dev)
     call("ensvs_scale_cols", x.data_ptr(), x.stride(0), T, C, a_.data_ptr(), b_.data_ptr(),
          int(mode), stream())
     return x
@@ -160,11 +185,11 @@ def postprocess_acoustic(device, acoustic_features, duration_modified_labels, bi
     if pitch_idx is None:
         pitch_idx = get_pitch_index(binary_dict, numeric_dict)
     ling_t = ling if isinstance(ling, torch.Tensor) else torch.from_numpy(np.asarray(ling))
-    score = ling_t[:, pitch_idx].to(dev)
+    score = ling_t[:, pitch_idx].to(device=dev, dtype=torch.float32)
     if post_filter_type in ("gv", "nnsvs"):
         m = sizes[0]
         gv = np.asarray(acoustic_out_static_scaler.var_, dtype=np.float64).reshape(-1)[:m]
-        variance_scaling(gv, feats[:, :m], offset=2, note_mask=score > 0)
+        variance_scaling(gv, feats[:, :m], offset=2, note_mask=note_mask(score, T))
     o = np.cumsum([0] + sizes)
     lf0, vuv = feats[:, o[1]:o[2]], feats[:, o[2]:o[3]]
     shift = f0_shift_in_cent * np.log(2) / 1200 if f0_shift_in_cent != 0 else 0.0
@@ -213,7 +238,8 @@ def usfgan_inputs(mgc, lf0, vuv, bap, vocoder_in_scaler=None, sine_f0_type="f0",
         raise NotImplementedError("mel-cepstral aperiodicity (pysptk) is not in the recipe")
     if vocoder_in_scaler is not None:
         transform(vocoder_in_scaler, aux)
-    f0 = torch.exp(lf0.float())
-    if sine_f0_type == "f0":
-        f0 = torch.where(vuv < vuv_threshold, torch.zeros_like(f0), f0)
-    return f0.contiguous(), aux
+    lf0, vuv = lf0.float(), vuv.float()
+    f0 = torch.empty(T, 1, device=dev)
+    call("ensvs_f0_from_lf0", lf0.data_ptr(), lf0.stride(0), vuv.data_ptr(), vuv.stride(0), T,
+         float(vuv_threshold), int(sine_f0_type == "f0"), f0.data_ptr(), stream())
+    return f0, aux

@@ -20,6 +20,7 @@ parameter version.  The nn.Conv modules are parameter containers; their forward 
 called.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -325,6 +326,10 @@ class _Prepared:
 
 # ------------------------------------------------------------------ generator
 
+# inference blocks as one launch each (ensvs_usf_block; ENSVS_USF_FUSED=0: two GEMMs)
+FUSED_BLOCK = {"on": os.environ.get("ENSVS_USF_FUSED", "1") != "0"}
+
+
 class ParallelHnUSFGANGenerator(nn.Module):
     """usfgan/models/generator.py:359-544."""
 
@@ -448,6 +453,15 @@ class ParallelHnUSFGANGenerator(nn.Module):
                              pad=_lib.PAD_REFLECT)
             seg1 = (K.Seg(c, ldc, ldc, P.ref[key + ".aux"], L) if cb is None else
                     K.Seg(cb, cb.shape[1], Ca, P.ref[key + ".aux"], L))
+            r2 = P.ref[key + ".out"]
+            if zb is not None and FUSED_BLOCK["on"] and Gh == 64 and R == 64 and r2.Kp == 64:
+                # the whole block in one launch, z kept on chip (ensvs_usf_block)
+                b1, b2 = P.bias(key + ".g"), P.bias(key + ".out")
+                K.usf_block([seg0, seg1], B, L, P.fwd, Gh, r2, x, R, SQRT1_2,
+                            relu=relu_last and i == nb - 1, xb=xb,
+                            bias=b1.get("bias"), bias_off=b1.get("bias_off", 0),
+                            bias2=b2.get("bias"), bias2_off=b2.get("bias_off", 0))
+                continue
             K.gemm([seg0, seg1], B, L, 2 * Gh, P.fwd, z, Gh, epi=_lib.EPI_GATE_TS, C=Gh,
                    ybf=zb, ybf_ld=Gh, keep_y=zb is None, **P.bias(key + ".g"))
             K.gemm([K.Seg(z, Gh, Gh, P.ref[key + ".out"], L) if zb is None else
@@ -488,22 +502,9 @@ class ParallelHnUSFGANGenerator(nn.Module):
             call("ensvs_usf_upsample", c.data_ptr(), ldc, B, Tc, Ca, s, float(1.0 / s),
                  P.fir_taps(i).data_ptr(), nxt.data_ptr(), stream())
             c, Tc = nxt, Tc * s
-        # periodicity estimator (ReLU, ReLU, sigmoid)
-        pe = self._pe_convs()
-        pad = _PAD[self.periodicity_estimator.padding_mode]
-        a, lda, Kin = c, ldc, ldc
-        for i, m in enumerate(pe):
-            k, dl = m.kernel_size[0], m.dilation[0]
-            out = empty(M, R, device=dev)
-            K.gemm([K.Seg(a, lda, Kin, P.ref[f"pe{i}"], L, taps=k, dil=dl,
-                          shift0=-(k // 2) * dl, pad=pad)], B, L, R, P.fwd, out, R,
-                   relu=_lib.ACT_SIGMOID if i == len(pe) - 1 else _lib.ACT_RELU,
-                   **P.bias(f"pe{i}"))
-            a, lda, Kin = out, R, R
-        h = empty(M, R, device=dev)
-        n = empty(M, R, device=dev)
         # inference with bf16 operands: the residual streams' bf16 copies ride along in the
         # epilogues, the auxiliary features are rounded once (zero K padding) for all blocks
+        # and the periodicity estimator
         b16 = not keep and K.bf16_operands(P.fwd, M)
         hb = nb_ = cb = zb = None
         if b16:
@@ -512,6 +513,24 @@ class ParallelHnUSFGANGenerator(nn.Module):
             zb = empty(M, Gh, device=dev, dtype=torch.bfloat16)
             cb = empty(M, -(-Ca // 8) * 8, device=dev, dtype=torch.bfloat16)
             K.cast_bf16(c, ldc, Ca, M, out=cb, out_ld=cb.shape[1])
+        # periodicity estimator (ReLU, ReLU, sigmoid); bf16: each conv's epilogue writes the
+        # next one's operand copy
+        pe = self._pe_convs()
+        pad = _PAD[self.periodicity_estimator.padding_mode]
+        a, lda, Kin = (c, ldc, ldc) if cb is None else (cb, cb.shape[1], Ca)
+        for i, m in enumerate(pe):
+            k, dl = m.kernel_size[0], m.dilation[0]
+            out = empty(M, R, device=dev)
+            last = i == len(pe) - 1
+            ob = empty(M, R, device=dev, dtype=torch.bfloat16) if b16 and not last else None
+            K.gemm([K.Seg(a, lda, Kin, P.ref[f"pe{i}"], L, taps=k, dil=dl,
+                          shift0=-(k // 2) * dl, pad=pad)], B, L, R, P.fwd, out, R,
+                   relu=_lib.ACT_SIGMOID if last else _lib.ACT_RELU, ybf=ob, ybf_ld=R,
+                   **P.bias(f"pe{i}"))
+            a, lda, Kin = (out, R, R) if ob is None else (ob, R, R)
+        a = out
+        h = empty(M, R, device=dev)
+        n = empty(M, R, device=dev)
         K.gemm([K.Seg(xsrc, 2, 1, P.ref["first_sine"], L)], B, L, R, P.fwd, h, R,
                ybf=hb, ybf_ld=R, **P.bias("first_sine"))
         K.gemm([K.Seg(xsrc, 2, 1, P.ref["first_noise"], L, xoff=1)], B, L, R, P.fwd, n, R,

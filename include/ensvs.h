@@ -86,6 +86,15 @@ int ensvs_set_small(int on);
  * workgroup of a concurrent stream lands beside them (default on, ENSVS_LSTM_EXCLUSIVE);
  * read at each launch, so a caller can choose per branch. */
 int ensvs_set_recurrence_exclusive(int on);
+/* One uSFGAN residual block in one launch (usfgan/layers/residual_block.py): the gate GEMM
+ * over bf16 segments (x's copy with taps 3 / optional pd, the aux features' copy; packed
+ * gate/filter columns interleaved by 16, 2C = 128), z = tanh(gate) * sigmoid(filter) kept on
+ * chip in bf16, the 1x1 output conv (packed at wofs2, Kp2 = 64) and
+ * x = alpha * x + out + bias2 (ReLU when relu) in place, with x's bf16 copy in xb (optional).
+ * C = 64.  Same bits as the gate GEMM with a bf16 z copy followed by the output GEMM. */
+int ensvs_usf_block(const ensvs_conv_seg* segs, int nseg, int B, int Tout, const void* W,
+                    const float* bias1, int C, long long wofs2, int Kp2, const float* bias2,
+                    float* x, int ldx, float alpha, int relu, void* xb, int xb_ld, void* stream);
 /* part / part_floats (optional, may be NULL / 0): fp32 workspace for split-K.  Launches of
  * fewer than 128 output tiles (small M: the 2 000-frame reverse-diffusion GEMMs) split their
  * K-steps over up to 8 workgroups per tile when part holds ksplit x M x Npad floats; the
@@ -445,6 +454,12 @@ int ensvs_filtfilt(float* x, int ld, int T, int C, const double* ba, int nb, con
 /* bap clip [-60, 0] (gen.py:1520-1522) and the WORLD aperiodicity codec round trip before
  * uSFGAN (gen.py:1649-1670). */
 int ensvs_bap_post(float* bap, int ld, int T, int D, int clip, int codec, void* stream);
+/* note[t] = score[t * lds] > 0: the note frames of the GV post-filter (gen.py:1339-1340). */
+int ensvs_note_mask(const float* score, int lds, int T, unsigned char* note, void* stream);
+/* f0[t] = exp(lf0[t * ldl]), 0 where vuv[t * ldv] < thr when zero_unvoiced: the uSFGAN sine
+ * source F0 (gen.py:1662-1666). */
+int ensvs_f0_from_lf0(const float* lf0, int ldl, const float* vuv, int ldv, int T, float thr,
+                      int zero_unvoiced, float* f0, void* stream);
 /* sklearn scaler arithmetic in place (float32 data, float64 statistics a, b per column):
  * mode 0 x = x*a + b (StandardScaler.inverse_transform, gen.py:1299; MinMaxScaler.transform),
  * mode 1 x = (x - b)/a (StandardScaler.transform: the vocoder input scaler, gen.py:1678-1684). */

@@ -12,6 +12,7 @@ import torch
 
 from ensemble_svs_with_interactions_amd import _lib, configs, engine
 from ensemble_svs_with_interactions_amd import kernels as K
+from ensemble_svs_with_interactions_amd import usfgan
 from ensemble_svs_with_interactions_amd.usfgan import USFGANWrapper
 from golden_util import load_case, params_from_shapes, rel, rel_l2
 
@@ -146,9 +147,9 @@ def test_bf16_generator():
 def test_bf16_operand_copies_bitwise():
     """Inference on bf16 operand copies (the residual streams' copies from the output-GEMM
     epilogues, the zero-padded auxiliary features rounded once, z in bf16 only, the
-    pitch-dependent gather on the bf16 copy) = the register-staged kernels that round the
-    fp32 operands while staging: identical waveform bits, full-size generator (bench config),
-    two tracks."""
+    pitch-dependent gather on the bf16 copy), with two GEMMs per block and with the fused
+    one-launch block, = the register-staged kernels that round the fp32 operands while
+    staging: identical waveform bits, full-size generator (bench config), two tracks."""
     engine.set_gemm_precision("bf16")
     saved = dict(K.BF16_ACT)
     try:
@@ -165,13 +166,16 @@ def test_bf16_operand_copies_bitwise():
         g = torch.Generator(device="cuda").manual_seed(4)
         nz = [torch.randn(2, L, device="cuda", generator=g) for _ in range(2)]
         outs = []
-        for on in (False, True):
+        for on, fused in ((False, False), (True, False), (True, True)):
             K.BF16_ACT.update(on=on)
+            usfgan.FUSED_BLOCK["on"] = fused
             outs.append(wr.inference_batch(f0, aux, noises=nz))
             torch.cuda.synchronize()
-        assert torch.isfinite(outs[1]).all()
-        assert torch.equal(outs[0], outs[1])
+        assert torch.isfinite(outs[2]).all()
+        assert torch.equal(outs[0], outs[1])  # bf16 operand copies, two GEMMs per block
+        assert torch.equal(outs[0], outs[2])  # one launch per block (ensvs_usf_block)
     finally:
         K.BF16_ACT.clear()
         K.BF16_ACT.update(saved)
+        usfgan.FUSED_BLOCK["on"] = True
         engine.set_gemm_precision("fp32")

@@ -4,7 +4,8 @@ weight-gradient shape that issued it; aggregated by (entry point, shape), larges
 first.   python tools/census.py [rows] [synth]
 synth: the mgc DiffNet's 100-step reverse diffusion of one (main, sub) pair at 2 000 frames
 (eager, the launches the inference graph captures) instead of the training step; voc: one
-uSFGAN generator pass over one 2 000-frame track (480 000 samples).
+uSFGAN generator pass over one 2 000-frame track (480 000 samples); post: the bench's
+per-track post-acoustic processing and uSFGAN inputs of one 2 000-frame track.
 """
 import collections
 import os
@@ -20,6 +21,7 @@ from ensemble_svs_with_interactions_amd.train import FusedAdam, train_step  # no
 ROWS = int(sys.argv[1]) if len(sys.argv) > 1 else 45
 SYNTH = len(sys.argv) > 2 and sys.argv[2] == "synth"
 VOC = len(sys.argv) > 2 and sys.argv[2] == "voc"
+POST = len(sys.argv) > 2 and sys.argv[2] == "post"
 REC = []
 TAG = [None]
 ON = [False]
@@ -103,9 +105,41 @@ def run_voc(dev):
     ON[0] = False
 
 
+def run_post(dev):
+    import types
+    import numpy as np
+    from ensemble_svs_with_interactions_amd import postprocess, scalers
+    T = 2000
+    b = data.synthetic_batch(1, T, 5)
+    xm = torch.from_numpy(b["x_main"]).to(dev)[0]
+    feats = torch.randn(T, 67, device=dev)
+    mean_, var_ = np.zeros(67), np.full(67, 0.25)
+    sc = scalers.StandardScaler(mean_, var_)
+    cfg = types.SimpleNamespace(stream_sizes=[60, 1, 1, 5], num_windows=1,
+                                has_dynamic_features=[False] * 4)
+    post = dict(frame_period=5, post_filter_type="gv", trajectory_smoothing=True,
+                trajectory_smoothing_cutoff=50, trajectory_smoothing_cutoff_f0=20,
+                vuv_threshold=0.3)
+
+    def one():
+        f = feats.clone()
+        postprocess.inverse_transform(sc, f)
+        st = postprocess.postprocess_acoustic(dev, f, xm, {}, {}, cfg, sc, pitch_idx=51, **post)
+        postprocess.usfgan_inputs(*st, sine_f0_type="f0", vuv_threshold=0.3)
+    one()
+    torch.cuda.synchronize()
+    ON[0] = True
+    one()
+    torch.cuda.synchronize()
+    ON[0] = False
+
+
 def main():
     dev = torch.device("cuda")
     engine.set_concurrency(False)
+    if POST:
+        run_post(dev)
+        return report()
     if VOC:
         run_voc(dev)
         return report()
@@ -140,7 +174,7 @@ def report():
         a[1] += ms
         tot += ms
     print(f"{len(REC)} launches, {tot:.2f} ms (event-bracketed, serial eager "
-          f"{'reverse diffusion' if SYNTH else ('vocoder' if VOC else 'step')})")
+          f"{'reverse diffusion' if SYNTH else ('vocoder' if VOC else ('post' if POST else 'step'))})")
     for (name, tag), (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:ROWS]:
         print(f"{ms:8.3f} ms {n:4d}x {ms / n * 1e3:8.1f} us  {name:28s} {tag or ''}")
 

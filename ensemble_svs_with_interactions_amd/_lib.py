@@ -70,6 +70,8 @@ SIGNATURES = {
     "ensvs_set_small": [c_int],
     "ensvs_set_recurrence_exclusive": [c_int],
     "ensvs_note_mask": [c_vp, c_int, c_int, c_vp, c_vp],
+    "ensvs_filtfilt_multi": [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                             c_vp, c_vp],
     "ensvs_f0_from_lf0": [c_vp, c_int, c_vp, c_int, c_int, c_float, c_int, c_vp, c_vp],
     "ensvs_usf_block": [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_ll, c_int, c_vp, c_vp,
                         c_int, c_float, c_int, c_vp, c_int, c_vp],

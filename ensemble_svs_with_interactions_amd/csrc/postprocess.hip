@@ -188,6 +188,110 @@ __global__ void filtfilt_kernel(float* x, int ld, int T, int C, const double* ba
   for (int t = 0; t < T; ++t) x[(long long)t * ld + c] = (float)e[padlen + t];
 }
 
+// The same filter for a compile-time coefficient count NB (the order-5 Butterworth of the
+// recipe: NB = 6): state and coefficients in registers, the extended signal streamed through
+// registers 16 samples at a time with the next chunk's loads issued before the current
+// chunk's recursion -- the generic kernel keeps z in scratch (runtime-indexed) and pays a
+// dependent memory round trip per sample (3.1 ms per call at T = 2 000).  The per-sample
+// arithmetic is the generic kernel's, term for term (contraction off): the same bits.
+// Up to 4 column groups of one feature matrix, each with its own filter, in one launch
+// (blockIdx.y): the post-filter's lf0 / mgc / bap smoothing calls are independent and each
+// is a latency-bound recursion on a few lanes, so they run side by side.
+struct FFGroup {
+  float* x;             // first column of the group
+  const double* ba;     // b then a (NB each)
+  const double* zi;     // lfilter_zi (NB - 1)
+  double* work;         // C x (T + 2 padlen)
+  int C, padlen, guard;
+};
+struct FFGroups {
+  FFGroup g[4];
+};
+
+template <int NB>
+__global__ void filtfilt_nb_kernel(FFGroups gs, int ld, int T) {
+#pragma clang fp contract(off)
+  constexpr int CH = 16;
+  const FFGroup& G = gs.g[blockIdx.y];
+  float* x = G.x;
+  const double* ba = G.ba;
+  const double* zi = G.zi;
+  double* work = G.work;
+  const int C = G.C, padlen = G.padlen, guard = G.guard;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C || T <= guard) return;
+  double b[NB], a[NB], zi0[NB - 1];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    b[k] = ba[k];
+    a[k] = ba[NB + k];
+  }
+#pragma unroll
+  for (int k = 0; k < NB - 1; ++k) zi0[k] = zi[k];
+  const int n = T + 2 * padlen;
+  double* e = work + (long long)c * n;  // the forward pass's output
+  const float x0 = x[c], xl = x[(long long)(T - 1) * ld + c];
+  // sample i of the odd extension (evaluated in float32, as scipy's odd_ext on float input)
+  auto ext = [&](int i) -> double {
+    if (i < padlen) return (double)(2.f * x0 - x[(long long)(padlen - i) * ld + c]);
+    if (i < padlen + T) return (double)x[(long long)(i - padlen) * ld + c];
+    return (double)(2.f * xl - x[(long long)(T - 2 - (i - padlen - T)) * ld + c]);
+  };
+  // pass 0 reads the extension and writes e; pass 1 reads e backwards and writes the
+  // trimmed result into x (the generic kernel's values, without its two copy loops)
+#define FF_STEP(XI, Y)                                                                    \
+  do {                                                                                    \
+    const double xi_ = (XI);                                                              \
+    Y = z[0] + b[0] * xi_;                                                                \
+    _Pragma("unroll") for (int k = 0; k < NB - 2; ++k)                                    \
+      z[k] = z[k + 1] + xi_ * b[k + 1] - Y * a[k + 1];                                    \
+    z[NB - 2] = xi_ * b[NB - 1] - Y * a[NB - 1];                                          \
+  } while (0)
+  double z[NB - 1], cur[CH], nxt[CH];
+  {
+    const double s = ext(0);
+#pragma unroll
+    for (int k = 0; k < NB - 1; ++k) z[k] = zi0[k] * s;
+#pragma unroll
+    for (int q = 0; q < CH; ++q) cur[q] = q < n ? ext(q) : 0.0;
+    for (int j0 = 0; j0 < n; j0 += CH) {
+#pragma unroll
+      for (int q = 0; q < CH; ++q) nxt[q] = j0 + CH + q < n ? ext(j0 + CH + q) : 0.0;
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        if (j0 + q >= n) break;
+        double y;
+        FF_STEP(cur[q], y);
+        e[j0 + q] = y;
+      }
+#pragma unroll
+      for (int q = 0; q < CH; ++q) cur[q] = nxt[q];
+    }
+  }
+  {
+    const double s = e[n - 1];
+#pragma unroll
+    for (int k = 0; k < NB - 1; ++k) z[k] = zi0[k] * s;
+#pragma unroll
+    for (int q = 0; q < CH; ++q) cur[q] = q < n ? e[n - 1 - q] : 0.0;
+    for (int j0 = 0; j0 < n; j0 += CH) {
+#pragma unroll
+      for (int q = 0; q < CH; ++q) nxt[q] = j0 + CH + q < n ? e[n - 1 - (j0 + CH + q)] : 0.0;
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        if (j0 + q >= n) break;
+        double y;
+        FF_STEP(cur[q], y);
+        const int t = n - 1 - (j0 + q) - padlen;
+        if (t >= 0 && t < T) x[(long long)t * ld + c] = (float)y;
+      }
+#pragma unroll
+      for (int q = 0; q < CH; ++q) cur[q] = nxt[q];
+    }
+  }
+#undef FF_STEP
+}
+
 // bap clip to [-60, 0] (gen.py:1520-1522, band aperiodicity only) and the WORLD codec round
 // trip of predict_waveform's uSFGAN branch (gen.py:1649-1670): DecodeAperiodicity turns a
 // frame whose mean coded aperiodicity exceeds -0.5 into all (1 - 1e-12) (WORLD d4c.cpp
@@ -303,8 +407,35 @@ ENSVS_API int ensvs_filtfilt(float* x, int ld, int T, int C, const double* ba, i
                              void* stream) {
   if (T <= 0 || C <= 0 || nb < 2 || nb > 17) return ENSVS_E_SHAPE;
   if (T > guard && T <= padlen) return ENSVS_E_SHAPE;  // filtfilt's own length check
-  hipLaunchKernelGGL(filtfilt_kernel, dim3(cdiv(C, 64)), dim3(64), 0, (hipStream_t)stream, x, ld,
-                     T, C, ba, nb, zi, padlen, guard, work);
+  if (nb == 6) {
+    FFGroups gs{};
+    gs.g[0] = {x, ba, zi, work, C, padlen, guard};
+    hipLaunchKernelGGL(filtfilt_nb_kernel<6>, dim3(cdiv(C, 64), 1), dim3(64), 0,
+                       (hipStream_t)stream, gs, ld, T);
+  } else
+    hipLaunchKernelGGL(filtfilt_kernel, dim3(cdiv(C, 64)), dim3(64), 0, (hipStream_t)stream, x,
+                       ld, T, C, ba, nb, zi, padlen, guard, work);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+// ngroups (<= 4) independent ensvs_filtfilt calls on columns of one matrix (row stride ld, T
+// rows) in one launch: group i filters cols[i] .. cols[i] + C[i] - 1 of x with ba[i] / zi[i]
+// (nb = 6: order-5 Butterworth), workspace work[i] (C[i] x (T + 2 padlen[i]) doubles).
+ENSVS_API int ensvs_filtfilt_multi(float* x, int ld, int T, int ngroups, const int* cols,
+                                   const int* C, const double* const* ba, const double* const* zi,
+                                   const int* padlen, const int* guard, double* const* work,
+                                   void* stream) {
+  if (T <= 0 || ngroups < 1 || ngroups > 4) return ENSVS_E_SHAPE;
+  FFGroups gs{};
+  int cmax = 1;
+  for (int i = 0; i < ngroups; ++i) {
+    if (C[i] <= 0 || (T > guard[i] && T <= padlen[i])) return ENSVS_E_SHAPE;
+    gs.g[i] = {x + cols[i], ba[i], zi[i], work[i], C[i], padlen[i], guard[i]};
+    cmax = std::max(cmax, C[i]);
+  }
+  hipLaunchKernelGGL(filtfilt_nb_kernel<6>, dim3(cdiv(cmax, 64), ngroups), dim3(64), 0,
+                     (hipStream_t)stream, gs, ld, T);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }

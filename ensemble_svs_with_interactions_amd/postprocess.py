@@ -16,6 +16,8 @@ labels with nnmnkwii (fe.linguistic_features), which this image does not have; h
 Filter design (scipy.signal.butter / lfilter_zi, a handful of float64 coefficients) runs on
 the host once per cutoff.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -198,16 +200,38 @@ def postprocess_acoustic(device, acoustic_features, duration_modified_labels, bi
          float(shift), work.data_ptr(), stream())
     if trajectory_smoothing:
         modfs = int(1 / (frame_period * 0.001))
-        _lp_cols(feats, o[1], sizes[1], T, D, modfs, trajectory_smoothing_cutoff_f0)
-        _lp_cols(feats, o[0], sizes[0], T, D, modfs, trajectory_smoothing_cutoff)
-        _lp_cols(feats, o[3], sizes[3], T, D, modfs, trajectory_smoothing_cutoff)
+        _lp_cols_multi(feats, [(o[1], sizes[1], trajectory_smoothing_cutoff_f0),
+                               (o[0], sizes[0], trajectory_smoothing_cutoff),
+                               (o[3], sizes[3], trajectory_smoothing_cutoff)], T, D, modfs)
     if not sizes[3] > 5:  # use_mcep_aperiodicity (gen.py:1519-1522)
         call("ensvs_bap_post", feats.data_ptr() + 4 * int(o[3]), D, T, sizes[3], 1, 0, stream())
     return tuple(feats[:, o[i]:o[i + 1]] for i in range(4))
 
 
-def _lp_cols(feats, c0, C, T, D, fs, cutoff):
-    ba, zi, nb, guard = _filter(fs, cutoff, 5, feats.device)
+def _lp_cols_multi(feats, groups, T, D, fs):
+    """lowpass of several column groups (c0, C, cutoff) of feats in one launch (independent
+    filters: ensvs_filtfilt_multi); falls back to one call per group off the nb = 6 path."""
+    flt = [(c0, C) + _filter(fs, cutoff, 5, feats.device) for c0, C, cutoff in groups]
+    flt = [f for f in flt if T > f[5]]  # (guard: the reference's own length check)
+    if not flt:
+        return
+    if any(f[4] != 6 for f in flt):
+        for c0, C, ba, zi, nb, guard in flt:
+            _lp_cols(feats, c0, C, T, D, fs, None, (ba, zi, nb, guard))
+        return
+    n = len(flt)
+    works = [torch.empty(C * (T + 2 * 3 * nb), dtype=torch.float64, device=feats.device)
+             for c0, C, ba, zi, nb, guard in flt]
+    I = ctypes.c_int * n
+    P = ctypes.c_void_p * n
+    call("ensvs_filtfilt_multi", feats.data_ptr(), D, T, n, I(*[int(f[0]) for f in flt]),
+         I(*[int(f[1]) for f in flt]), P(*[f[2].data_ptr() for f in flt]),
+         P(*[f[3].data_ptr() for f in flt]), I(*[3 * f[4] for f in flt]),
+         I(*[f[5] for f in flt]), P(*[w.data_ptr() for w in works]), stream())
+
+
+def _lp_cols(feats, c0, C, T, D, fs, cutoff, flt=None):
+    ba, zi, nb, guard = flt if flt is not None else _filter(fs, cutoff, 5, feats.device)
     if T <= guard:
         return
     padlen = 3 * nb

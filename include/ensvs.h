@@ -451,6 +451,12 @@ int ensvs_world_lf0(float* lf0, int ldl, const float* vuv, int ldv, int T, float
  * when T <= guard.  work: C * (T + 2 padlen) doubles. */
 int ensvs_filtfilt(float* x, int ld, int T, int C, const double* ba, int nb, const double* zi,
                    int padlen, int guard, double* work, void* stream);
+/* ngroups (<= 4) ensvs_filtfilt calls with nb = 6 on column groups of one matrix, in one
+ * launch: group i filters columns cols[i] .. cols[i] + C[i] - 1 with ba[i], zi[i], padlen[i],
+ * guard[i] and workspace work[i] (the post-filter's independent lf0 / mgc / bap smoothing). */
+int ensvs_filtfilt_multi(float* x, int ld, int T, int ngroups, const int* cols, const int* C,
+                         const double* const* ba, const double* const* zi, const int* padlen,
+                         const int* guard, double* const* work, void* stream);
 /* bap clip [-60, 0] (gen.py:1520-1522) and the WORLD aperiodicity codec round trip before
  * uSFGAN (gen.py:1649-1670). */
 int ensvs_bap_post(float* bap, int ld, int T, int D, int clip, int codec, void* stream);

@@ -2816,8 +2816,10 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
 static int g_big_tile = -1, g_big_stages = 5;
 // split-K fills about this many workgroups (ENSVS_SPLITK=0 turns it off)
 static const int SPLITK_TARGET = 256;
-// launches of fewer than 128 tiles of 128 x 128 run the two-K-group kernel (-1: not read
-// yet; ENSVS_DUAL_SMALL, default 1; ensvs_set_dual_small)
+// launches of fewer than 128 tiles of 128 x 128 that the 64 x 64 kernel does not take (no
+// 16-B epilogue rows) run the two-K-group kernel when on (-1: not read yet; ENSVS_DUAL_SMALL,
+// default 0 since the 64 x 64 kernel: the one-group kernel keeps the register-staged bits,
+// e.g. the DiffNet output projection's 5-column rows; ensvs_set_dual_small)
 static int g_dual_small = -1;
 // launches of fewer than 128 tiles of 128 x 128 run the 64 x 64-tile kernel (-1: not read yet;
 // ENSVS_SMALL, default 1; ensvs_set_small); it takes precedence over split-K and dual
@@ -2945,7 +2947,7 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
   if (a.ksplit > 1) grid.z = a.ksplit;
   if (g_dual_small < 0) {
     const char* e = getenv("ENSVS_DUAL_SMALL");
-    g_dual_small = e ? atoi(e) : 1;
+    g_dual_small = e ? atoi(e) : 0;
   }
   if (g_dual_small && !has_pd && a.ksplit <= 1 && !a.csum &&
       (long long)grid.x * grid.y < 128) {

@@ -205,8 +205,9 @@ def set_small(on):
 
 
 def set_dual_small(on):
-    """Small-M bf16-operand launches (< 128 tiles) on the two-K-group kernel (default) or
-    the one-group kernel (the register-staged kernel's bits)."""
+    """Small-M bf16-operand launches (< 128 tiles) that the 64 x 64 kernel does not take on
+    the two-K-group kernel, or on the one-group kernel (default: the register-staged
+    kernel's bits)."""
     _lib.call("ensvs_set_dual_small", int(bool(on)))
 
 

@@ -72,10 +72,10 @@ int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N
  * (3..5; 0 keeps the current count); 2: 64-deep two-stage kernel.  Defaults: ENSVS_BIG_TILE
  * (2), ENSVS_BIG_STAGES (5). */
 int ensvs_set_big_tile(int mode, int stages);
-/* Launches of fewer than 128 output tiles (small M) run a 128 x 128 kernel with two K-groups
- * of 4 waves (each group half of the K-steps, tiles added through LDS; default on,
- * ENSVS_DUAL_SMALL); 0 keeps them on the one-group kernel (the same bits as the register-
- * staged kernel). */
+/* Launches of fewer than 128 output tiles (small M) that the 64 x 64 kernel does not take
+ * can run a 128 x 128 kernel with two K-groups of 4 waves (each group half of the K-steps,
+ * tiles added through LDS; ENSVS_DUAL_SMALL, default off: the one-group kernel, the same
+ * bits as the register-staged kernel). */
 int ensvs_set_dual_small(int on);
 /* Launches of fewer than 128 output tiles of 128 x 128 (small M: the 2 000-frame reverse-
  * diffusion GEMMs) run a 64 x 64-tile kernel that fills the chip (default on, ENSVS_SMALL; it

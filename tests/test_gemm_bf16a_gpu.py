@@ -38,7 +38,7 @@ def _both(run):
         K.BF16_ACT.clear()
         K.BF16_ACT.update(saved)
         K.SPLITK["on"] = split
-        K.set_dual_small(True)
+        K.set_dual_small(False)
     return outs
 
 
@@ -187,16 +187,17 @@ def _close(a, b, rtol):
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item() < rtol
 
 
+@pytest.mark.parametrize("C", [256, 128])
 @pytest.mark.parametrize("epi", [L.EPI_PLAIN, L.EPI_GATE, "gate_bf16", L.EPI_RESSKIP,
                                  L.EPI_GATE_BWD, L.EPI_ADDSCALE, L.EPI_RELU_MASK])
-def test_splitk_and_dual_match_unsplit(epi):
+def test_splitk_and_dual_match_unsplit(epi, C):
     """Small-M launches (2 x 1002 frames: 64 tiles, 16 K-steps): the 64 x 64-tile kernel (the
     default) bit-identical to the one-group kernel; the two-K-group kernel and split-K (4 K
     splits): the same results as the one-group kernel up
     to fp32 summation order (rel 1e-5; bf16 copies within one bf16 rounding), every epilogue
     and bf16 output copy, and bit-identical from run to run."""
     torch.manual_seed(21)
-    B, T, C, E = 2, 1002, 256, 256
+    B, T, E = 2, 1002 if C == 256 else 252, C
     M, N = B * T, 2 * C
     x = torch.randn(M, C, device=DEV).to(torch.bfloat16)
     cond = torch.randn(M, E, device=DEV).to(torch.bfloat16)
@@ -248,7 +249,7 @@ def test_splitk_and_dual_match_unsplit(epi):
         spl = [run(), run()]
     finally:
         K.SPLITK["on"] = split
-        K.set_dual_small(True)
+        K.set_dual_small(False)
         K.set_small(True)
     # the 64 x 64-tile kernel: the one-group kernel's accumulation order, identical bits
     for t0, t1 in zip(ref, small):
@@ -259,3 +260,37 @@ def test_splitk_and_dual_match_unsplit(epi):
         assert _close(y1, y0, 1e-5)
         assert _close(a1, a0, 1e-2 if a0.dtype == torch.bfloat16 else 1e-5)
         assert _close(b1.float(), b0.float(), 1e-2)
+
+
+@pytest.mark.parametrize("N", [5, 60, 128, 256])
+@pytest.mark.parametrize("relu", [False, True])
+def test_small_kernel_ragged_n_bitwise(N, relu):
+    """The 64 x 64 kernel (small M, and N <= 64 at any M) against the one-group 128 x 128
+    kernel: identical bits for ragged N (N = 5: a scalar epilogue column) with a bf16 copy
+    of the output, 2 x 252 rows (tiles across the sequence boundary)."""
+    torch.manual_seed(N)
+    B, T, Kc = 2, 252, 128
+    M = B * T
+    x = torch.randn(M, Kc, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, Kc, 1, device=DEV) / Kc ** 0.5
+    pb, (r,) = _pack([w])
+    bias = torch.randn(N, device=DEV)
+
+    def run():
+        y = torch.full((M, N), 7.0, device=DEV)
+        yb = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+        kw = dict(ybf=yb, ybf_ld=N) if N % 4 == 0 else {}
+        K.gemm([K.Seg(x, Kc, Kc, r, T)], B, T, N, pb, y, N, bias=bias, relu=relu, **kw)
+        torch.cuda.synchronize()
+        return y, yb
+    try:
+        K.set_small(False)
+        K.set_dual_small(False)
+        ref = run()
+        K.set_small(True)
+        got = run()
+    finally:
+        K.set_small(True)
+        K.set_dual_small(False)
+    assert torch.equal(ref[0], got[0])
+    assert torch.equal(ref[1], got[1])

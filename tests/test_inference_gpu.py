@@ -61,3 +61,43 @@ def test_model_inference_tiny_matches_reference(T):
     ref = a[f"T{T}::out"]
     assert tuple(out.shape) == tuple(meta[f"T{T}"]["out_shape"])
     assert rel(out.cpu(), ref) < 1e-3
+
+
+@pytest.mark.parametrize("which", ["mgc_model", "bap_model"])
+def test_bf16_reverse_operand_copies_bitwise(which):
+    """Production precision: the reverse process on bf16 operand copies (x_t's zero-padded
+    copy from p_sample, the condition rounded once, the input / skip projections' copies from
+    their epilogues) and the 64 x 64 small-M kernel = the register-staged kernels that round
+    the fp32 operands while staging, bit for bit; eager = graph replay.  Full-size denoiser,
+    two sequences of 252 frames (one ragged), K + 1 replayed draws."""
+    from ensemble_svs_with_interactions_amd import kernels as K
+    engine.set_gemm_precision("bf16")
+    saved = dict(K.BF16_ACT)
+    try:
+        torch.manual_seed(3)
+        cfg = configs.multitrack_diffusion(num_speakers=4)[which]
+        gd = build(cfg, full_shapes(), which + ".").eval()
+        from ensemble_svs_with_interactions_amd import data
+        B, T = 2, 252
+        b = data.synthetic_batch(B, T, 17)
+        x = torch.from_numpy(b["x_main"]).cuda()
+        D = cfg["encoder"]["in_dim"]  # the features + the predicted log-F0 column(s)
+        cond = torch.cat([x, 0.1 * torch.randn(B, T, D - x.shape[2], device="cuda")], 2)
+        cond = cond.contiguous()
+        spk = 0.1 * torch.randn(B, cfg["encoder"]["embed_dim"], device="cuda")
+        lens = torch.tensor([T, T - 40], device="cuda")
+        src = [(cond.view(B * T, D), D, 0, D)]
+        nz = torch.randn(gd.K_step + 1, B * T, gd.out_dim, device="cuda")
+        outs = []
+        for on, graph in ((False, False), (True, False), (True, True)):
+            K.BF16_ACT.update(on=on)
+            outs.append(gd._inference(src, B, T, lens, spk, spk.shape[1], noises=nz,
+                                      graph=graph))
+            torch.cuda.synchronize()
+        assert torch.isfinite(outs[1]).all()
+        assert torch.equal(outs[0], outs[1])
+        assert torch.equal(outs[1], outs[2])
+    finally:
+        K.BF16_ACT.clear()
+        K.BF16_ACT.update(saved)
+        engine.set_gemm_precision("fp32")

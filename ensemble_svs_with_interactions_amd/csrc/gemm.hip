@@ -2813,7 +2813,7 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
 // g_big_stages stages (ENSVS_BIG_STAGES, default 5), 2 the 64-deep two-stage kernel.
 // Gate GEMM (tools/gate_probe.py): 2 -> 44.8 us, 1 (5 / 4 / 3 stages) -> 53.3 / 53.0 /
 // 50.2 us, 0 (128 x 128) -> 51.0 us: more LDS stages in flight did not pay.
-static int g_big_tile = -1, g_big_stages = 5;
+static int g_big_tile = -1, g_big_stages = 5, g_big_all = 0;
 // split-K fills about this many workgroups (ENSVS_SPLITK=0 turns it off)
 static const int SPLITK_TARGET = 256;
 // launches of fewer than 128 tiles of 128 x 128 that the 64 x 64 kernel does not take (no
@@ -2837,6 +2837,24 @@ static bool use_big_tile(const GemmArgs& a) {
     const char* e = getenv("ENSVS_BIG_MIN_TILES");
     return e ? atoi(e) : 192;
   }();
+  // Only the gate GEMMs (K = 1 024) take the 256 x 256 kernel: the DiffNet res/skip GEMM
+  // (K = 256, an epilogue reading the residual and skip rows) runs 47 vs 55 us per launch on
+  // 128 x 128 tiles, the other wide launches (N = 512 plain / ReLU-mask, K = 256-512) 39 vs
+  // 46 and 62 vs 71 us; step 20.1 vs 20.75 ms (profiles/r2_schedule_ab.txt).
+  // ENSVS_BIG_RESSKIP=1 / ENSVS_BIG_OTHER=1 route them back (A/B knobs).
+  // (ensvs_set_big_tile mode 3: every eligible launch, as before -- the bitwise tests)
+  static const int big_resskip = [] {
+    const char* e = getenv("ENSVS_BIG_RESSKIP");
+    return e ? atoi(e) : 0;
+  }();
+  static const int big_other = [] {
+    const char* e = getenv("ENSVS_BIG_OTHER");
+    return e ? atoi(e) : 0;
+  }();
+  if (!g_big_all) {
+    if (a.epi == EPI_RESSKIP && !big_resskip) return false;
+    if (!big_other && a.epi != EPI_GATE && a.epi != EPI_RESSKIP) return false;
+  }
   return (long long)cdiv(a.M, BMB) * (a.Npad / BNB) >= min_tiles;
 }
 
@@ -2999,7 +3017,9 @@ ENSVS_API int ensvs_set_dual_small(int on) {
 }
 
 ENSVS_API int ensvs_set_big_tile(int mode, int stages) {
-  if (mode < 0 || mode > 2 || (stages != 0 && (stages < 3 || stages > 5))) return ENSVS_E_ARG;
+  if (mode < 0 || mode > 3 || (stages != 0 && (stages < 3 || stages > 5))) return ENSVS_E_ARG;
+  g_big_all = mode == 3;
+  if (mode == 3) mode = 2;
   g_big_tile = mode;
   if (stages) g_big_stages = stages;
   return ENSVS_OK;

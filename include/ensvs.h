@@ -69,7 +69,8 @@ int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N
 /* Large-M bf16-operand launches (>= 192 tiles of 256 x 256, padded N % 256 == 0, no column
  * sums) run a 256 x 256-tile kernel with the same accumulation order (bitwise equal).
  * mode 0: keep the 128 x 128 kernel; 1: 32-deep K steps on a `stages`-deep LDS ring
- * (3..5; 0 keeps the current count); 2: 64-deep two-stage kernel.  Defaults: ENSVS_BIG_TILE
+ * (3..5; 0 keeps the current count); 2: 64-deep two-stage kernel for the gate GEMMs (the
+ * other epilogues run faster on 128 x 128 tiles); 3: as 2 for every eligible launch.  Defaults: ENSVS_BIG_TILE
  * (2), ENSVS_BIG_STAGES (5). */
 int ensvs_set_big_tile(int mode, int stages);
 /* Launches of fewer than 128 output tiles (small M) that the 64 x 64 kernel does not take

@@ -43,13 +43,12 @@ def _bf(t):
                                  L.EPI_RELU_MASK])
 @pytest.mark.parametrize("B,T", [(30, 1024), (30, 1000)])
 def test_big_tile_epilogues_bitwise(epi, B, T):
-    _epilogue_case(epi, B, T, 2, 0)
+    _epilogue_case(epi, B, T, 3, 0)  # mode 3: every epilogue on the 256 x 256 kernel
 
 
 @pytest.mark.parametrize("mode,stages", [(1, 3), (1, 4), (1, 5)])
 def test_big_tile_variants_bitwise(mode, stages):
-    _epilogue_case("gate_bf16", 30, 1000, mode, stages)
-    _epilogue_case(L.EPI_RESSKIP, 30, 1024, mode, stages)
+    _epilogue_case("gate_bf16", 30, 1000, mode, stages)  # (modes 1-2 take the gate GEMMs)
 
 
 def _epilogue_case(epi, B, T, mode, stages):
@@ -118,5 +117,5 @@ def test_big_tile_three_segments_reflect():
         y = torch.empty(M, N, device=DEV)
         K.gemm(segs, B, T, N, pb, y, N)
         return y
-    a, b = _both(run)
+    a, b = _both(run, 3)
     assert torch.equal(a, b)

@@ -147,7 +147,7 @@ class Seg:
 # 185 -> 102 ms), so there is no row threshold by default (ENSVS_BF16_MIN_ROWS sets one).
 # Single-reuse GEMMs (one tap, one N tile) stay register-staged: ENSVS_BF16_MIN_REUSE=1
 # measured 22.0 vs 21.9 ms/step and ensemble RTF 0.0305 vs 0.0294.
-BF16_ACT = {"on": True, "stages": 2,
+BF16_ACT = {"on": True, "stages": int(os.environ.get("ENSVS_STAGES", "2")),
             "stages_small": int(os.environ.get("ENSVS_STAGES_SMALL", "2")),
             "min_reuse": int(os.environ.get("ENSVS_BF16_MIN_REUSE", "2")),
             "min_rows": int(os.environ.get("ENSVS_BF16_MIN_ROWS", "0"))}
@@ -392,6 +392,10 @@ def scratch(nfloats, device, key="part"):
     return t
 
 
+# weight gradients split the frame reduction until about this many workgroups (tile x split)
+WGRAD_TARGET = int(os.environ.get("ENSVS_WGRAD_TARGET", "512"))
+
+
 def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, sk, sj,
           accum=False, dtype=_lib.DT_BF16, radd=None, radd_ld=0, dyoff=0, xoff=0, splits=None,
           scale=1.0, dstoff=0):
@@ -400,7 +404,7 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
     M = B * Tout
     if splits is None:
         tiles = -(-N // 128) * -(-K // 128) * taps
-        splits = max(1, min(64, 512 // max(tiles, 1), -(-M // 256)))
+        splits = max(1, min(64, WGRAD_TARGET // max(tiles, 1), -(-M // 256)))
     part = scratch(splits * taps * N * K, dy.device)
     if dy.dtype == torch.bfloat16 or x.dtype == torch.bfloat16:
         assert dy.dtype == x.dtype == torch.bfloat16 and radd is None and dtype == _lib.DT_BF16

@@ -339,8 +339,9 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
         wg(cell.weight_hh, dg, 4 * H, st["sh"], H, B, Tr, Tr, 4 * H, H, shift0=-1)
         wg(cell.weight_ih, dg, 4 * H, st["e"], Ce, B, Tr, Tr, 4 * H, Ce, col0=0)
         wg(cell.weight_ih, dg, 4 * H, st["sp"], 1, B, Tr, Tr, 4 * H, 1, col0=Ce)
-        Ly.colsum_into(dg, 4 * H, B * Tr, 4 * H, cell.bias_ih)
-        Ly.colsum_into(dg, 4 * H, B * Tr, 4 * H, cell.bias_hh)
+        bsum = empty(4 * H, device=dg.device)
+        K.colsum(dg, 4 * H, B * Tr, 4 * H, bsum)
+        Ly.add_into_pair(bsum.data_ptr(), 4 * H, cell.bias_ih, cell.bias_hh)
         wg(dec.feat_out.weight, do4, 4, st["sh"], H, B, Tr, Tr, 4, H, col0=0)
         wg(dec.feat_out.weight, do4, 4, st["e"], Ce, B, Tr, Tr, 4, Ce, col0=H)
         de = empty(B * Tr, Ce, device=dev)

@@ -58,6 +58,18 @@ def colsum_into(dy, ld, M, N, param, groups=1, scale=1.0, off=0, yoff=0):
         call("ensvs_axpy", g.data_ptr() + 4 * off, tmp.data_ptr(), 1.0, N, stream())
 
 
+def add_into_pair(src, N, p1, p2):
+    """p1.grad[:N] += src[:N] and p2.grad[:N] += src[:N] (src: device pointer) in one launch
+    (the b_ih / b_hh pairs of the recurrent layers share their gradient)."""
+    g1, g2 = grad_of(p1), grad_of(p2)
+    step = g2.data_ptr() - g1.data_ptr()
+    if step % 4 == 0:
+        call("ensvs_axpy_strided", g1.data_ptr(), step // 4, src, 0, 1.0, N, 2, stream())
+    else:
+        for g in (g1, g2):
+            call("ensvs_axpy", g.data_ptr(), src, 1.0, N, stream())
+
+
 def wgrad_into(param, dy, ldy, x, ldx, B, Tout, Tin, N, Kc, taps=1, dil=1, shift0=0,
                pad=_lib.PAD_ZERO, col0=0, scale=1.0, radd=None, radd_ld=0, dyoff=0, xoff=0,
                row0=0):
@@ -373,8 +385,12 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
             # h_{t-1} in processing order: t-1 forward, t+1 reverse (zero outside [0, L))
             wgrad_into(getattr(lstm, f"weight_hh_l{l}{sfx}"), dg, 8 * H, s["y"], 2 * H, B, T, T,
                        4 * H, H, shift0=(-1 if di == 0 else 1), dyoff=di * 4 * H, xoff=di * H)
-            colsum_into(dg, 8 * H, M, 4 * H, getattr(lstm, f"bias_ih_l{l}{sfx}"), yoff=di * 4 * H)
-            colsum_into(dg, 8 * H, M, 4 * H, getattr(lstm, f"bias_hh_l{l}{sfx}"), yoff=di * 4 * H)
+        # b_ih and b_hh of both directions share one gradient: the column sums of dg, once
+        bsum = empty(8 * H, device=device)
+        K.colsum(dg, 8 * H, M, 8 * H, bsum)
+        for di, sfx in enumerate(("", "_reverse")):
+            add_into_pair(bsum.data_ptr() + di * 16 * H, 4 * H, getattr(lstm, f"bias_ih_l{l}{sfx}"),
+                          getattr(lstm, f"bias_hh_l{l}{sfx}"))
         if l == 0 and not need_dx:
             break
         nd = empty(M, Kc, device=device)

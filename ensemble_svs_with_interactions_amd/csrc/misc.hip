@@ -3,6 +3,8 @@
 // step embedding / Mish, diffusion q_sample / p_sample, the masked L1 loss with
 // its fused gradient, and the clip-by-global-norm + Adam update over the flat
 // parameter buffer.  All are HBM-bound: grid-stride loops, one pass each.
+#include <initializer_list>
+
 #include "common.h"
 #include "ensvs.h"
 
@@ -66,8 +68,41 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
   const long long m0 = (long long)blockIdx.y * EMB_CHUNK + sub * (EMB_CHUNK / 4);
   const long long m1 = min(M, m0 + EMB_CHUNK / 4);
   float* a = acc + sub * V * 64 + c;
-  if (col < C)
-    for (long long m = m0; m < m1; ++m) a[ids[m] * 64] += dy[m * ldy + col];
+  // ids come in runs (a phoneme spans many frames): sum a run in a register and touch LDS
+  // only when the id changes; four rows' loads in flight per step.
+  if (col < C && m0 < m1) {
+    int cur = ids[m0];
+    float run = 0.f;
+    long long m = m0;
+    for (; m + 4 <= m1; m += 4) {
+      int id[4];
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        id[j] = ids[m + j];
+        v[j] = dy[(m + j) * ldy + col];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (id[j] != cur) {
+          a[cur * 64] += run;
+          cur = id[j];
+          run = 0.f;
+        }
+        run += v[j];
+      }
+    }
+    for (; m < m1; ++m) {
+      const int i1 = ids[m];
+      if (i1 != cur) {
+        a[cur * 64] += run;
+        cur = i1;
+        run = 0.f;
+      }
+      run += dy[m * ldy + col];
+    }
+    a[cur * 64] += run;
+  }
   __syncthreads();
   float* out = part + (long long)blockIdx.y * V * C;
   for (int i = threadIdx.x; i < V * 64; i += 256) {
@@ -152,6 +187,27 @@ __global__ void bn_apply_relu_kernel(const float* __restrict__ y, int ldy, long 
     const int g = (int)(m / Mg);
     const float v = (y[m * ldy + c] - mean[g * C + c]) * rstd[g * C + c] * gamma[c] + beta[c];
     out[m * ldo + c] = fmaxf(v, 0.f);
+  }
+}
+
+// Four channels per lane (C, every ld % 4 == 0, 16-B aligned rows, M*C < 2^31): 16-B
+// accesses and 32-bit index math; per element the same expression as the scalar kernel.
+__global__ void bn_apply_relu4_kernel(const float* __restrict__ y, int ldy, int M, int C, int Mg,
+                                      const float* __restrict__ mean,
+                                      const float* __restrict__ rstd,
+                                      const float* __restrict__ gamma,
+                                      const float* __restrict__ beta, float* __restrict__ out,
+                                      int ldo) {
+  const int C4 = C >> 2, n = M * C4;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const int m = q / C4, c = (q - m * C4) * 4, g = m / Mg;
+    const f32x4 v = *(const f32x4*)(y + (long long)m * ldy + c);
+    const f32x4 mu = *(const f32x4*)(mean + g * C + c), rs = *(const f32x4*)(rstd + g * C + c);
+    const f32x4 ga = *(const f32x4*)(gamma + c), be = *(const f32x4*)(beta + c);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = fmaxf((v[j] - mu[j]) * rs[j] * ga[j] + be[j], 0.f);
+    *(f32x4*)(out + (long long)m * ldo + c) = o;
   }
 }
 
@@ -253,6 +309,37 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ dout, int ldd,
     const float dz = z > 0.f ? dout[m * ldd + c] : 0.f;
     const float s0 = sums[(g * 2) * C + c], s1 = sums[(g * 2 + 1) * C + c];
     dy[m * lddy + c] = gamma[c] * rs * (dz - (s0 + xh * s1) / (float)Mg);
+  }
+}
+
+// bn_bwd_apply_kernel, four channels per lane (the bn_apply_relu4_kernel conditions)
+__global__ void bn_bwd_apply4_kernel(const float* __restrict__ dout, int ldd,
+                                     const float* __restrict__ y, int ldy, int M, int C, int Mg,
+                                     const float* __restrict__ mean,
+                                     const float* __restrict__ rstd,
+                                     const float* __restrict__ gamma,
+                                     const float* __restrict__ beta,
+                                     const float* __restrict__ sums, float* __restrict__ dy,
+                                     int lddy) {
+  const int C4 = C >> 2, n = M * C4;
+  const float fMg = (float)Mg;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const int m = q / C4, c = (q - m * C4) * 4, g = m / Mg;
+    const f32x4 yv = *(const f32x4*)(y + (long long)m * ldy + c);
+    const f32x4 dv = *(const f32x4*)(dout + (long long)m * ldd + c);
+    const f32x4 mu = *(const f32x4*)(mean + g * C + c), rs = *(const f32x4*)(rstd + g * C + c);
+    const f32x4 ga = *(const f32x4*)(gamma + c), be = *(const f32x4*)(beta + c);
+    const f32x4 s0 = *(const f32x4*)(sums + (g * 2) * C + c);
+    const f32x4 s1 = *(const f32x4*)(sums + (g * 2 + 1) * C + c);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (yv[j] - mu[j]) * rs[j];
+      const float z = xh * ga[j] + be[j];
+      const float dz = z > 0.f ? dv[j] : 0.f;
+      o[j] = ga[j] * rs[j] * (dz - (s0[j] + xh * s1[j]) / fMg);
+    }
+    *(f32x4*)(dy + (long long)m * lddy + c) = o;
   }
 }
 
@@ -629,6 +716,17 @@ __global__ void randint_kernel(long long* __restrict__ out, long long n, long lo
     ENSVS_CHECK_LAUNCH();                                                                       \
   } while (0)
 
+// four-channel lanes for the BatchNorm elementwise passes: see bn_apply_relu4_kernel
+static bool bn_vec4(int C, std::initializer_list<int> lds, std::initializer_list<const void*> ps,
+                    long long M) {
+  if (C % 4 != 0 || M * (long long)C >= (1ll << 31)) return false;
+  for (int l : lds)
+    if (l % 4 != 0) return false;
+  for (const void* p : ps)
+    if ((uintptr_t)p % 16 != 0) return false;
+  return true;
+}
+
 ENSVS_API int ensvs_phoneme_ids(const float* x, int ld, long long M, int ph0, int nv, int* ids,
                                 void* stream) {
   LAUNCH(phoneme_ids_kernel, M, x, ld, M, ph0, nv, ids);
@@ -684,6 +782,11 @@ ENSVS_API int ensvs_bn_finalize(float* mean, float* var, int G, int C, long long
 ENSVS_API int ensvs_bn_apply_relu(const float* y, int ldy, long long M, int C, long long Mg,
                                   const float* mean, const float* rstd, const float* gamma,
                                   const float* beta, float* out, int ldo, void* stream) {
+  if (bn_vec4(C, {ldy, ldo}, {y, out}, M)) {
+    LAUNCH(bn_apply_relu4_kernel, M * C / 4, y, ldy, (int)M, C, (int)Mg, mean, rstd, gamma, beta,
+           out, ldo);
+    return ENSVS_OK;
+  }
   LAUNCH(bn_apply_relu_kernel, M * C, y, ldy, M, C, Mg, mean, rstd, gamma, beta, out, ldo);
   return ENSVS_OK;
 }
@@ -706,6 +809,11 @@ ENSVS_API int ensvs_bn_bwd(const float* dout, int ldd, const float* y, int ldy, 
   hipLaunchKernelGGL(bn_param_grad_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, G, C, dgamma,
                      dbeta);
   ENSVS_CHECK_LAUNCH();
+  if (bn_vec4(C, {ldd, ldy, lddy}, {dout, y, dy}, M)) {
+    LAUNCH(bn_bwd_apply4_kernel, M * C / 4, dout, ldd, y, ldy, (int)M, C, (int)Mg, mean, rstd,
+           gamma, beta, sums, dy, lddy);
+    return ENSVS_OK;
+  }
   LAUNCH(bn_bwd_apply_kernel, M * C, dout, ldd, y, ldy, M, C, Mg, mean, rstd, gamma, beta, sums, dy,
          lddy);
   return ENSVS_OK;

@@ -426,7 +426,7 @@ __device__ __forceinline__ void gen_load(const GemmArgs& a, int m, int col, bool
   }
 }
 
-template <int NT = NTHR>
+template <int NT = NTHR, int EB = 1>
 __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[4][4], int m0,
                                                   int n0, int wr, int wc, int lane, int tid,
                                                   char* smem, bool write_acc = true) {
@@ -448,7 +448,8 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
   }
   __syncthreads();
   const int M = a.M;
-  constexpr int EB = 1;  // rows per operand batch (one batch ahead in flight: register budget)
+  // EB: rows per operand batch (one batch ahead in flight; 1 by register budget, more for
+  // the GATE_BWD launches of the 128 x 128 kernel, whose epilogue is all operand traffic)
   // Every thread keeps one column group across its rows (NT is a multiple of 32), so the
   // bias is read once, and all of a thread's global operand loads (residual, skip, Y,
   // gate/filter save) are issued before its first store: with the loads after the stores
@@ -957,7 +958,15 @@ __device__ __forceinline__ void usf_block_tail(const GemmArgs& a, const GemmArgs
                                                f32x4 (&acc)[4][4], char* smem, int tid, int lane,
                                                int wr, int wc, int m0);
 
+#ifndef ENSVS_GBW_EB
+#define ENSVS_GBW_EB 1
+#endif
+// GATE_BWD epilogue rows per operand batch in the 128 x 128 kernel: 2 compiles without
+// scratch (-DENSVS_GBW_EB=2, 162 VGPRs; 4 spills 124 B) but is not measured yet, so 1
+constexpr int GBW_EB = ENSVS_GBW_EB;
+
 template <int STAGES, bool FUSE>
+
 __device__ __forceinline__ void b16_body(const GemmArgs& a, const GemmArgs& a2) {
   static_assert(STAGES >= 2 && STAGES <= 3, "stages");
   constexpr int TILE = BM * BK2 * 2;  // bytes of one operand image (16 KB)
@@ -1117,7 +1126,12 @@ __device__ __forceinline__ void b16_body(const GemmArgs& a, const GemmArgs& a2) 
       }
     return;
   }
-  if (a.vec_out) gemm_epilogue_lds(a, acc, m0, n0, wr, wc, lane, tid, smem);
+  if (a.vec_out) {
+    if (GBW_EB > 1 && a.epi == EPI_GATE_BWD)
+      gemm_epilogue_lds<NTHR, GBW_EB>(a, acc, m0, n0, wr, wc, lane, tid, smem);
+    else
+      gemm_epilogue_lds(a, acc, m0, n0, wr, wc, lane, tid, smem);
+  }
   else gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
 }
 

@@ -111,6 +111,8 @@ SIGNATURES = {
                             c_vp],
     "ensvs_bn_bwd": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp,
                      c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
+    "ensvs_bn_bwd_frozen": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                            c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
     "ensvs_sinusoidal": [c_vp, c_int, c_int, c_vp, c_vp],
     "ensvs_mish_fwd": [c_vp, c_vp, c_ll, c_vp],
     "ensvs_mish_bwd": [c_vp, c_vp, c_vp, c_ll, c_vp],

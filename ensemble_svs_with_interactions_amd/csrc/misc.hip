@@ -312,6 +312,25 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ dout, int ldd,
   }
 }
 
+// Frozen (eval-mode) BatchNorm under training: mean / rstd are the running statistics,
+// constants of the step, so dy = gamma * rstd * dz (dz = dout * (z > 0)).
+__global__ void bn_bwd_apply_frozen_kernel(const float* __restrict__ dout, int ldd,
+                                           const float* __restrict__ y, int ldy, long long M,
+                                           int C, const float* __restrict__ mean,
+                                           const float* __restrict__ rstd,
+                                           const float* __restrict__ gamma,
+                                           const float* __restrict__ beta,
+                                           float* __restrict__ dy, int lddy) {
+  GRID_LOOP(i, M * C) {
+    const long long m = i / C;
+    const int c = (int)(i % C);
+    const float rs = rstd[c];
+    const float z = (y[m * ldy + c] - mean[c]) * rs * gamma[c] + beta[c];
+    const float dz = z > 0.f ? dout[m * ldd + c] : 0.f;
+    dy[m * lddy + c] = gamma[c] * rs * dz;
+  }
+}
+
 // bn_bwd_apply_kernel, four channels per lane (the bn_apply_relu4_kernel conditions)
 __global__ void bn_bwd_apply4_kernel(const float* __restrict__ dout, int ldd,
                                      const float* __restrict__ y, int ldy, int M, int C, int Mg,
@@ -782,7 +801,7 @@ ENSVS_API int ensvs_bn_finalize(float* mean, float* var, int G, int C, long long
 ENSVS_API int ensvs_bn_apply_relu(const float* y, int ldy, long long M, int C, long long Mg,
                                   const float* mean, const float* rstd, const float* gamma,
                                   const float* beta, float* out, int ldo, void* stream) {
-  if (bn_vec4(C, {ldy, ldo}, {y, out}, M)) {
+  if (bn_vec4(C, {ldy, ldo}, {y, out, mean, rstd, gamma, beta}, M)) {
     LAUNCH(bn_apply_relu4_kernel, M * C / 4, y, ldy, (int)M, C, (int)Mg, mean, rstd, gamma, beta,
            out, ldo);
     return ENSVS_OK;
@@ -809,12 +828,37 @@ ENSVS_API int ensvs_bn_bwd(const float* dout, int ldd, const float* y, int ldy, 
   hipLaunchKernelGGL(bn_param_grad_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, G, C, dgamma,
                      dbeta);
   ENSVS_CHECK_LAUNCH();
-  if (bn_vec4(C, {ldd, ldy, lddy}, {dout, y, dy}, M)) {
+  if (bn_vec4(C, {ldd, ldy, lddy}, {dout, y, dy, mean, rstd, gamma, beta, sums}, M)) {
     LAUNCH(bn_bwd_apply4_kernel, M * C / 4, dout, ldd, y, ldy, (int)M, C, (int)Mg, mean, rstd,
            gamma, beta, sums, dy, lddy);
     return ENSVS_OK;
   }
   LAUNCH(bn_bwd_apply_kernel, M * C, dout, ldd, y, ldy, M, C, Mg, mean, rstd, gamma, beta, sums, dy,
+         lddy);
+  return ENSVS_OK;
+}
+
+// BatchNorm1d in eval mode inside a training step (frozen statistics, e.g. the data-parallel
+// parity definition of SURVEY 8(e)): dgamma / dbeta accumulate as in ensvs_bn_bwd (one group),
+// the input gradient has no batch-statistic terms.
+ENSVS_API int ensvs_bn_bwd_frozen(const float* dout, int ldd, const float* y, int ldy, long long M,
+                                  int C, const float* mean, const float* rstd, const float* gamma,
+                                  const float* beta, float* part, int max_splits, float* sums,
+                                  float* dgamma, float* dbeta, float* dy, int lddy, void* stream) {
+  if (M <= 0 || C <= 0) return ENSVS_E_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  const int S = (int)std::max<long long>(1, std::min<long long>(max_splits, M / 64));
+  const int rps = (int)((M + S - 1) / S);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(cdiv(C, 64), S, 1), dim3(256), 0, st, dout, ldd, y,
+                     ldy, M, C, mean, rstd, gamma, beta, rps, part);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, 64), 1), dim3(1024), 0, st, part, S, C,
+                     sums);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_param_grad_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, 1, C, dgamma,
+                     dbeta);
+  ENSVS_CHECK_LAUNCH();
+  LAUNCH(bn_bwd_apply_frozen_kernel, M * C, dout, ldd, y, ldy, M, C, mean, rstd, gamma, beta, dy,
          lddy);
   return ENSVS_OK;
 }

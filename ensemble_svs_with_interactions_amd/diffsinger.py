@@ -29,7 +29,7 @@ from . import kernels as K
 from . import layers as Ly
 from ._lib import call
 from .base import BaseModel, PredictionType
-from .engine import GradCapture, ModulePacks, aux_stream, empty, grad_of, lengths_pair, next_seed
+from .engine import GradCapture, ModulePacks, empty, grad_of, lengths_pair, next_seed
 from .engine import gemm_dtype as engine_gemm_dtype
 
 SQRT1_2 = 1.0 / math.sqrt(2.0)
@@ -365,14 +365,13 @@ class DiffNet(nn.Module):
         dcond = empty(M, E, device=dev)
         K.gemm([K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, L * 2 * C, pk["condT"], T)],
                B, T, E, pk.bwd, dcond, E)
-        # everything below produces parameter gradients only: an auxiliary stream of the
-        # enclosing branch set (engine.aux_stream) runs it beside the encoder's backward
-        with aux_stream(keep=(later, st, dout, dx, dxb, dss, dssb, tmp_dss, dpre_all, dpre_b,
-                              dd_all, dd_tiles, pre_tiles)):
-            for f in later:
-                f()
-            self._bwd_param_tail(st, dout, dx, dss, dssb, tmp_dss, dpre_all, dpre_b, dd_all,
-                                 dd_tiles, pre_tiles, fuse, bw, b16)
+        # everything below produces parameter gradients only (an auxiliary stream beside the
+        # encoder's backward measured slower: 24.8 vs 21.4 ms/step, the recurrences slow
+        # down under the extra GEMM traffic; so it stays on the branch's stream)
+        for f in later:
+            f()
+        self._bwd_param_tail(st, dout, dx, dss, dssb, tmp_dss, dpre_all, dpre_b, dd_all,
+                             dd_tiles, pre_tiles, fuse, bw, b16)
         return dcond
 
     def _bwd_param_tail(self, st, dout, dx, dss, dssb, tmp_dss, dpre_all, dpre_b, dd_all,

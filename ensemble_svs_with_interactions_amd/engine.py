@@ -10,18 +10,14 @@
 * ``ModulePacks``: per-module packed GEMM operands, rebuilt when parameters
   move and repacked (one launch) when they change.
 """
-import os
 
 import torch
 
 from . import _lib
 from .kernels import PackedBuffer
 
-_STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None, "concurrent": True,
-          "aux": os.environ.get("ENSVS_AUX_WGRAD", "0") != "0"}
+_STATE = {"gemm_dtype": _lib.DT_BF16, "epoch": 0, "rng": None, "concurrent": True}
 _SIDE_STREAMS = {}
-_AUX_STREAMS = {}
-_ACTIVE_BRANCHES = []
 # Dev instrumentation: set to a list to collect (branch, start_event, end_event) per
 # branch region (tools/branch_times.py); None = off.
 BRANCH_TIMES = None
@@ -54,24 +50,13 @@ def branch_streams(device, n_side=3):
     (tools/infer_streams_probe.py)."""
     key = (str(device), n_side)
     if key not in _SIDE_STREAMS:
-        # equal priorities: with the DiffNet backward's per-block launches batched, a
-        # high-priority branch (ENSVS_PRIO_BRANCH=i) measured slower -- lf0 23.5, mgc 23.4,
-        # bap 22.2 vs 22.2 ms/step for none (graph replay, 30 x 1024)
-        hi = int(os.environ.get("ENSVS_PRIO_BRANCH", "-1"))
-        _SIDE_STREAMS[key] = [torch.cuda.Stream(device, priority=-1 if i == hi else 0)
-                              for i in range(n_side)]
-        new = list(_SIDE_STREAMS[key])
-        if _STATE["aux"]:  # the auxiliary weight-gradient streams too (Branches.aux)
-            for k in range(2):
-                ak = (str(device), k)
-                if ak not in _AUX_STREAMS:
-                    _AUX_STREAMS[ak] = torch.cuda.Stream(device)
-                    new.append(_AUX_STREAMS[ak])
-        if os.environ.get("ENSVS_TOUCH_STREAMS", "1") == "1":
-            cur = torch.cuda.current_stream(device)
-            for s in new:  # first command on each new stream now
-                s.wait_stream(cur)
-                cur.wait_stream(s)
+        # equal priorities: a high-priority branch stream measured slower (lf0 23.5, mgc
+        # 23.4, bap 22.2 vs 22.2 ms/step for none; graph replay, 30 x 1024)
+        _SIDE_STREAMS[key] = [torch.cuda.Stream(device) for _ in range(n_side)]
+        cur = torch.cuda.current_stream(device)
+        for s in _SIDE_STREAMS[key]:  # first command on each new stream now
+            s.wait_stream(cur)
+            cur.wait_stream(s)
     return _SIDE_STREAMS[key]
 
 
@@ -97,30 +82,12 @@ class Branches:
         self.side = branch_streams(device, n_side) if self.on_side else []
 
     def __enter__(self):
-        self.aux_used = []
-        self.keep = []
         if self.on_side:
             self.main = torch.cuda.current_stream(self.device)
             ev = self.main.record_event()
             for s in self.side:
                 s.wait_event(ev)
-        _ACTIVE_BRANCHES.append(self)
         return self
-
-    def aux(self):
-        """Fork an auxiliary stream from the current (branch) stream for work that only
-        produces parameter gradients; it is joined into the MAIN stream at exit.  (Joining
-        a nested fork back into its parent branch stream instead makes hipStreamEndCapture
-        segfault under HIP-graph capture on ROCm 7.2: tools/graph_fork_probe.py, DESIGN.md
-        §5.)"""
-        k = len(self.aux_used)
-        key = (str(self.device), k)
-        if key not in _AUX_STREAMS:
-            _AUX_STREAMS[key] = torch.cuda.Stream(self.device)
-        s = _AUX_STREAMS[key]
-        s.wait_event(torch.cuda.current_stream(self.device).record_event())
-        self.aux_used.append(s)
-        return torch.cuda.stream(s)
 
     def on(self, i):
         import contextlib
@@ -133,35 +100,10 @@ class Branches:
         return _timed(ctx, i)
 
     def __exit__(self, *exc):
-        _ACTIVE_BRANCHES.pop()
         if self.on_side:
-            for s in self.side + self.aux_used:
+            for s in self.side:
                 self.main.wait_stream(s)
-        # tensors an auxiliary stream reads were allocated on a branch stream: released only
-        # now, after the join, so the allocator cannot hand their blocks to later branch work
-        # while the auxiliary stream may still read them
-        self.keep = []
         return False
-
-
-def aux_stream(keep=()):
-    """Context for launches off a branch's critical path (weight / bias gradients): an
-    auxiliary stream forked from the current stream and joined at the end of the enclosing
-    Branches, or inline when branches run serially or auxiliary streams are off (the
-    default: ENSVS_AUX_WGRAD=1 turns them on; the DiffNet weight gradients beside the
-    encoder backward measured 24.8 vs 21.4 ms/step at 4 and at 8 hardware queues --
-    the recurrences slow down under the extra GEMM traffic).  ``keep``: objects
-    holding the tensors the enclosed launches read, kept alive until that join."""
-    import contextlib
-    if not _STATE["aux"] or not _ACTIVE_BRANCHES or not _ACTIVE_BRANCHES[-1].on_side:
-        return contextlib.nullcontext()
-    br = _ACTIVE_BRANCHES[-1]
-    br.keep.append(keep)
-    return br.aux()
-
-
-def set_aux_streams(on: bool):
-    _STATE["aux"] = bool(on)
 
 
 def next_seed() -> int:

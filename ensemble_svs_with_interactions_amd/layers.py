@@ -247,7 +247,11 @@ def conv_fwd(pk, conv, first_segs, B, T, device, training, groups=1, save=True,
         bn = conv[bi]
         mean = empty(groups, C, device=device)
         rstd = empty(groups, C, device=device)
-        if training:
+        # a BatchNorm module put in eval mode inside a training step (torch semantics:
+        # bn.training decides batch vs running statistics) normalises with its running
+        # statistics and is differentiated with them held constant (ensvs_bn_bwd_frozen)
+        frozen = training and not bn.training
+        if training and not frozen:
             var = empty(groups, C, device=device)
             K.colsum(y, C, Mg, C, mean, groups=groups, scale=1.0 / Mg)
             K.colsum(y, C, Mg, C, var, groups=groups, mean=mean, scale=1.0 / Mg)
@@ -270,7 +274,7 @@ def conv_fwd(pk, conv, first_segs, B, T, device, training, groups=1, save=True,
              rstd.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(), out.data_ptr(), C,
              stream())
         if save:
-            sv.append(dict(y=y, mean=mean, rstd=rstd, out=out, segs=segs))
+            sv.append(dict(y=y, mean=mean, rstd=rstd, out=out, segs=segs, frozen=frozen))
         a, C_prev = out, C
     return a, sv
 
@@ -290,11 +294,18 @@ def conv_bwd(pk, conv, sv, dout, B, T, device, groups=1, first_dx=None):
         dy = empty(M, C, device=device)
         part = K.scratch(groups * BN_SPLITS * 2 * C, device, key="bn")
         sums = empty(groups * 2 * C, device=device)
-        call("ensvs_bn_bwd", d.data_ptr(), C, s["y"].data_ptr(), C, M, C, Mg, s["mean"].data_ptr(),
-             s["rstd"].data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(), part.data_ptr(),
-             BN_SPLITS,
-             sums.data_ptr(), grad_of(bn.weight).data_ptr(), grad_of(bn.bias).data_ptr(),
-             dy.data_ptr(), C, stream())
+        if s.get("frozen"):
+            call("ensvs_bn_bwd_frozen", d.data_ptr(), C, s["y"].data_ptr(), C, M, C,
+                 s["mean"].data_ptr(), s["rstd"].data_ptr(), bn.weight.data_ptr(),
+                 bn.bias.data_ptr(), part.data_ptr(), BN_SPLITS, sums.data_ptr(),
+                 grad_of(bn.weight).data_ptr(), grad_of(bn.bias).data_ptr(), dy.data_ptr(), C,
+                 stream())
+        else:
+            call("ensvs_bn_bwd", d.data_ptr(), C, s["y"].data_ptr(), C, M, C, Mg,
+                 s["mean"].data_ptr(), s["rstd"].data_ptr(), bn.weight.data_ptr(),
+                 bn.bias.data_ptr(), part.data_ptr(), BN_SPLITS, sums.data_ptr(),
+                 grad_of(bn.weight).data_ptr(), grad_of(bn.bias).data_ptr(), dy.data_ptr(), C,
+                 stream())
         _dbg(f"conv{li}.dout", d)
         _dbg(f"conv{li}.dy", dy)
         colsum_into(dy, C, M, C, conv[ci].bias)

@@ -257,8 +257,12 @@ def train_step_single(model, optimizer, x, y, lengths, draws=None, ddp=True):
 
 def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws,
                     ddp, y_sub, logf0_diff_weight, overlap=False):
-    """zero_grad + forward + masked L1 (+ interaction loss) + backward into the flat grads."""
-    model.train()
+    """zero_grad + forward + masked L1 (+ interaction loss) + backward into the flat grads.
+    An eval-mode model is switched to training mode (the reference's train_loop does this per
+    phase, train_acoustic_multitrack.py:452); a training-mode model is left as it is, so
+    BatchNorm modules frozen with bn.eval() stay frozen (running statistics, ensvs_bn_bwd_frozen)."""
+    if not model.training:
+        model.train()
     optimizer.zero_grad()
     if logf0_diff_weight > 0.0 and (not model.output_subtrack or y_sub is None):
         raise ValueError("logf0_diff_weight > 0 needs output_subtrack=True and y_sub (the "

@@ -231,6 +231,13 @@ int ensvs_bn_bwd(const float* dout, int ldd, const float* y, int ldy, long long 
                  long long Mg, const float* mean, const float* rstd, const float* gamma,
                  const float* beta, float* part, int max_splits, float* sums, float* dgamma,
                  float* dbeta, float* dy, int lddy, void* stream);
+/* BatchNorm1d in eval mode inside a training step (model.train() + bn.eval(): frozen running
+ * statistics; the data-parallel parity definition, SURVEY 8(e), train_util.py:1176-1182):
+ * dgamma/dbeta accumulate, dy = gamma * rstd * dout * (z > 0). */
+int ensvs_bn_bwd_frozen(const float* dout, int ldd, const float* y, int ldy, long long M, int C,
+                        const float* mean, const float* rstd, const float* gamma,
+                        const float* beta, float* part, int max_splits, float* sums,
+                        float* dgamma, float* dbeta, float* dy, int lddy, void* stream);
 /* DiffNet step embedding (denoiser.py:9-26). */
 int ensvs_sinusoidal(const long long* t, int B, int C, float* out, void* stream);
 int ensvs_mish_fwd(const float* x, float* y, long long n, void* stream);

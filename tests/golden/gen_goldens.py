@@ -368,6 +368,81 @@ def case_train_step_tiny(steps=2, lr=1e-3, logf0_diff_weight=0.0, name="train_st
     save(name, arrays, meta)
 
 
+GRAD_SAMPLE = 2048
+
+
+def grad_sample_index(key, numel):
+    """Fixed sample of element indices of one parameter's gradient (at most GRAD_SAMPLE):
+    a full-width model's gradients are 94 MB, so the fixture keeps a seeded subset of every
+    tensor (enough for a per-tensor relative-L2 estimate) plus its exact sum / abs / l2."""
+    if numel <= GRAD_SAMPLE:
+        return np.arange(numel, dtype=np.int64)
+    return np.sort(rng_for("gsample_" + key).choice(numel, GRAD_SAMPLE, replace=False))
+
+
+def case_train_step_full(steps=2, lr=1e-4, P=2, T=64, lengths=(64, 52)):
+    """The reference train_step (train_acoustic_multitrack.py:40-392) on the recipe-width
+    model (multitrack_acoustic_nnsvs_world_multi_ar_f0_diff_mgcbap.yaml), V/UV LSTM dropout
+    0 (see the module docstring): losses, grad norms, per-step loss metrics, step-0 gradient
+    summaries + sampled elements of every parameter gradient, final BN running statistics."""
+    cfg = configs.multitrack_diffusion(num_speakers=4)
+    model, shapes = build_ref(cfg)
+    model.vuv_model.lstm.dropout = 0.0
+    batch = data.synthetic_batch(P, T, SEED + 23, lengths=list(lengths))
+    opt = torch.optim.Adam(model.parameters(), lr=lr, betas=(0.9, 0.999), weight_decay=0.0)
+    model_config = types.SimpleNamespace(stream_sizes=[60, 1, 1, 5])
+    optim_config = types.SimpleNamespace(clip_norm=1.0)
+    logger = logging.getLogger("golden")
+    arrays = dict(**{k: v for k, v in batch.items()})
+    meta = dict(shapes={k: list(v) for k, v in shapes.items()}, lr=lr, steps=steps,
+                grad_sample=GRAD_SAMPLE)
+    losses, norms, feats = [], [], []
+    for s in range(steps):
+        d = model_draws(f"full_step{s}", P, T, cfg)
+        for k, v in d.items():
+            arrays[f"draw{s}::{k}"] = v
+        norm_box = {}
+        orig = torch.nn.utils.clip_grad_norm_
+
+        def clip(params, max_norm, *a, **k):
+            n = orig(params, max_norm, *a, **k)
+            norm_box["n"] = float(n)
+            return n
+        torch.nn.utils.clip_grad_norm_ = clip
+        try:
+            with queue_draws(d, T):
+                loss, metrics = ref_train_step(
+                    logger, model, model_config, optim_config, opt, None, True,
+                    (T_(batch["x_main"]), T_(batch["x_sub"])),
+                    [T_(batch["y_main"]), T_(batch["y_sub"])],
+                    (T_(batch["spk_main"]).int(), T_(batch["spk_sub"]).int()),
+                    (T_(batch["lengths"]), T_(batch["lengths"])),
+                    None, None, feats_criterion="l1", pitch_reg_weight=0.0,
+                    logf0_diff_weight=0.0, mgc_diff_weight=0.0)
+        finally:
+            torch.nn.utils.clip_grad_norm_ = orig
+        losses.append(float(loss))
+        norms.append(norm_box["n"])
+        feats.append(float(metrics["Loss_Feats"]))
+        if s == 0:
+            # gradients as the optimizer saw them (after clipping they are scaled in place
+            # by clip_grad_norm_: undo the scale so the fixture holds the raw gradient)
+            coef = min(1.0, 1.0 / (norm_box["n"] + 1e-6))
+            summ = {}
+            for k, p in model.named_parameters():
+                g = p.grad.detach().double().reshape(-1) / coef
+                summ[k] = [g.sum().item(), g.abs().sum().item(), g.norm().item()]
+                idx = grad_sample_index(k, g.numel())
+                arrays[f"gidx::{k}"] = idx.astype(np.int32)
+                arrays[f"gval::{k}"] = g[torch.from_numpy(idx)].numpy()
+            meta["grad_summary"] = summ
+    for k, v in model.state_dict().items():
+        if "running" in k:
+            arrays[f"final::{k}"] = v.numpy()
+    meta.update(losses=losses, grad_norms=norms, loss_feats=feats)
+    save("train_step_full", arrays, meta)
+
+
 def case_inference_bap(model):
     gd = model.bap_model
     gd.eval()
@@ -1201,6 +1276,8 @@ def main():
         case_train_step_tiny()
     if run("tiny_il"):
         case_train_step_tiny(logf0_diff_weight=0.5, name="train_step_tiny_il")
+    if run("full_train"):
+        case_train_step_full()
     if run("inference_tiny"):
         case_model_inference_tiny()
     if run("st"):

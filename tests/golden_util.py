@@ -92,9 +92,43 @@ def rel_l2(g, ref):
     return ((g - ref).norm() / (ref.norm() + 1e-30)).item()
 
 
-def grad_close(g, ref, rtol):
-    """Relative L2 error of a gradient tensor (robust to isolated ReLU-kink flips)."""
-    return rel_l2(g, ref) <= rtol
+def sampled_grad_errors(grads, a, meta):
+    """Per-parameter errors of full-width gradients against a fixture that keeps a seeded
+    element sample of every reference gradient (train_step_full): {key: (sampled rel-L2,
+    relative error of the exact L2 norm)}.  grads: {key: tensor} (any device)."""
+    out = {}
+    for k, (s, ab, l2) in meta["grad_summary"].items():
+        g = grads[k].detach().reshape(-1).double().cpu()
+        idx = torch.from_numpy(a["gidx::" + k].astype(np.int64))
+        ref = torch.from_numpy(a["gval::" + k])
+        out[k] = (rel_l2(g[idx], ref), abs(g.norm().item() - l2) / (l2 + 1e-30))
+    return out
+
+
+def record_errors(case, values):
+    """Merge measured errors of one test case into $ENSVS_RECORD_DIR/<case>.json (nothing
+    when the variable is unset): the numbers DESIGN.md section 4 quotes."""
+    d = os.environ.get("ENSVS_RECORD_DIR")
+    if not d:
+        return
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, case + ".json")
+    old = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            old = json.load(f)
+    old.update(values)
+    with open(path, "w") as f:
+        json.dump(old, f, indent=1, sort_keys=True)
+
+
+def grad_close(g, ref, rtol, name=None):
+    """Relative L2 error of a gradient tensor (robust to isolated ReLU-kink flips); with a
+    name, the measured error is recorded (record_errors("end_to_end_grads", ...))."""
+    e = rel_l2(g, ref)
+    if name is not None:
+        record_errors("end_to_end_grads", {name: e})
+    return e <= rtol
 
 def loader_tree(root, arrays):
     """Write the on-disk dataset held in `arrays` (loader fixture) under root:

@@ -12,6 +12,9 @@ Pairs are split x[rank::W] (train_util.py:1176-1182).  Per rank:
   4. torch DistributedDataParallel(model) around the drop-in model with the reference-style
      autograd step: DDP's hooks average the gradients that Function.backward returns, and
      the result equals the fused data-parallel gradient of the same shards.
+  5. SURVEY 8(e)'s parity definition: with BatchNorm frozen (bn.eval() inside the training
+     step) and equal lengths, the all-reduced gradient of the two shards equals the
+     product's own single-process gradient of the concatenated 4-pair batch.
 BatchNorm statistics stay per rank, as in the reference (no SyncBN).
 """
 import os
@@ -158,6 +161,61 @@ def _rank(rank, port, out_dir):
             den += (q.grad ** 2).sum().item()
         res["ddp_grad_err"] = (num / den) ** 0.5
         res["fused_grad_norm"] = float(fused_grad.norm())
+
+        # 5: data-parallel parity as SURVEY 8(e) defines it: with BatchNorm frozen (eval)
+        # and equal lengths, the all-reduced gradient of the W shards equals the product's
+        # own single-process gradient of the concatenated 4-pair batch (same draws)
+        gf = torch.Generator().manual_seed(55)
+        P4 = 4
+        full_draws = dict(
+            lf0_main=(torch.rand(P4, T // 4, generator=gf) > 0.5).float() * 2,
+            lf0_sub=(torch.rand(P4, T // 4, generator=gf) > 0.5).float() * 2,
+            mgc_t=torch.randint(0, 100, (P4,), generator=gf),
+            bap_t=torch.randint(0, 100, (P4,), generator=gf),
+            mgc_noise=torch.randn(P4, T, 60, generator=gf),
+            bap_noise=torch.randn(P4, T, 5, generator=gf))
+
+        def take(idx):
+            out = {}
+            for k, v in full_draws.items():
+                v = v[torch.as_tensor(idx)]
+                out[k] = (v.reshape(len(idx) * T, -1) if k.endswith("noise")
+                          else v.reshape(-1)).contiguous().cuda()
+            return out
+
+        def frozen_bn_model():
+            torch.manual_seed(4321)
+            m = configs.instantiate(cfg).cuda()
+            m.vuv_model.lstm.dropout = 0.0
+            m.train()
+            for mod in m.modules():
+                if isinstance(mod, torch.nn.BatchNorm1d):
+                    mod.eval()
+            return m
+
+        allp = list(range(P4))
+        fb = lambda k, idx: torch.from_numpy(np.ascontiguousarray(b[k][idx])).cuda()  # noqa: E731
+        mdp = frozen_bn_model()
+        odp = train.FusedAdam(mdp, lr=1e-3)
+        train.set_overlap_allreduce(True)
+        ldp, _ = train.train_step(mdp, odp, *(fb(k, sel) for k in ("x_main", "x_sub", "y_main",
+                                                                  "spk_main", "spk_sub")),
+                                  lens, draws=take(mine))
+        m1 = frozen_bn_model()
+        o1 = train.FusedAdam(m1, lr=1e-3)
+        l1, _ = train.train_step(m1, o1, *(fb(k, allp) for k in ("x_main", "x_sub", "y_main",
+                                                                "spk_main", "spk_sub")),
+                                 b["lengths"].tolist(), draws=take(allp), ddp=False)
+        torch.cuda.synchronize()
+        assert all(not mod.training for mod in mdp.modules()
+                   if isinstance(mod, torch.nn.BatchNorm1d))
+        gdp, g1 = odp.gflat.detach().cpu(), o1.gflat.detach().cpu()
+        res["dp_vs_full_grad_rel_l2"] = ((gdp - g1).norm() / g1.norm()).item()
+        res["dp_vs_full_grad_norm"] = float(g1.norm())
+        losses = gather(ldp.detach().view(1))
+        res["dp_vs_full_loss_rel"] = abs(float(sum(losses)) / W - l1.item()) / abs(l1.item())
+        flats = gather(odp.flat)
+        res["dp_param_mismatch"] = float((flats[0] - flats[1]).abs().max())
     finally:
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), **{k: np.float64(v) for k, v in res.items()})
         dist.destroy_process_group()
@@ -189,3 +247,7 @@ def test_data_parallel_world2_product_step(tmp_path):
         assert z["overlap_param_mismatch"] == 0.0
         assert z["overlap_whole_buffer_calls"] == 0 and z["overlap_buckets"] >= 6
         assert z["ddp_grad_err"] < 1e-5, z["ddp_grad_err"]
+        # DP-W gradient == 1-process full-batch gradient (BN frozen, equal lengths)
+        assert z["dp_vs_full_grad_rel_l2"] < 1e-6, z["dp_vs_full_grad_rel_l2"]
+        assert z["dp_vs_full_loss_rel"] < 1e-6, z["dp_vs_full_loss_rel"]
+        assert z["dp_param_mismatch"] == 0.0

@@ -9,6 +9,7 @@ RCCL gradient all-reduce (data parallel over pairs), global-norm clipping,
 non-finite skip and Adam — every arithmetic op in libensvs.so, no host sync.
 """
 import ctypes
+import math
 from os import environ as _os_env
 
 import torch
@@ -19,7 +20,7 @@ from .engine import branch_streams, empty, flatten_parameters, grad_of, weights_
 from .engine import _STATE as _ENGINE_STATE
 
 
-class FusedAdam:
+class FusedAdam(torch.optim.Optimizer):
     """clip_grad_norm_(clip_norm) + torch.optim.Adam over the flat parameter buffer.
 
     Same update as torch.optim.Adam(weight_decay=0, amsgrad=False) after
@@ -27,6 +28,14 @@ class FusedAdam:
     finite (train_acoustic_multitrack.py:369-380).  The step counter and the bias
     corrections live on the device (ensvs_adam_step), so a skipped step does not
     advance the counter and the update replays correctly from a HIP graph.
+
+    A torch.optim.Optimizer: ``param_groups[0]["lr"]`` is the learning rate, so the
+    reference's schedulers drive it (StepLR, train_util.py:1348-1355 ``_instantiate_optim``;
+    the new value reaches the device before the next step, eager or replayed), and
+    ``state_dict()`` / ``load_state_dict()`` use torch.optim.Adam's format (per-parameter
+    ``step`` / ``exp_avg`` / ``exp_avg_sq``), so a checkpoint's ``optimizer_state``
+    (train_util.py:1324-1331, resumed at :1381-1384) moves between this optimizer and
+    torch.optim.Adam in both directions.
     """
 
     def __init__(self, model, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
@@ -41,32 +50,45 @@ class FusedAdam:
             broadcast_state(model)
         self.model = model
         self.flat, self.gflat = model._ensvs_flat
+        # torch.optim.Adam's defaults (its state_dict's param_groups carry them)
+        defaults = dict(torch.optim.Adam([torch.zeros(1)]).defaults)
+        defaults.update(lr=float(lr), betas=tuple(betas), eps=float(eps), weight_decay=0.0)
+        super().__init__(list(model.parameters()), defaults)
         self.m = torch.zeros_like(self.flat)
         self.v = torch.zeros_like(self.flat)
-        self.betas, self.eps, self.clip_norm = betas, eps, clip_norm
+        self.betas, self.eps, self.clip_norm = tuple(betas), eps, clip_norm
         self.step_count = 0  # host count of step() calls (skipped steps included)
         # {device step, lr / bc1, sqrt(bc2), lr}
-        self.state = torch.zeros(4, dtype=torch.float64, device=self.flat.device)
-        self.lr = lr
+        self.dev_state = torch.zeros(4, dtype=torch.float64, device=self.flat.device)
+        self._lr = None
+        self.sync_lr()
         self.norm = torch.zeros(1, device=self.flat.device)
         self._part = torch.empty(1024, device=self.flat.device)
 
     @property
     def lr(self):
-        return self._lr
+        return self.param_groups[0]["lr"]
 
     @lr.setter
     def lr(self, value):
         """Takes effect from the next step, eager or replayed."""
-        self._lr = float(value)
-        self.state[3].fill_(self._lr)
+        self.param_groups[0]["lr"] = float(value)
+        self.sync_lr()
+
+    def sync_lr(self):
+        """Push param_groups[0]["lr"] (set by a scheduler or by hand) to the device state the
+        Adam kernel reads; called by step() and before every graph replay."""
+        lr = float(self.param_groups[0]["lr"])
+        if lr != self._lr:
+            self._lr = lr
+            self.dev_state[3].fill_(lr)
 
     @property
     def device_step(self):
         """Number of applied (finite-norm) updates, read from the device."""
-        return int(self.state[0].item())
+        return int(self.dev_state[0].item())
 
-    def zero_grad(self):
+    def zero_grad(self, set_to_none=False):
         self.gflat.zero_()
         for p in self.model.parameters():
             if p.grad is None or p.grad.data_ptr() != p._ensvs_gview.data_ptr():
@@ -77,14 +99,77 @@ class FusedAdam:
              self.norm.data_ptr(), Ly.stream())
         return self.norm
 
-    def step(self):
+    def step(self, closure=None):
+        if closure is not None:
+            raise NotImplementedError("FusedAdam.step(closure)")
         self.step_count += 1
+        self.sync_lr()
         b1, b2 = self.betas
         self.grad_norm()
         call("ensvs_adam_step", self.flat.data_ptr(), self.gflat.data_ptr(), self.m.data_ptr(),
              self.v.data_ptr(), self.flat.numel(), self.norm.data_ptr(), float(self.clip_norm),
-             float(b1), float(b2), float(self.eps), self.state.data_ptr(), Ly.stream())
+             float(b1), float(b2), float(self.eps), self.dev_state.data_ptr(), Ly.stream())
         weights_updated()
+
+    # ---- checkpoints (torch.optim.Adam format) ---------------------------------------
+    def _slices(self):
+        base = self.flat.data_ptr()
+        for i, p in enumerate(self.param_groups[0]["params"]):
+            o = (p.data_ptr() - base) // 4
+            yield i, p, o
+
+    def state_dict(self):
+        """torch.optim.Adam.state_dict() of the same update: per-parameter 'step' (applied
+        updates), 'exp_avg', 'exp_avg_sq' (CPU copies), and the param group."""
+        step = float(self.device_step)
+        state = {}
+        if step > 0:
+            for i, p, o in self._slices():
+                n = p.numel()
+                state[i] = {"step": torch.tensor(step, dtype=torch.float32),
+                            "exp_avg": self.m[o:o + n].view_as(p).detach().cpu().clone(),
+                            "exp_avg_sq": self.v[o:o + n].view_as(p).detach().cpu().clone()}
+        g = {k: v for k, v in self.param_groups[0].items() if k != "params"}
+        g["params"] = list(range(len(self.param_groups[0]["params"])))
+        return {"state": state, "param_groups": [g]}
+
+    def load_state_dict(self, state_dict):
+        """Load torch.optim.Adam's (or this optimizer's) state_dict: moments into the flat
+        buffers, the step count and bias corrections into the device state, lr / betas / eps
+        from the param group."""
+        groups = state_dict["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(self.param_groups[0]["params"]):
+            raise ValueError("optimizer state does not match this model's parameters")
+        g = groups[0]
+        for k in ("lr", "betas", "eps"):
+            if k in g:
+                self.param_groups[0][k] = tuple(g[k]) if k == "betas" else float(g[k])
+        if float(g.get("weight_decay", 0.0)) != 0.0 or g.get("amsgrad", False):
+            raise NotImplementedError("weight_decay / amsgrad state")
+        self.betas, self.eps = tuple(self.param_groups[0]["betas"]), self.param_groups[0]["eps"]
+        ids = g["params"]
+        st = state_dict["state"]
+        steps = set()
+        self.m.zero_()
+        self.v.zero_()
+        for i, p, o in self._slices():
+            s = st.get(ids[i])
+            if not s:
+                continue
+            n = p.numel()
+            self.m[o:o + n].copy_(s["exp_avg"].reshape(-1))
+            self.v[o:o + n].copy_(s["exp_avg_sq"].reshape(-1))
+            steps.add(float(s["step"]))
+        if len(steps) > 1:
+            raise ValueError(f"per-parameter step counts differ: {sorted(steps)}")
+        c = steps.pop() if steps else 0.0
+        b1, b2 = self.betas
+        self._lr = None
+        self.sync_lr()
+        self.dev_state[0].fill_(c)
+        if c > 0:  # what adam_prepare_kernel left after step c
+            self.dev_state[1].fill_(self.lr / (1.0 - b1 ** c))
+            self.dev_state[2].fill_(math.sqrt(1.0 - b2 ** c))
 
 
 def masked_l1(preds, targets, lengths_dev, n_valid_frames, B, T, grad_scale=1.0,
@@ -229,6 +314,41 @@ def _bucketed(model, optimizer):
     return br
 
 
+def _interaction(optimizer, outs, y_main, y_sub, Dy, o, lens_dev, B, T, w, W, loss, g_lf0):
+    """log-F0 interaction loss (train_acoustic_multitrack.py:175-182): its weighted value into
+    its own scalar (kept for the metrics), added to ``loss``; gradients into g_lf0 (+=) and a
+    new sub-track buffer, returned."""
+    ys = y_sub.contiguous().float()
+    dev = y_main.device
+    g_sub = empty(B * T, device=dev)
+    part = empty(1024, device=dev)
+    il = torch.zeros(1, device=dev)
+    call("ensvs_lf0_interaction", outs["lf0"].data_ptr(), outs["lf0_sub"].data_ptr(),
+         y_main.data_ptr(), ys.data_ptr(), Dy, o[1], o[2], lens_dev.data_ptr(), B, T, float(w),
+         1.0 / W, part.data_ptr(), il.data_ptr(), g_lf0.data_ptr(), g_sub.data_ptr(), Ly.stream())
+    call("ensvs_axpy", loss.data_ptr(), il.data_ptr(), 1.0, 1, Ly.stream())
+    optimizer._il = (il, float(w))
+    return g_sub
+
+
+def step_metrics(loss, optimizer):
+    """The reference's per-step log metrics (train_acoustic_multitrack.py:382-390) of the last
+    train_step, as host floats: Loss, Loss_Feats, Loss_Pitch (pitch_reg_weight 0 in the
+    recipe), Loss_LogF0_Interaction (unweighted), Loss_MGC-0th_Interaction (0) and GradNorm
+    (only when finite: the reference skips the step and the metric otherwise).  Reads the
+    device (a sync); call it only when logging."""
+    total = float(loss.item())
+    il = getattr(optimizer, "_il", None)
+    wil = float(il[0].item()) if il is not None else 0.0
+    out = {"Loss": total, "Loss_Feats": total - wil, "Loss_Pitch": 0.0,
+           "Loss_LogF0_Interaction": wil / il[1] if il is not None else 0.0,
+           "Loss_MGC-0th_Interaction": 0.0}
+    gn = float(optimizer.norm.item())
+    if math.isfinite(gn):
+        out["GradNorm"] = gn
+    return out
+
+
 def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws=None,
                ddp=True, y_sub=None, logf0_diff_weight=0.0):
     """One training step on a (main, sub) pair batch.  Returns (loss, grad_norm) device tensors.
@@ -258,12 +378,14 @@ def train_step_single(model, optimizer, x, y, lengths, draws=None, ddp=True):
 def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws,
                     ddp, y_sub, logf0_diff_weight, overlap=False):
     """zero_grad + forward + masked L1 (+ interaction loss) + backward into the flat grads.
+    The weighted interaction term is also kept apart (optimizer._il) for the step metrics.
     An eval-mode model is switched to training mode (the reference's train_loop does this per
     phase, train_acoustic_multitrack.py:452); a training-mode model is left as it is, so
     BatchNorm modules frozen with bn.eval() stay frozen (running statistics, ensvs_bn_bwd_frozen)."""
     if not model.training:
         model.train()
     optimizer.zero_grad()
+    optimizer._il = None
     if logf0_diff_weight > 0.0 and (not model.output_subtrack or y_sub is None):
         raise ValueError("logf0_diff_weight > 0 needs output_subtrack=True and y_sub (the "
                          "SeparateF0 model: through its forward, with autograd)")
@@ -273,8 +395,8 @@ def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, 
                 getattr(model, "mgc_model", None) is not None and
                 hasattr(model.mgc_model, "denoise_fn")):
             reducer = _bucketed(model, optimizer)
-        loss = _loss_and_grads_fused(model, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
-                                     draws, ddp, y_sub, logf0_diff_weight, reducer)
+        loss = _loss_and_grads_fused(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub,
+                                     lengths, draws, ddp, y_sub, logf0_diff_weight, reducer)
         if reducer is not None:
             reducer.finish()
             optimizer._reduced = True
@@ -291,14 +413,8 @@ def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, 
     if logf0_diff_weight > 0.0:
         if not model.output_subtrack or y_sub is None:
             raise ValueError("logf0_diff_weight > 0 needs output_subtrack=True and y_sub")
-        y_sub = y_sub.contiguous().float()
-        g_sub = empty(B * T, device=y_main.device)
-        part = empty(1024, device=y_main.device)
-        call("ensvs_lf0_interaction", outs["lf0"].data_ptr(), outs["lf0_sub"].data_ptr(),
-             y_main.data_ptr(), y_sub.data_ptr(), Dy, o[1], o[2], st["lens_dev"].data_ptr(), B, T,
-             float(logf0_diff_weight), 1.0 / W, part.data_ptr(), loss.data_ptr(),
-             g["lf0"].data_ptr(), g_sub.data_ptr(), Ly.stream())
-        g["lf0_sub"] = g_sub
+        g["lf0_sub"] = _interaction(optimizer, outs, y_main, y_sub, Dy, o, st["lens_dev"], B, T,
+                                    logf0_diff_weight, W, loss, g["lf0"])
     model._train_bwd(st, g)
     return loss
 
@@ -316,8 +432,8 @@ def set_fused_branches(on: bool):
     _STATE_FUSED["on"] = bool(on)
 
 
-def _loss_and_grads_fused(model, x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws,
-                          ddp, y_sub, logf0_diff_weight, reducer=None):
+def _loss_and_grads_fused(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
+                          draws, ddp, y_sub, logf0_diff_weight, reducer=None):
     """The loss of _loss_and_grads split by branch: each branch's masked L1 over its own
     streams with the whole loss's element count (same gradients, elementwise), the
     interaction loss inside the lf0 branch; partial losses summed after the join."""
@@ -342,14 +458,8 @@ def _loss_and_grads_fused(model, x_main, x_sub, y_main, spk_main, spk_sub, lengt
                                 total_cols=total)
         g = {pt[2]: gi.view(-1) if i == 0 else gi}
         if i == 0 and logf0_diff_weight > 0.0:
-            ys = y_sub.contiguous().float()
-            g_sub = empty(B * T, device=y_main.device)
-            part = empty(1024, device=y_main.device)
-            call("ensvs_lf0_interaction", outs["lf0"].data_ptr(), outs["lf0_sub"].data_ptr(),
-                 y_main.data_ptr(), ys.data_ptr(), Dy, o[1], o[2], st["lens_dev"].data_ptr(), B,
-                 T, float(logf0_diff_weight), 1.0 / W, part.data_ptr(), loss.data_ptr(),
-                 g["lf0"].data_ptr(), g_sub.data_ptr(), Ly.stream())
-            g["lf0_sub"] = g_sub
+            g["lf0_sub"] = _interaction(optimizer, outs, y_main, y_sub, Dy, o, st["lens_dev"], B,
+                                        T, logf0_diff_weight, W, loss, g["lf0"])
         return loss, g
 
     loss, _ = model._train_fused(x_main, x_sub, y_main, spk_main, spk_sub, lengths, draws,
@@ -367,7 +477,7 @@ class GraphedTrainStep:
     collective on the flat gradient buffer), so data-parallel runs never depend on
     collective capture.  Each replay draws fresh diffusion steps, noise and dropout masks
     (ensvs_rng_advance) and takes the Adam step count and bias corrections from the
-    device (FusedAdam.state), so replay k is the k-th training step, not a repeat.
+    device (FusedAdam.dev_state), so replay k is the k-th training step, not a repeat.
 
     ``warmup`` eager steps (real optimizer steps) run first on the capture stream so
     every lazily built cache (packed-weight descriptors, workspaces, lengths) exists
@@ -437,6 +547,7 @@ class GraphedTrainStep:
             if dst is None or dst.shape != v.shape:
                 raise ValueError(f"{k}: shape {tuple(v.shape)} differs from the captured one")
             dst.copy_(v, non_blocking=True)
+        self.opt.sync_lr()  # a scheduler's lr change reaches the replayed update
         self.g_grads.replay()
         if self.ddp and world_size() > 1:
             allreduce_grads(self.opt.gflat)

@@ -48,7 +48,7 @@ def test_graphed_steps_bitwise_equal_eager(prec):
         for s in range(meta["steps"]):
             assert abs(graphed[s][0] - meta["losses"][s]) < 1e-5 * abs(meta["losses"][s])
     assert torch.equal(o_g.flat, o_e.flat) and torch.equal(o_g.m, o_e.m)
-    assert torch.equal(o_g.v, o_e.v) and torch.equal(o_g.state, o_e.state)
+    assert torch.equal(o_g.v, o_e.v) and torch.equal(o_g.dev_state, o_e.dev_state)
     assert o_g.device_step == len(seq)
     se, sg = m_e.state_dict(), m_g.state_dict()
     for k in se:

@@ -5,7 +5,7 @@ import torch
 
 from oracle import ensvs_oracle as O
 from ensemble_svs_with_interactions_amd import configs, engine
-from ensemble_svs_with_interactions_amd.train import FusedAdam, train_step
+from ensemble_svs_with_interactions_amd.train import FusedAdam, step_metrics, train_step
 from golden_util import (load_case, full_shapes, rel, grad_close, rel_l2, _pre_bn_bias,
                          sampled_grad_errors, record_errors)
 from gpu_util import build
@@ -124,6 +124,16 @@ def test_train_step_tiny_matches_reference(case):
               f"norm {norm.item():.6f} ref {meta['grad_norms'][s]:.6f}")
         assert abs(loss.item() - meta["losses"][s]) < 1e-5 * abs(meta["losses"][s])
         assert abs(norm.item() - meta["grad_norms"][s]) < 1e-4 * meta["grad_norms"][s]
+        # the reference's per-step log metrics (train_acoustic_multitrack.py:382-390)
+        mt = step_metrics(loss, opt)
+        assert mt["Loss"] == loss.item() and mt["GradNorm"] == norm.item()
+        if w_il > 0:
+            il = meta["interaction_losses"][s]
+            assert abs(mt["Loss_LogF0_Interaction"] - il) < 1e-5 * abs(il)
+            assert abs(mt["Loss_Feats"] + w_il * mt["Loss_LogF0_Interaction"] - mt["Loss"]) \
+                <= 1e-6 * abs(mt["Loss"])
+        else:
+            assert mt["Loss_LogF0_Interaction"] == 0.0 and mt["Loss_Feats"] == mt["Loss"]
         if s == 0:
             bad = []
             grads = {k: p.grad.detach().cpu() for k, p in model.named_parameters()}

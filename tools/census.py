@@ -24,10 +24,31 @@ SYNTH = len(sys.argv) > 2 and sys.argv[2] == "synth"
 VOC = len(sys.argv) > 2 and sys.argv[2] == "voc"
 POST = len(sys.argv) > 2 and sys.argv[2] in ("post", "vocleg")
 VOCLEG = len(sys.argv) > 2 and sys.argv[2] == "vocleg"
+ONLY = sys.argv[3] if len(sys.argv) > 3 else None  # rows of one branch only (lf0/mgc/bap/vuv)
 REC = []
 TAG = [None]
 ON = [False]
+BR = [None]  # branch index of the enclosing engine.Branches.on(i) region (None: outside)
+BR_NAMES = {0: "lf0", 1: "mgc", 2: "bap", 3: "vuv"}
 orig_call = _lib.call
+orig_on = engine.Branches.on
+
+
+class _br:
+    def __init__(self, ctx, i):
+        self.ctx, self.i = ctx, i
+
+    def __enter__(self):
+        self.old = BR[0]
+        BR[0] = self.i
+        return self.ctx.__enter__()
+
+    def __exit__(self, *exc):
+        BR[0] = self.old
+        return self.ctx.__exit__(*exc)
+
+
+engine.Branches.on = lambda self, i: _br(orig_on(self, i), i)
 
 
 def call(name, *args):
@@ -37,7 +58,7 @@ def call(name, *args):
     s.record()
     orig_call(name, *args)
     e.record()
-    REC.append((name, TAG[0], s, e))
+    REC.append((name, TAG[0], s, e, BR[0]))
 
 
 def tagged(fn, fmt):
@@ -181,14 +202,20 @@ def main():
 def report():
     agg = collections.defaultdict(lambda: [0, 0.0])
     tot = 0.0
-    for name, tag, s, e in REC:
+    per_br = collections.defaultdict(float)
+    for name, tag, s, e, br in REC:
         ms = s.elapsed_time(e)
         a = agg[(name, tag)]
         a[0] += 1
         a[1] += ms
         tot += ms
+        per_br[BR_NAMES.get(br, "other")] += ms
+        if ONLY and BR_NAMES.get(br, "other") != ONLY:
+            a[0] -= 1
+            a[1] -= ms
     print(f"{len(REC)} launches, {tot:.2f} ms (event-bracketed, serial eager "
           f"{'reverse diffusion' if SYNTH else ('vocoder' if VOC else ('post' if POST else 'step'))})")
+    print("per branch: " + "  ".join(f"{k} {v:.2f} ms" for k, v in sorted(per_br.items())))
     for (name, tag), (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:ROWS]:
         print(f"{ms:8.3f} ms {n:4d}x {ms / n * 1e3:8.1f} us  {name:28s} {tag or ''}")
 

@@ -85,10 +85,14 @@ def parse():
                     help="run the lf0/mgc/bap/vuv branches serially (no side streams)")
     ap.add_argument("--eager", action="store_true",
                     help="issue every kernel from the host each step (no HIP graph replay)")
-    ap.add_argument("--overlap-ddp", action="store_true",
-                    help="with N > 1 ranks, run eager steps whose bucketed all-reduce overlaps "
-                         "the backward (train.BucketedAllReduce) instead of replaying the HIP "
-                         "graphs with one whole-buffer all-reduce between them (the default)")
+    ap.add_argument("--no-overlap-ddp", action="store_true",
+                    help="with N > 1 ranks, replay the HIP graphs with one whole-buffer "
+                         "all-reduce between them instead of the default eager steps whose "
+                         "bucketed all-reduce overlaps the backward (train.BucketedAllReduce)")
+    ap.add_argument("--no-sf0", action="store_true",
+                    help="skip the recipe-default (MultiTrackMultistreamSeparateF0) leg")
+    ap.add_argument("--no-census", action="store_true",
+                    help="skip the per-launch census and kernel rooflines")
     ap.add_argument("--no-config2", action="store_true",
                     help="skip the single-track (BASELINE config 2) training leg")
     ap.add_argument("--cpu-pairs", type=int, default=10)
@@ -145,6 +149,148 @@ def gate_gemm_timing(model, P, T, dev, iters=20):
         gemm = total
     flops = 2.0 * M * (2 * C) * (3 * C + E)
     return gemm, total, flops
+
+
+def step_census(model, opt, batch):
+    """Per-launch census of one serial, eager training step (every libensvs entry point
+    bracketed by HIP events on its stream; GEMM / weight-gradient launches tagged with their
+    shape, recurrences with H or T): {(entry, tag): [launches, total ms]} and the serial
+    total.  Each kernel runs alone on the GPU, so these are the per-launch times a roofline
+    compares against; the step itself overlaps the four branches."""
+    import torch
+    from ensemble_svs_with_interactions_amd import _lib, kernels as K
+    import importlib
+    import pkgutil
+    import ensemble_svs_with_interactions_amd as pkg
+    rec, tag = [], [None]
+    orig_call, orig_gemm, orig_wgrad = _lib.call, K.gemm, K.wgrad
+
+    def call(name, *args):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        orig_call(name, *args)
+        e.record()
+        t = tag[0]
+        if name in ("ensvs_lstm_fwd", "ensvs_lstm_bwd"):
+            t = f"H={args[7]} T={args[6]}"
+        elif name == "ensvs_ardec_fwd":  # frames T: T / 4 autoregressive steps
+            t = f"H={args[15]} T={args[14]}"
+        elif name == "ensvs_ardec_bwd":
+            t = f"H={args[10]} T={args[9]}"
+        rec.append((name, t, s, e))
+
+    def tagged(fn, fmt):
+        def w(*a, **k):
+            old = tag[0]
+            tag[0] = fmt(*a, **k)
+            try:
+                return fn(*a, **k)
+            finally:
+                tag[0] = old
+        return w
+
+    def gemm_tag(segs, B, Tout, N, W, Y, ldy, **k):
+        sg = "+".join(f"{s.K}x{s.taps}{'b' if s.x.dtype == torch.bfloat16 else 'f'}"
+                      for s in segs)
+        return f"gemm M={B * Tout} N={N} K=[{sg}] epi={k.get('epi', 0)}"
+
+    def wgrad_tag(dy, ldy, x, ldx, B, Tout, Tin, N, Kc, taps, *a, **k):
+        return f"wgrad M={B * Tout} N={N} K={Kc}x{taps} {'b' if dy.dtype == torch.bfloat16 else 'f'}"
+
+    mods = [importlib.import_module(f"{pkg.__name__}.{m.name}")
+            for m in pkgutil.iter_modules(pkg.__path__) if not m.name.startswith("lib")]
+    patched = [m for m in mods if getattr(m, "call", None) is orig_call]
+    for m in patched:
+        m.call = call
+    _lib.call, K.gemm, K.wgrad = call, tagged(orig_gemm, gemm_tag), tagged(orig_wgrad, wgrad_tag)
+    engine.set_concurrency(False)
+    try:
+        torch.cuda.synchronize()
+        train_step(model, opt, *batch)
+        torch.cuda.synchronize()
+    finally:
+        for m in patched:
+            m.call = orig_call
+        _lib.call, K.gemm, K.wgrad = orig_call, orig_gemm, orig_wgrad
+        engine.set_concurrency(True)
+    agg = {}
+    for name, t, s, e in rec:
+        a = agg.setdefault((name, t), [0, 0.0])
+        a[0] += 1
+        a[1] += s.elapsed_time(e)
+    return agg, sum(v[1] for v in agg.values())
+
+
+# MI355X per-CU VALU rate (fp32 FMA: one wave64 instruction per 4 cycles per SIMD) at the
+# sustained MFMA clock: the issue floor of a recurrence step's dot products on its CU
+CU_FMA_PER_S = 64 * 2.4e9
+
+
+def kernel_rooflines(agg, serial_ms, P, T, C=256, E=256):
+    """Per-launch rooflines of the training step's largest kernels (census times): the mgc
+    DiffNet block's five GEMM launches with their algorithmic FLOPs and HBM bytes, and the
+    recurrences' ns per step against the VALU issue floor of their dot products."""
+    M = P * T
+    bf, f4 = 2, 4
+    w = lambda n, k: n * k * bf  # noqa: E731  packed bf16 weights
+    # (census tag, name, flops, algorithmic bytes) -- bytes as the production bf16 path moves
+    # them (DESIGN.md section 3): operands read once, taps re-read from cache
+    shapes = [
+        (("ensvs_conv_gemm_bf16a_out", f"gemm M={M} N={2 * C} K=[{C}x3b+{E}x1b] epi=1"),
+         "DiffNet gate GEMM (dilated conv + conditioner, GATE epilogue)",
+         2.0 * M * 2 * C * (3 * C + E),
+         M * (C + E) * bf + w(2 * C, 3 * C + E) + M * 2 * C * bf + M * C * bf),
+        (("ensvs_conv_gemm_bf16a_out", f"gemm M={M} N={2 * C} K=[{C}x1b] epi=2"),
+         "DiffNet res/skip GEMM (output projection, RESSKIP epilogue)",
+         2.0 * M * 2 * C * C,
+         M * C * bf + w(2 * C, C) + 2 * M * C * f4 + M * C * bf + 2 * M * C * f4),
+        (("ensvs_conv_gemm_bf16a_out", f"gemm M={M} N={C} K=[{C}x1b+{C}x1b] epi=3"),
+         "DiffNet gate-backward dgrad (GATE_BWD epilogue)",
+         2.0 * M * C * 2 * C,
+         2 * M * C * bf + w(C, 2 * C) + M * 2 * C * bf + M * 2 * C * bf),
+        (("ensvs_conv_gemm_bf16a_out", f"gemm M={M} N={C} K=[{2 * C}x3b] epi=4"),
+         "DiffNet dilated-conv dgrad (ADDSCALE epilogue)",
+         2.0 * M * C * 2 * C * 3,
+         M * 2 * C * bf + w(C, 6 * C) + 2 * M * C * f4 + M * C * bf),
+        (("ensvs_conv_wgrad_bf16", f"wgrad M={M} N={2 * C} K={C}x3 b"),
+         "DiffNet dilated-conv weight gradient",
+         2.0 * M * 2 * C * C * 3, M * 2 * C * bf + M * C * bf + 2 * C * 3 * C * f4),
+    ]
+    out = []
+    for key, name, flops, nbytes in shapes:
+        n, ms = agg.get(key, (0, 0.0))
+        if not n:
+            continue
+        sec = ms / n / 1e3
+        tf, gbs = flops / sec / 1e12, nbytes / sec / 1e9
+        mfma = flops / (PEAK_BF16_TFLOPS * 1e12) >= nbytes / (PEAK_HBM_GBS * 1e9)
+        out.append({"kernel": name, "tag": key[1], "launches_per_step": n,
+                    "us_per_launch": sec * 1e6, "flops": flops, "algorithmic_bytes": nbytes,
+                    "bound": "mfma" if mfma else "hbm",
+                    "achieved": tf if mfma else gbs, "unit": "TFLOP/s" if mfma else "GB/s",
+                    "peak": PEAK_BF16_TFLOPS if mfma else PEAK_HBM_GBS,
+                    "frac": tf / PEAK_BF16_TFLOPS if mfma else gbs / PEAK_HBM_GBS,
+                    "share_of_serial_step": ms / serial_ms})
+    rec = []
+    for (name, tag), (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        if name not in ("ensvs_lstm_fwd", "ensvs_lstm_bwd", "ensvs_ardec_fwd", "ensvs_ardec_bwd"):
+            continue
+        kv = dict(p.split("=") for p in tag.split())
+        H, steps = int(kv["H"]), int(kv["T"])
+        if name.startswith("ensvs_lstm"):
+            macs = 4 * H * H  # h_{t-1} W_hh^T (fwd) / dG W_hh (bwd), one sequence-direction
+        else:
+            # LSTMCell W_hh + the prenet column of W_ih + feat_out per AR step (r = 4 frames)
+            steps //= 4
+            macs = 4 * H * H + 4 * H + 4 * (H + 130)
+        floor_ns = macs / CU_FMA_PER_S * 1e9
+        ns = ms / n * 1e6 / steps
+        rec.append({"kernel": f"{name[6:]} H={H}", "launches_per_step": n, "ns_per_step": ns,
+                    "floor_ns_per_step": floor_ns, "floor": "VALU fp32 FMA issue of the "
+                    "recurrent dot products on one CU (latency-bound: one workgroup per "
+                    "sequence-direction)", "frac": floor_ns / ns,
+                    "share_of_serial_step": ms / serial_ms})
+    return out, rec
 
 
 def _median_time(fn, reps):
@@ -439,6 +585,36 @@ def il_train(args, dev):
                 grad_norm=norm.item())
 
 
+def sf0_train(args, dev, steps=4):
+    """The recipe's default acoustic model (MultiTrackMultistreamSeparateF0ParametricModel,
+    multitrack_acoustic_nnsvs_world_multi_ar_f0.yaml; config.yaml:93-95): concatenation-fusion
+    MultiTrackLSTMEncoder (H = 512 x 3 layers), teacher-forced multi-track lf0 model, main
+    and sub FFConvLSTM decoders (H = 256 / 64 / 62), masked L1 over both tracks; same
+    per-GPU workload, graph replay, bf16 GEMM operands.  276.5 MFLOP per frame (SURVEY.md
+    section 6); the reference CPU path trains it at ~290 frames/s (8 threads, SURVEY probe)."""
+    torch.manual_seed(20250324)
+    model = configs.instantiate(configs.multitrack_separate_f0(num_speakers=4)).to(dev)
+    opt = FusedAdam(model, lr=1e-4, clip_norm=1.0)
+    P, T = args.pairs, args.frames
+    b = data.synthetic_batch(P, T, 4000)
+    g = lambda k: torch.from_numpy(b[k]).to(dev).contiguous()  # noqa: E731
+    step = GraphedTrainStep(model, opt, g("x_main"), g("x_sub"), g("y_main"), g("spk_main"),
+                            g("spk_sub"), b["lengths"].tolist(), warmup=1).step
+    step()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for _ in range(steps):
+        loss, norm = step()
+    torch.cuda.synchronize()
+    el = time.time() - t0
+    v = P * T * steps / el
+    return dict(metric="recipe-default acoustic model train frames/sec (SeparateF0, "
+                       "MultiTrackLSTMEncoder H=512)", value=v, unit="main-track frames/s",
+                ms_per_step=el / steps * 1e3, steps=steps, pairs=P, frames=T,
+                dtype=engine.gemm_precision(), train_loss=loss.item(), grad_norm=norm.item(),
+                model_tflops_per_s=v * 276.5e6 / 1e12)
+
+
 def config2_train(args, dev):
     """BASELINE config 2: single-track NPSSMDNMultistreamParametricModel (teacher-forced
     lf0 decoder, both diffusions, V/UV) training steps, same per-GPU workload (pairs ->
@@ -497,10 +673,13 @@ def main():
             dist.init_process_group(be)
         world = dist.get_world_size()
         backend = dist.get_backend()
-        # the overlapped bucketed all-reduce runs in eager steps (the collectives stay out of
-        # the captured graphs; eager and graph replay measured the same at one GPU).  Opt-in:
-        # correct at world size 2 (tests/test_ddp_gpu.py) but not yet measured over RCCL
-        if args.overlap_ddp:
+        # the default data-parallel schedule: eager steps whose bucketed gradient all-reduce
+        # (lf0 / bap / V/UV at their branch end, the mgc DiffNet before the mgc encoder's
+        # backward) overlaps the rest of the backward; the collectives stay out of captured
+        # graphs.  Eager issue and graph replay measured the same at one GPU (the step is
+        # GPU-bound); tests/test_ddp_gpu.py pins the reduced gradient and DP = 1-process
+        # full batch.  --no-overlap-ddp: graph replay + one 94 MB all-reduce between graphs
+        if not args.no_overlap_ddp:
             args.eager = True
     engine.set_gemm_precision(args.precision)
     engine.set_concurrency(not args.serial)
@@ -551,9 +730,32 @@ def main():
             dist.destroy_process_group()
         return
     sec, sec_call, flops = gate_gemm_timing(model, P, T, dev)
-    achieved = flops / sec / 1e12
     net = model.mgc_model.denoise_fn
     gbytes = gate_gemm_bytes(P * T, net.C, net.E, 2 if args.precision == "bf16" else 4)
+    per_gpu = value / world
+    step_tf = per_gpu * TRAIN_FLOP_PER_FRAME / 1e12
+    peak_tf = PEAK_BF16_TFLOPS if args.precision == "bf16" else 157.3
+    roof = {
+        "scope": "the whole training step (every kernel of forward, backward, clip and Adam; "
+                 "the lf0 / mgc / bap / vuv branches on concurrent streams)",
+        "bound": "mfma", "achieved": step_tf, "peak": peak_tf, "unit": "TFLOP/s",
+        "frac": step_tf / peak_tf, "traffic": _committed("r3_step_pmc.json",
+                                                         "hbm_bytes_per_step"),
+        "traffic_source": "profiles/r3_step_pmc.json (rocprofv3 --pmc FETCH_SIZE x2 + "
+                          "WRITE_SIZE summed over one step's dispatches, separate passes; "
+                          "committed, not this run)",
+        "work": f"{TRAIN_FLOP_PER_FRAME / 1e6:.1f} MFLOP per main-track frame (GEMM / conv / "
+                "LSTM FLOPs of forward + backward, torch.utils.flop_counter on the oracle, "
+                "SURVEY.md section 8(d)) x frames/s per GPU",
+        "gate_gemm_live": _gate_roofline(args, P, T, sec, sec_call, flops, gbytes)}
+    if world == 1 and not args.no_census:
+        agg, serial_ms = step_census(model, opt, (xm, xs, ym, s0, s1, lens))
+        roof["kernels"], roof["recurrences"] = kernel_rooflines(agg, serial_ms, P, T)
+        rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
+        census = {"serial_step_ms": serial_ms, "launches": sum(v[0] for v in agg.values()),
+                  "rows": [[k[0][6:], k[1] or "", n, round(ms / n * 1e3, 1), round(ms, 3)]
+                           for k, (n, ms) in rows[:30]],
+                  "columns": ["entry", "shape", "launches", "us_per_launch", "ms_total"]}
     out = {
         "metric": "acoustic-model train frames/sec/GPU (4-track ensemble); synth RTF",
         "value": value, "unit": "main-track frames/s", "n_gpus": world, "steps": args.steps,
@@ -576,8 +778,12 @@ def main():
         # (acoustic_models._bn_only): executed work per frame is 0.59 MFLOP less
         "model_tflops_per_s": value * TRAIN_FLOP_PER_FRAME / 1e12,
         "executed_tflops_per_s": value * (TRAIN_FLOP_PER_FRAME - SUBTRACK_SKIPPED_FLOP) / 1e12,
-        "roofline": _gate_roofline(args, P, T, sec, sec_call, flops, gbytes),
+        "roofline": roof,
     }
+    if world == 1 and not args.no_census:
+        out["census"] = census
+    if not args.no_sf0 and world == 1:
+        out["separate_f0"] = sf0_train(args, dev)
     if not args.no_config2 and world == 1:
         out["config2"] = config2_train(args, dev)
         out["interaction_loss"] = il_train(args, dev)
@@ -617,11 +823,15 @@ def _gate_roofline(args, P, T, sec, sec_call, flops, gbytes):
 
 def _traffic():
     """HBM bytes per launch of the gate GEMM from the committed rocprofv3 PMC pass
-    (profiles/gate_gemm_pmc.json, written by tools/profile_round.sh), if any."""
-    p = os.path.join(ROOT, "profiles", "gate_gemm_pmc.json")
+    (profiles/gate_gemm_pmc.json, written by tools/round_run.sh), if any."""
+    return _committed("gate_gemm_pmc.json", "hbm_bytes_per_launch")
+
+
+def _committed(name, key):
+    p = os.path.join(ROOT, "profiles", name)
     if os.path.exists(p):
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            return json.load(f).get(key)
     return None
 
 

@@ -198,6 +198,8 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
         cols = [("ff", (0, F)), ("s0", (F, F + 1))]
         if self._NTRACKS == 2:
             cols.append(("s1", (F + 1, F + 2)))
+        # the score log-F0 column(s) as one forward operand (_conv_in)
+        cols.append(("lf0", (F, F + self._NTRACKS)))
         Ly.conv_register(pk, self.conv, first_cols=cols, first_bwd_cols=["ff"])
         Ly.lstm_register(pk, self.lstm)
         cell = self.decoder.lstm[0].cell
@@ -242,7 +244,7 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
             t, lds, off = ph_src
             call("ensvs_phoneme_ids", t.data_ptr() + 4 * off, lds, M, 0, ph1 - ph0, idv.data_ptr(),
                  Ly.stream())
-            K.gemm([K.Seg(X, ldx, Kin, pk["fc_in"], T)], B, T, E, pk.fwd, Y, E, accum=k > 0,
+            K.gemm([Ly.fc_in_seg(pk, X, ldx, Kin, M, T)], B, T, E, pk.fwd, Y, E, accum=k > 0,
                    **pk.bias_ptr_args("fc_in.b"))
             saved.append(dict(ids=idv, X=X, Kin=Kin, ldx=ldx))
             ids.append(idv)
@@ -251,6 +253,25 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
              ids[0].data_ptr(), ids[1].data_ptr() if two else None, ptr(spks[0]),
              ptr(spks[1]) if two else None, spk_ld, Ly.stream())
         return Y, saved
+
+    def _conv_in(self, pk, h, xs, ld, B, T, dev):
+        """conv.1's input columns [FF output, score log-F0 of each track]: the fp32 segments
+        (weight gradients) and, with bf16 operands, the forward's bf16 copies -- the FF
+        output, and the 1-2 log-F0 columns gathered into one zero-padded 8-wide operand, so
+        the k7 conv runs on the LDS-DMA kernel (K = 256 + 1 + 1 fails its K % 8 contract
+        as three segments: 182 us on the register-staged fp32 path at 30 x 1024 frames)."""
+        F, li, M = h.shape[1], self.in_lf0_idx, B * T
+        segs = [("ff", h, F, F, 0)] + [(f"s{k}", x, ld, 1, li) for k, x in enumerate(xs)]
+        if not K.bf16_operands(pk.fwd, M) or F % 8:
+            return segs, None
+        hb = K.cast_bf16(h, F, F, M)
+        cols = empty(M, len(xs), device=dev)
+        for k, x in enumerate(xs):
+            call("ensvs_copy_cols", x.data_ptr() + 4 * li, ld, cols.data_ptr() + 4 * k,
+                 len(xs), M, 1, Ly.stream())
+        lb = K.cast_bf16(cols, len(xs), len(xs), M,
+                         out=torch.empty(M, 8, dtype=torch.bfloat16, device=dev), out_ld=8)
+        return segs, [("ff", hb, F, F), ("lf0", lb, 8, len(xs))]
 
     def _fwd(self, xs, ld, B, T, lens_dev, spks=(None, None), spk_ld=0, masks=None,
              training=None, save=True, teacher=None):
@@ -265,11 +286,9 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
         li = self.in_lf0_idx
         X0, esv = self._embed(pk, xs, ld, B, T, spks, spk_ld, dev)
         hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
-        F = hs[2].shape[1]
-        segs = [("ff", hs[2], F, F, 0), ("s0", xs[0], ld, 1, li)]
-        if len(xs) == 2:
-            segs.append(("s1", xs[1], ld, 1, li))
-        a, csv = Ly.conv_fwd(pk, self.conv, segs, B, T, dev, training, save=save)
+        segs, b16 = self._conv_in(pk, hs[2], xs, ld, B, T, dev)
+        a, csv = Ly.conv_fwd(pk, self.conv, segs, B, T, dev, training, save=save,
+                             first_b16=b16)
         C = a.shape[1]
         y, lsv = Ly.lstm_fwd(pk, self.lstm, a, C, B, T, lens_dev, dev, None, save=save)
         dec = self.decoder
@@ -439,9 +458,8 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BiLSTMResF0NonAttentiveDecoder):
         li = self.in_lf0_idx
         X0, _ = self._embed(pk, [x_main, x_sub], ld, B, T, [s_main, s_sub], spk_ld, dev)
         hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
-        F = hs[2].shape[1]
-        Ly.conv_fwd(pk, self.conv, [("ff", hs[2], F, F, 0), ("s0", x_main, ld, 1, li),
-                                    ("s1", x_sub, ld, 1, li)], B, T, dev, True, save=False)
+        segs, b16 = self._conv_in(pk, hs[2], [x_main, x_sub], ld, B, T, dev)
+        Ly.conv_fwd(pk, self.conv, segs, B, T, dev, True, save=False, first_b16=b16)
 
     # ---------------------------------------------------------------- reference API
     def forward(self, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths=None, y=None):

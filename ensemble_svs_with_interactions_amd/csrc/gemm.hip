@@ -2366,6 +2366,149 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
   }
 }
 
+// ------------------------------------ weight grads, fp32 operands, deep register prefetch
+// wgrad_kernel<bf16, VEC> with WR chunks of fp32 rows in flight per thread instead of one.
+// A 32-frame chunk is 16 MFMAs per wave: with one chunk loading behind one computing, every
+// chunk's HBM/L2 latency was exposed (N = 256, K = 64: 31.6 us for 39 MB, ~1.2 TB/s).  Here
+// chunk c lives in register slot c % WR from its load until it is rounded into the LDS image,
+// so WR - 1 chunks stay in flight while one is multiplied.  Same staging rounding, the same
+// LDS images and the same MFMA order as wgrad_kernel<bf16>: identical bits.
+constexpr int WR = 3;
+
+template <bool HAS_R>
+__global__ __launch_bounds__(NTHR, 2) void wgrad_f32r_kernel(const WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int IMG = BK * 256;  // bytes per bf16 operand image (32 frames x 128 channels)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int n0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
+  const int j = blockIdx.z % a.taps, s = blockIdx.z / a.taps;
+  const int mbeg = s * a.rows_per_split;
+  const int mend = min(a.M, mbeg + a.rows_per_split);
+  const int nch = mbeg < mend ? (mend - mbeg + BK - 1) / BK : 0;
+  int fb[4], ft[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mbeg + ((tid + NTHR * i) >> 5);
+    fb[i] = m / a.Tout;
+    ft[i] = m - fb[i] * a.Tout;
+  }
+  f32x4 ra[WR][4], rx[WR][4], rr[WR][HAS_R ? 4 : 1];
+  // chunk ch's rows into ring slot S (S is a compile-time constant at every call site)
+  auto load = [&](int ch, f32x4 (&A)[4], f32x4 (&X)[4], f32x4 (&RR)[HAS_R ? 4 : 1])
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = tid + NTHR * i, f = q >> 5, c4 = q & 31;
+      const int m = mbeg + ch * BK + f;
+      const bool mv = m < mend;
+      const int b = fb[i], t = ft[i];
+      const int n = n0 + c4 * 4, k = k0 + c4 * 4;
+      const int src = pad_src(t + a.shift0 + j * a.dil, a.Tin, a.pad);
+      const bool kq = mv && src >= 0 && k < a.K;
+      A[i] = *(const f32x4*)((mv && n < a.N) ? a.dy + (long long)m * a.ldy + n : g_zero);
+      X[i] = *(const f32x4*)(kq ? a.x + (long long)(b * a.Tin + src) * a.ldx + k : g_zero);
+      if constexpr (HAS_R) RR[i] = *(const f32x4*)(kq ? a.radd + (long long)b * a.radd_ld + k
+                                                      : g_zero);
+      int nt = t + BK, nb = b;
+      while (nt >= a.Tout) {
+        nt -= a.Tout;
+        ++nb;
+      }
+      fb[i] = nb;
+      ft[i] = nt;
+    }
+  };
+  auto store = [&](int buf, const f32x4 (&A)[4], const f32x4 (&X)[4],
+                   const f32x4 (&RR)[HAS_R ? 4 : 1]) __attribute__((always_inline)) {
+    char* As = smem + buf * 2 * IMG;
+    char* Bs = As + IMG;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = tid + NTHR * i, f = q >> 5, c4 = q & 31;
+      f32x4 xv = X[i];
+      if constexpr (HAS_R) xv += RR[i];
+      const int o = wg_off(f, c4 >> 1) + 8 * (c4 & 1);
+      *(bf16x4*)(As + o) = bf16x4{(__bf16)A[i][0], (__bf16)A[i][1], (__bf16)A[i][2],
+                                  (__bf16)A[i][3]};
+      *(bf16x4*)(Bs + o) = bf16x4{(__bf16)xv[0], (__bf16)xv[1], (__bf16)xv[2], (__bf16)xv[3]};
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const char* As = smem + buf * 2 * IMG;
+    const char* Bs = As + IMG;
+    bf16x8 fa[4], fbv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i] = wg_frag(As, wr * 64 + i * 16, lane);
+      fbv[i] = wg_frag(Bs, wc * 64 + i * 16, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fbv[jj], acc[i][jj], 0, 0, 0);
+  };
+  // Loads and stores are unconditional (chunks past the split read zeros through g_zero):
+  // a conditional load makes the waitcnt pass assume it may be missing and drain the ring
+  // (vmcnt(0) before every store) instead of waiting for one chunk (vmcnt(16)).
+#pragma unroll
+  for (int p = 0; p < WR; ++p) load(p, ra[p], rx[p], rr[p]);
+  store(0, ra[0], rx[0], rr[0]);
+  load(WR, ra[0], rx[0], rr[0]);
+  __syncthreads();
+  for (int c0 = 0; c0 < nch; c0 += WR) {
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+      const int ch = c0 + r;
+      if (ch >= nch) break;
+      const int ns = (r + 1) % WR;  // ring slot of chunk ch + 1 (constant after unrolling)
+      // buffer (ch + 1) & 1 was last read by chunk ch - 1, before the previous barrier
+      store((ch + 1) & 1, ra[ns], rx[ns], rr[ns]);
+      load(ch + 1 + WR, ra[ns], rx[ns], rr[ns]);
+      compute(ch & 1);
+      __syncthreads();
+    }
+  }
+  if (a.splits == 1) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int k = k0 + wc * 64 + nt * 16 + (lane & 15);
+      if (k >= a.K) continue;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + wr * 64 + mt * 16 + (lane >> 4) * 4 + r;
+          if (n < a.N) {
+            float* d = a.dst + n * a.sn + k * a.sk + j * a.sj;
+            const float v = acc[mt][nt][r] * a.scale;
+            *d = a.accum ? *d + v : v;
+          }
+        }
+    }
+    return;
+  }
+  float* out = a.part + ((long long)(s * a.taps + j) * a.N) * a.K;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int k = k0 + wc * 64 + nt * 16 + (lane & 15);
+    if (k >= a.K) continue;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wr * 64 + mt * 16 + (lane >> 4) * 4 + r;
+        if (n < a.N) out[(long long)n * a.K + k] = acc[mt][nt][r];
+      }
+  }
+}
+
 // ------------------------------------------------- weight grads, bf16 operands
 // wgrad_kernel<bf16> with dy and x already rounded to bf16 in HBM (the staging rounding of
 // wgrad_kernel, so the result is bit-identical): both [32 frames][128 channels] images
@@ -3239,7 +3382,11 @@ ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DT_BF16) {
     size_t lds = 2 * 2 * BK * 256;
-    if (vec)
+    static const int ring = getenv("ENSVS_WGRAD_RING") ? atoi(getenv("ENSVS_WGRAD_RING")) : 1;
+    // (with radd the ring's extra registers spill: that rare case keeps one chunk in flight)
+    if (vec && ring && !radd)
+      hipLaunchKernelGGL((wgrad_f32r_kernel<false>), grid, dim3(NTHR), lds, st, a);
+    else if (vec)
       hipLaunchKernelGGL((wgrad_kernel<__bf16, true>), grid, dim3(NTHR), lds, st, a);
     else
       hipLaunchKernelGGL((wgrad_kernel<__bf16, false>), grid, dim3(NTHR), lds, st, a);

@@ -121,6 +121,19 @@ def gather_input(sources, ph0, ph1, M, device):
     return ph_src, X, Kin, ldx
 
 
+def fc_in_seg(pk, X, ldx, Kin, M, T):
+    """GEMM operand of the phoneme-input Linear: with bf16 operands a zero-padded bf16 copy
+    (K = in_dim - 47 is not a multiple of 8, which would leave the launch on the
+    register-staged fp32 kernel: 38.6 us at 30 x 1024 frames)."""
+    if Kin % 8 and K.bf16_operands(pk.fwd, M):
+        ld8 = (Kin + 7) // 8 * 8
+        xb = K.cast_bf16(X, ldx, Kin, M,
+                         out=torch.empty(M, ld8, dtype=torch.bfloat16, device=X.device),
+                         out_ld=ld8)
+        return K.Seg(xb, ld8, Kin, pk["fc_in"], T)
+    return K.Seg(X, ldx, Kin, pk["fc_in"], T)
+
+
 def embed_fwd(pk, emb_weight, sources, ph0, ph1, B, T, spk_seq=None, spk_ld=0, device=None,
               out=None):
     """x = emb(argmax onehot) + fc_in(other cols) [+ spk]  -> (M, E); returns saved dict.
@@ -135,7 +148,7 @@ def embed_fwd(pk, emb_weight, sources, ph0, ph1, B, T, spk_seq=None, spk_ld=0, d
         Y, ldY, col = empty(M, E, device=device), E, 0
     else:
         Y, ldY, col = out
-    K.gemm([K.Seg(X, ldx, Kin, pk["fc_in"], T)], B, T, E, pk.fwd, Y, ldY, yoff=col,
+    K.gemm([fc_in_seg(pk, X, ldx, Kin, M, T)], B, T, E, pk.fwd, Y, ldY, yoff=col,
            **pk.bias_ptr_args("fc_in.b"))
     call("ensvs_embed_add", Y.data_ptr() + 4 * col, ldY, M, E, T, emb_weight.data_ptr(),
          ids.data_ptr(), None, ptr(spk_seq), None, spk_ld, stream())
@@ -213,7 +226,8 @@ CONV_IDX = ((1, 2), (5, 6), (9, 10))
 
 
 def conv_register(pk, conv, first_cols=None, first_bwd_cols=None):
-    """first_cols: list of (name, (c0, c1)) input-column ranges of conv.1 (segments)."""
+    """first_cols: list of (name, (c0, c1)) input-column ranges of conv.1 (segments; ranges
+    may overlap: a forward-only operand over several narrow segments' columns)."""
     for li, (ci, bi) in enumerate(CONV_IDX):
         w = conv[ci].weight
         if li == 0 and first_cols is not None:
@@ -226,24 +240,30 @@ def conv_register(pk, conv, first_cols=None, first_bwd_cols=None):
 
 
 def conv_fwd(pk, conv, first_segs, B, T, device, training, groups=1, save=True,
-             update_running=True, running_updates=1):
+             update_running=True, running_updates=1, first_b16=None):
     """first_segs: list of (name, tensor, ld, K, xoff) for conv.1.  Returns (out, saved).
     running_updates: BatchNorm running-statistic updates with this batch's statistics (2
-    stands for a second call of the stack on the same input whose outputs are unused)."""
+    stands for a second call of the stack on the same input whose outputs are unused).
+    first_b16: optional list of (name, bf16 tensor, ld, K) operands of conv.1's forward GEMM
+    in place of first_segs (caller-rounded copies, e.g. narrow columns gathered into one
+    zero-padded segment); first_segs stay the fp32 inputs of the weight gradient."""
     M = B * T
     Mg = M // groups
     sv = []
     segs = [K.Seg(t, ld, Kc, pk[f"conv1@{name}"] if name else pk["conv1"], T, taps=7, dil=1,
                   shift0=-3, pad=_lib.PAD_REFLECT, xoff=xoff)
             for (name, t, ld, Kc, xoff) in first_segs]
+    fsegs = segs if first_b16 is None else [
+        K.Seg(t, ld, Kc, pk[f"conv1@{name}"], T, taps=7, dil=1, shift0=-3, pad=_lib.PAD_REFLECT)
+        for (name, t, ld, Kc) in first_b16]
     a = None
     for li, (ci, bi) in enumerate(CONV_IDX):
         C = conv[ci].weight.shape[0]
         if li > 0:
-            segs = [K.Seg(a, C_prev, C_prev, pk[f"conv{ci}"], T, taps=7, dil=1, shift0=-3,
-                          pad=_lib.PAD_REFLECT)]
+            segs = fsegs = [K.Seg(a, C_prev, C_prev, pk[f"conv{ci}"], T, taps=7, dil=1,
+                                  shift0=-3, pad=_lib.PAD_REFLECT)]
         y = empty(M, C, device=device)
-        K.gemm(segs, B, T, C, pk.fwd, y, C, **pk.bias_ptr_args(f"conv{ci}.b"))
+        K.gemm(fsegs, B, T, C, pk.fwd, y, C, **pk.bias_ptr_args(f"conv{ci}.b"))
         bn = conv[bi]
         mean = empty(groups, C, device=device)
         rstd = empty(groups, C, device=device)

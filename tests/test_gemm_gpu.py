@@ -179,6 +179,34 @@ def test_wgrad_radd_tiles_splits(dt, tol, splits):
     assert rel(dw - dw0, 0.5 * w.grad) < tol
 
 
+@pytest.mark.parametrize("shape", [(30, 1024, 64, 256, 1, 1, L.PAD_ZERO),
+                                   (4, 333, 256, 512, 1, 1, L.PAD_ZERO),
+                                   (3, 517, 128, 128, 7, 1, L.PAD_REFLECT),
+                                   (5, 200, 256, 256, 3, 4, L.PAD_ZERO)])
+@pytest.mark.parametrize("splits", [1, 5, None])
+def test_wgrad_fp32_source_bitwise_equals_bf16_operands(shape, splits):
+    """The fp32-operand weight gradient in production precision (rows rounded to bf16 while
+    staged; the deep-prefetch ring kernel) gives the same bits as the bf16-operand kernel on
+    pre-rounded copies (ensvs_cast_bf16), incl. ragged M, taps/padding and split reduction."""
+    torch.manual_seed(11)
+    B, T, Cin, Cout, taps, dil, pad = shape
+    M = B * T
+    x = torch.randn(M, Cin, device=DEV)
+    g = torch.randn(M, Cout, device=DEV)
+    outs = []
+    for b16 in (False, True):
+        dw = torch.full((Cout, Cin, taps), 0.25, device=DEV)
+        xs, gs = (K.cast_bf16(x, Cin, Cin, M), K.cast_bf16(g, Cout, Cout, M)) if b16 else (x, g)
+        K.wgrad(gs, Cout, xs, Cin, B, T, T, Cout, Cin, taps, dil, -dil * (taps // 2), pad, dw,
+                Cin * taps, taps, 1, dtype=L.DT_BF16, accum=True, scale=0.5, splits=splits)
+        outs.append(dw)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = torch.einsum("mn,mk->nk", g.double(), x.double()).float() if taps == 1 else None
+    if ref is not None:
+        assert rel(outs[0][:, :, 0] - 0.25, 0.5 * ref) < 2e-2
+
+
 def test_colsum_vectorized_tail():
     torch.manual_seed(6)
     y = torch.randn(5000, 128, device=DEV)

@@ -89,6 +89,13 @@ SIGNATURES = {
     "ensvs_lstm_set_step": [c_int],
     "ensvs_lstm_bwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int,
                        c_vp, c_ll, c_vp],
+    "ensvs_lstm_coop_supported": [c_int, c_int],
+    "ensvs_lstm_coop_work_bytes": [c_int],
+    "ensvs_lstm_coop_pack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
+    "ensvs_lstm_coop_fwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
+                            c_ll, c_vp],
+    "ensvs_lstm_coop_bwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp,
+                            c_ll, c_vp],
     "ensvs_ardec_pack": [c_vp, c_int, c_vp, c_vp, c_vp],
     "ensvs_ardec_fwd": [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
                         c_vp, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp,
@@ -132,6 +139,7 @@ SIGNATURES = {
                         c_vp, c_vp],
     "ensvs_rng_advance": [c_vp],
     "ensvs_copy_cols": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_vp],
+    "ensvs_regroup_cols": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_int, c_int, c_vp],
     "ensvs_axpy": [c_vp, c_vp, c_float, c_ll, c_vp],
     "ensvs_axpy_strided": [c_vp, c_ll, c_vp, c_ll, c_float, c_int, c_int, c_vp],
     "ensvs_axpy_blocks2d": [c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_float, c_int, c_int, c_int,
@@ -192,7 +200,8 @@ SIGNATURES = {
 
 # entry points returning a value instead of a status code
 RESTYPES = {"ensvs_embed_bwd_workspace": c_ll, "ensvs_usf_source_workspace": c_ll,
-            "ensvs_attn_table_grad_workspace": c_ll, "ensvs_lstm_bwd_work_floats": c_ll}
+            "ensvs_attn_table_grad_workspace": c_ll, "ensvs_lstm_bwd_work_floats": c_ll,
+            "ensvs_lstm_coop_work_bytes": c_ll, "ensvs_lstm_coop_supported": ctypes.c_int}
 
 _lib = None
 

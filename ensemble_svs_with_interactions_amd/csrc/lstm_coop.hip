@@ -1,0 +1,487 @@
+// Cooperative bidirectional LSTM recurrence for the large hidden sizes (H = 256, 512: the
+// MultiTrackLSTMEncoder and the decoders of the recipe-default SeparateF0 model,
+// nnsvs/model.py:1435-1537, 862-869) in production (bf16 GEMM) precision.
+//
+// Same contract as lstm.hip's ensvs_lstm_fwd / ensvs_lstm_bwd (packed sequences, zero state,
+// zero outputs past each length, saved [B*T][2][5H] = i f g o c).  W_hh (4 MB fp32 per
+// direction at H = 512) does not fit one CU, and the per-step kernels of lstm.hip re-launch
+// and re-read it from L2 every step (17.5 / 52 us per step forward / backward at H = 512).
+// Here one launch runs every step:
+//   * each direction is split over NW = H / 16 workgroups; workgroup w owns hidden units
+//     [16 w, 16 w + 16) and holds their 64 gate rows of W_hh (forward) or their 16 columns
+//     (backward: dh = W_hh^T dG) as MFMA A fragments in VGPRs for the whole sequence;
+//   * the <= 32 sequences are the MFMA N dimension (two 16-column tiles), the K dimension is
+//     split over the four waves and their partial sums are added through LDS;
+//   * the recurrent products run in fp16 (forward: h in [-1, 1]) / bf16 (backward: dG spans
+//     many decades) with fp32 accumulation -- as the reference recipe's fp16 autocast runs its
+//     cuDNN LSTM (myconfig_notuseIL.yaml:6) -- while gates, cell state and every saved value
+//     stay fp32; the fp32 parity mode keeps lstm.hip's exact kernels;
+//   * h_t (fp16) / dG_t (bf16) is handed to every workgroup of the direction through a
+//     double-buffered slab in the caller's workspace: 16-B sc1 stores, s_waitcnt vmcnt(0) of
+//     every storing wave, then one agent-scope counter add per workgroup; readers poll the
+//     counter with sc1 loads and read the slab with sc1 loads only (the hand-off form of
+//     MI355X_MICROARCH.md, "Hand-offs measured with sc1 loads", first row).
+// Every workgroup of the grid must be resident at once (2 NW <= 64 workgroups, one per CU);
+// the polls are bounded, so a grid that cannot become resident ends (flagging the error word
+// of the workspace) instead of hanging.
+#include "common.h"
+#include "ensvs.h"
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_;
+
+namespace {
+
+constexpr int NT = 256;     // 4 waves
+constexpr int UW = 16;      // hidden units per workgroup
+constexpr int SB = 32;      // sequence columns: two MFMA N tiles
+constexpr int PSF = 68;     // forward partial-sum row per sequence: 64 gate rows + 4 (banks)
+constexpr int PSB = 20;     // backward: 16 units + 4
+constexpr int CP_SC1 = 16;  // buffer-op cache policy: sc1 (L1 bypass on both sides)
+constexpr int HDR = 256;    // workspace header: counters (one 64-B line per direction), error
+constexpr unsigned SPIN_MAX = 1u << 24;
+
+__device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_fast(float x) {
+  return fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)), 1.f);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab(unsigned* work, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((char*)work + HDR, 0, bytes, 0x00020000);
+}
+
+// wait until the direction's counter reaches `target` (one lane), then release the workgroup
+__device__ __forceinline__ void wait_count(unsigned* work, int d, unsigned target) {
+  if (threadIdx.x == 0) {
+    unsigned* cnt = work + d * 16;
+    unsigned it = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++it == SPIN_MAX) {  // a workgroup never arrived: flag it and go on
+        __hip_atomic_store(work + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void signal(unsigned* work, int d) {
+  __hip_atomic_fetch_add(work + d * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int H> struct CGeo {
+  static constexpr int NW = H / UW;       // workgroups per direction
+  static constexpr int KCW = H / 128;     // forward: 32-deep K chunks per wave (K = H)
+  static constexpr int KCBW = H / 32;     // backward: per wave (K = 4H)
+  static constexpr int FX = 2 * 2 * SB * H * 2;      // forward slab bytes: [dir][buf][s][H] f16
+  static constexpr int BX = 2 * 2 * SB * 4 * H * 2;  // backward: [dir][buf][s][4H] bf16
+  static_assert(H % 128 == 0, "H");
+};
+
+// W_hh [4H][H] fp32 (both directions) -> forward A fragments
+// [dir][w][wave][mt][kk][lane][8] fp16: row m = lane & 15 of tile mt is unit 16 w + 4 mt + m / 4,
+// gate m % 4; k = (wave KCW + kk) 32 + 8 (lane >> 4) + j.
+template <int H>
+__global__ void coop_pack_fwd_kernel(const float* __restrict__ w0, const float* __restrict__ w1,
+                                     _Float16* __restrict__ out) {
+  using G = CGeo<H>;
+  const int n = 2 * 4 * H * H;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int j = i & 7, lane = (i >> 3) & 63;
+    int r = i >> 9;
+    const int kk = r % G::KCW; r /= G::KCW;
+    const int mt = r % 4; r /= 4;
+    const int wv = r % 4; r /= 4;
+    const int w = r % G::NW, d = r / G::NW;
+    const int m = lane & 15, u = w * UW + 4 * mt + m / 4, g = m % 4;
+    const int k = (wv * G::KCW + kk) * 32 + 8 * (lane >> 4) + j;
+    out[i] = (_Float16)(d ? w1 : w0)[(long long)(g * H + u) * H + k];
+  }
+}
+
+// backward A fragments of W_hh^T [dir][w][wave][kk][lane][8] bf16: row m = lane & 15 is unit
+// 16 w + m; k = n' = (wave KCBW + kk) 32 + 8 (lane >> 4) + j in the dG slab's order
+// n' = 64 w' + 4 u' + g (workgroup-major, unit-major inside), i.e. gate row g H + 16 w' + u'.
+template <int H>
+__global__ void coop_pack_bwd_kernel(const float* __restrict__ w0, const float* __restrict__ w1,
+                                     __bf16* __restrict__ out) {
+  using G = CGeo<H>;
+  const int n = 2 * 4 * H * H;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int j = i & 7, lane = (i >> 3) & 63;
+    int r = i >> 9;
+    const int kk = r % G::KCBW; r /= G::KCBW;
+    const int wv = r % 4; r /= 4;
+    const int w = r % G::NW, d = r / G::NW;
+    const int u = w * UW + (lane & 15);
+    const int np = (wv * G::KCBW + kk) * 32 + 8 * (lane >> 4) + j;
+    const int row = (np % 4) * H + (np / 64) * UW + (np % 64) / 4;
+    out[i] = (__bf16)(d ? w1 : w0)[(long long)row * H + u];
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
+    const float* __restrict__ gx, int ldg,     // [B*T][ldg], dir d gate g unit u at d 4H + g H + u
+    const f16x8* __restrict__ wp,              // packed forward fragments
+    const long long* __restrict__ lengths, int B, int T,
+    float* __restrict__ y, int ldy,            // [B*T][ldy], dir d at d H + u
+    float* __restrict__ sv,                    // [B*T][2][5H]
+    unsigned* __restrict__ work) {
+  using G = CGeo<H>;
+  constexpr int KCW = G::KCW, NW = G::NW;
+  __shared__ __attribute__((aligned(16))) float part[4 * SB * PSF];
+  __shared__ __attribute__((aligned(16))) _Float16 hs[SB * UW];
+  __shared__ int sL[SB];
+  const int d = blockIdx.y, w = blockIdx.x, u0 = w * UW;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < SB) sL[tid] = tid < B ? (int)lengths[tid] : 0;
+
+  f16x8 wf[4][KCW];
+  {
+    const f16x8* src = wp + (((long long)(d * NW + w) * 4 + wv) * 4 * KCW) * 64 + lane;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int kk = 0; kk < KCW; ++kk) wf[mt][kk] = src[(mt * KCW + kk) * 64];
+  }
+  __syncthreads();
+  int maxL = 0;
+  for (int s = 0; s < B; ++s) maxL = max(maxL, sL[s]);
+  // pad_packed_sequence: this workgroup's output columns past each sequence's end are zero
+  for (int s = 0; s < B; ++s) {
+    const int L = sL[s];
+    for (int i = tid; i < (T - L) * UW; i += NT)
+      y[((long long)s * T + L + i / UW) * ldy + d * H + u0 + i % UW] = 0.f;
+  }
+  const __amdgpu_buffer_rsrc_t xr = slab(work, G::FX);
+
+  // cell pairs: (unit u = p & 15, sequence s = p >> 4), p = tid + 256 i
+  int cs[2], cu[2];
+  long long grow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = tid + NT * i;
+    cu[i] = p & 15;
+    cs[i] = p >> 4;
+  }
+  auto in_row = [&](int i, int t) -> long long {  // clamped: always a readable row
+    const int sc = min(cs[i], B - 1), L = sL[sc];
+    const int tt = max(min(t, L - 1), 0);
+    return (long long)sc * T + (d ? max(L - 1 - tt, 0) : tt);
+  };
+  float gin[2][4], cst[2] = {0.f, 0.f};
+  auto load_in = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      grow[i] = in_row(i, t);
+      const float* src = gx + grow[i] * ldg + d * 4 * H + u0 + cu[i];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) gin[i][g] = src[g * H];
+    }
+  };
+  load_in(0);
+
+  for (int t = 0; t < maxL; ++t) {
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (t > 0) {
+      wait_count(work, d, (unsigned)(NW * t));
+      f16x8 bf[KCW][2];
+#pragma unroll
+      for (int kk = 0; kk < KCW; ++kk)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int off = (((d * 2 + ((t - 1) & 1)) * SB + nt * 16 + (lane & 15)) * H +
+                           (wv * KCW + kk) * 32 + 8 * (lane >> 4)) * 2;
+          bf[kk][nt] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, CP_SC1));
+        }
+      // all slab loads in flight together (one L2 round trip), then the MFMAs
+#pragma unroll
+      for (int kk = 0; kk < KCW; ++kk)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
+#pragma unroll
+      for (int kk = 0; kk < KCW; ++kk)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[mt][kk], bf[kk][nt], acc[mt][nt], 0, 0, 0);
+    }
+    // partial sums: lane holds gate rows 16 mt + 4 (lane >> 4) + r of sequence 16 nt + (lane & 15)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * PSF + 16 * mt + 4 * (lane >> 4)] = acc[mt][nt];
+    __syncthreads();
+    float out[2][6];
+    bool val[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int s = cs[i], u = cu[i];
+      f32x4 a = *(const f32x4*)&part[s * PSF + 4 * u];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) a += *(const f32x4*)&part[(q * SB + s) * PSF + 4 * u];
+      const float ig = sigm(a[0] + gin[i][0]), fg = sigm(a[1] + gin[i][1]);
+      const float gg = tanh_fast(a[2] + gin[i][2]), og = sigm(a[3] + gin[i][3]);
+      const float cn = fg * cst[i] + ig * gg;
+      const float h = og * tanh_fast(cn);
+      val[i] = t < sL[s];
+      cst[i] = cn;
+      hs[s * UW + u] = (_Float16)(val[i] ? h : 0.f);
+      out[i][0] = h; out[i][1] = ig; out[i][2] = fg; out[i][3] = gg; out[i][4] = og; out[i][5] = cn;
+    }
+    __syncthreads();
+    if (wv == 0) {  // publish h_t: 32 sequences x 16 units, one 16-B sc1 store per lane
+      const f32x4 v = *(const f32x4*)&hs[(lane >> 1) * UW + (lane & 1) * 8];
+      const int off = (((d * 2 + (t & 1)) * SB + (lane >> 1)) * H + u0 + (lane & 1) * 8) * 2;
+      __builtin_amdgcn_raw_buffer_store_b128(v, xr, off, 0, CP_SC1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) signal(work, d);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (val[i]) {
+        const long long row = grow[i];
+        const int j = u0 + cu[i];
+        y[row * ldy + d * H + j] = out[i][0];
+        float* o = sv + (row * 2 + d) * 5 * H + j;
+#pragma unroll
+        for (int g = 0; g < 5; ++g) o[g * H] = out[i][1 + g];
+      }
+    if (t + 1 < maxL) load_in(t + 1);
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
+    const float* __restrict__ dy, int lddy,    // [B*T][lddy], grad of outputs
+    const bf16x8* __restrict__ wp,             // packed backward fragments
+    const long long* __restrict__ lengths, int B, int T,
+    const float* __restrict__ sv,              // saved [B*T][2][5H]
+    float* __restrict__ dg, int lddg,          // [B*T][lddg], dir d gate g unit u at d 4H + g H + u
+    unsigned* __restrict__ work) {
+  using G = CGeo<H>;
+  constexpr int KCBW = G::KCBW, NW = G::NW, G4 = 4 * H;
+  __shared__ __attribute__((aligned(16))) float part[4 * SB * PSB];
+  __shared__ __attribute__((aligned(16))) __bf16 gs[SB * 64];  // [s][4 u + g]
+  __shared__ int sL[SB];
+  const int d = blockIdx.y, w = blockIdx.x, u0 = w * UW;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < SB) sL[tid] = tid < B ? (int)lengths[tid] : 0;
+
+  bf16x8 wb[KCBW];
+  {
+    const bf16x8* src = wp + (((long long)(d * NW + w) * 4 + wv) * KCBW) * 64 + lane;
+#pragma unroll
+    for (int kk = 0; kk < KCBW; ++kk) wb[kk] = src[kk * 64];
+  }
+  __syncthreads();
+  int maxL = 0;
+  for (int s = 0; s < B; ++s) maxL = max(maxL, sL[s]);
+  for (int s = 0; s < B; ++s) {  // zero this workgroup's gate-gradient columns past the end
+    const int L = sL[s];
+    for (int i = tid; i < (T - L) * 64; i += NT) {
+      const int c = i % 64;
+      dg[((long long)s * T + L + i / 64) * lddg + d * G4 + (c / 16) * H + u0 + c % 16] = 0.f;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t xr = slab(work, G::BX);
+
+  int cs[2], cu[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = tid + NT * i;
+    cu[i] = p & 15;
+    cs[i] = p >> 4;
+  }
+  // processing index q of sequence s is its forward step L - 1 - q: row L-1-q (dir 0) or q
+  float in[2][7], dcs[2] = {0.f, 0.f};
+  long long grow[2];
+  auto load_in = [&](int q) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int sc = min(cs[i], B - 1), L = sL[sc];
+      const int qq = max(min(q, L - 1), 0);
+      const long long rb = (long long)sc * T;
+      grow[i] = rb + (d ? qq : max(L - 1 - qq, 0));
+      const bool hasp = qq < L - 1;  // c at forward step L - 2 - q exists
+      const long long prow = hasp ? rb + (d ? qq + 1 : L - 2 - qq) : grow[i];
+      const int j = u0 + cu[i];
+      const float* s5 = sv + (grow[i] * 2 + d) * 5 * H + j;
+#pragma unroll
+      for (int g = 0; g < 5; ++g) in[i][g] = s5[g * H];
+      const float cp = sv[(prow * 2 + d) * 5 * H + 4 * H + j];
+      in[i][5] = hasp ? cp : 0.f;
+      in[i][6] = dy[grow[i] * lddy + d * H + j];
+    }
+  };
+  load_in(0);
+
+  for (int q = 0; q < maxL; ++q) {
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    if (q > 0) {
+      wait_count(work, d, (unsigned)(NW * q));
+      bf16x8 bf[KCBW][2];
+#pragma unroll
+      for (int kk = 0; kk < KCBW; ++kk)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int off = (((d * 2 + ((q - 1) & 1)) * SB + nt * 16 + (lane & 15)) * G4 +
+                           (wv * KCBW + kk) * 32 + 8 * (lane >> 4)) * 2;
+          bf[kk][nt] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, CP_SC1));
+        }
+#pragma unroll
+      for (int kk = 0; kk < KCBW; ++kk)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
+#pragma unroll
+      for (int kk = 0; kk < KCBW; ++kk)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[kk], bf[kk][nt], acc[nt], 0, 0, 0);
+    }
+    // lane holds dh of units 4 (lane >> 4) + r for sequence 16 nt + (lane & 15)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * PSB + 4 * (lane >> 4)] = acc[nt];
+    __syncthreads();
+    float o[2][4];
+    bool val[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int s = cs[i], u = cu[i];
+      float dhr = part[s * PSB + u];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) dhr += part[(k * SB + s) * PSB + u];
+      const float ig = in[i][0], fg = in[i][1], gg = in[i][2], og = in[i][3];
+      const float dh = in[i][6] + dhr;
+      const float tc = tanh_fast(in[i][4]);
+      const float dcc = dcs[i] + dh * og * (1.f - tc * tc);
+      o[i][0] = dcc * gg * ig * (1.f - ig);
+      o[i][1] = dcc * in[i][5] * fg * (1.f - fg);
+      o[i][2] = dcc * ig * (1.f - gg * gg);
+      o[i][3] = dh * tc * og * (1.f - og);
+      dcs[i] = dcc * fg;
+      val[i] = q < sL[s];
+      bf16x4_ nb;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) nb[g] = (__bf16)(val[i] ? o[i][g] : 0.f);
+      *(bf16x4_*)&gs[s * 64 + 4 * u] = nb;
+    }
+    __syncthreads();
+    {  // publish dG: 32 sequences x 64 values, one 16-B sc1 store per thread
+      const f32x4 v = *(const f32x4*)&gs[(tid >> 3) * 64 + (tid & 7) * 8];
+      const int off = (((d * 2 + (q & 1)) * SB + (tid >> 3)) * G4 + w * 64 + (tid & 7) * 8) * 2;
+      __builtin_amdgcn_raw_buffer_store_b128(v, xr, off, 0, CP_SC1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) signal(work, d);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (val[i]) {
+        float* dst = dg + grow[i] * lddg + d * G4 + u0 + cu[i];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dst[g * H] = o[i][g];
+      }
+    if (q + 1 < maxL) load_in(q + 1);
+  }
+}
+
+size_t excl(size_t need) {
+  return ensvs_rec_exclusive() ? std::max<size_t>(need, 160 * 1024) : need;
+}
+
+template <int H>
+int launch_fwd(const float* gx, int ldg, const void* wp, const long long* lengths, int B, int T,
+               float* y, int ldy, float* sv, unsigned* work, hipStream_t st) {
+  using G = CGeo<H>;
+  const size_t st_lds = sizeof(float) * 4 * SB * PSF + 2 * SB * UW + 4 * SB;
+  const size_t dyn = excl(st_lds) - st_lds;
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)lstm_coop_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  if (attr != hipSuccess) return ENSVS_E_HIP;
+  if (hipMemsetAsync(work, 0, HDR, st) != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(lstm_coop_fwd_kernel<H>, dim3(G::NW, 2), dim3(NT), dyn, st, gx, ldg,
+                     (const f16x8*)wp, lengths, B, T, y, ldy, sv, work);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+template <int H>
+int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengths, int B, int T,
+               const float* sv, float* dg, int lddg, unsigned* work, hipStream_t st) {
+  using G = CGeo<H>;
+  const size_t st_lds = sizeof(float) * 4 * SB * PSB + 2 * SB * 64 + 4 * SB;
+  const size_t dyn = excl(st_lds) - st_lds;
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)lstm_coop_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  if (attr != hipSuccess) return ENSVS_E_HIP;
+  if (hipMemsetAsync(work, 0, HDR, st) != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(lstm_coop_bwd_kernel<H>, dim3(G::NW, 2), dim3(NT), dyn, st, dy, lddy,
+                     (const bf16x8*)wp, lengths, B, T, sv, dg, lddg, work);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+bool coop_shape(int B, int H) { return B >= 1 && B <= SB && (H == 256 || H == 512); }
+
+int check_work(const void* work, long long work_bytes, int H) {
+  if (!work || (uintptr_t)work % 256 || work_bytes < ensvs_lstm_coop_work_bytes(H)) return ENSVS_E_ARG;
+  return ENSVS_OK;
+}
+
+}  // namespace
+
+ENSVS_API int ensvs_lstm_coop_supported(int B, int H) { return coop_shape(B, H) ? 1 : 0; }
+
+ENSVS_API long long ensvs_lstm_coop_work_bytes(int H) {
+  return HDR + 2LL * 2 * SB * 4 * H * 2;  // header + the backward slab (the larger one)
+}
+
+ENSVS_API int ensvs_lstm_coop_pack(const float* whh_f, const float* whh_r, int H, int bwd,
+                                   void* out, void* stream) {
+  if (H != 256 && H != 512) return ENSVS_E_SHAPE;
+  if (!out || (uintptr_t)out % 16) return ENSVS_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid(cdiv(2LL * 4 * H * H, 256)), block(256);
+  if (bwd) {
+    if (H == 256) hipLaunchKernelGGL(coop_pack_bwd_kernel<256>, grid, block, 0, st, whh_f, whh_r, (__bf16*)out);
+    else hipLaunchKernelGGL(coop_pack_bwd_kernel<512>, grid, block, 0, st, whh_f, whh_r, (__bf16*)out);
+  } else {
+    if (H == 256) hipLaunchKernelGGL(coop_pack_fwd_kernel<256>, grid, block, 0, st, whh_f, whh_r, (_Float16*)out);
+    else hipLaunchKernelGGL(coop_pack_fwd_kernel<512>, grid, block, 0, st, whh_f, whh_r, (_Float16*)out);
+  }
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_lstm_coop_fwd(const float* gx, int ldg, const void* wpack,
+                                  const long long* lengths, int B, int T, int H, float* y, int ldy,
+                                  float* saved, void* work, long long work_bytes, void* stream) {
+  if (!coop_shape(B, H) || T <= 0 || ldg < 8 * H || ldy < 2 * H) return ENSVS_E_SHAPE;
+  if (check_work(work, work_bytes, H) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  unsigned* wk = (unsigned*)work;
+  return H == 256 ? launch_fwd<256>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st)
+                  : launch_fwd<512>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st);
+}
+
+ENSVS_API int ensvs_lstm_coop_bwd(const float* dy, int lddy, const void* wpack,
+                                  const long long* lengths, int B, int T, int H,
+                                  const float* saved, float* dg, int lddg, void* work,
+                                  long long work_bytes, void* stream) {
+  if (!coop_shape(B, H) || T <= 0 || lddy < 2 * H || lddg < 8 * H) return ENSVS_E_SHAPE;
+  if (check_work(work, work_bytes, H) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  unsigned* wk = (unsigned*)work;
+  return H == 256 ? launch_bwd<256>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st)
+                  : launch_bwd<512>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st);
+}

@@ -588,6 +588,18 @@ __global__ void copy_cols_kernel(const float* __restrict__ src, int lds, float* 
   }
 }
 
+// dst[m][b*dw + c] = c < sw ? src[m][b*sw + c] : 0 for b < nblk, c < dw: per-gate column blocks
+// widened (zero pad) or narrowed (the LSTM hidden sizes run by a padded persistent kernel)
+__global__ void regroup_cols_kernel(const float* __restrict__ src, int lds, float* __restrict__ dst,
+                                    int ldd, long long M, int nblk, int sw, int dw) {
+  const long long per = (long long)nblk * dw;
+  GRID_LOOP(i, M * per) {
+    const long long m = i / per;
+    const int j = (int)(i % per), b = j / dw, c = j % dw;
+    dst[m * ldd + j] = c < sw ? src[m * lds + (long long)b * sw + c] : 0.f;
+  }
+}
+
 __global__ void axpy_kernel(float* __restrict__ y, const float* __restrict__ x, float a,
                             long long n) {
   GRID_LOOP(i, n) y[i] += a * x[i];
@@ -966,6 +978,14 @@ ENSVS_API int ensvs_rng_advance(void* stream) {
 ENSVS_API int ensvs_copy_cols(const float* src, int lds, float* dst, int ldd, long long M, int n,
                               void* stream) {
   LAUNCH(copy_cols_kernel, M * n, src, lds, dst, ldd, M, n);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_regroup_cols(const float* src, int lds, float* dst, int ldd, long long M,
+                                 int nblk, int sw, int dw, void* stream) {
+  if (M < 0 || nblk <= 0 || sw <= 0 || dw <= 0) return ENSVS_E_SHAPE;
+  if (M == 0) return ENSVS_OK;
+  LAUNCH(regroup_cols_kernel, M * nblk * dw, src, lds, dst, ldd, M, nblk, sw, dw);
   return ENSVS_OK;
 }
 

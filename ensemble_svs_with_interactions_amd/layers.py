@@ -365,6 +365,73 @@ def lstm_register(pk, lstm):
                         b2=getattr(lstm, f"bias_hh_l{l}{sfx}"))
 
 
+def lstm_coop(B, H):
+    """Whether the layer's recurrence runs the cooperative kernels (lstm_coop.hip: H = 256 /
+    512, B <= 32, production bf16 precision; fp16 / bf16 recurrent products with fp32
+    accumulation and cell state).  The fp32 parity mode keeps lstm.hip's exact kernels."""
+    return gemm_dtype() == _lib.DT_BF16 and query("ensvs_lstm_coop_supported", B, H) == 1
+
+
+def _coop_pack(lstm, l, bwd):
+    """W_hh of layer l (both directions) as the cooperative kernels' MFMA fragments,
+    repacked whenever the weights changed (engine epoch / parameter versions, as the GEMM
+    ModulePacks: inside a captured step the repack is part of the graph)."""
+    from .engine import _sig
+    ws = [getattr(lstm, f"weight_hh_l{l}"), getattr(lstm, f"weight_hh_l{l}_reverse")]
+    cache = lstm.__dict__.setdefault("_ensvs_coop", {})
+    sig = _sig(ws)
+    ent = cache.get((l, bwd))
+    if ent is None or ent[0] != sig:
+        H = lstm.hidden_size
+        buf = ent[1] if ent is not None else torch.empty(
+            2 * 4 * H * H, dtype=torch.bfloat16 if bwd else torch.float16, device=ws[0].device)
+        call("ensvs_lstm_coop_pack", ws[0].data_ptr(), ws[1].data_ptr(), H, int(bwd),
+             buf.data_ptr(), stream())
+        ent = cache[(l, bwd)] = (sig, buf)
+    return ent[1]
+
+
+_PERSIST_H = (8, 16, 32, 64, 128)
+
+
+def lstm_pad(H):
+    """Hidden size of the exact fp32 persistent kernel that runs a layer of size H on
+    zero-padded gates (the SeparateF0 bap decoder's H = 62 -> 64: padded units have zero
+    weights and inputs, so their c and h stay exactly 0), or None (H has its own kernel)."""
+    if H in _PERSIST_H or H > _PERSIST_H[-1]:
+        return None
+    return next(p for p in _PERSIST_H if p >= H)
+
+
+def _regroup(src, lds, dst, ldd, M, nblk, sw, dw):
+    call("ensvs_regroup_cols", src.data_ptr(), lds, dst.data_ptr(), ldd, M, nblk, sw, dw, stream())
+
+
+def _whh_pad(lstm, l, HP):
+    """W_hh of layer l (both directions) zero-padded to [4 HP][HP], cached per weight
+    version (engine epoch / parameter versions; captured into a step graph like the packs)."""
+    from .engine import _sig
+    ws = [getattr(lstm, f"weight_hh_l{l}"), getattr(lstm, f"weight_hh_l{l}_reverse")]
+    cache = lstm.__dict__.setdefault("_ensvs_pad", {})
+    sig = _sig(ws)
+    ent = cache.get(l)
+    if ent is None or ent[0] != sig:
+        H = lstm.hidden_size
+        dev = ws[0].device
+        bufs = ent[1] if ent is not None else [empty(4 * HP, HP, device=dev) for _ in ws]
+        tmp = empty(4 * H, HP, device=dev)
+        for w, b in zip(ws, bufs):
+            _regroup(w, H, tmp, HP, 4 * H, 1, H, HP)            # columns k: H -> HP
+            _regroup(tmp, H * HP, b, HP * HP, 4, 1, H * HP, HP * HP)  # rows per gate: H -> HP
+        ent = cache[l] = (sig, bufs)
+    return ent[1]
+
+
+def _coop_work(H, device):
+    n = query("ensvs_lstm_coop_work_bytes", H)
+    return empty(n, device=device, dtype=torch.uint8), n
+
+
 def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=True):
     """Packed bidirectional multi-layer LSTM.  Returns (Y (M, 2H), saved list)."""
     M = B * T
@@ -378,10 +445,28 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
             K.gemm([K.Seg(h, ldh, Kc, pk[f"ih{l}{sfx}"], T)], B, T, 4 * H, pk.fwd, gx, 8 * H,
                    yoff=d * 4 * H, **pk.bias_ptr_args(f"b{l}{sfx}"))
         y = empty(M, 2 * H, device=device)
-        saved = empty(M * 2 * 5 * H, device=device)
-        call("ensvs_lstm_fwd", gx.data_ptr(), 8 * H, getattr(lstm, f"weight_hh_l{l}").data_ptr(),
-             getattr(lstm, f"weight_hh_l{l}_reverse").data_ptr(), lens_dev.data_ptr(), B, T, H,
-             y.data_ptr(), 2 * H, saved.data_ptr(), stream())
+        HP = lstm_pad(H)
+        saved = empty(M * 2 * 5 * (HP or H), device=device)
+        if lstm_coop(B, H):
+            work, nbytes = _coop_work(H, device)
+            call("ensvs_lstm_coop_fwd", gx.data_ptr(), 8 * H, _coop_pack(lstm, l, False).data_ptr(),
+                 lens_dev.data_ptr(), B, T, H, y.data_ptr(), 2 * H, saved.data_ptr(),
+                 work.data_ptr(), nbytes, stream())
+        elif HP:
+            gxp = empty(M, 8 * HP, device=device)
+            _regroup(gx, 8 * H, gxp, 8 * HP, M, 8, H, HP)
+            w0, w1 = _whh_pad(lstm, l, HP)
+            yp = empty(M, 2 * HP, device=device)
+            call("ensvs_lstm_fwd", gxp.data_ptr(), 8 * HP, w0.data_ptr(), w1.data_ptr(),
+                 lens_dev.data_ptr(), B, T, HP, yp.data_ptr(), 2 * HP, saved.data_ptr(),
+                 stream())
+            _regroup(yp, 2 * HP, y, 2 * H, M, 2, HP, H)
+            del gxp, yp
+        else:
+            call("ensvs_lstm_fwd", gx.data_ptr(), 8 * H,
+                 getattr(lstm, f"weight_hh_l{l}").data_ptr(),
+                 getattr(lstm, f"weight_hh_l{l}_reverse").data_ptr(), lens_dev.data_ptr(), B, T,
+                 H, y.data_ptr(), 2 * H, saved.data_ptr(), stream())
         del gx
         yin = y
         mask = None
@@ -391,7 +476,7 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
             call("ensvs_mul_out", yin.data_ptr(), y.data_ptr(), mask.data_ptr(), yin.numel(),
                  stream())
         if save:
-            sv.append(dict(x=h, ldx=ldh, y=y, saved=saved, mask=mask, yin=yin))
+            sv.append(dict(x=h, ldx=ldh, y=y, saved=saved, mask=mask, yin=yin, hp=HP))
         h, ldh = yin, 2 * H
     return h, sv
 
@@ -405,11 +490,31 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
         s = sv[l]
         Kc = getattr(lstm, f"weight_ih_l{l}").shape[1]
         dg = empty(M, 8 * H, device=device)
-        nw = query("ensvs_lstm_bwd_work_floats", B, H)
-        work = empty(max(nw, 1), device=device)
-        call("ensvs_lstm_bwd", d.data_ptr(), 2 * H, getattr(lstm, f"weight_hh_l{l}").data_ptr(),
-             getattr(lstm, f"weight_hh_l{l}_reverse").data_ptr(), lens_dev.data_ptr(), B, T, H,
-             s["saved"].data_ptr(), dg.data_ptr(), 8 * H, work.data_ptr(), nw, stream())
+        if lstm_coop(B, H):
+            work, nbytes = _coop_work(H, device)
+            call("ensvs_lstm_coop_bwd", d.data_ptr(), 2 * H, _coop_pack(lstm, l, True).data_ptr(),
+                 lens_dev.data_ptr(), B, T, H, s["saved"].data_ptr(), dg.data_ptr(), 8 * H,
+                 work.data_ptr(), nbytes, stream())
+        elif s.get("hp"):
+            HP = s["hp"]
+            dp = empty(M, 2 * HP, device=device)
+            _regroup(d, 2 * H, dp, 2 * HP, M, 2, H, HP)
+            dgp = empty(M, 8 * HP, device=device)
+            w0, w1 = _whh_pad(lstm, l, HP)
+            nw = query("ensvs_lstm_bwd_work_floats", B, HP)
+            work = empty(max(nw, 1), device=device)
+            call("ensvs_lstm_bwd", dp.data_ptr(), 2 * HP, w0.data_ptr(), w1.data_ptr(),
+                 lens_dev.data_ptr(), B, T, HP, s["saved"].data_ptr(), dgp.data_ptr(), 8 * HP,
+                 work.data_ptr(), nw, stream())
+            _regroup(dgp, 8 * HP, dg, 8 * H, M, 8, HP, H)
+            del dp, dgp
+        else:
+            nw = query("ensvs_lstm_bwd_work_floats", B, H)
+            work = empty(max(nw, 1), device=device)
+            call("ensvs_lstm_bwd", d.data_ptr(), 2 * H,
+                 getattr(lstm, f"weight_hh_l{l}").data_ptr(),
+                 getattr(lstm, f"weight_hh_l{l}_reverse").data_ptr(), lens_dev.data_ptr(), B, T,
+                 H, s["saved"].data_ptr(), dg.data_ptr(), 8 * H, work.data_ptr(), nw, stream())
         for di, sfx in enumerate(("", "_reverse")):
             wgrad_into(getattr(lstm, f"weight_ih_l{l}{sfx}"), dg, 8 * H, s["x"], s["ldx"], B, T, T,
                        4 * H, Kc, dyoff=di * 4 * H)

@@ -174,6 +174,27 @@ int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* w
                    const long long* lengths, int B, int T, int H, const float* saved, float* dg,
                    int lddg, float* work, long long work_floats, void* stream);
 
+/* Cooperative recurrence for H in {256, 512} and B <= 32 in production (bf16 GEMM)
+ * precision: one launch for every step, each direction split over H/16 workgroups that keep
+ * their W_hh slice in registers and exchange h (fp16) / dG (bf16) through `work` every step
+ * (fp16 / bf16 recurrent products, fp32 accumulation, gates, cell state and saved values).
+ * Same contract as ensvs_lstm_fwd / ensvs_lstm_bwd (the MultiTrackLSTMEncoder H = 512 and the
+ * SeparateF0 decoders' H = 256 of nnsvs/model.py:1483-1490, 861-869).  wpack: W_hh of both
+ * directions packed by ensvs_lstm_coop_pack (bwd = 0: forward fp16 fragments, bwd = 1:
+ * backward bf16 fragments of W_hh^T), 2*4*H*H 2-byte elements.  work: 256-B aligned,
+ * ensvs_lstm_coop_work_bytes(H) bytes, caller-owned, one per concurrent launch; bytes
+ * 128..131 read non-zero after a launch whose grid could not become resident. */
+int ensvs_lstm_coop_supported(int B, int H);
+long long ensvs_lstm_coop_work_bytes(int H);
+int ensvs_lstm_coop_pack(const float* whh_f, const float* whh_r, int H, int bwd, void* out,
+                         void* stream);
+int ensvs_lstm_coop_fwd(const float* gx, int ldg, const void* wpack, const long long* lengths,
+                        int B, int T, int H, float* y, int ldy, float* saved, void* work,
+                        long long work_bytes, void* stream);
+int ensvs_lstm_coop_bwd(const float* dy, int lddy, const void* wpack, const long long* lengths,
+                        int B, int T, int H, const float* saved, float* dg, int lddg, void* work,
+                        long long work_bytes, void* stream);
+
 /* Residual-F0 AR decoder (acoustic_models/tacotron_f0.py:126-237 with
  * ZoneOutCell(LSTMCell), tacotron/decoder.py:20-48).  H in {16,...,256}, T % 4 == 0.
  * teach == NULL: free-running (the multi-track diffusion model, multistream.py:1646-1651,
@@ -291,6 +312,12 @@ int ensvs_adam_step(float* p, float* g, float* m, float* v, long long n, const f
 int ensvs_rng_advance(void* stream);
 int ensvs_copy_cols(const float* src, int lds, float* dst, int ldd, long long M, int n,
                     void* stream);
+/* dst[m*ldd + b*dw + c] = c < sw ? src[m*lds + b*sw + c] : 0, b < nblk, c < dw: per-gate
+ * column blocks widened with zero padding (sw < dw) or narrowed (sw > dw).  The LSTM layers
+ * of hidden size 62 (the SeparateF0 bap decoder, nnsvs/model.py:861-869) run the exact fp32
+ * persistent H = 64 kernels on zero-padded gates (padded units keep c = h = 0). */
+int ensvs_regroup_cols(const float* src, int lds, float* dst, int ldd, long long M, int nblk,
+                       int sw, int dw, void* stream);
 int ensvs_axpy(float* y, const float* x, float a, long long n, void* stream);
 /* y[g*ystride + j] += a * x[g*xstride + j] for g < count, j < n (same-shaped parameters of
  * several layers, e.g. the 20 DiffNet residual blocks' bias gradients, in one launch). */

@@ -6,7 +6,8 @@ synth: the mgc DiffNet's 100-step reverse diffusion of one (main, sub) pair at 2
 (eager, the launches the inference graph captures) instead of the training step; voc: one
 uSFGAN generator pass over one 2 000-frame track (480 000 samples); post: the bench's
 per-track post-acoustic processing and uSFGAN inputs of one 2 000-frame track; vocleg: the
-bench's whole 6-part vocoder leg (post-processing per track, one batched generator pass).
+bench's whole 6-part vocoder leg (post-processing per track, one batched generator pass);
+sf0: the training step of the recipe-default SeparateF0 model instead.
 """
 import collections
 import os
@@ -24,6 +25,7 @@ SYNTH = len(sys.argv) > 2 and sys.argv[2] == "synth"
 VOC = len(sys.argv) > 2 and sys.argv[2] == "voc"
 POST = len(sys.argv) > 2 and sys.argv[2] in ("post", "vocleg")
 VOCLEG = len(sys.argv) > 2 and sys.argv[2] == "vocleg"
+SF0 = len(sys.argv) > 2 and sys.argv[2] == "sf0"
 ONLY = sys.argv[3] if len(sys.argv) > 3 else None  # rows of one branch only (lf0/mgc/bap/vuv)
 REC = []
 TAG = [None]
@@ -58,7 +60,12 @@ def call(name, *args):
     s.record()
     orig_call(name, *args)
     e.record()
-    REC.append((name, TAG[0], s, e, BR[0]))
+    tag = TAG[0]
+    if name in ("ensvs_lstm_fwd", "ensvs_lstm_bwd"):
+        tag = f"H={args[7]} B={args[5]} T={args[6]}"
+    elif name in ("ensvs_lstm_coop_fwd", "ensvs_lstm_coop_bwd"):
+        tag = f"H={args[6]} B={args[4]} T={args[5]}"
+    REC.append((name, tag, s, e, BR[0]))
 
 
 def tagged(fn, fmt):
@@ -182,7 +189,8 @@ def main():
         run_synth(dev)
         return report()
     torch.manual_seed(20250321)
-    model = configs.instantiate(configs.multitrack_diffusion(num_speakers=4)).to(dev)
+    cfg = configs.multitrack_separate_f0 if SF0 else configs.multitrack_diffusion
+    model = configs.instantiate(cfg(num_speakers=4)).to(dev)
     opt = FusedAdam(model, lr=1e-4, clip_norm=1.0)
     P, T = 30, 1024
     b = data.synthetic_batch(P, T, 1000)

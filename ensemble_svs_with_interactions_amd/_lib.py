@@ -102,6 +102,15 @@ SIGNATURES = {
                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ensvs_ardec_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
                         c_float, c_float, c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ensvs_ardec_coop_supported": [c_int, c_int],
+    "ensvs_ardec_coop_work_bytes": [c_int],
+    "ensvs_ardec_coop_pack": [c_vp, c_int, c_int, c_vp, c_vp],
+    "ensvs_ardec_coop_fwd": [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
+                             c_vp, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_float,
+                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp],
+    "ensvs_ardec_coop_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
+                             c_float, c_float, c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp,
+                             c_vp, c_ll, c_vp],
     "ensvs_downsample_fwd": [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp,
                              c_vp, c_int, c_int, c_vp, c_int, c_vp],
     "ensvs_downsample_bwd": [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_int,
@@ -201,7 +210,8 @@ SIGNATURES = {
 # entry points returning a value instead of a status code
 RESTYPES = {"ensvs_embed_bwd_workspace": c_ll, "ensvs_usf_source_workspace": c_ll,
             "ensvs_attn_table_grad_workspace": c_ll, "ensvs_lstm_bwd_work_floats": c_ll,
-            "ensvs_lstm_coop_work_bytes": c_ll, "ensvs_lstm_coop_supported": ctypes.c_int}
+            "ensvs_lstm_coop_work_bytes": c_ll, "ensvs_lstm_coop_supported": ctypes.c_int,
+            "ensvs_ardec_coop_work_bytes": c_ll, "ensvs_ardec_coop_supported": ctypes.c_int}
 
 _lib = None
 

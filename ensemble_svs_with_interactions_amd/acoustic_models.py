@@ -19,7 +19,7 @@ from torch import nn
 from . import _lib
 from . import kernels as K
 from . import layers as Ly
-from ._lib import call, ptr
+from ._lib import call, ptr, query
 from .base import BaseModel, PredictionType
 from .engine import Branches, GradCapture, ModulePacks, _sig, empty, grad_of, lengths_pair
 from .model import init_weights
@@ -43,6 +43,12 @@ BRANCH_AFTER = {int(b): int(a) for b, a in (kv.split(":") for kv in
                 os.environ.get("ENSVS_BRANCH_AFTER", "2:1").split(",") if kv)}
 EXCL_BRANCHES = {int(v) for v in os.environ.get("ENSVS_EXCL_BRANCHES", "0,1").split(",")
                  if v}
+
+
+def _ar_work(H, device):
+    """Workspace of one cooperative AR-decoder launch (counters + exchange slabs)."""
+    n = query("ensvs_ardec_coop_work_bytes", H)
+    return empty(n, device=device, dtype=torch.uint8), n
 
 class ZoneOutCell(nn.Module):
     """nnsvs/tacotron/decoder.py:20-48 (container).  The recipe uses zoneout 0, for which
@@ -210,7 +216,9 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
         pk.linear("dec_fo_e", self.decoder.feat_out.weight, cols=(H, H + Ce))
 
     def _ar_prepare(self):
-        """Packed W_hh layouts and the contiguous prenet column of W_ih for the ardec kernels."""
+        """Packed W_hh layouts and the contiguous prenet column of W_ih for the ardec kernels:
+        (wpf, wpb, wih_p), plus the cooperative kernels' fp16 / bf16 MFMA fragments (coop_f,
+        coop_b) when the decoder runs them (_ar_coop)."""
         cell = self.decoder.lstm[0].cell
         params = [cell.weight_hh, cell.weight_ih]
         sig = _sig(params)
@@ -226,8 +234,23 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
         wih_p = empty(4 * H, device=dev)
         call("ensvs_copy_cols", cell.weight_ih.data_ptr() + 4 * (Ce1 - 1), Ce1, wih_p.data_ptr(), 1,
              4 * H, 1, Ly.stream())
-        self._ar = (sig, (wpf, wpb, wih_p))
+        coop = None
+        if query("ensvs_ardec_coop_supported", 1, H) == 1:
+            coop = (torch.empty(4 * H * H, dtype=torch.float16, device=dev),
+                    torch.empty(4 * H * H, dtype=torch.bfloat16, device=dev))
+            for bwd, buf in enumerate(coop):
+                call("ensvs_ardec_coop_pack", cell.weight_hh.data_ptr(), H, bwd, buf.data_ptr(),
+                     Ly.stream())
+        self._ar = (sig, (wpf, wpb, wih_p, coop))
         return self._ar[1]
+
+    def _ar_coop(self, B):
+        """Whether the AR decoder runs the cooperative kernels (ardec.hip: H = 128 / 256,
+        B <= 32, production bf16 precision; fp16 / bf16 recurrent products with fp32
+        accumulation, gates, cell state and feat_out).  The fp32 parity mode keeps the exact
+        per-sequence kernels."""
+        H = self.decoder.lstm[0].cell.hidden_size
+        return Ly.gemm_dtype() == _lib.DT_BF16 and query("ensvs_ardec_coop_supported", B, H) == 1
 
     # ------------------------------------------------------------------ kernels
     def _embed(self, pk, xs, ld, B, T, spks, spk_ld, dev):
@@ -307,7 +330,7 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
                **pk.bias_ptr_args("dec_b"))
         ofx = empty(B * Tr, 4, device=dev)
         K.gemm([K.Seg(e, Ce, Ce, pk["dec_fo_e"], Tr)], B, Tr, 4, pk.fwd, ofx, 4)
-        wpf, wpb, wih_p = self._ar_prepare()
+        wpf, wpb, wih_p, coop = self._ar_prepare()
         if masks is None:
             masks = Ly.dropout_mask(B * Tr, dec.prenet_dropout, dev)
         lf0 = empty(M, device=dev)
@@ -319,12 +342,19 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
         sp = empty(B * Tr, device=dev)
         tptr, tld = (None, 0) if teacher is None else \
             (teacher[0].data_ptr() + 4 * teacher[2], teacher[1])
-        call("ensvs_ardec_fwd", gx.data_ptr(), 4 * H, ofx.data_ptr(), 4, wpf.data_ptr(),
-             wih_p.data_ptr(), dec.feat_out.weight.data_ptr(), dec.feat_out.weight.shape[1],
-             xs[0].data_ptr() + 4 * li, ld, masks.data_ptr(), tptr, tld, B, T, H,
-             float(dec.in_lf0_min), float(dec.in_lf0_max), float(dec.out_lf0_mean),
-             float(dec.out_lf0_scale), lf0.data_ptr(), res.data_ptr(), sg.data_ptr(),
-             sc.data_ptr(), sh.data_ptr(), so.data_ptr(), sp.data_ptr(), Ly.stream())
+        consts = (float(dec.in_lf0_min), float(dec.in_lf0_max), float(dec.out_lf0_mean),
+                  float(dec.out_lf0_scale))
+        outs = (lf0.data_ptr(), res.data_ptr(), sg.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+                so.data_ptr(), sp.data_ptr())
+        ins = (wih_p.data_ptr(), dec.feat_out.weight.data_ptr(), dec.feat_out.weight.shape[1],
+               xs[0].data_ptr() + 4 * li, ld, masks.data_ptr(), tptr, tld, B, T, H)
+        if coop is not None and self._ar_coop(B):
+            work, nbytes = _ar_work(H, dev)
+            call("ensvs_ardec_coop_fwd", gx.data_ptr(), 4 * H, ofx.data_ptr(), 4,
+                 coop[0].data_ptr(), *ins, *consts, *outs, work.data_ptr(), nbytes, Ly.stream())
+        else:
+            call("ensvs_ardec_fwd", gx.data_ptr(), 4 * H, ofx.data_ptr(), 4, wpf.data_ptr(),
+                 *ins, *consts, *outs, Ly.stream())
         st = None
         if save:
             st = dict(X0=X0, esv=esv, hs=hs, csv=csv, lsv=lsv, y=y, e=e, masks=masks, sg=sg,
@@ -345,14 +375,21 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
         H = cell.hidden_size
         Ce = st["e"].shape[1]
         xs = st["xs"]
-        wpf, wpb, wih_p = self._ar_prepare()
+        wpf, wpb, wih_p, coop = self._ar_prepare()
         dg = empty(B * Tr, 4 * H, device=dev)
         do4 = empty(B * Tr, 4, device=dev)
-        call("ensvs_ardec_bwd", dlf0.data_ptr(), ptr(dres), wpb.data_ptr(), wih_p.data_ptr(),
-             dec.feat_out.weight.data_ptr(), dec.feat_out.weight.shape[1], st["masks"].data_ptr(),
-             int(st["teacher"]), B, T, H, float(dec.in_lf0_min), float(dec.in_lf0_max),
-             float(dec.out_lf0_mean), float(dec.out_lf0_scale), st["sg"].data_ptr(),
-             st["sc"].data_ptr(), st["so"].data_ptr(), dg.data_ptr(), do4.data_ptr(), Ly.stream())
+        args = (wih_p.data_ptr(), dec.feat_out.weight.data_ptr(), dec.feat_out.weight.shape[1],
+                st["masks"].data_ptr(), int(st["teacher"]), B, T, H, float(dec.in_lf0_min),
+                float(dec.in_lf0_max), float(dec.out_lf0_mean), float(dec.out_lf0_scale),
+                st["sg"].data_ptr(), st["sc"].data_ptr(), st["so"].data_ptr(), dg.data_ptr(),
+                do4.data_ptr())
+        if coop is not None and self._ar_coop(B):
+            work, nbytes = _ar_work(H, dev)
+            call("ensvs_ardec_coop_bwd", dlf0.data_ptr(), ptr(dres), coop[1].data_ptr(), *args,
+                 work.data_ptr(), nbytes, Ly.stream())
+        else:
+            call("ensvs_ardec_bwd", dlf0.data_ptr(), ptr(dres), wpb.data_ptr(), *args,
+                 Ly.stream())
         wg = Ly.wgrad_into
         # decoder weights
         wg(cell.weight_hh, dg, 4 * H, st["sh"], H, B, Tr, Tr, 4 * H, H, shift0=-1)

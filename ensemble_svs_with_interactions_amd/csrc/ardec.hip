@@ -19,7 +19,7 @@
 // instruction); h / dG are exchanged through double-buffered LDS.  The
 // feat_out reduction maps output row r onto K-quarter lane q, so one
 // __syncthreads per step suffices in both directions.
-#include "common.h"
+#include "coop.h"
 #include "ensvs.h"
 
 namespace {
@@ -350,6 +350,462 @@ int bwd_launch(const float* glf0, const float* gres, const float* wpb, const flo
   return ENSVS_OK;
 }
 
+
+// ------------------------------------------------------------------ cooperative decoder
+// Production (bf16 GEMM) precision at H in {128, 256}, B <= 32: the per-sequence kernels above
+// stream the 1 MB fp32 W_hh from L2 every step (8.7 us per step at H = 256).  All sequences
+// step in lockstep on the same W_hh, so here the recurrence is one MFMA product per step,
+// W_hh . [h_1 .. h_B] (N = the sequences), split over NW = H/16 workgroups that keep their 64
+// gate rows (forward, fp16) or 16 columns of W_hh^T (backward, bf16) in VGPRs for the whole
+// launch -- the lstm_coop.hip scheme with one direction.  The AR feedback needs no extra hop:
+//   forward:  each workgroup publishes, with its 16 units of h_t (fp16), its fp32 partial sums
+//             of feat_out W_fo[r, :H] h_t (r = 0..3); every workgroup then forms o_t, lf0_t and
+//             the next prenet input p_{t+1} = lf0_t[3] * mask itself from the 16 partials;
+//   backward: with its 64 gate gradients (bf16) each workgroup publishes its fp32 partial of
+//             w_p . dG_t, from which every workgroup forms d prev and the feat_out gradients.
+// Gates, cell state and every saved value stay fp32 (the recurrent products in fp16 / bf16 as
+// the recipe's fp16 autocast runs the LSTMCell, myconfig_notuseIL.yaml:6); the fp32 parity
+// mode keeps the exact kernels above.
+template <int H> struct ArGeo {
+  static constexpr int NW = H / coop::UW, KCW = H / 128, KCBW = H / 32;
+  static constexpr int FH = coop::SB * H * 2;      // forward slab per buffer: h [s][H] fp16
+  static constexpr int FBUF = FH + coop::SB * NW * 16;  // + feat_out partials [s][w][4] fp32
+  static constexpr int BG = coop::SB * 4 * H * 2;  // backward per buffer: dG [s][4H] bf16
+  static constexpr int BBUF = BG + coop::SB * NW * 4;   // + prenet partials [s][w] fp32
+  static_assert(H % 128 == 0 && NW % 4 == 0, "H");
+};
+
+constexpr int AR_PSF = 68;  // forward partial-sum row per sequence: 64 gate rows + 4 (banks)
+constexpr int AR_PSB = 20;  // backward: 16 units + 4
+
+template <int H>
+__global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
+    const float* __restrict__ gx, int ldgx, const float* __restrict__ ofx, int ldo,
+    const f16x8* __restrict__ wp, const float* __restrict__ wih_p,
+    const float* __restrict__ wfo, int ldwfo, const float* __restrict__ score, int lds,
+    const float* __restrict__ mask, const float* __restrict__ teach, int ldt, int B, int T,
+    ArConsts k, float* __restrict__ lf0, float* __restrict__ res, float* __restrict__ sg,
+    float* __restrict__ sc, float* __restrict__ sh, float* __restrict__ so,
+    float* __restrict__ sp, unsigned* __restrict__ work) {
+  using namespace coop;
+  using G = ArGeo<H>;
+  constexpr int KCW = G::KCW, NW = G::NW;
+  __shared__ __attribute__((aligned(16))) float part[4 * SB * AR_PSF];
+  __shared__ __attribute__((aligned(16))) _Float16 hs[SB * UW];
+  __shared__ __attribute__((aligned(16))) float ops[SB * 4];
+  __shared__ float pv[SB];
+  const int w = blockIdx.x, u0 = w * UW;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int Tr = T / 4;
+  const float den = k.in_max - k.in_min;
+
+  f16x8 wf[4][KCW];
+  {
+    const f16x8* src = wp + (((long long)w * 4 + wv) * 4 * KCW) * 64 + lane;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int kk = 0; kk < KCW; ++kk) wf[mt][kk] = src[(mt * KCW + kk) * 64];
+  }
+  const __amdgpu_buffer_rsrc_t xr = slab(work, 2 * G::FBUF);
+
+  // cells (unit u = p & 15, sequence s = p >> 4), p = tid + 256 i: 16 lanes per sequence
+  int cs[2], cu[2];
+  float wpc[2][4], woc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = tid + NT * i;
+    cu[i] = p & 15;
+    cs[i] = p >> 4;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) wpc[i][g] = wih_p[g * H + u0 + cu[i]];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) woc[i][r] = wfo[(long long)r * ldwfo + u0 + cu[i]];
+  }
+  float gin[2][4], cst[2] = {0.f, 0.f};
+  auto load_in = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float* src = gx + ((long long)min(cs[i], B - 1) * Tr + t) * ldgx + u0 + cu[i];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) gin[i][g] = src[g * H];
+    }
+  };
+  // reducer lanes (tid < SB, sequence tid): the inputs of step t-1's outputs and step t's p
+  const int rsq = min(tid, B - 1);
+  const bool rw = tid < SB && tid < B && w == 0;  // writes the per-sequence outputs
+  float rofx[4], rsd[4], rmask = 0.f, rteach = 0.f;
+  auto load_red = [&](int t) {  // ofx / score of step t - 1, mask of step t
+    if (tid < SB) {
+      const long long row = (long long)rsq * Tr + max(t - 1, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        rofx[r] = ofx[row * ldo + r];
+        rsd[r] = score[((long long)rsq * T + 4 * max(t - 1, 0) + r) * lds];
+      }
+      if (t < Tr) rmask = mask[(long long)rsq * Tr + t];
+      if (teach) rteach = teach[((long long)rsq * T + 4 * max(t - 1, 0) + 3) * ldt];
+    }
+  };
+  // step t-1's outputs from the published feat_out partials (reducer lanes only); returns lf0[3]
+  auto reduce_out = [&](int t, int base) -> float {
+    f32x4 op[NW];
+#pragma unroll
+    for (int w2 = 0; w2 < NW; ++w2) op[w2] = ld16(xr, base + G::FH + (tid * NW + w2) * 16);
+    float l3 = 0.f;
+    const long long row = (long long)rsq * Tr + t - 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float ov = rofx[r];
+#pragma unroll
+      for (int w2 = 0; w2 < NW; ++w2) ov += op[w2][r];
+      const float rs = MAX_LF0_RATIO * tanhf(ov);
+      const float sd = rsd[r] * den + k.in_min;
+      const float l = (sd + rs - k.mean) / k.scale;
+      if (rw) {
+        const long long f = (long long)rsq * T + 4 * (t - 1) + r;
+        lf0[f] = l;
+        res[f] = rs;
+        so[row * 4 + r] = ov;
+      }
+      l3 = l;
+    }
+    return l3;
+  };
+  load_in(0);
+  load_red(0);
+
+  for (int t = 0; t < Tr; ++t) {
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (t > 0) {
+      wait_count(work, 0, (unsigned)(NW * t));
+      const int base = ((t - 1) & 1) * G::FBUF;
+      f16x8 bf[KCW][2];
+#pragma unroll
+      for (int kk = 0; kk < KCW; ++kk)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          bf[kk][nt] = __builtin_bit_cast(
+              f16x8, ld16(xr, ((nt * 16 + (lane & 15)) * H + (wv * KCW + kk) * 32 + 8 * (lane >> 4)) * 2 + base));
+#pragma unroll
+      for (int kk = 0; kk < KCW; ++kk)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
+#pragma unroll
+      for (int kk = 0; kk < KCW; ++kk)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[mt][kk], bf[kk][nt], acc[mt][nt], 0, 0, 0);
+      if (tid < SB) {
+        const float l3 = reduce_out(t, base);
+        // the next input: this step's last frame, or the target there (teacher forcing)
+        const float p = (teach ? rteach : l3) * rmask;
+        pv[tid] = p;
+        if (rw) sp[(long long)rsq * Tr + t] = p;
+      }
+    } else if (tid < SB) {
+      const float p = 0.f * rmask;  // prev = 0 before the first step
+      pv[tid] = p;
+      if (rw) sp[(long long)rsq * Tr] = p;
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * AR_PSF + 16 * mt + 4 * (lane >> 4)] = acc[mt][nt];
+    __syncthreads();
+    float out[2][6];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int s = cs[i], u = cu[i];
+      f32x4 a = *(const f32x4*)&part[s * AR_PSF + 4 * u];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) a += *(const f32x4*)&part[(q * SB + s) * AR_PSF + 4 * u];
+      const float p = pv[s];
+      float pre[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) pre[g] = fmaf(wpc[i][g], p, gin[i][g]) + a[g];
+      const float ig = sigm(pre[0]), fg = sigm(pre[1]);
+      const float gg = tanh_fast(pre[2]), og = sigm(pre[3]);
+      const float cn = fg * cst[i] + ig * gg;
+      const float h = og * tanh_fast(cn);
+      cst[i] = cn;
+      const bool val = s < B;
+      hs[s * UW + u] = (_Float16)(val ? h : 0.f);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = sum16(woc[i][r] * (val ? h : 0.f));
+        if (u == 0) ops[s * 4 + r] = v;
+      }
+      out[i][0] = ig; out[i][1] = fg; out[i][2] = gg; out[i][3] = og; out[i][4] = cn; out[i][5] = h;
+    }
+    __syncthreads();
+    if (wv == 0) {  // publish h_t (32 sequences x 16 units) and the feat_out partials
+      const int base = (t & 1) * G::FBUF;
+      st16(xr, base + ((lane >> 1) * H + u0 + (lane & 1) * 8) * 2,
+           *(const f32x4*)&hs[(lane >> 1) * UW + (lane & 1) * 8]);
+      if (lane < SB) st16(xr, base + G::FH + (lane * NW + w) * 16, *(const f32x4*)&ops[lane * 4]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) signal(work, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (cs[i] < B) {
+        const long long row = (long long)cs[i] * Tr + t;
+        const int j = u0 + cu[i];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) sg[row * 4 * H + g * H + j] = out[i][g];
+        sc[row * H + j] = out[i][4];
+        sh[row * H + j] = out[i][5];
+      }
+    if (t + 1 < Tr) load_in(t + 1);
+    load_red(t + 1);
+  }
+  if (w == 0) {  // the last step's outputs
+    wait_count(work, 0, (unsigned)(NW * Tr));
+    if (tid < SB) reduce_out(Tr, ((Tr - 1) & 1) * G::FBUF);
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
+    const float* __restrict__ glf0, const float* __restrict__ gres,
+    const bf16x8* __restrict__ wp, const float* __restrict__ wih_p,
+    const float* __restrict__ wfo, int ldwfo, const float* __restrict__ mask, int teacher, int B,
+    int T, ArConsts k, const float* __restrict__ sg, const float* __restrict__ sc,
+    const float* __restrict__ so, float* __restrict__ dg, float* __restrict__ do4,
+    unsigned* __restrict__ work) {
+  using namespace coop;
+  using G = ArGeo<H>;
+  constexpr int KCBW = G::KCBW, NW = G::NW;
+  __shared__ __attribute__((aligned(16))) float part[4 * SB * AR_PSB];
+  __shared__ __attribute__((aligned(16))) __bf16 gs[SB * 64];  // [s][4 u + g]
+  __shared__ float d4s[SB * 4];
+  __shared__ float dps[SB];
+  const int w = blockIdx.x, u0 = w * UW;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int Tr = T / 4;
+
+  bf16x8 wb[KCBW];
+  {
+    const bf16x8* src = wp + (((long long)w * 4 + wv) * KCBW) * 64 + lane;
+#pragma unroll
+    for (int kk = 0; kk < KCBW; ++kk) wb[kk] = src[kk * 64];
+  }
+  const __amdgpu_buffer_rsrc_t xr = slab(work, 2 * G::BBUF);
+
+  int cs[2], cu[2];
+  float wo[2][4], wpg[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = tid + NT * i;
+    cu[i] = p & 15;
+    cs[i] = p >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wo[i][r] = wfo[(long long)r * ldwfo + u0 + cu[i]];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) wpg[i][g] = wih_p[g * H + u0 + cu[i]];
+  }
+  float in[2][6], dcs[2] = {0.f, 0.f};
+  auto load_in = [&](int t) {  // saved i f g o, c_t, c_{t-1} of step t
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long long row = (long long)min(cs[i], B - 1) * Tr + t;
+      const int j = u0 + cu[i];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) in[i][g] = sg[row * 4 * H + g * H + j];
+      in[i][4] = sc[row * H + j];
+      in[i][5] = t > 0 ? sc[(row - 1) * H + j] : 0.f;
+    }
+  };
+  const int rsq = min(tid, B - 1);
+  const bool rw = tid < SB && tid < B && w == 0;
+  float rgl[4], rgr[4], rso[4], rmask = 0.f;
+  auto load_red = [&](int t) {  // output grads / saved o of step t, mask of step t + 1
+    if (tid < SB) {
+      const long long row = (long long)rsq * Tr + t;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long long f = (long long)rsq * T + 4 * t + r;
+        rgl[r] = glf0[f];
+        rgr[r] = gres ? gres[f] : 0.f;
+        rso[r] = so[row * 4 + r];
+      }
+      rmask = t + 1 < Tr ? mask[row + 1] : 0.f;
+    }
+  };
+  load_in(Tr - 1);
+  load_red(Tr - 1);
+
+  for (int q = 0; q < Tr; ++q) {
+    const int t = Tr - 1 - q;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    float dprev = 0.f;
+    if (q > 0) {
+      wait_count(work, 0, (unsigned)(NW * q));
+      const int base = ((q - 1) & 1) * G::BBUF;
+      bf16x8 bf[KCBW][2];
+#pragma unroll
+      for (int kk = 0; kk < KCBW; ++kk)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          bf[kk][nt] = __builtin_bit_cast(
+              bf16x8, ld16(xr, ((nt * 16 + (lane & 15)) * 4 * H + (wv * KCBW + kk) * 32 + 8 * (lane >> 4)) * 2 + base));
+      f32x4 pp[NW / 4];
+      if (tid < SB)
+#pragma unroll
+        for (int j = 0; j < NW / 4; ++j) pp[j] = ld16(xr, base + G::BG + (tid * NW + 4 * j) * 4);
+#pragma unroll
+      for (int kk = 0; kk < KCBW; ++kk)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
+#pragma unroll
+      for (int kk = 0; kk < KCBW; ++kk)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[kk], bf[kk][nt], acc[nt], 0, 0, 0);
+      if (tid < SB && !teacher) {
+        float dp = 0.f;
+#pragma unroll
+        for (int j = 0; j < NW / 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dp += pp[j][e];
+        dprev = dp * rmask;  // p_{t+1} = lf0_t[3] * mask_{t+1}
+      }
+    }
+    float d4[4];
+    if (tid < SB) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float dl = rgl[r] + (r == 3 ? dprev : 0.f);
+        const float dr = rgr[r] + dl / k.scale;
+        const float th = tanhf(rso[r]);
+        d4[r] = dr * MAX_LF0_RATIO * (1.f - th * th);
+        d4s[tid * 4 + r] = d4[r];
+      }
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * AR_PSB + 4 * (lane >> 4)] = acc[nt];
+    __syncthreads();
+    float o[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int s = cs[i], u = cu[i];
+      float dh = part[s * AR_PSB + u];
+#pragma unroll
+      for (int kq = 1; kq < 4; ++kq) dh += part[(kq * SB + s) * AR_PSB + u];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dh = fmaf(wo[i][r], d4s[s * 4 + r], dh);
+      const float ig = in[i][0], fg = in[i][1], gg = in[i][2], og = in[i][3];
+      const float tc = tanh_fast(in[i][4]);
+      const float dcc = dcs[i] + dh * og * (1.f - tc * tc);
+      o[i][0] = dcc * gg * ig * (1.f - ig);
+      o[i][1] = dcc * in[i][5] * fg * (1.f - fg);
+      o[i][2] = dcc * ig * (1.f - gg * gg);
+      o[i][3] = dh * tc * og * (1.f - og);
+      dcs[i] = dcc * fg;
+      const bool val = s < B;
+      bf16x4 nb;
+      float pp = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        nb[g] = (__bf16)(val ? o[i][g] : 0.f);
+        pp = fmaf(wpg[i][g], o[i][g], pp);
+      }
+      *(bf16x4*)&gs[s * 64 + 4 * u] = nb;
+      pp = sum16(val ? pp : 0.f);
+      if (u == 0) dps[s] = pp;
+    }
+    __syncthreads();
+    {  // publish dG_t (32 sequences x 64 values) and the prenet partials
+      const int base = (q & 1) * G::BBUF;
+      st16(xr, base + ((tid >> 3) * 4 * H + w * 64 + (tid & 7) * 8) * 2,
+           *(const f32x4*)&gs[(tid >> 3) * 64 + (tid & 7) * 8]);
+      if (tid < SB) st4(xr, base + G::BG + (tid * NW + w) * 4, dps[tid]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) signal(work, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (cs[i] < B) {
+        float* dst = dg + ((long long)cs[i] * Tr + t) * 4 * H + u0 + cu[i];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dst[g * H] = o[i][g];
+      }
+    if (rw) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) do4[((long long)rsq * Tr + t) * 4 + r] = d4[r];
+    }
+    if (t > 0) {
+      load_in(t - 1);
+      load_red(t - 1);
+    }
+  }
+}
+
+size_t ar_coop_lds(size_t st_lds) {
+  return ensvs_rec_exclusive() ? std::max<size_t>(st_lds, 160 * 1024) - st_lds : 0;
+}
+
+template <int H>
+int coop_fwd_launch(const float* gx, int ldgx, const float* ofx, int ldo, const void* wp,
+                    const float* wih_p, const float* wfo, int ldwfo, const float* score, int lds,
+                    const float* mask, const float* teach, int ldt, int B, int T, ArConsts k,
+                    float* lf0, float* res, float* sg, float* sc, float* sh, float* so, float* sp,
+                    unsigned* work, hipStream_t st) {
+  const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSF + coop::SB * 5) + 2 * coop::SB * coop::UW;
+  const size_t dyn = ar_coop_lds(st_lds);
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)ardec_coop_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  if (attr != hipSuccess) return ENSVS_E_HIP;
+  if (hipMemsetAsync(work, 0, coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(ardec_coop_fwd_kernel<H>, dim3(ArGeo<H>::NW), dim3(coop::NT), dyn, st, gx,
+                     ldgx, ofx, ldo, (const f16x8*)wp, wih_p, wfo, ldwfo, score, lds, mask, teach,
+                     ldt, B, T, k, lf0, res, sg, sc, sh, so, sp, work);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+template <int H>
+int coop_bwd_launch(const float* glf0, const float* gres, const void* wp, const float* wih_p,
+                    const float* wfo, int ldwfo, const float* mask, int teacher, int B, int T,
+                    ArConsts k, const float* sg, const float* sc, const float* so, float* dg,
+                    float* do4, unsigned* work, hipStream_t st) {
+  const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSB + coop::SB * 5) + 2 * coop::SB * 64;
+  const size_t dyn = ar_coop_lds(st_lds);
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)ardec_coop_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  if (attr != hipSuccess) return ENSVS_E_HIP;
+  if (hipMemsetAsync(work, 0, coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(ardec_coop_bwd_kernel<H>, dim3(ArGeo<H>::NW), dim3(coop::NT), dyn, st, glf0,
+                     gres, (const bf16x8*)wp, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc,
+                     so, dg, do4, work);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+bool ar_coop_shape(int B, int H) { return B >= 1 && B <= coop::SB && (H == 128 || H == 256); }
+
+long long ar_coop_work(int H) {
+  return H == 128 ? coop::HDR + 2LL * std::max(ArGeo<128>::FBUF, ArGeo<128>::BBUF)
+                  : coop::HDR + 2LL * std::max(ArGeo<256>::FBUF, ArGeo<256>::BBUF);
+}
+
+int ar_coop_check(int B, int T, int H, const void* wp, const void* work, long long work_bytes) {
+  if (!ar_coop_shape(B, H) || T <= 0 || T % 4) return ENSVS_E_SHAPE;
+  if (!wp || (uintptr_t)wp % 16 || !work || (uintptr_t)work % 256 || work_bytes < ar_coop_work(H))
+    return ENSVS_E_ARG;
+  return ENSVS_OK;
+}
+
 }  // namespace
 
 ENSVS_API int ensvs_ardec_pack(const float* whh, int H, float* wpf, float* wpb, void* stream) {
@@ -398,6 +854,48 @@ ENSVS_API int ensvs_ardec_bwd(const float* glf0, const float* gres, const float*
     case 256: return bwd_launch<256>(glf0, gres, wpb, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc, so, dg, do4, st);
     default: return ENSVS_E_SHAPE;
   }
+}
+
+ENSVS_API int ensvs_ardec_coop_supported(int B, int H) { return ar_coop_shape(B, H) ? 1 : 0; }
+
+ENSVS_API long long ensvs_ardec_coop_work_bytes(int H) {
+  return (H == 128 || H == 256) ? ar_coop_work(H) : 0;
+}
+
+ENSVS_API int ensvs_ardec_coop_pack(const float* whh, int H, int bwd, void* out, void* stream) {
+  if (H != 128 && H != 256) return ENSVS_E_SHAPE;
+  return coop::pack(whh, whh, 1, H, bwd, out, (hipStream_t)stream);
+}
+
+ENSVS_API int ensvs_ardec_coop_fwd(const float* gx, int ldgx, const float* ofx, int ldo,
+                                   const void* wpack, const float* wih_p, const float* wfo,
+                                   int ldwfo, const float* score, int lds, const float* mask,
+                                   const float* teach, int ldt, int B, int T, int H,
+                                   float in_min, float in_max, float mean, float scale,
+                                   float* lf0, float* res, float* sg, float* sc, float* sh,
+                                   float* so, float* sp, void* work, long long work_bytes,
+                                   void* stream) {
+  if (int e = ar_coop_check(B, T, H, wpack, work, work_bytes)) return e;
+  if (ldgx < 4 * H || ldo < 4) return ENSVS_E_SHAPE;
+  ArConsts k{in_min, in_max, mean, scale};
+  hipStream_t st = (hipStream_t)stream;
+  unsigned* wk = (unsigned*)work;
+  return H == 128 ? coop_fwd_launch<128>(gx, ldgx, ofx, ldo, wpack, wih_p, wfo, ldwfo, score, lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, so, sp, wk, st)
+                  : coop_fwd_launch<256>(gx, ldgx, ofx, ldo, wpack, wih_p, wfo, ldwfo, score, lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, so, sp, wk, st);
+}
+
+ENSVS_API int ensvs_ardec_coop_bwd(const float* glf0, const float* gres, const void* wpack,
+                                   const float* wih_p, const float* wfo, int ldwfo,
+                                   const float* mask, int teacher, int B, int T, int H,
+                                   float in_min, float in_max, float mean, float scale,
+                                   const float* sg, const float* sc, const float* so, float* dg,
+                                   float* do4, void* work, long long work_bytes, void* stream) {
+  if (int e = ar_coop_check(B, T, H, wpack, work, work_bytes)) return e;
+  ArConsts k{in_min, in_max, mean, scale};
+  hipStream_t st = (hipStream_t)stream;
+  unsigned* wk = (unsigned*)work;
+  return H == 128 ? coop_bwd_launch<128>(glf0, gres, wpack, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc, so, dg, do4, wk, st)
+                  : coop_bwd_launch<256>(glf0, gres, wpack, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc, so, dg, do4, wk, st);
 }
 
 ENSVS_API int ensvs_downsample_fwd(const float* p0, int ld0, int n0, const float* p1, int ld1,

@@ -24,51 +24,17 @@
 // Every workgroup of the grid must be resident at once (2 NW <= 64 workgroups, one per CU);
 // the polls are bounded, so a grid that cannot become resident ends (flagging the error word
 // of the workspace) instead of hanging.
-#include "common.h"
+#include "coop.h"
 #include "ensvs.h"
 
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_;
 
 namespace {
 
-constexpr int NT = 256;     // 4 waves
-constexpr int UW = 16;      // hidden units per workgroup
-constexpr int SB = 32;      // sequence columns: two MFMA N tiles
+using namespace coop;
+
 constexpr int PSF = 68;     // forward partial-sum row per sequence: 64 gate rows + 4 (banks)
 constexpr int PSB = 20;     // backward: 16 units + 4
-constexpr int CP_SC1 = 16;  // buffer-op cache policy: sc1 (L1 bypass on both sides)
-constexpr int HDR = 256;    // workspace header: counters (one 64-B line per direction), error
-constexpr unsigned SPIN_MAX = 1u << 24;
-
-__device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
-__device__ __forceinline__ float tanh_fast(float x) {
-  return fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)), 1.f);
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab(unsigned* work, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((char*)work + HDR, 0, bytes, 0x00020000);
-}
-
-// wait until the direction's counter reaches `target` (one lane), then release the workgroup
-__device__ __forceinline__ void wait_count(unsigned* work, int d, unsigned target) {
-  if (threadIdx.x == 0) {
-    unsigned* cnt = work + d * 16;
-    unsigned it = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++it == SPIN_MAX) {  // a workgroup never arrived: flag it and go on
-        __hip_atomic_store(work + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ void signal(unsigned* work, int d) {
-  __hip_atomic_fetch_add(work + d * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 template <int H> struct CGeo {
   static constexpr int NW = H / UW;       // workgroups per direction
@@ -84,9 +50,9 @@ template <int H> struct CGeo {
 // gate m % 4; k = (wave KCW + kk) 32 + 8 (lane >> 4) + j.
 template <int H>
 __global__ void coop_pack_fwd_kernel(const float* __restrict__ w0, const float* __restrict__ w1,
-                                     _Float16* __restrict__ out) {
+                                     int ndir, _Float16* __restrict__ out) {
   using G = CGeo<H>;
-  const int n = 2 * 4 * H * H;
+  const int n = ndir * 4 * H * H;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int j = i & 7, lane = (i >> 3) & 63;
     int r = i >> 9;
@@ -105,9 +71,9 @@ __global__ void coop_pack_fwd_kernel(const float* __restrict__ w0, const float* 
 // n' = 64 w' + 4 u' + g (workgroup-major, unit-major inside), i.e. gate row g H + 16 w' + u'.
 template <int H>
 __global__ void coop_pack_bwd_kernel(const float* __restrict__ w0, const float* __restrict__ w1,
-                                     __bf16* __restrict__ out) {
+                                     int ndir, __bf16* __restrict__ out) {
   using G = CGeo<H>;
-  const int n = 2 * 4 * H * H;
+  const int n = ndir * 4 * H * H;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int j = i & 7, lane = (i >> 3) & 63;
     int r = i >> 9;
@@ -446,21 +412,28 @@ ENSVS_API long long ensvs_lstm_coop_work_bytes(int H) {
   return HDR + 2LL * 2 * SB * 4 * H * 2;  // header + the backward slab (the larger one)
 }
 
+int coop::pack(const float* w0, const float* w1, int ndir, int H, int bwd, void* out,
+               hipStream_t st) {
+  if (H != 128 && H != 256 && H != 512) return ENSVS_E_SHAPE;
+  if (!out || (uintptr_t)out % 16) return ENSVS_E_ARG;
+  const dim3 grid(cdiv((long long)ndir * 4 * H * H, 256)), block(256);
+#define COOP_PACK(HH)                                                                            \
+  if (H == HH) {                                                                                 \
+    if (bwd) hipLaunchKernelGGL(coop_pack_bwd_kernel<HH>, grid, block, 0, st, w0, w1, ndir, (__bf16*)out); \
+    else hipLaunchKernelGGL(coop_pack_fwd_kernel<HH>, grid, block, 0, st, w0, w1, ndir, (_Float16*)out); \
+  }
+  COOP_PACK(128)
+  COOP_PACK(256)
+  COOP_PACK(512)
+#undef COOP_PACK
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
 ENSVS_API int ensvs_lstm_coop_pack(const float* whh_f, const float* whh_r, int H, int bwd,
                                    void* out, void* stream) {
   if (H != 256 && H != 512) return ENSVS_E_SHAPE;
-  if (!out || (uintptr_t)out % 16) return ENSVS_E_ARG;
-  hipStream_t st = (hipStream_t)stream;
-  const dim3 grid(cdiv(2LL * 4 * H * H, 256)), block(256);
-  if (bwd) {
-    if (H == 256) hipLaunchKernelGGL(coop_pack_bwd_kernel<256>, grid, block, 0, st, whh_f, whh_r, (__bf16*)out);
-    else hipLaunchKernelGGL(coop_pack_bwd_kernel<512>, grid, block, 0, st, whh_f, whh_r, (__bf16*)out);
-  } else {
-    if (H == 256) hipLaunchKernelGGL(coop_pack_fwd_kernel<256>, grid, block, 0, st, whh_f, whh_r, (_Float16*)out);
-    else hipLaunchKernelGGL(coop_pack_fwd_kernel<512>, grid, block, 0, st, whh_f, whh_r, (_Float16*)out);
-  }
-  ENSVS_CHECK_LAUNCH();
-  return ENSVS_OK;
+  return coop::pack(whh_f, whh_r, 2, H, bwd, out, (hipStream_t)stream);
 }
 
 ENSVS_API int ensvs_lstm_coop_fwd(const float* gx, int ldg, const void* wpack,

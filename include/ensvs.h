@@ -211,6 +211,29 @@ int ensvs_ardec_bwd(const float* glf0, const float* gres, const float* wpb, cons
                     const float* wfo, int ldwfo, const float* mask, int teacher, int B, int T,
                     int H, float in_min, float in_max, float mean, float scale, const float* sg,
                     const float* sc, const float* so, float* dg, float* do4, void* stream);
+/* Cooperative AR decoder for H in {128, 256}, B <= 32 in production (bf16 GEMM) precision:
+ * one launch for all T/4 steps, the recurrence W_hh [h_1 .. h_B] split over H/16 workgroups
+ * that keep their W_hh slice in registers (fp16 forward, bf16 W_hh^T backward, fp32
+ * accumulation, gates, cell state, feat_out and saved values) and exchange h / dG plus the
+ * feat_out / prenet partial sums through `work` every step.  Same contract and saved layout as
+ * ensvs_ardec_fwd / ensvs_ardec_bwd (tacotron_f0.py:183-228).  wpack: ensvs_ardec_coop_pack
+ * (bwd = 0 forward fp16 fragments, bwd = 1 backward bf16 fragments), 4*H*H 2-byte elements;
+ * work: 256-B aligned, ensvs_ardec_coop_work_bytes(H) bytes, caller-owned, one per concurrent
+ * launch; bytes 128..131 read non-zero after a launch whose grid could not become resident. */
+int ensvs_ardec_coop_supported(int B, int H);
+long long ensvs_ardec_coop_work_bytes(int H);
+int ensvs_ardec_coop_pack(const float* whh, int H, int bwd, void* out, void* stream);
+int ensvs_ardec_coop_fwd(const float* gx, int ldgx, const float* ofx, int ldo, const void* wpack,
+                         const float* wih_p, const float* wfo, int ldwfo, const float* score,
+                         int lds, const float* mask, const float* teach, int ldt, int B, int T,
+                         int H, float in_min, float in_max, float mean, float scale, float* lf0,
+                         float* res, float* sg, float* sc, float* sh, float* so, float* sp,
+                         void* work, long long work_bytes, void* stream);
+int ensvs_ardec_coop_bwd(const float* glf0, const float* gres, const void* wpack,
+                         const float* wih_p, const float* wfo, int ldwfo, const float* mask,
+                         int teacher, int B, int T, int H, float in_min, float in_max, float mean,
+                         float scale, const float* sg, const float* sc, const float* so, float* dg,
+                         float* do4, void* work, long long work_bytes, void* stream);
 /* Depthwise Conv1d(k=4, s=4, groups=C) down-sampling (tacotron_f0.py:104-111,161-164). */
 int ensvs_downsample_fwd(const float* p0, int ld0, int n0, const float* p1, int ld1, int n1,
                          const float* p2, int ld2, int n2, const float* w, const float* bias, int B,

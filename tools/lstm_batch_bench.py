@@ -1,7 +1,7 @@
 """Batched MFMA LSTM recurrence (lstm_batch.hip) vs the exact per-(sequence, direction) kernels
 (lstm.hip) at the bench workload (30 sequences x 1024 frames, synthetic lengths), HIP events:
 us per launch and ns per recurrent step, for 16 / 8 sequences per workgroup and input
-prefetch depths 4 / 6.
+prefetch depths 2 / 3.
 python tools/lstm_batch_bench.py"""
 import os
 import sys
@@ -58,7 +58,7 @@ for H in (64, 128):
                                lens.data_ptr(), B, T, H, sv.data_ptr(), dg.data_ptr(), 8 * H, st)),
     }
     for name, (f, b) in runs.items():
-        for spw, depth in (((16, 4), (8, 4), (16, 6), (8, 6)) if name == "batch" else ((0, 0),)):
+        for spw, depth in (((16, 2), (8, 2), (4, 2), (8, 3), (4, 3)) if name == "batch" else ((0, 0),)):
             if spw:
                 call("ensvs_lstm_batch_set_cfg", spw, depth)
             uf, ub = timeit(f), timeit(b)
@@ -66,4 +66,4 @@ for H in (64, 128):
             print(f"H={H:4d} {name:5s} spw={spw:2d} depth={depth}  fwd {uf:8.1f} us "
                   f"({uf * 1e3 / steps:5.0f} ns/step)  bwd {ub:8.1f} us "
                   f"({ub * 1e3 / steps:5.0f} ns/step)", flush=True)
-    call("ensvs_lstm_batch_set_cfg", 0, 4)
+    call("ensvs_lstm_batch_set_cfg", 4, 2)

@@ -184,25 +184,6 @@ int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* w
  * backward bf16 fragments of W_hh^T), 2*4*H*H 2-byte elements.  work: 256-B aligned,
  * ensvs_lstm_coop_work_bytes(H) bytes, caller-owned, one per concurrent launch; bytes
  * 128..131 read non-zero after a launch whose grid could not become resident. */
-/* Batched MFMA recurrence for H = 64 / 128 in production (bf16 GEMM) precision
- * (lstm_batch.hip): one workgroup per (group of 8 or 16 sequences, direction) holds the
- * direction's W_hh as fp16 (forward) / bf16 (backward, W_hh^T) MFMA fragments and runs every
- * step; h / dG are exchanged in LDS.  Same contract as ensvs_lstm_fwd / ensvs_lstm_bwd (the
- * FFConvLSTM encoders H = 64 / 128, nnsvs/model.py:862-869, 914-916, and the lf0 encoder,
- * acoustic_models/tacotron_f0.py:876-883).  wpack: ensvs_lstm_batch_pack output (bwd = 0:
- * fp16 forward fragments, bwd = 1: bf16 backward fragments), 2*4*H*H 2-byte elements.
- * gx / y / saved / dy / dg 16-B aligned, leading dimensions multiples of 4.
- * ensvs_lstm_batch_set_cfg: sequences per workgroup (8 / 16) and input prefetch depth (2 / 3),
- * a measurement knob; the packs do not depend on it. */
-int ensvs_lstm_batch_supported(int B, int H);
-int ensvs_lstm_batch_set_cfg(int seqs_per_wg, int depth);
-int ensvs_lstm_batch_pack(const float* whh_f, const float* whh_r, int H, int bwd, void* out,
-                          void* stream);
-int ensvs_lstm_batch_fwd(const float* gx, int ldg, const void* wpack, const long long* lengths,
-                         int B, int T, int H, float* y, int ldy, float* saved, void* stream);
-int ensvs_lstm_batch_bwd(const float* dy, int lddy, const void* wpack, const long long* lengths,
-                         int B, int T, int H, const float* saved, float* dg, int lddg,
-                         void* stream);
 int ensvs_lstm_coop_supported(int B, int H);
 long long ensvs_lstm_coop_work_bytes(int H);
 int ensvs_lstm_coop_pack(const float* whh_f, const float* whh_r, int H, int bwd, void* out,

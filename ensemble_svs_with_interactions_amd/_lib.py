@@ -89,6 +89,10 @@ SIGNATURES = {
     "ensvs_lstm_set_step": [c_int],
     "ensvs_lstm_bwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int,
                        c_vp, c_ll, c_vp],
+    "ensvs_lstm_mfma_supported": [c_int],
+    "ensvs_lstm_mfma_pack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
+    "ensvs_lstm_mfma_fwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp],
+    "ensvs_lstm_mfma_bwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp],
     "ensvs_lstm_coop_supported": [c_int, c_int],
     "ensvs_lstm_coop_work_bytes": [c_int],
     "ensvs_lstm_coop_pack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
@@ -211,6 +215,7 @@ SIGNATURES = {
 RESTYPES = {"ensvs_embed_bwd_workspace": c_ll, "ensvs_usf_source_workspace": c_ll,
             "ensvs_attn_table_grad_workspace": c_ll, "ensvs_lstm_bwd_work_floats": c_ll,
             "ensvs_lstm_coop_work_bytes": c_ll, "ensvs_lstm_coop_supported": ctypes.c_int,
+            "ensvs_lstm_mfma_supported": ctypes.c_int,
             "ensvs_ardec_coop_work_bytes": c_ll, "ensvs_ardec_coop_supported": ctypes.c_int}
 
 _lib = None

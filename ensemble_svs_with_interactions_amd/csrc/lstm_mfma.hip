@@ -1,0 +1,461 @@
+// Bidirectional LSTM recurrence with MFMA recurrent products for H = 64 / 128 (the FFConvLSTM
+// encoders of the lf0 / mgc / bap / vuv streams, nnsvs/model.py:862-869, 914-916, the
+// multi-track lf0 encoder, acoustic_models/tacotron_f0.py:876-883, and the SeparateF0 bap
+// decoder's H = 62 on zero-padded gates) in production (bf16 GEMM) precision.
+//
+// Same contract and structure as lstm.hip's persistent kernels -- one workgroup per (sequence,
+// direction) runs every step, inputs staged through LDS in chunks of CH steps loaded one chunk
+// ahead, outputs collected in LDS and written at chunk boundaries, h / dG exchanged through a
+// double-buffered LDS vector, one barrier per step -- with the step's recurrent product on the
+// matrix cores instead of fp32 VALU FMAs.  lstm.hip's steps are bound by that VALU work and its
+// LDS operand traffic (H = 128: 0.76 / 1.19 us forward / backward, 128 FMAs and 64 LDS floats
+// per lane per step).  Here the workgroup's 4 waves hold the direction's W_hh as fp16 (forward:
+// h in [-1, 1]) / bf16 (backward, W_hh^T: dG spans many decades) MFMA fragments in VGPRs --
+// as the reference recipe's fp16 autocast runs its cuDNN LSTM (myconfig_notuseIL.yaml:6) --
+// and every MFMA column reads the same h / dG vector (an LDS broadcast), so the 16 columns of
+// each 16 x 16 result are identical and lane n of a 16-lane row takes tile n's values: one cell
+// per lane, no cross-lane reduction.  Gates, cell state, saved values and outputs stay fp32;
+// the fp32 parity mode keeps lstm.hip's exact kernels.  One sequence per workgroup keeps each
+// CU's global traffic at lstm.hip's (a batched layout with 4-16 sequences per workgroup was
+// bound by the per-CU store/load issue rate: profiles/r3_lstm_batch_bench.txt).
+//
+// Forward: wave v owns units [v H/4, (v+1) H/4) = NMT = H/16 tiles of 16 gate rows; row m of
+// tile mt is gate m % 4 of unit v H/4 + (m / 4) NMT + mt, so lane (lg = lane / 16, n) holds the
+// four gates of unit v H/4 + lg NMT + mt in tile mt's result and applies the cell of
+// mt = n (n < NMT).  Backward: dh = W_hh^T dG, units as M (TPW = H/64 tiles per wave), K = 4H in
+// the exchange order n' = 4 unit + gate; lane (lg, n) applies the cell of unit
+// v H/4 + lg 4 TPW + n (n < 4 TPW), taken from tile n / 4, row n % 4.
+#include "coop.h"
+#include "ensvs.h"
+
+namespace {
+
+using coop::sigm;
+using coop::tanh_fast;
+
+constexpr int NT = 256;
+
+template <int H> struct MGeo {
+  static constexpr int UPW = H / 4;     // units per wave
+  static constexpr int NMT = H / 16;    // forward M tiles per wave
+  static constexpr int NKC = H / 32;    // forward K chunks (K = H)
+  static constexpr int TPW = H / 64;    // backward M tiles per wave
+  static constexpr int NKB = H / 8;     // backward K chunks (K = 4H)
+  static constexpr int HP = H + 8;      // fp16 h vector (halves)
+  static constexpr int GP = 4 * H + 8;  // bf16 dG vector
+  static constexpr int CH = 16;         // steps per staged chunk
+  // LDS bytes: fwd in[CH][4H] + out[CH][6H] fp32 + h[2][HP] fp16; bwd in[CH][7H] + out[CH][4H]
+  // fp32 + dG[2][GP] bf16
+  static constexpr int FWD_LDS = CH * 10 * H * 4 + 2 * HP * 2;
+  static constexpr int BWD_LDS = CH * 11 * H * 4 + 2 * GP * 2;
+};
+
+// ---------------------------------------------------------------------------------- packs
+// forward fragments [dir][v][mt][kk][lane][8] fp16: A[m][k] = W_hh[g H + unit][k], m = lane & 15,
+// unit = v H/4 + (m / 4) NMT + mt, g = m % 4, k = 32 kk + 8 (lane / 16) + e
+template <int H>
+__global__ void mfma_pack_fwd_kernel(const float* __restrict__ w0, const float* __restrict__ w1,
+                                     _Float16* __restrict__ out) {
+  using G = MGeo<H>;
+  const int n = 2 * 4 * H * H;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int e = i & 7, lane = (i >> 3) & 63;
+    int r = i >> 9;
+    const int kk = r % G::NKC; r /= G::NKC;
+    const int mt = r % G::NMT; r /= G::NMT;
+    const int v = r % 4, d = r / 4;
+    const int m = lane & 15;
+    const int unit = v * G::UPW + (m >> 2) * G::NMT + mt, g = m & 3;
+    const int k = kk * 32 + 8 * (lane >> 4) + e;
+    out[i] = (_Float16)(d ? w1 : w0)[(long long)(g * H + unit) * H + k];
+  }
+}
+
+// backward fragments of W_hh^T [dir][v][mt][kk][lane][8] bf16: row m = lane & 15 is unit
+// v H/4 + (m / 4) 4 TPW + 4 mt + m % 4; k = n' = 32 kk + 8 (lane / 16) + e in the exchange
+// order n' = 4 unit' + g (gate row g H + unit')
+template <int H>
+__global__ void mfma_pack_bwd_kernel(const float* __restrict__ w0, const float* __restrict__ w1,
+                                     __bf16* __restrict__ out) {
+  using G = MGeo<H>;
+  const int n = 2 * 4 * H * H;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int e = i & 7, lane = (i >> 3) & 63;
+    int r = i >> 9;
+    const int kk = r % G::NKB; r /= G::NKB;
+    const int mt = r % G::TPW; r /= G::TPW;
+    const int v = r % 4, d = r / 4;
+    const int m = lane & 15;
+    const int unit = v * G::UPW + (m >> 2) * 4 * G::TPW + 4 * mt + (m & 3);
+    const int np = kk * 32 + 8 * (lane >> 4) + e;
+    const int row = (np & 3) * H + (np >> 2);
+    out[i] = (__bf16)(d ? w1 : w0)[(long long)row * H + unit];
+  }
+}
+
+// ---------------------------------------------------------------------------------- helpers
+// b where the mask is set, else a: bit selects (v_bfi), so the compiler does not turn a
+// lane-dependent choice between registers into a scratch-indexed load
+__device__ __forceinline__ float bsel(unsigned m, float a, float b) {
+  return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, a) & ~m) |
+                                       (__builtin_bit_cast(unsigned, b) & m));
+}
+// v[idx] for a lane-dependent idx < N (N = 4 / 8); m[b]: all-ones where bit b of idx is set
+template <int N>
+__device__ __forceinline__ float pick(const float (&v)[N], const unsigned (&m)[3]) {
+  const float a0 = bsel(m[0], v[0], v[1]), a1 = bsel(m[0], v[2], v[3]);
+  const float b0 = bsel(m[1], a0, a1);
+  if constexpr (N == 4) {
+    return b0;
+  } else {
+    static_assert(N == 8, "pick");
+    const float a2 = bsel(m[0], v[4], v[5]), a3 = bsel(m[0], v[6], v[7]);
+    return bsel(m[2], b0, bsel(m[1], a2, a3));
+  }
+}
+
+// ---------------------------------------------------------------------------------- forward
+template <int H>
+__global__ __launch_bounds__(NT) void lstm_mfma_fwd_kernel(
+    const float* __restrict__ gx, int ldg,        // [B*T][ldg], dir d gates at cols d*4H + g*H + u
+    const f16x8* __restrict__ wp,                 // packed forward fragments
+    const long long* __restrict__ lengths, int T,
+    float* __restrict__ y, int ldy,               // [B*T][ldy], dir d at cols d*H + u
+    float* __restrict__ sv) {                     // saved [B*T][2][5H]: i,f,g,o,c
+  using G = MGeo<H>;
+  constexpr int NMT = G::NMT, NKC = G::NKC, HP = G::HP, CH = G::CH, GW = 4 * H, OW = 6 * H;
+  constexpr int PF = CH * GW / 4 / NT;  // float4 of one input chunk per thread
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* gin = lds;                          // [CH][4H] gate pre-activations x W_ih^T + b
+  float* out = gin + CH * GW;                // [CH][6H]: h, then i f g o c
+  _Float16* hb = (_Float16*)(out + CH * OW);  // [2][HP] h_{t-1} (fp16)
+  const int b = blockIdx.x, dir = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, v = tid >> 6, lg = lane >> 4, n = lane & 15;
+  const int L = (int)lengths[b];
+
+  f16x8 wf[NMT][NKC];
+  {
+    const f16x8* src = wp + ((long long)(dir * 4 + v) * NMT * NKC) * 64 + lane;
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt)
+#pragma unroll
+      for (int kk = 0; kk < NKC; ++kk) wf[mt][kk] = src[(mt * NKC + kk) * 64];
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt)
+#pragma unroll
+      for (int kk = 0; kk < NKC; ++kk) asm volatile("" ::"v"(wf[mt][kk]));
+  }
+  for (int i = tid; i < 2 * HP; i += NT) hb[i] = (_Float16)0.f;
+  // lane n takes tile n's cell (lanes n >= NMT repeat a tile's cell and do not write)
+  const int sel = n & (NMT - 1);
+  const bool act = n < NMT;
+  const unsigned msk[3] = {(sel & 1) ? ~0u : 0u, (sel & 2) ? ~0u : 0u, (sel & 4) ? ~0u : 0u};
+  const int u = v * G::UPW + lg * NMT + sel;
+  float c = 0.f;
+
+  const long long rowb = (long long)b * T;
+  for (int i = tid; i < (T - L) * H; i += NT)
+    y[(rowb + L + i / H) * ldy + dir * H + (i % H)] = 0.f;
+
+  const int nch = (L + CH - 1) / CH;
+  f32x4 rin[PF];
+  auto load_chunk = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + i * NT, st = e / (GW / 4), c4 = e % (GW / 4);
+      const int s = ch * CH + st;
+      const int row = dir ? L - 1 - s : s;
+      rin[i] = s < L ? *(const f32x4*)(gx + (rowb + row) * ldg + dir * GW + c4 * 4)
+                     : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_in = [&]() {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + i * NT;
+      *(f32x4*)(gin + (e / (GW / 4)) * GW + (e % (GW / 4)) * 4) = rin[i];
+    }
+  };
+  auto flush = [&](int ch) {
+    const int cnt = min(CH, L - ch * CH);
+    for (int e = tid; e < cnt * (OW / 4); e += NT) {
+      const int st = e / (OW / 4), c4 = e % (OW / 4);
+      const int s = ch * CH + st;
+      const long long row = rowb + (dir ? L - 1 - s : s);
+      const f32x4 val = *(const f32x4*)(out + st * OW + c4 * 4);
+      if (c4 < H / 4) *(f32x4*)(y + row * ldy + dir * H + c4 * 4) = val;
+      else *(f32x4*)(sv + (row * 2 + dir) * 5 * H + (c4 - H / 4) * 4) = val;
+    }
+  };
+
+  if (nch > 0) {
+    load_chunk(0);
+    store_in();
+  }
+  if (nch > 1) load_chunk(1);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const int cnt = min(CH, L - ch * CH);
+    for (int st = 0; st < cnt; ++st) {
+      const int s = ch * CH + st;
+      const _Float16* hc = hb + ((s + 1) & 1) * HP + 8 * lg;
+      f16x8 bf[NKC];
+#pragma unroll
+      for (int kk = 0; kk < NKC; ++kk) bf[kk] = *(const f16x8*)(hc + 32 * kk);
+      f32x4 acc[NMT];
+#pragma unroll
+      for (int mt = 0; mt < NMT; ++mt) {
+        acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < NKC; ++kk)
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[mt][kk], bf[kk], acc[mt], 0, 0, 0);
+      }
+      float a[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float col[NMT];
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt) col[mt] = acc[mt][g];
+        a[g] = pick<NMT>(col, msk) + gin[st * GW + g * H + u];
+      }
+      const float ig = sigm(a[0]), fg = sigm(a[1]), gg = tanh_fast(a[2]), og = sigm(a[3]);
+      c = fg * c + ig * gg;
+      const float h = og * tanh_fast(c);
+      if (act) {
+        hb[(s & 1) * HP + u] = (_Float16)h;
+        float* o = out + st * OW;
+        o[u] = h;
+        o[H + u] = ig;
+        o[2 * H + u] = fg;
+        o[3 * H + u] = gg;
+        o[4 * H + u] = og;
+        o[5 * H + u] = c;
+      }
+      __syncthreads();
+    }
+    if (ch + 1 < nch) store_in();
+    flush(ch);
+    if (ch + 2 < nch) load_chunk(ch + 2);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------- backward
+template <int H>
+__global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
+    const float* __restrict__ dy, int lddy,       // [B*T][lddy], grad of outputs
+    const bf16x8* __restrict__ wp,                // packed backward fragments
+    const long long* __restrict__ lengths, int T,
+    const float* __restrict__ sv,                 // saved [B*T][2][5H]
+    float* __restrict__ dg, int lddg) {           // [B*T][lddg], dir d pre-act grads at d*4H + g*H + u
+  using G = MGeo<H>;
+  constexpr int TPW = G::TPW, NKB = G::NKB, GP = G::GP, CH = G::CH, IW = 7 * H, GW = 4 * H;
+  constexpr int NIN = CH * IW / 4;  // float4 per input chunk
+  constexpr int PF = (NIN + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* gin = lds;                        // [CH][7H]: i f g o c (row t), dy (row t), c (previous step)
+  float* out = gin + CH * IW;              // [CH][4H]
+  __bf16* gb = (__bf16*)(out + CH * GW);   // [2][GP] dG of the previous processing step (bf16)
+  const int b = blockIdx.x, dir = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, v = tid >> 6, lg = lane >> 4, n = lane & 15;
+  const int L = (int)lengths[b];
+
+  bf16x8 wb[TPW][NKB];
+  {
+    const bf16x8* src = wp + ((long long)(dir * 4 + v) * TPW * NKB) * 64 + lane;
+#pragma unroll
+    for (int mt = 0; mt < TPW; ++mt)
+#pragma unroll
+      for (int kk = 0; kk < NKB; ++kk) wb[mt][kk] = src[(mt * NKB + kk) * 64];
+#pragma unroll
+    for (int mt = 0; mt < TPW; ++mt)
+#pragma unroll
+      for (int kk = 0; kk < NKB; ++kk) asm volatile("" ::"v"(wb[mt][kk]));
+  }
+  for (int i = tid; i < 2 * GP; i += NT) gb[i] = (__bf16)0.f;
+  // lane n takes the cell of tile n / 4, row n % 4 (lanes n >= 4 TPW repeat one and do not write)
+  const int sel = n & (4 * TPW - 1);
+  const bool act = n < 4 * TPW;
+  const unsigned msk[3] = {(sel & 1) ? ~0u : 0u, (sel & 2) ? ~0u : 0u, (sel & 4) ? ~0u : 0u};
+  const int u = v * G::UPW + lg * 4 * TPW + sel;
+
+  const long long rowb = (long long)b * T;
+  for (int i = tid; i < (T - L) * GW; i += NT)
+    dg[(rowb + L + i / GW) * lddg + dir * GW + (i % GW)] = 0.f;
+
+  // chunk ch holds processing steps s = L-1-ch*CH-st, st = 0..CH-1 (descending s)
+  const int nch = (L + CH - 1) / CH;
+  f32x4 rin[PF];
+  auto svrow = [&](int s) { return sv + ((rowb + (dir ? L - 1 - s : s)) * 2 + dir) * 5 * H; };
+  auto load_chunk = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + i * NT, st = e / (IW / 4), c4 = e % (IW / 4);
+      const int s = L - 1 - ch * CH - st;
+      f32x4 val = {0.f, 0.f, 0.f, 0.f};
+      if (e < NIN && s >= 0) {
+        if (c4 < 5 * H / 4) val = *(const f32x4*)(svrow(s) + c4 * 4);
+        else if (c4 < 6 * H / 4)
+          val = *(const f32x4*)(dy + (rowb + (dir ? L - 1 - s : s)) * lddy + dir * H +
+                                (c4 - 5 * H / 4) * 4);
+        else if (s > 0) val = *(const f32x4*)(svrow(s - 1) + 4 * H + (c4 - 6 * H / 4) * 4);
+      }
+      rin[i] = val;
+    }
+  };
+  auto store_in = [&]() {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = tid + i * NT;
+      if (e < NIN) *(f32x4*)(gin + (e / (IW / 4)) * IW + (e % (IW / 4)) * 4) = rin[i];
+    }
+  };
+  auto flush = [&](int ch) {
+    const int cnt = min(CH, L - ch * CH);
+    for (int e = tid; e < cnt * (GW / 4); e += NT) {
+      const int st = e / (GW / 4), c4 = e % (GW / 4);
+      const int s = L - 1 - ch * CH - st;
+      const long long row = rowb + (dir ? L - 1 - s : s);
+      *(f32x4*)(dg + row * lddg + dir * GW + c4 * 4) = *(const f32x4*)(out + st * GW + c4 * 4);
+    }
+  };
+
+  if (nch > 0) {
+    load_chunk(0);
+    store_in();
+  }
+  if (nch > 1) load_chunk(1);
+  __syncthreads();
+  float dc = 0.f;
+  for (int ch = 0; ch < nch; ++ch) {
+    const int cnt = min(CH, L - ch * CH);
+    for (int st = 0; st < cnt; ++st) {
+      const int p = ch * CH + st;  // processing index
+      const __bf16* gc = gb + ((p + 1) & 1) * GP + 8 * lg;
+      bf16x8 bf[NKB];
+#pragma unroll
+      for (int kk = 0; kk < NKB; ++kk) bf[kk] = *(const bf16x8*)(gc + 32 * kk);
+      f32x4 acc[TPW];
+#pragma unroll
+      for (int mt = 0; mt < TPW; ++mt) {
+        acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < NKB; ++kk)
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][kk], bf[kk], acc[mt], 0, 0, 0);
+      }
+      float flat[4 * TPW];
+#pragma unroll
+      for (int f = 0; f < 4 * TPW; ++f) flat[f] = acc[f >> 2][f & 3];
+      const float dhr = pick<4 * TPW>(flat, msk);
+      const float* in = gin + st * IW;
+      const float ig = in[u], fg = in[H + u], gg = in[2 * H + u], og = in[3 * H + u];
+      const float ct = in[4 * H + u], dyv = in[5 * H + u], cp = in[6 * H + u];
+      const float dh = dyv + dhr;
+      const float tc = tanh_fast(ct);
+      const float dcc = dc + dh * og * (1.f - tc * tc);
+      const float d_i = dcc * gg * ig * (1.f - ig);
+      const float d_f = dcc * cp * fg * (1.f - fg);
+      const float d_g = dcc * ig * (1.f - gg * gg);
+      const float d_o = dh * tc * og * (1.f - og);
+      dc = dcc * fg;
+      if (act) {
+        bf16x4 nb;
+        nb[0] = (__bf16)d_i;
+        nb[1] = (__bf16)d_f;
+        nb[2] = (__bf16)d_g;
+        nb[3] = (__bf16)d_o;
+        *(bf16x4*)(gb + (p & 1) * GP + 4 * u) = nb;
+        float* o = out + st * GW;
+        o[u] = d_i;
+        o[H + u] = d_f;
+        o[2 * H + u] = d_g;
+        o[3 * H + u] = d_o;
+      }
+      __syncthreads();
+    }
+    if (ch + 1 < nch) store_in();
+    flush(ch);
+    if (ch + 2 < nch) load_chunk(ch + 2);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------- launch
+size_t excl(size_t need) {
+  return ensvs_rec_exclusive() ? std::max<size_t>(need, 160 * 1024) : need;
+}
+
+template <int H>
+int launch_fwd(const float* gx, int ldg, const void* wp, const long long* lengths, int B, int T,
+               float* y, int ldy, float* sv, hipStream_t st) {
+  const size_t lds = excl(MGeo<H>::FWD_LDS);
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)lstm_mfma_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(lstm_mfma_fwd_kernel<H>, dim3(B, 2), dim3(NT), lds, st, gx, ldg,
+                     (const f16x8*)wp, lengths, T, y, ldy, sv);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+template <int H>
+int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengths, int B, int T,
+               const float* sv, float* dg, int lddg, hipStream_t st) {
+  const size_t lds = excl(MGeo<H>::BWD_LDS);
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)lstm_mfma_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(lstm_mfma_bwd_kernel<H>, dim3(B, 2), dim3(NT), lds, st, dy, lddy,
+                     (const bf16x8*)wp, lengths, T, sv, dg, lddg);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+bool aligned16(const void* p) { return (uintptr_t)p % 16 == 0; }
+
+}  // namespace
+
+ENSVS_API int ensvs_lstm_mfma_supported(int H) { return H == 64 || H == 128 ? 1 : 0; }
+
+ENSVS_API int ensvs_lstm_mfma_pack(const float* whh_f, const float* whh_r, int H, int bwd,
+                                   void* out, void* stream) {
+  if (!ensvs_lstm_mfma_supported(H)) return ENSVS_E_SHAPE;
+  if (!out || !aligned16(out) || !whh_f || !whh_r) return ENSVS_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid(cdiv(2LL * 4 * H * H, 256)), block(256);
+  if (H == 64) {
+    if (bwd) hipLaunchKernelGGL(mfma_pack_bwd_kernel<64>, grid, block, 0, st, whh_f, whh_r, (__bf16*)out);
+    else hipLaunchKernelGGL(mfma_pack_fwd_kernel<64>, grid, block, 0, st, whh_f, whh_r, (_Float16*)out);
+  } else {
+    if (bwd) hipLaunchKernelGGL(mfma_pack_bwd_kernel<128>, grid, block, 0, st, whh_f, whh_r, (__bf16*)out);
+    else hipLaunchKernelGGL(mfma_pack_fwd_kernel<128>, grid, block, 0, st, whh_f, whh_r, (_Float16*)out);
+  }
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_lstm_mfma_fwd(const float* gx, int ldg, const void* wpack,
+                                  const long long* lengths, int B, int T, int H, float* y, int ldy,
+                                  float* saved, void* stream) {
+  if (!ensvs_lstm_mfma_supported(H) || B <= 0 || T <= 0 || ldg < 8 * H || ldy < 2 * H)
+    return ENSVS_E_SHAPE;
+  if (ldg % 4 || ldy % 4 || !aligned16(gx) || !aligned16(y) || !aligned16(saved) ||
+      !aligned16(wpack) || !lengths)
+    return ENSVS_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  return H == 64 ? launch_fwd<64>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, st)
+                 : launch_fwd<128>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, st);
+}
+
+ENSVS_API int ensvs_lstm_mfma_bwd(const float* dy, int lddy, const void* wpack,
+                                  const long long* lengths, int B, int T, int H,
+                                  const float* saved, float* dg, int lddg, void* stream) {
+  if (!ensvs_lstm_mfma_supported(H) || B <= 0 || T <= 0 || lddy < 2 * H || lddg < 8 * H)
+    return ENSVS_E_SHAPE;
+  if (lddy % 4 || lddg % 4 || !aligned16(dy) || !aligned16(dg) || !aligned16(saved) ||
+      !aligned16(wpack) || !lengths)
+    return ENSVS_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  return H == 64 ? launch_bwd<64>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, st)
+                 : launch_bwd<128>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, st);
+}

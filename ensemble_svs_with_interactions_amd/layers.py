@@ -391,6 +391,33 @@ def _coop_pack(lstm, l, bwd):
     return ent[1]
 
 
+def lstm_mfma(H):
+    """Whether a layer of hidden size H (after zero padding, lstm_pad) runs the MFMA
+    recurrences (lstm_mfma.hip: H = 64 / 128 in production bf16 precision; fp16 / bf16
+    recurrent products with fp32 accumulation, gates and cell state).  The fp32 parity mode
+    keeps lstm.hip's exact kernels."""
+    return gemm_dtype() == _lib.DT_BF16 and query("ensvs_lstm_mfma_supported", H) == 1
+
+
+def _mfma_pack(lstm, l, bwd, HP=None):
+    """W_hh of layer l (both directions; zero-padded to HP when given) as the MFMA
+    recurrences' fragments, repacked whenever the weights changed (as _coop_pack)."""
+    from .engine import _sig
+    ws = [getattr(lstm, f"weight_hh_l{l}"), getattr(lstm, f"weight_hh_l{l}_reverse")]
+    cache = lstm.__dict__.setdefault("_ensvs_mfma", {})
+    sig = _sig(ws)
+    ent = cache.get((l, bwd))
+    if ent is None or ent[0] != sig:
+        H = HP or lstm.hidden_size
+        src = _whh_pad(lstm, l, HP) if HP else ws
+        buf = ent[1] if ent is not None else torch.empty(
+            2 * 4 * H * H, dtype=torch.bfloat16 if bwd else torch.float16, device=ws[0].device)
+        call("ensvs_lstm_mfma_pack", src[0].data_ptr(), src[1].data_ptr(), H, int(bwd),
+             buf.data_ptr(), stream())
+        ent = cache[(l, bwd)] = (sig, buf)
+    return ent[1]
+
+
 _PERSIST_H = (8, 16, 32, 64, 128)
 
 
@@ -455,13 +482,21 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
         elif HP:
             gxp = empty(M, 8 * HP, device=device)
             _regroup(gx, 8 * H, gxp, 8 * HP, M, 8, H, HP)
-            w0, w1 = _whh_pad(lstm, l, HP)
             yp = empty(M, 2 * HP, device=device)
-            call("ensvs_lstm_fwd", gxp.data_ptr(), 8 * HP, w0.data_ptr(), w1.data_ptr(),
-                 lens_dev.data_ptr(), B, T, HP, yp.data_ptr(), 2 * HP, saved.data_ptr(),
-                 stream())
+            if lstm_mfma(HP):
+                call("ensvs_lstm_mfma_fwd", gxp.data_ptr(), 8 * HP,
+                     _mfma_pack(lstm, l, False, HP).data_ptr(), lens_dev.data_ptr(), B, T, HP,
+                     yp.data_ptr(), 2 * HP, saved.data_ptr(), stream())
+            else:
+                w0, w1 = _whh_pad(lstm, l, HP)
+                call("ensvs_lstm_fwd", gxp.data_ptr(), 8 * HP, w0.data_ptr(), w1.data_ptr(),
+                     lens_dev.data_ptr(), B, T, HP, yp.data_ptr(), 2 * HP, saved.data_ptr(),
+                     stream())
             _regroup(yp, 2 * HP, y, 2 * H, M, 2, HP, H)
             del gxp, yp
+        elif lstm_mfma(H):
+            call("ensvs_lstm_mfma_fwd", gx.data_ptr(), 8 * H, _mfma_pack(lstm, l, False).data_ptr(),
+                 lens_dev.data_ptr(), B, T, H, y.data_ptr(), 2 * H, saved.data_ptr(), stream())
         else:
             call("ensvs_lstm_fwd", gx.data_ptr(), 8 * H,
                  getattr(lstm, f"weight_hh_l{l}").data_ptr(),
@@ -500,14 +535,23 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
             dp = empty(M, 2 * HP, device=device)
             _regroup(d, 2 * H, dp, 2 * HP, M, 2, H, HP)
             dgp = empty(M, 8 * HP, device=device)
-            w0, w1 = _whh_pad(lstm, l, HP)
-            nw = query("ensvs_lstm_bwd_work_floats", B, HP)
-            work = empty(max(nw, 1), device=device)
-            call("ensvs_lstm_bwd", dp.data_ptr(), 2 * HP, w0.data_ptr(), w1.data_ptr(),
-                 lens_dev.data_ptr(), B, T, HP, s["saved"].data_ptr(), dgp.data_ptr(), 8 * HP,
-                 work.data_ptr(), nw, stream())
+            if lstm_mfma(HP):
+                call("ensvs_lstm_mfma_bwd", dp.data_ptr(), 2 * HP,
+                     _mfma_pack(lstm, l, True, HP).data_ptr(), lens_dev.data_ptr(), B, T, HP,
+                     s["saved"].data_ptr(), dgp.data_ptr(), 8 * HP, stream())
+            else:
+                w0, w1 = _whh_pad(lstm, l, HP)
+                nw = query("ensvs_lstm_bwd_work_floats", B, HP)
+                work = empty(max(nw, 1), device=device)
+                call("ensvs_lstm_bwd", dp.data_ptr(), 2 * HP, w0.data_ptr(), w1.data_ptr(),
+                     lens_dev.data_ptr(), B, T, HP, s["saved"].data_ptr(), dgp.data_ptr(),
+                     8 * HP, work.data_ptr(), nw, stream())
             _regroup(dgp, 8 * HP, dg, 8 * H, M, 8, HP, H)
             del dp, dgp
+        elif lstm_mfma(H):
+            call("ensvs_lstm_mfma_bwd", d.data_ptr(), 2 * H, _mfma_pack(lstm, l, True).data_ptr(),
+                 lens_dev.data_ptr(), B, T, H, s["saved"].data_ptr(), dg.data_ptr(), 8 * H,
+                 stream())
         else:
             nw = query("ensvs_lstm_bwd_work_floats", B, H)
             work = empty(max(nw, 1), device=device)

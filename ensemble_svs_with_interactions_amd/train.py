@@ -235,6 +235,25 @@ def broadcast_state(model, src=0, group=None):
     weights_updated()
 
 
+def sync_buffers(model, src=0, group=None):
+    """DistributedDataParallel's default ``broadcast_buffers=True`` (the reference wraps the
+    model in DDP(model, device_ids=[...]), train_util.py:1446): rank ``src``'s buffers (the
+    BatchNorm running statistics) go to every rank before each step's forward, so an eval,
+    inference or checkpoint on any rank sees rank src's statistics.  One broadcast per dtype
+    of the coalesced buffers (a few KB)."""
+    import torch.distributed as dist
+    if world_size(group) == 1:
+        return
+    by_dtype = {}
+    for b in model.buffers():
+        by_dtype.setdefault((b.dtype, b.device), []).append(b)
+    for ts in by_dtype.values():
+        flat = torch._utils._flatten_dense_tensors(ts)
+        dist.broadcast(flat, src, group=group)
+        for t, f in zip(ts, torch._utils._unflatten_dense_tensors(flat, ts)):
+            t.copy_(f)
+
+
 def allreduce_grads(gflat, group=None):
     """Data-parallel gradient exchange: ONE sum all-reduce (RCCL over xGMI on the GPU
     box) of the flat gradient buffer.  The 1/world average is already folded into the
@@ -357,6 +376,8 @@ def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengt
     logf0_diff_weight > 0 adds the log-F0 interaction loss between the main and sub tracks
     (train_acoustic_multitrack.py:175-182, 296; needs the output_subtrack model and y_sub).
     """
+    if ddp and world_size() > 1:
+        sync_buffers(model)
     loss = _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
                            draws, ddp, y_sub, logf0_diff_weight, overlap=True)
     if ddp and world_size() > 1 and not getattr(optimizer, "_reduced", False):
@@ -548,6 +569,8 @@ class GraphedTrainStep:
                 raise ValueError(f"{k}: shape {tuple(v.shape)} differs from the captured one")
             dst.copy_(v, non_blocking=True)
         self.opt.sync_lr()  # a scheduler's lr change reaches the replayed update
+        if self.ddp and world_size() > 1:
+            sync_buffers(self.model)
         self.g_grads.replay()
         if self.ddp and world_size() > 1:
             allreduce_grads(self.opt.gflat)

@@ -184,6 +184,23 @@ int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* w
  * backward bf16 fragments of W_hh^T), 2*4*H*H 2-byte elements.  work: 256-B aligned,
  * ensvs_lstm_coop_work_bytes(H) bytes, caller-owned, one per concurrent launch; bytes
  * 128..131 read non-zero after a launch whose grid could not become resident. */
+/* MFMA recurrence for H = 64 / 128 in production (bf16 GEMM) precision (lstm_mfma.hip): the
+ * structure of the persistent kernels above (one workgroup per (sequence, direction), chunked
+ * LDS staging) with the recurrent product h W_hh^T (fp16 fragments) / dG W_hh (bf16) on MFMA,
+ * fp32 accumulation, gates, cell state and saved values.  Same contract as ensvs_lstm_fwd /
+ * ensvs_lstm_bwd (the FFConvLSTM encoders, nnsvs/model.py:862-869, 914-916; the lf0 encoder,
+ * acoustic_models/tacotron_f0.py:876-883).  wpack: ensvs_lstm_mfma_pack output for both
+ * directions (bwd = 0: fp16 forward fragments, bwd = 1: bf16 backward fragments of W_hh^T),
+ * 2*4*H*H 2-byte elements, 16-B aligned; gx / y / saved / dy / dg 16-B aligned, leading
+ * dimensions multiples of 4. */
+int ensvs_lstm_mfma_supported(int H);
+int ensvs_lstm_mfma_pack(const float* whh_f, const float* whh_r, int H, int bwd, void* out,
+                         void* stream);
+int ensvs_lstm_mfma_fwd(const float* gx, int ldg, const void* wpack, const long long* lengths,
+                        int B, int T, int H, float* y, int ldy, float* saved, void* stream);
+int ensvs_lstm_mfma_bwd(const float* dy, int lddy, const void* wpack, const long long* lengths,
+                        int B, int T, int H, const float* saved, float* dg, int lddg,
+                        void* stream);
 int ensvs_lstm_coop_supported(int B, int H);
 long long ensvs_lstm_coop_work_bytes(int H);
 int ensvs_lstm_coop_pack(const float* whh_f, const float* whh_r, int H, int bwd, void* out,

@@ -106,6 +106,24 @@ def _rank(rank, port, out_dir):
         torch.cuda.synchronize()
         check_mean(opt, "fused")
         fused_grad = opt.gflat.detach().cpu().clone()
+        # DDP's broadcast_buffers: the ranks' BatchNorm statistics differ after a step on
+        # their own shards; the next step starts from rank 0's on every rank
+        bufs = lambda m: torch.cat([b.detach().float().flatten() for b in m.buffers()])  # noqa: E731
+        after = gather(bufs(model))
+        res["bn_stats_differ_after_step"] = float((after[0] - after[1]).abs().max())
+        synced = []
+        orig_sync = train.sync_buffers
+
+        def sync_spy(m, *a, **k):
+            orig_sync(m, *a, **k)
+            synced.append(bufs(m).cpu())
+        train.sync_buffers = sync_spy
+        train.train_step(model, opt, xm, xs, ym, s0, s1, lens, draws=draws)
+        torch.cuda.synchronize()
+        train.sync_buffers = orig_sync
+        got = gather(synced[0])
+        res["bn_sync_rank_mismatch"] = float((got[0] - got[1]).abs().max())
+        res["bn_sync_vs_rank0"] = float((got[1] - after[0]).abs().max())
 
         # 2b: the same step with the bucketed all-reduce overlapped with the backward
         # (train.BucketedAllReduce): the same reduced gradient, no whole-buffer all-reduce
@@ -247,6 +265,9 @@ def test_data_parallel_world2_product_step(tmp_path):
         assert z["overlap_param_mismatch"] == 0.0
         assert z["overlap_whole_buffer_calls"] == 0 and z["overlap_buckets"] >= 6
         assert z["ddp_grad_err"] < 1e-5, z["ddp_grad_err"]
+        # broadcast_buffers: statistics differ after a step, equal rank 0's at the next one
+        assert z["bn_stats_differ_after_step"] > 0.0
+        assert z["bn_sync_rank_mismatch"] == 0.0 and z["bn_sync_vs_rank0"] == 0.0
         # DP-W gradient == 1-process full-batch gradient (BN frozen, equal lengths)
         assert z["dp_vs_full_grad_rel_l2"] < 1e-6, z["dp_vs_full_grad_rel_l2"]
         assert z["dp_vs_full_loss_rel"] < 1e-6, z["dp_vs_full_loss_rel"]

@@ -50,7 +50,7 @@ def test_lstm_step_kernels_long_and_wide_batch():
     _check(64 + 6, 61, 37, 8, lens, 1e-5, 1e-4)
 
 
-def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False):
+def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False, mfma=False):
     torch.manual_seed(H + T)
     lstm = torch.nn.LSTM(I, H, batch_first=True, bidirectional=True)
     x = torch.randn(B, T, I, requires_grad=True)
@@ -82,6 +82,15 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False):
         call("ensvs_lstm_coop_fwd", gx_d.data_ptr(), 8 * H, wpf.data_ptr(), lens.data_ptr(), B, T,
              H, y.data_ptr(), 2 * H, saved.data_ptr(), cwork.data_ptr(), nbytes, st)
         assert cwork[128:132].cpu().view(torch.int32).item() == 0  # every workgroup resident
+    elif mfma:
+        assert query("ensvs_lstm_mfma_supported", H) == 1
+        wpf = torch.empty(2 * 4 * H * H, dtype=torch.float16, device=dev)
+        wpb = torch.empty(2 * 4 * H * H, dtype=torch.bfloat16, device=dev)
+        call("ensvs_lstm_mfma_pack", whh[0].data_ptr(), whh[1].data_ptr(), H, 0, wpf.data_ptr(), st)
+        call("ensvs_lstm_mfma_pack", whh[0].data_ptr(), whh[1].data_ptr(), H, 1, wpb.data_ptr(), st)
+        y.fill_(float("nan"))
+        call("ensvs_lstm_mfma_fwd", gx_d.data_ptr(), 8 * H, wpf.data_ptr(), lens.data_ptr(), B, T,
+             H, y.data_ptr(), 2 * H, saved.data_ptr(), st)
     else:
         call("ensvs_lstm_fwd", gx_d.data_ptr(), 8 * H, whh[0].data_ptr(), whh[1].data_ptr(),
              lens.data_ptr(), B, T, H, y.data_ptr(), 2 * H, saved.data_ptr(), st)
@@ -97,6 +106,10 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False):
         call("ensvs_lstm_coop_bwd", gy_d.data_ptr(), 2 * H, wpb.data_ptr(), lens.data_ptr(), B, T,
              H, saved.data_ptr(), dg.data_ptr(), 8 * H, cwork.data_ptr(), nbytes, st)
         assert cwork[128:132].cpu().view(torch.int32).item() == 0
+    elif mfma:
+        dg.fill_(float("nan"))
+        call("ensvs_lstm_mfma_bwd", gy_d.data_ptr(), 2 * H, wpb.data_ptr(), lens.data_ptr(), B, T,
+             H, saved.data_ptr(), dg.data_ptr(), 8 * H, st)
     else:
         call("ensvs_lstm_bwd", gy_d.data_ptr(), 2 * H, whh[0].data_ptr(), whh[1].data_ptr(),
              lens.data_ptr(), B, T, H, saved.data_ptr(), dg.data_ptr(), 8 * H, work.data_ptr(),
@@ -125,8 +138,8 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False):
     dx = sum(dg[:, :, 4 * H * d:4 * H * (d + 1)] @ P["weight_ih_l0" + s].detach()
              for d, s in enumerate(("", "_reverse")))
     errs["dx"] = rel(dx, x.grad)
-    if coop:
-        record_errors(f"lstm_coop_H{H}_B{B}_T{T}", errs)
+    if coop or mfma:
+        record_errors(f"lstm_{'coop' if coop else 'mfma'}_H{H}_B{B}_T{T}", errs)
     assert errs["dx"] < tol_g
 
 
@@ -145,3 +158,22 @@ def test_lstm_coop_matches_torch(H, B, T, lengths):
         g = torch.Generator().manual_seed(H + B)
         lengths = [T] + torch.randint(1, T + 1, (B - 1,), generator=g).tolist()
     _check(H, B, T, 24, lengths, 5e-3, 2e-2, coop=True)
+
+
+# MFMA recurrences (lstm_mfma.hip): H = 64 / 128 in production precision (fp16 recurrent
+# products forward, bf16 backward, fp32 accumulation / gates / cell state), lengths ending
+# inside, at and one past a 16-step staging chunk and a length-1 sequence; bounds as the
+# cooperative kernels' (measured values in DESIGN.md section 4).
+@pytest.mark.parametrize("H,B,T,lengths", [
+    (64, 5, 37, [37, 17, 16, 9, 1]),
+    (128, 5, 37, [37, 17, 16, 9, 1]),
+    (64, 19, 300, None),
+    (128, 37, 200, None),
+    (64, 30, 1024, None),
+    (128, 30, 1024, None),
+])
+def test_lstm_mfma_matches_torch(H, B, T, lengths):
+    if lengths is None:
+        g = torch.Generator().manual_seed(H + B)
+        lengths = [T] + torch.randint(1, T + 1, (B - 1,), generator=g).tolist()
+    _check(H, B, T, 24, lengths, 5e-3, 2e-2, mfma=True)

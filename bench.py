@@ -173,9 +173,11 @@ def step_census(model, opt, batch):
         t = tag[0]
         if name in ("ensvs_lstm_fwd", "ensvs_lstm_bwd"):
             t = f"H={args[7]} T={args[6]}"
-        elif name == "ensvs_ardec_fwd":  # frames T: T / 4 autoregressive steps
+        elif name in ("ensvs_lstm_mfma_fwd", "ensvs_lstm_mfma_bwd"):
+            t = f"H={args[6]} T={args[5]}"
+        elif name in ("ensvs_ardec_fwd", "ensvs_ardec_coop_fwd"):  # T / 4 autoregressive steps
             t = f"H={args[15]} T={args[14]}"
-        elif name == "ensvs_ardec_bwd":
+        elif name in ("ensvs_ardec_bwd", "ensvs_ardec_coop_bwd"):
             t = f"H={args[10]} T={args[9]}"
         rec.append((name, t, s, e))
 
@@ -224,6 +226,11 @@ def step_census(model, opt, batch):
 # MI355X per-CU VALU rate (fp32 FMA: one wave64 instruction per 4 cycles per SIMD) at the
 # sustained MFMA clock: the issue floor of a recurrence step's dot products on its CU
 CU_FMA_PER_S = 64 * 2.4e9
+# one v_mfma_f32_16x16x32 (16 cycles) per SIMD, 4 SIMDs per CU
+CU_MFMA16_PER_S = 4 * 2.4e9 / 16
+RECURRENCES = ("ensvs_lstm_fwd", "ensvs_lstm_bwd", "ensvs_lstm_mfma_fwd", "ensvs_lstm_mfma_bwd",
+               "ensvs_ardec_fwd", "ensvs_ardec_bwd", "ensvs_ardec_coop_fwd",
+               "ensvs_ardec_coop_bwd")
 
 
 def kernel_rooflines(agg, serial_ms, P, T, C=256, E=256):
@@ -273,23 +280,36 @@ def kernel_rooflines(agg, serial_ms, P, T, C=256, E=256):
                     "share_of_serial_step": ms / serial_ms})
     rec = []
     for (name, tag), (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-        if name not in ("ensvs_lstm_fwd", "ensvs_lstm_bwd", "ensvs_ardec_fwd", "ensvs_ardec_bwd"):
+        if name not in RECURRENCES or not tag:
             continue
         kv = dict(p.split("=") for p in tag.split())
         H, steps = int(kv["H"]), int(kv["T"])
-        if name.startswith("ensvs_lstm"):
-            macs = 4 * H * H  # h_{t-1} W_hh^T (fwd) / dG W_hh (bwd), one sequence-direction
+        ent = {"kernel": f"{name[6:]} H={H}", "launches_per_step": n,
+               "share_of_serial_step": ms / serial_ms}
+        if name.startswith("ensvs_lstm_mfma"):
+            # h_{t-1} W_hh^T (fwd) / dG W_hh (bwd) of one sequence-direction as 16x16x32 MFMAs
+            # (4H/16 x H/32 of them, one useful column), spread over the CU's 4 SIMDs
+            floor_ns = (4 * H // 16) * (H // 32) / CU_MFMA16_PER_S * 1e9
+            ent["floor"] = ("MFMA issue of the recurrent product on one CU (one workgroup per "
+                            "sequence-direction; 16x16x32 tiles, one useful column)")
+        elif name.startswith("ensvs_lstm"):
+            floor_ns = 4 * H * H / CU_FMA_PER_S * 1e9
+            ent["floor"] = ("VALU fp32 FMA issue of the recurrent dot products on one CU "
+                            "(latency-bound: one workgroup per sequence-direction)")
+        elif "coop" in name:
+            steps //= 4  # r = 4 frames per AR step
+            floor_ns = None
+            ent["floor"] = ("per-step cross-workgroup hand-off of h / dG (H/16 workgroups, "
+                            "coop.h); no compute floor quoted")
         else:
             # LSTMCell W_hh + the prenet column of W_ih + feat_out per AR step (r = 4 frames)
             steps //= 4
-            macs = 4 * H * H + 4 * H + 4 * (H + 130)
-        floor_ns = macs / CU_FMA_PER_S * 1e9
+            floor_ns = (4 * H * H + 4 * H + 4 * (H + 130)) / CU_FMA_PER_S * 1e9
+            ent["floor"] = "VALU fp32 FMA issue of one AR step on one CU"
         ns = ms / n * 1e6 / steps
-        rec.append({"kernel": f"{name[6:]} H={H}", "launches_per_step": n, "ns_per_step": ns,
-                    "floor_ns_per_step": floor_ns, "floor": "VALU fp32 FMA issue of the "
-                    "recurrent dot products on one CU (latency-bound: one workgroup per "
-                    "sequence-direction)", "frac": floor_ns / ns,
-                    "share_of_serial_step": ms / serial_ms})
+        ent.update(ns_per_step=ns, floor_ns_per_step=floor_ns,
+                   frac=floor_ns / ns if floor_ns else None)
+        rec.append(ent)
     return out, rec
 
 

@@ -11,7 +11,6 @@ Same constructor arguments, forward/inference signatures, prediction types
 and state_dict keys as the reference; ``_target_`` strings are the only change
 a recipe needs (configs.py).
 """
-import os
 
 import torch
 from torch import nn
@@ -26,23 +25,16 @@ from .model import init_weights
 
 
 
-# Backward schedule option: the V/UV branch's backward starts after the mgc DiffNet
-# backward (ENSVS_VUV_AFTER_MGC=1).  Off: measured 24.9 vs 22.2 ms/step (graph replay,
-# 30 x 1024) -- the V/UV recurrences then lengthen the tail instead of filling it.
-_VUV_AFTER_MGC = {"on": os.environ.get("ENSVS_VUV_AFTER_MGC", "0") == "1"}
-
-
 # Step schedule of the fused branches (0 lf0, 1 mgc, 2 bap, 3 vuv; profiles/r2_schedule_ab.txt).
 # BRANCH_AFTER {branch: branch whose forward must finish first}: the bap branch starts when
 # the mgc forward ends, so mgc -- the critical branch (13.9 ms alone) -- runs its forward
-# beside the latency-bound lf0 / vuv chains only (ENSVS_BRANCH_AFTER, "" = all at once:
-# 20.9 vs 21.2 ms/step).  EXCL_BRANCHES: branches whose recurrence workgroups reserve their
-# CU's LDS (the lf0 and mgc chains; bap / vuv LSTM workgroups share CUs with GEMMs:
-# 20.8 vs 21.0 ms/step; ENSVS_EXCL_BRANCHES).
-BRANCH_AFTER = {int(b): int(a) for b, a in (kv.split(":") for kv in
-                os.environ.get("ENSVS_BRANCH_AFTER", "2:1").split(",") if kv)}
-EXCL_BRANCHES = {int(v) for v in os.environ.get("ENSVS_EXCL_BRANCHES", "0,1").split(",")
-                 if v}
+# beside the latency-bound lf0 / vuv chains only (all at once: 20.9 vs 21.2 ms/step).
+# EXCL_BRANCHES: branches whose recurrence workgroups reserve their CU's LDS (the lf0 and mgc
+# chains; bap / vuv LSTM workgroups share CUs with GEMMs: 20.8 vs 21.0 ms/step).  Not kept:
+# the V/UV backward after the mgc DiffNet backward (24.9 vs 22.2 ms/step: the V/UV
+# recurrences then lengthen the tail instead of filling it).
+BRANCH_AFTER = {2: 1}
+EXCL_BRANCHES = {0, 1}
 
 
 def _ar_work(H, device):
@@ -703,10 +695,6 @@ class _MultistreamHybrid(BaseModel):
                                                            g.get("lf0_residual_sub"))
         elif i == 1:
             hooks = []
-            if _VUV_AFTER_MGC["on"] and torch.cuda.is_available() and g["mgc_recon"].is_cuda:
-                ev = torch.cuda.Event()
-                dsp["_mgc_denoiser_done"] = ev
-                hooks.append(lambda: ev.record(torch.cuda.current_stream()))
             if dsp.get("_reduce") is not None:
                 red = dsp["_reduce"]
                 hooks.append(lambda: red("mgc_denoiser"))
@@ -716,12 +704,6 @@ class _MultistreamHybrid(BaseModel):
         elif i == 2:
             dsp["bap"] = self.bap_model._bwd(st["bap"], g["bap_recon"], want_spk=spk)
         else:
-            ev = dsp.get("_mgc_denoiser_done")
-            if ev is not None:
-                # the V/UV backward (LSTM recurrences on 2B workgroups) waits for the mgc
-                # DiffNet backward so that it overlaps the mgc encoder's recurrences at the
-                # tail of the step instead of contending with the DiffNet GEMMs
-                torch.cuda.current_stream().wait_event(ev)
             _, dsp["vuv"] = self.vuv_model._bwd(st["vuv"], g["vuv"], want_spk=spk)
 
     def _l1_terms(self, outs, y_main):

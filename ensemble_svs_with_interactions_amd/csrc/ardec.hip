@@ -314,7 +314,7 @@ __global__ void downsample_wgrad_kernel(DsArgs a, const float* __restrict__ de, 
   if (threadIdx.x == 4) db[c] += red[4][0];
 }
 
-// The decoder workgroup reserves its CU's LDS (lstm.hip ensvs_rec_exclusive: ENSVS_LSTM_EXCLUSIVE,
+// The decoder workgroup reserves its CU's LDS (lstm.hip ensvs_rec_exclusive,
 // ensvs_set_recurrence_exclusive)
 static size_t ar_excl_lds() {
   return ensvs_rec_exclusive() ? 96 * 1024 : 0;  // + the static LDS: no 64 KB GEMM workgroup fits beside it

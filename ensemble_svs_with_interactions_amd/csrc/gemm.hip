@@ -958,12 +958,9 @@ __device__ __forceinline__ void usf_block_tail(const GemmArgs& a, const GemmArgs
                                                f32x4 (&acc)[4][4], char* smem, int tid, int lane,
                                                int wr, int wc, int m0);
 
-#ifndef ENSVS_GBW_EB
-#define ENSVS_GBW_EB 2
-#endif
 // GATE_BWD epilogue rows per operand batch in the 128 x 128 kernel: 2 builds without scratch
 // (162 VGPRs; 4 spills 124 B) and takes the C = 256 gate-backward dgrad from 51.4 to 47.5 us
-constexpr int GBW_EB = ENSVS_GBW_EB;
+constexpr int GBW_EB = 2;
 
 template <int STAGES, bool FUSE>
 
@@ -2918,11 +2915,7 @@ static int fill_gemm_args(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int
   auto al8 = [](const void* p, int ld) { return !p || ((((uintptr_t)p) & 7) == 0 && ld % 4 == 0); };
   a.vec_out = al(Y, ldy) && (a.aux0_bf ? al8(aux0, ld0) : al(aux0, ld0)) &&
               (a.aux1_bf ? al8(aux1, ld1) : al(aux1, ld1)) && (C % 4 == 0);
-  static const int gate8_on = [] {
-    const char* e = getenv("ENSVS_GATE8");  // A/B switch for the 8-channel gate epilogue
-    return e ? atoi(e) : 1;
-  }();
-  a.gate8 = gate8_on && a.vec_out && C % 8 == 0 &&
+  a.gate8 = a.vec_out && C % 8 == 0 &&
             (!a.aux0_bf || (((uintptr_t)aux0 & 15) == 0 && ld0 % 8 == 0));
   return ENSVS_OK;
 }
@@ -2965,54 +2958,35 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
 
 // The 256 x 256 kernel takes a bf16-operand launch when it fills the chip with whole
 // tiles (>= 192 workgroups of 256 x 256), its LDS epilogue applies (16-B rows, no column
-// sums) and the padded N is a multiple of 256; ENSVS_BIG_TILE=0 disables it.
-// -1: not read yet (ENSVS_BIG_TILE, default 2): 0 off, 1 the 32-deep ring kernel with
-// g_big_stages stages (ENSVS_BIG_STAGES, default 5), 2 the 64-deep two-stage kernel.
-// Gate GEMM (tools/gate_probe.py): 2 -> 44.8 us, 1 (5 / 4 / 3 stages) -> 53.3 / 53.0 /
-// 50.2 us, 0 (128 x 128) -> 51.0 us: more LDS stages in flight did not pay.
-static int g_big_tile = -1, g_big_stages = 5, g_big_all = 0;
-// split-K fills about this many workgroups (ENSVS_SPLITK=0 turns it off)
+// sums) and the padded N is a multiple of 256.  Mode (ensvs_set_big_tile): 0 off, 1 the
+// 32-deep ring kernel with g_big_stages stages, 2 (default) the 64-deep two-stage kernel,
+// 3 as 2 for every eligible epilogue (the bitwise tests).  Gate GEMM (tools/gate_probe.py):
+// 2 -> 44.8 us, 1 (5 / 4 / 3 stages) -> 53.3 / 53.0 / 50.2 us, 0 (128 x 128) -> 51.0 us:
+// more LDS stages in flight did not pay.
+static int g_big_tile = 2, g_big_stages = 5, g_big_all = 0;
+// split-K fills about this many workgroups (only when the caller passes a workspace)
 static const int SPLITK_TARGET = 256;
 // launches of fewer than 128 tiles of 128 x 128 that the 64 x 64 kernel does not take (no
-// 16-B epilogue rows) run the two-K-group kernel when on (-1: not read yet; ENSVS_DUAL_SMALL,
-// default 0 since the 64 x 64 kernel: the one-group kernel keeps the register-staged bits,
-// e.g. the DiffNet output projection's 5-column rows; ensvs_set_dual_small)
-static int g_dual_small = -1;
-// launches of fewer than 128 tiles of 128 x 128 run the 64 x 64-tile kernel (-1: not read yet;
-// ENSVS_SMALL, default 1; ensvs_set_small); it takes precedence over split-K and dual
-static int g_small = -1;
+// 16-B epilogue rows) run the two-K-group kernel when on (ensvs_set_dual_small; off: the
+// one-group kernel keeps the register-staged bits, e.g. the DiffNet output projection's
+// 5-column rows)
+static int g_dual_small = 0;
+// launches of fewer than 128 tiles of 128 x 128 run the 64 x 64-tile kernel (ensvs_set_small,
+// default on); it takes precedence over split-K and dual
+static int g_small = 1;
+// the 64 x 64 kernel's LDS-DMA ring depth (3..5 measured on the 2 000-frame reverse process)
+static const int SMALL_STAGES = 5;
+// at least this many 256 x 256 tiles (the chip's 256 CUs less a margin) for the big kernel
+static const int BIG_MIN_TILES = 192;
 
 static bool use_big_tile(const GemmArgs& a) {
-  if (g_big_tile < 0) {
-    const char* e = getenv("ENSVS_BIG_TILE");
-    g_big_tile = e ? atoi(e) : 2;
-    const char* s = getenv("ENSVS_BIG_STAGES");
-    if (s) g_big_stages = atoi(s);
-  }
   if (!g_big_tile || a.csum || !a.vec_out || a.Npad % BNB) return false;
-  static const int min_tiles = [] {  // ENSVS_BIG_MIN_TILES: A/B knob of the row threshold
-    const char* e = getenv("ENSVS_BIG_MIN_TILES");
-    return e ? atoi(e) : 192;
-  }();
   // Only the gate GEMMs (K = 1 024) take the 256 x 256 kernel: the DiffNet res/skip GEMM
   // (K = 256, an epilogue reading the residual and skip rows) runs 47 vs 55 us per launch on
   // 128 x 128 tiles, the other wide launches (N = 512 plain / ReLU-mask, K = 256-512) 39 vs
   // 46 and 62 vs 71 us; step 20.1 vs 20.75 ms (profiles/r2_schedule_ab.txt).
-  // ENSVS_BIG_RESSKIP=1 / ENSVS_BIG_OTHER=1 route them back (A/B knobs).
-  // (ensvs_set_big_tile mode 3: every eligible launch, as before -- the bitwise tests)
-  static const int big_resskip = [] {
-    const char* e = getenv("ENSVS_BIG_RESSKIP");
-    return e ? atoi(e) : 0;
-  }();
-  static const int big_other = [] {
-    const char* e = getenv("ENSVS_BIG_OTHER");
-    return e ? atoi(e) : 0;
-  }();
-  if (!g_big_all) {
-    if (a.epi == EPI_RESSKIP && !big_resskip) return false;
-    if (!big_other && a.epi != EPI_GATE && a.epi != EPI_RESSKIP) return false;
-  }
-  return (long long)cdiv(a.M, BMB) * (a.Npad / BNB) >= min_tiles;
+  if (!g_big_all && a.epi != EPI_GATE) return false;
+  return (long long)cdiv(a.M, BMB) * (a.Npad / BNB) >= BIG_MIN_TILES;
 }
 
 static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, int Npad,
@@ -3072,17 +3046,9 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
   // small M (fewer than 128 tiles of 128 x 128): the 64 x 64-tile kernel fills the chip; it
   // also takes N <= 64 at any M (a 128-wide tile would leave half its columns and half the
   // epilogue threads idle: the uSFGAN block output GEMMs, 480 000 x 64)
-  if (g_small < 0) {
-    const char* e = getenv("ENSVS_SMALL");
-    g_small = e ? atoi(e) : 1;
-  }
   if (g_small && !has_pd && !a.csum && a.vec_out && Npad % BNS == 0 &&
       ((long long)grid.x * grid.y < 128 || a.N <= BNS)) {
-    static const int sms = [] {
-      const char* e = getenv("ENSVS_SMALL_STAGES");
-      const int v = e ? atoi(e) : 5;
-      return v < 3 ? 3 : (v > 5 ? 5 : v);
-    }();
+    constexpr int sms = SMALL_STAGES;
     const dim3 gs(cdiv(a.M, BMS), a.N <= BNS ? 1 : Npad / BNS);
 #define SMALL(S)                                                                          \
   do {                                                                                    \
@@ -3103,11 +3069,7 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
   // small M: split K over up to 8 workgroups per output tile so the launch fills the chip
   // (a 2 000-frame DiffNet GEMM is 64 tiles of 128 x 128; each tile's 16 K-steps would run
   // serially on one CU).  Needs a caller workspace for ksplit x M x Npad fp32 partials.
-  static const bool splitk_on = [] {
-    const char* e = getenv("ENSVS_SPLITK");
-    return !(e && e[0] == '0');
-  }();
-  if (splitk_on && !has_pd && a.part && !a.csum && a.vec_out && a.epi != EPI_NONE) {
+  if (!has_pd && a.part && !a.csum && a.vec_out && a.epi != EPI_NONE) {
     const long long tiles = (long long)grid.x * grid.y;
     int nit = 0;
     for (int s = 0; s < nseg; ++s) nit += cdiv(segs[s].K, BK2) * segs[s].taps;
@@ -3120,10 +3082,6 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
   // the LDS-staged epilogue reuses the stage buffers for the fp32 output tile
   const size_t l2 = std::max<size_t>(2 * lds, EPI_LDS), l3 = std::max<size_t>(3 * lds, EPI_LDS);
   if (a.ksplit > 1) grid.z = a.ksplit;
-  if (g_dual_small < 0) {
-    const char* e = getenv("ENSVS_DUAL_SMALL");
-    g_dual_small = e ? atoi(e) : 0;
-  }
   if (g_dual_small && !has_pd && a.ksplit <= 1 && !a.csum &&
       (long long)grid.x * grid.y < 128) {
     const size_t ld2 = std::max<size_t>(4 * lds, EPI_LDS);  // 2 stages x 2 K-groups
@@ -3382,9 +3340,8 @@ ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DT_BF16) {
     size_t lds = 2 * 2 * BK * 256;
-    static const int ring = getenv("ENSVS_WGRAD_RING") ? atoi(getenv("ENSVS_WGRAD_RING")) : 1;
     // (with radd the ring's extra registers spill: that rare case keeps one chunk in flight)
-    if (vec && ring && !radd)
+    if (vec && !radd)
       hipLaunchKernelGGL((wgrad_f32r_kernel<false>), grid, dim3(NTHR), lds, st, a);
     else if (vec)
       hipLaunchKernelGGL((wgrad_kernel<__bf16, true>), grid, dim3(NTHR), lds, st, a);

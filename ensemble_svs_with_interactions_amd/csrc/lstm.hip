@@ -28,14 +28,8 @@
 #include "common.h"
 #include "ensvs.h"
 
-static int g_rec_excl = -1;
-int ensvs_rec_exclusive() {  // (common.h)
-  if (g_rec_excl < 0) {
-    const char* e = getenv("ENSVS_LSTM_EXCLUSIVE");
-    g_rec_excl = e ? atoi(e) : 1;
-  }
-  return g_rec_excl;
-}
+static int g_rec_excl = 1;
+int ensvs_rec_exclusive() { return g_rec_excl; }  // (common.h)
 
 namespace {
 
@@ -378,8 +372,8 @@ __global__ __launch_bounds__(Geo<H>::TB) void lstm_bwd_kernel(
 // Each persistent recurrence workgroup reserves its CU's whole LDS, so no GEMM workgroup
 // of a concurrent branch stream lands beside it (a co-resident GEMM stretches the
 // latency-bound step): 20.8 vs 21.3 ms per training step (profiles/r2_schedule_ab.txt).
-// ENSVS_LSTM_EXCLUSIVE=0 turns it off; ensvs_set_recurrence_exclusive switches it per
-// launch (the caller's branch schedule; read at launch, so a captured graph keeps it).
+// ensvs_set_recurrence_exclusive switches it per launch (the caller's branch schedule; read
+// at launch, so a captured graph keeps it).
 static size_t excl_lds(size_t need) {
   return ensvs_rec_exclusive() ? std::max<size_t>(need, 160 * 1024) : need;
 }
@@ -678,12 +672,8 @@ int launch_step_bwd(const float* dy, int lddy, const float* w0, const float* w1,
   return ENSVS_OK;
 }
 
-int g_force_step = -1;  // ENSVS_LSTM_STEP=1: the per-step kernels at every H (tests)
+int g_force_step = 0;  // ensvs_lstm_set_step(1): the per-step kernels at every H (tests)
 bool use_step(int H) {
-  if (g_force_step < 0) {
-    const char* e = getenv("ENSVS_LSTM_STEP");
-    g_force_step = e ? atoi(e) : 0;
-  }
   return g_force_step || !(H == 8 || H == 16 || H == 32 || H == 64 || H == 128);
 }
 

@@ -4,7 +4,6 @@ Everything here only moves pointers and sizes; all arithmetic happens in the
 HIP kernels of ``csrc/``.  Tensors are fp32, channels-last frame rows.
 """
 import ctypes
-import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -144,19 +143,18 @@ class Seg:
 # register-staged kernel; pays where the A tile is re-read (several N tiles or taps) --
 # at every row count: at M = 2 000 (one pair of 10 s in the reverse diffusion) a
 # register-staged DiffNet GEMM launch averaged 33 us against ~10 us here (pair inference
-# 185 -> 102 ms), so there is no row threshold by default (ENSVS_BF16_MIN_ROWS sets one).
-# Single-reuse GEMMs (one tap, one N tile) stay register-staged: ENSVS_BF16_MIN_REUSE=1
-# measured 22.0 vs 21.9 ms/step and ensemble RTF 0.0305 vs 0.0294.
-BF16_ACT = {"on": True, "stages": int(os.environ.get("ENSVS_STAGES", "2")),
-            "stages_small": int(os.environ.get("ENSVS_STAGES_SMALL", "2")),
-            "min_reuse": int(os.environ.get("ENSVS_BF16_MIN_REUSE", "2")),
-            "min_rows": int(os.environ.get("ENSVS_BF16_MIN_ROWS", "0"))}
+# 185 -> 102 ms), so there is no row threshold (min_rows 0).  Single-reuse GEMMs (one tap,
+# one N tile) stay register-staged: min_reuse 1 measured 22.0 vs 21.9 ms/step and ensemble
+# RTF 0.0305 vs 0.0294.  Two LDS stages (three: 22.3 vs 20.1 ms/step).  Tests switch the
+# entries to compare the paths bitwise.
+BF16_ACT = {"on": True, "stages": 2, "stages_small": 2, "min_reuse": 2, "min_rows": 0}
 
 
 # Small-M bf16-operand GEMMs split their K-steps over up to max_split workgroups per output
 # tile (ensvs_conv_gemm_bf16a: part / part_floats) when the launch has fewer than max_tiles
-# tiles; ENSVS_SPLITK=0 turns it off.
-SPLITK = {"on": os.environ.get("ENSVS_SPLITK", "0") != "0", "max_split": 8, "max_tiles": 128}
+# tiles.  Off: the 64 x 64-tile kernel fills the chip at small M instead (its accumulation
+# order is the register-staged kernel's); the sum-order tests switch it on.
+SPLITK = {"on": False, "max_split": 8, "max_tiles": 128}
 
 
 def _castable(s):
@@ -393,7 +391,7 @@ def scratch(nfloats, device, key="part"):
 
 
 # weight gradients split the frame reduction until about this many workgroups (tile x split)
-WGRAD_TARGET = int(os.environ.get("ENSVS_WGRAD_TARGET", "512"))
+WGRAD_TARGET = 512  # workgroups a weight gradient aims for (256: 20.7, 1024: 20.5 vs 20.1 ms/step)
 
 
 def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, sk, sj,

@@ -10,7 +10,6 @@ non-finite skip and Adam — every arithmetic op in libensvs.so, no host sync.
 """
 import ctypes
 import math
-from os import environ as _os_env
 
 import torch
 
@@ -317,9 +316,9 @@ class BucketedAllReduce:
         self.works = []
 
 
-# overlapped bucketed all-reduce in the eager fused step (W > 1); ENSVS_OVERLAP_ALLREDUCE=0:
+# overlapped bucketed all-reduce in the eager fused step (W > 1); set_overlap_allreduce(False):
 # one all-reduce of the whole buffer after the backward
-_STATE_OVERLAP = {"on": _os_env.get("ENSVS_OVERLAP_ALLREDUCE", "1") == "1"}
+_STATE_OVERLAP = {"on": True}
 
 
 def set_overlap_allreduce(on: bool):
@@ -444,9 +443,8 @@ def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, 
 # stream, acoustic_models._train_fused), the default: with 8 hardware queues it measured
 # 20.4 vs 20.6 ms/step for the forward-all / loss / backward-all schedule (graph replay,
 # 30 x 1024; with 4 queues it was 22.3 vs 22.0).  Same gradients bitwise; the loss is the
-# sum of the branches' partial losses.  ENSVS_FUSED_BRANCHES=0 turns it off.
-import os as _os  # noqa: E402
-_STATE_FUSED = {"on": _os.environ.get("ENSVS_FUSED_BRANCHES", "1") == "1"}
+# sum of the branches' partial losses.  set_fused_branches(False) turns it off.
+_STATE_FUSED = {"on": True}
 
 
 def set_fused_branches(on: bool):

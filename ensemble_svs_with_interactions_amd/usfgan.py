@@ -20,7 +20,6 @@ parameter version.  The nn.Conv modules are parameter containers; their forward 
 called.
 """
 import math
-import os
 
 import numpy as np
 import torch
@@ -326,8 +325,8 @@ class _Prepared:
 
 # ------------------------------------------------------------------ generator
 
-# inference blocks as one launch each (ensvs_usf_block; ENSVS_USF_FUSED=0: two GEMMs)
-FUSED_BLOCK = {"on": os.environ.get("ENSVS_USF_FUSED", "1") != "0"}
+# inference blocks as one launch each (ensvs_usf_block; off: two GEMMs, the bitwise tests)
+FUSED_BLOCK = {"on": True}
 
 
 class ParallelHnUSFGANGenerator(nn.Module):

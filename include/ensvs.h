@@ -70,21 +70,21 @@ int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N
  * sums) run a 256 x 256-tile kernel with the same accumulation order (bitwise equal).
  * mode 0: keep the 128 x 128 kernel; 1: 32-deep K steps on a `stages`-deep LDS ring
  * (3..5; 0 keeps the current count); 2: 64-deep two-stage kernel for the gate GEMMs (the
- * other epilogues run faster on 128 x 128 tiles); 3: as 2 for every eligible launch.  Defaults: ENSVS_BIG_TILE
- * (2), ENSVS_BIG_STAGES (5). */
+ * other epilogues run faster on 128 x 128 tiles); 3: as 2 for every eligible launch.
+ * Defaults: mode 2, 5 stages. */
 int ensvs_set_big_tile(int mode, int stages);
 /* Launches of fewer than 128 output tiles (small M) that the 64 x 64 kernel does not take
  * can run a 128 x 128 kernel with two K-groups of 4 waves (each group half of the K-steps,
- * tiles added through LDS; ENSVS_DUAL_SMALL, default off: the one-group kernel, the same
- * bits as the register-staged kernel). */
+ * tiles added through LDS; default off: the one-group kernel, the same bits as the
+ * register-staged kernel; kept for the sum-order tests). */
 int ensvs_set_dual_small(int on);
 /* Launches of fewer than 128 output tiles of 128 x 128 (small M: the 2 000-frame reverse-
- * diffusion GEMMs) run a 64 x 64-tile kernel that fills the chip (default on, ENSVS_SMALL; it
- * takes precedence over the two-K-group kernel and split-K); same accumulation order as the
+ * diffusion GEMMs) run a 64 x 64-tile kernel that fills the chip (default on; it takes
+ * precedence over the two-K-group kernel and split-K); same accumulation order as the
  * one-group kernel, so the same bits.  0 turns it off. */
 int ensvs_set_small(int on);
 /* Persistent recurrence workgroups (LSTM, AR decoder) reserve their CU's LDS so no GEMM
- * workgroup of a concurrent stream lands beside them (default on, ENSVS_LSTM_EXCLUSIVE);
+ * workgroup of a concurrent stream lands beside them (default on);
  * read at each launch, so a caller can choose per branch. */
 int ensvs_set_recurrence_exclusive(int on);
 /* One uSFGAN residual block in one launch (usfgan/layers/residual_block.py): the gate GEMM
@@ -100,7 +100,7 @@ int ensvs_usf_block(const ensvs_conv_seg* segs, int nseg, int B, int Tout, const
  * fewer than 128 output tiles (small M: the 2 000-frame reverse-diffusion GEMMs) split their
  * K-steps over up to 8 workgroups per tile when part holds ksplit x M x Npad floats; the
  * slices are summed in a fixed order by a second kernel that runs the epilogue
- * (deterministic; ENSVS_SPLITK=0 disables).  Operand rows: bf16, ld % 8 == 0, 16-B aligned;
+ * (deterministic; the Python wrapper passes no workspace by default).  Operand rows: bf16, ld % 8 == 0, 16-B aligned;
  * a segment with K % 8 != 0 has its rows zero-padded to a multiple of 8 within ld. */
 int ensvs_conv_gemm_bf16a(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N, int Npad,
                           const void* W, const float* bias, float* Y, int ldy, int epi, int relu,
@@ -167,7 +167,7 @@ int ensvs_lstm_fwd(const float* gx, int ldg, const float* whh_f, const float* wh
 /* Workspace floats ensvs_lstm_bwd needs for (B, H): 2*B*H (cell-gradient carry) for the
  * per-step kernels, 0 for the persistent ones. */
 long long ensvs_lstm_bwd_work_floats(int B, int H);
-/* Test knob: force != 0 runs the per-step kernels at every H (default: ENSVS_LSTM_STEP). */
+/* Test knob: force != 0 runs the per-step kernels at every H (default 0). */
 int ensvs_lstm_set_step(int force);
 /* Backward through time: pre-activation gate gradients dg [B*T][lddg] (zero past L_b). */
 int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* whh_r,

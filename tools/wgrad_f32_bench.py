@@ -1,6 +1,6 @@
 """fp32-operand weight gradients of the training step (production bf16 staging) timed with
 HIP events: the census's 'wgrad ... f' shapes at M = 30 x 1024 frames (dev tool).
-    ENSVS_WGRAD_RING=0|1 python tools/wgrad_f32_bench.py"""
+    python tools/wgrad_f32_bench.py"""
 import os
 import sys
 

@@ -245,12 +245,14 @@ class ModulePacks:
         return self
 
     # ---- registration helpers ------------------------------------------------
-    def linear(self, name, w, cols=None, bwd=True, scale=1.0, perm_c=0):
-        """Linear weight (N, K) or a column range of it."""
+    def linear(self, name, w, cols=None, bwd=True, scale=1.0, perm_c=0, fwd=True):
+        """Linear weight (N, K) or a column range of it (fwd=False: only its transpose)."""
         N, K = w.shape
         c0, c1 = (0, K) if cols is None else cols
         src = w[:, c0:c1]
-        self.refs[name] = self.fwd.add(src, N, c1 - c0, 1, K, 1, 1, perm_c=perm_c, scale=scale)
+        if fwd:
+            self.refs[name] = self.fwd.add(src, N, c1 - c0, 1, K, 1, 1, perm_c=perm_c,
+                                           scale=scale)
         if bwd:
             self.refs[name + "^T"] = self.bwd.add(src, N, c1 - c0, 1, K, 1, 1, transpose=True,
                                                    scale=scale)

@@ -358,11 +358,24 @@ def conv_bwd(pk, conv, sv, dout, B, T, device, groups=1, first_dx=None):
 # ----------------------------------------------------------------- bi-LSTM
 
 def lstm_register(pk, lstm):
+    """Per layer: both directions' W_ih stacked as one forward operand "ih{l}" (one input-
+    projection GEMM of N = 8H reads the layer input once) when 4H is a multiple of the
+    128-row packing (the summed bias pairs b_ih + b_hh are then consecutive, so "b{l}"
+    addresses all 8H); otherwise one operand per direction.  Their transposes for the
+    input-gradient GEMM."""
+    H = lstm.hidden_size
     for l in range(lstm.num_layers):
-        for sfx in ("", "_reverse"):
-            pk.linear(f"ih{l}{sfx}", getattr(lstm, f"weight_ih_l{l}{sfx}"))
+        ws = [getattr(lstm, f"weight_ih_l{l}{sfx}") for sfx in ("", "_reverse")]
+        if lstm_fused_proj(H):
+            pk.refs[f"ih{l}"] = pk.fwd.add_rowcat(ws, 4 * H, ws[0].shape[1])
+        for sfx, w in zip(("", "_reverse"), ws):
+            pk.linear(f"ih{l}{sfx}", w, fwd=not lstm_fused_proj(H))
             pk.bias_vec(f"b{l}{sfx}", getattr(lstm, f"bias_ih_l{l}{sfx}"),
                         b2=getattr(lstm, f"bias_hh_l{l}{sfx}"))
+
+
+def lstm_fused_proj(H):
+    return (4 * H) % K.BM == 0
 
 
 def lstm_coop(B, H):
@@ -468,9 +481,14 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
     for l in range(lstm.num_layers):
         Kc = getattr(lstm, f"weight_ih_l{l}").shape[1]
         gx = empty(M, 8 * H, device=device)
-        for d, sfx in enumerate(("", "_reverse")):
-            K.gemm([K.Seg(h, ldh, Kc, pk[f"ih{l}{sfx}"], T)], B, T, 4 * H, pk.fwd, gx, 8 * H,
-                   yoff=d * 4 * H, **pk.bias_ptr_args(f"b{l}{sfx}"))
+        if lstm_fused_proj(H):
+            assert pk[f"b{l}_reverse"].offset == pk[f"b{l}"].offset + 4 * H
+            K.gemm([K.Seg(h, ldh, Kc, pk[f"ih{l}"], T)], B, T, 8 * H, pk.fwd, gx, 8 * H,
+                   **pk.bias_ptr_args(f"b{l}"))
+        else:
+            for d, sfx in enumerate(("", "_reverse")):
+                K.gemm([K.Seg(h, ldh, Kc, pk[f"ih{l}{sfx}"], T)], B, T, 4 * H, pk.fwd, gx,
+                       8 * H, yoff=d * 4 * H, **pk.bias_ptr_args(f"b{l}{sfx}"))
         y = empty(M, 2 * H, device=device)
         HP = lstm_pad(H)
         saved = empty(M * 2 * 5 * (HP or H), device=device)

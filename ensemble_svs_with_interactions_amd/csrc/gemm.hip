@@ -2201,14 +2201,41 @@ __device__ __forceinline__ bf16x8 wg_frag(const char* img, int c0, int lane) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// XCD-aware workgroup -> (tile, tap, row split) map of the weight-gradient kernels.  Every
+// (N tile, K tile, tap) workgroup of one row split reads that split's dy and x rows; the
+// dispatcher deals consecutive workgroups round-robin over the 8 XCDs (8 L2s), so the raw
+// blockIdx order sent each split's workgroups to different XCDs and every one of them fetched
+// the shared rows through the fabric (rocprofv3 FETCH_SIZE: 15 GB per training step across
+// the wgrad kernels, profiles/r3_step_pmc.json).  When the split count is a multiple of 8,
+// split s runs all its workgroups on XCD s % 8: hardware id b -> xcd = b % 8, then the
+// workgroup index w inside the split and s = 8 (b / 8 / W) + xcd.  Bijective; the partial of
+// split s covers the same rows as before, so the results are bitwise unchanged.
+__device__ __forceinline__ void wgrad_tile(const WgradArgs& a, int& n0, int& k0, int& j, int& s) {
+  const int gx = gridDim.x, gy = gridDim.y;
+  if (a.splits % 8 == 0) {
+    const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int W = gx * gy * a.taps;  // workgroups per split
+    const int k = b >> 3, w = k % W;
+    s = (k / W) * 8 + (b & 7);
+    n0 = (w % gx) * BM;
+    k0 = ((w / gx) % gy) * BN;
+    j = w / (gx * gy);
+  } else {
+    n0 = blockIdx.x * BM;
+    k0 = blockIdx.y * BN;
+    j = blockIdx.z % a.taps;
+    s = blockIdx.z / a.taps;
+  }
+}
+
 template <typename T, bool VEC>
 __global__ __launch_bounds__(NTHR) void wgrad_kernel(const WgradArgs a) {
   constexpr int LK = Lds<T>::K;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int n0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
-  const int j = blockIdx.z % a.taps, s = blockIdx.z / a.taps;
+  int n0, k0, j, s;
+  wgrad_tile(a, n0, k0, j, s);
   const int mbeg = s * a.rows_per_split;
   const int mend = min(a.M, mbeg + a.rows_per_split);
   const int nch = mbeg < mend ? (mend - mbeg + BK - 1) / BK : 0;
@@ -2378,8 +2405,8 @@ __global__ __launch_bounds__(NTHR, 2) void wgrad_f32r_kernel(const WgradArgs a) 
   constexpr int IMG = BK * 256;  // bytes per bf16 operand image (32 frames x 128 channels)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int n0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
-  const int j = blockIdx.z % a.taps, s = blockIdx.z / a.taps;
+  int n0, k0, j, s;
+  wgrad_tile(a, n0, k0, j, s);
   const int mbeg = s * a.rows_per_split;
   const int mend = min(a.M, mbeg + a.rows_per_split);
   const int nch = mbeg < mend ? (mend - mbeg + BK - 1) / BK : 0;
@@ -2540,8 +2567,8 @@ __global__ __launch_bounds__(NTHR) void wgrad_b16_kernel(const WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 1, wc = wid & 1;
-  const int n0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
-  const int j = blockIdx.z % a.taps, s = blockIdx.z / a.taps;
+  int n0, k0, j, s;
+  wgrad_tile(a, n0, k0, j, s);
   const int mbeg = s * a.rows_per_split;
   const int mend = min(a.M, mbeg + a.rows_per_split);
   const int nch = mbeg < mend ? (mend - mbeg + BK - 1) / BK : 0;

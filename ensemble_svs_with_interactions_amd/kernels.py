@@ -403,6 +403,8 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
     if splits is None:
         tiles = -(-N // 128) * -(-K // 128) * taps
         splits = max(1, min(64, WGRAD_TARGET // max(tiles, 1), -(-M // 256)))
+        if splits >= 8:  # a multiple of 8: each split's workgroups share one XCD's L2
+            splits = max(8, (splits + 4) // 8 * 8)
     part = scratch(splits * taps * N * K, dy.device)
     if dy.dtype == torch.bfloat16 or x.dtype == torch.bfloat16:
         assert dy.dtype == x.dtype == torch.bfloat16 and radd is None and dtype == _lib.DT_BF16

@@ -6,6 +6,7 @@ uncalibrated, so the figure is an estimate for the few kernels that issue them).
 usage: python tools/step_pmc_sum.py FETCH_CSV WRITE_CSV OUT_JSON [STEPS]"""
 import csv
 import json
+import re
 import sys
 
 STEPS = int(sys.argv[4]) if len(sys.argv) > 4 else 4
@@ -27,7 +28,8 @@ def between_markers(path, counter):
     inside = [rows[d] for d in ids if a < d < b]
     per_kernel = {}
     for name, v in inside:
-        k = name.split("(")[0][:90]
+        m = re.search(r"(\w+_kernel\w*|ensvs_\w+|\w+Kernel\w*)", name)
+        k = m.group(1) if m else name[:60]
         per_kernel[k] = per_kernel.get(k, 0.0) + v
     return sum(v for _, v in inside), len(inside), per_kernel
 

@@ -257,8 +257,9 @@ class DiffNet(nn.Module):
         K.gemm(segs, B, T, 2 * C, pk.fwd, z, ldz, epi=_lib.EPI_GATE, aux0=gf, ld0=2 * C, C=C,
                ybf=zb, ybf_ld=ldz, keep_y=zb is None, **pk.bias_ptr_args(f"g{l}.b"))
 
-    def _bwd(self, st, dout):
-        """dout (B*T, in_dim) -> dcond (B*T, E); parameter grads accumulated."""
+    def _bwd(self, st, dout, after_params=None):
+        """dout (B*T, in_dim) -> dcond (B*T, E); parameter grads accumulated.  after_params:
+        called once every parameter gradient of the DiffNet is issued (on their stream)."""
         pk = self._packs
         dev = dout.device
         C, L, E, Mc = self.C, len(self.residual_layers), self.E, self.in_dim
@@ -365,13 +366,15 @@ class DiffNet(nn.Module):
         dcond = empty(M, E, device=dev)
         K.gemm([K.Seg(dpre_b if b16 else dpre_all, L * 2 * C, L * 2 * C, pk["condT"], T)],
                B, T, E, pk.bwd, dcond, E)
-        # everything below produces parameter gradients only (an auxiliary stream beside the
-        # encoder's backward measured slower: 24.8 vs 21.4 ms/step, the recurrences slow
-        # down under the extra GEMM traffic; so it stays on the branch's stream)
+        # everything below produces parameter gradients only.  It stays on the branch's
+        # stream: on an auxiliary stream beside the encoder's backward the step measured
+        # 22.9 vs 17.5 ms (round 3, tools/step_ab.py; round 2: 24.8 vs 21.4)
         for f in later:
             f()
         self._bwd_param_tail(st, dout, dx, dss, dssb, tmp_dss, dpre_all, dpre_b, dd_all,
                              dd_tiles, pre_tiles, fuse, bw, b16)
+        if after_params is not None:
+            after_params()
         return dcond
 
     def _bwd_param_tail(self, st, dout, dx, dss, dssb, tmp_dss, dpre_all, dpre_b, dd_all,
@@ -615,12 +618,10 @@ class GaussianDiffusion(BaseModel):
         return noise, xr, dict(est=est, dst=dst)
 
     def _bwd(self, st, dxr, after_denoiser=None, want_spk=True):
-        """after_denoiser: called between the DiffNet and the encoder backward (the step
-        schedule records a stream event there).  Returns the per-sequence speaker-vector
-        gradient (B, E) when want_spk."""
-        dcond = self.denoise_fn._bwd(st["dst"], dxr)
-        if after_denoiser is not None:
-            after_denoiser()
+        """after_denoiser: called once the DiffNet's parameter gradients are issued, on their
+        stream (the data-parallel bucket of those parameters).  Returns the per-sequence
+        speaker-vector gradient (B, E) when want_spk."""
+        dcond = self.denoise_fn._bwd(st["dst"], dxr, after_params=after_denoiser)
         _, dspk = self.encoder._bwd(st["est"], dcond, want_spk=want_spk)
         return dspk
 

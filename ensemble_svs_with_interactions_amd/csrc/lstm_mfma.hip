@@ -198,6 +198,9 @@ __global__ __launch_bounds__(NT) void lstm_mfma_fwd_kernel(
     const int cnt = min(CH, L - ch * CH);
     for (int st = 0; st < cnt; ++st) {
       const int s = ch * CH + st;
+      float gv[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) gv[g] = gin[st * GW + g * H + u];
       const _Float16* hc = hb + ((s + 1) & 1) * HP + 8 * lg;
       f16x8 bf[NKC];
 #pragma unroll
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(NT) void lstm_mfma_fwd_kernel(
         float col[NMT];
 #pragma unroll
         for (int mt = 0; mt < NMT; ++mt) col[mt] = acc[mt][g];
-        a[g] = pick<NMT>(col, msk) + gin[st * GW + g * H + u];
+        a[g] = pick<NMT>(col, msk) + gv[g];
       }
       const float ig = sigm(a[0]), fg = sigm(a[1]), gg = tanh_fast(a[2]), og = sigm(a[3]);
       c = fg * c + ig * gg;
@@ -331,6 +334,14 @@ __global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
     const int cnt = min(CH, L - ch * CH);
     for (int st = 0; st < cnt; ++st) {
       const int p = ch * CH + st;  // processing index
+      const float* in = gin + st * IW;
+      float iv[7];
+#pragma unroll
+      for (int g = 0; g < 7; ++g) iv[g] = in[g * H + u];
+      // read before the product: their LDS latency hides under the dG reads and the MFMAs
+      // (H = 128: 711 -> 672 ns per step; the forward's four reads gain nothing this way)
+#pragma unroll
+      for (int g = 0; g < 7; ++g) asm volatile("" : "+v"(iv[g]));
       const __bf16* gc = gb + ((p + 1) & 1) * GP + 8 * lg;
       bf16x8 bf[NKB];
 #pragma unroll
@@ -347,9 +358,8 @@ __global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
 #pragma unroll
       for (int f = 0; f < 4 * TPW; ++f) flat[f] = acc[f >> 2][f & 3];
       const float dhr = pick<4 * TPW>(flat, msk);
-      const float* in = gin + st * IW;
-      const float ig = in[u], fg = in[H + u], gg = in[2 * H + u], og = in[3 * H + u];
-      const float ct = in[4 * H + u], dyv = in[5 * H + u], cp = in[6 * H + u];
+      const float ig = iv[0], fg = iv[1], gg = iv[2], og = iv[3];
+      const float ct = iv[4], dyv = iv[5], cp = iv[6];
       const float dh = dyv + dhr;
       const float tc = tanh_fast(ct);
       const float dcc = dc + dh * og * (1.f - tc * tc);

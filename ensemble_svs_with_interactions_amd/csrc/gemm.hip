@@ -2209,7 +2209,8 @@ __device__ __forceinline__ bf16x8 wg_frag(const char* img, int c0, int lane) {
 // the wgrad kernels, profiles/r3_step_pmc.json).  When the split count is a multiple of 8,
 // split s runs all its workgroups on XCD s % 8: hardware id b -> xcd = b % 8, then the
 // workgroup index w inside the split and s = 8 (b / 8 / W) + xcd.  Bijective; the partial of
-// split s covers the same rows as before, so the results are bitwise unchanged.
+// split s covers the same rows as before, so the results are bitwise unchanged.  (Grouping by
+// (split, tap) instead measured 17.50 vs 17.40 ms/step; the raw order 17.72.)
 __device__ __forceinline__ void wgrad_tile(const WgradArgs& a, int& n0, int& k0, int& j, int& s) {
   const int gx = gridDim.x, gy = gridDim.y;
   if (a.splits % 8 == 0) {

@@ -403,8 +403,12 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
     if splits is None:
         tiles = -(-N // 128) * -(-K // 128) * taps
         splits = max(1, min(64, WGRAD_TARGET // max(tiles, 1), -(-M // 256)))
-        if splits >= 8:  # a multiple of 8: each split's workgroups share one XCD's L2
-            splits = max(8, (splits + 4) // 8 * 8)
+        # a multiple of 8 lets each split's workgroups share one XCD's L2 (gemm.hip
+        # wgrad_tile) -- when that still fits one wave of WGRAD_TARGET workgroups: rounding
+        # the DiffNet dilated conv's 21 splits up to 24 (576 workgroups) cost 51 -> 68 us
+        up = -(-splits // 8) * 8
+        if splits >= 8 and up * tiles <= WGRAD_TARGET:
+            splits = up
     part = scratch(splits * taps * N * K, dy.device)
     if dy.dtype == torch.bfloat16 or x.dtype == torch.bfloat16:
         assert dy.dtype == x.dtype == torch.bfloat16 and radd is None and dtype == _lib.DT_BF16

@@ -61,7 +61,9 @@ def call(name, *args):
     orig_call(name, *args)
     e.record()
     tag = TAG[0]
-    if name in ("ensvs_lstm_fwd", "ensvs_lstm_bwd"):
+    if name in ("ensvs_lstm_mfma_fwd", "ensvs_lstm_mfma_bwd"):
+        t = f"H={args[6]} T={args[5]}"
+    elif name in ("ensvs_lstm_fwd", "ensvs_lstm_bwd"):
         tag = f"H={args[7]} B={args[5]} T={args[6]}"
     elif name in ("ensvs_lstm_coop_fwd", "ensvs_lstm_coop_bwd"):
         tag = f"H={args[6]} B={args[4]} T={args[5]}"

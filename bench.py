@@ -453,11 +453,12 @@ def synth_rtf(model, dev, T=2000, parts=6, reps=3):
                                   "GEMM/conv FLOPs of the whole pipeline over its wall time"})
 
 
-def cpu_synth_baseline(T=400):
+def cpu_synth_baseline(T=2000):
     """The oracle's synthesis of one (main, sub) pair on the host cores: multi-track
     acoustic inference (100 reverse-diffusion steps) + uSFGAN, full-size random weights,
-    T frames; RTF = elapsed / (T * 5 ms).  Bounded sample (the reference probe: acoustic
-    RTF 0.776 at T = 2000, uSFGAN 0.70 at 1 s)."""
+    T frames; RTF = elapsed / (T * 5 ms).  The GPU leg's length (synth_rtf, T = 2000 =
+    10 s of audio: about 20 s of CPU work on 16 cores), so the two RTFs compare like for
+    like (the reference probe: acoustic RTF 0.776 at T = 2000, uSFGAN 0.70 at 1 s)."""
     from oracle import ensvs_oracle as O
     from oracle import usfgan_oracle as U
     from oracle.weights import seeded_state_dict
@@ -812,7 +813,7 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(args)
         if "synth" in out:
-            out["synth"]["cpu_baseline"] = cpu_synth_baseline()
+            out["synth"]["cpu_baseline"] = cpu_synth_baseline(out["synth"]["frames"])
     print(json.dumps(out), flush=True)
 
 

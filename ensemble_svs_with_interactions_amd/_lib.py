@@ -91,8 +91,10 @@ SIGNATURES = {
                        c_vp, c_ll, c_vp],
     "ensvs_lstm_mfma_supported": [c_int],
     "ensvs_lstm_mfma_pack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
-    "ensvs_lstm_mfma_fwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp],
-    "ensvs_lstm_mfma_bwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp],
+    "ensvs_lstm_mfma_fwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
+                            c_int, c_vp],
+    "ensvs_lstm_mfma_bwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp,
+                            c_int, c_vp, c_vp],
     "ensvs_lstm_coop_supported": [c_int, c_int],
     "ensvs_lstm_coop_work_bytes": [c_int],
     "ensvs_lstm_coop_pack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],

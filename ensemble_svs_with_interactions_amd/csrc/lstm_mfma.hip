@@ -121,7 +121,8 @@ __global__ __launch_bounds__(NT) void lstm_mfma_fwd_kernel(
     const f16x8* __restrict__ wp,                 // packed forward fragments
     const long long* __restrict__ lengths, int T,
     float* __restrict__ y, int ldy,               // [B*T][ldy], dir d at cols d*H + u
-    float* __restrict__ sv) {                     // saved [B*T][2][5H]: i,f,g,o,c
+    float* __restrict__ sv,                       // saved [B*T][2][5H]: i,f,g,o,c
+    __bf16* __restrict__ yb, int ldyb) {          // optional bf16 copy of y (as y)
   using G = MGeo<H>;
   constexpr int NMT = G::NMT, NKC = G::NKC, HP = G::HP, CH = G::CH, GW = 4 * H, OW = 6 * H;
   constexpr int PF = CH * GW / 4 / NT;  // float4 of one input chunk per thread
@@ -154,8 +155,10 @@ __global__ __launch_bounds__(NT) void lstm_mfma_fwd_kernel(
   float c = 0.f;
 
   const long long rowb = (long long)b * T;
-  for (int i = tid; i < (T - L) * H; i += NT)
+  for (int i = tid; i < (T - L) * H; i += NT) {
     y[(rowb + L + i / H) * ldy + dir * H + (i % H)] = 0.f;
+    if (yb) yb[(rowb + L + i / H) * ldyb + dir * H + (i % H)] = (__bf16)0.f;
+  }
 
   const int nch = (L + CH - 1) / CH;
   f32x4 rin[PF];
@@ -183,8 +186,12 @@ __global__ __launch_bounds__(NT) void lstm_mfma_fwd_kernel(
       const int s = ch * CH + st;
       const long long row = rowb + (dir ? L - 1 - s : s);
       const f32x4 val = *(const f32x4*)(out + st * OW + c4 * 4);
-      if (c4 < H / 4) *(f32x4*)(y + row * ldy + dir * H + c4 * 4) = val;
-      else *(f32x4*)(sv + (row * 2 + dir) * 5 * H + (c4 - H / 4) * 4) = val;
+      if (c4 < H / 4) {
+        *(f32x4*)(y + row * ldy + dir * H + c4 * 4) = val;
+        if (yb)
+          *(bf16x4*)(yb + row * ldyb + dir * H + c4 * 4) =
+              bf16x4{(__bf16)val[0], (__bf16)val[1], (__bf16)val[2], (__bf16)val[3]};
+      } else *(f32x4*)(sv + (row * 2 + dir) * 5 * H + (c4 - H / 4) * 4) = val;
     }
   };
 
@@ -250,7 +257,9 @@ __global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
     const bf16x8* __restrict__ wp,                // packed backward fragments
     const long long* __restrict__ lengths, int T,
     const float* __restrict__ sv,                 // saved [B*T][2][5H]
-    float* __restrict__ dg, int lddg) {           // [B*T][lddg], dir d pre-act grads at d*4H + g*H + u
+    float* __restrict__ dg, int lddg,             // [B*T][lddg], dir d pre-act grads at d*4H + g*H + u
+    __bf16* __restrict__ dgb, int lddgb,          // optional bf16 copy of dg (either may be null)
+    float* __restrict__ bsum) {                   // optional [B][8H]: sum over t of dg row (b, t)
   using G = MGeo<H>;
   constexpr int TPW = G::TPW, NKB = G::NKB, GP = G::GP, CH = G::CH, IW = 7 * H, GW = 4 * H;
   constexpr int NIN = CH * IW / 4;  // float4 per input chunk
@@ -283,8 +292,10 @@ __global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
   const int u = v * G::UPW + lg * 4 * TPW + sel;
 
   const long long rowb = (long long)b * T;
-  for (int i = tid; i < (T - L) * GW; i += NT)
-    dg[(rowb + L + i / GW) * lddg + dir * GW + (i % GW)] = 0.f;
+  for (int i = tid; i < (T - L) * GW; i += NT) {
+    if (dg) dg[(rowb + L + i / GW) * lddg + dir * GW + (i % GW)] = 0.f;
+    if (dgb) dgb[(rowb + L + i / GW) * lddgb + dir * GW + (i % GW)] = (__bf16)0.f;
+  }
 
   // chunk ch holds processing steps s = L-1-ch*CH-st, st = 0..CH-1 (descending s)
   const int nch = (L + CH - 1) / CH;
@@ -319,7 +330,11 @@ __global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
       const int st = e / (GW / 4), c4 = e % (GW / 4);
       const int s = L - 1 - ch * CH - st;
       const long long row = rowb + (dir ? L - 1 - s : s);
-      *(f32x4*)(dg + row * lddg + dir * GW + c4 * 4) = *(const f32x4*)(out + st * GW + c4 * 4);
+      const f32x4 val = *(const f32x4*)(out + st * GW + c4 * 4);
+      if (dg) *(f32x4*)(dg + row * lddg + dir * GW + c4 * 4) = val;
+      if (dgb)
+        *(bf16x4*)(dgb + row * lddgb + dir * GW + c4 * 4) =
+            bf16x4{(__bf16)val[0], (__bf16)val[1], (__bf16)val[2], (__bf16)val[3]};
     }
   };
 
@@ -330,6 +345,7 @@ __global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
   if (nch > 1) load_chunk(1);
   __syncthreads();
   float dc = 0.f;
+  float ds[4] = {0.f, 0.f, 0.f, 0.f};  // this cell's dg summed over its steps (bias gradient)
   for (int ch = 0; ch < nch; ++ch) {
     const int cnt = min(CH, L - ch * CH);
     for (int st = 0; st < cnt; ++st) {
@@ -368,6 +384,10 @@ __global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
       const float d_g = dcc * ig * (1.f - gg * gg);
       const float d_o = dh * tc * og * (1.f - og);
       dc = dcc * fg;
+      ds[0] += d_i;
+      ds[1] += d_f;
+      ds[2] += d_g;
+      ds[3] += d_o;
       if (act) {
         bf16x4 nb;
         nb[0] = (__bf16)d_i;
@@ -388,6 +408,10 @@ __global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
     if (ch + 2 < nch) load_chunk(ch + 2);
     __syncthreads();
   }
+  if (bsum && act) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bsum[(long long)b * 2 * GW + dir * GW + g * H + u] = ds[g];
+  }
 }
 
 // ---------------------------------------------------------------------------------- launch
@@ -397,26 +421,27 @@ size_t excl(size_t need) {
 
 template <int H>
 int launch_fwd(const float* gx, int ldg, const void* wp, const long long* lengths, int B, int T,
-               float* y, int ldy, float* sv, hipStream_t st) {
+               float* y, int ldy, float* sv, __bf16* yb, int ldyb, hipStream_t st) {
   const size_t lds = excl(MGeo<H>::FWD_LDS);
   static const hipError_t attr = hipFuncSetAttribute(
       (const void*)lstm_mfma_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return ENSVS_E_HIP;
   hipLaunchKernelGGL(lstm_mfma_fwd_kernel<H>, dim3(B, 2), dim3(NT), lds, st, gx, ldg,
-                     (const f16x8*)wp, lengths, T, y, ldy, sv);
+                     (const f16x8*)wp, lengths, T, y, ldy, sv, yb, ldyb);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
 
 template <int H>
 int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengths, int B, int T,
-               const float* sv, float* dg, int lddg, hipStream_t st) {
+               const float* sv, float* dg, int lddg, __bf16* dgb, int lddgb, float* bsum,
+               hipStream_t st) {
   const size_t lds = excl(MGeo<H>::BWD_LDS);
   static const hipError_t attr = hipFuncSetAttribute(
       (const void*)lstm_mfma_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return ENSVS_E_HIP;
   hipLaunchKernelGGL(lstm_mfma_bwd_kernel<H>, dim3(B, 2), dim3(NT), lds, st, dy, lddy,
-                     (const bf16x8*)wp, lengths, T, sv, dg, lddg);
+                     (const bf16x8*)wp, lengths, T, sv, dg, lddg, dgb, lddgb, bsum);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
@@ -446,26 +471,34 @@ ENSVS_API int ensvs_lstm_mfma_pack(const float* whh_f, const float* whh_r, int H
 
 ENSVS_API int ensvs_lstm_mfma_fwd(const float* gx, int ldg, const void* wpack,
                                   const long long* lengths, int B, int T, int H, float* y, int ldy,
-                                  float* saved, void* stream) {
-  if (!ensvs_lstm_mfma_supported(H) || B <= 0 || T <= 0 || ldg < 8 * H || ldy < 2 * H)
+                                  float* saved, void* ybf, int ldyb, void* stream) {
+  if (!ensvs_lstm_mfma_supported(H) || B <= 0 || T <= 0 || ldg < 8 * H || ldy < 2 * H ||
+      (ybf && ldyb < 2 * H))
     return ENSVS_E_SHAPE;
   if (ldg % 4 || ldy % 4 || !aligned16(gx) || !aligned16(y) || !aligned16(saved) ||
-      !aligned16(wpack) || !lengths)
+      !aligned16(wpack) || !lengths || (ybf && (ldyb % 4 || (uintptr_t)ybf % 8)))
     return ENSVS_E_ARG;
   hipStream_t st = (hipStream_t)stream;
-  return H == 64 ? launch_fwd<64>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, st)
-                 : launch_fwd<128>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, st);
+  __bf16* yb = (__bf16*)ybf;
+  return H == 64 ? launch_fwd<64>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, yb, ldyb, st)
+                 : launch_fwd<128>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, yb, ldyb, st);
 }
 
 ENSVS_API int ensvs_lstm_mfma_bwd(const float* dy, int lddy, const void* wpack,
                                   const long long* lengths, int B, int T, int H,
-                                  const float* saved, float* dg, int lddg, void* stream) {
-  if (!ensvs_lstm_mfma_supported(H) || B <= 0 || T <= 0 || lddy < 2 * H || lddg < 8 * H)
+                                  const float* saved, float* dg, int lddg, void* dgbf,
+                                  int lddgb, float* bsum, void* stream) {
+  if (!ensvs_lstm_mfma_supported(H) || B <= 0 || T <= 0 || lddy < 2 * H ||
+      (dg && lddg < 8 * H) || (dgbf && lddgb < 8 * H))
     return ENSVS_E_SHAPE;
-  if (lddy % 4 || lddg % 4 || !aligned16(dy) || !aligned16(dg) || !aligned16(saved) ||
-      !aligned16(wpack) || !lengths)
+  if (lddy % 4 || !aligned16(dy) || !aligned16(saved) || !aligned16(wpack) || !lengths ||
+      (!dg && !dgbf) || (dg && (lddg % 4 || !aligned16(dg))) ||
+      (dgbf && (lddgb % 4 || (uintptr_t)dgbf % 8)))
     return ENSVS_E_ARG;
   hipStream_t st = (hipStream_t)stream;
-  return H == 64 ? launch_bwd<64>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, st)
-                 : launch_bwd<128>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, st);
+  __bf16* dgb = (__bf16*)dgbf;
+  return H == 64 ? launch_bwd<64>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, dgb, lddgb,
+                                  bsum, st)
+                 : launch_bwd<128>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, dgb, lddgb,
+                                   bsum, st);
 }

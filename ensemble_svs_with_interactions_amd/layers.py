@@ -478,19 +478,35 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
     H = lstm.hidden_size
     sv = []
     h, ldh = X, ldx
+    h16 = None  # bf16 copy of h (the previous layer's output straight from its recurrence)
     for l in range(lstm.num_layers):
         Kc = getattr(lstm, f"weight_ih_l{l}").shape[1]
+        HP = lstm_pad(H)
+        # MFMA recurrences on unpadded H: the layer input and output also kept as bf16 for
+        # the backward's bf16-operand GEMMs (the same roundings those GEMMs apply to fp32)
+        direct = not lstm_coop(B, H) and not HP and lstm_mfma(H)
+        x16 = None
+        if direct:
+            if h16 is not None:
+                x16 = h16
+            elif Kc % 8 == 0 and K._castable(K.Seg(h, ldh, Kc, None, T)):
+                x16 = K.cast_bf16(h, ldh, Kc, M)
+        xa, lda = (x16, Kc if h16 is None else 2 * H) if x16 is not None else (h, ldh)
         gx = empty(M, 8 * H, device=device)
         if lstm_fused_proj(H):
             assert pk[f"b{l}_reverse"].offset == pk[f"b{l}"].offset + 4 * H
-            K.gemm([K.Seg(h, ldh, Kc, pk[f"ih{l}"], T)], B, T, 8 * H, pk.fwd, gx, 8 * H,
+            K.gemm([K.Seg(xa, lda, Kc, pk[f"ih{l}"], T)], B, T, 8 * H, pk.fwd, gx, 8 * H,
                    **pk.bias_ptr_args(f"b{l}"))
         else:
             for d, sfx in enumerate(("", "_reverse")):
-                K.gemm([K.Seg(h, ldh, Kc, pk[f"ih{l}{sfx}"], T)], B, T, 4 * H, pk.fwd, gx,
+                K.gemm([K.Seg(xa, lda, Kc, pk[f"ih{l}{sfx}"], T)], B, T, 4 * H, pk.fwd, gx,
                        8 * H, yoff=d * 4 * H, **pk.bias_ptr_args(f"b{l}{sfx}"))
         y = empty(M, 2 * H, device=device)
-        HP = lstm_pad(H)
+        last = l == lstm.num_layers - 1
+        drop = dropout_masks is not None and not last
+        y16 = None
+        if direct and (save or not (last or drop)):
+            y16 = torch.empty(M, 2 * H, dtype=torch.bfloat16, device=device)
         saved = empty(M * 2 * 5 * (HP or H), device=device)
         if lstm_coop(B, H):
             work, nbytes = _coop_work(H, device)
@@ -504,7 +520,7 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
             if lstm_mfma(HP):
                 call("ensvs_lstm_mfma_fwd", gxp.data_ptr(), 8 * HP,
                      _mfma_pack(lstm, l, False, HP).data_ptr(), lens_dev.data_ptr(), B, T, HP,
-                     yp.data_ptr(), 2 * HP, saved.data_ptr(), stream())
+                     yp.data_ptr(), 2 * HP, saved.data_ptr(), None, 0, stream())
             else:
                 w0, w1 = _whh_pad(lstm, l, HP)
                 call("ensvs_lstm_fwd", gxp.data_ptr(), 8 * HP, w0.data_ptr(), w1.data_ptr(),
@@ -512,9 +528,10 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
                      stream())
             _regroup(yp, 2 * HP, y, 2 * H, M, 2, HP, H)
             del gxp, yp
-        elif lstm_mfma(H):
+        elif direct:
             call("ensvs_lstm_mfma_fwd", gx.data_ptr(), 8 * H, _mfma_pack(lstm, l, False).data_ptr(),
-                 lens_dev.data_ptr(), B, T, H, y.data_ptr(), 2 * H, saved.data_ptr(), stream())
+                 lens_dev.data_ptr(), B, T, H, y.data_ptr(), 2 * H, saved.data_ptr(),
+                 ptr(y16), 2 * H, stream())
         else:
             call("ensvs_lstm_fwd", gx.data_ptr(), 8 * H,
                  getattr(lstm, f"weight_hh_l{l}").data_ptr(),
@@ -529,8 +546,10 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
             call("ensvs_mul_out", yin.data_ptr(), y.data_ptr(), mask.data_ptr(), yin.numel(),
                  stream())
         if save:
-            sv.append(dict(x=h, ldx=ldh, y=y, saved=saved, mask=mask, yin=yin, hp=HP))
+            sv.append(dict(x=h, ldx=ldh, y=y, saved=saved, mask=mask, yin=yin, hp=HP, x16=x16,
+                           y16=y16))
         h, ldh = yin, 2 * H
+        h16 = None if mask is not None else y16
     return h, sv
 
 
@@ -542,7 +561,14 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
     for l in reversed(range(lstm.num_layers)):
         s = sv[l]
         Kc = getattr(lstm, f"weight_ih_l{l}").shape[1]
-        dg = empty(M, 8 * H, device=device)
+        x16, y16 = s.get("x16"), s.get("y16")
+        # bf16 dg for the GEMMs (fp32 dg only when the layer input has no bf16 copy) and the
+        # bias gradient's per-sequence partial sums, all from the MFMA recurrence
+        dgb = bpart = None
+        if y16 is not None:
+            dgb = torch.empty(M, 8 * H, dtype=torch.bfloat16, device=device)
+            bpart = empty(B, 8 * H, device=device)
+        dg = empty(M, 8 * H, device=device) if dgb is None or x16 is None else None
         if lstm_coop(B, H):
             work, nbytes = _coop_work(H, device)
             call("ensvs_lstm_coop_bwd", d.data_ptr(), 2 * H, _coop_pack(lstm, l, True).data_ptr(),
@@ -556,7 +582,7 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
             if lstm_mfma(HP):
                 call("ensvs_lstm_mfma_bwd", dp.data_ptr(), 2 * HP,
                      _mfma_pack(lstm, l, True, HP).data_ptr(), lens_dev.data_ptr(), B, T, HP,
-                     s["saved"].data_ptr(), dgp.data_ptr(), 8 * HP, stream())
+                     s["saved"].data_ptr(), dgp.data_ptr(), 8 * HP, None, 0, None, stream())
             else:
                 w0, w1 = _whh_pad(lstm, l, HP)
                 nw = query("ensvs_lstm_bwd_work_floats", B, HP)
@@ -568,8 +594,8 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
             del dp, dgp
         elif lstm_mfma(H):
             call("ensvs_lstm_mfma_bwd", d.data_ptr(), 2 * H, _mfma_pack(lstm, l, True).data_ptr(),
-                 lens_dev.data_ptr(), B, T, H, s["saved"].data_ptr(), dg.data_ptr(), 8 * H,
-                 stream())
+                 lens_dev.data_ptr(), B, T, H, s["saved"].data_ptr(), ptr(dg), 8 * H, ptr(dgb),
+                 8 * H, ptr(bpart), stream())
         else:
             nw = query("ensvs_lstm_bwd_work_floats", B, H)
             work = empty(max(nw, 1), device=device)
@@ -577,23 +603,30 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
                  getattr(lstm, f"weight_hh_l{l}").data_ptr(),
                  getattr(lstm, f"weight_hh_l{l}_reverse").data_ptr(), lens_dev.data_ptr(), B, T,
                  H, s["saved"].data_ptr(), dg.data_ptr(), 8 * H, work.data_ptr(), nw, stream())
+        gy, yy = (dgb, y16) if dgb is not None else (dg, s["y"])
+        gi, xi, ldi = (dgb, x16, x16.shape[1]) if x16 is not None and dgb is not None else \
+            (dg, s["x"], s["ldx"])
         for di, sfx in enumerate(("", "_reverse")):
-            wgrad_into(getattr(lstm, f"weight_ih_l{l}{sfx}"), dg, 8 * H, s["x"], s["ldx"], B, T, T,
+            wgrad_into(getattr(lstm, f"weight_ih_l{l}{sfx}"), gi, 8 * H, xi, ldi, B, T, T,
                        4 * H, Kc, dyoff=di * 4 * H)
             # h_{t-1} in processing order: t-1 forward, t+1 reverse (zero outside [0, L))
-            wgrad_into(getattr(lstm, f"weight_hh_l{l}{sfx}"), dg, 8 * H, s["y"], 2 * H, B, T, T,
+            wgrad_into(getattr(lstm, f"weight_hh_l{l}{sfx}"), gy, 8 * H, yy, 2 * H, B, T, T,
                        4 * H, H, shift0=(-1 if di == 0 else 1), dyoff=di * 4 * H, xoff=di * H)
         # b_ih and b_hh of both directions share one gradient: the column sums of dg, once
         bsum = empty(8 * H, device=device)
-        K.colsum(dg, 8 * H, M, 8 * H, bsum)
+        if bpart is not None:
+            K.colsum(bpart, 8 * H, B, 8 * H, bsum)
+        else:
+            K.colsum(dg, 8 * H, M, 8 * H, bsum)
         for di, sfx in enumerate(("", "_reverse")):
             add_into_pair(bsum.data_ptr() + di * 16 * H, 4 * H, getattr(lstm, f"bias_ih_l{l}{sfx}"),
                           getattr(lstm, f"bias_hh_l{l}{sfx}"))
         if l == 0 and not need_dx:
             break
         nd = empty(M, Kc, device=device)
-        K.gemm([K.Seg(dg, 8 * H, 4 * H, pk[f"ih{l}^T"], T),
-                K.Seg(dg, 8 * H, 4 * H, pk[f"ih{l}_reverse^T"], T, xoff=4 * H)],
+        gd = dgb if dgb is not None else dg
+        K.gemm([K.Seg(gd, 8 * H, 4 * H, pk[f"ih{l}^T"], T),
+                K.Seg(gd, 8 * H, 4 * H, pk[f"ih{l}_reverse^T"], T, xoff=4 * H)],
                B, T, Kc, pk.bwd, nd, Kc)
         if l > 0:
             prev_mask = sv[l - 1].get("mask")

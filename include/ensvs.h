@@ -192,15 +192,21 @@ int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* w
  * acoustic_models/tacotron_f0.py:876-883).  wpack: ensvs_lstm_mfma_pack output for both
  * directions (bwd = 0: fp16 forward fragments, bwd = 1: bf16 backward fragments of W_hh^T),
  * 2*4*H*H 2-byte elements, 16-B aligned; gx / y / saved / dy / dg 16-B aligned, leading
- * dimensions multiples of 4. */
+ * dimensions multiples of 4.  Optional outputs for the bf16-operand GEMMs that consume them
+ * (the layer's weight gradients and input gradient), written from the same chunk flush:
+ * ybf (bf16 [B*T][ldyb]) = y rounded to bf16; dgbf (bf16 [B*T][lddgb]) = dg rounded to bf16
+ * (dg itself may then be NULL, one of the two is required); bsum (fp32 [B][8H]): row b =
+ * sum over t of dg row (b, t), the per-sequence partials of the bias gradient (the column
+ * sums of dg the reference's autograd forms for b_ih / b_hh).  8-B aligned bf16 pointers. */
 int ensvs_lstm_mfma_supported(int H);
 int ensvs_lstm_mfma_pack(const float* whh_f, const float* whh_r, int H, int bwd, void* out,
                          void* stream);
 int ensvs_lstm_mfma_fwd(const float* gx, int ldg, const void* wpack, const long long* lengths,
-                        int B, int T, int H, float* y, int ldy, float* saved, void* stream);
+                        int B, int T, int H, float* y, int ldy, float* saved, void* ybf,
+                        int ldyb, void* stream);
 int ensvs_lstm_mfma_bwd(const float* dy, int lddy, const void* wpack, const long long* lengths,
                         int B, int T, int H, const float* saved, float* dg, int lddg,
-                        void* stream);
+                        void* dgbf, int lddgb, float* bsum, void* stream);
 int ensvs_lstm_coop_supported(int B, int H);
 long long ensvs_lstm_coop_work_bytes(int H);
 int ensvs_lstm_coop_pack(const float* whh_f, const float* whh_r, int H, int bwd, void* out,

@@ -89,8 +89,11 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False, mfma=False):
         call("ensvs_lstm_mfma_pack", whh[0].data_ptr(), whh[1].data_ptr(), H, 0, wpf.data_ptr(), st)
         call("ensvs_lstm_mfma_pack", whh[0].data_ptr(), whh[1].data_ptr(), H, 1, wpb.data_ptr(), st)
         y.fill_(float("nan"))
+        yb = torch.full((B * T, 2 * H), float("nan"), dtype=torch.bfloat16, device=dev)
         call("ensvs_lstm_mfma_fwd", gx_d.data_ptr(), 8 * H, wpf.data_ptr(), lens.data_ptr(), B, T,
-             H, y.data_ptr(), 2 * H, saved.data_ptr(), st)
+             H, y.data_ptr(), 2 * H, saved.data_ptr(), yb.data_ptr(), 2 * H, st)
+        # the bf16 copy is y rounded to nearest even, padded frames included (zeros)
+        assert torch.equal(yb.view(torch.int16), y.to(torch.bfloat16).view(torch.int16))
     else:
         call("ensvs_lstm_fwd", gx_d.data_ptr(), 8 * H, whh[0].data_ptr(), whh[1].data_ptr(),
              lens.data_ptr(), B, T, H, y.data_ptr(), 2 * H, saved.data_ptr(), st)
@@ -108,8 +111,17 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False, mfma=False):
         assert cwork[128:132].cpu().view(torch.int32).item() == 0
     elif mfma:
         dg.fill_(float("nan"))
+        dgb = torch.full((B * T, 8 * H), float("nan"), dtype=torch.bfloat16, device=dev)
+        bsum = torch.full((B, 8 * H), float("nan"), device=dev)
         call("ensvs_lstm_mfma_bwd", gy_d.data_ptr(), 2 * H, wpb.data_ptr(), lens.data_ptr(), B, T,
-             H, saved.data_ptr(), dg.data_ptr(), 8 * H, st)
+             H, saved.data_ptr(), dg.data_ptr(), 8 * H, None, 0, None, st)
+        # the bf16 copy alone (no fp32 dg) plus the per-sequence bias partials: the same
+        # values, rounded, and sums of dg's rows within 1e-5 of its column sums
+        call("ensvs_lstm_mfma_bwd", gy_d.data_ptr(), 2 * H, wpb.data_ptr(), lens.data_ptr(), B, T,
+             H, saved.data_ptr(), None, 0, dgb.data_ptr(), 8 * H, bsum.data_ptr(), st)
+        assert torch.equal(dgb.view(torch.int16), dg.to(torch.bfloat16).view(torch.int16))
+        want = dg.view(B, T, 8 * H).double().sum(1)
+        assert (bsum.double() - want).abs().max().item() <= 1e-5 * want.abs().max().item() + 1e-6
     else:
         call("ensvs_lstm_bwd", gy_d.data_ptr(), 2 * H, whh[0].data_ptr(), whh[1].data_ptr(),
              lens.data_ptr(), B, T, H, saved.data_ptr(), dg.data_ptr(), 8 * H, work.data_ptr(),

@@ -51,9 +51,11 @@ for H in (64, 128):
                                w[1].data_ptr(), lens.data_ptr(), B, T, H, sv.data_ptr(),
                                dg.data_ptr(), 8 * H, work.data_ptr(), nw, st)),
         "mfma": (lambda: call("ensvs_lstm_mfma_fwd", gx.data_ptr(), 8 * H, wpf.data_ptr(),
-                              lens.data_ptr(), B, T, H, y.data_ptr(), 2 * H, sv.data_ptr(), st),
+                              lens.data_ptr(), B, T, H, y.data_ptr(), 2 * H, sv.data_ptr(), None,
+                              0, st),
                  lambda: call("ensvs_lstm_mfma_bwd", dy.data_ptr(), 2 * H, wpb.data_ptr(),
-                              lens.data_ptr(), B, T, H, sv.data_ptr(), dg.data_ptr(), 8 * H, st)),
+                              lens.data_ptr(), B, T, H, sv.data_ptr(), dg.data_ptr(), 8 * H,
+                              None, 0, None, st)),
     }
     for name, (f, b) in runs.items():
         uf, ub = timeit(f), timeit(b)

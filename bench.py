@@ -175,6 +175,8 @@ def step_census(model, opt, batch):
             t = f"H={args[7]} T={args[6]}"
         elif name in ("ensvs_lstm_mfma_fwd", "ensvs_lstm_mfma_bwd"):
             t = f"H={args[6]} T={args[5]}"
+        elif name == "ensvs_colsum":
+            t = f"M={args[2]} groups={args[3]} N={args[4]}{' centred' if args[5] else ''}"
         elif name in ("ensvs_ardec_fwd", "ensvs_ardec_coop_fwd"):  # T / 4 autoregressive steps
             t = f"H={args[15]} T={args[14]}"
         elif name in ("ensvs_ardec_bwd", "ensvs_ardec_coop_bwd"):

@@ -130,9 +130,9 @@ SIGNATURES = {
     "ensvs_bn_finalize": [c_vp, c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_vp, c_float, c_int,
                           c_vp],
     "ensvs_bn_apply_relu": [c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
-                            c_vp],
+                            c_vp, c_int, c_vp],
     "ensvs_bn_bwd": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp,
-                     c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
+                     c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
     "ensvs_bn_bwd_frozen": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                             c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
     "ensvs_sinusoidal": [c_vp, c_int, c_int, c_vp, c_vp],
@@ -165,7 +165,7 @@ SIGNATURES = {
     "ensvs_axpby_to_bf16": [c_vp, c_vp, c_vp, c_float, c_vp, c_float, c_ll, c_vp],
     "ensvs_mul": [c_vp, c_vp, c_ll, c_vp],
     "ensvs_mul_out": [c_vp, c_vp, c_vp, c_ll, c_vp],
-    "ensvs_relu_mask": [c_vp, c_vp, c_vp, c_ll, c_vp],
+    "ensvs_relu_mask": [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp],
     "ensvs_reflect_fold": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "ensvs_randn": [c_vp, c_ll, ctypes.c_ulonglong, c_vp],
     "ensvs_dropout_mask": [c_vp, c_ll, c_float, ctypes.c_ulonglong, c_vp],

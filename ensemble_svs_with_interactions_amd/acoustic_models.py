@@ -269,17 +269,19 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
              ptr(spks[1]) if two else None, spk_ld, Ly.stream())
         return Y, saved
 
-    def _conv_in(self, pk, h, xs, ld, B, T, dev):
+    def _conv_in(self, pk, h, xs, ld, B, T, dev, hb=None):
         """conv.1's input columns [FF output, score log-F0 of each track]: the fp32 segments
         (weight gradients) and, with bf16 operands, the forward's bf16 copies -- the FF
-        output, and the 1-2 log-F0 columns gathered into one zero-padded 8-wide operand, so
+        output (hb: the FF GEMM's own copy), and the 1-2 log-F0 columns gathered into one
+        zero-padded 8-wide operand, so
         the k7 conv runs on the LDS-DMA kernel (K = 256 + 1 + 1 fails its K % 8 contract
         as three segments: 182 us on the register-staged fp32 path at 30 x 1024 frames)."""
         F, li, M = h.shape[1], self.in_lf0_idx, B * T
         segs = [("ff", h, F, F, 0)] + [(f"s{k}", x, ld, 1, li) for k, x in enumerate(xs)]
         if not K.bf16_operands(pk.fwd, M) or F % 8:
             return segs, None
-        hb = K.cast_bf16(h, F, F, M)
+        if hb is None:
+            hb = K.cast_bf16(h, F, F, M)
         cols = empty(M, len(xs), device=dev)
         for k, x in enumerate(xs):
             call("ensvs_copy_cols", x.data_ptr() + 4 * li, ld, cols.data_ptr() + 4 * k,
@@ -300,12 +302,13 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
         M = B * T
         li = self.in_lf0_idx
         X0, esv = self._embed(pk, xs, ld, B, T, spks, spk_ld, dev)
-        hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
-        segs, b16 = self._conv_in(pk, hs[2], xs, ld, B, T, dev)
+        hs, hs16 = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
+        segs, b16 = self._conv_in(pk, hs[2], xs, ld, B, T, dev, hs16[2])
         a, csv = Ly.conv_fwd(pk, self.conv, segs, B, T, dev, training, save=save,
                              first_b16=b16)
         C = a.shape[1]
-        y, lsv = Ly.lstm_fwd(pk, self.lstm, a, C, B, T, lens_dev, dev, None, save=save)
+        y, lsv = Ly.lstm_fwd(pk, self.lstm, a, C, B, T, lens_dev, dev, None, save=save,
+                             x16=csv[-1]["out16"] if csv else None)
         dec = self.decoder
         cell = dec.lstm[0].cell
         H = cell.hidden_size
@@ -349,7 +352,7 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
                  *ins, *consts, *outs, Ly.stream())
         st = None
         if save:
-            st = dict(X0=X0, esv=esv, hs=hs, csv=csv, lsv=lsv, y=y, e=e, masks=masks, sg=sg,
+            st = dict(X0=X0, esv=esv, hs=hs, hs16=hs16, csv=csv, lsv=lsv, y=y, e=e, masks=masks, sg=sg,
                       sc=sc, sh=sh, so=so, sp=sp, B=B, T=T, lens=lens_dev, xs=xs, ld=ld,
                       teacher=teacher is not None)
         return lf0, res, st
@@ -408,7 +411,7 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
         da = Ly.lstm_bwd(pk, self.lstm, st["lsv"], dy, B, T, st["lens"], dev)
         F = st["hs"][2].shape[1]
         (dh3,) = Ly.conv_bwd(pk, self.conv, st["csv"], da, B, T, dev, first_dx=[("ff", F)])
-        dX0 = Ly.ff_bwd(pk, self.ff, st["X0"], st["hs"], dh3, B, T, dev)
+        dX0 = Ly.ff_bwd(pk, self.ff, st["X0"], st["hs"], st["hs16"], dh3, B, T, dev)
         E = self.embed_dim
         dspk = torch.zeros(B, E, device=dev) if want_spk else None
         for k, sv in enumerate(st["esv"]):
@@ -486,8 +489,8 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BiLSTMResF0NonAttentiveDecoder):
         dev = self.fc_in.weight.device
         li = self.in_lf0_idx
         X0, _ = self._embed(pk, [x_main, x_sub], ld, B, T, [s_main, s_sub], spk_ld, dev)
-        hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
-        segs, b16 = self._conv_in(pk, hs[2], [x_main, x_sub], ld, B, T, dev)
+        hs, hs16 = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
+        segs, b16 = self._conv_in(pk, hs[2], [x_main, x_sub], ld, B, T, dev, hs16[2])
         Ly.conv_fwd(pk, self.conv, segs, B, T, dev, True, save=False, first_b16=b16)
 
     # ---------------------------------------------------------------- reference API

@@ -33,6 +33,12 @@ enum { DT_F32 = 0, DT_BF16 = 1 };
     if (_e != hipSuccess) return ENSVS_E_HIP;              \
   } while (0)
 
+// Four fp32 values rounded to bf16 (nearest even) as one 8-B store: the rounding the GEMMs
+// apply to fp32 operands, so a copy written here is the operand they would have staged.
+__device__ __forceinline__ void store_bf16x4(__bf16* p, f32x4 v) {
+  *(bf16x4*)p = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
+
 // PyTorch ReflectionPad1d index map (valid for |pad| < n).
 __device__ __forceinline__ int reflect_idx(int i, int n) {
   i = i < 0 ? -i : i;

@@ -580,6 +580,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
           for (int e = 0; e < 4; ++e) v[e] = p1[k][e] > 0.f ? v[e] : 0.f;
           if (a.accum) v += p2[k];
           st4(y, v);
+          shadow4(a, m, col, v);
         } else if (a.epi == EPI_GATE_BWD) {
           f32x4 dg, df;
 #pragma unroll
@@ -1482,6 +1483,7 @@ __device__ __forceinline__ void epilogue_tile(const GemmArgs& a, const float* T,
         for (int e = 0; e < 4; ++e) v[e] = p1[e] > 0.f ? v[e] : 0.f;
         if (a.accum) v += p2;
         st4(y, v);
+        shadow4(a, m, col, v);
       } else if (a.epi == EPI_GATE_BWD) {
         f32x4 dg, df;
 #pragma unroll

@@ -197,7 +197,7 @@ __global__ void bn_apply_relu4_kernel(const float* __restrict__ y, int ldy, int 
                                       const float* __restrict__ rstd,
                                       const float* __restrict__ gamma,
                                       const float* __restrict__ beta, float* __restrict__ out,
-                                      int ldo) {
+                                      int ldo, __bf16* __restrict__ outb, int ldob) {
   const int C4 = C >> 2, n = M * C4;
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
     const int m = q / C4, c = (q - m * C4) * 4, g = m / Mg;
@@ -208,6 +208,7 @@ __global__ void bn_apply_relu4_kernel(const float* __restrict__ y, int ldy, int 
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = fmaxf((v[j] - mu[j]) * rs[j] * ga[j] + be[j], 0.f);
     *(f32x4*)(out + (long long)m * ldo + c) = o;
+    if (outb) store_bf16x4(outb + (long long)m * ldob + c, o);
   }
 }
 
@@ -339,7 +340,7 @@ __global__ void bn_bwd_apply4_kernel(const float* __restrict__ dout, int ldd,
                                      const float* __restrict__ gamma,
                                      const float* __restrict__ beta,
                                      const float* __restrict__ sums, float* __restrict__ dy,
-                                     int lddy) {
+                                     int lddy, __bf16* __restrict__ dyb, int lddyb) {
   const int C4 = C >> 2, n = M * C4;
   const float fMg = (float)Mg;
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
@@ -359,6 +360,7 @@ __global__ void bn_bwd_apply4_kernel(const float* __restrict__ dout, int ldd,
       o[j] = ga[j] * rs[j] * (dz - (s0[j] + xh * s1[j]) / fMg);
     }
     *(f32x4*)(dy + (long long)m * lddy + c) = o;
+    if (dyb) store_bf16x4(dyb + (long long)m * lddyb + c, o);
   }
 }
 
@@ -668,6 +670,20 @@ __global__ void relu_mask_kernel(float* __restrict__ out, const float* __restric
   GRID_LOOP(i, n) out[i] = act[i] > 0.f ? dy[i] : 0.f;
 }
 
+// the same, four elements per lane, plus the bf16 copy (n % 4 == 0, 16-B aligned)
+__global__ void relu_mask4_kernel(float* __restrict__ out, __bf16* __restrict__ outb,
+                                  const float* __restrict__ dy, const float* __restrict__ act,
+                                  long long n4) {
+  GRID_LOOP(q, n4) {
+    const f32x4 a = *(const f32x4*)(act + 4 * q), d = *(const f32x4*)(dy + 4 * q);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = a[j] > 0.f ? d[j] : 0.f;
+    *(f32x4*)(out + 4 * q) = o;
+    store_bf16x4(outb + 4 * q, o);
+  }
+}
+
 __global__ void mul_out_kernel(float* __restrict__ out, const float* __restrict__ a,
                                const float* __restrict__ b, long long n) {
   GRID_LOOP(i, n) out[i] = a[i] * b[i];
@@ -812,12 +828,15 @@ ENSVS_API int ensvs_bn_finalize(float* mean, float* var, int G, int C, long long
 
 ENSVS_API int ensvs_bn_apply_relu(const float* y, int ldy, long long M, int C, long long Mg,
                                   const float* mean, const float* rstd, const float* gamma,
-                                  const float* beta, float* out, int ldo, void* stream) {
-  if (bn_vec4(C, {ldy, ldo}, {y, out, mean, rstd, gamma, beta}, M)) {
+                                  const float* beta, float* out, int ldo, void* outb, int ldob,
+                                  void* stream) {
+  if (bn_vec4(C, {ldy, ldo}, {y, out, mean, rstd, gamma, beta}, M) &&
+      (!outb || (ldob % 4 == 0 && (uintptr_t)outb % 8 == 0))) {
     LAUNCH(bn_apply_relu4_kernel, M * C / 4, y, ldy, (int)M, C, (int)Mg, mean, rstd, gamma, beta,
-           out, ldo);
+           out, ldo, (__bf16*)outb, ldob);
     return ENSVS_OK;
   }
+  if (outb) return ENSVS_E_ARG;  // the bf16 copy needs the four-channel layout
   LAUNCH(bn_apply_relu_kernel, M * C, y, ldy, M, C, Mg, mean, rstd, gamma, beta, out, ldo);
   return ENSVS_OK;
 }
@@ -826,7 +845,11 @@ ENSVS_API int ensvs_bn_apply_relu(const float* y, int ldy, long long M, int C, l
 ENSVS_API int ensvs_bn_bwd(const float* dout, int ldd, const float* y, int ldy, long long M, int C,
                            long long Mg, const float* mean, const float* rstd, const float* gamma,
                            const float* beta, float* part, int max_splits, float* sums,
-                           float* dgamma, float* dbeta, float* dy, int lddy, void* stream) {
+                           float* dgamma, float* dbeta, float* dy, int lddy, void* dyb, int lddyb,
+                           void* stream) {
+  if (dyb && !(bn_vec4(C, {ldd, ldy, lddy}, {dout, y, dy, mean, rstd, gamma, beta, sums}, M) &&
+               lddyb % 4 == 0 && (uintptr_t)dyb % 8 == 0))
+    return ENSVS_E_ARG;  // the bf16 copy needs the four-channel layout
   hipStream_t st = (hipStream_t)stream;
   const int G = (int)(M / Mg);
   int S = (int)std::max<long long>(1, std::min<long long>(max_splits, Mg / 64));
@@ -842,7 +865,7 @@ ENSVS_API int ensvs_bn_bwd(const float* dout, int ldd, const float* y, int ldy, 
   ENSVS_CHECK_LAUNCH();
   if (bn_vec4(C, {ldd, ldy, lddy}, {dout, y, dy, mean, rstd, gamma, beta, sums}, M)) {
     LAUNCH(bn_bwd_apply4_kernel, M * C / 4, dout, ldd, y, ldy, (int)M, C, (int)Mg, mean, rstd,
-           gamma, beta, sums, dy, lddy);
+           gamma, beta, sums, dy, lddy, (__bf16*)dyb, lddyb);
     return ENSVS_OK;
   }
   LAUNCH(bn_bwd_apply_kernel, M * C, dout, ldd, y, ldy, M, C, Mg, mean, rstd, gamma, beta, sums, dy,
@@ -1065,8 +1088,15 @@ ENSVS_API int ensvs_randint(long long* out, long long n, long long hi, unsigned 
   return ENSVS_OK;
 }
 
-ENSVS_API int ensvs_relu_mask(float* out, const float* dy, const float* act, long long n,
-                              void* stream) {
+ENSVS_API int ensvs_relu_mask(float* out, void* outb, const float* dy, const float* act,
+                              long long n, void* stream) {
+  if (outb) {
+    if (n % 4 || (uintptr_t)out % 16 || (uintptr_t)dy % 16 || (uintptr_t)act % 16 ||
+        (uintptr_t)outb % 8)
+      return ENSVS_E_ARG;
+    LAUNCH(relu_mask4_kernel, n / 4, out, (__bf16*)outb, dy, act, n / 4);
+    return ENSVS_OK;
+  }
   LAUNCH(relu_mask_kernel, n, out, dy, act, n);
   return ENSVS_OK;
 }

@@ -453,7 +453,7 @@ class DiffNet(nn.Module):
         cs(dm1, 4 * C, B, 4 * C, m0.bias)
         # input projection (+ReLU)
         dpre0 = empty(M, C, device=dev)
-        call("ensvs_relu_mask", dpre0.data_ptr(), dx.data_ptr(), st["X"][0].data_ptr(), M * C,
+        call("ensvs_relu_mask", dpre0.data_ptr(), None, dx.data_ptr(), st["X"][0].data_ptr(), M * C,
              Ly.stream())
         ip = self.input_projection
         wg(ip.weight, dpre0, C, st["xin"], st["ldx"], B, T, T, C, Mc)

@@ -282,7 +282,8 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
     if ybf is not None and csum is None:
         assert ybf.dtype == torch.bfloat16 and epi in (_lib.EPI_PLAIN, _lib.EPI_GATE,
                                                        _lib.EPI_RESSKIP, _lib.EPI_GATE_BWD,
-                                                       _lib.EPI_GATE_TS, _lib.EPI_ADDSCALE)
+                                                       _lib.EPI_GATE_TS, _lib.EPI_ADDSCALE,
+                                                       _lib.EPI_RELU_MASK)
         yp = Y.data_ptr() + 4 * yoff
         vec = (yp % 16 == 0 and ldy % 4 == 0 and N % 4 == 0 and C % 4 == 0 and
                all(t is None or (t.data_ptr() % 16 == 0 and ld % 4 == 0)

@@ -179,44 +179,74 @@ def ff_register(pk, ff):
         pk.bias_vec(f"ff{i}.b", ff[i].bias)
 
 
+# Producers write bf16 copies of their outputs for the bf16-operand GEMMs that consume them
+# (FF / BatchNorm+ReLU / ReLU-mask passes, MFMA LSTM recurrences).  Off: the consumers round
+# the fp32 tensors themselves -- the same bits (tests compare the two).
+BF16_COPIES = {"on": True}
+
+
+def bf16_copy(pk, M, C, device):
+    """A bf16 [M, C] buffer for a producer's rounded copy of its output when the packed
+    weights take bf16 operands (the copy is the operand rounding the consuming GEMMs apply,
+    so it only saves their cast / register staging), else None."""
+    if not BF16_COPIES["on"] or C % 8 or not K.bf16_operands(pk.fwd, M):
+        return None
+    return torch.empty(M, C, dtype=torch.bfloat16, device=device)
+
+
 def ff_fwd(pk, ff, X, B, T, device):
+    """The three Linear + ReLU layers.  Returns (outputs, their bf16 copies or None): each
+    GEMM epilogue also writes its output rounded to bf16 -- the next layer's operand and the
+    backward's weight-gradient operand."""
     M = B * T
-    hs = []
+    hs, hs16 = [], []
     h, ldh = X, X.shape[1]
     for i in (0, 2, 4):
         N = ff[i].weight.shape[0]
         Kc = ff[i].weight.shape[1]
         out = empty(M, N, device=device)
+        ob = bf16_copy(pk, M, N, device)
         K.gemm([K.Seg(h, ldh, Kc, pk[f"ff{i}"], T)], B, T, N, pk.fwd, out, N, relu=True,
-               **pk.bias_ptr_args(f"ff{i}.b"))
+               ybf=ob, ybf_ld=N, **pk.bias_ptr_args(f"ff{i}.b"))
         hs.append(out)
-        h, ldh = out, N
-    return hs
+        hs16.append(ob)
+        h, ldh = (out, N) if ob is None else (ob, N)
+    return hs, hs16
 
 
-def ff_bwd(pk, ff, X, hs, dH3, B, T, device, need_dx=True):
-    """dH3: grad of the last ReLU output.  Returns grad w.r.t. X."""
+def ff_bwd(pk, ff, X, hs, hs16, dH3, B, T, device, need_dx=True):
+    """dH3: grad of the last ReLU output.  Returns grad w.r.t. X.  The layer gradients d
+    also come as bf16 copies (ReLU mask pass, ReLU-mask dgrad epilogue) for the weight
+    gradients against the forward's bf16 copies and for the dgrad GEMMs."""
     M = B * T
-    ins = [X, hs[0], hs[1]]
+    ins, ins16 = [X, hs[0], hs[1]], [None, hs16[0], hs16[1]]
     d = empty(M, dH3.shape[1], device=device)
-    call("ensvs_relu_mask", d.data_ptr(), dH3.data_ptr(), hs[2].data_ptr(), d.numel(), stream())
+    d16 = bf16_copy(pk, M, dH3.shape[1], device) if hs16[2] is not None else None
+    call("ensvs_relu_mask", d.data_ptr(), ptr(d16), dH3.data_ptr(), hs[2].data_ptr(), d.numel(),
+         stream())
     dx = None
     for li, i in enumerate((4, 2, 0)):
         lay = ff[i]
         N, Kc = lay.weight.shape
-        xin = ins[2 - li]
-        wgrad_into(lay.weight, d, N, xin, xin.shape[1], B, T, T, N, Kc)
+        xin, xin16 = ins[2 - li], ins16[2 - li]
+        if d16 is not None and xin16 is not None:
+            wgrad_into(lay.weight, d16, N, xin16, Kc, B, T, T, N, Kc)
+        else:
+            wgrad_into(lay.weight, d, N, xin, xin.shape[1], B, T, T, N, Kc)
         colsum_into(d, N, M, N, lay.bias)
         if i == 0 and not need_dx:
             break
         nd = empty(M, Kc, device=device)
+        dseg = K.Seg(d if d16 is None else d16, N, N, pk[f"ff{i}^T"], T)
+        nd16 = None
         if i > 0:
-            K.gemm([K.Seg(d, N, N, pk[f"ff{i}^T"], T)], B, T, Kc, pk.bwd, nd, Kc,
-                   epi=_lib.EPI_RELU_MASK, aux1=hs[2 - li - 1], ld1=Kc)
+            nd16 = bf16_copy(pk, M, Kc, device) if ins16[2 - li] is not None else None
+            K.gemm([dseg], B, T, Kc, pk.bwd, nd, Kc, epi=_lib.EPI_RELU_MASK,
+                   aux1=hs[2 - li - 1], ld1=Kc, ybf=nd16, ybf_ld=Kc)
         else:
-            K.gemm([K.Seg(d, N, N, pk[f"ff{i}^T"], T)], B, T, Kc, pk.bwd, nd, Kc)
+            K.gemm([dseg], B, T, Kc, pk.bwd, nd, Kc)
             dx = nd
-        d = nd
+        d, d16 = nd, nd16
     return dx
 
 
@@ -246,22 +276,34 @@ def conv_fwd(pk, conv, first_segs, B, T, device, training, groups=1, save=True,
     stands for a second call of the stack on the same input whose outputs are unused).
     first_b16: optional list of (name, bf16 tensor, ld, K) operands of conv.1's forward GEMM
     in place of first_segs (caller-rounded copies, e.g. narrow columns gathered into one
-    zero-padded segment); first_segs stay the fp32 inputs of the weight gradient."""
+    zero-padded segment); first_segs stay the fp32 inputs of the weight gradient, and a
+    first_b16 operand with a first_segs segment's name and width is also its bf16 weight-
+    gradient operand.  With bf16 operands every later layer's BatchNorm + ReLU pass writes
+    its output's bf16 copy too (the next convolution's operand; the last layer's is
+    returned in saved[-1]["out16"] for the caller's next GEMM)."""
     M = B * T
     Mg = M // groups
     sv = []
-    segs = [K.Seg(t, ld, Kc, pk[f"conv1@{name}"] if name else pk["conv1"], T, taps=7, dil=1,
-                  shift0=-3, pad=_lib.PAD_REFLECT, xoff=xoff)
+    key = lambda name: pk[f"conv1@{name}"] if name else pk["conv1"]  # noqa: E731
+    segs = [K.Seg(t, ld, Kc, key(name), T, taps=7, dil=1, shift0=-3, pad=_lib.PAD_REFLECT,
+                  xoff=xoff)
             for (name, t, ld, Kc, xoff) in first_segs]
     fsegs = segs if first_b16 is None else [
-        K.Seg(t, ld, Kc, pk[f"conv1@{name}"], T, taps=7, dil=1, shift0=-3, pad=_lib.PAD_REFLECT)
+        K.Seg(t, ld, Kc, key(name), T, taps=7, dil=1, shift0=-3, pad=_lib.PAD_REFLECT)
         for (name, t, ld, Kc) in first_b16]
-    a = None
+    twin = {name: (t, ld) for (name, t, ld, Kc) in (first_b16 or [])
+            if any(n == name and k == Kc for (n, _, _, k, _) in first_segs)}
+    segs16 = [twin.get(name) for (name, _, _, _, _) in first_segs]
+    a = a16 = None
     for li, (ci, bi) in enumerate(CONV_IDX):
         C = conv[ci].weight.shape[0]
         if li > 0:
-            segs = fsegs = [K.Seg(a, C_prev, C_prev, pk[f"conv{ci}"], T, taps=7, dil=1,
-                                  shift0=-3, pad=_lib.PAD_REFLECT)]
+            segs = [K.Seg(a, C_prev, C_prev, pk[f"conv{ci}"], T, taps=7, dil=1,
+                          shift0=-3, pad=_lib.PAD_REFLECT)]
+            fsegs = segs if a16 is None else [
+                K.Seg(a16, C_prev, C_prev, pk[f"conv{ci}"], T, taps=7, dil=1, shift0=-3,
+                      pad=_lib.PAD_REFLECT)]
+            segs16 = [None if a16 is None else (a16, C_prev)]
         y = empty(M, C, device=device)
         K.gemm(fsegs, B, T, C, pk.fwd, y, C, **pk.bias_ptr_args(f"conv{ci}.b"))
         bn = conv[bi]
@@ -290,12 +332,14 @@ def conv_fwd(pk, conv, first_segs, B, T, device, training, groups=1, save=True,
                  float(bn.eps), rstd.data_ptr(), None, None, 0.0, 0, stream())
             Mg_apply = M
         out = empty(M, C, device=device)
+        out16 = bf16_copy(pk, M, C, device) if save or li < len(CONV_IDX) - 1 else None
         call("ensvs_bn_apply_relu", y.data_ptr(), C, M, C, Mg_apply, mean.data_ptr(),
              rstd.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(), out.data_ptr(), C,
-             stream())
+             ptr(out16), C, stream())
         if save:
-            sv.append(dict(y=y, mean=mean, rstd=rstd, out=out, segs=segs, frozen=frozen))
-        a, C_prev = out, C
+            sv.append(dict(y=y, mean=mean, rstd=rstd, out=out, segs=segs, segs16=segs16,
+                           frozen=frozen, out16=out16))
+        a, a16, C_prev = out, out16, C
     return a, sv
 
 
@@ -312,6 +356,7 @@ def conv_bwd(pk, conv, sv, dout, B, T, device, groups=1, first_dx=None):
         C = conv[ci].weight.shape[0]
         bn = conv[bi]
         dy = empty(M, C, device=device)
+        dy16 = None if s.get("frozen") else bf16_copy(pk, M, C, device)
         part = K.scratch(groups * BN_SPLITS * 2 * C, device, key="bn")
         sums = empty(groups * 2 * C, device=device)
         if s.get("frozen"):
@@ -325,20 +370,25 @@ def conv_bwd(pk, conv, sv, dout, B, T, device, groups=1, first_dx=None):
                  s["mean"].data_ptr(), s["rstd"].data_ptr(), bn.weight.data_ptr(),
                  bn.bias.data_ptr(), part.data_ptr(), BN_SPLITS, sums.data_ptr(),
                  grad_of(bn.weight).data_ptr(), grad_of(bn.bias).data_ptr(), dy.data_ptr(), C,
-                 stream())
+                 ptr(dy16), C, stream())
         _dbg(f"conv{li}.dout", d)
         _dbg(f"conv{li}.dy", dy)
         colsum_into(dy, C, M, C, conv[ci].bias)
         w = conv[ci].weight
         col = 0
-        for seg in s["segs"]:
-            wgrad_into(w, dy, C, seg.x, seg.ld, B, T, T, C, seg.K, taps=7, dil=1, shift0=-3,
-                       pad=_lib.PAD_REFLECT, col0=col, xoff=seg.xoff)
+        for seg, seg16 in zip(s["segs"], s.get("segs16") or [None] * len(s["segs"])):
+            if dy16 is not None and seg16 is not None:
+                wgrad_into(w, dy16, C, seg16[0], seg16[1], B, T, T, C, seg.K, taps=7, dil=1,
+                           shift0=-3, pad=_lib.PAD_REFLECT, col0=col)
+            else:
+                wgrad_into(w, dy, C, seg.x, seg.ld, B, T, T, C, seg.K, taps=7, dil=1, shift0=-3,
+                           pad=_lib.PAD_REFLECT, col0=col, xoff=seg.xoff)
             col += seg.K
+        dyo = dy if dy16 is None else dy16
         if li > 0:
             Cin = w.shape[1]
             dxp = empty(B * (T + 6), Cin, device=device)
-            K.gemm([K.Seg(dy, C, C, pk[f"conv{ci}^T"], T, taps=7, dil=1, shift0=-6)], B, T + 6,
+            K.gemm([K.Seg(dyo, C, C, pk[f"conv{ci}^T"], T, taps=7, dil=1, shift0=-6)], B, T + 6,
                    Cin, pk.bwd, dxp, Cin)
             dprev = empty(M, Cin, device=device)
             call("ensvs_reflect_fold", dxp.data_ptr(), B, T, 3, Cin, dprev.data_ptr(), stream())
@@ -347,8 +397,8 @@ def conv_bwd(pk, conv, sv, dout, B, T, device, groups=1, first_dx=None):
             for (name, Kc) in (first_dx or []):
                 ref = pk[f"conv{ci}@{name}^T"] if name else pk[f"conv{ci}^T"]
                 dxp = empty(B * (T + 6), Kc, device=device)
-                K.gemm([K.Seg(dy, C, C, ref, T, taps=7, dil=1, shift0=-6)], B, T + 6, Kc, pk.bwd,
-                       dxp, Kc)
+                K.gemm([K.Seg(dyo, C, C, ref, T, taps=7, dil=1, shift0=-6)], B, T + 6, Kc,
+                       pk.bwd, dxp, Kc)
                 dx = empty(M, Kc, device=device)
                 call("ensvs_reflect_fold", dxp.data_ptr(), B, T, 3, Kc, dx.data_ptr(), stream())
                 res.append(dx)
@@ -472,26 +522,28 @@ def _coop_work(H, device):
     return empty(n, device=device, dtype=torch.uint8), n
 
 
-def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=True):
-    """Packed bidirectional multi-layer LSTM.  Returns (Y (M, 2H), saved list)."""
+def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=True,
+             x16=None):
+    """Packed bidirectional multi-layer LSTM.  Returns (Y (M, 2H), saved list).  x16: an
+    optional bf16 copy of X (row stride = the input width) from its producer."""
     M = B * T
     H = lstm.hidden_size
     sv = []
     h, ldh = X, ldx
-    h16 = None  # bf16 copy of h (the previous layer's output straight from its recurrence)
+    h16 = x16  # bf16 copy of h (the producer's, or the previous layer's recurrence output)
     for l in range(lstm.num_layers):
         Kc = getattr(lstm, f"weight_ih_l{l}").shape[1]
         HP = lstm_pad(H)
         # MFMA recurrences on unpadded H: the layer input and output also kept as bf16 for
         # the backward's bf16-operand GEMMs (the same roundings those GEMMs apply to fp32)
-        direct = not lstm_coop(B, H) and not HP and lstm_mfma(H)
+        direct = BF16_COPIES["on"] and not lstm_coop(B, H) and not HP and lstm_mfma(H)
         x16 = None
         if direct:
             if h16 is not None:
                 x16 = h16
             elif Kc % 8 == 0 and K._castable(K.Seg(h, ldh, Kc, None, T)):
                 x16 = K.cast_bf16(h, ldh, Kc, M)
-        xa, lda = (x16, Kc if h16 is None else 2 * H) if x16 is not None else (h, ldh)
+        xa, lda = (x16, Kc) if x16 is not None else (h, ldh)
         gx = empty(M, 8 * H, device=device)
         if lstm_fused_proj(H):
             assert pk[f"b{l}_reverse"].offset == pk[f"b{l}"].offset + 4 * H
@@ -528,7 +580,7 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
                      stream())
             _regroup(yp, 2 * HP, y, 2 * H, M, 2, HP, H)
             del gxp, yp
-        elif direct:
+        elif lstm_mfma(H):
             call("ensvs_lstm_mfma_fwd", gx.data_ptr(), 8 * H, _mfma_pack(lstm, l, False).data_ptr(),
                  lens_dev.data_ptr(), B, T, H, y.data_ptr(), 2 * H, saved.data_ptr(),
                  ptr(y16), 2 * H, stream())

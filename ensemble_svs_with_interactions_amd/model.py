@@ -156,22 +156,25 @@ class FFConvLSTM(BaseModel):
             if spk_seq is not None:
                 raise NotImplementedError("FFConvLSTM(embed_dim=None) with spk_embs")
             X0, esv = _plain_input(sources, self.in_dim, B * T, dev), None
-        hs = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
+        hs, hs16 = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
         F = hs[2].shape[1]
         a, csv = Ly.conv_fwd(pk, self.conv, [("", hs[2], F, F, 0)], B, T, dev, training,
-                             save=save, running_updates=bn_updates)
+                             save=save, running_updates=bn_updates,
+                             first_b16=None if hs16[2] is None else [("", hs16[2], F, F)])
         if training and self.lstm.dropout > 0 and lstm_masks is None:
             lstm_masks = [Ly.dropout_mask(B * T * 2 * self.lstm.hidden_size, self.lstm.dropout,
                                           dev)
                           for _ in range(self.lstm.num_layers - 1)]
         C = a.shape[1]
         y, lsv = Ly.lstm_fwd(pk, self.lstm, a, C, B, T, lens_dev, dev,
-                             lstm_masks if training else None, save=save)
+                             lstm_masks if training else None, save=save,
+                             x16=csv[-1]["out16"] if csv else None)
         out = empty(B * T, self.out_dim, device=dev)
         H2 = 2 * self.lstm.hidden_size
         Ly.K.gemm([Ly.K.Seg(y, H2, H2, pk["fc"], T)], B, T, self.out_dim, pk.fwd, out,
                   self.out_dim, **pk.bias_ptr_args("fc.b"))
-        st = dict(X0=X0, esv=esv, hs=hs, csv=csv, lsv=lsv, y=y, B=B, T=T, lens=lens_dev) \
+        st = dict(X0=X0, esv=esv, hs=hs, hs16=hs16, csv=csv, lsv=lsv, y=y, B=B, T=T,
+                  lens=lens_dev) \
             if save else None
         return out, st
 
@@ -191,7 +194,7 @@ class FFConvLSTM(BaseModel):
         da = Ly.lstm_bwd(pk, self.lstm, st["lsv"], dy, B, T, st["lens"], dev)
         F = st["hs"][2].shape[1]
         (dh3,) = Ly.conv_bwd(pk, self.conv, st["csv"], da, B, T, dev, first_dx=[("", F)])
-        dX0 = Ly.ff_bwd(pk, self.ff, st["X0"], st["hs"], dh3, B, T, dev)
+        dX0 = Ly.ff_bwd(pk, self.ff, st["X0"], st["hs"], st["hs16"], dh3, B, T, dev)
         dspk = None
         if self.embed_dim is None:
             return dX0, None

@@ -303,7 +303,7 @@ class _MdnModelFn(torch.autograd.Function):
         for li in reversed(range(len(lins))):
             i, m = lins[li]
             out, inp = hs[li + 1], hs[li]
-            call("ensvs_relu_mask", d.data_ptr(), d.data_ptr(), out.data_ptr(), d.numel(), stream())
+            call("ensvs_relu_mask", d.data_ptr(), None, d.data_ptr(), out.data_ptr(), d.numel(), stream())
             Ly.wgrad_into(m.weight, d, m.out_features, inp, inp.shape[1], B, T, T, m.out_features,
                           m.in_features)
             Ly.colsum_into(d, m.out_features, M, m.out_features, m.bias)
@@ -496,7 +496,7 @@ class _VPFn(torch.autograd.Function):
                  dyx.data_ptr(), stream())
             Ly.colsum_into(dyx, H, M, H, ln.weight)
             Ly.colsum_into(d, H, M, H, ln.bias)
-            call("ensvs_relu_mask", dyc.data_ptr(), dyc.data_ptr(), yc.data_ptr(), M * H, stream())
+            call("ensvs_relu_mask", dyc.data_ptr(), None, dyc.data_ptr(), yc.data_ptr(), M * H, stream())
             Ly.colsum_into(dyc, H, M, H, conv.bias)
             Ly.wgrad_into(conv.weight, dyc, H, hin, ldh, B, T, T, H, Kin, taps=k_, shift0=sh)
             if i > 0:

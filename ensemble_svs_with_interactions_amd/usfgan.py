@@ -553,7 +553,7 @@ class ParallelHnUSFGANGenerator(nn.Module):
         outs = [self._conv_last(P, x, B, L, dev)]
         for t in (s, h, n):
             tr = empty(M, R, device=dev)
-            call("ensvs_relu_mask", tr.data_ptr(), t.data_ptr(), t.data_ptr(), M * R, stream())
+            call("ensvs_relu_mask", tr.data_ptr(), None, t.data_ptr(), t.data_ptr(), M * R, stream())
             outs.append(self._conv_last(P, tr, B, L, dev))
         return outs + [a]
 

@@ -291,13 +291,17 @@ int ensvs_gather_rows(const float* table, const long long* idx, int B, int C, fl
  * apply+ReLU, and backward (+ReLU).  Groups of Mg rows keep separate statistics. */
 int ensvs_bn_finalize(float* mean, float* var, int G, int C, long long Mg, float eps, float* rstd,
                       float* rmean, float* rvar, float momentum, int update, void* stream);
+/* outb / dyb (optional, bf16, 8-B aligned rows, ld % 4 == 0; C % 4 == 0 and 16-B aligned fp32
+ * operands, else ENSVS_E_ARG): the output / input gradient also rounded to bf16 for the
+ * next convolution's bf16-operand GEMMs (forward input, dgrad, weight gradient). */
 int ensvs_bn_apply_relu(const float* y, int ldy, long long M, int C, long long Mg,
                         const float* mean, const float* rstd, const float* gamma,
-                        const float* beta, float* out, int ldo, void* stream);
+                        const float* beta, float* out, int ldo, void* outb, int ldob,
+                        void* stream);
 int ensvs_bn_bwd(const float* dout, int ldd, const float* y, int ldy, long long M, int C,
                  long long Mg, const float* mean, const float* rstd, const float* gamma,
                  const float* beta, float* part, int max_splits, float* sums, float* dgamma,
-                 float* dbeta, float* dy, int lddy, void* stream);
+                 float* dbeta, float* dy, int lddy, void* dyb, int lddyb, void* stream);
 /* BatchNorm1d in eval mode inside a training step (model.train() + bn.eval(): frozen running
  * statistics; the data-parallel parity definition, SURVEY 8(e), train_util.py:1176-1182):
  * dgamma/dbeta accumulate, dy = gamma * rstd * dout * (z > 0). */
@@ -391,8 +395,10 @@ int ensvs_axpby_to_bf16(float* out, void* outb, const float* y, float a, const f
                         long long n, void* stream);
 int ensvs_mul(float* y, const float* x, long long n, void* stream);
 int ensvs_mul_out(float* out, const float* a, const float* b, long long n, void* stream);
-/* out = act > 0 ? dy : 0 (ReLU backward; out may alias dy) */
-int ensvs_relu_mask(float* out, const float* dy, const float* act, long long n, void* stream);
+/* out = act > 0 ? dy : 0 (ReLU backward; out may alias dy); outb (optional, bf16): its copy
+ * for the bf16-operand GEMMs (n % 4 == 0, 16-B aligned fp32 pointers, 8-B aligned outb) */
+int ensvs_relu_mask(float* out, void* outb, const float* dy, const float* act, long long n,
+                    void* stream);
 /* Gradient of ReflectionPad1d(pad) (model.py:846-859): dx[b][t] from dxp[b][T+2pad]. */
 int ensvs_reflect_fold(const float* dxp, int B, int T, int pad, int C, float* dx, void* stream);
 /* Counter-based RNG (stateless hash of (seed, index)): N(0,1), keep-masks scaled by

@@ -62,7 +62,9 @@ def call(name, *args):
     e.record()
     tag = TAG[0]
     if name in ("ensvs_lstm_mfma_fwd", "ensvs_lstm_mfma_bwd"):
-        t = f"H={args[6]} T={args[5]}"
+        tag = f"H={args[6]} T={args[5]}"
+    elif name == "ensvs_colsum":
+        tag = f"M={args[2]} groups={args[3]} N={args[4]}{' centred' if args[5] else ''}"
     elif name in ("ensvs_lstm_fwd", "ensvs_lstm_bwd"):
         tag = f"H={args[7]} B={args[5]} T={args[6]}"
     elif name in ("ensvs_lstm_coop_fwd", "ensvs_lstm_coop_bwd"):

@@ -426,11 +426,13 @@ __device__ __forceinline__ void gen_load(const GemmArgs& a, int m, int col, bool
   }
 }
 
-template <int NT = NTHR, int EB = 1>
+// MASK: the epilogues an instance may meet (bit e: a.epi == e), the others compiled out
+template <int NT = NTHR, int EB = 1, unsigned MASK = ~0u>
 __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[4][4], int m0,
                                                   int n0, int wr, int wc, int lane, int tid,
                                                   char* smem, bool write_acc = true) {
-  if (a.epi == EPI_NONE) {
+  auto ep = [&](int e) { return ((MASK >> e) & 1u) && a.epi == e; };
+  if (ep(EPI_NONE)) {
     if (write_acc) gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
     return;
   }
@@ -455,11 +457,11 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
   // gate/filter save) are issued before its first store: with the loads after the stores
   // the compiler cannot reorder them (possible aliasing) and each row paid a full L2 / HBM
   // latency -- 12 of 18 us of a 2 000-row GEMM (tools/small_gemm_probe.py).
-  if (a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS)) {
+  if (a.gate8 && (ep(EPI_GATE) || ep(EPI_GATE_TS))) {
     gate_tile8<NT, BM, 8>(a, T, EP, m0, n0, tid);  // 64 channels per row: 8 threads
     return;
   }
-  if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) {
+  if (ep(EPI_GATE) || ep(EPI_RESSKIP) || ep(EPI_GATE_TS)) {
     // this tile holds 64 output channels (gate/filter interleaved by 16 in the packed columns)
     constexpr int NI = BM * 16 / NT;
     const int q4 = tid & 15, q = q4 >> 2, j = (q4 & 3) * 4;
@@ -473,13 +475,13 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
     }
     static_assert(NI % EB == 0, "rows per thread in batches of EB");
     RsOps cur[EB], nxt[EB];
-    if (a.epi == EPI_RESSKIP) {
+    if (ep(EPI_RESSKIP)) {
 #pragma unroll
       for (int k = 0; k < EB; ++k) rs_load(a, m0 + (tid >> 4) + k * (NT / 16), c, cur[k]);
     }
 #pragma unroll 1
     for (int kb = 0; kb < NI; kb += EB) {
-    if (a.epi == EPI_RESSKIP && kb + EB < NI) {
+    if (ep(EPI_RESSKIP) && kb + EB < NI) {
 #pragma unroll
       for (int k = 0; k < EB; ++k)
         rs_load(a, m0 + (tid >> 4) + (kb + EB + k) * (NT / 16), c, nxt[k]);
@@ -494,9 +496,9 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         g += bg;
         f += bfl;
       }
-      if (a.epi == EPI_RESSKIP) {
+      if (ep(EPI_RESSKIP)) {
         rs_store(a, m, c, g, f, cur[k]);
-      } else if (a.epi == EPI_GATE) {
+      } else if (ep(EPI_GATE)) {
         st4_aux0(a, (long long)m * a.ld0 + c, g);
         st4_aux0(a, (long long)m * a.ld0 + a.C + c, f);
         f32x4 z;
@@ -504,7 +506,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         for (int e = 0; e < 4; ++e) z[e] = fsigmoid_(g[e]) * ftanh_(f[e]);
         if (a.Y) st4(a.Y + (long long)m * a.ldy + c, z);
         shadow4(a, m, c, z);
-      } else if (a.epi == EPI_GATE_TS) {
+      } else if (ep(EPI_GATE_TS)) {
         f32x4 z;
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = ftanh_(g[e]) * fsigmoid_(f[e]);
@@ -529,9 +531,9 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
       for (int e = 0; e < 4; ++e)
         if (e < ne) bv[e] = a.bias[col + e];
     }
-    const bool want1 = (a.epi == EPI_PLAIN && a.accum) || a.epi == EPI_ADDSCALE ||
-                       a.epi == EPI_RELU_MASK || a.epi == EPI_GATE_BWD;
-    const bool want2 = (a.epi == EPI_RELU_MASK && a.accum) || a.epi == EPI_GATE_BWD;
+    const bool want1 = (ep(EPI_PLAIN) && a.accum) || ep(EPI_ADDSCALE) ||
+                       ep(EPI_RELU_MASK) || ep(EPI_GATE_BWD);
+    const bool want2 = (ep(EPI_RELU_MASK) && a.accum) || ep(EPI_GATE_BWD);
     static_assert(NI % EB == 0, "rows per thread in batches of EB");
     // operands of a batch of rows, loaded before the previous batch's stores
     const bool wl = ne == 4 && (want1 || want2);
@@ -558,7 +560,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
       if (a.bias) v += bv;
       float* y = a.Y + (long long)m * a.ldy + col;
       if (ne == 4) {
-        if (a.epi == EPI_PLAIN) {
+        if (ep(EPI_PLAIN)) {
           if (a.accum) v += p1[k];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -567,7 +569,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
           }
           st4(y, v);
           shadow4(a, m, col, v);
-        } else if (a.epi == EPI_ADDSCALE) {
+        } else if (ep(EPI_ADDSCALE)) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             v[e] = __builtin_fmaf(a.alpha, p1[k][e], v[e]);
@@ -575,13 +577,13 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
           }
           st4(y, v);
           shadow4(a, m, col, v);
-        } else if (a.epi == EPI_RELU_MASK) {
+        } else if (ep(EPI_RELU_MASK)) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = p1[k][e] > 0.f ? v[e] : 0.f;
           if (a.accum) v += p2[k];
           st4(y, v);
           shadow4(a, m, col, v);
-        } else if (a.epi == EPI_GATE_BWD) {
+        } else if (ep(EPI_GATE_BWD)) {
           f32x4 dg, df;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -605,18 +607,18 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
         for (int e = 0; e < ne; ++e) {
           float w = v[e];
           float* ye = y + e;
-          if (a.epi == EPI_PLAIN) {
+          if (ep(EPI_PLAIN)) {
             if (a.accum) w += *ye;
             if (a.relu == 1) w = fmaxf(w, 0.f);
             else if (a.relu == 2) w = sigmoidf_(w);
             *ye = w;
-          } else if (a.epi == EPI_ADDSCALE) {
+          } else if (ep(EPI_ADDSCALE)) {
             w = __builtin_fmaf(a.alpha, a.aux1[(long long)m * a.ld1 + col + e], w);
             *ye = a.relu == 1 ? fmaxf(w, 0.f) : w;
-          } else if (a.epi == EPI_RELU_MASK) {
+          } else if (ep(EPI_RELU_MASK)) {
             w = a.aux1[(long long)m * a.ld1 + col + e] > 0.f ? w : 0.f;
             *ye = a.accum ? *ye + w : w;
-          } else if (a.epi == EPI_GATE_BWD) {
+          } else if (ep(EPI_GATE_BWD)) {
             const float g = ld_aux1(a, (long long)m * a.ld1 + col + e);
             const float f = ld_aux1(a, (long long)m * a.ld1 + a.C + col + e);
             gate_bwd_(w, g, f, ye[0], ye[a.C]);
@@ -638,7 +640,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& a, f32x4 (&acc
     *(f32x4*)(X + g * 2 * BN + BN + c4) = cs1;
     __syncthreads();
     const int j = tid;  // NTHR == 2 * BN: first BN the accumulator / d(gate), then d(filter)
-    const bool bwd = a.epi == EPI_GATE_BWD;
+    const bool bwd = ep(EPI_GATE_BWD);
     if (j < BN || bwd) {
       const int c = n0 + (j & (BN - 1));
       if (c < a.N) {
@@ -963,7 +965,12 @@ __device__ __forceinline__ void usf_block_tail(const GemmArgs& a, const GemmArgs
 // (162 VGPRs; 4 spills 124 B) and takes the C = 256 gate-backward dgrad from 51.4 to 47.5 us
 constexpr int GBW_EB = 2;
 
-template <int STAGES, bool FUSE>
+// EPK = 1: the instance launched for the RESSKIP / ADDSCALE epilogues (the DiffNet residual /
+// skip update and the dilated-conv dgrad), whose epilogues also batch 2 rows of operands
+// (res/skip 46.0 -> 39.4 us, dilated dgrad 59.8 -> 56.5 us at M = 30 720, C = 256): a
+// separate instance because the shared one then allocates 168 VGPRs and its GATE_BWD
+// launches slow down (48.2 -> 50.5 us).
+template <int STAGES, bool FUSE, int EPK = 0>
 
 __device__ __forceinline__ void b16_body(const GemmArgs& a, const GemmArgs& a2) {
   static_assert(STAGES >= 2 && STAGES <= 3, "stages");
@@ -1125,7 +1132,10 @@ __device__ __forceinline__ void b16_body(const GemmArgs& a, const GemmArgs& a2) 
     return;
   }
   if (a.vec_out) {
-    if (GBW_EB > 1 && a.epi == EPI_GATE_BWD)
+    if (EPK == 1)
+      gemm_epilogue_lds<NTHR, GBW_EB, (1u << EPI_RESSKIP) | (1u << EPI_ADDSCALE)>(
+          a, acc, m0, n0, wr, wc, lane, tid, smem);
+    else if (GBW_EB > 1 && a.epi == EPI_GATE_BWD)
       gemm_epilogue_lds<NTHR, GBW_EB>(a, acc, m0, n0, wr, wc, lane, tid, smem);
     else
       gemm_epilogue_lds(a, acc, m0, n0, wr, wc, lane, tid, smem);
@@ -1133,9 +1143,9 @@ __device__ __forceinline__ void b16_body(const GemmArgs& a, const GemmArgs& a2) 
   else gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
 }
 
-template <int STAGES>
+template <int STAGES, int EPK = 0>
 __global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a) {
-  b16_body<STAGES, false>(a, a);
+  b16_body<STAGES, false, EPK>(a, a);
 }
 
 __global__ __launch_bounds__(NTHR, 2) void usf_block_kernel(const GemmArgs a, const GemmArgs a2) {
@@ -3123,7 +3133,14 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     ENSVS_CHECK_LAUNCH();
     return ENSVS_OK;
   }
-  if (stages == 2) {
+  if (stages == 2 && a.ksplit <= 1 && a.vec_out &&
+      (a.epi == EPI_RESSKIP || a.epi == EPI_ADDSCALE)) {
+    static const hipError_t e2s = hipFuncSetAttribute((const void*)conv_gemm_b16_kernel<2, 1>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      (int)l2);
+    if (e2s != hipSuccess) return ENSVS_E_HIP;
+    hipLaunchKernelGGL((conv_gemm_b16_kernel<2, 1>), grid, dim3(NTHR), l2, st, a);
+  } else if (stages == 2) {
     static const hipError_t e2 = hipFuncSetAttribute((const void*)conv_gemm_b16_kernel<2>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                                      (int)l2);

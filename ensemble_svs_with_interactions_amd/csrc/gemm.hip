@@ -965,12 +965,15 @@ __device__ __forceinline__ void usf_block_tail(const GemmArgs& a, const GemmArgs
 // (162 VGPRs; 4 spills 124 B) and takes the C = 256 gate-backward dgrad from 51.4 to 47.5 us
 constexpr int GBW_EB = 2;
 
-// EPK = 1: the instance launched for the RESSKIP / ADDSCALE epilogues (the DiffNet residual /
-// skip update and the dilated-conv dgrad), whose epilogues also batch 2 rows of operands
-// (res/skip 46.0 -> 39.4 us, dilated dgrad 59.8 -> 56.5 us at M = 30 720, C = 256): a
-// separate instance because the shared one then allocates 168 VGPRs and its GATE_BWD
-// launches slow down (48.2 -> 50.5 us).
-template <int STAGES, bool FUSE, int EPK = 0>
+// EPK = EPI_RESSKIP / EPI_ADDSCALE: an instance compiled for that epilogue alone, its
+// operands EB_* rows per batch (the DiffNet residual / skip update and the dilated-conv
+// dgrad).  Batching 2 rows in the shared instance took it to 168 VGPRs and slowed its
+// GATE_BWD launches (48.2 -> 50.5 us); one instance per epilogue keeps each one's registers
+// to what it uses: res/skip 46.0 -> 38.9 us (2 rows; 144-151 VGPRs, no scratch), dilated
+// dgrad 59.8 -> 48.9 us (4 rows) at M = 30 720, C = 256.  GATE_BWD stays in the shared
+// instance: its own (2 rows, 166 VGPRs) measured 47.8 us and +0.08 ms/step, 4 rows spill.
+constexpr int EB_RS = 2, EB_AS = 4;
+template <int STAGES, bool FUSE, int EPK = -1>
 
 __device__ __forceinline__ void b16_body(const GemmArgs& a, const GemmArgs& a2) {
   static_assert(STAGES >= 2 && STAGES <= 3, "stages");
@@ -1132,9 +1135,10 @@ __device__ __forceinline__ void b16_body(const GemmArgs& a, const GemmArgs& a2) 
     return;
   }
   if (a.vec_out) {
-    if (EPK == 1)
-      gemm_epilogue_lds<NTHR, GBW_EB, (1u << EPI_RESSKIP) | (1u << EPI_ADDSCALE)>(
-          a, acc, m0, n0, wr, wc, lane, tid, smem);
+    if (EPK == EPI_RESSKIP)
+      gemm_epilogue_lds<NTHR, EB_RS, 1u << EPI_RESSKIP>(a, acc, m0, n0, wr, wc, lane, tid, smem);
+    else if (EPK == EPI_ADDSCALE)
+      gemm_epilogue_lds<NTHR, EB_AS, 1u << EPI_ADDSCALE>(a, acc, m0, n0, wr, wc, lane, tid, smem);
     else if (GBW_EB > 1 && a.epi == EPI_GATE_BWD)
       gemm_epilogue_lds<NTHR, GBW_EB>(a, acc, m0, n0, wr, wc, lane, tid, smem);
     else
@@ -1143,7 +1147,7 @@ __device__ __forceinline__ void b16_body(const GemmArgs& a, const GemmArgs& a2) 
   else gemm_epilogue(a, acc, m0, n0, wr, wc, lane);
 }
 
-template <int STAGES, int EPK = 0>
+template <int STAGES, int EPK = -1>
 __global__ __launch_bounds__(NTHR, 3) void conv_gemm_b16_kernel(const GemmArgs a) {
   b16_body<STAGES, false, EPK>(a, a);
 }
@@ -3133,13 +3137,19 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     ENSVS_CHECK_LAUNCH();
     return ENSVS_OK;
   }
-  if (stages == 2 && a.ksplit <= 1 && a.vec_out &&
-      (a.epi == EPI_RESSKIP || a.epi == EPI_ADDSCALE)) {
-    static const hipError_t e2s = hipFuncSetAttribute((const void*)conv_gemm_b16_kernel<2, 1>,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                      (int)l2);
-    if (e2s != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL((conv_gemm_b16_kernel<2, 1>), grid, dim3(NTHR), l2, st, a);
+  const bool spec = stages == 2 && a.ksplit <= 1 && a.vec_out;
+#define SPEC(E)                                                                                \
+  do {                                                                                         \
+    static const hipError_t es = hipFuncSetAttribute((const void*)conv_gemm_b16_kernel<2, E>, \
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                                     (int)l2);                                 \
+    if (es != hipSuccess) return ENSVS_E_HIP;                                                  \
+    hipLaunchKernelGGL((conv_gemm_b16_kernel<2, E>), grid, dim3(NTHR), l2, st, a);             \
+  } while (0)
+  if (spec && a.epi == EPI_RESSKIP) {
+    SPEC(EPI_RESSKIP);
+  } else if (spec && a.epi == EPI_ADDSCALE) {
+    SPEC(EPI_ADDSCALE);
   } else if (stages == 2) {
     static const hipError_t e2 = hipFuncSetAttribute((const void*)conv_gemm_b16_kernel<2>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3155,6 +3165,7 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
   } else {
     return ENSVS_E_ARG;
   }
+#undef SPEC
   ENSVS_CHECK_LAUNCH();
   if (a.ksplit > 1) {
     const size_t le = (size_t)CHR * EPB * 4;

@@ -10,21 +10,24 @@
 // matrix cores instead of fp32 VALU FMAs.  lstm.hip's steps are bound by that VALU work and its
 // LDS operand traffic (H = 128: 0.76 / 1.19 us forward / backward, 128 FMAs and 64 LDS floats
 // per lane per step).  Here the workgroup's 4 waves hold the direction's W_hh as fp16 (forward:
-// h in [-1, 1]) / bf16 (backward, W_hh^T: dG spans many decades) MFMA fragments in VGPRs --
-// as the reference recipe's fp16 autocast runs its cuDNN LSTM (myconfig_notuseIL.yaml:6) --
-// and every MFMA column reads the same h / dG vector (an LDS broadcast), so the 16 columns of
-// each 16 x 16 result are identical and lane n of a 16-lane row takes tile n's values: one cell
-// per lane, no cross-lane reduction.  Gates, cell state, saved values and outputs stay fp32;
+// h in [-1, 1]) / bf16 (backward, W_hh^T: dG spans many decades) MFMA B-operand fragments in
+// VGPRs -- as the reference recipe's fp16 autocast runs its cuDNN LSTM (myconfig_notuseIL.yaml:6)
+// -- and the A operand is the h / dG vector in every row (an LDS broadcast), so the 16 rows of
+// each 16 x 16 result are identical and result column n, which lane n of every 16-lane row
+// holds, is one gate row's product: the lane owns a cell's values straight from the MFMA, no
+// cross-lane reduction and no selection among tiles (the transposed layout, with W as A and h
+// in every column, left each lane choosing its cell among H/16 tiles: H = 128 forward 768 ->
+// see DESIGN.md §3 for the per-step times).  Gates, cell state, saved values and outputs stay fp32;
 // the fp32 parity mode keeps lstm.hip's exact kernels.  One sequence per workgroup keeps each
 // CU's global traffic at lstm.hip's (a batched layout with 4-16 sequences per workgroup was
 // bound by the per-CU store/load issue rate: profiles/r3_lstm_batch_bench.txt).
 //
-// Forward: wave v owns units [v H/4, (v+1) H/4) = NMT = H/16 tiles of 16 gate rows; row m of
-// tile mt is gate m % 4 of unit v H/4 + (m / 4) NMT + mt, so lane (lg = lane / 16, n) holds the
-// four gates of unit v H/4 + lg NMT + mt in tile mt's result and applies the cell of
-// mt = n (n < NMT).  Backward: dh = W_hh^T dG, units as M (TPW = H/64 tiles per wave), K = 4H in
-// the exchange order n' = 4 unit + gate; lane (lg, n) applies the cell of unit
-// v H/4 + lg 4 TPW + n (n < 4 TPW), taken from tile n / 4, row n % 4.
+// Forward: wave v owns units [v H/4, (v+1) H/4) in NUG = H/64 groups of 16; N tile t = 4 ug + g
+// holds gate g of unit group ug (column n: unit v H/4 + 16 ug + n), so lane (lg = lane / 16, n)
+// of unit group ug = lg / 2 (H = 128; 0 for H = 64) reads its four gates from tiles 4 ug + g.
+// Backward: dh = W_hh^T dG with the units as N (TPW = H/64 tiles of 16 per wave) and K = 4H in
+// the exchange order n' = 4 unit + gate; lane (lg, n) of tile lg / 2 (H = 128) applies the cell
+// of unit v H/4 + 16 (lg / 2) + n.  Lanes of the other row groups hold copies and do not write.
 #include "coop.h"
 #include "ensvs.h"
 
@@ -51,8 +54,8 @@ template <int H> struct MGeo {
 };
 
 // ---------------------------------------------------------------------------------- packs
-// forward fragments [dir][v][mt][kk][lane][8] fp16: A[m][k] = W_hh[g H + unit][k], m = lane & 15,
-// unit = v H/4 + (m / 4) NMT + mt, g = m % 4, k = 32 kk + 8 (lane / 16) + e
+// forward B fragments [dir][v][t][kk][lane][8] fp16: B[k][n] = W_hh[g H + unit][k], n = lane & 15,
+// unit = v H/4 + 16 (t / 4) + n, g = t % 4, k = 32 kk + 8 (lane / 16) + e
 template <int H>
 __global__ void mfma_pack_fwd_kernel(const float* __restrict__ w0, const float* __restrict__ w1,
                                      _Float16* __restrict__ out) {
@@ -62,17 +65,16 @@ __global__ void mfma_pack_fwd_kernel(const float* __restrict__ w0, const float* 
     const int e = i & 7, lane = (i >> 3) & 63;
     int r = i >> 9;
     const int kk = r % G::NKC; r /= G::NKC;
-    const int mt = r % G::NMT; r /= G::NMT;
+    const int t = r % G::NMT; r /= G::NMT;
     const int v = r % 4, d = r / 4;
-    const int m = lane & 15;
-    const int unit = v * G::UPW + (m >> 2) * G::NMT + mt, g = m & 3;
+    const int unit = v * G::UPW + 16 * (t >> 2) + (lane & 15), g = t & 3;
     const int k = kk * 32 + 8 * (lane >> 4) + e;
     out[i] = (_Float16)(d ? w1 : w0)[(long long)(g * H + unit) * H + k];
   }
 }
 
-// backward fragments of W_hh^T [dir][v][mt][kk][lane][8] bf16: row m = lane & 15 is unit
-// v H/4 + (m / 4) 4 TPW + 4 mt + m % 4; k = n' = 32 kk + 8 (lane / 16) + e in the exchange
+// backward B fragments [dir][v][t][kk][lane][8] bf16: B[k][n] = W_hh[gate row of k][unit], column
+// n = lane & 15 is unit v H/4 + 16 t + n; k = n' = 32 kk + 8 (lane / 16) + e in the exchange
 // order n' = 4 unit' + g (gate row g H + unit')
 template <int H>
 __global__ void mfma_pack_bwd_kernel(const float* __restrict__ w0, const float* __restrict__ w1,
@@ -83,10 +85,9 @@ __global__ void mfma_pack_bwd_kernel(const float* __restrict__ w0, const float* 
     const int e = i & 7, lane = (i >> 3) & 63;
     int r = i >> 9;
     const int kk = r % G::NKB; r /= G::NKB;
-    const int mt = r % G::TPW; r /= G::TPW;
+    const int t = r % G::TPW; r /= G::TPW;
     const int v = r % 4, d = r / 4;
-    const int m = lane & 15;
-    const int unit = v * G::UPW + (m >> 2) * 4 * G::TPW + 4 * mt + (m & 3);
+    const int unit = v * G::UPW + 16 * t + (lane & 15);
     const int np = kk * 32 + 8 * (lane >> 4) + e;
     const int row = (np & 3) * H + (np >> 2);
     out[i] = (__bf16)(d ? w1 : w0)[(long long)row * H + unit];
@@ -94,24 +95,11 @@ __global__ void mfma_pack_bwd_kernel(const float* __restrict__ w0, const float* 
 }
 
 // ---------------------------------------------------------------------------------- helpers
-// b where the mask is set, else a: bit selects (v_bfi), so the compiler does not turn a
+// b where the mask is set, else a: a bit select (v_bfi), so the compiler does not turn a
 // lane-dependent choice between registers into a scratch-indexed load
 __device__ __forceinline__ float bsel(unsigned m, float a, float b) {
   return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, a) & ~m) |
                                        (__builtin_bit_cast(unsigned, b) & m));
-}
-// v[idx] for a lane-dependent idx < N (N = 4 / 8); m[b]: all-ones where bit b of idx is set
-template <int N>
-__device__ __forceinline__ float pick(const float (&v)[N], const unsigned (&m)[3]) {
-  const float a0 = bsel(m[0], v[0], v[1]), a1 = bsel(m[0], v[2], v[3]);
-  const float b0 = bsel(m[1], a0, a1);
-  if constexpr (N == 4) {
-    return b0;
-  } else {
-    static_assert(N == 8, "pick");
-    const float a2 = bsel(m[0], v[4], v[5]), a3 = bsel(m[0], v[6], v[7]);
-    return bsel(m[2], b0, bsel(m[1], a2, a3));
-  }
 }
 
 // ---------------------------------------------------------------------------------- forward
@@ -147,11 +135,13 @@ __global__ __launch_bounds__(NT) void lstm_mfma_fwd_kernel(
       for (int kk = 0; kk < NKC; ++kk) asm volatile("" ::"v"(wf[mt][kk]));
   }
   for (int i = tid; i < 2 * HP; i += NT) hb[i] = (_Float16)0.f;
-  // lane n takes tile n's cell (lanes n >= NMT repeat a tile's cell and do not write)
-  const int sel = n & (NMT - 1);
-  const bool act = n < NMT;
-  const unsigned msk[3] = {(sel & 1) ? ~0u : 0u, (sel & 2) ? ~0u : 0u, (sel & 4) ? ~0u : 0u};
-  const int u = v * G::UPW + lg * NMT + sel;
+  // lane (lg, n) takes unit 16 ug + n of its wave, ug = lg / 2 for two unit groups (H = 128);
+  // the row groups with the same unit hold copies and do not write
+  constexpr int NUG = H / 64;
+  const int ug = NUG == 2 ? (lg >> 1) : 0;
+  const bool act = NUG == 2 ? (lg & 1) == 0 : lg == 0;
+  const unsigned mug = ug ? ~0u : 0u;
+  const int u = v * G::UPW + 16 * ug + n;
   float c = 0.f;
 
   const long long rowb = (long long)b * T;
@@ -218,16 +208,12 @@ __global__ __launch_bounds__(NT) void lstm_mfma_fwd_kernel(
         acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < NKC; ++kk)
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[mt][kk], bf[kk], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kk], wf[mt][kk], acc[mt], 0, 0, 0);
       }
       float a[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float col[NMT];
-#pragma unroll
-        for (int mt = 0; mt < NMT; ++mt) col[mt] = acc[mt][g];
-        a[g] = pick<NMT>(col, msk) + gv[g];
-      }
+      for (int g = 0; g < 4; ++g)
+        a[g] = (NUG == 2 ? bsel(mug, acc[g][0], acc[4 + g][0]) : acc[g][0]) + gv[g];
       const float ig = sigm(a[0]), fg = sigm(a[1]), gg = tanh_fast(a[2]), og = sigm(a[3]);
       c = fg * c + ig * gg;
       const float h = og * tanh_fast(c);
@@ -285,11 +271,12 @@ __global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
       for (int kk = 0; kk < NKB; ++kk) asm volatile("" ::"v"(wb[mt][kk]));
   }
   for (int i = tid; i < 2 * GP; i += NT) gb[i] = (__bf16)0.f;
-  // lane n takes the cell of tile n / 4, row n % 4 (lanes n >= 4 TPW repeat one and do not write)
-  const int sel = n & (4 * TPW - 1);
-  const bool act = n < 4 * TPW;
-  const unsigned msk[3] = {(sel & 1) ? ~0u : 0u, (sel & 2) ? ~0u : 0u, (sel & 4) ? ~0u : 0u};
-  const int u = v * G::UPW + lg * 4 * TPW + sel;
+  // lane (lg, n) takes unit 16 tb + n of its wave, tb = lg / 2 for two tiles (H = 128); the
+  // row groups with the same unit hold copies and do not write
+  const int tb = TPW == 2 ? (lg >> 1) : 0;
+  const bool act = TPW == 2 ? (lg & 1) == 0 : lg == 0;
+  const unsigned mtb = tb ? ~0u : 0u;
+  const int u = v * G::UPW + 16 * tb + n;
 
   const long long rowb = (long long)b * T;
   for (int i = tid; i < (T - L) * GW; i += NT) {
@@ -368,12 +355,9 @@ __global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
         acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < NKB; ++kk)
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[mt][kk], bf[kk], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[kk], wb[mt][kk], acc[mt], 0, 0, 0);
       }
-      float flat[4 * TPW];
-#pragma unroll
-      for (int f = 0; f < 4 * TPW; ++f) flat[f] = acc[f >> 2][f & 3];
-      const float dhr = pick<4 * TPW>(flat, msk);
+      const float dhr = TPW == 2 ? bsel(mtb, acc[0][0], acc[TPW - 1][0]) : acc[0][0];
       const float ig = iv[0], fg = iv[1], gg = iv[2], og = iv[3];
       const float ct = iv[4], dyv = iv[5], cp = iv[6];
       const float dh = dyv + dhr;

@@ -290,10 +290,10 @@ def kernel_rooflines(agg, serial_ms, P, T, C=256, E=256):
                "share_of_serial_step": ms / serial_ms}
         if name.startswith("ensvs_lstm_mfma"):
             # h_{t-1} W_hh^T (fwd) / dG W_hh (bwd) of one sequence-direction as 16x16x32 MFMAs
-            # (4H/16 x H/32 of them, one useful column), spread over the CU's 4 SIMDs
+            # (4H/16 x H/32 of them, one useful row), spread over the CU's 4 SIMDs
             floor_ns = (4 * H // 16) * (H // 32) / CU_MFMA16_PER_S * 1e9
             ent["floor"] = ("MFMA issue of the recurrent product on one CU (one workgroup per "
-                            "sequence-direction; 16x16x32 tiles, one useful column)")
+                            "sequence-direction; 16x16x32 tiles, the h / dG vector in every row: one useful row)")
         elif name.startswith("ensvs_lstm"):
             floor_ns = 4 * H * H / CU_FMA_PER_S * 1e9
             ent["floor"] = ("VALU fp32 FMA issue of the recurrent dot products on one CU "

@@ -293,7 +293,8 @@ def kernel_rooflines(agg, serial_ms, P, T, C=256, E=256):
             # (4H/16 x H/32 of them, one useful row), spread over the CU's 4 SIMDs
             floor_ns = (4 * H // 16) * (H // 32) / CU_MFMA16_PER_S * 1e9
             ent["floor"] = ("MFMA issue of the recurrent product on one CU (one workgroup per "
-                            "sequence-direction; 16x16x32 tiles, the h / dG vector in every row: one useful row)")
+                            "sequence-direction; 16x16x32 tiles, the h / dG vector in every "
+                            "row: one useful row)")
         elif name.startswith("ensvs_lstm"):
             floor_ns = 4 * H * H / CU_FMA_PER_S * 1e9
             ent["floor"] = ("VALU fp32 FMA issue of the recurrent dot products on one CU "

@@ -1,0 +1,26 @@
+"""Interleaved A/B of the step schedule constants (acoustic_models.BRANCH_AFTER /
+EXCL_BRANCHES) on the bench workload (graph replay, 30 x 1024, bf16), fresh model and
+capture per run: python tools/schedule_ab.py -> ms/step per variant, two rounds."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import step_ab  # noqa: E402  (model / graph step runner; importing it runs nothing)
+from ensemble_svs_with_interactions_amd import acoustic_models as AM, engine  # noqa: E402
+
+engine.set_gemm_precision("bf16")
+
+VARIANTS = {
+    "current": ({2: 1}, {0, 1}),
+    "vuv_after_mgc_fwd": ({2: 1, 3: 1}, {0, 1}),
+    "vuv_after_mgc_excl_all": ({2: 1, 3: 1}, {0, 1, 2, 3}),
+    "bap_now_vuv_after_mgc": ({3: 1}, {0, 1}),
+    "vuv_after_bap_fwd": ({2: 1, 3: 2}, {0, 1}),
+    "lf0_bap_vuv_after_mgc": ({0: 1, 2: 1, 3: 1}, {0, 1}),
+}
+for rnd in range(2):
+    for name, (after, excl) in VARIANTS.items():
+        AM.BRANCH_AFTER, AM.EXCL_BRANCHES = dict(after), set(excl)
+        ms, loss = step_ab.run()
+        print(f"{name} round {rnd}: {ms:.3f} ms/step (loss {loss:.6f})", flush=True)
+        step_ab.torch.cuda.empty_cache()

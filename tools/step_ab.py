@@ -33,11 +33,12 @@ def run(steps=20):
     return (time.time() - t0) / steps * 1e3, loss.item()
 
 
-engine.set_gemm_precision("bf16")
-name = sys.argv[1]
-for rnd in range(2):
-    for on in (False, True):
-        SWITCHES[name](on)
-        ms, loss = run()
-        print(f"{name}={int(on)} round {rnd}: {ms:.3f} ms/step (loss {loss:.6f})", flush=True)
-        torch.cuda.empty_cache()
+if __name__ == "__main__":
+    engine.set_gemm_precision("bf16")
+    name = sys.argv[1]
+    for rnd in range(2):
+        for on in (False, True):
+            SWITCHES[name](on)
+            ms, loss = run()
+            print(f"{name}={int(on)} round {rnd}: {ms:.3f} ms/step (loss {loss:.6f})", flush=True)
+            torch.cuda.empty_cache()

@@ -25,15 +25,16 @@ from .model import init_weights
 
 
 
-# Step schedule of the fused branches (0 lf0, 1 mgc, 2 bap, 3 vuv; profiles/r2_schedule_ab.txt).
-# BRANCH_AFTER {branch: branch whose forward must finish first}: the bap branch starts when
-# the mgc forward ends, so mgc -- the critical branch (13.9 ms alone) -- runs its forward
-# beside the latency-bound lf0 / vuv chains only (all at once: 20.9 vs 21.2 ms/step).
+# Step schedule of the fused branches (0 lf0, 1 mgc, 2 bap, 3 vuv; profiles/r2_schedule_ab.txt,
+# tools/schedule_ab.py).  BRANCH_AFTER {branch: earlier-issued branch whose forward must finish
+# first}: the bap and V/UV branches start when the mgc forward ends, so mgc -- the critical
+# branch -- runs its forward beside the lf0 chain only (round 2, bap alone: 20.9 vs 21.2
+# ms/step all at once; round 3, V/UV too: 15.63 vs 15.80 ms/step, all at once 16.14).
 # EXCL_BRANCHES: branches whose recurrence workgroups reserve their CU's LDS (the lf0 and mgc
 # chains; bap / vuv LSTM workgroups share CUs with GEMMs: 20.8 vs 21.0 ms/step).  Not kept:
 # the V/UV backward after the mgc DiffNet backward (24.9 vs 22.2 ms/step: the V/UV
 # recurrences then lengthen the tail instead of filling it).
-BRANCH_AFTER = {2: 1}
+BRANCH_AFTER = {2: 1, 3: 1}
 EXCL_BRANCHES = {0, 1}
 
 

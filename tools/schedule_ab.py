@@ -11,12 +11,11 @@ from ensemble_svs_with_interactions_amd import acoustic_models as AM, engine  # 
 engine.set_gemm_precision("bf16")
 
 VARIANTS = {
-    "current": ({2: 1}, {0, 1}),
-    "vuv_after_mgc_fwd": ({2: 1, 3: 1}, {0, 1}),
+    "bap_after_mgc_fwd": ({2: 1}, {0, 1}),
+    "current": ({2: 1, 3: 1}, {0, 1}),
     "vuv_after_mgc_excl_all": ({2: 1, 3: 1}, {0, 1, 2, 3}),
     "bap_now_vuv_after_mgc": ({3: 1}, {0, 1}),
     "vuv_after_bap_fwd": ({2: 1, 3: 2}, {0, 1}),
-    "lf0_bap_vuv_after_mgc": ({0: 1, 2: 1, 3: 1}, {0, 1}),
 }
 for rnd in range(2):
     for name, (after, excl) in VARIANTS.items():

@@ -50,11 +50,12 @@ SYNTH_POST = dict(frame_period=5, post_filter_type="gv", trajectory_smoothing=Tr
 def _imports():
     """Package imports (they load libensvs.so): only after the launcher decision."""
     global np, torch, configs, data, engine, FusedAdam, GraphedTrainStep, train_step
+    global set_overlap_allreduce
     import numpy as np  # noqa: F811
     import torch  # noqa: F811
     from ensemble_svs_with_interactions_amd import configs, data, engine  # noqa: F811
     from ensemble_svs_with_interactions_amd.train import (FusedAdam, GraphedTrainStep,  # noqa
-                                                          train_step)
+                                                          set_overlap_allreduce, train_step)
 
 
 def launch_ranks(args):
@@ -85,10 +86,13 @@ def parse():
                     help="run the lf0/mgc/bap/vuv branches serially (no side streams)")
     ap.add_argument("--eager", action="store_true",
                     help="issue every kernel from the host each step (no HIP graph replay)")
+    ap.add_argument("--overlap-ddp", action="store_true",
+                    help="with N > 1 ranks, run eager steps whose bucketed all-reduce overlaps "
+                         "the backward (train.BucketedAllReduce) instead of the default: the "
+                         "HIP-graph replay of the N = 1 line with one whole-buffer all-reduce "
+                         "between its two graphs")
     ap.add_argument("--no-overlap-ddp", action="store_true",
-                    help="with N > 1 ranks, replay the HIP graphs with one whole-buffer "
-                         "all-reduce between them instead of the default eager steps whose "
-                         "bucketed all-reduce overlaps the backward (train.BucketedAllReduce)")
+                    help="(the default; kept for old command lines)")
     ap.add_argument("--no-sf0", action="store_true",
                     help="skip the recipe-default (MultiTrackMultistreamSeparateF0) leg")
     ap.add_argument("--no-census", action="store_true",
@@ -697,14 +701,17 @@ def main():
             dist.init_process_group(be)
         world = dist.get_world_size()
         backend = dist.get_backend()
-        # the default data-parallel schedule: eager steps whose bucketed gradient all-reduce
-        # (lf0 / bap / V/UV at their branch end, the mgc DiffNet before the mgc encoder's
-        # backward) overlaps the rest of the backward; the collectives stay out of captured
-        # graphs.  Eager issue and graph replay measured the same at one GPU (the step is
-        # GPU-bound); tests/test_ddp_gpu.py pins the reduced gradient and DP = 1-process
-        # full batch.  --no-overlap-ddp: graph replay + one 94 MB all-reduce between graphs
-        if not args.no_overlap_ddp:
+        # the default data-parallel schedule: the N = 1 line's HIP-graph replay with one
+        # 94 MB all-reduce of the flat gradient between the grads and update graphs (gloo
+        # rehearsal, 2 ranks on one GPU: 62 ms/step, profiles/r4_bench_gloo2.json).
+        # --overlap-ddp: eager steps whose bucketed all-reduce (lf0 / bap / V/UV at their
+        # branch end, the mgc DiffNet before the mgc encoder's backward) overlaps the rest of
+        # the backward (same rehearsal: 2.65 s/step -- see DESIGN.md section 6); --eager
+        # alone: eager steps with the one all-reduce after the backward.
+        if args.overlap_ddp:
             args.eager = True
+        else:
+            set_overlap_allreduce(False)
     engine.set_gemm_precision(args.precision)
     engine.set_concurrency(not args.serial)
     torch.manual_seed(20250321)
@@ -794,8 +801,10 @@ def main():
                    "process_group": {"backend": backend, "world_size": world} if world > 1
                    else None,
                    "execution": ("eager, bucketed all-reduce overlapped with the backward"
-                                 if world > 1 and args.eager else
-                                 "eager" if args.eager else "hip-graph replay")},
+                                 if world > 1 and args.overlap_ddp else
+                                 "eager" if args.eager else "hip-graph replay") +
+                                (", one whole-buffer all-reduce per step" if world > 1 and
+                                 not args.overlap_ddp else "")},
         "train_loss": loss_v, "grad_norm": norm_v,
         # reference-equivalent work (the oracle's flop count); the path skips the sub-track
         # lf0 BiLSTM + AR decoder forward, whose output the plain recipe never reads

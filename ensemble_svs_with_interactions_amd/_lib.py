@@ -5,13 +5,33 @@ be loaded, importing anything that launches a kernel raises immediately.
 """
 import ctypes
 import os
+import sys
+import warnings
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # The training step runs its branches on concurrent HIP streams (engine.Branches).  With
 # HIP's default 4 hardware queues per process the step's streams share queues; 8 measured
 # 20.6 vs 21.0-21.4 ms per 30 x 1024 step (16: 22.8).  Only takes effect when the HIP
 # runtime is not initialised yet; an explicit GPU_MAX_HW_QUEUES wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+HW_QUEUES = "8"
+
+
+def _set_hw_queues():
+    if "GPU_MAX_HW_QUEUES" in os.environ:
+        return
+    os.environ["GPU_MAX_HW_QUEUES"] = HW_QUEUES
+    torch = sys.modules.get("torch")
+    cuda = getattr(torch, "cuda", None) if torch is not None else None
+    if cuda is not None and cuda.is_initialized():
+        warnings.warn(
+            "ensvs: the HIP runtime was initialised before ensemble_svs_with_interactions_amd "
+            f"was imported, so GPU_MAX_HW_QUEUES={HW_QUEUES} does not apply (HIP keeps its "
+            "default 4 hardware queues; the concurrent branch schedule measured slower with "
+            "4).  Import the package, or export GPU_MAX_HW_QUEUES, before the first CUDA call.",
+            RuntimeWarning, stacklevel=3)
+
+
+_set_hw_queues()
 # ENSVS_LIB: another in-tree build of the same ABI, for A/B timing of a kernel change
 # (tools/ab_lib.sh); the default is the package's own libensvs.so
 LIB_PATH = os.environ.get("ENSVS_LIB") or os.path.join(_HERE, "libensvs.so")
@@ -96,7 +116,7 @@ SIGNATURES = {
     "ensvs_lstm_mfma_bwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp,
                             c_int, c_vp, c_vp],
     "ensvs_lstm_coop_supported": [c_int, c_int],
-    "ensvs_lstm_coop_work_bytes": [c_int],
+    "ensvs_lstm_coop_work_bytes": [c_int, c_int],
     "ensvs_lstm_coop_pack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
     "ensvs_lstm_coop_fwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
                             c_ll, c_vp],
@@ -109,7 +129,10 @@ SIGNATURES = {
     "ensvs_ardec_bwd": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
                         c_float, c_float, c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ensvs_ardec_coop_supported": [c_int, c_int],
-    "ensvs_ardec_coop_work_bytes": [c_int],
+    "ensvs_ardec_coop_work_bytes": [c_int, c_int],
+    "ensvs_coop_set_error_word": [c_vp],
+    "ensvs_coop_set_timeout_us": [c_ll],
+    "ensvs_coop_inject_fault": [c_int],
     "ensvs_ardec_coop_pack": [c_vp, c_int, c_int, c_vp, c_vp],
     "ensvs_ardec_coop_fwd": [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
                              c_vp, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_float,
@@ -148,6 +171,8 @@ SIGNATURES = {
     "ensvs_lf0_interaction": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_int,
                               c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ensvs_l2norm": [c_vp, c_ll, c_vp, c_vp, c_vp],
+    "ensvs_l2norm_chk": [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp],
+    "ensvs_poison_on_error": [c_vp, c_vp, c_vp],
     "ensvs_adam": [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_float, c_float, c_float, c_float, c_float,
                    c_float, c_float, c_vp],
     "ensvs_adam_step": [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_float, c_double, c_double, c_float,

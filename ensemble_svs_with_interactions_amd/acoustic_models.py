@@ -38,9 +38,12 @@ BRANCH_AFTER = {2: 1, 3: 1}
 EXCL_BRANCHES = {0, 1}
 
 
-def _ar_work(H, device):
-    """Workspace of one cooperative AR-decoder launch (counters + exchange slabs)."""
-    n = query("ensvs_ardec_coop_work_bytes", H)
+def _ar_work(H, B, device):
+    """Workspace of one cooperative AR-decoder launch (per 32-sequence tile: counters +
+    exchange slabs); registers the process's coop error word first."""
+    from .engine import coop_error_word
+    coop_error_word(device)
+    n = query("ensvs_ardec_coop_work_bytes", H, B)
     return empty(n, device=device, dtype=torch.uint8), n
 
 class ZoneOutCell(nn.Module):
@@ -239,7 +242,7 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
 
     def _ar_coop(self, B):
         """Whether the AR decoder runs the cooperative kernels (ardec.hip: H = 128 / 256,
-        B <= 32, production bf16 precision; fp16 / bf16 recurrent products with fp32
+        B <= 256 in tiles of 32 sequences, production bf16 precision; fp16 / bf16 recurrent products with fp32
         accumulation, gates, cell state and feat_out).  The fp32 parity mode keeps the exact
         per-sequence kernels."""
         H = self.decoder.lstm[0].cell.hidden_size
@@ -345,7 +348,7 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
         ins = (wih_p.data_ptr(), dec.feat_out.weight.data_ptr(), dec.feat_out.weight.shape[1],
                xs[0].data_ptr() + 4 * li, ld, masks.data_ptr(), tptr, tld, B, T, H)
         if coop is not None and self._ar_coop(B):
-            work, nbytes = _ar_work(H, dev)
+            work, nbytes = _ar_work(H, B, dev)
             call("ensvs_ardec_coop_fwd", gx.data_ptr(), 4 * H, ofx.data_ptr(), 4,
                  coop[0].data_ptr(), *ins, *consts, *outs, work.data_ptr(), nbytes, Ly.stream())
         else:
@@ -380,7 +383,7 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
                 st["sg"].data_ptr(), st["sc"].data_ptr(), st["so"].data_ptr(), dg.data_ptr(),
                 do4.data_ptr())
         if coop is not None and self._ar_coop(B):
-            work, nbytes = _ar_work(H, dev)
+            work, nbytes = _ar_work(H, B, dev)
             call("ensvs_ardec_coop_bwd", dlf0.data_ptr(), ptr(dres), coop[1].data_ptr(), *args,
                  work.data_ptr(), nbytes, Ly.stream())
         else:

@@ -372,6 +372,7 @@ template <int H> struct ArGeo {
   static constexpr int FBUF = FH + coop::SB * NW * 16;  // + feat_out partials [s][w][4] fp32
   static constexpr int BG = coop::SB * 4 * H * 2;  // backward per buffer: dG [s][4H] bf16
   static constexpr int BBUF = BG + coop::SB * NW * 4;   // + prenet partials [s][w] fp32
+  static constexpr int SLAB = 2 * (FBUF > BBUF ? FBUF : BBUF);  // one tile's double buffer
   static_assert(H % 128 == 0 && NW % 4 == 0, "H");
 };
 
@@ -386,7 +387,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
     const float* __restrict__ mask, const float* __restrict__ teach, int ldt, int B, int T,
     ArConsts k, float* __restrict__ lf0, float* __restrict__ res, float* __restrict__ sg,
     float* __restrict__ sc, float* __restrict__ sh, float* __restrict__ so,
-    float* __restrict__ sp, unsigned* __restrict__ work) {
+    float* __restrict__ sp, unsigned* __restrict__ work, coop::Ctl c) {
   using namespace coop;
   using G = ArGeo<H>;
   constexpr int KCW = G::KCW, NW = G::NW;
@@ -397,6 +398,24 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
   const int w = blockIdx.x, u0 = w * UW;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int Tr = T / 4;
+  {  // this workgroup's sequence tile (blockIdx.y): sequences [32 y, 32 y + 32)
+    const int s0 = blockIdx.y * SB;
+    B = min(SB, B - s0);
+    const long long r = (long long)s0 * Tr, f = (long long)s0 * T;
+    gx += r * ldgx;
+    ofx += r * ldo;
+    score += f * lds;
+    mask += r;
+    if (teach) teach += f * ldt;
+    lf0 += f;
+    res += f;
+    sg += r * 4 * H;
+    sc += r * H;
+    sh += r * H;
+    so += r * 4;
+    sp += r;
+  }
+  unsigned* hdr = tile_hdr(work, blockIdx.y);
   const float den = k.in_max - k.in_min;
 
   f16x8 wf[4][KCW];
@@ -407,7 +426,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk) wf[mt][kk] = src[(mt * KCW + kk) * 64];
   }
-  const __amdgpu_buffer_rsrc_t xr = slab(work, 2 * G::FBUF);
+  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.y, blockIdx.y, G::SLAB);
 
   // cells (unit u = p & 15, sequence s = p >> 4), p = tid + 256 i: 16 lanes per sequence
   int cs[2], cu[2];
@@ -482,7 +501,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (t > 0) {
-      wait_count(work, 0, (unsigned)(NW * t));
+      wait_count(hdr, 0, (unsigned)(NW * t), c);
       const int base = ((t - 1) & 1) * G::FBUF;
       f16x8 bf[KCW][2];
 #pragma unroll
@@ -552,7 +571,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
            *(const f32x4*)&hs[(lane >> 1) * UW + (lane & 1) * 8]);
       if (lane < SB) st16(xr, base + G::FH + (lane * NW + w) * 16, *(const f32x4*)&ops[lane * 4]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) signal(work, 0);
+      if (lane == 0) signal(hdr, 0, t, c);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -568,7 +587,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
     load_red(t + 1);
   }
   if (w == 0) {  // the last step's outputs
-    wait_count(work, 0, (unsigned)(NW * Tr));
+    wait_count(hdr, 0, (unsigned)(NW * Tr), c);
     if (tid < SB) reduce_out(Tr, ((Tr - 1) & 1) * G::FBUF);
   }
 }
@@ -580,7 +599,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
     const float* __restrict__ wfo, int ldwfo, const float* __restrict__ mask, int teacher, int B,
     int T, ArConsts k, const float* __restrict__ sg, const float* __restrict__ sc,
     const float* __restrict__ so, float* __restrict__ dg, float* __restrict__ do4,
-    unsigned* __restrict__ work) {
+    unsigned* __restrict__ work, coop::Ctl c) {
   using namespace coop;
   using G = ArGeo<H>;
   constexpr int KCBW = G::KCBW, NW = G::NW;
@@ -591,6 +610,20 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
   const int w = blockIdx.x, u0 = w * UW;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int Tr = T / 4;
+  {  // this workgroup's sequence tile (blockIdx.y)
+    const int s0 = blockIdx.y * SB;
+    B = min(SB, B - s0);
+    const long long r = (long long)s0 * Tr, f = (long long)s0 * T;
+    glf0 += f;
+    if (gres) gres += f;
+    mask += r;
+    sg += r * 4 * H;
+    sc += r * H;
+    so += r * 4;
+    dg += r * 4 * H;
+    do4 += r * 4;
+  }
+  unsigned* hdr = tile_hdr(work, blockIdx.y);
 
   bf16x8 wb[KCBW];
   {
@@ -598,7 +631,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
 #pragma unroll
     for (int kk = 0; kk < KCBW; ++kk) wb[kk] = src[kk * 64];
   }
-  const __amdgpu_buffer_rsrc_t xr = slab(work, 2 * G::BBUF);
+  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.y, blockIdx.y, G::SLAB);
 
   int cs[2], cu[2];
   float wo[2][4], wpg[2][4];
@@ -648,7 +681,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     float dprev = 0.f;
     if (q > 0) {
-      wait_count(work, 0, (unsigned)(NW * q));
+      wait_count(hdr, 0, (unsigned)(NW * q), c);
       const int base = ((q - 1) & 1) * G::BBUF;
       bf16x8 bf[KCBW][2];
 #pragma unroll
@@ -731,7 +764,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
       if (tid < SB) st4(xr, base + G::BG + (tid * NW + w) * 4, dps[tid]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) signal(work, 0);
+      if (tid == 0) signal(hdr, 0, q, c);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -751,10 +784,6 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
   }
 }
 
-size_t ar_coop_lds(size_t st_lds) {
-  return ensvs_rec_exclusive() ? std::max<size_t>(st_lds, 160 * 1024) - st_lds : 0;
-}
-
 template <int H>
 int coop_fwd_launch(const float* gx, int ldgx, const float* ofx, int ldo, const void* wp,
                     const float* wih_p, const float* wfo, int ldwfo, const float* score, int lds,
@@ -762,14 +791,14 @@ int coop_fwd_launch(const float* gx, int ldgx, const float* ofx, int ldo, const 
                     float* lf0, float* res, float* sg, float* sc, float* sh, float* so, float* sp,
                     unsigned* work, hipStream_t st) {
   const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSF + coop::SB * 5) + 2 * coop::SB * coop::UW;
-  const size_t dyn = ar_coop_lds(st_lds);
-  static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)ardec_coop_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-  if (attr != hipSuccess) return ENSVS_E_HIP;
-  if (hipMemsetAsync(work, 0, coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
-  hipLaunchKernelGGL(ardec_coop_fwd_kernel<H>, dim3(ArGeo<H>::NW), dim3(coop::NT), dyn, st, gx,
-                     ldgx, ofx, ldo, (const f16x8*)wp, wih_p, wfo, ldwfo, score, lds, mask, teach,
-                     ldt, B, T, k, lf0, res, sg, sc, sh, so, sp, work);
+  static const bool attr = coop::set_max_lds((const void*)ardec_coop_fwd_kernel<H>, st_lds);
+  if (!attr) return ENSVS_E_HIP;
+  const int nt = coop::ntiles(B);
+  if (hipMemsetAsync(work, 0, (size_t)nt * coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(ardec_coop_fwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(coop::NT),
+                     coop::dyn_lds(st_lds), st, gx, ldgx, ofx, ldo, (const f16x8*)wp, wih_p, wfo,
+                     ldwfo, score, lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, so, sp,
+                     work, coop::host_ctl());
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
@@ -780,28 +809,32 @@ int coop_bwd_launch(const float* glf0, const float* gres, const void* wp, const 
                     ArConsts k, const float* sg, const float* sc, const float* so, float* dg,
                     float* do4, unsigned* work, hipStream_t st) {
   const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSB + coop::SB * 5) + 2 * coop::SB * 64;
-  const size_t dyn = ar_coop_lds(st_lds);
-  static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)ardec_coop_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-  if (attr != hipSuccess) return ENSVS_E_HIP;
-  if (hipMemsetAsync(work, 0, coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
-  hipLaunchKernelGGL(ardec_coop_bwd_kernel<H>, dim3(ArGeo<H>::NW), dim3(coop::NT), dyn, st, glf0,
-                     gres, (const bf16x8*)wp, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc,
-                     so, dg, do4, work);
+  static const bool attr = coop::set_max_lds((const void*)ardec_coop_bwd_kernel<H>, st_lds);
+  if (!attr) return ENSVS_E_HIP;
+  const int nt = coop::ntiles(B);
+  if (hipMemsetAsync(work, 0, (size_t)nt * coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(ardec_coop_bwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(coop::NT),
+                     coop::dyn_lds(st_lds), st, glf0, gres, (const bf16x8*)wp, wih_p, wfo, ldwfo,
+                     mask, teacher, B, T, k, sg, sc, so, dg, do4, work, coop::host_ctl());
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
 
-bool ar_coop_shape(int B, int H) { return B >= 1 && B <= coop::SB && (H == 128 || H == 256); }
+// any B up to 8 tiles of 32 sequences (coop.h): at H = 256 a launch is 16 x 8 workgroups
+constexpr int AR_MAX_TILES = 8;
+bool ar_coop_shape(int B, int H) {
+  return B >= 1 && B <= AR_MAX_TILES * coop::SB && (H == 128 || H == 256);
+}
 
-long long ar_coop_work(int H) {
-  return H == 128 ? coop::HDR + 2LL * std::max(ArGeo<128>::FBUF, ArGeo<128>::BBUF)
-                  : coop::HDR + 2LL * std::max(ArGeo<256>::FBUF, ArGeo<256>::BBUF);
+long long ar_coop_work(int H, int B) {
+  const long long slab = H == 128 ? ArGeo<128>::SLAB : ArGeo<256>::SLAB;
+  return (long long)coop::ntiles(B) * (coop::HDR + slab);
 }
 
 int ar_coop_check(int B, int T, int H, const void* wp, const void* work, long long work_bytes) {
   if (!ar_coop_shape(B, H) || T <= 0 || T % 4) return ENSVS_E_SHAPE;
-  if (!wp || (uintptr_t)wp % 16 || !work || (uintptr_t)work % 256 || work_bytes < ar_coop_work(H))
+  if (!wp || (uintptr_t)wp % 16 || !work || (uintptr_t)work % 256 ||
+      work_bytes < ar_coop_work(H, B))
     return ENSVS_E_ARG;
   return ENSVS_OK;
 }
@@ -858,8 +891,8 @@ ENSVS_API int ensvs_ardec_bwd(const float* glf0, const float* gres, const float*
 
 ENSVS_API int ensvs_ardec_coop_supported(int B, int H) { return ar_coop_shape(B, H) ? 1 : 0; }
 
-ENSVS_API long long ensvs_ardec_coop_work_bytes(int H) {
-  return (H == 128 || H == 256) ? ar_coop_work(H) : 0;
+ENSVS_API long long ensvs_ardec_coop_work_bytes(int H, int B) {
+  return ar_coop_shape(B, H) ? ar_coop_work(H, B) : 0;
 }
 
 ENSVS_API int ensvs_ardec_coop_pack(const float* whh, int H, int bwd, void* out, void* stream) {

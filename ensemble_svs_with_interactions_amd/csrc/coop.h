@@ -9,9 +9,26 @@
 // barrier when one lane signals for several waves), one agent-scope counter add per workgroup;
 // readers poll the counter from one lane and read the slab with sc1 loads only.
 //
-// Workspace: HDR bytes of header (one 64-B counter line per direction at word 16 d, the error
-// word at byte 128), then the slab.  The polls are bounded: a grid that cannot become resident
-// flags the error word and runs on instead of hanging.
+// Sequence tiles.  The MFMA N dimension holds SB = 32 sequences; a batch of B > 32 sequences is
+// split into ceil(B / 32) independent tiles, one per blockIdx.z (lstm_coop) / blockIdx.y
+// (ardec), each with its own counters and slabs.  Tiles never wait on each other, so a tile
+// needs only its own workgroups co-resident: workgroups are dispatched in block order, every
+// tile's workgroups come before the next tile's, and a resident tile runs to the end and frees
+// its CUs for the next.  The tiles run concurrently when the chip holds them (P = 60 pairs of
+// 512 frames: two tiles side by side, the same step count as 30 x 1024).
+//
+// Workspace of ntiles tiles: ntiles headers of HDR bytes (one 64-B counter line per direction
+// at word 16 d, the tile's error word at byte 128), then ntiles slabs of the kernel's slab size.
+//
+// Failure handling (a grid that cannot become resident, e.g. CUs held by another stream's
+// long-running kernel): the polls are bounded in time (Ctl::timeout ticks of the 100 MHz
+// steady counter, 1 s by default).  The workgroup that times out sets the ABORT bit of the
+// direction's counter -- every later poll of any workgroup of the tile then passes at once, so
+// the launch ends within one timeout instead of one per step -- and ORs 1 into the tile's
+// header word and into Ctl::err, a caller-registered persistent device word
+// (ensvs_coop_set_error_word) that the launch's header memset does not clear.  The product
+// folds that word into the step's gradient-norm check (ensvs_l2norm_chk: the update is
+// skipped) and raises on the host (engine.check_coop_errors).
 #pragma once
 #include "common.h"
 
@@ -21,38 +38,67 @@ namespace coop {
 
 constexpr int NT = 256;     // 4 waves per workgroup
 constexpr int UW = 16;      // hidden units per workgroup
-constexpr int SB = 32;      // sequence columns: two MFMA N tiles
+constexpr int SB = 32;      // sequence columns of one tile: two MFMA N tiles
 constexpr int CP_SC1 = 16;  // buffer-op cache policy: sc1 (L1 bypass on both sides)
-constexpr int HDR = 256;    // workspace header
-constexpr unsigned SPIN_MAX = 1u << 24;
+constexpr int HDR = 256;    // workspace header per tile
+constexpr unsigned ABORT = 0x80000000u;  // counter bit: a workgroup of the tile timed out
+
+// per-launch failure controls (by value in the kernel arguments)
+struct Ctl {
+  unsigned* err;            // persistent error word (the tile header's word when none is set)
+  long long timeout;        // poll bound in steady-counter ticks
+  int fault;                // test only: workgroup (0, 0) of tile 0 skips its step-1 signal
+};
+
+// host side (lstm_coop.hip): the registered error word, timeout and fault switch
+Ctl host_ctl();
+
+inline int ntiles(int B) { return (B + SB - 1) / SB; }
 
 __device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float tanh_fast(float x) {
   return fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)), 1.f);
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab(unsigned* work, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((char*)work + HDR, 0, bytes, 0x00020000);
+// tile z's header and slab resource in a workspace of nt tiles with slab_bytes per slab
+__device__ __forceinline__ unsigned* tile_hdr(unsigned* work, int z) {
+  return work + z * (HDR / 4);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab(unsigned* work, int nt, int z,
+                                                       int slab_bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((char*)work + (long long)nt * HDR +
+                                               (long long)z * slab_bytes, 0, slab_bytes, 0x00020000);
 }
 
-// wait until direction d's counter reaches `target` (one lane), then release the workgroup
-__device__ __forceinline__ void wait_count(unsigned* work, int d, unsigned target) {
+// wait until direction d's counter of the tile reaches `target` (one lane polls), then release
+// the workgroup.  The first poll costs what the unbounded loop did; the clock is read only
+// once the counter is behind, and then every 8th poll.
+__device__ __forceinline__ void wait_count(unsigned* hdr, int d, unsigned target, const Ctl& c) {
   if (threadIdx.x == 0) {
-    unsigned* cnt = work + d * 16;
-    unsigned it = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++it == SPIN_MAX) {  // a workgroup never arrived: flag it and go on
-        __hip_atomic_store(work + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+    unsigned* cnt = hdr + d * 16;
+    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      const long long t0 = wall_clock64();
+      for (unsigned it = 1;; ++it) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+        if ((it & 7) == 0 && wall_clock64() - t0 > c.timeout) {
+          // a workgroup never arrived: release every waiter of this direction, flag the failure
+          __hip_atomic_fetch_or(cnt, ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_or(hdr + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_or(c.err ? c.err : hdr + 32, 1u, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
       }
     }
   }
   __syncthreads();
 }
 
-__device__ __forceinline__ void signal(unsigned* work, int d) {
-  __hip_atomic_fetch_add(work + d * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// publish step `step`'s slice: one agent-scope counter add (skipped by the test fault)
+__device__ __forceinline__ void signal(unsigned* hdr, int d, int step, const Ctl& c) {
+  if (c.fault && step == 1 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) return;
+  __hip_atomic_fetch_add(hdr + d * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ f32x4 ld16(__amdgpu_buffer_rsrc_t r, int off) {
@@ -79,5 +125,16 @@ __device__ __forceinline__ float sum16(float v) {
 // bwd = 1 bf16 fragments of W_hh^T (16 unit columns per workgroup, K in the dG slab order
 // n' = 64 w' + 4 u' + g).  H in {128, 256, 512}; out holds ndir*4*H*H 2-byte elements.
 int pack(const float* w0, const float* w1, int ndir, int H, int bwd, void* out, hipStream_t st);
+
+// dynamic LDS of a launch: the rest of the CU's 160 KB when the recurrence reserves its CU
+// (ensvs_rec_exclusive, read per launch), else none.  The kernel attribute is set once to the
+// exclusive size, whatever the first launch's setting.
+inline size_t dyn_lds(size_t static_lds) {
+  return ensvs_rec_exclusive() ? 160 * 1024 - static_lds : 0;
+}
+inline bool set_max_lds(const void* kernel, size_t static_lds) {
+  return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)(160 * 1024 - static_lds)) == hipSuccess;
+}
 
 }  // namespace coop

@@ -94,13 +94,22 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
     const long long* __restrict__ lengths, int B, int T,
     float* __restrict__ y, int ldy,            // [B*T][ldy], dir d at d H + u
     float* __restrict__ sv,                    // [B*T][2][5H]
-    unsigned* __restrict__ work) {
+    unsigned* __restrict__ work, Ctl c) {
   using G = CGeo<H>;
   constexpr int KCW = G::KCW, NW = G::NW;
   __shared__ __attribute__((aligned(16))) float part[4 * SB * PSF];
   __shared__ __attribute__((aligned(16))) _Float16 hs[SB * UW];
   __shared__ int sL[SB];
   const int d = blockIdx.y, w = blockIdx.x, u0 = w * UW;
+  {  // this workgroup's sequence tile: sequences [32 z, 32 z + 32)
+    const int s0 = blockIdx.z * SB;
+    B = min(SB, B - s0);
+    lengths += s0;
+    gx += (long long)s0 * T * ldg;
+    y += (long long)s0 * T * ldy;
+    sv += (long long)s0 * T * 10 * H;
+  }
+  unsigned* hdr = tile_hdr(work, blockIdx.z);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < SB) sL[tid] = tid < B ? (int)lengths[tid] : 0;
 
@@ -121,7 +130,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
     for (int i = tid; i < (T - L) * UW; i += NT)
       y[((long long)s * T + L + i / UW) * ldy + d * H + u0 + i % UW] = 0.f;
   }
-  const __amdgpu_buffer_rsrc_t xr = slab(work, G::FX);
+  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.z, blockIdx.z, G::BX);
 
   // cell pairs: (unit u = p & 15, sequence s = p >> 4), p = tid + 256 i
   int cs[2], cu[2];
@@ -156,7 +165,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (t > 0) {
-      wait_count(work, d, (unsigned)(NW * t));
+      wait_count(hdr, d, (unsigned)(NW * t), c);
       f16x8 bf[KCW][2];
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk)
@@ -209,7 +218,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
       const int off = (((d * 2 + (t & 1)) * SB + (lane >> 1)) * H + u0 + (lane & 1) * 8) * 2;
       __builtin_amdgcn_raw_buffer_store_b128(v, xr, off, 0, CP_SC1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) signal(work, d);
+      if (lane == 0) signal(hdr, d, t, c);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -232,13 +241,22 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
     const long long* __restrict__ lengths, int B, int T,
     const float* __restrict__ sv,              // saved [B*T][2][5H]
     float* __restrict__ dg, int lddg,          // [B*T][lddg], dir d gate g unit u at d 4H + g H + u
-    unsigned* __restrict__ work) {
+    unsigned* __restrict__ work, Ctl c) {
   using G = CGeo<H>;
   constexpr int KCBW = G::KCBW, NW = G::NW, G4 = 4 * H;
   __shared__ __attribute__((aligned(16))) float part[4 * SB * PSB];
   __shared__ __attribute__((aligned(16))) __bf16 gs[SB * 64];  // [s][4 u + g]
   __shared__ int sL[SB];
   const int d = blockIdx.y, w = blockIdx.x, u0 = w * UW;
+  {  // this workgroup's sequence tile
+    const int s0 = blockIdx.z * SB;
+    B = min(SB, B - s0);
+    lengths += s0;
+    dy += (long long)s0 * T * lddy;
+    sv += (long long)s0 * T * 10 * H;
+    dg += (long long)s0 * T * lddg;
+  }
+  unsigned* hdr = tile_hdr(work, blockIdx.z);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < SB) sL[tid] = tid < B ? (int)lengths[tid] : 0;
 
@@ -258,7 +276,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
       dg[((long long)s * T + L + i / 64) * lddg + d * G4 + (c / 16) * H + u0 + c % 16] = 0.f;
     }
   }
-  const __amdgpu_buffer_rsrc_t xr = slab(work, G::BX);
+  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.z, blockIdx.z, G::BX);
 
   int cs[2], cu[2];
 #pragma unroll
@@ -293,7 +311,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
   for (int q = 0; q < maxL; ++q) {
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     if (q > 0) {
-      wait_count(work, d, (unsigned)(NW * q));
+      wait_count(hdr, d, (unsigned)(NW * q), c);
       bf16x8 bf[KCBW][2];
 #pragma unroll
       for (int kk = 0; kk < KCBW; ++kk)
@@ -348,7 +366,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
       __builtin_amdgcn_raw_buffer_store_b128(v, xr, off, 0, CP_SC1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) signal(work, d);
+      if (tid == 0) signal(hdr, d, q, c);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -361,22 +379,17 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
   }
 }
 
-size_t excl(size_t need) {
-  return ensvs_rec_exclusive() ? std::max<size_t>(need, 160 * 1024) : need;
-}
-
 template <int H>
 int launch_fwd(const float* gx, int ldg, const void* wp, const long long* lengths, int B, int T,
                float* y, int ldy, float* sv, unsigned* work, hipStream_t st) {
   using G = CGeo<H>;
   const size_t st_lds = sizeof(float) * 4 * SB * PSF + 2 * SB * UW + 4 * SB;
-  const size_t dyn = excl(st_lds) - st_lds;
-  static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)lstm_coop_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-  if (attr != hipSuccess) return ENSVS_E_HIP;
-  if (hipMemsetAsync(work, 0, HDR, st) != hipSuccess) return ENSVS_E_HIP;
-  hipLaunchKernelGGL(lstm_coop_fwd_kernel<H>, dim3(G::NW, 2), dim3(NT), dyn, st, gx, ldg,
-                     (const f16x8*)wp, lengths, B, T, y, ldy, sv, work);
+  static const bool attr = set_max_lds((const void*)lstm_coop_fwd_kernel<H>, st_lds);
+  if (!attr) return ENSVS_E_HIP;
+  const int nt = ntiles(B);
+  if (hipMemsetAsync(work, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(lstm_coop_fwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds), st,
+                     gx, ldg, (const f16x8*)wp, lengths, B, T, y, ldy, sv, work, host_ctl());
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
@@ -386,30 +399,70 @@ int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengt
                const float* sv, float* dg, int lddg, unsigned* work, hipStream_t st) {
   using G = CGeo<H>;
   const size_t st_lds = sizeof(float) * 4 * SB * PSB + 2 * SB * 64 + 4 * SB;
-  const size_t dyn = excl(st_lds) - st_lds;
-  static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)lstm_coop_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-  if (attr != hipSuccess) return ENSVS_E_HIP;
-  if (hipMemsetAsync(work, 0, HDR, st) != hipSuccess) return ENSVS_E_HIP;
-  hipLaunchKernelGGL(lstm_coop_bwd_kernel<H>, dim3(G::NW, 2), dim3(NT), dyn, st, dy, lddy,
-                     (const bf16x8*)wp, lengths, B, T, sv, dg, lddg, work);
+  static const bool attr = set_max_lds((const void*)lstm_coop_bwd_kernel<H>, st_lds);
+  if (!attr) return ENSVS_E_HIP;
+  const int nt = ntiles(B);
+  if (hipMemsetAsync(work, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
+  hipLaunchKernelGGL(lstm_coop_bwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds), st,
+                     dy, lddy, (const bf16x8*)wp, lengths, B, T, sv, dg, lddg, work, host_ctl());
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
 
-bool coop_shape(int B, int H) { return B >= 1 && B <= SB && (H == 256 || H == 512); }
+// any B: tiles of 32 sequences (coop.h); up to 8 tiles (256 sequences) per launch keeps a
+// launch's grid within the chip at H = 512 (8 x 64 workgroups)
+constexpr int MAX_TILES = 8;
+bool coop_shape(int B, int H) { return B >= 1 && B <= MAX_TILES * SB && (H == 256 || H == 512); }
 
-int check_work(const void* work, long long work_bytes, int H) {
-  if (!work || (uintptr_t)work % 256 || work_bytes < ensvs_lstm_coop_work_bytes(H)) return ENSVS_E_ARG;
+long long work_bytes(int H, int B) {
+  const long long slab = H == 256 ? CGeo<256>::BX : CGeo<512>::BX;
+  return (long long)ntiles(B) * (HDR + slab);
+}
+
+int check_work(const void* work, long long nbytes, int H, int B) {
+  if (!work || (uintptr_t)work % 256 || nbytes < work_bytes(H, B)) return ENSVS_E_ARG;
   return ENSVS_OK;
 }
 
+// failure controls shared by every cooperative launch (coop.h Ctl)
+unsigned* g_err = nullptr;
+long long g_timeout_us = 1000000;
+int g_fault = 0;
+
 }  // namespace
+
+coop::Ctl coop::host_ctl() {
+  static int rate_khz = [] {
+    int dev = 0, r = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&r, hipDeviceAttributeWallClockRate, dev) != hipSuccess || r <= 0)
+      r = 100000;  // 100 MHz
+    return r;
+  }();
+  return Ctl{g_err, g_timeout_us * rate_khz / 1000, g_fault};
+}
+
+ENSVS_API int ensvs_coop_set_error_word(unsigned* word) {
+  if ((uintptr_t)word % 4) return ENSVS_E_ARG;
+  g_err = word;
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_coop_set_timeout_us(long long us) {
+  if (us <= 0) return ENSVS_E_ARG;
+  g_timeout_us = us;
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_coop_inject_fault(int on) {
+  g_fault = on ? 1 : 0;
+  return ENSVS_OK;
+}
 
 ENSVS_API int ensvs_lstm_coop_supported(int B, int H) { return coop_shape(B, H) ? 1 : 0; }
 
-ENSVS_API long long ensvs_lstm_coop_work_bytes(int H) {
-  return HDR + 2LL * 2 * SB * 4 * H * 2;  // header + the backward slab (the larger one)
+ENSVS_API long long ensvs_lstm_coop_work_bytes(int H, int B) {
+  return coop_shape(B, H) ? work_bytes(H, B) : 0;
 }
 
 int coop::pack(const float* w0, const float* w1, int ndir, int H, int bwd, void* out,
@@ -440,7 +493,7 @@ ENSVS_API int ensvs_lstm_coop_fwd(const float* gx, int ldg, const void* wpack,
                                   const long long* lengths, int B, int T, int H, float* y, int ldy,
                                   float* saved, void* work, long long work_bytes, void* stream) {
   if (!coop_shape(B, H) || T <= 0 || ldg < 8 * H || ldy < 2 * H) return ENSVS_E_SHAPE;
-  if (check_work(work, work_bytes, H) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
+  if (check_work(work, work_bytes, H, B) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;
   return H == 256 ? launch_fwd<256>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st)
@@ -452,7 +505,7 @@ ENSVS_API int ensvs_lstm_coop_bwd(const float* dy, int lddy, const void* wpack,
                                   const float* saved, float* dg, int lddg, void* work,
                                   long long work_bytes, void* stream) {
   if (!coop_shape(B, H) || T <= 0 || lddy < 2 * H || lddg < 8 * H) return ENSVS_E_SHAPE;
-  if (check_work(work, work_bytes, H) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
+  if (check_work(work, work_bytes, H, B) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;
   return H == 256 ? launch_bwd<256>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st)

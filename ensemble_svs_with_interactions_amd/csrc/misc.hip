@@ -530,7 +530,8 @@ __global__ void sumsq_kernel(const float* __restrict__ x, long long n, float* __
   if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
-__global__ void norm_final_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
+__global__ void norm_final_kernel(const float* __restrict__ part, int n, float* __restrict__ out,
+                                  const unsigned* __restrict__ err) {
   __shared__ double red[256];
   double acc = 0.0;
   for (int i = threadIdx.x; i < n; i += 256) acc += part[i];
@@ -540,7 +541,14 @@ __global__ void norm_final_kernel(const float* __restrict__ part, int n, float* 
     if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] = (float)sqrt(red[0]);
+  // a failed cooperative recurrence (coop.h error word) makes the norm NaN: the update skips
+  if (threadIdx.x == 0) out[0] = (err && *err) ? __builtin_nanf("") : (float)sqrt(red[0]);
+}
+
+// data parallel: a rank whose cooperative recurrence failed writes NaN into one gradient
+// element before the all-reduce, so every rank's norm is NaN and every rank skips the update
+__global__ void poison_kernel(const unsigned* __restrict__ err, float* __restrict__ x) {
+  if (threadIdx.x == 0 && *err) x[0] = __builtin_nanf("");
 }
 
 // clip_grad_norm_(max_norm) then torch.optim.Adam (weight_decay 0, amsgrad off);
@@ -967,7 +975,26 @@ ENSVS_API int ensvs_l2norm(const float* x, long long n, float* part, float* norm
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(sumsq_kernel, dim3(blocks), dim3(256), 0, st, x, n, part);
   ENSVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(256), 0, st, part, blocks, norm_out);
+  hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(256), 0, st, part, blocks, norm_out,
+                     (const unsigned*)nullptr);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_l2norm_chk(const float* x, long long n, float* part, float* norm_out,
+                               const unsigned* err, void* stream) {
+  int blocks = std::min(1024, grid_for(n));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(blocks), dim3(256), 0, st, x, n, part);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(256), 0, st, part, blocks, norm_out, err);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_poison_on_error(const unsigned* err, float* x, void* stream) {
+  if (!err || !x) return ENSVS_E_ARG;
+  hipLaunchKernelGGL(poison_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, err, x);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }

@@ -295,6 +295,73 @@ class ModulePacks:
         return dict(bias=self.bias.buf, bias_off=self.refs[name].offset)
 
 
+# ---- cooperative-recurrence failure flag (coop.h) ------------------------------------------
+class CoopError(RuntimeError):
+    """A cooperative recurrence (lstm_coop.hip / ardec.hip) could not get all workgroups of a
+    sequence tile resident and timed out: its outputs of that launch are invalid.  The step
+    that ran it skipped its update (the gradient norm read the flag); raised on the host by
+    check_coop_errors / step_metrics / the next train_step."""
+
+
+_COOP = {}  # device -> (int32 error word, pinned host copy, event or None)
+
+
+def _dev_key(device):
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return str(d)
+
+
+def coop_error_word(device):
+    """The persistent device word every cooperative launch ORs 1 into on a residency
+    timeout (registered with the library on first use; one per process and device)."""
+    key = _dev_key(device)
+    ent = _COOP.get(key)
+    if ent is None:
+        word = torch.zeros(1, dtype=torch.int32, device=device)
+        host = torch.zeros(1, dtype=torch.int32, pin_memory=torch.cuda.is_available())
+        _lib.call("ensvs_coop_set_error_word", word.data_ptr())
+        ent = _COOP[key] = [word, host, None]
+    return ent[0]
+
+
+def _coop_raise(ent):
+    ent[0].zero_()
+    ent[1].zero_()
+    raise CoopError("ensvs: a cooperative recurrence timed out waiting for its workgroups "
+                    "(grid not co-resident); the step's update was skipped (non-finite "
+                    "gradient norm).  The flag is cleared; the next step runs normally.")
+
+
+def check_coop_errors(device=None, sync=True):
+    """Raise CoopError if a cooperative launch flagged a failure.  sync=True reads the word
+    now (a device sync); sync=False only looks at the copy taken by note_coop_check() once
+    the device has reached it (no wait), so the host never blocks the step pipeline."""
+    for key, ent in list(_COOP.items()):
+        if device is not None and key != _dev_key(device):
+            continue
+        if sync:
+            if int(ent[0].item()):
+                _coop_raise(ent)
+        elif ent[2] is not None and ent[2].query():
+            ent[2] = None
+            if int(ent[1][0]):
+                _coop_raise(ent)
+
+
+def note_coop_check(device):
+    """Enqueue an asynchronous copy of the error word after this step's kernels (checked
+    without waiting by the next check_coop_errors(sync=False))."""
+    ent = _COOP.get(_dev_key(device))
+    if ent is None or ent[2] is not None:
+        return
+    ent[1].copy_(ent[0], non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    ent[2] = ev
+
+
 def empty(*shape, device, dtype=torch.float32):
     return torch.empty(*shape, dtype=dtype, device=device)
 

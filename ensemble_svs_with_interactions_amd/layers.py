@@ -430,7 +430,7 @@ def lstm_fused_proj(H):
 
 def lstm_coop(B, H):
     """Whether the layer's recurrence runs the cooperative kernels (lstm_coop.hip: H = 256 /
-    512, B <= 32, production bf16 precision; fp16 / bf16 recurrent products with fp32
+    512, B <= 256 in tiles of 32 sequences, production bf16 precision; fp16 / bf16 recurrent products with fp32
     accumulation and cell state).  The fp32 parity mode keeps lstm.hip's exact kernels."""
     return gemm_dtype() == _lib.DT_BF16 and query("ensvs_lstm_coop_supported", B, H) == 1
 
@@ -517,8 +517,12 @@ def _whh_pad(lstm, l, HP):
     return ent[1]
 
 
-def _coop_work(H, device):
-    n = query("ensvs_lstm_coop_work_bytes", H)
+def _coop_work(H, B, device):
+    """Workspace of one cooperative launch (ceil(B/32) tile headers + slabs); the process's
+    coop error word is registered first (engine.coop_error_word)."""
+    from .engine import coop_error_word
+    coop_error_word(device)
+    n = query("ensvs_lstm_coop_work_bytes", H, B)
     return empty(n, device=device, dtype=torch.uint8), n
 
 
@@ -561,7 +565,7 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
             y16 = torch.empty(M, 2 * H, dtype=torch.bfloat16, device=device)
         saved = empty(M * 2 * 5 * (HP or H), device=device)
         if lstm_coop(B, H):
-            work, nbytes = _coop_work(H, device)
+            work, nbytes = _coop_work(H, B, device)
             call("ensvs_lstm_coop_fwd", gx.data_ptr(), 8 * H, _coop_pack(lstm, l, False).data_ptr(),
                  lens_dev.data_ptr(), B, T, H, y.data_ptr(), 2 * H, saved.data_ptr(),
                  work.data_ptr(), nbytes, stream())
@@ -622,7 +626,7 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
             bpart = empty(B, 8 * H, device=device)
         dg = empty(M, 8 * H, device=device) if dgb is None or x16 is None else None
         if lstm_coop(B, H):
-            work, nbytes = _coop_work(H, device)
+            work, nbytes = _coop_work(H, B, device)
             call("ensvs_lstm_coop_bwd", d.data_ptr(), 2 * H, _coop_pack(lstm, l, True).data_ptr(),
                  lens_dev.data_ptr(), B, T, H, s["saved"].data_ptr(), dg.data_ptr(), 8 * H,
                  work.data_ptr(), nbytes, stream())

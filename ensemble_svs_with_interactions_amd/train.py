@@ -15,7 +15,8 @@ import torch
 
 from . import layers as Ly
 from ._lib import call
-from .engine import branch_streams, empty, flatten_parameters, grad_of, weights_updated
+from .engine import (branch_streams, check_coop_errors, coop_error_word, empty,
+                     flatten_parameters, grad_of, note_coop_check, weights_updated)
 from .engine import _STATE as _ENGINE_STATE
 
 
@@ -63,6 +64,8 @@ class FusedAdam(torch.optim.Optimizer):
         self.sync_lr()
         self.norm = torch.zeros(1, device=self.flat.device)
         self._part = torch.empty(1024, device=self.flat.device)
+        # a cooperative recurrence that timed out (coop.h) makes the norm NaN: update skipped
+        self._err = coop_error_word(self.flat.device) if self.flat.is_cuda else None
 
     @property
     def lr(self):
@@ -94,8 +97,9 @@ class FusedAdam(torch.optim.Optimizer):
                 p.grad = p._ensvs_gview
 
     def grad_norm(self):
-        call("ensvs_l2norm", self.gflat.data_ptr(), self.gflat.numel(), self._part.data_ptr(),
-             self.norm.data_ptr(), Ly.stream())
+        call("ensvs_l2norm_chk", self.gflat.data_ptr(), self.gflat.numel(), self._part.data_ptr(),
+             self.norm.data_ptr(), None if self._err is None else self._err.data_ptr(),
+             Ly.stream())
         return self.norm
 
     def step(self, closure=None):
@@ -262,7 +266,17 @@ def allreduce_grads(gflat, group=None):
     import torch.distributed as dist
     if world_size(group) == 1:
         return
+    _poison(gflat, 0)
     dist.all_reduce(gflat, op=dist.ReduceOp.SUM, group=group)
+
+
+def _poison(gflat, i):
+    """NaN into gflat[i] when this rank's cooperative recurrence failed (coop.h error word),
+    before the all-reduce that carries element i: every rank's norm is then NaN and every
+    rank skips the update (a local skip alone would let the ranks' parameters diverge)."""
+    if gflat.is_cuda:
+        call("ensvs_poison_on_error", coop_error_word(gflat.device).data_ptr(),
+             gflat.data_ptr() + 4 * i, Ly.stream())
 
 
 class BucketedAllReduce:
@@ -303,6 +317,14 @@ class BucketedAllReduce:
         groups["rest"] = [p for p in model.parameters() if id(p) not in seen]
         self.buckets = {k: rng(v) for k, v in groups.items() if v}
 
+    def _reduce_flag(self):
+        """No bucket is launched after the join: share the failure flag itself (MAX)."""
+        import torch.distributed as dist
+        if self.gflat.is_cuda:
+            w = coop_error_word(self.gflat.device)
+            self.works.append(dist.all_reduce(w, op=dist.ReduceOp.MAX, group=self.group,
+                                              async_op=True))
+
     def launch(self, tag):
         import torch.distributed as dist
         for a, b in self.buckets.get(tag, ()):
@@ -310,6 +332,11 @@ class BucketedAllReduce:
                                               group=self.group, async_op=True))
 
     def finish(self):
+        rest = self.buckets.get("rest")
+        if rest:  # the last bucket carries the failure flag of this rank's recurrences
+            _poison(self.gflat, rest[0][0])
+        else:
+            self._reduce_flag()
         self.launch("rest")
         for w in self.works:
             w.wait()
@@ -354,13 +381,15 @@ def step_metrics(loss, optimizer):
     train_step, as host floats: Loss, Loss_Feats, Loss_Pitch (pitch_reg_weight 0 in the
     recipe), Loss_LogF0_Interaction (unweighted), Loss_MGC-0th_Interaction (0) and GradNorm
     (only when finite: the reference skips the step and the metric otherwise).  Reads the
-    device (a sync); call it only when logging."""
+    device (a sync); call it only when logging.  Raises engine.CoopError when a cooperative
+    recurrence of the step failed (its update was skipped); "Coop_Timeout" is 0 otherwise."""
+    check_coop_errors(loss.device, sync=True)
     total = float(loss.item())
     il = getattr(optimizer, "_il", None)
     wil = float(il[0].item()) if il is not None else 0.0
     out = {"Loss": total, "Loss_Feats": total - wil, "Loss_Pitch": 0.0,
            "Loss_LogF0_Interaction": wil / il[1] if il is not None else 0.0,
-           "Loss_MGC-0th_Interaction": 0.0}
+           "Loss_MGC-0th_Interaction": 0.0, "Coop_Timeout": 0.0}
     gn = float(optimizer.norm.item())
     if math.isfinite(gn):
         out["GradNorm"] = gn
@@ -375,6 +404,9 @@ def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengt
     logf0_diff_weight > 0 adds the log-F0 interaction loss between the main and sub tracks
     (train_acoustic_multitrack.py:175-182, 296; needs the output_subtrack model and y_sub).
     """
+    dev = x_main.device
+    # an earlier step's cooperative-recurrence failure, once the device got there (no wait)
+    check_coop_errors(dev, sync=False)
     if ddp and world_size() > 1:
         sync_buffers(model)
     loss = _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
@@ -383,6 +415,8 @@ def train_step(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengt
         allreduce_grads(optimizer.gflat)
     optimizer._reduced = False
     optimizer.step()
+    if dev.type == "cuda" and not torch.cuda.is_current_stream_capturing():
+        note_coop_check(dev)
     return loss, optimizer.norm
 
 
@@ -566,6 +600,8 @@ class GraphedTrainStep:
             if dst is None or dst.shape != v.shape:
                 raise ValueError(f"{k}: shape {tuple(v.shape)} differs from the captured one")
             dst.copy_(v, non_blocking=True)
+        dev = self.opt.flat.device
+        check_coop_errors(dev, sync=False)  # an earlier replay's failure (no wait)
         self.opt.sync_lr()  # a scheduler's lr change reaches the replayed update
         if self.ddp and world_size() > 1:
             sync_buffers(self.model)
@@ -575,6 +611,7 @@ class GraphedTrainStep:
         self.g_update.replay()
         self.opt.step_count += 1
         weights_updated()
+        note_coop_check(dev)
         return self.loss, self.norm
 
 
@@ -594,4 +631,6 @@ def train_epoch(model, optimizer, feeder, logf0_diff_weight=0.0, ddp=True):
                                 b["spk_main"], b["spk_sub"], lengths, ddp=ddp, y_sub=y_sub,
                                 logf0_diff_weight=logf0_diff_weight)
         out.append((loss, norm.clone()))
+    if out:
+        check_coop_errors(out[0][0].device, sync=True)
     return out

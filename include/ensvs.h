@@ -174,16 +174,19 @@ int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* w
                    const long long* lengths, int B, int T, int H, const float* saved, float* dg,
                    int lddg, float* work, long long work_floats, void* stream);
 
-/* Cooperative recurrence for H in {256, 512} and B <= 32 in production (bf16 GEMM)
+/* Cooperative recurrence for H in {256, 512} and B <= 256 in production (bf16 GEMM)
  * precision: one launch for every step, each direction split over H/16 workgroups that keep
  * their W_hh slice in registers and exchange h (fp16) / dG (bf16) through `work` every step
  * (fp16 / bf16 recurrent products, fp32 accumulation, gates, cell state and saved values).
  * Same contract as ensvs_lstm_fwd / ensvs_lstm_bwd (the MultiTrackLSTMEncoder H = 512 and the
  * SeparateF0 decoders' H = 256 of nnsvs/model.py:1483-1490, 861-869).  wpack: W_hh of both
  * directions packed by ensvs_lstm_coop_pack (bwd = 0: forward fp16 fragments, bwd = 1:
- * backward bf16 fragments of W_hh^T), 2*4*H*H 2-byte elements.  work: 256-B aligned,
- * ensvs_lstm_coop_work_bytes(H) bytes, caller-owned, one per concurrent launch; bytes
- * 128..131 read non-zero after a launch whose grid could not become resident. */
+ * backward bf16 fragments of W_hh^T), 2*4*H*H 2-byte elements.  Sequences run in tiles of
+ * 32 (blockIdx.z), each tile an independent hand-off group.  work: 256-B aligned,
+ * ensvs_lstm_coop_work_bytes(H, B) bytes, caller-owned, one per concurrent launch: ceil(B/32)
+ * 256-B tile headers, then the tiles' slabs; header bytes 128..131 of a tile read non-zero
+ * after a launch in which that tile's grid could not become resident (see
+ * ensvs_coop_set_error_word for the persistent flag). */
 /* MFMA recurrence for H = 64 / 128 in production (bf16 GEMM) precision (lstm_mfma.hip): the
  * structure of the persistent kernels above (one workgroup per (sequence, direction), chunked
  * LDS staging) with the recurrent product h W_hh^T (fp16 fragments) / dG W_hh (bf16) on MFMA,
@@ -208,7 +211,7 @@ int ensvs_lstm_mfma_bwd(const float* dy, int lddy, const void* wpack, const long
                         int B, int T, int H, const float* saved, float* dg, int lddg,
                         void* dgbf, int lddgb, float* bsum, void* stream);
 int ensvs_lstm_coop_supported(int B, int H);
-long long ensvs_lstm_coop_work_bytes(int H);
+long long ensvs_lstm_coop_work_bytes(int H, int B);
 int ensvs_lstm_coop_pack(const float* whh_f, const float* whh_r, int H, int bwd, void* out,
                          void* stream);
 int ensvs_lstm_coop_fwd(const float* gx, int ldg, const void* wpack, const long long* lengths,
@@ -234,17 +237,27 @@ int ensvs_ardec_bwd(const float* glf0, const float* gres, const float* wpb, cons
                     const float* wfo, int ldwfo, const float* mask, int teacher, int B, int T,
                     int H, float in_min, float in_max, float mean, float scale, const float* sg,
                     const float* sc, const float* so, float* dg, float* do4, void* stream);
-/* Cooperative AR decoder for H in {128, 256}, B <= 32 in production (bf16 GEMM) precision:
+/* Cooperative AR decoder for H in {128, 256}, B <= 256 in production (bf16 GEMM) precision:
  * one launch for all T/4 steps, the recurrence W_hh [h_1 .. h_B] split over H/16 workgroups
  * that keep their W_hh slice in registers (fp16 forward, bf16 W_hh^T backward, fp32
  * accumulation, gates, cell state, feat_out and saved values) and exchange h / dG plus the
  * feat_out / prenet partial sums through `work` every step.  Same contract and saved layout as
  * ensvs_ardec_fwd / ensvs_ardec_bwd (tacotron_f0.py:183-228).  wpack: ensvs_ardec_coop_pack
  * (bwd = 0 forward fp16 fragments, bwd = 1 backward bf16 fragments), 4*H*H 2-byte elements;
- * work: 256-B aligned, ensvs_ardec_coop_work_bytes(H) bytes, caller-owned, one per concurrent
- * launch; bytes 128..131 read non-zero after a launch whose grid could not become resident. */
+ * sequences in tiles of 32 (blockIdx.y) as the LSTM above; work: 256-B aligned,
+ * ensvs_ardec_coop_work_bytes(H, B) bytes, caller-owned, one per concurrent launch, laid out
+ * and flagged as the LSTM's. */
 int ensvs_ardec_coop_supported(int B, int H);
-long long ensvs_ardec_coop_work_bytes(int H);
+long long ensvs_ardec_coop_work_bytes(int H, int B);
+/* Failure controls of every cooperative launch (coop.h).  A tile whose workgroups cannot all
+ * become resident times out after `us` microseconds (default 1 s) of polling, releases its
+ * waiters (the launch ends within one timeout) and ORs 1 into the registered persistent device
+ * word (4-B aligned, caller-owned, never cleared by the library; NULL unregisters).  The word
+ * is read by ensvs_l2norm_chk / ensvs_poison_on_error, so the training step skips its update.
+ * ensvs_coop_inject_fault(1) is a test switch: workgroup 0 of tile 0 skips its step-1 signal. */
+int ensvs_coop_set_error_word(unsigned* word);
+int ensvs_coop_set_timeout_us(long long us);
+int ensvs_coop_inject_fault(int on);
 int ensvs_ardec_coop_pack(const float* whh, int H, int bwd, void* out, void* stream);
 int ensvs_ardec_coop_fwd(const float* gx, int ldgx, const float* ofx, int ldo, const void* wpack,
                          const float* wih_p, const float* wfo, int ldwfo, const float* score,
@@ -348,6 +361,13 @@ int ensvs_lf0_interaction(const float* lf0_m, const float* lf0_s, const float* y
 /* clip_grad_norm_ + torch.optim.Adam over the flat parameter buffer
  * (bin/train_acoustic_multitrack.py:369-380). */
 int ensvs_l2norm(const float* x, long long n, float* part, float* norm_out, void* stream);
+/* ensvs_l2norm whose result is NaN when *err != 0 (a failed cooperative recurrence, see
+ * ensvs_coop_set_error_word): the non-finite-norm skip then drops the step's update. */
+int ensvs_l2norm_chk(const float* x, long long n, float* part, float* norm_out,
+                     const unsigned* err, void* stream);
+/* x[0] = NaN when *err != 0: before a data-parallel all-reduce, so every rank's norm is NaN
+ * and every rank skips the update when any rank's recurrence failed. */
+int ensvs_poison_on_error(const unsigned* err, float* x, void* stream);
 int ensvs_adam(float* p, float* g, float* m, float* v, long long n, const float* norm,
                float max_norm, float lr, float b1, float b2, float eps, float bc1,
                float sqrt_bc2, void* stream);

@@ -1,8 +1,8 @@
 """Cooperative AR residual-F0 decoder (ensvs_ardec_coop_fwd / _bwd, ardec.hip) against the exact
 per-sequence kernels (ensvs_ardec_fwd / _bwd, fp32; themselves pinned to the reference decoder,
 tacotron_f0.py:126-237, by the lf0-model goldens of test_multitrack_gpu.py) on the same inputs:
-free-running and teacher-forced, the recipe's H = 256 at the bench's 30 sequences x 1024 frames
-and H = 128 at a ragged batch of 5.  The cooperative kernels run the recurrent products in
+free-running and teacher-forced, the recipe's H = 256 at the bench's 30 sequences x 1024 frames,
+H = 128 at a ragged batch of 5, and batches of 33 / 64 / 70 sequences (2-3 tiles of 32).  The cooperative kernels run the recurrent products in
 fp16 (forward) / bf16 (backward) with fp32 accumulation, as the recipe's fp16 autocast runs the
 LSTMCell (myconfig_notuseIL.yaml:6).  Bounds (max-abs relative): outputs and saved state 1e-3,
 gate / feat_out / W_hh gradients 3e-3 (measured: outputs <= 1.1e-4, gradients <= 5e-4;
@@ -36,6 +36,12 @@ def _inputs(B, T, H, seed):
     return {k: v.cuda().contiguous() for k, v in d.items()}
 
 
+def _resident(work, B):
+    """Every 32-sequence tile's residency flag (byte 128 of its 256-B header) clear."""
+    return all(work[256 * z + 128:256 * z + 132].cpu().view(torch.int32).item() == 0
+               for z in range((B + 31) // 32))
+
+
 def _run(a, B, T, H, coop, teacher):
     st = torch.cuda.current_stream().cuda_stream
     Tr = T // 4
@@ -53,7 +59,7 @@ def _run(a, B, T, H, coop, teacher):
              out["so"].data_ptr(), dg.data_ptr(), do4.data_ptr())
     if coop:
         assert query("ensvs_ardec_coop_supported", B, H) == 1
-        nbytes = query("ensvs_ardec_coop_work_bytes", H)
+        nbytes = query("ensvs_ardec_coop_work_bytes", H, B)
         work = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
         wf = torch.empty(4 * H * H, dtype=torch.float16, device=dev)
         wb = torch.empty(4 * H * H, dtype=torch.bfloat16, device=dev)
@@ -61,10 +67,10 @@ def _run(a, B, T, H, coop, teacher):
         call("ensvs_ardec_coop_pack", a["whh"].data_ptr(), H, 1, wb.data_ptr(), st)
         call("ensvs_ardec_coop_fwd", a["gx"].data_ptr(), 4 * H, a["ofx"].data_ptr(), 4,
              wf.data_ptr(), *ins, *outs, work.data_ptr(), nbytes, st)
-        assert work[128:132].cpu().view(torch.int32).item() == 0  # every workgroup resident
+        assert _resident(work, B)  # every workgroup of every tile resident
         call("ensvs_ardec_coop_bwd", a["glf0"].data_ptr(), a["gres"].data_ptr(), wb.data_ptr(),
              *bargs, work.data_ptr(), nbytes, st)
-        assert work[128:132].cpu().view(torch.int32).item() == 0
+        assert _resident(work, B)
     else:
         wpf = torch.empty(4 * H * H, device=dev)
         wpb = torch.empty(4 * H * H, device=dev)
@@ -83,6 +89,10 @@ def _run(a, B, T, H, coop, teacher):
     (256, 30, 1024, True),
     (256, 32, 256, False),
     (128, 5, 200, False),
+    # B > 32: tiles of 32 sequences (the recipe's batch_by_size packs up to 32 000 frames)
+    (256, 33, 128, False),
+    (256, 64, 512, True),
+    (128, 70, 120, False),
 ])
 def test_ardec_coop_matches_exact(H, B, T, teacher):
     a = _inputs(B, T, H, H + B + T)

@@ -99,6 +99,10 @@ def parse():
                     help="skip the per-launch census and kernel rooflines")
     ap.add_argument("--no-config2", action="store_true",
                     help="skip the single-track (BASELINE config 2) training leg")
+    ap.add_argument("--no-shapes", action="store_true",
+                    help="skip the 60 x 512 and ragged-length legs of the main model")
+    ap.add_argument("--no-real-data", action="store_true",
+                    help="skip the on-disk data-path leg (feeder + train_epoch)")
     ap.add_argument("--cpu-pairs", type=int, default=10)
     ap.add_argument("--cpu-frames", type=int, default=1024)
     return ap.parse_args()
@@ -214,8 +218,10 @@ def step_census(model, opt, batch):
     engine.set_concurrency(False)
     try:
         torch.cuda.synchronize()
+        a0 = torch.cuda.memory_stats(opt.flat.device)["allocated_bytes.all.allocated"]
         train_step(model, opt, *batch)
         torch.cuda.synchronize()
+        alloc = torch.cuda.memory_stats(opt.flat.device)["allocated_bytes.all.allocated"] - a0
     finally:
         for m in patched:
             m.call = orig_call
@@ -226,7 +232,7 @@ def step_census(model, opt, batch):
         a = agg.setdefault((name, t), [0, 0.0])
         a[0] += 1
         a[1] += s.elapsed_time(e)
-    return agg, sum(v[1] for v in agg.values())
+    return agg, sum(v[1] for v in agg.values()), alloc
 
 
 # MI355X per-CU VALU rate (fp32 FMA: one wave64 instruction per 4 cycles per SIMD) at the
@@ -521,6 +527,15 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
+def _host_cores():
+    cores = os.cpu_count() or 1
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    return min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+
+
 def cpu_baseline(args):
     """The oracle (CPU PyTorch restatement of the reference, fused CPU LSTM) on the host
     cores, BASELINE.md §3: full-size model, P pairs x T frames fp32 (10 x
@@ -528,12 +543,7 @@ def cpu_baseline(args):
     speed to the reference's own train_step."""
     from oracle import ensvs_oracle as O
     from oracle.weights import seeded_state_dict
-    cores = os.cpu_count() or 1
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        pass
-    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    cores = _host_cores()
     torch.set_num_threads(cores)
     cfg = configs.multitrack_diffusion(num_speakers=4)
     model = configs.instantiate(cfg)
@@ -613,34 +623,179 @@ def il_train(args, dev):
                 grad_norm=norm.item())
 
 
-def sf0_train(args, dev, steps=4):
-    """The recipe's default acoustic model (MultiTrackMultistreamSeparateF0ParametricModel,
-    multitrack_acoustic_nnsvs_world_multi_ar_f0.yaml; config.yaml:93-95): concatenation-fusion
-    MultiTrackLSTMEncoder (H = 512 x 3 layers), teacher-forced multi-track lf0 model, main
-    and sub FFConvLSTM decoders (H = 256 / 64 / 62), masked L1 over both tracks; same
-    per-GPU workload, graph replay, bf16 GEMM operands.  276.5 MFLOP per frame (SURVEY.md
-    section 6); the reference CPU path trains it at ~290 frames/s (8 threads, SURVEY probe)."""
-    torch.manual_seed(20250324)
-    model = configs.instantiate(configs.multitrack_separate_f0(num_speakers=4)).to(dev)
-    opt = FusedAdam(model, lr=1e-4, clip_norm=1.0)
-    P, T = args.pairs, args.frames
-    b = data.synthetic_batch(P, T, 4000)
-    g = lambda k: torch.from_numpy(b[k]).to(dev).contiguous()  # noqa: E731
+SF0_TRAIN_FLOP_PER_FRAME = 276.5e6  # SURVEY.md section 6 (torch.utils.flop_counter on the oracle)
+
+
+def _graphed_leg(model, opt, P, T, seed, steps, lengths=None, warmup=1):
+    """Graph-replayed training steps of `model` on a synthetic P x T batch (optionally ragged
+    `lengths`, fixed across steps): (ms per step, valid main-track frames per step, loss,
+    grad norm)."""
+    b = data.synthetic_batch(P, T, seed, lengths=lengths)
+    g = lambda k: torch.from_numpy(b[k]).to(opt.flat.device).contiguous()  # noqa: E731
     step = GraphedTrainStep(model, opt, g("x_main"), g("x_sub"), g("y_main"), g("spk_main"),
                             g("spk_sub"), b["lengths"].tolist(), warmup=1).step
-    step()
+    for _ in range(max(0, warmup - 1)):
+        step()
     torch.cuda.synchronize()
     t0 = time.time()
     for _ in range(steps):
         loss, norm = step()
     torch.cuda.synchronize()
     el = time.time() - t0
-    v = P * T * steps / el
-    return dict(metric="recipe-default acoustic model train frames/sec (SeparateF0, "
-                       "MultiTrackLSTMEncoder H=512)", value=v, unit="main-track frames/s",
-                ms_per_step=el / steps * 1e3, steps=steps, pairs=P, frames=T,
-                dtype=engine.gemm_precision(), train_loss=loss.item(), grad_norm=norm.item(),
-                model_tflops_per_s=v * 276.5e6 / 1e12)
+    return el / steps * 1e3, int(b["lengths"].sum()), loss.item(), norm.item()
+
+
+def sf0_train(args, dev, steps=4):
+    """The recipe's default acoustic model (MultiTrackMultistreamSeparateF0ParametricModel,
+    multitrack_acoustic_nnsvs_world_multi_ar_f0.yaml; config.yaml:93-95): concatenation-fusion
+    MultiTrackLSTMEncoder (H = 512 x 3 layers), teacher-forced multi-track lf0 model, main
+    and sub FFConvLSTM decoders (H = 256 / 64 / 62), masked L1 over the main output; same
+    per-GPU workload, graph replay, bf16 GEMM operands, and the same 30 720 frames as 60
+    pairs x 512 (two 32-sequence tiles of the cooperative recurrences).  276.5 MFLOP per
+    frame."""
+    torch.manual_seed(20250324)
+    model = configs.instantiate(configs.multitrack_separate_f0(num_speakers=4)).to(dev)
+    opt = FusedAdam(model, lr=1e-4, clip_norm=1.0)
+    P, T = args.pairs, args.frames
+    ms, frames, loss, norm = _graphed_leg(model, opt, P, T, 4000, steps)
+    v = frames / ms * 1e3
+    tf = v * SF0_TRAIN_FLOP_PER_FRAME / 1e12
+    out = dict(metric="recipe-default acoustic model train frames/sec (SeparateF0, "
+                      "MultiTrackLSTMEncoder H=512)", value=v, unit="main-track frames/s",
+               ms_per_step=ms, steps=steps, pairs=P, frames=T, dtype=engine.gemm_precision(),
+               train_loss=loss, grad_norm=norm, model_tflops_per_s=tf,
+               roofline={"bound": "mfma", "achieved": tf, "peak": PEAK_BF16_TFLOPS,
+                         "unit": "TFLOP/s", "frac": tf / PEAK_BF16_TFLOPS, "traffic": None,
+                         "work": f"{SF0_TRAIN_FLOP_PER_FRAME / 1e6:.1f} MFLOP per main-track "
+                                 "frame (forward + backward GEMM / conv / LSTM FLOPs, SURVEY.md "
+                                 "section 6) x frames/s"})
+    P2, T2 = 2 * P, T // 2
+    ms2, frames2, loss2, norm2 = _graphed_leg(model, opt, P2, T2, 4001, steps)
+    out[f"p{P2}x{T2}"] = dict(value=frames2 / ms2 * 1e3, ms_per_step=ms2, pairs=P2, frames=T2,
+                              train_loss=loss2, grad_norm=norm2,
+                              ratio_to_p30=(frames2 / ms2) / (frames / ms))
+    return out
+
+
+def sf0_cpu_baseline(pairs=4, frames=512, warm=1, timed=3):
+    """The oracle's SeparateF0 training step (separate_f0_forward with teacher forcing, the
+    main output's masked L1, backward, clip + Adam) on the host cores: a bounded sample of
+    the leg's workload (the CPU needs ~7 s per 2 048-frame step)."""
+    from oracle import ensvs_oracle as O
+    from oracle.weights import seeded_state_dict
+    cores = _host_cores()
+    torch.set_num_threads(cores)
+    cfg = configs.multitrack_separate_f0(num_speakers=4)
+    model = configs.instantiate(cfg)
+    shapes = {k: tuple(v.shape) for k, v in model.state_dict().items()}
+    del model
+    P = {k: torch.from_numpy(v) for k, v in seeded_state_dict(shapes, 2).items()}
+    trainable = [k for k in P if "running" not in k and "num_batches" not in k]
+    b = data.synthetic_batch(pairs, frames, 9)
+    x = [torch.from_numpy(b[k]) for k in ("x_main", "x_sub")]
+    y = [torch.from_numpy(b[k]) for k in ("y_main", "y_sub")]
+    spk = (torch.from_numpy(b["spk_main"]), torch.from_numpy(b["spk_sub"]))
+    rng = torch.Generator().manual_seed(4)
+    state, times = {}, []
+    for step in range(warm + timed):
+        for k in trainable:
+            P[k] = P[k].detach().requires_grad_()
+        draws = dict(lf0_main=(torch.rand(pairs, frames // 4, 1, generator=rng) < 0.5).float() * 2,
+                     lf0_sub=(torch.rand(pairs, frames // 4, 1, generator=rng) < 0.5).float() * 2)
+        t0 = time.time()
+        (om, _), _ = O.separate_f0_forward(P, cfg, x[0], x[1], spk, b["lengths"].tolist(), y,
+                                           draws, training=True, bn_updates={}, fast=True)
+        loss = O.masked_l1_loss(O.split_streams(om, cfg["stream_sizes"]), y[0], b["lengths"],
+                                cfg["stream_sizes"])
+        loss.backward()
+        grads = {k: P[k].grad for k in trainable if P[k].grad is not None}
+        params = {k: P[k].detach() for k in grads}
+        O.clip_and_adam(params, grads, state, step=step + 1)
+        P.update(params)
+        times.append(time.time() - t0)
+    sec = float(np.median(times[warm:]))
+    return dict(value=pairs * frames / sec, unit="main-track frames/s", cores=cores, kind="port",
+                cpu_model=_cpu_model(),
+                sample=f"oracle SeparateF0 step (CPU PyTorch restatement, fused CPU LSTM), "
+                       f"{pairs} pairs x {frames} frames fp32, median of {timed} steps after "
+                       f"{warm} warm-up ({sum(times):.1f} s of CPU work)")
+
+
+def shape_legs(args, dev, model, opt, base_ms, steps=5):
+    """The main line's model at other batch shapes of the same workload size (graph replay):
+    60 pairs x 512 frames (the recipe's batch_by_size packs up to 32 000 frames, so short
+    pairs come 60+ to a batch: two 32-sequence tiles of the cooperative AR decoder) and the
+    30 x 1024 batch with ragged lengths U[T/2, T] (multiples of 4; the recurrences run to
+    each sequence's own length, the per-frame kernels over the padded batch)."""
+    P, T = args.pairs, args.frames
+    out = {}
+    ms, frames, loss, norm = _graphed_leg(model, opt, 2 * P, T // 2, 1500, steps)
+    out[f"p{2 * P}x{T // 2}"] = dict(value=frames / ms * 1e3, ms_per_step=ms, pairs=2 * P,
+                                     frames=T // 2, train_loss=loss, grad_norm=norm,
+                                     ratio_to_main=base_ms / ms)
+    rng = np.random.default_rng(8)
+    lens = (rng.integers(T // 2, T + 1, size=P) // 4) * 4
+    ms, frames, loss, norm = _graphed_leg(model, opt, P, T, 1501, steps, lengths=lens)
+    out[f"ragged_p{P}x{T}"] = dict(
+        value=frames / ms * 1e3, unit="valid main-track frames/s", ms_per_step=ms,
+        padded_frames_per_s=P * T / ms * 1e3, valid_fraction=frames / (P * T), pairs=P,
+        frames=T, lengths="U[T/2, T], multiples of 4", train_loss=loss, grad_norm=norm,
+        ratio_to_main=(frames / ms) / (P * T / base_ms))
+    return out
+
+
+def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
+    """The path a user runs (train_acoustic_multitrack.py:461-563): synthetic on-disk
+    `-feats.npy` corpus (4 SATB parts x `segments` songs, lengths U[256, 2048] per song),
+    file pairing, shuffled batch_by_size(32 000 frames) buckets, PairBatchFeeder (reader
+    thread -> pinned buffers -> copy stream) and train.train_epoch (eager: every batch has
+    its own shape).  One untimed epoch, then `epochs` timed ones."""
+    import tempfile
+    from ensemble_svs_with_interactions_amd import loader
+    from ensemble_svs_with_interactions_amd.train import train_epoch
+    rng = np.random.default_rng(21)
+    spks = ["S", "A", "T", "B"]
+    with tempfile.TemporaryDirectory() as root:
+        dirs = {k: os.path.join(root, "dump", s, d) for k, s, d in
+                (("in", "norm", "in_acoustic"), ("out", "norm", "out_acoustic"),
+                 ("times", "org", "in_acoustic"))}
+        for d in dirs.values():
+            os.makedirs(d)
+        for i in range(segments):
+            n = int(rng.integers(256, 2049))
+            sb = data.synthetic_batch(4, n, 7000 + i)
+            for j, spk in enumerate(spks):
+                seg = f"song_{i:03d}"
+                np.save(os.path.join(dirs["in"], f"{spk}_{seg}-feats.npy"), sb["x_main"][j])
+                np.save(os.path.join(dirs["out"], f"{spk}_{seg}-feats.npy"), sb["y_main"][j])
+                np.save(os.path.join(dirs["times"], f"{spk}_{seg}-times.npy"),
+                        np.arange(5) * 50000)
+        torch.manual_seed(20250325)
+        model = configs.instantiate(configs.multitrack_diffusion(num_speakers=4)).to(dev)
+        opt = FusedAdam(model, lr=1e-4, clip_norm=1.0)
+        np.random.seed(1)
+        ds, batches = loader.setup_multitrack_batches(dirs["in"], dirs["out"], spks,
+                                                      batch_max_frames=batch_max_frames,
+                                                      allow_cache=True)
+        feeder = loader.PairBatchFeeder(ds, batches, device=dev)
+        valid = sum(max(ds.lengths[i]) for b in batches for i in b)
+        padded = sum(len(b) * max(max(ds.lengths[i]) for i in b) for b in batches)
+        train_epoch(model, opt, feeder)  # warm-up: caches, workspaces, file cache
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for _ in range(epochs):
+            res = train_epoch(model, opt, feeder)
+        torch.cuda.synchronize()
+        el = (time.time() - t0) / epochs
+    sizes = [len(b) for b in batches]
+    return dict(metric="acoustic-model train frames/sec on the on-disk data path (feeder + "
+                       "train_epoch, ragged dynamic batches)",
+                value=valid / el, unit="main-track frames/s (pair length max(L_main, L_sub))",
+                padded_frames_per_s=padded / el, s_per_epoch=el, steps_per_epoch=len(batches),
+                pairs=sum(sizes), pairs_per_batch=[min(sizes), max(sizes)],
+                batch_max_frames=batch_max_frames, lengths="U[256, 2048] per song",
+                execution="eager train_step per batch (shapes change every step)",
+                last_loss=float(res[-1][0].item()), dtype=engine.gemm_precision())
 
 
 def config2_train(args, dev):
@@ -780,7 +935,19 @@ def main():
                 "SURVEY.md section 8(d)) x frames/s per GPU",
         "gate_gemm_live": _gate_roofline(args, P, T, sec, sec_call, flops, gbytes)}
     if world == 1 and not args.no_census:
-        agg, serial_ms = step_census(model, opt, (xm, xs, ym, s0, s1, lens))
+        agg, serial_ms, alloc = step_census(model, opt, (xm, xs, ym, s0, s1, lens))
+        # step-level algorithmic bytes: every tensor the step materialises written once and
+        # read once (2 x the bytes the step allocates: activations, saved state, gradients
+        # of activations, bf16 copies), plus 9 passes over the flat fp32 parameters (weight
+        # repack read, zero_grad, clip + Adam: p, g, m, v read, p, m, v written)
+        flat_bytes = opt.flat.numel() * 4
+        alg = 2 * alloc + 9 * flat_bytes
+        roof["algorithmic_bytes"] = alg
+        roof["algorithmic_bytes_model"] = (
+            f"2 x {alloc / 1e9:.2f} GB allocated by one eager step (each tensor written once, "
+            f"read once) + 9 x {flat_bytes / 1e6:.0f} MB of flat parameters")
+        if roof["traffic"]:
+            roof["traffic_over_algorithmic"] = roof["traffic"] / alg
         roof["kernels"], roof["recurrences"] = kernel_rooflines(agg, serial_ms, P, T)
         rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
         census = {"serial_step_ms": serial_ms, "launches": sum(v[0] for v in agg.values()),
@@ -815,6 +982,11 @@ def main():
     }
     if world == 1 and not args.no_census:
         out["census"] = census
+    if not args.no_shapes and world == 1:
+        out["shapes"] = shape_legs(args, dev, model, opt, elapsed / args.steps * 1e3)
+    if not args.no_real_data and world == 1:
+        out["real_data"] = real_data_train(args, dev)
+        out["real_data"]["ratio_to_fixed_shape"] = out["real_data"]["value"] / value
     if not args.no_sf0 and world == 1:
         out["separate_f0"] = sf0_train(args, dev)
     if not args.no_config2 and world == 1:
@@ -824,6 +996,8 @@ def main():
         out["synth"] = synth_rtf(model, dev)
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(args)
+        if "separate_f0" in out:
+            out["separate_f0"]["cpu_baseline"] = sf0_cpu_baseline()
         if "synth" in out:
             out["synth"]["cpu_baseline"] = cpu_synth_baseline(out["synth"]["frames"])
     print(json.dumps(out), flush=True)

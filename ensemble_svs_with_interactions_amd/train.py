@@ -144,11 +144,18 @@ class FusedAdam(torch.optim.Optimizer):
         if len(groups) != 1 or len(groups[0]["params"]) != len(self.param_groups[0]["params"]):
             raise ValueError("optimizer state does not match this model's parameters")
         g = groups[0]
+        if float(g.get("weight_decay", 0.0)) != 0.0 or g.get("amsgrad", False):
+            raise NotImplementedError("weight_decay / amsgrad state")
+        new_b = tuple(g.get("betas", self.betas))
+        new_e = float(g.get("eps", self.eps))
+        if getattr(self, "_captured", False) and (new_b != tuple(self.betas) or new_e != self.eps):
+            # a GraphedTrainStep baked b1, b2, eps into its captured Adam launch
+            raise ValueError("FusedAdam.load_state_dict: betas / eps differ from the ones a "
+                             "captured GraphedTrainStep replays; load the state before "
+                             "capturing (or capture a new GraphedTrainStep)")
         for k in ("lr", "betas", "eps"):
             if k in g:
                 self.param_groups[0][k] = tuple(g[k]) if k == "betas" else float(g[k])
-        if float(g.get("weight_decay", 0.0)) != 0.0 or g.get("amsgrad", False):
-            raise NotImplementedError("weight_decay / amsgrad state")
         self.betas, self.eps = tuple(self.param_groups[0]["betas"]), self.param_groups[0]["eps"]
         ids = g["params"]
         st = state_dict["state"]
@@ -165,6 +172,15 @@ class FusedAdam(torch.optim.Optimizer):
             steps.add(float(s["step"]))
         if len(steps) > 1:
             raise ValueError(f"per-parameter step counts differ: {sorted(steps)}")
+        n_state = sum(1 for i in ids if st.get(i))
+        if 0 < n_state < len(ids):
+            # one device step count serves every parameter: the ones without state get zero
+            # moments but the shared count's bias correction (torch.optim.Adam would start
+            # them at step 1)
+            import warnings
+            warnings.warn(f"FusedAdam.load_state_dict: optimizer state for {n_state} of "
+                          f"{len(ids)} parameters; the others start from zero moments with the "
+                          "shared step count", RuntimeWarning, stacklevel=2)
         c = steps.pop() if steps else 0.0
         b1, b2 = self.betas
         self._lr = None
@@ -566,6 +582,7 @@ class GraphedTrainStep:
             self.loss = self._grads()
         with torch.cuda.graph(self.g_update, pool=self.g_grads.pool()):
             optimizer.step()
+        optimizer._captured = True  # b1, b2, eps are now kernel arguments of g_update
         self.norm = optimizer.norm
 
     def _grads(self):

@@ -78,3 +78,21 @@ def test_steplr_drives_lr_and_round_trips():
     s2.step()
     sched.step()
     assert opt2.lr == opt.lr
+
+
+def test_load_guards():
+    """betas / eps of a captured GraphedTrainStep's Adam launch cannot change under it, and
+    a checkpoint covering only some parameters is loaded with a warning."""
+    model, opt = _fused()
+    sd = opt.state_dict()
+    opt._captured = True  # as GraphedTrainStep marks it
+    opt.load_state_dict(sd)  # same betas / eps: fine
+    bad = opt.state_dict()
+    bad["param_groups"][0]["betas"] = (0.5, 0.9)
+    with pytest.raises(ValueError):
+        opt.load_state_dict(bad)
+    opt._captured = False
+    part = opt.state_dict()
+    del part["state"][0]
+    with pytest.warns(RuntimeWarning):
+        opt.load_state_dict(part)

@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 for rep in 1 2; do
   for lib in "" "$@"; do
     ENSVS_LIB=$lib timeout -k 10 240 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline \
-      --no-synth --no-sf0 --no-census --no-config2 2>/dev/null | \
+      --no-synth --no-sf0 --no-census --no-config2 --no-shapes --no-real-data 2>/dev/null | \
       python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('lib=[$lib]', round(d['ms_per_step'], 3), 'ms')" || exit 1
   done
 done

@@ -7,7 +7,7 @@ root=$(pwd)
 for rep in 1 2; do
   for d in "$@"; do
     (cd "$root/$d" && ENSVS_LIB= timeout -k 10 240 python -u bench.py --steps 20 --warmup 3 \
-      --no-cpu-baseline --no-synth --no-sf0 --no-census --no-config2 2>/dev/null) | \
+      --no-cpu-baseline --no-synth --no-sf0 --no-census --no-config2 --no-shapes --no-real-data 2>/dev/null) | \
       python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('tree=[$d]', round(d['ms_per_step'], 3), 'ms')" || exit 1
   done
 done

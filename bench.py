@@ -240,6 +240,8 @@ def step_census(model, opt, batch):
 CU_FMA_PER_S = 64 * 2.4e9
 # one v_mfma_f32_16x16x32 (16 cycles) per SIMD, 4 SIMDs per CU
 CU_MFMA16_PER_S = 4 * 2.4e9 / 16
+# per AR step: handoff-flag (1.3 us, drained sc1, idle) + 16 KB payload read (~1.0 us)
+COOP_HANDOFF_FLOOR_NS = 2300.0
 RECURRENCES = ("ensvs_lstm_fwd", "ensvs_lstm_bwd", "ensvs_lstm_mfma_fwd", "ensvs_lstm_mfma_bwd",
                "ensvs_ardec_fwd", "ensvs_ardec_bwd", "ensvs_ardec_coop_fwd",
                "ensvs_ardec_coop_bwd")
@@ -311,9 +313,12 @@ def kernel_rooflines(agg, serial_ms, P, T, C=256, E=256):
                             "(latency-bound: one workgroup per sequence-direction)")
         elif "coop" in name:
             steps //= 4  # r = 4 frames per AR step
-            floor_ns = None
-            ent["floor"] = ("per-step cross-workgroup hand-off of h / dG (H/16 workgroups, "
-                            "coop.h); no compute floor quoted")
+            floor_ns = COOP_HANDOFF_FLOOR_NS
+            ent["floor"] = ("per-step all-to-all hand-off of h / dG among the H/16 workgroups "
+                            "(coop.h): MI355X_MICROARCH.md price list, handoff-flag with drained "
+                            "sc1 stores 1.3 us idle + the 16 KB slab read latency-bound at "
+                            "~16 GB/s per consumer (handoff-payload) 1.0 us; the step's MFMA "
+                            "work (4H/16 x 4 tiles per workgroup) hides under the read")
         else:
             # LSTMCell W_hh + the prenet column of W_ih + feat_out per AR step (r = 4 frames)
             steps //= 4

@@ -2227,22 +2227,25 @@ __device__ __forceinline__ bf16x8 wg_frag(const char* img, int c0, int lane) {
 // workgroup index w inside the split and s = 8 (b / 8 / W) + xcd.  Bijective; the partial of
 // split s covers the same rows as before, so the results are bitwise unchanged.  (Grouping by
 // (split, tap) instead measured 17.50 vs 17.40 ms/step; the raw order 17.72.)
+// Any split count: XCD x receives the hardware ids b = x (mod 8), count_x = q + (x < r) of
+// them for total = 8 q + r workgroups; it runs the contiguous range [x q + min(x, r), + count_x)
+// of the split-major (split, tap, K tile, N tile) order, so a split's workgroups share one XCD
+// (a split straddles two XCDs at most at a range boundary).  The first version required
+// splits % 8 == 0 and left the DiffNet dilated conv's 21 splits in raw order (2.8x its operand
+// bytes fetched, profiles/r3_step_pmc.json).
 __device__ __forceinline__ void wgrad_tile(const WgradArgs& a, int& n0, int& k0, int& j, int& s) {
   const int gx = gridDim.x, gy = gridDim.y;
-  if (a.splits % 8 == 0) {
-    const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    const int W = gx * gy * a.taps;  // workgroups per split
-    const int k = b >> 3, w = k % W;
-    s = (k / W) * 8 + (b & 7);
-    n0 = (w % gx) * BM;
-    k0 = ((w / gx) % gy) * BN;
-    j = w / (gx * gy);
-  } else {
-    n0 = blockIdx.x * BM;
-    k0 = blockIdx.y * BN;
-    j = blockIdx.z % a.taps;
-    s = blockIdx.z / a.taps;
-  }
+  const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int total = gx * gy * gridDim.z;
+  const int q = total >> 3, r = total & 7, x = b & 7;
+  const int idx = x * q + min(x, r) + (b >> 3);
+  const int W = gx * gy * a.taps;  // workgroups per split
+  s = idx / W;
+  const int w = idx - s * W;
+  j = w / (gx * gy);
+  const int t = w - j * gx * gy;
+  k0 = (t / gx) * BN;
+  n0 = (t % gx) * BM;
 }
 
 template <typename T, bool VEC>

@@ -386,7 +386,7 @@ int launch_fwd(const float* gx, int ldg, const float* w0, const float* w1,
     return ENSVS_E_ARG;
   const size_t lds = excl_lds(Geo<H>::FWD_LDS);
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)lstm_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 
+      (const void*)lstm_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)std::max<size_t>(lds, 160 * 1024));  // the exclusive size, whatever this launch asks
   if (attr != hipSuccess) return ENSVS_E_HIP;
   hipLaunchKernelGGL(lstm_fwd_kernel<H>, dim3(B, 2), dim3(Geo<H>::TF), lds, st,
@@ -403,7 +403,7 @@ int launch_bwd(const float* dy, int lddy, const float* w0, const float* w1,
     return ENSVS_E_ARG;
   const size_t lds = excl_lds(Geo<H>::BWD_LDS);
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)lstm_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 
+      (const void*)lstm_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)std::max<size_t>(lds, 160 * 1024));  // the exclusive size, whatever this launch asks
   if (attr != hipSuccess) return ENSVS_E_HIP;
   hipLaunchKernelGGL(lstm_bwd_kernel<H>, dim3(B, 2), dim3(Geo<H>::TB), lds, st,

@@ -408,7 +408,7 @@ int launch_fwd(const float* gx, int ldg, const void* wp, const long long* length
                float* y, int ldy, float* sv, __bf16* yb, int ldyb, hipStream_t st) {
   const size_t lds = excl(MGeo<H>::FWD_LDS);
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)lstm_mfma_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 
+      (const void*)lstm_mfma_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)std::max<size_t>(lds, 160 * 1024));  // the exclusive size, whatever this launch asks
   if (attr != hipSuccess) return ENSVS_E_HIP;
   hipLaunchKernelGGL(lstm_mfma_fwd_kernel<H>, dim3(B, 2), dim3(NT), lds, st, gx, ldg,
@@ -423,7 +423,7 @@ int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengt
                hipStream_t st) {
   const size_t lds = excl(MGeo<H>::BWD_LDS);
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)lstm_mfma_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 
+      (const void*)lstm_mfma_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)std::max<size_t>(lds, 160 * 1024));  // the exclusive size, whatever this launch asks
   if (attr != hipSuccess) return ENSVS_E_HIP;
   hipLaunchKernelGGL(lstm_mfma_bwd_kernel<H>, dim3(B, 2), dim3(NT), lds, st, dy, lddy,

@@ -217,6 +217,10 @@ __global__ __launch_bounds__(NT) void lstm_mfma_fwd_kernel(
       const float ig = sigm(a[0]), fg = sigm(a[1]), gg = tanh_fast(a[2]), og = sigm(a[3]);
       c = fg * c + ig * gg;
       const float h = og * tanh_fast(c);
+      // h on every lane before the branch: otherwise the compiler sinks the o gate (its gin
+      // read and activation) into the writing lanes' branch, a second LDS round trip after
+      // the MFMAs on every step
+      asm volatile("" ::"v"(h));
       if (act) {
         hb[(s & 1) * HP + u] = (_Float16)h;
         float* o = out + st * OW;
@@ -230,8 +234,12 @@ __global__ __launch_bounds__(NT) void lstm_mfma_fwd_kernel(
       __syncthreads();
     }
     if (ch + 1 < nch) store_in();
-    flush(ch);
+    // the next loads before this chunk's stores: vmcnt counts both in issue order, so loads
+    // issued after the stores made the compiler drain every store first (s_waitcnt vmcnt(0)
+    // at each chunk boundary; tools/lstm_phase_probe.py: global I/O cost 100-140 ns per
+    // step at H = 128)
     if (ch + 2 < nch) load_chunk(ch + 2);
+    flush(ch);
     __syncthreads();
   }
 }
@@ -388,8 +396,12 @@ __global__ __launch_bounds__(NT) void lstm_mfma_bwd_kernel(
       __syncthreads();
     }
     if (ch + 1 < nch) store_in();
-    flush(ch);
+    // the next loads before this chunk's stores: vmcnt counts both in issue order, so loads
+    // issued after the stores made the compiler drain every store first (s_waitcnt vmcnt(0)
+    // at each chunk boundary; tools/lstm_phase_probe.py: global I/O cost 100-140 ns per
+    // step at H = 128)
     if (ch + 2 < nch) load_chunk(ch + 2);
+    flush(ch);
     __syncthreads();
   }
   if (bsum && act) {

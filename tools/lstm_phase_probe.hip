@@ -9,6 +9,8 @@
 //   3 no global traffic (no chunk loads or flushes: LDS staging buffers reused)
 //   4 no LDS read of h / dG (constant MFMA operand; the MFMAs stay)
 //   5 barrier + loop only (nothing above)
+//   6 chunk flush only (no chunk loads)      7 chunk loads only (no flush)
+//   8 flush reads LDS and computes addresses but stores nothing
 // Outputs are garbage for modes > 0.  Built by tools/lstm_phase_probe.py into
 // tools/liblstm_probe.so (hipcc --offload-arch=gfx950).
 #include <hip/hip_runtime.h>
@@ -48,6 +50,7 @@ __global__ __launch_bounds__(NT) void probe_fwd(const float* __restrict__ gx, in
   constexpr int PF = CH * GW / 4 / NT;
   constexpr bool MF = MODE != 1 && MODE != 5, ACT = MODE != 2 && MODE != 5;
   constexpr bool GIO = MODE != 3 && MODE != 5, HRD = MODE != 4 && MODE != 5;
+  constexpr bool LDC = MODE != 6, FLS = MODE != 7, STO = MODE != 8;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* gin = lds;
   float* out = gin + CH * GW;
@@ -97,6 +100,10 @@ __global__ __launch_bounds__(NT) void probe_fwd(const float* __restrict__ gx, in
       const int s = ch * CH + st;
       const long long row = rowb + (dir ? L - 1 - s : s);
       const f32x4 val = *(const f32x4*)(out + st * OW + c4 * 4);
+      if (!STO) {
+        asm volatile("" ::"v"(val), "v"(row));
+        continue;
+      }
       if (c4 < H / 4) *(f32x4*)(y + row * ldy + dir * H + c4 * 4) = val;
       else *(f32x4*)(sv + (row * 2 + dir) * 5 * H + (c4 - H / 4) * 4) = val;
     }
@@ -167,9 +174,9 @@ __global__ __launch_bounds__(NT) void probe_fwd(const float* __restrict__ gx, in
       __syncthreads();
     }
     if (GIO) {
-      if (ch + 1 < nch) store_in();
-      flush(ch);
-      if (ch + 2 < nch) load_chunk(ch + 2);
+      if (LDC && ch + 1 < nch) store_in();
+      if (LDC && ch + 2 < nch) load_chunk(ch + 2);  // loads before the stores (lstm_mfma.hip)
+      if (FLS) flush(ch);
     }
     __syncthreads();
   }
@@ -186,6 +193,7 @@ __global__ __launch_bounds__(NT) void probe_bwd(const float* __restrict__ dy, in
   constexpr int PF = (NIN + NT - 1) / NT;
   constexpr bool MF = MODE != 1 && MODE != 5, ACT = MODE != 2 && MODE != 5;
   constexpr bool GIO = MODE != 3 && MODE != 5, HRD = MODE != 4 && MODE != 5;
+  constexpr bool LDC = MODE != 6, FLS = MODE != 7, STO = MODE != 8;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* gin = lds;
   float* out = gin + CH * IW;
@@ -239,7 +247,12 @@ __global__ __launch_bounds__(NT) void probe_bwd(const float* __restrict__ dy, in
       const int st = e / (GW / 4), c4 = e % (GW / 4);
       const int s = L - 1 - ch * CH - st;
       const long long row = rowb + (dir ? L - 1 - s : s);
-      *(f32x4*)(dg + row * lddg + dir * GW + c4 * 4) = *(const f32x4*)(out + st * GW + c4 * 4);
+      const f32x4 val = *(const f32x4*)(out + st * GW + c4 * 4);
+      if (!STO) {
+        asm volatile("" ::"v"(val), "v"(row));
+        continue;
+      }
+      *(f32x4*)(dg + row * lddg + dir * GW + c4 * 4) = val;
     }
   };
   if (GIO) {
@@ -311,9 +324,9 @@ __global__ __launch_bounds__(NT) void probe_bwd(const float* __restrict__ dy, in
       __syncthreads();
     }
     if (GIO) {
-      if (ch + 1 < nch) store_in();
-      flush(ch);
-      if (ch + 2 < nch) load_chunk(ch + 2);
+      if (LDC && ch + 1 < nch) store_in();
+      if (LDC && ch + 2 < nch) load_chunk(ch + 2);  // loads before the stores (lstm_mfma.hip)
+      if (FLS) flush(ch);
     }
     __syncthreads();
   }
@@ -348,7 +361,10 @@ void launch_mode(int mode, int bwd, const void* in, const void* wp, int B, int T
     case 2: launch<H, 2>(bwd, in, wp, B, T, o1, o2, st); break;
     case 3: launch<H, 3>(bwd, in, wp, B, T, o1, o2, st); break;
     case 4: launch<H, 4>(bwd, in, wp, B, T, o1, o2, st); break;
-    default: launch<H, 5>(bwd, in, wp, B, T, o1, o2, st); break;
+    case 5: launch<H, 5>(bwd, in, wp, B, T, o1, o2, st); break;
+    case 6: launch<H, 6>(bwd, in, wp, B, T, o1, o2, st); break;
+    case 7: launch<H, 7>(bwd, in, wp, B, T, o1, o2, st); break;
+    default: launch<H, 8>(bwd, in, wp, B, T, o1, o2, st); break;
   }
 }
 

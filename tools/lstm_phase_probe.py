@@ -12,7 +12,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 SO = os.path.join(HERE, "liblstm_probe.so")
 MODES = ["full step", "no MFMA", "no activations", "no global I/O", "no LDS h/dG read",
-         "loop + barrier only"]
+         "loop + barrier only", "flush only", "chunk loads only", "flush without stores"]
 
 
 def build():

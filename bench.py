@@ -362,7 +362,11 @@ def _timing_models(dev):
     return out
 
 
-def synth_rtf(model, dev, T=2000, parts=6, reps=3):
+# tools/synth_pmc.py: called before and after the measured passes of one synthesis case
+SYNTH_MARK = None
+
+
+def synth_rtf(model, dev, T=2000, parts=6, reps=3, only=None):
     """Synthesis real-time factor (BASELINE metric part 2 and config 5):
     elapsed / audio seconds (svs.py:449-452, 581-582) of the pipeline of
     synthesis_multitrack.py:113-288 -- timing inference (time-lag + duration MDN models with
@@ -403,6 +407,8 @@ def synth_rtf(model, dev, T=2000, parts=6, reps=3):
                         (f"ensemble_{parts}part", [(i, (i + 1) % parts) for i in range(parts)]),
                         (f"n2_sweep_{parts}part", [(i, j) for i in range(parts)
                                                    for j in range(parts)])):
+        if only is not None and name != only:
+            continue
         B = len(pairs)
         b = data.synthetic_batch(B, T, 4242 + B)
         g = lambda k: torch.from_numpy(b[k]).to(dev).contiguous()  # noqa: E731
@@ -443,9 +449,13 @@ def synth_rtf(model, dev, T=2000, parts=6, reps=3):
         timing()
         feats = acoustic()  # warm-up (weight packing, graph capture)
         vocoder(feats)
+        if SYNTH_MARK is not None:
+            SYNTH_MARK()
         tt, _ = _median_time(timing, reps)
         ta, feats = _median_time(acoustic, reps)
         tv, wav = _median_time(lambda: vocoder(feats), reps)
+        if SYNTH_MARK is not None:
+            SYNTH_MARK()
         assert torch.isfinite(wav).all()
         sec = T * 0.005
         flops = B * T * (ACOUSTIC_INFER_FLOP_PER_FRAME + VOCODER_FLOP_PER_FRAME)
@@ -464,7 +474,11 @@ def synth_rtf(model, dev, T=2000, parts=6, reps=3):
                 dtype=engine.gemm_precision(), **out,
                 roofline={"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                           "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
-                          "traffic": None,
+                          "traffic": _committed("r4_synth_pmc.json", "hbm_bytes_per_step"),
+                          "traffic_source": "profiles/r4_synth_pmc.json (rocprofv3 --pmc "
+                                            "FETCH_SIZE x2 + WRITE_SIZE over one ensemble pass: "
+                                            "timing + acoustic + post-processing + uSFGAN; "
+                                            "tools/synth_pmc.py; committed, not this run)",
                           "work": f"ensemble_{parts}part acoustic inference "
                                   f"({ACOUSTIC_INFER_FLOP_PER_FRAME / 1e9:.2f} GFLOP/frame) + "
                                   f"uSFGAN ({VOCODER_FLOP_PER_FRAME / 1e9:.2f} GFLOP/frame), "

@@ -480,6 +480,11 @@ __global__ __launch_bounds__(NTW) void lstm_mfma_bwd_kernel(
       bf16x8 bf[NKB];
 #pragma unroll
       for (int kk = 0; kk < NKB; ++kk) bf[kk] = *(const bf16x8*)(gcur + 32 * kk);
+      // every dG read in flight before the first MFMA (with the I/O wave's two waves on one
+      // SIMD the compiler otherwise reuses one register quad: a read and its full LDS latency
+      // per MFMA pair, H = 128 645 -> 753 ns per step)
+#pragma unroll
+      for (int kk = 0; kk < NKB; ++kk) asm volatile("" : "+v"(bf[kk]));
       f32x4 acc[TPW];
 #pragma unroll
       for (int mt = 0; mt < TPW; ++mt) {

@@ -103,6 +103,8 @@ def parse():
                     help="skip the 60 x 512 and ragged-length legs of the main model")
     ap.add_argument("--no-real-data", action="store_true",
                     help="skip the on-disk data-path leg (feeder + train_epoch)")
+    ap.add_argument("--no-transformer", action="store_true",
+                    help="skip the tier-2 Transformer encoder training leg")
     ap.add_argument("--cpu-pairs", type=int, default=10)
     ap.add_argument("--cpu-frames", type=int, default=1024)
     return ap.parse_args()
@@ -817,6 +819,122 @@ def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
                 last_loss=float(res[-1][0].item()), dtype=engine.gemm_precision())
 
 
+TF_CFG = dict(in_dim=87, out_dim=67, hidden_dim=256, attention_dim=1024, num_heads=2,
+              num_layers=2, kernel_size=3, dropout=0.1)
+
+
+def transformer_flops(B, T, cfg=TF_CFG):
+    """Forward GEMM / attention FLOPs of TransformerEncoder (nnsvs/model.py:1540-1671) on B x T
+    frames: fc, per layer the q / k / v / o projections, QK^T and PV (T x T per head), the
+    relative-key / value band (2w + 1 = 9 per row) and the two k-tap FFN convolutions, fc_out."""
+    M, C, F, k = B * T, cfg["hidden_dim"], cfg["attention_dim"], cfg["kernel_size"]
+    per_layer = 4 * 2 * M * C * C + 2 * 2 * B * T * T * C + 2 * 2 * M * 9 * C \
+        + 2 * 2 * M * C * F * k
+    return 2 * M * cfg["in_dim"] * C + cfg["num_layers"] * per_layer + 2 * M * C * cfg["out_dim"]
+
+
+def transformer_train(dev, B=8, T=1024, steps=10, warm=3):
+    """Tier-2 Transformer encoder (no recipe instantiates it, so
+    the reference's constructor defaults at acoustic-model widths: hidden 256, FFN filter
+    1 024, 2 heads, 2 layers, kernel 3, dropout 0.1): training steps (forward with dropout,
+    backward through autograd, clip + Adam) on B x T ragged frames, eager issue."""
+    from ensemble_svs_with_interactions_amd.transformer import TransformerEncoder
+    torch.manual_seed(20250326)
+    mod = TransformerEncoder(**TF_CFG).to(dev)
+    mod.train()
+    opt = FusedAdam(mod, lr=1e-4, clip_norm=1.0)
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(B, T, TF_CFG["in_dim"], device=dev, generator=g)
+    y = torch.randn(B, T, TF_CFG["out_dim"], device=dev, generator=g)
+    lens = [T - 64 * (i % 4) for i in range(B)]
+    mask = torch.zeros(B, T, 1, device=dev)
+    for i, n in enumerate(lens):
+        mask[i, :n] = 1.0
+
+    denom = mask.sum() * TF_CFG["out_dim"]
+
+    def grads():
+        opt.zero_grad()
+        out = mod(x, lens)
+        loss = ((out - y).abs() * mask).sum() / denom
+        loss.backward()
+        return loss
+
+    def step():
+        loss = grads()
+        opt.step()
+        return loss
+    # eager warm-up on a side stream (workspaces, packed weights, lengths), then the step
+    # captured as two HIP graphs (RNG epoch + forward + loss + backward; clip + Adam), as
+    # train.GraphedTrainStep does: the eager step is launch-bound (~1 100 launches per step)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(warm):
+            step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize()
+    from ensemble_svs_with_interactions_amd._lib import call
+    g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g1):
+        call("ensvs_rng_advance", torch.cuda.current_stream().cuda_stream)
+        gloss = grads()
+    with torch.cuda.graph(g2, pool=g1.pool()):
+        opt.step()
+    opt._captured = True
+
+    def replay():
+        g1.replay()
+        g2.replay()
+        return gloss
+    replay()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for _ in range(steps):
+        loss = replay()
+    torch.cuda.synchronize()
+    el = (time.time() - t0) / steps
+    fl = 3 * transformer_flops(B, T)
+    tf = fl / el / 1e12
+    peak = PEAK_BF16_TFLOPS if engine.gemm_precision() == "bf16" else 157.3
+    return dict(metric="Transformer encoder train frames/sec (tier 2, row a14)",
+                value=B * T / el, unit="frames/s", ms_per_step=el * 1e3, steps=steps,
+                batch=B, frames=T, lengths=lens, config=TF_CFG, dtype=engine.gemm_precision(),
+                execution="hip-graph replay of the autograd step through the drop-in module",
+                train_loss=float(loss.item()),
+                roofline={"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s",
+                          "frac": tf / peak, "traffic": None,
+                          "work": f"3 x {transformer_flops(B, T) / 1e9:.1f} GFLOP forward per "
+                                  "step (backward = 2 x forward: input and weight gradients)"})
+
+
+def transformer_cpu_baseline(B=4, T=1024, warm=1, timed=5):
+    """The oracle's Transformer encoder (float32, no dropout) forward + backward on the host
+    cores: a bounded sample of the leg's workload."""
+    from ensemble_svs_with_interactions_amd.transformer import TransformerEncoder
+    from oracle import ensvs_oracle as O
+    cores = _host_cores()
+    torch.set_num_threads(cores)
+    torch.manual_seed(20250326)
+    P = {k: v.detach().clone().requires_grad_() for k, v in
+         TransformerEncoder(**TF_CFG).state_dict().items()}
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, T, TF_CFG["in_dim"], generator=g)
+    y = torch.randn(B, T, TF_CFG["out_dim"], generator=g)
+    times = []
+    for _ in range(warm + timed):
+        t0 = time.time()
+        out = O.transformer_encoder(P, TF_CFG, x, [T] * B)
+        (out - y).abs().mean().backward()
+        times.append(time.time() - t0)
+    sec = float(np.median(times[warm:]))
+    return dict(value=B * T / sec, unit="frames/s", cores=cores, kind="port",
+                cpu_model=_cpu_model(),
+                sample=f"oracle transformer_encoder forward + backward (CPU PyTorch, fp32, no "
+                       f"dropout, no optimizer), {B} x {T} frames, median of {timed} steps after "
+                       f"{warm} warm-up")
+
+
 def config2_train(args, dev):
     """BASELINE config 2: single-track NPSSMDNMultistreamParametricModel (teacher-forced
     lf0 decoder, both diffusions, V/UV) training steps, same per-GPU workload (pairs ->
@@ -1011,6 +1129,8 @@ def main():
     if not args.no_config2 and world == 1:
         out["config2"] = config2_train(args, dev)
         out["interaction_loss"] = il_train(args, dev)
+    if not args.no_transformer and world == 1:
+        out["transformer"] = transformer_train(dev)
     if not args.no_synth and world == 1:
         out["synth"] = synth_rtf(model, dev)
     if not args.no_cpu_baseline and world == 1:
@@ -1019,6 +1139,8 @@ def main():
             out["separate_f0"]["cpu_baseline"] = sf0_cpu_baseline()
         if "synth" in out:
             out["synth"]["cpu_baseline"] = cpu_synth_baseline(out["synth"]["frames"])
+        if "transformer" in out:
+            out["transformer"]["cpu_baseline"] = transformer_cpu_baseline()
     print(json.dumps(out), flush=True)
 
 

@@ -215,6 +215,9 @@ SIGNATURES = {
     "ensvs_masked_mean_bwd": [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp],
     "ensvs_bgemm": [c_vp, c_ll, c_ll, c_ll, c_ll, c_vp, c_ll, c_ll, c_ll, c_ll, c_vp, c_ll, c_ll,
                     c_ll, c_ll, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_vp],
+    "ensvs_bgemm_bf16": [c_vp, c_ll, c_ll, c_ll, c_ll, c_vp, c_ll, c_ll, c_ll, c_ll, c_vp, c_ll,
+                         c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
+                         c_vp],
     "ensvs_div": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_float, c_vp],
     "ensvs_attn_softmax": [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
                            c_vp, c_vp, c_vp],

@@ -85,6 +85,153 @@ __global__ __launch_bounds__(256) void bgemm_kernel(BG A, BG B, float* C, long l
   }
 }
 
+// ------------------------------------------------ batched GEMM, bf16 MFMA (production mode)
+// The same products as bgemm_kernel with operands rounded to bf16 while staged and fp32
+// accumulation on v_mfma_f32_16x16x32_bf16: 128 x 128 output tile per 256 threads (2 x 2 waves
+// of 64 x 64), K in steps of 32, the next step's operands loaded into registers while the
+// current one runs.  Each operand is staged in the layout of its contiguous axis, so every
+// global load is a float4 run along it:
+//  * k contiguous (A: sc == 1, B: sr == 1): image [128 rows][32 k], 80-B rows; a fragment is
+//    one ds_read_b128 (8 k of one row);
+//  * rows contiguous (A: sr == 1, B: sc == 1): image [32 k][128 rows], 256-B rows with XOR-
+//    swizzled 16-B chunks; a fragment is two ds_read_b64_tr_b16 (transposed reads).
+// Element (z, r, c) of an operand at p + zb*sb + zh*sh + r*sr + c*sc; for A (r, c) = (m, k),
+// for B (r, c) = (k, n); the image row ("q") is m for A and n for B.
+constexpr int QB = 128, KS = 32, IMGB = QB * 80;  // image bytes (the k-major one is 8 KB)
+
+__device__ __forceinline__ int kmaj_off(int k, int ch) {  // [k][128 q] bf16, chunk ch = q / 8
+  return 256 * k + 16 * (ch ^ (((k & 3) << 2) | ((k >> 2) & 3)));
+}
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+__device__ __forceinline__ bf16x8 frag_kmaj(const char* img, int q0, int lane) {
+  const int g = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
+  const int ch = (q0 >> 3) + (p >> 1);
+  const int o0 = kmaj_off(8 * g + qq, ch) + 8 * (p & 1);
+  const int o1 = kmaj_off(8 * g + 4 + qq, ch) + 8 * (p & 1);
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(img + o0));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(img + o1));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x8 frag_qmaj(const char* img, int q0, int lane) {
+  return *(const bf16x8*)(img + (q0 + (lane & 15)) * 80 + 16 * (lane >> 4));
+}
+
+struct Stage {  // one operand's staging: 16 consecutive elements along its contiguous axis
+  const float* p;
+  long long sq, sk;  // strides of q and k
+  int Q, K;
+  bool kfast;
+};
+// this thread's 16 elements of step k0: k-fast: q = tid/2, k = k0 + 16 (tid&1) ..;
+// q-fast: k = k0 + tid/8, q = q0 + 16 (tid&7) ..; zeros outside [Q) x [K)
+__device__ __forceinline__ void stage_load(const Stage& S, int q0, int k0, int tid, f32x4 (&v)[4]) {
+  int q, k, n;
+  const float* base;
+  long long st;
+  if (S.kfast) {
+    q = q0 + (tid >> 1);
+    k = k0 + 16 * (tid & 1);
+    n = q < S.Q ? S.K - k : 0;
+    base = S.p + q * S.sq + k;
+    st = 1;
+  } else {
+    k = k0 + (tid >> 3);
+    q = q0 + 16 * (tid & 7);
+    n = k < S.K ? S.Q - q : 0;
+    base = S.p + k * S.sk + q;
+    st = 1;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rem = n - 4 * i;
+    if (rem >= 4) {
+      v[i] = *(const f32x4*)(base + 4 * i);
+    } else {
+      f32x4 t = {0.f, 0.f, 0.f, 0.f};
+      for (int e = 0; e < rem; ++e) t[e] = base[4 * i + e * st];
+      v[i] = t;
+    }
+  }
+}
+__device__ __forceinline__ void stage_store(const Stage& S, char* img, int tid, const f32x4 (&v)[4]) {
+  bf16x8 lo, hi;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    lo[e] = (__bf16)v[0][e];
+    lo[4 + e] = (__bf16)v[1][e];
+    hi[e] = (__bf16)v[2][e];
+    hi[4 + e] = (__bf16)v[3][e];
+  }
+  if (S.kfast) {
+    char* r = img + (tid >> 1) * 80 + 32 * (tid & 1);
+    *(bf16x8*)r = lo;
+    *(bf16x8*)(r + 16) = hi;
+  } else {
+    const int k = tid >> 3, ch = 2 * (tid & 7);
+    *(bf16x8*)(img + kmaj_off(k, ch)) = lo;
+    *(bf16x8*)(img + kmaj_off(k, ch + 1)) = hi;
+  }
+}
+
+__global__ __launch_bounds__(256) void bgemm_b16_kernel(BG A, BG B, float* C, long long csb,
+                                                        long long csh, long long csr,
+                                                        long long csc, int H, int M, int N,
+                                                        int K, float alpha, int accum) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][IMGB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  const int z = blockIdx.z, zb = z / H, zh = z % H;
+  const int m0 = blockIdx.x * QB, n0 = blockIdx.y * QB;
+  Stage SA{A.p + zb * A.sb + zh * A.sh + m0 * A.sr, A.sr, A.sc, M - m0, K, A.sc == 1};
+  Stage SB{B.p + zb * B.sb + zh * B.sh + n0 * B.sc, B.sc, B.sr, N - n0, K, B.sr == 1};
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 va[4], vb[4];
+  const int nk = (K + KS - 1) / KS;
+  stage_load(SA, 0, 0, tid, va);
+  stage_load(SB, 0, 0, tid, vb);
+  for (int it = 0; it < nk; ++it) {
+    char* IA = smem[it & 1][0];
+    char* IB = smem[it & 1][1];
+    stage_store(SA, IA, tid, va);
+    stage_store(SB, IB, tid, vb);
+    __syncthreads();
+    if (it + 1 < nk) {
+      stage_load(SA, 0, (it + 1) * KS, tid, va);
+      stage_load(SB, 0, (it + 1) * KS, tid, vb);
+    }
+    bf16x8 fa[4], fb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i] = SA.kfast ? frag_qmaj(IA, wr * 64 + 16 * i, lane) : frag_kmaj(IA, wr * 64 + 16 * i, lane);
+      fb[i] = SB.kfast ? frag_qmaj(IB, wc * 64 + 16 * i, lane) : frag_kmaj(IB, wc * 64 + 16 * i, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  }
+  float* c = C + zb * csb + zh * csh;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wr * 64 + 16 * i + 4 * (lane >> 4) + r;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wc * 64 + 16 * j + (lane & 15);
+        if (n >= N) continue;
+        float* p = c + m * csr + n * csc;
+        const float v = alpha * acc[i][j][r];
+        *p = accum ? *p + v : v;
+      }
+    }
+}
+
 __device__ __forceinline__ float wsum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -163,6 +310,183 @@ __global__ __launch_bounds__(256) void softmax_kernel(float* S, const float* qs,
   }
 }
 
+// lane r <= 2w: v . tab[r] over dk (float4 runs when vec4: dk % 4 == 0, 16-B aligned rows)
+__device__ __forceinline__ float band_lane_dot(const float* v, const float* tab, int dk, int w,
+                                               int lane, int vec4) {
+  float acc = 0.f;
+  if (lane > 2 * w) return acc;
+  const float* e = tab + (long long)lane * dk;
+  if (vec4) {
+    f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+    for (int d = 0; d < dk; d += 4) {
+      const f32x4 x = *(const f32x4*)(v + d), y = *(const f32x4*)(e + d);
+      a4 = x * y + a4;
+    }
+    acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+  } else {
+    for (int d = 0; d < dk; ++d) acc = fmaf(v[d], e[d], acc);
+  }
+  return acc;
+}
+
+// softmax_kernel with the row held in registers (T <= 64 NJ): S read once and P written once
+// (the three-pass form re-read and re-wrote the row in global memory: 159 us per 16 384 rows
+// of 1 024, profiles/r4_tf_prof_before.txt).
+template <int NJ>
+__global__ __launch_bounds__(256) void softmax_reg_kernel(float* S, const float* qs, int ldq,
+                                                          const float* ek, const long long* lens,
+                                                          long long rows, int H, int T, int dk,
+                                                          int w, const float* keep, float* Pd,
+                                                          int vec4) {
+  const long long row = blockIdx.x * 4LL + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;  // wave-uniform
+  const RowIdx ri = row_idx(row, H, T);
+  float* s = S + row * T;
+  const int L = (int)lens[ri.b];
+  const float rel = band_lane_dot(qs + ((long long)ri.b * T + ri.i) * ldq + ri.h * dk, ek, dk, w,
+                                  lane, vec4);
+  float v[NJ];
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) {
+    const int j = jj * 64 + lane;
+    v[jj] = j < T ? s[j] : -INFINITY;
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) {
+    const int j = jj * 64 + lane;
+    const int r = j - ri.i + w;
+    const float rv = __shfl(rel, min(max(r, 0), 63));
+    if (j < T) {
+      float x = v[jj];
+      if (r >= 0 && r <= 2 * w) x += rv;
+      if (ri.i >= L || j >= L) x = -1e4f;
+      v[jj] = x;
+      m = fmaxf(m, x);
+    }
+  }
+  m = wmax(m);
+  float sum = 0.f;
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) {
+    const int j = jj * 64 + lane;
+    const float e = j < T ? __expf(v[jj] - m) : 0.f;
+    v[jj] = e;
+    sum += e;
+  }
+  sum = wsum(sum);
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) {
+    const int j = jj * 64 + lane;
+    if (j < T) {
+      const float p = v[jj] / sum;
+      s[j] = p;
+      if (keep) Pd[row * T + j] = p * keep[row * T + j];
+    }
+  }
+}
+
+// softmax_bwd_kernel with the row in registers (dS, P and keep read once, dS written once)
+template <int NJ>
+__global__ __launch_bounds__(256) void softmax_bwd_reg_kernel(float* dS, const float* P,
+                                                              const float* keep,
+                                                              const long long* lens,
+                                                              long long rows, int H, int T) {
+  const long long row = blockIdx.x * 4LL + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const RowIdx ri = row_idx(row, H, T);
+  const int L = (int)lens[ri.b];
+  float* g = dS + row * T;
+  const float* p = P + row * T;
+  const float* kp = keep ? keep + row * T : nullptr;
+  float gv[NJ], pv[NJ];
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) {
+    const int j = jj * 64 + lane;
+    gv[jj] = j < T ? (kp ? g[j] * kp[j] : g[j]) : 0.f;
+    pv[jj] = j < T ? p[j] : 0.f;
+  }
+  float dot = 0.f;
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) dot = fmaf(pv[jj], gv[jj], dot);
+  dot = wsum(dot);
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) {
+    const int j = jj * 64 + lane;
+    if (j < T) g[j] = (ri.i >= L || j >= L) ? 0.f : pv[jj] * (gv[jj] - dot);
+  }
+}
+
+// band_table_grad_kernel as one workgroup per block of rows: each wave walks its rows with the
+// band values in registers (loaded once per row) and accumulates all 2w + 1 table rows for its
+// dk columns (lane d, d + 64, ...); the 4 waves' sums are combined in a fixed order through LDS.
+// (The per-(r, chunk) form walked 64 rows per thread one dependent load pair at a time, and its
+// 256-chunk reduction ran one thread per output: 65 + 60 us, profiles/r4_tf_prof_before.txt.)
+constexpr int TG_W2 = 9;  // 2w + 1 <= 9 (the encoder's window_size 4)
+template <int ND>
+__global__ __launch_bounds__(256) void band_table_grad2_kernel(const float* A, const float* X,
+                                                               int ldx, long long rows, int H,
+                                                               int T, int dk, int w, int rpb,
+                                                               float* part) {
+  extern __shared__ float red[];  // [4][W2][dk]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, W2 = 2 * w + 1;
+  float acc[TG_W2][ND];
+#pragma unroll
+  for (int r = 0; r < TG_W2; ++r)
+#pragma unroll
+    for (int q = 0; q < ND; ++q) acc[r][q] = 0.f;
+  const long long r0 = (long long)blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  for (long long row = r0 + wid; row < r1; row += 4) {
+    const RowIdx ri = row_idx(row, H, T);
+    float av[TG_W2];
+#pragma unroll
+    for (int r = 0; r < TG_W2; ++r) {
+      const int j = ri.i + r - w;
+      av[r] = (r < W2 && j >= 0 && j < T) ? A[row * T + j] : 0.f;
+    }
+    const float* x = X + ((long long)ri.b * T + ri.i) * ldx + ri.h * dk;
+    float xv[ND];
+#pragma unroll
+    for (int q = 0; q < ND; ++q) xv[q] = lane + 64 * q < dk ? x[lane + 64 * q] : 0.f;
+#pragma unroll
+    for (int r = 0; r < TG_W2; ++r)
+#pragma unroll
+      for (int q = 0; q < ND; ++q) acc[r][q] = fmaf(av[r], xv[q], acc[r][q]);
+  }
+#pragma unroll
+  for (int r = 0; r < TG_W2; ++r)
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+      const int d = lane + 64 * q;
+      if (r < W2 && d < dk) red[(wid * W2 + r) * dk + d] = acc[r][q];
+    }
+  __syncthreads();
+  for (int e = tid; e < W2 * dk; e += 256) {
+    const float t = ((red[e] + red[W2 * dk + e]) + red[2 * W2 * dk + e]) + red[3 * W2 * dk + e];
+    part[(long long)blockIdx.x * W2 * dk + e] = t;
+  }
+}
+
+// out[e] (+)= sum_c part[c][e] in chunk order, 8 chunk loads in flight per step
+__global__ void reduce_parts2_kernel(const float* part, int nchunks, int n, float* out,
+                                     int accum) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  float s = 0.f;
+  int c = 0;
+  for (; c + 8 <= nchunks; c += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = part[(long long)(c + k) * n + e];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k];
+  }
+  for (; c < nchunks; ++c) s += part[(long long)c * n + e];
+  out[e] = accum ? out[e] + s : s;
+}
+
 // O[(b*T + i)*ldo + h*dk + d] += sum_{|j - i| <= w} P[row][j] ev[j - i + w][d]
 __global__ void relv_kernel(const float* P, const float* ev, float* O, int ldo, long long rows,
                             int H, int T, int dk, int w) {
@@ -184,17 +508,15 @@ __global__ void relv_kernel(const float* P, const float* ev, float* O, int ldo, 
 // D[row][i + r - w] += vec_i . tab[r]   (one wave per row; lanes r <= 2w form the dots)
 __global__ __launch_bounds__(256) void band_dot_kernel(float* D, const float* vec, int ldv,
                                                        const float* tab, long long rows, int H,
-                                                       int T, int dk, int w) {
+                                                       int T, int dk, int w, int vec4) {
   const long long row = blockIdx.x * 4LL + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const RowIdx ri = row_idx(row, H, T);
   const int j = ri.i + lane - w;
   if (lane > 2 * w || j < 0 || j >= T) return;
-  const float* v = vec + ((long long)ri.b * T + ri.i) * ldv + ri.h * dk;
-  const float* e = tab + (long long)lane * dk;
-  float dot = 0.f;
-  for (int d = 0; d < dk; ++d) dot = fmaf(v[d], e[d], dot);
+  const float dot = band_lane_dot(vec + ((long long)ri.b * T + ri.i) * ldv + ri.h * dk, tab, dk,
+                                  w, lane, vec4);
   D[row * T + j] += dot;
 }
 
@@ -355,6 +677,31 @@ ENSVS_API int ensvs_bgemm(const float* a, long long asb, long long ash, long lon
   return ENSVS_OK;
 }
 
+// bf16-operand MFMA form of ensvs_bgemm (production precision).  Each operand needs a unit
+// stride on its row or its reduction axis, 16-B aligned rows and the other strides multiples
+// of 4 floats; other layouts run the exact kernel.
+ENSVS_API int ensvs_bgemm_bf16(const float* a, long long asb, long long ash, long long asr,
+                               long long asc, const float* b, long long bsb, long long bsh,
+                               long long bsr, long long bsc, float* c, long long csb,
+                               long long csh, long long csr, long long csc, int Bn, int H, int M,
+                               int N, int K, float alpha, int accum, void* stream) {
+  if (Bn <= 0 || H <= 0 || M <= 0 || N <= 0 || K <= 0 || Bn * (long long)H > 65535)
+    return ENSVS_E_SHAPE;
+  auto ok = [](const float* p, long long sb, long long sh, long long sr, long long sc) {
+    const bool unit = sr == 1 || sc == 1;
+    const long long other = sr == 1 ? sc : sr;
+    return unit && (((uintptr_t)p) & 15) == 0 && other % 4 == 0 && sb % 4 == 0 && sh % 4 == 0;
+  };
+  if (!ok(a, asb, ash, asr, asc) || !ok(b, bsb, bsh, bsr, bsc))
+    return ensvs_bgemm(a, asb, ash, asr, asc, b, bsb, bsh, bsr, bsc, c, csb, csh, csr, csc, Bn,
+                       H, M, N, K, alpha, accum, stream);
+  BG A{a, asb, ash, asr, asc}, Bo{b, bsb, bsh, bsr, bsc};
+  hipLaunchKernelGGL(bgemm_b16_kernel, dim3(cdiv(M, QB), cdiv(N, QB), Bn * H), dim3(256), 0,
+                     (hipStream_t)stream, A, Bo, c, csb, csh, csr, csc, H, M, N, K, alpha, accum);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
 ENSVS_API int ensvs_div(const float* x, int ldx, float* y, int ldy, long long M, int C, float s,
                         void* stream) {
   if (M <= 0 || C <= 0) return ENSVS_E_SHAPE;
@@ -370,8 +717,22 @@ ENSVS_API int ensvs_attn_softmax(float* S, const float* qs, int ldq, const float
   if (w < 0 || 2 * w + 1 > 64 || T <= 0 || B <= 0 || H <= 0) return ENSVS_E_SHAPE;
   if ((keep == nullptr) != (Pd == nullptr)) return ENSVS_E_ARG;
   const long long rows = (long long)B * H * T;
-  hipLaunchKernelGGL(softmax_kernel, dim3((int)((rows + 3) / 4)), dim3(256), 0,
-                     (hipStream_t)stream, S, qs, ldq, ek, lens, rows, H, T, dk, w, keep, Pd);
+  const int vec4 = dk % 4 == 0 && ldq % 4 == 0 && ((((uintptr_t)qs) | (uintptr_t)ek) & 15) == 0;
+  const dim3 grid((int)((rows + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+#define SMX(NJ)                                                                                  \
+  hipLaunchKernelGGL(softmax_reg_kernel<NJ>, grid, dim3(256), 0, st, S, qs, ldq, ek, lens, rows, \
+                     H, T, dk, w, keep, Pd, vec4)
+  if (T <= 64) SMX(1);
+  else if (T <= 128) SMX(2);
+  else if (T <= 256) SMX(4);
+  else if (T <= 512) SMX(8);
+  else if (T <= 1024) SMX(16);
+  else if (T <= 2048) SMX(32);
+  else
+    hipLaunchKernelGGL(softmax_kernel, grid, dim3(256), 0, st, S, qs, ldq, ek, lens, rows, H, T,
+                       dk, w, keep, Pd);
+#undef SMX
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
@@ -391,8 +752,9 @@ ENSVS_API int ensvs_attn_band_dot(float* D, const float* vec, int ldv, const flo
   if (w < 0 || 2 * w + 1 > 64) return ENSVS_E_SHAPE;
   const long long rows = (long long)B * H * T;
   if (rows <= 0) return ENSVS_E_SHAPE;
+  const int vec4 = dk % 4 == 0 && ldv % 4 == 0 && ((((uintptr_t)vec) | (uintptr_t)tab) & 15) == 0;
   hipLaunchKernelGGL(band_dot_kernel, dim3((int)((rows + 3) / 4)), dim3(256), 0,
-                     (hipStream_t)stream, D, vec, ldv, tab, rows, H, T, dk, w);
+                     (hipStream_t)stream, D, vec, ldv, tab, rows, H, T, dk, w, vec4);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
@@ -407,13 +769,31 @@ ENSVS_API int ensvs_attn_table_grad(const float* A, const float* X, int ldx, int
                                     void* stream) {
   const long long rows = (long long)B * H * T;
   if (rows <= 0 || w < 0) return ENSVS_E_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  const int n = (2 * w + 1) * dk;
+  if (2 * w + 1 <= TG_W2 && dk <= 256) {
+    // blocks of rpb rows (a multiple of the 4 waves), at most 256 partials (the workspace)
+    const long long rpb = std::max<long long>(128, (cdiv(rows, 256) + 3) / 4 * 4);
+    const int nch = cdiv(rows, rpb);
+    const size_t lds = 4 * (size_t)n * sizeof(float);
+#define TG(ND)                                                                                \
+  hipLaunchKernelGGL(band_table_grad2_kernel<ND>, dim3(nch), dim3(256), lds, st, A, X, ldx, rows, \
+                     H, T, dk, w, (int)rpb, part)
+    if (dk <= 64) TG(1);
+    else if (dk <= 128) TG(2);
+    else TG(4);
+#undef TG
+    ENSVS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(reduce_parts2_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, part, nch, n,
+                       out, accum);
+    ENSVS_CHECK_LAUNCH();
+    return ENSVS_OK;
+  }
   const int nch = (int)std::min<long long>(256, (rows + 63) / 64);
   const long long chunk = (rows + nch - 1) / nch;
-  hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(band_table_grad_kernel, dim3(2 * w + 1, nch), dim3(128), 0, st, A, X, ldx,
                      rows, H, T, dk, w, chunk, part);
   ENSVS_CHECK_LAUNCH();
-  const int n = (2 * w + 1) * dk;
   hipLaunchKernelGGL(reduce_parts_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, part, nch, n, out,
                      accum);
   ENSVS_CHECK_LAUNCH();
@@ -424,8 +804,18 @@ ENSVS_API int ensvs_attn_softmax_bwd(float* dS, const float* P, const float* kee
                                      const long long* lens, int B, int H, int T, void* stream) {
   const long long rows = (long long)B * H * T;
   if (rows <= 0) return ENSVS_E_SHAPE;
-  hipLaunchKernelGGL(softmax_bwd_kernel, dim3((int)((rows + 3) / 4)), dim3(256), 0,
-                     (hipStream_t)stream, dS, P, keep, lens, rows, H, T);
+  const dim3 grid((int)((rows + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+#define SMB(NJ) \
+  hipLaunchKernelGGL(softmax_bwd_reg_kernel<NJ>, grid, dim3(256), 0, st, dS, P, keep, lens, rows, H, T)
+  if (T <= 64) SMB(1);
+  else if (T <= 128) SMB(2);
+  else if (T <= 256) SMB(4);
+  else if (T <= 512) SMB(8);
+  else if (T <= 1024) SMB(16);
+  else if (T <= 2048) SMB(32);
+  else hipLaunchKernelGGL(softmax_bwd_kernel, grid, dim3(256), 0, st, dS, P, keep, lens, rows, H, T);
+#undef SMB
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }

@@ -22,6 +22,7 @@ import torch
 from torch import nn
 
 from . import _lib
+from . import engine
 from . import kernels as K
 from . import layers as Ly
 from ._lib import call, ptr
@@ -141,7 +142,10 @@ def _bg(t, off, sb, sh, sr, sc):
 
 
 def _bgemm(a, b, c, Bn, H, M, N, Kd, alpha=1.0, accum=False):
-    call("ensvs_bgemm", *a, *b, *c, Bn, H, M, N, Kd, float(alpha), int(accum), stream())
+    """Per-head products: bf16-operand MFMA in production precision, exact fp32 in parity
+    mode (engine.set_gemm_precision)."""
+    fn = "ensvs_bgemm_bf16" if engine.gemm_precision() == "bf16" else "ensvs_bgemm"
+    call(fn, *a, *b, *c, Bn, H, M, N, Kd, float(alpha), int(accum), stream())
 
 
 def _mask(x, ld, B, T, C, lens, out=None, out_ld=None):

@@ -505,6 +505,15 @@ int ensvs_bgemm(const float* a, long long asb, long long ash, long long asr, lon
                 const float* b, long long bsb, long long bsh, long long bsr, long long bsc,
                 float* c, long long csb, long long csh, long long csr, long long csc, int Bn,
                 int H, int M, int N, int K, float alpha, int accum, void* stream);
+/* The same product with bf16 operands (rounded while staged) and fp32 accumulation on the
+ * MFMA units: the production-precision form (the reference recipe's fp16 autocast runs these
+ * torch.matmul calls in half precision).  Each operand needs a unit stride on its row or
+ * reduction axis, 16-B aligned base and strides that are multiples of 4 floats; other
+ * layouts run ensvs_bgemm. */
+int ensvs_bgemm_bf16(const float* a, long long asb, long long ash, long long asr, long long asc,
+                     const float* b, long long bsb, long long bsh, long long bsr, long long bsc,
+                     float* c, long long csb, long long csh, long long csr, long long csc, int Bn,
+                     int H, int M, int N, int K, float alpha, int accum, void* stream);
 /* y = x / s (the query scaling query / sqrt(k_channels), attentions.py:93). */
 int ensvs_div(const float* x, int ldx, float* y, int ldy, long long M, int C, float s,
               void* stream);

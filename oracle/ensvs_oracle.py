@@ -643,7 +643,8 @@ def rel_attention(q, k, v, ek, ev, lengths, w, keep=None):
 def transformer_encoder(P, cfg, x, lengths, keeps=None):
     """nnsvs/model.py:1625-1671 + transformer/encoder.py:24-142 on (B, T, in_dim) -> (B,
     T'*r, out_dim).  keeps: optional dict of dropout keep-masks keyed like the module path
-    ('L{i}.attn_p', 'L{i}.attn_y', 'L{i}.ffn_h', 'L{i}.ffn_y'); None -> no dropout."""
+    ('L{i}.attn_p', 'L{i}.attn_y', 'L{i}.ffn_h', 'L{i}.ffn_y'; None -> no dropout) and
+    optionally the FFN ReLU decisions to replay ('L{i}.ffn_relu')."""
     keeps = keeps or {}
     H, nl = cfg.get("num_heads", 2), cfg.get("num_layers", 2)
     kz, r = cfg.get("kernel_size", 3), cfg.get("reduction_factor", 1)
@@ -688,7 +689,11 @@ def transformer_encoder(P, cfg, x, lengths, keeps=None):
             y = y * keeps[f"L{i}.attn_y"]
         h = ln(f"encoder.norm_layers_1.{i}", h + y)
         f = f"encoder.ffn_layers.{i}."
-        z = torch.relu(conv(f + "conv_1", h * m))
+        z = conv(f + "conv_1", h * m)
+        # 'L{i}.ffn_relu': replayed ReLU decisions (1 where the device's pre-activation was > 0),
+        # so a gradient check is not decided by units whose pre-activation is fp32 rounding away
+        # from zero
+        z = z * keeps[f"L{i}.ffn_relu"] if f"L{i}.ffn_relu" in keeps else torch.relu(z)
         if f"L{i}.ffn_h" in keeps:
             z = z * keeps[f"L{i}.ffn_h"]
         y = conv(f + "conv_2", z * m) * m

@@ -87,6 +87,7 @@ SIGNATURES = {
                                   c_ll, c_vp],
     "ensvs_set_big_tile": [c_int, c_int],
     "ensvs_set_dual_small": [c_int],
+    "ensvs_set_gbw_dma": [c_int],
     "ensvs_set_small": [c_int],
     "ensvs_set_recurrence_exclusive": [c_int],
     "ensvs_note_mask": [c_vp, c_int, c_int, c_vp, c_vp],

@@ -87,6 +87,9 @@ struct GemmArgs {
   float* part;
   long long part_floats;
   int ksplit;
+  // GATE_BWD in the production form (bf16 aux1 and ybf, no Y / bias / ybf_radd, C and M
+  // multiples of 128, 16-B aligned rows): the 128 x 128 kernel's LDS-DMA epilogue
+  int gbw_dma;
 };
 
 template <typename T>
@@ -961,6 +964,133 @@ __device__ __forceinline__ void usf_block_tail(const GemmArgs& a, const GemmArgs
                                                f32x4 (&acc)[4][4], char* smem, int tid, int lane,
                                                int wr, int wc, int m0);
 
+// GATE_BWD epilogue of the 128 x 128 bf16 kernel with its operands staged by LDS-DMA (the
+// production form: bf16 gate/filter save in, bf16 d(pre) out, no fp32 Y, per-tile column
+// sums).  The register form loads each thread's gate/filter values two rows ahead of its
+// stores, ~2 x 8 B in flight per thread: 23.6 of the launch's 36.5 us (K loop alone 12.9 us,
+// tools/dgrad_probe.py).  Here the accumulator rows go through LDS a 64-row half at a time
+// and the half's gate / filter rows in 32-row quarters (2 x 8 KB), double-buffered and
+// fetched by global_load_lds (no registers) one quarter ahead: a quarter's DMA is issued
+// before the previous quarter's stores, so the counted wait for it never waits for stores
+// (vmcnt counts both, in issue order).  A one-burst form (a half's operands, one wait) took
+// 40.0 us: its wait covered the previous half's stores.  Rows and the column-sum order are the
+// register form's (thread group g sums rows g, g + 8, .. in order): the same bits.
+typedef __attribute__((address_space(3))) char lds_char;
+constexpr int GBW_T = 64 * EP * 4, GBW_Q = 32 * 256;  // T half; one operand quarter (bf16)
+static_assert(GBW_T + 4 * GBW_Q + CS_GROUPS * 2 * BN * 4 <= EPI_LDS, "GATE_BWD DMA LDS");
+// The waits are counted by hand, so the LDS reads, the global stores and the barriers are
+// issued as inline asm: the compiler drains every outstanding LDS-DMA (s_waitcnt vmcnt(0))
+// in front of an LDS read it can see, and __syncthreads() drains the stores.
+__device__ __forceinline__ void gbw_bar() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+__device__ __forceinline__ void gbw_st8(__bf16* p, f32x4 v) {
+  const bf16x4 h = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(__builtin_bit_cast(u32x2, h))
+               : "memory");
+}
+__device__ __forceinline__ void gate_bwd_epilogue_dma(const GemmArgs& a, f32x4 (&acc)[4][4],
+                                                      int m0, int n0, int wr, int wc, int lane,
+                                                      int tid, char* smem) {
+  float* T = (float*)smem;               // [64][EP] accumulator rows of the half
+  char* GF = smem + GBW_T;               // [2 buffers][gate, filter][32][128] bf16
+  float* X = (float*)(GF + 4 * GBW_Q);  // [group][2 * BN] column-sum exchange
+  const int wid = tid >> 6, cq = tid & 31, grp = tid >> 5, col = n0 + cq * 4;
+  const __bf16* aux = (const __bf16*)a.aux1;
+  // quarter q's gate and filter rows into buffer q & 1: wave wid moves rows 8 wid .. 8 wid + 7,
+  // 4 rows (1 KB) per instruction: 4 instructions per lane and quarter
+  auto fetch = [&](int q) {
+    char* G = GF + (q & 1) * 2 * GBW_Q;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = 8 * wid + 4 * i;
+      const __bf16* src =
+          aux + (long long)(m0 + 32 * q + r + (lane >> 4)) * a.ld1 + n0 + (lane & 15) * 8;
+      glds16(src, G + r * 256);
+      glds16(src + a.C, G + GBW_Q + r * 256);
+    }
+  };
+  auto stage = [&](int h) {  // the waves holding rows 64 h .. 64 h + 63 write them to T
+    if (wr == h) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            T[(mt * 16 + (lane >> 4) * 4 + r) * EP + wc * 64 + nt * 16 + (lane & 15)] =
+                acc[mt][nt][r];
+    }
+  };
+  const unsigned tb = (unsigned)(size_t)(const lds_char*)(const char*)T;
+  const unsigned gb = (unsigned)(size_t)(const lds_char*)(const char*)GF;
+  f32x4 cs0 = {0.f, 0.f, 0.f, 0.f}, cs1 = {0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int q) {  // rows 32 q + grp + 8 k, k = 0..3: 8 stores per thread
+    const unsigned g0 = gb + (q & 1) * 2 * GBW_Q + cq * 8;
+    const unsigned t0 = tb + ((q & 1) * 32) * EP * 4 + cq * 16;
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {
+      const int row = grp + 8 * k;
+      const int m = m0 + 32 * q + row;
+      f32x4 v;
+      bf16x4 gv, fv;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(t0 + row * EP * 4) : "memory");
+      asm volatile("ds_read_b64 %0, %1" : "=v"(gv) : "v"(g0 + row * 256) : "memory");
+      asm volatile("ds_read_b64 %0, %1" : "=v"(fv) : "v"(g0 + GBW_Q + row * 256) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v), "+v"(gv), "+v"(fv));
+      f32x4 dg, df;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float d0, d1;
+        gate_bwd_(v[e], (float)gv[e], (float)fv[e], d0, d1);
+        dg[e] = d0;
+        df[e] = d1;
+      }
+      if (a.csum) {
+        cs0 += dg;
+        cs1 += df;
+      }
+      __bf16* yr = a.ybf + (long long)m * a.ybf_ld + col;
+      gbw_st8(yr, dg);
+      gbw_st8(yr + a.C, df);
+    }
+  };
+  gbw_bar();  // every wave is done with the K loop's images (no loads outstanding)
+  fetch(0);
+  fetch(1);
+  stage(0);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // quarter 0 landed (quarter 1 may not)
+  gbw_bar();
+  compute(0);
+  gbw_bar();  // buffer 0 free
+  fetch(2);
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // quarter 1 (then 8 stores, quarter 2)
+  gbw_bar();
+  compute(1);
+  gbw_bar();  // buffer 1 and T free
+  fetch(3);
+  stage(1);
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // quarter 2 (then 8 stores, quarter 3)
+  gbw_bar();
+  compute(2);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // quarter 3 (then 8 stores)
+  gbw_bar();
+  compute(3);
+  if (a.csum) {  // uniform
+    const int c4 = cq * 4;
+    *(f32x4*)(X + grp * 2 * BN + c4) = cs0;
+    *(f32x4*)(X + grp * 2 * BN + BN + c4) = cs1;
+    gbw_bar();
+    const int j = tid;  // NTHR == 2 * BN: d(gate) columns, then d(filter)
+    const int c = n0 + (j & (BN - 1));
+    float t = X[j];
+#pragma unroll
+    for (int q = 1; q < CS_GROUPS; ++q) t += X[q * 2 * BN + j];
+    a.csum[(long long)(m0 / BM) * a.csum_ld + (j < BN ? c : a.C + c)] = t;
+  }
+}
+
 // GATE_BWD epilogue rows per operand batch in the 128 x 128 kernel: 2 builds without scratch
 // (162 VGPRs; 4 spills 124 B) and takes the C = 256 gate-backward dgrad from 51.4 to 47.5 us
 constexpr int GBW_EB = 2;
@@ -1132,6 +1262,10 @@ __device__ __forceinline__ void b16_body(const GemmArgs& a, const GemmArgs& a2) 
         for (int j = 0; j < 4; ++j)
           pz[(long long)row * Npad + n0 + wc * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
       }
+    return;
+  }
+  if constexpr (EPK == EPI_GATE_BWD) {  // instance launched only with a.gbw_dma
+    gate_bwd_epilogue_dma(a, acc, m0, n0, wr, wc, lane, tid, smem);
     return;
   }
   if (a.vec_out) {
@@ -2568,7 +2702,6 @@ __device__ __forceinline__ int wg_swz(int row) { return ((row & 3) << 2) | ((row
 // it: it cannot tell the read from the ring slots being filled), which serialised each
 // chunk's DMA with the MFMAs.  The caller waits with a counted lgkmcnt that takes the
 // destination registers as operands, so nothing reads them earlier.
-typedef __attribute__((address_space(3))) char lds_char;
 __device__ __forceinline__ void wg_frag_issue(const char* img, int c0, int lane, bf16x4& lo,
                                               bf16x4& hi) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
@@ -3011,6 +3144,8 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
 // 2 -> 44.8 us, 1 (5 / 4 / 3 stages) -> 53.3 / 53.0 / 50.2 us, 0 (128 x 128) -> 51.0 us:
 // more LDS stages in flight did not pay.
 static int g_big_tile = 2, g_big_stages = 5, g_big_all = 0;
+// GATE_BWD LDS-DMA epilogue (gate_bwd_epilogue_dma); off: the register form, same bits
+static int g_gbw_dma = 1;
 // split-K fills about this many workgroups (only when the caller passes a workspace)
 static const int SPLITK_TARGET = 256;
 // launches of fewer than 128 tiles of 128 x 128 that the 64 x 64 kernel does not take (no
@@ -3149,7 +3284,9 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     if (es != hipSuccess) return ENSVS_E_HIP;                                                  \
     hipLaunchKernelGGL((conv_gemm_b16_kernel<2, E>), grid, dim3(NTHR), l2, st, a);             \
   } while (0)
-  if (spec && a.epi == EPI_RESSKIP) {
+  if (spec && a.gbw_dma) {
+    SPEC(EPI_GATE_BWD);
+  } else if (spec && a.epi == EPI_RESSKIP) {
     SPEC(EPI_RESSKIP);
   } else if (spec && a.epi == EPI_ADDSCALE) {
     SPEC(EPI_ADDSCALE);
@@ -3189,6 +3326,11 @@ ENSVS_API int ensvs_set_small(int on) {
 
 ENSVS_API int ensvs_set_dual_small(int on) {
   g_dual_small = on ? 1 : 0;
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_set_gbw_dma(int on) {
+  g_gbw_dma = on ? 1 : 0;
   return ENSVS_OK;
 }
 
@@ -3254,6 +3396,9 @@ ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, in
     a.ybf_radd_ld = ybf_radd_ld;
     a.gate8 = a.gate8 && ((uintptr_t)ybf & 15) == 0 && ybf_ld % 8 == 0;
   }
+  a.gbw_dma = g_gbw_dma && a.epi == EPI_GATE_BWD && a.aux1_bf && a.ybf && !a.Y && !a.bias &&
+              !a.ybf_radd && C % BN == 0 && a.M % BM == 0 && ((uintptr_t)aux1 & 15) == 0 &&
+              ld1 % 8 == 0 && ((uintptr_t)ybf & 15) == 0 && ybf_ld % 8 == 0;
   return launch_b16(a, segs, nseg, B, Npad, W, stages, (hipStream_t)stream);
 }
 

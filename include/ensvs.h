@@ -78,6 +78,9 @@ int ensvs_set_big_tile(int mode, int stages);
  * tiles added through LDS; default off: the one-group kernel, the same bits as the
  * register-staged kernel; kept for the sum-order tests). */
 int ensvs_set_dual_small(int on);
+/* DiffNet gate-backward dgrad (EPI_GATE_BWD, production form) through the LDS-DMA epilogue
+ * (default 1) or the register-batched one (0): same bits; for the bitwise test. */
+int ensvs_set_gbw_dma(int on);
 /* Launches of fewer than 128 output tiles of 128 x 128 (small M: the 2 000-frame reverse-
  * diffusion GEMMs) run a 64 x 64-tile kernel that fills the chip (default on; it takes
  * precedence over the two-K-group kernel and split-K); same accumulation order as the

@@ -294,3 +294,43 @@ def test_small_kernel_ragged_n_bitwise(N, relu):
         K.set_dual_small(False)
     assert torch.equal(ref[0], got[0])
     assert torch.equal(ref[1], got[1])
+
+
+@pytest.mark.parametrize("C,B,T,ldm", [(256, 3, 256, 1), (128, 2, 384, 3), (256, 30, 1024, 1)])
+def test_gate_bwd_dma_epilogue_bitwise(C, B, T, ldm):
+    """The DiffNet gate-backward dgrad in its production form (bf16 dx / dss segments, bf16
+    gate/filter save in, bf16 d(pre) out into a wider [M][ldm * 2C] buffer, per-tile column
+    sums, no fp32 Y): the LDS-DMA epilogue equals the register-batched one bit for bit."""
+    torch.manual_seed(C + T)
+    M = B * T
+    dx = torch.randn(M, C, device=DEV).to(torch.bfloat16)
+    dss = torch.randn(M, C, device=DEV).to(torch.bfloat16)
+    w0 = (torch.randn(C, C, 1, device=DEV) / C ** 0.5).to(torch.bfloat16).float()
+    w1 = (torch.randn(C, C, 1, device=DEV) / C ** 0.5).to(torch.bfloat16).float()
+    pb, (r0, r1) = _pack([w0, w1])
+    segs = [K.Seg(dx, C, C, r0, T), K.Seg(dss, C, C, r1, T)]
+    gf = (torch.randn(M, 2 * C, device=DEV) * 2).to(torch.bfloat16)
+    Y = torch.empty(M, 2 * C, device=DEV)
+
+    def run(on):
+        L.call("ensvs_set_gbw_dma", int(on))
+        yb = torch.full((M, ldm * 2 * C), 3.0, device=DEV).to(torch.bfloat16)
+        cs = torch.full((M // 128, ldm * 2 * C), 7.0, device=DEV)
+        K.gemm(segs, B, T, C, pb, Y, 2 * C, epi=L.EPI_GATE_BWD, aux1=gf, ld1=2 * C, C=C,
+               ybf=yb, ybf_ld=ldm * 2 * C, csum=cs, csum_ld=ldm * 2 * C, keep_y=False)
+        torch.cuda.synchronize()
+        return yb, cs
+    try:
+        y0, c0 = run(False)
+        y1, c1 = run(True)
+    finally:
+        L.call("ensvs_set_gbw_dma", 1)
+    assert torch.equal(y0, y1) and torch.equal(c0, c1)
+    assert (y1[:, 2 * C:] == 3.0).all() and (c1[:, 2 * C:] == 7.0).all()
+    # and the values: d(gate), d(filter) of z = sigmoid(g) tanh(f) against float64
+    g, f = gf.double()[:, :C], gf.double()[:, C:]
+    dz = dx.double() @ w0.double()[:, :, 0].t() + dss.double() @ w1.double()[:, :, 0].t()
+    sg, th = torch.sigmoid(g), torch.tanh(f)
+    ref = torch.cat([dz * th * sg * (1 - sg), dz * sg * (1 - th * th)], 1)
+    got = y1[:, :2 * C].double()
+    assert ((got - ref).abs().max() / ref.abs().max()).item() < 1e-2

@@ -40,13 +40,17 @@ def run(conc, P, T, steps=3):
     rec = engine.BRANCH_TIMES
     engine.BRANCH_TIMES = None
     n = len(rec) // steps
-    last = rec[-n:]  # last step: 4 fwd regions then 4 bwd regions
+    last = rec[-n:]  # last step: the branch regions (+ tagged single events)
     out = {}
-    t_ref = last[0][1]
-    for k, (i, s, e) in enumerate(last):
-        phase = "fwd" if k < 4 else "bwd"
-        out[f"{NAMES[i]}.{phase}"] = (f"{s.elapsed_time(e):.2f}"
-                                      f"[{t_ref.elapsed_time(s):.1f}-{t_ref.elapsed_time(e):.1f}]")
+    regions = [r for r in last if len(r) == 3]
+    t_ref = regions[0][1]
+    for k, (i, s, e) in enumerate(regions):
+        phase = "fwd" if k < len(regions) // 2 and len(regions) == 8 else "bwd" if len(regions) == 8 else "br"
+        out[f"{NAMES[i]}.{phase}.{k}"] = (f"{s.elapsed_time(e):.2f}"
+                                          f"[{t_ref.elapsed_time(s):.1f}-{t_ref.elapsed_time(e):.1f}]")
+    for r in last:
+        if len(r) == 2:
+            out[f"{r[0]}@{len(out)}"] = f"{t_ref.elapsed_time(r[1]):.1f}"
     return step_ms, out
 
 

@@ -64,6 +64,30 @@ cases = {
                                        accum=True, alpha=0.2236, C=C, ybf=Yb, ybf_ld=C),
     "res_skip NONE": lambda: K.gemm(segs_rs, B, T, 2 * C, pb, Y, 2 * C, epi=EPI_NONE),
 }
+# FFConvLSTM encoder launches: the LSTM input projection (K = 128 conv channels -> 8H = 512
+# gates, bias, fp32 out) and the ReLU-mask conv dgrad (K = N = 256, fp32 mask, bf16 copy)
+xk = bf(M, 128)
+w_ih = pb2 = K.PackedBuffer(L.DT_BF16)
+r_ih = pb2.add(torch.randn(512, 128, 1, device=dev) * 0.05, 512, 128, 1, 128, 1, 1)
+r_rm = pb2.add(torch.randn(256, 256, 1, device=dev) * 0.05, 256, 256, 1, 256, 1, 1)
+pb2.finalize(dev)
+pb2.repack()
+gates = torch.empty(M, 512, device=dev)
+b512 = torch.randn(512, device=dev)
+mask_src = torch.randn(M, 256, device=dev)
+nd = torch.empty(M, 256, device=dev)
+ndb = torch.empty(M, 256, device=dev, dtype=torch.bfloat16)
+cases.update({
+    "w_ih PLAIN": lambda: K.gemm([K.Seg(xk, 128, 128, r_ih, T)], B, T, 512, pb2, gates, 512,
+                                 bias=b512),
+    "w_ih NONE": lambda: K.gemm([K.Seg(xk, 128, 128, r_ih, T)], B, T, 512, pb2, gates, 512,
+                                epi=EPI_NONE),
+    "relu_mask RELU_MASK": lambda: K.gemm([K.Seg(z, C, C, r_rm, T)], B, T, 256, pb2, nd, 256,
+                                          epi=L.EPI_RELU_MASK, aux1=mask_src, ld1=256, ybf=ndb,
+                                          ybf_ld=256),
+    "relu_mask NONE": lambda: K.gemm([K.Seg(z, C, C, r_rm, T)], B, T, 256, pb2, nd, 256,
+                                     epi=EPI_NONE),
+})
 only = sys.argv[1:] or list(cases)
 for name in cases:
     if any(o in name for o in only):

@@ -5,33 +5,13 @@ be loaded, importing anything that launches a kernel raises immediately.
 """
 import ctypes
 import os
-import sys
-import warnings
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# The training step runs its branches on concurrent HIP streams (engine.Branches).  With
-# HIP's default 4 hardware queues per process the step's streams share queues; 8 measured
-# 20.6 vs 21.0-21.4 ms per 30 x 1024 step (16: 22.8).  Only takes effect when the HIP
-# runtime is not initialised yet; an explicit GPU_MAX_HW_QUEUES wins.
-HW_QUEUES = "8"
-
-
-def _set_hw_queues():
-    if "GPU_MAX_HW_QUEUES" in os.environ:
-        return
-    os.environ["GPU_MAX_HW_QUEUES"] = HW_QUEUES
-    torch = sys.modules.get("torch")
-    cuda = getattr(torch, "cuda", None) if torch is not None else None
-    if cuda is not None and cuda.is_initialized():
-        warnings.warn(
-            "ensvs: the HIP runtime was initialised before ensemble_svs_with_interactions_amd "
-            f"was imported, so GPU_MAX_HW_QUEUES={HW_QUEUES} does not apply (HIP keeps its "
-            "default 4 hardware queues; the concurrent branch schedule measured slower with "
-            "4).  Import the package, or export GPU_MAX_HW_QUEUES, before the first CUDA call.",
-            RuntimeWarning, stacklevel=3)
-
-
-_set_hw_queues()
+# The training step runs its branches on concurrent HIP streams (engine.Branches), one
+# hardware queue each under HIP's default GPU_MAX_HW_QUEUES=4 (what the GPU boxes export).
+# No queue count is forced: 8 queues measured 15.9 vs 14.6 ms per 30 x 1024 step in round 4
+# (profiles/r4_defer_params_ab.txt; round 2's schedule had measured the opposite, 20.6 vs
+# 21.0-21.4 ms, before the branch start order and the recurrence LDS reservation).
 # ENSVS_LIB: another in-tree build of the same ABI, for A/B timing of a kernel change
 # (tools/ab_lib.sh); the default is the package's own libensvs.so
 LIB_PATH = os.environ.get("ENSVS_LIB") or os.path.join(_HERE, "libensvs.so")
@@ -88,6 +68,7 @@ SIGNATURES = {
     "ensvs_set_big_tile": [c_int, c_int],
     "ensvs_set_dual_small": [c_int],
     "ensvs_set_gbw_dma": [c_int],
+    "ensvs_set_wgrad_big": [c_int],
     "ensvs_set_small": [c_int],
     "ensvs_set_recurrence_exclusive": [c_int],
     "ensvs_note_mask": [c_vp, c_int, c_int, c_vp, c_vp],

@@ -2845,6 +2845,142 @@ __global__ __launch_bounds__(NTHR) void wgrad_b16_kernel(const WgradArgs a) {
   }
 }
 
+// ------------------------------------------------- weight grads, 256 x 256 tiles
+// wgrad_b16_kernel with a 256 (dy channels) x 256 (x channels) output tile per workgroup of 8
+// waves (2 x 4 of 128 x 64: 8 x 4 MFMA tiles), one workgroup per CU (a 4-slot ring of 32 KB
+// chunks).  Per frame of a row split it stages 2 x 256 channels where the 128 x 128 kernel's
+// four workgroups stage 4 x 256: half the L2 -> LDS bytes, the bound of the 128 x 128 form
+// (the DiffNet dilated conv: 380 MB per launch, 42 us).  Each output element takes the same
+// chunk sequence and MFMA order as in wgrad_b16_kernel for the same split count: the same bits.
+// Staging: the chunk's four [32 frames][128 channels] sub-images (dy lo / hi, x lo / hi, with
+// wg_off's swizzle); wave w moves rows 4w .. 4w + 3 of each (one 1-KB DMA per sub-image).
+constexpr int WGB = 256, NTHRW = 512;
+__device__ __forceinline__ void wgrad_tile_big(const WgradArgs& a, int& n0, int& k0, int& j,
+                                               int& s) {
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int total = gx * gy * gridDim.z;
+  const int q = total >> 3, r = total & 7, x = b & 7;
+  const int idx = x * q + min(x, r) + (b >> 3);  // XCD-contiguous, as wgrad_tile
+  const int W = gx * gy * a.taps;
+  s = idx / W;
+  const int w = idx - s * W;
+  j = w / (gx * gy);
+  const int t = w - j * gx * gy;
+  k0 = (t / gx) * WGB;
+  n0 = (t % gx) * WGB;
+}
+
+__global__ __launch_bounds__(NTHRW) void wgrad_b16_big_kernel(const WgradArgs a) {
+  constexpr int IMG = BK * 256;  // one sub-image: 32 frames x 128 channels bf16
+  constexpr int STG = 4 * IMG;   // dy lo, dy hi, x lo, x hi
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  int n0, k0, j, s;
+  wgrad_tile_big(a, n0, k0, j, s);
+  const int mbeg = s * a.rows_per_split;
+  const int mend = min(a.M, mbeg + a.rows_per_split);
+  const int nch = mbeg < mend ? (mend - mbeg + BK - 1) / BK : 0;
+  const __bf16* dy = (const __bf16*)a.dy;
+  const __bf16* x = (const __bf16*)a.x;
+  unsigned long long zpu = (unsigned long long)(const void*)g_zero;
+  asm volatile("" : "+s"(zpu));
+  const char* zp = (const char*)zpu;
+  const int fr = wid * 4 + (lane >> 4);            // this lane's frame row of the chunk
+  const int cc = (lane & 15) ^ wg_swz(fr);         // the logical 16-B chunk it fetches
+  int fb = (mbeg + fr) / a.Tout, ft = mbeg + fr - fb * a.Tout;
+  auto issue = [&](int ch) __attribute__((always_inline)) {
+    char* base = smem + (ch % WNS) * STG + (wid * 4) * 256;
+    const int m = mbeg + ch * BK + fr;
+    const bool mv = m < mend;
+    const int src = pad_src(ft + a.shift0 + j * a.dil, a.Tin, a.pad);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int n = n0 + h * 128 + cc * 8, k = k0 + h * 128 + cc * 8;
+      glds16((mv && n < a.N) ? (const void*)(dy + (long long)m * a.ldy + n) : (const void*)zp,
+             base + h * IMG);
+      glds16((mv && src >= 0 && k < a.K)
+                 ? (const void*)(x + (long long)(fb * a.Tin + src) * a.ldx + k)
+                 : (const void*)zp,
+             base + (2 + h) * IMG);
+    }
+    ft += BK;
+    while (ft >= a.Tout) {
+      ft -= a.Tout;
+      ++fb;
+    }
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // 4 DMA instructions per lane and chunk, as wgrad_b16_kernel
+#pragma unroll
+  for (int c = 0; c < WNS - 1; ++c)
+    if (c < nch) issue(c);
+  for (int ch = 0; ch < nch; ++ch) {
+    const int ahead = min(WNS - 2, nch - 1 - ch);
+    if (ahead >= 2) wait_vm_n<8>();
+    else if (ahead == 1) wait_vm_n<4>();
+    else wait_vm_n<0>();
+    __builtin_amdgcn_s_barrier();  // chunk ch visible; chunk ch-1's slot free for the refill
+    if (ch + WNS - 1 < nch) issue(ch + WNS - 1);
+    const char* St = smem + (ch % WNS) * STG;
+    const char* Ad = St + wr * IMG;                  // this wave's 128 dy channels
+    const char* Bx = St + (2 + (wc >> 1)) * IMG;     // the x sub-image of its 64 channels
+    const int cb = (wc & 1) * 64;
+    bf16x4 blo[4], bhi[4], alo[8], ahi[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wg_frag_issue(Bx, cb + 16 * q, lane, blo[q], bhi[q]);
+    wg_frag_issue(Ad, 0, lane, alo[0], ahi[0]);
+    wg_frag_issue(Ad, 16, lane, alo[1], ahi[1]);
+    asm volatile("s_waitcnt lgkmcnt(4)"
+                 : "+v"(blo[0]), "+v"(bhi[0]), "+v"(blo[1]), "+v"(bhi[1]), "+v"(blo[2]),
+                   "+v"(bhi[2]), "+v"(blo[3]), "+v"(bhi[3]));
+    bf16x8 fbv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      fbv[q] = __builtin_shufflevector(blo[q], bhi[q], 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i + 2 < 8) {
+        wg_frag_issue(Ad, 16 * (i + 2), lane, alo[i + 2], ahi[i + 2]);
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(alo[i]), "+v"(ahi[i]));
+      } else if (i == 6) {
+        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(alo[i]), "+v"(ahi[i]));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(alo[i]), "+v"(ahi[i]));
+      }
+      const bf16x8 fa = __builtin_shufflevector(alo[i], ahi[i], 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc[i][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fbv[q], acc[i][q], 0, 0, 0);
+    }
+  }
+  float* out = a.splits == 1 ? nullptr : a.part + ((long long)(s * a.taps + j) * a.N) * a.K;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = k0 + wc * 64 + q * 16 + (lane & 15);
+    if (k >= a.K) continue;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wr * 128 + i * 16 + (lane >> 4) * 4 + r;
+        if (n >= a.N) continue;
+        if (out) {
+          out[(long long)n * a.K + k] = acc[i][q][r];
+        } else {
+          float* d = a.dst + n * a.sn + k * a.sk + j * a.sj;
+          const float v = acc[i][q][r] * a.scale;
+          *d = a.accum ? *d + v : v;
+        }
+      }
+  }
+}
+
 // dst[n*sn + k*sk + j*sj] (+)= scale * sum_s part[s][j][n][k]   (fixed summation order)
 // grid (cdiv(K, 256), N * taps): one (tap, n) row of K per block row, coalesced over k.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
@@ -3146,6 +3282,18 @@ ENSVS_API int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int T
 static int g_big_tile = 2, g_big_stages = 5, g_big_all = 0;
 // GATE_BWD LDS-DMA epilogue (gate_bwd_epilogue_dma); off: the register form, same bits
 static int g_gbw_dma = 1;
+// bf16 weight gradients with N, K >= 256 on the 256 x 256-tile kernel (same bits for the same
+// split count); off: the 128 x 128 one
+static int g_wgrad_big = 1;
+// Only where there are many output tiles (>= 16 of 256 x 256): the 256 x 256 form was slower
+// wherever a few tiles take many row splits (tools/wgrad_bench.py: DiffNet dilated conv 48.2
+// -> 52.5 us, residual 1x1 24.5 -> 35.0, LSTM W_ih 33.5 -> 42.9) and faster on the block-shared
+// conditioner (N = 10 240: 296 -> 231 us) and skip projection (K = 5 120: 131 -> 118 us):
+// with one workgroup per CU its chunks ran 1.8 us apart, twice the 128 x 128 kernel's per-CU
+// byte rate lost to the barrier of one 8-wave workgroup (profiles/r4_wgrad_big_bench.txt).
+static bool wgrad_big_shape(int N, int K, int taps) {
+  return g_wgrad_big && N >= WGB && K >= WGB && (long long)cdiv(N, WGB) * cdiv(K, WGB) * taps >= 16;
+}
 // split-K fills about this many workgroups (only when the caller passes a workspace)
 static const int SPLITK_TARGET = 256;
 // launches of fewer than 128 tiles of 128 x 128 that the 64 x 64 kernel does not take (no
@@ -3326,6 +3474,11 @@ ENSVS_API int ensvs_set_small(int on) {
 
 ENSVS_API int ensvs_set_dual_small(int on) {
   g_dual_small = on ? 1 : 0;
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_set_wgrad_big(int on) {
+  g_wgrad_big = on ? 1 : 0;
   return ENSVS_OK;
 }
 
@@ -3602,10 +3755,19 @@ ENSVS_API int ensvs_conv_wgrad_bf16(const void* dy, int ldy, const void* x, int 
   a.sj = sj;
   a.scale = scale;
   a.accum = accum;
-  dim3 grid(cdiv(N, BM), cdiv(K, BN), taps * splits);
   if (N * taps > 65535) return ENSVS_E_SHAPE;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(wgrad_b16_kernel, grid, dim3(NTHR), WNS * 2 * BK * 256, st, a);
+  if (wgrad_big_shape(N, K, taps)) {
+    const size_t lds = WNS * 4 * BK * 256;
+    static const hipError_t e = hipFuncSetAttribute(
+        (const void*)wgrad_b16_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return ENSVS_E_HIP;
+    hipLaunchKernelGGL(wgrad_b16_big_kernel, dim3(cdiv(N, WGB), cdiv(K, WGB), taps * splits),
+                       dim3(NTHRW), lds, st, a);
+  } else {
+    dim3 grid(cdiv(N, BM), cdiv(K, BN), taps * splits);
+    hipLaunchKernelGGL(wgrad_b16_kernel, grid, dim3(NTHR), WNS * 2 * BK * 256, st, a);
+  }
   ENSVS_CHECK_LAUNCH();
   if (splits > 1) {
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(K, 256), N * taps), dim3(256), 0, st, part,

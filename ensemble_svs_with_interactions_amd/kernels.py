@@ -393,6 +393,10 @@ def scratch(nfloats, device, key="part"):
 
 # weight gradients split the frame reduction until about this many workgroups (tile x split)
 WGRAD_TARGET = 512  # workgroups a weight gradient aims for (256: 20.7, 1024: 20.5 vs 20.1 ms/step)
+# bf16 weight gradients with >= 16 output tiles of 256 x 256: the 256 x 256-tile kernel (its
+# switch is ensvs_set_wgrad_big, the shape rule gemm.hip wgrad_big_shape; splits are chosen
+# here for one workgroup per CU)
+WGRAD_BIG = {"on": True, "target": 256}
 
 
 def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, sk, sj,
@@ -401,6 +405,12 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
     """dst (+)= scale * dy^T x (conv/linear weight gradient).  dy and x may both be bf16
     tensors already rounded (radd then folded into x): the glds-staged kernel, same bits."""
     M = B * Tout
+    if (splits is None and WGRAD_BIG["on"] and N >= 256 and K >= 256 and
+            -(-N // 256) * -(-K // 256) * taps >= 16):
+        # the 256 x 256-tile kernel (gemm.hip wgrad_b16_big_kernel) for bf16 operands, one
+        # workgroup per CU; fp32 sources take the same split count (the same bits)
+        tiles = -(-N // 256) * -(-K // 256) * taps
+        splits = max(1, min(64, WGRAD_BIG["target"] // max(tiles, 1), -(-M // 512)))
     if splits is None:
         tiles = -(-N // 128) * -(-K // 128) * taps
         splits = max(1, min(64, WGRAD_TARGET // max(tiles, 1), -(-M // 256)))

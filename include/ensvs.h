@@ -81,6 +81,9 @@ int ensvs_set_dual_small(int on);
 /* DiffNet gate-backward dgrad (EPI_GATE_BWD, production form) through the LDS-DMA epilogue
  * (default 1) or the register-batched one (0): same bits; for the bitwise test. */
 int ensvs_set_gbw_dma(int on);
+/* bf16-operand weight gradients with N, K >= 256 on the 256 x 256-tile kernel (default 1) or
+ * the 128 x 128 one (0): same bits for the same split count. */
+int ensvs_set_wgrad_big(int on);
 /* Launches of fewer than 128 output tiles of 128 x 128 (small M: the 2 000-frame reverse-
  * diffusion GEMMs) run a 64 x 64-tile kernel that fills the chip (default on; it takes
  * precedence over the two-K-group kernel and split-K); same accumulation order as the

@@ -248,3 +248,36 @@ def test_embedding_and_speaker_backward_deterministic():
     ref = torch.full((R, C), 0.5, device=DEV).index_add_(0, spk, dseq)
     torch.cuda.synchronize()
     assert rel(tab, ref) < 1e-6
+
+
+@pytest.mark.parametrize("shape", [(30, 1024, 256, 512, 3, 4, L.PAD_ZERO),
+                                   (3, 517, 264, 296, 1, 1, L.PAD_ZERO),
+                                   (2, 333, 512, 256, 7, 1, L.PAD_REFLECT),
+                                   (4, 250, 256, 10240, 1, 1, L.PAD_ZERO),
+                                   (2, 300, 1032, 1016, 1, 1, L.PAD_ZERO),
+                                   (3, 200, 520, 2048, 3, 2, L.PAD_ZERO)])
+@pytest.mark.parametrize("splits", [1, 5, 21])
+def test_wgrad_big_tile_bitwise(shape, splits):
+    """bf16 weight gradients on the 256 x 256-tile kernel (shapes with >= 16 of its tiles)
+    equal the 128 x 128 kernel's bits for the same split count (ragged N / K / M, taps,
+    padding, direct and split-reduced); other shapes run the 128 x 128 kernel either way."""
+    torch.manual_seed(13)
+    B, T, Cin, Cout, taps, dil, pad = shape
+    M = B * T
+    xs = K.cast_bf16(torch.randn(M, Cin, device=DEV), Cin, Cin, M)
+    gs = K.cast_bf16(torch.randn(M, Cout, device=DEV), Cout, Cout, M)
+    outs = []
+    try:
+        for big in (False, True):
+            L.call("ensvs_set_wgrad_big", int(big))
+            dw = torch.full((Cout, Cin, taps), 0.25, device=DEV)
+            K.wgrad(gs, Cout, xs, Cin, B, T, T, Cout, Cin, taps, dil, -dil * (taps // 2), pad, dw,
+                    Cin * taps, taps, 1, dtype=L.DT_BF16, accum=True, scale=0.5, splits=splits)
+            outs.append(dw)
+        torch.cuda.synchronize()
+    finally:
+        L.call("ensvs_set_wgrad_big", 1)
+    assert torch.equal(outs[0], outs[1])
+    if taps == 1:
+        ref = torch.einsum("mn,mk->nk", gs.double(), xs.double())
+        assert rel(outs[1][:, :, 0].double() - 0.25, 0.5 * ref) < 1e-5

@@ -88,6 +88,11 @@ cases.update({
     "relu_mask NONE": lambda: K.gemm([K.Seg(z, C, C, r_rm, T)], B, T, 256, pb2, nd, 256,
                                      epi=EPI_NONE),
 })
+cases["dil_dgrad ADDSCALE nocsum"] = lambda: K.gemm(segs_dil, B, T, C, pb, Y, C,
+                                                   epi=L.EPI_ADDSCALE, aux1=xres, ld1=C,
+                                                   alpha=0.7071)
+if os.environ.get("BIG"):  # 256 x 256 tiles for every epilogue that allows them
+    L.call("ensvs_set_big_tile", 3, 0)
 only = sys.argv[1:] or list(cases)
 for name in cases:
     if any(o in name for o in only):

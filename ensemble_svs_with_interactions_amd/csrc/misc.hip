@@ -249,6 +249,69 @@ __global__ void bn_bwd_reduce_kernel(const float* __restrict__ dout, int ldd,
   }
 }
 
+// bn_bwd_reduce_kernel with four channels per lane (the bn_vec4 conditions): a 256-thread
+// block covers LPR = min(64, C / 4) lanes of 4 channels per row and 256 / LPR rows at a time,
+// 16-B loads with 4 rows in flight per lane (the scalar form read 4 B per lane: 21 us per
+// 30 720 x 256 launch, profiles/r4_train_kernel_stats.csv).  Rows r0 + rl + RB k per lane in
+// order, then the RB row lanes folded in order: deterministic.
+template <int LPR>
+__global__ __launch_bounds__(256) void bn_bwd_reduce4_kernel(
+    const float* __restrict__ dout, int ldd, const float* __restrict__ y, int ldy, long long Mg,
+    int C, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, int rps,
+    float* __restrict__ part) {
+  // grid: (ceil(C / (4 LPR)), S, G); part[g][s][2][C]
+  constexpr int RB = 256 / LPR;
+  __shared__ f32x4 red[2][RB][LPR + 1];
+  const int cq = threadIdx.x % LPR, rl = threadIdx.x / LPR;
+  const int col = (blockIdx.x * LPR + cq) * 4;
+  const int s = blockIdx.y, g = blockIdx.z, S = gridDim.y;
+  const long long r0 = (long long)g * Mg + (long long)s * rps;
+  const long long r1 = min((long long)g * Mg + Mg, r0 + rps);
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, bs = {0.f, 0.f, 0.f, 0.f};
+  if (col < C) {
+    const f32x4 mu = *(const f32x4*)(mean + g * C + col), rs = *(const f32x4*)(rstd + g * C + col);
+    const f32x4 ga = *(const f32x4*)(gamma + col), be = *(const f32x4*)(beta + col);
+    auto step = [&](f32x4 yv, f32x4 dv) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xh = (yv[e] - mu[e]) * rs[e];
+        const float z = xh * ga[e] + be[e];
+        const float dz = z > 0.f ? dv[e] : 0.f;
+        a[e] += dz;
+        bs[e] += dz * xh;
+      }
+    };
+    long long r = r0 + rl;
+    for (; r + 3 * RB < r1; r += 4 * RB) {
+      f32x4 yv[4], dv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        yv[k] = *(const f32x4*)(y + (r + k * RB) * ldy + col);
+        dv[k] = *(const f32x4*)(dout + (r + k * RB) * ldd + col);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) step(yv[k], dv[k]);
+    }
+    for (; r < r1; r += RB)
+      step(*(const f32x4*)(y + r * ldy + col), *(const f32x4*)(dout + r * ldd + col));
+  }
+  red[0][rl][cq] = a;
+  red[1][rl][cq] = bs;
+  __syncthreads();
+  if (rl == 0 && col < C) {
+    f32x4 ta = red[0][0][cq], tb = red[1][0][cq];
+#pragma unroll
+    for (int i = 1; i < RB; ++i) {
+      ta += red[0][i][cq];
+      tb += red[1][i][cq];
+    }
+    float* p = part + (((long long)g * S + s) * 2) * C;
+    *(f32x4*)(p + col) = ta;
+    *(f32x4*)(p + C + col) = tb;
+  }
+}
+
 // sums[g][0|1][c] = sum_s part; dgamma[c] += sum_g sums1, dbeta[c] += sum_g sums0
 // grid (ceil(C/64), G), 1024 threads: 16 lane rows split the S partials of 64 channels
 // (s = row, row + 16, ...), then fold in a fixed order; one workgroup per group g (a
@@ -862,8 +925,20 @@ ENSVS_API int ensvs_bn_bwd(const float* dout, int ldd, const float* y, int ldy, 
   const int G = (int)(M / Mg);
   int S = (int)std::max<long long>(1, std::min<long long>(max_splits, Mg / 64));
   int rps = (int)((Mg + S - 1) / S);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(cdiv(C, 64), S, G), dim3(256), 0, st, dout, ldd, y,
-                     ldy, Mg, C, mean, rstd, gamma, beta, rps, part);
+  if (bn_vec4(C, {ldd, ldy}, {dout, y, mean, rstd, gamma, beta, part}, M)) {
+    if (C >= 256)
+      hipLaunchKernelGGL(bn_bwd_reduce4_kernel<64>, dim3(cdiv(C, 256), S, G), dim3(256), 0, st,
+                         dout, ldd, y, ldy, Mg, C, mean, rstd, gamma, beta, rps, part);
+    else if (C >= 128)
+      hipLaunchKernelGGL(bn_bwd_reduce4_kernel<32>, dim3(cdiv(C, 128), S, G), dim3(256), 0, st,
+                         dout, ldd, y, ldy, Mg, C, mean, rstd, gamma, beta, rps, part);
+    else
+      hipLaunchKernelGGL(bn_bwd_reduce4_kernel<16>, dim3(cdiv(C, 64), S, G), dim3(256), 0, st,
+                         dout, ldd, y, ldy, Mg, C, mean, rstd, gamma, beta, rps, part);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(cdiv(C, 64), S, G), dim3(256), 0, st, dout, ldd,
+                       y, ldy, Mg, C, mean, rstd, gamma, beta, rps, part);
+  }
   ENSVS_CHECK_LAUNCH();
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(cdiv(C, 64), G), dim3(1024), 0, st, part, S, C,
                      sums);

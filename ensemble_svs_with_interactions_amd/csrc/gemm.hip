@@ -90,6 +90,9 @@ struct GemmArgs {
   // GATE_BWD in the production form (bf16 aux1 and ybf, no Y / bias / ybf_radd, C and M
   // multiples of 128, 16-B aligned rows): the 128 x 128 kernel's LDS-DMA epilogue
   int gbw_dma;
+  // ADDSCALE with fp32 aux1 and Y, a bf16 copy, no relu / ybf_radd, M and N multiples of 128,
+  // 16-B aligned rows: the LDS-DMA epilogue (addscale_epilogue_dma)
+  int as_dma;
 };
 
 template <typename T>
@@ -1091,6 +1094,105 @@ __device__ __forceinline__ void gate_bwd_epilogue_dma(const GemmArgs& a, f32x4 (
   }
 }
 
+// The dilated-conv dgrad's ADDSCALE epilogue (Y = alpha aux1 + acc [+ bias], its bf16 copy,
+// the accumulator's per-tile column sums) in the same form as gate_bwd_epilogue_dma: the fp32
+// aux1 rows (512 B of the tile's columns per row) fetched by LDS-DMA in double-buffered
+// 32-row quarters one quarter ahead, two stores per row (Y, bf16 copy), counted waits.  Same
+// rows, arithmetic and column-sum order as the register form: the same bits.
+// A store of more than 8 bytes reads its data VGPRs after issue: a VALU write to them in the
+// next slot is a hazard the compiler's hazard recognizer cannot see inside inline asm (it put
+// the bf16 packing of the same registers right behind the store, and lanes 12-15 of each
+// 16 stored the packed bits), hence the s_nop.
+__device__ __forceinline__ void gbw_st16(float* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void addscale_epilogue_dma(const GemmArgs& a, f32x4 (&acc)[4][4],
+                                                      int m0, int n0, int wr, int wc, int lane,
+                                                      int tid, char* smem) {
+  float* T = (float*)smem;               // [64][EP] accumulator rows of the half
+  char* AX = smem + GBW_T;               // [2 buffers][32][128] fp32 aux1 rows
+  float* X = (float*)(AX + 4 * GBW_Q);  // [group][BN] column-sum exchange
+  const int wid = tid >> 6, cq = tid & 31, grp = tid >> 5, col = n0 + cq * 4;
+  auto fetch = [&](int q) {  // wave wid: rows 8 wid .. 8 wid + 7 of quarter q, 2 rows per DMA
+    char* D = AX + (q & 1) * 2 * GBW_Q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 8 * wid + 2 * i;
+      const float* src = a.aux1 + (long long)(m0 + 32 * q + r + (lane >> 5)) * a.ld1 + n0 +
+                         (lane & 31) * 4;
+      glds16(src, D + r * 512);
+    }
+  };
+  auto stage = [&](int h) {
+    if (wr == h) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            T[(mt * 16 + (lane >> 4) * 4 + r) * EP + wc * 64 + nt * 16 + (lane & 15)] =
+                acc[mt][nt][r];
+    }
+  };
+  const unsigned tb = (unsigned)(size_t)(const lds_char*)(const char*)T;
+  const unsigned ab = (unsigned)(size_t)(const lds_char*)(const char*)AX;
+  f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+  if (a.bias) bv = ld4(a.bias + col);
+  f32x4 cs0 = {0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int q) {
+    const unsigned a0 = ab + (q & 1) * 2 * GBW_Q + cq * 16;
+    const unsigned t0 = tb + ((q & 1) * 32) * EP * 4 + cq * 16;
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {
+      const int row = grp + 8 * k;
+      const int m = m0 + 32 * q + row;
+      f32x4 v, x;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(t0 + row * EP * 4) : "memory");
+      asm volatile("ds_read_b128 %0, %1" : "=v"(x) : "v"(a0 + row * 512) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v), "+v"(x));
+      if (a.csum) cs0 += v;
+      if (a.bias) v += bv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf(a.alpha, x[e], v[e]);
+      gbw_st16(a.Y + (long long)m * a.ldy + col, v);
+      gbw_st8(a.ybf + (long long)m * a.ybf_ld + col, v);
+    }
+  };
+  gbw_bar();
+  fetch(0);
+  fetch(1);
+  stage(0);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  gbw_bar();
+  compute(0);
+  gbw_bar();
+  fetch(2);
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  gbw_bar();
+  compute(1);
+  gbw_bar();
+  fetch(3);
+  stage(1);
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  gbw_bar();
+  compute(2);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  gbw_bar();
+  compute(3);
+  if (a.csum) {  // as gemm_epilogue_lds: group sums, then the 8 groups in order
+    *(f32x4*)(X + grp * 2 * BN + cq * 4) = cs0;
+    gbw_bar();
+    if (tid < BN) {
+      const int c = n0 + tid;
+      float t = X[tid];
+#pragma unroll
+      for (int g = 1; g < CS_GROUPS; ++g) t += X[g * 2 * BN + tid];
+      a.csum[(long long)(m0 / BM) * a.csum_ld + c] = t;
+    }
+  }
+}
+
 // GATE_BWD epilogue rows per operand batch in the 128 x 128 kernel: 2 builds without scratch
 // (162 VGPRs; 4 spills 124 B) and takes the C = 256 gate-backward dgrad from 51.4 to 47.5 us
 constexpr int GBW_EB = 2;
@@ -1266,6 +1368,10 @@ __device__ __forceinline__ void b16_body(const GemmArgs& a, const GemmArgs& a2) 
   }
   if constexpr (EPK == EPI_GATE_BWD) {  // instance launched only with a.gbw_dma
     gate_bwd_epilogue_dma(a, acc, m0, n0, wr, wc, lane, tid, smem);
+    return;
+  }
+  if constexpr (EPK == EPI_ADDSCALE + 16) {  // instance launched only with a.as_dma
+    addscale_epilogue_dma(a, acc, m0, n0, wr, wc, lane, tid, smem);
     return;
   }
   if (a.vec_out) {
@@ -3434,6 +3540,8 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
   } while (0)
   if (spec && a.gbw_dma) {
     SPEC(EPI_GATE_BWD);
+  } else if (spec && a.as_dma) {
+    SPEC(EPI_ADDSCALE + 16);
   } else if (spec && a.epi == EPI_RESSKIP) {
     SPEC(EPI_RESSKIP);
   } else if (spec && a.epi == EPI_ADDSCALE) {
@@ -3552,6 +3660,10 @@ ENSVS_API int ensvs_conv_gemm_bf16a_out(const ensvs_conv_seg* segs, int nseg, in
   a.gbw_dma = g_gbw_dma && a.epi == EPI_GATE_BWD && a.aux1_bf && a.ybf && !a.Y && !a.bias &&
               !a.ybf_radd && C % BN == 0 && a.M % BM == 0 && ((uintptr_t)aux1 & 15) == 0 &&
               ld1 % 8 == 0 && ((uintptr_t)ybf & 15) == 0 && ybf_ld % 8 == 0;
+  a.as_dma = g_gbw_dma && a.epi == EPI_ADDSCALE && !a.aux1_bf && a.Y && a.ybf && !a.ybf_radd &&
+             !a.relu && N % BN == 0 && a.M % BM == 0 && ((uintptr_t)aux1 & 15) == 0 &&
+             ld1 % 4 == 0 && ((uintptr_t)Y & 15) == 0 && ldy % 4 == 0 &&
+             ((uintptr_t)ybf & 7) == 0 && ybf_ld % 4 == 0 && (!a.bias || ((uintptr_t)a.bias & 15) == 0);
   return launch_b16(a, segs, nseg, B, Npad, W, stages, (hipStream_t)stream);
 }
 

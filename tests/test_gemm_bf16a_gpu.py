@@ -334,3 +334,43 @@ def test_gate_bwd_dma_epilogue_bitwise(C, B, T, ldm):
     ref = torch.cat([dz * th * sg * (1 - sg), dz * sg * (1 - th * th)], 1)
     got = y1[:, :2 * C].double()
     assert ((got - ref).abs().max() / ref.abs().max()).item() < 1e-2
+
+
+@pytest.mark.parametrize("C,B,T,bias", [(256, 3, 256, False), (128, 2, 384, True),
+                                        (256, 30, 1024, False)])
+def test_addscale_dma_epilogue_bitwise(C, B, T, bias):
+    """The DiffNet dilated-conv dgrad (3-tap bf16 d(pre) segment, ADDSCALE: dx_l = dx_l+1 /
+    sqrt 2 + dy, fp32 out + bf16 copy, per-tile column sums): the LDS-DMA epilogue equals the
+    register one bit for bit."""
+    torch.manual_seed(C + T + 1)
+    M = B * T
+    dpre = torch.randn(M, 2 * C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(C, 2 * C, 3, device=DEV) / (6 * C) ** 0.5).to(torch.bfloat16).float()
+    pb, (r,) = _pack([w])
+    segs = [K.Seg(dpre, 2 * C, 2 * C, r, T, taps=3, dil=2, shift0=-2)]
+    dx = torch.randn(M, C, device=DEV)
+    b = torch.randn(C, device=DEV) if bias else None
+
+    def run(on):
+        L.call("ensvs_set_gbw_dma", int(on))
+        y = torch.full((M, C), 5.0, device=DEV)
+        yb = torch.empty(M, C, device=DEV, dtype=torch.bfloat16)
+        kw = dict(epi=L.EPI_ADDSCALE, aux1=dx, ld1=C, alpha=0.7071, ybf=yb, ybf_ld=C)
+        if b is None:
+            cs = torch.full((M // 128, 3 * C), 7.0, device=DEV)
+            kw.update(csum=cs, csum_ld=3 * C, csum_off=C)
+        else:
+            cs = None
+            kw.update(bias=b)
+        K.gemm(segs, B, T, C, pb, y, C, **kw)
+        torch.cuda.synchronize()
+        return y, yb, cs
+    try:
+        y0, b0, c0 = run(False)
+        y1, b1, c1 = run(True)
+    finally:
+        L.call("ensvs_set_gbw_dma", 1)
+    assert torch.equal(y0, y1) and torch.equal(b0, b1)
+    if c0 is not None:
+        assert torch.equal(c0, c1)
+    assert torch.equal(b1, y1.to(torch.bfloat16))

@@ -2818,8 +2818,29 @@ __device__ __forceinline__ void wg_frag_issue(const char* img, int c0, int lane,
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(o0) : "memory");
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(o1) : "memory");
 }
-constexpr int WNS = 4;  // wgrad_b16 ring slots (static_assert below: wait counts cover WNS-2)
-static_assert(WNS >= 2 && WNS - 2 <= 2, "wgrad_b16 waits for at most 2 chunks ahead");
+constexpr int WNS = 4;  // wgrad_b16 / wgrad_b16_big ring slots
+// (an 8-slot ring, 7 chunks in flight at one workgroup per CU, measured no faster: 74 vs 77 us
+// for N = K = 128 at 8 splits -- a split's chunks stream at the per-CU rate, ~26 GB/s, not at a
+// latency limit; tools/wgrad_split_sweep.py, profiles/r4_wgrad_split_sweep.txt)
+// s_waitcnt vmcnt(N) for a compile-time N (the ring waits below count 4 DMAs per chunk)
+template <int N>
+__device__ __forceinline__ void wait_vm_c() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// wait until at most `ahead` chunks (4 DMAs each) are outstanding, ahead in [0, MAXA]
+template <int MAXA>
+__device__ __forceinline__ void wait_chunks(int ahead) {
+  if constexpr (MAXA > 0) {
+    if (ahead >= MAXA) {
+      wait_vm_c<4 * MAXA>();
+      return;
+    }
+    wait_chunks<MAXA - 1>(ahead);
+  } else {
+    wait_vm_c<0>();
+  }
+}
 
 __global__ __launch_bounds__(NTHR) void wgrad_b16_kernel(const WgradArgs a) {
   constexpr int IMG = BK * 256;  // bytes per operand image (32 frames x 128 channels bf16)
@@ -2883,10 +2904,7 @@ __global__ __launch_bounds__(NTHR) void wgrad_b16_kernel(const WgradArgs a) {
   for (int c = 0; c < WNS - 1; ++c)
     if (c < nch) issue(c);
   for (int ch = 0; ch < nch; ++ch) {
-    const int ahead = min(WNS - 2, nch - 1 - ch);
-    if (ahead >= 2) wait_vm_n<8>();
-    else if (ahead == 1) wait_vm_n<4>();
-    else wait_vm_n<0>();
+    wait_chunks<WNS - 2>(min(WNS - 2, nch - 1 - ch));
     // chunk ch visible to every wave; every wave is done with chunk ch-1, whose slot the
     // next issue refills
     __builtin_amdgcn_s_barrier();
@@ -3087,28 +3105,29 @@ __global__ __launch_bounds__(NTHRW) void wgrad_b16_big_kernel(const WgradArgs a)
   }
 }
 
-// dst[n*sn + k*sk + j*sj] (+)= scale * sum_s part[s][j][n][k]   (fixed summation order)
-// grid (cdiv(K, 256), N * taps): one (tap, n) row of K per block row, coalesced over k.
+// dst[n*sn + k*sk + j*sj] (+)= scale * sum_s part[s][j][n][k]   (fixed summation order: split
+// 0, 1, 2, ..). One thread per (j, n, k) element, 16 split loads in flight per thread (4
+// measured as a latency-bound 7 us average launch: 4 waves per CU x 4 loads).
+constexpr int WRED_ILP = 16;
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
                                                            float* __restrict__ dst, int splits,
                                                            int taps, int N, int K, long long sn,
                                                            long long sk, long long sj, int accum,
                                                            float scale) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= K) return;
-  const int row = blockIdx.y;  // j * N + n
-  const int j = row / N, n = row - j * N;
   const long long stride = (long long)N * K * taps;
-  const float* p = part + (long long)row * K + k;
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;  // (j * N + n) * K + k
+  if (e >= stride) return;
+  const int row = (int)(e / K), k = (int)(e - (long long)row * K);
+  const int j = row / N, n = row - j * N;
+  const float* p = part + e;
   float v = 0.f;
   int sp = 0;
-  for (; sp + 4 <= splits; sp += 4) {
-    const float a0 = p[sp * stride], a1 = p[(sp + 1) * stride];
-    const float a2 = p[(sp + 2) * stride], a3 = p[(sp + 3) * stride];
-    v += a0;
-    v += a1;
-    v += a2;
-    v += a3;
+  for (; sp + WRED_ILP <= splits; sp += WRED_ILP) {
+    float t[WRED_ILP];
+#pragma unroll
+    for (int i = 0; i < WRED_ILP; ++i) t[i] = p[(sp + i) * stride];
+#pragma unroll
+    for (int i = 0; i < WRED_ILP; ++i) v += t[i];
   }
   for (; sp < splits; ++sp) v += p[sp * stride];
   v *= scale;
@@ -3255,6 +3274,8 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
 }  // namespace
 
 // =================================================================== C ABI
+
+static inline long long cdiv_ll(long long a, long long b) { return (a + b - 1) / b; }
 
 
 static int fill_gemm_args(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, int Tout,
@@ -3827,8 +3848,8 @@ ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx
   }
   ENSVS_CHECK_LAUNCH();
   if (splits > 1) {
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(K, 256), N * taps), dim3(256), 0, st, part,
-                       dst, splits, taps, N, K, sn, sk, sj, accum, scale);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv_ll((long long)N * taps * K, 256)),
+                       dim3(256), 0, st, part, dst, splits, taps, N, K, sn, sk, sj, accum, scale);
     ENSVS_CHECK_LAUNCH();
   }
   return ENSVS_OK;
@@ -3882,8 +3903,8 @@ ENSVS_API int ensvs_conv_wgrad_bf16(const void* dy, int ldy, const void* x, int 
   }
   ENSVS_CHECK_LAUNCH();
   if (splits > 1) {
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(K, 256), N * taps), dim3(256), 0, st, part,
-                       dst, splits, taps, N, K, sn, sk, sj, accum, scale);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv_ll((long long)N * taps * K, 256)),
+                       dim3(256), 0, st, part, dst, splits, taps, N, K, sn, sk, sj, accum, scale);
     ENSVS_CHECK_LAUNCH();
   }
   return ENSVS_OK;

@@ -223,10 +223,63 @@ def test_colsum_vectorized_tail():
     assert rel(grp, y[:, :102].reshape(4, 1250, 102).sum(1)) < 1e-5
 
 
-def test_embedding_and_speaker_backward_deterministic():
+@pytest.mark.parametrize("M,ld,ph0,nv", [(3000, 96, 5, 60), (30720, 87, 0, 47), (100, 300, 10, 129),
+                                         (65, 8, 1, 1)])
+def test_phoneme_ids_argmax(M, ld, ph0, nv):
+    """ensvs_phoneme_ids = torch.argmax over the phoneme columns (first maximum; ties and
+    all-zero rows -> the first column): the LDS-tiled kernel (nv <= 128) and the per-row one."""
+    from ensemble_svs_with_interactions_amd._lib import call
+    torch.manual_seed(M + nv)
+    x = torch.randn(M, ld, device=DEV)
+    oh = torch.zeros(M, nv, device=DEV)
+    oh[torch.arange(M, device=DEV), torch.randint(0, nv, (M,), device=DEV)] = 1.0
+    oh[::7] = 0.0  # all-zero rows
+    oh[3::11, : min(2, nv)] = 1.0  # ties
+    x[:, ph0:ph0 + nv] = oh
+    ids = torch.full((M,), -1, dtype=torch.int32, device=DEV)
+    call("ensvs_phoneme_ids", x.data_ptr(), ld, M, ph0, nv, ids.data_ptr(), K.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(ids.long(), torch.argmax(x[:, ph0:ph0 + nv], dim=1))
+
+
+@pytest.mark.parametrize("M,C,T,ldy,off,two", [(30720, 256, 1024, 256, 0, True),
+                                               (3000, 200, 300, 520, 3, False),
+                                               (2048, 64, 512, 128, 64, True)])
+def test_embed_add_rows(M, C, T, ldy, off, two):
+    """ensvs_embed_add: Y[m] += emb[ids0[m]] (+ emb[ids1[m]]) + spk0[m / T] (+ spk1[m / T]),
+    float4 lanes where aligned (off = 3: the scalar form), bitwise against torch in the same
+    addition order."""
+    from ensemble_svs_with_interactions_amd._lib import call
+    torch.manual_seed(M + C)
+    V, B = 47, M // T
+    y = torch.randn(M, ldy, device=DEV)
+    emb = torch.randn(V, C, device=DEV)
+    ids0 = torch.randint(0, V, (M,), device=DEV, dtype=torch.int32)
+    ids1 = torch.randint(0, V, (M,), device=DEV, dtype=torch.int32)
+    spk = torch.randn(2, B, C + 4, device=DEV)
+    ref = y.clone()
+    r = ref[:, off:off + C]
+    bt = torch.arange(M, device=DEV) // T
+    r += emb[ids0.long()]
+    if two:
+        r += emb[ids1.long()]
+    r += spk[0, :, :C][bt]
+    if two:
+        r += spk[1, :, :C][bt]
+    call("ensvs_embed_add", y.data_ptr() + 4 * off, ldy, M, C, T, emb.data_ptr(), ids0.data_ptr(),
+         ids1.data_ptr() if two else None, spk[0].data_ptr(), spk[1].data_ptr() if two else None,
+         C + 4, K.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("M", [3000, 30720])
+def test_embedding_and_speaker_backward_deterministic(M):
+    """3 000 frames: 12 chunk partials (the reduce's tail loop); 30 720: 120 (its 16-wide
+    batches)."""
     from ensemble_svs_with_interactions_amd._lib import call, query
     torch.manual_seed(7)
-    M, C, V, ld = 3000, 200, 47, 208
+    C, V, ld = 200, 47, 208
     dy = torch.randn(M, ld, device=DEV)
     ids = torch.randint(0, V, (M,), device=DEV, dtype=torch.int32)
     outs = []

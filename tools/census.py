@@ -229,6 +229,8 @@ def report():
           f"{'reverse diffusion' if SYNTH else ('vocoder' if VOC else ('post' if POST else 'step'))})")
     print("per branch: " + "  ".join(f"{k} {v:.2f} ms" for k, v in sorted(per_br.items())))
     for (name, tag), (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:ROWS]:
+        if n <= 0:  # (entries of other branches only, with ONLY set)
+            continue
         print(f"{ms:8.3f} ms {n:4d}x {ms / n * 1e3:8.1f} us  {name:28s} {tag or ''}")
 
 

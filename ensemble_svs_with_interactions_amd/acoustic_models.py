@@ -30,11 +30,13 @@ from .model import init_weights
 # first}: the bap and V/UV branches start when the mgc forward ends, so mgc -- the critical
 # branch -- runs its forward beside the lf0 chain only (round 2, bap alone: 20.9 vs 21.2
 # ms/step all at once; round 3, V/UV too: 15.63 vs 15.80 ms/step, all at once 16.14).
+# Round 4: V/UV after the bap forward instead (14.06 / 14.06 vs 14.34 / 14.29 ms/step; after
+# the lf0 forward: 18.1, bap after lf0: 19.1-19.8; profiles/r4_branch_order_ab.txt).
 # EXCL_BRANCHES: branches whose recurrence workgroups reserve their CU's LDS (the lf0 and mgc
 # chains; bap / vuv LSTM workgroups share CUs with GEMMs: 20.8 vs 21.0 ms/step).  Not kept:
 # the V/UV backward after the mgc DiffNet backward (24.9 vs 22.2 ms/step: the V/UV
 # recurrences then lengthen the tail instead of filling it).
-BRANCH_AFTER = {2: 1, 3: 1}
+BRANCH_AFTER = {2: 1, 3: 2}
 EXCL_BRANCHES = {0, 1}
 
 

@@ -38,6 +38,9 @@ from .model import init_weights
 # recurrences then lengthen the tail instead of filling it).
 BRANCH_AFTER = {2: 1, 3: 2}
 EXCL_BRANCHES = {0, 1}
+# PREPACK_ON: the branch whose stream issues the mgc denoiser's weight repack at its head
+# (None: the mgc branch itself, when its denoiser runs)
+PREPACK_ON = 0
 
 
 def _ar_work(H, B, device):
@@ -662,7 +665,9 @@ class _MultistreamHybrid(BaseModel):
         elif i == 1:
             nm, rm, st["mgc"] = self.mgc_model._fwd(c["enc_src"], B, T, lens_dev, (y_main, Dy, o[0]),
                                                     s0, E, t=draws.get("mgc_t"),
-                                                    noise=draws.get("mgc_noise"))
+                                                    noise=draws.get("mgc_noise"),
+                                                    **({"pack_ev": c["mgc_pack_ev"]}
+                                                       if c.get("mgc_pack_ev") else {}))
             outs.update(mgc_noise=nm, mgc_recon=rm)
         elif i == 2:
             nb, rb, st["bap"] = self.bap_model._fwd(c["enc_src"], B, T, lens_dev, (y_main, Dy, o[3]),
@@ -781,6 +786,9 @@ class _MultistreamHybrid(BaseModel):
                     a = BRANCH_AFTER.get(i)
                     if a is not None and a in fwd_done:
                         torch.cuda.current_stream().wait_event(fwd_done[a])
+                    if i == PREPACK_ON and hasattr(self.mgc_model, "prepack"):
+                        # the mgc denoiser's weight repack at the head of this branch
+                        c["mgc_pack_ev"] = self.mgc_model.prepack()
                     self._fwd_branch(i, c, outs, st)
                     if i in BRANCH_AFTER.values():
                         fwd_done[i] = torch.cuda.current_stream().record_event()

@@ -596,9 +596,19 @@ class GaussianDiffusion(BaseModel):
         return PredictionType.DIFFUSION
 
     # ------------------------------------------------------------------ kernels
+    def prepack(self):
+        """Issue the denoiser's weight repack on the current stream and return its event.
+        The multitrack step issues it at the head of another branch's stream; _fwd makes
+        its own stream wait for the event just before the denoiser, so the repack (the
+        largest of the branch's weight packs) leaves this branch's critical path."""
+        dn = self.denoise_fn
+        dn._packs.ensure(dn, dn._register)
+        return torch.cuda.current_stream().record_event()
+
     def _fwd(self, sources, B, T, lens_dev, y_src, spk=None, spk_ld=0, t=None, noise=None,
-             save=True):
-        """Training step.  y_src = (tensor, ld, col0) of the target stream.
+             save=True, pack_ev=None):
+        """Training step.  y_src = (tensor, ld, col0) of the target stream.  pack_ev: the
+        event of a prepack() issued elsewhere, waited for before the denoiser.
         Returns (noise (B*T, M), x_recon (B*T, M), state)."""
         dev = self.betas.device
         M, Mc = B * T, self.out_dim
@@ -614,6 +624,8 @@ class GaussianDiffusion(BaseModel):
         call("ensvs_q_sample", yt.data_ptr() + 4 * ycol, yld, noise.data_ptr(), Mc, t.data_ptr(),
              self.sqrt_alphas_cumprod.data_ptr(), self.sqrt_one_minus_alphas_cumprod.data_ptr(), M,
              Mc, T, 1.0 / self.norm_scale, xn.data_ptr(), Mc, Ly.stream())
+        if pack_ev is not None:
+            torch.cuda.current_stream().wait_event(pack_ev)
         xr, dst = self.denoise_fn._fwd(xn, Mc, t, cond, E, B, T, save=save)
         return noise, xr, dict(est=est, dst=dst)
 

@@ -669,6 +669,46 @@ __global__ void sumsq_kernel(const float* __restrict__ x, long long n, float* __
   if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
+// The same over 16-B aligned x: float4 loads, two in flight per thread with their own
+// accumulators (the scalar loop above walked ~90 dependent loads per thread: 42 us for the
+// 94 MB gradient buffer)
+__global__ __launch_bounds__(256) void sumsq4_kernel(const float* __restrict__ x, long long n,
+                                                     float* __restrict__ part) {
+  __shared__ float red[256];
+  const long long n4 = n >> 2, stride = (long long)gridDim.x * 256;
+  const f32x4* x4 = (const f32x4*)x;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const f32x4 u = x4[i], w = x4[i + stride];
+    a += u * u;
+    b += w * w;
+  }
+  if (i < n4) {
+    const f32x4 u = x4[i];
+    a += u * u;
+  }
+  float acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((b[0] + b[1]) + (b[2] + b[3]));
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const float v = x[4 * n4 + threadIdx.x];
+    acc = fmaf(v, v, acc);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+static void launch_sumsq(const float* x, long long n, float* part, int blocks, hipStream_t st) {
+  if (((uintptr_t)x & 15) == 0)
+    hipLaunchKernelGGL(sumsq4_kernel, dim3(blocks), dim3(256), 0, st, x, n, part);
+  else
+    hipLaunchKernelGGL(sumsq_kernel, dim3(blocks), dim3(256), 0, st, x, n, part);
+}
+
 __global__ void norm_final_kernel(const float* __restrict__ part, int n, float* __restrict__ out,
                                   const unsigned* __restrict__ err) {
   __shared__ double red[256];
@@ -1145,7 +1185,7 @@ ENSVS_API int ensvs_masked_l1(const float* const* a, const float* const* b, floa
 ENSVS_API int ensvs_l2norm(const float* x, long long n, float* part, float* norm_out, void* stream) {
   int blocks = std::min(1024, grid_for(n));
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(blocks), dim3(256), 0, st, x, n, part);
+  launch_sumsq(x, n, part, blocks, st);
   ENSVS_CHECK_LAUNCH();
   hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(256), 0, st, part, blocks, norm_out,
                      (const unsigned*)nullptr);
@@ -1157,7 +1197,7 @@ ENSVS_API int ensvs_l2norm_chk(const float* x, long long n, float* part, float* 
                                const unsigned* err, void* stream) {
   int blocks = std::min(1024, grid_for(n));
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(blocks), dim3(256), 0, st, x, n, part);
+  launch_sumsq(x, n, part, blocks, st);
   ENSVS_CHECK_LAUNCH();
   hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(256), 0, st, part, blocks, norm_out, err);
   ENSVS_CHECK_LAUNCH();

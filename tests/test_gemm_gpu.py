@@ -273,6 +273,23 @@ def test_embed_add_rows(M, C, T, ldy, off, two):
     assert torch.equal(y, ref)
 
 
+@pytest.mark.parametrize("n,off", [(23_501_237, 0), (23_501_237, 1), (1000, 0), (7, 0), (4, 1)])
+def test_l2norm(n, off):
+    """ensvs_l2norm / ensvs_l2norm_chk (the clip-by-global-norm of the fused Adam): float4
+    form on aligned buffers (off = 0, any n: the n % 4 tail), the scalar one otherwise."""
+    from ensemble_svs_with_interactions_amd._lib import call
+    torch.manual_seed(n % 1000 + off)
+    buf = torch.randn(n + off, device=DEV) * 1e-2
+    x = buf[off:]
+    part, out = torch.empty(1024, device=DEV), torch.empty(1, device=DEV)
+    ref = torch.linalg.vector_norm(x.double()).item()
+    for name, extra in (("ensvs_l2norm", ()), ("ensvs_l2norm_chk", (None,))):
+        out.fill_(-1.0)
+        call(name, x.data_ptr(), n, part.data_ptr(), out.data_ptr(), *extra, K.stream())
+        torch.cuda.synchronize()
+        assert abs(out.item() - ref) <= 2e-6 * ref, (name, out.item(), ref)
+
+
 @pytest.mark.parametrize("M", [3000, 30720])
 def test_embedding_and_speaker_backward_deterministic(M):
     """3 000 frames: 12 chunk partials (the reduce's tail loop); 30 720: 120 (its 16-wide

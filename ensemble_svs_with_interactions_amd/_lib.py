@@ -113,6 +113,8 @@ SIGNATURES = {
     "ensvs_ardec_coop_supported": [c_int, c_int],
     "ensvs_ardec_coop_work_bytes": [c_int, c_int],
     "ensvs_coop_set_error_word": [c_vp],
+    "ensvs_coop_set_error_word_dev": [c_int, c_vp],
+    "ensvs_coop_error_word": [c_int],
     "ensvs_coop_set_timeout_us": [c_ll],
     "ensvs_coop_inject_fault": [c_int],
     "ensvs_ardec_coop_pack": [c_vp, c_int, c_int, c_vp, c_vp],
@@ -228,7 +230,8 @@ RESTYPES = {"ensvs_embed_bwd_workspace": c_ll, "ensvs_usf_source_workspace": c_l
             "ensvs_attn_table_grad_workspace": c_ll, "ensvs_lstm_bwd_work_floats": c_ll,
             "ensvs_lstm_coop_work_bytes": c_ll, "ensvs_lstm_coop_supported": ctypes.c_int,
             "ensvs_lstm_mfma_supported": ctypes.c_int,
-            "ensvs_ardec_coop_work_bytes": c_ll, "ensvs_ardec_coop_supported": ctypes.c_int}
+            "ensvs_ardec_coop_work_bytes": c_ll, "ensvs_ardec_coop_supported": ctypes.c_int,
+            "ensvs_coop_error_word": c_vp}
 
 _lib = None
 

@@ -24,6 +24,8 @@
 // Every workgroup of the grid must be resident at once (2 NW <= 64 workgroups, one per CU);
 // the polls are bounded, so a grid that cannot become resident ends (flagging the error word
 // of the workspace) instead of hanging.
+#include <atomic>
+
 #include "coop.h"
 #include "ensvs.h"
 
@@ -424,28 +426,47 @@ int check_work(const void* work, long long nbytes, int H, int B) {
   return ENSVS_OK;
 }
 
-// failure controls shared by every cooperative launch (coop.h Ctl)
-unsigned* g_err = nullptr;
+// failure controls of every cooperative launch (coop.h Ctl): one error word and one wall-clock
+// rate per device, picked by the launching thread's current device (hipGetDevice), so a
+// process driving several GPUs never points a kernel at another device's word
+constexpr int MAX_DEV = 64;
+std::atomic<unsigned*> g_err[MAX_DEV];
+std::atomic<int> g_rate_khz[MAX_DEV];
 long long g_timeout_us = 1000000;
 int g_fault = 0;
+
+int current_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) dev = 0;
+  return dev;
+}
 
 }  // namespace
 
 coop::Ctl coop::host_ctl() {
-  static int rate_khz = [] {
-    int dev = 0, r = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&r, hipDeviceAttributeWallClockRate, dev) != hipSuccess || r <= 0)
-      r = 100000;  // 100 MHz
-    return r;
-  }();
-  return Ctl{g_err, g_timeout_us * rate_khz / 1000, g_fault};
+  const int dev = current_device();
+  int rate_khz = g_rate_khz[dev].load(std::memory_order_relaxed);
+  if (rate_khz <= 0) {
+    if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+        rate_khz <= 0)
+      rate_khz = 100000;  // 100 MHz
+    g_rate_khz[dev].store(rate_khz, std::memory_order_relaxed);
+  }
+  return Ctl{g_err[dev].load(std::memory_order_acquire), g_timeout_us * rate_khz / 1000, g_fault};
+}
+
+ENSVS_API int ensvs_coop_set_error_word_dev(int device, unsigned* word) {
+  if (device < 0 || device >= MAX_DEV || (uintptr_t)word % 4) return ENSVS_E_ARG;
+  g_err[device].store(word, std::memory_order_release);
+  return ENSVS_OK;
+}
+
+ENSVS_API unsigned* ensvs_coop_error_word(int device) {
+  return device < 0 || device >= MAX_DEV ? nullptr : g_err[device].load(std::memory_order_acquire);
 }
 
 ENSVS_API int ensvs_coop_set_error_word(unsigned* word) {
-  if ((uintptr_t)word % 4) return ENSVS_E_ARG;
-  g_err = word;
-  return ENSVS_OK;
+  return ensvs_coop_set_error_word_dev(current_device(), word);
 }
 
 ENSVS_API int ensvs_coop_set_timeout_us(long long us) {

@@ -710,7 +710,7 @@ static void launch_sumsq(const float* x, long long n, float* part, int blocks, h
 }
 
 __global__ void norm_final_kernel(const float* __restrict__ part, int n, float* __restrict__ out,
-                                  const unsigned* __restrict__ err) {
+                                  unsigned* __restrict__ err) {
   __shared__ double red[256];
   double acc = 0.0;
   for (int i = threadIdx.x; i < n; i += 256) acc += part[i];
@@ -720,8 +720,18 @@ __global__ void norm_final_kernel(const float* __restrict__ part, int n, float* 
     if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
     __syncthreads();
   }
-  // a failed cooperative recurrence (coop.h error word) makes the norm NaN: the update skips
-  if (threadIdx.x == 0) out[0] = (err && *err) ? __builtin_nanf("") : (float)sqrt(red[0]);
+  // a failed cooperative recurrence (coop.h error word) makes the norm NaN: the update skips.
+  // The word is snapshotted and cleared here, once per step: err[0] (the live word the
+  // recurrences OR into) moves into err[1] (failed steps, cleared by the host when it raises),
+  // so steps enqueued after a failure run their own updates normally.
+  if (threadIdx.x == 0) {
+    const unsigned e = err ? err[0] : 0u;
+    out[0] = e ? __builtin_nanf("") : (float)sqrt(red[0]);
+    if (e) {
+      err[1] += 1u;
+      err[0] = 0u;
+    }
+  }
 }
 
 // data parallel: a rank whose cooperative recurrence failed writes NaN into one gradient
@@ -1188,13 +1198,13 @@ ENSVS_API int ensvs_l2norm(const float* x, long long n, float* part, float* norm
   launch_sumsq(x, n, part, blocks, st);
   ENSVS_CHECK_LAUNCH();
   hipLaunchKernelGGL(norm_final_kernel, dim3(1), dim3(256), 0, st, part, blocks, norm_out,
-                     (const unsigned*)nullptr);
+                     (unsigned*)nullptr);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }
 
 ENSVS_API int ensvs_l2norm_chk(const float* x, long long n, float* part, float* norm_out,
-                               const unsigned* err, void* stream) {
+                               unsigned* err, void* stream) {
   int blocks = std::min(1024, grid_for(n));
   hipStream_t st = (hipStream_t)stream;
   launch_sumsq(x, n, part, blocks, st);

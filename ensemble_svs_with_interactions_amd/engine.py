@@ -303,7 +303,7 @@ class CoopError(RuntimeError):
     check_coop_errors / step_metrics / the next train_step."""
 
 
-_COOP = {}  # device -> (int32 error word, pinned host copy, event or None)
+_COOP = {}  # device -> (int32 error words [live, failed steps], pinned host copy, event or None)
 
 
 def _dev_key(device):
@@ -315,13 +315,17 @@ def _dev_key(device):
 
 def coop_error_word(device):
     """The persistent device word every cooperative launch ORs 1 into on a residency
-    timeout (registered with the library on first use; one per process and device)."""
+    timeout (registered with the library on first use; one per process and device: the
+    library keeps one word per device ordinal and each launch picks its current device's)."""
     key = _dev_key(device)
     ent = _COOP.get(key)
     if ent is None:
-        word = torch.zeros(1, dtype=torch.int32, device=device)
-        host = torch.zeros(1, dtype=torch.int32, pin_memory=torch.cuda.is_available())
-        _lib.call("ensvs_coop_set_error_word", word.data_ptr())
+        d = torch.device(key)
+        # [0]: the live word the cooperative launches OR into; [1]: failed steps, counted by
+        # the step's gradient norm (ensvs_l2norm_chk snapshots [0] into [1] and clears [0])
+        word = torch.zeros(2, dtype=torch.int32, device=d)
+        host = torch.zeros(2, dtype=torch.int32, pin_memory=torch.cuda.is_available())
+        _lib.call("ensvs_coop_set_error_word_dev", d.index, word.data_ptr())
         ent = _COOP[key] = [word, host, None]
     return ent[0]
 
@@ -342,12 +346,19 @@ def check_coop_errors(device=None, sync=True):
         if device is not None and key != _dev_key(device):
             continue
         if sync:
-            if int(ent[0].item()):
+            if int(ent[0].max().item()):
                 _coop_raise(ent)
         elif ent[2] is not None and ent[2].query():
             ent[2] = None
-            if int(ent[1][0]):
+            if int(ent[1].max()):
                 _coop_raise(ent)
+
+
+def coop_failed(device):
+    """Host read (a device sync) of the failure words: nonzero when a cooperative launch
+    flagged a timeout that no step has counted yet, or a step counted one."""
+    ent = _COOP.get(_dev_key(device))
+    return 0 if ent is None else int(ent[0].max().item())
 
 
 def note_coop_check(device):

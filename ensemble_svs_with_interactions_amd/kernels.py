@@ -399,16 +399,25 @@ WGRAD_TARGET = 512  # workgroups a weight gradient aims for (256: 20.7, 1024: 20
 WGRAD_BIG = {"on": True, "target": 256}
 
 
+def set_wgrad_big(on: bool):
+    """The 256 x 256 weight-gradient kernel on / off, in the library (ensvs_set_wgrad_big) and
+    in the split-count rule below together, so the splits always match the kernel that runs."""
+    call("ensvs_set_wgrad_big", int(bool(on)))
+    WGRAD_BIG["on"] = bool(on)
+
+
 def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, sk, sj,
           accum=False, dtype=_lib.DT_BF16, radd=None, radd_ld=0, dyoff=0, xoff=0, splits=None,
           scale=1.0, dstoff=0):
     """dst (+)= scale * dy^T x (conv/linear weight gradient).  dy and x may both be bf16
     tensors already rounded (radd then folded into x): the glds-staged kernel, same bits."""
     M = B * Tout
-    if (splits is None and WGRAD_BIG["on"] and N >= 256 and K >= 256 and
-            -(-N // 256) * -(-K // 256) * taps >= 16):
+    if (splits is None and dtype == _lib.DT_BF16 and WGRAD_BIG["on"] and N >= 256 and
+            K >= 256 and -(-N // 256) * -(-K // 256) * taps >= 16):
         # the 256 x 256-tile kernel (gemm.hip wgrad_b16_big_kernel) for bf16 operands, one
-        # workgroup per CU; fp32 sources take the same split count (the same bits)
+        # workgroup per CU; fp32 sources rounded in staging (production precision) take the
+        # same split count, so they give the same bits.  Exact-fp32 parity mode (DT_F32)
+        # keeps the 128 x 128 kernel's split rule.
         tiles = -(-N // 256) * -(-K // 256) * taps
         splits = max(1, min(64, WGRAD_BIG["target"] // max(tiles, 1), -(-M // 512)))
     if splits is None:

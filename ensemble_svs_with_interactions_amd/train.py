@@ -282,17 +282,20 @@ def allreduce_grads(gflat, group=None):
     import torch.distributed as dist
     if world_size(group) == 1:
         return
-    _poison(gflat, 0)
     dist.all_reduce(gflat, op=dist.ReduceOp.SUM, group=group)
+    _reduce_flag(gflat, group)
 
 
-def _poison(gflat, i):
-    """NaN into gflat[i] when this rank's cooperative recurrence failed (coop.h error word),
-    before the all-reduce that carries element i: every rank's norm is then NaN and every
-    rank skips the update (a local skip alone would let the ranks' parameters diverge)."""
-    if gflat.is_cuda:
-        call("ensvs_poison_on_error", coop_error_word(gflat.device).data_ptr(),
-             gflat.data_ptr() + 4 * i, Ly.stream())
+def _reduce_flag(gflat, group, async_op=False):
+    """MAX all-reduce of this rank's cooperative-recurrence failure word (coop.h, 4 bytes)
+    after the gradient's last collective: when any rank's recurrence failed, every rank's
+    gradient norm is NaN, every rank skips the update (a local skip alone would let the
+    ranks' parameters diverge) and every rank raises CoopError on the same step."""
+    import torch.distributed as dist
+    if not gflat.is_cuda:
+        return None
+    w = coop_error_word(gflat.device)[:1]
+    return dist.all_reduce(w, op=dist.ReduceOp.MAX, group=group, async_op=async_op)
 
 
 class BucketedAllReduce:
@@ -333,14 +336,6 @@ class BucketedAllReduce:
         groups["rest"] = [p for p in model.parameters() if id(p) not in seen]
         self.buckets = {k: rng(v) for k, v in groups.items() if v}
 
-    def _reduce_flag(self):
-        """No bucket is launched after the join: share the failure flag itself (MAX)."""
-        import torch.distributed as dist
-        if self.gflat.is_cuda:
-            w = coop_error_word(self.gflat.device)
-            self.works.append(dist.all_reduce(w, op=dist.ReduceOp.MAX, group=self.group,
-                                              async_op=True))
-
     def launch(self, tag):
         import torch.distributed as dist
         for a, b in self.buckets.get(tag, ()):
@@ -348,12 +343,10 @@ class BucketedAllReduce:
                                               group=self.group, async_op=True))
 
     def finish(self):
-        rest = self.buckets.get("rest")
-        if rest:  # the last bucket carries the failure flag of this rank's recurrences
-            _poison(self.gflat, rest[0][0])
-        else:
-            self._reduce_flag()
         self.launch("rest")
+        w = _reduce_flag(self.gflat, self.group, async_op=True)  # the failure word, MAX
+        if w is not None:
+            self.works.append(w)
         for w in self.works:
             w.wait()
         self.works = []
@@ -398,14 +391,14 @@ def step_metrics(loss, optimizer):
     recipe), Loss_LogF0_Interaction (unweighted), Loss_MGC-0th_Interaction (0) and GradNorm
     (only when finite: the reference skips the step and the metric otherwise).  Reads the
     device (a sync); call it only when logging.  Raises engine.CoopError when a cooperative
-    recurrence of the step failed (its update was skipped); "Coop_Timeout" is 0 otherwise."""
+    recurrence of a step since the last check failed (that step's update was skipped)."""
     check_coop_errors(loss.device, sync=True)
     total = float(loss.item())
     il = getattr(optimizer, "_il", None)
     wil = float(il[0].item()) if il is not None else 0.0
     out = {"Loss": total, "Loss_Feats": total - wil, "Loss_Pitch": 0.0,
            "Loss_LogF0_Interaction": wil / il[1] if il is not None else 0.0,
-           "Loss_MGC-0th_Interaction": 0.0, "Coop_Timeout": 0.0}
+           "Loss_MGC-0th_Interaction": 0.0}
     gn = float(optimizer.norm.item())
     if math.isfinite(gn):
         out["GradNorm"] = gn

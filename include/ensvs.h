@@ -78,8 +78,9 @@ int ensvs_set_big_tile(int mode, int stages);
  * tiles added through LDS; default off: the one-group kernel, the same bits as the
  * register-staged kernel; kept for the sum-order tests). */
 int ensvs_set_dual_small(int on);
-/* DiffNet gate-backward dgrad (EPI_GATE_BWD, production form) through the LDS-DMA epilogue
- * (default 1) or the register-batched one (0): same bits; for the bitwise test. */
+/* Both LDS-DMA epilogues -- the DiffNet gate-backward dgrad (EPI_GATE_BWD, production form)
+ * and the dilated-conv dgrad's ADDSCALE epilogue -- (default 1) or their register-batched
+ * forms (0): same bits; for the bitwise tests.  One switch covers both. */
 int ensvs_set_gbw_dma(int on);
 /* bf16-operand weight gradients with N, K >= 256 on the 256 x 256-tile kernel (default 1) or
  * the 128 x 128 one (0): same bits for the same split count. */
@@ -258,10 +259,16 @@ long long ensvs_ardec_coop_work_bytes(int H, int B);
 /* Failure controls of every cooperative launch (coop.h).  A tile whose workgroups cannot all
  * become resident times out after `us` microseconds (default 1 s) of polling, releases its
  * waiters (the launch ends within one timeout) and ORs 1 into the registered persistent device
- * word (4-B aligned, caller-owned, never cleared by the library; NULL unregisters).  The word
- * is read by ensvs_l2norm_chk / ensvs_poison_on_error, so the training step skips its update.
+ * word of the launching thread's current device (4-B aligned, caller-owned, never cleared by
+ * the library; NULL unregisters).  One word per device: ensvs_coop_set_error_word_dev
+ * registers `device`'s word (0..63), ensvs_coop_set_error_word the current device's, and
+ * ensvs_coop_error_word returns what is registered for `device` (host-side bookkeeping only, no
+ * HIP call).  The word is read by ensvs_l2norm_chk (which also snapshots and clears it once
+ * per step), so the training step skips its update.
  * ensvs_coop_inject_fault(1) is a test switch: workgroup 0 of tile 0 skips its step-1 signal. */
 int ensvs_coop_set_error_word(unsigned* word);
+int ensvs_coop_set_error_word_dev(int device, unsigned* word);
+unsigned* ensvs_coop_error_word(int device);
 int ensvs_coop_set_timeout_us(long long us);
 int ensvs_coop_inject_fault(int on);
 int ensvs_ardec_coop_pack(const float* whh, int H, int bwd, void* out, void* stream);
@@ -367,10 +374,12 @@ int ensvs_lf0_interaction(const float* lf0_m, const float* lf0_s, const float* y
 /* clip_grad_norm_ + torch.optim.Adam over the flat parameter buffer
  * (bin/train_acoustic_multitrack.py:369-380). */
 int ensvs_l2norm(const float* x, long long n, float* part, float* norm_out, void* stream);
-/* ensvs_l2norm whose result is NaN when *err != 0 (a failed cooperative recurrence, see
- * ensvs_coop_set_error_word): the non-finite-norm skip then drops the step's update. */
+/* ensvs_l2norm whose result is NaN when err[0] != 0 (a failed cooperative recurrence, see
+ * ensvs_coop_set_error_word): the non-finite-norm skip then drops the step's update.  err
+ * points at two words: a set err[0] is cleared and counted into err[1] (the host reads and
+ * clears err[1] when it raises), so only the step whose recurrence failed skips. */
 int ensvs_l2norm_chk(const float* x, long long n, float* part, float* norm_out,
-                     const unsigned* err, void* stream);
+                     unsigned* err, void* stream);
 /* x[0] = NaN when *err != 0: before a data-parallel all-reduce, so every rank's norm is NaN
  * and every rank skips the update when any rank's recurrence failed. */
 int ensvs_poison_on_error(const unsigned* err, float* x, void* stream);

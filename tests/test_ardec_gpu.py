@@ -93,6 +93,9 @@ def _run(a, B, T, H, coop, teacher):
     (256, 33, 128, False),
     (256, 64, 512, True),
     (128, 70, 120, False),
+    # long sequences, free-running (fp16 recurrent products fed back for T/4 AR steps)
+    (256, 8, 4096, False),
+    (256, 4, 6000, False),
 ])
 def test_ardec_coop_matches_exact(H, B, T, teacher):
     a = _inputs(B, T, H, H + B + T)

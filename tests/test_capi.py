@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared():
     src = open(os.path.join(ROOT, "include", "ensvs.h")).read()
-    return sorted(set(re.findall(r"^(?:int|long long) (ensvs_\w+)\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|long long|unsigned\*) (ensvs_\w+)\(", src, flags=re.M)))
 
 
 def test_header_symbols_exported():
@@ -83,3 +83,27 @@ def test_gemm_rejects_inconsistent_epilogue_shapes():
     rc = f(seg, 1, 1, 64, 512, 512, P(16), 1, None, P(16), 256, _lib.EPI_RESSKIP, 0, 0, None,
            0, None, 0, ctypes.c_float(0.0), 256, None)
     assert rc == 4
+
+
+def test_coop_error_word_per_device():
+    """The cooperative kernels' persistent error word is registered per device ordinal
+    (ADVICE r4): registering device 1 does not move device 0's word, NULL unregisters, and
+    out-of-range ordinals or misaligned words are rejected.  Host bookkeeping only."""
+    g = _lib.query
+    try:
+        _lib.call("ensvs_coop_set_error_word_dev", 0, 0x1000)
+        _lib.call("ensvs_coop_set_error_word_dev", 1, 0x2000)
+        assert g("ensvs_coop_error_word", 0) == 0x1000
+        assert g("ensvs_coop_error_word", 1) == 0x2000
+        assert not g("ensvs_coop_error_word", 2)
+        _lib.call("ensvs_coop_set_error_word_dev", 1, None)
+        assert not g("ensvs_coop_error_word", 1)
+        assert g("ensvs_coop_error_word", 0) == 0x1000
+        lib = _lib.load()
+        assert lib.ensvs_coop_set_error_word_dev(64, 0x1000) == 4
+        assert lib.ensvs_coop_set_error_word_dev(-1, 0x1000) == 4
+        assert lib.ensvs_coop_set_error_word_dev(0, 0x1002) == 4
+        assert not g("ensvs_coop_error_word", 64)
+    finally:
+        _lib.call("ensvs_coop_set_error_word_dev", 0, None)
+        _lib.call("ensvs_coop_set_error_word_dev", 1, None)

@@ -10,7 +10,9 @@ workgroup 0 skip its step-1 signal) the polls time out, the launch ends within o
 * the training step's gradient norm is NaN, so the update is skipped (parameters, Adam moments
   and the device step counter unchanged) -- the step does not apply the garbage gradients;
 * the host raises engine.CoopError from step_metrics and from the next train_step, and the
-  flag is cleared so training can go on.
+  flag is cleared so training can go on;
+* the step's gradient norm snapshots and clears the live word, so a step enqueued after the
+  failed one (before the host noticed) applies its own update.
 """
 import math
 import time
@@ -18,7 +20,7 @@ import time
 import pytest
 import torch
 
-from ensemble_svs_with_interactions_amd import configs, data, engine
+from ensemble_svs_with_interactions_amd import configs, data, engine, train
 from ensemble_svs_with_interactions_amd._lib import call, query
 from ensemble_svs_with_interactions_amd.train import FusedAdam, step_metrics, train_step
 
@@ -67,13 +69,13 @@ def test_coop_timeout_ends_launch_and_sets_flags(fault):
     # one timeout for the whole launch (512 steps would take >= 10 s at one per step)
     assert el < 2.0, el
     assert flags[0] == 1 and flags[1] == 0  # tile 0 failed, tile 1 ran normally
-    assert int(word.item()) == 1
+    assert int(word[0].item()) == 1 and int(word[1].item()) == 0  # live word, no step yet
     with pytest.raises(engine.CoopError):
         engine.check_coop_errors("cuda")
-    assert int(word.item()) == 0  # cleared by the raise
+    assert int(word.max().item()) == 0  # cleared by the raise
     call("ensvs_coop_inject_fault", 0)
     el, flags = _lstm_launch(H, B, T)
-    assert flags == [0, 0] and int(word.item()) == 0
+    assert flags == [0, 0] and int(word.max().item()) == 0
     engine.check_coop_errors("cuda")
 
 
@@ -93,8 +95,10 @@ def test_train_step_skips_update_and_raises(fault):
     before = opt.flat.clone()
     loss, norm = train_step(m, opt, *args)
     torch.cuda.synchronize()
-    # the cooperative AR decoder of the lf0 branch hit the fault: flagged, update skipped
-    assert int(engine.coop_error_word("cuda").item()) == 1
+    # the cooperative AR decoder of the lf0 branch hit the fault: flagged, update skipped;
+    # the norm moved the live word into the failed-step count
+    word = engine.coop_error_word("cuda")
+    assert int(word[0].item()) == 0 and int(word[1].item()) == 1
     assert not math.isfinite(norm.item())
     assert torch.equal(opt.flat, before)
     assert opt.device_step == 0 and float(opt.m.abs().max()) == 0.0
@@ -103,7 +107,7 @@ def test_train_step_skips_update_and_raises(fault):
     call("ensvs_coop_inject_fault", 0)
     loss, norm = train_step(m, opt, *args)
     metrics = step_metrics(loss, opt)
-    assert metrics["Coop_Timeout"] == 0.0 and math.isfinite(metrics["GradNorm"])
+    assert math.isfinite(metrics["GradNorm"])
     assert opt.device_step == 1 and not torch.equal(opt.flat, before)
 
 
@@ -116,3 +120,22 @@ def test_next_train_step_raises(fault):
     call("ensvs_coop_inject_fault", 0)
     loss, norm = train_step(m, opt, *args)
     assert math.isfinite(norm.item()) and opt.device_step == 1
+
+
+def test_step_after_failure_applies_its_update(fault):
+    """the host runs ahead of the device, so a step can be enqueued before the host
+    sees the previous step's failure.  Only the failed step skips: the next one (fault off)
+    applies its update, and the failure is still raised afterwards."""
+    m, opt, args = _setup()
+    train_step(m, opt, *args)  # faulted: skipped
+    call("ensvs_coop_inject_fault", 0)
+    # the next step without any host check in between (what train_step does when the device
+    # has not reached the failed step's flag copy yet)
+    train._loss_and_grads(m, opt, *args, None, True, None, 0.0)
+    opt.step()
+    torch.cuda.synchronize()
+    assert opt.device_step == 1 and math.isfinite(opt.norm.item())
+    assert engine.coop_failed("cuda") == 1
+    with pytest.raises(engine.CoopError):
+        engine.check_coop_errors("cuda")
+    assert engine.coop_failed("cuda") == 0

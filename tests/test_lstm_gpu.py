@@ -173,6 +173,10 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False, mfma=False):
     (512, 33, 64, None),
     (256, 64, 512, None),
     (512, 70, 40, None),
+    # long sequences (SURVEY §8(d) T = 4096; the multitrack pairing never filters long
+    # segments, train_util.py:160-166), ragged
+    (256, 8, 4096, None),
+    (512, 8, 4096, None),
 ])
 def test_lstm_coop_matches_torch(H, B, T, lengths):
     if lengths is None:
@@ -192,6 +196,8 @@ def test_lstm_coop_matches_torch(H, B, T, lengths):
     (128, 37, 200, None),
     (64, 30, 1024, None),
     (128, 30, 1024, None),
+    (64, 8, 4096, None),
+    (128, 8, 4096, None),
 ])
 def test_lstm_mfma_matches_torch(H, B, T, lengths):
     if lengths is None:

@@ -1,0 +1,34 @@
+#!/bin/bash
+# One parametrised GPU-box job (replaces round 4's one-off tools/r4_gpu_*.sh):
+#   gpurun -- 'bash tools/gpu_job.sh TAG STEP [STEP ...]'
+# STEP is one of
+#   tests:<pytest args>     -m gpu tests (-x -v, thread timeout) -> gpurun_out/TAG_tests<i>.log
+#   bench:<bench.py args>   one bench line                        -> gpurun_out/TAG_bench<i>.json
+#   prof:<bench.py args>    rocprofv3 --kernel-trace --stats of a bench run -> gpurun_out/TAG_prof<i>/
+#   py:<script + args>      any python script                     -> gpurun_out/TAG_py<i>.txt
+#   ab:<dir> <dir> ...      interleaved whole-tree A/B (tools/tree_ab.sh) -> gpurun_out/TAG_ab<i>.txt
+#   smoke                   __graft_entry__.smoke()               -> gpurun_out/TAG_smoke.log
+# Every step has its own time limit; the job stops at the first failing step.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 9
+tag=$1; shift
+i=0
+for step in "$@"; do
+  i=$((i + 1)); kind=${step%%:*}; args=${step#*:}
+  case $kind in
+    tests) timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $args \
+             > gpurun_out/${tag}_tests$i.log 2>&1 ;;
+    bench) timeout -k 10 900 python -u bench.py $args > gpurun_out/${tag}_bench$i.json \
+             2> gpurun_out/${tag}_bench$i.err ;;
+    prof)  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d gpurun_out/${tag}_prof$i -o prof -- python3 bench.py $args > gpurun_out/${tag}_prof$i.log 2>&1 ;;
+    py)    timeout -k 10 900 python -u $args > gpurun_out/${tag}_py$i.txt 2>&1 ;;
+    ab)    timeout -k 10 1100 bash tools/tree_ab.sh $args > gpurun_out/${tag}_ab$i.txt 2>&1 ;;
+    smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" \
+             > gpurun_out/${tag}_smoke.log 2>&1 ;;
+    *) echo "unknown step $step"; exit 8 ;;
+  esac
+  rc=$?
+  echo "step $i ($kind) rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done

@@ -247,7 +247,7 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
 
     def _ar_coop(self, B):
         """Whether the AR decoder runs the cooperative kernels (ardec.hip: H = 128 / 256,
-        B <= 256 in tiles of 32 sequences, production bf16 precision; fp16 / bf16 recurrent products with fp32
+        any B in tiles of 32 sequences (8 tiles per launch), production bf16 precision; fp16 / bf16 recurrent products with fp32
         accumulation, gates, cell state and feat_out).  The fp32 parity mode keeps the exact
         per-sequence kernels."""
         H = self.decoder.lstm[0].cell.hidden_size

@@ -784,6 +784,14 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
   }
 }
 
+// any B: tiles of 32 sequences (coop.h) in waves of up to AR_MAX_TILES tiles per launch (at
+// H = 256 a wave is 16 x 8 workgroups); wave k owns its tiles' workspace region (headers, then
+// slabs), as lstm_coop.hip's waves do
+constexpr int AR_MAX_TILES = 8;
+
+template <int H>
+long long ar_wave_bytes() { return (long long)AR_MAX_TILES * (coop::HDR + ArGeo<H>::SLAB); }
+
 template <int H>
 int coop_fwd_launch(const float* gx, int ldgx, const float* ofx, int ldo, const void* wp,
                     const float* wih_p, const float* wfo, int ldwfo, const float* score, int lds,
@@ -793,13 +801,20 @@ int coop_fwd_launch(const float* gx, int ldgx, const float* ofx, int ldo, const 
   const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSF + coop::SB * 5) + 2 * coop::SB * coop::UW;
   static const bool attr = coop::set_max_lds((const void*)ardec_coop_fwd_kernel<H>, st_lds);
   if (!attr) return ENSVS_E_HIP;
-  const int nt = coop::ntiles(B);
-  if (hipMemsetAsync(work, 0, (size_t)nt * coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
-  hipLaunchKernelGGL(ardec_coop_fwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(coop::NT),
-                     coop::dyn_lds(st_lds), st, gx, ldgx, ofx, ldo, (const f16x8*)wp, wih_p, wfo,
-                     ldwfo, score, lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, so, sp,
-                     work, coop::host_ctl());
-  ENSVS_CHECK_LAUNCH();
+  const coop::Ctl ctl = coop::host_ctl();
+  const int ntt = coop::ntiles(B), Tr = T / 4;
+  for (int t0 = 0; t0 < ntt; t0 += AR_MAX_TILES) {
+    const int nt = std::min(AR_MAX_TILES, ntt - t0);
+    const long long b0 = (long long)t0 * coop::SB, r = b0 * Tr, f = b0 * T;
+    unsigned* wk = (unsigned*)((char*)work + (t0 / AR_MAX_TILES) * ar_wave_bytes<H>());
+    if (hipMemsetAsync(wk, 0, (size_t)nt * coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
+    hipLaunchKernelGGL(ardec_coop_fwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(coop::NT),
+                       coop::dyn_lds(st_lds), st, gx + r * ldgx, ldgx, ofx + r * ldo, ldo,
+                       (const f16x8*)wp, wih_p, wfo, ldwfo, score + f * lds, lds, mask + r,
+                       teach ? teach + f * ldt : teach, ldt, (int)(B - b0), T, k, lf0 + f, res + f,
+                       sg + r * 4 * H, sc + r * H, sh + r * H, so + r * 4, sp + r, wk, ctl);
+    ENSVS_CHECK_LAUNCH();
+  }
   return ENSVS_OK;
 }
 
@@ -811,20 +826,24 @@ int coop_bwd_launch(const float* glf0, const float* gres, const void* wp, const 
   const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSB + coop::SB * 5) + 2 * coop::SB * 64;
   static const bool attr = coop::set_max_lds((const void*)ardec_coop_bwd_kernel<H>, st_lds);
   if (!attr) return ENSVS_E_HIP;
-  const int nt = coop::ntiles(B);
-  if (hipMemsetAsync(work, 0, (size_t)nt * coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
-  hipLaunchKernelGGL(ardec_coop_bwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(coop::NT),
-                     coop::dyn_lds(st_lds), st, glf0, gres, (const bf16x8*)wp, wih_p, wfo, ldwfo,
-                     mask, teacher, B, T, k, sg, sc, so, dg, do4, work, coop::host_ctl());
-  ENSVS_CHECK_LAUNCH();
+  const coop::Ctl ctl = coop::host_ctl();
+  const int ntt = coop::ntiles(B), Tr = T / 4;
+  for (int t0 = 0; t0 < ntt; t0 += AR_MAX_TILES) {
+    const int nt = std::min(AR_MAX_TILES, ntt - t0);
+    const long long b0 = (long long)t0 * coop::SB, r = b0 * Tr, f = b0 * T;
+    unsigned* wk = (unsigned*)((char*)work + (t0 / AR_MAX_TILES) * ar_wave_bytes<H>());
+    if (hipMemsetAsync(wk, 0, (size_t)nt * coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
+    hipLaunchKernelGGL(ardec_coop_bwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(coop::NT),
+                       coop::dyn_lds(st_lds), st, glf0 + f, gres ? gres + f : gres,
+                       (const bf16x8*)wp, wih_p, wfo, ldwfo, mask + r, teacher, (int)(B - b0), T,
+                       k, sg + r * 4 * H, sc + r * H, so + r * 4, dg + r * 4 * H, do4 + r * 4, wk,
+                       ctl);
+    ENSVS_CHECK_LAUNCH();
+  }
   return ENSVS_OK;
 }
 
-// any B up to 8 tiles of 32 sequences (coop.h): at H = 256 a launch is 16 x 8 workgroups
-constexpr int AR_MAX_TILES = 8;
-bool ar_coop_shape(int B, int H) {
-  return B >= 1 && B <= AR_MAX_TILES * coop::SB && (H == 128 || H == 256);
-}
+bool ar_coop_shape(int B, int H) { return B >= 1 && (H == 128 || H == 256); }
 
 long long ar_coop_work(int H, int B) {
   const long long slab = H == 128 ? ArGeo<128>::SLAB : ArGeo<256>::SLAB;

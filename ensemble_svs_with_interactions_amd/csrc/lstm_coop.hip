@@ -381,6 +381,16 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
   }
 }
 
+// any B: tiles of 32 sequences (coop.h), launched in waves of up to MAX_TILES tiles (256
+// sequences; at H = 512 a wave is 8 x 64 workgroups).  Wave k owns the workspace region of its
+// tiles -- their headers, then their slabs -- so every launch sees the layout coop.h describes;
+// a wave's tiles need only be co-resident one at a time (tiles never wait on each other), and
+// consecutive waves on the stream run one after the other.
+constexpr int MAX_TILES = 8;
+
+template <int H>
+long long wave_bytes() { return (long long)MAX_TILES * (HDR + CGeo<H>::BX); }
+
 template <int H>
 int launch_fwd(const float* gx, int ldg, const void* wp, const long long* lengths, int B, int T,
                float* y, int ldy, float* sv, unsigned* work, hipStream_t st) {
@@ -388,11 +398,17 @@ int launch_fwd(const float* gx, int ldg, const void* wp, const long long* length
   const size_t st_lds = sizeof(float) * 4 * SB * PSF + 2 * SB * UW + 4 * SB;
   static const bool attr = set_max_lds((const void*)lstm_coop_fwd_kernel<H>, st_lds);
   if (!attr) return ENSVS_E_HIP;
-  const int nt = ntiles(B);
-  if (hipMemsetAsync(work, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
-  hipLaunchKernelGGL(lstm_coop_fwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds), st,
-                     gx, ldg, (const f16x8*)wp, lengths, B, T, y, ldy, sv, work, host_ctl());
-  ENSVS_CHECK_LAUNCH();
+  const Ctl ctl = host_ctl();
+  for (int t0 = 0; t0 < ntiles(B); t0 += MAX_TILES) {
+    const int nt = std::min(MAX_TILES, ntiles(B) - t0);
+    const long long b0 = (long long)t0 * SB;
+    unsigned* wk = (unsigned*)((char*)work + (t0 / MAX_TILES) * wave_bytes<H>());
+    if (hipMemsetAsync(wk, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
+    hipLaunchKernelGGL(lstm_coop_fwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds), st,
+                       gx + b0 * T * ldg, ldg, (const f16x8*)wp, lengths + b0, (int)(B - b0), T,
+                       y + b0 * T * ldy, ldy, sv + b0 * T * 10 * H, wk, ctl);
+    ENSVS_CHECK_LAUNCH();
+  }
   return ENSVS_OK;
 }
 
@@ -403,19 +419,23 @@ int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengt
   const size_t st_lds = sizeof(float) * 4 * SB * PSB + 2 * SB * 64 + 4 * SB;
   static const bool attr = set_max_lds((const void*)lstm_coop_bwd_kernel<H>, st_lds);
   if (!attr) return ENSVS_E_HIP;
-  const int nt = ntiles(B);
-  if (hipMemsetAsync(work, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
-  hipLaunchKernelGGL(lstm_coop_bwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds), st,
-                     dy, lddy, (const bf16x8*)wp, lengths, B, T, sv, dg, lddg, work, host_ctl());
-  ENSVS_CHECK_LAUNCH();
+  const Ctl ctl = host_ctl();
+  for (int t0 = 0; t0 < ntiles(B); t0 += MAX_TILES) {
+    const int nt = std::min(MAX_TILES, ntiles(B) - t0);
+    const long long b0 = (long long)t0 * SB;
+    unsigned* wk = (unsigned*)((char*)work + (t0 / MAX_TILES) * wave_bytes<H>());
+    if (hipMemsetAsync(wk, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
+    hipLaunchKernelGGL(lstm_coop_bwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds), st,
+                       dy + b0 * T * lddy, lddy, (const bf16x8*)wp, lengths + b0, (int)(B - b0), T,
+                       sv + b0 * T * 10 * H, dg + b0 * T * lddg, lddg, wk, ctl);
+    ENSVS_CHECK_LAUNCH();
+  }
   return ENSVS_OK;
 }
 
-// any B: tiles of 32 sequences (coop.h); up to 8 tiles (256 sequences) per launch keeps a
-// launch's grid within the chip at H = 512 (8 x 64 workgroups)
-constexpr int MAX_TILES = 8;
-bool coop_shape(int B, int H) { return B >= 1 && B <= MAX_TILES * SB && (H == 256 || H == 512); }
+bool coop_shape(int B, int H) { return B >= 1 && (H == 256 || H == 512); }
 
+// full waves of MAX_TILES tiles, then the last wave's tiles
 long long work_bytes(int H, int B) {
   const long long slab = H == 256 ? CGeo<256>::BX : CGeo<512>::BX;
   return (long long)ntiles(B) * (HDR + slab);

@@ -430,7 +430,7 @@ def lstm_fused_proj(H):
 
 def lstm_coop(B, H):
     """Whether the layer's recurrence runs the cooperative kernels (lstm_coop.hip: H = 256 /
-    512, B <= 256 in tiles of 32 sequences, production bf16 precision; fp16 / bf16 recurrent products with fp32
+    512, any B in tiles of 32 sequences (8 tiles per launch), production bf16 precision; fp16 / bf16 recurrent products with fp32
     accumulation and cell state).  The fp32 parity mode keeps lstm.hip's exact kernels."""
     return gemm_dtype() == _lib.DT_BF16 and query("ensvs_lstm_coop_supported", B, H) == 1
 

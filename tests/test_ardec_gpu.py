@@ -36,9 +36,12 @@ def _inputs(B, T, H, seed):
     return {k: v.cuda().contiguous() for k, v in d.items()}
 
 
-def _resident(work, B):
-    """Every 32-sequence tile's residency flag (byte 128 of its 256-B header) clear."""
-    return all(work[256 * z + 128:256 * z + 132].cpu().view(torch.int32).item() == 0
+def _resident(work, B, H):
+    """Every 32-sequence tile's residency flag (byte 128 of its 256-B header) clear; tiles run
+    in launches of 8, each owning its tiles' workspace region (coop.h)."""
+    wave = query("ensvs_ardec_coop_work_bytes", H, 256)
+    return all(work[wave * (z // 8) + 256 * (z % 8) + 128:
+                    wave * (z // 8) + 256 * (z % 8) + 132].cpu().view(torch.int32).item() == 0
                for z in range((B + 31) // 32))
 
 
@@ -67,10 +70,10 @@ def _run(a, B, T, H, coop, teacher):
         call("ensvs_ardec_coop_pack", a["whh"].data_ptr(), H, 1, wb.data_ptr(), st)
         call("ensvs_ardec_coop_fwd", a["gx"].data_ptr(), 4 * H, a["ofx"].data_ptr(), 4,
              wf.data_ptr(), *ins, *outs, work.data_ptr(), nbytes, st)
-        assert _resident(work, B)  # every workgroup of every tile resident
+        assert _resident(work, B, H)  # every workgroup of every tile resident
         call("ensvs_ardec_coop_bwd", a["glf0"].data_ptr(), a["gres"].data_ptr(), wb.data_ptr(),
              *bargs, work.data_ptr(), nbytes, st)
-        assert _resident(work, B)
+        assert _resident(work, B, H)
     else:
         wpf = torch.empty(4 * H * H, device=dev)
         wpb = torch.empty(4 * H * H, device=dev)
@@ -96,6 +99,9 @@ def _run(a, B, T, H, coop, teacher):
     # long sequences, free-running (fp16 recurrent products fed back for T/4 AR steps)
     (256, 8, 4096, False),
     (256, 4, 6000, False),
+    # more than 256 sequences: two launches (8 + 2 tiles)
+    (256, 300, 64, False),
+    (256, 300, 64, True),
 ])
 def test_ardec_coop_matches_exact(H, B, T, teacher):
     a = _inputs(B, T, H, H + B + T)

@@ -75,10 +75,12 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False, mfma=False):
         nbytes = query("ensvs_lstm_coop_work_bytes", H, B)
         cwork = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         ntile = (B + 31) // 32
+        wave = query("ensvs_lstm_coop_work_bytes", H, 256)  # one launch's 8 tiles (coop.h)
 
         def resident():  # every tile's residency flag (header byte 128 of each tile) clear
-            return all(cwork[256 * z + 128:256 * z + 132].cpu().view(torch.int32).item() == 0
-                       for z in range(ntile))
+            return all(cwork[wave * (z // 8) + 256 * (z % 8) + 128:
+                             wave * (z // 8) + 256 * (z % 8) + 132].cpu().view(torch.int32).item()
+                       == 0 for z in range(ntile))
         wpf = torch.empty(2 * 4 * H * H, dtype=torch.float16, device=dev)
         wpb = torch.empty(2 * 4 * H * H, dtype=torch.bfloat16, device=dev)
         call("ensvs_lstm_coop_pack", whh[0].data_ptr(), whh[1].data_ptr(), H, 0, wpf.data_ptr(), st)
@@ -177,6 +179,10 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False, mfma=False):
     # segments, train_util.py:160-166), ragged
     (256, 8, 4096, None),
     (512, 8, 4096, None),
+    # more than 256 sequences: launches in waves of 8 tiles (batch_by_size(32 000) packs 300
+    # pairs of about 100 frames into one batch)
+    (256, 300, 64, None),
+    (512, 300, 40, None),
 ])
 def test_lstm_coop_matches_torch(H, B, T, lengths):
     if lengths is None:

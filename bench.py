@@ -750,6 +750,21 @@ def shape_legs(args, dev, model, opt, base_ms, steps=5):
     each sequence's own length, the per-frame kernels over the padded batch)."""
     P, T = args.pairs, args.frames
     out = {}
+    # the main batch issued eagerly (every launch from the host): graph replay's gain
+    b = data.synthetic_batch(P, T, 1499)
+    g = lambda k: torch.from_numpy(b[k]).to(dev).contiguous()  # noqa: E731
+    args_e = (g("x_main"), g("x_sub"), g("y_main"), g("spk_main"), g("spk_sub"),
+              b["lengths"].tolist())
+    train_step(model, opt, *args_e)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for _ in range(steps):
+        loss, norm = train_step(model, opt, *args_e)
+    torch.cuda.synchronize()
+    ms = (time.time() - t0) / steps * 1e3
+    out[f"eager_p{P}x{T}"] = dict(value=P * T / ms * 1e3, ms_per_step=ms, pairs=P, frames=T,
+                                  execution="eager train_step (host issues every launch)",
+                                  train_loss=loss.item(), ratio_to_main=base_ms / ms)
     ms, frames, loss, norm = _graphed_leg(model, opt, 2 * P, T // 2, 1500, steps)
     out[f"p{2 * P}x{T // 2}"] = dict(value=frames / ms * 1e3, ms_per_step=ms, pairs=2 * P,
                                      frames=T // 2, train_loss=loss, grad_norm=norm,
@@ -780,7 +795,7 @@ def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
     its own shape).  One untimed epoch, then `epochs` timed ones."""
     import tempfile
     from ensemble_svs_with_interactions_amd import loader
-    from ensemble_svs_with_interactions_amd.train import train_epoch
+    from ensemble_svs_with_interactions_amd.train import StepGraphCache, train_epoch
     rng = np.random.default_rng(21)
     spks = ["S", "A", "T", "B"]
     with tempfile.TemporaryDirectory() as root:
@@ -808,13 +823,26 @@ def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
         feeder = loader.PairBatchFeeder(ds, batches, device=dev)
         valid = sum(max(ds.lengths[i]) for b in batches for i in b)
         padded = sum(len(b) * max(max(ds.lengths[i]) for i in b) for b in batches)
-        train_epoch(model, opt, feeder)  # warm-up: caches, workspaces, file cache
+        # epoch 1 (untimed): every bucket's step runs eagerly once and is captured
+        # (train.StepGraphCache); the timed epochs replay the captured steps
+        graphs = StepGraphCache(model, opt)
+        t0 = time.time()
+        train_epoch(model, opt, feeder, graphs=graphs)
         torch.cuda.synchronize()
+        el_first = time.time() - t0
         t0 = time.time()
         for _ in range(epochs):
-            res = train_epoch(model, opt, feeder)
+            res = train_epoch(model, opt, feeder, graphs=graphs)
         torch.cuda.synchronize()
         el = (time.time() - t0) / epochs
+        # the same epochs issued eagerly (every launch from the host), for the host-issue cost
+        t0 = time.time()
+        for _ in range(epochs):
+            train_epoch(model, opt, feeder)
+        torch.cuda.synchronize()
+        el_eager = (time.time() - t0) / epochs
+        n_graphs, reserved = len(graphs.graphs), torch.cuda.memory_reserved(dev)
+        del graphs
     sizes = [len(b) for b in batches]
     return dict(metric="acoustic-model train frames/sec on the on-disk data path (feeder + "
                        "train_epoch, ragged dynamic batches)",
@@ -822,7 +850,12 @@ def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
                 padded_frames_per_s=padded / el, s_per_epoch=el, steps_per_epoch=len(batches),
                 pairs=sum(sizes), pairs_per_batch=[min(sizes), max(sizes)],
                 batch_max_frames=batch_max_frames, lengths="U[256, 2048] per song",
-                execution="eager train_step per batch (shapes change every step)",
+                execution="train.StepGraphCache: one captured step per batch_by_size bucket "
+                          "(captured in the untimed first epoch, replayed from then on), all "
+                          "graphs in one shared memory pool",
+                first_epoch_s=el_first, captured_signatures=n_graphs,
+                memory_reserved_gb=reserved / 1e9,
+                eager_value=valid / el_eager, eager_s_per_epoch=el_eager,
                 last_loss=float(res[-1][0].item()), dtype=engine.gemm_precision())
 
 

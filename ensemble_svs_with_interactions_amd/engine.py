@@ -390,9 +390,19 @@ def lengths_pair(lengths, B, T, device):
     dev = _LENGTHS.get(key)
     if dev is None:
         if len(_LENGTHS) >= 256:
+            for t in _LENGTHS.values():
+                retire(t)
             _LENGTHS.clear()
         dev = _LENGTHS[key] = torch.tensor(host, dtype=torch.int64, device=device)
     return host, dev
 
 
 _LENGTHS = {}
+_RETIRED = []
+
+
+def retire(t):
+    """Keep a device buffer that a cache is replacing allocated for the life of the process: a
+    captured step graph (train.GraphedTrainStep, kept per batch shape by train.StepGraphCache)
+    may hold its address, and freeing it would let the allocator hand it to someone else."""
+    _RETIRED.append(t)

@@ -386,7 +386,11 @@ def scratch(nfloats, device, key="part"):
     ck = (key, device, torch.cuda.current_stream(device).cuda_stream)
     t = _part_cache.get(ck)
     if t is None or t.numel() < nfloats:
-        t = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
+        if t is not None:  # a captured graph may hold the old one (engine.retire)
+            from .engine import retire
+            retire(t)
+        grow = 2 * t.numel() if t is not None else 0
+        t = torch.empty(max(nfloats, grow, 1 << 20), dtype=torch.float32, device=device)
         _part_cache[ck] = t
     return t
 

@@ -548,7 +548,7 @@ class GraphedTrainStep:
     """
 
     def __init__(self, model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
-                 warmup=1, ddp=True, y_sub=None, logf0_diff_weight=0.0, draws=None):
+                 warmup=1, ddp=True, y_sub=None, logf0_diff_weight=0.0, draws=None, pool=None):
         self.model, self.opt, self.ddp = model, optimizer, ddp
         # explicit draws (train_step's `draws`) become static buffers refilled per step
         self.draws = None if draws is None else {k: v.clone() for k, v in draws.items()}
@@ -570,13 +570,16 @@ class GraphedTrainStep:
         torch.cuda.synchronize(dev)
         self.warmup_result = (loss, optimizer.norm.clone())
         self.g_grads, self.g_update = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_grads):
+        with torch.cuda.graph(self.g_grads, pool=pool):
             call("ensvs_rng_advance", Ly.stream())
             self.loss = self._grads()
-        with torch.cuda.graph(self.g_update, pool=self.g_grads.pool()):
+        self.pool = self.g_grads.pool()
+        with torch.cuda.graph(self.g_update, pool=self.pool):
             optimizer.step()
         optimizer._captured = True  # b1, b2, eps are now kernel arguments of g_update
         self.norm = optimizer.norm
+        # the interaction-loss scalar was allocated in the capture: keep it with the graph
+        self.il = getattr(optimizer, "_il", None)
 
     def _grads(self):
         i = self.inputs
@@ -620,27 +623,98 @@ class GraphedTrainStep:
             allreduce_grads(self.opt.gflat)
         self.g_update.replay()
         self.opt.step_count += 1
+        self.opt._il = self.il
         weights_updated()
         note_coop_check(dev)
         return self.loss, self.norm
 
 
-def train_epoch(model, optimizer, feeder, logf0_diff_weight=0.0, ddp=True):
+class StepGraphCache:
+    """Training steps of ragged dynamic batches at graph speed: one GraphedTrainStep per batch
+    signature (pair count, frames, per-pair lengths, sub-track target and draw shapes),
+    captured the first time the signature comes and replayed whenever it comes again.
+
+    The reference's loop (train_acoustic_multitrack.py:461-563) iterates batch_by_size buckets
+    (train_util.py:190-246) that are fixed for the run -- ShuffleBatchSampler only reorders
+    them -- so every batch shape of epoch 1 recurs in every later epoch.  A miss runs the
+    batch's step eagerly (GraphedTrainStep's warm-up step IS that batch's training step, a real
+    update) and captures it; a hit copies the batch into the graph's static inputs and replays.
+    So every batch is exactly one training step either way, with the same bits as eager
+    train_step calls given the same draws (tests/test_graph_cache_gpu.py).
+
+    Memory: every graph captures into ONE shared pool, so the cache costs about one step's
+    working set plus each graph's static inputs, not one working set per shape.  That is safe
+    because the graphs replay one at a time on one stream, and what a replay leaves for later
+    (parameters, gradients, Adam moments, BatchNorm statistics, the gradient norm) lives
+    outside the pool; the loss a replay writes into its static buffer is copied out at once
+    (step() returns copies), and caches that a graph's launches point into are never freed
+    (engine.retire).  At most ``max_graphs`` signatures are kept (least recently used first out).
+    """
+
+    def __init__(self, model, optimizer, ddp=True, logf0_diff_weight=0.0, max_graphs=64):
+        from collections import OrderedDict
+        self.model, self.opt, self.ddp = model, optimizer, ddp
+        self.logf0_diff_weight = float(logf0_diff_weight)
+        self.max_graphs = int(max_graphs)
+        self.graphs = OrderedDict()
+        self.pool = None
+        self.captures = self.replays = 0
+
+    @staticmethod
+    def signature(x_main, x_sub, y_main, spk_main, spk_sub, lengths, y_sub=None, draws=None):
+        shp = lambda t: None if t is None else (tuple(t.shape), t.dtype)  # noqa: E731
+        return (shp(x_main), shp(x_sub), shp(y_main), shp(spk_main), shp(spk_sub),
+                tuple(int(v) for v in lengths), shp(y_sub),
+                None if draws is None else tuple(sorted((k, shp(v)) for k, v in draws.items())))
+
+    def step(self, x_main, x_sub, y_main, spk_main, spk_sub, lengths, y_sub=None, draws=None):
+        """One training step on this batch; returns (loss, grad_norm) as fresh device tensors."""
+        key = self.signature(x_main, x_sub, y_main, spk_main, spk_sub, lengths, y_sub, draws)
+        g = self.graphs.get(key)
+        if g is None:
+            while len(self.graphs) >= self.max_graphs:
+                self.graphs.popitem(last=False)
+            check_coop_errors(x_main.device, sync=False)
+            g = GraphedTrainStep(self.model, self.opt, x_main, x_sub, y_main, spk_main, spk_sub,
+                                 lengths, warmup=1, ddp=self.ddp, y_sub=y_sub,
+                                 logf0_diff_weight=self.logf0_diff_weight, draws=draws,
+                                 pool=self.pool)
+            self.pool = g.pool
+            self.graphs[key] = g
+            self.captures += 1
+            loss, norm = g.warmup_result
+            note_coop_check(x_main.device)
+            return loss, norm
+        self.graphs.move_to_end(key)
+        batch = dict(x_main=x_main, y_main=y_main)
+        for k, v in (("x_sub", x_sub), ("spk_main", spk_main), ("spk_sub", spk_sub),
+                     ("y_sub", y_sub)):
+            if v is not None:
+                batch[k] = v
+        loss, norm = g.step(draws=draws, **batch)
+        self.replays += 1
+        return loss.clone(), norm.clone()
+
+
+def train_epoch(model, optimizer, feeder, logf0_diff_weight=0.0, ddp=True, graphs=None):
     """The batch loop of train_loop (train_acoustic_multitrack.py:461-484, 94-100) over a
     loader.PairBatchFeeder: each fed batch (tracks already sorted independently by
-    length, lengths = max(L0, L1)) goes through one fused train_step.  Ragged batches
-    change shape from step to step, so this runs eagerly (GraphedTrainStep is for
-    fixed-shape buckets).  Returns the per-step (loss, grad_norm) device tensors (the
-    norm copied out of the optimizer's static buffer); the host reads them only when it
-    asks."""
+    length, lengths = max(L0, L1)) goes through one fused training step.  With ``graphs`` (a
+    StepGraphCache kept across epochs) each batch shape is captured once and replayed from
+    then on; without, every step is issued eagerly (train_step).  Returns the per-step
+    (loss, grad_norm) device tensors (copies); the host reads them only when it asks."""
     out = []
     for b in feeder:
         lengths = [int(v) for v in b["host_lengths"]]
         y_sub = b["y_sub"] if logf0_diff_weight > 0 else None
-        loss, norm = train_step(model, optimizer, b["x_main"], b["x_sub"], b["y_main"],
-                                b["spk_main"], b["spk_sub"], lengths, ddp=ddp, y_sub=y_sub,
-                                logf0_diff_weight=logf0_diff_weight)
-        out.append((loss, norm.clone()))
+        args = (b["x_main"], b["x_sub"], b["y_main"], b["spk_main"], b["spk_sub"], lengths)
+        if graphs is not None:
+            loss, norm = graphs.step(*args, y_sub=y_sub)
+        else:
+            loss, norm = train_step(model, optimizer, *args, ddp=ddp, y_sub=y_sub,
+                                    logf0_diff_weight=logf0_diff_weight)
+            norm = norm.clone()
+        out.append((loss, norm))
     if out:
         check_coop_errors(out[0][0].device, sync=True)
     return out

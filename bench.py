@@ -50,12 +50,13 @@ SYNTH_POST = dict(frame_period=5, post_filter_type="gv", trajectory_smoothing=Tr
 def _imports():
     """Package imports (they load libensvs.so): only after the launcher decision."""
     global np, torch, configs, data, engine, FusedAdam, GraphedTrainStep, train_step
-    global set_overlap_allreduce
+    global set_overlap_allreduce, train_mod
     import numpy as np  # noqa: F811
     import torch  # noqa: F811
     from ensemble_svs_with_interactions_amd import configs, data, engine  # noqa: F811
     from ensemble_svs_with_interactions_amd.train import (FusedAdam, GraphedTrainStep,  # noqa
                                                           set_overlap_allreduce, train_step)
+    from ensemble_svs_with_interactions_amd import train as train_mod  # noqa: F811
 
 
 def launch_ranks(args):
@@ -1040,12 +1041,13 @@ def main():
         world = dist.get_world_size()
         backend = dist.get_backend()
         # the default data-parallel schedule: the N = 1 line's HIP-graph replay with one
-        # 94 MB all-reduce of the flat gradient between the grads and update graphs (gloo
-        # rehearsal, 2 ranks on one GPU: 62 ms/step, profiles/r4_bench_gloo2.json).
-        # --overlap-ddp: eager steps whose bucketed all-reduce (lf0 / bap / V/UV at their
-        # branch end, the mgc DiffNet before the mgc encoder's backward) overlaps the rest of
-        # the backward (same rehearsal: 2.65 s/step -- see DESIGN.md section 6); --eager
-        # alone: eager steps with the one all-reduce after the backward.
+        # 94 MB all-reduce of the flat gradient (+ the 4-byte failure word) between the grads
+        # and update graphs (gloo rehearsal, 2 ranks on one GPU: 62 ms/step,
+        # profiles/r4_bench_gloo2.json).  --overlap-ddp: eager steps whose bucketed all-reduce
+        # (lf0 / bap / V/UV at their branch end, the mgc DiffNet before the mgc encoder's
+        # backward) overlaps the rest of the backward (same rehearsal: 1 535 ms/step,
+        # profiles/r4_bench_gloo2_overlap.json, DESIGN.md section 6 -- gloo reduces on the
+        # host); --eager alone: eager steps with the one all-reduce after the backward.
         if args.overlap_ddp:
             args.eager = True
         else:
@@ -1080,11 +1082,18 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
     barrier()
+    if world > 1:  # event-time the whole-buffer exchange of every timed step
+        train_mod.EXCHANGE_EVENTS = []
     t0 = time.time()
     for _ in range(args.steps):
         loss, norm = step()
     barrier()
     elapsed = time.time() - t0
+    exchange = None
+    if world > 1:
+        exchange = exchange_report(train_mod.EXCHANGE_EVENTS, opt, model, world, backend,
+                                   args, elapsed / args.steps * 1e3)
+        train_mod.EXCHANGE_EVENTS = None
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([elapsed], device=dev)
@@ -1156,6 +1165,7 @@ def main():
                                 (", one whole-buffer all-reduce per step" if world > 1 and
                                  not args.overlap_ddp else "")},
         "train_loss": loss_v, "grad_norm": norm_v,
+        "exchange": exchange,
         # reference-equivalent work (the oracle's flop count); the path skips the sub-track
         # lf0 BiLSTM + AR decoder forward, whose output the plain recipe never reads
         # (acoustic_models._bn_only): executed work per frame is 0.59 MFLOP less
@@ -1188,6 +1198,35 @@ def main():
         if "transformer" in out:
             out["transformer"]["cpu_baseline"] = transformer_cpu_baseline()
     print(json.dumps(out), flush=True)
+
+
+def exchange_report(events, opt, model, world, backend, args, step_ms):
+    """The data-parallel exchange of the timed steps (rank 0's view): the whole-buffer
+    all-reduce of the flat gradient (+ the 4-byte failure word, MAX) timed with HIP events on
+    the stream the collectives are ordered on, its bytes, algorithm and bus bandwidth (ring:
+    2 (W-1)/W of the buffer through every rank's links), and the number of collectives one
+    step issues.  The overlap path's bucketed collectives run beside the backward, so only
+    their count and bytes are reported."""
+    nbytes = opt.gflat.numel() * 4
+    out = {"backend": backend, "world_size": world, "bytes_per_step": nbytes + 4,
+           "reference": "nnsvs/train_util.py:1444-1446 (DistributedDataParallel all-reduce)"}
+    if args.overlap_ddp:
+        br = getattr(opt, "_bucketed", None)
+        out.update(schedule="bucketed all-reduce overlapped with the backward (eager)",
+                   collectives_per_step=getattr(br, "collectives_last_step", None),
+                   buckets={k: len(v) for k, v in br.buckets.items()} if br else None)
+        return out
+    torch.cuda.synchronize()
+    ms = [s.elapsed_time(e) for s, e in events]
+    per = float(np.mean(ms)) if ms else None
+    out.update(schedule="one whole-buffer all-reduce between the grads and update graphs",
+               collectives_per_step=2, exchanges_timed=len(ms))
+    if per:
+        alg = nbytes / (per * 1e-3) / 1e9
+        out.update(allreduce_ms_per_step=per, allreduce_ms_max=float(np.max(ms)),
+                   algbw_gbs=alg, busbw_gbs=alg * 2 * (world - 1) / world,
+                   share_of_step=per / step_ms)
+    return out
 
 
 def _gate_roofline(args, P, T, sec, sec_call, flops, gbytes):

@@ -273,6 +273,11 @@ def sync_buffers(model, src=0, group=None):
             t.copy_(f)
 
 
+# measurement hook (bench.py): when a list, every whole-buffer exchange of allreduce_grads
+# appends its (start, end) HIP events, recorded on the stream the collectives are ordered on
+EXCHANGE_EVENTS = None
+
+
 def allreduce_grads(gflat, group=None):
     """Data-parallel gradient exchange: ONE sum all-reduce (RCCL over xGMI on the GPU
     box) of the flat gradient buffer.  The 1/world average is already folded into the
@@ -282,8 +287,16 @@ def allreduce_grads(gflat, group=None):
     import torch.distributed as dist
     if world_size(group) == 1:
         return
+    ev = EXCHANGE_EVENTS if gflat.is_cuda else None
+    if ev is not None:
+        s = torch.cuda.Event(enable_timing=True)
+        s.record()
     dist.all_reduce(gflat, op=dist.ReduceOp.SUM, group=group)
     _reduce_flag(gflat, group)
+    if ev is not None:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        ev.append((s, e))
 
 
 def _reduce_flag(gflat, group, async_op=False):
@@ -347,6 +360,7 @@ class BucketedAllReduce:
         w = _reduce_flag(self.gflat, self.group, async_op=True)  # the failure word, MAX
         if w is not None:
             self.works.append(w)
+        self.collectives_last_step = len(self.works)  # bench.py reports it
         for w in self.works:
             w.wait()
         self.works = []

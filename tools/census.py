@@ -26,6 +26,9 @@ VOC = len(sys.argv) > 2 and sys.argv[2] == "voc"
 POST = len(sys.argv) > 2 and sys.argv[2] in ("post", "vocleg")
 VOCLEG = len(sys.argv) > 2 and sys.argv[2] == "vocleg"
 SF0 = len(sys.argv) > 2 and sys.argv[2] == "sf0"
+# sites: the training step with column-sum / weight-gradient launches tagged by the product's
+# Python call site (which layer issues them)
+SITES = len(sys.argv) > 2 and sys.argv[2] == "sites"
 ONLY = sys.argv[3] if len(sys.argv) > 3 else None  # rows of one branch only (lf0/mgc/bap/vuv)
 REC = []
 TAG = [None]
@@ -65,11 +68,21 @@ def call(name, *args):
         tag = f"H={args[6]} T={args[5]}"
     elif name == "ensvs_colsum":
         tag = f"M={args[2]} groups={args[3]} N={args[4]}{' centred' if args[5] else ''}"
+        if SITES:
+            tag += " @" + _site()
     elif name in ("ensvs_lstm_fwd", "ensvs_lstm_bwd"):
         tag = f"H={args[7]} B={args[5]} T={args[6]}"
     elif name in ("ensvs_lstm_coop_fwd", "ensvs_lstm_coop_bwd"):
         tag = f"H={args[6]} B={args[4]} T={args[5]}"
     REC.append((name, tag, s, e, BR[0]))
+
+
+def _site():
+    import traceback
+    fr = [f for f in traceback.extract_stack()[:-3]
+          if "ensemble_svs_with_interactions_amd" in f.filename
+          and not f.filename.endswith(("kernels.py", "_lib.py"))]
+    return " < ".join(f"{os.path.basename(f.filename)}:{f.name}:{f.lineno}" for f in fr[-2:][::-1])
 
 
 def tagged(fn, fmt):
@@ -90,7 +103,7 @@ def gemm_tag(segs, B, Tout, N, W, Y, ldy, **k):
 
 def wgrad_tag(dy, ldy, x, ldx, B, Tout, Tin, N, Kc, taps, *a, **k):
     return (f"wgrad M={B * Tout} N={N} K={Kc}x{taps} "
-            f"{'b' if dy.dtype == torch.bfloat16 else 'f'}")
+            f"{'b' if dy.dtype == torch.bfloat16 else 'f'}" + (" @" + _site() if SITES else ""))
 
 
 import importlib  # noqa: E402

@@ -83,6 +83,8 @@ SIGNATURES = {
                          c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_ll, c_ll, c_int,
                          c_float, c_int, c_vp],
     "ensvs_pack_weights": [c_vp, c_int, c_int, c_vp],
+    "ensvs_colsum_once": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_vp,
+                          c_vp, c_int, c_int, c_vp],
     "ensvs_colsum": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_vp, c_int,
                      c_int, c_vp],
     "ensvs_lstm_fwd": [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp,
@@ -112,6 +114,7 @@ SIGNATURES = {
                         c_float, c_float, c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ensvs_ardec_coop_supported": [c_int, c_int],
     "ensvs_ardec_coop_work_bytes": [c_int, c_int],
+    "ensvs_wgrad_reduce_batch": [c_vp, c_int, c_vp],
     "ensvs_coop_set_error_word": [c_vp],
     "ensvs_coop_set_error_word_dev": [c_int, c_vp],
     "ensvs_coop_error_word": [c_int],

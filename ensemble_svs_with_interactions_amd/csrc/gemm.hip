@@ -3135,6 +3135,39 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   *d = accum ? (*d + v) : v;
 }
 
+// Deferred reductions of several weight gradients in one launch (ensvs_wgrad_reduce_batch):
+// blockIdx.y picks the descriptor, each thread one destination element -- the per-element sum
+// of wgrad_reduce_kernel, so the bits are the same.
+constexpr int WRED_BATCH = 48;
+struct WredBatch {
+  ensvs_wred_desc d[WRED_BATCH];
+};
+static_assert(sizeof(WredBatch) <= 3584, "kernel argument size");
+
+__global__ __launch_bounds__(256) void wgrad_reduce_batch_kernel(const WredBatch b) {
+  const ensvs_wred_desc& d = b.d[blockIdx.y];
+  const long long stride = (long long)d.N * d.K * d.taps;
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;  // (j * N + n) * K + k
+  if (e >= stride) return;
+  const int row = (int)(e / d.K), k = (int)(e - (long long)row * d.K);
+  const int j = row / d.N, n = row - j * d.N;
+  const float* p = d.part + e;
+  const int splits = d.splits;
+  float v = 0.f;
+  int sp = 0;
+  for (; sp + WRED_ILP <= splits; sp += WRED_ILP) {
+    float t[WRED_ILP];
+#pragma unroll
+    for (int i = 0; i < WRED_ILP; ++i) t[i] = p[(sp + i) * stride];
+#pragma unroll
+    for (int i = 0; i < WRED_ILP; ++i) v += t[i];
+  }
+  for (; sp < splits; ++sp) v += p[sp * stride];
+  v *= d.scale;
+  float* o = d.dst + n * d.sn + k * d.sk + j * d.sj;
+  *o = (d.accum & 1) ? (*o + v) : v;
+}
+
 // ---------------------------------------------------------- weight packing
 struct PackDesc {
   const float* src;
@@ -3268,6 +3301,118 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
     for (int i = 0; i < 16; ++i) t += red[i][c];
     const float v = (float)(t * scale);
     out[col] = accum ? out[col] + v : v;
+  }
+}
+
+// colsum_partial_kernel + colsum_final_kernel in one launch: each block writes its split's
+// partial row as the partial kernel does, then takes a ticket on its (column block, group)
+// counter; the block that draws the last ticket runs the final kernel's sums for its 64
+// columns (four 16-column passes of the same 16 split lanes, the same double-precision order:
+// the same bits) and resets the counter.  Publish / acquire: the guide's in-launch split
+// reduction (cdna_hip_programming.md, "Projection GEMM at M = 256" item 2): plain partial
+// stores -> vmcnt(0) -> barrier -> agent release fence -> vmcnt(0) -> relaxed agent ticket;
+// the last block: agent acquire fence -> vmcnt(0) -> barrier -> plain loads.
+template <bool VEC>
+__global__ __launch_bounds__(256) void colsum_once_kernel(const float* __restrict__ y, int ld,
+                                                          int M, int N, int rps,
+                                                          const float* __restrict__ mean,
+                                                          float* __restrict__ part,
+                                                          unsigned* __restrict__ cnt, float scale,
+                                                          float* __restrict__ out, int ldo,
+                                                          int accum) {
+  __shared__ f32x4 red[16][17];
+  __shared__ double dred[16][17];
+  __shared__ int last;
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col = blockIdx.x * 64 + cq * 4;
+  const int s = blockIdx.y, S = gridDim.y;
+  y += (long long)blockIdx.z * M * ld;
+  float* gpart = part + (long long)blockIdx.z * S * N;
+  const int r0 = s * rps, r1 = min(M, r0 + rps);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 mu = {0.f, 0.f, 0.f, 0.f};
+  if (mean) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (col + e < N) mu[e] = mean[(long long)blockIdx.z * N + col + e];
+  }
+  auto ld4 = [&](int r) -> f32x4 {
+    const float* q = y + (long long)r * ld + col;
+    f32x4 v;
+    if (VEC && col + 3 < N) {
+      v = *(const f32x4*)q;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = col + e < N ? q[e] : 0.f;
+    }
+    if (mean) {
+      v -= mu;
+      v *= v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) if (col + e >= N) v[e] = 0.f;
+    }
+    return v;
+  };
+  if (col < N) {
+    int r = r0 + rl;
+    for (; r + 48 < r1; r += 64) {
+      const f32x4 v0 = ld4(r), v1 = ld4(r + 16), v2 = ld4(r + 32), v3 = ld4(r + 48);
+      acc += (v0 + v1) + (v2 + v3);
+    }
+    for (; r < r1; r += 16) acc += ld4(r);
+  }
+  red[rl][cq] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = threadIdx.x;
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][c >> 2][c & 3];
+    const int gc = blockIdx.x * 64 + c;
+    if (gc < N) gpart[(long long)s * N + gc] = t;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned* c = cnt + blockIdx.z * gridDim.x + blockIdx.x;
+    const unsigned tk = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = tk == (unsigned)(S - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  // colsum_final_kernel's body for columns blockIdx.x * 64 + 16 q + c
+  float* o = out + (long long)blockIdx.z * ldo;
+  const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  for (int q = 0; q < 4; ++q) {
+    const int cc = blockIdx.x * 64 + q * 16 + c;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    if (cc < N) {
+      int sp = sl;
+      for (; sp + 48 < S; sp += 64) {
+        a0 += gpart[(long long)sp * N + cc];
+        a1 += gpart[(long long)(sp + 16) * N + cc];
+        a2 += gpart[(long long)(sp + 32) * N + cc];
+        a3 += gpart[(long long)(sp + 48) * N + cc];
+      }
+      for (; sp < S; sp += 16) a0 += gpart[(long long)sp * N + cc];
+    }
+    dred[sl][c] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (sl == 0 && cc < N) {
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t += dred[i][c];
+      const float v = (float)(t * scale);
+      o[cc] = accum ? o[cc] + v : v;
+    }
+    __syncthreads();
   }
 }
 
@@ -3797,6 +3942,8 @@ ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx
                                int shift0, int pad, int splits, float* part, float* dst,
                                long long sn, long long sk, long long sj, int accum, float scale,
                                int dtype, void* stream) {
+  const int defer = accum;  // ENSVS_WGRAD_DEFER: partials only
+  accum &= 1;
   if (B <= 0 || Tout <= 0 || N <= 0 || K <= 0 || taps <= 0 || splits <= 0) return ENSVS_E_SHAPE;
   WgradArgs a{};
   a.dy = dy;
@@ -3847,7 +3994,7 @@ ENSVS_API int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx
       hipLaunchKernelGGL((wgrad_kernel<float, false>), grid, dim3(NTHR), lds, st, a);
   }
   ENSVS_CHECK_LAUNCH();
-  if (splits > 1) {
+  if (splits > 1 && !(defer & ENSVS_WGRAD_DEFER)) {
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv_ll((long long)N * taps * K, 256)),
                        dim3(256), 0, st, part, dst, splits, taps, N, K, sn, sk, sj, accum, scale);
     ENSVS_CHECK_LAUNCH();
@@ -3862,6 +4009,8 @@ ENSVS_API int ensvs_conv_wgrad_bf16(const void* dy, int ldy, const void* x, int 
                                     int pad, int splits, float* part, float* dst, long long sn,
                                     long long sk, long long sj, int accum, float scale,
                                     void* stream) {
+  const int defer = accum;  // ENSVS_WGRAD_DEFER: partials only
+  accum &= 1;
   if (B <= 0 || Tout <= 0 || N <= 0 || K <= 0 || taps <= 0 || splits <= 0) return ENSVS_E_SHAPE;
   if (N % 8 || K % 8 || ldy % 8 || ldx % 8 || (((uintptr_t)dy | (uintptr_t)x) & 15))
     return ENSVS_E_ARG;
@@ -3902,9 +4051,29 @@ ENSVS_API int ensvs_conv_wgrad_bf16(const void* dy, int ldy, const void* x, int 
     hipLaunchKernelGGL(wgrad_b16_kernel, grid, dim3(NTHR), WNS * 2 * BK * 256, st, a);
   }
   ENSVS_CHECK_LAUNCH();
-  if (splits > 1) {
+  if (splits > 1 && !(defer & ENSVS_WGRAD_DEFER)) {
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv_ll((long long)N * taps * K, 256)),
                        dim3(256), 0, st, part, dst, splits, taps, N, K, sn, sk, sj, accum, scale);
+    ENSVS_CHECK_LAUNCH();
+  }
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_wgrad_reduce_batch(const ensvs_wred_desc* descs, int n, void* stream) {
+  if (n < 0 || (n > 0 && !descs)) return ENSVS_E_ARG;
+  for (int i0 = 0; i0 < n; i0 += WRED_BATCH) {
+    const int m = std::min(WRED_BATCH, n - i0);
+    WredBatch b{};
+    long long most = 0;
+    for (int i = 0; i < m; ++i) {
+      const ensvs_wred_desc& d = descs[i0 + i];
+      if (!d.part || !d.dst || d.splits < 1 || d.taps < 1 || d.N < 1 || d.K < 1)
+        return ENSVS_E_ARG;
+      b.d[i] = d;
+      most = std::max(most, (long long)d.N * d.K * d.taps);
+    }
+    hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3((unsigned)cdiv_ll(most, 256), m),
+                       dim3(256), 0, (hipStream_t)stream, b);
     ENSVS_CHECK_LAUNCH();
   }
   return ENSVS_OK;
@@ -3923,6 +4092,26 @@ ENSVS_API int ensvs_pack_weights(const ensvs_pack_desc* descs, int n, int max_el
 
 // out[g][n] (+)= scale * sum_{m < M} f(Y[g*M + m, n]) for g < groups;
 // f = identity, or (y - mean[g][n])^2 when mean != null.  `part` holds groups*max_splits*N floats.
+ENSVS_API int ensvs_colsum_once(const float* y, int ld, int M, int groups, int N,
+                                const float* mean, float scale, float* part, int max_splits,
+                                unsigned* counters, float* out, int ldo, int accum, void* stream) {
+  if (M <= 0 || N <= 0 || groups <= 0) return ENSVS_E_SHAPE;
+  if (!counters || !part || !out) return ENSVS_E_ARG;
+  const int cb = cdiv(N, 64);  // the split count ensvs_colsum picks
+  int S = std::max(1, std::min({max_splits, M / 128, cdiv(2048, cb * groups)}));
+  int rps = cdiv(M, S);
+  hipStream_t st = (hipStream_t)stream;
+  const bool vec = (ld % 4 == 0) && (((uintptr_t)y & 15) == 0);
+  if (vec)
+    hipLaunchKernelGGL(colsum_once_kernel<true>, dim3(cb, S, groups), dim3(256), 0, st, y, ld, M,
+                       N, rps, mean, part, counters, scale, out, ldo > 0 ? ldo : N, accum);
+  else
+    hipLaunchKernelGGL(colsum_once_kernel<false>, dim3(cb, S, groups), dim3(256), 0, st, y, ld, M,
+                       N, rps, mean, part, counters, scale, out, ldo > 0 ? ldo : N, accum);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
 ENSVS_API int ensvs_colsum(const float* y, int ld, int M, int groups, int N, const float* mean,
                            float scale, float* part, int max_splits, float* out, int ldo, int accum,
                            void* stream) {

@@ -95,6 +95,7 @@ class Branches:
             ctx = torch.cuda.stream(self.side[i])
         else:
             ctx = contextlib.nullcontext()
+        ctx = _flushing(ctx)
         if BRANCH_TIMES is None:
             return ctx
         return _timed(ctx, i)
@@ -104,6 +105,23 @@ class Branches:
             for s in self.side:
                 self.main.wait_stream(s)
         return False
+
+
+class _flushing:
+    """A branch region that issues its stream's queued weight-gradient reductions
+    (kernels.flush_wgrad) before it ends, so the join sees final gradients."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def __enter__(self):
+        return self.ctx.__enter__()
+
+    def __exit__(self, *exc):
+        if exc[0] is None:
+            from .kernels import flush_wgrad
+            flush_wgrad()
+        return self.ctx.__exit__(*exc)
 
 
 def next_seed() -> int:

@@ -3,6 +3,7 @@
 Everything here only moves pointers and sizes; all arithmetic happens in the
 HIP kernels of ``csrc/``.  Tensors are fp32, channels-last frame rows.
 """
+import contextlib
 import ctypes
 from dataclasses import dataclass
 from typing import List, Optional
@@ -410,11 +411,60 @@ def set_wgrad_big(on: bool):
     WGRAD_BIG["on"] = bool(on)
 
 
+class WredDesc(ctypes.Structure):  # include/ensvs.h ensvs_wred_desc
+    _fields_ = [("part", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("sn", ctypes.c_longlong),
+                ("sk", ctypes.c_longlong), ("sj", ctypes.c_longlong), ("splits", ctypes.c_int),
+                ("taps", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int),
+                ("accum", ctypes.c_int), ("scale", ctypes.c_float)]
+
+
+# Deferred split reductions of the weight gradients of one training step: inside
+# deferred_wgrad(), a parameter gradient split over row splits (wgrad_into) writes its
+# partials into a buffer of its own and the reduction is queued per stream; flush_wgrad()
+# issues every queued reduction of the current stream as ONE launch
+# (ensvs_wgrad_reduce_batch: the same per-element sums, the same bits).  Branch ends
+# (engine.Branches) and the data-parallel bucket launches flush, so no reader sees a gradient
+# before its reduction.  ~140 reduce launches per training step become a handful.
+_DEFER = {"depth": 0, "pending": {}}  # stream handle -> [(desc fields, part, (lo, hi))]
+
+
+@contextlib.contextmanager
+def deferred_wgrad():
+    _DEFER["depth"] += 1
+    try:
+        yield
+    finally:
+        _DEFER["depth"] -= 1
+        flush_wgrad()
+        if _DEFER["depth"] == 0 and _DEFER["pending"]:
+            left = {k: len(v) for k, v in _DEFER["pending"].items()}
+            _DEFER["pending"].clear()
+            raise RuntimeError(f"weight-gradient reductions queued on streams {left} were "
+                               "never flushed (a wgrad outside an engine.Branches region)")
+
+
+def flush_wgrad():
+    """Issue the current stream's queued weight-gradient reductions (one launch per 48)."""
+    if not _DEFER["pending"]:
+        return
+    key = stream()
+    items = _DEFER["pending"].pop(key, None)
+    if not items:
+        return
+    arr = (WredDesc * len(items))()
+    for i, (f, _, _) in enumerate(items):
+        arr[i] = WredDesc(*f)
+    call("ensvs_wgrad_reduce_batch", ctypes.addressof(arr), len(items), key)
+    # the partial buffers go back to the caching allocator here: stream-ordered, so a later
+    # allocation on this stream reuses them only after the reduction has read them
+
+
 def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, sk, sj,
           accum=False, dtype=_lib.DT_BF16, radd=None, radd_ld=0, dyoff=0, xoff=0, splits=None,
-          scale=1.0, dstoff=0):
+          scale=1.0, dstoff=0, defer=False):
     """dst (+)= scale * dy^T x (conv/linear weight gradient).  dy and x may both be bf16
-    tensors already rounded (radd then folded into x): the glds-staged kernel, same bits."""
+    tensors already rounded (radd then folded into x): the glds-staged kernel, same bits.
+    defer: inside deferred_wgrad(), queue the split reduction (see flush_wgrad)."""
     M = B * Tout
     if (splits is None and dtype == _lib.DT_BF16 and WGRAD_BIG["on"] and N >= 256 and
             K >= 256 and -(-N // 256) * -(-K // 256) * taps >= 16):
@@ -433,24 +483,61 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
         up = -(-splits // 8) * 8
         if splits >= 8 and up * tiles <= WGRAD_TARGET:
             splits = up
-    part = scratch(splits * taps * N * K, dy.device)
+    flag = int(accum)
+    dptr = dst.data_ptr() + 4 * dstoff
+    queue = None
+    if defer and splits > 1 and _DEFER["depth"] > 0:
+        lo = dptr
+        hi = dptr + 4 * ((N - 1) * sn + (K - 1) * sk + (taps - 1) * sj + 1)
+        key = stream()
+        if any(a < hi and lo < b for _, _, (a, b) in _DEFER["pending"].get(key, ())):
+            flush_wgrad()  # one launch's destinations must not overlap
+        part = torch.empty(splits * taps * N * K, dtype=torch.float32, device=dy.device)
+        queue = ((part.data_ptr(), dptr, sn, sk, sj, splits, taps, N, K, int(accum),
+                  float(scale)), part, (lo, hi))
+        flag |= 2  # ENSVS_WGRAD_DEFER
+    else:
+        part = scratch(splits * taps * N * K, dy.device)
     if dy.dtype == torch.bfloat16 or x.dtype == torch.bfloat16:
         assert dy.dtype == x.dtype == torch.bfloat16 and radd is None and dtype == _lib.DT_BF16
         call("ensvs_conv_wgrad_bf16", dy.data_ptr() + 2 * dyoff, ldy, x.data_ptr() + 2 * xoff,
              ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, splits, part.data_ptr(),
-             dst.data_ptr() + 4 * dstoff, sn, sk, sj, int(accum), float(scale), stream())
-        return
-    call("ensvs_conv_wgrad", dy.data_ptr() + 4 * dyoff, ldy, x.data_ptr() + 4 * xoff, ldx,
-         ptr(radd), radd_ld, B, Tout, Tin, N, K, taps, dil, shift0, pad, splits,
-         part.data_ptr(), dst.data_ptr() + 4 * dstoff, sn, sk, sj, int(accum), float(scale),
-         dtype, stream())
+             dptr, sn, sk, sj, flag, float(scale), stream())
+    else:
+        call("ensvs_conv_wgrad", dy.data_ptr() + 4 * dyoff, ldy, x.data_ptr() + 4 * xoff, ldx,
+             ptr(radd), radd_ld, B, Tout, Tin, N, K, taps, dil, shift0, pad, splits,
+             part.data_ptr(), dptr, sn, sk, sj, flag, float(scale), dtype, stream())
+    if queue is not None:
+        _DEFER["pending"].setdefault(stream(), []).append(queue)
+
+
+_cnt_cache = {}
+
+
+def counters(n, device):
+    """Zero-initialised ticket counters of the single-launch reductions (ensvs_colsum_once),
+    one buffer per (device, stream): every launch leaves them zero, launches on one stream
+    are ordered, concurrent streams get their own."""
+    ck = (device, torch.cuda.current_stream(device).cuda_stream)
+    t = _cnt_cache.get(ck)
+    if t is None or t.numel() < n:
+        if t is not None:  # a captured graph may hold the old one (engine.retire)
+            from .engine import retire
+            retire(t)
+        t = torch.zeros(max(n, 1 << 14), dtype=torch.int32, device=device)
+        _cnt_cache[ck] = t
+    return t
 
 
 def colsum(y, ld, M, N, out, groups=1, mean=None, scale=1.0, accum=False, yoff=0, ldo=0,
            outoff=0):
-    """out[g*ldo + n] (+)= scale * sum over the M rows of group g (ldo 0 -> N)."""
+    """out[g*ldo + n] (+)= scale * sum over the M rows of group g (ldo 0 -> N): one launch
+    (ensvs_colsum_once: the split partials are reduced by the last block of each column block,
+    the same sums as the two-launch ensvs_colsum)."""
     # row splits: what ensvs_colsum picks (>= 2048 blocks, >= 128 rows per split)
     max_splits = max(1, min(256, M // 128, -(-2048 // (-(-N // 64) * groups))))
     part = scratch(groups * max_splits * N, y.device, key="colsum")
-    call("ensvs_colsum", y.data_ptr() + 4 * yoff, ld, M, groups, N, ptr(mean), float(scale),
-         part.data_ptr(), max_splits, out.data_ptr() + 4 * outoff, ldo, int(accum), stream())
+    cnt = counters(-(-N // 64) * groups, y.device)
+    call("ensvs_colsum_once", y.data_ptr() + 4 * yoff, ld, M, groups, N, ptr(mean),
+         float(scale), part.data_ptr(), max_splits, cnt.data_ptr(),
+         out.data_ptr() + 4 * outoff, ldo, int(accum), stream())

@@ -82,7 +82,7 @@ def wgrad_into(param, dy, ldy, x, ldx, B, Tout, Tin, N, Kc, taps=1, dil=1, shift
         sn, sk, sj = g.shape[1] * g.shape[2], g.shape[2], 1
     K.wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, Kc, taps, dil, shift0, pad, g, sn, sk, sj,
             accum=True, dtype=gemm_dtype(), radd=radd, radd_ld=radd_ld, dyoff=dyoff, xoff=xoff,
-            scale=scale, dstoff=row0 * sn + col0 * sk)
+            scale=scale, dstoff=row0 * sn + col0 * sk, defer=True)
 
 
 # ----------------------------------------------------------------- input

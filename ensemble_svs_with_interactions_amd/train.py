@@ -351,6 +351,8 @@ class BucketedAllReduce:
 
     def launch(self, tag):
         import torch.distributed as dist
+        from .kernels import flush_wgrad
+        flush_wgrad()  # this stream's queued weight-gradient reductions first
         for a, b in self.buckets.get(tag, ()):
             self.works.append(dist.all_reduce(self.gflat[a:b], op=dist.ReduceOp.SUM,
                                               group=self.group, async_op=True))
@@ -463,6 +465,14 @@ def _loss_and_grads(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, 
         model.train()
     optimizer.zero_grad()
     optimizer._il = None
+    with Ly.K.deferred_wgrad():
+        return _loss_and_grads_body(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub,
+                                    lengths, draws, ddp, y_sub, logf0_diff_weight, overlap)
+
+
+def _loss_and_grads_body(model, optimizer, x_main, x_sub, y_main, spk_main, spk_sub, lengths,
+                         draws, ddp, y_sub, logf0_diff_weight, overlap):
+    """_loss_and_grads with the weight-gradient reductions queued (kernels.deferred_wgrad)."""
     if logf0_diff_weight > 0.0 and (not model.output_subtrack or y_sub is None):
         raise ValueError("logf0_diff_weight > 0 needs output_subtrack=True and y_sub (the "
                          "SeparateF0 model: through its forward, with autograd)")

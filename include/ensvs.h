@@ -137,7 +137,12 @@ int ensvs_tile_colsum(const float* y, int ldy, int M, int N, float* out, int ldo
 int ensvs_cast_bf16(const float* x, int ldx, const float* radd, int radd_ld, int T, long long M,
                     int K, void* y, int ldy, void* stream);
 
-/* Weight gradient of the same contraction (autograd of nn.Conv1d/nn.Linear weights). */
+/* Weight gradient of the same contraction (autograd of nn.Conv1d/nn.Linear weights).
+ * accum: bit 0 adds into dst (else overwrites); bit 1 (ENSVS_WGRAD_DEFER) with splits > 1 only
+ * writes the split partials [splits][taps][N][K] into `part` -- the caller reduces them later,
+ * many weight gradients in one launch, with ensvs_wgrad_reduce_batch (same summation order,
+ * same bits as the reduction the call would have launched). */
+#define ENSVS_WGRAD_DEFER 2
 int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx, const float* radd,
                      int radd_ld, int B, int Tout, int Tin, int N, int K, int taps, int dil,
                      int shift0, int pad, int splits, float* part, float* dst, long long sn,
@@ -150,12 +155,32 @@ int ensvs_conv_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, int B
                           float* part, float* dst, long long sn, long long sk, long long sj,
                           int accum, float scale, void* stream);
 
+/* Deferred split reductions of ENSVS_WGRAD_DEFER weight gradients, n descriptors (a HOST
+ * array, passed by value to the kernels in chunks of 48): dst[n*sn + k*sk + j*sj] (+)= scale *
+ * sum over s of part[s][j][n][k], splits summed in order.  The destinations of one call must
+ * not overlap (one thread per destination element). */
+typedef struct {
+  const float* part;
+  float* dst;
+  long long sn, sk, sj;
+  int splits, taps, N, K, accum;
+  float scale;
+} ensvs_wred_desc;
+int ensvs_wgrad_reduce_batch(const ensvs_wred_desc* descs, int n, void* stream);
+
 /* Batched weight repack (descs is a DEVICE array). */
 int ensvs_pack_weights(const ensvs_pack_desc* descs, int n, int max_elems, void* stream);
 
 /* Grouped column sums (bias grads, BatchNorm statistics). */
 int ensvs_colsum(const float* y, int ld, int M, int groups, int N, const float* mean, float scale,
                  float* part, int max_splits, float* out, int ldo, int accum, void* stream);
+/* ensvs_colsum in one launch (same splits, same bits): the block that finishes a column
+ * block's last split reduces its partials.  counters: cdiv(N, 64) * groups zero-initialised
+ * words, left zero by every launch (reuse them on one stream; give concurrent streams their
+ * own). */
+int ensvs_colsum_once(const float* y, int ld, int M, int groups, int N, const float* mean,
+                      float scale, float* part, int max_splits, unsigned* counters, float* out,
+                      int ldo, int accum, void* stream);
 
 
 /* ---- recurrences ------------------------------------------------------ */

@@ -38,7 +38,8 @@ def test_loader_has_no_fallback(monkeypatch, tmp_path):
 
 def test_struct_layouts_match_header():
     import subprocess, tempfile
-    src = '#include "ensvs.h"\n#include <stdio.h>\nint main(){printf("%zu %zu\\n", sizeof(ensvs_conv_seg), sizeof(ensvs_pack_desc));}\n'
+    src = ('#include "ensvs.h"\n#include <stdio.h>\nint main(){printf("%zu %zu %zu\\n", '
+           'sizeof(ensvs_conv_seg), sizeof(ensvs_pack_desc), sizeof(ensvs_wred_desc));}\n')
     with tempfile.TemporaryDirectory() as d:
         with open(os.path.join(d, "t.c"), "w") as f:
             f.write(src)
@@ -47,6 +48,8 @@ def test_struct_layouts_match_header():
         out = subprocess.check_output([os.path.join(d, "t")]).decode().split()
     assert int(out[0]) == ctypes.sizeof(_lib.ConvSeg)
     assert int(out[1]) == ctypes.sizeof(_lib.PackDesc)
+    from ensemble_svs_with_interactions_amd.kernels import WredDesc
+    assert int(out[2]) == ctypes.sizeof(WredDesc)
 
 
 def test_library_newer_than_sources():

@@ -1,0 +1,85 @@
+"""Launch-count reductions of the training step's partial sums.
+
+* ensvs_colsum_once -- the column sums (bias gradients, BatchNorm statistics, per-sequence sums)
+  in one launch, the last block of each column block reducing the split partials -- returns the
+  bits of the two-launch ensvs_colsum (partial + final kernels), for plain and centred sums,
+  groups, accumulation and ragged column counts, and leaves its ticket counters at zero.
+* kernels.deferred_wgrad -- split weight gradients whose reductions are queued and issued as
+  one ensvs_wgrad_reduce_batch launch -- returns the bits of the immediate reductions,
+  overlapping destinations included (the queue flushes before an overlapping one).
+"""
+import pytest
+import torch
+
+from ensemble_svs_with_interactions_amd import _lib as L
+from ensemble_svs_with_interactions_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("M,N,groups,centred,accum", [
+    (30720, 256, 1, False, False), (30720, 256, 1, True, False), (1024, 128, 30, False, True),
+    (1024, 128, 30, True, False), (3000, 61, 1, False, True), (512, 1000, 4, False, False),
+    (200, 67, 1, False, False), (100, 5, 3, True, True)])
+def test_colsum_once_bitwise(M, N, groups, centred, accum):
+    torch.manual_seed(M + N)
+    y = torch.randn(groups * M, N + 3, device=DEV)
+    ld = N + 3
+    mean = torch.randn(groups, N, device=DEV) * 0.1 if centred else None
+    max_splits = max(1, min(256, M // 128, -(-2048 // (-(-N // 64) * groups))))
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for once in (False, True):
+        out = torch.full((groups, N + 1), 0.5, device=DEV)
+        part = torch.empty(groups * max_splits * N, device=DEV)
+        if once:
+            cnt = torch.zeros(-(-N // 64) * groups, dtype=torch.int32, device=DEV)
+            for _ in range(2):  # the counters are left zero: a second launch works as well
+                o2 = out.clone()
+                L.call("ensvs_colsum_once", y.data_ptr(), ld, M, groups, N, L.ptr(mean), 0.75,
+                       part.data_ptr(), max_splits, cnt.data_ptr(), o2.data_ptr(), N + 1,
+                       int(accum), st)
+            torch.cuda.synchronize()
+            assert int(cnt.abs().max()) == 0
+            outs.append(o2)
+        else:
+            L.call("ensvs_colsum", y.data_ptr(), ld, M, groups, N, L.ptr(mean), 0.75,
+                   part.data_ptr(), max_splits, out.data_ptr(), N + 1, int(accum), st)
+            outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    yy = y.view(groups, M, ld)[:, :, :N].double()
+    if centred:
+        yy = (yy - mean.double()[:, None, :]) ** 2
+    ref = 0.75 * yy.sum(1) + (0.5 if accum else 0.0)
+    assert torch.allclose(outs[1][:, :N].double(), ref, rtol=1e-5, atol=1e-4)
+
+
+def test_deferred_wgrad_batch_bitwise():
+    torch.manual_seed(3)
+    shapes = [(4, 1000, 256, 256, 3, 2), (2, 2048, 512, 128, 1, 1), (30, 256, 128, 192, 7, 1),
+              (3, 600, 64, 40, 1, 1)]
+    srcs = []
+    for B, T, N, Kc, taps, dil in shapes:
+        dy = K.cast_bf16(torch.randn(B * T, N, device=DEV), N, N, B * T)
+        x = K.cast_bf16(torch.randn(B * T, Kc, device=DEV), Kc, Kc, B * T)
+        srcs.append((B, T, N, Kc, taps, dil, dy, x))
+    res = []
+    for defer in (False, True):
+        dsts = [torch.full((N, Kc, taps), 0.25, device=DEV) for (_, _, N, Kc, taps, _, _, _)
+                in srcs]
+        shared = torch.full((srcs[0][2], srcs[0][3], srcs[0][4]), 0.125, device=DEV)
+        with K.deferred_wgrad():
+            for (B, T, N, Kc, taps, dil, dy, x), d in zip(srcs, dsts):
+                K.wgrad(dy, N, x, Kc, B, T, T, N, Kc, taps, dil, -dil * (taps // 2),
+                        L.PAD_ZERO, d, Kc * taps, taps, 1, accum=True, scale=0.5, defer=defer)
+            # two contributions into one destination: the queue flushes in between
+            B, T, N, Kc, taps, dil, dy, x = srcs[0]
+            for sc in (1.0, -0.5):
+                K.wgrad(dy, N, x, Kc, B, T, T, N, Kc, taps, dil, -dil * (taps // 2), L.PAD_ZERO,
+                        shared, Kc * taps, taps, 1, accum=True, scale=sc, defer=defer)
+        torch.cuda.synchronize()
+        res.append(dsts + [shared])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

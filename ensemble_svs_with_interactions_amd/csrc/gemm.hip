@@ -3309,9 +3309,11 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
 // counter; the block that draws the last ticket runs the final kernel's sums for its 64
 // columns (four 16-column passes of the same 16 split lanes, the same double-precision order:
 // the same bits) and resets the counter.  Publish / acquire: the guide's in-launch split
-// reduction (cdna_hip_programming.md, "Projection GEMM at M = 256" item 2): plain partial
-// stores -> vmcnt(0) -> barrier -> agent release fence -> vmcnt(0) -> relaxed agent ticket;
-// the last block: agent acquire fence -> vmcnt(0) -> barrier -> plain loads.
+// reduction in its write-through form (cdna_hip_programming.md, "Projection GEMM at M = 256"
+// item 2): sc1 partial stores -> vmcnt(0) -> barrier -> relaxed agent ticket; the last block
+// reads every partial with sc1 loads.  (The release / acquire-fence form wrote the L2 back in
+// every one of the ~1 000 blocks of a step's column sums: 23.6 us per launch against 10.3 for
+// the two launches, profiles/r5_colsum_once_fence.txt.)
 template <bool VEC>
 __global__ __launch_bounds__(256) void colsum_once_kernel(const float* __restrict__ y, int ld,
                                                           int M, int N, int rps,
@@ -3363,27 +3365,26 @@ __global__ __launch_bounds__(256) void colsum_once_kernel(const float* __restric
   }
   red[rl][cq] = acc;
   __syncthreads();
+  // this group's partials [S][N] through a buffer resource: sc1 stores and loads
+  const __amdgpu_buffer_rsrc_t pr =
+      __builtin_amdgcn_make_buffer_rsrc(gpart, 0, (int)((long long)S * N * 4), 0x00020000);
   if (threadIdx.x < 64) {
     const int c = threadIdx.x;
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += red[i][c >> 2][c & 3];
     const int gc = blockIdx.x * 64 + c;
-    if (gc < N) gpart[(long long)s * N + gc] = t;
+    if (gc < N)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, t), pr,
+                                            (s * N + gc) * 4, 0, 16 /* sc1 */);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned* c = cnt + blockIdx.z * gridDim.x + blockIdx.x;
     const unsigned tk = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = tk == (unsigned)(S - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (!last) return;
@@ -3395,13 +3396,17 @@ __global__ __launch_bounds__(256) void colsum_once_kernel(const float* __restric
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     if (cc < N) {
       int sp = sl;
+      auto ldp = [&](int i) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(pr, (i * N + cc) * 4,
+                                                                              0, 16 /* sc1 */));
+      };
       for (; sp + 48 < S; sp += 64) {
-        a0 += gpart[(long long)sp * N + cc];
-        a1 += gpart[(long long)(sp + 16) * N + cc];
-        a2 += gpart[(long long)(sp + 32) * N + cc];
-        a3 += gpart[(long long)(sp + 48) * N + cc];
+        a0 += ldp(sp);
+        a1 += ldp(sp + 16);
+        a2 += ldp(sp + 32);
+        a3 += ldp(sp + 48);
       }
-      for (; sp < S; sp += 16) a0 += gpart[(long long)sp * N + cc];
+      for (; sp < S; sp += 16) a0 += ldp(sp);
     }
     dred[sl][c] = (a0 + a1) + (a2 + a3);
     __syncthreads();

@@ -486,7 +486,7 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
     flag = int(accum)
     dptr = dst.data_ptr() + 4 * dstoff
     queue = None
-    if defer and splits > 1 and _DEFER["depth"] > 0:
+    if defer and DEFER_WGRAD["on"] and splits > 1 and _DEFER["depth"] > 0:
         lo = dptr
         hi = dptr + 4 * ((N - 1) * sn + (K - 1) * sk + (taps - 1) * sj + 1)
         key = stream()
@@ -512,6 +512,11 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
 
 
 _cnt_cache = {}
+# column sums in one launch (ensvs_colsum_once) or two (partial + final kernels); same bits
+COLSUM_ONCE = {"on": True}
+# queue the split reductions of parameter gradients inside deferred_wgrad() (one batched launch
+# per branch) or reduce each weight gradient right after it (same bits either way)
+DEFER_WGRAD = {"on": True}
 
 
 def counters(n, device):
@@ -537,6 +542,11 @@ def colsum(y, ld, M, N, out, groups=1, mean=None, scale=1.0, accum=False, yoff=0
     # row splits: what ensvs_colsum picks (>= 2048 blocks, >= 128 rows per split)
     max_splits = max(1, min(256, M // 128, -(-2048 // (-(-N // 64) * groups))))
     part = scratch(groups * max_splits * N, y.device, key="colsum")
+    if not COLSUM_ONCE["on"]:
+        call("ensvs_colsum", y.data_ptr() + 4 * yoff, ld, M, groups, N, ptr(mean),
+             float(scale), part.data_ptr(), max_splits, out.data_ptr() + 4 * outoff, ldo,
+             int(accum), stream())
+        return
     cnt = counters(-(-N // 64) * groups, y.device)
     call("ensvs_colsum_once", y.data_ptr() + 4 * yoff, ld, M, groups, N, ptr(mean),
          float(scale), part.data_ptr(), max_splits, cnt.data_ptr(),

@@ -466,11 +466,14 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
       if (teach) rteach = teach[((long long)rsq * T + 4 * max(t - 1, 0) + 3) * ldt];
     }
   };
-  // step t-1's outputs from the published feat_out partials (reducer lanes only); returns lf0[3]
-  auto reduce_out = [&](int t, int base) -> float {
-    f32x4 op[NW];
+  // step t-1's outputs from the published feat_out partials op (reducer lanes only); returns
+  // lf0[3].  The partials are loaded with the step's h slab (one L2 round trip for both: the
+  // loads after the MFMAs made a second dependent round trip per AR step)
+  auto load_op = [&](int base, f32x4 (&op)[NW]) {
 #pragma unroll
     for (int w2 = 0; w2 < NW; ++w2) op[w2] = ld16(xr, base + G::FH + (tid * NW + w2) * 16);
+  };
+  auto reduce_out = [&](int t, const f32x4 (&op)[NW]) -> float {
     float l3 = 0.f;
     const long long row = (long long)rsq * Tr + t - 1;
 #pragma unroll
@@ -510,6 +513,8 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
         for (int nt = 0; nt < 2; ++nt)
           bf[kk][nt] = __builtin_bit_cast(
               f16x8, ld16(xr, ((nt * 16 + (lane & 15)) * H + (wv * KCW + kk) * 32 + 8 * (lane >> 4)) * 2 + base));
+      f32x4 op[NW];
+      if (tid < SB) load_op(base, op);
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk)
 #pragma unroll
@@ -522,7 +527,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
           for (int nt = 0; nt < 2; ++nt)
             acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[mt][kk], bf[kk][nt], acc[mt][nt], 0, 0, 0);
       if (tid < SB) {
-        const float l3 = reduce_out(t, base);
+        const float l3 = reduce_out(t, op);
         // the next input: this step's last frame, or the target there (teacher forcing)
         const float p = (teach ? rteach : l3) * rmask;
         pv[tid] = p;
@@ -588,7 +593,11 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
   }
   if (w == 0) {  // the last step's outputs
     wait_count(hdr, 0, (unsigned)(NW * Tr), c);
-    if (tid < SB) reduce_out(Tr, ((Tr - 1) & 1) * G::FBUF);
+    if (tid < SB) {
+      f32x4 op[NW];
+      load_op(((Tr - 1) & 1) * G::FBUF, op);
+      reduce_out(Tr, op);
+    }
   }
 }
 

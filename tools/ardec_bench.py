@@ -29,7 +29,7 @@ bargs = (a["wih_p"].data_ptr(), a["wfo"].data_ptr(), H + 130, a["mask"].data_ptr
          do4.data_ptr())
 wpf, wpb = E(4 * H * H), E(4 * H * H)
 call("ensvs_ardec_pack", a["whh"].data_ptr(), H, wpf.data_ptr(), wpb.data_ptr(), st)
-nbytes = query("ensvs_ardec_coop_work_bytes", H)
+nbytes = query("ensvs_ardec_coop_work_bytes", H, B)
 work = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
 wf = torch.empty(4 * H * H, dtype=torch.float16, device=dev)
 wb = torch.empty(4 * H * H, dtype=torch.bfloat16, device=dev)

@@ -512,10 +512,14 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
 
 
 _cnt_cache = {}
-# column sums in one launch (ensvs_colsum_once) or two (partial + final kernels); same bits
-COLSUM_ONCE = {"on": True}
+# column sums in one launch (ensvs_colsum_once, the last block of each column block reducing
+# the split partials) or two (partial + final kernels); same bits.  Off: the one-launch form
+# measured slower in the step, 14.27 / 14.31 vs 13.98 / 14.04 ms (write-through form;
+# 15.48 ms with release / acquire fences), profiles/r5_reduction_ab.txt
+COLSUM_ONCE = {"on": False}
 # queue the split reductions of parameter gradients inside deferred_wgrad() (one batched launch
-# per branch) or reduce each weight gradient right after it (same bits either way)
+# per branch, ~140 -> ~10 reduce launches per step) or reduce each weight gradient right after
+# it (same bits either way): 13.91 / 13.92 vs 13.98 / 14.04 ms, profiles/r5_reduction_ab.txt
 DEFER_WGRAD = {"on": True}
 
 

@@ -771,12 +771,13 @@ def shape_legs(args, dev, model, opt, base_ms, steps=5):
                                      frames=T // 2, train_loss=loss, grad_norm=norm,
                                      ratio_to_main=base_ms / ms)
     # long segments: the multitrack pairing never filters them (train_util.py:160-166 hard-codes
-    # filter_long_segments=False), so 4096-step recurrences reach the step
-    PL, TL = 8, 4096
-    ms, frames, loss, norm = _graphed_leg(model, opt, PL, TL, 1502, steps)
-    out[f"p{PL}x{TL}"] = dict(value=frames / ms * 1e3, ms_per_step=ms, pairs=PL, frames=TL,
-                              train_loss=loss, grad_norm=norm,
-                              ratio_to_main=(frames / ms) / (P * T / base_ms))
+    # filter_long_segments=False), so 4096-step recurrences reach the step;
+    # 15 x 2048 is the on-disk leg's longest bucket shape (songs of up to 2 048 frames)
+    for PL, TL, seed in ((15, 2048, 1503), (8, 4096, 1502)):
+        ms, frames, loss, norm = _graphed_leg(model, opt, PL, TL, seed, steps)
+        out[f"p{PL}x{TL}"] = dict(value=frames / ms * 1e3, ms_per_step=ms, pairs=PL, frames=TL,
+                                  train_loss=loss, grad_norm=norm,
+                                  ratio_to_main=(frames / ms) / (P * T / base_ms))
     rng = np.random.default_rng(8)
     lens = (rng.integers(T // 2, T + 1, size=P) // 4) * 4
     ms, frames, loss, norm = _graphed_leg(model, opt, P, T, 1501, steps, lengths=lens)

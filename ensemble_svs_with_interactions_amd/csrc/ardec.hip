@@ -369,7 +369,7 @@ int bwd_launch(const float* glf0, const float* gres, const float* wpb, const flo
 template <int H> struct ArGeo {
   static constexpr int NW = H / coop::UW, KCW = H / 128, KCBW = H / 32;
   static constexpr int FH = coop::SB * H * 2;      // forward slab per buffer: h [s][H] fp16
-  static constexpr int FBUF = FH + coop::SB * NW * 16;  // + feat_out partials [s][w][4] fp32
+  static constexpr int FBUF = FH + coop::SB * NW * 16;  // + feat_out partials [w][s][4] fp32
   static constexpr int BG = coop::SB * 4 * H * 2;  // backward per buffer: dG [s][4H] bf16
   static constexpr int BBUF = BG + coop::SB * NW * 4;   // + prenet partials [s][w] fp32
   static constexpr int SLAB = 2 * (FBUF > BBUF ? FBUF : BBUF);  // one tile's double buffer
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
   // loads after the MFMAs made a second dependent round trip per AR step)
   auto load_op = [&](int base, f32x4 (&op)[NW]) {
 #pragma unroll
-    for (int w2 = 0; w2 < NW; ++w2) op[w2] = ld16(xr, base + G::FH + (tid * NW + w2) * 16);
+    for (int w2 = 0; w2 < NW; ++w2) op[w2] = ld16(xr, base + G::FH + (w2 * SB + tid) * 16);
   };
   auto reduce_out = [&](int t, const f32x4 (&op)[NW]) -> float {
     float l3 = 0.f;
@@ -543,7 +543,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
         *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * AR_PSF + 16 * mt + 4 * (lane >> 4)] = acc[mt][nt];
-    __syncthreads();
+    lds_barrier();
     float out[2][6];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -569,12 +569,12 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
       }
       out[i][0] = ig; out[i][1] = fg; out[i][2] = gg; out[i][3] = og; out[i][4] = cn; out[i][5] = h;
     }
-    __syncthreads();
+    lds_barrier();
     if (wv == 0) {  // publish h_t (32 sequences x 16 units) and the feat_out partials
       const int base = (t & 1) * G::FBUF;
       st16(xr, base + ((lane >> 1) * H + u0 + (lane & 1) * 8) * 2,
            *(const f32x4*)&hs[(lane >> 1) * UW + (lane & 1) * 8]);
-      if (lane < SB) st16(xr, base + G::FH + (lane * NW + w) * 16, *(const f32x4*)&ops[lane * 4]);
+      if (lane < SB) st16(xr, base + G::FH + (w * SB + lane) * 16, *(const f32x4*)&ops[lane * 4]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(hdr, 0, t, c);
     }
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
       *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * AR_PSB + 4 * (lane >> 4)] = acc[nt];
-    __syncthreads();
+    lds_barrier();
     float o[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -765,14 +765,14 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
       pp = sum16(val ? pp : 0.f);
       if (u == 0) dps[s] = pp;
     }
-    __syncthreads();
+    lds_barrier();
     {  // publish dG_t (32 sequences x 64 values) and the prenet partials
       const int base = (q & 1) * G::BBUF;
       st16(xr, base + ((tid >> 3) * 4 * H + w * 64 + (tid & 7) * 8) * 2,
            *(const f32x4*)&gs[(tid >> 3) * 64 + (tid & 7) * 8]);
       if (tid < SB) st4(xr, base + G::BG + (tid * NW + w) * 4, dps[tid]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      lds_barrier();
       if (tid == 0) signal(hdr, 0, q, c);
     }
 #pragma unroll

@@ -70,6 +70,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t slab(unsigned* work, int nt, i
                                                (long long)z * slab_bytes, 0, slab_bytes, 0x00020000);
 }
 
+// A workgroup barrier for LDS exchange only: the wave's LDS operations done, then s_barrier.
+// __syncthreads() is a workgroup release / acquire, and hipcc drains every outstanding global
+// load AND store (s_waitcnt vmcnt(0)) before its s_barrier: in the step loops that made every
+// barrier wait for the previous step's saved-state stores (tools/ardec_phase_probe.py: the AR
+// step without those stores 4.85 -> 4.39 us).  Global data is never exchanged between the
+// waves of a workgroup through these barriers (the hand-off slabs have their own vmcnt(0) and
+// counters), and the compiler still waits for each global load before its first use.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // wait until direction d's counter of the tile reaches `target` (one lane polls), then release
 // the workgroup.  The first poll costs what the unbounded loop did; the clock is read only
 // once the counter is behind, and then every 8th poll.
@@ -92,7 +105,7 @@ __device__ __forceinline__ void wait_count(unsigned* hdr, int d, unsigned target
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 // publish step `step`'s slice: one agent-scope counter add (skipped by the test fault)

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
         *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * PSF + 16 * mt + 4 * (lane >> 4)] = acc[mt][nt];
-    __syncthreads();
+    lds_barrier();
     float out[2][6];
     bool val[2];
 #pragma unroll
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
       hs[s * UW + u] = (_Float16)(val[i] ? h : 0.f);
       out[i][0] = h; out[i][1] = ig; out[i][2] = fg; out[i][3] = gg; out[i][4] = og; out[i][5] = cn;
     }
-    __syncthreads();
+    lds_barrier();
     if (wv == 0) {  // publish h_t: 32 sequences x 16 units, one 16-B sc1 store per lane
       const f32x4 v = *(const f32x4*)&hs[(lane >> 1) * UW + (lane & 1) * 8];
       const int off = (((d * 2 + (t & 1)) * SB + (lane >> 1)) * H + u0 + (lane & 1) * 8) * 2;
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
       *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * PSB + 4 * (lane >> 4)] = acc[nt];
-    __syncthreads();
+    lds_barrier();
     float o[2][4];
     bool val[2];
 #pragma unroll
@@ -361,13 +361,13 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
       for (int g = 0; g < 4; ++g) nb[g] = (__bf16)(val[i] ? o[i][g] : 0.f);
       *(bf16x4_*)&gs[s * 64 + 4 * u] = nb;
     }
-    __syncthreads();
+    lds_barrier();
     {  // publish dG: 32 sequences x 64 values, one 16-B sc1 store per thread
       const f32x4 v = *(const f32x4*)&gs[(tid >> 3) * 64 + (tid & 7) * 8];
       const int off = (((d * 2 + (q & 1)) * SB + (tid >> 3)) * G4 + w * 64 + (tid & 7) * 8) * 2;
       __builtin_amdgcn_raw_buffer_store_b128(v, xr, off, 0, CP_SC1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      lds_barrier();
       if (tid == 0) signal(hdr, d, q, c);
     }
 #pragma unroll

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(NT) void probe_kernel(
         f32x4 op[NW];
         if (tid < SB && MODE != 5)
 #pragma unroll
-          for (int w2 = 0; w2 < NW; ++w2) op[w2] = ld16(xr, base + FH + (tid * NW + w2) * 16);
+          for (int w2 = 0; w2 < NW; ++w2) op[w2] = ld16(xr, base + FH + (w2 * SB + tid) * 16);
 #pragma unroll
         for (int kk = 0; kk < KCW; ++kk)
 #pragma unroll
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(NT) void probe_kernel(
       const int base = (t & 1) * FBUF;
       st16(xr, base + ((lane >> 1) * H + u0 + (lane & 1) * 8) * 2,
            *(const f32x4*)&hs[(lane >> 1) * UW + (lane & 1) * 8]);
-      if (lane < SB) st16(xr, base + FH + (lane * NW + w) * 16, *(const f32x4*)&ops[lane * 4]);
+      if (lane < SB) st16(xr, base + FH + (w * SB + lane) * 16, *(const f32x4*)&ops[lane * 4]);
       if (MODE != 6) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(hdr, 0, t, c);
     }

@@ -139,7 +139,7 @@ __global__ __launch_bounds__(NT) void probe_kernel(
         for (int nt = 0; nt < 2; ++nt)
           *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * PSF + 16 * mt + 4 * (lane >> 4)] = acc[mt][nt];
     }
-    __syncthreads();
+    lds_barrier();
     float out[2][6];
     if (MODE != 7) {
 #pragma unroll
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(NT) void probe_kernel(
         out[i][0] = ig; out[i][1] = fg; out[i][2] = gg; out[i][3] = og; out[i][4] = cn; out[i][5] = h;
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (wv == 0) {
       const int base = (t & 1) * FBUF;
       st16(xr, base + ((lane >> 1) * H + u0 + (lane & 1) * 8) * 2,

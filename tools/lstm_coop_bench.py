@@ -37,7 +37,7 @@ for H in (256, 512):
     dg = torch.empty(B * T, 8 * H, device=dev)
     nw = query("ensvs_lstm_bwd_work_floats", B, H)
     work = torch.empty(max(nw, 1), device=dev)
-    nb = query("ensvs_lstm_coop_work_bytes", H)
+    nb = query("ensvs_lstm_coop_work_bytes", H, B)
     cw = torch.empty(nb, dtype=torch.uint8, device=dev)
     wpf = torch.empty(2 * 4 * H * H, dtype=torch.float16, device=dev)
     wpb = torch.empty(2 * 4 * H * H, dtype=torch.bfloat16, device=dev)

@@ -379,8 +379,19 @@ template <int H> struct ArGeo {
 constexpr int AR_PSF = 68;  // forward partial-sum row per sequence: 64 gate rows + 4 (banks)
 constexpr int AR_PSB = 20;  // backward: 16 units + 4
 
+// Forward, with a fifth "service" wave per workgroup (round 5, tools/ardec_phase_probe.py):
+// the four compute waves run the recurrent product and the cell update and issue no global
+// store; the service wave forms step t-1's outputs from the published feat_out partials (its
+// reducer lanes, one per sequence: lf0, residual, o, and the next input p, which the compute
+// waves read from LDS) and writes every saved value of step t (i f g o c h, staged in LDS by
+// the compute waves) with 16-B stores after the step's second barrier.  Its stores never sit
+// in a compute wave's vmcnt, and the reduction no longer lengthens compute wave 0's step
+// (probe: 4.57 us per AR step with both in the compute waves, 4.13 without the stores, 3.71
+// without the reduction).
+constexpr int AR_NTS = coop::NT + 64;
+
 template <int H>
-__global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
+__global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
     const float* __restrict__ gx, int ldgx, const float* __restrict__ ofx, int ldo,
     const f16x8* __restrict__ wp, const float* __restrict__ wih_p,
     const float* __restrict__ wfo, int ldwfo, const float* __restrict__ score, int lds,
@@ -395,8 +406,10 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
   __shared__ __attribute__((aligned(16))) _Float16 hs[SB * UW];
   __shared__ __attribute__((aligned(16))) float ops[SB * 4];
   __shared__ float pv[SB];
+  __shared__ __attribute__((aligned(16))) float sv6[SB * 6 * UW];  // [s][i f g o c h][u]
   const int w = blockIdx.x, u0 = w * UW;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const bool service = wv == 4;
   const int Tr = T / 4;
   {  // this workgroup's sequence tile (blockIdx.y): sequences [32 y, 32 y + 32)
     const int s0 = blockIdx.y * SB;
@@ -417,7 +430,90 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
   }
   unsigned* hdr = tile_hdr(work, blockIdx.y);
   const float den = k.in_max - k.in_min;
+  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.y, blockIdx.y, G::SLAB);
 
+  if (service) {
+    // ---------------------------------------------------------------- the service wave
+    // reducer lane `lane` < SB owns sequence `lane`: the inputs of step t-1's outputs and p_t
+    const int rsq = min(lane, B - 1);
+    const bool red = lane < SB;
+    const bool rw = red && lane < B && w == 0;  // writes the per-sequence outputs
+    float rofx[4], rsd[4], rmask = 0.f, rteach = 0.f;
+    auto load_red = [&](int t) {  // ofx / score of step t - 1, mask of step t
+      if (red) {
+        const long long row = (long long)rsq * Tr + max(t - 1, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          rofx[r] = ofx[row * ldo + r];
+          rsd[r] = score[((long long)rsq * T + 4 * max(t - 1, 0) + r) * lds];
+        }
+        if (t < Tr) rmask = mask[(long long)rsq * Tr + t];
+        if (teach) rteach = teach[((long long)rsq * T + 4 * max(t - 1, 0) + 3) * ldt];
+      }
+    };
+    // step t-1's outputs from the published feat_out partials (slab layout [w][s][4]); lf0[3]
+    auto reduce_out = [&](int t, int base) -> float {
+      f32x4 op[NW];
+#pragma unroll
+      for (int w2 = 0; w2 < NW; ++w2) op[w2] = ld16(xr, base + G::FH + (w2 * SB + lane) * 16);
+      float l3 = 0.f;
+      const long long row = (long long)rsq * Tr + t - 1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float ov = rofx[r];
+#pragma unroll
+        for (int w2 = 0; w2 < NW; ++w2) ov += op[w2][r];
+        const float rs = MAX_LF0_RATIO * tanhf(ov);
+        const float sd = rsd[r] * den + k.in_min;
+        const float l = (sd + rs - k.mean) / k.scale;
+        if (rw) {
+          const long long f = (long long)rsq * T + 4 * (t - 1) + r;
+          lf0[f] = l;
+          res[f] = rs;
+          so[row * 4 + r] = ov;
+        }
+        l3 = l;
+      }
+      return l3;
+    };
+    load_red(0);
+    for (int t = 0; t < Tr; ++t) {
+      float l3 = 0.f;
+      if (t > 0) {
+        wait_count(hdr, 0, (unsigned)(NW * t), c);
+        if (red) l3 = reduce_out(t, ((t - 1) & 1) * G::FBUF);
+      }
+      if (red) {
+        // the next input: the last frame of step t-1, or the target there (teacher forcing);
+        // prev = 0 before the first step
+        const float p = (t == 0 ? 0.f : (teach ? rteach : l3)) * rmask;
+        pv[lane] = p;
+        if (rw) sp[(long long)rsq * Tr + t] = p;
+      }
+      lds_barrier();  // (1) p of every sequence in LDS
+      lds_barrier();  // (2) step t's saved values in sv6
+      // step t's saved values: 32 sequences x 6 rows of 16 units, 16 B per store
+#pragma unroll
+      for (int k4 = 0; k4 < SB * 6 * UW / 4 / 64; ++k4) {
+        const int gi = lane + 64 * k4, sq = gi / (6 * UW / 4), rem = gi % (6 * UW / 4);
+        const int q = rem / (UW / 4), c4 = (rem % (UW / 4)) * 4;
+        const f32x4 v = *(const f32x4*)&sv6[(sq * 6 + q) * UW + c4];
+        if (sq < B) {
+          const long long row = (long long)sq * Tr + t;
+          float* dst = q < 4 ? sg + row * 4 * H + q * H : (q == 4 ? sc : sh) + row * H;
+          *(f32x4*)(dst + u0 + c4) = v;
+        }
+      }
+      load_red(t + 1);
+    }
+    if (w == 0) {  // the last step's outputs
+      wait_count(hdr, 0, (unsigned)(NW * Tr), c);
+      if (red) reduce_out(Tr, ((Tr - 1) & 1) * G::FBUF);
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------ the compute waves
   f16x8 wf[4][KCW];
   {
     const f16x8* src = wp + (((long long)w * 4 + wv) * 4 * KCW) * 64 + lane;
@@ -426,8 +522,6 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk) wf[mt][kk] = src[(mt * KCW + kk) * 64];
   }
-  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.y, blockIdx.y, G::SLAB);
-
   // cells (unit u = p & 15, sequence s = p >> 4), p = tid + 256 i: 16 lanes per sequence
   int cs[2], cu[2];
   float wpc[2][4], woc[2][4];
@@ -450,52 +544,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
       for (int g = 0; g < 4; ++g) gin[i][g] = src[g * H];
     }
   };
-  // reducer lanes (tid < SB, sequence tid): the inputs of step t-1's outputs and step t's p
-  const int rsq = min(tid, B - 1);
-  const bool rw = tid < SB && tid < B && w == 0;  // writes the per-sequence outputs
-  float rofx[4], rsd[4], rmask = 0.f, rteach = 0.f;
-  auto load_red = [&](int t) {  // ofx / score of step t - 1, mask of step t
-    if (tid < SB) {
-      const long long row = (long long)rsq * Tr + max(t - 1, 0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        rofx[r] = ofx[row * ldo + r];
-        rsd[r] = score[((long long)rsq * T + 4 * max(t - 1, 0) + r) * lds];
-      }
-      if (t < Tr) rmask = mask[(long long)rsq * Tr + t];
-      if (teach) rteach = teach[((long long)rsq * T + 4 * max(t - 1, 0) + 3) * ldt];
-    }
-  };
-  // step t-1's outputs from the published feat_out partials op (reducer lanes only); returns
-  // lf0[3].  The partials are loaded with the step's h slab (one L2 round trip for both: the
-  // loads after the MFMAs made a second dependent round trip per AR step)
-  auto load_op = [&](int base, f32x4 (&op)[NW]) {
-#pragma unroll
-    for (int w2 = 0; w2 < NW; ++w2) op[w2] = ld16(xr, base + G::FH + (w2 * SB + tid) * 16);
-  };
-  auto reduce_out = [&](int t, const f32x4 (&op)[NW]) -> float {
-    float l3 = 0.f;
-    const long long row = (long long)rsq * Tr + t - 1;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float ov = rofx[r];
-#pragma unroll
-      for (int w2 = 0; w2 < NW; ++w2) ov += op[w2][r];
-      const float rs = MAX_LF0_RATIO * tanhf(ov);
-      const float sd = rsd[r] * den + k.in_min;
-      const float l = (sd + rs - k.mean) / k.scale;
-      if (rw) {
-        const long long f = (long long)rsq * T + 4 * (t - 1) + r;
-        lf0[f] = l;
-        res[f] = rs;
-        so[row * 4 + r] = ov;
-      }
-      l3 = l;
-    }
-    return l3;
-  };
   load_in(0);
-  load_red(0);
 
   for (int t = 0; t < Tr; ++t) {
     f32x4 acc[4][2];
@@ -513,8 +562,6 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
         for (int nt = 0; nt < 2; ++nt)
           bf[kk][nt] = __builtin_bit_cast(
               f16x8, ld16(xr, ((nt * 16 + (lane & 15)) * H + (wv * KCW + kk) * 32 + 8 * (lane >> 4)) * 2 + base));
-      f32x4 op[NW];
-      if (tid < SB) load_op(base, op);
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk)
 #pragma unroll
@@ -526,25 +573,13 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt)
             acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[mt][kk], bf[kk][nt], acc[mt][nt], 0, 0, 0);
-      if (tid < SB) {
-        const float l3 = reduce_out(t, op);
-        // the next input: this step's last frame, or the target there (teacher forcing)
-        const float p = (teach ? rteach : l3) * rmask;
-        pv[tid] = p;
-        if (rw) sp[(long long)rsq * Tr + t] = p;
-      }
-    } else if (tid < SB) {
-      const float p = 0.f * rmask;  // prev = 0 before the first step
-      pv[tid] = p;
-      if (rw) sp[(long long)rsq * Tr] = p;
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
         *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * AR_PSF + 16 * mt + 4 * (lane >> 4)] = acc[mt][nt];
-    lds_barrier();
-    float out[2][6];
+    lds_barrier();  // (1)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int s = cs[i], u = cu[i];
@@ -567,9 +602,15 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
         const float v = sum16(woc[i][r] * (val ? h : 0.f));
         if (u == 0) ops[s * 4 + r] = v;
       }
-      out[i][0] = ig; out[i][1] = fg; out[i][2] = gg; out[i][3] = og; out[i][4] = cn; out[i][5] = h;
+      float* o6 = sv6 + s * 6 * UW + u;
+      o6[0] = ig;
+      o6[UW] = fg;
+      o6[2 * UW] = gg;
+      o6[3 * UW] = og;
+      o6[4 * UW] = cn;
+      o6[5 * UW] = h;
     }
-    lds_barrier();
+    lds_barrier();  // (2)
     if (wv == 0) {  // publish h_t (32 sequences x 16 units) and the feat_out partials
       const int base = (t & 1) * G::FBUF;
       st16(xr, base + ((lane >> 1) * H + u0 + (lane & 1) * 8) * 2,
@@ -578,27 +619,9 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_fwd_kernel(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(hdr, 0, t, c);
     }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (cs[i] < B) {
-        const long long row = (long long)cs[i] * Tr + t;
-        const int j = u0 + cu[i];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) sg[row * 4 * H + g * H + j] = out[i][g];
-        sc[row * H + j] = out[i][4];
-        sh[row * H + j] = out[i][5];
-      }
     if (t + 1 < Tr) load_in(t + 1);
-    load_red(t + 1);
   }
-  if (w == 0) {  // the last step's outputs
-    wait_count(hdr, 0, (unsigned)(NW * Tr), c);
-    if (tid < SB) {
-      f32x4 op[NW];
-      load_op(((Tr - 1) & 1) * G::FBUF, op);
-      reduce_out(Tr, op);
-    }
-  }
+  if (w == 0) wait_count(hdr, 0, (unsigned)(NW * Tr), c);  // (the service wave's last outputs)
 }
 
 template <int H>
@@ -807,7 +830,8 @@ int coop_fwd_launch(const float* gx, int ldgx, const float* ofx, int ldo, const 
                     const float* mask, const float* teach, int ldt, int B, int T, ArConsts k,
                     float* lf0, float* res, float* sg, float* sc, float* sh, float* so, float* sp,
                     unsigned* work, hipStream_t st) {
-  const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSF + coop::SB * 5) + 2 * coop::SB * coop::UW;
+  const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSF + coop::SB * 5 +
+                                         coop::SB * 6 * coop::UW) + 2 * coop::SB * coop::UW;
   static const bool attr = coop::set_max_lds((const void*)ardec_coop_fwd_kernel<H>, st_lds);
   if (!attr) return ENSVS_E_HIP;
   const coop::Ctl ctl = coop::host_ctl();
@@ -817,7 +841,7 @@ int coop_fwd_launch(const float* gx, int ldgx, const float* ofx, int ldo, const 
     const long long b0 = (long long)t0 * coop::SB, r = b0 * Tr, f = b0 * T;
     unsigned* wk = (unsigned*)((char*)work + (t0 / AR_MAX_TILES) * ar_wave_bytes<H>());
     if (hipMemsetAsync(wk, 0, (size_t)nt * coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(ardec_coop_fwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(coop::NT),
+    hipLaunchKernelGGL(ardec_coop_fwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(AR_NTS),
                        coop::dyn_lds(st_lds), st, gx + r * ldgx, ldgx, ofx + r * ldo, ldo,
                        (const f16x8*)wp, wih_p, wfo, ldwfo, score + f * lds, lds, mask + r,
                        teach ? teach + f * ldt : teach, ldt, (int)(B - b0), T, k, lf0 + f, res + f,
@@ -938,6 +962,7 @@ ENSVS_API int ensvs_ardec_coop_fwd(const float* gx, int ldgx, const float* ofx, 
                                    void* stream) {
   if (int e = ar_coop_check(B, T, H, wpack, work, work_bytes)) return e;
   if (ldgx < 4 * H || ldo < 4) return ENSVS_E_SHAPE;
+  if (((uintptr_t)sg | (uintptr_t)sc | (uintptr_t)sh) & 15) return ENSVS_E_ARG;  // 16-B stores
   ArConsts k{in_min, in_max, mean, scale};
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;

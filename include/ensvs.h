@@ -278,7 +278,8 @@ int ensvs_ardec_bwd(const float* glf0, const float* gres, const float* wpb, cons
  * (bwd = 0 forward fp16 fragments, bwd = 1 backward bf16 fragments), 4*H*H 2-byte elements;
  * sequences in tiles of 32 (blockIdx.y) as the LSTM above; work: 256-B aligned,
  * ensvs_ardec_coop_work_bytes(H, B) bytes, caller-owned, one per concurrent launch, laid out
- * and flagged as the LSTM's. */
+ * and flagged as the LSTM's.  The forward's saved-state outputs sg / sc / sh are 16-B aligned
+ * (written with 16-B stores). */
 int ensvs_ardec_coop_supported(int B, int H);
 long long ensvs_ardec_coop_work_bytes(int H, int B);
 /* Failure controls of every cooperative launch (coop.h).  A tile whose workgroups cannot all

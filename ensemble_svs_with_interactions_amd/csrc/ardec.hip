@@ -624,8 +624,13 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
   if (w == 0) wait_count(hdr, 0, (unsigned)(NW * Tr), c);  // (the service wave's last outputs)
 }
 
+// Backward, with the forward's service wave: it forms d o_t (the feat_out output gradient,
+// tanhf of the saved o) and d prev from the published prenet partials (reducer lanes, one
+// per sequence) and writes the gate gradients dG_t (staged in LDS by the compute waves) and
+// d o_t with 16-B stores after the step's barriers; the compute waves run W_hh^T dG, the cell
+// backward and the dG hand-off, and issue no other global store.
 template <int H>
-__global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
+__global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
     const float* __restrict__ glf0, const float* __restrict__ gres,
     const bf16x8* __restrict__ wp, const float* __restrict__ wih_p,
     const float* __restrict__ wfo, int ldwfo, const float* __restrict__ mask, int teacher, int B,
@@ -639,6 +644,7 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
   __shared__ __attribute__((aligned(16))) __bf16 gs[SB * 64];  // [s][4 u + g]
   __shared__ float d4s[SB * 4];
   __shared__ float dps[SB];
+  __shared__ __attribute__((aligned(16))) float dg4[SB * 4 * UW];  // [s][g][u]
   const int w = blockIdx.x, u0 = w * UW;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int Tr = T / 4;
@@ -656,15 +662,80 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
     do4 += r * 4;
   }
   unsigned* hdr = tile_hdr(work, blockIdx.y);
+  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.y, blockIdx.y, G::SLAB);
 
+  if (wv == 4) {
+    // ---------------------------------------------------------------- the service wave
+    const int rsq = min(lane, B - 1);
+    const bool red = lane < SB;
+    const bool rw = red && lane < B && w == 0;
+    float rgl[4], rgr[4], rso[4], rmask = 0.f;
+    auto load_red = [&](int t) {  // output grads / saved o of step t, mask of step t + 1
+      if (red) {
+        const long long row = (long long)rsq * Tr + t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long long f = (long long)rsq * T + 4 * t + r;
+          rgl[r] = glf0[f];
+          rgr[r] = gres ? gres[f] : 0.f;
+          rso[r] = so[row * 4 + r];
+        }
+        rmask = t + 1 < Tr ? mask[row + 1] : 0.f;
+      }
+    };
+    load_red(Tr - 1);
+    for (int q = 0; q < Tr; ++q) {
+      const int t = Tr - 1 - q;
+      float dprev = 0.f;
+      if (q > 0) {
+        wait_count(hdr, 0, (unsigned)(NW * q), c);
+        if (red && !teacher) {
+          const int base = ((q - 1) & 1) * G::BBUF;
+          f32x4 pp[NW / 4];
+#pragma unroll
+          for (int j = 0; j < NW / 4; ++j) pp[j] = ld16(xr, base + G::BG + (lane * NW + 4 * j) * 4);
+          float dp = 0.f;
+#pragma unroll
+          for (int j = 0; j < NW / 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dp += pp[j][e];
+          dprev = dp * rmask;  // p_{t+1} = lf0_t[3] * mask_{t+1}
+        }
+      }
+      float d4[4];
+      if (red) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float dl = rgl[r] + (r == 3 ? dprev : 0.f);
+          const float dr = rgr[r] + dl / k.scale;
+          const float th = tanhf(rso[r]);
+          d4[r] = dr * MAX_LF0_RATIO * (1.f - th * th);
+          d4s[lane * 4 + r] = d4[r];
+        }
+        if (rw) *(f32x4*)(do4 + ((long long)rsq * Tr + t) * 4) = f32x4{d4[0], d4[1], d4[2], d4[3]};
+      }
+      lds_barrier();  // (1) d o_t in LDS
+      lds_barrier();  // (2) dG_t staged
+      lds_barrier();  // (3) dG_t published
+      // dG_t: 32 sequences x 4 gates x 16 units, 16 B per store
+#pragma unroll
+      for (int k4 = 0; k4 < SB * 4 * UW / 4 / 64; ++k4) {
+        const int gi = lane + 64 * k4, sq = gi / UW, g = (gi / (UW / 4)) % 4, c4 = (gi % (UW / 4)) * 4;
+        const f32x4 v = *(const f32x4*)&dg4[(sq * 4 + g) * UW + c4];
+        if (sq < B) *(f32x4*)(dg + ((long long)sq * Tr + t) * 4 * H + g * H + u0 + c4) = v;
+      }
+      if (t > 0) load_red(t - 1);
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------ the compute waves
   bf16x8 wb[KCBW];
   {
     const bf16x8* src = wp + (((long long)w * 4 + wv) * KCBW) * 64 + lane;
 #pragma unroll
     for (int kk = 0; kk < KCBW; ++kk) wb[kk] = src[kk * 64];
   }
-  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.y, blockIdx.y, G::SLAB);
-
   int cs[2], cu[2];
   float wo[2][4], wpg[2][4];
 #pragma unroll
@@ -689,29 +760,11 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
       in[i][5] = t > 0 ? sc[(row - 1) * H + j] : 0.f;
     }
   };
-  const int rsq = min(tid, B - 1);
-  const bool rw = tid < SB && tid < B && w == 0;
-  float rgl[4], rgr[4], rso[4], rmask = 0.f;
-  auto load_red = [&](int t) {  // output grads / saved o of step t, mask of step t + 1
-    if (tid < SB) {
-      const long long row = (long long)rsq * Tr + t;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long long f = (long long)rsq * T + 4 * t + r;
-        rgl[r] = glf0[f];
-        rgr[r] = gres ? gres[f] : 0.f;
-        rso[r] = so[row * 4 + r];
-      }
-      rmask = t + 1 < Tr ? mask[row + 1] : 0.f;
-    }
-  };
   load_in(Tr - 1);
-  load_red(Tr - 1);
 
   for (int q = 0; q < Tr; ++q) {
     const int t = Tr - 1 - q;
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    float dprev = 0.f;
     if (q > 0) {
       wait_count(hdr, 0, (unsigned)(NW * q), c);
       const int base = ((q - 1) & 1) * G::BBUF;
@@ -722,10 +775,6 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
         for (int nt = 0; nt < 2; ++nt)
           bf[kk][nt] = __builtin_bit_cast(
               bf16x8, ld16(xr, ((nt * 16 + (lane & 15)) * 4 * H + (wv * KCBW + kk) * 32 + 8 * (lane >> 4)) * 2 + base));
-      f32x4 pp[NW / 4];
-      if (tid < SB)
-#pragma unroll
-        for (int j = 0; j < NW / 4; ++j) pp[j] = ld16(xr, base + G::BG + (tid * NW + 4 * j) * 4);
 #pragma unroll
       for (int kk = 0; kk < KCBW; ++kk)
 #pragma unroll
@@ -735,31 +784,11 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
           acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[kk], bf[kk][nt], acc[nt], 0, 0, 0);
-      if (tid < SB && !teacher) {
-        float dp = 0.f;
-#pragma unroll
-        for (int j = 0; j < NW / 4; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) dp += pp[j][e];
-        dprev = dp * rmask;  // p_{t+1} = lf0_t[3] * mask_{t+1}
-      }
-    }
-    float d4[4];
-    if (tid < SB) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float dl = rgl[r] + (r == 3 ? dprev : 0.f);
-        const float dr = rgr[r] + dl / k.scale;
-        const float th = tanhf(rso[r]);
-        d4[r] = dr * MAX_LF0_RATIO * (1.f - th * th);
-        d4s[tid * 4 + r] = d4[r];
-      }
     }
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
       *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * AR_PSB + 4 * (lane >> 4)] = acc[nt];
-    lds_barrier();
-    float o[2][4];
+    lds_barrier();  // (1)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int s = cs[i], u = cu[i];
@@ -771,48 +800,36 @@ __global__ __launch_bounds__(coop::NT) void ardec_coop_bwd_kernel(
       const float ig = in[i][0], fg = in[i][1], gg = in[i][2], og = in[i][3];
       const float tc = tanh_fast(in[i][4]);
       const float dcc = dcs[i] + dh * og * (1.f - tc * tc);
-      o[i][0] = dcc * gg * ig * (1.f - ig);
-      o[i][1] = dcc * in[i][5] * fg * (1.f - fg);
-      o[i][2] = dcc * ig * (1.f - gg * gg);
-      o[i][3] = dh * tc * og * (1.f - og);
+      float o[4];
+      o[0] = dcc * gg * ig * (1.f - ig);
+      o[1] = dcc * in[i][5] * fg * (1.f - fg);
+      o[2] = dcc * ig * (1.f - gg * gg);
+      o[3] = dh * tc * og * (1.f - og);
       dcs[i] = dcc * fg;
       const bool val = s < B;
       bf16x4 nb;
       float pp = 0.f;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        nb[g] = (__bf16)(val ? o[i][g] : 0.f);
-        pp = fmaf(wpg[i][g], o[i][g], pp);
+        nb[g] = (__bf16)(val ? o[g] : 0.f);
+        pp = fmaf(wpg[i][g], o[g], pp);
+        dg4[(s * 4 + g) * UW + u] = o[g];
       }
       *(bf16x4*)&gs[s * 64 + 4 * u] = nb;
       pp = sum16(val ? pp : 0.f);
       if (u == 0) dps[s] = pp;
     }
-    lds_barrier();
+    lds_barrier();  // (2)
     {  // publish dG_t (32 sequences x 64 values) and the prenet partials
       const int base = (q & 1) * G::BBUF;
       st16(xr, base + ((tid >> 3) * 4 * H + w * 64 + (tid & 7) * 8) * 2,
            *(const f32x4*)&gs[(tid >> 3) * 64 + (tid & 7) * 8]);
       if (tid < SB) st4(xr, base + G::BG + (tid * NW + w) * 4, dps[tid]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
+      lds_barrier();  // (3)
       if (tid == 0) signal(hdr, 0, q, c);
     }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (cs[i] < B) {
-        float* dst = dg + ((long long)cs[i] * Tr + t) * 4 * H + u0 + cu[i];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) dst[g * H] = o[i][g];
-      }
-    if (rw) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) do4[((long long)rsq * Tr + t) * 4 + r] = d4[r];
-    }
-    if (t > 0) {
-      load_in(t - 1);
-      load_red(t - 1);
-    }
+    if (t > 0) load_in(t - 1);
   }
 }
 
@@ -856,7 +873,8 @@ int coop_bwd_launch(const float* glf0, const float* gres, const void* wp, const 
                     const float* wfo, int ldwfo, const float* mask, int teacher, int B, int T,
                     ArConsts k, const float* sg, const float* sc, const float* so, float* dg,
                     float* do4, unsigned* work, hipStream_t st) {
-  const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSB + coop::SB * 5) + 2 * coop::SB * 64;
+  const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSB + coop::SB * 5 +
+                                         coop::SB * 4 * coop::UW) + 2 * coop::SB * 64;
   static const bool attr = coop::set_max_lds((const void*)ardec_coop_bwd_kernel<H>, st_lds);
   if (!attr) return ENSVS_E_HIP;
   const coop::Ctl ctl = coop::host_ctl();
@@ -866,7 +884,7 @@ int coop_bwd_launch(const float* glf0, const float* gres, const void* wp, const 
     const long long b0 = (long long)t0 * coop::SB, r = b0 * Tr, f = b0 * T;
     unsigned* wk = (unsigned*)((char*)work + (t0 / AR_MAX_TILES) * ar_wave_bytes<H>());
     if (hipMemsetAsync(wk, 0, (size_t)nt * coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(ardec_coop_bwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(coop::NT),
+    hipLaunchKernelGGL(ardec_coop_bwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(AR_NTS),
                        coop::dyn_lds(st_lds), st, glf0 + f, gres ? gres + f : gres,
                        (const bf16x8*)wp, wih_p, wfo, ldwfo, mask + r, teacher, (int)(B - b0), T,
                        k, sg + r * 4 * H, sc + r * H, so + r * 4, dg + r * 4 * H, do4 + r * 4, wk,
@@ -977,6 +995,7 @@ ENSVS_API int ensvs_ardec_coop_bwd(const float* glf0, const float* gres, const v
                                    const float* sg, const float* sc, const float* so, float* dg,
                                    float* do4, void* work, long long work_bytes, void* stream) {
   if (int e = ar_coop_check(B, T, H, wpack, work, work_bytes)) return e;
+  if (((uintptr_t)dg | (uintptr_t)do4) & 15) return ENSVS_E_ARG;  // 16-B stores
   ArConsts k{in_min, in_max, mean, scale};
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;

@@ -89,8 +89,14 @@ __global__ void coop_pack_bwd_kernel(const float* __restrict__ w0, const float* 
   }
 }
 
+// Round 5: a fifth "service" wave per workgroup writes every step's outputs (y and the saved
+// i f g o c, staged in LDS by the compute waves) with 16-B stores after the step's barriers,
+// so no compute wave carries a global store in its vmcnt (ardec.hip's forward does the same;
+// tools/ardec_phase_probe.py measured the stores at ~0.44 us of a 4.6 us step there).
+constexpr int NTS = NT + 64;
+
 template <int H>
-__global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
+__global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
     const float* __restrict__ gx, int ldg,     // [B*T][ldg], dir d gate g unit u at d 4H + g H + u
     const f16x8* __restrict__ wp,              // packed forward fragments
     const long long* __restrict__ lengths, int B, int T,
@@ -102,6 +108,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
   __shared__ __attribute__((aligned(16))) float part[4 * SB * PSF];
   __shared__ __attribute__((aligned(16))) _Float16 hs[SB * UW];
   __shared__ int sL[SB];
+  __shared__ __attribute__((aligned(16))) float st6[SB * 6 * UW];  // [s][h i f g o c][u]
   const int d = blockIdx.y, w = blockIdx.x, u0 = w * UW;
   {  // this workgroup's sequence tile: sequences [32 z, 32 z + 32)
     const int s0 = blockIdx.z * SB;
@@ -114,6 +121,39 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
   unsigned* hdr = tile_hdr(work, blockIdx.z);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < SB) sL[tid] = tid < B ? (int)lengths[tid] : 0;
+  __syncthreads();
+  int maxL = 0;
+  for (int s = 0; s < B; ++s) maxL = max(maxL, sL[s]);
+  // pad_packed_sequence: this workgroup's output columns past each sequence's end are zero
+  for (int s = 0; s < B; ++s) {
+    const int L = sL[s];
+    for (int i = tid; i < (T - L) * UW; i += NTS)
+      y[((long long)s * T + L + i / UW) * ldy + d * H + u0 + i % UW] = 0.f;
+  }
+  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.z, blockIdx.z, G::BX);
+
+  if (wv == 4) {
+    // ---------------------------------------------------------------- the service wave
+    for (int t = 0; t < maxL; ++t) {
+      if (t > 0) wait_count(hdr, d, (unsigned)(NW * t), c);
+      lds_barrier();  // (1)
+      lds_barrier();  // (2) step t's outputs staged in st6
+      // 32 sequences x 6 rows (h i f g o c) of 16 units, 16 B per store
+#pragma unroll
+      for (int k4 = 0; k4 < SB * 6 * UW / 4 / 64; ++k4) {
+        const int gi = lane + 64 * k4, sq = gi / (6 * UW / 4), rem = gi % (6 * UW / 4);
+        const int q = rem / (UW / 4), c4 = (rem % (UW / 4)) * 4;
+        const f32x4 v = *(const f32x4*)&st6[(sq * 6 + q) * UW + c4];
+        const int L = sq < B ? sL[sq] : 0;
+        if (t < L) {
+          const long long row = (long long)sq * T + (d ? L - 1 - t : t);
+          float* dst = q == 0 ? y + row * ldy + d * H : sv + (row * 2 + d) * 5 * H + (q - 1) * H;
+          *(f32x4*)(dst + u0 + c4) = v;
+        }
+      }
+    }
+    return;
+  }
 
   f16x8 wf[4][KCW];
   {
@@ -123,16 +163,6 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk) wf[mt][kk] = src[(mt * KCW + kk) * 64];
   }
-  __syncthreads();
-  int maxL = 0;
-  for (int s = 0; s < B; ++s) maxL = max(maxL, sL[s]);
-  // pad_packed_sequence: this workgroup's output columns past each sequence's end are zero
-  for (int s = 0; s < B; ++s) {
-    const int L = sL[s];
-    for (int i = tid; i < (T - L) * UW; i += NT)
-      y[((long long)s * T + L + i / UW) * ldy + d * H + u0 + i % UW] = 0.f;
-  }
-  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.z, blockIdx.z, G::BX);
 
   // cell pairs: (unit u = p & 15, sequence s = p >> 4), p = tid + 256 i
   int cs[2], cu[2];
@@ -197,8 +227,6 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
       for (int nt = 0; nt < 2; ++nt)
         *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * PSF + 16 * mt + 4 * (lane >> 4)] = acc[mt][nt];
     lds_barrier();
-    float out[2][6];
-    bool val[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int s = cs[i], u = cu[i];
@@ -209,10 +237,16 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
       const float gg = tanh_fast(a[2] + gin[i][2]), og = sigm(a[3] + gin[i][3]);
       const float cn = fg * cst[i] + ig * gg;
       const float h = og * tanh_fast(cn);
-      val[i] = t < sL[s];
+      const bool val = t < sL[s];
       cst[i] = cn;
-      hs[s * UW + u] = (_Float16)(val[i] ? h : 0.f);
-      out[i][0] = h; out[i][1] = ig; out[i][2] = fg; out[i][3] = gg; out[i][4] = og; out[i][5] = cn;
+      hs[s * UW + u] = (_Float16)(val ? h : 0.f);
+      float* o6 = st6 + s * 6 * UW + u;
+      o6[0] = h;
+      o6[UW] = ig;
+      o6[2 * UW] = fg;
+      o6[3 * UW] = gg;
+      o6[4 * UW] = og;
+      o6[5 * UW] = cn;
     }
     lds_barrier();
     if (wv == 0) {  // publish h_t: 32 sequences x 16 units, one 16-B sc1 store per lane
@@ -222,22 +256,12 @@ __global__ __launch_bounds__(NT) void lstm_coop_fwd_kernel(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(hdr, d, t, c);
     }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (val[i]) {
-        const long long row = grow[i];
-        const int j = u0 + cu[i];
-        y[row * ldy + d * H + j] = out[i][0];
-        float* o = sv + (row * 2 + d) * 5 * H + j;
-#pragma unroll
-        for (int g = 0; g < 5; ++g) o[g * H] = out[i][1 + g];
-      }
     if (t + 1 < maxL) load_in(t + 1);
   }
 }
 
 template <int H>
-__global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
+__global__ __launch_bounds__(NTS) void lstm_coop_bwd_kernel(
     const float* __restrict__ dy, int lddy,    // [B*T][lddy], grad of outputs
     const bf16x8* __restrict__ wp,             // packed backward fragments
     const long long* __restrict__ lengths, int B, int T,
@@ -249,6 +273,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
   __shared__ __attribute__((aligned(16))) float part[4 * SB * PSB];
   __shared__ __attribute__((aligned(16))) __bf16 gs[SB * 64];  // [s][4 u + g]
   __shared__ int sL[SB];
+  __shared__ __attribute__((aligned(16))) float dg4[SB * 4 * UW];  // [s][g][u]
   const int d = blockIdx.y, w = blockIdx.x, u0 = w * UW;
   {  // this workgroup's sequence tile
     const int s0 = blockIdx.z * SB;
@@ -261,6 +286,39 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
   unsigned* hdr = tile_hdr(work, blockIdx.z);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < SB) sL[tid] = tid < B ? (int)lengths[tid] : 0;
+  __syncthreads();
+  int maxL = 0;
+  for (int s = 0; s < B; ++s) maxL = max(maxL, sL[s]);
+  for (int s = 0; s < B; ++s) {  // zero this workgroup's gate-gradient columns past the end
+    const int L = sL[s];
+    for (int i = tid; i < (T - L) * 64; i += NTS) {
+      const int c = i % 64;
+      dg[((long long)s * T + L + i / 64) * lddg + d * G4 + (c / 16) * H + u0 + c % 16] = 0.f;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.z, blockIdx.z, G::BX);
+
+  if (wv == 4) {
+    // ---------------------------------------------------------------- the service wave
+    for (int q = 0; q < maxL; ++q) {
+      if (q > 0) wait_count(hdr, d, (unsigned)(NW * q), c);
+      lds_barrier();  // (1)
+      lds_barrier();  // (2) dG staged
+      lds_barrier();  // (3) dG published
+      // 32 sequences x 4 gates x 16 units, 16 B per store
+#pragma unroll
+      for (int k4 = 0; k4 < SB * 4 * UW / 4 / 64; ++k4) {
+        const int gi = lane + 64 * k4, sq = gi / UW, g = (gi / (UW / 4)) % 4, c4 = (gi % (UW / 4)) * 4;
+        const f32x4 v = *(const f32x4*)&dg4[(sq * 4 + g) * UW + c4];
+        const int L = sq < B ? sL[sq] : 0;
+        if (q < L) {
+          const long long row = (long long)sq * T + (d ? q : L - 1 - q);
+          *(f32x4*)(dg + row * lddg + d * G4 + g * H + u0 + c4) = v;
+        }
+      }
+    }
+    return;
+  }
 
   bf16x8 wb[KCBW];
   {
@@ -268,17 +326,6 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
 #pragma unroll
     for (int kk = 0; kk < KCBW; ++kk) wb[kk] = src[kk * 64];
   }
-  __syncthreads();
-  int maxL = 0;
-  for (int s = 0; s < B; ++s) maxL = max(maxL, sL[s]);
-  for (int s = 0; s < B; ++s) {  // zero this workgroup's gate-gradient columns past the end
-    const int L = sL[s];
-    for (int i = tid; i < (T - L) * 64; i += NT) {
-      const int c = i % 64;
-      dg[((long long)s * T + L + i / 64) * lddg + d * G4 + (c / 16) * H + u0 + c % 16] = 0.f;
-    }
-  }
-  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.z, blockIdx.z, G::BX);
 
   int cs[2], cu[2];
 #pragma unroll
@@ -338,8 +385,6 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
     for (int nt = 0; nt < 2; ++nt)
       *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * PSB + 4 * (lane >> 4)] = acc[nt];
     lds_barrier();
-    float o[2][4];
-    bool val[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int s = cs[i], u = cu[i];
@@ -350,15 +395,19 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
       const float dh = in[i][6] + dhr;
       const float tc = tanh_fast(in[i][4]);
       const float dcc = dcs[i] + dh * og * (1.f - tc * tc);
-      o[i][0] = dcc * gg * ig * (1.f - ig);
-      o[i][1] = dcc * in[i][5] * fg * (1.f - fg);
-      o[i][2] = dcc * ig * (1.f - gg * gg);
-      o[i][3] = dh * tc * og * (1.f - og);
+      float o[4];
+      o[0] = dcc * gg * ig * (1.f - ig);
+      o[1] = dcc * in[i][5] * fg * (1.f - fg);
+      o[2] = dcc * ig * (1.f - gg * gg);
+      o[3] = dh * tc * og * (1.f - og);
       dcs[i] = dcc * fg;
-      val[i] = q < sL[s];
+      const bool val = q < sL[s];
       bf16x4_ nb;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) nb[g] = (__bf16)(val[i] ? o[i][g] : 0.f);
+      for (int g = 0; g < 4; ++g) {
+        nb[g] = (__bf16)(val ? o[g] : 0.f);
+        dg4[(s * 4 + g) * UW + u] = o[g];
+      }
       *(bf16x4_*)&gs[s * 64 + 4 * u] = nb;
     }
     lds_barrier();
@@ -370,13 +419,6 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
       lds_barrier();
       if (tid == 0) signal(hdr, d, q, c);
     }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (val[i]) {
-        float* dst = dg + grow[i] * lddg + d * G4 + u0 + cu[i];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) dst[g * H] = o[i][g];
-      }
     if (q + 1 < maxL) load_in(q + 1);
   }
 }
@@ -395,7 +437,7 @@ template <int H>
 int launch_fwd(const float* gx, int ldg, const void* wp, const long long* lengths, int B, int T,
                float* y, int ldy, float* sv, unsigned* work, hipStream_t st) {
   using G = CGeo<H>;
-  const size_t st_lds = sizeof(float) * 4 * SB * PSF + 2 * SB * UW + 4 * SB;
+  const size_t st_lds = sizeof(float) * (4 * SB * PSF + SB * 6 * UW) + 2 * SB * UW + 4 * SB;
   static const bool attr = set_max_lds((const void*)lstm_coop_fwd_kernel<H>, st_lds);
   if (!attr) return ENSVS_E_HIP;
   const Ctl ctl = host_ctl();
@@ -404,7 +446,7 @@ int launch_fwd(const float* gx, int ldg, const void* wp, const long long* length
     const long long b0 = (long long)t0 * SB;
     unsigned* wk = (unsigned*)((char*)work + (t0 / MAX_TILES) * wave_bytes<H>());
     if (hipMemsetAsync(wk, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(lstm_coop_fwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds), st,
+    hipLaunchKernelGGL(lstm_coop_fwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NTS), dyn_lds(st_lds), st,
                        gx + b0 * T * ldg, ldg, (const f16x8*)wp, lengths + b0, (int)(B - b0), T,
                        y + b0 * T * ldy, ldy, sv + b0 * T * 10 * H, wk, ctl);
     ENSVS_CHECK_LAUNCH();
@@ -416,7 +458,7 @@ template <int H>
 int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengths, int B, int T,
                const float* sv, float* dg, int lddg, unsigned* work, hipStream_t st) {
   using G = CGeo<H>;
-  const size_t st_lds = sizeof(float) * 4 * SB * PSB + 2 * SB * 64 + 4 * SB;
+  const size_t st_lds = sizeof(float) * (4 * SB * PSB + SB * 4 * UW) + 2 * SB * 64 + 4 * SB;
   static const bool attr = set_max_lds((const void*)lstm_coop_bwd_kernel<H>, st_lds);
   if (!attr) return ENSVS_E_HIP;
   const Ctl ctl = host_ctl();
@@ -425,7 +467,7 @@ int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengt
     const long long b0 = (long long)t0 * SB;
     unsigned* wk = (unsigned*)((char*)work + (t0 / MAX_TILES) * wave_bytes<H>());
     if (hipMemsetAsync(wk, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(lstm_coop_bwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds), st,
+    hipLaunchKernelGGL(lstm_coop_bwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NTS), dyn_lds(st_lds), st,
                        dy + b0 * T * lddy, lddy, (const bf16x8*)wp, lengths + b0, (int)(B - b0), T,
                        sv + b0 * T * 10 * H, dg + b0 * T * lddg, lddg, wk, ctl);
     ENSVS_CHECK_LAUNCH();
@@ -535,6 +577,7 @@ ENSVS_API int ensvs_lstm_coop_fwd(const float* gx, int ldg, const void* wpack,
                                   float* saved, void* work, long long work_bytes, void* stream) {
   if (!coop_shape(B, H) || T <= 0 || ldg < 8 * H || ldy < 2 * H) return ENSVS_E_SHAPE;
   if (check_work(work, work_bytes, H, B) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
+  if ((uintptr_t)y % 16 || ldy % 4 || (uintptr_t)saved % 16) return ENSVS_E_ARG;  // 16-B stores
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;
   return H == 256 ? launch_fwd<256>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st)
@@ -547,6 +590,7 @@ ENSVS_API int ensvs_lstm_coop_bwd(const float* dy, int lddy, const void* wpack,
                                   long long work_bytes, void* stream) {
   if (!coop_shape(B, H) || T <= 0 || lddy < 2 * H || lddg < 8 * H) return ENSVS_E_SHAPE;
   if (check_work(work, work_bytes, H, B) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
+  if ((uintptr_t)dg % 16 || lddg % 4) return ENSVS_E_ARG;  // 16-B stores
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;
   return H == 256 ? launch_bwd<256>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st)

@@ -260,8 +260,12 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
   }
 }
 
+// The backward keeps its gate-gradient stores in the compute waves: with the service wave
+// (round 5) it measured slower, H = 256 4.39 -> 4.73 and H = 512 6.16 -> 6.57 us per step
+// (tools/lstm_coop_bench.py, profiles/r5_coop_service_wave.txt) -- its dG payload (32 KB per
+// wave per step at H = 512) shares SIMD 0 with the fifth wave.
 template <int H>
-__global__ __launch_bounds__(NTS) void lstm_coop_bwd_kernel(
+__global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
     const float* __restrict__ dy, int lddy,    // [B*T][lddy], grad of outputs
     const bf16x8* __restrict__ wp,             // packed backward fragments
     const long long* __restrict__ lengths, int B, int T,
@@ -273,7 +277,6 @@ __global__ __launch_bounds__(NTS) void lstm_coop_bwd_kernel(
   __shared__ __attribute__((aligned(16))) float part[4 * SB * PSB];
   __shared__ __attribute__((aligned(16))) __bf16 gs[SB * 64];  // [s][4 u + g]
   __shared__ int sL[SB];
-  __shared__ __attribute__((aligned(16))) float dg4[SB * 4 * UW];  // [s][g][u]
   const int d = blockIdx.y, w = blockIdx.x, u0 = w * UW;
   {  // this workgroup's sequence tile
     const int s0 = blockIdx.z * SB;
@@ -286,39 +289,6 @@ __global__ __launch_bounds__(NTS) void lstm_coop_bwd_kernel(
   unsigned* hdr = tile_hdr(work, blockIdx.z);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < SB) sL[tid] = tid < B ? (int)lengths[tid] : 0;
-  __syncthreads();
-  int maxL = 0;
-  for (int s = 0; s < B; ++s) maxL = max(maxL, sL[s]);
-  for (int s = 0; s < B; ++s) {  // zero this workgroup's gate-gradient columns past the end
-    const int L = sL[s];
-    for (int i = tid; i < (T - L) * 64; i += NTS) {
-      const int c = i % 64;
-      dg[((long long)s * T + L + i / 64) * lddg + d * G4 + (c / 16) * H + u0 + c % 16] = 0.f;
-    }
-  }
-  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.z, blockIdx.z, G::BX);
-
-  if (wv == 4) {
-    // ---------------------------------------------------------------- the service wave
-    for (int q = 0; q < maxL; ++q) {
-      if (q > 0) wait_count(hdr, d, (unsigned)(NW * q), c);
-      lds_barrier();  // (1)
-      lds_barrier();  // (2) dG staged
-      lds_barrier();  // (3) dG published
-      // 32 sequences x 4 gates x 16 units, 16 B per store
-#pragma unroll
-      for (int k4 = 0; k4 < SB * 4 * UW / 4 / 64; ++k4) {
-        const int gi = lane + 64 * k4, sq = gi / UW, g = (gi / (UW / 4)) % 4, c4 = (gi % (UW / 4)) * 4;
-        const f32x4 v = *(const f32x4*)&dg4[(sq * 4 + g) * UW + c4];
-        const int L = sq < B ? sL[sq] : 0;
-        if (q < L) {
-          const long long row = (long long)sq * T + (d ? q : L - 1 - q);
-          *(f32x4*)(dg + row * lddg + d * G4 + g * H + u0 + c4) = v;
-        }
-      }
-    }
-    return;
-  }
 
   bf16x8 wb[KCBW];
   {
@@ -326,6 +296,17 @@ __global__ __launch_bounds__(NTS) void lstm_coop_bwd_kernel(
 #pragma unroll
     for (int kk = 0; kk < KCBW; ++kk) wb[kk] = src[kk * 64];
   }
+  __syncthreads();
+  int maxL = 0;
+  for (int s = 0; s < B; ++s) maxL = max(maxL, sL[s]);
+  for (int s = 0; s < B; ++s) {  // zero this workgroup's gate-gradient columns past the end
+    const int L = sL[s];
+    for (int i = tid; i < (T - L) * 64; i += NT) {
+      const int c = i % 64;
+      dg[((long long)s * T + L + i / 64) * lddg + d * G4 + (c / 16) * H + u0 + c % 16] = 0.f;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.z, blockIdx.z, G::BX);
 
   int cs[2], cu[2];
 #pragma unroll
@@ -385,6 +366,8 @@ __global__ __launch_bounds__(NTS) void lstm_coop_bwd_kernel(
     for (int nt = 0; nt < 2; ++nt)
       *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * PSB + 4 * (lane >> 4)] = acc[nt];
     lds_barrier();
+    float o[2][4];
+    bool val[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int s = cs[i], u = cu[i];
@@ -395,19 +378,15 @@ __global__ __launch_bounds__(NTS) void lstm_coop_bwd_kernel(
       const float dh = in[i][6] + dhr;
       const float tc = tanh_fast(in[i][4]);
       const float dcc = dcs[i] + dh * og * (1.f - tc * tc);
-      float o[4];
-      o[0] = dcc * gg * ig * (1.f - ig);
-      o[1] = dcc * in[i][5] * fg * (1.f - fg);
-      o[2] = dcc * ig * (1.f - gg * gg);
-      o[3] = dh * tc * og * (1.f - og);
+      o[i][0] = dcc * gg * ig * (1.f - ig);
+      o[i][1] = dcc * in[i][5] * fg * (1.f - fg);
+      o[i][2] = dcc * ig * (1.f - gg * gg);
+      o[i][3] = dh * tc * og * (1.f - og);
       dcs[i] = dcc * fg;
-      const bool val = q < sL[s];
+      val[i] = q < sL[s];
       bf16x4_ nb;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        nb[g] = (__bf16)(val ? o[g] : 0.f);
-        dg4[(s * 4 + g) * UW + u] = o[g];
-      }
+      for (int g = 0; g < 4; ++g) nb[g] = (__bf16)(val[i] ? o[i][g] : 0.f);
       *(bf16x4_*)&gs[s * 64 + 4 * u] = nb;
     }
     lds_barrier();
@@ -419,6 +398,13 @@ __global__ __launch_bounds__(NTS) void lstm_coop_bwd_kernel(
       lds_barrier();
       if (tid == 0) signal(hdr, d, q, c);
     }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (val[i]) {
+        float* dst = dg + grow[i] * lddg + d * G4 + u0 + cu[i];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dst[g * H] = o[i][g];
+      }
     if (q + 1 < maxL) load_in(q + 1);
   }
 }
@@ -458,7 +444,7 @@ template <int H>
 int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengths, int B, int T,
                const float* sv, float* dg, int lddg, unsigned* work, hipStream_t st) {
   using G = CGeo<H>;
-  const size_t st_lds = sizeof(float) * (4 * SB * PSB + SB * 4 * UW) + 2 * SB * 64 + 4 * SB;
+  const size_t st_lds = sizeof(float) * 4 * SB * PSB + 2 * SB * 64 + 4 * SB;
   static const bool attr = set_max_lds((const void*)lstm_coop_bwd_kernel<H>, st_lds);
   if (!attr) return ENSVS_E_HIP;
   const Ctl ctl = host_ctl();
@@ -467,7 +453,7 @@ int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengt
     const long long b0 = (long long)t0 * SB;
     unsigned* wk = (unsigned*)((char*)work + (t0 / MAX_TILES) * wave_bytes<H>());
     if (hipMemsetAsync(wk, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(lstm_coop_bwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NTS), dyn_lds(st_lds), st,
+    hipLaunchKernelGGL(lstm_coop_bwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds), st,
                        dy + b0 * T * lddy, lddy, (const bf16x8*)wp, lengths + b0, (int)(B - b0), T,
                        sv + b0 * T * 10 * H, dg + b0 * T * lddg, lddg, wk, ctl);
     ENSVS_CHECK_LAUNCH();
@@ -590,7 +576,6 @@ ENSVS_API int ensvs_lstm_coop_bwd(const float* dy, int lddy, const void* wpack,
                                   long long work_bytes, void* stream) {
   if (!coop_shape(B, H) || T <= 0 || lddy < 2 * H || lddg < 8 * H) return ENSVS_E_SHAPE;
   if (check_work(work, work_bytes, H, B) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
-  if ((uintptr_t)dg % 16 || lddg % 4) return ENSVS_E_ARG;  // 16-B stores
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;
   return H == 256 ? launch_bwd<256>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st)

@@ -254,28 +254,18 @@ __global__ __launch_bounds__(NTW) void lstm_mfma_fwd_kernel(
   }
 
   // -------------------------------------------------------------------- the compute waves
-  // H = 128 ("own chunk first"): K chunk kk of the product is h's units [32 kk, 32 kk + 32) --
-  // exactly wave kk's units -- so wave v multiplies its own chunk right after writing its h,
-  // before the step barrier, and only the other three chunks after it.  The fragments are
-  // held rotated (slot j = chunk (v + j) % NKC: static register indices); the accumulation
-  // order is own chunk, then the others in rotation order.
-  constexpr bool OWN = NKC == 4 && H / 4 == 32;
   f16x8 wf[NMT][NKC];
   {
     const f16x8* src = wp + ((long long)(dir * 4 + v) * NMT * NKC) * 64 + lane;
 #pragma unroll
     for (int mt = 0; mt < NMT; ++mt)
 #pragma unroll
-      for (int kk = 0; kk < NKC; ++kk)
-        wf[mt][kk] = src[(mt * NKC + (OWN ? (v + kk) % NKC : kk)) * 64];
+      for (int kk = 0; kk < NKC; ++kk) wf[mt][kk] = src[(mt * NKC + kk) * 64];
 #pragma unroll
     for (int mt = 0; mt < NMT; ++mt)
 #pragma unroll
       for (int kk = 0; kk < NKC; ++kk) asm volatile("" ::"v"(wf[mt][kk]));
   }
-  f32x4 own[NMT];  // the own chunk's product for the next step (h_{-1} = 0: zero)
-#pragma unroll
-  for (int mt = 0; mt < NMT; ++mt) own[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   // lane (lg, n) takes unit 16 ug + n of its wave, ug = lg / 2 for two unit groups (H = 128);
   // the row groups with the same unit hold copies and do not write
   constexpr int NUG = H / 64;
@@ -296,27 +286,15 @@ __global__ __launch_bounds__(NTW) void lstm_mfma_fwd_kernel(
       for (int g = 0; g < 4; ++g) gv[g] = gc[st * GW + g * H + u];
       const _Float16* hc = hb + ((s + 1) & 1) * HP + 8 * lg;
       f16x8 bf[NKC];
+#pragma unroll
+      for (int kk = 0; kk < NKC; ++kk) bf[kk] = *(const f16x8*)(hc + 32 * kk);
       f32x4 acc[NMT];
-      if constexpr (OWN) {
 #pragma unroll
-        for (int kk = 1; kk < NKC; ++kk) bf[kk] = *(const f16x8*)(hc + 32 * ((v + kk) % NKC));
+      for (int mt = 0; mt < NMT; ++mt) {
+        acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int mt = 0; mt < NMT; ++mt) {
-          acc[mt] = own[mt];
-#pragma unroll
-          for (int kk = 1; kk < NKC; ++kk)
-            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kk], wf[mt][kk], acc[mt], 0, 0, 0);
-        }
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < NKC; ++kk) bf[kk] = *(const f16x8*)(hc + 32 * kk);
-#pragma unroll
-        for (int mt = 0; mt < NMT; ++mt) {
-          acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int kk = 0; kk < NKC; ++kk)
-            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kk], wf[mt][kk], acc[mt], 0, 0, 0);
-        }
+        for (int kk = 0; kk < NKC; ++kk)
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kk], wf[mt][kk], acc[mt], 0, 0, 0);
       }
       float a[4];
 #pragma unroll
@@ -338,15 +316,6 @@ __global__ __launch_bounds__(NTW) void lstm_mfma_fwd_kernel(
         o[3 * H + u] = gg;
         o[4 * H + u] = og;
         o[5 * H + u] = c;
-      }
-      if constexpr (OWN) {
-        // this wave's h chunk (just written by its own lanes: LDS keeps a wave's order) times
-        // its W_hh columns, for the next step, while the other waves finish theirs
-        asm volatile("" ::: "memory");
-        const f16x8 bo = *(const f16x8*)(hb + (s & 1) * HP + 8 * lg + 32 * v);
-#pragma unroll
-        for (int mt = 0; mt < NMT; ++mt)
-          own[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bo, wf[mt][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       }
       __syncthreads();
     }
@@ -470,18 +439,13 @@ __global__ __launch_bounds__(NTW) void lstm_mfma_bwd_kernel(
   }
 
   // -------------------------------------------------------------------- the compute waves
-  // H = 128, as the forward: K chunks 4 v .. 4 v + 3 of dh = W_hh^T dG (exchange order
-  // n' = 4 unit + gate) are this wave's own units' dG, multiplied right after it writes them
-  constexpr int OWNK = NKB / 4;  // chunks per wave's units
-  constexpr bool OWN = TPW == 2;
   bf16x8 wb[TPW][NKB];
   {
     const bf16x8* src = wp + ((long long)(dir * 4 + v) * TPW * NKB) * 64 + lane;
 #pragma unroll
     for (int mt = 0; mt < TPW; ++mt)
 #pragma unroll
-      for (int kk = 0; kk < NKB; ++kk)
-        wb[mt][kk] = src[(mt * NKB + (OWN ? (OWNK * v + kk) % NKB : kk)) * 64];
+      for (int kk = 0; kk < NKB; ++kk) wb[mt][kk] = src[(mt * NKB + kk) * 64];
 #pragma unroll
     for (int mt = 0; mt < TPW; ++mt)
 #pragma unroll
@@ -495,9 +459,6 @@ __global__ __launch_bounds__(NTW) void lstm_mfma_bwd_kernel(
   const int u = v * G::UPW + 16 * tb + n;
   float dc = 0.f;
   float ds[4] = {0.f, 0.f, 0.f, 0.f};  // this cell's dg summed over its steps (bias gradient)
-  f32x4 own[TPW];
-#pragma unroll
-  for (int mt = 0; mt < TPW; ++mt) own[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
   for (int ch = 0; ch < nch; ++ch) {
     const int cnt = min(CH, L - ch * CH);
@@ -516,22 +477,20 @@ __global__ __launch_bounds__(NTW) void lstm_mfma_bwd_kernel(
 #pragma unroll
       for (int g = 0; g < 7; ++g) asm volatile("" : "+v"(iv[g]));
       const __bf16* gcur = gb + ((p + 1) & 1) * GP + 8 * lg;
-      constexpr int K0 = OWN ? OWNK : 0;  // chunks already multiplied before the last barrier
       bf16x8 bf[NKB];
 #pragma unroll
-      for (int kk = K0; kk < NKB; ++kk)
-        bf[kk] = *(const bf16x8*)(gcur + 32 * (OWN ? (OWNK * v + kk) % NKB : kk));
+      for (int kk = 0; kk < NKB; ++kk) bf[kk] = *(const bf16x8*)(gcur + 32 * kk);
       // every dG read in flight before the first MFMA (with the I/O wave's two waves on one
       // SIMD the compiler otherwise reuses one register quad: a read and its full LDS latency
       // per MFMA pair, H = 128 645 -> 753 ns per step)
 #pragma unroll
-      for (int kk = K0; kk < NKB; ++kk) asm volatile("" : "+v"(bf[kk]));
+      for (int kk = 0; kk < NKB; ++kk) asm volatile("" : "+v"(bf[kk]));
       f32x4 acc[TPW];
 #pragma unroll
       for (int mt = 0; mt < TPW; ++mt) {
-        acc[mt] = OWN ? own[mt] : f32x4{0.f, 0.f, 0.f, 0.f};
+        acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kk = K0; kk < NKB; ++kk)
+        for (int kk = 0; kk < NKB; ++kk)
           acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[kk], wb[mt][kk], acc[mt], 0, 0, 0);
       }
       const float dhr = TPW == 2 ? bsel(mtb, acc[0][0], acc[TPW - 1][0]) : acc[0][0];
@@ -561,20 +520,6 @@ __global__ __launch_bounds__(NTW) void lstm_mfma_bwd_kernel(
         o[H + u] = d_f;
         o[2 * H + u] = d_g;
         o[3 * H + u] = d_o;
-      }
-      if constexpr (OWN) {
-        asm volatile("" ::: "memory");
-        const __bf16* gown = gb + (p & 1) * GP + 8 * lg + 32 * OWNK * v;
-        bf16x8 bo[OWNK];
-#pragma unroll
-        for (int j = 0; j < OWNK; ++j) bo[j] = *(const bf16x8*)(gown + 32 * j);
-#pragma unroll
-        for (int mt = 0; mt < TPW; ++mt) {
-          own[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int j = 0; j < OWNK; ++j)
-            own[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bo[j], wb[mt][j], own[mt], 0, 0, 0);
-        }
       }
       __syncthreads();
     }

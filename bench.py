@@ -843,6 +843,19 @@ def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
             train_epoch(model, opt, feeder)
         torch.cuda.synchronize()
         el_eager = (time.time() - t0) / epochs
+        # the same shapes at fixed-shape speed: each bucket's captured step replayed back to
+        # back on its static batch (real updates), weighted by its batches per epoch -- what an
+        # epoch costs with no loop at all around the steps (feeder, copies, cache lookup)
+        fixed = 0.0
+        reps = 3
+        for key, g in graphs.graphs.items():
+            g.step()
+            torch.cuda.synchronize()
+            t0 = time.time()
+            for _ in range(reps):
+                g.step()
+            torch.cuda.synchronize()
+            fixed += (time.time() - t0) / reps * graphs.uses[key] / (1 + epochs)
         n_graphs, reserved = len(graphs.graphs), torch.cuda.memory_reserved(dev)
         del graphs
     sizes = [len(b) for b in batches]
@@ -858,6 +871,8 @@ def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
                 first_epoch_s=el_first, captured_signatures=n_graphs,
                 memory_reserved_gb=reserved / 1e9,
                 eager_value=valid / el_eager, eager_s_per_epoch=el_eager,
+                same_shapes_back_to_back_s_per_epoch=fixed,
+                ratio_to_same_shapes_back_to_back=fixed / el,
                 last_loss=float(res[-1][0].item()), dtype=engine.gemm_precision())
 
 

@@ -599,11 +599,10 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
       cst[i] = cn;
       const bool val = s < B;
       hs[s * UW + u] = (_Float16)(val ? h : 0.f);
+      f32x4 ov;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = sum16(woc[i][r] * (val ? h : 0.f));
-        if (u == 0) ops[s * 4 + r] = v;
-      }
+      for (int r = 0; r < 4; ++r) ov[r] = sum16(woc[i][r] * (val ? h : 0.f));
+      if (u == 0) *(f32x4*)&ops[s * 4] = ov;
       float* o6 = sv6 + s * 6 * UW + u;
       o6[0] = ig;
       o6[UW] = fg;
@@ -671,21 +670,40 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
     const int rsq = min(lane, B - 1);
     const bool red = lane < SB;
     const bool rw = red && lane < B && w == 0;
-    float rgl[4], rgr[4], rso[4], rmask = 0.f;
+    // Step inputs two steps ahead (steps run t = Tr-1 .. 0): at the end of step t, behind its
+    // dG stores, the inputs of step t-1 -- loaded (n*) at the end of step t+1 -- are taken,
+    // with 1 - tanh^2 of the saved o (c1), and the loads of step t-2 are issued.  That load has
+    // landed by then, and the wait for it (vmcnt counts loads and stores in issue order) does
+    // not cover the stores.  tanhf after the hand-off wait lengthened every step; formed right
+    // after a load issued behind the stores, it stalled the service wave until they drained.
+    float ngl[4], ngr[4], nso[4], nmask = 0.f;
+    float rgl[4], rgr[4], c1[4], rmask = 0.f;
     auto load_red = [&](int t) {  // output grads / saved o of step t, mask of step t + 1
       if (red) {
         const long long row = (long long)rsq * Tr + t;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const long long f = (long long)rsq * T + 4 * t + r;
-          rgl[r] = glf0[f];
-          rgr[r] = gres ? gres[f] : 0.f;
-          rso[r] = so[row * 4 + r];
+          ngl[r] = glf0[f];
+          ngr[r] = gres ? gres[f] : 0.f;
+          nso[r] = so[row * 4 + r];
         }
-        rmask = t + 1 < Tr ? mask[row + 1] : 0.f;
+        nmask = t + 1 < Tr ? mask[row + 1] : 0.f;
       }
     };
+    auto take = [&]() {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        rgl[r] = ngl[r];
+        rgr[r] = ngr[r];
+        const float th = tanhf(nso[r]);
+        c1[r] = 1.f - th * th;
+      }
+      rmask = nmask;
+    };
     load_red(Tr - 1);
+    take();
+    if (Tr > 1) load_red(Tr - 2);
     for (int q = 0; q < Tr; ++q) {
       const int t = Tr - 1 - q;
       float dprev = 0.f;
@@ -708,13 +726,9 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
       if (red) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          // (tanhf of the saved o here, after the hand-off wait: computed right after its load,
-          // before the wait, it stalled the service wave into the next step's barrier: 4.40 ->
-          // 4.65 us per AR step)
           const float dl = rgl[r] + (r == 3 ? dprev : 0.f);
           const float dr = rgr[r] + dl / k.scale;
-          const float th = tanhf(rso[r]);
-          d4[r] = dr * MAX_LF0_RATIO * (1.f - th * th);
+          d4[r] = dr * MAX_LF0_RATIO * c1[r];
           d4s[lane * 4 + r] = d4[r];
         }
         if (rw) *(f32x4*)(do4 + ((long long)rsq * Tr + t) * 4) = f32x4{d4[0], d4[1], d4[2], d4[3]};
@@ -729,7 +743,10 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
         const f32x4 v = *(const f32x4*)&dg4[(sq * 4 + g) * UW + c4];
         if (sq < B) *(f32x4*)(dg + ((long long)sq * Tr + t) * 4 * H + g * H + u0 + c4) = v;
       }
-      if (t > 0) load_red(t - 1);
+      if (t > 0) {
+        take();
+        if (t > 1) load_red(t - 2);
+      }
     }
     return;
   }

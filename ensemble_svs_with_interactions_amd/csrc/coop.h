@@ -124,12 +124,24 @@ __device__ __forceinline__ void st4(__amdgpu_buffer_rsrc_t r, int off, float v) 
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, CP_SC1);
 }
 
-// sum over the 16 lanes of a unit group (lanes 16 j .. 16 j + 15), every lane gets the sum
+// lane i reads lane perm(i) of its DPP row (ctrl: quad_perm 0x00-0xFF, row_mirror 0x140,
+// row_half_mirror 0x141); every lane of every row is enabled
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+// sum over the 16 lanes of a unit group (lanes 16 j .. 16 j + 15), every lane gets the sum.
+// Four DPP adds within the row: xor 1, xor 2 (quad_perm), then the half-row and row mirrors,
+// which pair each lane with a lane of the other quad / other half as xor 4 / xor 8 would
+// (the same operand pairs, so the bits of the xor butterfly).  __shfl_xor compiles to
+// ds_bpermute_b32, an LDS round trip per level: 32 dependent ones per AR forward step.
 __device__ __forceinline__ float sum16(float v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 8);
+  v += dpp<0xB1>(v);   // quad_perm(1, 0, 3, 2)
+  v += dpp<0x4E>(v);   // quad_perm(2, 3, 0, 1)
+  v += dpp<0x141>(v);  // row_half_mirror: lane 7 - i of the 8
+  v += dpp<0x140>(v);  // row_mirror: lane 15 - i of the 16
   return v;
 }
 

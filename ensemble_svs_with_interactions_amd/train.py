@@ -681,6 +681,7 @@ class StepGraphCache:
         self.logf0_diff_weight = float(logf0_diff_weight)
         self.max_graphs = int(max_graphs)
         self.graphs = OrderedDict()
+        self.uses = {}  # steps run per signature (capture included)
         self.pool = None
         self.captures = self.replays = 0
 
@@ -694,6 +695,7 @@ class StepGraphCache:
     def step(self, x_main, x_sub, y_main, spk_main, spk_sub, lengths, y_sub=None, draws=None):
         """One training step on this batch; returns (loss, grad_norm) as fresh device tensors."""
         key = self.signature(x_main, x_sub, y_main, spk_main, spk_sub, lengths, y_sub, draws)
+        self.uses[key] = self.uses.get(key, 0) + 1
         g = self.graphs.get(key)
         if g is None:
             while len(self.graphs) >= self.max_graphs:

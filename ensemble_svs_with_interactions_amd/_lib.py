@@ -101,6 +101,10 @@ SIGNATURES = {
                             c_int, c_vp, c_vp],
     "ensvs_lstm_coop_supported": [c_int, c_int],
     "ensvs_lstm_coop_work_bytes": [c_int, c_int],
+    "ensvs_lstm_coop_tile_seqs": [c_int, c_int],
+    "ensvs_lstm_coop_set_tile_seqs": [c_int],
+    "ensvs_ardec_coop_tile_seqs": [c_int, c_int],
+    "ensvs_ardec_coop_set_tile_seqs": [c_int],
     "ensvs_lstm_coop_pack": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
     "ensvs_lstm_coop_fwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
                             c_ll, c_vp],

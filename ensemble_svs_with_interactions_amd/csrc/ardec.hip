@@ -352,7 +352,7 @@ int bwd_launch(const float* glf0, const float* gres, const float* wpb, const flo
 
 
 // ------------------------------------------------------------------ cooperative decoder
-// Production (bf16 GEMM) precision at H in {128, 256}, B <= 32: the per-sequence kernels above
+// Production (bf16 GEMM) precision at H in {128, 256}, any B: the per-sequence kernels above
 // stream the 1 MB fp32 W_hh from L2 every step (8.7 us per step at H = 256).  All sequences
 // step in lockstep on the same W_hh, so here the recurrence is one MFMA product per step,
 // W_hh . [h_1 .. h_B] (N = the sequences), split over NW = H/16 workgroups that keep their 64
@@ -366,14 +366,18 @@ int bwd_launch(const float* glf0, const float* gres, const float* wpb, const flo
 // Gates, cell state and every saved value stay fp32 (the recurrent products in fp16 / bf16 as
 // the recipe's fp16 autocast runs the LSTMCell, myconfig_notuseIL.yaml:6); the fp32 parity
 // mode keeps the exact kernels above.
-template <int H> struct ArGeo {
+// S = sequences per tile: 32 (two MFMA N tiles, two cells per compute thread) or 16 (one N
+// tile, one cell per thread: half the slab bytes every workgroup reads per step, at twice the
+// workgroups); ar_tile_seqs() picks it per batch.
+template <int H, int S> struct ArGeo {
   static constexpr int NW = H / coop::UW, KCW = H / 128, KCBW = H / 32;
-  static constexpr int FH = coop::SB * H * 2;      // forward slab per buffer: h [s][H] fp16
-  static constexpr int FBUF = FH + coop::SB * NW * 16;  // + feat_out partials [w][s][4] fp32
-  static constexpr int BG = coop::SB * 4 * H * 2;  // backward per buffer: dG [s][4H] bf16
-  static constexpr int BBUF = BG + coop::SB * NW * 4;   // + prenet partials [s][w] fp32
+  static constexpr int NTN = S / 16, NC = S * coop::UW / coop::NT;
+  static constexpr int FH = S * H * 2;           // forward slab per buffer: h [s][H] fp16
+  static constexpr int FBUF = FH + S * NW * 16;  // + feat_out partials [w][s][4] fp32
+  static constexpr int BG = S * 4 * H * 2;       // backward per buffer: dG [s][4H] bf16
+  static constexpr int BBUF = BG + S * NW * 4;   // + prenet partials [s][w] fp32
   static constexpr int SLAB = 2 * (FBUF > BBUF ? FBUF : BBUF);  // one tile's double buffer
-  static_assert(H % 128 == 0 && NW % 4 == 0, "H");
+  static_assert(H % 128 == 0 && NW % 4 == 0 && (S == 16 || S == 32), "H, S");
 };
 
 constexpr int AR_PSF = 68;  // forward partial-sum row per sequence: 64 gate rows + 4 (banks)
@@ -390,7 +394,7 @@ constexpr int AR_PSB = 20;  // backward: 16 units + 4
 // without the reduction).
 constexpr int AR_NTS = coop::NT + 64;
 
-template <int H>
+template <int H, int S>
 __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
     const float* __restrict__ gx, int ldgx, const float* __restrict__ ofx, int ldo,
     const f16x8* __restrict__ wp, const float* __restrict__ wih_p,
@@ -400,20 +404,20 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
     float* __restrict__ sc, float* __restrict__ sh, float* __restrict__ so,
     float* __restrict__ sp, unsigned* __restrict__ work, coop::Ctl c) {
   using namespace coop;
-  using G = ArGeo<H>;
-  constexpr int KCW = G::KCW, NW = G::NW;
-  __shared__ __attribute__((aligned(16))) float part[4 * SB * AR_PSF];
-  __shared__ __attribute__((aligned(16))) _Float16 hs[SB * UW];
-  __shared__ __attribute__((aligned(16))) float ops[SB * 4];
-  __shared__ float pv[SB];
-  __shared__ __attribute__((aligned(16))) float sv6[SB * 6 * UW];  // [s][i f g o c h][u]
+  using G = ArGeo<H, S>;
+  constexpr int KCW = G::KCW, NW = G::NW, NTN = G::NTN, NC = G::NC;
+  __shared__ __attribute__((aligned(16))) float part[4 * S * AR_PSF];
+  __shared__ __attribute__((aligned(16))) _Float16 hs[S * UW];
+  __shared__ __attribute__((aligned(16))) float ops[S * 4];
+  __shared__ float pv[S];
+  __shared__ __attribute__((aligned(16))) float sv6[S * 6 * UW];  // [s][i f g o c h][u]
   const int w = blockIdx.x, u0 = w * UW;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const bool service = wv == 4;
   const int Tr = T / 4;
   {  // this workgroup's sequence tile (blockIdx.y): sequences [32 y, 32 y + 32)
-    const int s0 = blockIdx.y * SB;
-    B = min(SB, B - s0);
+    const int s0 = blockIdx.y * S;
+    B = min(S, B - s0);
     const long long r = (long long)s0 * Tr, f = (long long)s0 * T;
     gx += r * ldgx;
     ofx += r * ldo;
@@ -434,9 +438,9 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
 
   if (service) {
     // ---------------------------------------------------------------- the service wave
-    // reducer lane `lane` < SB owns sequence `lane`: the inputs of step t-1's outputs and p_t
+    // reducer lane `lane` < S owns sequence `lane`: the inputs of step t-1's outputs and p_t
     const int rsq = min(lane, B - 1);
-    const bool red = lane < SB;
+    const bool red = lane < S;
     const bool rw = red && lane < B && w == 0;  // writes the per-sequence outputs
     float rofx[4], rsd[4], rmask = 0.f, rteach = 0.f;
     auto load_red = [&](int t) {  // ofx / score of step t - 1, mask of step t
@@ -455,7 +459,7 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
     auto reduce_out = [&](int t, int base) -> float {
       f32x4 op[NW];
 #pragma unroll
-      for (int w2 = 0; w2 < NW; ++w2) op[w2] = ld16(xr, base + G::FH + (w2 * SB + lane) * 16);
+      for (int w2 = 0; w2 < NW; ++w2) op[w2] = ld16(xr, base + G::FH + (w2 * S + lane) * 16);
       float l3 = 0.f;
       const long long row = (long long)rsq * Tr + t - 1;
 #pragma unroll
@@ -496,7 +500,7 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
       lds_barrier();  // (2) step t's saved values in sv6
       // step t's saved values: 32 sequences x 6 rows of 16 units, 16 B per store
 #pragma unroll
-      for (int k4 = 0; k4 < SB * 6 * UW / 4 / 64; ++k4) {
+      for (int k4 = 0; k4 < S * 6 * UW / 4 / 64; ++k4) {
         const int gi = lane + 64 * k4, sq = gi / (6 * UW / 4), rem = gi % (6 * UW / 4);
         const int q = rem / (UW / 4), c4 = (rem % (UW / 4)) * 4;
         const f32x4 v = *(const f32x4*)&sv6[(sq * 6 + q) * UW + c4];
@@ -525,10 +529,10 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
       for (int kk = 0; kk < KCW; ++kk) wf[mt][kk] = src[(mt * KCW + kk) * 64];
   }
   // cells (unit u = p & 15, sequence s = p >> 4), p = tid + 256 i: 16 lanes per sequence
-  int cs[2], cu[2];
-  float wpc[2][4], woc[2][4];
+  int cs[NC], cu[NC];
+  float wpc[NC][4], woc[NC][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int p = tid + NT * i;
     cu[i] = p & 15;
     cs[i] = p >> 4;
@@ -537,10 +541,12 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) woc[i][r] = wfo[(long long)r * ldwfo + u0 + cu[i]];
   }
-  float gin[2][4], cst[2] = {0.f, 0.f};
+  float gin[NC][4], cst[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) cst[i] = 0.f;
   auto load_in = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NC; ++i) {
       const float* src = gx + ((long long)min(cs[i], B - 1) * Tr + t) * ldgx + u0 + cu[i];
 #pragma unroll
       for (int g = 0; g < 4; ++g) gin[i][g] = src[g * H];
@@ -549,45 +555,45 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
   load_in(0);
 
   for (int t = 0; t < Tr; ++t) {
-    f32x4 acc[4][2];
+    f32x4 acc[4][NTN];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int nt = 0; nt < NTN; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (t > 0) {
       wait_count(hdr, 0, (unsigned)(NW * t), c);
       const int base = ((t - 1) & 1) * G::FBUF;
-      f16x8 bf[KCW][2];
+      f16x8 bf[KCW][NTN];
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+        for (int nt = 0; nt < NTN; ++nt)
           bf[kk][nt] = __builtin_bit_cast(
               f16x8, ld16(xr, ((nt * 16 + (lane & 15)) * H + (wv * KCW + kk) * 32 + 8 * (lane >> 4)) * 2 + base));
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
+        for (int nt = 0; nt < NTN; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk)
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt)
+          for (int nt = 0; nt < NTN; ++nt)
             acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[mt][kk], bf[kk][nt], acc[mt][nt], 0, 0, 0);
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-        *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * AR_PSF + 16 * mt + 4 * (lane >> 4)] = acc[mt][nt];
+      for (int nt = 0; nt < NTN; ++nt)
+        *(f32x4*)&part[(wv * S + nt * 16 + (lane & 15)) * AR_PSF + 16 * mt + 4 * (lane >> 4)] = acc[mt][nt];
     lds_barrier();  // (1)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NC; ++i) {
       const int s = cs[i], u = cu[i];
       f32x4 a = *(const f32x4*)&part[s * AR_PSF + 4 * u];
 #pragma unroll
-      for (int q = 1; q < 4; ++q) a += *(const f32x4*)&part[(q * SB + s) * AR_PSF + 4 * u];
+      for (int q = 1; q < 4; ++q) a += *(const f32x4*)&part[(q * S + s) * AR_PSF + 4 * u];
       const float p = pv[s];
       float pre[4];
 #pragma unroll
@@ -614,9 +620,10 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
     lds_barrier();  // (2)
     if (wv == 0) {  // publish h_t (32 sequences x 16 units) and the feat_out partials
       const int base = (t & 1) * G::FBUF;
-      st16(xr, base + ((lane >> 1) * H + u0 + (lane & 1) * 8) * 2,
-           *(const f32x4*)&hs[(lane >> 1) * UW + (lane & 1) * 8]);
-      if (lane < SB) st16(xr, base + G::FH + (w * SB + lane) * 16, *(const f32x4*)&ops[lane * 4]);
+      if (lane < 2 * S)
+        st16(xr, base + ((lane >> 1) * H + u0 + (lane & 1) * 8) * 2,
+             *(const f32x4*)&hs[(lane >> 1) * UW + (lane & 1) * 8]);
+      if (lane < S) st16(xr, base + G::FH + (w * S + lane) * 16, *(const f32x4*)&ops[lane * 4]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(hdr, 0, t, c);
     }
@@ -630,7 +637,7 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_fwd_kernel(
 // per sequence) and writes the gate gradients dG_t (staged in LDS by the compute waves) and
 // d o_t with 16-B stores after the step's barriers; the compute waves run W_hh^T dG, the cell
 // backward and the dG hand-off, and issue no other global store.
-template <int H>
+template <int H, int S>
 __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
     const float* __restrict__ glf0, const float* __restrict__ gres,
     const bf16x8* __restrict__ wp, const float* __restrict__ wih_p,
@@ -639,19 +646,19 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
     const float* __restrict__ so, float* __restrict__ dg, float* __restrict__ do4,
     unsigned* __restrict__ work, coop::Ctl c) {
   using namespace coop;
-  using G = ArGeo<H>;
-  constexpr int KCBW = G::KCBW, NW = G::NW;
-  __shared__ __attribute__((aligned(16))) float part[4 * SB * AR_PSB];
-  __shared__ __attribute__((aligned(16))) __bf16 gs[SB * 64];  // [s][4 u + g]
-  __shared__ float d4s[SB * 4];
-  __shared__ float dps[SB];
-  __shared__ __attribute__((aligned(16))) float dg4[SB * 4 * UW];  // [s][g][u]
+  using G = ArGeo<H, S>;
+  constexpr int KCBW = G::KCBW, NW = G::NW, NTN = G::NTN, NC = G::NC;
+  __shared__ __attribute__((aligned(16))) float part[4 * S * AR_PSB];
+  __shared__ __attribute__((aligned(16))) __bf16 gs[S * 64];  // [s][4 u + g]
+  __shared__ float d4s[S * 4];
+  __shared__ float dps[S];
+  __shared__ __attribute__((aligned(16))) float dg4[S * 4 * UW];  // [s][g][u]
   const int w = blockIdx.x, u0 = w * UW;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int Tr = T / 4;
   {  // this workgroup's sequence tile (blockIdx.y)
-    const int s0 = blockIdx.y * SB;
-    B = min(SB, B - s0);
+    const int s0 = blockIdx.y * S;
+    B = min(S, B - s0);
     const long long r = (long long)s0 * Tr, f = (long long)s0 * T;
     glf0 += f;
     if (gres) gres += f;
@@ -668,7 +675,7 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
   if (wv == 4) {
     // ---------------------------------------------------------------- the service wave
     const int rsq = min(lane, B - 1);
-    const bool red = lane < SB;
+    const bool red = lane < S;
     const bool rw = red && lane < B && w == 0;
     // Step inputs two steps ahead (steps run t = Tr-1 .. 0): at the end of step t, behind its
     // dG stores, the inputs of step t-1 -- loaded (n*) at the end of step t+1 -- are taken,
@@ -738,7 +745,7 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
       lds_barrier();  // (3) dG_t published
       // dG_t: 32 sequences x 4 gates x 16 units, 16 B per store
 #pragma unroll
-      for (int k4 = 0; k4 < SB * 4 * UW / 4 / 64; ++k4) {
+      for (int k4 = 0; k4 < S * 4 * UW / 4 / 64; ++k4) {
         const int gi = lane + 64 * k4, sq = gi / UW, g = (gi / (UW / 4)) % 4, c4 = (gi % (UW / 4)) * 4;
         const f32x4 v = *(const f32x4*)&dg4[(sq * 4 + g) * UW + c4];
         if (sq < B) *(f32x4*)(dg + ((long long)sq * Tr + t) * 4 * H + g * H + u0 + c4) = v;
@@ -758,10 +765,10 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
 #pragma unroll
     for (int kk = 0; kk < KCBW; ++kk) wb[kk] = src[kk * 64];
   }
-  int cs[2], cu[2];
-  float wo[2][4], wpg[2][4];
+  int cs[NC], cu[NC];
+  float wo[NC][4], wpg[NC][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int p = tid + NT * i;
     cu[i] = p & 15;
     cs[i] = p >> 4;
@@ -770,10 +777,12 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
 #pragma unroll
     for (int g = 0; g < 4; ++g) wpg[i][g] = wih_p[g * H + u0 + cu[i]];
   }
-  float in[2][6], dcs[2] = {0.f, 0.f};
+  float in[NC][6], dcs[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) dcs[i] = 0.f;
   auto load_in = [&](int t) {  // saved i f g o, c_t, c_{t-1} of step t
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NC; ++i) {
       const long long row = (long long)min(cs[i], B - 1) * Tr + t;
       const int j = u0 + cu[i];
 #pragma unroll
@@ -786,37 +795,39 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
 
   for (int q = 0; q < Tr; ++q) {
     const int t = Tr - 1 - q;
-    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 acc[NTN];
+#pragma unroll
+    for (int nt = 0; nt < NTN; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (q > 0) {
       wait_count(hdr, 0, (unsigned)(NW * q), c);
       const int base = ((q - 1) & 1) * G::BBUF;
-      bf16x8 bf[KCBW][2];
+      bf16x8 bf[KCBW][NTN];
 #pragma unroll
       for (int kk = 0; kk < KCBW; ++kk)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+        for (int nt = 0; nt < NTN; ++nt)
           bf[kk][nt] = __builtin_bit_cast(
               bf16x8, ld16(xr, ((nt * 16 + (lane & 15)) * 4 * H + (wv * KCBW + kk) * 32 + 8 * (lane >> 4)) * 2 + base));
 #pragma unroll
       for (int kk = 0; kk < KCBW; ++kk)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
+        for (int nt = 0; nt < NTN; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
 #pragma unroll
       for (int kk = 0; kk < KCBW; ++kk)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+        for (int nt = 0; nt < NTN; ++nt)
           acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[kk], bf[kk][nt], acc[nt], 0, 0, 0);
     }
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-      *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * AR_PSB + 4 * (lane >> 4)] = acc[nt];
+    for (int nt = 0; nt < NTN; ++nt)
+      *(f32x4*)&part[(wv * S + nt * 16 + (lane & 15)) * AR_PSB + 4 * (lane >> 4)] = acc[nt];
     lds_barrier();  // (1)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NC; ++i) {
       const int s = cs[i], u = cu[i];
       float dh = part[s * AR_PSB + u];
 #pragma unroll
-      for (int kq = 1; kq < 4; ++kq) dh += part[(kq * SB + s) * AR_PSB + u];
+      for (int kq = 1; kq < 4; ++kq) dh += part[(kq * S + s) * AR_PSB + u];
 #pragma unroll
       for (int r = 0; r < 4; ++r) dh = fmaf(wo[i][r], d4s[s * 4 + r], dh);
       const float ig = in[i][0], fg = in[i][1], gg = in[i][2], og = in[i][3];
@@ -844,9 +855,10 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
     lds_barrier();  // (2)
     {  // publish dG_t (32 sequences x 64 values) and the prenet partials
       const int base = (q & 1) * G::BBUF;
-      st16(xr, base + ((tid >> 3) * 4 * H + w * 64 + (tid & 7) * 8) * 2,
-           *(const f32x4*)&gs[(tid >> 3) * 64 + (tid & 7) * 8]);
-      if (tid < SB) st4(xr, base + G::BG + (tid * NW + w) * 4, dps[tid]);
+      if (tid < 8 * S)
+        st16(xr, base + ((tid >> 3) * 4 * H + w * 64 + (tid & 7) * 8) * 2,
+             *(const f32x4*)&gs[(tid >> 3) * 64 + (tid & 7) * 8]);
+      if (tid < S) st4(xr, base + G::BG + (tid * NW + w) * 4, dps[tid]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();  // (3)
       if (tid == 0) signal(hdr, 0, q, c);
@@ -855,32 +867,45 @@ __global__ __launch_bounds__(AR_NTS) void ardec_coop_bwd_kernel(
   }
 }
 
-// any B: tiles of 32 sequences (coop.h) in waves of up to AR_MAX_TILES tiles per launch (at
-// H = 256 a wave is 16 x 8 workgroups); wave k owns its tiles' workspace region (headers, then
+// any B: tiles of S sequences in waves of up to AR_MAX_TILES tiles per launch (at H = 256 and
+// S = 32 a wave is 16 x 8 workgroups); wave k owns its tiles' workspace region (headers, then
 // slabs), as lstm_coop.hip's waves do
 constexpr int AR_MAX_TILES = 8;
 
-template <int H>
-long long ar_wave_bytes() { return (long long)AR_MAX_TILES * (coop::HDR + ArGeo<H>::SLAB); }
+// sequences per tile: 16 when that takes no more workgroups than tiles of 32 (B <= 16), else 32.
+// At the bench's 30 pairs x 1024 frames 16-sequence tiles run the AR step in 2.79 / 3.24 us
+// instead of 3.43 / 4.41 (forward / backward) but hold 32 CUs instead of 16 for the decoder's
+// ~2 ms, and the training step measured 14.24 vs 13.97 ms (profiles/r5_ar_tile_ab.txt): there
+// the decoder is off the critical path, and its CUs are worth more to the concurrent DiffNet
+// GEMMs.  ensvs_ardec_coop_set_tile_seqs forces one (A/B runs, tests).
+int g_ar_tile_seqs = 0;
+int ar_tile_seqs(int B, int H) {
+  (void)H;
+  if (g_ar_tile_seqs) return g_ar_tile_seqs;
+  return B <= 16 ? 16 : 32;
+}
 
-template <int H>
+template <int H, int S>
+long long ar_wave_bytes() { return (long long)AR_MAX_TILES * (coop::HDR + ArGeo<H, S>::SLAB); }
+
+template <int H, int S>
 int coop_fwd_launch(const float* gx, int ldgx, const float* ofx, int ldo, const void* wp,
                     const float* wih_p, const float* wfo, int ldwfo, const float* score, int lds,
                     const float* mask, const float* teach, int ldt, int B, int T, ArConsts k,
                     float* lf0, float* res, float* sg, float* sc, float* sh, float* so, float* sp,
                     unsigned* work, hipStream_t st) {
-  const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSF + coop::SB * 5 +
-                                         coop::SB * 6 * coop::UW) + 2 * coop::SB * coop::UW;
-  static const bool attr = coop::set_max_lds((const void*)ardec_coop_fwd_kernel<H>, st_lds);
+  const size_t st_lds = sizeof(float) * (4 * S * AR_PSF + S * 5 + S * 6 * coop::UW) +
+                        2 * S * coop::UW;
+  static const bool attr = coop::set_max_lds((const void*)ardec_coop_fwd_kernel<H, S>, st_lds);
   if (!attr) return ENSVS_E_HIP;
   const coop::Ctl ctl = coop::host_ctl();
-  const int ntt = coop::ntiles(B), Tr = T / 4;
+  const int ntt = (B + S - 1) / S, Tr = T / 4;
   for (int t0 = 0; t0 < ntt; t0 += AR_MAX_TILES) {
     const int nt = std::min(AR_MAX_TILES, ntt - t0);
-    const long long b0 = (long long)t0 * coop::SB, r = b0 * Tr, f = b0 * T;
-    unsigned* wk = (unsigned*)((char*)work + (t0 / AR_MAX_TILES) * ar_wave_bytes<H>());
+    const long long b0 = (long long)t0 * S, r = b0 * Tr, f = b0 * T;
+    unsigned* wk = (unsigned*)((char*)work + (t0 / AR_MAX_TILES) * ar_wave_bytes<H, S>());
     if (hipMemsetAsync(wk, 0, (size_t)nt * coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(ardec_coop_fwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(AR_NTS),
+    hipLaunchKernelGGL((ardec_coop_fwd_kernel<H, S>), dim3(ArGeo<H, S>::NW, nt), dim3(AR_NTS),
                        coop::dyn_lds(st_lds), st, gx + r * ldgx, ldgx, ofx + r * ldo, ldo,
                        (const f16x8*)wp, wih_p, wfo, ldwfo, score + f * lds, lds, mask + r,
                        teach ? teach + f * ldt : teach, ldt, (int)(B - b0), T, k, lf0 + f, res + f,
@@ -890,23 +915,22 @@ int coop_fwd_launch(const float* gx, int ldgx, const float* ofx, int ldo, const 
   return ENSVS_OK;
 }
 
-template <int H>
+template <int H, int S>
 int coop_bwd_launch(const float* glf0, const float* gres, const void* wp, const float* wih_p,
                     const float* wfo, int ldwfo, const float* mask, int teacher, int B, int T,
                     ArConsts k, const float* sg, const float* sc, const float* so, float* dg,
                     float* do4, unsigned* work, hipStream_t st) {
-  const size_t st_lds = sizeof(float) * (4 * coop::SB * AR_PSB + coop::SB * 5 +
-                                         coop::SB * 4 * coop::UW) + 2 * coop::SB * 64;
-  static const bool attr = coop::set_max_lds((const void*)ardec_coop_bwd_kernel<H>, st_lds);
+  const size_t st_lds = sizeof(float) * (4 * S * AR_PSB + S * 5 + S * 4 * coop::UW) + 2 * S * 64;
+  static const bool attr = coop::set_max_lds((const void*)ardec_coop_bwd_kernel<H, S>, st_lds);
   if (!attr) return ENSVS_E_HIP;
   const coop::Ctl ctl = coop::host_ctl();
-  const int ntt = coop::ntiles(B), Tr = T / 4;
+  const int ntt = (B + S - 1) / S, Tr = T / 4;
   for (int t0 = 0; t0 < ntt; t0 += AR_MAX_TILES) {
     const int nt = std::min(AR_MAX_TILES, ntt - t0);
-    const long long b0 = (long long)t0 * coop::SB, r = b0 * Tr, f = b0 * T;
-    unsigned* wk = (unsigned*)((char*)work + (t0 / AR_MAX_TILES) * ar_wave_bytes<H>());
+    const long long b0 = (long long)t0 * S, r = b0 * Tr, f = b0 * T;
+    unsigned* wk = (unsigned*)((char*)work + (t0 / AR_MAX_TILES) * ar_wave_bytes<H, S>());
     if (hipMemsetAsync(wk, 0, (size_t)nt * coop::HDR, st) != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(ardec_coop_bwd_kernel<H>, dim3(ArGeo<H>::NW, nt), dim3(AR_NTS),
+    hipLaunchKernelGGL((ardec_coop_bwd_kernel<H, S>), dim3(ArGeo<H, S>::NW, nt), dim3(AR_NTS),
                        coop::dyn_lds(st_lds), st, glf0 + f, gres ? gres + f : gres,
                        (const bf16x8*)wp, wih_p, wfo, ldwfo, mask + r, teacher, (int)(B - b0), T,
                        k, sg + r * 4 * H, sc + r * H, so + r * 4, dg + r * 4 * H, do4 + r * 4, wk,
@@ -919,8 +943,10 @@ int coop_bwd_launch(const float* glf0, const float* gres, const void* wp, const 
 bool ar_coop_shape(int B, int H) { return B >= 1 && (H == 128 || H == 256); }
 
 long long ar_coop_work(int H, int B) {
-  const long long slab = H == 128 ? ArGeo<128>::SLAB : ArGeo<256>::SLAB;
-  return (long long)coop::ntiles(B) * (coop::HDR + slab);
+  const int S = ar_tile_seqs(B, H);
+  const long long slab = H == 128 ? (S == 16 ? ArGeo<128, 16>::SLAB : ArGeo<128, 32>::SLAB)
+                                  : (S == 16 ? ArGeo<256, 16>::SLAB : ArGeo<256, 32>::SLAB);
+  return (long long)((B + S - 1) / S) * (coop::HDR + slab);
 }
 
 int ar_coop_check(int B, int T, int H, const void* wp, const void* work, long long work_bytes) {
@@ -983,6 +1009,16 @@ ENSVS_API int ensvs_ardec_bwd(const float* glf0, const float* gres, const float*
 
 ENSVS_API int ensvs_ardec_coop_supported(int B, int H) { return ar_coop_shape(B, H) ? 1 : 0; }
 
+ENSVS_API int ensvs_ardec_coop_set_tile_seqs(int s) {
+  if (s != 0 && s != 16 && s != 32) return ENSVS_E_ARG;
+  g_ar_tile_seqs = s;
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_ardec_coop_tile_seqs(int B, int H) {
+  return ar_coop_shape(B, H) ? ar_tile_seqs(B, H) : 0;
+}
+
 ENSVS_API long long ensvs_ardec_coop_work_bytes(int H, int B) {
   return ar_coop_shape(B, H) ? ar_coop_work(H, B) : 0;
 }
@@ -1006,8 +1042,13 @@ ENSVS_API int ensvs_ardec_coop_fwd(const float* gx, int ldgx, const float* ofx, 
   ArConsts k{in_min, in_max, mean, scale};
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;
-  return H == 128 ? coop_fwd_launch<128>(gx, ldgx, ofx, ldo, wpack, wih_p, wfo, ldwfo, score, lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, so, sp, wk, st)
-                  : coop_fwd_launch<256>(gx, ldgx, ofx, ldo, wpack, wih_p, wfo, ldwfo, score, lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, so, sp, wk, st);
+#define AR_FWD(HH, SS) coop_fwd_launch<HH, SS>(gx, ldgx, ofx, ldo, wpack, wih_p, wfo, ldwfo, score, \
+                                             lds, mask, teach, ldt, B, T, k, lf0, res, sg, sc, sh, \
+                                             so, sp, wk, st)
+  const bool s16 = ar_tile_seqs(B, H) == 16;
+  if (H == 128) return s16 ? AR_FWD(128, 16) : AR_FWD(128, 32);
+  return s16 ? AR_FWD(256, 16) : AR_FWD(256, 32);
+#undef AR_FWD
 }
 
 ENSVS_API int ensvs_ardec_coop_bwd(const float* glf0, const float* gres, const void* wpack,
@@ -1021,8 +1062,12 @@ ENSVS_API int ensvs_ardec_coop_bwd(const float* glf0, const float* gres, const v
   ArConsts k{in_min, in_max, mean, scale};
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;
-  return H == 128 ? coop_bwd_launch<128>(glf0, gres, wpack, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc, so, dg, do4, wk, st)
-                  : coop_bwd_launch<256>(glf0, gres, wpack, wih_p, wfo, ldwfo, mask, teacher, B, T, k, sg, sc, so, dg, do4, wk, st);
+#define AR_BWD(HH, SS) coop_bwd_launch<HH, SS>(glf0, gres, wpack, wih_p, wfo, ldwfo, mask, teacher, \
+                                             B, T, k, sg, sc, so, dg, do4, wk, st)
+  const bool s16 = ar_tile_seqs(B, H) == 16;
+  if (H == 128) return s16 ? AR_BWD(128, 16) : AR_BWD(128, 32);
+  return s16 ? AR_BWD(256, 16) : AR_BWD(256, 32);
+#undef AR_BWD
 }
 
 ENSVS_API int ensvs_downsample_fwd(const float* p0, int ld0, int n0, const float* p1, int ld1,

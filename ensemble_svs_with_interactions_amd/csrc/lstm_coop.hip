@@ -10,8 +10,9 @@
 //   * each direction is split over NW = H / 16 workgroups; workgroup w owns hidden units
 //     [16 w, 16 w + 16) and holds their 64 gate rows of W_hh (forward) or their 16 columns
 //     (backward: dh = W_hh^T dG) as MFMA A fragments in VGPRs for the whole sequence;
-//   * the <= 32 sequences are the MFMA N dimension (two 16-column tiles), the K dimension is
-//     split over the four waves and their partial sums are added through LDS;
+//   * the sequences of a tile (16 or 32) are the MFMA N dimension (one or two 16-column
+//     tiles), the K dimension is split over the four waves and their partial sums are added
+//     through LDS;
 //   * the recurrent products run in fp16 (forward: h in [-1, 1]) / bf16 (backward: dG spans
 //     many decades) with fp32 accumulation -- as the reference recipe's fp16 autocast runs its
 //     cuDNN LSTM (myconfig_notuseIL.yaml:6) -- while gates, cell state and every saved value
@@ -21,7 +22,7 @@
 //     every storing wave, then one agent-scope counter add per workgroup; readers poll the
 //     counter with sc1 loads and read the slab with sc1 loads only (the hand-off form of
 //     MI355X_MICROARCH.md, "Hand-offs measured with sc1 loads", first row).
-// Every workgroup of the grid must be resident at once (2 NW <= 64 workgroups, one per CU);
+// Every workgroup of a tile must be resident at once (2 NW <= 64 workgroups, one per CU);
 // the polls are bounded, so a grid that cannot become resident ends (flagging the error word
 // of the workspace) instead of hanging.
 #include <atomic>
@@ -38,13 +39,20 @@ using namespace coop;
 constexpr int PSF = 68;     // forward partial-sum row per sequence: 64 gate rows + 4 (banks)
 constexpr int PSB = 20;     // backward: 16 units + 4
 
-template <int H> struct CGeo {
+// S = sequences per tile: 32 (two MFMA N tiles, two cells per thread) or 16 (one N tile, one
+// cell per thread).  A 16-sequence tile halves what every workgroup reads from the slab each
+// step -- the backward's whole dG_t, 64 KB instead of 128 KB at H = 512, which the per-CU
+// read rate from the Infinity Cache (~65 GB/s, MI355X_MICROARCH.md handoff-payload) turns
+// into ~1 us per step -- at twice the workgroups; tile_seqs() picks it for small batches.
+template <int H, int S> struct CGeo {
   static constexpr int NW = H / UW;       // workgroups per direction
   static constexpr int KCW = H / 128;     // forward: 32-deep K chunks per wave (K = H)
   static constexpr int KCBW = H / 32;     // backward: per wave (K = 4H)
-  static constexpr int FX = 2 * 2 * SB * H * 2;      // forward slab bytes: [dir][buf][s][H] f16
-  static constexpr int BX = 2 * 2 * SB * 4 * H * 2;  // backward: [dir][buf][s][4H] bf16
-  static_assert(H % 128 == 0, "H");
+  static constexpr int NTN = S / 16;      // MFMA N tiles
+  static constexpr int NC = S * UW / NT;  // cells per compute thread
+  static constexpr int FX = 2 * 2 * S * H * 2;      // forward slab bytes: [dir][buf][s][H] f16
+  static constexpr int BX = 2 * 2 * S * 4 * H * 2;  // backward: [dir][buf][s][4H] bf16
+  static_assert(H % 128 == 0 && (S == 16 || S == 32), "H, S");
 };
 
 // W_hh [4H][H] fp32 (both directions) -> forward A fragments
@@ -53,7 +61,7 @@ template <int H> struct CGeo {
 template <int H>
 __global__ void coop_pack_fwd_kernel(const float* __restrict__ w0, const float* __restrict__ w1,
                                      int ndir, _Float16* __restrict__ out) {
-  using G = CGeo<H>;
+  using G = CGeo<H, 32>;
   const int n = ndir * 4 * H * H;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int j = i & 7, lane = (i >> 3) & 63;
@@ -74,7 +82,7 @@ __global__ void coop_pack_fwd_kernel(const float* __restrict__ w0, const float* 
 template <int H>
 __global__ void coop_pack_bwd_kernel(const float* __restrict__ w0, const float* __restrict__ w1,
                                      int ndir, __bf16* __restrict__ out) {
-  using G = CGeo<H>;
+  using G = CGeo<H, 32>;
   const int n = ndir * 4 * H * H;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int j = i & 7, lane = (i >> 3) & 63;
@@ -95,7 +103,7 @@ __global__ void coop_pack_bwd_kernel(const float* __restrict__ w0, const float* 
 // tools/ardec_phase_probe.py measured the stores at ~0.44 us of a 4.6 us step there).
 constexpr int NTS = NT + 64;
 
-template <int H>
+template <int H, int S>
 __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
     const float* __restrict__ gx, int ldg,     // [B*T][ldg], dir d gate g unit u at d 4H + g H + u
     const f16x8* __restrict__ wp,              // packed forward fragments
@@ -103,16 +111,16 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
     float* __restrict__ y, int ldy,            // [B*T][ldy], dir d at d H + u
     float* __restrict__ sv,                    // [B*T][2][5H]
     unsigned* __restrict__ work, Ctl c) {
-  using G = CGeo<H>;
-  constexpr int KCW = G::KCW, NW = G::NW;
-  __shared__ __attribute__((aligned(16))) float part[4 * SB * PSF];
-  __shared__ __attribute__((aligned(16))) _Float16 hs[SB * UW];
-  __shared__ int sL[SB];
-  __shared__ __attribute__((aligned(16))) float st6[SB * 6 * UW];  // [s][h i f g o c][u]
+  using G = CGeo<H, S>;
+  constexpr int KCW = G::KCW, NW = G::NW, NTN = G::NTN, NC = G::NC;
+  __shared__ __attribute__((aligned(16))) float part[4 * S * PSF];
+  __shared__ __attribute__((aligned(16))) _Float16 hs[S * UW];
+  __shared__ int sL[S];
+  __shared__ __attribute__((aligned(16))) float st6[S * 6 * UW];  // [s][h i f g o c][u]
   const int d = blockIdx.y, w = blockIdx.x, u0 = w * UW;
-  {  // this workgroup's sequence tile: sequences [32 z, 32 z + 32)
-    const int s0 = blockIdx.z * SB;
-    B = min(SB, B - s0);
+  {  // this workgroup's sequence tile: sequences [S z, S z + S)
+    const int s0 = blockIdx.z * S;
+    B = min(S, B - s0);
     lengths += s0;
     gx += (long long)s0 * T * ldg;
     y += (long long)s0 * T * ldy;
@@ -120,7 +128,7 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
   }
   unsigned* hdr = tile_hdr(work, blockIdx.z);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid < SB) sL[tid] = tid < B ? (int)lengths[tid] : 0;
+  if (tid < S) sL[tid] = tid < B ? (int)lengths[tid] : 0;
   __syncthreads();
   int maxL = 0;
   for (int s = 0; s < B; ++s) maxL = max(maxL, sL[s]);
@@ -138,9 +146,9 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
       if (t > 0) wait_count(hdr, d, (unsigned)(NW * t), c);
       lds_barrier();  // (1)
       lds_barrier();  // (2) step t's outputs staged in st6
-      // 32 sequences x 6 rows (h i f g o c) of 16 units, 16 B per store
+      // S sequences x 6 rows (h i f g o c) of 16 units, 16 B per store
 #pragma unroll
-      for (int k4 = 0; k4 < SB * 6 * UW / 4 / 64; ++k4) {
+      for (int k4 = 0; k4 < S * 6 * UW / 4 / 64; ++k4) {
         const int gi = lane + 64 * k4, sq = gi / (6 * UW / 4), rem = gi % (6 * UW / 4);
         const int q = rem / (UW / 4), c4 = (rem % (UW / 4)) * 4;
         const f32x4 v = *(const f32x4*)&st6[(sq * 6 + q) * UW + c4];
@@ -164,11 +172,11 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
       for (int kk = 0; kk < KCW; ++kk) wf[mt][kk] = src[(mt * KCW + kk) * 64];
   }
 
-  // cell pairs: (unit u = p & 15, sequence s = p >> 4), p = tid + 256 i
-  int cs[2], cu[2];
-  long long grow[2];
+  // cells (unit u = p & 15, sequence s = p >> 4), p = tid + 256 i
+  int cs[NC], cu[NC];
+  long long grow[NC];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int p = tid + NT * i;
     cu[i] = p & 15;
     cs[i] = p >> 4;
@@ -178,10 +186,12 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
     const int tt = max(min(t, L - 1), 0);
     return (long long)sc * T + (d ? max(L - 1 - tt, 0) : tt);
   };
-  float gin[2][4], cst[2] = {0.f, 0.f};
+  float gin[NC][4], cst[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) cst[i] = 0.f;
   auto load_in = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NC; ++i) {
       grow[i] = in_row(i, t);
       const float* src = gx + grow[i] * ldg + d * 4 * H + u0 + cu[i];
 #pragma unroll
@@ -191,19 +201,19 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
   load_in(0);
 
   for (int t = 0; t < maxL; ++t) {
-    f32x4 acc[4][2];
+    f32x4 acc[4][NTN];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int nt = 0; nt < NTN; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (t > 0) {
       wait_count(hdr, d, (unsigned)(NW * t), c);
-      f16x8 bf[KCW][2];
+      f16x8 bf[KCW][NTN];
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const int off = (((d * 2 + ((t - 1) & 1)) * SB + nt * 16 + (lane & 15)) * H +
+        for (int nt = 0; nt < NTN; ++nt) {
+          const int off = (((d * 2 + ((t - 1) & 1)) * S + nt * 16 + (lane & 15)) * H +
                            (wv * KCW + kk) * 32 + 8 * (lane >> 4)) * 2;
           bf[kk][nt] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, CP_SC1));
         }
@@ -211,28 +221,28 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
+        for (int nt = 0; nt < NTN; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
 #pragma unroll
       for (int kk = 0; kk < KCW; ++kk)
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt)
+          for (int nt = 0; nt < NTN; ++nt)
             acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[mt][kk], bf[kk][nt], acc[mt][nt], 0, 0, 0);
     }
     // partial sums: lane holds gate rows 16 mt + 4 (lane >> 4) + r of sequence 16 nt + (lane & 15)
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-        *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * PSF + 16 * mt + 4 * (lane >> 4)] = acc[mt][nt];
+      for (int nt = 0; nt < NTN; ++nt)
+        *(f32x4*)&part[(wv * S + nt * 16 + (lane & 15)) * PSF + 16 * mt + 4 * (lane >> 4)] = acc[mt][nt];
     lds_barrier();
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NC; ++i) {
       const int s = cs[i], u = cu[i];
       f32x4 a = *(const f32x4*)&part[s * PSF + 4 * u];
 #pragma unroll
-      for (int q = 1; q < 4; ++q) a += *(const f32x4*)&part[(q * SB + s) * PSF + 4 * u];
+      for (int q = 1; q < 4; ++q) a += *(const f32x4*)&part[(q * S + s) * PSF + 4 * u];
       const float ig = sigm(a[0] + gin[i][0]), fg = sigm(a[1] + gin[i][1]);
       const float gg = tanh_fast(a[2] + gin[i][2]), og = sigm(a[3] + gin[i][3]);
       const float cn = fg * cst[i] + ig * gg;
@@ -249,10 +259,12 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
       o6[5 * UW] = cn;
     }
     lds_barrier();
-    if (wv == 0) {  // publish h_t: 32 sequences x 16 units, one 16-B sc1 store per lane
-      const f32x4 v = *(const f32x4*)&hs[(lane >> 1) * UW + (lane & 1) * 8];
-      const int off = (((d * 2 + (t & 1)) * SB + (lane >> 1)) * H + u0 + (lane & 1) * 8) * 2;
-      __builtin_amdgcn_raw_buffer_store_b128(v, xr, off, 0, CP_SC1);
+    if (wv == 0) {  // publish h_t: S sequences x 16 units, one 16-B sc1 store per lane < 2 S
+      if (lane < 2 * S) {
+        const f32x4 v = *(const f32x4*)&hs[(lane >> 1) * UW + (lane & 1) * 8];
+        const int off = (((d * 2 + (t & 1)) * S + (lane >> 1)) * H + u0 + (lane & 1) * 8) * 2;
+        __builtin_amdgcn_raw_buffer_store_b128(v, xr, off, 0, CP_SC1);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(hdr, d, t, c);
     }
@@ -264,7 +276,7 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
 // (round 5) it measured slower, H = 256 4.39 -> 4.73 and H = 512 6.16 -> 6.57 us per step
 // (tools/lstm_coop_bench.py, profiles/r5_coop_service_wave.txt) -- its dG payload (32 KB per
 // wave per step at H = 512) shares SIMD 0 with the fifth wave.
-template <int H>
+template <int H, int S>
 __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
     const float* __restrict__ dy, int lddy,    // [B*T][lddy], grad of outputs
     const bf16x8* __restrict__ wp,             // packed backward fragments
@@ -272,15 +284,15 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
     const float* __restrict__ sv,              // saved [B*T][2][5H]
     float* __restrict__ dg, int lddg,          // [B*T][lddg], dir d gate g unit u at d 4H + g H + u
     unsigned* __restrict__ work, Ctl c) {
-  using G = CGeo<H>;
-  constexpr int KCBW = G::KCBW, NW = G::NW, G4 = 4 * H;
-  __shared__ __attribute__((aligned(16))) float part[4 * SB * PSB];
-  __shared__ __attribute__((aligned(16))) __bf16 gs[SB * 64];  // [s][4 u + g]
-  __shared__ int sL[SB];
+  using G = CGeo<H, S>;
+  constexpr int KCBW = G::KCBW, NW = G::NW, G4 = 4 * H, NTN = G::NTN, NC = G::NC;
+  __shared__ __attribute__((aligned(16))) float part[4 * S * PSB];
+  __shared__ __attribute__((aligned(16))) __bf16 gs[S * 64];  // [s][4 u + g]
+  __shared__ int sL[S];
   const int d = blockIdx.y, w = blockIdx.x, u0 = w * UW;
   {  // this workgroup's sequence tile
-    const int s0 = blockIdx.z * SB;
-    B = min(SB, B - s0);
+    const int s0 = blockIdx.z * S;
+    B = min(S, B - s0);
     lengths += s0;
     dy += (long long)s0 * T * lddy;
     sv += (long long)s0 * T * 10 * H;
@@ -288,7 +300,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
   }
   unsigned* hdr = tile_hdr(work, blockIdx.z);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid < SB) sL[tid] = tid < B ? (int)lengths[tid] : 0;
+  if (tid < S) sL[tid] = tid < B ? (int)lengths[tid] : 0;
 
   bf16x8 wb[KCBW];
   {
@@ -308,19 +320,21 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
   }
   const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.z, blockIdx.z, G::BX);
 
-  int cs[2], cu[2];
+  int cs[NC], cu[NC];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int p = tid + NT * i;
     cu[i] = p & 15;
     cs[i] = p >> 4;
   }
   // processing index q of sequence s is its forward step L - 1 - q: row L-1-q (dir 0) or q
-  float in[2][7], dcs[2] = {0.f, 0.f};
-  long long grow[2];
+  float in[NC][7], dcs[NC];
+  long long grow[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) dcs[i] = 0.f;
   auto load_in = [&](int q) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NC; ++i) {
       const int sc = min(cs[i], B - 1), L = sL[sc];
       const int qq = max(min(q, L - 1), 0);
       const long long rb = (long long)sc * T;
@@ -339,41 +353,43 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
   load_in(0);
 
   for (int q = 0; q < maxL; ++q) {
-    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 acc[NTN];
+#pragma unroll
+    for (int nt = 0; nt < NTN; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (q > 0) {
       wait_count(hdr, d, (unsigned)(NW * q), c);
-      bf16x8 bf[KCBW][2];
+      bf16x8 bf[KCBW][NTN];
 #pragma unroll
       for (int kk = 0; kk < KCBW; ++kk)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const int off = (((d * 2 + ((q - 1) & 1)) * SB + nt * 16 + (lane & 15)) * G4 +
+        for (int nt = 0; nt < NTN; ++nt) {
+          const int off = (((d * 2 + ((q - 1) & 1)) * S + nt * 16 + (lane & 15)) * G4 +
                            (wv * KCBW + kk) * 32 + 8 * (lane >> 4)) * 2;
           bf[kk][nt] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, CP_SC1));
         }
 #pragma unroll
       for (int kk = 0; kk < KCBW; ++kk)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
+        for (int nt = 0; nt < NTN; ++nt) asm volatile("" ::"v"(bf[kk][nt]));
 #pragma unroll
       for (int kk = 0; kk < KCBW; ++kk)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+        for (int nt = 0; nt < NTN; ++nt)
           acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[kk], bf[kk][nt], acc[nt], 0, 0, 0);
     }
     // lane holds dh of units 4 (lane >> 4) + r for sequence 16 nt + (lane & 15)
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-      *(f32x4*)&part[(wv * SB + nt * 16 + (lane & 15)) * PSB + 4 * (lane >> 4)] = acc[nt];
+    for (int nt = 0; nt < NTN; ++nt)
+      *(f32x4*)&part[(wv * S + nt * 16 + (lane & 15)) * PSB + 4 * (lane >> 4)] = acc[nt];
     lds_barrier();
-    float o[2][4];
-    bool val[2];
+    float o[NC][4];
+    bool val[NC];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NC; ++i) {
       const int s = cs[i], u = cu[i];
       float dhr = part[s * PSB + u];
 #pragma unroll
-      for (int k = 1; k < 4; ++k) dhr += part[(k * SB + s) * PSB + u];
+      for (int k = 1; k < 4; ++k) dhr += part[(k * S + s) * PSB + u];
       const float ig = in[i][0], fg = in[i][1], gg = in[i][2], og = in[i][3];
       const float dh = in[i][6] + dhr;
       const float tc = tanh_fast(in[i][4]);
@@ -390,16 +406,18 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
       *(bf16x4_*)&gs[s * 64 + 4 * u] = nb;
     }
     lds_barrier();
-    {  // publish dG: 32 sequences x 64 values, one 16-B sc1 store per thread
-      const f32x4 v = *(const f32x4*)&gs[(tid >> 3) * 64 + (tid & 7) * 8];
-      const int off = (((d * 2 + (q & 1)) * SB + (tid >> 3)) * G4 + w * 64 + (tid & 7) * 8) * 2;
-      __builtin_amdgcn_raw_buffer_store_b128(v, xr, off, 0, CP_SC1);
+    {  // publish dG: S sequences x 64 values, one 16-B sc1 store per thread < 8 S
+      if (tid < 8 * S) {
+        const f32x4 v = *(const f32x4*)&gs[(tid >> 3) * 64 + (tid & 7) * 8];
+        const int off = (((d * 2 + (q & 1)) * S + (tid >> 3)) * G4 + w * 64 + (tid & 7) * 8) * 2;
+        __builtin_amdgcn_raw_buffer_store_b128(v, xr, off, 0, CP_SC1);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();
       if (tid == 0) signal(hdr, d, q, c);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NC; ++i)
       if (val[i]) {
         float* dst = dg + grow[i] * lddg + d * G4 + u0 + cu[i];
 #pragma unroll
@@ -409,53 +427,64 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
   }
 }
 
-// any B: tiles of 32 sequences (coop.h), launched in waves of up to MAX_TILES tiles (256
-// sequences; at H = 512 a wave is 8 x 64 workgroups).  Wave k owns the workspace region of its
-// tiles -- their headers, then their slabs -- so every launch sees the layout coop.h describes;
-// a wave's tiles need only be co-resident one at a time (tiles never wait on each other), and
+// any B: tiles of S sequences (coop.h), launched in waves of up to MAX_TILES tiles (at H = 512
+// and S = 32 a wave is 8 x 64 workgroups).  Wave k owns the workspace region of its tiles --
+// their headers, then their slabs -- so every launch sees the layout coop.h describes; a wave's
+// tiles need only be co-resident one at a time (tiles never wait on each other), and
 // consecutive waves on the stream run one after the other.
 constexpr int MAX_TILES = 8;
 
-template <int H>
-long long wave_bytes() { return (long long)MAX_TILES * (HDR + CGeo<H>::BX); }
+// sequences per tile: 16 while the launch stays within 128 workgroups (H = 512: B <= 32, H = 256:
+// B <= 64), else 32; ensvs_lstm_coop_set_tile_seqs forces one (A/B runs, tests)
+int g_tile_seqs = 0;
+int tile_seqs(int B, int H) {
+  if (g_tile_seqs) return g_tile_seqs;
+  return 2 * (H / UW) * ((B + 15) / 16) <= 128 ? 16 : 32;
+}
+inline int ntiles_s(int B, int S) { return (B + S - 1) / S; }
 
-template <int H>
+template <int H, int S>
+long long wave_bytes() { return (long long)MAX_TILES * (HDR + CGeo<H, S>::BX); }
+
+template <int H, int S>
 int launch_fwd(const float* gx, int ldg, const void* wp, const long long* lengths, int B, int T,
                float* y, int ldy, float* sv, unsigned* work, hipStream_t st) {
-  using G = CGeo<H>;
-  const size_t st_lds = sizeof(float) * (4 * SB * PSF + SB * 6 * UW) + 2 * SB * UW + 4 * SB;
-  static const bool attr = set_max_lds((const void*)lstm_coop_fwd_kernel<H>, st_lds);
+  using G = CGeo<H, S>;
+  const size_t st_lds = sizeof(float) * (4 * S * PSF + S * 6 * UW) + 2 * S * UW + 4 * S;
+  static const bool attr = set_max_lds((const void*)lstm_coop_fwd_kernel<H, S>, st_lds);
   if (!attr) return ENSVS_E_HIP;
   const Ctl ctl = host_ctl();
-  for (int t0 = 0; t0 < ntiles(B); t0 += MAX_TILES) {
-    const int nt = std::min(MAX_TILES, ntiles(B) - t0);
-    const long long b0 = (long long)t0 * SB;
-    unsigned* wk = (unsigned*)((char*)work + (t0 / MAX_TILES) * wave_bytes<H>());
+  const int ntt = ntiles_s(B, S);
+  for (int t0 = 0; t0 < ntt; t0 += MAX_TILES) {
+    const int nt = std::min(MAX_TILES, ntt - t0);
+    const long long b0 = (long long)t0 * S;
+    unsigned* wk = (unsigned*)((char*)work + (t0 / MAX_TILES) * wave_bytes<H, S>());
     if (hipMemsetAsync(wk, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(lstm_coop_fwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NTS), dyn_lds(st_lds), st,
-                       gx + b0 * T * ldg, ldg, (const f16x8*)wp, lengths + b0, (int)(B - b0), T,
-                       y + b0 * T * ldy, ldy, sv + b0 * T * 10 * H, wk, ctl);
+    hipLaunchKernelGGL((lstm_coop_fwd_kernel<H, S>), dim3(G::NW, 2, nt), dim3(NTS), dyn_lds(st_lds),
+                       st, gx + b0 * T * ldg, ldg, (const f16x8*)wp, lengths + b0, (int)(B - b0),
+                       T, y + b0 * T * ldy, ldy, sv + b0 * T * 10 * H, wk, ctl);
     ENSVS_CHECK_LAUNCH();
   }
   return ENSVS_OK;
 }
 
-template <int H>
+template <int H, int S>
 int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengths, int B, int T,
                const float* sv, float* dg, int lddg, unsigned* work, hipStream_t st) {
-  using G = CGeo<H>;
-  const size_t st_lds = sizeof(float) * 4 * SB * PSB + 2 * SB * 64 + 4 * SB;
-  static const bool attr = set_max_lds((const void*)lstm_coop_bwd_kernel<H>, st_lds);
+  using G = CGeo<H, S>;
+  const size_t st_lds = sizeof(float) * 4 * S * PSB + 2 * S * 64 + 4 * S;
+  static const bool attr = set_max_lds((const void*)lstm_coop_bwd_kernel<H, S>, st_lds);
   if (!attr) return ENSVS_E_HIP;
   const Ctl ctl = host_ctl();
-  for (int t0 = 0; t0 < ntiles(B); t0 += MAX_TILES) {
-    const int nt = std::min(MAX_TILES, ntiles(B) - t0);
-    const long long b0 = (long long)t0 * SB;
-    unsigned* wk = (unsigned*)((char*)work + (t0 / MAX_TILES) * wave_bytes<H>());
+  const int ntt = ntiles_s(B, S);
+  for (int t0 = 0; t0 < ntt; t0 += MAX_TILES) {
+    const int nt = std::min(MAX_TILES, ntt - t0);
+    const long long b0 = (long long)t0 * S;
+    unsigned* wk = (unsigned*)((char*)work + (t0 / MAX_TILES) * wave_bytes<H, S>());
     if (hipMemsetAsync(wk, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
-    hipLaunchKernelGGL(lstm_coop_bwd_kernel<H>, dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds), st,
-                       dy + b0 * T * lddy, lddy, (const bf16x8*)wp, lengths + b0, (int)(B - b0), T,
-                       sv + b0 * T * 10 * H, dg + b0 * T * lddg, lddg, wk, ctl);
+    hipLaunchKernelGGL((lstm_coop_bwd_kernel<H, S>), dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds),
+                       st, dy + b0 * T * lddy, lddy, (const bf16x8*)wp, lengths + b0,
+                       (int)(B - b0), T, sv + b0 * T * 10 * H, dg + b0 * T * lddg, lddg, wk, ctl);
     ENSVS_CHECK_LAUNCH();
   }
   return ENSVS_OK;
@@ -465,8 +494,10 @@ bool coop_shape(int B, int H) { return B >= 1 && (H == 256 || H == 512); }
 
 // full waves of MAX_TILES tiles, then the last wave's tiles
 long long work_bytes(int H, int B) {
-  const long long slab = H == 256 ? CGeo<256>::BX : CGeo<512>::BX;
-  return (long long)ntiles(B) * (HDR + slab);
+  const int S = tile_seqs(B, H);
+  const long long slab = H == 256 ? (S == 16 ? CGeo<256, 16>::BX : CGeo<256, 32>::BX)
+                                  : (S == 16 ? CGeo<512, 16>::BX : CGeo<512, 32>::BX);
+  return (long long)ntiles_s(B, S) * (HDR + slab);
 }
 
 int check_work(const void* work, long long nbytes, int H, int B) {
@@ -530,6 +561,14 @@ ENSVS_API int ensvs_coop_inject_fault(int on) {
 
 ENSVS_API int ensvs_lstm_coop_supported(int B, int H) { return coop_shape(B, H) ? 1 : 0; }
 
+ENSVS_API int ensvs_lstm_coop_set_tile_seqs(int s) {
+  if (s != 0 && s != 16 && s != 32) return ENSVS_E_ARG;
+  g_tile_seqs = s;
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_lstm_coop_tile_seqs(int B, int H) { return coop_shape(B, H) ? tile_seqs(B, H) : 0; }
+
 ENSVS_API long long ensvs_lstm_coop_work_bytes(int H, int B) {
   return coop_shape(B, H) ? work_bytes(H, B) : 0;
 }
@@ -566,8 +605,12 @@ ENSVS_API int ensvs_lstm_coop_fwd(const float* gx, int ldg, const void* wpack,
   if ((uintptr_t)y % 16 || ldy % 4 || (uintptr_t)saved % 16) return ENSVS_E_ARG;  // 16-B stores
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;
-  return H == 256 ? launch_fwd<256>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st)
-                  : launch_fwd<512>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st);
+  const bool s16 = tile_seqs(B, H) == 16;
+  if (H == 256)
+    return s16 ? launch_fwd<256, 16>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st)
+               : launch_fwd<256, 32>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st);
+  return s16 ? launch_fwd<512, 16>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st)
+             : launch_fwd<512, 32>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st);
 }
 
 ENSVS_API int ensvs_lstm_coop_bwd(const float* dy, int lddy, const void* wpack,
@@ -578,6 +621,10 @@ ENSVS_API int ensvs_lstm_coop_bwd(const float* dy, int lddy, const void* wpack,
   if (check_work(work, work_bytes, H, B) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;
-  return H == 256 ? launch_bwd<256>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st)
-                  : launch_bwd<512>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st);
+  const bool s16 = tile_seqs(B, H) == 16;
+  if (H == 256)
+    return s16 ? launch_bwd<256, 16>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st)
+               : launch_bwd<256, 32>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st);
+  return s16 ? launch_bwd<512, 16>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st)
+             : launch_bwd<512, 32>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st);
 }

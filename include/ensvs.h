@@ -214,9 +214,9 @@ int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* w
  * SeparateF0 decoders' H = 256 of nnsvs/model.py:1483-1490, 861-869).  wpack: W_hh of both
  * directions packed by ensvs_lstm_coop_pack (bwd = 0: forward fp16 fragments, bwd = 1:
  * backward bf16 fragments of W_hh^T), 2*4*H*H 2-byte elements.  Sequences run in tiles of
- * 32 (blockIdx.z), each tile an independent hand-off group.  work: 256-B aligned,
- * ensvs_lstm_coop_work_bytes(H, B) bytes, caller-owned, one per concurrent launch: ceil(B/32)
- * 256-B tile headers, then the tiles' slabs; header bytes 128..131 of a tile read non-zero
+ * S = ensvs_lstm_coop_tile_seqs(B, H) (blockIdx.z), each tile an independent hand-off group.
+ * work: 256-B aligned, ensvs_lstm_coop_work_bytes(H, B) bytes, caller-owned, one per
+ * concurrent launch: ceil(B/S) 256-B tile headers, then the tiles' slabs; header bytes 128..131 of a tile read non-zero
  * after a launch in which that tile's grid could not become resident (see
  * ensvs_coop_set_error_word for the persistent flag). */
 /* MFMA recurrence for H = 64 / 128 in production (bf16 GEMM) precision (lstm_mfma.hip): the
@@ -244,6 +244,12 @@ int ensvs_lstm_mfma_bwd(const float* dy, int lddy, const void* wpack, const long
                         void* dgbf, int lddgb, float* bsum, void* stream);
 int ensvs_lstm_coop_supported(int B, int H);
 long long ensvs_lstm_coop_work_bytes(int H, int B);
+/* Sequences per tile of the cooperative LSTM for a batch of B at hidden size H: 16 while the
+ * launch stays within 128 workgroups (H = 512: B <= 32; H = 256: B <= 64) -- every workgroup
+ * then reads half the hand-off slab per step -- else 32.  ensvs_lstm_coop_set_tile_seqs(s)
+ * forces s in {16, 32} (0: automatic), for A/B runs and tests; set it before sizing `work`. */
+int ensvs_lstm_coop_tile_seqs(int B, int H);
+int ensvs_lstm_coop_set_tile_seqs(int s);
 int ensvs_lstm_coop_pack(const float* whh_f, const float* whh_r, int H, int bwd, void* out,
                          void* stream);
 int ensvs_lstm_coop_fwd(const float* gx, int ldg, const void* wpack, const long long* lengths,
@@ -269,19 +275,23 @@ int ensvs_ardec_bwd(const float* glf0, const float* gres, const float* wpb, cons
                     const float* wfo, int ldwfo, const float* mask, int teacher, int B, int T,
                     int H, float in_min, float in_max, float mean, float scale, const float* sg,
                     const float* sc, const float* so, float* dg, float* do4, void* stream);
-/* Cooperative AR decoder for H in {128, 256}, B <= 256 in production (bf16 GEMM) precision:
+/* Cooperative AR decoder for H in {128, 256}, any B, in production (bf16 GEMM) precision:
  * one launch for all T/4 steps, the recurrence W_hh [h_1 .. h_B] split over H/16 workgroups
  * that keep their W_hh slice in registers (fp16 forward, bf16 W_hh^T backward, fp32
  * accumulation, gates, cell state, feat_out and saved values) and exchange h / dG plus the
  * feat_out / prenet partial sums through `work` every step.  Same contract and saved layout as
  * ensvs_ardec_fwd / ensvs_ardec_bwd (tacotron_f0.py:183-228).  wpack: ensvs_ardec_coop_pack
  * (bwd = 0 forward fp16 fragments, bwd = 1 backward bf16 fragments), 4*H*H 2-byte elements;
- * sequences in tiles of 32 (blockIdx.y) as the LSTM above; work: 256-B aligned,
+ * sequences in tiles of S = ensvs_ardec_coop_tile_seqs(B, H) (blockIdx.y; 16 for B <= 16, else
+ * 32; ensvs_ardec_coop_set_tile_seqs forces 16 / 32, 0 automatic) in launches of up to 8 tiles;
+ * work: 256-B aligned,
  * ensvs_ardec_coop_work_bytes(H, B) bytes, caller-owned, one per concurrent launch, laid out
  * and flagged as the LSTM's.  The forward's saved-state outputs sg / sc / sh are 16-B aligned
  * (written with 16-B stores). */
 int ensvs_ardec_coop_supported(int B, int H);
 long long ensvs_ardec_coop_work_bytes(int H, int B);
+int ensvs_ardec_coop_tile_seqs(int B, int H);
+int ensvs_ardec_coop_set_tile_seqs(int s);
 /* Failure controls of every cooperative launch (coop.h).  A tile whose workgroups cannot all
  * become resident times out after `us` microseconds (default 1 s) of polling, releases its
  * waiters (the launch ends within one timeout) and ORs 1 into the registered persistent device

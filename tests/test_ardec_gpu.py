@@ -2,7 +2,8 @@
 per-sequence kernels (ensvs_ardec_fwd / _bwd, fp32; themselves pinned to the reference decoder,
 tacotron_f0.py:126-237, by the lf0-model goldens of test_multitrack_gpu.py) on the same inputs:
 free-running and teacher-forced, the recipe's H = 256 at the bench's 30 sequences x 1024 frames,
-H = 128 at a ragged batch of 5, and batches of 33 / 64 / 70 sequences (2-3 tiles of 32).  The cooperative kernels run the recurrent products in
+H = 128 at a ragged batch of 5, and batches of 33 / 64 / 70 / 300 sequences (tiles of 16 up to
+16 sequences, else of 32; both tile sizes also forced where the other is the default).  The cooperative kernels run the recurrent products in
 fp16 (forward) / bf16 (backward) with fp32 accumulation, as the recipe's fp16 autocast runs the
 LSTMCell (myconfig_notuseIL.yaml:6).  Bounds (max-abs relative): outputs and saved state 1e-3,
 gate / feat_out / W_hh gradients 3e-3 (measured: outputs <= 1.1e-4, gradients <= 5e-4;
@@ -37,12 +38,16 @@ def _inputs(B, T, H, seed):
 
 
 def _resident(work, B, H):
-    """Every 32-sequence tile's residency flag (byte 128 of its 256-B header) clear; tiles run
-    in launches of 8, each owning its tiles' workspace region (coop.h)."""
-    wave = query("ensvs_ardec_coop_work_bytes", H, 256)
+    """Every tile's residency flag (byte 128 of its 256-B header) clear; tiles of S = 16 or 32
+    sequences run in launches of 8, each owning its tiles' workspace region (coop.h); 16-sequence
+    tiles come in one launch."""
+    S = query("ensvs_ardec_coop_tile_seqs", B, H)
+    nt = (B + S - 1) // S
+    assert S == 32 or nt <= 8
+    wave = query("ensvs_ardec_coop_work_bytes", H, 256) if nt > 8 else 0  # 8 tiles of 32
     return all(work[wave * (z // 8) + 256 * (z % 8) + 128:
                     wave * (z // 8) + 256 * (z % 8) + 132].cpu().view(torch.int32).item() == 0
-               for z in range((B + 31) // 32))
+               for z in range(nt))
 
 
 def _run(a, B, T, H, coop, teacher):
@@ -124,3 +129,14 @@ def test_ardec_coop_matches_exact(H, B, T, teacher):
         assert errs[k] < 1e-3, (k, errs)
     for k in ("dg", "do4", "dwhh"):
         assert errs[k] < 3e-3, (k, errs)
+
+
+@pytest.mark.parametrize("H,B,T,S", [(256, 30, 1024, 16), (256, 40, 256, 16), (256, 100, 64, 16),
+                                     (128, 5, 200, 32), (256, 8, 512, 32)])
+def test_ardec_coop_tile_sizes_match_exact(H, B, T, S):
+    call("ensvs_ardec_coop_set_tile_seqs", S)
+    try:
+        assert query("ensvs_ardec_coop_tile_seqs", B, H) == S
+        test_ardec_coop_matches_exact(H, B, T, False)
+    finally:
+        call("ensvs_ardec_coop_set_tile_seqs", 0)

@@ -74,8 +74,11 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False, mfma=False):
         assert query("ensvs_lstm_coop_supported", B, H) == 1
         nbytes = query("ensvs_lstm_coop_work_bytes", H, B)
         cwork = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        ntile = (B + 31) // 32
-        wave = query("ensvs_lstm_coop_work_bytes", H, 256)  # one launch's 8 tiles (coop.h)
+        S = query("ensvs_lstm_coop_tile_seqs", B, H)  # sequences per tile: 16 or 32
+        ntile = (B + S - 1) // S
+        # one launch's 8 tiles (coop.h); 16-sequence tiles only come in a single launch
+        wave = query("ensvs_lstm_coop_work_bytes", H, 256) if ntile > 8 else 0
+        assert S == 32 or ntile <= 8
 
         def resident():  # every tile's residency flag (header byte 128 of each tile) clear
             return all(cwork[wave * (z // 8) + 256 * (z % 8) + 128:
@@ -185,6 +188,21 @@ def test_lstm_coop_matches_torch(H, B, T, lengths):
         g = torch.Generator().manual_seed(H + B)
         lengths = [T] + torch.randint(1, T + 1, (B - 1,), generator=g).tolist()
     _check(H, B, T, 24, lengths, 5e-3, 2e-2, coop=True)
+
+
+# Tiles of 16 sequences (small batches: H = 512 up to 32, H = 256 up to 64 sequences) and of 32,
+# each forced where the other is the default: the same bounds
+@pytest.mark.parametrize("H,B,T,S", [(512, 30, 200, 32), (256, 30, 200, 32), (512, 40, 64, 16),
+                                     (256, 5, 37, 32)])
+def test_lstm_coop_tile_sizes_match_torch(H, B, T, S):
+    g = torch.Generator().manual_seed(H + B + S)
+    lengths = [T] + torch.randint(1, T + 1, (B - 1,), generator=g).tolist()
+    call("ensvs_lstm_coop_set_tile_seqs", S)
+    try:
+        assert query("ensvs_lstm_coop_tile_seqs", B, H) == S
+        _check(H, B, T, 24, lengths, 5e-3, 2e-2, coop=True)
+    finally:
+        call("ensvs_lstm_coop_set_tile_seqs", 0)
 
 
 # MFMA recurrences (lstm_mfma.hip): H = 64 / 128 in production precision (fp16 recurrent

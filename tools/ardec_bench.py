@@ -29,7 +29,10 @@ bargs = (a["wih_p"].data_ptr(), a["wfo"].data_ptr(), H + 130, a["mask"].data_ptr
          do4.data_ptr())
 wpf, wpb = E(4 * H * H), E(4 * H * H)
 call("ensvs_ardec_pack", a["whh"].data_ptr(), H, wpf.data_ptr(), wpb.data_ptr(), st)
+call("ensvs_ardec_coop_set_tile_seqs", 32)  # the larger of the two tile layouts
 nbytes = query("ensvs_ardec_coop_work_bytes", H, B)
+call("ensvs_ardec_coop_set_tile_seqs", 0)
+nbytes = max(nbytes, query("ensvs_ardec_coop_work_bytes", H, B))
 work = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
 wf = torch.empty(4 * H * H, dtype=torch.float16, device=dev)
 wb = torch.empty(4 * H * H, dtype=torch.bfloat16, device=dev)
@@ -47,7 +50,10 @@ runs = {
                              wb.data_ptr(), *bargs, work.data_ptr(), nbytes, st),
 }
 line = []
-for name, fn in runs.items():
+runs = [(k, v, 0) for k, v in runs.items() if "exact" in k] + \
+    [(f"{k}{S}", v, S) for S in (32, 16) for k, v in runs.items() if "coop" in k]
+for name, fn, S in runs:
+    call("ensvs_ardec_coop_set_tile_seqs", S)
     fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -58,5 +64,6 @@ for name, fn in runs.items():
     torch.cuda.synchronize()
     us = s.elapsed_time(e) * 1e3 / iters
     line.append(f"{name} {us:9.1f} us ({us / Tr:5.2f} us/step)")
+call("ensvs_ardec_coop_set_tile_seqs", 0)
 err = work[128:132].cpu().view(torch.int32).item()
 print(f"H={H} B={B} T={T}: " + "  ".join(line) + f"  err={err}", flush=True)

@@ -1,6 +1,8 @@
 """Interleaved A/B of module switches on the bench's main training line (graph replay, 30 x
-1024): each arm sets kernels.<FLAG>["on"] values, runs the bench leg in a fresh process, two
-rounds.   python tools/flag_ab.py "COLSUM_ONCE=0,DEFER_WGRAD=0" "COLSUM_ONCE=1,DEFER_WGRAD=0" ..."""
+1024): each arm sets kernels.<FLAG>["on"] values or calls C-ABI switches (ensvs_*=value), runs
+the bench leg in a fresh process, two rounds.
+  python tools/flag_ab.py [--sf0] "COLSUM_ONCE=0,DEFER_WGRAD=0" "ensvs_ardec_coop_set_tile_seqs=32" ...
+--sf0: time the recipe-default SeparateF0 leg instead (its ms_per_step)."""
 import json
 import os
 import subprocess
@@ -11,22 +13,29 @@ RUN = """
 import sys
 sys.path.insert(0, {root!r})
 from ensemble_svs_with_interactions_amd import kernels as K
+from ensemble_svs_with_interactions_amd._lib import call
 for kv in {arm!r}.split(","):
     if kv:
         k, v = kv.split("=")
-        getattr(K, k)["on"] = bool(int(v))
+        if k.startswith("ensvs_"):
+            call(k, int(v))
+        else:
+            getattr(K, k)["on"] = bool(int(v))
 sys.argv = ["bench.py", "--steps", "20", "--warmup", "3", "--no-cpu-baseline", "--no-synth",
-            "--no-sf0", "--no-census", "--no-config2", "--no-shapes", "--no-real-data",
-            "--no-transformer"]
+            "--no-census", "--no-config2", "--no-shapes", "--no-real-data",
+            "--no-transformer"] + ([] if {sf0!r} else ["--no-sf0"])
 import bench
 bench.main()
 """
+SF0 = "--sf0" in sys.argv[1:]
+ARMS = [a for a in sys.argv[1:] if a != "--sf0"]
 for rep in range(2):
-    for arm in sys.argv[1:]:
-        out = subprocess.run([sys.executable, "-c", RUN.format(root=ROOT, arm=arm)], cwd=ROOT,
+    for arm in ARMS:
+        out = subprocess.run([sys.executable, "-c", RUN.format(root=ROOT, arm=arm, sf0=SF0)], cwd=ROOT,
                              capture_output=True, text=True, timeout=400)
         if out.returncode:
             print(out.stderr[-2000:])
             sys.exit(1)
         d = json.loads(out.stdout.strip().splitlines()[-1])
-        print(f"arm=[{arm}] {d['ms_per_step']:.3f} ms", flush=True)
+        ms = d["separate_f0"]["ms_per_step"] if SF0 else d["ms_per_step"]
+        print(f"arm=[{arm}] {ms:.3f} ms" + (" (SeparateF0)" if SF0 else ""), flush=True)

@@ -8,13 +8,15 @@
 #   py:<script + args>      any python script                     -> gpurun_out/TAG_py<i>.txt
 #   ab:<dir> <dir> ...      interleaved whole-tree A/B (tools/tree_ab.sh) -> gpurun_out/TAG_ab<i>.txt
 #   smoke                   __graft_entry__.smoke()               -> gpurun_out/TAG_smoke.log
+# Inside a STEP, commas stand for spaces (bench:--no-synth,--no-shapes), since the job's
+# arguments are split on spaces.
 # Every step has its own time limit; the job stops at the first failing step.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 9
 tag=$1; shift
 i=0
 for step in "$@"; do
-  i=$((i + 1)); kind=${step%%:*}; args=${step#*:}
+  i=$((i + 1)); kind=${step%%:*}; args=${step#*:}; args=${args//,/ }
   case $kind in
     tests) timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $args \
              > gpurun_out/${tag}_tests$i.log 2>&1 ;;

@@ -1,6 +1,7 @@
 """Time the large-H recurrences at the bench workload (30 sequences x 1024 frames, synthetic
 lengths): the cooperative kernels (lstm_coop.hip) against the per-step kernels (lstm.hip),
-us per launch and us per recurrent step (dev tool).   python tools/lstm_coop_bench.py"""
+us per launch and us per recurrent step, the cooperative kernels at both tile sizes (16 / 32
+sequences per tile) (dev tool).   python tools/lstm_coop_bench.py"""
 import os
 import sys
 
@@ -37,7 +38,10 @@ for H in (256, 512):
     dg = torch.empty(B * T, 8 * H, device=dev)
     nw = query("ensvs_lstm_bwd_work_floats", B, H)
     work = torch.empty(max(nw, 1), device=dev)
-    nb = query("ensvs_lstm_coop_work_bytes", H, B)
+    call("ensvs_lstm_coop_set_tile_seqs", 32)
+    nb = query("ensvs_lstm_coop_work_bytes", H, B)  # the larger of the two layouts
+    call("ensvs_lstm_coop_set_tile_seqs", 0)
+    nb = max(nb, query("ensvs_lstm_coop_work_bytes", H, B))
     cw = torch.empty(nb, dtype=torch.uint8, device=dev)
     wpf = torch.empty(2 * 4 * H * H, dtype=torch.float16, device=dev)
     wpb = torch.empty(2 * 4 * H * H, dtype=torch.bfloat16, device=dev)
@@ -50,12 +54,15 @@ for H in (256, 512):
     res["bwd_step"] = timed(lambda: call("ensvs_lstm_bwd", dy.data_ptr(), 2 * H, w[0].data_ptr(),
                                          w[1].data_ptr(), lens.data_ptr(), B, T, H, sv.data_ptr(),
                                          dg.data_ptr(), 8 * H, work.data_ptr(), nw, st), 2)
-    res["fwd_coop"] = timed(lambda: call("ensvs_lstm_coop_fwd", gx.data_ptr(), 8 * H, wpf.data_ptr(),
-                                         lens.data_ptr(), B, T, H, y.data_ptr(), 2 * H, sv.data_ptr(),
-                                         cw.data_ptr(), nb, st), 5)
-    res["bwd_coop"] = timed(lambda: call("ensvs_lstm_coop_bwd", dy.data_ptr(), 2 * H, wpb.data_ptr(),
-                                         lens.data_ptr(), B, T, H, sv.data_ptr(), dg.data_ptr(),
-                                         8 * H, cw.data_ptr(), nb, st), 5)
+    for S in (32, 16):
+        call("ensvs_lstm_coop_set_tile_seqs", S)
+        res[f"fwd_coop{S}"] = timed(lambda: call("ensvs_lstm_coop_fwd", gx.data_ptr(), 8 * H, wpf.data_ptr(),
+                                             lens.data_ptr(), B, T, H, y.data_ptr(), 2 * H, sv.data_ptr(),
+                                             cw.data_ptr(), nb, st), 5)
+        res[f"bwd_coop{S}"] = timed(lambda: call("ensvs_lstm_coop_bwd", dy.data_ptr(), 2 * H, wpb.data_ptr(),
+                                             lens.data_ptr(), B, T, H, sv.data_ptr(), dg.data_ptr(),
+                                             8 * H, cw.data_ptr(), nb, st), 5)
+    call("ensvs_lstm_coop_set_tile_seqs", 0)
     err = cw[128:132].cpu().view(torch.int32).item()
     steps = max(lengths)
     print(f"H={H:4d} " + "  ".join(f"{k} {v:9.1f} us ({v / steps:6.2f} us/step)"

@@ -33,6 +33,10 @@ from .engine import GradCapture, ModulePacks, empty, grad_of, lengths_pair, next
 from .engine import gemm_dtype as engine_gemm_dtype
 
 SQRT1_2 = 1.0 / math.sqrt(2.0)
+# Training forward: each block's output projection computes the residual half only and the
+# skip sum of all blocks is one GEMM after them (off: the skip half in every block's RESSKIP
+# epilogue, as inference runs it)
+SKIP_GEMM = {"on": True}
 # Reverse diffusion as a captured HIP graph when no noise is injected (set "on" False to
 # launch eagerly).
 USE_GRAPHS = {"on": True}
@@ -124,8 +128,21 @@ class DiffNet(nn.Module):
                                                  scale=SQRT1_2)
             pk.refs[f"out{l}^Tskip"] = pk.bwd.add(w[C:], C, C, 1, C, 1, 1, transpose=True)
             pk.bias_vec(f"o{l}.b", blk.output_projection.bias, perm_c=C)
+            # training forward: the residual half alone, pre-scaled by 1/sqrt2 (ADDSCALE
+            # epilogue x' = x/sqrt2 + acc + b'); the skip halves go into one GEMM below
+            pk.refs[f"res{l}"] = pk.fwd.add(w[:C], C, C, 1, C, 1, 1, scale=SQRT1_2)
+            pk.refs[f"r{l}.b"] = pk.bias.add(blk.output_projection.bias[:C].view(C, 1, 1), C, 1,
+                                             1, 1, 1, 1, scale=SQRT1_2, kpad_to=1)
             conds.append(blk.conditioner_projection.weight)
         pk.refs["condT"] = pk.bwd.add_rowcat(conds, 2 * C, self.E, transpose_blocks=True)
+        # the skip sum of all blocks, sum_l (W_l[C:] z_l + b_l[C:]) / sqrt(L), as ONE GEMM
+        # over [z_0 .. z_L-1] (K = L*C) and the blocks' skip biases (summed per forward)
+        blocks = self.residual_layers
+        pk.refs["skipall"] = pk.fwd.add_colcat([b.output_projection.weight[C:] for b in blocks],
+                                               C, C, scale=1.0 / math.sqrt(L))
+        pk.refs["skipall.b"] = pk.bias.add_rowcat(
+            [b.output_projection.bias[C:].view(C, 1) for b in blocks], C, 1, kpad_to=1,
+            scale=1.0 / math.sqrt(L))
         pk.conv("skip", self.skip_projection.weight, bwd_scale=1.0 / math.sqrt(L))
         pk.bias_vec("skip.b", self.skip_projection.bias)
         pk.conv("outp", self.output_projection.weight)
@@ -214,12 +231,19 @@ class DiffNet(nn.Module):
             xn = empty(M, C, device=dev) if save else x
             nxt = b16 and l + 1 < L
             xbn = empty(M, C, device=dev, dtype=torch.bfloat16) if nxt else None
-            K.gemm([K.Seg(z, ldz, C, pk[f"out{l}"], T) if zb is None else
-                    K.Seg(zb, ldz, C, pk[f"out{l}"], T)], B, T, 2 * C, pk.fwd, xn, C,
-                   epi=_lib.EPI_RESSKIP, aux0=S, ld0=C, aux1=x, ld1=C, accum=l > 0,
-                   alpha=1.0 / math.sqrt(L), C=C, ybf=xbn, ybf_ld=C,
-                   ybf_radd=ds[:, (l + 1) * C:] if nxt else None, ybf_radd_ld=L * C,
-                   **pk.bias_ptr_args(f"o{l}.b"))
+            radd = dict(ybf=xbn, ybf_ld=C, ybf_radd=ds[:, (l + 1) * C:] if nxt else None,
+                        ybf_radd_ld=L * C)
+            zseg = K.Seg(z, ldz, C, None, T) if zb is None else K.Seg(zb, ldz, C, None, T)
+            if save and SKIP_GEMM["on"]:
+                # training: the residual half alone, x' = x / sqrt2 + (W_l[:C] / sqrt2) z_l + b'
+                zseg.ref = pk[f"res{l}"]
+                K.gemm([zseg], B, T, C, pk.fwd, xn, C, epi=_lib.EPI_ADDSCALE, aux1=x, ld1=C,
+                       alpha=SQRT1_2, **radd, **pk.bias_ptr_args(f"r{l}.b"))
+            else:
+                zseg.ref = pk[f"out{l}"]
+                K.gemm([zseg], B, T, 2 * C, pk.fwd, xn, C, epi=_lib.EPI_RESSKIP, aux0=S, ld0=C,
+                       aux1=x, ld1=C, accum=l > 0, alpha=1.0 / math.sqrt(L), C=C, **radd,
+                       **pk.bias_ptr_args(f"o{l}.b"))
             xb = xbn
             if save:
                 Z.append(z)
@@ -227,6 +251,15 @@ class DiffNet(nn.Module):
                 if l + 1 < L:
                     X.append(xn)
             x = xn
+        if save and SKIP_GEMM["on"]:
+            # S = sum_l (W_l[C:] z_l + b_l[C:]) / sqrt(L): one K = L*C GEMM over the z of every
+            # block (kept for the backward anyway) instead of a read-modify-write of S in each
+            # block's epilogue (2 x 31 MB per block at 30 x 1024 frames)
+            bsk = empty(C, device=dev)
+            ob = pk["skipall.b"].offset
+            K.colsum(pk.bias.buf[ob:ob + L * C], C, L, C, bsk)
+            K.gemm([K.Seg(ZBall if b16 else Zall, L * C, L * C, pk["skipall"], T)], B, T, C,
+                   pk.fwd, S, C, bias=bsk, bias_off=0)
         p1 = empty(M, C, device=dev)
         p1b = empty(M, C, device=dev, dtype=torch.bfloat16) if b16 else None
         K.gemm([K.Seg(S, C, C, pk["skip"], T)], B, T, C, pk.fwd, p1, C, relu=True,

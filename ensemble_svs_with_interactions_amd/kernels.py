@@ -94,6 +94,23 @@ class PackedBuffer:
         self._max = max(self._max, n)
         return ref
 
+    def add_colcat(self, srcs, N, K, scale=1.0):
+        """Several (N, K) weights (row stride K) side by side along the reduction: packed
+        N x (len*K) -- one output summed over the inputs of every block (the DiffNet skip
+        halves)."""
+        L = len(srcs)
+        Npad, Kp = _roundup(N, BM), _roundup(L * K, BK)
+        ref = PackedRef(self.size, N, L * K, 1, Npad, Kp)
+        for l, w in enumerate(srcs):
+            sub = PackedRef(self.size + l * K, N, K, 1, Npad, K)
+            self.specs.append(dict(src=w, src2=None, sn=K, sk=1, sj=1, N=N, K=K, taps=1,
+                                   Npad=Npad, Kp=K, perm_c=0, flip=0, transpose=0,
+                                   scale=float(scale), ref=sub, ldk=Kp))
+        n = Npad * Kp
+        self.size += _roundup(n, 64)
+        self._max = max(self._max, n)
+        return ref
+
     def finalize(self, device):
         tdtype = torch.bfloat16 if self.dtype == _lib.DT_BF16 else torch.float32
         self.buf = torch.zeros(max(self.size, 64), dtype=tdtype, device=device)

@@ -19,6 +19,11 @@ for kv in {arm!r}.split(","):
         k, v = kv.split("=")
         if k.startswith("ensvs_"):
             call(k, int(v))
+        elif "." in k:  # module.FLAG of the package, e.g. diffsinger.SKIP_GEMM
+            import importlib
+            mod, flag = k.rsplit(".", 1)
+            getattr(importlib.import_module("ensemble_svs_with_interactions_amd." + mod),
+                    flag)["on"] = bool(int(v))
         else:
             getattr(K, k)["on"] = bool(int(v))
 sys.argv = ["bench.py", "--steps", "20", "--warmup", "3", "--no-cpu-baseline", "--no-synth",

@@ -83,6 +83,8 @@ SIGNATURES = {
                          c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_ll, c_ll, c_int,
                          c_float, c_int, c_vp],
     "ensvs_pack_weights": [c_vp, c_int, c_int, c_vp],
+    "ensvs_colsum_batch": [c_vp, c_int, c_vp, c_ll, c_vp],
+    "ensvs_colsum_batch_part_floats": [c_vp, c_int],
     "ensvs_colsum_once": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_vp,
                           c_vp, c_int, c_int, c_vp],
     "ensvs_colsum": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_vp, c_int,
@@ -238,7 +240,7 @@ RESTYPES = {"ensvs_embed_bwd_workspace": c_ll, "ensvs_usf_source_workspace": c_l
             "ensvs_lstm_coop_work_bytes": c_ll, "ensvs_lstm_coop_supported": ctypes.c_int,
             "ensvs_lstm_mfma_supported": ctypes.c_int,
             "ensvs_ardec_coop_work_bytes": c_ll, "ensvs_ardec_coop_supported": ctypes.c_int,
-            "ensvs_coop_error_word": c_vp}
+            "ensvs_coop_error_word": c_vp, "ensvs_colsum_batch_part_floats": c_ll}
 
 _lib = None
 

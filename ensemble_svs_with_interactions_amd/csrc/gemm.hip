@@ -3304,6 +3304,95 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
   }
 }
 
+// Deferred column sums of several parameter gradients (ensvs_colsum_batch): blockIdx.z /
+// blockIdx.y picks the descriptor; each block runs colsum_partial_kernel's / colsum_final_kernel's
+// body on its columns (the same split count, rows per split and summation order: the same bits).
+struct CsDesc {
+  const float* y;
+  float* out;
+  int ld, M, N, rps, S, vec;
+  long long part_off;
+  float scale;
+  int accum;
+};
+constexpr int CS_BATCH = 48;
+struct CsBatch {
+  CsDesc d[CS_BATCH];
+};
+static_assert(sizeof(CsBatch) <= 3584, "kernel argument size");
+
+__global__ __launch_bounds__(256) void colsum_partial_batch_kernel(const CsBatch b,
+                                                                   float* __restrict__ part) {
+  const CsDesc& d = b.d[blockIdx.z];
+  if ((int)blockIdx.x * 64 >= d.N || (int)blockIdx.y >= d.S) return;
+  __shared__ f32x4 red[16][17];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int N = d.N, col = blockIdx.x * 64 + cq * 4;
+  const int s = blockIdx.y;
+  const int r0 = s * d.rps, r1 = min(d.M, r0 + d.rps);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  auto ld4 = [&](int r) -> f32x4 {
+    const float* q = d.y + (long long)r * d.ld + col;
+    f32x4 v;
+    if (d.vec && col + 3 < N) {
+      v = *(const f32x4*)q;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = col + e < N ? q[e] : 0.f;
+    }
+    return v;
+  };
+  if (col < N) {
+    int r = r0 + rl;
+    for (; r + 48 < r1; r += 64) {
+      const f32x4 v0 = ld4(r), v1 = ld4(r + 16), v2 = ld4(r + 32), v3 = ld4(r + 48);
+      acc += (v0 + v1) + (v2 + v3);
+    }
+    for (; r < r1; r += 16) acc += ld4(r);
+  }
+  red[rl][cq] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = threadIdx.x;
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][c >> 2][c & 3];
+    const int gc = blockIdx.x * 64 + c;
+    if (gc < N) part[d.part_off + (long long)s * N + gc] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_final_batch_kernel(const CsBatch b,
+                                                                 const float* __restrict__ part) {
+  const CsDesc& d = b.d[blockIdx.y];
+  if ((int)blockIdx.x * 16 >= d.N) return;
+  __shared__ double red[16][17];
+  const int N = d.N, S = d.S;
+  const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + c;
+  const float* p = part + d.part_off;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (col < N) {
+    int s = sl;
+    for (; s + 48 < S; s += 64) {
+      a0 += p[(long long)s * N + col];
+      a1 += p[(long long)(s + 16) * N + col];
+      a2 += p[(long long)(s + 32) * N + col];
+      a3 += p[(long long)(s + 48) * N + col];
+    }
+    for (; s < S; s += 16) a0 += p[(long long)s * N + col];
+  }
+  red[sl][c] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (sl == 0 && col < N) {
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][c];
+    const float v = (float)(t * d.scale);
+    d.out[col] = d.accum ? d.out[col] + v : v;
+  }
+}
+
 // colsum_partial_kernel + colsum_final_kernel in one launch: each block writes its split's
 // partial row as the partial kernel does, then takes a ticket on its (column block, group)
 // counter; the block that draws the last ticket runs the final kernel's sums for its 64
@@ -4079,6 +4168,58 @@ ENSVS_API int ensvs_wgrad_reduce_batch(const ensvs_wred_desc* descs, int n, void
     }
     hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3((unsigned)cdiv_ll(most, 256), m),
                        dim3(256), 0, (hipStream_t)stream, b);
+    ENSVS_CHECK_LAUNCH();
+  }
+  return ENSVS_OK;
+}
+
+// the split count ensvs_colsum picks for one group (>= ~2048 blocks, >= 128 rows per split)
+static int colsum_splits(int M, int N, int groups, int max_splits) {
+  return std::max(1, std::min({max_splits, M / 128, cdiv(2048, cdiv(N, 64) * groups)}));
+}
+
+ENSVS_API long long ensvs_colsum_batch_part_floats(const ensvs_colsum_desc* descs, int n) {
+  long long t = 0;
+  for (int i = 0; i < n; ++i)
+    t += (long long)colsum_splits(descs[i].M, descs[i].N, 1, descs[i].max_splits) * descs[i].N;
+  return t;
+}
+
+ENSVS_API int ensvs_colsum_batch(const ensvs_colsum_desc* descs, int n, float* part,
+                                 long long part_floats, void* stream) {
+  if (n < 0 || (n > 0 && (!descs || !part))) return ENSVS_E_ARG;
+  if (part_floats < ensvs_colsum_batch_part_floats(descs, n)) return ENSVS_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  long long off = 0;
+  for (int i0 = 0; i0 < n; i0 += CS_BATCH) {
+    const int m = std::min(CS_BATCH, n - i0);
+    CsBatch b{};
+    int most_cb = 1, most_s = 1, most_c16 = 1;
+    for (int i = 0; i < m; ++i) {
+      const ensvs_colsum_desc& e = descs[i0 + i];
+      if (!e.y || !e.out || e.M <= 0 || e.N <= 0 || e.ld < e.N || e.max_splits < 1)
+        return ENSVS_E_ARG;
+      CsDesc& d = b.d[i];
+      d.y = e.y;
+      d.out = e.out;
+      d.ld = e.ld;
+      d.M = e.M;
+      d.N = e.N;
+      d.S = colsum_splits(e.M, e.N, 1, e.max_splits);
+      d.rps = cdiv(e.M, d.S);
+      d.vec = (e.ld % 4 == 0) && (((uintptr_t)e.y & 15) == 0);
+      d.part_off = off;
+      d.scale = e.scale;
+      d.accum = e.accum;
+      off += (long long)d.S * e.N;
+      most_cb = std::max(most_cb, cdiv(e.N, 64));
+      most_s = std::max(most_s, d.S);
+      most_c16 = std::max(most_c16, cdiv(e.N, 16));
+    }
+    hipLaunchKernelGGL(colsum_partial_batch_kernel, dim3(most_cb, most_s, m), dim3(256), 0, st,
+                       b, part);
+    ENSVS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(colsum_final_batch_kernel, dim3(most_c16, m), dim3(256), 0, st, b, part);
     ENSVS_CHECK_LAUNCH();
   }
   return ENSVS_OK;

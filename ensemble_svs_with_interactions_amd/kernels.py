@@ -442,7 +442,9 @@ class WredDesc(ctypes.Structure):  # include/ensvs.h ensvs_wred_desc
 # (ensvs_wgrad_reduce_batch: the same per-element sums, the same bits).  Branch ends
 # (engine.Branches) and the data-parallel bucket launches flush, so no reader sees a gradient
 # before its reduction.  ~140 reduce launches per training step become a handful.
-_DEFER = {"depth": 0, "pending": {}}  # stream handle -> [(desc fields, part, (lo, hi))]
+# stream handle -> [(desc fields, part or source, (lo, hi))]: weight-gradient reductions and
+# bias-gradient column sums
+_DEFER = {"depth": 0, "pending": {}, "colsum": {}}
 
 
 @contextlib.contextmanager
@@ -453,18 +455,29 @@ def deferred_wgrad():
     finally:
         _DEFER["depth"] -= 1
         flush_wgrad()
-        if _DEFER["depth"] == 0 and _DEFER["pending"]:
-            left = {k: len(v) for k, v in _DEFER["pending"].items()}
+        if _DEFER["depth"] == 0 and (_DEFER["pending"] or _DEFER["colsum"]):
+            left = {k: len(v) for k, v in list(_DEFER["pending"].items()) +
+                    list(_DEFER["colsum"].items())}
             _DEFER["pending"].clear()
+            _DEFER["colsum"].clear()
             raise RuntimeError(f"weight-gradient reductions queued on streams {left} were "
                                "never flushed (a wgrad outside an engine.Branches region)")
 
 
 def flush_wgrad():
-    """Issue the current stream's queued weight-gradient reductions (one launch per 48)."""
-    if not _DEFER["pending"]:
+    """Issue the current stream's queued weight-gradient reductions (one launch per 48) and
+    column sums (two launches per 48)."""
+    if not _DEFER["pending"] and not _DEFER["colsum"]:
         return
     key = stream()
+    cols = _DEFER["colsum"].pop(key, None)
+    if cols:
+        carr = (ColsumDesc * len(cols))()
+        for i, (f, _, _) in enumerate(cols):
+            carr[i] = ColsumDesc(*f)
+        nf = _lib.query("ensvs_colsum_batch_part_floats", ctypes.addressof(carr), len(cols))
+        part = scratch(nf, cols[0][1].device, key="colsum_batch")
+        call("ensvs_colsum_batch", ctypes.addressof(carr), len(cols), part.data_ptr(), nf, key)
     items = _DEFER["pending"].pop(key, None)
     if not items:
         return
@@ -538,6 +551,9 @@ COLSUM_ONCE = {"on": False}
 # per branch, ~140 -> ~10 reduce launches per step) or reduce each weight gradient right after
 # it (same bits either way): 13.91 / 13.92 vs 13.98 / 14.04 ms, profiles/r5_reduction_ab.txt
 DEFER_WGRAD = {"on": True}
+# queue the bias-gradient column sums (layers.colsum_into) the same way: one ensvs_colsum_batch
+# (two launches) per flush instead of two launches per bias
+DEFER_COLSUM = {"on": True}
 
 
 def counters(n, device):
@@ -555,13 +571,31 @@ def counters(n, device):
     return t
 
 
+class ColsumDesc(ctypes.Structure):  # include/ensvs.h ensvs_colsum_desc
+    _fields_ = [("y", ctypes.c_void_p), ("out", ctypes.c_void_p), ("ld", ctypes.c_int),
+                ("M", ctypes.c_int), ("N", ctypes.c_int), ("max_splits", ctypes.c_int),
+                ("scale", ctypes.c_float), ("accum", ctypes.c_int)]
+
+
 def colsum(y, ld, M, N, out, groups=1, mean=None, scale=1.0, accum=False, yoff=0, ldo=0,
-           outoff=0):
-    """out[g*ldo + n] (+)= scale * sum over the M rows of group g (ldo 0 -> N): one launch
-    (ensvs_colsum_once: the split partials are reduced by the last block of each column block,
-    the same sums as the two-launch ensvs_colsum)."""
+           outoff=0, defer=False):
+    """out[g*ldo + n] (+)= scale * sum over the M rows of group g (ldo 0 -> N): partial and
+    final launches (ensvs_colsum; COLSUM_ONCE: ensvs_colsum_once).  defer (a parameter
+    gradient: groups 1, no mean): inside deferred_wgrad(), queued and issued with the stream's
+    other deferred column sums by flush_wgrad (ensvs_colsum_batch, the same bits)."""
     # row splits: what ensvs_colsum picks (>= 2048 blocks, >= 128 rows per split)
     max_splits = max(1, min(256, M // 128, -(-2048 // (-(-N // 64) * groups))))
+    if (defer and DEFER_COLSUM["on"] and _DEFER["depth"] > 0 and groups == 1 and mean is None
+            and ldo == 0):
+        lo = out.data_ptr() + 4 * outoff
+        hi = lo + 4 * N
+        key = stream()
+        if any(a < hi and lo < b for _, _, (a, b) in _DEFER["colsum"].get(key, ())):
+            flush_wgrad()  # one launch's outputs must not overlap
+        _DEFER["colsum"].setdefault(key, []).append(
+            ((y.data_ptr() + 4 * yoff, lo, ld, M, N, max_splits, float(scale), int(accum)), y,
+             (lo, hi)))
+        return
     part = scratch(groups * max_splits * N, y.device, key="colsum")
     if not COLSUM_ONCE["on"]:
         call("ensvs_colsum", y.data_ptr() + 4 * yoff, ld, M, groups, N, ptr(mean),

@@ -51,7 +51,7 @@ def colsum_into(dy, ld, M, N, param, groups=1, scale=1.0, off=0, yoff=0):
     """param.grad[off:off+N] += scale * column sums of dy."""
     g = grad_of(param)
     if off == 0 and groups == 1:
-        K.colsum(dy, ld, M, N, g, scale=scale, accum=True, yoff=yoff)
+        K.colsum(dy, ld, M, N, g, scale=scale, accum=True, yoff=yoff, defer=True)
     else:
         tmp = empty(groups * N, device=dy.device)
         K.colsum(dy, ld, M // groups, N, tmp, groups=groups, scale=scale, yoff=yoff)

@@ -167,6 +167,24 @@ typedef struct {
   float scale;
 } ensvs_wred_desc;
 int ensvs_wgrad_reduce_batch(const ensvs_wred_desc* descs, int n, void* stream);
+/* Column sums of several parameter gradients in two launches (the deferred bias gradients
+ * of a training step: kernels.deferred_wgrad queues them, flush_wgrad issues them):
+ * out[n] (+)= scale * sum over the M rows of y[row * ld + n], with ensvs_colsum's split count
+ * for max_splits, rows per split and summation order -- the same bits as one ensvs_colsum
+ * (groups 1, no mean) per descriptor.  Descriptors must not share output elements.  `part`:
+ * ensvs_colsum_batch_part_floats(descs, n) floats.  Replaces the per-layer
+ * `grad_bias = dy.sum(0)` reductions of the reference's autograd (e.g. nn.Linear / nn.Conv1d
+ * bias gradients in nnsvs/model.py FFConvLSTM, denoiser.py). */
+typedef struct {
+  const float* y;
+  float* out;
+  int ld, M, N, max_splits;
+  float scale;
+  int accum;
+} ensvs_colsum_desc;
+long long ensvs_colsum_batch_part_floats(const ensvs_colsum_desc* descs, int n);
+int ensvs_colsum_batch(const ensvs_colsum_desc* descs, int n, float* part, long long part_floats,
+                       void* stream);
 
 /* Batched weight repack (descs is a DEVICE array). */
 int ensvs_pack_weights(const ensvs_pack_desc* descs, int n, int max_elems, void* stream);

@@ -38,8 +38,9 @@ def test_loader_has_no_fallback(monkeypatch, tmp_path):
 
 def test_struct_layouts_match_header():
     import subprocess, tempfile
-    src = ('#include "ensvs.h"\n#include <stdio.h>\nint main(){printf("%zu %zu %zu\\n", '
-           'sizeof(ensvs_conv_seg), sizeof(ensvs_pack_desc), sizeof(ensvs_wred_desc));}\n')
+    src = ('#include "ensvs.h"\n#include <stdio.h>\nint main(){printf("%zu %zu %zu %zu\\n", '
+           'sizeof(ensvs_conv_seg), sizeof(ensvs_pack_desc), sizeof(ensvs_wred_desc), '
+           'sizeof(ensvs_colsum_desc));}\n')
     with tempfile.TemporaryDirectory() as d:
         with open(os.path.join(d, "t.c"), "w") as f:
             f.write(src)
@@ -48,8 +49,9 @@ def test_struct_layouts_match_header():
         out = subprocess.check_output([os.path.join(d, "t")]).decode().split()
     assert int(out[0]) == ctypes.sizeof(_lib.ConvSeg)
     assert int(out[1]) == ctypes.sizeof(_lib.PackDesc)
-    from ensemble_svs_with_interactions_amd.kernels import WredDesc
+    from ensemble_svs_with_interactions_amd.kernels import ColsumDesc, WredDesc
     assert int(out[2]) == ctypes.sizeof(WredDesc)
+    assert int(out[3]) == ctypes.sizeof(ColsumDesc)
 
 
 def test_library_newer_than_sources():

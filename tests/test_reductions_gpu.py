@@ -83,3 +83,79 @@ def test_deferred_wgrad_batch_bitwise():
         res.append(dsts + [shared])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_colsum_batch_bitwise():
+    """ensvs_colsum_batch (the deferred bias gradients): each descriptor's sums carry the bits
+    of one ensvs_colsum with the same max_splits, accumulation and scale included, over row
+    counts / widths / strides / alignments a step issues (and a ragged one)."""
+    torch.manual_seed(9)
+    specs = [(30720, 256, 256, 0), (30720, 128, 131, 0), (1024, 512, 512, 0), (200, 67, 70, 1),
+             (30720, 5, 8, 0), (30, 1024, 1024, 0), (3000, 61, 64, 3)]
+    st = torch.cuda.current_stream().cuda_stream
+    outs, descs, keep = [], [], []
+    for M, N, ld, yoff in specs:
+        y = torch.randn(M * ld + yoff, device=DEV)
+        out = torch.full((N,), 0.5, device=DEV)
+        ref = out.clone()
+        ms = max(1, min(256, M // 128, -(-2048 // (-(-N // 64)))))
+        part = torch.empty(ms * N, device=DEV)
+        L.call("ensvs_colsum", y.data_ptr() + 4 * yoff, ld, M, 1, N, None, 0.75, part.data_ptr(),
+               ms, ref.data_ptr(), 0, 1, st)
+        descs.append(K.ColsumDesc(y.data_ptr() + 4 * yoff, out.data_ptr(), ld, M, N, ms, 0.75, 1))
+        outs.append((out, ref))
+        keep.append(y)
+    import ctypes
+    arr = (K.ColsumDesc * len(descs))(*descs)
+    nf = L.query("ensvs_colsum_batch_part_floats", ctypes.addressof(arr), len(descs))
+    part = torch.empty(nf, device=DEV)
+    L.call("ensvs_colsum_batch", ctypes.addressof(arr), len(descs), part.data_ptr(), nf, st)
+    torch.cuda.synchronize()
+    for out, ref in outs:
+        assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_deferred_colsum_train_step_bitwise(prec):
+    """A training step with the bias-gradient column sums deferred and batched per branch
+    (kernels.DEFER_COLSUM) leaves the bits of the step with one ensvs_colsum per bias:
+    loss, gradient norm, every parameter and Adam moment."""
+    import numpy as np
+    from ensemble_svs_with_interactions_amd import configs, data, engine
+    from ensemble_svs_with_interactions_amd.train import FusedAdam, train_step
+    engine.set_gemm_precision(prec)
+    try:
+        P, T = 4, 128
+        b = data.synthetic_batch(P, T, 5)
+        g = lambda k: torch.from_numpy(b[k]).cuda().contiguous()  # noqa: E731
+        args = (g("x_main"), g("x_sub"), g("y_main"), g("spk_main"), g("spk_sub"),
+                b["lengths"].tolist())
+        gen = torch.Generator(device=DEV).manual_seed(1)
+        res = []
+        for on in (True, False):
+            K.DEFER_COLSUM["on"] = on
+            try:
+                torch.manual_seed(0)
+                m = configs.instantiate(configs.multitrack_diffusion(num_speakers=4)).cuda()
+                m.vuv_model.lstm.dropout = 0.0
+                opt = FusedAdam(m)
+                nm, nb = m.stream_sizes[0], m.stream_sizes[3]
+                gen.manual_seed(1)
+                draws = dict(
+                    lf0_main=(torch.rand(P * T // 4, device=DEV, generator=gen) < .5).float() * 2,
+                    lf0_sub=(torch.rand(P * T // 4, device=DEV, generator=gen) < .5).float() * 2,
+                    mgc_t=torch.randint(0, 100, (P,), device=DEV, generator=gen),
+                    bap_t=torch.randint(0, 100, (P,), device=DEV, generator=gen),
+                    mgc_noise=torch.randn(P * T, nm, device=DEV, generator=gen),
+                    bap_noise=torch.randn(P * T, nb, device=DEV, generator=gen))
+                loss, norm = train_step(m, opt, *args, draws=draws)
+                torch.cuda.synchronize()
+                res.append((loss.clone(), norm.clone(), opt.flat.clone(), opt.gflat.clone(),
+                            opt.m.clone(), opt.v.clone()))
+            finally:
+                K.DEFER_COLSUM["on"] = True
+        for a, b_ in zip(*res):
+            assert torch.equal(a, b_)
+        assert np.isfinite(res[0][0].item())
+    finally:
+        engine.set_gemm_precision("bf16")

@@ -17,8 +17,8 @@ from ensemble_svs_with_interactions_amd._lib import call
 for kv in {arm!r}.split(","):
     if kv:
         k, v = kv.split("=")
-        if k.startswith("ensvs_"):
-            call(k, int(v))
+        if k.startswith("ensvs_"):  # integer arguments separated by ':'
+            call(k, *[int(x) for x in v.split(":")])
         elif "." in k:  # module.FLAG of the package, e.g. diffsinger.SKIP_GEMM
             import importlib
             mod, flag = k.rsplit(".", 1)

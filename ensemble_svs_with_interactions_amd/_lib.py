@@ -112,6 +112,10 @@ SIGNATURES = {
                             c_ll, c_vp],
     "ensvs_lstm_coop_bwd": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp,
                             c_ll, c_vp],
+    "ensvs_lstm_coop_fwd_ex": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp,
+                               c_vp, c_int, c_vp, c_ll, c_vp],
+    "ensvs_lstm_coop_bwd_ex": [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int,
+                               c_vp, c_int, c_vp, c_vp, c_ll, c_vp],
     "ensvs_ardec_pack": [c_vp, c_int, c_vp, c_vp, c_vp],
     "ensvs_ardec_fwd": [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
                         c_vp, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_vp,

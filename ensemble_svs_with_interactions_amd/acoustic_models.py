@@ -20,9 +20,16 @@ from . import kernels as K
 from . import layers as Ly
 from ._lib import call, ptr, query
 from .base import BaseModel, PredictionType
-from .engine import Branches, GradCapture, ModulePacks, _sig, empty, grad_of, lengths_pair
+from .engine import (Branches, GradCapture, ModulePacks, _sig, empty, gemm_dtype, grad_of,
+                     lengths_pair)
 from .model import init_weights
 
+# SeparateF0: the decoders' [encoder out, rest flag, lf0] input in rows of a multiple of 8
+# columns (zero pad) with a bf16 copy, so its GEMMs run on bf16 operands (A/B switch)
+DEC_PAD = {"on": True}
+# SeparateF0: the decoders' weight / bias gradients issued after their input gradients, on
+# their streams beside the encoder's backward (which waits for those input gradients only)
+DEC_LATER = {"on": True}
 
 
 # Step schedule of the fused branches (0 lf0, 1 mgc, 2 bap, 3 vuv; profiles/r2_schedule_ab.txt,
@@ -1098,7 +1105,11 @@ class MultiTrackMultistreamSeparateF0ParametricModel(_MultistreamHybrid):
         if self.encoder is not None:
             N = self.encoder.out_dim
             Din = N + 2
-            X = empty(M, (Din + 3) // 4 * 4, device=dev)
+            # rows padded to a multiple of 8 columns (zeros): the decoders' first GEMM and its
+            # weight gradient then take a bf16 copy, and their input gradients come back in
+            # rows the encoder's bf16 GEMMs can read (DEC_PAD off: the fp32 form)
+            ldX = (Din + 7) // 8 * 8 if DEC_PAD["on"] else (Din + 3) // 4 * 4
+            X = empty(M, ldX, device=dev)
         # phase 1: the lf0 model (main and sub calls) beside the encoder
         with Branches(dev) as br:
             with br.on(0):
@@ -1128,8 +1139,15 @@ class MultiTrackMultistreamSeparateF0ParametricModel(_MultistreamHybrid):
             call("ensvs_copy_cols", lsrc, lld, X.data_ptr() + 4 * (N + 1), X.shape[1], M, 1,
                  Ly.stream())
             src = [(X, X.shape[1], 0, Din)]
+            X16 = None
+            if DEC_PAD["on"] and ldX > Din and gemm_dtype() == _lib.DT_BF16:
+                X.narrow(1, Din, ldX - Din).zero_()
+                X16 = K.cast_bf16(X, ldX, ldX, M)
+            st["dx_ld"] = ldX if DEC_PAD["on"] else None
         else:
             src = [(x_main, D, 0, D)]
+            X16 = None
+            st["dx_ld"] = None
         st["X"] = src
         # phase 2: the three decoders (sub calls on the same input: multistream.py:519-521)
         with Branches(dev) as br:
@@ -1138,11 +1156,11 @@ class MultiTrackMultistreamSeparateF0ParametricModel(_MultistreamHybrid):
                     outs[name], st[name] = m._fwd(
                         src, B, T, lens_dev, training=training, save=save,
                         lstm_masks=dr.get(f"{name}_lstm"),
-                        bn_updates=1 if sub_decoders or not training else 2)
+                        bn_updates=1 if sub_decoders or not training else 2, x16=X16)
                     if sub_decoders:
                         outs[name + "_sub"], st[name + "_sub"] = m._fwd(
                             src, B, T, lens_dev, training=training, save=save,
-                            lstm_masks=dr.get(f"{name}_sub_lstm"))
+                            lstm_masks=dr.get(f"{name}_sub_lstm"), x16=X16)
         return outs, st
 
     def _bwd_core(self, st, g):
@@ -1151,6 +1169,7 @@ class MultiTrackMultistreamSeparateF0ParametricModel(_MultistreamHybrid):
         M = B * T
         dev = st["lens_dev"].device
         dX = {}
+        later = {}
         with Branches(dev) as br:
             for bi, (name, m) in enumerate(self._decoders()):
                 with br.on(bi):
@@ -1158,7 +1177,9 @@ class MultiTrackMultistreamSeparateF0ParametricModel(_MultistreamHybrid):
                     for key in (name, name + "_sub"):
                         if key not in st or g.get(key) is None:
                             continue
-                        d, _ = m._bwd(st[key], g[key].contiguous())
+                        d, _ = m._bwd(st[key], g[key].contiguous(), dx_ld=st.get("dx_ld"),
+                                      later=later.setdefault(bi, []) if DEC_LATER["on"]
+                                      else None)
                         if acc is None:
                             acc = d
                         else:
@@ -1195,6 +1216,11 @@ class MultiTrackMultistreamSeparateF0ParametricModel(_MultistreamHybrid):
                         gs = torch.zeros(M, device=dev)
                     dsp["lf0_sub"], _, _ = self.lf0_model._bwd(
                         st["lf0_sub"], gs.contiguous().view(-1), g.get("lf0_residual_sub"))
+            # the decoders' parameter gradients, each on its forward's stream
+            for bi, fns in later.items():
+                with br.on(bi):
+                    for f in fns:
+                        f()
             if enc and dsum is not None:
                 dsp["enc0"], dsp["enc1"], _ = self.encoder._bwd(
                     st["enc"], dsum, ld=dsum.shape[1], want_spk=True)

@@ -109,6 +109,7 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
     const f16x8* __restrict__ wp,              // packed forward fragments
     const long long* __restrict__ lengths, int B, int T,
     float* __restrict__ y, int ldy,            // [B*T][ldy], dir d at d H + u
+    __bf16* __restrict__ y16, int ldy16,       // optional bf16 copy of y (the next GEMMs' operand)
     float* __restrict__ sv,                    // [B*T][2][5H]
     unsigned* __restrict__ work, Ctl c) {
   using G = CGeo<H, S>;
@@ -124,6 +125,7 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
     lengths += s0;
     gx += (long long)s0 * T * ldg;
     y += (long long)s0 * T * ldy;
+    if (y16) y16 += (long long)s0 * T * ldy16;
     sv += (long long)s0 * T * 10 * H;
   }
   unsigned* hdr = tile_hdr(work, blockIdx.z);
@@ -135,8 +137,11 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
   // pad_packed_sequence: this workgroup's output columns past each sequence's end are zero
   for (int s = 0; s < B; ++s) {
     const int L = sL[s];
-    for (int i = tid; i < (T - L) * UW; i += NTS)
-      y[((long long)s * T + L + i / UW) * ldy + d * H + u0 + i % UW] = 0.f;
+    for (int i = tid; i < (T - L) * UW; i += NTS) {
+      const long long row = (long long)s * T + L + i / UW;
+      y[row * ldy + d * H + u0 + i % UW] = 0.f;
+      if (y16) y16[row * ldy16 + d * H + u0 + i % UW] = (__bf16)0.f;
+    }
   }
   const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.z, blockIdx.z, G::BX);
 
@@ -157,6 +162,12 @@ __global__ __launch_bounds__(NTS) void lstm_coop_fwd_kernel(
           const long long row = (long long)sq * T + (d ? L - 1 - t : t);
           float* dst = q == 0 ? y + row * ldy + d * H : sv + (row * 2 + d) * 5 * H + (q - 1) * H;
           *(f32x4*)(dst + u0 + c4) = v;
+          if (q == 0 && y16) {
+            bf16x4_ b;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[e];
+            *(bf16x4_*)(y16 + row * ldy16 + d * H + u0 + c4) = b;
+          }
         }
       }
     }
@@ -283,6 +294,8 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
     const long long* __restrict__ lengths, int B, int T,
     const float* __restrict__ sv,              // saved [B*T][2][5H]
     float* __restrict__ dg, int lddg,          // [B*T][lddg], dir d gate g unit u at d 4H + g H + u
+    __bf16* __restrict__ dgb, int lddgb,       // optional bf16 copy of dg (either may be null)
+    float* __restrict__ bpart,                 // optional [B][8H]: dg summed over each sequence
     unsigned* __restrict__ work, Ctl c) {
   using G = CGeo<H, S>;
   constexpr int KCBW = G::KCBW, NW = G::NW, G4 = 4 * H, NTN = G::NTN, NC = G::NC;
@@ -296,7 +309,9 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
     lengths += s0;
     dy += (long long)s0 * T * lddy;
     sv += (long long)s0 * T * 10 * H;
-    dg += (long long)s0 * T * lddg;
+    if (dg) dg += (long long)s0 * T * lddg;
+    if (dgb) dgb += (long long)s0 * T * lddgb;
+    if (bpart) bpart += (long long)s0 * 8 * H;
   }
   unsigned* hdr = tile_hdr(work, blockIdx.z);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -315,7 +330,10 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
     const int L = sL[s];
     for (int i = tid; i < (T - L) * 64; i += NT) {
       const int c = i % 64;
-      dg[((long long)s * T + L + i / 64) * lddg + d * G4 + (c / 16) * H + u0 + c % 16] = 0.f;
+      const long long row = (long long)s * T + L + i / 64;
+      const int col = d * G4 + (c / 16) * H + u0 + c % 16;
+      if (dg) dg[row * lddg + col] = 0.f;
+      if (dgb) dgb[row * lddgb + col] = (__bf16)0.f;
     }
   }
   const __amdgpu_buffer_rsrc_t xr = slab(work, gridDim.z, blockIdx.z, G::BX);
@@ -328,10 +346,14 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
     cs[i] = p >> 4;
   }
   // processing index q of sequence s is its forward step L - 1 - q: row L-1-q (dir 0) or q
-  float in[NC][7], dcs[NC];
+  float in[NC][7], dcs[NC], bs[NC][4];
   long long grow[NC];
 #pragma unroll
-  for (int i = 0; i < NC; ++i) dcs[i] = 0.f;
+  for (int i = 0; i < NC; ++i) {
+    dcs[i] = 0.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bs[i][g] = 0.f;
+  }
   auto load_in = [&](int q) {
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
@@ -383,6 +405,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
       *(f32x4*)&part[(wv * S + nt * 16 + (lane & 15)) * PSB + 4 * (lane >> 4)] = acc[nt];
     lds_barrier();
     float o[NC][4];
+    bf16x4_ ob[NC];
     bool val[NC];
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
@@ -404,6 +427,7 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) nb[g] = (__bf16)(val[i] ? o[i][g] : 0.f);
       *(bf16x4_*)&gs[s * 64 + 4 * u] = nb;
+      ob[i] = nb;
     }
     lds_barrier();
     {  // publish dG: S sequences x 64 values, one 16-B sc1 store per thread < 8 S
@@ -419,11 +443,29 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
 #pragma unroll
     for (int i = 0; i < NC; ++i)
       if (val[i]) {
-        float* dst = dg + grow[i] * lddg + d * G4 + u0 + cu[i];
+        if (dg) {
+          float* dst = dg + grow[i] * lddg + d * G4 + u0 + cu[i];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) dst[g * H] = o[i][g];
+          for (int g = 0; g < 4; ++g) dst[g * H] = o[i][g];
+        }
+        if (dgb) {
+          __bf16* dst = dgb + grow[i] * lddgb + d * G4 + u0 + cu[i];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) dst[g * H] = ob[i][g];
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bs[i][g] += o[i][g];
       }
     if (q + 1 < maxL) load_in(q + 1);
+  }
+  if (bpart) {  // the bias gradient's per-sequence sums (b_ih and b_hh share them)
+#pragma unroll
+    for (int i = 0; i < NC; ++i)
+      if (cs[i] < B) {
+        float* dst = bpart + (long long)cs[i] * 8 * H + d * G4 + u0 + cu[i];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dst[g * H] = bs[i][g];
+      }
   }
 }
 
@@ -448,7 +490,8 @@ long long wave_bytes() { return (long long)MAX_TILES * (HDR + CGeo<H, S>::BX); }
 
 template <int H, int S>
 int launch_fwd(const float* gx, int ldg, const void* wp, const long long* lengths, int B, int T,
-               float* y, int ldy, float* sv, unsigned* work, hipStream_t st) {
+               float* y, int ldy, __bf16* y16, int ldy16, float* sv, unsigned* work,
+               hipStream_t st) {
   using G = CGeo<H, S>;
   const size_t st_lds = sizeof(float) * (4 * S * PSF + S * 6 * UW) + 2 * S * UW + 4 * S;
   static const bool attr = set_max_lds((const void*)lstm_coop_fwd_kernel<H, S>, st_lds);
@@ -462,7 +505,8 @@ int launch_fwd(const float* gx, int ldg, const void* wp, const long long* length
     if (hipMemsetAsync(wk, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
     hipLaunchKernelGGL((lstm_coop_fwd_kernel<H, S>), dim3(G::NW, 2, nt), dim3(NTS), dyn_lds(st_lds),
                        st, gx + b0 * T * ldg, ldg, (const f16x8*)wp, lengths + b0, (int)(B - b0),
-                       T, y + b0 * T * ldy, ldy, sv + b0 * T * 10 * H, wk, ctl);
+                       T, y + b0 * T * ldy, ldy, y16 ? y16 + b0 * T * ldy16 : nullptr, ldy16,
+                       sv + b0 * T * 10 * H, wk, ctl);
     ENSVS_CHECK_LAUNCH();
   }
   return ENSVS_OK;
@@ -470,7 +514,8 @@ int launch_fwd(const float* gx, int ldg, const void* wp, const long long* length
 
 template <int H, int S>
 int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengths, int B, int T,
-               const float* sv, float* dg, int lddg, unsigned* work, hipStream_t st) {
+               const float* sv, float* dg, int lddg, __bf16* dgb, int lddgb, float* bpart,
+               unsigned* work, hipStream_t st) {
   using G = CGeo<H, S>;
   const size_t st_lds = sizeof(float) * 4 * S * PSB + 2 * S * 64 + 4 * S;
   static const bool attr = set_max_lds((const void*)lstm_coop_bwd_kernel<H, S>, st_lds);
@@ -484,7 +529,9 @@ int launch_bwd(const float* dy, int lddy, const void* wp, const long long* lengt
     if (hipMemsetAsync(wk, 0, (size_t)nt * HDR, st) != hipSuccess) return ENSVS_E_HIP;
     hipLaunchKernelGGL((lstm_coop_bwd_kernel<H, S>), dim3(G::NW, 2, nt), dim3(NT), dyn_lds(st_lds),
                        st, dy + b0 * T * lddy, lddy, (const bf16x8*)wp, lengths + b0,
-                       (int)(B - b0), T, sv + b0 * T * 10 * H, dg + b0 * T * lddg, lddg, wk, ctl);
+                       (int)(B - b0), T, sv + b0 * T * 10 * H, dg ? dg + b0 * T * lddg : nullptr,
+                       lddg, dgb ? dgb + b0 * T * lddgb : nullptr, lddgb,
+                       bpart ? bpart + b0 * 8 * H : nullptr, wk, ctl);
     ENSVS_CHECK_LAUNCH();
   }
   return ENSVS_OK;
@@ -597,34 +644,56 @@ ENSVS_API int ensvs_lstm_coop_pack(const float* whh_f, const float* whh_r, int H
   return coop::pack(whh_f, whh_r, 2, H, bwd, out, (hipStream_t)stream);
 }
 
-ENSVS_API int ensvs_lstm_coop_fwd(const float* gx, int ldg, const void* wpack,
-                                  const long long* lengths, int B, int T, int H, float* y, int ldy,
-                                  float* saved, void* work, long long work_bytes, void* stream) {
+ENSVS_API int ensvs_lstm_coop_fwd_ex(const float* gx, int ldg, const void* wpack,
+                                     const long long* lengths, int B, int T, int H, float* y,
+                                     int ldy, float* saved, void* y16, int ldy16, void* work,
+                                     long long work_bytes, void* stream) {
   if (!coop_shape(B, H) || T <= 0 || ldg < 8 * H || ldy < 2 * H) return ENSVS_E_SHAPE;
   if (check_work(work, work_bytes, H, B) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
   if ((uintptr_t)y % 16 || ldy % 4 || (uintptr_t)saved % 16) return ENSVS_E_ARG;  // 16-B stores
+  if (y16 && ((uintptr_t)y16 % 8 || ldy16 % 4 || ldy16 < 2 * H)) return ENSVS_E_ARG;  // 8-B stores
   hipStream_t st = (hipStream_t)stream;
   unsigned* wk = (unsigned*)work;
+  __bf16* yb = (__bf16*)y16;
   const bool s16 = tile_seqs(B, H) == 16;
   if (H == 256)
-    return s16 ? launch_fwd<256, 16>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st)
-               : launch_fwd<256, 32>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st);
-  return s16 ? launch_fwd<512, 16>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st)
-             : launch_fwd<512, 32>(gx, ldg, wpack, lengths, B, T, y, ldy, saved, wk, st);
+    return s16 ? launch_fwd<256, 16>(gx, ldg, wpack, lengths, B, T, y, ldy, yb, ldy16, saved, wk, st)
+               : launch_fwd<256, 32>(gx, ldg, wpack, lengths, B, T, y, ldy, yb, ldy16, saved, wk, st);
+  return s16 ? launch_fwd<512, 16>(gx, ldg, wpack, lengths, B, T, y, ldy, yb, ldy16, saved, wk, st)
+             : launch_fwd<512, 32>(gx, ldg, wpack, lengths, B, T, y, ldy, yb, ldy16, saved, wk, st);
+}
+
+ENSVS_API int ensvs_lstm_coop_fwd(const float* gx, int ldg, const void* wpack,
+                                  const long long* lengths, int B, int T, int H, float* y, int ldy,
+                                  float* saved, void* work, long long work_bytes, void* stream) {
+  return ensvs_lstm_coop_fwd_ex(gx, ldg, wpack, lengths, B, T, H, y, ldy, saved, nullptr, 0, work,
+                                work_bytes, stream);
+}
+
+ENSVS_API int ensvs_lstm_coop_bwd_ex(const float* dy, int lddy, const void* wpack,
+                                     const long long* lengths, int B, int T, int H,
+                                     const float* saved, float* dg, int lddg, void* dgb, int lddgb,
+                                     float* bpart, void* work, long long work_bytes, void* stream) {
+  if (!coop_shape(B, H) || T <= 0 || lddy < 2 * H) return ENSVS_E_SHAPE;
+  if ((dg && lddg < 8 * H) || (dgb && lddgb < 8 * H)) return ENSVS_E_SHAPE;
+  if (!dg && !dgb) return ENSVS_E_ARG;
+  if (check_work(work, work_bytes, H, B) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  unsigned* wk = (unsigned*)work;
+  __bf16* gb = (__bf16*)dgb;
+  const bool s16 = tile_seqs(B, H) == 16;
+#define COOP_BWD(HH, SS) \
+  launch_bwd<HH, SS>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, gb, lddgb, bpart, wk, st)
+  if (H == 256) return s16 ? COOP_BWD(256, 16) : COOP_BWD(256, 32);
+  return s16 ? COOP_BWD(512, 16) : COOP_BWD(512, 32);
+#undef COOP_BWD
 }
 
 ENSVS_API int ensvs_lstm_coop_bwd(const float* dy, int lddy, const void* wpack,
                                   const long long* lengths, int B, int T, int H,
                                   const float* saved, float* dg, int lddg, void* work,
                                   long long work_bytes, void* stream) {
-  if (!coop_shape(B, H) || T <= 0 || lddy < 2 * H || lddg < 8 * H) return ENSVS_E_SHAPE;
-  if (check_work(work, work_bytes, H, B) || !wpack || (uintptr_t)wpack % 16) return ENSVS_E_ARG;
-  hipStream_t st = (hipStream_t)stream;
-  unsigned* wk = (unsigned*)work;
-  const bool s16 = tile_seqs(B, H) == 16;
-  if (H == 256)
-    return s16 ? launch_bwd<256, 16>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st)
-               : launch_bwd<256, 32>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st);
-  return s16 ? launch_bwd<512, 16>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st)
-             : launch_bwd<512, 32>(dy, lddy, wpack, lengths, B, T, saved, dg, lddg, wk, st);
+  if (!dg) return ENSVS_E_ARG;
+  return ensvs_lstm_coop_bwd_ex(dy, lddy, wpack, lengths, B, T, H, saved, dg, lddg, nullptr, 0,
+                                nullptr, work, work_bytes, stream);
 }

@@ -58,6 +58,15 @@ def colsum_into(dy, ld, M, N, param, groups=1, scale=1.0, off=0, yoff=0):
         call("ensvs_axpy", g.data_ptr() + 4 * off, tmp.data_ptr(), 1.0, N, stream())
 
 
+def issue(later, fn):
+    """Run fn (parameter-gradient work only) now, or append it to `later` for the caller to
+    issue once the critical input gradient is out (see FFConvLSTM._bwd)."""
+    if later is None:
+        fn()
+    else:
+        later.append(fn)
+
+
 def add_into_pair(src, N, p1, p2):
     """p1.grad[:N] += src[:N] and p2.grad[:N] += src[:N] (src: device pointer) in one launch
     (the b_ih / b_hh pairs of the recurrent layers share their gradient)."""
@@ -183,6 +192,9 @@ def ff_register(pk, ff):
 # (FF / BatchNorm+ReLU / ReLU-mask passes, MFMA LSTM recurrences).  Off: the consumers round
 # the fp32 tensors themselves -- the same bits (tests compare the two).
 BF16_COPIES = {"on": True}
+# the cooperative LSTMs' bf16 copies of y / dg and per-sequence bias partials
+# (ensvs_lstm_coop_fwd_ex / _bwd_ex); off: fp32 outputs cast by their consumers (A/B switch)
+COOP_BF16 = {"on": True}
 
 
 def bf16_copy(pk, M, C, device):
@@ -194,13 +206,14 @@ def bf16_copy(pk, M, C, device):
     return torch.empty(M, C, dtype=torch.bfloat16, device=device)
 
 
-def ff_fwd(pk, ff, X, B, T, device):
+def ff_fwd(pk, ff, X, B, T, device, x16=None):
     """The three Linear + ReLU layers.  Returns (outputs, their bf16 copies or None): each
     GEMM epilogue also writes its output rounded to bf16 -- the next layer's operand and the
-    backward's weight-gradient operand."""
+    backward's weight-gradient operand.  x16: an optional bf16 copy of X (rows zero-padded to
+    a multiple of 8 columns when the input width is not one) for the first GEMM."""
     M = B * T
     hs, hs16 = [], []
-    h, ldh = X, X.shape[1]
+    h, ldh = (X, X.shape[1]) if x16 is None else (x16, x16.shape[1])
     for i in (0, 2, 4):
         N = ff[i].weight.shape[0]
         Kc = ff[i].weight.shape[1]
@@ -214,12 +227,15 @@ def ff_fwd(pk, ff, X, B, T, device):
     return hs, hs16
 
 
-def ff_bwd(pk, ff, X, hs, hs16, dH3, B, T, device, need_dx=True):
+def ff_bwd(pk, ff, X, hs, hs16, dH3, B, T, device, need_dx=True, x16=None, dx_ld=None,
+           later=None):
     """dH3: grad of the last ReLU output.  Returns grad w.r.t. X.  The layer gradients d
     also come as bf16 copies (ReLU mask pass, ReLU-mask dgrad epilogue) for the weight
-    gradients against the forward's bf16 copies and for the dgrad GEMMs."""
+    gradients against the forward's bf16 copies and for the dgrad GEMMs.  x16: ff_fwd's bf16
+    copy of X; dx_ld: row stride of the returned grad (default: the input width); later:
+    a list that receives the weight / bias gradients as closures (issue())."""
     M = B * T
-    ins, ins16 = [X, hs[0], hs[1]], [None, hs16[0], hs16[1]]
+    ins, ins16 = [X, hs[0], hs[1]], [None if x16 is None else x16, hs16[0], hs16[1]]
     d = empty(M, dH3.shape[1], device=device)
     d16 = bf16_copy(pk, M, dH3.shape[1], device) if hs16[2] is not None else None
     call("ensvs_relu_mask", d.data_ptr(), ptr(d16), dH3.data_ptr(), hs[2].data_ptr(), d.numel(),
@@ -230,10 +246,12 @@ def ff_bwd(pk, ff, X, hs, hs16, dH3, B, T, device, need_dx=True):
         N, Kc = lay.weight.shape
         xin, xin16 = ins[2 - li], ins16[2 - li]
         if d16 is not None and xin16 is not None:
-            wgrad_into(lay.weight, d16, N, xin16, Kc, B, T, T, N, Kc)
+            issue(later, lambda w=lay.weight, g=d16, x=xin16, N=N, Kc=Kc:
+                  wgrad_into(w, g, N, x, x.shape[1], B, T, T, N, Kc))
         else:
-            wgrad_into(lay.weight, d, N, xin, xin.shape[1], B, T, T, N, Kc)
-        colsum_into(d, N, M, N, lay.bias)
+            issue(later, lambda w=lay.weight, g=d, x=xin, N=N, Kc=Kc:
+                  wgrad_into(w, g, N, x, x.shape[1], B, T, T, N, Kc))
+        issue(later, lambda g=d, N=N, b=lay.bias: colsum_into(g, N, M, N, b))
         if i == 0 and not need_dx:
             break
         nd = empty(M, Kc, device=device)
@@ -244,7 +262,9 @@ def ff_bwd(pk, ff, X, hs, hs16, dH3, B, T, device, need_dx=True):
             K.gemm([dseg], B, T, Kc, pk.bwd, nd, Kc, epi=_lib.EPI_RELU_MASK,
                    aux1=hs[2 - li - 1], ld1=Kc, ybf=nd16, ybf_ld=Kc)
         else:
-            K.gemm([dseg], B, T, Kc, pk.bwd, nd, Kc)
+            if dx_ld is not None and dx_ld != Kc:
+                nd = empty(M, dx_ld, device=device)
+            K.gemm([dseg], B, T, Kc, pk.bwd, nd, nd.shape[1])
             dx = nd
         d, d16 = nd, nd16
     return dx
@@ -343,9 +363,10 @@ def conv_fwd(pk, conv, first_segs, B, T, device, training, groups=1, save=True,
     return a, sv
 
 
-def conv_bwd(pk, conv, sv, dout, B, T, device, groups=1, first_dx=None):
+def conv_bwd(pk, conv, sv, dout, B, T, device, groups=1, first_dx=None, later=None):
     """dout: grad of the stack output.  first_dx: list of (name, K) of conv.1 segments whose
-    input gradient is wanted (returned in order as a list)."""
+    input gradient is wanted (returned in order as a list).  later: a list that receives the
+    conv weight / bias gradients as closures (issue())."""
     M = B * T
     Mg = M // groups
     d = dout
@@ -373,16 +394,18 @@ def conv_bwd(pk, conv, sv, dout, B, T, device, groups=1, first_dx=None):
                  ptr(dy16), C, stream())
         _dbg(f"conv{li}.dout", d)
         _dbg(f"conv{li}.dy", dy)
-        colsum_into(dy, C, M, C, conv[ci].bias)
+        issue(later, lambda g=dy, C=C, b=conv[ci].bias: colsum_into(g, C, M, C, b))
         w = conv[ci].weight
         col = 0
         for seg, seg16 in zip(s["segs"], s.get("segs16") or [None] * len(s["segs"])):
             if dy16 is not None and seg16 is not None:
-                wgrad_into(w, dy16, C, seg16[0], seg16[1], B, T, T, C, seg.K, taps=7, dil=1,
-                           shift0=-3, pad=_lib.PAD_REFLECT, col0=col)
+                issue(later, lambda w=w, g=dy16, C=C, x=seg16, K_=seg.K, col=col:
+                      wgrad_into(w, g, C, x[0], x[1], B, T, T, C, K_, taps=7, dil=1, shift0=-3,
+                                 pad=_lib.PAD_REFLECT, col0=col))
             else:
-                wgrad_into(w, dy, C, seg.x, seg.ld, B, T, T, C, seg.K, taps=7, dil=1, shift0=-3,
-                           pad=_lib.PAD_REFLECT, col0=col, xoff=seg.xoff)
+                issue(later, lambda w=w, g=dy, C=C, sg=seg, col=col:
+                      wgrad_into(w, g, C, sg.x, sg.ld, B, T, T, C, sg.K, taps=7, dil=1,
+                                 shift0=-3, pad=_lib.PAD_REFLECT, col0=col, xoff=sg.xoff))
             col += seg.K
         dyo = dy if dy16 is None else dy16
         if li > 0:
@@ -538,9 +561,12 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
     for l in range(lstm.num_layers):
         Kc = getattr(lstm, f"weight_ih_l{l}").shape[1]
         HP = lstm_pad(H)
-        # MFMA recurrences on unpadded H: the layer input and output also kept as bf16 for
-        # the backward's bf16-operand GEMMs (the same roundings those GEMMs apply to fp32)
-        direct = BF16_COPIES["on"] and not lstm_coop(B, H) and not HP and lstm_mfma(H)
+        # MFMA / cooperative recurrences on unpadded H: the layer input and output also kept
+        # as bf16 for the bf16-operand GEMMs that read them (the next layer's input projection,
+        # the backward's) -- the same roundings those GEMMs apply to fp32
+        coop = lstm_coop(B, H)
+        direct = BF16_COPIES["on"] and not HP and (
+            (coop and COOP_BF16["on"]) or (not coop and lstm_mfma(H)))
         x16 = None
         if direct:
             if h16 is not None:
@@ -564,11 +590,11 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
         if direct and (save or not (last or drop)):
             y16 = torch.empty(M, 2 * H, dtype=torch.bfloat16, device=device)
         saved = empty(M * 2 * 5 * (HP or H), device=device)
-        if lstm_coop(B, H):
+        if coop:
             work, nbytes = _coop_work(H, B, device)
-            call("ensvs_lstm_coop_fwd", gx.data_ptr(), 8 * H, _coop_pack(lstm, l, False).data_ptr(),
-                 lens_dev.data_ptr(), B, T, H, y.data_ptr(), 2 * H, saved.data_ptr(),
-                 work.data_ptr(), nbytes, stream())
+            call("ensvs_lstm_coop_fwd_ex", gx.data_ptr(), 8 * H,
+                 _coop_pack(lstm, l, False).data_ptr(), lens_dev.data_ptr(), B, T, H, y.data_ptr(),
+                 2 * H, saved.data_ptr(), ptr(y16), 2 * H, work.data_ptr(), nbytes, stream())
         elif HP:
             gxp = empty(M, 8 * HP, device=device)
             _regroup(gx, 8 * H, gxp, 8 * HP, M, 8, H, HP)
@@ -609,7 +635,9 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
     return h, sv
 
 
-def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
+def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True, later=None):
+    """Packed bidirectional LSTM backward; returns the input gradient.  later: a list that
+    receives each layer's weight / bias gradients as closures (issue())."""
     M = B * T
     H = lstm.hidden_size
     d = dY
@@ -619,7 +647,7 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
         Kc = getattr(lstm, f"weight_ih_l{l}").shape[1]
         x16, y16 = s.get("x16"), s.get("y16")
         # bf16 dg for the GEMMs (fp32 dg only when the layer input has no bf16 copy) and the
-        # bias gradient's per-sequence partial sums, all from the MFMA recurrence
+        # bias gradient's per-sequence partial sums, all from the MFMA / cooperative recurrence
         dgb = bpart = None
         if y16 is not None:
             dgb = torch.empty(M, 8 * H, dtype=torch.bfloat16, device=device)
@@ -627,8 +655,9 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
         dg = empty(M, 8 * H, device=device) if dgb is None or x16 is None else None
         if lstm_coop(B, H):
             work, nbytes = _coop_work(H, B, device)
-            call("ensvs_lstm_coop_bwd", d.data_ptr(), 2 * H, _coop_pack(lstm, l, True).data_ptr(),
-                 lens_dev.data_ptr(), B, T, H, s["saved"].data_ptr(), dg.data_ptr(), 8 * H,
+            call("ensvs_lstm_coop_bwd_ex", d.data_ptr(), 2 * H,
+                 _coop_pack(lstm, l, True).data_ptr(), lens_dev.data_ptr(), B, T, H,
+                 s["saved"].data_ptr(), ptr(dg), 8 * H, ptr(dgb), 8 * H, ptr(bpart),
                  work.data_ptr(), nbytes, stream())
         elif s.get("hp"):
             HP = s["hp"]
@@ -662,21 +691,26 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True):
         gy, yy = (dgb, y16) if dgb is not None else (dg, s["y"])
         gi, xi, ldi = (dgb, x16, x16.shape[1]) if x16 is not None and dgb is not None else \
             (dg, s["x"], s["ldx"])
-        for di, sfx in enumerate(("", "_reverse")):
-            wgrad_into(getattr(lstm, f"weight_ih_l{l}{sfx}"), gi, 8 * H, xi, ldi, B, T, T,
-                       4 * H, Kc, dyoff=di * 4 * H)
-            # h_{t-1} in processing order: t-1 forward, t+1 reverse (zero outside [0, L))
-            wgrad_into(getattr(lstm, f"weight_hh_l{l}{sfx}"), gy, 8 * H, yy, 2 * H, B, T, T,
-                       4 * H, H, shift0=(-1 if di == 0 else 1), dyoff=di * 4 * H, xoff=di * H)
-        # b_ih and b_hh of both directions share one gradient: the column sums of dg, once
-        bsum = empty(8 * H, device=device)
-        if bpart is not None:
-            K.colsum(bpart, 8 * H, B, 8 * H, bsum)
-        else:
-            K.colsum(dg, 8 * H, M, 8 * H, bsum)
-        for di, sfx in enumerate(("", "_reverse")):
-            add_into_pair(bsum.data_ptr() + di * 16 * H, 4 * H, getattr(lstm, f"bias_ih_l{l}{sfx}"),
-                          getattr(lstm, f"bias_hh_l{l}{sfx}"))
+
+        def params(l=l, Kc=Kc, gy=gy, yy=yy, gi=gi, xi=xi, ldi=ldi, dg=dg, bpart=bpart):
+            for di, sfx in enumerate(("", "_reverse")):
+                wgrad_into(getattr(lstm, f"weight_ih_l{l}{sfx}"), gi, 8 * H, xi, ldi, B, T, T,
+                           4 * H, Kc, dyoff=di * 4 * H)
+                # h_{t-1} in processing order: t-1 forward, t+1 reverse (zero outside [0, L))
+                wgrad_into(getattr(lstm, f"weight_hh_l{l}{sfx}"), gy, 8 * H, yy, 2 * H, B, T, T,
+                           4 * H, H, shift0=(-1 if di == 0 else 1), dyoff=di * 4 * H,
+                           xoff=di * H)
+            # b_ih and b_hh of both directions share one gradient: the column sums of dg, once
+            bsum = empty(8 * H, device=device)
+            if bpart is not None:
+                K.colsum(bpart, 8 * H, B, 8 * H, bsum)
+            else:
+                K.colsum(dg, 8 * H, M, 8 * H, bsum)
+            for di, sfx in enumerate(("", "_reverse")):
+                add_into_pair(bsum.data_ptr() + di * 16 * H, 4 * H,
+                              getattr(lstm, f"bias_ih_l{l}{sfx}"),
+                              getattr(lstm, f"bias_hh_l{l}{sfx}"))
+        issue(later, params)
         if l == 0 and not need_dx:
             break
         nd = empty(M, Kc, device=device)

@@ -142,9 +142,11 @@ class FFConvLSTM(BaseModel):
         pk.bias_vec("fc.b", self.fc.bias)
 
     def _fwd(self, sources, B, T, lens_dev, spk_seq=None, spk_ld=0, training=None,
-             lstm_masks=None, save=True, bn_updates=1):
+             lstm_masks=None, save=True, bn_updates=1, x16=None):
         """sources: [(tensor, ld, col_offset, ncols)] of the logical input columns (without
-        phoneme embedding: one (X, ldx, 0, in_dim) source is read in place).
+        phoneme embedding: one (X, ldx, 0, in_dim) source is read in place); x16: an optional
+        bf16 copy of that single source (rows zero-padded to a multiple of 8 columns), the
+        first FF GEMM's operand and its weight gradient's.
         Returns (out (B*T, out_dim), saved state)."""
         training = self.training if training is None else training
         pk = self._packs.ensure(self, self._register)
@@ -156,7 +158,10 @@ class FFConvLSTM(BaseModel):
             if spk_seq is not None:
                 raise NotImplementedError("FFConvLSTM(embed_dim=None) with spk_embs")
             X0, esv = _plain_input(sources, self.in_dim, B * T, dev), None
-        hs, hs16 = Ly.ff_fwd(pk, self.ff, X0, B, T, dev)
+        if x16 is not None and (self.embed_dim is not None or
+                                not Ly.K.bf16_operands(pk.fwd, B * T)):
+            x16 = None
+        hs, hs16 = Ly.ff_fwd(pk, self.ff, X0, B, T, dev, x16=x16)
         F = hs[2].shape[1]
         a, csv = Ly.conv_fwd(pk, self.conv, [("", hs[2], F, F, 0)], B, T, dev, training,
                              save=save, running_updates=bn_updates,
@@ -173,28 +178,36 @@ class FFConvLSTM(BaseModel):
         H2 = 2 * self.lstm.hidden_size
         Ly.K.gemm([Ly.K.Seg(y, H2, H2, pk["fc"], T)], B, T, self.out_dim, pk.fwd, out,
                   self.out_dim, **pk.bias_ptr_args("fc.b"))
-        st = dict(X0=X0, esv=esv, hs=hs, hs16=hs16, csv=csv, lsv=lsv, y=y, B=B, T=T,
+        st = dict(X0=X0, X16=x16, esv=esv, hs=hs, hs16=hs16, csv=csv, lsv=lsv, y=y, B=B, T=T,
                   lens=lens_dev) \
             if save else None
         return out, st
 
-    def _bwd(self, st, dout, want_spk=False):
+    def _bwd(self, st, dout, want_spk=False, dx_ld=None, later=None):
         """dout (B*T, out_dim).  Accumulates parameter grads; returns (dX0 per-frame input
-        grad (B*T, E), dspk per-sequence (B, E) or None)."""
+        grad (B*T, E) -- rows of stride dx_ld when given --, dspk per-sequence (B, E) or
+        None).  later (a list): the weight and bias gradients are appended to it as closures
+        instead of being issued between the input-gradient launches -- the caller issues
+        them once dX0 is out (the SeparateF0 decoders: the encoder's backward waits for dX0
+        only)."""
         pk = self._packs
         dev = dout.device
         B, T = st["B"], st["T"]
         M = B * T
         H2 = 2 * self.lstm.hidden_size
-        Ly.wgrad_into(self.fc.weight, dout, self.out_dim, st["y"], H2, B, T, T, self.out_dim, H2)
-        Ly.colsum_into(dout, self.out_dim, M, self.out_dim, self.fc.bias)
+        D = self.out_dim
+        Ly.issue(later, lambda: (
+            Ly.wgrad_into(self.fc.weight, dout, D, st["y"], H2, B, T, T, D, H2),
+            Ly.colsum_into(dout, D, M, D, self.fc.bias)))
         dy = empty(M, H2, device=dev)
         Ly.K.gemm([Ly.K.Seg(dout, self.out_dim, self.out_dim, pk["fc^T"], T)], B, T, H2, pk.bwd,
                   dy, H2)
-        da = Ly.lstm_bwd(pk, self.lstm, st["lsv"], dy, B, T, st["lens"], dev)
+        da = Ly.lstm_bwd(pk, self.lstm, st["lsv"], dy, B, T, st["lens"], dev, later=later)
         F = st["hs"][2].shape[1]
-        (dh3,) = Ly.conv_bwd(pk, self.conv, st["csv"], da, B, T, dev, first_dx=[("", F)])
-        dX0 = Ly.ff_bwd(pk, self.ff, st["X0"], st["hs"], st["hs16"], dh3, B, T, dev)
+        (dh3,) = Ly.conv_bwd(pk, self.conv, st["csv"], da, B, T, dev, first_dx=[("", F)],
+                             later=later)
+        dX0 = Ly.ff_bwd(pk, self.ff, st["X0"], st["hs"], st["hs16"], dh3, B, T, dev,
+                        x16=st.get("X16"), dx_ld=dx_ld, later=later)
         dspk = None
         if self.embed_dim is None:
             return dX0, None
@@ -350,10 +363,22 @@ class MultiTrackLSTMEncoder(BaseModel):
         ld = N if ld is None else ld
         H2 = 2 * self.lstm.hidden_size
         E = self.embed_dim
-        Ly.wgrad_into(self.hidden2out.weight, dout, ld, st["y"], H2, B, T, T, N, H2)
+        # the output gradient rounded to bf16 once, for the weight gradient (against the last
+        # recurrence's bf16 output copy) and the input-gradient GEMM, when both can take it
+        y16 = st["lsv"][-1].get("y16") if st["lsv"] else None
+        d16 = None
+        if (y16 is not None and N % 8 == 0 and Ly.K.bf16_operands(pk.bwd, M)
+                and Ly.K._castable(Ly.K.Seg(dout, ld, N, None, T))):
+            d16 = Ly.K.cast_bf16(dout, ld, N, M)
+        if d16 is not None:
+            Ly.wgrad_into(self.hidden2out.weight, d16, N, y16, H2, B, T, T, N, H2)
+        else:
+            Ly.wgrad_into(self.hidden2out.weight, dout, ld, st["y"], H2, B, T, T, N, H2)
         Ly.colsum_into(dout, ld, M, N, self.hidden2out.bias)
         dy = empty(M, H2, device=dev)
-        Ly.K.gemm([Ly.K.Seg(dout, ld, N, pk["h2o^T"], T)], B, T, H2, pk.bwd, dy, H2)
+        seg = Ly.K.Seg(dout, ld, N, pk["h2o^T"], T) if d16 is None else \
+            Ly.K.Seg(d16, N, N, pk["h2o^T"], T)
+        Ly.K.gemm([seg], B, T, H2, pk.bwd, dy, H2)
         dX = Ly.lstm_bwd(pk, self.lstm, st["lsv"], dy, B, T, st["lens"], dev)
         dspk = [torch.zeros(B, E, device=dev) if want_spk else None for _ in range(2)]
         for k in range(2):

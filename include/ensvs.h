@@ -149,7 +149,10 @@ int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx, const fl
                      long long sk, long long sj, int accum, float scale, int dtype, void* stream);
 
 /* ensvs_conv_wgrad with bf16 operands (dy, x already rounded to bf16, radd folded into x;
- * N, K, ldy, ldx multiples of 8): identical bits, operands staged by global_load_lds. */
+ * N, ldy, ldx multiples of 8): identical bits, operands staged by global_load_lds.  K need not
+ * be a multiple of 8 when every x row holds K rounded up to 8 readable columns (ldx >= that):
+ * the columns past K are read in the last 16-B chunk and only feed outputs that are never
+ * written (the SeparateF0 decoders' 1 026-column input, zero-padded to 1 032). */
 int ensvs_conv_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, int B, int Tout,
                           int Tin, int N, int K, int taps, int dil, int shift0, int pad, int splits,
                           float* part, float* dst, long long sn, long long sk, long long sj,
@@ -276,6 +279,20 @@ int ensvs_lstm_coop_fwd(const float* gx, int ldg, const void* wpack, const long 
 int ensvs_lstm_coop_bwd(const float* dy, int lddy, const void* wpack, const long long* lengths,
                         int B, int T, int H, const float* saved, float* dg, int lddg, void* work,
                         long long work_bytes, void* stream);
+/* The same launches with the optional outputs of ensvs_lstm_mfma_fwd / _bwd for the layer's
+ * bf16-operand GEMMs (the next layer's input projection, the weight gradients, the input
+ * gradient): y16 (bf16 [B*T][ldy16], 8-B aligned, ldy16 % 4 == 0) = y rounded to bf16, written
+ * by the forward's service wave with y; dgb (bf16 [B*T][lddgb]) = dg rounded to bf16 -- the
+ * bits the backward already hands off -- with dg itself optional (one of the two required);
+ * bpart (fp32 [B][8H]) = dg summed over each sequence's steps, the bias gradient's partials.
+ * Null optional pointers give the plain entry points above. */
+int ensvs_lstm_coop_fwd_ex(const float* gx, int ldg, const void* wpack, const long long* lengths,
+                           int B, int T, int H, float* y, int ldy, float* saved, void* y16,
+                           int ldy16, void* work, long long work_bytes, void* stream);
+int ensvs_lstm_coop_bwd_ex(const float* dy, int lddy, const void* wpack,
+                           const long long* lengths, int B, int T, int H, const float* saved,
+                           float* dg, int lddg, void* dgb, int lddgb, float* bpart, void* work,
+                           long long work_bytes, void* stream);
 
 /* Residual-F0 AR decoder (acoustic_models/tacotron_f0.py:126-237 with
  * ZoneOutCell(LSTMCell), tacotron/decoder.py:20-48).  H in {16,...,256}, T % 4 == 0.

@@ -92,6 +92,16 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False, mfma=False):
         call("ensvs_lstm_coop_fwd", gx_d.data_ptr(), 8 * H, wpf.data_ptr(), lens.data_ptr(), B, T,
              H, y.data_ptr(), 2 * H, saved.data_ptr(), cwork.data_ptr(), nbytes, st)
         assert resident()
+        # the launch with the bf16 copy: the same y bits, and y rounded to nearest even in the
+        # copy, padded frames included (zeros)
+        y2 = torch.full_like(y, float("nan"))
+        yb = torch.full((B * T, 2 * H), float("nan"), dtype=torch.bfloat16, device=dev)
+        call("ensvs_lstm_coop_fwd_ex", gx_d.data_ptr(), 8 * H, wpf.data_ptr(), lens.data_ptr(), B,
+             T, H, y2.data_ptr(), 2 * H, saved.data_ptr(), yb.data_ptr(), 2 * H, cwork.data_ptr(),
+             nbytes, st)
+        assert resident()
+        assert torch.equal(y2.view(torch.int32), y.view(torch.int32))
+        assert torch.equal(yb.view(torch.int16), y.to(torch.bfloat16).view(torch.int16))
     elif mfma:
         assert query("ensvs_lstm_mfma_supported", H) == 1
         wpf = torch.empty(2 * 4 * H * H, dtype=torch.float16, device=dev)
@@ -119,6 +129,17 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False, mfma=False):
         call("ensvs_lstm_coop_bwd", gy_d.data_ptr(), 2 * H, wpb.data_ptr(), lens.data_ptr(), B, T,
              H, saved.data_ptr(), dg.data_ptr(), 8 * H, cwork.data_ptr(), nbytes, st)
         assert resident()
+        # the bf16 copy alone (no fp32 dg) plus the per-sequence bias partials, as the MFMA
+        # recurrence's: dg rounded, and sums of dg's rows within 1e-5 of its column sums
+        dgb = torch.full((B * T, 8 * H), float("nan"), dtype=torch.bfloat16, device=dev)
+        bsum = torch.full((B, 8 * H), float("nan"), device=dev)
+        call("ensvs_lstm_coop_bwd_ex", gy_d.data_ptr(), 2 * H, wpb.data_ptr(), lens.data_ptr(), B,
+             T, H, saved.data_ptr(), None, 0, dgb.data_ptr(), 8 * H, bsum.data_ptr(),
+             cwork.data_ptr(), nbytes, st)
+        assert resident()
+        assert torch.equal(dgb.view(torch.int16), dg.to(torch.bfloat16).view(torch.int16))
+        want = dg.view(B, T, 8 * H).double().sum(1)
+        assert (bsum.double() - want).abs().max().item() <= 1e-5 * want.abs().max().item() + 1e-6
     elif mfma:
         dg.fill_(float("nan"))
         dgb = torch.full((B * T, 8 * H), float("nan"), dtype=torch.bfloat16, device=dev)

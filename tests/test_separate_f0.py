@@ -15,7 +15,8 @@ import torch
 
 from oracle import ensvs_oracle as O
 from ensemble_svs_with_interactions_amd import configs, engine
-from golden_util import _pre_bn_bias, check_grad_summary, load_case, params_from_shapes, rel
+from golden_util import (_pre_bn_bias, check_grad_summary, load_case, params_from_shapes, rel,
+                         rel_l2)
 
 
 def _cfg(tiny):
@@ -256,3 +257,59 @@ def test_recipe_size_graph_replay_equals_eager_bf16():
     assert graphed == eager, (graphed, eager)
     assert all(np.isfinite(v) for step in eager for v in step)
     assert torch.equal(o_g.flat, o_e.flat) and torch.equal(o_g.m, o_e.m)
+
+
+@pytest.mark.gpu
+def test_bf16_copies_match_cast_by_consumers():
+    """Recipe-size model, bf16 GEMM operands: the production step -- the decoders' input in
+    zero-padded 1 032-column rows with one bf16 copy (acoustic_models.DEC_PAD), the
+    cooperative LSTMs' bf16 copies of y / dg and per-sequence bias partials
+    (layers.COOP_BF16) -- against the same step with both off, where every consumer rounds the
+    fp32 tensors itself.  The forward is the same bits (the same roundings feed the same
+    GEMMs); the gradients agree within 1e-4 (rel L2, the whole flat gradient and each
+    parameter with a norm above 1e-3 of the largest): the bias sums run in another order and
+    the decoders' 1 026-column weight gradient runs on the bf16-operand kernel.  The
+    decoders' parameter gradients issued after their input gradients (DEC_LATER) or between
+    them: the same bits."""
+    from ensemble_svs_with_interactions_amd import acoustic_models as AM, data
+    from ensemble_svs_with_interactions_amd import layers as Ly
+    from ensemble_svs_with_interactions_amd.train import FusedAdam, train_step
+    engine.set_gemm_precision("bf16")
+    P, T = 8, 256
+    lens = [T, 240, 200, 256, 128, 64, 180, 252]
+    b = data.synthetic_batch(P, T, 91, lengths=lens)
+    g = lambda k: torch.from_numpy(b[k]).cuda().contiguous()  # noqa: E731
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    keep = [((torch.rand(P * T // 4, device="cuda", generator=gen) < 0.5).float() * 2.0)
+            for _ in range(2)]
+    res = []
+    try:
+        for on, later in ((True, True), (False, True), (True, False)):
+            AM.DEC_PAD["on"] = on
+            Ly.COOP_BF16["on"] = on
+            AM.DEC_LATER["on"] = later
+            torch.manual_seed(0)
+            m = configs.instantiate(_cfg(False)).cuda()
+            for sub in (m.mgc_model, m.vuv_model, m.bap_model, m.encoder):
+                sub.lstm.dropout = 0.0
+            opt = FusedAdam(m)
+            loss, norm = train_step(m, opt, g("x_main"), g("x_sub"), g("y_main"), g("spk_main"),
+                                    g("spk_sub"), lens, draws=dict(lf0_main=keep[0],
+                                                                    lf0_sub=keep[1]))
+            torch.cuda.synchronize()
+            grads = {k: p.grad.detach().clone() for k, p in m.named_parameters()
+                     if p.grad is not None}
+            res.append((loss.item(), norm.item(), opt.gflat.detach().clone(), grads))
+    finally:
+        AM.DEC_PAD["on"] = True
+        Ly.COOP_BF16["on"] = True
+        AM.DEC_LATER["on"] = True
+    (l1, n1, g1, p1), (l0, n0, g0, p0), (l2, n2, g2, _) = res
+    assert (l2, n2) == (l1, n1) and torch.equal(g2, g1)
+    assert l1 == l0, (l1, l0)
+    assert abs(n1 - n0) <= 1e-4 * n0
+    assert rel_l2(g1.cpu(), g0.cpu()) < 1e-4
+    big = max(v.norm().item() for v in p0.values())
+    bad = [(k, rel_l2(p1[k].cpu(), v.cpu())) for k, v in p0.items()
+           if v.norm().item() > 1e-3 * big and rel_l2(p1[k].cpu(), v.cpu()) > 1e-4]
+    assert not bad, bad[:5]

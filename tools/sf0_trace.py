@@ -1,4 +1,5 @@
-"""Graph-replayed SeparateF0 training steps for a kernel trace (dev tool):
+"""Graph-replayed SeparateF0 (MODEL=main: the bench's main line) training steps for a
+kernel trace (dev tool):
    rocprofv3 --kernel-trace --output-format csv -d DIR -o sf0 -- python3 tools/sf0_trace.py
 then  python3 tools/sf0_trace.py --show DIR/sf0_kernel_trace.csv  prints, for the step between
 the last two Adam launches, every queue's kernels in start order (ms from the step start,
@@ -53,12 +54,16 @@ def run(steps=6):
     from ensemble_svs_with_interactions_amd import configs, data
     from ensemble_svs_with_interactions_amd.train import FusedAdam, GraphedTrainStep
     dev = torch.device("cuda:0")
-    torch.manual_seed(20250324)
-    model = configs.instantiate(configs.multitrack_separate_f0(num_speakers=4)).to(dev)
+    if os.environ.get("MODEL") == "main":  # the bench's main line (multi-track diffusion)
+        torch.manual_seed(20250321)
+        model = configs.instantiate(configs.multitrack_diffusion(num_speakers=4)).to(dev)
+    else:
+        torch.manual_seed(20250324)
+        model = configs.instantiate(configs.multitrack_separate_f0(num_speakers=4)).to(dev)
     opt = FusedAdam(model, lr=1e-4, clip_norm=1.0)
     P = int(os.environ.get("P", 30))
     T = int(os.environ.get("T", 1024))
-    b = data.synthetic_batch(P, T, 4000)
+    b = data.synthetic_batch(P, T, 1000 if os.environ.get("MODEL") == "main" else 4000)
     g = lambda k: torch.from_numpy(b[k]).to(dev).contiguous()  # noqa: E731
     step = GraphedTrainStep(model, opt, g("x_main"), g("x_sub"), g("y_main"), g("spk_main"),
                             g("spk_sub"), b["lengths"].tolist(), warmup=1).step

@@ -149,6 +149,9 @@ SIGNATURES = {
     "ensvs_gather_rows": [c_vp, c_vp, c_int, c_int, c_vp, c_vp],
     "ensvs_bn_finalize": [c_vp, c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_vp, c_float, c_int,
                           c_vp],
+    "ensvs_bn_stats_part_floats": [c_ll, c_int, c_ll],
+    "ensvs_bn_stats": [c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_ll, c_float, c_vp, c_vp, c_vp, c_vp,
+                       c_vp, c_float, c_int, c_vp, c_vp],
     "ensvs_bn_apply_relu": [c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                             c_vp, c_int, c_vp],
     "ensvs_bn_bwd": [c_vp, c_int, c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -244,7 +247,8 @@ RESTYPES = {"ensvs_embed_bwd_workspace": c_ll, "ensvs_usf_source_workspace": c_l
             "ensvs_lstm_coop_work_bytes": c_ll, "ensvs_lstm_coop_supported": ctypes.c_int,
             "ensvs_lstm_mfma_supported": ctypes.c_int,
             "ensvs_ardec_coop_work_bytes": c_ll, "ensvs_ardec_coop_supported": ctypes.c_int,
-            "ensvs_coop_error_word": c_vp, "ensvs_colsum_batch_part_floats": c_ll}
+            "ensvs_coop_error_word": c_vp, "ensvs_colsum_batch_part_floats": c_ll,
+            "ensvs_bn_stats_part_floats": c_ll}
 
 _lib = None
 

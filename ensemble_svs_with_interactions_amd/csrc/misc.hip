@@ -14,6 +14,8 @@ namespace {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (n); \
        i += (long long)gridDim.x * blockDim.x)
 
+constexpr int BN_STATS_MAX_SPLITS = 256;
+
 inline int grid_for(long long n) { return (int)std::min<long long>(8192, (n + 255) / 256); }
 
 // ------------------------------------------------------------- embeddings
@@ -246,6 +248,151 @@ __global__ void bn_finalize_kernel(float* __restrict__ mean, float* __restrict__
     }
   }
   if (update) {
+    rmean[c] = rm;
+    rvar[c] = rv;
+  }
+}
+
+// BatchNorm training statistics in two launches (round 5; were two column-sum launch pairs and
+// bn_finalize).  bn_stats_partial: per (64-column block, row split s, group g) the split's
+// column sums and its sums of squared deviations from the split's own mean (the split's rows
+// are read twice, the second time from L2); part[g][s] = [sum (C) | M2 (C)].  bn_stats_final:
+// per column, the group's mean (split sums added in a fixed order in double) and biased
+// variance by Chan's merge of the splits (double, fixed order): var = (sum_s M2_s +
+// n_s (mean_s - mean)^2) / Mg -- deterministic, and as exact as the two-pass form -- then
+// bn_finalize's rstd and running-statistic updates (`updates` EMA steps per group, the
+// module's num_batches_tracked advanced by G * updates).
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __restrict__ y, int ld,
+                                                               int Mg, int C, int rps, int vec,
+                                                               float* __restrict__ part) {
+  __shared__ f32x4 red[16][17];
+  __shared__ f32x4 tot[16];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col = blockIdx.x * 64 + cq * 4;
+  const int s = blockIdx.y, S = gridDim.y;
+  y += (long long)blockIdx.z * Mg * ld;
+  float* pg = part + ((long long)blockIdx.z * S + s) * 2 * C;
+  const int r0 = s * rps, r1 = min(Mg, r0 + rps);
+  auto ld4 = [&](int r) -> f32x4 {
+    const float* q = y + (long long)r * ld + col;
+    f32x4 v;
+    if (vec && col + 3 < C) {
+      v = *(const f32x4*)q;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = col + e < C ? q[e] : 0.f;
+    }
+    return v;
+  };
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (col < C) {
+    int r = r0 + rl;
+    for (; r + 48 < r1; r += 64) {
+      const f32x4 v0 = ld4(r), v1 = ld4(r + 16), v2 = ld4(r + 32), v3 = ld4(r + 48);
+      acc += (v0 + v1) + (v2 + v3);
+    }
+    for (; r < r1; r += 16) acc += ld4(r);
+  }
+  red[rl][cq] = acc;
+  __syncthreads();
+  if (rl == 0) {
+    f32x4 t = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][cq];
+    tot[cq] = t;
+  }
+  __syncthreads();
+  const f32x4 sum = tot[cq];
+  const float inv_n = 1.f / (float)max(r1 - r0, 1);
+  const f32x4 mu = sum * inv_n;
+  f32x4 q2 = {0.f, 0.f, 0.f, 0.f};
+  if (col < C) {
+    int r = r0 + rl;
+    for (; r + 48 < r1; r += 64) {
+      const f32x4 v0 = ld4(r) - mu, v1 = ld4(r + 16) - mu, v2 = ld4(r + 32) - mu,
+                  v3 = ld4(r + 48) - mu;
+      q2 += (v0 * v0 + v1 * v1) + (v2 * v2 + v3 * v3);
+    }
+    for (; r < r1; r += 16) {
+      const f32x4 v = ld4(r) - mu;
+      q2 += v * v;
+    }
+  }
+  red[rl][cq] = q2;  // every lane has read red (the sums) before the barrier above
+  __syncthreads();
+  if (rl == 0) {
+    f32x4 t = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][cq];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (col + e < C) {
+        pg[col + e] = sum[e];
+        pg[C + col + e] = t[e];
+      }
+  }
+}
+
+// 16 columns x 16 split lanes per block: lane sl takes splits sl, sl + 16, ..., and the 16
+// lane totals are added in lane order (fixed: deterministic)
+__global__ __launch_bounds__(256) void bn_stats_final_kernel(
+    const float* __restrict__ part, int S, int G, int C, int Mg, int rps, float eps,
+    float* __restrict__ mean, float* __restrict__ var, float* __restrict__ rstd,
+    float* __restrict__ rmean, float* __restrict__ rvar, float momentum, int updates,
+    long long* __restrict__ nbt) {
+  __shared__ double red[16][17];
+  __shared__ double mus[16];
+  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && updates > 0 && nbt) nbt[0] += (long long)G * updates;
+  const double inv_rps = 1.0 / (double)rps;
+  for (int g = 0; g < G; ++g) {
+    const float* pg = part + (long long)g * S * 2 * C;
+    double a = 0.0;
+    if (c < C)
+      for (int s = sl; s < S; s += 16) a += (double)pg[(long long)s * 2 * C + c];
+    red[sl][cl] = a;
+    __syncthreads();
+    if (sl == 0) {
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t += red[i][cl];
+      mus[cl] = t / (double)Mg;
+    }
+    __syncthreads();
+    const double mu = mus[cl];
+    double m2 = 0.0;
+    if (c < C)
+      for (int s = sl; s < S; s += 16) {
+        const int n = min(rps, Mg - s * rps);
+        if (n <= 0) continue;
+        const double ms = (double)pg[(long long)s * 2 * C + c] *
+                          (n == rps ? inv_rps : 1.0 / (double)n);
+        const double d = ms - mu;
+        m2 += (double)pg[(long long)s * 2 * C + C + c] + (double)n * d * d;
+      }
+    red[sl][cl] = m2;
+    __syncthreads();
+    if (sl == 0 && c < C) {
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t += red[i][cl];
+      const float vb = (float)(t / (double)Mg);
+      mean[g * C + c] = (float)mu;
+      var[g * C + c] = vb;
+      rstd[g * C + c] = 1.f / sqrtf(vb + eps);
+    }
+    __syncthreads();
+  }
+  if (sl == 0 && c < C && updates > 0) {  // bn_finalize's order: every group, `updates` times
+    float rm = rmean[c], rv = rvar[c];
+    for (int u = 0; u < updates; ++u)
+      for (int g = 0; g < G; ++g) {
+        const float mu = mean[g * C + c], vb = var[g * C + c];
+        const float vu = Mg > 1 ? vb * (float)Mg / (float)(Mg - 1) : vb;
+        rm = (1.f - momentum) * rm + momentum * mu;
+        rv = (1.f - momentum) * rv + momentum * vu;
+      }
     rmean[c] = rm;
     rvar[c] = rv;
   }
@@ -1040,6 +1187,40 @@ ENSVS_API int ensvs_bn_finalize(float* mean, float* var, int G, int C, long long
                                 void* stream) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream,
                      mean, var, G, C, Mg, eps, rstd, rmean, rvar, momentum, update);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+// row splits of ensvs_bn_stats (as the column sums: >= ~2048 blocks, >= 128 rows per split)
+static int bn_stats_splits(long long Mg, int C, int G) {
+  return (int)std::max<long long>(
+      1, std::min<long long>({(long long)BN_STATS_MAX_SPLITS, Mg / 128,
+                              (long long)cdiv(2048, cdiv(C, 64) * G)}));
+}
+
+ENSVS_API long long ensvs_bn_stats_part_floats(long long M, int C, long long Mg) {
+  if (M <= 0 || C <= 0 || Mg <= 0 || M % Mg) return 0;
+  const int G = (int)(M / Mg);
+  return (long long)G * bn_stats_splits(Mg, C, G) * 2 * C;
+}
+
+ENSVS_API int ensvs_bn_stats(const float* y, int ldy, long long M, int C, long long Mg,
+                             float* part, long long part_floats, float eps, float* mean, float* var,
+                             float* rstd, float* rmean, float* rvar, float momentum, int updates,
+                             long long* nbt, void* stream) {
+  if (M <= 0 || C <= 0 || Mg <= 0 || M % Mg || ldy < C || Mg > INT32_MAX) return ENSVS_E_SHAPE;
+  const int G = (int)(M / Mg);
+  const int S = bn_stats_splits(Mg, C, G);
+  if (!part || part_floats < (long long)G * S * 2 * C || !mean || !var || !rstd) return ENSVS_E_ARG;
+  if (updates > 0 && (!rmean || !rvar)) return ENSVS_E_ARG;
+  const int rps = (int)cdiv(Mg, (long long)S);
+  const int vec = (ldy % 4 == 0) && (((uintptr_t)y & 15) == 0);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(cdiv(C, 64), S, G), dim3(256), 0, st, y, ldy,
+                     (int)Mg, C, rps, vec, part);
+  ENSVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_stats_final_kernel, dim3(cdiv(C, 16)), dim3(256), 0, st, part, S, G, C,
+                     (int)Mg, rps, eps, mean, var, rstd, rmean, rvar, momentum, updates, nbt);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }

@@ -195,6 +195,9 @@ BF16_COPIES = {"on": True}
 # the cooperative LSTMs' bf16 copies of y / dg and per-sequence bias partials
 # (ensvs_lstm_coop_fwd_ex / _bwd_ex); off: fp32 outputs cast by their consumers (A/B switch)
 COOP_BF16 = {"on": True}
+# BatchNorm training statistics by ensvs_bn_stats (two launches: split sums / deviations, then
+# the merge + rstd + running updates) or by two column sums + ensvs_bn_finalize (A/B switch)
+BN_STATS = {"on": True}
 
 
 def bf16_copy(pk, M, C, device):
@@ -335,15 +338,26 @@ def conv_fwd(pk, conv, first_segs, B, T, device, training, groups=1, save=True,
         frozen = training and not bn.training
         if training and not frozen:
             var = empty(groups, C, device=device)
-            K.colsum(y, C, Mg, C, mean, groups=groups, scale=1.0 / Mg)
-            K.colsum(y, C, Mg, C, var, groups=groups, mean=mean, scale=1.0 / Mg)
             upd = int(update_running and bn.track_running_stats)
-            for _ in range(max(1, running_updates if upd else 1)):
-                call("ensvs_bn_finalize", mean.data_ptr(), var.data_ptr(), groups, C, Mg,
-                     float(bn.eps), rstd.data_ptr(), bn.running_mean.data_ptr(),
-                     bn.running_var.data_ptr(), float(bn.momentum), upd, stream())
-                if upd:
-                    bn.num_batches_tracked.add_(groups)
+            if BN_STATS["on"]:
+                # statistics, rstd, running updates and num_batches_tracked in two launches
+                n = query("ensvs_bn_stats_part_floats", M, C, Mg)
+                part = K.scratch(n, device, key="bnstats")
+                call("ensvs_bn_stats", y.data_ptr(), C, M, C, Mg, part.data_ptr(), n,
+                     float(bn.eps), mean.data_ptr(), var.data_ptr(), rstd.data_ptr(),
+                     bn.running_mean.data_ptr() if upd else None,
+                     bn.running_var.data_ptr() if upd else None, float(bn.momentum),
+                     max(1, running_updates) if upd else 0,
+                     bn.num_batches_tracked.data_ptr() if upd else None, stream())
+            else:
+                K.colsum(y, C, Mg, C, mean, groups=groups, scale=1.0 / Mg)
+                K.colsum(y, C, Mg, C, var, groups=groups, mean=mean, scale=1.0 / Mg)
+                for _ in range(max(1, running_updates if upd else 1)):
+                    call("ensvs_bn_finalize", mean.data_ptr(), var.data_ptr(), groups, C, Mg,
+                         float(bn.eps), rstd.data_ptr(), bn.running_mean.data_ptr(),
+                         bn.running_var.data_ptr(), float(bn.momentum), upd, stream())
+                    if upd:
+                        bn.num_batches_tracked.add_(groups)
             Mg_apply = Mg
         else:
             # eval: running statistics, one group

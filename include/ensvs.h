@@ -388,6 +388,18 @@ int ensvs_gather_rows(const float* table, const long long* idx, int B, int C, fl
  * apply+ReLU, and backward (+ReLU).  Groups of Mg rows keep separate statistics. */
 int ensvs_bn_finalize(float* mean, float* var, int G, int C, long long Mg, float eps, float* rstd,
                       float* rmean, float* rvar, float momentum, int update, void* stream);
+/* BatchNorm1d training statistics of y [M][ldy] in groups of Mg rows in two launches (the two
+ * column sums + ensvs_bn_finalize they replace): mean / var (biased) [G][C], rstd = 1 /
+ * sqrt(var + eps), and with updates > 0 the running statistics updated `updates` times per
+ * group (bn_finalize's order) and *nbt (the module's num_batches_tracked, int64) += G * updates.
+ * part: ensvs_bn_stats_part_floats(M, C, Mg) floats of workspace.  Per row split the column
+ * sums and the squared deviations from the split's own mean; merged in a fixed order (Chan's
+ * parallel variance, double): deterministic (nnsvs/model.py:837-859 nn.BatchNorm1d). */
+long long ensvs_bn_stats_part_floats(long long M, int C, long long Mg);
+int ensvs_bn_stats(const float* y, int ldy, long long M, int C, long long Mg, float* part,
+                   long long part_floats, float eps, float* mean, float* var, float* rstd,
+                   float* rmean, float* rvar, float momentum, int updates, long long* nbt,
+                   void* stream);
 /* outb / dyb (optional, bf16, 8-B aligned rows, ld % 4 == 0; C % 4 == 0 and 16-B aligned fp32
  * operands, else ENSVS_E_ARG): the output / input gradient also rounded to bf16 for the
  * next convolution's bf16-operand GEMMs (forward input, dgrad, weight gradient). */

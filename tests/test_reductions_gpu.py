@@ -159,3 +159,52 @@ def test_deferred_colsum_train_step_bitwise(prec):
         assert np.isfinite(res[0][0].item())
     finally:
         engine.set_gemm_precision("bf16")
+
+
+@pytest.mark.parametrize("M,C,G,ld,updates", [
+    (30720, 128, 1, 128, 1), (30720, 256, 2, 256, 2), (30720, 512, 1, 512, 0),
+    (2000, 60, 1, 61, 1),  # unaligned rows: the scalar loads
+    (1000, 1024, 2, 1024, 1), (100, 8, 1, 8, 1),
+])
+def test_bn_stats_matches_two_pass(M, C, G, ld, updates):
+    """ensvs_bn_stats (split sums / deviations, Chan merge in double) against the two-pass
+    form it replaces (two column sums + ensvs_bn_finalize, `updates` calls): mean and variance
+    within 1e-6 / 1e-5 relative of the two-pass values, rstd and running statistics likewise,
+    num_batches_tracked advanced by G * updates."""
+    dev = "cuda"
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device=dev).manual_seed(M + C)
+    y = (torch.randn(M, ld, device=dev, generator=g) * 3.0 + 5.0)  # |mean| >> std per column
+    Mg = M // G
+    eps, mom = 1e-5, 0.1
+    rm0 = torch.randn(C, device=dev, generator=g)
+    rv0 = torch.rand(C, device=dev, generator=g) + 0.5
+    # two-pass reference
+    mean_r, var_r, rstd_r = (torch.empty(G, C, device=dev) for _ in range(3))
+    K.colsum(y, ld, Mg, C, mean_r, groups=G, scale=1.0 / Mg)
+    K.colsum(y, ld, Mg, C, var_r, groups=G, mean=mean_r, scale=1.0 / Mg)
+    rm_r, rv_r = rm0.clone(), rv0.clone()
+    for _ in range(max(1, updates)):
+        L.call("ensvs_bn_finalize", mean_r.data_ptr(), var_r.data_ptr(), G, C, Mg, eps,
+               rstd_r.data_ptr(), rm_r.data_ptr(), rv_r.data_ptr(), mom, int(updates > 0), st)
+    # fused
+    n = L.query("ensvs_bn_stats_part_floats", M, C, Mg)
+    part = torch.full((n,), float("nan"), device=dev)
+    mean, var, rstd = (torch.full((G, C), float("nan"), device=dev) for _ in range(3))
+    rm, rv = rm0.clone(), rv0.clone()
+    nbt = torch.tensor([7], dtype=torch.int64, device=dev)
+    L.call("ensvs_bn_stats", y.data_ptr(), ld, M, C, Mg, part.data_ptr(), n, eps, mean.data_ptr(),
+           var.data_ptr(), rstd.data_ptr(), rm.data_ptr() if updates else None,
+           rv.data_ptr() if updates else None, mom, updates, nbt.data_ptr() if updates else None,
+           st)
+    torch.cuda.synchronize()
+
+    def close(a, b, tol):
+        return ((a.double() - b.double()).abs().max() / b.double().abs().max()).item() <= tol
+
+    assert close(mean, mean_r, 1e-6) and close(var, var_r, 1e-5) and close(rstd, rstd_r, 1e-5)
+    if updates:
+        assert close(rm, rm_r, 1e-6) and close(rv, rv_r, 1e-5)
+        assert nbt.item() == 7 + G * updates
+    else:
+        assert torch.equal(rm, rm0) and torch.equal(rv, rv0)

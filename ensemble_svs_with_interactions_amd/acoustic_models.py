@@ -30,6 +30,9 @@ DEC_PAD = {"on": True}
 # SeparateF0: the decoders' weight / bias gradients issued after their input gradients, on
 # their streams beside the encoder's backward (which waits for those input gradients only)
 DEC_LATER = {"on": True}
+# SeparateF0: the V/UV and bap decoders start once the mgc decoder's FF + conv stack is issued
+# (their stacks then run beside its recurrences instead of beside its stack; A/B switch)
+DEC_ORDER = {"on": True}
 
 
 # Step schedule of the fused branches (0 lf0, 1 mgc, 2 bap, 3 vuv; profiles/r2_schedule_ab.txt,
@@ -1150,13 +1153,21 @@ class MultiTrackMultistreamSeparateF0ParametricModel(_MultistreamHybrid):
             st["dx_ld"] = None
         st["X"] = src
         # phase 2: the three decoders (sub calls on the same input: multistream.py:519-521)
+        conv_ev = []
+        order = DEC_ORDER["on"] and not sub_decoders
+
+        def mark():
+            conv_ev.append(torch.cuda.current_stream().record_event())
         with Branches(dev) as br:
             for bi, (name, m) in enumerate(self._decoders()):
                 with br.on(bi):
+                    if order and bi > 0 and conv_ev and br.on_side:
+                        torch.cuda.current_stream().wait_event(conv_ev[0])
                     outs[name], st[name] = m._fwd(
                         src, B, T, lens_dev, training=training, save=save,
                         lstm_masks=dr.get(f"{name}_lstm"),
-                        bn_updates=1 if sub_decoders or not training else 2, x16=X16)
+                        bn_updates=1 if sub_decoders or not training else 2, x16=X16,
+                        after_conv=mark if order and bi == 0 else None)
                     if sub_decoders:
                         outs[name + "_sub"], st[name + "_sub"] = m._fwd(
                             src, B, T, lens_dev, training=training, save=save,

@@ -142,11 +142,12 @@ class FFConvLSTM(BaseModel):
         pk.bias_vec("fc.b", self.fc.bias)
 
     def _fwd(self, sources, B, T, lens_dev, spk_seq=None, spk_ld=0, training=None,
-             lstm_masks=None, save=True, bn_updates=1, x16=None):
+             lstm_masks=None, save=True, bn_updates=1, x16=None, after_conv=None):
         """sources: [(tensor, ld, col_offset, ncols)] of the logical input columns (without
         phoneme embedding: one (X, ldx, 0, in_dim) source is read in place); x16: an optional
         bf16 copy of that single source (rows zero-padded to a multiple of 8 columns), the
-        first FF GEMM's operand and its weight gradient's.
+        first FF GEMM's operand and its weight gradient's; after_conv: called once the FF +
+        conv stack is issued (before the recurrence; a schedule hook).
         Returns (out (B*T, out_dim), saved state)."""
         training = self.training if training is None else training
         pk = self._packs.ensure(self, self._register)
@@ -166,6 +167,8 @@ class FFConvLSTM(BaseModel):
         a, csv = Ly.conv_fwd(pk, self.conv, [("", hs[2], F, F, 0)], B, T, dev, training,
                              save=save, running_updates=bn_updates,
                              first_b16=None if hs16[2] is None else [("", hs16[2], F, F)])
+        if after_conv is not None:
+            after_conv()
         if training and self.lstm.dropout > 0 and lstm_masks is None:
             lstm_masks = [Ly.dropout_mask(B * T * 2 * self.lstm.hidden_size, self.lstm.dropout,
                                           dev)

@@ -270,7 +270,8 @@ def test_bf16_copies_match_cast_by_consumers():
     parameter with a norm above 1e-3 of the largest): the bias sums run in another order and
     the decoders' 1 026-column weight gradient runs on the bf16-operand kernel.  The
     decoders' parameter gradients issued after their input gradients (DEC_LATER) or between
-    them: the same bits."""
+    them, and the V/UV and bap decoders started after the mgc decoder's conv stack
+    (DEC_ORDER) or with it: the same bits."""
     from ensemble_svs_with_interactions_amd import acoustic_models as AM, data
     from ensemble_svs_with_interactions_amd import layers as Ly
     from ensemble_svs_with_interactions_amd.train import FusedAdam, train_step
@@ -284,10 +285,12 @@ def test_bf16_copies_match_cast_by_consumers():
             for _ in range(2)]
     res = []
     try:
-        for on, later in ((True, True), (False, True), (True, False)):
+        for on, later, order in ((True, True, True), (False, True, True), (True, False, True),
+                                 (True, True, False)):
             AM.DEC_PAD["on"] = on
             Ly.COOP_BF16["on"] = on
             AM.DEC_LATER["on"] = later
+            AM.DEC_ORDER["on"] = order
             torch.manual_seed(0)
             m = configs.instantiate(_cfg(False)).cuda()
             for sub in (m.mgc_model, m.vuv_model, m.bap_model, m.encoder):
@@ -304,6 +307,7 @@ def test_bf16_copies_match_cast_by_consumers():
         AM.DEC_PAD["on"] = True
         Ly.COOP_BF16["on"] = True
         AM.DEC_LATER["on"] = True
+        AM.DEC_ORDER["on"] = True
     (l1, n1, g1, p1), (l0, n0, g0, p0) = res[:2]
     for l2, n2, g2, _ in res[2:]:
         assert (l2, n2) == (l1, n1) and torch.equal(g2, g1)

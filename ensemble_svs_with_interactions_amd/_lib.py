@@ -150,6 +150,8 @@ SIGNATURES = {
     "ensvs_bn_finalize": [c_vp, c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_vp, c_float, c_int,
                           c_vp],
     "ensvs_bn_stats_part_floats": [c_ll, c_int, c_ll],
+    "ensvs_blas_gemm": [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int,
+                        c_vp, c_ll, c_vp],
     "ensvs_bn_stats": [c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_ll, c_float, c_vp, c_vp, c_vp, c_vp,
                        c_vp, c_float, c_int, c_vp, c_vp],
     "ensvs_bn_apply_relu": [c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,

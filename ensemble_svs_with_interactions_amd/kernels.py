@@ -389,6 +389,27 @@ def usf_block(segs: List[Seg], B, Tout, W: PackedBuffer, C, ref2, x, ldx, alpha,
          float(alpha), int(bool(relu)), ptr(xb), 0 if xb is None else xb.shape[1], stream())
 
 
+# plain bf16 GEMMs on hipBLASLt (ensvs_blas_gemm): the recurrences' input projections and input
+# gradients (layers.lstm_fwd / lstm_bwd); off: the implicit-GEMM engine (A/B switch)
+BLAS = {"on": True, "min_rows": 4096, "ws_bytes": 32 << 20}
+
+
+def blas_ok(x, ld, K, M, W):
+    """Whether a plain GEMM over bf16 rows x (ld, K) and packed weights W runs on hipBLASLt."""
+    return (BLAS["on"] and x.dtype == torch.bfloat16 and W.dtype == _lib.DT_BF16 and
+            M >= BLAS["min_rows"] and K % 8 == 0 and ld % 8 == 0)
+
+
+def blas_gemm(x, ldx, ref, W, M, N, K, Y, ldy, bias=None, bias_off=0, accum=False, xoff=0):
+    """Y[M][N] (+)= x[M][K] (bf16 rows of ldx, from element xoff) W_ref^T (+ bias) on hipBLASLt
+    (ensvs_blas_gemm): W_ref is a packed [Npad][Kp] bf16 operand of W."""
+    assert x.dtype == torch.bfloat16 and W.dtype == _lib.DT_BF16 and ref.Kp >= K and ref.taps == 1
+    ws = scratch(BLAS["ws_bytes"] // 4, x.device, key="blas")
+    call("ensvs_blas_gemm", x.data_ptr() + 2 * xoff, ldx, W.buf.data_ptr() + 2 * ref.offset,
+         ref.Kp, M, N, K, None if bias is None else bias.data_ptr() + 4 * bias_off,
+         Y.data_ptr(), ldy, int(accum), ws.data_ptr(), BLAS["ws_bytes"], stream())
+
+
 def bf16_operands(W, M):
     """Whether GEMMs on these packed weights with M rows take pre-rounded bf16 operands
     (callers then round an operand shared by several GEMMs once, instead of per GEMM)."""

@@ -388,6 +388,16 @@ int ensvs_gather_rows(const float* table, const long long* idx, int B, int C, fl
  * apply+ReLU, and backward (+ReLU).  Groups of Mg rows keep separate statistics. */
 int ensvs_bn_finalize(float* mean, float* var, int G, int C, long long Mg, float eps, float* rstd,
                       float* rmean, float* rvar, float momentum, int update, void* stream);
+/* Plain bf16 GEMM on hipBLASLt: Y[M][N] (+)= X[M][K] W[N][K]^T (+ bias[N]); X bf16 rows of ldx,
+ * W bf16 rows of ldw (the GEMM engine's packed [Npad][Kp] weights, ldw = Kp), Y fp32 rows of
+ * ldy, fp32 accumulation; accum: beta = 1.  ws / ws_bytes: workspace (the plan's algorithm
+ * must fit it).  One plan per shape, made on first use (before graph capture).  The
+ * recurrences' input projections / input gradients of the SeparateF0 model
+ * (nnsvs/model.py:1435-1537 nn.LSTM's x W_ih^T + b and its input gradient). */
+int ensvs_blas_gemm(const void* x, int ldx, const void* w, int ldw, int M, int N, int K,
+                    const float* bias, float* y, int ldy, int accum, void* ws, long long ws_bytes,
+                    void* stream);
+
 /* BatchNorm1d training statistics of y [M][ldy] in groups of Mg rows in two launches (the two
  * column sums + ensvs_bn_finalize they replace): mean / var (biased) [G][C], rstd = 1 /
  * sqrt(var + eps), and with updates > 0 the running statistics updated `updates` times per

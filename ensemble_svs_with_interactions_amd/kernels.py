@@ -389,8 +389,9 @@ def usf_block(segs: List[Seg], B, Tout, W: PackedBuffer, C, ref2, x, ldx, alpha,
          float(alpha), int(bool(relu)), ptr(xb), 0 if xb is None else xb.shape[1], stream())
 
 
-# plain bf16 GEMMs on hipBLASLt (ensvs_blas_gemm): the recurrences' input projections and input
-# gradients (layers.lstm_fwd / lstm_bwd); off: the implicit-GEMM engine (A/B switch)
+# plain bf16 GEMMs on hipBLASLt (ensvs_blas_gemm, data-parallel grids): the recurrences' input
+# projections and input gradients (layers.lstm_fwd / lstm_bwd); off: the implicit-GEMM engine
+# (A/B switch)
 BLAS = {"on": True, "min_rows": 4096, "ws_bytes": 32 << 20}
 
 
@@ -400,14 +401,35 @@ def blas_ok(x, ld, K, M, W):
             M >= BLAS["min_rows"] and K % 8 == 0 and ld % 8 == 0)
 
 
+_blas_shapes = {}
+
+
+def blas_supported(M, N, K, ldx, ldw, ldy, bias):
+    """Whether hipBLASLt has a data-parallel plan for ensvs_blas_gemm's shape
+    (ensvs_blas_supported; cached per process and device)."""
+    key = (torch.cuda.current_device(), M, N, K, ldx, ldw, ldy, bool(bias))
+    ok = _blas_shapes.get(key)
+    if ok is None:
+        rc = _lib.query("ensvs_blas_supported", M, N, K, ldx, ldw, ldy, int(bool(bias)),
+                        BLAS["ws_bytes"])
+        if rc < 0:
+            raise RuntimeError(f"ensvs_blas_supported failed: {rc}")
+        ok = _blas_shapes[key] = rc == 1
+    return ok
+
+
 def blas_gemm(x, ldx, ref, W, M, N, K, Y, ldy, bias=None, bias_off=0, accum=False, xoff=0):
     """Y[M][N] (+)= x[M][K] (bf16 rows of ldx, from element xoff) W_ref^T (+ bias) on hipBLASLt
-    (ensvs_blas_gemm): W_ref is a packed [Npad][Kp] bf16 operand of W."""
+    (ensvs_blas_gemm): W_ref is a packed [Npad][Kp] bf16 operand of W.  Returns False (nothing
+    issued) when hipBLASLt has no data-parallel algorithm for the shape."""
     assert x.dtype == torch.bfloat16 and W.dtype == _lib.DT_BF16 and ref.Kp >= K and ref.taps == 1
+    if not blas_supported(M, N, K, ldx, ref.Kp, ldy, bias is not None):
+        return False
     ws = scratch(BLAS["ws_bytes"] // 4, x.device, key="blas")
     call("ensvs_blas_gemm", x.data_ptr() + 2 * xoff, ldx, W.buf.data_ptr() + 2 * ref.offset,
          ref.Kp, M, N, K, None if bias is None else bias.data_ptr() + 4 * bias_off,
          Y.data_ptr(), ldy, int(accum), ws.data_ptr(), BLAS["ws_bytes"], stream())
+    return True
 
 
 def bf16_operands(W, M):

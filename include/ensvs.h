@@ -394,6 +394,13 @@ int ensvs_bn_finalize(float* mean, float* var, int G, int C, long long Mg, float
  * must fit it).  One plan per shape, made on first use (before graph capture).  The
  * recurrences' input projections / input gradients of the SeparateF0 model
  * (nnsvs/model.py:1435-1537 nn.LSTM's x W_ih^T + b and its input gradient). */
+/* 1 when hipBLASLt has a data-parallel plan for ensvs_blas_gemm's shape (made here, reused by
+ * the calls), 0 when not -- keep the implicit-GEMM engine.  Plans need
+ * TENSILE_STREAMK_DATA_PARALLEL=1, which the library sets when loaded unless the process set it:
+ * hipBLASLt's stream-K grids wait across workgroups, and beside the cooperative recurrences a
+ * waiting workgroup's producer may never become resident. */
+int ensvs_blas_supported(int M, int N, int K, int ldx, int ldw, int ldy, int bias,
+                         long long ws_bytes);
 int ensvs_blas_gemm(const void* x, int ldx, const void* w, int ldw, int M, int N, int K,
                     const float* bias, float* y, int ldy, int accum, void* ws, long long ws_bytes,
                     void* stream);

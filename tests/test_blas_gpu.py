@@ -3,7 +3,8 @@ on the same bf16 operands and packed weights: the recurrences' input projection 
 epilogue) and the two-segment input gradient (second call accumulating), at the SeparateF0
 encoder's shapes and a ragged one.  Both accumulate the same bf16 products in fp32, so they
 agree to summation order (1e-5 relative of the output scale); repeated calls and a captured
-graph replay give the same bits (one plan, one algorithm per shape)."""
+graph replay give the same bits (one plan, one algorithm per shape, on data-parallel grids:
+TENSILE_STREAMK_DATA_PARALLEL=1, set by the library, csrc/blas.hip)."""
 import pytest
 import torch
 
@@ -36,9 +37,9 @@ def test_blas_projection_matches_engine(M, N, Kc, T):
     want = torch.empty(M, N, device="cuda")
     K.gemm([K.Seg(x, Kc, Kc, ref, T)], M // T, T, N, pb, want, N, bias=bias)
     got = torch.full((M, N), float("nan"), device="cuda")
-    K.blas_gemm(x, Kc, ref, pb, M, N, Kc, got, N, bias=bias)
+    assert K.blas_gemm(x, Kc, ref, pb, M, N, Kc, got, N, bias=bias)
     again = torch.full((M, N), float("nan"), device="cuda")
-    K.blas_gemm(x, Kc, ref, pb, M, N, Kc, again, N, bias=bias)
+    assert K.blas_gemm(x, Kc, ref, pb, M, N, Kc, again, N, bias=bias)
     torch.cuda.synchronize()
     assert _close(got, want)
     assert torch.equal(got.view(torch.int32), again.view(torch.int32))
@@ -60,8 +61,8 @@ def test_blas_two_segment_input_gradient_and_graph():
            M // T, T, Kc, pb, want, Kc)
 
     def run(out):
-        K.blas_gemm(gd, 8 * H, refs[0], pb, M, Kc, 4 * H, out, Kc)
-        K.blas_gemm(gd, 8 * H, refs[1], pb, M, Kc, 4 * H, out, Kc, accum=True, xoff=4 * H)
+        assert K.blas_gemm(gd, 8 * H, refs[0], pb, M, Kc, 4 * H, out, Kc)
+        assert K.blas_gemm(gd, 8 * H, refs[1], pb, M, Kc, 4 * H, out, Kc, accum=True, xoff=4 * H)
     got = torch.full((M, Kc), float("nan"), device="cuda")
     run(got)
     torch.cuda.synchronize()
@@ -77,3 +78,4 @@ def test_blas_two_segment_input_gradient_and_graph():
     graph.replay()
     torch.cuda.synchronize()
     assert torch.equal(cap.view(torch.int32), got.view(torch.int32))
+

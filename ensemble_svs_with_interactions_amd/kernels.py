@@ -255,6 +255,15 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
     outputs.  keep_y=False (GATE with ybf, GATE_BWD with ybf / csum): the fp32 Y is not
     needed by the caller and the fused epilogue skips it (Y stays allocated for the
     fallback paths, which still write it)."""
+    if (BLAS["generic"] and len(segs) == 1 and epi == _lib.EPI_PLAIN and not relu and not accum
+            and aux0 is None and aux1 is None and ybf is None and csum is None and yoff == 0):
+        s = segs[0]  # a plain (1-tap, unshifted, bf16) product: hipBLASLt when it has a plan
+        if (s.taps == 1 and s.shift0 == 0 and s.pd is None and s.radd is None and s.Tin == Tout
+                and s.ref.taps == 1 and N * s.K * B * Tout >= BLAS["min_macs"]
+                and blas_ok(s.x, s.ld, s.K, B * Tout, W)
+                and blas_gemm(s.x, s.ld, s.ref, W, B * Tout, N, s.K, Y, ldy, bias=bias,
+                              bias_off=bias_off, xoff=s.xoff)):
+            return
     arr = (ConvSeg * len(segs))()
     Npad = segs[0].ref.Npad
     # C-ABI epilogue flags: a bf16 gate/filter save (DiffNet production path)
@@ -392,7 +401,10 @@ def usf_block(segs: List[Seg], B, Tout, W: PackedBuffer, C, ref2, x, ldx, alpha,
 # plain bf16 GEMMs on hipBLASLt (ensvs_blas_gemm, data-parallel grids): the recurrences' input
 # projections and input gradients (layers.lstm_fwd / lstm_bwd); off: the implicit-GEMM engine
 # (A/B switch)
-BLAS = {"on": True, "min_rows": 4096, "ws_bytes": 32 << 20}
+BLAS = {"on": True, "min_rows": 4096, "ws_bytes": 32 << 20,
+        # gemm(): any single plain bf16 segment (1 tap, no shift, PLAIN epilogue with at most a
+        # bias, fp32 Y) of at least min_macs multiply-adds also goes to hipBLASLt
+        "generic": True, "min_macs": 1 << 34}
 
 
 def blas_ok(x, ld, K, M, W):

@@ -1,7 +1,8 @@
 """Interleaved A/B of module switches on the bench's main training line (graph replay, 30 x
 1024): each arm sets kernels.<FLAG>["on"] values or calls C-ABI switches (ensvs_*=value), runs
 the bench leg in a fresh process, two rounds.
-  python tools/flag_ab.py [--sf0] "COLSUM_ONCE=0,DEFER_WGRAD=0" "ensvs_ardec_coop_set_tile_seqs=32" ...
+  python tools/flag_ab.py [--sf0] "COLSUM_ONCE=0,DEFER_WGRAD=0" "ensvs_ardec_coop_set_tile_seqs=32" \
+      "diffsinger.SKIP_GEMM=0" "BLAS:generic=0" ...
 --sf0: time the recipe-default SeparateF0 leg instead (its ms_per_step)."""
 import json
 import os
@@ -19,13 +20,12 @@ for kv in {arm!r}.split(","):
         k, v = kv.split("=")
         if k.startswith("ensvs_"):  # integer arguments separated by ':'
             call(k, *[int(x) for x in v.split(":")])
-        elif "." in k:  # module.FLAG of the package, e.g. diffsinger.SKIP_GEMM
+        else:  # [module.]FLAG[:key] of the package (default module kernels, key "on")
             import importlib
-            mod, flag = k.rsplit(".", 1)
+            k, key = k.split(":") if ":" in k else (k, "on")
+            mod, flag = k.rsplit(".", 1) if "." in k else ("kernels", k)
             getattr(importlib.import_module("ensemble_svs_with_interactions_amd." + mod),
-                    flag)["on"] = bool(int(v))
-        else:
-            getattr(K, k)["on"] = bool(int(v))
+                    flag)[key] = bool(int(v))
 sys.argv = ["bench.py", "--steps", "20", "--warmup", "3", "--no-cpu-baseline", "--no-synth",
             "--no-census", "--no-config2", "--no-shapes", "--no-real-data",
             "--no-transformer"] + ([] if {sf0!r} else ["--no-sf0"])

@@ -17,8 +17,16 @@
 // its CUs for the next.  The tiles run concurrently when the chip holds them (P = 60 pairs of
 // 512 frames: two tiles side by side, the same step count as 30 x 1024).
 //
-// Workspace of ntiles tiles: ntiles headers of HDR bytes (one 64-B counter line per direction
-// at word 16 d, the tile's error word at byte 128), then ntiles slabs of the kernel's slab size.
+// Workspace of ntiles tiles: ntiles headers of HDR bytes (the tile's error word at byte 128;
+// from byte 256 the step counters, SHARDS per direction, each on a 64-B line of its own), then
+// ntiles slabs of the kernel's slab size.
+//
+// Sharded counters (round 5): workgroup w adds to shard w % SHARDS of its direction, and a
+// waiter's first wave polls every shard with one load per lane and sums them (DPP adds).  One
+// counter took all NW agent-scope adds of a step serially at the memory side (~12 ns each,
+// MI355X_MICROARCH.md fanin: 32 arrivals ~0.4 us) under the pollers' loads of the same line; the
+// guide's fanin row: "for many arrivers shard the counter", and a sharded counter is polled
+// "every shard" (Valid forms, first row).
 //
 // Failure handling (a grid that cannot become resident, e.g. CUs held by another stream's
 // long-running kernel): the polls are bounded in time (Ctl::timeout ticks of the 100 MHz
@@ -40,7 +48,9 @@ constexpr int NT = 256;     // 4 waves per workgroup
 constexpr int UW = 16;      // hidden units per workgroup
 constexpr int SB = 32;      // sequence columns of one tile: two MFMA N tiles
 constexpr int CP_SC1 = 16;  // buffer-op cache policy: sc1 (L1 bypass on both sides)
-constexpr int HDR = 256;    // workspace header per tile
+constexpr int HDR = 2048;   // workspace header per tile
+constexpr int SHARDS = 8;   // step-counter shards per direction (one 64-B line each)
+constexpr int CNT0 = 64;    // first counter word (byte 256)
 constexpr unsigned ABORT = 0x80000000u;  // counter bit: a workgroup of the tile timed out
 
 // per-launch failure controls (by value in the kernel arguments)
@@ -83,23 +93,45 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// wait until direction d's counter of the tile reaches `target` (one lane polls), then release
-// the workgroup.  The first poll costs what the unbounded loop did; the clock is read only
-// once the counter is behind, and then every 8th poll.
+__device__ __forceinline__ unsigned* shard(unsigned* hdr, int d, int s) {
+  return hdr + CNT0 + (d * SHARDS + s) * 16;
+}
+
+// direction d's step count: lanes 0..SHARDS-1 of the calling wave each load one shard (the
+// others contribute 0), summed over each 8-lane group by three DPP adds (the xor 1, xor 2 and
+// half-row-mirror pairs of coop::sum16's first three levels); the wave's first lane's total,
+// as a uniform value
+__device__ __forceinline__ unsigned shard_total(unsigned* hdr, int d, int lane) {
+  unsigned v = lane < SHARDS
+                   ? __hip_atomic_load(shard(hdr, d, lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : 0u;
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // xor 1
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // xor 2
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // 7 - i
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+// wait until direction d's count of the tile reaches `target` (the workgroup's first wave
+// polls every shard), then release the workgroup.  The first poll costs what the unbounded
+// loop did; the clock is read only once the count is behind, and then every 8th poll.
 __device__ __forceinline__ void wait_count(unsigned* hdr, int d, unsigned target, const Ctl& c) {
-  if (threadIdx.x == 0) {
-    unsigned* cnt = hdr + d * 16;
-    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    if (shard_total(hdr, d, lane) < target) {
       const long long t0 = wall_clock64();
       for (unsigned it = 1;; ++it) {
         __builtin_amdgcn_s_sleep(1);
-        if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+        if (shard_total(hdr, d, lane) >= target) break;
         if ((it & 7) == 0 && wall_clock64() - t0 > c.timeout) {
-          // a workgroup never arrived: release every waiter of this direction, flag the failure
-          __hip_atomic_fetch_or(cnt, ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_or(hdr + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_or(c.err ? c.err : hdr + 32, 1u, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_SYSTEM);
+          // a workgroup never arrived: release every waiter of this direction (the ABORT bit
+          // in one shard makes every total pass), flag the failure
+          if (lane == 0) {
+            __hip_atomic_fetch_or(shard(hdr, d, 0), ABORT, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_or(hdr + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_or(c.err ? c.err : hdr + 32, 1u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_SYSTEM);
+          }
           break;
         }
       }
@@ -108,10 +140,12 @@ __device__ __forceinline__ void wait_count(unsigned* hdr, int d, unsigned target
   lds_barrier();
 }
 
-// publish step `step`'s slice: one agent-scope counter add (skipped by the test fault)
+// publish step `step`'s slice: one agent-scope add to this workgroup's shard (blockIdx.x is
+// the workgroup's unit block in every cooperative kernel; skipped by the test fault)
 __device__ __forceinline__ void signal(unsigned* hdr, int d, int step, const Ctl& c) {
   if (c.fault && step == 1 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) return;
-  __hip_atomic_fetch_add(hdr + d * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(shard(hdr, d, blockIdx.x % SHARDS), 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ f32x4 ld16(__amdgpu_buffer_rsrc_t r, int off) {

@@ -237,7 +237,7 @@ int ensvs_lstm_bwd(const float* dy, int lddy, const float* whh_f, const float* w
  * backward bf16 fragments of W_hh^T), 2*4*H*H 2-byte elements.  Sequences run in tiles of
  * S = ensvs_lstm_coop_tile_seqs(B, H) (blockIdx.z), each tile an independent hand-off group.
  * work: 256-B aligned, ensvs_lstm_coop_work_bytes(H, B) bytes, caller-owned, one per
- * concurrent launch: ceil(B/S) 256-B tile headers, then the tiles' slabs; header bytes 128..131 of a tile read non-zero
+ * concurrent launch: ceil(B/S) 2 048-B tile headers, then the tiles' slabs; header bytes 128..131 of a tile read non-zero
  * after a launch in which that tile's grid could not become resident (see
  * ensvs_coop_set_error_word for the persistent flag). */
 /* MFMA recurrence for H = 64 / 128 in production (bf16 GEMM) precision (lstm_mfma.hip): the

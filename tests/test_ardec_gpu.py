@@ -45,8 +45,8 @@ def _resident(work, B, H):
     nt = (B + S - 1) // S
     assert S == 32 or nt <= 8
     wave = query("ensvs_ardec_coop_work_bytes", H, 256) if nt > 8 else 0  # 8 tiles of 32
-    return all(work[wave * (z // 8) + 256 * (z % 8) + 128:
-                    wave * (z // 8) + 256 * (z % 8) + 132].cpu().view(torch.int32).item() == 0
+    return all(work[wave * (z // 8) + 2048 * (z % 8) + 128:
+                    wave * (z // 8) + 2048 * (z % 8) + 132].cpu().view(torch.int32).item() == 0
                for z in range(nt))
 
 

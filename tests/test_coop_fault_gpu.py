@@ -57,7 +57,7 @@ def _lstm_launch(H, B, T):
     call("ensvs_lstm_coop_fwd", gx.data_ptr(), 8 * H, wpf.data_ptr(), lens.data_ptr(), B, T, H,
          y.data_ptr(), 2 * H, saved.data_ptr(), work.data_ptr(), nbytes, st)
     torch.cuda.synchronize()
-    flags = [work[256 * z + 128:256 * z + 132].cpu().view(torch.int32).item()
+    flags = [work[2048 * z + 128:2048 * z + 132].cpu().view(torch.int32).item()
              for z in range((B + 31) // 32)]
     return time.time() - t0, flags
 

@@ -81,8 +81,8 @@ def _check(H, B, T, I, lengths, tol_y, tol_g, coop=False, mfma=False):
         assert S == 32 or ntile <= 8
 
         def resident():  # every tile's residency flag (header byte 128 of each tile) clear
-            return all(cwork[wave * (z // 8) + 256 * (z % 8) + 128:
-                             wave * (z // 8) + 256 * (z % 8) + 132].cpu().view(torch.int32).item()
+            return all(cwork[wave * (z // 8) + 2048 * (z % 8) + 128:
+                             wave * (z // 8) + 2048 * (z % 8) + 132].cpu().view(torch.int32).item()
                        == 0 for z in range(ntile))
         wpf = torch.empty(2 * 4 * H * H, dtype=torch.float16, device=dev)
         wpb = torch.empty(2 * 4 * H * H, dtype=torch.bfloat16, device=dev)

@@ -29,10 +29,10 @@ bargs = (a["wih_p"].data_ptr(), a["wfo"].data_ptr(), H + 130, a["mask"].data_ptr
          do4.data_ptr())
 wpf, wpb = E(4 * H * H), E(4 * H * H)
 call("ensvs_ardec_pack", a["whh"].data_ptr(), H, wpf.data_ptr(), wpb.data_ptr(), st)
-call("ensvs_ardec_coop_set_tile_seqs", 32)  # the larger of the two tile layouts
-nbytes = query("ensvs_ardec_coop_work_bytes", H, B)
-call("ensvs_ardec_coop_set_tile_seqs", 0)
-nbytes = max(nbytes, query("ensvs_ardec_coop_work_bytes", H, B))
+nbytes = 0  # the largest of the tile layouts the runs force
+for S in (32, 16, 0):
+    call("ensvs_ardec_coop_set_tile_seqs", S)
+    nbytes = max(nbytes, query("ensvs_ardec_coop_work_bytes", H, B))
 work = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
 wf = torch.empty(4 * H * H, dtype=torch.float16, device=dev)
 wb = torch.empty(4 * H * H, dtype=torch.bfloat16, device=dev)

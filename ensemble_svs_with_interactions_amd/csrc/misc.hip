@@ -333,24 +333,33 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __re
   }
 }
 
-// 16 columns x 16 split lanes per block: lane sl takes splits sl, sl + 16, ..., and the 16
-// lane totals are added in lane order (fixed: deterministic)
+// 16 columns x 16 split lanes per block: lane sl takes splits sl, sl + 16, ... (at most
+// BN_STATS_MAX_SPLITS / 16 = 16: all its (sum, M2) pairs are loaded into registers at once,
+// one round trip), and the 16 lane totals are added in lane order (fixed: deterministic)
 __global__ __launch_bounds__(256) void bn_stats_final_kernel(
     const float* __restrict__ part, int S, int G, int C, int Mg, int rps, float eps,
     float* __restrict__ mean, float* __restrict__ var, float* __restrict__ rstd,
     float* __restrict__ rmean, float* __restrict__ rvar, float momentum, int updates,
     long long* __restrict__ nbt) {
+  constexpr int PER = BN_STATS_MAX_SPLITS / 16;
   __shared__ double red[16][17];
   __shared__ double mus[16];
   const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   if (blockIdx.x == 0 && threadIdx.x == 0 && updates > 0 && nbt) nbt[0] += (long long)G * updates;
-  const double inv_rps = 1.0 / (double)rps;
   for (int g = 0; g < G; ++g) {
     const float* pg = part + (long long)g * S * 2 * C;
+    float sv[PER], qv[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int s = sl + 16 * i;
+      const bool ok = c < C && s < S;
+      sv[i] = ok ? pg[(long long)s * 2 * C + c] : 0.f;
+      qv[i] = ok ? pg[(long long)s * 2 * C + C + c] : 0.f;
+    }
     double a = 0.0;
-    if (c < C)
-      for (int s = sl; s < S; s += 16) a += (double)pg[(long long)s * 2 * C + c];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) a += (double)sv[i];
     red[sl][cl] = a;
     __syncthreads();
     if (sl == 0) {
@@ -362,15 +371,16 @@ __global__ __launch_bounds__(256) void bn_stats_final_kernel(
     __syncthreads();
     const double mu = mus[cl];
     double m2 = 0.0;
-    if (c < C)
-      for (int s = sl; s < S; s += 16) {
-        const int n = min(rps, Mg - s * rps);
-        if (n <= 0) continue;
-        const double ms = (double)pg[(long long)s * 2 * C + c] *
-                          (n == rps ? inv_rps : 1.0 / (double)n);
-        const double d = ms - mu;
-        m2 += (double)pg[(long long)s * 2 * C + C + c] + (double)n * d * d;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int s = sl + 16 * i;
+      const int n = min(rps, Mg - s * rps);
+      if (c < C && s < S && n > 0) {
+        const double d = (double)sv[i] / (double)n - mu;
+        m2 += (double)qv[i] + (double)n * d * d;
       }
+    }
+    __syncthreads();  // every lane has read red (the sums)
     red[sl][cl] = m2;
     __syncthreads();
     if (sl == 0 && c < C) {

@@ -556,6 +556,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_final_kernel(
   const int c = blockIdx.x * 64 + cl, g = blockIdx.y;
   double a = 0.0, b = 0.0;
   if (c < C)
+#pragma unroll 4  // the loads of four splits in flight (the adds keep their order: same bits)
     for (int s = row; s < S; s += 16) {
       a += part[(((long long)g * S + s) * 2) * C + c];
       b += part[(((long long)g * S + s) * 2 + 1) * C + c];

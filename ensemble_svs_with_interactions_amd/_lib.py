@@ -53,7 +53,7 @@ class PackDesc(ctypes.Structure):
         ("sn", c_ll), ("sk", c_ll), ("sj", c_ll),
         ("N", c_int), ("K", c_int), ("taps", c_int), ("Npad", c_int), ("Kp", c_int),
         ("perm_c", c_int), ("flip", c_int), ("transpose", c_int), ("dtype", c_int),
-        ("scale", c_float), ("ldk", c_int), ("pad_", c_int),
+        ("scale", c_float), ("ldk", c_int), ("tile0", c_int),
     ]
 
 
@@ -89,6 +89,7 @@ SIGNATURES = {
                          c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_ll, c_ll, c_int,
                          c_float, c_int, c_vp],
     "ensvs_pack_weights": [c_vp, c_int, c_int, c_vp],
+    "ensvs_pack_weights_tiled": [c_vp, c_int, c_int, c_vp],
     "ensvs_colsum_batch": [c_vp, c_int, c_vp, c_ll, c_vp],
     "ensvs_colsum_batch_part_floats": [c_vp, c_int],
     "ensvs_colsum_once": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_float, c_vp, c_int, c_vp,

@@ -3176,7 +3176,8 @@ struct PackDesc {
   long long sn, sk, sj;
   int N, K, taps, Npad, Kp, perm_c, flip, transpose, dtype;
   float scale;
-  int ldk, pad_;  // dst row stride (elements); 0 -> Kp
+  int ldk;    // dst row stride (elements); 0 -> Kp
+  int tile0;  // pack_tile_kernel: the descriptor's first tile in the launch
 };
 
 __global__ void pack_kernel(const PackDesc* __restrict__ descs) {
@@ -3205,6 +3206,88 @@ __global__ void pack_kernel(const PackDesc* __restrict__ descs) {
       v *= d.scale;
     }
     const long long o = d.ldk > 0 ? ((long long)j * d.Npad + n) * d.ldk + k : i;
+    if (d.dtype == DT_BF16) ((__bf16*)d.dst)[o] = (__bf16)v;
+    else ((float*)d.dst)[o] = v;
+  }
+}
+
+// Tiled repack: one workgroup per 64 x 64 (n, k) tile of one tap of one descriptor, the
+// descriptors' tiles numbered consecutively (tile0: prefix sums of taps * cdiv(Npad, 64) *
+// cdiv(Kp, 64)).  The tile is read along the source's unit-stride axis into LDS and written
+// along the packed rows, so both sides are coalesced -- the transposed (input-gradient)
+// operands read a column per wavefront in pack_kernel -- with 32-bit index arithmetic, and the
+// grid is exactly the tiles (pack_kernel launches max-size x n workgroups, most of them idle).
+// Each element is the same value as in pack_kernel (same source element, same adds and
+// scaling, same rounding).
+constexpr int PACK_T = 64;
+
+__global__ __launch_bounds__(256) void pack_tile_kernel(const PackDesc* __restrict__ descs,
+                                                        int n) {
+  __shared__ float tile[PACK_T][PACK_T + 1];
+  const int b = blockIdx.x;
+  // the last descriptor with tile0 <= b (tile0 ascending): a count, one load round per 256
+  int cnt = 0;
+  for (int base = 0; base < n; base += 256) {
+    const int i = base + (int)threadIdx.x;
+    cnt += __syncthreads_count(i < n && descs[i].tile0 <= b);
+  }
+  if (cnt < 1) return;
+  const PackDesc d = descs[cnt - 1];
+  const int nt = (d.Npad + PACK_T - 1) / PACK_T, kt = (d.Kp + PACK_T - 1) / PACK_T;
+  int t = b - d.tile0;
+  const int kb = t % kt;
+  t /= kt;
+  const int nb = t % nt, j = t / nt;
+  if (t < 0 || j >= d.taps) return;  // (a tile count that does not match the descriptors)
+  const int n0 = nb * PACK_T, k0 = kb * PACK_T;
+  const int jj = d.flip ? (d.taps - 1 - j) : j;
+  const int nlim = d.transpose ? d.K : d.N;
+  const int klim = d.transpose ? d.N : d.K;
+  const int nmax = d.perm_c > 0 ? 2 * d.perm_c : nlim;
+  const long long s_n = d.transpose ? d.sk : d.sn;  // source stride along packed n
+  const long long s_k = d.transpose ? d.sn : d.sk;  // ... along packed k
+  const float* src = d.src + jj * d.sj;
+  const float* src2 = d.src2 ? d.src2 + jj * d.sj : nullptr;
+  const bool kfast = s_k <= s_n;
+  // all 16 loads of a lane in flight before the first use (then the adds, scaling and LDS
+  // stores), so a tile costs about one memory latency
+  constexpr int PER = PACK_T * PACK_T / 256;
+  float v[PER], v2[PER];
+  bool in[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = threadIdx.x + i * 256;
+    const int a = e & (PACK_T - 1), c = e / PACK_T;
+    const int pn = n0 + (kfast ? c : a), k = k0 + (kfast ? a : c);
+    int nn = pn;
+    if (d.perm_c > 0) {  // 16-interleave of two halves of width perm_c
+      const int q = pn >> 5, w = pn & 31;
+      nn = (w < 16) ? q * 16 + w : d.perm_c + q * 16 + (w - 16);
+    }
+    in[i] = nn < nlim && k < klim && pn < nmax;
+    const long long off = in[i] ? (long long)nn * s_n + (long long)k * s_k : 0;
+    v[i] = in[i] ? src[off] : 0.f;
+    v2[i] = (in[i] && src2) ? src2[off] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = threadIdx.x + i * 256;
+    const int a = e & (PACK_T - 1), c = e / PACK_T;
+    float x = v[i];
+    if (in[i]) {
+      if (src2) x += v2[i];
+      x *= d.scale;
+    }
+    tile[kfast ? c : a][kfast ? a : c] = x;
+  }
+  __syncthreads();
+  const int ld = d.ldk > 0 ? d.ldk : d.Kp;
+  for (int e = threadIdx.x; e < PACK_T * PACK_T; e += 256) {
+    const int tk = e & (PACK_T - 1), tn = e / PACK_T;
+    const int pn = n0 + tn, k = k0 + tk;
+    if (pn >= d.Npad || k >= d.Kp) continue;
+    const long long o = ((long long)j * d.Npad + pn) * ld + k;
+    const float v = tile[tn][tk];
     if (d.dtype == DT_BF16) ((__bf16*)d.dst)[o] = (__bf16)v;
     else ((float*)d.dst)[o] = v;
   }
@@ -4233,6 +4316,16 @@ ENSVS_API int ensvs_pack_weights(const ensvs_pack_desc* descs, int n, int max_el
   int bx = std::min(1024, std::max(1, (max_elems + 255) / 256));
   hipLaunchKernelGGL(pack_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream,
                      (const PackDesc*)descs);
+  ENSVS_CHECK_LAUNCH();
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_pack_weights_tiled(const ensvs_pack_desc* descs, int n, int tiles,
+                                       void* stream) {
+  if (n <= 0 || tiles <= 0) return ENSVS_OK;
+  if (!descs) return ENSVS_E_ARG;
+  hipLaunchKernelGGL(pack_tile_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream,
+                     (const PackDesc*)descs, n);
   ENSVS_CHECK_LAUNCH();
   return ENSVS_OK;
 }

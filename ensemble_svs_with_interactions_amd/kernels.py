@@ -25,6 +25,13 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+# weight repacks as one workgroup per 64 x 64 tile (ensvs_pack_weights_tiled: coalesced
+# reads and writes through LDS, exactly the tiles) or the element-per-thread pack_kernel;
+# same bits
+PACK_TILED = {"on": True}
+PACK_TILE = 64  # gemm.hip PACK_T
+
+
 @dataclass
 class PackedRef:
     """Where one packed GEMM operand lives inside a PackedBuffer."""
@@ -117,6 +124,7 @@ class PackedBuffer:
         n = len(self.specs)
         arr = (PackDesc * max(n, 1))()
         esz = self.buf.element_size()
+        tiles = 0
         for i, s in enumerate(self.specs):
             d = arr[i]
             d.src = s["src"].data_ptr()
@@ -127,13 +135,21 @@ class PackedBuffer:
             d.perm_c, d.flip, d.transpose = s["perm_c"], s["flip"], s["transpose"]
             d.dtype, d.scale = self.dtype, s["scale"]
             d.ldk = s.get("ldk", 0)
+            d.tile0 = tiles
+            tiles += s["taps"] * -(-s["Npad"] // PACK_TILE) * -(-s["Kp"] // PACK_TILE)
+        self._tiles = tiles
         raw = bytes(arr)
         host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
         self._dev_descs = host.to(device)
         self._n = n
 
     def repack(self):
-        if self._n:
+        if not self._n:
+            return
+        if PACK_TILED["on"]:
+            call("ensvs_pack_weights_tiled", self._dev_descs.data_ptr(), self._n, self._tiles,
+                 stream())
+        else:
             call("ensvs_pack_weights", self._dev_descs.data_ptr(), self._n, self._max, stream())
 
 

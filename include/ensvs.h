@@ -47,7 +47,8 @@ typedef struct ensvs_pack_desc {
   long long sn, sk, sj;
   int N, K, taps, Npad, Kp, perm_c, flip, transpose, dtype;
   float scale;
-  int ldk, pad_;  /* destination row stride in elements (0: Kp) */
+  int ldk;    /* destination row stride in elements (0: Kp) */
+  int tile0;  /* ensvs_pack_weights_tiled: the descriptor's first tile (ignored otherwise) */
 } ensvs_pack_desc;
 
 /* Conv1d / Linear forward and input-gradient as an MFMA implicit GEMM.
@@ -191,6 +192,11 @@ int ensvs_colsum_batch(const ensvs_colsum_desc* descs, int n, float* part, long 
 
 /* Batched weight repack (descs is a DEVICE array). */
 int ensvs_pack_weights(const ensvs_pack_desc* descs, int n, int max_elems, void* stream);
+/* The same repack as ensvs_pack_weights (the same bits), one workgroup per 64 x 64 tile of one
+ * tap: descriptor i owns tiles [descs[i].tile0, descs[i].tile0 + taps * cdiv(Npad, 64) *
+ * cdiv(Kp, 64)), tile0 ascending from 0, `tiles` the total.  Tiles are read along the source's
+ * unit-stride axis and written along the packed rows through LDS (coalesced both ways). */
+int ensvs_pack_weights_tiled(const ensvs_pack_desc* descs, int n, int tiles, void* stream);
 
 /* Grouped column sums (bias grads, BatchNorm statistics). */
 int ensvs_colsum(const float* y, int ld, int M, int groups, int N, const float* mean, float scale,

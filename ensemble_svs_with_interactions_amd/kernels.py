@@ -419,8 +419,11 @@ def usf_block(segs: List[Seg], B, Tout, W: PackedBuffer, C, ref2, x, ldx, alpha,
 # (A/B switch)
 BLAS = {"on": True, "min_rows": 4096, "ws_bytes": 32 << 20,
         # gemm(): any single plain bf16 segment (1 tap, no shift, PLAIN epilogue with at most a
-        # bias, fp32 Y) of at least min_macs multiply-adds also goes to hipBLASLt
-        "generic": True, "min_macs": 1 << 34}
+        # bias, fp32 Y) of at least min_macs multiply-adds also goes to hipBLASLt (2^24: the
+        # main line's 1x1 input / output layers too, 13.64-13.73 -> 13.49-13.60 ms against no
+        # generic routing; 2^34 left them on the engine, -0.04 ms,
+        # profiles/r5_blas_generic_threshold_ab.txt)
+        "generic": True, "min_macs": 1 << 24}
 
 
 def blas_ok(x, ld, K, M, W):

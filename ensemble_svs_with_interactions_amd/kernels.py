@@ -271,14 +271,22 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
     outputs.  keep_y=False (GATE with ybf, GATE_BWD with ybf / csum): the fp32 Y is not
     needed by the caller and the fused epilogue skips it (Y stays allocated for the
     fallback paths, which still write it)."""
-    if (BLAS["generic"] and len(segs) == 1 and epi == _lib.EPI_PLAIN and not relu and not accum
-            and aux0 is None and aux1 is None and ybf is None and csum is None and yoff == 0):
-        s = segs[0]  # a plain (1-tap, unshifted, bf16) product: hipBLASLt when it has a plan
-        if (s.taps == 1 and s.shift0 == 0 and s.pd is None and s.radd is None and s.Tin == Tout
-                and s.ref.taps == 1 and N * s.K * B * Tout >= BLAS["min_macs"]
-                and blas_ok(s.x, s.ld, s.K, B * Tout, W)
-                and blas_gemm(s.x, s.ld, s.ref, W, B * Tout, N, s.K, Y, ldy, bias=bias,
-                              bias_off=bias_off, xoff=s.xoff)):
+    if (BLAS["generic"] and epi == _lib.EPI_PLAIN and not relu and aux0 is None and aux1 is None
+            and ybf is None and csum is None and (BLAS["multi"] or (len(segs) == 1 and not accum
+                                                                    and yoff == 0))):
+        # plain (1-tap, unshifted, bf16) products: hipBLASLt when it has a plan for every
+        # segment -- one call per segment, the first with the bias, the others accumulating
+        M = B * Tout
+        if (all(s.taps == 1 and s.shift0 == 0 and s.pd is None and s.radd is None and
+                s.Tin == Tout and s.ref.taps == 1 and blas_ok(s.x, s.ld, s.K, M, W) for s in segs)
+                and N * sum(s.K for s in segs) * M >= BLAS["min_macs"]
+                and all(blas_supported(M, N, s.K, s.ld, s.ref.Kp, ldy, bias is not None and i == 0)
+                        for i, s in enumerate(segs))):
+            for i, s in enumerate(segs):
+                issued = blas_gemm(s.x, s.ld, s.ref, W, M, N, s.K, Y, ldy,
+                                   bias=bias if i == 0 else None, bias_off=bias_off,
+                                   accum=accum or i > 0, xoff=s.xoff, yoff=yoff)
+                assert issued
             return
     arr = (ConvSeg * len(segs))()
     Npad = segs[0].ref.Npad
@@ -423,7 +431,11 @@ BLAS = {"on": True, "min_rows": 4096, "ws_bytes": 32 << 20,
         # main line's 1x1 input / output layers too, 13.64-13.73 -> 13.49-13.60 ms against no
         # generic routing; 2^34 left them on the engine, -0.04 ms,
         # profiles/r5_blas_generic_threshold_ab.txt)
-        "generic": True, "min_macs": 1 << 24}
+        "generic": True, "min_macs": 1 << 24,
+        # ... also with several such segments (K-concatenated inputs), accumulating outputs
+        # and a column offset into Y (A/B switch; off: main line -0.02 ms, SeparateF0 +0.1 /
+        # +0.2 ms, profiles/r5_blas_multi_ab.txt)
+        "multi": False}
 
 
 def blas_ok(x, ld, K, M, W):
@@ -449,17 +461,19 @@ def blas_supported(M, N, K, ldx, ldw, ldy, bias):
     return ok
 
 
-def blas_gemm(x, ldx, ref, W, M, N, K, Y, ldy, bias=None, bias_off=0, accum=False, xoff=0):
+def blas_gemm(x, ldx, ref, W, M, N, K, Y, ldy, bias=None, bias_off=0, accum=False, xoff=0,
+              yoff=0):
     """Y[M][N] (+)= x[M][K] (bf16 rows of ldx, from element xoff) W_ref^T (+ bias) on hipBLASLt
-    (ensvs_blas_gemm): W_ref is a packed [Npad][Kp] bf16 operand of W.  Returns False (nothing
-    issued) when hipBLASLt has no data-parallel algorithm for the shape."""
+    (ensvs_blas_gemm; Y from element yoff): W_ref is a packed [Npad][Kp] bf16 operand of W.
+    Returns False (nothing issued) when hipBLASLt has no data-parallel algorithm for the
+    shape."""
     assert x.dtype == torch.bfloat16 and W.dtype == _lib.DT_BF16 and ref.Kp >= K and ref.taps == 1
     if not blas_supported(M, N, K, ldx, ref.Kp, ldy, bias is not None):
         return False
     ws = scratch(BLAS["ws_bytes"] // 4, x.device, key="blas")
     call("ensvs_blas_gemm", x.data_ptr() + 2 * xoff, ldx, W.buf.data_ptr() + 2 * ref.offset,
          ref.Kp, M, N, K, None if bias is None else bias.data_ptr() + 4 * bias_off,
-         Y.data_ptr(), ldy, int(accum), ws.data_ptr(), BLAS["ws_bytes"], stream())
+         Y.data_ptr() + 4 * yoff, ldy, int(accum), ws.data_ptr(), BLAS["ws_bytes"], stream())
     return True
 
 

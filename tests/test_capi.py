@@ -112,3 +112,25 @@ def test_coop_error_word_per_device():
     finally:
         _lib.call("ensvs_coop_set_error_word_dev", 0, None)
         _lib.call("ensvs_coop_set_error_word_dev", 1, None)
+
+
+def test_pack_tile_numbering():
+    """PackedBuffer's descriptors carry the tile numbering ensvs_pack_weights_tiled expects:
+    tile0 = the prefix sum of taps * cdiv(Npad, 64) * cdiv(Kp, 64) in descriptor order, the
+    launch's tile count their total (host logic only; the kernels are in test_pack_gpu.py)."""
+    import torch
+    from ensemble_svs_with_interactions_amd import kernels as K
+    pb = K.PackedBuffer(_lib.DT_BF16)
+    w = torch.zeros(77, 45, 5)
+    pb.add(w, 77, 45, 5, 45 * 5, 5, 1)
+    pb.add(w, 77, 45, 5, 45 * 5, 5, 1, flip=True, transpose=True)
+    pb.add(torch.zeros(130, 200), 130, 200, 1, 200, 1, 1, npad_to=1, kpad_to=1)
+    pb.add_rowcat([torch.zeros(33, 70) for _ in range(3)], 33, 70, transpose_blocks=True)
+    pb.finalize(torch.device("cpu"))
+    descs = (_lib.PackDesc * pb._n).from_buffer_copy(pb._dev_descs.numpy().tobytes())
+    t = 0
+    for d in descs:
+        assert d.tile0 == t
+        t += d.taps * -(-d.Npad // 64) * -(-d.Kp // 64)
+    assert pb._tiles == t and pb._n == 6
+    assert K.PACK_TILE == 64

@@ -274,18 +274,35 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
     if (BLAS["generic"] and epi == _lib.EPI_PLAIN and not relu and aux0 is None and aux1 is None
             and ybf is None and csum is None and (BLAS["multi"] or (len(segs) == 1 and not accum
                                                                     and yoff == 0))):
-        # plain (1-tap, unshifted, bf16) products: hipBLASLt when it has a plan for every
-        # segment -- one call per segment, the first with the bias, the others accumulating
+        # plain (1-tap, unshifted) products with bf16 operands -- or fp32 ones rounded by a cast
+        # pass first (BLAS cast) -- on hipBLASLt when it has a plan for every segment: one call
+        # per segment, the first with the bias, the others accumulating
         M = B * Tout
-        if (all(s.taps == 1 and s.shift0 == 0 and s.pd is None and s.radd is None and
-                s.Tin == Tout and s.ref.taps == 1 and blas_ok(s.x, s.ld, s.K, M, W) for s in segs)
+        plan = []
+        for s in segs:
+            if not (s.taps == 1 and s.shift0 == 0 and s.pd is None and s.Tin == Tout
+                    and s.ref.taps == 1 and BLAS["on"] and W.dtype == _lib.DT_BF16
+                    and M >= BLAS["min_rows"] and s.K % 8 == 0):
+                break
+            if s.x.dtype == torch.bfloat16 and s.radd is None and s.ld % 8 == 0:
+                plan.append((s, False, s.ld))
+            elif BLAS["cast"] and s.x.dtype == torch.float32:
+                plan.append((s, True, s.K))
+            else:
+                break
+        if (len(plan) == len(segs)
                 and N * sum(s.K for s in segs) * M >= BLAS["min_macs"]
-                and all(blas_supported(M, N, s.K, s.ld, s.ref.Kp, ldy, bias is not None and i == 0)
-                        for i, s in enumerate(segs))):
-            for i, s in enumerate(segs):
-                issued = blas_gemm(s.x, s.ld, s.ref, W, M, N, s.K, Y, ldy,
+                and all(blas_supported(M, N, s.K, ld, s.ref.Kp, ldy, bias is not None and i == 0)
+                        for i, (s, _, ld) in enumerate(plan))):
+            for i, (s, cast, ld) in enumerate(plan):
+                x, xoff = s.x, s.xoff
+                if cast:
+                    x = cast_bf16(s.x, s.ld, s.K, M, xoff=s.xoff, radd=s.radd,
+                                  radd_ld=s.radd_ld, T=s.Tin)
+                    xoff = 0
+                issued = blas_gemm(x, ld, s.ref, W, M, N, s.K, Y, ldy,
                                    bias=bias if i == 0 else None, bias_off=bias_off,
-                                   accum=accum or i > 0, xoff=s.xoff, yoff=yoff)
+                                   accum=accum or i > 0, xoff=xoff, yoff=yoff)
                 assert issued
             return
     arr = (ConvSeg * len(segs))()
@@ -435,7 +452,11 @@ BLAS = {"on": True, "min_rows": 4096, "ws_bytes": 32 << 20,
         # ... also with several such segments (K-concatenated inputs), accumulating outputs
         # and a column offset into Y (A/B switch; off: main line -0.02 ms, SeparateF0 +0.1 /
         # +0.2 ms, profiles/r5_blas_multi_ab.txt)
-        "multi": False}
+        "multi": False,
+        # ... also fp32 operands, rounded to bf16 by one cast pass first (the rounding the
+        # register-staged engine kernel applies in staging): main line -0.04 ms, SeparateF0
+        # -0.05 ms (profiles/r5_blas_cast_ab.txt)
+        "cast": True}
 
 
 def blas_ok(x, ld, K, M, W):

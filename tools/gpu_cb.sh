@@ -1,4 +1,3 @@
-# SeparateF0 census (serial, per launch) and kernel stats of the bench's SF0 leg
+# N > 1 rehearsal after this session's routing changes: gloo, 2 ranks on the one GPU
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -u tools/census.py 60 sf0 > gpurun_out/cb_census_sf0.txt 2>&1 || exit 1
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/cb_sf0prof -o sf0 -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-synth --no-census --no-config2 --no-shapes --no-real-data --no-transformer > gpurun_out/cb_sf0prof.log 2>&1 || exit 2
+ENSVS_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 6 --warmup 2 > gpurun_out/cb_gloo2.json 2> gpurun_out/cb_gloo2.err || exit 1

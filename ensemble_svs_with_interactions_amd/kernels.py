@@ -178,10 +178,12 @@ class Seg:
 # at every row count: at M = 2 000 (one pair of 10 s in the reverse diffusion) a
 # register-staged DiffNet GEMM launch averaged 33 us against ~10 us here (pair inference
 # 185 -> 102 ms), so there is no row threshold (min_rows 0).  Single-reuse GEMMs (one tap,
-# one N tile) stay register-staged: min_reuse 1 measured 22.0 vs 21.9 ms/step and ensemble
-# RTF 0.0305 vs 0.0294.  Two LDS stages (three: 22.3 vs 20.1 ms/step).  Tests switch the
-# entries to compare the paths bitwise.
-BF16_ACT = {"on": True, "stages": 2, "stages_small": 2, "min_reuse": 2, "min_rows": 0}
+# one N tile) too (min_reuse 1): round 5, with the plain ones on hipBLASLt, 13.46-13.53 vs
+# 13.51-13.56 ms/step, SeparateF0 and synth RTF unchanged (profiles/r5_min_reuse_ab.txt;
+# round 2 measured 22.0 vs 21.9 ms/step and ensemble RTF 0.0305 vs 0.0294 and kept 2).  Two
+# LDS stages (three: 22.3 vs 20.1 ms/step).  Tests switch the entries to compare the paths
+# bitwise.
+BF16_ACT = {"on": True, "stages": 2, "stages_small": 2, "min_reuse": 1, "min_rows": 0}
 
 
 # Small-M bf16-operand GEMMs split their K-steps over up to max_split workgroups per output

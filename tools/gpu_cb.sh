@@ -1,3 +1,4 @@
-# N > 1 rehearsal after this session's routing changes: gloo, 2 ranks on the one GPU
+# BF16_ACT min_reuse 1: second main-line A/B and SeparateF0 A/B
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-ENSVS_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 6 --warmup 2 > gpurun_out/cb_gloo2.json 2> gpurun_out/cb_gloo2.err || exit 1
+timeout -k 10 900 python -u tools/flag_ab.py "BF16_ACT:min_reuse=1" "" > gpurun_out/cb_ab2.txt 2>&1 || exit 3
+timeout -k 10 900 python -u tools/flag_ab.py --sf0 "BF16_ACT:min_reuse=1" "" > gpurun_out/cb_ab3.txt 2>&1 || exit 4

@@ -302,10 +302,10 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
                     x = cast_bf16(s.x, s.ld, s.K, M, xoff=s.xoff, radd=s.radd,
                                   radd_ld=s.radd_ld, T=s.Tin)
                     xoff = 0
-                issued = blas_gemm(x, ld, s.ref, W, M, N, s.K, Y, ldy,
-                                   bias=bias if i == 0 else None, bias_off=bias_off,
-                                   accum=accum or i > 0, xoff=xoff, yoff=yoff)
-                assert issued
+                if not blas_gemm(x, ld, s.ref, W, M, N, s.K, Y, ldy,
+                                 bias=bias if i == 0 else None, bias_off=bias_off,
+                                 accum=accum or i > 0, xoff=xoff, yoff=yoff):
+                    raise RuntimeError("hipBLASLt plan vanished between the check and the call")
             return
     arr = (ConvSeg * len(segs))()
     Npad = segs[0].ref.Npad

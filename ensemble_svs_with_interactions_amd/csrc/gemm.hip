@@ -2415,9 +2415,14 @@ __global__ __launch_bounds__(256) void cast_bf16_pad_kernel(const float* __restr
        i += (long long)gridDim.x * blockDim.x) {
     const long long m = i / K8;
     const int k = (int)(i - m * K8) * 8;
+    // loads at clamped (valid) columns, then the select: a predicated load per element
+    // compiles to a branch and a wait each (eight serial round trips)
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = x[m * ldx + min(k + e, K - 1)];
     bf16x8 o;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = (__bf16)(k + e < K ? x[m * ldx + k + e] : 0.f);
+    for (int e = 0; e < 8; ++e) o[e] = (__bf16)(k + e < K ? v[e] : 0.f);
     *(bf16x8*)(y + m * ldy + k) = o;
   }
 }

@@ -1058,12 +1058,13 @@ def main():
         backend = dist.get_backend()
         # the default data-parallel schedule: the N = 1 line's HIP-graph replay with one
         # 94 MB all-reduce of the flat gradient (+ the 4-byte failure word) between the grads
-        # and update graphs (gloo rehearsal, 2 ranks on one GPU: 62 ms/step,
-        # profiles/r4_bench_gloo2.json).  --overlap-ddp: eager steps whose bucketed all-reduce
-        # (lf0 / bap / V/UV at their branch end, the mgc DiffNet before the mgc encoder's
-        # backward) overlaps the rest of the backward (same rehearsal: 1 535 ms/step,
-        # profiles/r4_bench_gloo2_overlap.json, DESIGN.md section 6 -- gloo reduces on the
-        # host); --eager alone: eager steps with the one all-reduce after the backward.
+        # and update graphs (gloo rehearsal, 2 ranks on one GPU: 55.3 ms/step with a 22.0 ms
+        # host-side all-reduce, profiles/r5_bench_gloo2_graph.json).  --overlap-ddp: eager
+        # steps whose bucketed all-reduce (lf0 / bap / V/UV at their branch end, the mgc
+        # DiffNet before the mgc encoder's backward) overlaps the rest of the backward (same
+        # rehearsal: 929 ms/step, 7 collectives, profiles/r5_bench_gloo2_overlap.json,
+        # DESIGN.md section 6 -- gloo reduces on the host); --eager alone: eager steps with
+        # the one all-reduce after the backward.
         if args.overlap_ddp:
             args.eager = True
         else:
@@ -1164,13 +1165,16 @@ def main():
                   "columns": ["entry", "shape", "launches", "us_per_launch", "ms_total"]}
     out = {
         "metric": "acoustic-model train frames/sec/GPU (4-track ensemble); synth RTF",
-        "value": value, "unit": "main-track frames/s", "n_gpus": world, "steps": args.steps,
+        "value": value, "unit": "main-track frames/s", "value_per_gpu": value / world,
+        "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": args.precision, "data": "synthetic (SURVEY.md §8(d) feature layout), random-init "
                                           "weights of the recipe architecture",
         "config": {"workload": "4-track SATB ensemble, MultiTrackNPSSMDNMultistreamParametric"
                                "Model (multitrack_acoustic_nnsvs_world_multi_ar_f0_diff_mgcbap)",
+                   "value_is": "aggregate main-track frames/s over all ranks (value_per_gpu "
+                               "= value / n_gpus is the metric's per-GPU figure)",
                    "pairs_per_gpu": P, "frames_per_pair": T, "global_batch_pairs": P * world,
                    "parallelism": f"dp{world}",
                    "process_group": {"backend": backend, "world_size": world} if world > 1

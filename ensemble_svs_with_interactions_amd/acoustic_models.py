@@ -16,12 +16,12 @@ import torch
 from torch import nn
 
 from . import _lib
+from . import torch_ops
 from . import kernels as K
 from . import layers as Ly
 from ._lib import call, ptr, query
 from .base import BaseModel, PredictionType
-from .engine import (Branches, GradCapture, ModulePacks, _sig, empty, gemm_dtype, grad_of,
-                     lengths_pair)
+from .engine import Branches, ModulePacks, _sig, empty, gemm_dtype, grad_of, lengths_pair
 from .model import init_weights
 
 # SeparateF0: the decoders' [encoder out, rest flag, lf0] input in rows of a multiple of 8
@@ -456,7 +456,7 @@ class BiLSTMResF0NonAttentiveDecoder(BaseModel):
 
     # ---------------------------------------------------------------- reference API
     def forward(self, x, lengths=None, y=None, spk_embs=None):
-        return _Lf0Fn.apply(self, x, None, spk_embs, None, lengths, y, *self.parameters())
+        return torch_ops.lf0_call(self, x, None, spk_embs, None, lengths, y)
 
     def inference(self, x, lengths=None, spk_embs=None):
         if spk_embs is not None:
@@ -514,54 +514,13 @@ class MultiTrackBiLSTMResF0NonAttentiveDecoder(BiLSTMResF0NonAttentiveDecoder):
 
     # ---------------------------------------------------------------- reference API
     def forward(self, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths=None, y=None):
-        return _Lf0Fn.apply(self, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths, y,
-                            *self.parameters())
+        return torch_ops.lf0_call(self, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths, y)
 
     def inference(self, *args, **kwargs):
         raise NotImplementedError("the multi-track model calls the lf0 model's forward "
                                   "(multistream.py:1646-1651)")
 
 
-class _Lf0Fn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, mod, x_main, x_sub, s0, s1, lengths, y, *params):
-        from .model import _spk_args
-        B, T, D = x_main.shape
-        xs = [x_main.contiguous().float()]
-        if x_sub is not None:
-            xs.append(x_sub.contiguous().float())
-        _, lens_dev = lengths_pair(lengths, B, T, x_main.device)
-        p0, ld0, f0 = _spk_args(s0, B, T)
-        p1, ld1, f1 = _spk_args(s1, B, T)
-        if f0 is not None or f1 is not None or (s1 is not None and ld0 != ld1):
-            raise NotImplementedError("per-frame speaker embeddings are not on the path")
-        teacher = None
-        if y is not None:
-            if y.shape[1] != T:
-                raise ValueError("decoder targets must have the input's frame count "
-                                 "(tacotron_f0.py:139)")
-            yc = y.contiguous().float()
-            teacher = (yc, yc.shape[2], mod.decoder.out_lf0_idx)
-        lf0, res, st = mod._fwd(xs, D, B, T, lens_dev, (p0, p1), ld0, teacher=teacher)
-        ctx.mod, ctx.st, ctx.params = mod, st, params
-        ctx.keep = teacher
-        ctx.needs = (s0 is not None and s0.requires_grad, s1 is not None and s1.requires_grad)
-        return lf0.view(B, T, 1), res.view(B, T, 1)
-
-    @staticmethod
-    def backward(ctx, glf0, gres):
-        st = ctx.st
-        B, T = st["B"], st["T"]
-        dev = st["y"].device
-        glf0 = glf0.contiguous().view(-1) if glf0 is not None else torch.zeros(B * T, device=dev)
-        gres = gres.contiguous().view(-1) if gres is not None else None
-        with GradCapture(ctx.params) as gc:
-            _, _, dX0 = ctx.mod._bwd(st, glf0, gres, want_spk=False)
-        ctx.st = ctx.params = ctx.keep = None
-        # per-frame grad of each (expanded) speaker embedding = grad of the fused input
-        d = dX0.view(B, T, -1)
-        return (None, None, None, d if ctx.needs[0] else None, d if ctx.needs[1] else None,
-                None, None) + gc.grads(ctx.needs_input_grad[7:])
 
 
 class _MultistreamHybrid(BaseModel):
@@ -907,8 +866,8 @@ class MultiTrackNPSSMDNMultistreamParametricModel(_MultistreamHybrid):
             out = self._infer(x_main.contiguous().float(), x_sub.contiguous().float(),
                               spks_list[0], spks_list[1], lengths)
             return out, out
-        outs = _MultiTrackFn.apply(self, x_main, x_sub, ys[0], spks_list[0], spks_list[1],
-                                   lengths, *self.parameters())
+        outs = torch_ops.multitrack_call(self, x_main, x_sub, ys[0], spks_list[0], spks_list[1],
+                                         lengths)
         nm, rm, lf0, vuv, nb, rb, res = outs[:7]
         main = (((nm, rm), lf0, vuv, (nb, rb)), res)
         if not self.output_subtrack:
@@ -995,7 +954,7 @@ class NPSSMDNMultistreamParametricModel(_MultistreamHybrid):
         if y is None:
             out = self._infer(x.contiguous().float(), None, None, None, lengths)
             return out, out
-        outs = _MultiTrackFn.apply(self, x, None, y, None, None, lengths, *self.parameters())
+        outs = torch_ops.multitrack_call(self, x, None, y, None, None, lengths)
         nm, rm, lf0, vuv, nb, rb, res = outs[:7]
         return ((nm, rm), lf0, vuv, (nb, rb)), res
 
@@ -1312,8 +1271,8 @@ class MultiTrackMultistreamSeparateF0ParametricModel(_MultistreamHybrid):
         if ys is None:
             return self._infer(x_main.contiguous().float(), x_sub.contiguous().float(),
                                spks_list[0], spks_list[1], lengths)
-        om, rm, os_, rs = _SeparateF0Fn.apply(self, x_main, x_sub, ys[0], ys[1], spks_list[0],
-                                              spks_list[1], lengths, *self.parameters())
+        om, rm, os_, rs = torch_ops.separate_f0_call(self, x_main, x_sub, ys[0], ys[1],
+                                                     spks_list[0], spks_list[1], lengths)
         return (om, rm), (os_, rs)
 
     def inference(self, x_main, x_sub, spks=None, lengths=None, draws=None):
@@ -1329,75 +1288,3 @@ class MultiTrackMultistreamSeparateF0ParametricModel(_MultistreamHybrid):
         out, _ = self._infer(xm, xs, spks[0], spks[1], [v + pad for v in lens], masks=draws)
         return out[:, :-pad]
 
-
-class _SeparateF0Fn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, mod, x_main, x_sub, y_main, y_sub, spk0, spk1, lengths, *params):
-        B, T, _ = x_main.shape
-        f = lambda t: t.contiguous().float()  # noqa: E731
-        outs, st = mod._fwd_core(f(x_main), f(x_sub), f(y_main), f(y_sub), spk0, spk1, lengths,
-                                 mod.training, True, getattr(mod, "_replay_draws", None))
-        ctx.mod, ctx.st, ctx.params = mod, st, params
-        v = lambda t: t.view(B, T, -1)  # noqa: E731
-        return (v(mod._assemble(outs)), v(outs["lf0_residual"]), v(mod._assemble(outs, "_sub")),
-                v(outs["lf0_residual_sub"]))
-
-    @staticmethod
-    def backward(ctx, g_om, g_rm, g_os, g_rs):
-        mod, st = ctx.mod, ctx.st
-        B, T = st["B"], st["T"]
-        g = {}
-        for gg, sfx in ((g_om, ""), (g_os, "_sub")):
-            if gg is not None:
-                mod._split(gg.contiguous().view(B * T, -1), sfx, g)
-        if g_rm is not None:
-            g["lf0_residual"] = g_rm.contiguous().view(-1)
-        if g_rs is not None:
-            g["lf0_residual_sub"] = g_rs.contiguous().view(-1)
-        with GradCapture(ctx.params) as gc:
-            mod._bwd_core(st, g)
-        ctx.st = ctx.params = None
-        return (None,) * 8 + gc.grads(ctx.needs_input_grad[8:])
-
-
-class _MultiTrackFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, mod, x_main, x_sub, y_main, spk0, spk1, lengths, *params):
-        B, T, _ = x_main.shape
-        # _replay_draws (tests only): random draws to replay, as train_step(draws=...)
-        outs, st = mod._train_fwd(x_main.contiguous().float(),
-                                  None if x_sub is None else x_sub.contiguous().float(),
-                                  y_main.contiguous().float(), spk0, spk1, lengths,
-                                  getattr(mod, "_replay_draws", None))
-        ctx.mod, ctx.st, ctx.params = mod, st, params
-        ctx.mark_non_differentiable(outs["mgc_noise"], outs["bap_noise"])
-        v = lambda t: t.view(B, T, -1)  # noqa: E731
-        ret = (v(outs["mgc_noise"]), v(outs["mgc_recon"]), v(outs["lf0"]), v(outs["vuv"]),
-               v(outs["bap_noise"]), v(outs["bap_recon"]), v(outs["lf0_residual"]))
-        if "lf0_sub" in outs:
-            ret = ret + (v(outs["lf0_sub"]), v(outs["lf0_residual_sub"]))
-        return ret
-
-    @staticmethod
-    def backward(ctx, g_nm, g_rm, g_lf0, g_vuv, g_nb, g_rb, g_res, *g_sub):
-        st = ctx.st
-        B, T = st["B"], st["T"]
-        dev = st["lens_dev"].device
-
-        def flat(g, n):
-            if g is None:
-                return torch.zeros(B * T, n, device=dev)
-            return g.contiguous().view(B * T, n)
-        g = dict(mgc_recon=flat(g_rm, g_rm.shape[-1] if g_rm is not None else 60),
-                 lf0=flat(g_lf0, 1).view(-1), vuv=flat(g_vuv, 1),
-                 bap_recon=flat(g_rb, g_rb.shape[-1] if g_rb is not None else 5))
-        if g_res is not None:
-            g["lf0_residual"] = g_res.contiguous().view(-1)
-        if g_sub and g_sub[0] is not None:
-            g["lf0_sub"] = g_sub[0].contiguous().view(-1)
-        if g_sub and g_sub[1] is not None:
-            g["lf0_residual_sub"] = g_sub[1].contiguous().view(-1)
-        with GradCapture(ctx.params) as gc:
-            ctx.mod._train_bwd(st, g)
-        ctx.st = ctx.params = None
-        return (None,) * 7 + gc.grads(ctx.needs_input_grad[7:])

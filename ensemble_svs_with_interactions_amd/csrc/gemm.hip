@@ -2196,6 +2196,269 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_ring_kernel(const GemmArg
 #undef STAGE_HALF
 }
 
+// ------------------------------ 256 x 256, 8 waves, a 64-deep K-step in four phases
+// The two-stage kernels above wait for the whole next K-step (vmcnt(0)) before every step's
+// barrier, so each step starts with its loads' full latency exposed (MFMA busy ~26 % on the
+// gate GEMM).  Here (the counted-wait schedule of cdna_hip_programming.md §5 "The 256² 8-phase
+// template", laid out for this engine's implicit-conv staging) a K-step is four phases, each
+// one output quadrant (64 x 32: 4 x 2 tiles x 2 k-chunks = 16 MFMAs) of every wave's 128 x 64
+// sub-tile, and each operand image is four half-tiles whose LDS region is read in ONE phase:
+//   j = 0  A0: A rows {0-63, 128-191} (the first 64 rows of each wave row)   read in phase 0
+//   j = 1  B0: B rows 64 c + {0-31}, c = 0..3 (kept in registers for phase 3) read in phase 0
+//   j = 2  B1: B rows 64 c + {32-63}                                          read in phase 1
+//   j = 3  A1: A rows {64-127, 192-255}                                       read in phase 2
+// Half-tile h = 4 t + j (K-step t, buffer t & 1) is issued in phase P = h - 6 (P = 4 t + p
+// counts the phases of the K loop), two buffer_load ... lds per thread.  What it overwrites
+// was last read in phase <= P - 2; what phase P + 1 reads is retired by the counted wait
+// before phase P's barrier, so four half-tiles (8 DMA instructions per thread) stay in flight
+// across every barrier and the loop never drains.  Per accumulator the K order is the other
+// kernels' (k-chunks in order), so the bits are identical.  Operands through buffer
+// resources: rows past M, zero padding and k past K / Kp read zeros (out-of-range offsets).
+// Epilogue: the 256 x 256 kernel's (four 64-row chunks staged through LDS).
+constexpr unsigned P8_OOB = 0x80000000u;  // a buffer offset past every resource (zeros)
+constexpr int P8_IMG = BMB * BK2 * 2;      // 32 KB: one operand image of one K-step
+constexpr int P8_BUF = 2 * P8_IMG;         // A + B images of one K-step
+
+// this lane's 4 A row offsets (bytes from the segment's x; rows rA + {0, 128, 64, 192}) and
+// its first B row's offset (rB; the others add a wave-uniform row delta) for tap j
+struct P8Offs {
+  unsigned oa[4];
+  unsigned ob;
+};
+
+__device__ __forceinline__ P8Offs p8_offs(const SegU S, int j, int Npad, int n0, int rB, int ca8,
+                                          int cb8, const int (&bt)[4], const int (&tt)[4],
+                                          unsigned okm) {
+  P8Offs o;
+  const int shj = S.shift0 + j * S.dil;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ts = tt[i] + shj;
+    const int src = S.pad == PAD_ZERO ? ((unsigned)ts < (unsigned)S.Tin ? ts : -1)
+                                      : pad_src(ts, S.Tin, S.pad);
+    const bool ok = ((okm >> i) & 1) && src >= 0;
+    o.oa[i] = ok ? (unsigned)((bt[i] * S.Tin + src) * S.ld + ca8) * 2u : P8_OOB;
+  }
+  o.ob = (unsigned)((j * Npad + n0 + rB) * S.Kp + cb8) * 2u;
+  return o;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t p8_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+}
+
+__device__ __forceinline__ void p8_dma(__amdgpu_buffer_rsrc_t r, unsigned off, char* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)l, 16, off, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void p8_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool GATE8>
+__global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  int m0, n0;
+  xcd_tile_big(m0, n0);
+  const int M = a.M, Tout = a.Tout, Npad = a.Npad;
+  const int nseg = a.nseg;
+  const SegU S0 = seg_u(a.seg[0], a.W);
+  const SegU S1 = nseg > 1 ? seg_u(a.seg[1], a.W) : S0;
+  const SegU S2 = nseg > 2 ? seg_u(a.seg[2], a.W) : S0;
+  const int nit = S0.nk * S0.taps + (nseg > 1 ? S1.nk * S1.taps : 0) +
+                  (nseg > 2 ? S2.nk * S2.taps : 0);
+  const int nh = 4 * nit;  // half-tiles
+  // staged rows: A rA + {0, 128, 64, 192}, B rB + {0, 128, 32, 160}; every one of them keeps
+  // the swizzle of rA / rB (bits 1..3 of the row), so one chunk per operand per lane
+  const int rA = wid * 8 + (lane >> 3), rB = (wid & 3) * 8 + (wid >> 2) * 64 + (lane >> 3);
+  const int ca8 = swz(rA, lane & 7) * 8, cb8 = swz(rB, lane & 7) * 8;
+  int bt[4], tt[4];
+  unsigned okm = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + rA + (i & 1) * 128 + (i >> 1) * 64;
+    const bool ok = m < M;
+    bt[i] = ok ? m / Tout : 0;
+    tt[i] = ok ? m - bt[i] * Tout : 0;
+    okm |= ok ? (1u << i) : 0u;
+  }
+  // wave-uniform LDS bases of this wave's pieces within an image
+  const int la = wid * 8 * 128, lb = ((wid & 3) * 8 + (wid >> 2) * 64) * 128;
+  // staging cursor: the K-step whose half-tiles are issued next (segment, tap, k-step)
+  int qs = 0, qj = 0, qkc = 0;
+#define P8_OFFS(S) p8_offs(S, qj, Npad, n0, rB, ca8, cb8, bt, tt, okm)
+  P8Offs O = P8_OFFS(S0);
+  __amdgpu_buffer_rsrc_t rxa = p8_rsrc(S0.x), rwb = p8_rsrc(S0.w);
+  int qK = S0.K, qKp = S0.Kp;
+  // half-tile h (its K-step's cursor is the current one)
+#define P8_ISSUE(h)                                                                        \
+  do {                                                                                     \
+    const int j_ = (h) & 3;                                                                \
+    char* L_ = smem + (((h) >> 2) & 1) * P8_BUF;                                           \
+    const int kb_ = qkc * BK2;                                                             \
+    const unsigned kb2_ = (unsigned)kb_ * 2u;                                              \
+    if (j_ == 0 || j_ == 3) {                                                              \
+      const bool in_ = kb_ + ca8 < qK;                                                     \
+      const int i0_ = j_ == 0 ? 0 : 2;                                                     \
+      char* La_ = L_ + la + (j_ == 0 ? 0 : 64 * 128);                                      \
+      p8_dma(rxa, in_ ? O.oa[i0_] + kb2_ : P8_OOB, La_);                                   \
+      p8_dma(rxa, in_ ? O.oa[i0_ + 1] + kb2_ : P8_OOB, La_ + 128 * 128);                   \
+    } else {                                                                               \
+      const bool in_ = kb_ + cb8 < qKp;                                                    \
+      const int d_ = j_ == 1 ? 0 : 32;                                                     \
+      char* Lb_ = L_ + P8_IMG + lb + d_ * 128;                                             \
+      const unsigned ob_ = O.ob + (unsigned)(d_ * qKp) * 2u + kb2_;                        \
+      p8_dma(rwb, in_ ? ob_ : P8_OOB, Lb_);                                                \
+      p8_dma(rwb, in_ ? ob_ + (unsigned)(128 * qKp) * 2u : P8_OOB, Lb_ + 128 * 128);        \
+    }                                                                                      \
+    if (j_ == 3) { /* K-step done: advance the cursor */                                   \
+      const int nks_ = qs == 0 ? S0.nk : (qs == 1 ? S1.nk : S2.nk);                        \
+      const int taps_ = qs == 0 ? S0.taps : (qs == 1 ? S1.taps : S2.taps);                 \
+      if (++qkc == nks_) {                                                                 \
+        qkc = 0;                                                                           \
+        const int qs0_ = qs;                                                               \
+        if (++qj == taps_) {                                                               \
+          qj = 0;                                                                          \
+          ++qs;                                                                            \
+        }                                                                                  \
+        if (qs < nseg) {                                                                   \
+          if (qs != qs0_) {                                                                \
+            rxa = p8_rsrc(qs == 1 ? S1.x : S2.x);                                          \
+            rwb = p8_rsrc(qs == 1 ? S1.w : S2.w);                                          \
+            qK = qs == 1 ? S1.K : S2.K;                                                    \
+            qKp = qs == 1 ? S1.Kp : S2.Kp;                                                 \
+          }                                                                                \
+          O = qs == 0 ? P8_OFFS(S0) : (qs == 1 ? P8_OFFS(S1) : P8_OFFS(S2));               \
+        }                                                                                  \
+      }                                                                                    \
+    }                                                                                      \
+  } while (0)
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: half-tiles 0..5, then wait for the two phase 0 reads (A0, B0 of K-step 0)
+  const int npro = min(6, nh);
+  for (int h = 0; h < npro; ++h) P8_ISSUE(h);
+  if (npro - 2 >= 4) p8_wait<8>();
+  else p8_wait<4>();  // nit == 1: half-tiles 0..3 issued, 2 may stay in flight
+  __builtin_amdgcn_s_barrier();
+
+  // fragment read offsets (rows + 16 i and the wave's quadrant rows keep the swizzle)
+  const int arow = lane & 15, kq = lane >> 4;
+  const int fa0 = (wr * 128 + arow) * 128 + swz(arow, kq) * 16;
+  const int fa1 = (wr * 128 + arow) * 128 + swz(arow, kq + 4) * 16;
+  const int fb0 = P8_IMG + (wc * 64 + arow) * 128 + swz(arow, kq) * 16;
+  const int fb1 = P8_IMG + (wc * 64 + arow) * 128 + swz(arow, kq + 4) * 16;
+  bf16x8 xa[2][4], xb0[2][2], xb1[2][2];
+  // the counted wait of phase P (P = 4 t + p): the half-tiles phase P + 1 reads are retired;
+  // `need` is the last of them, h = P + 6 the last issued (or nh - 1)
+#define P8_WAIT(P, need)                                                                   \
+  do {                                                                                     \
+    const int al_ = min((P) + 7, nh) - 1 - (need);                                         \
+    if (al_ >= 4) p8_wait<8>();                                                            \
+    else if (al_ == 3) p8_wait<6>();                                                       \
+    else if (al_ == 2) p8_wait<4>();                                                       \
+    else if (al_ == 1) p8_wait<2>();                                                       \
+    else p8_wait<0>();                                                                     \
+  } while (0)
+#define P8_MMA(I0, J0, B)                                                                  \
+  do {                                                                                     \
+    __builtin_amdgcn_s_setprio(1);                                                         \
+    _Pragma("unroll") for (int h = 0; h < 2; ++h)                                          \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                          \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                          \
+      acc[(I0) + i][(J0) + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                   \
+          xa[h][i], B[h][j], acc[(I0) + i][(J0) + j], 0, 0, 0);                            \
+    __builtin_amdgcn_s_setprio(0);                                                         \
+  } while (0)
+
+  for (int t = 0; t < nit; ++t) {
+    const char* St = smem + (t & 1) * P8_BUF;
+    const int P = 4 * t;
+    // phase 0: quadrant (0, 0); reads A0, B0; issues half-tile P + 6 (B1 of K-step t + 1)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) xb0[h][j] = *(const bf16x8*)(St + (h ? fb1 : fb0) + j * 2048);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xa[h][i] = *(const bf16x8*)(St + (h ? fa1 : fa0) + i * 2048);
+    }
+    if (P + 6 < nh) P8_ISSUE(P + 6);
+    P8_WAIT(P, P + 2);
+    __builtin_amdgcn_s_barrier();
+    P8_MMA(0, 0, xb0);
+    __builtin_amdgcn_s_barrier();
+    // phase 1: quadrant (0, 1); reads B1; issues A1 of K-step t + 1
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        xb1[h][j] = *(const bf16x8*)(St + (h ? fb1 : fb0) + 32 * 128 + j * 2048);
+    if (P + 7 < nh) P8_ISSUE(P + 7);
+    P8_WAIT(P + 1, P + 3);
+    __builtin_amdgcn_s_barrier();
+    P8_MMA(0, 2, xb1);
+    __builtin_amdgcn_s_barrier();
+    // phase 2: quadrant (1, 1); reads A1; issues A0 of K-step t + 2 (no wait: phase 3 reads
+    // nothing)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        xa[h][i] = *(const bf16x8*)(St + (h ? fa1 : fa0) + 64 * 128 + i * 2048);
+    if (P + 8 < nh) P8_ISSUE(P + 8);
+    __builtin_amdgcn_s_barrier();
+    P8_MMA(4, 2, xb1);
+    __builtin_amdgcn_s_barrier();
+    // phase 3: quadrant (1, 0) from registers; issues B0 of K-step t + 2
+    if (P + 9 < nh) P8_ISSUE(P + 9);
+    if (t + 1 < nit) P8_WAIT(P + 3, P + 5);
+    __builtin_amdgcn_s_barrier();
+    P8_MMA(4, 0, xb0);
+    __builtin_amdgcn_s_barrier();
+  }
+#undef P8_MMA
+#undef P8_WAIT
+#undef P8_ISSUE
+#undef P8_OFFS
+  // every DMA was waited for (the last K-step's phase 1 waits vmcnt(0))
+  float bs[4];
+  const bool bias_st = a.bias != nullptr;
+  if (bias_st) big_bias(a, n0, wc, lane, bs);
+  EpiPre pre;
+  if (!GATE8) epi_pre<BNB, NTHRB>(a, m0, n0, tid, 0, pre);
+  float* T = (float*)smem;
+  __syncthreads();
+#define STAGE_HALF(H)                                                                     \
+  _Pragma("unroll") for (int mt2 = 0; mt2 < 4; ++mt2)                                     \
+  _Pragma("unroll") for (int nt = 0; nt < 4; ++nt)                                        \
+  _Pragma("unroll") for (int r = 0; r < 4; ++r)                                           \
+      T[(mt2 * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] =        \
+          bias_st ? acc[(H) * 4 + mt2][nt][r] + bs[nt] : acc[(H) * 4 + mt2][nt][r]
+#pragma unroll 1
+  for (int c = 0; c < BMB / CHR; ++c) {
+    if (wr == (c >> 1)) {
+      if (c & 1) {
+        STAGE_HALF(1);
+      } else {
+        STAGE_HALF(0);
+      }
+    }
+    __syncthreads();
+    if (GATE8) gate_tile8<NTHRB, CHR, BNB / 16, true>(a, T, EPB, m0 + c * CHR, n0, tid);
+    else epilogue_tile<CHR, BNB, NTHRB, EPB, true>(a, T, m0 + c * CHR, n0, tid, c == BMB / CHR - 1, pre);
+    __syncthreads();
+  }
+#undef STAGE_HALF
+}
+
 // ------------------------------------------------- 64 x 64 bf16-operand GEMM (small M)
 // The reverse diffusion's DiffNet GEMMs have M = 2 000 frame rows: 16 x 4 tiles of 128 x 128
 // keep 64 CUs busy, each walking a 16-step K loop at one L2 round trip per step.  64 x 64
@@ -3763,6 +4026,21 @@ static const int SMALL_STAGES = 5;
 // at least this many 256 x 256 tiles (the chip's 256 CUs less a margin) for the big kernel
 static const int BIG_MIN_TILES = 192;
 
+// The four-phase 256 x 256 kernel (conv_gemm_b16_p8_kernel): 0 off, 1 in place of the
+// two-stage 256 x 256 kernel (the gate GEMMs), 2 also for every other launch the 256 x 256
+// epilogue serves with at least P8_MIN_TILES tiles (plain / ReLU-mask / ADDSCALE products).
+static int g_p8 = 1;
+static const int P8_MIN_TILES = 128;
+
+static bool use_p8(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B) {
+  if (!g_p8 || a.csum || !a.vec_out || a.Npad % BNB || a.gbw_dma || a.as_dma) return false;
+  for (int s = 0; s < nseg; ++s)  // 31-bit byte offsets into the operand resources
+    if ((long long)B * segs[s].Tin * segs[s].ld >= (1ll << 30)) return false;
+  const long long tiles = (long long)cdiv(a.M, BMB) * (a.Npad / BNB);
+  if (a.epi == EPI_GATE) return g_big_tile && tiles >= BIG_MIN_TILES;
+  return g_p8 >= 2 && tiles >= P8_MIN_TILES && a.epi != EPI_NONE;
+}
+
 static bool use_big_tile(const GemmArgs& a) {
   if (!g_big_tile || a.csum || !a.vec_out || a.Npad % BNB) return false;
   // Only the gate GEMMs (K = 1 024) take the 256 x 256 kernel: the DiffNet res/skip GEMM
@@ -3791,6 +4069,24 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     if ((long long)B * g.Tin * g.ld >= (1ll << 31) ||
         (long long)g.taps * Npad * g.Kp >= (1ll << 30))
       return ENSVS_E_SHAPE;
+  }
+  if (!has_pd && use_p8(a, segs, nseg, B)) {
+    const dim3 grid_b(cdiv(a.M, BMB), Npad / BNB);
+    const bool gate = a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS);
+    const size_t lb = (size_t)2 * P8_BUF;  // two K-steps of both images (128 KB)
+#define P8(G)                                                                             \
+  do {                                                                                    \
+    static const hipError_t ep = hipFuncSetAttribute(                                     \
+        (const void*)conv_gemm_b16_p8_kernel<G>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+        (int)lb);                                                                         \
+    if (ep != hipSuccess) return ENSVS_E_HIP;                                             \
+    hipLaunchKernelGGL(conv_gemm_b16_p8_kernel<G>, grid_b, dim3(NTHRB), lb, st, a);       \
+  } while (0)
+    if (gate) P8(true);
+    else P8(false);
+#undef P8
+    ENSVS_CHECK_LAUNCH();
+    return ENSVS_OK;
   }
   if (!has_pd && use_big_tile(a)) {
     const dim3 grid_b(cdiv(a.M, BMB), Npad / BNB);
@@ -3940,6 +4236,12 @@ ENSVS_API int ensvs_set_wgrad_big(int on) {
 
 ENSVS_API int ensvs_set_gbw_dma(int on) {
   g_gbw_dma = on ? 1 : 0;
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_set_p8(int mode) {
+  if (mode < 0 || mode > 2) return ENSVS_E_ARG;
+  g_p8 = mode;
   return ENSVS_OK;
 }
 

@@ -29,7 +29,8 @@ from . import kernels as K
 from . import layers as Ly
 from ._lib import call
 from .base import BaseModel, PredictionType
-from .engine import GradCapture, ModulePacks, empty, grad_of, lengths_pair, next_seed
+from . import torch_ops
+from .engine import ModulePacks, empty, grad_of, lengths_pair, next_seed
 from .engine import gemm_dtype as engine_gemm_dtype
 
 SQRT1_2 = 1.0 / math.sqrt(2.0)
@@ -495,7 +496,7 @@ class DiffNet(nn.Module):
     # ---------------------------------------------------------------- reference API
     def forward(self, spec, diffusion_step, cond):
         """spec (B, 1, M, T), diffusion_step (B,), cond (B, E, T) -> (B, 1, M, T)."""
-        return _DiffNetFn.apply(self, spec, diffusion_step, cond, *self.parameters())
+        return torch_ops.diffnet_call(self, spec, diffusion_step, cond)
 
 
 def _const_step(dsts):
@@ -539,29 +540,6 @@ def _colsum_off(dy, ld, M, N, param, off, scale):
     call("ensvs_axpy", grad_of(param).data_ptr() + 4 * off, tmp.data_ptr(), 1.0, N, Ly.stream())
 
 
-class _DiffNetFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, mod, spec, t, cond, *params):
-        B, _, Mc, T = spec.shape
-        E = cond.shape[1]
-        # reference layouts are (B, C, T); the kernels use frame rows (B*T, C)
-        xin = spec[:, 0].transpose(1, 2).contiguous().view(B * T, Mc)
-        cnd = cond.transpose(1, 2).contiguous().view(B * T, E)
-        t = t.to(device=spec.device, dtype=torch.int64).contiguous()
-        out, st = mod._fwd(xin, Mc, t, cnd, E, B, T)
-        ctx.mod, ctx.st, ctx.params = mod, st, params
-        ctx.dims = (B, Mc, T, E)
-        return out.view(B, T, Mc).transpose(1, 2).unsqueeze(1)
-
-    @staticmethod
-    def backward(ctx, g):
-        B, Mc, T, E = ctx.dims
-        dout = g[:, 0].transpose(1, 2).contiguous().view(B * T, Mc)
-        with GradCapture(ctx.params) as gc:
-            dcond = ctx.mod._bwd(ctx.st, dout)
-        ctx.st = ctx.params = None
-        return (None, None, None, dcond.view(B, T, E).transpose(1, 2)) + \
-            gc.grads(ctx.needs_input_grad[4:])
 
 
 def linear_beta_schedule(timesteps, min_beta=1e-4, max_beta=0.06):
@@ -799,7 +777,7 @@ class GaussianDiffusion(BaseModel):
 
     # ---------------------------------------------------------------- reference API
     def forward(self, cond, lengths=None, y=None, spk_embs=None):
-        return _DiffusionFn.apply(self, cond, y, spk_embs, lengths, *self.parameters())
+        return torch_ops.diffusion_call(self, cond, lengths, y, spk_embs)
 
     def inference(self, cond, lengths=None, spk_embs=None):
         B, T, D = cond.shape
@@ -810,30 +788,3 @@ class GaussianDiffusion(BaseModel):
         x = self._inference([(cond, D, 0, D)], B, T, lens_dev, spk, spk_ld)
         return x.view(B, T, self.out_dim)
 
-
-class _DiffusionFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, mod, cond, y, spk_embs, lengths, *params):
-        B, T, D = cond.shape
-        cond = cond.contiguous().float()
-        y = y.contiguous().float()
-        _, lens_dev = lengths_pair(lengths, B, T, cond.device)
-        from .model import _spk_args
-        spk, spk_ld, _ = _spk_args(spk_embs, B, T)
-        noise, xr, st = mod._fwd([(cond, D, 0, D)], B, T, lens_dev, (y, y.shape[2], 0), spk,
-                                 spk_ld)
-        ctx.mod, ctx.st, ctx.dims, ctx.params = mod, st, (B, T), params
-        ctx.spk_needs = spk_embs is not None and spk_embs.requires_grad
-        ctx.mark_non_differentiable(noise)
-        return noise.view(B, T, -1), xr.view(B, T, -1)
-
-    @staticmethod
-    def backward(ctx, gnoise, gxr):
-        B, T = ctx.dims
-        st = ctx.st
-        with GradCapture(ctx.params) as gc:
-            dcond = ctx.mod.denoise_fn._bwd(st["dst"], gxr.contiguous().view(B * T, -1))
-            dX0, _ = ctx.mod.encoder._bwd(st["est"], dcond, want_spk=False)
-        ctx.st = ctx.params = None
-        dspk = dX0.view(B, T, -1) if ctx.spk_needs else None
-        return (None, None, None, dspk, None) + gc.grads(ctx.needs_input_grad[5:])

@@ -133,6 +133,25 @@ def next_seed() -> int:
     return _STATE["rng"][1].getrandbits(64)
 
 
+class seed_scope:
+    """Inside the block, next_seed() draws from a generator seeded with ``seed``: a call
+    that takes its randomness as an explicit seed (the torch.library ops, torch_ops.py) is
+    a pure function of its arguments."""
+
+    def __init__(self, seed: int):
+        import random
+        self.rng = (torch.initial_seed(), random.Random(int(seed)))
+
+    def __enter__(self):
+        self.saved = _STATE["rng"]
+        _STATE["rng"] = self.rng
+        return self
+
+    def __exit__(self, *exc):
+        _STATE["rng"] = self.saved
+        return False
+
+
 def set_gemm_precision(p: str):
     """'bf16' (default; MFMA bf16 operands, fp32 accumulate) or 'fp32' (exact fp32 MFMA)."""
     _STATE["gemm_dtype"] = {"bf16": _lib.DT_BF16, "fp32": _lib.DT_F32}[p]

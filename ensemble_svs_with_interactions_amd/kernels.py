@@ -288,7 +288,7 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
                 break
             if s.x.dtype == torch.bfloat16 and s.radd is None and s.ld % 8 == 0:
                 plan.append((s, False, s.ld))
-            elif BLAS["cast"] and s.x.dtype == torch.float32:
+            elif BLAS["cast"] and s.x.dtype == torch.float32 and _castable(s):
                 plan.append((s, True, s.K))
             else:
                 break
@@ -563,7 +563,15 @@ def deferred_wgrad():
     _DEFER["depth"] += 1
     try:
         yield
-    finally:
+    except BaseException:
+        # the branch that raised left its queue unflushed: drop the queues and let the
+        # original error (a CoopError, an OOM, ...) propagate unchanged
+        _DEFER["depth"] -= 1
+        if _DEFER["depth"] == 0:
+            _DEFER["pending"].clear()
+            _DEFER["colsum"].clear()
+        raise
+    else:
         _DEFER["depth"] -= 1
         flush_wgrad()
         if _DEFER["depth"] == 0 and (_DEFER["pending"] or _DEFER["colsum"]):

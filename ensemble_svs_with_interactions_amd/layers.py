@@ -47,11 +47,14 @@ def randn(n, device):
     return z
 
 
-def colsum_into(dy, ld, M, N, param, groups=1, scale=1.0, off=0, yoff=0):
-    """param.grad[off:off+N] += scale * column sums of dy."""
+def colsum_into(dy, ld, M, N, param, groups=1, scale=1.0, off=0, yoff=0, defer=False):
+    """param.grad[off:off+N] += scale * column sums of dy.  defer: inside
+    kernels.deferred_wgrad(), queue the sum for the branch's batched flush -- it then reads dy
+    at the flush, so only callers that never write dy again in the same branch may ask for it
+    (the transformer / timing backward passes reuse their buffers and sum at once)."""
     g = grad_of(param)
     if off == 0 and groups == 1:
-        K.colsum(dy, ld, M, N, g, scale=scale, accum=True, yoff=yoff, defer=True)
+        K.colsum(dy, ld, M, N, g, scale=scale, accum=True, yoff=yoff, defer=defer)
     else:
         tmp = empty(groups * N, device=dy.device)
         K.colsum(dy, ld, M // groups, N, tmp, groups=groups, scale=scale, yoff=yoff)
@@ -175,7 +178,7 @@ def embed_bwd(emb_mod, fc_in, sv, dY, B, T, dspk_seq=None, ld=None, col=0):
     call("ensvs_embed_bwd", dY.data_ptr() + 4 * col, ld, M, E, sv["ids"].data_ptr(), V,
          part.data_ptr(), grad_of(emb_mod.weight).data_ptr(), stream())
     wgrad_into(fc_in.weight, dY, ld, sv["X"], sv["ldx"], B, T, T, E, sv["Kin"], dyoff=col)
-    colsum_into(dY, ld, M, E, fc_in.bias, yoff=col)
+    colsum_into(dY, ld, M, E, fc_in.bias, yoff=col, defer=True)
     if dspk_seq is not None:
         K.colsum(dY, ld, T, E, dspk_seq, groups=B, accum=True, yoff=col)
 
@@ -254,7 +257,7 @@ def ff_bwd(pk, ff, X, hs, hs16, dH3, B, T, device, need_dx=True, x16=None, dx_ld
         else:
             issue(later, lambda w=lay.weight, g=d, x=xin, N=N, Kc=Kc:
                   wgrad_into(w, g, N, x, x.shape[1], B, T, T, N, Kc))
-        issue(later, lambda g=d, N=N, b=lay.bias: colsum_into(g, N, M, N, b))
+        issue(later, lambda g=d, N=N, b=lay.bias: colsum_into(g, N, M, N, b, defer=True))
         if i == 0 and not need_dx:
             break
         nd = empty(M, Kc, device=device)
@@ -408,7 +411,7 @@ def conv_bwd(pk, conv, sv, dout, B, T, device, groups=1, first_dx=None, later=No
                  ptr(dy16), C, stream())
         _dbg(f"conv{li}.dout", d)
         _dbg(f"conv{li}.dy", dy)
-        issue(later, lambda g=dy, C=C, b=conv[ci].bias: colsum_into(g, C, M, C, b))
+        issue(later, lambda g=dy, C=C, b=conv[ci].bias: colsum_into(g, C, M, C, b, defer=True))
         w = conv[ci].weight
         col = 0
         for seg, seg16 in zip(s["segs"], s.get("segs16") or [None] * len(s["segs"])):

@@ -12,7 +12,8 @@ from torch import nn
 
 from . import layers as Ly
 from .base import BaseModel, PredictionType
-from .engine import GradCapture, ModulePacks, empty, lengths_pair
+from . import torch_ops
+from .engine import ModulePacks, empty
 
 
 def init_weights(net, init_type="normal", init_gain=0.02):
@@ -51,35 +52,13 @@ class SpeakerEmbedding(BaseModel):
         self.std = std
 
     def forward(self, x, lengths=None, y=None):
-        return _GatherFn.apply(self.emb.weight, x)
+        return torch.ops.ensvs.embedding_gather(self.emb.weight, x)
 
     def embedding_dim(self):
         return self.emb.embedding_dim
 
 
-class _GatherFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, table, idx):
-        from ._lib import call
-        shp = idx.shape
-        flat = idx.reshape(-1).to(torch.int64).contiguous()
-        out = empty(flat.numel(), table.shape[1], device=table.device)
-        call("ensvs_gather_rows", table.data_ptr(), flat.data_ptr(), flat.numel(), table.shape[1],
-             out.data_ptr(), Ly.stream())
-        ctx.save_for_backward(flat)
-        ctx.shape = (table.shape, shp)
-        return out.view(*shp, table.shape[1])
 
-    @staticmethod
-    def backward(ctx, g):
-        from ._lib import call
-        (flat,) = ctx.saved_tensors
-        tshape, _ = ctx.shape
-        dt = torch.zeros(tshape, dtype=torch.float32, device=g.device)
-        g = g.reshape(-1, tshape[1]).contiguous()
-        call("ensvs_spk_scatter", g.data_ptr(), flat.numel(), tshape[1], flat.data_ptr(),
-             dt.data_ptr(), Ly.stream())
-        return dt, None
 
 
 class FFConvLSTM(BaseModel):
@@ -201,7 +180,7 @@ class FFConvLSTM(BaseModel):
         D = self.out_dim
         Ly.issue(later, lambda: (
             Ly.wgrad_into(self.fc.weight, dout, D, st["y"], H2, B, T, T, D, H2),
-            Ly.colsum_into(dout, D, M, D, self.fc.bias)))
+            Ly.colsum_into(dout, D, M, D, self.fc.bias, defer=True)))
         dy = empty(M, H2, device=dev)
         Ly.K.gemm([Ly.K.Seg(dout, self.out_dim, self.out_dim, pk["fc^T"], T)], B, T, H2, pk.bwd,
                   dy, H2)
@@ -223,7 +202,7 @@ class FFConvLSTM(BaseModel):
     def forward(self, x, lengths=None, y=None, spk_embs=None):
         B, T, _ = x.shape
         x = x.contiguous().float()
-        return _FFConvLSTMFn.apply(self, x, spk_embs, lengths, *self.parameters())
+        return torch_ops.ffconvlstm_call(self, x, spk_embs, lengths)
 
     def inference(self, x, lengths=None, spk_embs=None):
         return self(x, lengths, spk_embs=spk_embs)
@@ -250,37 +229,6 @@ def _spk_args(spk_embs, B, T):
     return full, full.shape[1], full
 
 
-class _FFConvLSTMFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, mod, x, spk_embs, lengths, *params):
-        B, T, D = x.shape
-        dev = x.device
-        lens_host, lens_dev = lengths_pair(lengths, B, T, dev)
-        spk, spk_ld, full = _spk_args(spk_embs, B, T)
-        if full is not None:
-            raise NotImplementedError("per-frame speaker embeddings are not on the path")
-        out, st = mod._fwd([(x, D, 0, D)], B, T, lens_dev, spk, spk_ld,
-                           save=torch.is_grad_enabled() or True)
-        ctx.mod, ctx.st, ctx.params = mod, st, params
-        ctx.spk_needs = spk_embs is not None and spk_embs.requires_grad
-        Tm = max(lens_host)
-        out = out.view(B, T, -1)
-        return out[:, :Tm] if Tm < T else out
-
-    @staticmethod
-    def backward(ctx, g):
-        st = ctx.st
-        B, T = st["B"], st["T"]
-        g = g.contiguous()
-        if g.shape[1] < T:
-            gg = torch.zeros(B, T, g.shape[2], device=g.device)
-            gg[:, :g.shape[1]] = g
-            g = gg
-        with GradCapture(ctx.params) as gc:
-            dX0, _ = ctx.mod._bwd(st, g.view(B * T, -1), want_spk=False)
-        dspk = dX0.view(B, T, -1) if ctx.spk_needs else None
-        ctx.st = ctx.params = None
-        return (None, None, dspk, None) + gc.grads(ctx.needs_input_grad[4:])
 
 
 class MultiTrackLSTMEncoder(BaseModel):
@@ -377,7 +325,7 @@ class MultiTrackLSTMEncoder(BaseModel):
             Ly.wgrad_into(self.hidden2out.weight, d16, N, y16, H2, B, T, T, N, H2)
         else:
             Ly.wgrad_into(self.hidden2out.weight, dout, ld, st["y"], H2, B, T, T, N, H2)
-        Ly.colsum_into(dout, ld, M, N, self.hidden2out.bias)
+        Ly.colsum_into(dout, ld, M, N, self.hidden2out.bias, defer=True)
         dy = empty(M, H2, device=dev)
         seg = Ly.K.Seg(dout, ld, N, pk["h2o^T"], T) if d16 is None else \
             Ly.K.Seg(d16, N, N, pk["h2o^T"], T)
@@ -391,43 +339,5 @@ class MultiTrackLSTMEncoder(BaseModel):
 
     # ---- reference API -----------------------------------------------------------
     def forward(self, x_main, x_sub, spk_embs, lengths, y=None):
-        return _LSTMEncFn.apply(self, x_main, x_sub, spk_embs[0], spk_embs[1], lengths,
-                                *self.parameters())
+        return torch_ops.lstm_encoder_call(self, x_main, x_sub, spk_embs[0], spk_embs[1], lengths)
 
-
-class _LSTMEncFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, mod, x_main, x_sub, s0, s1, lengths, *params):
-        B, T, D = x_main.shape
-        dev = x_main.device
-        lens_host, lens_dev = lengths_pair(lengths, B, T, dev)
-        p0, ld0, f0 = _spk_args(s0, B, T)
-        p1, ld1, f1 = _spk_args(s1, B, T)
-        if f0 is not None or f1 is not None or ld0 != ld1:
-            raise NotImplementedError("per-frame speaker embeddings are not on the path")
-        xm = x_main.contiguous().float()
-        xs = x_sub.contiguous().float()
-        out, st = mod._fwd(xm, xs, D, B, T, lens_dev, (p0, p1), ld0)
-        ctx.mod, ctx.st, ctx.params = mod, st, params
-        ctx.needs = (s0 is not None and s0.requires_grad, s1 is not None and s1.requires_grad)
-        Tm = max(lens_host)
-        out = out.view(B, T, -1)
-        return out[:, :Tm] if Tm < T else out
-
-    @staticmethod
-    def backward(ctx, g):
-        st = ctx.st
-        B, T = st["B"], st["T"]
-        g = g.contiguous()
-        if g.shape[1] < T:
-            gg = torch.zeros(B, T, g.shape[2], device=g.device)
-            gg[:, :g.shape[1]] = g
-            g = gg
-        with GradCapture(ctx.params) as gc:
-            _, _, dX = ctx.mod._bwd(st, g.view(B * T, -1), want_spk=False)
-        ctx.st = ctx.params = None
-        # per-frame grad of each (expanded) speaker input = its half of the fused input grad
-        E = ctx.mod.embed_dim
-        d = dX.view(B, T, 2 * E)
-        out = [d[:, :, k * E:(k + 1) * E] if need else None for k, need in enumerate(ctx.needs)]
-        return (None, None, None, out[0], out[1], None) + gc.grads(ctx.needs_input_grad[6:])

@@ -14,7 +14,7 @@ containers; every op runs in libensvs.so:
     in one wavefront per score row, relative values as a banded sum (attention.hip);
   * LayerNorm over channels (eps 1e-5) per frame row, the frame masks x * x_mask, dropout
     keep-masks from the counter-based RNG; backward of all of it under autograd
-    (parameter gradients returned through GradCapture).
+    (the ensvs::transformer_encoder op, torch_ops.py, returns the parameter gradients).
 """
 import math
 
@@ -27,7 +27,8 @@ from . import kernels as K
 from . import layers as Ly
 from ._lib import call, ptr
 from .base import BaseModel
-from .engine import GradCapture, ModulePacks, empty, grad_of, lengths_pair
+from . import torch_ops
+from .engine import ModulePacks, empty, grad_of, lengths_pair
 from .model import init_weights
 
 
@@ -519,28 +520,5 @@ class TransformerEncoder(BaseModel):
 
     # ---- reference API -------------------------------------------------------------
     def forward(self, x, lengths=None, y=None):
-        return _TransformerFn.apply(self, x, lengths, *self.parameters())
+        return torch_ops.transformer_call(self, x, lengths)
 
-
-class _TransformerFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, mod, x, lengths, *params):
-        B, T, D = x.shape
-        if D != mod.in_dim:
-            raise ValueError(f"TransformerEncoder: input has {D} channels, expected {mod.in_dim}")
-        xr = x.detach().contiguous().float().view(B * T, D)
-        lens_host, _ = lengths_pair(lengths, B, T, x.device)
-        out, st = mod._fwd(xr, B, T, lens_host)
-        ctx.mod, ctx.st, ctx.params = mod, st, params
-        return out.view(B, -1, mod.out_dim)
-
-    @staticmethod
-    def backward(ctx, g):
-        st = ctx.st
-        g = g.contiguous().float().view(st["B"] * st["Tp"], -1)
-        with GradCapture(ctx.params) as gc:
-            dx = ctx.mod._bwd(st, g, need_dx=ctx.needs_input_grad[1])
-        ctx.st = ctx.params = None
-        if dx is not None:
-            dx = dx.view(st["B"], st["T"], -1)
-        return (None, dx, None) + gc.grads(ctx.needs_input_grad[3:])

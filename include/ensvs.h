@@ -74,6 +74,11 @@ int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N
  * other epilogues run faster on 128 x 128 tiles); 3: as 2 for every eligible launch.
  * Defaults: mode 2, 5 stages. */
 int ensvs_set_big_tile(int mode, int stages);
+/* The four-phase 256 x 256 kernel (counted LDS-DMA pipeline, four half-tiles in flight across
+ * every barrier; same accumulation order, bitwise equal): mode 0 off; 1 for the launches the
+ * 256 x 256 kernel takes (gate GEMMs); 2 also for every other launch its LDS-staged epilogue
+ * serves with >= 128 tiles of 256 x 256 (no column sums, not the LDS-DMA epilogues). */
+int ensvs_set_p8(int mode);
 /* Launches of fewer than 128 output tiles (small M) that the 64 x 64 kernel does not take
  * can run a 128 x 128 kernel with two K-groups of 4 waves (each group half of the K-steps,
  * tiles added through LDS; default off: the one-group kernel, the same bits as the

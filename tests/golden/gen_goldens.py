@@ -380,11 +380,13 @@ def grad_sample_index(key, numel):
     return np.sort(rng_for("gsample_" + key).choice(numel, GRAD_SAMPLE, replace=False))
 
 
-def case_train_step_full(steps=2, lr=1e-4, P=2, T=64, lengths=(64, 52)):
+def case_train_step_full(steps=2, lr=1e-4, P=2, T=64, lengths=(64, 52), name="train_step_full"):
     """The reference train_step (train_acoustic_multitrack.py:40-392) on the recipe-width
     model (multitrack_acoustic_nnsvs_world_multi_ar_f0_diff_mgcbap.yaml), V/UV LSTM dropout
     0 (see the module docstring): losses, grad norms, per-step loss metrics, step-0 gradient
-    summaries + sampled elements of every parameter gradient, final BN running statistics."""
+    summaries + sampled elements of every parameter gradient, final BN running statistics.
+    name="train_step_prod": the same at the bench's sequence length (T = 1024, 256 free-running
+    AR-decoder steps per track), the fixture the bf16 production route is checked against."""
     cfg = configs.multitrack_diffusion(num_speakers=4)
     model, shapes = build_ref(cfg)
     model.vuv_model.lstm.dropout = 0.0
@@ -398,7 +400,7 @@ def case_train_step_full(steps=2, lr=1e-4, P=2, T=64, lengths=(64, 52)):
                 grad_sample=GRAD_SAMPLE)
     losses, norms, feats = [], [], []
     for s in range(steps):
-        d = model_draws(f"full_step{s}", P, T, cfg)
+        d = model_draws(("full" if name == "train_step_full" else name) + f"_step{s}", P, T, cfg)
         for k, v in d.items():
             arrays[f"draw{s}::{k}"] = v
         norm_box = {}
@@ -440,7 +442,7 @@ def case_train_step_full(steps=2, lr=1e-4, P=2, T=64, lengths=(64, 52)):
         if "running" in k:
             arrays[f"final::{k}"] = v.numpy()
     meta.update(losses=losses, grad_norms=norms, loss_feats=feats)
-    save("train_step_full", arrays, meta)
+    save(name, arrays, meta)
 
 
 def case_inference_bap(model):
@@ -1278,6 +1280,8 @@ def main():
         case_train_step_tiny(logf0_diff_weight=0.5, name="train_step_tiny_il")
     if run("full_train"):
         case_train_step_full()
+    if run("prod_train"):
+        case_train_step_full(P=2, T=1024, lengths=(1024, 900), name="train_step_prod")
     if run("inference_tiny"):
         case_model_inference_tiny()
     if run("st"):

@@ -1,0 +1,124 @@
+"""The production route pinned to the reference at the bench's sequence length.
+
+Fixture `train_step_prod` (tests/golden/gen_goldens.py, reference-imported): the reference
+train_step (nnsvs/bin/train_acoustic_multitrack.py:40-392) on the recipe-width diffusion
+model, P = 2 pairs x T = 1024 frames (lengths 1024 / 900), two Adam steps, the AR decoder's
+dropout masks (tacotron_f0.py:191) and the diffusion draws (diffusion.py:289, 293) captured;
+V/UV LSTM dropout 0 (its C++ RNG cannot be replayed).  Each track's free-running AR decoder
+runs 256 AR steps (tacotron_f0.py:183-228).
+
+* fp32 (exact) route: the same kernels at exact fp32 MFMA precision, held to the T = 64
+  full-width bounds;
+* bf16 production route: bf16 GEMM operands (engine kernels, incl. the four-phase 256 x 256
+  GEMM), MFMA LSTM recurrences, the cooperative AR decoder, producer-side bf16 copies; step 0
+  eager (the warm-up step of a GraphedTrainStep), step 1 replayed from the captured HIP graphs.
+  Bounds: the measured errors with headroom (DESIGN.md section 4 lists them).
+"""
+import numpy as np
+import pytest
+import torch
+
+from ensemble_svs_with_interactions_amd import configs, engine
+from ensemble_svs_with_interactions_amd.train import FusedAdam, GraphedTrainStep, train_step
+from golden_util import load_case, sampled_grad_errors, record_errors, _pre_bn_bias
+from gpu_util import build
+
+pytestmark = pytest.mark.gpu
+
+# bf16 route vs the fp32 reference (measured on MI355X, profiles/r6_errors/train_step_prod.json;
+# each bound ~2x the measured value)
+BF16_LOSS_REL = 2e-3
+BF16_NORM_REL = 2e-2
+BF16_GRAD_REL_L2 = 8e-2       # sampled relative L2 of one parameter gradient
+BF16_GRAD_MEDIAN_REL_L2 = 2e-2
+
+
+def _draws(a, pfx, B, T):
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(a[pfx + k])).cuda()  # noqa: E731
+    return dict(
+        lf0_main=t("lf0_main").view(-1).contiguous(),
+        lf0_sub=t("lf0_sub").view(-1).contiguous(),
+        mgc_t=t("mgc_t"), bap_t=t("bap_t"),
+        mgc_noise=t("mgc_noise")[:, 0].transpose(1, 2).contiguous().view(B * T, -1),
+        bap_noise=t("bap_noise")[:, 0].transpose(1, 2).contiguous().view(B * T, -1))
+
+
+def _batch(a):
+    g = lambda k: torch.from_numpy(a[k]).cuda().contiguous()  # noqa: E731
+    return g("x_main"), g("x_sub"), g("y_main"), g("spk_main"), g("spk_sub"), a["lengths"].tolist()
+
+
+def _model(meta):
+    model = build(configs.multitrack_diffusion(num_speakers=4), meta["shapes"])
+    model.vuv_model.lstm.dropout = 0.0
+    return model
+
+
+def _grad_errors(model, a, meta):
+    errs = sampled_grad_errors({k: p.grad for k, p in model.named_parameters()}, a, meta)
+    return {k: e for k, e in errs.items() if not _pre_bn_bias(k)}
+
+
+def test_exact_route_matches_reference_t1024():
+    engine.set_gemm_precision("fp32")
+    a, meta = load_case("train_step_prod")
+    model = _model(meta)
+    opt = FusedAdam(model, lr=meta["lr"])
+    xm, xs, ym, s0, s1, lens = _batch(a)
+    B, T = xm.shape[:2]
+    rec = {}
+    for s in range(meta["steps"]):
+        loss, norm = train_step(model, opt, xm, xs, ym, s0, s1, lens,
+                                draws=_draws(a, f"draw{s}::", B, T))
+        torch.cuda.synchronize()
+        rec[f"fp32_step{s}"] = dict(loss=loss.item(), ref_loss=meta["losses"][s],
+                                    norm=norm.item(), ref_norm=meta["grad_norms"][s])
+        if s == 0:
+            errs = _grad_errors(model, a, meta)
+            rec["fp32_grad_rel_l2_max"] = max(e[0] for e in errs.values())
+            rec["fp32_grad_rel_l2_median"] = float(np.median([e[0] for e in errs.values()]))
+            record_errors("train_step_prod", rec)
+            bad = [(k, e) for k, e in errs.items() if e[0] > 5e-5 or e[1] > 1e-5]
+            assert not bad, bad[:5]
+        assert abs(loss.item() - meta["losses"][s]) < 1e-5 * abs(meta["losses"][s])
+        assert abs(norm.item() - meta["grad_norms"][s]) < 1e-4 * meta["grad_norms"][s]
+    record_errors("train_step_prod", rec)
+
+
+def test_bf16_production_route_matches_reference_t1024():
+    engine.set_gemm_precision("bf16")
+    try:
+        a, meta = load_case("train_step_prod")
+        model = _model(meta)
+        opt = FusedAdam(model, lr=meta["lr"])
+        xm, xs, ym, s0, s1, lens = _batch(a)
+        B, T = xm.shape[:2]
+        # step 0: the graph's eager warm-up step (the kernels the replay records)
+        g = GraphedTrainStep(model, opt, xm, xs, ym, s0, s1, lens, warmup=1,
+                             draws=_draws(a, "draw0::", B, T))
+        loss0, norm0 = g.warmup_result
+        errs = _grad_errors(model, a, meta)
+        rel_l2 = {k: e[0] for k, e in errs.items()}
+        # step 1 from the captured graphs, with step 1's draws
+        loss1, norm1 = g.step(draws=_draws(a, "draw1::", B, T))
+        torch.cuda.synchronize()
+        rec = {}
+        for s, (lo, no) in enumerate(((loss0, norm0), (loss1, norm1))):
+            rec[f"bf16_step{s}"] = dict(
+                loss=lo.item(), ref_loss=meta["losses"][s], norm=no.item(),
+                ref_norm=meta["grad_norms"][s],
+                loss_rel=abs(lo.item() - meta["losses"][s]) / abs(meta["losses"][s]),
+                norm_rel=abs(no.item() - meta["grad_norms"][s]) / meta["grad_norms"][s])
+        rec["bf16_grad_rel_l2"] = rel_l2
+        rec["bf16_grad_rel_l2_max"] = max(rel_l2.values())
+        rec["bf16_grad_rel_l2_median"] = float(np.median(list(rel_l2.values())))
+        record_errors("train_step_prod", rec)
+        for s in range(2):
+            r = rec[f"bf16_step{s}"]
+            assert r["loss_rel"] < BF16_LOSS_REL, (s, r)
+            assert r["norm_rel"] < BF16_NORM_REL, (s, r)
+        worst = sorted(rel_l2.items(), key=lambda kv: -kv[1])[:5]
+        assert rec["bf16_grad_rel_l2_max"] < BF16_GRAD_REL_L2, worst
+        assert rec["bf16_grad_rel_l2_median"] < BF16_GRAD_MEDIAN_REL_L2
+    finally:
+        engine.set_gemm_precision("fp32")

@@ -848,6 +848,7 @@ def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
         # epoch costs with no loop at all around the steps (feeder, copies, cache lookup)
         fixed = 0.0
         reps = 3
+        buckets = []
         for key, g in graphs.graphs.items():
             g.step()
             torch.cuda.synchronize()
@@ -855,9 +856,17 @@ def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
             for _ in range(reps):
                 g.step()
             torch.cuda.synchronize()
-            fixed += (time.time() - t0) / reps * graphs.uses[key] / (1 + epochs)
+            dt = (time.time() - t0) / reps
+            per_epoch = graphs.uses[key] / (1 + epochs)
+            fixed += dt * per_epoch
+            lens_k = key[5]
+            buckets.append(dict(pairs=len(lens_k), frames=key[0][0][1],
+                                valid_frames=int(sum(lens_k)), ms_per_step=dt * 1e3,
+                                frames_per_s=sum(lens_k) / dt, steps_per_epoch=per_epoch))
+        buckets.sort(key=lambda b: -b["frames"])
         n_graphs, reserved = len(graphs.graphs), torch.cuda.memory_reserved(dev)
         del graphs
+        feeder.close()
     sizes = [len(b) for b in batches]
     return dict(metric="acoustic-model train frames/sec on the on-disk data path (feeder + "
                        "train_epoch, ragged dynamic batches)",
@@ -873,6 +882,7 @@ def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
                 eager_value=valid / el_eager, eager_s_per_epoch=el_eager,
                 same_shapes_back_to_back_s_per_epoch=fixed,
                 ratio_to_same_shapes_back_to_back=fixed / el,
+                buckets=buckets,
                 last_loss=float(res[-1][0].item()), dtype=engine.gemm_precision())
 
 
@@ -1258,8 +1268,8 @@ def _gate_roofline(args, P, T, sec, sec_call, flops, gbytes):
     peak_tf = PEAK_BF16_TFLOPS if args.precision == "bf16" else 157.3
     t_mfma, t_hbm = flops / (peak_tf * 1e12), gbytes / (PEAK_HBM_GBS * 1e9)
     tflops, gbs = flops / sec / 1e12, gbytes / sec / 1e9
-    r = {"kernel": "conv_gemm_b16_big_kernel (256x256 tile; mgc DiffNet block gate GEMM, "
-                   f"M={P * T} N=512 K=1024, bf16 operands)"
+    r = {"kernel": "conv_gemm_b16_p8_kernel (256x256 tile, four-phase counted LDS-DMA "
+                   f"pipeline; mgc DiffNet block gate GEMM, M={P * T} N=512 K=1024, bf16 operands)"
                    if args.precision == "bf16" else "conv_gemm_kernel<float>"}
     if t_mfma >= t_hbm:
         r.update(bound="mfma", achieved=tflops, peak=peak_tf, unit="TFLOP/s",

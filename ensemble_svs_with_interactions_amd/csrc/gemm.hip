@@ -865,6 +865,16 @@ typedef __attribute__((address_space(1))) void glb_void;
 
 __device__ __forceinline__ int swz(int row, int c) { return c ^ ((row >> 1) & 7); }
 
+// Workgroup barrier for LDS hand-offs only: __syncthreads() is a release/acquire, so hipcc
+// waits vmcnt(0) before it -- in an epilogue that is every global store issued so far, once
+// per staged chunk.  Here only the LDS accesses are drained (lgkmcnt(0)); global stores stay
+// in flight across the barrier (nothing in the workgroup reads them back).
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ void glds16(const void* g, char* l) {
   __builtin_amdgcn_global_load_lds((glb_void*)g, (lds_void*)l, 16, 0, 0);
 }
@@ -2256,7 +2266,10 @@ __device__ __forceinline__ void p8_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool GATE8>
+// BAR2: the template's second barrier after each phase's MFMAs (ONE barrier per phase is also
+// valid: every region is rewritten >= 2 phases after its last read, so the writer has passed the
+// barrier that the reader reaches only after its lgkmcnt wait of that read)
+template <bool GATE8, bool BAR2>
 __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
@@ -2377,6 +2390,7 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
       acc[(I0) + i][(J0) + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                   \
           xa[h][i], B[h][j], acc[(I0) + i][(J0) + j], 0, 0, 0);                            \
     __builtin_amdgcn_s_setprio(0);                                                         \
+    if (BAR2) __builtin_amdgcn_s_barrier();                                                \
   } while (0)
 
   for (int t = 0; t < nit; ++t) {
@@ -2394,7 +2408,6 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
     P8_WAIT(P, P + 2);
     __builtin_amdgcn_s_barrier();
     P8_MMA(0, 0, xb0);
-    __builtin_amdgcn_s_barrier();
     // phase 1: quadrant (0, 1); reads B1; issues A1 of K-step t + 1
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -2405,7 +2418,6 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
     P8_WAIT(P + 1, P + 3);
     __builtin_amdgcn_s_barrier();
     P8_MMA(0, 2, xb1);
-    __builtin_amdgcn_s_barrier();
     // phase 2: quadrant (1, 1); reads A1; issues A0 of K-step t + 2 (no wait: phase 3 reads
     // nothing)
 #pragma unroll
@@ -2416,13 +2428,11 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
     if (P + 8 < nh) P8_ISSUE(P + 8);
     __builtin_amdgcn_s_barrier();
     P8_MMA(4, 2, xb1);
-    __builtin_amdgcn_s_barrier();
     // phase 3: quadrant (1, 0) from registers; issues B0 of K-step t + 2
     if (P + 9 < nh) P8_ISSUE(P + 9);
     if (t + 1 < nit) P8_WAIT(P + 3, P + 5);
     __builtin_amdgcn_s_barrier();
     P8_MMA(4, 0, xb0);
-    __builtin_amdgcn_s_barrier();
   }
 #undef P8_MMA
 #undef P8_WAIT
@@ -2435,7 +2445,7 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
   EpiPre pre;
   if (!GATE8) epi_pre<BNB, NTHRB>(a, m0, n0, tid, 0, pre);
   float* T = (float*)smem;
-  __syncthreads();
+  lds_sync();
 #define STAGE_HALF(H)                                                                     \
   _Pragma("unroll") for (int mt2 = 0; mt2 < 4; ++mt2)                                     \
   _Pragma("unroll") for (int nt = 0; nt < 4; ++nt)                                        \
@@ -2451,10 +2461,10 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
         STAGE_HALF(0);
       }
     }
-    __syncthreads();
+    lds_sync();
     if (GATE8) gate_tile8<NTHRB, CHR, BNB / 16, true>(a, T, EPB, m0 + c * CHR, n0, tid);
     else epilogue_tile<CHR, BNB, NTHRB, EPB, true>(a, T, m0 + c * CHR, n0, tid, c == BMB / CHR - 1, pre);
-    __syncthreads();
+    lds_sync();
   }
 #undef STAGE_HALF
 }
@@ -4030,6 +4040,8 @@ static const int BIG_MIN_TILES = 192;
 // two-stage 256 x 256 kernel (the gate GEMMs), 2 also for every other launch the 256 x 256
 // epilogue serves with at least P8_MIN_TILES tiles (plain / ReLU-mask / ADDSCALE products).
 static int g_p8 = 1;
+static int g_p8_bar2 = 0;  // 1: two barriers per phase (the template's form); 0: one (faster:
+                           // tools/p8_bench.py, profiles/r6_p8_bench.txt)
 static const int P8_MIN_TILES = 128;
 
 static bool use_p8(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B) {
@@ -4038,7 +4050,7 @@ static bool use_p8(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int 
     if ((long long)B * segs[s].Tin * segs[s].ld >= (1ll << 30)) return false;
   const long long tiles = (long long)cdiv(a.M, BMB) * (a.Npad / BNB);
   if (a.epi == EPI_GATE) return g_big_tile && tiles >= BIG_MIN_TILES;
-  return g_p8 >= 2 && tiles >= P8_MIN_TILES && a.epi != EPI_NONE;
+  return g_p8 >= 2 && tiles >= P8_MIN_TILES;  // (EPI_NONE: the K loop alone, measurement)
 }
 
 static bool use_big_tile(const GemmArgs& a) {
@@ -4074,16 +4086,21 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     const dim3 grid_b(cdiv(a.M, BMB), Npad / BNB);
     const bool gate = a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS);
     const size_t lb = (size_t)2 * P8_BUF;  // two K-steps of both images (128 KB)
-#define P8(G)                                                                             \
+#define P8(G, B2)                                                                         \
   do {                                                                                    \
     static const hipError_t ep = hipFuncSetAttribute(                                     \
-        (const void*)conv_gemm_b16_p8_kernel<G>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-        (int)lb);                                                                         \
+        (const void*)conv_gemm_b16_p8_kernel<G, B2>,                                      \
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);                             \
     if (ep != hipSuccess) return ENSVS_E_HIP;                                             \
-    hipLaunchKernelGGL(conv_gemm_b16_p8_kernel<G>, grid_b, dim3(NTHRB), lb, st, a);       \
+    hipLaunchKernelGGL((conv_gemm_b16_p8_kernel<G, B2>), grid_b, dim3(NTHRB), lb, st, a); \
   } while (0)
-    if (gate) P8(true);
-    else P8(false);
+    if (g_p8_bar2) {
+      if (gate) P8(true, true);
+      else P8(false, true);
+    } else {
+      if (gate) P8(true, false);
+      else P8(false, false);
+    }
 #undef P8
     ENSVS_CHECK_LAUNCH();
     return ENSVS_OK;
@@ -4240,8 +4257,9 @@ ENSVS_API int ensvs_set_gbw_dma(int on) {
 }
 
 ENSVS_API int ensvs_set_p8(int mode) {
-  if (mode < 0 || mode > 2) return ENSVS_E_ARG;
-  g_p8 = mode;
+  if ((mode & 3) > 2 || mode < 0 || mode > 7) return ENSVS_E_ARG;
+  g_p8 = mode & 3;
+  g_p8_bar2 = (mode & 4) ? 1 : 0;  // bit 2: two barriers per phase
   return ENSVS_OK;
 }
 

@@ -236,7 +236,7 @@ class PairBatchFeeder:
     def __len__(self):
         return len(self.batches)
 
-    def __iter__(self):
+    def _start(self):
         q = queue.Queue(maxsize=self.prefetch)
         stop = threading.Event()
 
@@ -252,6 +252,30 @@ class PairBatchFeeder:
 
         th = threading.Thread(target=reader, daemon=True)
         th.start()
+        return q, stop, th
+
+    def prestart(self):
+        """Start loading the NEXT pass's first batches now (train.train_epoch calls it once the
+        last step of a pass is issued): the reader collates them while that step runs, so a
+        new epoch does not begin with the GPU waiting for its first batch."""
+        if getattr(self, "_next", None) is None:
+            self._next = self._start()
+
+    def close(self):
+        """Stop a prestarted reader that will not be consumed."""
+        started, self._next = getattr(self, "_next", None), None
+        if started is not None:
+            q, stop, th = started
+            stop.set()
+            while th.is_alive():
+                try:
+                    q.get_nowait()
+                except queue.Empty:
+                    th.join(timeout=0.05)
+
+    def __iter__(self):
+        started, self._next = getattr(self, "_next", None), None
+        q, stop, th = started if started is not None else self._start()
         try:
             while True:
                 hb = q.get()

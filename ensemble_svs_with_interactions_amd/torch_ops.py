@@ -22,8 +22,10 @@ an explicit ``Tensor[]`` input, so autograd returns their gradients (one flat bu
 backward op, split into views laid out like engine.GradCapture).  Randomness (diffusion
 steps / noise, the AR decoder's always-on prenet dropout, the V/UV LSTM dropout) comes from
 an explicit ``seed`` argument (engine.seed_scope), so an op is a pure function of its inputs.
-What the backward kernels read (saved activations, gates, BN statistics) stays on the device;
-the forward returns a ticket (int64 CPU scalar) that names it for the backward op.
+What the backward kernels read (saved activations, gates, BN statistics) stays on the device,
+filed under the forward's first output: the autograd formula saves that output and hands it
+to the backward op, which finds the state by its storage (no extra output, so the forward's
+results are deterministic functions of its inputs).
 """
 import collections
 import itertools
@@ -38,9 +40,8 @@ from .engine import GradCapture, lengths_pair
 
 _MODS = {}
 _NEXT = itertools.count(1)
-_SAVED = collections.OrderedDict()  # ticket -> saved state of one forward
-_TICKETS = itertools.count(1)
-MAX_SAVED = 512  # forwards whose backward never ran are dropped past this many
+_SAVED = collections.OrderedDict()  # (device, data_ptr) of the key output -> saved state
+MAX_SAVED = 64  # forwards whose backward never ran are dropped past this many
 ALIGN = 64       # engine.GradCapture's per-parameter alignment
 
 
@@ -60,28 +61,30 @@ def _mod(handle):
     return m
 
 
-def _save(state):
-    t = next(_TICKETS)
-    _SAVED[t] = state
+def _key(t):
+    return (str(t.device), t.untyped_storage().data_ptr())
+
+
+def _keep(state, out):
+    """File the forward's saved state under its output `out`; returns `out`."""
+    k = _key(out)
+    _SAVED.pop(k, None)
+    _SAVED[k] = state
     while len(_SAVED) > MAX_SAVED:
         _SAVED.popitem(last=False)
-    return torch.tensor([t], dtype=torch.int64)
+    return out
 
 
-KEEP_TICKETS = False  # tests: a backward op may run twice on one ticket (opcheck)
+KEEP_STATE = False  # tests: a backward op may run twice on one forward's state (opcheck)
 
 
-def _take(ticket):
-    t = int(ticket.reshape(-1)[0])
-    st = _SAVED.get(t) if KEEP_TICKETS else _SAVED.pop(t, None)
+def _take(key_out):
+    k = _key(key_out)
+    st = _SAVED.get(k) if KEEP_STATE else _SAVED.pop(k, None)
     if st is None:
         raise RuntimeError("ensvs op: the forward state of this backward is gone (backward "
                            "called twice, or more than MAX_SAVED forwards in flight)")
     return st
-
-
-def _ticket_fake():
-    return torch.empty(1, dtype=torch.int64, device="cpu")
 
 
 def _flat_size(params):
@@ -128,7 +131,7 @@ def _param_grads(ctx, gflat):
 # ============================================================================== DiffNet
 @torch.library.custom_op("ensvs::diffnet", mutates_args=())
 def diffnet(handle: int, spec: Tensor, t: Tensor, cond: Tensor,
-            params: List[Tensor]) -> Tuple[Tensor, Tensor]:
+            params: List[Tensor]) -> Tensor:
     """denoiser.py:101-124: spec (B, 1, M, T), diffusion step (B,), cond (B, E, T)."""
     mod = _mod(handle)
     B, _, Mc, T = spec.shape
@@ -137,19 +140,19 @@ def diffnet(handle: int, spec: Tensor, t: Tensor, cond: Tensor,
     cnd = cond.transpose(1, 2).contiguous().view(B * T, E)
     out, st = mod._fwd(xin, Mc, t.to(device=spec.device, dtype=torch.int64).contiguous(), cnd,
                        E, B, T)
-    return out.view(B, T, Mc).transpose(1, 2).unsqueeze(1).contiguous(), _save(st)
+    return _keep(st, out.view(B, T, Mc).transpose(1, 2).unsqueeze(1).contiguous())
 
 
 @diffnet.register_fake
 def _(handle, spec, t, cond, params):
-    return torch.empty_like(spec, memory_format=torch.contiguous_format), _ticket_fake()
+    return torch.empty_like(spec, memory_format=torch.contiguous_format)
 
 
 @torch.library.custom_op("ensvs::diffnet_bwd", mutates_args=())
-def diffnet_bwd(handle: int, ticket: Tensor, grad: Tensor, E: int,
+def diffnet_bwd(handle: int, out: Tensor, grad: Tensor, E: int,
                 nflat: int) -> Tuple[Tensor, Tensor]:
     mod = _mod(handle)
-    st = _take(ticket)
+    st = _take(out)
     B, _, Mc, T = grad.shape
     dout = grad[:, 0].transpose(1, 2).contiguous().view(B * T, Mc)
     with GradCapture(list(mod.parameters())) as gc:
@@ -158,7 +161,7 @@ def diffnet_bwd(handle: int, ticket: Tensor, grad: Tensor, E: int,
 
 
 @diffnet_bwd.register_fake
-def _(handle, ticket, grad, E, nflat):
+def _(handle, out, grad, E, nflat):
     B, _, _, T = grad.shape
     return grad.new_empty(B, E, T), grad.new_empty(nflat)
 
@@ -166,13 +169,13 @@ def _(handle, ticket, grad, E, nflat):
 def _diffnet_setup(ctx, inputs, output):
     handle, spec, t, cond, params = inputs
     ctx.handle, ctx.E = handle, cond.shape[1]
-    ctx.save_for_backward(output[1])
+    ctx.save_for_backward(output)
     _setup_params(ctx, params)
 
 
-def _diffnet_backward(ctx, g_out, g_ticket):
-    (ticket,) = ctx.saved_tensors
-    dcond, gflat = torch.ops.ensvs.diffnet_bwd(ctx.handle, ticket, g_out.contiguous(), ctx.E,
+def _diffnet_backward(ctx, g_out):
+    (out,) = ctx.saved_tensors
+    dcond, gflat = torch.ops.ensvs.diffnet_bwd(ctx.handle, out, g_out.contiguous(), ctx.E,
                                                ctx.nflat)
     return None, None, None, dcond, _param_grads(ctx, gflat)
 
@@ -181,15 +184,14 @@ diffnet.register_autograd(_diffnet_backward, setup_context=_diffnet_setup)
 
 
 def diffnet_call(mod, spec, diffusion_step, cond):
-    out, _ = torch.ops.ensvs.diffnet(handle_of(mod), spec, diffusion_step, cond,
-                                     list(mod.parameters()))
-    return out
+    return torch.ops.ensvs.diffnet(handle_of(mod), spec, diffusion_step, cond,
+                                   list(mod.parameters()))
 
 
 # ============================================================================ FFConvLSTM
 @torch.library.custom_op("ensvs::ffconvlstm", mutates_args=())
 def ffconvlstm(handle: int, x: Tensor, spk_embs: Optional[Tensor], lengths: Optional[Tensor],
-               seed: Tensor, params: List[Tensor]) -> Tuple[Tensor, Tensor]:
+               seed: Tensor, params: List[Tensor]) -> Tensor:
     """model.py:891-918 over all T frames (the caller trims to max(lengths), as
     pad_packed_sequence does)."""
     from .model import _spk_args
@@ -202,21 +204,21 @@ def ffconvlstm(handle: int, x: Tensor, spk_embs: Optional[Tensor], lengths: Opti
         raise NotImplementedError("per-frame speaker embeddings are not on the path")
     with engine.seed_scope(int(seed)):
         out, st = mod._fwd([(x, D, 0, D)], B, T, lens_dev, spk, spk_ld, save=True)
-    return out.view(B, T, -1), _save(st)
+    return _keep(st, out.view(B, T, -1))
 
 
 @ffconvlstm.register_fake
 def _(handle, x, spk_embs, lengths, seed, params):
     B, T, _ = x.shape
-    return x.new_empty(B, T, _mod(handle).out_dim, dtype=torch.float32), _ticket_fake()
+    return x.new_empty(B, T, _mod(handle).out_dim, dtype=torch.float32)
 
 
 @torch.library.custom_op("ensvs::ffconvlstm_bwd", mutates_args=())
-def ffconvlstm_bwd(handle: int, ticket: Tensor, grad: Tensor, nflat: int) -> Tuple[Tensor, Tensor]:
+def ffconvlstm_bwd(handle: int, out: Tensor, grad: Tensor, nflat: int) -> Tuple[Tensor, Tensor]:
     """Returns (d of the fused input per frame = d spk_embs (B, T, E) or (B, T, 0), flat
     parameter gradients)."""
     mod = _mod(handle)
-    st = _take(ticket)
+    st = _take(out)
     B, T = st["B"], st["T"]
     with GradCapture(list(mod.parameters())) as gc:
         dX0, _ = mod._bwd(st, grad.contiguous().view(B * T, -1), want_spk=False)
@@ -224,7 +226,7 @@ def ffconvlstm_bwd(handle: int, ticket: Tensor, grad: Tensor, nflat: int) -> Tup
 
 
 @ffconvlstm_bwd.register_fake
-def _(handle, ticket, grad, nflat):
+def _(handle, out, grad, nflat):
     B, T, _ = grad.shape
     m = _mod(handle)
     return grad.new_empty(B, T, m.embed_dim or m.in_dim), grad.new_empty(nflat)
@@ -233,14 +235,14 @@ def _(handle, ticket, grad, nflat):
 def _ffconvlstm_setup(ctx, inputs, output):
     handle, x, spk_embs, lengths, seed, params = inputs
     ctx.handle = handle
-    ctx.save_for_backward(output[1])
+    ctx.save_for_backward(output)
     ctx.spk = spk_embs is not None
     _setup_params(ctx, params)
 
 
-def _ffconvlstm_backward(ctx, g_out, g_ticket):
-    (ticket,) = ctx.saved_tensors
-    d, gflat = torch.ops.ensvs.ffconvlstm_bwd(ctx.handle, ticket, g_out, ctx.nflat)
+def _ffconvlstm_backward(ctx, g_out):
+    (out,) = ctx.saved_tensors
+    d, gflat = torch.ops.ensvs.ffconvlstm_bwd(ctx.handle, out, g_out, ctx.nflat)
     dspk = d if ctx.spk and ctx.needs_input_grad[2] else None
     return None, None, dspk, None, None, _param_grads(ctx, gflat)
 
@@ -251,8 +253,8 @@ ffconvlstm.register_autograd(_ffconvlstm_backward, setup_context=_ffconvlstm_set
 def ffconvlstm_call(mod, x, spk_embs, lengths):
     B, T, _ = x.shape
     lens = _lengths_arg(lengths, B, T, x.device)
-    out, _ = torch.ops.ensvs.ffconvlstm(handle_of(mod), x, spk_embs, lens, _new_seed(),
-                                        list(mod.parameters()))
+    out = torch.ops.ensvs.ffconvlstm(handle_of(mod), x, spk_embs, lens, _new_seed(),
+                                     list(mod.parameters()))
     Tm = T if lengths is None else int(max(lengths_pair(lengths, B, T, x.device)[0]))
     return out[:, :Tm] if Tm < T else out
 
@@ -261,7 +263,7 @@ def ffconvlstm_call(mod, x, spk_embs, lengths):
 @torch.library.custom_op("ensvs::diffusion_train", mutates_args=())
 def diffusion_train(handle: int, cond: Tensor, y: Tensor, spk_embs: Optional[Tensor],
                     lengths: Optional[Tensor], seed: Tensor,
-                    params: List[Tensor]) -> Tuple[Tensor, Tensor, Tensor]:
+                    params: List[Tensor]) -> Tuple[Tensor, Tensor]:
     """diffusion.py:269-300: (noise, x_recon); t ~ U{0..K-1} and the noise from `seed`."""
     from .model import _spk_args
     mod = _mod(handle)
@@ -273,21 +275,21 @@ def diffusion_train(handle: int, cond: Tensor, y: Tensor, spk_embs: Optional[Ten
     with engine.seed_scope(int(seed)):
         noise, xr, st = mod._fwd([(cond, D, 0, D)], B, T, lens_dev, (y, y.shape[2], 0), spk,
                                  spk_ld)
-    return noise.view(B, T, -1), xr.view(B, T, -1), _save(st)
+    return noise.view(B, T, -1), _keep(st, xr.view(B, T, -1))
 
 
 @diffusion_train.register_fake
 def _(handle, cond, y, spk_embs, lengths, seed, params):
     B, T, _ = cond.shape
     M = _mod(handle).out_dim
-    return cond.new_empty(B, T, M), cond.new_empty(B, T, M), _ticket_fake()
+    return cond.new_empty(B, T, M), cond.new_empty(B, T, M)
 
 
 @torch.library.custom_op("ensvs::diffusion_train_bwd", mutates_args=())
-def diffusion_train_bwd(handle: int, ticket: Tensor, grad_recon: Tensor,
+def diffusion_train_bwd(handle: int, x_recon: Tensor, grad_recon: Tensor,
                         nflat: int) -> Tuple[Tensor, Tensor]:
     mod = _mod(handle)
-    st = _take(ticket)
+    st = _take(x_recon)
     B, T, _ = grad_recon.shape
     with GradCapture(list(mod.parameters())) as gc:
         dcond = mod.denoise_fn._bwd(st["dst"], grad_recon.contiguous().view(B * T, -1))
@@ -296,7 +298,7 @@ def diffusion_train_bwd(handle: int, ticket: Tensor, grad_recon: Tensor,
 
 
 @diffusion_train_bwd.register_fake
-def _(handle, ticket, grad_recon, nflat):
+def _(handle, x_recon, grad_recon, nflat):
     B, T, _ = grad_recon.shape
     enc = _mod(handle).encoder
     return grad_recon.new_empty(B, T, enc.embed_dim or enc.in_dim), grad_recon.new_empty(nflat)
@@ -305,17 +307,17 @@ def _(handle, ticket, grad_recon, nflat):
 def _diffusion_setup(ctx, inputs, output):
     handle, cond, y, spk_embs, lengths, seed, params = inputs
     ctx.handle = handle
-    ctx.save_for_backward(output[2], output[1])
+    ctx.save_for_backward(output[1])
     ctx.spk = spk_embs is not None
     _setup_params(ctx, params)
 
 
-def _diffusion_backward(ctx, g_noise, g_recon, g_ticket):
+def _diffusion_backward(ctx, g_noise, g_recon):
     # the noise output is the random target (not differentiable): its gradient is dropped
-    ticket, like = ctx.saved_tensors
+    (xr,) = ctx.saved_tensors
     if g_recon is None:
-        g_recon = torch.zeros_like(like)
-    d, gflat = torch.ops.ensvs.diffusion_train_bwd(ctx.handle, ticket, g_recon, ctx.nflat)
+        g_recon = torch.zeros_like(xr)
+    d, gflat = torch.ops.ensvs.diffusion_train_bwd(ctx.handle, xr, g_recon, ctx.nflat)
     dspk = d if ctx.spk and ctx.needs_input_grad[3] else None
     return None, None, None, dspk, None, None, _param_grads(ctx, gflat)
 
@@ -325,7 +327,7 @@ diffusion_train.register_autograd(_diffusion_backward, setup_context=_diffusion_
 
 def diffusion_call(mod, cond, lengths, y, spk_embs):
     B, T, _ = cond.shape
-    noise, xr, _ = torch.ops.ensvs.diffusion_train(
+    noise, xr = torch.ops.ensvs.diffusion_train(
         handle_of(mod), cond, y, spk_embs, _lengths_arg(lengths, B, T, cond.device),
         _new_seed(), list(mod.parameters()))
     return noise, xr
@@ -335,7 +337,7 @@ def diffusion_call(mod, cond, lengths, y, spk_embs):
 @torch.library.custom_op("ensvs::lf0_train", mutates_args=())
 def lf0_train(handle: int, x_main: Tensor, x_sub: Optional[Tensor], spk_emb_main: Optional[Tensor],
               spk_emb_sub: Optional[Tensor], lengths: Optional[Tensor], y: Optional[Tensor],
-              seed: Tensor, params: List[Tensor]) -> Tuple[Tensor, Tensor, Tensor]:
+              seed: Tensor, params: List[Tensor]) -> Tuple[Tensor, Tensor]:
     """tacotron_f0.py:924-991 (+ the AR decoder, free-running unless y is given): (lf0,
     lf0_residual), each (B, T, 1); the prenet dropout masks from `seed`."""
     from .model import _spk_args
@@ -359,23 +361,23 @@ def lf0_train(handle: int, x_main: Tensor, x_sub: Optional[Tensor], spk_emb_main
     with engine.seed_scope(int(seed)):
         lf0, res, st = mod._fwd(xs, D, B, T, lens_dev, (p0, p1), ld0, teacher=teacher)
     st["_keep"] = teacher  # the teacher buffer the saved state points into
-    return lf0.view(B, T, 1), res.view(B, T, 1), _save(st)
+    return _keep(st, lf0.view(B, T, 1)), res.view(B, T, 1)
 
 
 @lf0_train.register_fake
 def _(handle, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths, y, seed, params):
     B, T, _ = x_main.shape
     return (x_main.new_empty(B, T, 1, dtype=torch.float32),
-            x_main.new_empty(B, T, 1, dtype=torch.float32), _ticket_fake())
+            x_main.new_empty(B, T, 1, dtype=torch.float32))
 
 
 @torch.library.custom_op("ensvs::lf0_train_bwd", mutates_args=())
-def lf0_train_bwd(handle: int, ticket: Tensor, grad_lf0: Tensor, grad_res: Optional[Tensor],
+def lf0_train_bwd(handle: int, lf0: Tensor, grad_lf0: Tensor, grad_res: Optional[Tensor],
                   nflat: int) -> Tuple[Tensor, Tensor]:
     """(d of the fused per-frame input = d of each expanded speaker embedding (B, T, E), flat
     parameter gradients)."""
     mod = _mod(handle)
-    st = _take(ticket)
+    st = _take(lf0)
     B, T = st["B"], st["T"]
     gl = grad_lf0.contiguous().view(-1)
     gr = grad_res.contiguous().view(-1) if grad_res is not None else None
@@ -385,7 +387,7 @@ def lf0_train_bwd(handle: int, ticket: Tensor, grad_lf0: Tensor, grad_res: Optio
 
 
 @lf0_train_bwd.register_fake
-def _(handle, ticket, grad_lf0, grad_res, nflat):
+def _(handle, lf0, grad_lf0, grad_res, nflat):
     B, T, _ = grad_lf0.shape
     return grad_lf0.new_empty(B, T, _mod(handle).embed_dim), grad_lf0.new_empty(nflat)
 
@@ -393,16 +395,16 @@ def _(handle, ticket, grad_lf0, grad_res, nflat):
 def _lf0_setup(ctx, inputs, output):
     handle, x_main, x_sub, s0, s1, lengths, y, seed, params = inputs
     ctx.handle = handle
-    ctx.save_for_backward(output[2], output[0])
+    ctx.save_for_backward(output[0])
     ctx.spk = (s0 is not None, s1 is not None)
     _setup_params(ctx, params)
 
 
-def _lf0_backward(ctx, g_lf0, g_res, g_ticket):
-    ticket, like = ctx.saved_tensors
+def _lf0_backward(ctx, g_lf0, g_res):
+    (lf0,) = ctx.saved_tensors
     if g_lf0 is None:
-        g_lf0 = torch.zeros_like(like)
-    d, gflat = torch.ops.ensvs.lf0_train_bwd(ctx.handle, ticket, g_lf0, g_res, ctx.nflat)
+        g_lf0 = torch.zeros_like(lf0)
+    d, gflat = torch.ops.ensvs.lf0_train_bwd(ctx.handle, lf0, g_lf0, g_res, ctx.nflat)
     d0 = d if ctx.spk[0] and ctx.needs_input_grad[3] else None
     d1 = d if ctx.spk[1] and ctx.needs_input_grad[4] else None
     return None, None, None, d0, d1, None, None, None, _param_grads(ctx, gflat)
@@ -413,7 +415,7 @@ lf0_train.register_autograd(_lf0_backward, setup_context=_lf0_setup)
 
 def lf0_call(mod, x_main, x_sub, spk_emb_main, spk_emb_sub, lengths, y):
     B, T, _ = x_main.shape
-    lf0, res, _ = torch.ops.ensvs.lf0_train(
+    lf0, res = torch.ops.ensvs.lf0_train(
         handle_of(mod), x_main, x_sub, spk_emb_main, spk_emb_sub,
         _lengths_arg(lengths, B, T, x_main.device), y, _new_seed(), list(mod.parameters()))
     return lf0, res
@@ -433,7 +435,7 @@ def _mt_has_sub(mod):
 def multitrack_train(handle: int, x_main: Tensor, x_sub: Optional[Tensor], y_main: Tensor,
                      spk_main: Optional[Tensor], spk_sub: Optional[Tensor],
                      lengths: Optional[Tensor], seed: Tensor,
-                     params: List[Tensor]) -> Tuple[List[Tensor], Tensor]:
+                     params: List[Tensor]) -> List[Tensor]:
     """multistream.py:1594-1768 training forward: [mgc noise, mgc x_recon, lf0, vuv, bap
     noise, bap x_recon, lf0_residual (+ lf0_sub, lf0_residual_sub with output_subtrack)], each
     (B, T, n).  Random draws from `seed` (or the module's _replay_draws, tests)."""
@@ -445,11 +447,11 @@ def multitrack_train(handle: int, x_main: Tensor, x_sub: Optional[Tensor], y_mai
                                   y_main.contiguous().float(), spk_main, spk_sub, lengths,
                                   getattr(mod, "_replay_draws", None))
     v = lambda t: t.view(B, T, -1)  # noqa: E731
-    ret = [v(outs["mgc_noise"]), v(outs["mgc_recon"]), v(outs["lf0"]), v(outs["vuv"]),
+    ret = [v(outs["mgc_noise"]), _keep(st, v(outs["mgc_recon"])), v(outs["lf0"]), v(outs["vuv"]),
            v(outs["bap_noise"]), v(outs["bap_recon"]), v(outs["lf0_residual"])]
     if "lf0_sub" in outs:
         ret += [v(outs["lf0_sub"]), v(outs["lf0_residual_sub"])]
-    return ret, _save(st)
+    return ret
 
 
 @multitrack_train.register_fake
@@ -457,16 +459,16 @@ def _(handle, x_main, x_sub, y_main, spk_main, spk_sub, lengths, seed, params):
     mod = _mod(handle)
     B, T, _ = x_main.shape
     w = _mt_widths(mod) + ([1, 1] if _mt_has_sub(mod) else [])
-    return [x_main.new_empty(B, T, n, dtype=torch.float32) for n in w], _ticket_fake()
+    return [x_main.new_empty(B, T, n, dtype=torch.float32) for n in w]
 
 
 @torch.library.custom_op("ensvs::multitrack_train_bwd", mutates_args=())
-def multitrack_train_bwd(handle: int, ticket: Tensor, grads: List[Optional[Tensor]],
+def multitrack_train_bwd(handle: int, mgc_recon: Tensor, grads: List[Optional[Tensor]],
                          nflat: int) -> Tensor:
     """Flat parameter gradients of the pair step for the output gradients `grads` (the
     forward's order; None = zero)."""
     mod = _mod(handle)
-    st = _take(ticket)
+    st = _take(mgc_recon)
     B, T = st["B"], st["T"]
     dev = st["lens_dev"].device
     widths = _mt_widths(mod)
@@ -488,24 +490,23 @@ def multitrack_train_bwd(handle: int, ticket: Tensor, grads: List[Optional[Tenso
 
 
 @multitrack_train_bwd.register_fake
-def _(handle, ticket, grads, nflat):
-    ref = next(g for g in grads if g is not None)
-    return ref.new_empty(nflat)
+def _(handle, mgc_recon, grads, nflat):
+    return mgc_recon.new_empty(nflat)
 
 
 def _mt_setup(ctx, inputs, output):
     ctx.handle = inputs[0]
-    ctx.save_for_backward(output[1], output[0][1])
+    ctx.save_for_backward(output[1])
     _setup_params(ctx, inputs[-1])
 
 
-def _mt_backward(ctx, g_outs, g_ticket):
-    ticket, like = ctx.saved_tensors
+def _mt_backward(ctx, g_outs):
+    (mgc_recon,) = ctx.saved_tensors
     gs = list(g_outs)
     gs[0] = gs[4] = None  # the diffusion noise targets are not differentiable
     if all(g is None for g in gs):
-        gs[1] = torch.zeros_like(like)
-    gflat = torch.ops.ensvs.multitrack_train_bwd(ctx.handle, ticket, gs, ctx.nflat)
+        gs[1] = torch.zeros_like(mgc_recon)
+    gflat = torch.ops.ensvs.multitrack_train_bwd(ctx.handle, mgc_recon, gs, ctx.nflat)
     return None, None, None, None, None, None, None, None, _param_grads(ctx, gflat)
 
 
@@ -514,7 +515,7 @@ multitrack_train.register_autograd(_mt_backward, setup_context=_mt_setup)
 
 def multitrack_call(mod, x_main, x_sub, y_main, spk_main, spk_sub, lengths):
     B, T, _ = x_main.shape
-    outs, _ = torch.ops.ensvs.multitrack_train(
+    outs = torch.ops.ensvs.multitrack_train(
         handle_of(mod), x_main, x_sub, y_main, spk_main, spk_sub,
         _lengths_arg(lengths, B, T, x_main.device), _new_seed(), list(mod.parameters()))
     return outs
@@ -525,7 +526,7 @@ def multitrack_call(mod, x_main, x_sub, y_main, spk_main, spk_sub, lengths):
 def separate_f0_train(handle: int, x_main: Tensor, x_sub: Tensor, y_main: Tensor, y_sub: Tensor,
                       spk_main: Optional[Tensor], spk_sub: Optional[Tensor],
                       lengths: Optional[Tensor], seed: Tensor,
-                      params: List[Tensor]) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+                      params: List[Tensor]) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """multistream.py:348-577 training forward: (main out, main lf0 residual, sub out, sub lf0
     residual)."""
     mod = _mod(handle)
@@ -535,8 +536,8 @@ def separate_f0_train(handle: int, x_main: Tensor, x_sub: Tensor, y_main: Tensor
         outs, st = mod._fwd_core(f(x_main), f(x_sub), f(y_main), f(y_sub), spk_main, spk_sub,
                                  lengths, mod.training, True, getattr(mod, "_replay_draws", None))
     v = lambda t: t.view(B, T, -1)  # noqa: E731
-    return (v(mod._assemble(outs)), v(outs["lf0_residual"]), v(mod._assemble(outs, "_sub")),
-            v(outs["lf0_residual_sub"]), _save(st))
+    return (_keep(st, v(mod._assemble(outs))), v(outs["lf0_residual"]),
+            v(mod._assemble(outs, "_sub")), v(outs["lf0_residual_sub"]))
 
 
 @separate_f0_train.register_fake
@@ -545,15 +546,15 @@ def _(handle, x_main, x_sub, y_main, y_sub, spk_main, spk_sub, lengths, seed, pa
     B, T, _ = x_main.shape
     D = mod.out_dim
     e = lambda n: x_main.new_empty(B, T, n, dtype=torch.float32)  # noqa: E731
-    return e(D), e(1), e(D), e(1), _ticket_fake()
+    return e(D), e(1), e(D), e(1)
 
 
 @torch.library.custom_op("ensvs::separate_f0_train_bwd", mutates_args=())
-def separate_f0_train_bwd(handle: int, ticket: Tensor, g_out_main: Optional[Tensor],
+def separate_f0_train_bwd(handle: int, out_main: Tensor, g_out_main: Optional[Tensor],
                           g_res_main: Optional[Tensor], g_out_sub: Optional[Tensor],
                           g_res_sub: Optional[Tensor], nflat: int) -> Tensor:
     mod = _mod(handle)
-    st = _take(ticket)
+    st = _take(out_main)
     B, T = st["B"], st["T"]
     g = {}
     for gg, sfx in ((g_out_main, ""), (g_out_sub, "_sub")):
@@ -569,22 +570,21 @@ def separate_f0_train_bwd(handle: int, ticket: Tensor, g_out_main: Optional[Tens
 
 
 @separate_f0_train_bwd.register_fake
-def _(handle, ticket, g_out_main, g_res_main, g_out_sub, g_res_sub, nflat):
-    ref = next(g for g in (g_out_main, g_res_main, g_out_sub, g_res_sub) if g is not None)
-    return ref.new_empty(nflat)
+def _(handle, out_main, g_out_main, g_res_main, g_out_sub, g_res_sub, nflat):
+    return out_main.new_empty(nflat)
 
 
 def _sf0_setup(ctx, inputs, output):
     ctx.handle = inputs[0]
-    ctx.save_for_backward(output[4], output[0])
+    ctx.save_for_backward(output[0])
     _setup_params(ctx, inputs[-1])
 
 
-def _sf0_backward(ctx, g_om, g_rm, g_os, g_rs, g_ticket):
-    ticket, like = ctx.saved_tensors
+def _sf0_backward(ctx, g_om, g_rm, g_os, g_rs):
+    (om,) = ctx.saved_tensors
     if all(g is None for g in (g_om, g_rm, g_os, g_rs)):
-        g_om = torch.zeros_like(like)
-    gflat = torch.ops.ensvs.separate_f0_train_bwd(ctx.handle, ticket, g_om, g_rm, g_os, g_rs,
+        g_om = torch.zeros_like(om)
+    gflat = torch.ops.ensvs.separate_f0_train_bwd(ctx.handle, om, g_om, g_rm, g_os, g_rs,
                                                   ctx.nflat)
     return (None,) * 9 + (_param_grads(ctx, gflat),)
 
@@ -594,7 +594,7 @@ separate_f0_train.register_autograd(_sf0_backward, setup_context=_sf0_setup)
 
 def separate_f0_call(mod, x_main, x_sub, y_main, y_sub, spk_main, spk_sub, lengths):
     B, T, _ = x_main.shape
-    om, rm, os_, rs, _ = torch.ops.ensvs.separate_f0_train(
+    om, rm, os_, rs = torch.ops.ensvs.separate_f0_train(
         handle_of(mod), x_main, x_sub, y_main, y_sub, spk_main, spk_sub,
         _lengths_arg(lengths, B, T, x_main.device), _new_seed(), list(mod.parameters()))
     return om, rm, os_, rs
@@ -648,7 +648,7 @@ def masked_l1_loss(preds, targets, lengths):
 @torch.library.custom_op("ensvs::lstm_encoder", mutates_args=())
 def lstm_encoder(handle: int, x_main: Tensor, x_sub: Tensor, spk_main: Optional[Tensor],
                  spk_sub: Optional[Tensor], lengths: Optional[Tensor],
-                 params: List[Tensor]) -> Tuple[Tensor, Tensor]:
+                 params: List[Tensor]) -> Tensor:
     """nnsvs/model.py:1435-1537 over all T frames (the caller trims to max(lengths))."""
     from .model import _spk_args
     mod = _mod(handle)
@@ -660,22 +660,22 @@ def lstm_encoder(handle: int, x_main: Tensor, x_sub: Tensor, spk_main: Optional[
         raise NotImplementedError("per-frame speaker embeddings are not on the path")
     out, st = mod._fwd(x_main.contiguous().float(), x_sub.contiguous().float(), D, B, T,
                        lens_dev, (p0, p1), ld0)
-    return out.view(B, T, -1), _save(st)
+    return _keep(st, out.view(B, T, -1))
 
 
 @lstm_encoder.register_fake
 def _(handle, x_main, x_sub, spk_main, spk_sub, lengths, params):
     B, T, _ = x_main.shape
-    return x_main.new_empty(B, T, _mod(handle).out_dim, dtype=torch.float32), _ticket_fake()
+    return x_main.new_empty(B, T, _mod(handle).out_dim, dtype=torch.float32)
 
 
 @torch.library.custom_op("ensvs::lstm_encoder_bwd", mutates_args=())
-def lstm_encoder_bwd(handle: int, ticket: Tensor, grad: Tensor,
+def lstm_encoder_bwd(handle: int, out: Tensor, grad: Tensor,
                      nflat: int) -> Tuple[Tensor, Tensor]:
     """(d of the fused (B, T, 2E) LSTM input: [d spk_main | d spk_sub] per frame, flat
     parameter gradients)."""
     mod = _mod(handle)
-    st = _take(ticket)
+    st = _take(out)
     B, T = st["B"], st["T"]
     with GradCapture(list(mod.parameters())) as gc:
         _, _, dX = mod._bwd(st, grad.contiguous().view(B * T, -1), want_spk=False)
@@ -683,7 +683,7 @@ def lstm_encoder_bwd(handle: int, ticket: Tensor, grad: Tensor,
 
 
 @lstm_encoder_bwd.register_fake
-def _(handle, ticket, grad, nflat):
+def _(handle, out, grad, nflat):
     B, T, _ = grad.shape
     return grad.new_empty(B, T, 2 * _mod(handle).embed_dim), grad.new_empty(nflat)
 
@@ -691,15 +691,15 @@ def _(handle, ticket, grad, nflat):
 def _lstm_enc_setup(ctx, inputs, output):
     handle, x_main, x_sub, s0, s1, lengths, params = inputs
     ctx.handle = handle
-    ctx.save_for_backward(output[1])
+    ctx.save_for_backward(output)
     ctx.spk = (s0 is not None, s1 is not None)
     ctx.E = _mod(handle).embed_dim
     _setup_params(ctx, params)
 
 
-def _lstm_enc_backward(ctx, g_out, g_ticket):
-    (ticket,) = ctx.saved_tensors
-    d, gflat = torch.ops.ensvs.lstm_encoder_bwd(ctx.handle, ticket, g_out, ctx.nflat)
+def _lstm_enc_backward(ctx, g_out):
+    (out,) = ctx.saved_tensors
+    d, gflat = torch.ops.ensvs.lstm_encoder_bwd(ctx.handle, out, g_out, ctx.nflat)
     E = ctx.E
     d0 = d[:, :, :E] if ctx.spk[0] and ctx.needs_input_grad[3] else None
     d1 = d[:, :, E:] if ctx.spk[1] and ctx.needs_input_grad[4] else None
@@ -711,9 +711,9 @@ lstm_encoder.register_autograd(_lstm_enc_backward, setup_context=_lstm_enc_setup
 
 def lstm_encoder_call(mod, x_main, x_sub, spk_main, spk_sub, lengths):
     B, T, _ = x_main.shape
-    out, _ = torch.ops.ensvs.lstm_encoder(handle_of(mod), x_main, x_sub, spk_main, spk_sub,
-                                          _lengths_arg(lengths, B, T, x_main.device),
-                                          list(mod.parameters()))
+    out = torch.ops.ensvs.lstm_encoder(handle_of(mod), x_main, x_sub, spk_main, spk_sub,
+                                       _lengths_arg(lengths, B, T, x_main.device),
+                                       list(mod.parameters()))
     Tm = T if lengths is None else int(max(lengths_pair(lengths, B, T, x_main.device)[0]))
     return out[:, :Tm] if Tm < T else out
 
@@ -721,7 +721,7 @@ def lstm_encoder_call(mod, x_main, x_sub, spk_main, spk_sub, lengths):
 # ============================================================ Transformer encoder (tier 2)
 @torch.library.custom_op("ensvs::transformer_encoder", mutates_args=())
 def transformer_encoder(handle: int, x: Tensor, lengths: Optional[Tensor], seed: Tensor,
-                        params: List[Tensor]) -> Tuple[Tensor, Tensor]:
+                        params: List[Tensor]) -> Tensor:
     """nnsvs/model.py:1540-1671 (transformer/encoder.py:82-142): (B, T / r, out * r)."""
     mod = _mod(handle)
     B, T, D = x.shape
@@ -730,7 +730,7 @@ def transformer_encoder(handle: int, x: Tensor, lengths: Optional[Tensor], seed:
     lens_host, _ = lengths_pair(lengths, B, T, x.device)
     with engine.seed_scope(int(seed)):
         out, st = mod._fwd(x.contiguous().float().view(B * T, D), B, T, lens_host)
-    return out.view(B, -1, mod.out_dim), _save(st)
+    return _keep(st, out.view(B, -1, mod.out_dim))
 
 
 def _tf_frames(mod, T):
@@ -742,15 +742,15 @@ def _tf_frames(mod, T):
 def _(handle, x, lengths, seed, params):
     mod = _mod(handle)
     B, T, _ = x.shape
-    return x.new_empty(B, _tf_frames(mod, T), mod.out_dim, dtype=torch.float32), _ticket_fake()
+    return x.new_empty(B, _tf_frames(mod, T), mod.out_dim, dtype=torch.float32)
 
 
 @torch.library.custom_op("ensvs::transformer_encoder_bwd", mutates_args=())
-def transformer_encoder_bwd(handle: int, ticket: Tensor, grad: Tensor, T: int, need_dx: bool,
+def transformer_encoder_bwd(handle: int, out: Tensor, grad: Tensor, T: int, need_dx: bool,
                             nflat: int) -> Tuple[Tensor, Tensor]:
     """(d input (B, T, in_dim) -- zeros when not needed --, flat parameter gradients)."""
     mod = _mod(handle)
-    st = _take(ticket)
+    st = _take(out)
     g = grad.contiguous().float().view(st["B"] * st["Tp"], -1)
     with GradCapture(list(mod.parameters())) as gc:
         dx = mod._bwd(st, g, need_dx=need_dx)
@@ -760,21 +760,21 @@ def transformer_encoder_bwd(handle: int, ticket: Tensor, grad: Tensor, T: int, n
 
 
 @transformer_encoder_bwd.register_fake
-def _(handle, ticket, grad, T, need_dx, nflat):
+def _(handle, out, grad, T, need_dx, nflat):
     return grad.new_empty(grad.shape[0], T, _mod(handle).in_dim), grad.new_empty(nflat)
 
 
 def _tf_setup(ctx, inputs, output):
     handle, x, lengths, seed, params = inputs
     ctx.handle, ctx.T = handle, x.shape[1]
-    ctx.save_for_backward(output[1])
+    ctx.save_for_backward(output)
     _setup_params(ctx, params)
 
 
-def _tf_backward(ctx, g_out, g_ticket):
-    (ticket,) = ctx.saved_tensors
+def _tf_backward(ctx, g_out):
+    (out,) = ctx.saved_tensors
     need = bool(ctx.needs_input_grad[1])
-    dx, gflat = torch.ops.ensvs.transformer_encoder_bwd(ctx.handle, ticket, g_out, ctx.T, need,
+    dx, gflat = torch.ops.ensvs.transformer_encoder_bwd(ctx.handle, out, g_out, ctx.T, need,
                                                         ctx.nflat)
     return None, dx if need else None, None, None, _param_grads(ctx, gflat)
 
@@ -784,10 +784,9 @@ transformer_encoder.register_autograd(_tf_backward, setup_context=_tf_setup)
 
 def transformer_call(mod, x, lengths):
     B, T, _ = x.shape
-    out, _ = torch.ops.ensvs.transformer_encoder(handle_of(mod), x,
-                                                 _lengths_arg(lengths, B, T, x.device),
-                                                 _new_seed(), list(mod.parameters()))
-    return out
+    return torch.ops.ensvs.transformer_encoder(handle_of(mod), x,
+                                               _lengths_arg(lengths, B, T, x.device),
+                                               _new_seed(), list(mod.parameters()))
 
 
 # ======================================================== speaker embedding (row gather)

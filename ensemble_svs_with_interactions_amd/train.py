@@ -730,7 +730,10 @@ def train_epoch(model, optimizer, feeder, logf0_diff_weight=0.0, ddp=True, graph
     then on; without, every step is issued eagerly (train_step).  Returns the per-step
     (loss, grad_norm) device tensors (copies); the host reads them only when it asks."""
     out = []
-    for b in feeder:
+    n = len(feeder) if hasattr(feeder, "__len__") else None
+    for i, b in enumerate(feeder):
+        if i + 1 == n and hasattr(feeder, "prestart"):
+            feeder.prestart()  # the next pass's first batches load while this step runs
         lengths = [int(v) for v in b["host_lengths"]]
         y_sub = b["y_sub"] if logf0_diff_weight > 0 else None
         args = (b["x_main"], b["x_sub"], b["y_main"], b["spk_main"], b["spk_sub"], lengths)

@@ -24,7 +24,7 @@ BWD_TESTS = ("test_schema", "test_faketensor")
 def _fp32():
     engine.set_gemm_precision("fp32")
     yield
-    torch_ops.KEEP_TICKETS = False
+    torch_ops.KEEP_STATE = False
 
 
 def _tiny():
@@ -55,18 +55,19 @@ def _params(mod):
 
 
 def _check_pair(fwd, fwd_args, bwd_name):
-    """opcheck the forward op, then its backward op on the ticket of one more forward."""
+    """opcheck the forward op; returns the outputs of one more forward (whose saved state the
+    backward op's check then uses)."""
     torch.library.opcheck(fwd, fwd_args, test_utils=FWD_TESTS)
     outs = fwd(*fwd_args)
     return outs
 
 
 def _check_bwd(bwd, args):
-    torch_ops.KEEP_TICKETS = True
+    torch_ops.KEEP_STATE = True
     try:
         torch.library.opcheck(bwd, args, test_utils=BWD_TESTS)
     finally:
-        torch_ops.KEEP_TICKETS = False
+        torch_ops.KEEP_STATE = False
 
 
 def test_opcheck_diffnet():
@@ -80,10 +81,10 @@ def test_opcheck_diffnet():
     cond = torch.randn(B, E, T, device="cuda", generator=r).requires_grad_()
     t = torch.tensor([3, 71], device="cuda")
     h = torch_ops.handle_of(net)
-    out, ticket = _check_pair(torch.ops.ensvs.diffnet.default, (h, spec, t, cond, _params(net)),
-                              "diffnet_bwd")
+    out = _check_pair(torch.ops.ensvs.diffnet.default, (h, spec, t, cond, _params(net)),
+                      "diffnet_bwd")
     _check_bwd(torch.ops.ensvs.diffnet_bwd.default,
-               (h, ticket, torch.randn_like(out), E, torch_ops._flat_size(_params(net))))
+               (h, out.detach(), torch.randn_like(out), E, torch_ops._flat_size(_params(net))))
 
 
 @pytest.mark.parametrize("which", ["mgc", "vuv"])
@@ -99,10 +100,10 @@ def test_opcheck_ffconvlstm(which):
         spk = _spk(B, T, enc.embed_dim)
     lens = torch.tensor(a["lengths"].tolist())
     h = torch_ops.handle_of(enc)
-    out, ticket = _check_pair(torch.ops.ensvs.ffconvlstm.default,
-                              (h, x, spk, lens, torch.tensor(12345), _params(enc)), "ffconvlstm_bwd")
+    out = _check_pair(torch.ops.ensvs.ffconvlstm.default,
+                      (h, x, spk, lens, torch.tensor(12345), _params(enc)), "ffconvlstm_bwd")
     _check_bwd(torch.ops.ensvs.ffconvlstm_bwd.default,
-               (h, ticket, torch.randn_like(out), torch_ops._flat_size(_params(enc))))
+               (h, out.detach(), torch.randn_like(out), torch_ops._flat_size(_params(enc))))
 
 
 def test_opcheck_diffusion():
@@ -114,10 +115,10 @@ def test_opcheck_diffusion():
     spk = _spk(B, T, gd.encoder.embed_dim)
     lens = torch.tensor(a["lengths"].tolist())
     h = torch_ops.handle_of(gd)
-    noise, xr, ticket = _check_pair(torch.ops.ensvs.diffusion_train.default,
-                                    (h, cond, y, spk, lens, torch.tensor(777), _params(gd)), "")
+    noise, xr = _check_pair(torch.ops.ensvs.diffusion_train.default,
+                            (h, cond, y, spk, lens, torch.tensor(777), _params(gd)), "")
     _check_bwd(torch.ops.ensvs.diffusion_train_bwd.default,
-               (h, ticket, torch.randn_like(xr), torch_ops._flat_size(_params(gd))))
+               (h, xr.detach(), torch.randn_like(xr), torch_ops._flat_size(_params(gd))))
 
 
 def test_opcheck_lf0():
@@ -129,11 +130,11 @@ def test_opcheck_lf0():
     s0, s1 = _spk(B, T, E), _spk(B, T, E)
     lens = torch.tensor(a["lengths"].tolist())
     h = torch_ops.handle_of(lm)
-    lf0, res, ticket = _check_pair(torch.ops.ensvs.lf0_train.default,
+    lf0, res = _check_pair(torch.ops.ensvs.lf0_train.default,
                                    (h, g("x_main"), g("x_sub"), s0, s1, lens, None, torch.tensor(99),
                                     _params(lm)), "")
     _check_bwd(torch.ops.ensvs.lf0_train_bwd.default,
-               (h, ticket, torch.randn_like(lf0), torch.randn_like(res),
+               (h, lf0.detach(), torch.randn_like(lf0), torch.randn_like(res),
                 torch_ops._flat_size(_params(lm))))
 
 
@@ -143,12 +144,12 @@ def test_opcheck_multitrack():
     model._replay_draws = _draws(a, B, T)
     lens = torch.from_numpy(a["lengths"]).cuda()
     h = torch_ops.handle_of(model)
-    outs, ticket = _check_pair(torch.ops.ensvs.multitrack_train.default,
+    outs = _check_pair(torch.ops.ensvs.multitrack_train.default,
                                (h, g("x_main"), g("x_sub"), g("y_main"), g("spk_main"),
                                 g("spk_sub"), lens, torch.tensor(5), _params(model)), "")
     grads = [None if i in (0, 4) else torch.randn_like(o) for i, o in enumerate(outs)]
     _check_bwd(torch.ops.ensvs.multitrack_train_bwd.default,
-               (h, ticket, grads, torch_ops._flat_size(_params(model))))
+               (h, outs[1].detach(), grads, torch_ops._flat_size(_params(model))))
 
 
 def test_opcheck_separate_f0_and_lstm_encoder():
@@ -163,21 +164,21 @@ def test_opcheck_separate_f0_and_lstm_encoder():
                                lf0_sub=g("draw0::lf0_sub").view(-1))
     lens = torch.from_numpy(a["lengths"]).cuda()
     h = torch_ops.handle_of(model)
-    om, rm, os_, rs, ticket = _check_pair(
+    om, rm, os_, rs = _check_pair(
         torch.ops.ensvs.separate_f0_train.default,
         (h, g("x_main"), g("x_sub"), g("y_main"), g("y_sub"), g("spk_main"), g("spk_sub"), lens,
          torch.tensor(5), _params(model)), "")
     _check_bwd(torch.ops.ensvs.separate_f0_train_bwd.default,
-               (h, ticket, torch.randn_like(om), torch.randn_like(rm), None, torch.randn_like(rs),
+               (h, om.detach(), torch.randn_like(om), torch.randn_like(rm), None, torch.randn_like(rs),
                 torch_ops._flat_size(_params(model))))
     enc = model.encoder
     E = enc.embed_dim
     s0, s1 = _spk(B, T, E), _spk(B, T, E)
     he = torch_ops.handle_of(enc)
-    out, t2 = _check_pair(torch.ops.ensvs.lstm_encoder.default,
+    out = _check_pair(torch.ops.ensvs.lstm_encoder.default,
                           (he, g("x_main"), g("x_sub"), s0, s1, lens.cpu(), _params(enc)), "")
     _check_bwd(torch.ops.ensvs.lstm_encoder_bwd.default,
-               (he, t2, torch.randn_like(out), torch_ops._flat_size(_params(enc))))
+               (he, out.detach(), torch.randn_like(out), torch_ops._flat_size(_params(enc))))
 
 
 def test_opcheck_transformer_embedding_loss():
@@ -192,10 +193,10 @@ def test_opcheck_transformer_embedding_loss():
     x = torch.randn(B, T, mod.in_dim, device="cuda").requires_grad_()
     lens = torch.tensor([40, 31])
     h = torch_ops.handle_of(mod)
-    out, ticket = _check_pair(torch.ops.ensvs.transformer_encoder.default,
-                              (h, x, lens, torch.tensor(4), _params(mod)), "")
+    out = _check_pair(torch.ops.ensvs.transformer_encoder.default,
+                      (h, x, lens, torch.tensor(4), _params(mod)), "")
     _check_bwd(torch.ops.ensvs.transformer_encoder_bwd.default,
-               (h, ticket, torch.randn_like(out), T, True, torch_ops._flat_size(_params(mod))))
+               (h, out.detach(), torch.randn_like(out), T, True, torch_ops._flat_size(_params(mod))))
     table = torch.randn(4, 16, device="cuda").requires_grad_()
     idx = torch.tensor([[1], [3], [1]], device="cuda", dtype=torch.int32)
     torch.library.opcheck(torch.ops.ensvs.embedding_gather.default, (table, idx),

@@ -58,7 +58,8 @@ def case(name, M, N, spec, epi=L.EPI_PLAIN, bias=True, accum=False):
     res = dict(case=name, M=M, N=N, K=Kt)
     flops = 2.0 * M * N * Kt
     ref = None
-    for tag, p8, blas in (("eng128", 0, False), ("p8", 2, False), ("blas", 0, True)):
+    for tag, p8, blas in (("eng128", 0, False), ("p8b2", 6, False), ("p8", 2, False),
+                          ("blas", 0, True)):
         if blas and epi != L.EPI_PLAIN:
             continue
         K.BLAS["on"] = blas
@@ -89,6 +90,28 @@ def _lib_call(name, *args):
     L.call(name, *args)
 
 
+def none_case(name, M, N, spec):
+    """The K loop alone (EPI_NONE: no output) on the 128 x 128 and four-phase kernels."""
+    pb = K.PackedBuffer(L.DT_BF16)
+    segs = []
+    for (Kc, taps, dil) in spec:
+        ref = pb.add(torch.randn(N, Kc, taps, device=dev) * 0.03, N, Kc, taps, Kc * taps, taps, 1)
+        segs.append(K.Seg(torch.randn(M, Kc, device=dev).to(torch.bfloat16), Kc, Kc, ref, T,
+                          taps=taps, dil=dil, shift0=-(taps // 2) * dil))
+    pb.finalize(dev)
+    pb.repack()
+    Y = torch.empty(M, N, device=dev)
+    res = dict(case=name + " (K loop only)", M=M, N=N, K=sum(k * t for k, t, _ in spec))
+    K.BLAS["on"] = False
+    for tag, p8 in (("eng128", 0), ("p8", 2)):
+        _lib_call("ensvs_set_p8", p8)
+        res[f"{tag}_us"] = round(timeit(lambda: K.gemm(segs, M // T, T, N, pb, Y, N,
+                                                       epi=L.EPI_NONE)), 1)
+    K.BLAS["on"] = True
+    _lib_call("ensvs_set_p8", 1)
+    print(json.dumps(res), flush=True)
+
+
 if __name__ == "__main__":
     L.load()
     M = 30 * 1024
@@ -101,3 +124,5 @@ if __name__ == "__main__":
     case("mgc lstm proj 512->1024", M, 1024, [(512, 1, 1)])
     case("mgc enc conv k7 512->512", M, 512, [(512, 7, 1)])
     case("diffnet res 256->512", M, 512, [(256, 1, 1)])
+    none_case("enc l0 proj 512->4096", M, 4096, [(512, 1, 1)])
+    none_case("enc dgrad 2x2048->1024", M, 1024, [(2048, 1, 1), (2048, 1, 1)])

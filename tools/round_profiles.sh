@@ -23,7 +23,7 @@ timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $o/${tag}_g
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $o/${tag}_gpmc_write -o pmc \
   -- python3 tools/gate_gemm_pmc.py > $o/${tag}_gpmc_write.log 2>&1 || exit 6
 python3 tools/pmc_summary.py $o/${tag}_gpmc_fetch/pmc_counter_collection.csv \
-  $o/${tag}_gpmc_write/pmc_counter_collection.csv $o/${tag}_gate_pmc.json conv_gemm_b16_big_kernel \
+  $o/${tag}_gpmc_write/pmc_counter_collection.csv $o/${tag}_gate_pmc.json conv_gemm_b16_p8_kernel \
   > /dev/null || exit 7
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $o/${tag}_prof_gate -o gate \
   -- python3 tools/gate_gemm_pmc.py > $o/${tag}_prof_gate.log 2>&1 || exit 8

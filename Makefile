@@ -15,7 +15,7 @@ build/%.o: $(PKG)/csrc/%.hip $(wildcard $(PKG)/csrc/*.h) include/ensvs.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(PKG)/libensvs.so: $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L/opt/rocm/lib -lhipblaslt
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
 clean:
 	rm -rf build $(PKG)/libensvs.so

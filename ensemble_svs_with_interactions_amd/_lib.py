@@ -16,12 +16,6 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # (tools/ab_lib.sh); the default is the package's own libensvs.so
 LIB_PATH = os.environ.get("ENSVS_LIB") or os.path.join(_HERE, "libensvs.so")
 
-# hipBLASLt (csrc/blas.hip) launches its stream-K kernels on data-parallel grids: one workgroup
-# per tile, none waiting on another (beside the cooperative recurrences a waiting workgroup's
-# producer may never become resident).  Tensile reads this once, at the first hipBLASLt call
-# of the process; the library also sets it when it is loaded.
-os.environ.setdefault("TENSILE_STREAMK_DATA_PARALLEL", "1")
-
 c_int = ctypes.c_int
 c_ll = ctypes.c_longlong
 c_float = ctypes.c_float
@@ -158,9 +152,6 @@ SIGNATURES = {
     "ensvs_bn_finalize": [c_vp, c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_vp, c_float, c_int,
                           c_vp],
     "ensvs_bn_stats_part_floats": [c_ll, c_int, c_ll],
-    "ensvs_blas_gemm": [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int,
-                        c_vp, c_ll, c_vp],
-    "ensvs_blas_supported": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_ll],
     "ensvs_bn_stats": [c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_ll, c_float, c_vp, c_vp, c_vp, c_vp,
                        c_vp, c_float, c_int, c_vp, c_vp],
     "ensvs_bn_apply_relu": [c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,

@@ -2269,8 +2269,14 @@ __device__ __forceinline__ void p8_wait() {
 // BAR2: the template's second barrier after each phase's MFMAs (ONE barrier per phase is also
 // valid: every region is rewritten >= 2 phases after its last read, so the writer has passed the
 // barrier that the reader reaches only after its lgkmcnt wait of that read)
-template <bool GATE8, bool BAR2>
+// EPK: EPI_GATE -- the 16-B gate epilogue (DiffNet gate GEMM); EPI_PLAIN -- the lean plain
+// epilogue (fp32 Y = acc + bias, no accumulate / activation / copies, N % 4 == 0: the
+// projections), the whole tile staged in two 128-row passes by all 8 waves; -1 -- every other
+// epilogue (epilogue_tile, 64-row chunks).  Instances per epilogue keep the other epilogues'
+// operand registers out of the K loop (the generic instance spills in its epilogue).
+template <int EPK, bool BAR2>
 __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs a) {
+  constexpr bool GATE8 = EPK == EPI_GATE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
@@ -2442,9 +2448,43 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
   float bs[4];
   const bool bias_st = a.bias != nullptr;
   if (bias_st) big_bias(a, n0, wc, lane, bs);
+  float* T = (float*)smem;
+  if constexpr (EPK == EPI_PLAIN) {
+    // T rows [64 wr, 64 wr + 64) hold tile rows 128 wr + 64 pass + (0..63) of every wave's
+    // half `pass`; a thread stores 4 consecutive columns of 16 rows (one 1-KB row per wave
+    // instruction)
+    lds_sync();
+    const int cq = tid & 63, r0 = tid >> 6;
+    const int col = n0 + cq * 4;
+    const bool colok = col < a.N;
+#define STAGE_P(H)                                                                        \
+    _Pragma("unroll") for (int mt2 = 0; mt2 < 4; ++mt2)                                   \
+    _Pragma("unroll") for (int nt = 0; nt < 4; ++nt)                                      \
+    _Pragma("unroll") for (int r = 0; r < 4; ++r)                                         \
+        T[(wr * 64 + mt2 * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] = \
+            bias_st ? acc[(H) * 4 + mt2][nt][r] + bs[nt] : acc[(H) * 4 + mt2][nt][r]
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass) {
+        STAGE_P(1);
+      } else {
+        STAGE_P(0);
+      }
+#undef STAGE_P
+      lds_sync();
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int tr = r0 + 8 * i;  // T row
+        const int m = m0 + (tr < 64 ? 0 : 64) + pass * 64 + tr;
+        const f32x4 v = ld4(T + tr * EPB + cq * 4);
+        if (colok && m < a.M) st4(a.Y + (long long)m * a.ldy + col, v);
+      }
+      lds_sync();
+    }
+    return;
+  }
   EpiPre pre;
   if (!GATE8) epi_pre<BNB, NTHRB>(a, m0, n0, tid, 0, pre);
-  float* T = (float*)smem;
   lds_sync();
 #define STAGE_HALF(H)                                                                     \
   _Pragma("unroll") for (int mt2 = 0; mt2 < 4; ++mt2)                                     \
@@ -4037,9 +4077,14 @@ static const int SMALL_STAGES = 5;
 static const int BIG_MIN_TILES = 192;
 
 // The four-phase 256 x 256 kernel (conv_gemm_b16_p8_kernel): 0 off, 1 in place of the
-// two-stage 256 x 256 kernel (the gate GEMMs), 2 also for every other launch the 256 x 256
-// epilogue serves with at least P8_MIN_TILES tiles (plain / ReLU-mask / ADDSCALE products).
-static int g_p8 = 1;
+// two-stage 256 x 256 kernel (the gate GEMMs), 2 (default) also for every other launch the
+// 256 x 256 epilogue serves with at least P8_MIN_TILES tiles -- the recurrences' input
+// projections and input gradients, the 1 x 1 and conv-stack GEMMs: with the lean plain epilogue
+// at or below hipBLASLt on those shapes (tools/p8_bench.py, profiles/r6_p8_bench.txt), main line
+// 13.47 / 13.47 ms vs 13.44 / 13.38 with hipBLASLt for the plain GEMMs and 13.61 / 13.63 with
+// them on the 128 x 128 kernel; SeparateF0 43.0 / 42.5 vs 42.9 / 42.9 and 43.9 / 43.9
+// (profiles/r6_blas_ab.txt, r6_blas_ab_sf0.txt).
+static int g_p8 = 2;
 static int g_p8_bar2 = 0;  // 1: two barriers per phase (the template's form); 0: one (faster:
                            // tools/p8_bench.py, profiles/r6_p8_bench.txt)
 static const int P8_MIN_TILES = 128;
@@ -4086,20 +4131,27 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     const dim3 grid_b(cdiv(a.M, BMB), Npad / BNB);
     const bool gate = a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS);
     const size_t lb = (size_t)2 * P8_BUF;  // two K-steps of both images (128 KB)
-#define P8(G, B2)                                                                         \
+    // the lean plain epilogue: fp32 Y = acc (+ bias), nothing else, 16-B aligned rows
+    const bool plain = a.epi == EPI_PLAIN && !a.accum && !a.relu && !a.ybf && a.Y &&
+                       a.N % 4 == 0 && a.ldy % 4 == 0 && ((uintptr_t)a.Y & 15) == 0 &&
+                       (!a.bias || ((uintptr_t)a.bias & 3) == 0);
+    const size_t lbp = std::max<size_t>(lb, (size_t)128 * EPB * 4);  // two 128-row passes
+#define P8(E, B2, L)                                                                      \
   do {                                                                                    \
     static const hipError_t ep = hipFuncSetAttribute(                                     \
-        (const void*)conv_gemm_b16_p8_kernel<G, B2>,                                      \
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);                             \
+        (const void*)conv_gemm_b16_p8_kernel<E, B2>,                                      \
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)(L));                            \
     if (ep != hipSuccess) return ENSVS_E_HIP;                                             \
-    hipLaunchKernelGGL((conv_gemm_b16_p8_kernel<G, B2>), grid_b, dim3(NTHRB), lb, st, a); \
+    hipLaunchKernelGGL((conv_gemm_b16_p8_kernel<E, B2>), grid_b, dim3(NTHRB), (L), st, a); \
   } while (0)
     if (g_p8_bar2) {
-      if (gate) P8(true, true);
-      else P8(false, true);
+      if (gate) P8(EPI_GATE, true, lb);
+      else if (plain) P8(EPI_PLAIN, true, lbp);
+      else P8(-1, true, lb);
     } else {
-      if (gate) P8(true, false);
-      else P8(false, false);
+      if (gate) P8(EPI_GATE, false, lb);
+      else if (plain) P8(EPI_PLAIN, false, lbp);
+      else P8(-1, false, lb);
     }
 #undef P8
     ENSVS_CHECK_LAUNCH();

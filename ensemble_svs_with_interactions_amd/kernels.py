@@ -273,40 +273,6 @@ def gemm(segs: List[Seg], B: int, Tout: int, N: int, W: PackedBuffer, Y, ldy: in
     outputs.  keep_y=False (GATE with ybf, GATE_BWD with ybf / csum): the fp32 Y is not
     needed by the caller and the fused epilogue skips it (Y stays allocated for the
     fallback paths, which still write it)."""
-    if (BLAS["generic"] and epi == _lib.EPI_PLAIN and not relu and aux0 is None and aux1 is None
-            and ybf is None and csum is None and (BLAS["multi"] or (len(segs) == 1 and not accum
-                                                                    and yoff == 0))):
-        # plain (1-tap, unshifted) products with bf16 operands -- or fp32 ones rounded by a cast
-        # pass first (BLAS cast) -- on hipBLASLt when it has a plan for every segment: one call
-        # per segment, the first with the bias, the others accumulating
-        M = B * Tout
-        plan = []
-        for s in segs:
-            if not (s.taps == 1 and s.shift0 == 0 and s.pd is None and s.Tin == Tout
-                    and s.ref.taps == 1 and BLAS["on"] and W.dtype == _lib.DT_BF16
-                    and M >= BLAS["min_rows"] and s.K % 8 == 0):
-                break
-            if s.x.dtype == torch.bfloat16 and s.radd is None and s.ld % 8 == 0:
-                plan.append((s, False, s.ld))
-            elif BLAS["cast"] and s.x.dtype == torch.float32 and _castable(s):
-                plan.append((s, True, s.K))
-            else:
-                break
-        if (len(plan) == len(segs)
-                and N * sum(s.K for s in segs) * M >= BLAS["min_macs"]
-                and all(blas_supported(M, N, s.K, ld, s.ref.Kp, ldy, bias is not None and i == 0)
-                        for i, (s, _, ld) in enumerate(plan))):
-            for i, (s, cast, ld) in enumerate(plan):
-                x, xoff = s.x, s.xoff
-                if cast:
-                    x = cast_bf16(s.x, s.ld, s.K, M, xoff=s.xoff, radd=s.radd,
-                                  radd_ld=s.radd_ld, T=s.Tin)
-                    xoff = 0
-                if not blas_gemm(x, ld, s.ref, W, M, N, s.K, Y, ldy,
-                                 bias=bias if i == 0 else None, bias_off=bias_off,
-                                 accum=accum or i > 0, xoff=xoff, yoff=yoff):
-                    raise RuntimeError("hipBLASLt plan vanished between the check and the call")
-            return
     arr = (ConvSeg * len(segs))()
     Npad = segs[0].ref.Npad
     # C-ABI epilogue flags: a bf16 gate/filter save (DiffNet production path)
@@ -439,65 +405,6 @@ def usf_block(segs: List[Seg], B, Tout, W: PackedBuffer, C, ref2, x, ldx, alpha,
          None if bias is None else bias.data_ptr() + 4 * bias_off, C, ref2.offset, ref2.Kp,
          None if bias2 is None else bias2.data_ptr() + 4 * bias2_off, x.data_ptr(), ldx,
          float(alpha), int(bool(relu)), ptr(xb), 0 if xb is None else xb.shape[1], stream())
-
-
-# plain bf16 GEMMs on hipBLASLt (ensvs_blas_gemm, data-parallel grids): the recurrences' input
-# projections and input gradients (layers.lstm_fwd / lstm_bwd); off: the implicit-GEMM engine
-# (A/B switch)
-BLAS = {"on": True, "min_rows": 4096, "ws_bytes": 32 << 20,
-        # gemm(): any single plain bf16 segment (1 tap, no shift, PLAIN epilogue with at most a
-        # bias, fp32 Y) of at least min_macs multiply-adds also goes to hipBLASLt (2^24: the
-        # main line's 1x1 input / output layers too, 13.64-13.73 -> 13.49-13.60 ms against no
-        # generic routing; 2^34 left them on the engine, -0.04 ms,
-        # profiles/r5_blas_generic_threshold_ab.txt)
-        "generic": True, "min_macs": 1 << 24,
-        # ... also with several such segments (K-concatenated inputs), accumulating outputs
-        # and a column offset into Y (A/B switch; off: main line -0.02 ms, SeparateF0 +0.1 /
-        # +0.2 ms, profiles/r5_blas_multi_ab.txt)
-        "multi": False,
-        # ... also fp32 operands, rounded to bf16 by one cast pass first (the rounding the
-        # register-staged engine kernel applies in staging): main line -0.04 ms, SeparateF0
-        # -0.05 ms (profiles/r5_blas_cast_ab.txt)
-        "cast": True}
-
-
-def blas_ok(x, ld, K, M, W):
-    """Whether a plain GEMM over bf16 rows x (ld, K) and packed weights W runs on hipBLASLt."""
-    return (BLAS["on"] and x.dtype == torch.bfloat16 and W.dtype == _lib.DT_BF16 and
-            M >= BLAS["min_rows"] and K % 8 == 0 and ld % 8 == 0)
-
-
-_blas_shapes = {}
-
-
-def blas_supported(M, N, K, ldx, ldw, ldy, bias):
-    """Whether hipBLASLt has a data-parallel plan for ensvs_blas_gemm's shape
-    (ensvs_blas_supported; cached per process and device)."""
-    key = (torch.cuda.current_device(), M, N, K, ldx, ldw, ldy, bool(bias))
-    ok = _blas_shapes.get(key)
-    if ok is None:
-        rc = _lib.query("ensvs_blas_supported", M, N, K, ldx, ldw, ldy, int(bool(bias)),
-                        BLAS["ws_bytes"])
-        if rc < 0:
-            raise RuntimeError(f"ensvs_blas_supported failed: {rc}")
-        ok = _blas_shapes[key] = rc == 1
-    return ok
-
-
-def blas_gemm(x, ldx, ref, W, M, N, K, Y, ldy, bias=None, bias_off=0, accum=False, xoff=0,
-              yoff=0):
-    """Y[M][N] (+)= x[M][K] (bf16 rows of ldx, from element xoff) W_ref^T (+ bias) on hipBLASLt
-    (ensvs_blas_gemm; Y from element yoff): W_ref is a packed [Npad][Kp] bf16 operand of W.
-    Returns False (nothing issued) when hipBLASLt has no data-parallel algorithm for the
-    shape."""
-    assert x.dtype == torch.bfloat16 and W.dtype == _lib.DT_BF16 and ref.Kp >= K and ref.taps == 1
-    if not blas_supported(M, N, K, ldx, ref.Kp, ldy, bias is not None):
-        return False
-    ws = scratch(BLAS["ws_bytes"] // 4, x.device, key="blas")
-    call("ensvs_blas_gemm", x.data_ptr() + 2 * xoff, ldx, W.buf.data_ptr() + 2 * ref.offset,
-         ref.Kp, M, N, K, None if bias is None else bias.data_ptr() + 4 * bias_off,
-         Y.data_ptr() + 4 * yoff, ldy, int(accum), ws.data_ptr(), BLAS["ws_bytes"], stream())
-    return True
 
 
 def bf16_operands(W, M):

@@ -594,11 +594,8 @@ def lstm_fwd(pk, lstm, X, ldx, B, T, lens_dev, device, dropout_masks=None, save=
         gx = empty(M, 8 * H, device=device)
         if lstm_fused_proj(H):
             assert pk[f"b{l}_reverse"].offset == pk[f"b{l}"].offset + 4 * H
-            if not (K.blas_ok(xa, lda, Kc, M, pk.fwd) and
-                    K.blas_gemm(xa, lda, pk[f"ih{l}"], pk.fwd, M, 8 * H, Kc, gx, 8 * H,
-                                **pk.bias_ptr_args(f"b{l}"))):
-                K.gemm([K.Seg(xa, lda, Kc, pk[f"ih{l}"], T)], B, T, 8 * H, pk.fwd, gx, 8 * H,
-                       **pk.bias_ptr_args(f"b{l}"))
+            K.gemm([K.Seg(xa, lda, Kc, pk[f"ih{l}"], T)], B, T, 8 * H, pk.fwd, gx, 8 * H,
+                   **pk.bias_ptr_args(f"b{l}"))
         else:
             for d, sfx in enumerate(("", "_reverse")):
                 K.gemm([K.Seg(xa, lda, Kc, pk[f"ih{l}{sfx}"], T)], B, T, 4 * H, pk.fwd, gx,
@@ -735,15 +732,9 @@ def lstm_bwd(pk, lstm, sv, dY, B, T, lens_dev, device, need_dx=True, later=None)
             break
         nd = empty(M, Kc, device=device)
         gd = dgb if dgb is not None else dg
-        r0, r1 = pk[f"ih{l}^T"], pk[f"ih{l}_reverse^T"]
-        if (K.blas_ok(gd, 8 * H, 4 * H, M, pk.bwd) and r0.Kp == r1.Kp and
-                K.blas_supported(M, Kc, 4 * H, 8 * H, r0.Kp, Kc, False)):
-            K.blas_gemm(gd, 8 * H, r0, pk.bwd, M, Kc, 4 * H, nd, Kc)
-            K.blas_gemm(gd, 8 * H, r1, pk.bwd, M, Kc, 4 * H, nd, Kc, accum=True, xoff=4 * H)
-        else:
-            K.gemm([K.Seg(gd, 8 * H, 4 * H, pk[f"ih{l}^T"], T),
-                    K.Seg(gd, 8 * H, 4 * H, pk[f"ih{l}_reverse^T"], T, xoff=4 * H)],
-                   B, T, Kc, pk.bwd, nd, Kc)
+        K.gemm([K.Seg(gd, 8 * H, 4 * H, pk[f"ih{l}^T"], T),
+                K.Seg(gd, 8 * H, 4 * H, pk[f"ih{l}_reverse^T"], T, xoff=4 * H)],
+               B, T, Kc, pk.bwd, nd, Kc)
         if l > 0:
             prev_mask = sv[l - 1].get("mask")
             if prev_mask is not None:

@@ -75,12 +75,9 @@ def _keep(state, out):
     return out
 
 
-KEEP_STATE = False  # tests: a backward op may run twice on one forward's state (opcheck)
-
-
 def _take(key_out):
     k = _key(key_out)
-    st = _SAVED.get(k) if KEEP_STATE else _SAVED.pop(k, None)
+    st = _SAVED.pop(k, None)
     if st is None:
         raise RuntimeError("ensvs op: the forward state of this backward is gone (backward "
                            "called twice, or more than MAX_SAVED forwards in flight)")
@@ -109,6 +106,21 @@ def _new_seed():
     return torch.randint(0, 1 << 62, (), dtype=torch.int64)
 
 
+def _spk_rows(spk, B, T):
+    """Per-sequence speaker vectors (B, E) contiguous, and their row stride, from a (B, T, E)
+    speaker input: the reference expands a (B, 1, E) vector over frames (multistream.py:
+    1620-1628); a materialised copy of such an expansion is accepted after checking that every
+    frame holds the first frame's vector (per-frame vectors are not on the path).  The op keeps
+    the rows with its saved state."""
+    if spk is None:
+        return None, 0
+    first = spk[:, 0, :]
+    if spk.stride(1) != 0 and not torch.equal(spk, first.unsqueeze(1).expand_as(spk)):
+        raise NotImplementedError("per-frame speaker embeddings are not on the path")
+    rows = first.contiguous().float()
+    return rows, rows.shape[1]
+
+
 def _lengths_arg(lengths, B, T, device):
     """Module-call lengths (None / list / tensor) as the op's Optional[Tensor]."""
     if lengths is None or isinstance(lengths, torch.Tensor):
@@ -116,9 +128,13 @@ def _lengths_arg(lengths, B, T, device):
     return lengths_pair(lengths, B, T, device)[1]
 
 
-def _setup_params(ctx, params):
-    ctx.param_shapes = [tuple(p.shape) for p in params]
-    ctx.nflat = _flat_size(params)
+def _setup_params(ctx, params, handle=None):
+    """Per-parameter shapes and the flat gradient size, from the module's own (concrete)
+    parameters: under symbolic tracing the `params` input carries symbolic sizes, and a sum
+    over ~200 of them as nflat overflows the tracer's recursion."""
+    src = list(_mod(handle).parameters()) if handle is not None else params
+    ctx.param_shapes = [tuple(int(d) for d in p.shape) for p in src]
+    ctx.nflat = _flat_size(src)
 
 
 def _param_grads(ctx, gflat):
@@ -170,7 +186,7 @@ def _diffnet_setup(ctx, inputs, output):
     handle, spec, t, cond, params = inputs
     ctx.handle, ctx.E = handle, cond.shape[1]
     ctx.save_for_backward(output)
-    _setup_params(ctx, params)
+    _setup_params(ctx, params, handle)
 
 
 def _diffnet_backward(ctx, g_out):
@@ -194,16 +210,14 @@ def ffconvlstm(handle: int, x: Tensor, spk_embs: Optional[Tensor], lengths: Opti
                seed: Tensor, params: List[Tensor]) -> Tensor:
     """model.py:891-918 over all T frames (the caller trims to max(lengths), as
     pad_packed_sequence does)."""
-    from .model import _spk_args
     mod = _mod(handle)
     B, T, D = x.shape
     x = x.contiguous().float()
     _, lens_dev = lengths_pair(lengths, B, T, x.device)
-    spk, spk_ld, full = _spk_args(spk_embs, B, T)
-    if full is not None:
-        raise NotImplementedError("per-frame speaker embeddings are not on the path")
+    spk, spk_ld = _spk_rows(spk_embs, B, T)
     with engine.seed_scope(int(seed)):
         out, st = mod._fwd([(x, D, 0, D)], B, T, lens_dev, spk, spk_ld, save=True)
+    st["_keep_spk"] = spk
     return _keep(st, out.view(B, T, -1))
 
 
@@ -237,7 +251,7 @@ def _ffconvlstm_setup(ctx, inputs, output):
     ctx.handle = handle
     ctx.save_for_backward(output)
     ctx.spk = spk_embs is not None
-    _setup_params(ctx, params)
+    _setup_params(ctx, params, handle)
 
 
 def _ffconvlstm_backward(ctx, g_out):
@@ -265,16 +279,16 @@ def diffusion_train(handle: int, cond: Tensor, y: Tensor, spk_embs: Optional[Ten
                     lengths: Optional[Tensor], seed: Tensor,
                     params: List[Tensor]) -> Tuple[Tensor, Tensor]:
     """diffusion.py:269-300: (noise, x_recon); t ~ U{0..K-1} and the noise from `seed`."""
-    from .model import _spk_args
     mod = _mod(handle)
     B, T, D = cond.shape
     cond = cond.contiguous().float()
     y = y.contiguous().float()
     _, lens_dev = lengths_pair(lengths, B, T, cond.device)
-    spk, spk_ld, _ = _spk_args(spk_embs, B, T)
+    spk, spk_ld = _spk_rows(spk_embs, B, T)
     with engine.seed_scope(int(seed)):
         noise, xr, st = mod._fwd([(cond, D, 0, D)], B, T, lens_dev, (y, y.shape[2], 0), spk,
                                  spk_ld)
+    st["_keep_spk"] = (spk, y)
     return noise.view(B, T, -1), _keep(st, xr.view(B, T, -1))
 
 
@@ -309,7 +323,7 @@ def _diffusion_setup(ctx, inputs, output):
     ctx.handle = handle
     ctx.save_for_backward(output[1])
     ctx.spk = spk_embs is not None
-    _setup_params(ctx, params)
+    _setup_params(ctx, params, handle)
 
 
 def _diffusion_backward(ctx, g_noise, g_recon):
@@ -340,17 +354,14 @@ def lf0_train(handle: int, x_main: Tensor, x_sub: Optional[Tensor], spk_emb_main
               seed: Tensor, params: List[Tensor]) -> Tuple[Tensor, Tensor]:
     """tacotron_f0.py:924-991 (+ the AR decoder, free-running unless y is given): (lf0,
     lf0_residual), each (B, T, 1); the prenet dropout masks from `seed`."""
-    from .model import _spk_args
     mod = _mod(handle)
     B, T, D = x_main.shape
     xs = [x_main.contiguous().float()]
     if x_sub is not None:
         xs.append(x_sub.contiguous().float())
     _, lens_dev = lengths_pair(lengths, B, T, x_main.device)
-    p0, ld0, f0 = _spk_args(spk_emb_main, B, T)
-    p1, ld1, f1 = _spk_args(spk_emb_sub, B, T)
-    if f0 is not None or f1 is not None or (spk_emb_sub is not None and ld0 != ld1):
-        raise NotImplementedError("per-frame speaker embeddings are not on the path")
+    p0, ld0 = _spk_rows(spk_emb_main, B, T)
+    p1, ld1 = _spk_rows(spk_emb_sub, B, T)
     teacher = None
     if y is not None:
         if y.shape[1] != T:
@@ -360,7 +371,7 @@ def lf0_train(handle: int, x_main: Tensor, x_sub: Optional[Tensor], spk_emb_main
         teacher = (yc, yc.shape[2], mod.decoder.out_lf0_idx)
     with engine.seed_scope(int(seed)):
         lf0, res, st = mod._fwd(xs, D, B, T, lens_dev, (p0, p1), ld0, teacher=teacher)
-    st["_keep"] = teacher  # the teacher buffer the saved state points into
+    st["_keep"] = (teacher, p0, p1)  # buffers the saved state points into
     return _keep(st, lf0.view(B, T, 1)), res.view(B, T, 1)
 
 
@@ -397,7 +408,7 @@ def _lf0_setup(ctx, inputs, output):
     ctx.handle = handle
     ctx.save_for_backward(output[0])
     ctx.spk = (s0 is not None, s1 is not None)
-    _setup_params(ctx, params)
+    _setup_params(ctx, params, handle)
 
 
 def _lf0_backward(ctx, g_lf0, g_res):
@@ -497,7 +508,7 @@ def _(handle, mgc_recon, grads, nflat):
 def _mt_setup(ctx, inputs, output):
     ctx.handle = inputs[0]
     ctx.save_for_backward(output[1])
-    _setup_params(ctx, inputs[-1])
+    _setup_params(ctx, inputs[-1], inputs[0])
 
 
 def _mt_backward(ctx, g_outs):
@@ -577,7 +588,7 @@ def _(handle, out_main, g_out_main, g_res_main, g_out_sub, g_res_sub, nflat):
 def _sf0_setup(ctx, inputs, output):
     ctx.handle = inputs[0]
     ctx.save_for_backward(output[0])
-    _setup_params(ctx, inputs[-1])
+    _setup_params(ctx, inputs[-1], inputs[0])
 
 
 def _sf0_backward(ctx, g_om, g_rm, g_os, g_rs):
@@ -631,8 +642,7 @@ def _ml1_setup(ctx, inputs, output):
 def _ml1_backward(ctx, g_loss, g_grads):
     gs = ctx.saved_tensors
     dp = [g_loss * g for g in gs]
-    dt = [-d for d in dp] if any(ctx.needs_input_grad[1]) else None
-    return dp, dt, None
+    return dp, [-d for d in dp], None  # (L1: the targets' gradient is the negation)
 
 
 masked_l1.register_autograd(_ml1_backward, setup_context=_ml1_setup)
@@ -650,16 +660,16 @@ def lstm_encoder(handle: int, x_main: Tensor, x_sub: Tensor, spk_main: Optional[
                  spk_sub: Optional[Tensor], lengths: Optional[Tensor],
                  params: List[Tensor]) -> Tensor:
     """nnsvs/model.py:1435-1537 over all T frames (the caller trims to max(lengths))."""
-    from .model import _spk_args
     mod = _mod(handle)
     B, T, D = x_main.shape
     _, lens_dev = lengths_pair(lengths, B, T, x_main.device)
-    p0, ld0, f0 = _spk_args(spk_main, B, T)
-    p1, ld1, f1 = _spk_args(spk_sub, B, T)
-    if f0 is not None or f1 is not None or ld0 != ld1:
-        raise NotImplementedError("per-frame speaker embeddings are not on the path")
+    p0, ld0 = _spk_rows(spk_main, B, T)
+    p1, ld1 = _spk_rows(spk_sub, B, T)
+    if ld0 != ld1:
+        raise NotImplementedError("the two speaker inputs must share one layout")
     out, st = mod._fwd(x_main.contiguous().float(), x_sub.contiguous().float(), D, B, T,
                        lens_dev, (p0, p1), ld0)
+    st["_keep_spk"] = (p0, p1)
     return _keep(st, out.view(B, T, -1))
 
 
@@ -694,7 +704,7 @@ def _lstm_enc_setup(ctx, inputs, output):
     ctx.save_for_backward(output)
     ctx.spk = (s0 is not None, s1 is not None)
     ctx.E = _mod(handle).embed_dim
-    _setup_params(ctx, params)
+    _setup_params(ctx, params, handle)
 
 
 def _lstm_enc_backward(ctx, g_out):
@@ -768,7 +778,7 @@ def _tf_setup(ctx, inputs, output):
     handle, x, lengths, seed, params = inputs
     ctx.handle, ctx.T = handle, x.shape[1]
     ctx.save_for_backward(output)
-    _setup_params(ctx, params)
+    _setup_params(ctx, params, handle)
 
 
 def _tf_backward(ctx, g_out):

@@ -76,7 +76,7 @@ int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N
 int ensvs_set_big_tile(int mode, int stages);
 /* The four-phase 256 x 256 kernel (counted LDS-DMA pipeline, four half-tiles in flight across
  * every barrier; same accumulation order, bitwise equal): mode 0 off; 1 for the launches the
- * 256 x 256 kernel takes (gate GEMMs); 2 also for every other launch its LDS-staged epilogue
+ * 256 x 256 kernel takes (gate GEMMs); 2 (default) also for every other launch its LDS-staged epilogue
  * serves with >= 128 tiles of 256 x 256 (no column sums, not the LDS-DMA epilogues); + 4: two
  * barriers per phase (the template's form) instead of one (A/B). */
 int ensvs_set_p8(int mode);
@@ -400,22 +400,6 @@ int ensvs_gather_rows(const float* table, const long long* idx, int B, int C, fl
  * apply+ReLU, and backward (+ReLU).  Groups of Mg rows keep separate statistics. */
 int ensvs_bn_finalize(float* mean, float* var, int G, int C, long long Mg, float eps, float* rstd,
                       float* rmean, float* rvar, float momentum, int update, void* stream);
-/* Plain bf16 GEMM on hipBLASLt: Y[M][N] (+)= X[M][K] W[N][K]^T (+ bias[N]); X bf16 rows of ldx,
- * W bf16 rows of ldw (the GEMM engine's packed [Npad][Kp] weights, ldw = Kp), Y fp32 rows of
- * ldy, fp32 accumulation; accum: beta = 1.  ws / ws_bytes: workspace (the plan's algorithm
- * must fit it).  One plan per shape, made on first use (before graph capture).  The
- * recurrences' input projections / input gradients of the SeparateF0 model
- * (nnsvs/model.py:1435-1537 nn.LSTM's x W_ih^T + b and its input gradient). */
-/* 1 when hipBLASLt has a data-parallel plan for ensvs_blas_gemm's shape (made here, reused by
- * the calls), 0 when not -- keep the implicit-GEMM engine.  Plans need
- * TENSILE_STREAMK_DATA_PARALLEL=1, which the library sets when loaded unless the process set it:
- * hipBLASLt's stream-K grids wait across workgroups, and beside the cooperative recurrences a
- * waiting workgroup's producer may never become resident. */
-int ensvs_blas_supported(int M, int N, int K, int ldx, int ldw, int ldy, int bias,
-                         long long ws_bytes);
-int ensvs_blas_gemm(const void* x, int ldx, const void* w, int ldw, int M, int N, int K,
-                    const float* bias, float* y, int ldy, int accum, void* ws, long long ws_bytes,
-                    void* stream);
 
 /* BatchNorm1d training statistics of y [M][ldy] in groups of Mg rows in two launches (the two
  * column sums + ensvs_bn_finalize they replace): mean / var (biased) [G][C], rstd = 1 /

@@ -12,6 +12,6 @@ for f in "$D"/ensemble_svs_with_interactions_amd/csrc/*.hip; do
     -I"$D"/include -c "$f" -o "$D/$(basename "$f" .hip).o" &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "ab/libensvs_$REV.so" "$D"/*.o -L/opt/rocm/lib -lhipblaslt
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "ab/libensvs_$REV.so" "$D"/*.o
 rm -rf "$D"
 echo "ab/libensvs_$REV.so"

@@ -2,7 +2,7 @@
 1024): each arm sets kernels.<FLAG>["on"] values or calls C-ABI switches (ensvs_*=value), runs
 the bench leg in a fresh process, two rounds.
   python tools/flag_ab.py [--sf0] "COLSUM_ONCE=0,DEFER_WGRAD=0" "ensvs_ardec_coop_set_tile_seqs=32" \
-      "diffsinger.SKIP_GEMM=0" "BLAS:generic=0" ...
+      "diffsinger.SKIP_GEMM=0" "ensvs_set_p8=1" ...
 --sf0: time the recipe-default SeparateF0 leg instead (its ms_per_step)."""
 import json
 import os

@@ -1,6 +1,8 @@
-"""The four-phase 256 x 256 GEMM kernel (ensvs_set_p8) against the engine's other kernels,
-hipBLASLt (the plain products, BLAS on) and torch's bf16 matmul on the step's large shapes
-(dev tool): HIP-event time per launch and a bitwise check against the 128 x 128 kernel.
+"""The four-phase 256 x 256 GEMM kernel (ensvs_set_p8) against the engine's 128 x 128 kernel
+and, as a library anchor, torch's bf16 matmul (hipBLASLt, bf16 output, no epilogue) on the same
+M, N, K of the step's large shapes (dev tool): HIP-event time per launch and a bitwise check
+against the 128 x 128 kernel.  (Round 6 until the hipBLASLt route was removed: a "blas" arm,
+hipBLASLt with fp32 output and bias: profiles/r6_p8_bench.txt.)
    python tools/p8_bench.py [iters]"""
 import json
 import os
@@ -58,11 +60,7 @@ def case(name, M, N, spec, epi=L.EPI_PLAIN, bias=True, accum=False):
     res = dict(case=name, M=M, N=N, K=Kt)
     flops = 2.0 * M * N * Kt
     ref = None
-    for tag, p8, blas in (("eng128", 0, False), ("p8b2", 6, False), ("p8", 2, False),
-                          ("blas", 0, True)):
-        if blas and epi != L.EPI_PLAIN:
-            continue
-        K.BLAS["on"] = blas
+    for tag, p8 in (("eng128", 0), ("p8b2", 6), ("p8", 2)):
         _lib_call("ensvs_set_p8", p8)
         for o in outs:
             o.zero_()
@@ -77,8 +75,7 @@ def case(name, M, N, spec, epi=L.EPI_PLAIN, bias=True, accum=False):
         us = timeit(fn)
         res[f"{tag}_us"] = round(us, 1)
         res[f"{tag}_tflops"] = round(flops / us / 1e6, 1)
-    K.BLAS["on"] = True
-    _lib_call("ensvs_set_p8", 1)
+    _lib_call("ensvs_set_p8", 2)
     a = torch.randn(M, Kt, device=dev, dtype=torch.bfloat16)
     b = torch.randn(Kt, N, device=dev, dtype=torch.bfloat16)
     us = timeit(lambda: torch.matmul(a, b))
@@ -102,13 +99,11 @@ def none_case(name, M, N, spec):
     pb.repack()
     Y = torch.empty(M, N, device=dev)
     res = dict(case=name + " (K loop only)", M=M, N=N, K=sum(k * t for k, t, _ in spec))
-    K.BLAS["on"] = False
     for tag, p8 in (("eng128", 0), ("p8", 2)):
         _lib_call("ensvs_set_p8", p8)
         res[f"{tag}_us"] = round(timeit(lambda: K.gemm(segs, M // T, T, N, pb, Y, N,
                                                        epi=L.EPI_NONE)), 1)
-    K.BLAS["on"] = True
-    _lib_call("ensvs_set_p8", 1)
+    _lib_call("ensvs_set_p8", 2)
     print(json.dumps(res), flush=True)
 
 

@@ -2368,6 +2368,14 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
   if (npro - 2 >= 4) p8_wait<8>();
   else p8_wait<4>();  // nit == 1: half-tiles 0..3 issued, 2 may stay in flight
   __builtin_amdgcn_s_barrier();
+  // BAR2: the two wave rows run half a phase apart (row 1 takes one extra barrier here, row 0
+  // one after the loop), so on every SIMD one wave issues MFMAs while the other issues its LDS
+  // reads and DMAs.  Phase P of row 0 is [barrier 2P-1, 2P] memory, [2P, 2P+1] MFMA; row 1 is
+  // one barrier later.  WAR: a DMA of phase P (issued after barrier 2P-1 / 2P) overwrites data
+  // last read at phase P-2, whose reads completed before the reader's MFMAs ended (barrier
+  // 2P-3 / 2P-2).  RAW: each row's counted wait precedes its first barrier of the phase, which
+  // the other row's reads of phase P+1 follow.
+  if (BAR2 && wr == 1) __builtin_amdgcn_s_barrier();
 
   // fragment read offsets (rows + 16 i and the wave's quadrant rows keep the swizzle)
   const int arow = lane & 15, kq = lane >> 4;
@@ -2440,6 +2448,7 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
     __builtin_amdgcn_s_barrier();
     P8_MMA(4, 0, xb0);
   }
+  if (BAR2 && wr == 0) __builtin_amdgcn_s_barrier();  // pairs with row 1's last barrier
 #undef P8_MMA
 #undef P8_WAIT
 #undef P8_ISSUE
@@ -4085,8 +4094,10 @@ static const int BIG_MIN_TILES = 192;
 // them on the 128 x 128 kernel; SeparateF0 43.0 / 42.5 vs 42.9 / 42.9 and 43.9 / 43.9
 // (profiles/r6_blas_ab.txt, r6_blas_ab_sf0.txt).
 static int g_p8 = 2;
-static int g_p8_bar2 = 0;  // 1: two barriers per phase (the template's form); 0: one (faster:
-                           // tools/p8_bench.py, profiles/r6_p8_bench.txt)
+// 1: two barriers per phase with the wave rows staggered half a phase (default: 1-5 % faster
+// than one barrier per phase on every shape, bit-identical output; tools/p8_bench.py,
+// profiles/r6_p8_stagger.txt); 0: one barrier per phase, rows in lockstep
+static int g_p8_bar2 = 1;
 static const int P8_MIN_TILES = 128;
 
 static bool use_p8(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B) {
@@ -4311,7 +4322,7 @@ ENSVS_API int ensvs_set_gbw_dma(int on) {
 ENSVS_API int ensvs_set_p8(int mode) {
   if ((mode & 3) > 2 || mode < 0 || mode > 7) return ENSVS_E_ARG;
   g_p8 = mode & 3;
-  g_p8_bar2 = (mode & 4) ? 1 : 0;  // bit 2: two barriers per phase
+  g_p8_bar2 = (mode & 4) ? 1 : 0;  // bit 2: two barriers per phase, rows staggered
   return ENSVS_OK;
 }
 

@@ -84,6 +84,15 @@ def _take(key_out):
     return st
 
 
+def peek(out):
+    """The saved forward state filed under the output `out` (or a view of it), not consumed
+    (tests read the device's intermediate decisions from it)."""
+    st = _SAVED.get(_key(out))
+    if st is None:
+        raise KeyError("ensvs op: no forward state saved under this output")
+    return st
+
+
 def _flat_size(params):
     return max(sum((p.numel() + ALIGN - 1) // ALIGN * ALIGN for p in params), 1)
 

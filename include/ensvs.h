@@ -77,8 +77,10 @@ int ensvs_set_big_tile(int mode, int stages);
 /* The four-phase 256 x 256 kernel (counted LDS-DMA pipeline, four half-tiles in flight across
  * every barrier; same accumulation order, bitwise equal): mode 0 off; 1 for the launches the
  * 256 x 256 kernel takes (gate GEMMs); 2 (default) also for every other launch its LDS-staged epilogue
- * serves with >= 128 tiles of 256 x 256 (no column sums, not the LDS-DMA epilogues); + 4: two
- * barriers per phase (the template's form) instead of one (A/B). */
+ * serves with >= 128 tiles of 256 x 256 (no column sums, not the LDS-DMA epilogues); + 4
+ * (default 6): two barriers per phase with the wave rows staggered half a phase, so one wave of
+ * each SIMD issues MFMAs while the other issues its LDS reads and DMAs; without it one barrier
+ * per phase, rows in lockstep (A/B). */
 int ensvs_set_p8(int mode);
 /* Launches of fewer than 128 output tiles (small M) that the 64 x 64 kernel does not take
  * can run a 128 x 128 kernel with two K-groups of 4 waves (each group half of the K-steps,

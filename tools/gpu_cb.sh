@@ -1,18 +1,14 @@
 #!/bin/bash
-# scratch GPU experiment (round 6): lean-epilogue four-phase GEMM bench, torch.library ops,
-# step A/B: hipBLASLt route vs the engine (p8 for the gate GEMMs / for every eligible launch)
+# round-6 GPU check: main-line A/B of the p8 stagger and SQ counters of the K loop
 set -o pipefail
-mkdir -p gpurun_out
+mkdir -p gpurun_out/pmc
 ( while sleep 45; do date >> gpurun_out/hb.txt; done ) &
 HB=$!
 trap "kill $HB" EXIT
-timeout -k 10 300 python -u tools/p8_bench.py 30 > gpurun_out/p8_bench.log 2>&1
-rc=$?; tail -11 gpurun_out/p8_bench.log; [ $rc -ne 0 ] && exit $rc
-T="python -u -m pytest -v --timeout 400 --timeout-method thread -m gpu -rf"
-timeout -k 10 700 $T tests/test_torch_ops_gpu.py > gpurun_out/r6_tests_b.log 2>&1
-rc=$?; grep -E "PASS|FAIL|Error |error:" gpurun_out/r6_tests_b.log | tail -30; case $rc in 124|137|134|139) exit $rc;; esac
-timeout -k 10 900 python -u tools/flag_ab.py "" "BLAS=0" "BLAS=0,ensvs_set_p8=2" > gpurun_out/r6_blas_ab.txt 2>&1
-rc2=$?; cat gpurun_out/r6_blas_ab.txt | tail -8; [ $rc2 -ne 0 ] && exit $rc2
-timeout -k 10 900 python -u tools/flag_ab.py --sf0 "" "BLAS=0" "BLAS=0,ensvs_set_p8=2" > gpurun_out/r6_blas_ab_sf0.txt 2>&1
-rc3=$?; cat gpurun_out/r6_blas_ab_sf0.txt | tail -8
-exit $(( rc > rc3 ? rc : rc3 ))
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+SQ="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
+for m in 2 6; do
+  timeout -s KILL 90 rocprofv3 --pmc $SQ -d gpurun_out/pmc/sq_m$m -o sq --output-format csv -- python3 tools/p8_pmc.py dgrad $m > gpurun_out/pmc/sq_m$m.log 2>&1 || exit 1
+done
+timeout -k 10 500 python -u tools/flag_ab.py "ensvs_set_p8=2" "ensvs_set_p8=6" > gpurun_out/ab_stag.txt 2>&1
+rc=$?; tail -5 gpurun_out/ab_stag.txt; exit $rc

@@ -60,7 +60,7 @@ def case(name, M, N, spec, epi=L.EPI_PLAIN, bias=True, accum=False):
     res = dict(case=name, M=M, N=N, K=Kt)
     flops = 2.0 * M * N * Kt
     ref = None
-    for tag, p8 in (("eng128", 0), ("p8b2", 6), ("p8", 2)):
+    for tag, p8 in (("eng128", 0), ("p8", 2), ("p8stag", 6)):
         _lib_call("ensvs_set_p8", p8)
         for o in outs:
             o.zero_()
@@ -75,7 +75,7 @@ def case(name, M, N, spec, epi=L.EPI_PLAIN, bias=True, accum=False):
         us = timeit(fn)
         res[f"{tag}_us"] = round(us, 1)
         res[f"{tag}_tflops"] = round(flops / us / 1e6, 1)
-    _lib_call("ensvs_set_p8", 2)
+    _lib_call("ensvs_set_p8", 6)
     a = torch.randn(M, Kt, device=dev, dtype=torch.bfloat16)
     b = torch.randn(Kt, N, device=dev, dtype=torch.bfloat16)
     us = timeit(lambda: torch.matmul(a, b))
@@ -99,11 +99,11 @@ def none_case(name, M, N, spec):
     pb.repack()
     Y = torch.empty(M, N, device=dev)
     res = dict(case=name + " (K loop only)", M=M, N=N, K=sum(k * t for k, t, _ in spec))
-    for tag, p8 in (("eng128", 0), ("p8", 2)):
+    for tag, p8 in (("eng128", 0), ("p8", 2), ("p8stag", 6)):
         _lib_call("ensvs_set_p8", p8)
         res[f"{tag}_us"] = round(timeit(lambda: K.gemm(segs, M // T, T, N, pb, Y, N,
                                                        epi=L.EPI_NONE)), 1)
-    _lib_call("ensvs_set_p8", 2)
+    _lib_call("ensvs_set_p8", 6)
     print(json.dumps(res), flush=True)
 
 

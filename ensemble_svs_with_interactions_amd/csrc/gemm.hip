@@ -2274,9 +2274,11 @@ __device__ __forceinline__ void p8_wait() {
 // projections), the whole tile staged in two 128-row passes by all 8 waves; -1 -- every other
 // epilogue (epilogue_tile, 64-row chunks).  Instances per epilogue keep the other epilogues'
 // operand registers out of the K loop (the generic instance spills in its epilogue).
+constexpr int P8_PROBE_NODMA = 100 + EPI_NONE;
 template <int EPK, bool BAR2>
 __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs a) {
   constexpr bool GATE8 = EPK == EPI_GATE;
+  constexpr bool NODMA = EPK == P8_PROBE_NODMA;  // measurement: the K loop without its loads
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
@@ -2323,15 +2325,15 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
       const bool in_ = kb_ + ca8 < qK;                                                     \
       const int i0_ = j_ == 0 ? 0 : 2;                                                     \
       char* La_ = L_ + la + (j_ == 0 ? 0 : 64 * 128);                                      \
-      p8_dma(rxa, in_ ? O.oa[i0_] + kb2_ : P8_OOB, La_);                                   \
-      p8_dma(rxa, in_ ? O.oa[i0_ + 1] + kb2_ : P8_OOB, La_ + 128 * 128);                   \
+      if (!NODMA) p8_dma(rxa, in_ ? O.oa[i0_] + kb2_ : P8_OOB, La_);                                   \
+      if (!NODMA) p8_dma(rxa, in_ ? O.oa[i0_ + 1] + kb2_ : P8_OOB, La_ + 128 * 128);                   \
     } else {                                                                               \
       const bool in_ = kb_ + cb8 < qKp;                                                    \
       const int d_ = j_ == 1 ? 0 : 32;                                                     \
       char* Lb_ = L_ + P8_IMG + lb + d_ * 128;                                             \
       const unsigned ob_ = O.ob + (unsigned)(d_ * qKp) * 2u + kb2_;                        \
-      p8_dma(rwb, in_ ? ob_ : P8_OOB, Lb_);                                                \
-      p8_dma(rwb, in_ ? ob_ + (unsigned)(128 * qKp) * 2u : P8_OOB, Lb_ + 128 * 128);        \
+      if (!NODMA) p8_dma(rwb, in_ ? ob_ : P8_OOB, Lb_);                                                \
+      if (!NODMA) p8_dma(rwb, in_ ? ob_ + (unsigned)(128 * qKp) * 2u : P8_OOB, Lb_ + 128 * 128);        \
     }                                                                                      \
     if (j_ == 3) { /* K-step done: advance the cursor */                                   \
       const int nks_ = qs == 0 ? S0.nk : (qs == 1 ? S1.nk : S2.nk);                        \
@@ -2454,6 +2456,7 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
 #undef P8_ISSUE
 #undef P8_OFFS
   // every DMA was waited for (the last K-step's phase 1 waits vmcnt(0))
+  if constexpr (NODMA) return;
   float bs[4];
   const bool bias_st = a.bias != nullptr;
   if (bias_st) big_bias(a, n0, wc, lane, bs);
@@ -2516,6 +2519,391 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
     lds_sync();
   }
 #undef STAGE_HALF
+}
+
+// ------------------------------ 128 x 256, 8 waves, a 64-deep K-step in two phases
+// For the N = 256 launches at 30 k frames (the DiffNet's dilated-conv input gradient, gate
+// backward, residual and skip GEMMs): 256 x 256 tiles would be 120 workgroups, half the chip,
+// and the 128 x 128 kernel keeps one K-step in flight.  Here the four-phase kernel's counted
+// LDS-DMA pipeline on a 128 x 256 tile (240 workgroups): 8 waves in 2 x 4, each a 64 x 64
+// sub-tile, a K-step in two phases of 16 MFMAs per wave (phase 0 reads the wave's A rows and
+// its B columns 0-31, phase 1 its B columns 32-63 with A kept in registers).  A K-step's
+// operands are six 8-KB pieces, one buffer_load ... lds per thread each:
+//   part 0 / 1  A rows rA / rA + 64                          (read in phase 0)
+//   part 2 / 3  B rows rB / rB + 128   (64 c + 0-31)         (read in phase 0)
+//   part 4 / 5  B rows rB + 32 / + 160 (64 c + 32-63)        (read in phase 1)
+// K-step t + 2 is issued in the two phases of K-step t (three pieces each) into buffer
+// (t + 2) % 3 of three (3 x 48 KB): a region is rewritten >= 2 phases after its last read, and
+// 8-9 pieces (64-72 KB per CU) stay in flight across every barrier.  Two barriers per phase
+// with the wave rows staggered half a phase, as the four-phase kernel's default.  Per
+// accumulator the K order is the other kernels' (k-chunks in order): the same bits.
+// Epilogue: the tile staged through LDS; PLAIN lean (fp32 Y = acc + bias), or the non-pair
+// epilogues of gemm_epilogue_lds (PLAIN with accumulate / activation / bf16 copy, ADDSCALE,
+// RELU_MASK, GATE_BWD) with their column sums in the 128 x 128 kernel's row order.
+constexpr int BMH = 128;
+constexpr int P8H_AIMG = BMH * BK2 * 2;          // 16 KB
+constexpr int P8H_BUF = P8H_AIMG + P8_IMG;       // 48 KB: A + B of one K-step
+constexpr int P8H_LDS = 3 * P8H_BUF;             // 144 KB
+constexpr int P8H_LDS_EPI = BMH * EPB * 4 + CS_GROUPS * 2 * BNB * 4;  // tile + column sums
+
+__device__ __forceinline__ void xcd_tile_h(int& m0, int& n0) {
+  const int nM = gridDim.x, nN = gridDim.y, total = nM * nN;
+  const int orig = blockIdx.x + blockIdx.y * nM;
+  const int xcd = orig & 7, q = total >> 3, r = total & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  m0 = (wg / nN) * BMH;
+  n0 = (wg % nN) * BNB;
+}
+
+struct P8HOffs {
+  unsigned oa[2];
+  unsigned ob;
+};
+
+__device__ __forceinline__ P8HOffs p8h_offs(const SegU S, int j, int Npad, int n0, int rB,
+                                            int ca8, int cb8, const int (&bt)[2],
+                                            const int (&tt)[2], unsigned okm) {
+  P8HOffs o;
+  const int shj = S.shift0 + j * S.dil;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ts = tt[i] + shj;
+    const int src = S.pad == PAD_ZERO ? ((unsigned)ts < (unsigned)S.Tin ? ts : -1)
+                                      : pad_src(ts, S.Tin, S.pad);
+    const bool ok = ((okm >> i) & 1) && src >= 0;
+    o.oa[i] = ok ? (unsigned)((bt[i] * S.Tin + src) * S.ld + ca8) * 2u : P8_OOB;
+  }
+  o.ob = (unsigned)((j * Npad + n0 + rB) * S.Kp + cb8) * 2u;
+  return o;
+}
+
+// The non-pair epilogues of a staged 128 x 256 tile T [128][EPB] (no bias in T): thread tid
+// takes columns 4 (tid & 63) .. + 3 and rows (tid >> 6) + 8 k, k = 0..15, its next row's
+// operands loaded before this row's stores.  Per column these are the rows and the order of
+// the 128 x 128 kernel's column sums (row group g = 0..7 ascending, then the groups in order).
+template <unsigned MASK>
+__device__ __forceinline__ void p8h_epilogue(const GemmArgs& a, const float* T, float* X, int m0,
+                                             int n0, int tid) {
+  auto ep = [&](int e) { return ((MASK >> e) & 1u) && a.epi == e; };
+  const int cq = tid & 63, g = tid >> 6, col = n0 + cq * 4;
+  const int ne = min(4, a.N - col);
+  f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+  if (a.bias && ne > 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (e < ne) bv[e] = a.bias[col + e];
+  }
+  const bool want1 = (ep(EPI_PLAIN) && a.accum) || ep(EPI_ADDSCALE) || ep(EPI_RELU_MASK) ||
+                     ep(EPI_GATE_BWD);
+  const bool want2 = (ep(EPI_RELU_MASK) && a.accum) || ep(EPI_GATE_BWD);
+  const bool wl = ne == 4 && (want1 || want2);
+  f32x4 cs0 = {0.f, 0.f, 0.f, 0.f}, cs1 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 p1 = cs0, p2 = cs0, q1 = cs0, q2 = cs0;
+  if (wl) gen_load(a, m0 + g, col, want2, p1, p2);
+#pragma unroll 1
+  for (int k = 0; k < BMH / 8; ++k) {
+    const int row = g + 8 * k;
+    const int m = m0 + row;
+    if (wl && k + 1 < BMH / 8) gen_load(a, m + 8, col, want2, q1, q2);
+    if (m < a.M && ne > 0) {
+      f32x4 v = ld4(T + row * EPB + cq * 4);
+      if (a.csum && a.epi != EPI_GATE_BWD) cs0 += v;
+      if (a.bias) v += bv;
+      float* y = a.Y + (long long)m * a.ldy + col;
+      if (ne == 4) {
+        if (ep(EPI_PLAIN)) {
+          if (a.accum) v += p1;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (a.relu == 1) v[e] = fmaxf(v[e], 0.f);
+            else if (a.relu == 2) v[e] = sigmoidf_(v[e]);
+          }
+          st4(y, v);
+          shadow4(a, m, col, v);
+        } else if (ep(EPI_ADDSCALE)) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = __builtin_fmaf(a.alpha, p1[e], v[e]);
+            v[e] = a.relu == 1 ? fmaxf(v[e], 0.f) : v[e];
+          }
+          st4(y, v);
+          shadow4(a, m, col, v);
+        } else if (ep(EPI_RELU_MASK)) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = p1[e] > 0.f ? v[e] : 0.f;
+          if (a.accum) v += p2;
+          st4(y, v);
+          shadow4(a, m, col, v);
+        } else if (ep(EPI_GATE_BWD)) {
+          f32x4 dg, df;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float t0, t1;
+            gate_bwd_(v[e], p1[e], p2[e], t0, t1);
+            dg[e] = t0;
+            df[e] = t1;
+          }
+          if (a.csum) {
+            cs0 += dg;
+            cs1 += df;
+          }
+          if (a.Y) {
+            st4(y, dg);
+            st4(y + a.C, df);
+          }
+          shadow4(a, m, col, dg);
+          shadow4(a, m, a.C + col, df);
+        }
+      } else {
+        for (int e = 0; e < ne; ++e) {
+          float w = v[e];
+          float* ye = y + e;
+          if (ep(EPI_PLAIN)) {
+            if (a.accum) w += *ye;
+            if (a.relu == 1) w = fmaxf(w, 0.f);
+            else if (a.relu == 2) w = sigmoidf_(w);
+            *ye = w;
+          } else if (ep(EPI_ADDSCALE)) {
+            w = __builtin_fmaf(a.alpha, a.aux1[(long long)m * a.ld1 + col + e], w);
+            *ye = a.relu == 1 ? fmaxf(w, 0.f) : w;
+          } else if (ep(EPI_RELU_MASK)) {
+            w = a.aux1[(long long)m * a.ld1 + col + e] > 0.f ? w : 0.f;
+            *ye = a.accum ? *ye + w : w;
+          } else if (ep(EPI_GATE_BWD)) {
+            const float gg = ld_aux1(a, (long long)m * a.ld1 + col + e);
+            const float ff = ld_aux1(a, (long long)m * a.ld1 + a.C + col + e);
+            gate_bwd_(w, gg, ff, ye[0], ye[a.C]);
+          }
+        }
+      }
+    }
+    p1 = q1;
+    p2 = q2;
+  }
+  if (a.csum) {  // uniform: every thread reaches the barrier
+    *(f32x4*)(X + g * 2 * BNB + cq * 4) = cs0;
+    *(f32x4*)(X + g * 2 * BNB + BNB + cq * 4) = cs1;
+    lds_sync();
+    const int j = tid;  // NTHRB == 2 * BNB: the accumulator / d(gate) columns, then d(filter)
+    if (j < BNB || ep(EPI_GATE_BWD)) {
+      const int c = n0 + (j & (BNB - 1));
+      if (c < a.N) {
+        float t = X[j];
+#pragma unroll
+        for (int q = 1; q < CS_GROUPS; ++q) t += X[q * 2 * BNB + j];
+        a.csum[(long long)(m0 / BM) * a.csum_ld + (j < BNB ? c : a.C + c)] = t;
+      }
+    }
+  }
+}
+
+// EPK: EPI_PLAIN -- the lean plain epilogue (as the four-phase kernel's); -1 -- p8h_epilogue
+template <int EPK>
+__global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8h_kernel(const GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  int m0, n0;
+  xcd_tile_h(m0, n0);
+  const int M = a.M, Tout = a.Tout, Npad = a.Npad;
+  const int nseg = a.nseg;
+  const SegU S0 = seg_u(a.seg[0], a.W);
+  const SegU S1 = nseg > 1 ? seg_u(a.seg[1], a.W) : S0;
+  const SegU S2 = nseg > 2 ? seg_u(a.seg[2], a.W) : S0;
+  const int nit = S0.nk * S0.taps + (nseg > 1 ? S1.nk * S1.taps : 0) +
+                  (nseg > 2 ? S2.nk * S2.taps : 0);
+  const int np = 6 * nit;  // pieces
+  const int rA = wid * 8 + (lane >> 3), rB = (wid & 3) * 8 + (wid >> 2) * 64 + (lane >> 3);
+  const int ca8 = swz(rA, lane & 7) * 8, cb8 = swz(rB, lane & 7) * 8;
+  int bt[2], tt[2];
+  unsigned okm = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + rA + i * 64;
+    const bool ok = m < M;
+    bt[i] = ok ? m / Tout : 0;
+    tt[i] = ok ? m - bt[i] * Tout : 0;
+    okm |= ok ? (1u << i) : 0u;
+  }
+  const int la = wid * 8 * 128, lb = ((wid & 3) * 8 + (wid >> 2) * 64) * 128;
+  // staging cursor: the K-step whose pieces are issued next (segment, tap, k-step, buffer)
+  int qs = 0, qj = 0, qkc = 0, qb = 0, nis = 0;
+#define P8H_OFFS(S) p8h_offs(S, qj, Npad, n0, rB, ca8, cb8, bt, tt, okm)
+  P8HOffs O = P8H_OFFS(S0);
+  __amdgpu_buffer_rsrc_t rxa = p8_rsrc(S0.x), rwb = p8_rsrc(S0.w);
+  int qK = S0.K, qKp = S0.Kp;
+#define P8H_ISSUE(part)                                                                    \
+  do {                                                                                     \
+    char* L_ = smem + qb * P8H_BUF;                                                        \
+    const int kb_ = qkc * BK2;                                                             \
+    const unsigned kb2_ = (unsigned)kb_ * 2u;                                              \
+    if ((part) < 2) {                                                                      \
+      const bool in_ = kb_ + ca8 < qK;                                                     \
+      p8_dma(rxa, in_ ? O.oa[(part) & 1] + kb2_ : P8_OOB, L_ + la + ((part) & 1) * 64 * 128);\
+    } else {                                                                               \
+      constexpr int d_ = (part) == 2 ? 0 : ((part) == 3 ? 128 : ((part) == 4 ? 32 : 160)); \
+      const bool in_ = kb_ + cb8 < qKp;                                                    \
+      p8_dma(rwb, in_ ? O.ob + (unsigned)(d_ * qKp) * 2u + kb2_ : P8_OOB,                   \
+             L_ + P8H_AIMG + lb + d_ * 128);                                               \
+    }                                                                                      \
+    ++nis;                                                                                 \
+    if ((part) == 5) { /* K-step done: advance the cursor */                               \
+      qb = qb == 2 ? 0 : qb + 1;                                                           \
+      const int nks_ = qs == 0 ? S0.nk : (qs == 1 ? S1.nk : S2.nk);                        \
+      const int taps_ = qs == 0 ? S0.taps : (qs == 1 ? S1.taps : S2.taps);                 \
+      if (++qkc == nks_) {                                                                 \
+        qkc = 0;                                                                           \
+        const int qs0_ = qs;                                                               \
+        if (++qj == taps_) {                                                               \
+          qj = 0;                                                                          \
+          ++qs;                                                                            \
+        }                                                                                  \
+        if (qs < nseg) {                                                                   \
+          if (qs != qs0_) {                                                                \
+            rxa = p8_rsrc(qs == 1 ? S1.x : S2.x);                                          \
+            rwb = p8_rsrc(qs == 1 ? S1.w : S2.w);                                          \
+            qK = qs == 1 ? S1.K : S2.K;                                                    \
+            qKp = qs == 1 ? S1.Kp : S2.Kp;                                                 \
+          }                                                                                \
+          O = qs == 0 ? P8H_OFFS(S0) : (qs == 1 ? P8H_OFFS(S1) : P8H_OFFS(S2));            \
+        }                                                                                  \
+      }                                                                                    \
+    }                                                                                      \
+  } while (0)
+#define P8H_KSTEP_LO() \
+  do {                 \
+    P8H_ISSUE(0);      \
+    P8H_ISSUE(1);      \
+    P8H_ISSUE(2);      \
+  } while (0)
+#define P8H_KSTEP_HI() \
+  do {                 \
+    P8H_ISSUE(3);      \
+    P8H_ISSUE(4);      \
+    P8H_ISSUE(5);      \
+  } while (0)
+  // the counted wait: at most nis - 1 - need pieces of this thread still in flight
+#define P8H_WAIT(need)                            \
+  do {                                            \
+    const int al_ = nis - 1 - (need);             \
+    if (al_ >= 9) p8_wait<9>();                   \
+    else if (al_ == 8) p8_wait<8>();              \
+    else if (al_ == 7) p8_wait<7>();              \
+    else if (al_ == 6) p8_wait<6>();              \
+    else if (al_ == 5) p8_wait<5>();              \
+    else if (al_ == 4) p8_wait<4>();              \
+    else if (al_ == 3) p8_wait<3>();              \
+    else if (al_ == 2) p8_wait<2>();              \
+    else if (al_ == 1) p8_wait<1>();              \
+    else p8_wait<0>();                            \
+  } while (0)
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-steps 0 and 1, then wait for phase 0's pieces (0..3)
+  for (int t = 0; t < min(2, nit); ++t) {
+    P8H_KSTEP_LO();
+    P8H_KSTEP_HI();
+  }
+  P8H_WAIT(3);
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // rows staggered half a phase (see the p8 kernel)
+
+  const int arow = lane & 15, kq = lane >> 4;
+  const int fa0 = (wr * 64 + arow) * 128 + swz(arow, kq) * 16;
+  const int fa1 = (wr * 64 + arow) * 128 + swz(arow, kq + 4) * 16;
+  const int fb0 = P8H_AIMG + (wc * 64 + arow) * 128 + swz(arow, kq) * 16;
+  const int fb1 = P8H_AIMG + (wc * 64 + arow) * 128 + swz(arow, kq + 4) * 16;
+  bf16x8 xa[2][4], xb0[2][2], xb1[2][2];
+#define P8H_MMA(J0, B)                                                                     \
+  do {                                                                                     \
+    __builtin_amdgcn_s_setprio(1);                                                         \
+    _Pragma("unroll") for (int h = 0; h < 2; ++h)                                          \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                          \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                          \
+      acc[i][(J0) + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[h][i], B[h][j],         \
+                                                                acc[i][(J0) + j], 0, 0, 0); \
+    __builtin_amdgcn_s_setprio(0);                                                         \
+    __builtin_amdgcn_s_barrier();                                                          \
+  } while (0)
+
+  int rb = 0;  // buffer of K-step t
+  for (int t = 0; t < nit; ++t) {
+    const char* St = smem + rb * P8H_BUF;
+    // phase 0: A rows and B columns 0-31 of the wave; issues K-step t + 2's pieces 0-2
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) xb0[h][j] = *(const bf16x8*)(St + (h ? fb1 : fb0) + j * 2048);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xa[h][i] = *(const bf16x8*)(St + (h ? fa1 : fa0) + i * 2048);
+    }
+    if (t + 2 < nit) P8H_KSTEP_LO();
+    P8H_WAIT(6 * t + 5);
+    __builtin_amdgcn_s_barrier();
+    P8H_MMA(0, xb0);
+    // phase 1: B columns 32-63; issues pieces 3-5
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        xb1[h][j] = *(const bf16x8*)(St + (h ? fb1 : fb0) + 32 * 128 + j * 2048);
+    if (t + 2 < nit) P8H_KSTEP_HI();
+    if (t + 1 < nit) P8H_WAIT(6 * t + 9);
+    __builtin_amdgcn_s_barrier();
+    P8H_MMA(2, xb1);
+    rb = rb == 2 ? 0 : rb + 1;
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // pairs with row 1's last barrier
+#undef P8H_MMA
+#undef P8H_WAIT
+#undef P8H_KSTEP_LO
+#undef P8H_KSTEP_HI
+#undef P8H_ISSUE
+#undef P8H_OFFS
+  // every DMA was waited for (the last K-step's phase 0 waits vmcnt(0))
+  float* T = (float*)smem;
+  if constexpr (EPK == EPI_PLAIN) {
+    float bs[4];
+    const bool bias_st = a.bias != nullptr;
+    if (bias_st) big_bias(a, n0, wc, lane, bs);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          T[(wr * 64 + mt * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] =
+              bias_st ? acc[mt][nt][r] + bs[nt] : acc[mt][nt][r];
+    lds_sync();
+    const int cq = tid & 63, r0 = tid >> 6;
+    const int col = n0 + cq * 4;
+    if (col < a.N) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = m0 + r0 + 8 * i;
+        const f32x4 v = ld4(T + (r0 + 8 * i) * EPB + cq * 4);
+        if (m < a.M) st4(a.Y + (long long)m * a.ldy + col, v);
+      }
+    }
+    return;
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          T[(wr * 64 + mt * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] =
+              acc[mt][nt][r];
+    lds_sync();
+    constexpr unsigned MASK = EPK < 0 ? ~0u : (1u << EPK);
+    p8h_epilogue<MASK>(a, T, T + BMH * EPB, m0, n0, tid);
+  }
 }
 
 // ------------------------------------------------- 64 x 64 bf16-operand GEMM (small M)
@@ -4098,6 +4486,7 @@ static int g_p8 = 2;
 // than one barrier per phase on every shape, bit-identical output; tools/p8_bench.py,
 // profiles/r6_p8_stagger.txt); 0: one barrier per phase, rows in lockstep
 static int g_p8_bar2 = 1;
+static int g_p8_nodma = 0;  // measurement (EPI_NONE launches only): skip the K loop's loads
 static const int P8_MIN_TILES = 128;
 
 static bool use_p8(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B) {
@@ -4107,6 +4496,32 @@ static bool use_p8(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int 
   const long long tiles = (long long)cdiv(a.M, BMB) * (a.Npad / BNB);
   if (a.epi == EPI_GATE) return g_big_tile && tiles >= BIG_MIN_TILES;
   return g_p8 >= 2 && tiles >= P8_MIN_TILES;  // (EPI_NONE: the K loop alone, measurement)
+}
+
+// The 128 x 256 kernel (conv_gemm_b16_p8h_kernel) for the launches the 256 x 256 one leaves
+// with too few tiles -- the N = 256 GEMMs at 30 k frames (240 workgroups of 128 x 256 vs 120 of
+// 256 x 256).  Its K loop streams ~33 GB/s of operands per CU, as the four-phase kernel's
+// does (the bytes in flight per CU over the L2 / fabric latency bound both), which at 48 KB
+// per 4.2-MFLOP K-step is 0.29 of the MFMA peak, and its one workgroup per CU runs an
+// operand-heavy epilogue at one row of loads in flight per thread: on the DiffNet's dilated
+// dgrad, gate-backward and residual launches it measured 49 / 38 / 25 us against the 128 x 128
+// kernel's 38.7 / 24.9 / 21.7 (two workgroups per CU, LDS-DMA epilogues), the step +1.2 ms
+// (tools/p8h_bench.py, profiles/r6_p8h_bench.txt, r6_p8h_ab.txt).  It runs where it wins: the
+// lean plain epilogue over a long K (>= 32 K-steps: the skip sum K = 5 120, 111.7 vs
+// 123.6 us; the conditioner input gradient K = 10 240).  Every epilogue stays available
+// (ensvs_set_p8h(2), bitwise tests).  0: off; 1: long-K plain launches; 2: every launch.
+static int g_p8h = 1;
+
+static bool use_p8h(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B) {
+  if (!g_p8h || !a.vec_out || a.Npad % BNB) return false;
+  if (a.epi == EPI_GATE || a.epi == EPI_RESSKIP || a.epi == EPI_GATE_TS) return false;
+  for (int s = 0; s < nseg; ++s)  // 31-bit byte offsets into the operand resources
+    if ((long long)B * segs[s].Tin * segs[s].ld >= (1ll << 30)) return false;
+  if ((long long)cdiv(a.M, BMH) * (a.Npad / BNB) < P8_MIN_TILES) return false;
+  if (g_p8h >= 2) return true;
+  int nit = 0;
+  for (int s = 0; s < nseg; ++s) nit += cdiv(segs[s].K, BK2) * segs[s].taps;
+  return a.epi == EPI_PLAIN && !a.accum && !a.relu && !a.ybf && !a.csum && nit >= 32;
 }
 
 static bool use_big_tile(const GemmArgs& a) {
@@ -4155,7 +4570,9 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     if (ep != hipSuccess) return ENSVS_E_HIP;                                             \
     hipLaunchKernelGGL((conv_gemm_b16_p8_kernel<E, B2>), grid_b, dim3(NTHRB), (L), st, a); \
   } while (0)
-    if (g_p8_bar2) {
+    if (a.epi == EPI_NONE && g_p8_nodma) {
+      P8(P8_PROBE_NODMA, true, lb);
+    } else if (g_p8_bar2) {
       if (gate) P8(EPI_GATE, true, lb);
       else if (plain) P8(EPI_PLAIN, true, lbp);
       else P8(-1, true, lb);
@@ -4165,6 +4582,28 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
       else P8(-1, false, lb);
     }
 #undef P8
+    ENSVS_CHECK_LAUNCH();
+    return ENSVS_OK;
+  }
+  if (!has_pd && use_p8h(a, segs, nseg, B)) {
+    const dim3 grid_h(cdiv(a.M, BMH), Npad / BNB);
+    const bool plain = a.epi == EPI_PLAIN && !a.accum && !a.relu && !a.ybf && !a.csum && a.Y &&
+                       a.N % 4 == 0 && a.ldy % 4 == 0 && ((uintptr_t)a.Y & 15) == 0 &&
+                       (!a.bias || ((uintptr_t)a.bias & 3) == 0);
+    const size_t lh = std::max<size_t>(P8H_LDS, plain ? (size_t)BMH * EPB * 4 : P8H_LDS_EPI);
+#define P8H(E)                                                                            \
+  do {                                                                                    \
+    static const hipError_t eh = hipFuncSetAttribute(                                     \
+        (const void*)conv_gemm_b16_p8h_kernel<E>,                                         \
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lh);                             \
+    if (eh != hipSuccess) return ENSVS_E_HIP;                                             \
+    hipLaunchKernelGGL((conv_gemm_b16_p8h_kernel<E>), grid_h, dim3(NTHRB), lh, st, a);    \
+  } while (0)
+    if (plain) P8H(EPI_PLAIN);
+    else if (a.epi == EPI_ADDSCALE) P8H(EPI_ADDSCALE);
+    else if (a.epi == EPI_GATE_BWD) P8H(EPI_GATE_BWD);
+    else P8H(-1);
+#undef P8H
     ENSVS_CHECK_LAUNCH();
     return ENSVS_OK;
   }
@@ -4320,9 +4759,16 @@ ENSVS_API int ensvs_set_gbw_dma(int on) {
 }
 
 ENSVS_API int ensvs_set_p8(int mode) {
-  if ((mode & 3) > 2 || mode < 0 || mode > 7) return ENSVS_E_ARG;
+  if ((mode & 3) > 2 || mode < 0 || mode > 15) return ENSVS_E_ARG;
   g_p8 = mode & 3;
   g_p8_bar2 = (mode & 4) ? 1 : 0;  // bit 2: two barriers per phase, rows staggered
+  g_p8_nodma = (mode & 8) ? 1 : 0;  // bit 3: EPI_NONE probes without the K loop's loads
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_set_p8h(int mode) {
+  if (mode < 0 || mode > 2) return ENSVS_E_ARG;
+  g_p8h = mode;
   return ENSVS_OK;
 }
 

@@ -80,8 +80,15 @@ int ensvs_set_big_tile(int mode, int stages);
  * serves with >= 128 tiles of 256 x 256 (no column sums, not the LDS-DMA epilogues); + 4
  * (default 6): two barriers per phase with the wave rows staggered half a phase, so one wave of
  * each SIMD issues MFMAs while the other issues its LDS reads and DMAs; without it one barrier
- * per phase, rows in lockstep (A/B). */
+ * per phase, rows in lockstep (A/B); + 8: measurement only -- EPI_NONE launches run the K
+ * loop without its operand loads (what the loads cost). */
 int ensvs_set_p8(int mode);
+/* The 128 x 256 kernel (the four-phase pipeline on half-height tiles, two phases per K-step,
+ * three K-step buffers) for launches the 256 x 256 kernel leaves with < 128 tiles: mode 0 off;
+ * 1 (default) the lean plain epilogue over >= 32 K-steps (where it beats the 128 x 128
+ * kernel); 2 every launch but the pair epilogues (gate, res/skip), column sums included (A/B,
+ * tests).  Same accumulation and column-sum order: bitwise equal. */
+int ensvs_set_p8h(int mode);
 /* Launches of fewer than 128 output tiles (small M) that the 64 x 64 kernel does not take
  * can run a 128 x 128 kernel with two K-groups of 4 waves (each group half of the K-steps,
  * tiles added through LDS; default off: the one-group kernel, the same bits as the

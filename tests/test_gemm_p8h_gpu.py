@@ -1,0 +1,143 @@
+"""128 x 256-tile bf16-operand GEMM (conv_gemm_b16_p8h_kernel, ensvs_set_p8h) against the
+128 x 128 kernel: identical bits for every epilogue it takes -- lean plain, plain with
+accumulate / ReLU / bf16 copy, ADDSCALE, RELU_MASK, GATE_BWD (fp32 and bf16 gate/filter save)
+-- and for the 128-row-tile column sums, multi-segment / multi-tap K with padding, a ragged M
+tail, N = 256 (the DiffNet's C; wider launches with >= 128 tiles of 256 x 256 go to the
+four-phase kernel first), K-loops of 1 to 80 K-steps (three-buffer ring wrap, the prologue's
+short cases)."""
+import pytest
+import torch
+
+from ensemble_svs_with_interactions_amd import _lib as L
+from ensemble_svs_with_interactions_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _pack(ws):
+    pb = K.PackedBuffer(L.DT_BF16)
+    refs = [pb.add(w, w.shape[0], w.shape[1], w.shape[2], w.shape[1] * w.shape[2], w.shape[2], 1)
+            for w in ws]
+    pb.finalize(DEV)
+    pb.repack()
+    return pb, refs
+
+
+def _both(run):
+    """run() on the 128 x 128 kernel (p8h off), then on the 128 x 256 kernel (mode 2: every
+    launch it can take)."""
+    outs = []
+    try:
+        for on in (0, 2):
+            L.call("ensvs_set_p8h", on)
+            outs.append(run())
+            torch.cuda.synchronize()
+    finally:
+        L.call("ensvs_set_p8h", 1)
+    return outs
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).contiguous()
+
+
+def _assert_same(a, b):
+    for u, v in zip(a, b):
+        if u is not None:
+            assert torch.equal(u, v), (u.float() - v.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("epi", ["plain_lean", "plain_full", "plain_csum", L.EPI_ADDSCALE,
+                                 "addscale_csum", L.EPI_RELU_MASK, L.EPI_GATE_BWD,
+                                 "gate_bwd_bf16", "gate_bwd_no_y"])
+@pytest.mark.parametrize("B,T", [(30, 1024), (30, 1000)])
+def test_p8h_epilogues_bitwise(epi, B, T):
+    csum = epi in ("plain_csum", "addscale_csum", L.EPI_GATE_BWD, "gate_bwd_bf16",
+                   "gate_bwd_no_y")
+    if csum and T % 128:
+        pytest.skip("column sums take whole 128-row tiles")
+    torch.manual_seed(13)
+    C = 256
+    M = B * T
+    N = C
+    # the dilated-conv input gradient's shape: 3 taps over 2C channels, plus a plain segment
+    dp = _bf(torch.randn(M, 2 * C, device=DEV))
+    x2 = _bf(torch.randn(M, C, device=DEV))
+    wd = torch.randn(N, 2 * C, 3, device=DEV) / (6 * C) ** 0.5
+    w2 = torch.randn(N, C, 1, device=DEV) / C ** 0.5
+    pb, (rd, r2) = _pack([wd, w2])
+    segs = [K.Seg(dp, 2 * C, 2 * C, rd, T, taps=3, dil=8, shift0=-8), K.Seg(x2, C, C, r2, T)]
+    bias = torch.randn(N, device=DEV)
+    aux1 = torch.randn(M, 2 * N, device=DEV)
+    radd = torch.randn(B, N, device=DEV)
+
+    def run():
+        g = torch.Generator(DEV).manual_seed(5)
+        y = torch.randn(M, 2 * N, device=DEV, generator=g)
+        ybf = torch.zeros(M, 2 * N, device=DEV, dtype=torch.bfloat16)
+        cs = torch.zeros(M // 128, 2 * N, device=DEV) if csum else None
+        kw = dict(bias=bias)
+        if epi == "plain_lean":
+            pass
+        elif epi == "plain_full":
+            kw.update(relu=True, accum=True, ybf=ybf, ybf_ld=2 * N, ybf_radd=radd,
+                      ybf_radd_ld=N)
+        elif epi == "plain_csum":
+            kw = dict(ybf=ybf, ybf_ld=2 * N, csum=cs, csum_ld=2 * N)
+        elif epi == L.EPI_ADDSCALE:
+            kw.update(epi=epi, aux1=aux1, ld1=2 * N, alpha=0.7071, ybf=ybf, ybf_ld=2 * N)
+        elif epi == "addscale_csum":
+            kw = dict(epi=L.EPI_ADDSCALE, aux1=aux1, ld1=2 * N, alpha=0.7071, ybf=ybf,
+                      ybf_ld=2 * N, csum=cs, csum_ld=2 * N)
+        elif epi == L.EPI_RELU_MASK:
+            kw = dict(epi=epi, aux1=aux1, ld1=2 * N, accum=True)
+        else:
+            a1 = aux1 if epi == L.EPI_GATE_BWD else _bf(aux1)
+            kw = dict(epi=L.EPI_GATE_BWD, aux1=a1, ld1=2 * N, C=C, ybf=ybf, ybf_ld=2 * N,
+                      csum=cs, csum_ld=2 * N, keep_y=epi != "gate_bwd_no_y")
+        K.gemm(segs, B, T, N, pb, y, 2 * N, **kw)
+        return y, ybf, cs
+    a, b = _both(run)
+    _assert_same(a, b)
+
+
+@pytest.mark.parametrize("N,specs", [
+    (256, [(128, 7, 1, L.PAD_REFLECT), (40, 1, 1, L.PAD_ZERO), (72, 3, 2, L.PAD_REPLICATE)]),
+    (256, [(64, 1, 1, L.PAD_ZERO)]),                  # one K-step
+    (256, [(128, 1, 1, L.PAD_ZERO)]),                 # two (prologue only)
+    (256, [(192, 1, 1, L.PAD_ZERO)]),                 # three: the ring's first wrap
+    (256, [(5120, 1, 1, L.PAD_ZERO)]),                # the DiffNet skip sum, K = L C
+    (256, [(256, 3, 4, L.PAD_ZERO), (256, 1, 1, L.PAD_ZERO)]),
+])
+@pytest.mark.parametrize("B,T", [(30, 1024), (17, 999)])
+def test_p8h_segments_bitwise(N, specs, B, T):
+    torch.manual_seed(7)
+    M = B * T
+    if (M + 127) // 128 * (N // 256) < 128:
+        pytest.skip("fewer than 128 tiles: the 128 x 128 kernel's launch")
+    xs, ws = [], []
+    for (Kc, taps, dil, pad) in specs:
+        xs.append(_bf(torch.randn(M, Kc, device=DEV)))
+        ws.append(torch.randn(N, Kc, taps, device=DEV) / (Kc * taps) ** 0.5)
+    pb, refs = _pack(ws)
+    segs = [K.Seg(x, Kc, Kc, r, T, taps=taps, dil=dil, shift0=-(taps // 2) * dil, pad=pad)
+            for x, r, (Kc, taps, dil, pad) in zip(xs, refs, specs)]
+    bias = torch.randn(N, device=DEV)
+
+    def run():
+        y = torch.empty(M, N, device=DEV)
+        K.gemm(segs, B, T, N, pb, y, N, bias=bias)
+        return (y,)
+    a, b = _both(run)
+    _assert_same(a, b)
+    ref = sum(torch.nn.functional.conv1d(
+        torch.nn.functional.pad(x.float().view(B, T, -1).transpose(1, 2),
+                                ((taps // 2) * dil, (taps // 2) * dil),
+                                mode={L.PAD_ZERO: "constant", L.PAD_REFLECT: "reflect",
+                                      L.PAD_REPLICATE: "replicate"}[pad]),
+        w.to(torch.bfloat16).float(), dilation=dil)
+        for x, w, (Kc, taps, dil, pad) in zip(xs, ws, specs))
+    ref = ref.transpose(1, 2).reshape(M, N) + bias
+    err = (b[0] - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-5, err

@@ -833,10 +833,12 @@ def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
         torch.cuda.synchronize()
         el_first = time.time() - t0
         t0 = time.time()
+        w0 = feeder.wait_s
         for _ in range(epochs):
             res = train_epoch(model, opt, feeder, graphs=graphs)
         torch.cuda.synchronize()
         el = (time.time() - t0) / epochs
+        feeder_wait = (feeder.wait_s - w0) / epochs
         # the same epochs issued eagerly (every launch from the host), for the host-issue cost
         t0 = time.time()
         for _ in range(epochs):
@@ -878,6 +880,7 @@ def real_data_train(args, dev, segments=24, epochs=2, batch_max_frames=32000):
                           "(captured in the untimed first epoch, replayed from then on), all "
                           "graphs in one shared memory pool",
                 first_epoch_s=el_first, captured_signatures=n_graphs,
+                feeder_wait_s_per_epoch=feeder_wait,
                 memory_reserved_gb=reserved / 1e9,
                 eager_value=valid / el_eager, eager_s_per_epoch=el_eager,
                 same_shapes_back_to_back_s_per_epoch=fixed,

@@ -2456,7 +2456,13 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
 #undef P8_ISSUE
 #undef P8_OFFS
   // every DMA was waited for (the last K-step's phase 1 waits vmcnt(0))
-  if constexpr (NODMA) return;
+  if constexpr (NODMA) {  // keep the MFMAs: the accumulators reach an (empty) use
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   float bs[4];
   const bool bias_st = a.bias != nullptr;
   if (bias_st) big_bias(a, n0, wc, lane, bs);

@@ -19,6 +19,7 @@ import os
 import random
 import sys
 import threading
+import time
 import queue
 from glob import glob
 
@@ -215,6 +216,7 @@ class PairBatchFeeder:
         if self.cuda and not torch.cuda.is_available():
             raise RuntimeError("PairBatchFeeder: a CUDA device was requested but none is visible")
         self.copy_stream = torch.cuda.Stream(device=self.device) if self.cuda else None
+        self.wait_s = 0.0  # host time the consumer spent waiting for the reader (diagnostic)
 
     def _host_batch(self, batch):
         cols = _data.collate_syncmultitrack_acoustic([self.dataset[i] for i in batch],
@@ -278,7 +280,9 @@ class PairBatchFeeder:
         q, stop, th = started if started is not None else self._start()
         try:
             while True:
+                t0 = time.perf_counter()
                 hb = q.get()
+                self.wait_s += time.perf_counter() - t0
                 if hb is None:
                     break
                 if isinstance(hb, BaseException):

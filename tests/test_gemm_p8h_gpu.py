@@ -141,3 +141,58 @@ def test_p8h_segments_bitwise(N, specs, B, T):
     ref = ref.transpose(1, 2).reshape(M, N) + bias
     err = (b[0] - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("N,specs,epi", [
+    (4096, [(512, 1, 1, L.PAD_ZERO)], "plain"),                      # 8 K-steps
+    (1024, [(2048, 1, 1, L.PAD_ZERO), (2048, 1, 1, L.PAD_ZERO)], "plain"),
+    (512, [(64, 1, 1, L.PAD_ZERO)], "plain"),                        # 1 K-step
+    (512, [(128, 1, 1, L.PAD_ZERO)], "plain"),                       # 2
+    (512, [(192, 1, 1, L.PAD_ZERO)], "plain"),                       # 3: short of the lead
+    (512, [(320, 1, 1, L.PAD_ZERO)], "relu_bf16"),                   # 5: the generic epilogue
+    (512, [(256, 3, 4, L.PAD_ZERO), (256, 1, 1, L.PAD_ZERO)], "gate"),
+    (768, [(128, 7, 1, L.PAD_REFLECT), (40, 1, 1, L.PAD_ZERO), (72, 3, 2, L.PAD_REPLICATE)],
+     "plain"),
+])
+@pytest.mark.parametrize("B,T", [(30, 1024), (31, 999)])
+def test_p8_barrier_forms_bitwise(N, specs, epi, B, T):
+    """The four-phase 256 x 256 kernel, one barrier per phase and two with the wave rows
+    staggered, against the 128 x 128 kernel (ensvs_set_p8 0 / 2 / 6): the same bits, K-loops
+    of 1 to 64 K-steps, multi-segment / multi-tap K, the plain, generic and gate epilogues."""
+    torch.manual_seed(9)
+    M = B * T
+    xs, ws = [], []
+    for (Kc, taps, dil, pad) in specs:
+        xs.append(_bf(torch.randn(M, Kc, device=DEV)))
+        ws.append(torch.randn(N, Kc, taps, device=DEV) / (Kc * taps) ** 0.5)
+    pb, refs = _pack(ws)
+    segs = [K.Seg(x, Kc, Kc, r, T, taps=taps, dil=dil, shift0=-(taps // 2) * dil, pad=pad)
+            for x, r, (Kc, taps, dil, pad) in zip(xs, refs, specs)]
+    bias = torch.randn(N, device=DEV)
+    C = N // 2
+
+    def run():
+        if epi == "gate":
+            z = torch.zeros(M, C, device=DEV)
+            gf = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+            zb = torch.zeros(M, C, device=DEV, dtype=torch.bfloat16)
+            K.gemm(segs, B, T, N, pb, z, C, epi=L.EPI_GATE, aux0=gf, ld0=N, C=C, ybf=zb,
+                   ybf_ld=C, keep_y=True, bias=bias)
+            return z, gf, zb
+        y = torch.empty(M, N, device=DEV)
+        if epi == "relu_bf16":
+            yb = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+            K.gemm(segs, B, T, N, pb, y, N, bias=bias, relu=True, ybf=yb, ybf_ld=N)
+            return y, yb
+        K.gemm(segs, B, T, N, pb, y, N, bias=bias)
+        return (y,)
+    outs = []
+    try:
+        for mode in (0, 2, 6):
+            L.call("ensvs_set_p8", mode)
+            outs.append(run())
+            torch.cuda.synchronize()
+    finally:
+        L.call("ensvs_set_p8", 6)
+    _assert_same(outs[0], outs[1])
+    _assert_same(outs[0], outs[2])

@@ -1147,9 +1147,9 @@ def main():
         "scope": "the whole training step (every kernel of forward, backward, clip and Adam; "
                  "the lf0 / mgc / bap / vuv branches on concurrent streams)",
         "bound": "mfma", "achieved": step_tf, "peak": peak_tf, "unit": "TFLOP/s",
-        "frac": step_tf / peak_tf, "traffic": _committed("r5_step_pmc.json",
+        "frac": step_tf / peak_tf, "traffic": _committed("r6_step_pmc.json",
                                                          "hbm_bytes_per_step"),
-        "traffic_source": "profiles/r5_step_pmc.json (rocprofv3 --pmc FETCH_SIZE x2 + "
+        "traffic_source": "profiles/r6_step_pmc.json (rocprofv3 --pmc FETCH_SIZE x2 + "
                           "WRITE_SIZE summed over one step's dispatches, separate passes; "
                           "committed, not this run)",
         "work": f"{TRAIN_FLOP_PER_FRAME / 1e6:.1f} MFLOP per main-track frame (GEMM / conv / "
@@ -1282,15 +1282,15 @@ def _gate_roofline(args, P, T, sec, sec_call, flops, gbytes):
                  frac=gbs / PEAK_HBM_GBS, tflops=tflops, mfma_frac=tflops / peak_tf)
     r.update(flops=flops, algorithmic_bytes=gbytes, launch_us=sec * 1e6,
              call_us_incl_operand_casts=sec_call * 1e6, traffic=_traffic(),
-             traffic_source="profiles/r5_gate_gemm_pmc.json (rocprofv3 --pmc FETCH_SIZE x2 + "
+             traffic_source="profiles/r6_gate_gemm_pmc.json (rocprofv3 --pmc FETCH_SIZE x2 + "
                             "WRITE_SIZE per dispatch, separate passes; not this run)")
     return r
 
 
 def _traffic():
     """HBM bytes per launch of the gate GEMM from the committed rocprofv3 PMC pass
-    (profiles/r5_gate_gemm_pmc.json, written by tools/round_profiles.sh), if any."""
-    return _committed("r5_gate_gemm_pmc.json", "hbm_bytes_per_launch")
+    (profiles/r6_gate_gemm_pmc.json, written by tools/round_profiles.sh), if any."""
+    return _committed("r6_gate_gemm_pmc.json", "hbm_bytes_per_launch")
 
 
 def _committed(name, key):

@@ -430,15 +430,20 @@ __global__ __launch_bounds__(NT) void lstm_coop_bwd_kernel(
       ob[i] = nb;
     }
     lds_barrier();
-    {  // publish dG: S sequences x 64 values, one 16-B sc1 store per thread < 8 S
-      if (tid < 8 * S) {
-        const f32x4 v = *(const f32x4*)&gs[(tid >> 3) * 64 + (tid & 7) * 8];
-        const int off = (((d * 2 + (q & 1)) * S + (tid >> 3)) * G4 + w * 64 + (tid & 7) * 8) * 2;
+    // publish dG (S sequences x 64 values, 8 S 16-B sc1 stores) from wave 0 alone, as the
+    // forward publishes h: only wave 0's memory operations gate the signal, and the other
+    // waves go on to their gate-gradient stores and next inputs without a second barrier
+    // (the earlier form stored from waves 0 and 1, waited vmcnt(0) in every wave -- their
+    // previous step's dg stores and next inputs included -- and signalled after a barrier)
+    if (wv == 0) {
+#pragma unroll
+      for (int k = lane; k < 8 * S; k += 64) {
+        const f32x4 v = *(const f32x4*)&gs[(k >> 3) * 64 + (k & 7) * 8];
+        const int off = (((d * 2 + (q & 1)) * S + (k >> 3)) * G4 + w * 64 + (k & 7) * 8) * 2;
         __builtin_amdgcn_raw_buffer_store_b128(v, xr, off, 0, CP_SC1);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
-      if (tid == 0) signal(hdr, d, q, c);
+      if (lane == 0) signal(hdr, d, q, c);
     }
 #pragma unroll
     for (int i = 0; i < NC; ++i)

@@ -1071,8 +1071,9 @@ def main():
         backend = dist.get_backend()
         # the default data-parallel schedule: the N = 1 line's HIP-graph replay with one
         # 94 MB all-reduce of the flat gradient (+ the 4-byte failure word) between the grads
-        # and update graphs (gloo rehearsal, 2 ranks on one GPU: 55.3 ms/step with a 22.0 ms
-        # host-side all-reduce, profiles/r5_bench_gloo2_graph.json).  --overlap-ddp: eager
+        # and update graphs (gloo rehearsal, 2 ranks on one GPU: 51.8 ms/step with a 20.4 ms
+        # host-side all-reduce, profiles/r6_bench_gloo2.json; round 5 55.3 / 22.0 ms,
+        # profiles/r5_bench_gloo2_graph.json).  --overlap-ddp: eager
         # steps whose bucketed all-reduce (lf0 / bap / V/UV at their branch end, the mgc
         # DiffNet before the mgc encoder's backward) overlaps the rest of the backward (same
         # rehearsal: 929 ms/step, 7 collectives, profiles/r5_bench_gloo2_overlap.json,

@@ -2274,11 +2274,12 @@ __device__ __forceinline__ void p8_wait() {
 // projections), the whole tile staged in two 128-row passes by all 8 waves; -1 -- every other
 // epilogue (epilogue_tile, 64-row chunks).  Instances per epilogue keep the other epilogues'
 // operand registers out of the K loop (the generic instance spills in its epilogue).
-constexpr int P8_PROBE_NODMA = 100 + EPI_NONE;
+constexpr int P8_PROBE_NODMA = 100 + EPI_NONE, P8_PROBE_NOMMA = 200 + EPI_NONE;
 template <int EPK, bool BAR2>
 __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs a) {
   constexpr bool GATE8 = EPK == EPI_GATE;
   constexpr bool NODMA = EPK == P8_PROBE_NODMA;  // measurement: the K loop without its loads
+  constexpr bool NOMMA = EPK == P8_PROBE_NOMMA;  // measurement: the loads (and LDS reads) alone
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
@@ -2403,7 +2404,8 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
     _Pragma("unroll") for (int h = 0; h < 2; ++h)                                          \
     _Pragma("unroll") for (int i = 0; i < 4; ++i)                                          \
     _Pragma("unroll") for (int j = 0; j < 2; ++j)                                          \
-      acc[(I0) + i][(J0) + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                   \
+      if (NOMMA) asm volatile("" ::"v"(xa[h][i]), "v"(B[h][j]));                           \
+      else acc[(I0) + i][(J0) + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(              \
           xa[h][i], B[h][j], acc[(I0) + i][(J0) + j], 0, 0, 0);                            \
     __builtin_amdgcn_s_setprio(0);                                                         \
     if (BAR2) __builtin_amdgcn_s_barrier();                                                \
@@ -2456,6 +2458,7 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
 #undef P8_ISSUE
 #undef P8_OFFS
   // every DMA was waited for (the last K-step's phase 1 waits vmcnt(0))
+  if constexpr (NOMMA) return;
   if constexpr (NODMA) {  // keep the MFMAs: the accumulators reach an (empty) use
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -4495,13 +4498,23 @@ static int g_p8_bar2 = 1;
 static int g_p8_nodma = 0;  // measurement (EPI_NONE launches only): skip the K loop's loads
 static const int P8_MIN_TILES = 128;
 
+// the lean plain epilogue's launches: fp32 Y = acc (+ bias), nothing else, 16-B aligned rows
+static bool p8_plain(const GemmArgs& a) {
+  return a.epi == EPI_PLAIN && !a.accum && !a.relu && !a.ybf && !a.csum && a.Y &&
+         a.N % 4 == 0 && a.ldy % 4 == 0 && ((uintptr_t)a.Y & 15) == 0 &&
+         (!a.bias || ((uintptr_t)a.bias & 3) == 0);
+}
+
 static bool use_p8(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B) {
   if (!g_p8 || a.csum || !a.vec_out || a.Npad % BNB || a.gbw_dma || a.as_dma) return false;
   for (int s = 0; s < nseg; ++s)  // 31-bit byte offsets into the operand resources
     if ((long long)B * segs[s].Tin * segs[s].ld >= (1ll << 30)) return false;
   const long long tiles = (long long)cdiv(a.M, BMB) * (a.Npad / BNB);
   if (a.epi == EPI_GATE) return g_big_tile && tiles >= BIG_MIN_TILES;
-  return g_p8 >= 2 && tiles >= P8_MIN_TILES;  // (EPI_NONE: the K loop alone, measurement)
+  if (tiles < P8_MIN_TILES || g_p8 < 2) return false;
+  // mode 3: the lean plain launches only (the generic epilogue's launches on the 128 x 128
+  // kernel); EPI_NONE: the K loop alone, measurement
+  return g_p8 == 2 || p8_plain(a) || a.epi == EPI_NONE;
 }
 
 // The 128 x 256 kernel (conv_gemm_b16_p8h_kernel) for the launches the 256 x 256 one leaves
@@ -4563,10 +4576,7 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     const dim3 grid_b(cdiv(a.M, BMB), Npad / BNB);
     const bool gate = a.gate8 && (a.epi == EPI_GATE || a.epi == EPI_GATE_TS);
     const size_t lb = (size_t)2 * P8_BUF;  // two K-steps of both images (128 KB)
-    // the lean plain epilogue: fp32 Y = acc (+ bias), nothing else, 16-B aligned rows
-    const bool plain = a.epi == EPI_PLAIN && !a.accum && !a.relu && !a.ybf && a.Y &&
-                       a.N % 4 == 0 && a.ldy % 4 == 0 && ((uintptr_t)a.Y & 15) == 0 &&
-                       (!a.bias || ((uintptr_t)a.bias & 3) == 0);
+    const bool plain = p8_plain(a);
     const size_t lbp = std::max<size_t>(lb, (size_t)128 * EPB * 4);  // two 128-row passes
 #define P8(E, B2, L)                                                                      \
   do {                                                                                    \
@@ -4576,7 +4586,9 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     if (ep != hipSuccess) return ENSVS_E_HIP;                                             \
     hipLaunchKernelGGL((conv_gemm_b16_p8_kernel<E, B2>), grid_b, dim3(NTHRB), (L), st, a); \
   } while (0)
-    if (a.epi == EPI_NONE && g_p8_nodma) {
+    if (a.epi == EPI_NONE && g_p8_nodma == 2) {
+      P8(P8_PROBE_NOMMA, true, lb);
+    } else if (a.epi == EPI_NONE && g_p8_nodma) {
       P8(P8_PROBE_NODMA, true, lb);
     } else if (g_p8_bar2) {
       if (gate) P8(EPI_GATE, true, lb);
@@ -4765,10 +4777,11 @@ ENSVS_API int ensvs_set_gbw_dma(int on) {
 }
 
 ENSVS_API int ensvs_set_p8(int mode) {
-  if ((mode & 3) > 2 || mode < 0 || mode > 15) return ENSVS_E_ARG;
+  if (mode < 0 || mode > 31) return ENSVS_E_ARG;
   g_p8 = mode & 3;
   g_p8_bar2 = (mode & 4) ? 1 : 0;  // bit 2: two barriers per phase, rows staggered
-  g_p8_nodma = (mode & 8) ? 1 : 0;  // bit 3: EPI_NONE probes without the K loop's loads
+  // bit 3: EPI_NONE probes without the K loop's loads; bit 4: without its MFMAs
+  g_p8_nodma = (mode & 16) ? 2 : ((mode & 8) ? 1 : 0);
   return ENSVS_OK;
 }
 

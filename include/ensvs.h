@@ -80,8 +80,8 @@ int ensvs_set_big_tile(int mode, int stages);
  * serves with >= 128 tiles of 256 x 256 (no column sums, not the LDS-DMA epilogues); + 4
  * (default 6): two barriers per phase with the wave rows staggered half a phase, so one wave of
  * each SIMD issues MFMAs while the other issues its LDS reads and DMAs; without it one barrier
- * per phase, rows in lockstep (A/B); + 8: measurement only -- EPI_NONE launches run the K
- * loop without its operand loads (what the loads cost). */
+ * per phase, rows in lockstep (A/B); + 8 / + 16: measurement only -- EPI_NONE launches run
+ * the K loop without its operand loads / without its MFMAs (what each costs). */
 int ensvs_set_p8(int mode);
 /* The 128 x 256 kernel (the four-phase pipeline on half-height tiles, two phases per K-step,
  * three K-step buffers) for launches the 256 x 256 kernel leaves with < 128 tiles: mode 0 off;

@@ -100,7 +100,7 @@ def none_case(name, M, N, spec):
     Y = torch.empty(M, N, device=dev)
     res = dict(case=name + " (K loop only)", M=M, N=N, K=sum(k * t for k, t, _ in spec))
     for tag, p8 in (("eng128", 0), ("p8", 2), ("p8stag", 6), ("p8_noload", 10),
-                    ("p8stag_noload", 14)):
+                    ("p8stag_noload", 14), ("p8stag_nomfma", 22)):
         _lib_call("ensvs_set_p8", p8)
         res[f"{tag}_us"] = round(timeit(lambda: K.gemm(segs, M // T, T, N, pb, Y, N,
                                                        epi=L.EPI_NONE)), 1)

@@ -4490,7 +4490,11 @@ static const int BIG_MIN_TILES = 192;
 // 13.47 / 13.47 ms vs 13.44 / 13.38 with hipBLASLt for the plain GEMMs and 13.61 / 13.63 with
 // them on the 128 x 128 kernel; SeparateF0 43.0 / 42.5 vs 42.9 / 42.9 and 43.9 / 43.9
 // (profiles/r6_blas_ab.txt, r6_blas_ab_sf0.txt).
-static int g_p8 = 2;
+// 3 (default): the gate GEMMs and the lean plain launches; the generic epilogue's launches stay on
+// the 128 x 128 kernel (its instance spills): Transformer leg 3.81 / 3.88 -> 3.65 / 3.75 ms,
+// main line 13.35 / 13.38 -> 13.32 / 13.36, SeparateF0 unchanged (profiles/r6_tf_p8_ab.txt,
+// r6_p8_mode7_ab.txt); 2: every launch of >= 128 tiles its epilogues serve
+static int g_p8 = 3;
 // 1: two barriers per phase with the wave rows staggered half a phase (default: 1-5 % faster
 // than one barrier per phase on every shape, bit-identical output; tools/p8_bench.py,
 // profiles/r6_p8_stagger.txt); 0: one barrier per phase, rows in lockstep

@@ -75,13 +75,13 @@ int ensvs_conv_gemm(const ensvs_conv_seg* segs, int nseg, int B, int Tout, int N
  * Defaults: mode 2, 5 stages. */
 int ensvs_set_big_tile(int mode, int stages);
 /* The four-phase 256 x 256 kernel (counted LDS-DMA pipeline, four half-tiles in flight across
- * every barrier; same accumulation order, bitwise equal): mode 0 off; 1 for the launches the
- * 256 x 256 kernel takes (gate GEMMs); 2 (default) also for every other launch its LDS-staged epilogue
- * serves with >= 128 tiles of 256 x 256 (no column sums, not the LDS-DMA epilogues); + 4
- * (default 6): two barriers per phase with the wave rows staggered half a phase, so one wave of
- * each SIMD issues MFMAs while the other issues its LDS reads and DMAs; without it one barrier
- * per phase, rows in lockstep (A/B); + 8 / + 16: measurement only -- EPI_NONE launches run
- * the K loop without its operand loads / without its MFMAs (what each costs). */
+ * every barrier; same accumulation order, bitwise equal): mode & 3 -- 0 off; 1 for the launches
+ * the 256 x 256 kernel takes (gate GEMMs); 2 also for every other launch its LDS-staged
+ * epilogue serves with >= 128 tiles of 256 x 256 (no column sums, not the LDS-DMA epilogues);
+ * 3 the gate GEMMs and the lean plain launches only; + 4: two barriers per phase with the wave
+ * rows staggered half a phase (without: one barrier per phase, rows in lockstep); default 7;
+ * + 8 / + 16: measurement only -- EPI_NONE launches run the K loop without its operand loads /
+ * without its MFMAs (what each costs). */
 int ensvs_set_p8(int mode);
 /* The 128 x 256 kernel (the four-phase pipeline on half-height tiles, two phases per K-step,
  * three K-step buffers) for launches the 256 x 256 kernel leaves with < 128 tiles: mode 0 off;

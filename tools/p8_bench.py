@@ -75,7 +75,7 @@ def case(name, M, N, spec, epi=L.EPI_PLAIN, bias=True, accum=False):
         us = timeit(fn)
         res[f"{tag}_us"] = round(us, 1)
         res[f"{tag}_tflops"] = round(flops / us / 1e6, 1)
-    _lib_call("ensvs_set_p8", 6)
+    _lib_call("ensvs_set_p8", 7)
     a = torch.randn(M, Kt, device=dev, dtype=torch.bfloat16)
     b = torch.randn(Kt, N, device=dev, dtype=torch.bfloat16)
     us = timeit(lambda: torch.matmul(a, b))
@@ -104,7 +104,7 @@ def none_case(name, M, N, spec):
         _lib_call("ensvs_set_p8", p8)
         res[f"{tag}_us"] = round(timeit(lambda: K.gemm(segs, M // T, T, N, pb, Y, N,
                                                        epi=L.EPI_NONE)), 1)
-    _lib_call("ensvs_set_p8", 6)
+    _lib_call("ensvs_set_p8", 7)
     print(json.dumps(res), flush=True)
 
 

@@ -2505,6 +2505,38 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8_kernel(const GemmArgs 
     return;
   }
   EpiPre pre;
+  if constexpr (EPK == -1) {
+    // every other epilogue: the tile staged in two passes of both wave rows' halves (T rows
+    // [64 wr, 64 wr + 64) = tile rows 128 wr + 64 pass + (0..63)), so at most half of the
+    // accumulators stay live across an epilogue (staging one wave row's quarter per 64-row
+    // chunk kept all 128 live in the other row's waves, and the instance spilled); each 64-row
+    // block runs epilogue_tile with its own operand prefetch (epi_pre)
+    lds_sync();
+#define STAGE_P(H)                                                                        \
+    _Pragma("unroll") for (int mt2 = 0; mt2 < 4; ++mt2)                                   \
+    _Pragma("unroll") for (int nt = 0; nt < 4; ++nt)                                      \
+    _Pragma("unroll") for (int r = 0; r < 4; ++r)                                         \
+        T[(wr * 64 + mt2 * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] = \
+            bias_st ? acc[(H) * 4 + mt2][nt][r] + bs[nt] : acc[(H) * 4 + mt2][nt][r]
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass) {
+        STAGE_P(1);
+      } else {
+        STAGE_P(0);
+      }
+      lds_sync();
+#pragma unroll 1
+      for (int blk = 0; blk < 2; ++blk) {
+        const int mb = m0 + blk * 128 + pass * 64;
+        epi_pre<BNB, NTHRB>(a, mb, n0, tid, 0, pre);
+        epilogue_tile<CHR, BNB, NTHRB, EPB, true>(a, T + blk * 64 * EPB, mb, n0, tid, true, pre);
+      }
+      lds_sync();
+    }
+#undef STAGE_P
+    return;
+  }
   if (!GATE8) epi_pre<BNB, NTHRB>(a, m0, n0, tid, 0, pre);
   lds_sync();
 #define STAGE_HALF(H)                                                                     \
@@ -4490,11 +4522,14 @@ static const int BIG_MIN_TILES = 192;
 // 13.47 / 13.47 ms vs 13.44 / 13.38 with hipBLASLt for the plain GEMMs and 13.61 / 13.63 with
 // them on the 128 x 128 kernel; SeparateF0 43.0 / 42.5 vs 42.9 / 42.9 and 43.9 / 43.9
 // (profiles/r6_blas_ab.txt, r6_blas_ab_sf0.txt).
-// 3 (default): the gate GEMMs and the lean plain launches; the generic epilogue's launches stay on
-// the 128 x 128 kernel (its instance spills): Transformer leg 3.81 / 3.88 -> 3.65 / 3.75 ms,
-// main line 13.35 / 13.38 -> 13.32 / 13.36, SeparateF0 unchanged (profiles/r6_tf_p8_ab.txt,
-// r6_p8_mode7_ab.txt); 2: every launch of >= 128 tiles its epilogues serve
-static int g_p8 = 3;
+// 2 (default): every launch of >= 128 tiles its epilogues serve.  The generic instance stages
+// the tile in two passes (no spills): relu + bf16-copy and ReLU-mask launches 77 / 86 / 127 us
+// vs the 128 x 128 kernel's 87 / 107 / 170, main line 13.33 / 13.33 vs 13.41 / 13.38 ms with
+// them on the 128 x 128 kernel (mode 3), Transformer leg 3.74 vs 3.78 (profiles/
+// r6_p8_generic_bench.txt, r6_p8_generic_ab.txt; with the spilling one-pass instance mode 3 was
+// the faster: r6_tf_p8_ab.txt, r6_p8_mode7_ab.txt).  3: the gate GEMMs and the lean plain
+// launches only.
+static int g_p8 = 2;
 // 1: two barriers per phase with the wave rows staggered half a phase (default: 1-5 % faster
 // than one barrier per phase on every shape, bit-identical output; tools/p8_bench.py,
 // profiles/r6_p8_stagger.txt); 0: one barrier per phase, rows in lockstep
@@ -4597,11 +4632,11 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     } else if (g_p8_bar2) {
       if (gate) P8(EPI_GATE, true, lb);
       else if (plain) P8(EPI_PLAIN, true, lbp);
-      else P8(-1, true, lb);
+      else P8(-1, true, lbp);
     } else {
       if (gate) P8(EPI_GATE, false, lb);
       else if (plain) P8(EPI_PLAIN, false, lbp);
-      else P8(-1, false, lb);
+      else P8(-1, false, lbp);
     }
 #undef P8
     ENSVS_CHECK_LAUNCH();

@@ -79,7 +79,7 @@ int ensvs_set_big_tile(int mode, int stages);
  * the 256 x 256 kernel takes (gate GEMMs); 2 also for every other launch its LDS-staged
  * epilogue serves with >= 128 tiles of 256 x 256 (no column sums, not the LDS-DMA epilogues);
  * 3 the gate GEMMs and the lean plain launches only; + 4: two barriers per phase with the wave
- * rows staggered half a phase (without: one barrier per phase, rows in lockstep); default 7;
+ * rows staggered half a phase (without: one barrier per phase, rows in lockstep); default 6;
  * + 8 / + 16: measurement only -- EPI_NONE launches run the K loop without its operand loads /
  * without its MFMAs (what each costs). */
 int ensvs_set_p8(int mode);

@@ -193,6 +193,6 @@ def test_p8_barrier_forms_bitwise(N, specs, epi, B, T):
             outs.append(run())
             torch.cuda.synchronize()
     finally:
-        L.call("ensvs_set_p8", 7)
+        L.call("ensvs_set_p8", 6)
     _assert_same(outs[0], outs[1])
     _assert_same(outs[0], outs[2])

@@ -30,7 +30,7 @@ def timeit(fn, iters=ITERS):
     return s.elapsed_time(e) / iters * 1e3  # us
 
 
-def case(name, M, N, spec, epi=L.EPI_PLAIN, bias=True, accum=False):
+def case(name, M, N, spec, epi=L.EPI_PLAIN, bias=True, accum=False, relu_bf16=False):
     """spec: list of (K, taps, dil) bf16 segments."""
     g = torch.Generator(device=dev).manual_seed(1)
     pb = K.PackedBuffer(L.DT_BF16)
@@ -52,6 +52,17 @@ def case(name, M, N, spec, epi=L.EPI_PLAIN, bias=True, accum=False):
         def fn():
             K.gemm(segs, M // T, T, N, pb, outs[0], C, epi=epi, aux0=outs[1], ld0=N, C=C,
                    ybf=outs[2], ybf_ld=C, keep_y=False, bias=bv)
+    elif epi == L.EPI_RELU_MASK:
+        outs = [torch.zeros(M, N, device=dev)]
+        mask = torch.randn(M, N, device=dev, generator=g)
+
+        def fn():
+            K.gemm(segs, M // T, T, N, pb, outs[0], N, epi=epi, aux1=mask, ld1=N)
+    elif relu_bf16:
+        outs = [torch.zeros(M, N, device=dev), torch.zeros(M, N, device=dev, dtype=torch.bfloat16)]
+
+        def fn():
+            K.gemm(segs, M // T, T, N, pb, outs[0], N, bias=bv, relu=True, ybf=outs[1], ybf_ld=N)
     else:
         outs = [torch.zeros(M, N, device=dev)]
 
@@ -60,7 +71,7 @@ def case(name, M, N, spec, epi=L.EPI_PLAIN, bias=True, accum=False):
     res = dict(case=name, M=M, N=N, K=Kt)
     flops = 2.0 * M * N * Kt
     ref = None
-    for tag, p8 in (("eng128", 0), ("p8", 2), ("p8stag", 6)):
+    for tag, p8 in (("eng128", 0), ("p8", 2), ("p8stag", 6), ("default", 7)):
         _lib_call("ensvs_set_p8", p8)
         for o in outs:
             o.zero_()
@@ -75,7 +86,7 @@ def case(name, M, N, spec, epi=L.EPI_PLAIN, bias=True, accum=False):
         us = timeit(fn)
         res[f"{tag}_us"] = round(us, 1)
         res[f"{tag}_tflops"] = round(flops / us / 1e6, 1)
-    _lib_call("ensvs_set_p8", 7)
+    _lib_call("ensvs_set_p8", 6)
     a = torch.randn(M, Kt, device=dev, dtype=torch.bfloat16)
     b = torch.randn(Kt, N, device=dev, dtype=torch.bfloat16)
     us = timeit(lambda: torch.matmul(a, b))
@@ -104,7 +115,7 @@ def none_case(name, M, N, spec):
         _lib_call("ensvs_set_p8", p8)
         res[f"{tag}_us"] = round(timeit(lambda: K.gemm(segs, M // T, T, N, pb, Y, N,
                                                        epi=L.EPI_NONE)), 1)
-    _lib_call("ensvs_set_p8", 7)
+    _lib_call("ensvs_set_p8", 6)
     print(json.dumps(res), flush=True)
 
 
@@ -120,5 +131,9 @@ if __name__ == "__main__":
     case("mgc lstm proj 512->1024", M, 1024, [(512, 1, 1)])
     case("mgc enc conv k7 512->512", M, 512, [(512, 7, 1)])
     case("diffnet res 256->512", M, 512, [(256, 1, 1)])
+    case("ff relu + bf16 copy 512->1024 (generic)", M, 1024, [(512, 1, 1)], relu_bf16=True)
+    case("conv relu + bf16 copy k5 512->512 (generic)", M, 512, [(512, 5, 1)], relu_bf16=True)
+    case("relu-mask dgrad 1024->1024 (generic)", M, 1024, [(1024, 1, 1)], epi=L.EPI_RELU_MASK,
+         bias=False)
     none_case("enc l0 proj 512->4096", M, 4096, [(512, 1, 1)])
     none_case("enc dgrad 2x2048->1024", M, 1024, [(2048, 1, 1), (2048, 1, 1)])

@@ -66,7 +66,7 @@ SIGNATURES = {
                                   c_int, c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_vp,
                                   c_ll, c_vp],
     "ensvs_set_big_tile": [c_int, c_int],
-    "ensvs_set_p8": [c_int], "ensvs_set_p8h": [c_int],
+    "ensvs_set_p8": [c_int], "ensvs_set_p8_min_tiles": [c_int], "ensvs_set_p8h": [c_int],
     "ensvs_set_dual_small": [c_int],
     "ensvs_set_gbw_dma": [c_int],
     "ensvs_set_wgrad_big": [c_int],

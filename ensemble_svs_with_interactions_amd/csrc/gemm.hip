@@ -4536,6 +4536,9 @@ static int g_p8 = 2;
 static int g_p8_bar2 = 1;
 static int g_p8_nodma = 0;  // measurement (EPI_NONE launches only): skip the K loop's loads
 static const int P8_MIN_TILES = 128;
+// the four-phase kernel's smallest launch (tiles of 256 x 256) for its non-gate epilogues
+// (ensvs_set_p8_min_tiles; A/B)
+static int g_p8_min_tiles = P8_MIN_TILES;
 
 // the lean plain epilogue's launches: fp32 Y = acc (+ bias), nothing else, 16-B aligned rows
 static bool p8_plain(const GemmArgs& a) {
@@ -4550,7 +4553,7 @@ static bool use_p8(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int 
     if ((long long)B * segs[s].Tin * segs[s].ld >= (1ll << 30)) return false;
   const long long tiles = (long long)cdiv(a.M, BMB) * (a.Npad / BNB);
   if (a.epi == EPI_GATE) return g_big_tile && tiles >= BIG_MIN_TILES;
-  if (tiles < P8_MIN_TILES || g_p8 < 2) return false;
+  if (tiles < g_p8_min_tiles || g_p8 < 2) return false;
   // mode 3: the lean plain launches only (the generic epilogue's launches on the 128 x 128
   // kernel); EPI_NONE: the K loop alone, measurement
   return g_p8 == 2 || p8_plain(a) || a.epi == EPI_NONE;
@@ -4821,6 +4824,12 @@ ENSVS_API int ensvs_set_p8(int mode) {
   g_p8_bar2 = (mode & 4) ? 1 : 0;  // bit 2: two barriers per phase, rows staggered
   // bit 3: EPI_NONE probes without the K loop's loads; bit 4: without its MFMAs
   g_p8_nodma = (mode & 16) ? 2 : ((mode & 8) ? 1 : 0);
+  return ENSVS_OK;
+}
+
+ENSVS_API int ensvs_set_p8_min_tiles(int n) {
+  if (n < 1) return ENSVS_E_ARG;
+  g_p8_min_tiles = n;
   return ENSVS_OK;
 }
 

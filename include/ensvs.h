@@ -83,6 +83,9 @@ int ensvs_set_big_tile(int mode, int stages);
  * + 8 / + 16: measurement only -- EPI_NONE launches run the K loop without its operand loads /
  * without its MFMAs (what each costs). */
 int ensvs_set_p8(int mode);
+/* The four-phase kernel's smallest launch for its non-gate epilogues, in tiles of 256 x 256
+ * (default 128; A/B). */
+int ensvs_set_p8_min_tiles(int n);
 /* The 128 x 256 kernel (the four-phase pipeline on half-height tiles, two phases per K-step,
  * three K-step buffers) for launches the 256 x 256 kernel leaves with < 128 tiles: mode 0 off;
  * 1 (default) the lean plain epilogue over >= 32 K-steps (where it beats the 128 x 128

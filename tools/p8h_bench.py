@@ -41,11 +41,17 @@ def pack(ws):
     return pb, refs
 
 
+ARMS = (("eng128", "ensvs_set_p8h", 0), ("p8h", "ensvs_set_p8h", 2),
+        ("p8_120tiles", "ensvs_set_p8_min_tiles", 96))
+
+
 def run_case(name, fn, outs, flops):
     res = dict(case=name)
     ref = None
-    for tag, on in (("eng128", 0), ("p8h", 2)):
-        L.call("ensvs_set_p8h", on)
+    for tag, sw, on in ARMS:
+        L.call("ensvs_set_p8h", 0)
+        L.call("ensvs_set_p8_min_tiles", 128)
+        L.call(sw, on)
         for o in outs:
             o.zero_()
         fn()
@@ -60,6 +66,7 @@ def run_case(name, fn, outs, flops):
         res[f"{tag}_us"] = round(us, 1)
         res[f"{tag}_tflops"] = round(flops / us / 1e6, 1)
     L.call("ensvs_set_p8h", 1)
+    L.call("ensvs_set_p8_min_tiles", 128)
     print(json.dumps(res), flush=True)
 
 
@@ -111,6 +118,13 @@ def main():
     run_case("skip sum (K = 5120, PLAIN)", lambda: K.gemm(
         [K.Seg(zall, LL * C, LL * C, r4, T)], B, T, C, pb3, S, C, bias=bias), [S],
         2.0 * M * C * LL * C)
+    # the skip projection with ReLU and its bf16 copy (K = 256), the dss GEMM (plain, K = 256)
+    p1, p1b = torch.empty(M, C, device=dev), torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    run_case("skip relu + bf16 copy (K = 256)", lambda: K.gemm(
+        [K.Seg(zb, C, C, r3, T)], B, T, C, pb3, p1, C, relu=True, ybf=p1b, ybf_ld=C, bias=bias),
+        [p1, p1b], 2.0 * M * C * C)
+    run_case("dss plain (K = 256)", lambda: K.gemm(
+        [K.Seg(zb, C, C, r3, T)], B, T, C, pb3, p1, C), [p1], 2.0 * M * C * C)
     # the conditioner input gradient: K = L 2C over every block's d(pre)
     pb4, (r5,) = pack([torch.randn(C, LL * 2 * C, 1, device=dev) * 0.01])
     run_case("cond dgrad (K = 10240, PLAIN)", lambda: K.gemm(

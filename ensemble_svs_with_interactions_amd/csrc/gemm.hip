@@ -4572,6 +4572,10 @@ static bool use_p8(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int 
 // 123.6 us; the conditioner input gradient K = 10 240).  Every epilogue stays available
 // (ensvs_set_p8h(2), bitwise tests).  0: off; 1: long-K plain launches; 2: every launch.
 static int g_p8h = 1;
+// the lean plain launches it takes: >= this many K-steps.  1 (default): the short-K ones win
+// too -- the DiffNet's d(skip) GEMM (K = 256) 14.4 vs 20.6 us on the 128 x 128 kernel (16.8 on
+// the 256 x 256 kernel at 120 tiles; r6_p8_n256_bench.txt); 32 was round 6's first rule
+static int g_p8h_min_ksteps = 1;
 
 static bool use_p8h(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B) {
   if (!g_p8h || !a.vec_out || a.Npad % BNB) return false;
@@ -4582,7 +4586,8 @@ static bool use_p8h(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int
   if (g_p8h >= 2) return true;
   int nit = 0;
   for (int s = 0; s < nseg; ++s) nit += cdiv(segs[s].K, BK2) * segs[s].taps;
-  return a.epi == EPI_PLAIN && !a.accum && !a.relu && !a.ybf && !a.csum && nit >= 32;
+  return a.epi == EPI_PLAIN && !a.accum && !a.relu && !a.ybf && !a.csum &&
+         nit >= g_p8h_min_ksteps;
 }
 
 static bool use_big_tile(const GemmArgs& a) {
@@ -4834,8 +4839,9 @@ ENSVS_API int ensvs_set_p8_min_tiles(int n) {
 }
 
 ENSVS_API int ensvs_set_p8h(int mode) {
-  if (mode < 0 || mode > 2) return ENSVS_E_ARG;
-  g_p8h = mode;
+  if (mode < 0 || mode > 2 + 4 * 64) return ENSVS_E_ARG;
+  g_p8h = mode & 3;
+  if (mode >> 2) g_p8h_min_ksteps = mode >> 2;  // + 4 k: lean plain launches of >= k K-steps
   return ENSVS_OK;
 }
 

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 HB=$!
 trap "kill $HB" EXIT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 python -u tools/p8h_bench.py > gpurun_out/p8_120_bench.txt 2>&1 || exit 4
-grep -v amdgpu gpurun_out/p8_120_bench.txt
-timeout -k 10 550 python -u tools/flag_ab.py "ensvs_set_p8_min_tiles=128" "ensvs_set_p8_min_tiles=96" > gpurun_out/ab_p8_120.txt 2>&1
-rc=$?; cat gpurun_out/ab_p8_120.txt; exit $rc
+timeout -k 10 300 python -u tools/p8h_bench.py > gpurun_out/p8h_short_bench.txt 2>&1 || exit 4
+grep -v amdgpu gpurun_out/p8h_short_bench.txt
+timeout -k 10 550 python -u tools/flag_ab.py "ensvs_set_p8h=129" "ensvs_set_p8h=1" > gpurun_out/ab_p8h_short.txt 2>&1
+rc=$?; cat gpurun_out/ab_p8h_short.txt; exit $rc

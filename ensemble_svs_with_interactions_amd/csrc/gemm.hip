@@ -2626,6 +2626,8 @@ template <unsigned MASK>
 __device__ __forceinline__ void p8h_epilogue(const GemmArgs& a, const float* T, float* X, int m0,
                                              int n0, int tid) {
   auto ep = [&](int e) { return ((MASK >> e) & 1u) && a.epi == e; };
+  // rows whose operands are loaded together, one batch ahead (the all-epilogue instance: 2)
+  constexpr int EBH = MASK == ~0u ? 2 : 8;
   const int cq = tid & 63, g = tid >> 6, col = n0 + cq * 4;
   const int ne = min(4, a.N - col);
   f32x4 bv = {0.f, 0.f, 0.f, 0.f};
@@ -2638,41 +2640,53 @@ __device__ __forceinline__ void p8h_epilogue(const GemmArgs& a, const float* T, 
                      ep(EPI_GATE_BWD);
   const bool want2 = (ep(EPI_RELU_MASK) && a.accum) || ep(EPI_GATE_BWD);
   const bool wl = ne == 4 && (want1 || want2);
+  // the bf16 copy's per-sequence add (PLAIN / ADDSCALE), loaded with the batch
+  const bool wrr = ne == 4 && a.ybf && a.ybf_radd && (ep(EPI_PLAIN) || ep(EPI_ADDSCALE));
   f32x4 cs0 = {0.f, 0.f, 0.f, 0.f}, cs1 = {0.f, 0.f, 0.f, 0.f};
-  f32x4 p1 = cs0, p2 = cs0, q1 = cs0, q2 = cs0;
-  if (wl) gen_load(a, m0 + g, col, want2, p1, p2);
+  f32x4 p1[EBH], p2[EBH], pr[EBH], q1[EBH], q2[EBH], qr[EBH];
+  auto load_batch = [&](int kb, f32x4 (&x1)[EBH], f32x4 (&x2)[EBH], f32x4 (&xr)[EBH]) {
+#pragma unroll
+    for (int k = 0; k < EBH; ++k) {
+      const int m = m0 + g + 8 * (kb + k);
+      if (wl) gen_load(a, m, col, want2, x1[k], x2[k]);
+      if (wrr && m < a.M) xr[k] = ld4(a.ybf_radd + (long long)(m / a.Tout) * a.ybf_radd_ld + col);
+    }
+  };
+  load_batch(0, p1, p2, pr);
 #pragma unroll 1
-  for (int k = 0; k < BMH / 8; ++k) {
-    const int row = g + 8 * k;
-    const int m = m0 + row;
-    if (wl && k + 1 < BMH / 8) gen_load(a, m + 8, col, want2, q1, q2);
-    if (m < a.M && ne > 0) {
+  for (int kb = 0; kb < BMH / 8; kb += EBH) {
+    if (kb + EBH < BMH / 8) load_batch(kb + EBH, q1, q2, qr);
+#pragma unroll
+    for (int k = 0; k < EBH; ++k) {
+      const int row = g + 8 * (kb + k);
+      const int m = m0 + row;
+      if (m >= a.M || ne <= 0) continue;
       f32x4 v = ld4(T + row * EPB + cq * 4);
       if (a.csum && a.epi != EPI_GATE_BWD) cs0 += v;
       if (a.bias) v += bv;
       float* y = a.Y + (long long)m * a.ldy + col;
       if (ne == 4) {
         if (ep(EPI_PLAIN)) {
-          if (a.accum) v += p1;
+          if (a.accum) v += p1[k];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             if (a.relu == 1) v[e] = fmaxf(v[e], 0.f);
             else if (a.relu == 2) v[e] = sigmoidf_(v[e]);
           }
           st4(y, v);
-          shadow4(a, m, col, v);
+          shadow4r(a, m, col, v, pr[k]);
         } else if (ep(EPI_ADDSCALE)) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            v[e] = __builtin_fmaf(a.alpha, p1[e], v[e]);
+            v[e] = __builtin_fmaf(a.alpha, p1[k][e], v[e]);
             v[e] = a.relu == 1 ? fmaxf(v[e], 0.f) : v[e];
           }
           st4(y, v);
-          shadow4(a, m, col, v);
+          shadow4r(a, m, col, v, pr[k]);
         } else if (ep(EPI_RELU_MASK)) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = p1[e] > 0.f ? v[e] : 0.f;
-          if (a.accum) v += p2;
+          for (int e = 0; e < 4; ++e) v[e] = p1[k][e] > 0.f ? v[e] : 0.f;
+          if (a.accum) v += p2[k];
           st4(y, v);
           shadow4(a, m, col, v);
         } else if (ep(EPI_GATE_BWD)) {
@@ -2680,7 +2694,7 @@ __device__ __forceinline__ void p8h_epilogue(const GemmArgs& a, const float* T, 
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float t0, t1;
-            gate_bwd_(v[e], p1[e], p2[e], t0, t1);
+            gate_bwd_(v[e], p1[k][e], p2[k][e], t0, t1);
             dg[e] = t0;
             df[e] = t1;
           }
@@ -2718,8 +2732,12 @@ __device__ __forceinline__ void p8h_epilogue(const GemmArgs& a, const float* T, 
         }
       }
     }
-    p1 = q1;
-    p2 = q2;
+#pragma unroll
+    for (int k = 0; k < EBH; ++k) {
+      p1[k] = q1[k];
+      p2[k] = q2[k];
+      pr[k] = qr[k];
+    }
   }
   if (a.csum) {  // uniform: every thread reaches the barrier
     *(f32x4*)(X + g * 2 * BNB + cq * 4) = cs0;
@@ -2942,7 +2960,9 @@ __global__ __launch_bounds__(NTHRB) void conv_gemm_b16_p8h_kernel(const GemmArgs
           T[(wr * 64 + mt * 16 + (lane >> 4) * 4 + r) * EPB + wc * 64 + nt * 16 + (lane & 15)] =
               acc[mt][nt][r];
     lds_sync();
-    constexpr unsigned MASK = EPK < 0 ? ~0u : (1u << EPK);
+    // EPK = 16 + e: epilogue e through p8h_epilogue (PLAIN with accumulate / activation /
+    // copies); EPK = e (not PLAIN): that epilogue alone; -1: every epilogue
+    constexpr unsigned MASK = EPK < 0 ? ~0u : (1u << (EPK >= 16 ? EPK - 16 : EPK));
     p8h_epilogue<MASK>(a, T, T + BMH * EPB, m0, n0, tid);
   }
 }
@@ -4583,11 +4603,18 @@ static bool use_p8h(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int
   for (int s = 0; s < nseg; ++s)  // 31-bit byte offsets into the operand resources
     if ((long long)B * segs[s].Tin * segs[s].ld >= (1ll << 30)) return false;
   if ((long long)cdiv(a.M, BMH) * (a.Npad / BNB) < P8_MIN_TILES) return false;
-  if (g_p8h >= 2) return true;
+  if (g_p8h == 2) return true;
   int nit = 0;
   for (int s = 0; s < nseg; ++s) nit += cdiv(segs[s].K, BK2) * segs[s].taps;
-  return a.epi == EPI_PLAIN && !a.accum && !a.relu && !a.ybf && !a.csum &&
-         nit >= g_p8h_min_ksteps;
+  if (nit < g_p8h_min_ksteps) return false;
+  const bool lean = a.epi == EPI_PLAIN && !a.accum && !a.relu && !a.ybf && !a.csum;
+  if (g_p8h == 3) return lean;
+  // mode 1: also the PLAIN epilogues with operands / copies / column sums and ADDSCALE without
+  // column sums, whose operands the epilogue prefetches 8 rows ahead (skip ReLU + bf16 copy
+  // 20.0 vs 23.1 us, first dilated dgrad with tile sums 45.8 vs 47.3, residual ADDSCALE 21.1
+  // vs 21.7); the gate backward and the ADDSCALE dgrad with tile sums stay on the 128 x 128
+  // kernel's LDS-DMA epilogues (38.7 vs 25.6, 46.6 vs 39.2 us; profiles/r6_p8h_epi_bench.txt)
+  return a.epi == EPI_PLAIN || (a.epi == EPI_ADDSCALE && !a.csum);
 }
 
 static bool use_big_tile(const GemmArgs& a) {
@@ -4665,6 +4692,7 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     hipLaunchKernelGGL((conv_gemm_b16_p8h_kernel<E>), grid_h, dim3(NTHRB), lh, st, a);    \
   } while (0)
     if (plain) P8H(EPI_PLAIN);
+    else if (a.epi == EPI_PLAIN) P8H(16 + EPI_PLAIN);
     else if (a.epi == EPI_ADDSCALE) P8H(EPI_ADDSCALE);
     else if (a.epi == EPI_GATE_BWD) P8H(EPI_GATE_BWD);
     else P8H(-1);
@@ -4839,7 +4867,7 @@ ENSVS_API int ensvs_set_p8_min_tiles(int n) {
 }
 
 ENSVS_API int ensvs_set_p8h(int mode) {
-  if (mode < 0 || mode > 2 + 4 * 64) return ENSVS_E_ARG;
+  if (mode < 0 || mode > 3 + 4 * 64) return ENSVS_E_ARG;
   g_p8h = mode & 3;
   if (mode >> 2) g_p8h_min_ksteps = mode >> 2;  // + 4 k: lean plain launches of >= k K-steps
   return ENSVS_OK;

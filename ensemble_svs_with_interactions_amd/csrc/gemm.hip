@@ -4612,9 +4612,11 @@ static bool use_p8h(const GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int
   // mode 1: also the PLAIN epilogues with operands / copies / column sums and ADDSCALE without
   // column sums, whose operands the epilogue prefetches 8 rows ahead (skip ReLU + bf16 copy
   // 20.0 vs 23.1 us, first dilated dgrad with tile sums 45.8 vs 47.3, residual ADDSCALE 21.1
-  // vs 21.7); the gate backward and the ADDSCALE dgrad with tile sums stay on the 128 x 128
-  // kernel's LDS-DMA epilogues (38.7 vs 25.6, 46.6 vs 39.2 us; profiles/r6_p8h_epi_bench.txt)
-  return a.epi == EPI_PLAIN || (a.epi == EPI_ADDSCALE && !a.csum);
+  // vs 21.7) and RELU_MASK without column sums (19.0 vs 24.0 us,
+  // profiles/r6_p8h_relumask_bench.txt); the gate backward and the ADDSCALE dgrad with tile
+  // sums stay on the 128 x 128 kernel's LDS-DMA epilogues (38.7 vs 25.6, 46.6 vs 39.2 us;
+  // profiles/r6_p8h_epi_bench.txt)
+  return a.epi == EPI_PLAIN || ((a.epi == EPI_ADDSCALE || a.epi == EPI_RELU_MASK) && !a.csum);
 }
 
 static bool use_big_tile(const GemmArgs& a) {
@@ -4695,6 +4697,7 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
     else if (a.epi == EPI_PLAIN) P8H(16 + EPI_PLAIN);
     else if (a.epi == EPI_ADDSCALE) P8H(EPI_ADDSCALE);
     else if (a.epi == EPI_GATE_BWD) P8H(EPI_GATE_BWD);
+    else if (a.epi == EPI_RELU_MASK) P8H(EPI_RELU_MASK);
     else P8H(-1);
 #undef P8H
     ENSVS_CHECK_LAUNCH();

@@ -125,6 +125,11 @@ def main():
         [p1, p1b], 2.0 * M * C * C)
     run_case("dss plain (K = 256)", lambda: K.gemm(
         [K.Seg(zb, C, C, r3, T)], B, T, C, pb3, p1, C), [p1], 2.0 * M * C * C)
+    # the output projection's input gradient through the skip projection's ReLU (RELU_MASK)
+    mask = torch.randn(M, C, device=dev)
+    run_case("relu-mask dgrad (K = 256)", lambda: K.gemm(
+        [K.Seg(zb, C, C, r3, T)], B, T, C, pb3, p1, C, epi=L.EPI_RELU_MASK, aux1=mask, ld1=C),
+        [p1], 2.0 * M * C * C)
     # the conditioner input gradient: K = L 2C over every block's d(pre)
     pb4, (r5,) = pack([torch.randn(C, LL * 2 * C, 1, device=dev) * 0.01])
     run_case("cond dgrad (K = 10240, PLAIN)", lambda: K.gemm(

@@ -88,8 +88,8 @@ int ensvs_set_p8(int mode);
 int ensvs_set_p8_min_tiles(int n);
 /* The 128 x 256 kernel (the four-phase pipeline on half-height tiles, two phases per K-step,
  * three K-step buffers) for launches the 256 x 256 kernel leaves with < 128 tiles: mode 0 off;
- * 1 (default) the plain epilogues (lean or with operands, copies, column sums) and ADDSCALE
- * without column sums (where it beats the 128 x 128 kernel); 2 every launch but the pair
+ * 1 (default) the plain epilogues (lean or with operands, copies, column sums) and ADDSCALE /
+ * RELU_MASK without column sums (where it beats the 128 x 128 kernel); 2 every launch but the pair
  * epilogues (gate, res/skip), column sums included (A/B, tests); 3 the lean plain launches only;
  * + 4 k: modes 1 / 3 only for launches of >= k K-steps (default k = 1).  Same accumulation and
  * column-sum order: bitwise equal. */

@@ -4742,7 +4742,8 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
   // also takes N <= 64 at any M (a 128-wide tile would leave half its columns and half the
   // epilogue threads idle: the uSFGAN block output GEMMs, 480 000 x 64)
   if (g_small && !has_pd && !a.csum && a.vec_out && Npad % BNS == 0 &&
-      ((long long)grid.x * grid.y < 128 || a.N <= BNS)) {
+      ((long long)grid.x * grid.y < 128 || a.N <= BNS ||
+       (g_small == 2 && Npad <= 2 * BNS && (long long)grid.x * grid.y < 256))) {
     constexpr int sms = SMALL_STAGES;
     const dim3 gs(cdiv(a.M, BMS), a.N <= BNS ? 1 : Npad / BNS);
 #define SMALL(S)                                                                          \
@@ -4835,7 +4836,7 @@ static int launch_b16(GemmArgs& a, const ensvs_conv_seg* segs, int nseg, int B, 
 }
 
 ENSVS_API int ensvs_set_small(int on) {
-  g_small = on ? 1 : 0;
+  g_small = on == 2 ? 2 : on ? 1 : 0;
   return ENSVS_OK;
 }
 

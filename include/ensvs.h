@@ -109,7 +109,8 @@ int ensvs_set_wgrad_big(int on);
 /* Launches of fewer than 128 output tiles of 128 x 128 (small M: the 2 000-frame reverse-
  * diffusion GEMMs) run a 64 x 64-tile kernel that fills the chip (default on; it takes
  * precedence over the two-K-group kernel and split-K); same accumulation order as the
- * one-group kernel, so the same bits.  0 turns it off. */
+ * one-group kernel, so the same bits.  0 turns it off; 2 (A/B) also gives it the N <= 128
+ * launches of < 256 tiles of 128 x 128 (one workgroup per CU on the 128 x 128 kernel). */
 int ensvs_set_small(int on);
 /* Persistent recurrence workgroups (LSTM, AR decoder) reserve their CU's LDS so no GEMM
  * workgroup of a concurrent stream lands beside them (default on);

@@ -1,12 +1,10 @@
 #!/bin/bash
-# round-6 GPU check: the 128 x 256 kernel's RELU_MASK instance -- tests, per-launch times
+# round-6 GPU check: the main step's N = 128 launches on the 128 x 128 / 64 x 64 kernels
 set -o pipefail
 mkdir -p gpurun_out
 ( while sleep 45; do date >> gpurun_out/hb.txt; done ) &
 HB=$!
 trap "kill $HB" EXIT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 400 python -u -m pytest -v --timeout 200 --timeout-method thread -m gpu -rf -x tests/test_gemm_p8h_gpu.py > gpurun_out/p8h_rm_tests.log 2>&1
-rc=$?; grep -E "FAIL|passed|failed|Error" gpurun_out/p8h_rm_tests.log | tail -20; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u tools/p8h_bench.py > gpurun_out/p8h_rm_bench.txt 2>&1
-rc=$?; grep -v amdgpu gpurun_out/p8h_rm_bench.txt | cut -c1-160; exit $rc
+timeout -k 10 300 python -u tools/n128_bench.py > gpurun_out/n128_bench.txt 2>&1
+rc=$?; grep -v amdgpu gpurun_out/n128_bench.txt | cut -c1-220; exit $rc

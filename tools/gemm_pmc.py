@@ -4,7 +4,9 @@
 CASE: gate_fwd (mgc gate GEMM, 256 x 256 kernel), gate_bwd (mgc gate-backward dgrad,
 M 30720, N 512, K 512, EPI_GATE_BWD + tile column sums), dil_dgrad (mgc dilated-conv
 dgrad, N 256, K 3 x 512), wgrad_cond (conditioner weight gradient, N 10240, K 256),
-wgrad_dil (dilated-conv weight gradient, N 512, K 256 x 3).
+wgrad_dil (dilated-conv weight gradient, N 512, K 256 x 3); the 128 x 256 kernel's launches:
+skip_sum (N 256, K 5 120, lean plain), cond_dgrad (N 256, K 10 240, lean plain), res_fwd
+(N 256, K 256, ADDSCALE with the bf16 copy and its per-sequence add).
 """
 import os
 import sys
@@ -29,6 +31,25 @@ def main(case, iters=20):
         fn = lambda: K.wgrad(dy, N, x, Kc, B, T, T, N, Kc, taps, dil,  # noqa: E731
                              -dil if taps > 1 else 0, _lib.PAD_ZERO, dst, Kc * taps, taps, 1,
                              accum=True)
+    elif case in ("skip_sum", "cond_dgrad", "res_fwd"):
+        N = 256
+        Kc = {"skip_sum": 20 * N, "cond_dgrad": 40 * N, "res_fwd": N}[case]
+        pb = K.PackedBuffer(_lib.DT_BF16)
+        ref = pb.add(rnd(N, Kc, 1) * 0.01, N, Kc, 1, Kc, 1, 1)
+        pb.finalize(dev)
+        pb.repack()
+        x = rnd(M, Kc).bfloat16()
+        y = torch.empty(M, N, device=dev)
+        segs = [K.Seg(x, Kc, Kc, ref, T)]
+        if case == "res_fwd":
+            xr = rnd(M, N)
+            yb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ds, bias = rnd(B, 20 * N), rnd(N)
+            fn = lambda: K.gemm(segs, B, T, N, pb, y, N, epi=_lib.EPI_ADDSCALE, aux1=xr,  # noqa
+                                ld1=N, alpha=0.7071, ybf=yb, ybf_ld=N, ybf_radd=ds[:, N:],
+                                ybf_radd_ld=20 * N, bias=bias)
+        else:
+            fn = lambda: K.gemm(segs, B, T, N, pb, y, N)  # noqa: E731
     else:
         pb = K.PackedBuffer(_lib.DT_BF16)
         if case == "gate_fwd":

@@ -196,3 +196,35 @@ def test_p8_barrier_forms_bitwise(N, specs, epi, B, T):
         L.call("ensvs_set_p8", 6)
     _assert_same(outs[0], outs[1])
     _assert_same(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("case", ["conv_k7", "addscale"])
+@pytest.mark.parametrize("B,T", [(30, 1024), (7, 1000)])
+def test_small_n128_bitwise(case, B, T):
+    """ensvs_set_small(2) (A/B): the N = 128 launches of < 256 tiles of 128 x 128 on the 64 x 64
+    kernel give the 128 x 128 kernel's bits (tools/n128_bench.py, profiles/r6_n128_bench.txt)."""
+    torch.manual_seed(17)
+    C = 128
+    if case == "conv_k7":
+        x = _bf(torch.randn(B * T, C, device=DEV))
+        pb, (r,) = _pack([torch.randn(C, C, 7, device=DEV) * 0.03])
+        bias = torch.randn(C, device=DEV)
+        segs = [K.Seg(x, C, C, r, T, taps=7, shift0=-3)]
+        kw = dict(bias=bias)
+    else:
+        x = _bf(torch.randn(B * T, 2 * C, device=DEV))
+        pb, (r,) = _pack([torch.randn(C, 2 * C, 3, device=DEV) * 0.03])
+        segs = [K.Seg(x, 2 * C, 2 * C, r, T, taps=3, dil=2, shift0=-2)]
+        kw = dict(epi=L.EPI_ADDSCALE, aux1=torch.randn(B * T, C, device=DEV), ld1=C, alpha=0.7071)
+    outs = []
+    try:
+        for mode in (1, 2):
+            L.call("ensvs_set_small", mode)
+            y = torch.full((B * T, C), float("nan"), device=DEV)
+            K.gemm(segs, B, T, C, pb, y, C, **kw)
+            torch.cuda.synchronize()
+            outs.append(y)
+    finally:
+        L.call("ensvs_set_small", 1)
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max().item()

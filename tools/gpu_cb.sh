@@ -1,13 +1,10 @@
 #!/bin/bash
-# round-6 GPU check: PMC passes over the 128 x 256 kernel's launches (tools/pmc_gemm_cases.sh)
+# round-6 GPU check: the 128 x 256 / 64 x 64 routing bitwise tests
 set -o pipefail
 mkdir -p gpurun_out
 ( while sleep 45; do date >> gpurun_out/hb.txt; done ) &
 HB=$!
 trap "kill $HB" EXIT
-CASES="skip_sum cond_dgrad res_fwd" bash tools/pmc_gemm_cases.sh || exit 1
-for c in skip_sum cond_dgrad res_fwd; do
-  echo "### $c"; cat gpurun_out/pmc_$c.txt | grep -v amdgpu
-  python3 tools/pmc_table.py gpurun_out/pmc_${c}_1 gpurun_out/pmc_${c}_2 gpurun_out/pmc_${c}_3 gpurun_out/pmc_${c}_4 --match conv_gemm
-done > gpurun_out/pmc_p8h.txt 2>&1
-cat gpurun_out/pmc_p8h.txt
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 400 python -u -m pytest -v --timeout 200 --timeout-method thread -m gpu -rf -x tests/test_gemm_p8h_gpu.py > gpurun_out/p8h_small_tests.log 2>&1
+rc=$?; grep -E "FAIL|passed|failed|Error" gpurun_out/p8h_small_tests.log | tail -20; exit $rc

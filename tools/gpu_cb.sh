@@ -1,10 +1,11 @@
 #!/bin/bash
-# round-6 GPU check: the 128 x 256 / 64 x 64 routing bitwise tests
+# round-6 GPU check: kernel stats of the graph-replayed SeparateF0 step on the final tree
 set -o pipefail
 mkdir -p gpurun_out
 ( while sleep 45; do date >> gpurun_out/hb.txt; done ) &
 HB=$!
 trap "kill $HB" EXIT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 400 python -u -m pytest -v --timeout 200 --timeout-method thread -m gpu -rf -x tests/test_gemm_p8h_gpu.py > gpurun_out/p8h_small_tests.log 2>&1
-rc=$?; grep -E "FAIL|passed|failed|Error" gpurun_out/p8h_small_tests.log | tail -20; exit $rc
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/sf0z -o sf0 -- python3 tools/sf0_trace.py > gpurun_out/sf0z.log 2>&1
+rc=$?; tail -3 gpurun_out/sf0z.log; [ $rc -eq 0 ] || exit $rc
+python3 tools/sf0_trace.py --show gpurun_out/sf0z/sf0_kernel_trace.csv > gpurun_out/sf0z_show.txt 2>&1; head -3 gpurun_out/sf0z_show.txt

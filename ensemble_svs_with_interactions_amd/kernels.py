@@ -431,6 +431,9 @@ def scratch(nfloats, device, key="part"):
     return t
 
 
+# fp32-operand weight gradients whose channel count the vector kernels cannot stage (K % 4)
+# run on bf16 copies through the LDS-DMA kernel (wgrad above); off: the register kernel
+WGRAD_CAST = {"on": True}
 # weight gradients split the frame reduction until about this many workgroups (tile x split)
 WGRAD_TARGET = 512  # workgroups a weight gradient aims for (256: 20.7, 1024: 20.5 vs 20.1 ms/step)
 # bf16 weight gradients with >= 16 output tiles of 256 x 256: the 256 x 256-tile kernel (its
@@ -539,6 +542,19 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
         up = -(-splits // 8) * 8
         if splits >= 8 and up * tiles <= WGRAD_TARGET:
             splits = up
+    if (WGRAD_CAST["on"] and dtype == _lib.DT_BF16 and radd is None and K % 4 and N % 8 == 0
+            and ldy % 4 == 0 and (dy.data_ptr() + 4 * dyoff) % 16 == 0 and
+            dy.dtype == x.dtype == torch.float32):
+        # fp32 operands with an odd channel count (the input-feature embeddings, K = 39 / 130;
+        # the 1-channel k7 conv; K = 5) stage one element per lane on the register kernel:
+        # bf16 copies (x zero-padded to 8 channels, the rounding the kernel applies while
+        # staging) and the LDS-DMA kernel instead, same split count
+        K8 = -(-K // 8) * 8
+        xb = torch.empty(B * Tin, K8, dtype=torch.bfloat16, device=x.device)
+        call("ensvs_cast_bf16", x.data_ptr() + 4 * xoff, ldx, None, 0, 1, B * Tin, K,
+             xb.data_ptr(), K8, stream())
+        dy, ldy, x, ldx = cast_bf16(dy, ldy, N, M, dyoff), N, xb, K8
+        dyoff = xoff = 0
     flag = int(accum)
     dptr = dst.data_ptr() + 4 * dstoff
     queue = None

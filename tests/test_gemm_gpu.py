@@ -207,6 +207,37 @@ def test_wgrad_fp32_source_bitwise_equals_bf16_operands(shape, splits):
         assert rel(outs[0][:, :, 0] - 0.25, 0.5 * ref) < 2e-2
 
 
+@pytest.mark.parametrize("shape", [(30, 1024, 39, 256, 1, 1, L.PAD_ZERO),
+                                   (30, 1024, 1, 128, 7, 1, L.PAD_ZERO),
+                                   (30, 1024, 5, 128, 1, 1, L.PAD_ZERO),
+                                   (7, 1097, 130, 1024, 1, 1, L.PAD_ZERO),
+                                   (3, 517, 3, 64, 3, 2, L.PAD_REFLECT)])
+def test_wgrad_odd_channels_cast_route(shape):
+    """fp32-operand weight gradients with K % 4 != 0 (kernels.WGRAD_CAST: bf16 copies, x
+    zero-padded to 8 channels, through the LDS-DMA kernel) against the register kernel they
+    replace and a float64 reference, incl. taps with reflect padding and ragged M."""
+    torch.manual_seed(12)
+    B, T, Cin, Cout, taps, dil, pad = shape
+    M = B * T
+    x = torch.randn(M, Cin, device=DEV)
+    g = torch.randn(M, Cout, device=DEV)
+    outs = []
+    try:
+        for on in (False, True):
+            K.WGRAD_CAST["on"] = on
+            dw = torch.full((Cout, Cin, taps), 0.25, device=DEV)
+            K.wgrad(g, Cout, x, Cin, B, T, T, Cout, Cin, taps, dil, -dil * (taps // 2), pad, dw,
+                    Cin * taps, taps, 1, dtype=L.DT_BF16, accum=True, scale=0.5)
+            outs.append(dw)
+    finally:
+        K.WGRAD_CAST["on"] = True
+    torch.cuda.synchronize()
+    assert rel(outs[1] - 0.25, outs[0] - 0.25) < 1e-5
+    if taps == 1:
+        ref = torch.einsum("mn,mk->nk", g.double(), x.double()).float()
+        assert rel(outs[1][:, :, 0] - 0.25, 0.5 * ref) < 2e-2
+
+
 def test_colsum_vectorized_tail():
     torch.manual_seed(6)
     y = torch.randn(5000, 128, device=DEV)

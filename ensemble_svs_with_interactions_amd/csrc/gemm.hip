@@ -5128,8 +5128,10 @@ ENSVS_API int ensvs_conv_wgrad_bf16(const void* dy, int ldy, const void* x, int 
   const int defer = accum;  // ENSVS_WGRAD_DEFER: partials only
   accum &= 1;
   if (B <= 0 || Tout <= 0 || N <= 0 || K <= 0 || taps <= 0 || splits <= 0) return ENSVS_E_SHAPE;
-  // K % 8 != 0: the last 16-B chunk of an x row reads up to K rounded to 8 (stores check k < K)
-  if (N % 8 || ldy % 8 || ldx % 8 || ldx < (K + 7) / 8 * 8 || (((uintptr_t)dy | (uintptr_t)x) & 15))
+  // K (N) % 8 != 0: the last 16-B chunk of an x (dy) row reads up to K (N) rounded to 8, the
+  // caller's zero padding (stores check k < K, n < N)
+  if (ldy % 8 || ldy < (N + 7) / 8 * 8 || ldx % 8 || ldx < (K + 7) / 8 * 8 ||
+      (((uintptr_t)dy | (uintptr_t)x) & 15))
     return ENSVS_E_ARG;
   WgradArgs a{};
   a.dy = (const float*)dy;

@@ -542,18 +542,24 @@ def wgrad(dy, ldy, x, ldx, B, Tout, Tin, N, K, taps, dil, shift0, pad, dst, sn, 
         up = -(-splits // 8) * 8
         if splits >= 8 and up * tiles <= WGRAD_TARGET:
             splits = up
-    if (WGRAD_CAST["on"] and dtype == _lib.DT_BF16 and radd is None and K % 4 and N % 8 == 0
-            and ldy % 4 == 0 and (dy.data_ptr() + 4 * dyoff) % 16 == 0 and
-            dy.dtype == x.dtype == torch.float32):
+    def castable(t, ld, C, off):  # ensvs_cast_bf16: the padded copy, or 16-B rows
+        return C % 8 or (ld % 4 == 0 and (t.data_ptr() + 4 * off) % 16 == 0)
+    if (WGRAD_CAST["on"] and dtype == _lib.DT_BF16 and radd is None and (K % 4 or N % 4)
+            and dy.dtype == x.dtype == torch.float32 and castable(x, ldx, K, xoff) and
+            castable(dy, ldy, N, dyoff)):
         # fp32 operands with an odd channel count (the input-feature embeddings, K = 39 / 130;
-        # the 1-channel k7 conv; K = 5) stage one element per lane on the register kernel:
-        # bf16 copies (x zero-padded to 8 channels, the rounding the kernel applies while
-        # staging) and the LDS-DMA kernel instead, same split count
-        K8 = -(-K // 8) * 8
-        xb = torch.empty(B * Tin, K8, dtype=torch.bfloat16, device=x.device)
-        call("ensvs_cast_bf16", x.data_ptr() + 4 * xoff, ldx, None, 0, 1, B * Tin, K,
-             xb.data_ptr(), K8, stream())
-        dy, ldy, x, ldx = cast_bf16(dy, ldy, N, M, dyoff), N, xb, K8
+        # the 1-channel k7 conv; K = 5; the 1 / 4 / 5-wide output projections) stage one
+        # element per lane on the register kernel: bf16 copies (zero-padded to 8 channels, the
+        # rounding the kernel applies while staging) and the LDS-DMA kernel instead, same split
+        # count
+        def b16(t, ld, C, rows, off):
+            C8 = -(-C // 8) * 8
+            out = torch.empty(rows, C8, dtype=torch.bfloat16, device=t.device)
+            call("ensvs_cast_bf16", t.data_ptr() + 4 * off, ld, None, 0, 1, rows, C,
+                 out.data_ptr(), C8, stream())
+            return out, C8
+        x, ldx = b16(x, ldx, K, B * Tin, xoff)
+        dy, ldy = b16(dy, ldy, N, M, dyoff)
         dyoff = xoff = 0
     flag = int(accum)
     dptr = dst.data_ptr() + 4 * dstoff

@@ -171,10 +171,11 @@ int ensvs_conv_wgrad(const float* dy, int ldy, const float* x, int ldx, const fl
                      long long sk, long long sj, int accum, float scale, int dtype, void* stream);
 
 /* ensvs_conv_wgrad with bf16 operands (dy, x already rounded to bf16, radd folded into x;
- * N, ldy, ldx multiples of 8): identical bits, operands staged by global_load_lds.  K need not
- * be a multiple of 8 when every x row holds K rounded up to 8 readable columns (ldx >= that):
- * the columns past K are read in the last 16-B chunk and only feed outputs that are never
- * written (the SeparateF0 decoders' 1 026-column input, zero-padded to 1 032). */
+ * ldy, ldx multiples of 8): identical bits, operands staged by global_load_lds.  K (N) need
+ * not be a multiple of 8 when every x (dy) row holds K (N) rounded up to 8 readable columns
+ * (ldx, ldy >= that): the columns past K (N) are read in the last 16-B chunk and only feed
+ * outputs that are never written (the SeparateF0 decoders' 1 026-column input, zero-padded
+ * to 1 032; the odd-width fp32 operands' padded copies, kernels.WGRAD_CAST). */
 int ensvs_conv_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, int B, int Tout,
                           int Tin, int N, int K, int taps, int dil, int shift0, int pad, int splits,
                           float* part, float* dst, long long sn, long long sk, long long sj,

@@ -211,11 +211,16 @@ def test_wgrad_fp32_source_bitwise_equals_bf16_operands(shape, splits):
                                    (30, 1024, 1, 128, 7, 1, L.PAD_ZERO),
                                    (30, 1024, 5, 128, 1, 1, L.PAD_ZERO),
                                    (7, 1097, 130, 1024, 1, 1, L.PAD_ZERO),
-                                   (3, 517, 3, 64, 3, 2, L.PAD_REFLECT)])
+                                   (3, 517, 3, 64, 3, 2, L.PAD_REFLECT),
+                                   (30, 1024, 128, 5, 1, 1, L.PAD_ZERO),
+                                   (30, 1024, 128, 1, 1, 1, L.PAD_ZERO),
+                                   (7, 1097, 130, 4, 1, 1, L.PAD_ZERO),
+                                   (5, 700, 256, 60, 1, 1, L.PAD_ZERO)])
 def test_wgrad_odd_channels_cast_route(shape):
-    """fp32-operand weight gradients with K % 4 != 0 (kernels.WGRAD_CAST: bf16 copies, x
-    zero-padded to 8 channels, through the LDS-DMA kernel) against the register kernel they
-    replace and a float64 reference, incl. taps with reflect padding and ragged M."""
+    """fp32-operand weight gradients with K % 4 != 0 or N % 4 != 0 (kernels.WGRAD_CAST: bf16
+    copies zero-padded to 8 channels, through the LDS-DMA kernel) against the register kernel
+    they replace and a float64 reference, incl. taps with reflect padding and ragged M (N = 60:
+    the vector kernel, unchanged)."""
     torch.manual_seed(12)
     B, T, Cin, Cout, taps, dil, pad = shape
     M = B * T
